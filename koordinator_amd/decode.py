@@ -1,0 +1,723 @@
+"""Host-side decode of Kubernetes-shaped objects into the engine's node and pod columns.
+
+This is the work the Go side of the boundary does before calling the C ABI (SURVEY.md §8b,
+"Host-side pre-computation"): resource.Quantity arithmetic, PodRequests, priority / QoS
+classification, the LoadAware estimator and podAssignCache aggregates at a frozen snapshot time,
+EstimateNode, custom threshold annotations and the NUMA topology options.
+
+Objects are plain dicts in the shape of the Kubernetes JSON (``metadata``, ``spec``, ``status``).
+Times are float seconds relative to the frozen snapshot time ``now`` (None = unset).
+"""
+from __future__ import annotations
+
+import json
+import math
+import re
+from dataclasses import dataclass, field
+from fractions import Fraction
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .config import (BATCH_CPU, BATCH_MEMORY, CPU, EPHEMERAL, LA_RESOURCES, MEMORY, MID_CPU, MID_MEMORY, PODS,
+                     LoadAwareArgs, SchedulerConfig)
+
+
+class Unsupported(Exception):
+    """The object needs a feature that is not on the device path (caller keeps the Go plugin)."""
+
+
+# ---------------------------------------------------------------------------------------------
+# resource.Quantity (k8s.io/apimachinery v0.35.6)
+
+_SUFFIX = {
+    "Ki": Fraction(2 ** 10), "Mi": Fraction(2 ** 20), "Gi": Fraction(2 ** 30), "Ti": Fraction(2 ** 40),
+    "Pi": Fraction(2 ** 50), "Ei": Fraction(2 ** 60),
+    "n": Fraction(1, 10 ** 9), "u": Fraction(1, 10 ** 6), "m": Fraction(1, 1000), "": Fraction(1),
+    "k": Fraction(10 ** 3), "M": Fraction(10 ** 6), "G": Fraction(10 ** 9), "T": Fraction(10 ** 12),
+    "P": Fraction(10 ** 15), "E": Fraction(10 ** 18),
+}
+_QRE = re.compile(r"^([+-]?[0-9.]+)([eE][+-]?[0-9]+|[a-zA-Z]*)$")
+
+
+def parse_quantity(q) -> Fraction:
+    """Exact value of a Quantity string (or number)."""
+    if isinstance(q, Fraction):
+        return q
+    if isinstance(q, int):
+        return Fraction(q)
+    if isinstance(q, float):
+        return Fraction(q)
+    m = _QRE.match(str(q).strip())
+    if not m:
+        raise ValueError(f"invalid quantity {q!r}")
+    num, suf = m.groups()
+    v = Fraction(num)
+    if suf and suf[0] in "eE" and len(suf) > 1 and (suf[1:].lstrip("+-").isdigit()):
+        return v * Fraction(10) ** int(suf[1:])
+    if suf not in _SUFFIX:
+        raise ValueError(f"invalid quantity suffix {q!r}")
+    return v * _SUFFIX[suf]
+
+
+def value(q) -> int:
+    """Quantity.Value(): rounded up to the nearest integer."""
+    return math.ceil(parse_quantity(q))
+
+
+def milli_value(q) -> int:
+    """Quantity.MilliValue(): value*1000 rounded up."""
+    return math.ceil(parse_quantity(q) * 1000)
+
+
+def vec_value(name: str, q) -> int:
+    """getResourceValue (loadaware/helper.go:124-129): cpu in milli, others as Value()."""
+    return milli_value(q) if name == CPU else value(q)
+
+
+def go_round(x: float) -> float:
+    """math.Round: nearest integer, halves away from zero."""
+    t = math.trunc(x)
+    if abs(x - t) >= 0.5:
+        t += math.copysign(1.0, x)
+    return t
+
+
+ResourceList = Dict[str, Fraction]
+
+
+def _rl(d) -> ResourceList:
+    return {k: parse_quantity(v) for k, v in (d or {}).items()}
+
+
+def _add(dst: ResourceList, src: ResourceList):
+    for k, v in src.items():
+        dst[k] = dst.get(k, Fraction(0)) + v
+
+
+def _max(dst: ResourceList, src: ResourceList):
+    for k, v in src.items():
+        if k not in dst or v > dst[k]:
+            dst[k] = v
+
+
+# ---------------------------------------------------------------------------------------------
+# Pods
+
+def _containers(pod):
+    return (pod.get("spec") or {}).get("containers") or []
+
+
+def _init_containers(pod):
+    return (pod.get("spec") or {}).get("initContainers") or []
+
+
+def _restartable(c) -> bool:
+    return c.get("restartPolicy") == "Always"
+
+
+def pod_requests(pod, non_missing: Optional[ResourceList] = None) -> ResourceList:
+    """k8s.io/component-helpers resource.PodRequests (KEP-753 sidecar rules, overhead added)."""
+    def creqs(c):
+        r = _rl((c.get("resources") or {}).get("requests"))
+        if non_missing:
+            for k, v in non_missing.items():
+                if k not in r:
+                    r[k] = v
+        return r
+
+    reqs: ResourceList = {}
+    for c in _containers(pod):
+        _add(reqs, creqs(c))
+    restartable: ResourceList = {}
+    init_reqs: ResourceList = {}
+    for c in _init_containers(pod):
+        cr = creqs(c)
+        if _restartable(c):
+            _add(reqs, cr)
+            _add(restartable, cr)
+            cr = dict(restartable)
+        else:
+            tmp: ResourceList = {}
+            _add(tmp, cr)
+            _add(tmp, restartable)
+            cr = tmp
+        _max(init_reqs, cr)
+    _max(reqs, init_reqs)
+    overhead = (pod.get("spec") or {}).get("overhead")
+    if overhead:
+        _add(reqs, _rl(overhead))
+    return reqs
+
+
+def pod_limits(pod) -> ResourceList:
+    """resource.PodLimits: container limits aggregated like requests; overhead added to present limits."""
+    lim: ResourceList = {}
+    for c in _containers(pod):
+        _add(lim, _rl((c.get("resources") or {}).get("limits")))
+    restartable: ResourceList = {}
+    init_lim: ResourceList = {}
+    for c in _init_containers(pod):
+        cl = _rl((c.get("resources") or {}).get("limits"))
+        if _restartable(c):
+            _add(lim, cl)
+            _add(restartable, cl)
+            cl = dict(restartable)
+        else:
+            tmp: ResourceList = {}
+            _add(tmp, cl)
+            _add(tmp, restartable)
+            cl = tmp
+        _max(init_lim, cl)
+    _max(lim, init_lim)
+    overhead = (pod.get("spec") or {}).get("overhead")
+    if overhead:
+        for k, v in _rl(overhead).items():
+            if k in lim:
+                lim[k] += v
+    return lim
+
+
+# upstream schedutil.DefaultMilliCPURequest / DefaultMemoryRequest (100m / 200Mi)
+NON_MISSING = {CPU: Fraction(1, 10), MEMORY: Fraction(200 * 1024 * 1024)}
+
+LABEL_PRIORITY_CLASS = "koordinator.sh/priority-class"
+LABEL_QOS = "koordinator.sh/qosClass"
+PRIORITY_RANGES = [("koord-prod", 9000, 9999), ("koord-mid", 7000, 7999), ("koord-batch", 5000, 5999),
+                   ("koord-free", 3000, 3999)]
+PROD, MID, BATCH, FREE, NONE = "koord-prod", "koord-mid", "koord-batch", "koord-free", ""
+
+
+def kube_qos(pod) -> str:
+    """qos.GetPodQOS (k8s.io/kubernetes pkg/apis/core/v1/helper/qos): cpu/memory only."""
+    st = (pod.get("status") or {}).get("qosClass")
+    if st:
+        return st
+    requests: ResourceList = {}
+    limits: ResourceList = {}
+    guaranteed = True
+    for c in list(_containers(pod)) + list(_init_containers(pod)):
+        res = c.get("resources") or {}
+        for name, q in _rl(res.get("requests")).items():
+            if name in (CPU, MEMORY) and q > 0:
+                requests[name] = requests.get(name, Fraction(0)) + q
+        found = set()
+        for name, q in _rl(res.get("limits")).items():
+            if name in (CPU, MEMORY) and q > 0:
+                found.add(name)
+                limits[name] = limits.get(name, Fraction(0)) + q
+        if not {CPU, MEMORY} <= found:
+            guaranteed = False
+    if not requests and not limits:
+        return "BestEffort"
+    if guaranteed:
+        for name, req in requests.items():
+            if name not in limits or limits[name] != req:
+                guaranteed = False
+                break
+    if guaranteed and len(requests) == len(limits):
+        return "Guaranteed"
+    return "Burstable"
+
+
+def koord_qos_raw(pod) -> str:
+    labels = (pod.get("metadata") or {}).get("labels") or {}
+    q = labels.get(LABEL_QOS)
+    return q if q in ("LSE", "LSR", "LS", "BE", "SYSTEM") else ""
+
+
+def priority_class(pod) -> str:
+    """extension.GetPodPriorityClassWithDefault (apis/extension/priority_utils.go:37-57)."""
+    labels = (pod.get("metadata") or {}).get("labels") or {}
+    raw = NONE
+    if LABEL_PRIORITY_CLASS in labels:
+        v = labels[LABEL_PRIORITY_CLASS]
+        raw = v if v in (PROD, MID, BATCH, FREE) else NONE
+    else:
+        p = (pod.get("spec") or {}).get("priority")
+        if p is not None:
+            for name, lo, hi in PRIORITY_RANGES:
+                if lo <= p <= hi:
+                    raw = name
+                    break
+    if raw != NONE:
+        return raw
+    qos = koord_qos_raw(pod)
+    if not qos:
+        qos = {"Guaranteed": "LSR", "Burstable": "LS", "BestEffort": "BE"}[kube_qos(pod)]
+    if qos in ("SYSTEM", "LSE", "LSR", "LS"):
+        return PROD
+    if qos == "BE":
+        return BATCH
+    return NONE
+
+
+def translate_resource(pclass: str, name: str) -> str:
+    """TranslateResourceNameByPriorityClass (apis/extension/resource.go:64-70)."""
+    if pclass in (PROD, NONE):
+        return name
+    table = {BATCH: {CPU: BATCH_CPU, MEMORY: BATCH_MEMORY}, MID: {CPU: MID_CPU, MEMORY: MID_MEMORY}}
+    return table.get(pclass, {}).get(name, "")
+
+
+DEFAULT_EST_MILLI_CPU = 250
+DEFAULT_EST_MEMORY = 200 * 1024 * 1024
+
+
+def _estimated_used_by_resource(requests: ResourceList, limits: ResourceList, name: str, factor: int) -> int:
+    """estimatedUsedByResource (loadaware/estimator/default_estimator.go:87-120)."""
+    lq = limits.get(name, Fraction(0))
+    rq = requests.get(name, Fraction(0))
+    q = lq if lq > rq else rq
+    if q == 0:
+        if name in (CPU, BATCH_CPU):
+            return DEFAULT_EST_MILLI_CPU
+        if name in (MEMORY, BATCH_MEMORY):
+            return DEFAULT_EST_MEMORY
+        return 0
+    if name == CPU:
+        est = int(go_round(float(milli_value(q)) * float(factor) / 100))
+        lim = milli_value(lq)
+    else:
+        est = int(go_round(float(value(q)) * float(factor) / 100))
+        lim = value(lq)
+    if lim > 0 and est > lim:
+        est = lim
+    return est
+
+
+ANN_CUSTOM_ESTIMATED_SCALING_FACTORS = "scheduling.koordinator.sh/load-estimated-scaling-factors"
+
+
+def estimate_pod(pod, la: LoadAwareArgs) -> List[int]:
+    """DefaultEstimator.EstimatePod -> vectorizer.ToFactorVec (default_estimator.go:57-85)."""
+    factors = dict(la.estimated_scaling_factors or {})
+    if la.allow_customize_estimation:
+        ann = ((pod.get("metadata") or {}).get("annotations") or {}).get(ANN_CUSTOM_ESTIMATED_SCALING_FACTORS)
+        if ann:
+            try:
+                custom = {k: int(v) for k, v in json.loads(ann).items()}
+            except Exception:
+                custom = {}
+            if custom:
+                for k, v in factors.items():
+                    custom.setdefault(k, v)
+                factors = custom
+    requests, limits = pod_requests(pod), pod_limits(pod)
+    pc = priority_class(pod)
+    est = {}
+    for name, f in factors.items():
+        est[name] = _estimated_used_by_resource(requests, limits, translate_resource(pc, name), f)
+    return [est.get(r, 0) for r in LA_RESOURCES]
+
+
+def is_daemonset_pod(pod) -> bool:
+    return any(o.get("kind") == "DaemonSet" for o in ((pod.get("metadata") or {}).get("ownerReferences") or []))
+
+
+ANN_NUMA_TOPOLOGY_SPEC = "scheduling.koordinator.sh/numa-topology-spec"
+ANN_RESOURCE_SPEC = "scheduling.koordinator.sh/resource-spec"
+
+
+def pod_row(pod, cfg: SchedulerConfig) -> Dict[str, int]:
+    """Pod columns (kg_pod_columns) for one pending pod."""
+    la = cfg.la()
+    req = pod_requests(pod)
+    nz = pod_requests(pod, NON_MISSING)
+    row = {
+        "req_cpu": milli_value(req.get(CPU, 0)),
+        "req_mem": value(req.get(MEMORY, 0)),
+        "req_eph": value(req.get(EPHEMERAL, 0)),
+        "nz_cpu": milli_value(nz.get(CPU, 0)),
+        "nz_mem": value(nz.get(MEMORY, 0)),
+    }
+    for k, name in enumerate(cfg.scalar_resources):
+        row[f"sc_req{k}"] = value(req.get(name, 0))
+    if cfg.plugins & abi.KG_PLUGIN_NRF:
+        # fitsRequest checks every requested scalar; only the snapshot's scalar slots are on device
+        for name, q in req.items():
+            if name in (CPU, MEMORY, EPHEMERAL, PODS) or name in cfg.scalar_resources:
+                continue
+            if q != 0:
+                raise Unsupported(f"scalar resource {name} is not a snapshot column")
+    for r, v in enumerate(estimate_pod(pod, la)):
+        row[f"la_est{r}"] = v
+    flags = 0
+    if is_daemonset_pod(pod):
+        flags |= abi.KG_POD_DAEMONSET
+    pc = priority_class(pod)
+    if pc == PROD:
+        flags |= abi.KG_POD_PROD
+    if all(v == 0 for v in req.values()):
+        flags |= abi.KG_POD_NUMA_SKIP
+    if CPU in req:
+        flags |= abi.KG_POD_HAS_CPU
+    if MEMORY in req:
+        flags |= abi.KG_POD_HAS_MEM
+    # AllowUseCPUSet (nodenumaresource/util.go:49-56): LSE/LSR prod pods bind cpusets by default
+    # (DefaultCPUBindPolicy FullPCPUs) -> host path.
+    if koord_qos_raw(pod) in ("LSE", "LSR") and pc == PROD and (cfg.plugins & abi.KG_PLUGIN_NUMA):
+        if row["req_cpu"] > 0:
+            flags |= abi.KG_POD_CPU_BIND
+    ann = (pod.get("metadata") or {}).get("annotations") or {}
+    if ann.get(ANN_NUMA_TOPOLOGY_SPEC):
+        raise Unsupported("pod NUMA topology spec (exclusive-policy admission) is not on the device path")
+    row["flags"] = flags
+    row["numa_policy"] = abi.KG_NUMA_NONE
+    return row
+
+
+def pods_table(pods: Sequence[dict], cfg: SchedulerConfig) -> abi.Table:
+    t = abi.empty_pods(len(pods))
+    for j, p in enumerate(pods):
+        for k, v in pod_row(p, cfg).items():
+            t[k][j] = v
+    return t
+
+
+# ---------------------------------------------------------------------------------------------
+# Nodes
+
+ANN_CUSTOM_USAGE_THRESHOLDS = "scheduling.koordinator.sh/usage-thresholds"
+ANN_RAW_ALLOCATABLE = "node.koordinator.sh/raw-allocatable"
+ANN_AMPLIFICATION = "node.koordinator.sh/resource-amplification-ratio"
+LABEL_NUMA_POLICY = "node.koordinator.sh/numa-topology-policy"
+NUMA_POLICIES = {"": abi.KG_NUMA_NONE, "BestEffort": abi.KG_NUMA_BEST_EFFORT,
+                 "Restricted": abi.KG_NUMA_RESTRICTED, "SingleNUMANode": abi.KG_NUMA_SINGLE_NODE}
+
+
+def amplify(origin: int, ratio: float) -> int:
+    """extension.Amplify (apis/extension/node_resource_amplification.go:170-175)."""
+    if ratio <= 1:
+        return origin
+    return int(math.ceil(float(origin) * float(ratio)))
+
+
+def _pod_key(pod) -> Tuple[str, str]:
+    md = pod.get("metadata") or {}
+    return (md.get("namespace", ""), md.get("name", ""))
+
+
+def _is_terminated(pod) -> bool:
+    return ((pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"))
+
+
+@dataclass
+class _Profile:
+    usage: List[int]
+    prod: List[int]
+    agg: Optional[Tuple[List[int], str, float]]
+
+
+def _factor_vec(m: Dict[str, int]) -> List[int]:
+    return [int(m.get(r, 0)) for r in LA_RESOURCES]
+
+
+def filter_profile(node, la: LoadAwareArgs) -> _Profile:
+    """NewUsageThresholdsFilterProfile + generateUsageThresholdsFilterProfile (loadaware/helper.go:59-121)."""
+    base_agg = None
+    a = la.aggregated
+    if a is not None and len(a.usage_thresholds) > 0 and a.usage_aggregation_type != "":
+        base_agg = (_factor_vec(a.usage_thresholds), a.usage_aggregation_type, a.usage_aggregated_duration)
+    prof = _Profile(usage=_factor_vec(la.usage_thresholds) if la.usage_thresholds else [0] * abi.KG_LA_R,
+                    prod=_factor_vec(la.prod_usage_thresholds) if la.prod_usage_thresholds else [0] * abi.KG_LA_R,
+                    agg=base_agg)
+    ann = ((node.get("metadata") or {}).get("annotations") or {}).get(ANN_CUSTOM_USAGE_THRESHOLDS)
+    if ann is None:
+        return prof
+    try:
+        c = json.loads(ann)
+    except Exception:
+        return prof
+    cu = c.get("usageThresholds") or {}
+    cp = c.get("prodUsageThresholds") or {}
+    ca = c.get("aggregatedUsage")
+    if ca is not None and not (len(ca.get("usageThresholds") or {}) > 0 and ca.get("usageAggregationType", "") != ""):
+        ca = None
+    if len(cu) == 0 and len(cp) == 0 and ca is None:
+        return prof
+    out = _Profile(usage=prof.usage if len(cu) == 0 else _factor_vec(cu),
+                   prod=prof.prod if len(cp) == 0 else _factor_vec(cp), agg=prof.agg)
+    if ca is not None:
+        out.agg = (_factor_vec(ca["usageThresholds"]), ca["usageAggregationType"],
+                   _duration(ca.get("usageAggregatedDuration")))
+    return out
+
+
+def _duration(d) -> float:
+    """metav1.Duration from a Go duration string ("5m", "300s", "1h30m") or seconds."""
+    if d is None:
+        return 0.0
+    if isinstance(d, (int, float)):
+        return float(d)
+    total = 0.0
+    for num, unit in re.findall(r"([0-9.]+)(ns|us|ms|s|m|h)", d):
+        total += float(num) * {"ns": 1e-9, "us": 1e-6, "ms": 1e-3, "s": 1, "m": 60, "h": 3600}[unit]
+    return total
+
+
+def estimate_node_allocatable(node) -> Dict[str, Fraction]:
+    """DefaultEstimator.EstimateNode (default_estimator.go:122-141)."""
+    alloc = _rl((node.get("status") or {}).get("allocatable"))
+    ann = ((node.get("metadata") or {}).get("annotations") or {}).get(ANN_RAW_ALLOCATABLE)
+    if ann:
+        try:
+            raw = _rl(json.loads(ann))
+        except Exception:
+            raw = {}
+        for k, v in raw.items():
+            alloc[k] = v
+    return alloc
+
+
+@dataclass
+class AssignedPod:
+    pod: dict
+    timestamp: float  # podAssignInfo.timestamp, seconds relative to now
+
+
+class LoadAwareNodeCache:
+    """nodeInfo of loadaware/pod_assign_cache.go:93-125 for one node at a frozen time."""
+
+    def __init__(self, metric: Optional[dict], assigned: Iterable[AssignedPod], la: LoadAwareArgs):
+        self.metric = metric
+        self.la = la
+        zero = [0] * abi.KG_LA_R
+        self.node_usage = None
+        self.prod_usage = list(zero)
+        self.agg_usages: Dict[Tuple[str, float], List[int]] = {}
+        self.pod_usages: Dict[Tuple[str, str], List[int]] = {}
+        self.prod_pods = set()
+        self.update_time = -math.inf
+        self.report_interval = 60.0
+        self.node_delta, self.prod_delta, self.node_estimated = list(zero), list(zero), list(zero)
+        if metric is None:
+            return
+        st = metric.get("status") or {}
+        spec = metric.get("spec") or {}
+        info = st.get("nodeMetric")
+        if info is not None:
+            self.node_usage = self._vec((info.get("nodeUsage") or {}).get("resources"))
+            aggs = info.get("aggregatedNodeUsages") or []
+            max_d: Dict[str, float] = {}
+            for agg in aggs:
+                d = _duration(agg.get("duration"))
+                for t, u in (agg.get("usage") or {}).items():
+                    res = (u or {}).get("resources") or {}
+                    if len(res) == 0:
+                        continue
+                    self.agg_usages[(t, d)] = self._vec(res)
+                    if d > max_d.get(t, 0.0):
+                        max_d[t] = d
+            for t, d in max_d.items():
+                self.agg_usages[(t, 0.0)] = self.agg_usages[(t, d)]
+            if la.prod_usage_include_sys:
+                sysu = self._vec((info.get("systemUsage") or {}).get("resources"))
+                self.prod_usage = [a + b for a, b in zip(self.prod_usage, sysu)]
+        for pm in st.get("podsMetric") or []:
+            if pm is None:
+                continue
+            res = (pm.get("podUsage") or {}).get("resources") or {}
+            if len(res) == 0:
+                continue
+            key = (pm.get("namespace", ""), pm.get("name", ""))
+            self.pod_usages[key] = self._vec(res)
+            if pm.get("priority") == PROD:
+                self.prod_pods.add(key)
+        ut = st.get("updateTime")
+        if ut is not None:
+            self.update_time = float(ut)
+        ri = (spec.get("collectPolicy") or {}).get("reportIntervalSeconds")
+        if ri is not None:
+            self.report_interval = float(ri)
+        for ap in assigned:
+            self._add_pod(ap)
+
+    @staticmethod
+    def _vec(resources) -> List[int]:
+        res = resources or {}
+        return [vec_value(r, res[r]) if r in res else 0 for r in LA_RESOURCES]
+
+    def _add_pod(self, ap: AssignedPod):
+        """nodeInfo.addPod (pod_assign_cache.go:618-662)."""
+        pod = ap.pod
+        key = _pod_key(pod)
+        u = self.pod_usages.get(key)
+        prod = priority_class(pod) == PROD
+        active_prod = prod and key in self.prod_pods
+        if active_prod:
+            self.prod_usage = [a + b for a, b in zip(self.prod_usage, u)]
+        e = estimate_pod(pod, self.la)
+        if all(x == 0 for x in e):  # assign(): empty estimate vector -> nil
+            return
+        should = u is None or (self.update_time - self.report_interval) < ap.timestamp
+        if should:
+            self.node_delta = _add_delta(self.node_delta, e, u)
+        self.node_estimated = [a + b for a, b in zip(self.node_estimated, e)]
+        if not prod:
+            return
+        if not active_prod and u is not None:
+            u, should = None, True
+        if should:
+            self.prod_delta = _add_delta(self.prod_delta, e, u)
+
+    def estimated_of_existing(self, prod_pod: bool, agg_type: str = "", agg_duration: float = 0.0):
+        """GetNodeMetricAndEstimatedOfExisting (pod_assign_cache.go:163-201); None = NotFound."""
+        if self.metric is None:
+            return None
+        if prod_pod:
+            return [a + b for a, b in zip(self.prod_usage, self.prod_delta)]
+        if agg_type:
+            usage = self.agg_usages.get((agg_type, agg_duration))
+            if usage is None and agg_duration == 0:
+                usage = self.node_usage
+        else:
+            usage = self.node_usage
+        if usage is not None:
+            return [a + b for a, b in zip(usage, self.node_delta)]
+        return list(self.node_estimated)
+
+
+def _add_delta(v, x, y):
+    out = list(v)
+    for i, val in enumerate(x):
+        if y is not None:
+            val -= y[i]
+        if val > 0:
+            out[i] += val
+    return out
+
+
+@dataclass
+class NodeInput:
+    """Everything the snapshot needs about one node."""
+
+    node: dict
+    pods: List[dict] = field(default_factory=list)           # pods bound/assumed on the node (NodeInfo)
+    node_metric: Optional[dict] = None                      # slo NodeMetric
+    assigned: Optional[List[AssignedPod]] = None            # podAssignCache entries (default: pods)
+    numa_zones: Optional[List[Dict[str, str]]] = None       # NodeResourceTopology zone resources
+    numa_used: Optional[List[Dict[str, str]]] = None        # resourceManager allocated per zone
+    kubelet_numa_policy: str = ""                           # NRT topology policy
+    cpuset_allocated_milli: int = 0
+
+
+def node_row(ni: NodeInput, cfg: SchedulerConfig) -> Dict[str, object]:
+    la = cfg.la()
+    node = ni.node
+    alloc = _rl((node.get("status") or {}).get("allocatable"))
+    row: Dict[str, object] = {
+        "alloc_cpu": milli_value(alloc.get(CPU, 0)),
+        "alloc_mem": value(alloc.get(MEMORY, 0)),
+        "alloc_eph": value(alloc.get(EPHEMERAL, 0)),
+        "alloc_pods": value(alloc.get(PODS, 0)),
+    }
+    for k, name in enumerate(cfg.scalar_resources):
+        row[f"sc_alloc{k}"] = value(alloc.get(name, 0))
+    # NodeInfo.AddPod for every pod on the node
+    req = {"cpu": 0, "mem": 0, "eph": 0}
+    sc = [0] * abi.KG_NSCALAR
+    nzc = nzm = 0
+    for p in ni.pods:
+        r = pod_requests(p)
+        nz = pod_requests(p, NON_MISSING)
+        req["cpu"] += milli_value(r.get(CPU, 0))
+        req["mem"] += value(r.get(MEMORY, 0))
+        req["eph"] += value(r.get(EPHEMERAL, 0))
+        for k, name in enumerate(cfg.scalar_resources):
+            sc[k] += value(r.get(name, 0))
+        nzc += milli_value(nz.get(CPU, 0))
+        nzm += value(nz.get(MEMORY, 0))
+    row.update(req_cpu=req["cpu"], req_mem=req["mem"], req_eph=req["eph"], num_pods=len(ni.pods),
+               nz_cpu=nzc, nz_mem=nzm)
+    for k in range(abi.KG_NSCALAR):
+        row[f"sc_req{k}"] = sc[k]
+
+    # LoadAwareScheduling
+    est_alloc = estimate_node_allocatable(node)
+    for r, name in enumerate(LA_RESOURCES):
+        row[f"la_alloc{r}"] = vec_value(name, est_alloc[name]) if name in est_alloc else 0
+    prof = filter_profile(node, la)
+    for r in range(abi.KG_LA_R):
+        row[f"la_thr_usage{r}"] = prof.usage[r]
+        row[f"la_thr_prod{r}"] = prof.prod[r]
+        row[f"la_thr_agg{r}"] = prof.agg[0][r] if prof.agg else 0
+    assigned = ni.assigned
+    if assigned is None:
+        assigned = [AssignedPod(p, 0.0) for p in ni.pods]
+    assigned = [a for a in assigned if not _is_terminated(a.pod)]
+    cache = LoadAwareNodeCache(ni.node_metric, assigned, la)
+    flags = 0
+    if any(x != 0 for x in prof.prod):
+        flags |= abi.KG_LA_PROD_THR
+    if prof.agg is not None:
+        flags |= abi.KG_LA_AGG_THR
+    zero = [0] * abi.KG_LA_R
+    fb_np = fb_prod = sb_np = sb_prod = zero
+    if ni.node_metric is not None:
+        flags |= abi.KG_LA_HAS_METRIC
+        st = ni.node_metric.get("status") or {}
+        if st.get("nodeMetric") is None:
+            flags |= abi.KG_LA_NM_NIL
+        secs = la.node_metric_expiration_seconds
+        if secs is not None:
+            ut = st.get("updateTime")
+            if ut is None or (secs > 0 and (0.0 - float(ut)) >= secs):
+                flags |= abi.KG_LA_EXPIRED
+        if prof.agg is not None:
+            fb_np = cache.estimated_of_existing(False, prof.agg[1], prof.agg[2])
+        else:
+            fb_np = cache.estimated_of_existing(False)
+        fb_prod = cache.estimated_of_existing(True)
+        a = la.aggregated
+        if a is not None and a.score_aggregation_type != "":
+            sb_np = cache.estimated_of_existing(False, a.score_aggregation_type, a.score_aggregated_duration)
+        else:
+            sb_np = cache.estimated_of_existing(False)
+        sb_prod = cache.estimated_of_existing(True)
+    row["la_flags"] = flags
+    for r in range(abi.KG_LA_R):
+        row[f"la_fbase_np{r}"] = fb_np[r]
+        row[f"la_fbase_prod{r}"] = fb_prod[r]
+        row[f"la_sbase_np{r}"] = sb_np[r]
+        row[f"la_sbase_prod{r}"] = sb_prod[r]
+
+    # NodeNUMAResource
+    md = node.get("metadata") or {}
+    labels = md.get("labels") or {}
+    policy_name = labels.get(LABEL_NUMA_POLICY, "") or ni.kubelet_numa_policy
+    if policy_name not in NUMA_POLICIES:
+        raise Unsupported(f"NUMA topology policy {policy_name!r}")
+    row["numa_policy"] = NUMA_POLICIES[policy_name]
+    ratio = 1.0
+    ann = (md.get("annotations") or {}).get(ANN_AMPLIFICATION)
+    if ann:
+        ratio = float(json.loads(ann).get(CPU, 1.0))
+    row["cpu_amp_ratio"] = ratio
+    row["cpuset_alloc_milli"] = ni.cpuset_allocated_milli
+    zones = ni.numa_zones or []
+    if len(zones) > abi.KG_MAX_ZONES:
+        raise Unsupported(f"{len(zones)} NUMA zones > {abi.KG_MAX_ZONES}")
+    row["numa_zones"] = len(zones)
+    used = ni.numa_used or [{} for _ in zones]
+    for z in range(abi.KG_MAX_ZONES):
+        if z < len(zones):
+            zr = _rl(zones[z])
+            # amplifyNUMANodeResources (nodenumaresource/util.go:101-124)
+            row[f"zone_cpu{z}"] = amplify(milli_value(zr.get(CPU, 0)), ratio)
+            row[f"zone_mem{z}"] = value(zr.get(MEMORY, 0))
+            ur = _rl(used[z])
+            row[f"zone_cpu_used{z}"] = milli_value(ur.get(CPU, 0))
+            row[f"zone_mem_used{z}"] = value(ur.get(MEMORY, 0))
+        else:
+            row[f"zone_cpu{z}"] = row[f"zone_mem{z}"] = row[f"zone_cpu_used{z}"] = row[f"zone_mem_used{z}"] = 0
+    return row
+
+
+def nodes_table(nodes: Sequence[NodeInput], cfg: SchedulerConfig) -> abi.Table:
+    t = abi.empty_nodes(len(nodes))
+    for i, ni in enumerate(nodes):
+        for k, v in node_row(ni, cfg).items():
+            t[k][i] = v
+    return t

@@ -1,0 +1,70 @@
+/*
+ * kg_oracle.h — CPU restatement of koord-scheduler's Filter/Score/selectHost/Assume arithmetic.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is the parity oracle for the MI355X engine: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only as the checker or
+ * as the timed CPU baseline. The product path (koordinator_amd/, libkoordgpu.so) never links or
+ * calls it.
+ *
+ * Parity pinning: the reference is Go (no Go toolchain in this image), so no
+ * oracle/_ref build exists. The restatement is pinned by the reference's own known-answer tests,
+ * transcribed as fixtures under tests/golden/ (see tests/test_oracle_golden.py).
+ */
+#ifndef KG_ORACLE_H
+#define KG_ORACLE_H
+
+#include "../include/koordgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct kgo_pair {
+    uint32_t status;   /* KG_ST_* bits, 0 = feasible */
+    int64_t s_nrf, s_la, s_numa;
+    int64_t total;     /* -1 when infeasible */
+    int32_t zone;      /* NUMA zone Reserve would allocate from, -1 = none */
+} kgo_pair;
+
+/* One (pod, node) evaluation of every enabled plugin. */
+void kgo_eval_pair(const kg_config* cfg, const kg_node_columns* nodes, uint32_t node,
+                   const kg_pod_columns* pods, uint32_t pod, kgo_pair* out);
+
+/* Verify matrix, [n_pods][n_nodes]. */
+void kgo_eval_verify(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes,
+                     const kg_pod_columns* pods, uint32_t n_pods, kg_verify_out* out);
+
+/* selectHost with the build-defined deterministic tie-break: top-k packed keys per pod. */
+void kgo_select(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes, uint32_t index_base,
+                const kg_pod_columns* pods, uint32_t n_pods, uint32_t k, uint64_t* keys);
+
+/* Upstream-shaped CPU baseline: per pod, Filter over all nodes on n_workers threads with the
+ * chunked parallelizer of pkg/util/parallelize/parallelism.go:29-49, then Score over the feasible
+ * nodes the same way, then selectHost. keys: one key per pod. */
+int kgo_select_parallel(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes,
+                        uint32_t index_base, const kg_pod_columns* pods, uint32_t n_pods,
+                        int n_workers, uint64_t* keys);
+
+/* Mutable copy of a snapshot for Assume/replay. */
+typedef struct kgo_state kgo_state;
+kgo_state* kgo_state_new(const kg_node_columns* cols, uint32_t n_nodes);
+void kgo_state_free(kgo_state* st);
+/* Column view of the state (pointers stay valid until kgo_state_free). */
+void kgo_state_view(kgo_state* st, kg_node_columns* view);
+/* Reserve of pod on node (a16: NodeInfo.AddPod, podAssignCache.assign, NUMA Reserve). */
+void kgo_assume(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod);
+/* Unreserve (reverse of kgo_assume with the zone chosen at Reserve). */
+void kgo_forget(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod,
+                int32_t zone);
+/* One-pod-per-cycle scheduling with Assume between pods. */
+void kgo_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, const kg_pod_columns* pods,
+                uint32_t n_pods, int32_t* out_node, int64_t* out_total);
+
+/* Helpers shared with tests. */
+int64_t kgo_amplify(int64_t origin, double ratio);
+int64_t kgo_la_usage_percent(int64_t estimated, int64_t total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

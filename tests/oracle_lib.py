@@ -1,0 +1,148 @@
+"""ctypes binding of the CPU parity oracle (oracle/liboracle_kg.so). Test infrastructure only."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from koordinator_amd import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle_kg.so")
+
+_lib = None
+
+
+class KgoPair(C.Structure):
+    _fields_ = [("status", C.c_uint32), ("s_nrf", C.c_int64), ("s_la", C.c_int64), ("s_numa", C.c_int64),
+                ("total", C.c_int64), ("zone", C.c_int32)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = C.CDLL(ORACLE_SO)
+        P = C.POINTER
+        L.kgo_eval_pair.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
+                                    P(KgoPair)]
+        L.kgo_eval_verify.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns),
+                                      C.c_uint32, P(abi.KgVerifyOut)]
+        L.kgo_select.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32, P(abi.KgPodColumns),
+                                 C.c_uint32, C.c_uint32, P(C.c_uint64)]
+        L.kgo_select_parallel.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
+                                          P(abi.KgPodColumns), C.c_uint32, C.c_int, P(C.c_uint64)]
+        L.kgo_select_parallel.restype = C.c_int
+        L.kgo_state_new.argtypes = [P(abi.KgNodeColumns), C.c_uint32]
+        L.kgo_state_new.restype = C.c_void_p
+        L.kgo_state_free.argtypes = [C.c_void_p]
+        L.kgo_state_view.argtypes = [C.c_void_p, P(abi.KgNodeColumns)]
+        L.kgo_assume.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32]
+        L.kgo_forget.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32, C.c_int32]
+        L.kgo_replay.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
+                                 P(C.c_int32), P(C.c_int64)]
+        L.kgo_amplify.argtypes = [C.c_int64, C.c_double]
+        L.kgo_amplify.restype = C.c_int64
+        L.kgo_la_usage_percent.argtypes = [C.c_int64, C.c_int64]
+        L.kgo_la_usage_percent.restype = C.c_int64
+        _lib = L
+    return _lib
+
+
+def eval_pair(cfg, nodes: abi.Table, i: int, pods: abi.Table, j: int) -> KgoPair:
+    out = KgoPair()
+    nc, pc = abi.node_columns(nodes), abi.pod_columns(pods)
+    lib().kgo_eval_pair(C.byref(cfg), C.byref(nc), i, C.byref(pc), j, C.byref(out))
+    return out
+
+
+def eval_verify(cfg, nodes: abi.Table, pods: abi.Table) -> abi.VerifyResult:
+    nn, np_ = abi.table_len(nodes), abi.table_len(pods)
+    res = abi.VerifyResult(np_, nn)
+    nc, pc, vo = abi.node_columns(nodes), abi.pod_columns(pods), res.struct()
+    lib().kgo_eval_verify(C.byref(cfg), C.byref(nc), nn, C.byref(pc), np_, C.byref(vo))
+    return res
+
+
+def select(cfg, nodes: abi.Table, pods: abi.Table, k: int = 1, index_base: int = 0) -> np.ndarray:
+    nn, np_ = abi.table_len(nodes), abi.table_len(pods)
+    keys = np.zeros((np_, k), np.uint64)
+    nc, pc = abi.node_columns(nodes), abi.pod_columns(pods)
+    lib().kgo_select(C.byref(cfg), C.byref(nc), nn, index_base, C.byref(pc), np_, k,
+                     keys.ctypes.data_as(C.POINTER(C.c_uint64)))
+    return keys
+
+
+def select_parallel(cfg, nodes: abi.Table, pods: abi.Table, workers: int = 16, index_base: int = 0) -> np.ndarray:
+    nn, np_ = abi.table_len(nodes), abi.table_len(pods)
+    keys = np.zeros(np_, np.uint64)
+    nc, pc = abi.node_columns(nodes), abi.pod_columns(pods)
+    rc = lib().kgo_select_parallel(C.byref(cfg), C.byref(nc), nn, index_base, C.byref(pc), np_, workers,
+                                   keys.ctypes.data_as(C.POINTER(C.c_uint64)))
+    assert rc == 0
+    return keys
+
+
+class OracleState:
+    """Mutable oracle snapshot for Assume / replay."""
+
+    def __init__(self, cfg, nodes: abi.Table):
+        self.cfg = cfg
+        self.n = abi.table_len(nodes)
+        nc = abi.node_columns(nodes)
+        self.h = lib().kgo_state_new(C.byref(nc), self.n)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().kgo_state_free(self.h)
+            self.h = None
+
+    def assume(self, node: int, pods: abi.Table, pod: int):
+        pc = abi.pod_columns(pods)
+        lib().kgo_assume(C.byref(self.cfg), self.h, node, C.byref(pc), pod)
+
+    def forget(self, node: int, pods: abi.Table, pod: int, zone: int):
+        pc = abi.pod_columns(pods)
+        lib().kgo_forget(C.byref(self.cfg), self.h, node, C.byref(pc), pod, zone)
+
+    def replay(self, pods: abi.Table, index_base: int = 0):
+        np_ = abi.table_len(pods)
+        out_node = np.zeros(np_, np.int32)
+        out_total = np.zeros(np_, np.int64)
+        pc = abi.pod_columns(pods)
+        lib().kgo_replay(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_,
+                         out_node.ctypes.data_as(C.POINTER(C.c_int32)), out_total.ctypes.data_as(C.POINTER(C.c_int64)))
+        return out_node, out_total
+
+    def table(self) -> abi.Table:
+        """Copy of the current node columns."""
+        v = abi.KgNodeColumns()
+        lib().kgo_state_view(self.h, C.byref(v))
+        n = self.n
+        t = {}
+
+        def grab(ptr, dtype):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+        for k in ["alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "req_cpu", "req_mem", "req_eph", "num_pods",
+                  "nz_cpu", "nz_mem", "cpuset_alloc_milli"]:
+            t[k] = grab(getattr(v, k), np.int64)
+        for k in range(abi.KG_NSCALAR):
+            t[f"sc_alloc{k}"] = grab(v.sc_alloc[k], np.int64)
+            t[f"sc_req{k}"] = grab(v.sc_req[k], np.int64)
+        for name in ["la_alloc", "la_thr_usage", "la_thr_prod", "la_thr_agg", "la_fbase_np", "la_fbase_prod",
+                     "la_sbase_np", "la_sbase_prod"]:
+            for r in range(abi.KG_LA_R):
+                t[f"{name}{r}"] = grab(getattr(v, name)[r], np.int64)
+        for name in ["zone_cpu", "zone_mem", "zone_cpu_used", "zone_mem_used"]:
+            for z in range(abi.KG_MAX_ZONES):
+                t[f"{name}{z}"] = grab(getattr(v, name)[z], np.int64)
+        t["la_flags"] = grab(v.la_flags, np.uint32)
+        t["numa_policy"] = grab(v.numa_policy, np.uint32)
+        t["numa_zones"] = grab(v.numa_zones, np.uint32)
+        t["cpu_amp_ratio"] = grab(v.cpu_amp_ratio, np.float64)
+        return t
