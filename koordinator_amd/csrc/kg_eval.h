@@ -1,0 +1,300 @@
+// kg_eval.h — per-(pod, node) Filter/Score arithmetic on the device.
+//
+// One function evaluates every enabled plugin for one pair; the kernels differ only in how they
+// map pairs to lanes. The arithmetic restates (with the same integer results):
+//   NodeResourcesFit Fits + LeastAllocated   upstream k8s v1.35.6,
+//                                            mirror noderesourcefitplus/node_resource_fit_plus_utils.go:47-139
+//   LoadAwareScheduling Filter / Score       loadaware/load_aware.go:150-220, 235-292, 316-376
+//   NodeNUMAResource Filter / Score          nodenumaresource/plugin.go:363-498, scoring.go:67-151,
+//                                            topology_hint.go:31-41, resource_manager.go:272-318,529-626,
+//                                            frameworkext/topologymanager/policy.go:198-256
+// Divisions: Go's truncating int64 division of non-negative operands is computed as an exactly
+// corrected IEEE-double quotient (operands are < 2^46 — the host checks and otherwise selects the
+// EXACT=true instantiation that divides in int64). The LoadAware usage-percent filter
+// int64(math.Round(float64(e)/float64(t)*100)) <= thr is monotone in e; the host turns it into an
+// exact integer cut-off per node, so the kernel compares integers only.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/koordgpu.h"
+#include "kg_layout.h"
+
+namespace kg {
+
+struct PodV {
+    int64_t req_cpu, req_mem, req_eph, sc0, sc1, nz_cpu, nz_mem, est0, est1;
+    uint32_t flags;
+};
+
+__device__ __forceinline__ PodV load_pod(const PodsDev& P, uint32_t j) {
+    PodV p;
+    p.req_cpu = P.req_cpu[j];
+    p.req_mem = P.req_mem[j];
+    p.req_eph = P.req_eph[j];
+    p.sc0 = P.sc_req0[j];
+    p.sc1 = P.sc_req1[j];
+    p.nz_cpu = P.nz_cpu[j];
+    p.nz_mem = P.nz_mem[j];
+    p.est0 = P.la_est0[j];
+    p.est1 = P.la_est1[j];
+    p.flags = P.flags[j];
+    return p;
+}
+
+__device__ __forceinline__ double as_f64(int64_t bits) { return __longlong_as_double(bits); }
+
+// leastRequestedScore(requested, capacity) = ((capacity - requested) * 100) / capacity,
+// 0 when capacity == 0 or requested > capacity.
+template <bool EXACT>
+__device__ __forceinline__ int64_t least_req(int64_t requested, int64_t capacity, double rcp) {
+    const int64_t x = capacity - requested;
+    const bool zero = (capacity == 0) | (x < 0);
+    if constexpr (EXACT) {
+        const int64_t cap = zero ? 1 : capacity;
+        return zero ? 0 : ((zero ? 0 : x) * 100) / cap;
+    } else {
+        const double cap_d = (double)capacity;
+        const double t = (double)x * 100.0;  // exact when |x| < 2^46
+        double q = floor(t * rcp);
+        const double r = fma(-q, cap_d, t);  // exact remainder t - q*cap
+        q += (r < 0.0) ? -1.0 : ((r >= cap_d) ? 1.0 : 0.0);
+        int64_t s = (int64_t)(int32_t)q;
+        // operands outside the exact-double range (|x| or capacity >= 2^46): Go's int64 arithmetic
+        // (wrapping multiply, truncating divide) on the rare lanes that need it
+        const bool big = ((uint64_t)(x + (1ll << 46)) >= (1ull << 47)) | (capacity >= (1ll << 46));
+        if (__builtin_expect(big & !zero, 0)) s = (int64_t)((uint64_t)x * 100ull) / capacity;
+        return zero ? 0 : s;
+    }
+}
+
+// Σ score / Σ weight for small non-negative operands (weights are validated on the host).
+__device__ __forceinline__ int64_t wdiv(int64_t sum, int64_t wsum) {
+    return wsum == 0 ? 0 : (int64_t)((uint32_t)sum / (uint32_t)(wsum == 0 ? 1 : wsum));
+}
+
+template <bool EXACT>
+__device__ __forceinline__ int64_t numa_least(int64_t w_cpu, int64_t w_mem, int64_t alloc_cpu, int64_t req_cpu,
+                                              double rcp_cpu, int64_t alloc_mem, int64_t req_mem, double rcp_mem) {
+    int64_t sum = 0, wsum = 0;
+    const bool on_c = (alloc_cpu != 0) & (w_cpu != 0);
+    const bool on_m = (alloc_mem != 0) & (w_mem != 0);
+    sum += on_c ? least_req<EXACT>(req_cpu, alloc_cpu, rcp_cpu) * w_cpu : 0;
+    wsum += on_c ? w_cpu : 0;
+    sum += on_m ? least_req<EXACT>(req_mem, alloc_mem, rcp_mem) * w_mem : 0;
+    wsum += on_m ? w_mem : 0;
+    return wdiv(sum, wsum);
+}
+
+struct PairOut {
+    uint32_t status;
+    int64_t s_nrf, s_la, s_numa;
+    int32_t zone;
+};
+
+// NodeNUMAResource Filter + Score for a SingleNUMANode / None node.
+template <bool EXACT>
+__device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restrict__ n, const ZoneRec* __restrict__ zr,
+                                          const PodV& p, uint32_t flags, PairOut& o) {
+    if (p.flags & KG_POD_NUMA_SKIP) return;
+    if (p.flags & KG_POD_CPU_BIND) {
+        o.status |= KG_ST_UNSUPPORTED;
+        return;
+    }
+    const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u;
+    const uint32_t pod_pol = (p.flags >> 16) & 15u;
+    if (node_pol != KG_NUMA_NONE && pod_pol != KG_NUMA_NONE && pod_pol != node_pol) {
+        o.status |= KG_ST_NUMA_CONFLICT;
+        return;
+    }
+    const uint32_t pol = pod_pol != KG_NUMA_NONE ? pod_pol : node_pol;
+    if (pol == KG_NUMA_RESTRICTED || pol == KG_NUMA_BEST_EFFORT) {
+        o.status |= KG_ST_UNSUPPORTED;
+        return;
+    }
+    const bool amp = (flags & F_AMP) != 0;
+    const int64_t pod_cpu = p.req_cpu;
+    // filterAmplifiedCPUs
+    if (pod_cpu != 0 && amp) {
+        int64_t requested = n[N_REQ_CPU];
+        const int64_t cs = n[N_CPUSET];
+        if (requested >= cs && cs > 0) requested = requested - cs + n[N_AMP_CPUSET];
+        if (pod_cpu > n[N_ALLOC_CPU] - requested) {
+            o.status |= KG_ST_NUMA_AMP_CPU;
+            return;
+        }
+    }
+    const double rcp_cpu = as_f64(n[N_RCP_CPU]), rcp_mem = as_f64(n[N_RCP_MEM]);
+    if (pol == KG_NUMA_SINGLE_NODE) {
+        const uint32_t Z = (flags >> F_NUMA_ZONES_SHIFT) & 15u;
+        if (Z == 0) {
+            o.status |= KG_ST_NUMA_NO_RES;
+            return;
+        }
+        const bool has_cpu = (p.flags & KG_POD_HAS_CPU) != 0, has_mem = (p.flags & KG_POD_HAS_MEM) != 0;
+        int32_t best = -1;
+        if (has_cpu || has_mem) {
+            int64_t best_score = 0;
+            for (uint32_t z = 0; z < Z; z++) {
+                const int64_t tc = zr->cpu[z], tm = zr->mem[z];
+                const int64_t uc = zr->cpu_used[z], um = zr->mem_used[z];
+                const int64_t ac = tc - uc < 0 ? 0 : tc - uc;
+                const int64_t am = tm - um < 0 ? 0 : tm - um;
+                const bool ok = (!has_cpu || (ac != 0 && p.req_cpu <= ac)) && (!has_mem || (am != 0 && p.req_mem <= am));
+                const int64_t rc = tc - ac < 0 ? 0 : tc - ac;
+                const int64_t rm = tm - am < 0 ? 0 : tm - am;
+                const int64_t s = numa_least<EXACT>(c.numa_hint_w_cpu, c.numa_hint_w_mem, tc, rc + p.req_cpu,
+                                                    zr->rcp_cpu[z], tm, rm + p.req_mem, zr->rcp_mem[z]);
+                const bool take = ok && (best < 0 || s > best_score);
+                best = take ? (int32_t)z : best;
+                best_score = take ? s : best_score;
+            }
+            if (best < 0) {
+                o.status |= KG_ST_NUMA_ALIGN;
+                return;
+            }
+        }
+        if (best < 0 || Z == 1) {  // best hint == default affinity: no NUMA allocation
+            o.zone = -1;
+            o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], n[N_REQ_CPU] + pod_cpu, rcp_cpu,
+                                         n[N_ALLOC_MEM], n[N_REQ_MEM] + p.req_mem, rcp_mem);
+            return;
+        }
+        o.zone = best;
+        o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, zr->cpu[best], zr->cpu_used[best] + pod_cpu,
+                                     zr->rcp_cpu[best], zr->mem[best], zr->mem_used[best] + p.req_mem,
+                                     zr->rcp_mem[best]);
+        return;
+    }
+    // policy None: scoreWithAmplifiedCPUs
+    int64_t req_cpu = n[N_REQ_CPU];
+    if (pod_cpu != 0 && amp) req_cpu = req_cpu - n[N_CPUSET] + n[N_AMP_CPUSET];
+    o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], req_cpu + pod_cpu, rcp_cpu,
+                                 n[N_ALLOC_MEM], n[N_REQ_MEM] + p.req_mem, rcp_mem);
+}
+
+template <bool EXACT>
+__device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __restrict__ n,
+                                             const ZoneRec* __restrict__ zr, const PodV& p) {
+    PairOut o;
+    o.status = 0;
+    o.s_nrf = o.s_la = o.s_numa = 0;
+    o.zone = -1;
+    const uint32_t flags = (uint32_t)n[N_FLAGS];
+
+    if (c.plugins & KG_PLUGIN_NRF) {
+        // Fits
+        uint32_t st = 0;
+        st |= (n[N_NUM_PODS] + 1 > n[N_ALLOC_PODS]) ? KG_ST_NRF_PODS : 0u;
+        st |= (p.req_cpu > 0 && p.req_cpu > n[N_ALLOC_CPU] - n[N_REQ_CPU]) ? KG_ST_NRF_CPU : 0u;
+        st |= (p.req_mem > 0 && p.req_mem > n[N_ALLOC_MEM] - n[N_REQ_MEM]) ? KG_ST_NRF_MEM : 0u;
+        st |= (p.req_eph > 0 && p.req_eph > n[N_ALLOC_EPH] - n[N_REQ_EPH]) ? KG_ST_NRF_EPH : 0u;
+        st |= (p.sc0 != 0 && p.sc0 > n[N_SC_ALLOC0] - n[N_SC_REQ0]) ? KG_ST_NRF_SC0 : 0u;
+        st |= (p.sc1 != 0 && p.sc1 > n[N_SC_ALLOC1] - n[N_SC_REQ1]) ? KG_ST_NRF_SC1 : 0u;
+        o.status |= st;
+        // LeastAllocated over {cpu, memory, scalar0, scalar1}
+        int64_t sum = 0, wsum = 0;
+        {
+            const int64_t cap = n[N_ALLOC_CPU], w = c.nrf_w[0];
+            const bool on = (w != 0) & (cap != 0);
+            sum += on ? least_req<EXACT>(n[N_NZ_CPU] + p.nz_cpu, cap, as_f64(n[N_RCP_CPU])) * w : 0;
+            wsum += on ? w : 0;
+        }
+        {
+            const int64_t cap = n[N_ALLOC_MEM], w = c.nrf_w[1];
+            const bool on = (w != 0) & (cap != 0);
+            sum += on ? least_req<EXACT>(n[N_NZ_MEM] + p.nz_mem, cap, as_f64(n[N_RCP_MEM])) * w : 0;
+            wsum += on ? w : 0;
+        }
+        {
+            const int64_t cap = n[N_SC_ALLOC0], w = c.nrf_w[2];
+            const bool on = (w != 0) & (cap != 0) & (p.sc0 != 0);
+            sum += on ? least_req<EXACT>(n[N_SC_REQ0] + p.sc0, cap, as_f64(n[N_RCP_SC0])) * w : 0;
+            wsum += on ? w : 0;
+        }
+        {
+            const int64_t cap = n[N_SC_ALLOC1], w = c.nrf_w[3];
+            const bool on = (w != 0) & (cap != 0) & (p.sc1 != 0);
+            sum += on ? least_req<EXACT>(n[N_SC_REQ1] + p.sc1, cap, as_f64(n[N_RCP_SC1])) * w : 0;
+            wsum += on ? w : 0;
+        }
+        o.s_nrf = wdiv(sum, wsum);
+    }
+
+    if (c.plugins & KG_PLUGIN_LA) {
+        // Filter
+        if (!(p.flags & KG_POD_DAEMONSET)) {
+            const bool prod = (flags & F_LA_PROD_THR) && (p.flags & KG_POD_PROD);
+            const uint32_t mode = (flags >> (prod ? F_LA_FMODE_PROD_SHIFT : F_LA_FMODE_NP_SHIFT)) & 3u;
+            if (mode == FMODE_FAIL_EXPIRED) {
+                o.status |= KG_ST_LA_EXPIRED;
+            } else if (mode == FMODE_CHECK) {
+                const int64_t e0 = (prod ? n[N_LA_FBASE_PROD0] : n[N_LA_FBASE_NP0]) + p.est0;
+                const int64_t e1 = (prod ? n[N_LA_FBASE_PROD1] : n[N_LA_FBASE_NP1]) + p.est1;
+                const int64_t c0 = prod ? n[N_LA_FCUT_PROD0] : n[N_LA_FCUT_NP0];
+                const int64_t c1 = prod ? n[N_LA_FCUT_PROD1] : n[N_LA_FCUT_NP1];
+                const uint32_t agg = (!prod && (flags & F_LA_NP_AGG)) ? KG_ST_LA_AGG : 0u;
+                o.status |= (e0 > c0) ? (KG_ST_LA_CPU | agg) : ((e1 > c1) ? (KG_ST_LA_MEM | agg) : 0u);
+            }
+        }
+        // Score
+        if (c.la_score_enabled && !(flags & F_LA_SCORE_ZERO)) {
+            const bool prod = c.la_score_prod && (p.flags & KG_POD_PROD);
+            const int64_t u0 = (prod ? n[N_LA_SBASE_PROD0] : n[N_LA_SBASE_NP0]) + p.est0;
+            const int64_t u1 = (prod ? n[N_LA_SBASE_PROD1] : n[N_LA_SBASE_NP1]) + p.est1;
+            const int64_t s0 = least_req<EXACT>(u0, n[N_LA_ALLOC0], as_f64(n[N_RCP_LA0]));
+            const int64_t s1 = least_req<EXACT>(u1, n[N_LA_ALLOC1], as_f64(n[N_RCP_LA1]));
+            int64_t dom = c.la_dom_w != 0 ? 100 : 0;
+            dom = dom > s0 ? s0 : dom;
+            dom = dom > s1 ? s1 : dom;
+            const int64_t sum = s0 * c.la_w[0] + s1 * c.la_w[1] + dom * c.la_dom_w;
+            o.s_la = c.la_wsum <= 0 ? 0 : wdiv(sum, c.la_wsum);
+        }
+    }
+
+    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT>(c, n, zr, p, flags, o);
+    if (o.status & (KG_ST_NUMA_MASK | KG_ST_UNSUPPORTED)) o.s_numa = 0;
+    if (o.status) o.zone = -1;
+    return o;
+}
+
+__device__ __forceinline__ int64_t pair_total(const KCfg& c, const PairOut& o) {
+    return c.w_nrf * o.s_nrf + c.w_la * o.s_la + c.w_numa * o.s_numa;
+}
+
+__device__ __forceinline__ uint64_t pair_key(const KCfg& c, const PairOut& o, uint32_t gidx) {
+    const uint64_t key = ((uint64_t)pair_total(c, o) << 32) | (uint64_t)(0xFFFFFFFFu - gidx);
+    return o.status ? 0ull : key;
+}
+
+// Reserve (sign = +1) / Unreserve (sign = -1) of pod p on node record n (a16).
+__device__ __forceinline__ void apply_assume(const KCfg& c, int64_t* n, ZoneRec* zr, const PodV& p, int32_t zone,
+                                             int64_t sign) {
+    n[N_REQ_CPU] += sign * p.req_cpu;
+    n[N_REQ_MEM] += sign * p.req_mem;
+    n[N_REQ_EPH] += sign * p.req_eph;
+    n[N_SC_REQ0] += sign * p.sc0;
+    n[N_SC_REQ1] += sign * p.sc1;
+    n[N_NZ_CPU] += sign * p.nz_cpu;
+    n[N_NZ_MEM] += sign * p.nz_mem;
+    n[N_NUM_PODS] += sign;
+    const uint32_t flags = (uint32_t)n[N_FLAGS];
+    if ((c.plugins & KG_PLUGIN_LA) && (flags & F_LA_HAS_METRIC)) {
+        const int64_t d0 = sign * (p.est0 > 0 ? p.est0 : 0), d1 = sign * (p.est1 > 0 ? p.est1 : 0);
+        n[N_LA_FBASE_NP0] += d0;
+        n[N_LA_FBASE_NP1] += d1;
+        n[N_LA_SBASE_NP0] += d0;
+        n[N_LA_SBASE_NP1] += d1;
+        if (p.flags & KG_POD_PROD) {
+            n[N_LA_FBASE_PROD0] += d0;
+            n[N_LA_FBASE_PROD1] += d1;
+            n[N_LA_SBASE_PROD0] += d0;
+            n[N_LA_SBASE_PROD1] += d1;
+        }
+    }
+    if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES) {
+        zr->cpu_used[zone] += sign * p.req_cpu;
+        zr->mem_used[zone] += sign * p.req_mem;
+    }
+}
+
+}  // namespace kg

@@ -1,0 +1,39 @@
+// kg_kernels.h — host-side launch interface of the device kernels (internal to libkoordgpu.so).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include "kg_layout.h"
+
+namespace kg {
+
+constexpr int KG_TOPK_MAX = 4;  // select kernels are instantiated for K = 1 and K = 4 (k <= 4)
+
+struct LaunchSelect {
+    const NodeRec* nodes;
+    const ZoneRec* zones;
+    PodsDev pods;
+    uint32_t n_pods, n_nodes, chunk, n_chunks, index_base, k;
+    bool exact;
+    KCfg cfg;
+    uint64_t* partial;
+};
+
+struct VerifyDev {
+    uint32_t* status;
+    int64_t *s_nrf, *s_la, *s_numa, *total;
+    int8_t* zone;
+};
+
+hipError_t launch_select(const LaunchSelect& a, hipStream_t s);
+hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k, uint64_t* out,
+                        hipStream_t s);
+hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, uint32_t n_pods,
+                         uint32_t n_nodes, const KCfg& cfg, bool exact, const VerifyDev& o, hipStream_t s);
+hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t n_pods, uint32_t n_nodes,
+                              uint32_t index_base, const KCfg& cfg, bool exact, const uint32_t* step_base,
+                              uint32_t step_off, uint64_t* winners, hipStream_t s);
+hipError_t launch_bump(uint32_t* step_base, uint32_t by, hipStream_t s);
+hipError_t launch_assume(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t pod, uint32_t node,
+                         int32_t zone, int64_t sign, const KCfg& cfg, bool exact, int32_t* zone_out, hipStream_t s);
+
+}  // namespace kg

@@ -1,0 +1,863 @@
+// kg_runtime.cpp — host runtime behind the C ABI of include/koordgpu.h.
+//
+// Owns the device-resident node snapshot (one record per node, see kg_layout.h), the pod batches
+// and their result buffers, the launch sequencing on one HIP stream per context, the event-based
+// timing of the dominant kernel, and the RCCL communicator of the node-sharded multi-GPU mode.
+// Host-side derivations done once per node row at upload (never per evaluation):
+//   * LoadAware usage-threshold cut-offs: the largest estimated usage e with
+//     int64(math.Round(float64(e)/float64(total)*100)) <= threshold (load_aware.go:326), found by
+//     bisection on the exact float64 expression (it is monotone in e);
+//   * per-profile LoadAware filter modes (thresholds empty / NodeMetric missing / expired / nil,
+//     load_aware.go:175-210) and the Score's zero cases (:265-279);
+//   * reciprocals of the static divisors (allocatable, zone totals) for the corrected quotient;
+//   * extension.Amplify of the node's cpuset-allocated milli-cpu (node_resource_amplification.go:170).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/koordgpu.h"
+#include "kg_kernels.h"
+#include "kg_layout.h"
+
+using namespace kg;
+
+struct kg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::mutex mu;  // serialises calls on one context (Unreserve may arrive from binding goroutines)
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_live;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free;
+    double prof_ms = 0.0;
+    uint64_t prof_launches = 0;
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+};
+
+struct kg_snap {
+    kg_ctx* ctx = nullptr;
+    kg_config cfg{};
+    KCfg kcfg{};
+    uint32_t n = 0, base = 0;
+    NodeRec* d_nodes = nullptr;
+    ZoneRec* d_zones = nullptr;
+    std::vector<NodeRec> h_nodes;
+    std::vector<ZoneRec> h_zones;
+    bool uploaded = false;
+};
+
+struct kg_pods {
+    kg_ctx* ctx = nullptr;
+    uint32_t cap = 0, n = 0;
+    int64_t* d_cols = nullptr;  // 9 int64 columns of `cap` entries
+    uint32_t* d_flags = nullptr;
+    PodsDev dev{};
+    // select results
+    uint64_t* d_partial = nullptr;
+    size_t partial_cap = 0;  // entries
+    uint64_t* d_keys = nullptr;
+    uint32_t k_last = 0, kk_last = 0;
+    // replay / shard scratch
+    uint64_t* d_winners = nullptr;
+    uint32_t* d_step = nullptr;
+    uint64_t* d_gather = nullptr;
+    size_t gather_cap = 0;
+};
+
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+kg_status fail(kg_ctx* ctx, kg_status s, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return s;
+}
+
+#define HIP_TRY(ctx, expr)                                                                                     \
+    do {                                                                                                       \
+        hipError_t e_ = (expr);                                                                                \
+        if (e_ != hipSuccess)                                                                                  \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? KG_OOM : KG_DEVICE_ERROR, "%s: %s (%s:%d)", #expr, \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                                            \
+    } while (0)
+
+#define NCCL_TRY(ctx, expr)                                                                                    \
+    do {                                                                                                       \
+        ncclResult_t r_ = (expr);                                                                              \
+        if (r_ != ncclSuccess)                                                                                 \
+            return fail((ctx), KG_DEVICE_ERROR, "%s: %s", #expr, ncclGetErrorString(r_));                     \
+    } while (0)
+
+constexpr int64_t I64_MAX = std::numeric_limits<int64_t>::max();
+
+int64_t amplify(int64_t origin, double ratio) {
+    if (ratio <= 1) return origin;
+    return (int64_t)std::ceil((double)origin * ratio);
+}
+
+// usage-percent predicate of filterNodeUsage, evaluated in float64 exactly as Go does
+bool usage_ok(int64_t e, int64_t total, int64_t thr) {
+    volatile double q = (double)e / (double)total;  // volatile: keep the two roundings separate
+    volatile double p = q * 100.0;
+    double r = std::round(p);
+    return r <= (double)thr;
+}
+
+// largest e with usage_ok(e) (cut-off), I64_MAX when no check applies
+int64_t la_cut(int64_t thr, int64_t total) {
+    if (thr == 0 || total == 0) return I64_MAX;
+    if (!usage_ok(0, total, thr)) return -1;
+    const int64_t top = (int64_t)1 << 53;
+    if (usage_ok(top, total, thr)) return I64_MAX;
+    int64_t lo = 0, hi = top;  // usage_ok(lo) && !usage_ok(hi)
+    while (hi - lo > 1) {
+        int64_t mid = lo + (hi - lo) / 2;
+        if (usage_ok(mid, total, thr))
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+int64_t rcp_bits(int64_t x) {
+    double r = x != 0 ? 1.0 / (double)x : 0.0;
+    int64_t b;
+    std::memcpy(&b, &r, 8);
+    return b;
+}
+
+bool valid_weight(int64_t w) { return w >= 0 && w <= (1 << 20); }
+
+kg_status build_kcfg(kg_ctx* ctx, const kg_config* c, KCfg* k) {
+    std::memset(k, 0, sizeof(*k));
+    const int64_t ws[] = {c->weight_nrf, c->weight_la, c->weight_numa, c->nrf_w_cpu, c->nrf_w_mem, c->nrf_w_sc[0],
+                          c->nrf_w_sc[1], c->la_w[0], c->la_w[1], c->la_dominant_w, c->numa_w_cpu, c->numa_w_mem,
+                          c->numa_hint_w_cpu, c->numa_hint_w_mem};
+    for (int64_t w : ws)
+        if (!valid_weight(w)) return fail(ctx, KG_INVALID_ARG, "weight %lld outside [0, 2^20]", (long long)w);
+    if (c->plugins & ~(KG_PLUGIN_NRF | KG_PLUGIN_LA | KG_PLUGIN_NUMA))
+        return fail(ctx, KG_UNSUPPORTED, "plugins mask 0x%x", c->plugins);
+    k->plugins = c->plugins;
+    k->la_score_enabled = c->la_score_enabled;
+    k->la_score_prod = c->la_score_prod;
+    k->w_nrf = c->weight_nrf;
+    k->w_la = c->weight_la;
+    k->w_numa = c->weight_numa;
+    k->nrf_w[0] = c->nrf_w_cpu;
+    k->nrf_w[1] = c->nrf_w_mem;
+    k->nrf_w[2] = c->nrf_w_sc[0];
+    k->nrf_w[3] = c->nrf_w_sc[1];
+    k->la_w[0] = c->la_w[0];
+    k->la_w[1] = c->la_w[1];
+    k->la_dom_w = c->la_dominant_w;
+    k->la_wsum = c->la_dominant_w + c->la_w[0] + c->la_w[1];
+    k->numa_w_cpu = c->numa_w_cpu;
+    k->numa_w_mem = c->numa_w_mem;
+    k->numa_hint_w_cpu = c->numa_hint_w_cpu;
+    k->numa_hint_w_mem = c->numa_hint_w_mem;
+    return KG_OK;
+}
+
+uint32_t la_fmode(const kg_config& c, uint32_t la_flags, const int64_t* thr) {
+    bool empty = true;
+    for (int r = 0; r < KG_LA_R; r++)
+        if (thr[r] != 0) empty = false;
+    if (empty) return FMODE_PASS;
+    if (!(la_flags & KG_LA_HAS_METRIC)) return FMODE_PASS;
+    if (c.la_filter_expired && (la_flags & KG_LA_EXPIRED)) return c.la_schedule_expired ? FMODE_PASS : FMODE_FAIL_EXPIRED;
+    if (la_flags & KG_LA_NM_NIL) return FMODE_PASS;
+    return FMODE_CHECK;
+}
+
+#define COL(p, i) ((p) ? (p)[i] : 0)
+
+kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, uint32_t i, NodeRec* rec, ZoneRec* zr) {
+    std::memset(rec, 0, sizeof(*rec));
+    std::memset(zr, 0, sizeof(*zr));
+    int64_t* v = rec->v;
+    v[N_ALLOC_CPU] = COL(s->alloc_cpu, i);
+    v[N_ALLOC_MEM] = COL(s->alloc_mem, i);
+    v[N_ALLOC_EPH] = COL(s->alloc_eph, i);
+    v[N_ALLOC_PODS] = COL(s->alloc_pods, i);
+    v[N_REQ_CPU] = COL(s->req_cpu, i);
+    v[N_REQ_MEM] = COL(s->req_mem, i);
+    v[N_REQ_EPH] = COL(s->req_eph, i);
+    v[N_NUM_PODS] = COL(s->num_pods, i);
+    v[N_NZ_CPU] = COL(s->nz_cpu, i);
+    v[N_NZ_MEM] = COL(s->nz_mem, i);
+    v[N_SC_ALLOC0] = COL(s->sc_alloc[0], i);
+    v[N_SC_ALLOC1] = COL(s->sc_alloc[1], i);
+    v[N_SC_REQ0] = COL(s->sc_req[0], i);
+    v[N_SC_REQ1] = COL(s->sc_req[1], i);
+    for (int64_t x : {v[N_ALLOC_CPU], v[N_ALLOC_MEM], v[N_SC_ALLOC0], v[N_SC_ALLOC1]})
+        if (x < 0) return fail(ctx, KG_INVALID_ARG, "node %u: negative allocatable", i);
+    const uint32_t laf = COL(s->la_flags, i);
+    int64_t thr_u[KG_LA_R], thr_p[KG_LA_R], thr_a[KG_LA_R], la_alloc[KG_LA_R];
+    for (int r = 0; r < KG_LA_R; r++) {
+        la_alloc[r] = COL(s->la_alloc[r], i);
+        if (la_alloc[r] < 0) return fail(ctx, KG_INVALID_ARG, "node %u: negative LoadAware allocatable", i);
+        thr_u[r] = COL(s->la_thr_usage[r], i);
+        thr_p[r] = COL(s->la_thr_prod[r], i);
+        thr_a[r] = COL(s->la_thr_agg[r], i);
+    }
+    const int64_t* thr_np = (laf & KG_LA_AGG_THR) ? thr_a : thr_u;
+    v[N_LA_ALLOC0] = la_alloc[0];
+    v[N_LA_ALLOC1] = la_alloc[1];
+    v[N_LA_FCUT_NP0] = la_cut(thr_np[0], la_alloc[0]);
+    v[N_LA_FCUT_NP1] = la_cut(thr_np[1], la_alloc[1]);
+    v[N_LA_FCUT_PROD0] = la_cut(thr_p[0], la_alloc[0]);
+    v[N_LA_FCUT_PROD1] = la_cut(thr_p[1], la_alloc[1]);
+    v[N_LA_FBASE_NP0] = COL(s->la_fbase_np[0], i);
+    v[N_LA_FBASE_NP1] = COL(s->la_fbase_np[1], i);
+    v[N_LA_FBASE_PROD0] = COL(s->la_fbase_prod[0], i);
+    v[N_LA_FBASE_PROD1] = COL(s->la_fbase_prod[1], i);
+    v[N_LA_SBASE_NP0] = COL(s->la_sbase_np[0], i);
+    v[N_LA_SBASE_NP1] = COL(s->la_sbase_np[1], i);
+    v[N_LA_SBASE_PROD0] = COL(s->la_sbase_prod[0], i);
+    v[N_LA_SBASE_PROD1] = COL(s->la_sbase_prod[1], i);
+    uint32_t f = 0;
+    f |= la_fmode(c, laf, thr_np) << F_LA_FMODE_NP_SHIFT;
+    f |= la_fmode(c, laf, thr_p) << F_LA_FMODE_PROD_SHIFT;
+    if (laf & KG_LA_AGG_THR) f |= F_LA_NP_AGG;
+    if (laf & KG_LA_PROD_THR) f |= F_LA_PROD_THR;
+    if (!(laf & KG_LA_HAS_METRIC) || (laf & KG_LA_EXPIRED) || (laf & KG_LA_NM_NIL)) f |= F_LA_SCORE_ZERO;
+    if (laf & KG_LA_HAS_METRIC) f |= F_LA_HAS_METRIC;
+    const uint32_t pol = COL(s->numa_policy, i);
+    const uint32_t Z = COL(s->numa_zones, i);
+    if (pol > KG_NUMA_SINGLE_NODE) return fail(ctx, KG_INVALID_ARG, "node %u: NUMA policy %u", i, pol);
+    if (Z > KG_MAX_ZONES) return fail(ctx, KG_UNSUPPORTED, "node %u: %u NUMA zones > %d", i, Z, KG_MAX_ZONES);
+    f |= pol << F_NUMA_POLICY_SHIFT;
+    f |= Z << F_NUMA_ZONES_SHIFT;
+    const double ratio = s->cpu_amp_ratio ? s->cpu_amp_ratio[i] : 0.0;
+    if (ratio > 1) f |= F_AMP;
+    v[N_FLAGS] = f;
+    v[N_CPUSET] = COL(s->cpuset_alloc_milli, i);
+    v[N_AMP_CPUSET] = amplify(v[N_CPUSET], ratio);
+    v[N_RCP_CPU] = rcp_bits(v[N_ALLOC_CPU]);
+    v[N_RCP_MEM] = rcp_bits(v[N_ALLOC_MEM]);
+    v[N_RCP_SC0] = rcp_bits(v[N_SC_ALLOC0]);
+    v[N_RCP_SC1] = rcp_bits(v[N_SC_ALLOC1]);
+    v[N_RCP_LA0] = rcp_bits(la_alloc[0]);
+    v[N_RCP_LA1] = rcp_bits(la_alloc[1]);
+    for (int z = 0; z < KG_MAX_ZONES; z++) {
+        zr->cpu[z] = COL(s->zone_cpu[z], i);
+        zr->mem[z] = COL(s->zone_mem[z], i);
+        zr->cpu_used[z] = COL(s->zone_cpu_used[z], i);
+        zr->mem_used[z] = COL(s->zone_mem_used[z], i);
+        if (zr->cpu[z] < 0 || zr->mem[z] < 0) return fail(ctx, KG_INVALID_ARG, "node %u: negative zone total", i);
+        zr->rcp_cpu[z] = zr->cpu[z] ? 1.0 / (double)zr->cpu[z] : 0.0;
+        zr->rcp_mem[z] = zr->mem[z] ? 1.0 / (double)zr->mem[z] : 0.0;
+    }
+    return KG_OK;
+}
+
+bool force_exact() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("KG_FORCE_EXACT");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
+// Node chunk of the select kernel: enough (pod-block, chunk) workgroups to fill 256 CUs several
+// times over, while each wave still walks a long run of nodes.
+uint32_t select_chunk(uint32_t n_nodes, uint32_t n_pods) {
+    const uint32_t pod_blocks = (n_pods + 255) / 256;
+    const uint32_t target_blocks = 2048;
+    uint32_t n_chunks = std::max<uint32_t>(1, (target_blocks + pod_blocks - 1) / pod_blocks);
+    uint32_t chunk = (n_nodes + n_chunks - 1) / n_chunks;
+    chunk = std::max<uint32_t>(chunk, 32);
+    return std::max<uint32_t>(1, std::min<uint32_t>(chunk, std::max<uint32_t>(n_nodes, 1)));
+}
+
+kg_status record_begin(kg_ctx* ctx, hipEvent_t* a, hipEvent_t* b) {
+    *a = *b = nullptr;
+    if (!ctx->profiling) return KG_OK;
+    if (!ctx->ev_free.empty()) {
+        *a = ctx->ev_free.back().first;
+        *b = ctx->ev_free.back().second;
+        ctx->ev_free.pop_back();
+    } else {
+        HIP_TRY(ctx, hipEventCreate(a));
+        HIP_TRY(ctx, hipEventCreate(b));
+    }
+    HIP_TRY(ctx, hipEventRecord(*a, ctx->stream));
+    return KG_OK;
+}
+
+kg_status record_end(kg_ctx* ctx, hipEvent_t a, hipEvent_t b) {
+    if (!a) return KG_OK;
+    HIP_TRY(ctx, hipEventRecord(b, ctx->stream));
+    ctx->ev_live.emplace_back(a, b);
+    return KG_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+int kg_abi_version(void) { return KG_ABI_VERSION; }
+
+const char* kg_status_string(kg_status s) {
+    switch (s) {
+        case KG_OK: return "ok";
+        case KG_INVALID_ARG: return "invalid argument";
+        case KG_DEVICE_ERROR: return "device error";
+        case KG_OOM: return "out of device memory";
+        case KG_UNSUPPORTED: return "unsupported on the device path";
+        case KG_NO_DEVICE: return "no device";
+    }
+    return "unknown";
+}
+
+int kg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+kg_status kg_open(int device, kg_ctx** out) {
+    if (!out) return KG_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return KG_NO_DEVICE;
+    if (device < 0 || device >= n) return KG_INVALID_ARG;
+    kg_ctx* ctx = new kg_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return KG_DEVICE_ERROR;
+    }
+    *out = ctx;
+    return KG_OK;
+}
+
+kg_status kg_close(kg_ctx* ctx) {
+    if (!ctx) return KG_INVALID_ARG;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
+    for (auto& e : ctx->ev_live) {
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+    }
+    for (auto& e : ctx->ev_free) {
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+    }
+    hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return KG_OK;
+}
+
+const char* kg_last_error(const kg_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+kg_status kg_sync(kg_ctx* ctx) {
+    if (!ctx) return KG_INVALID_ARG;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
+kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes, uint32_t index_base, kg_snap** out) {
+    if (!ctx || !cfg || !out) return KG_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    *out = nullptr;
+    if ((uint64_t)index_base + n_nodes > 0x7FFFFFFFull)
+        return fail(ctx, KG_INVALID_ARG, "node index range exceeds 2^31");
+    kg_snap* s = new kg_snap();
+    s->ctx = ctx;
+    s->cfg = *cfg;
+    kg_status st = build_kcfg(ctx, cfg, &s->kcfg);
+    if (st != KG_OK) {
+        delete s;
+        return st;
+    }
+    s->n = n_nodes;
+    s->base = index_base;
+    s->h_nodes.resize(n_nodes);
+    s->h_zones.resize(n_nodes);
+    hipSetDevice(ctx->device);
+    const size_t nb = sizeof(NodeRec) * std::max<uint32_t>(n_nodes, 1), zb = sizeof(ZoneRec) * std::max<uint32_t>(n_nodes, 1);
+    if (hipMalloc(&s->d_nodes, nb) != hipSuccess || hipMalloc(&s->d_zones, zb) != hipSuccess) {
+        hipFree(s->d_nodes);
+        delete s;
+        return fail(ctx, KG_OOM, "snapshot of %u nodes", n_nodes);
+    }
+    *out = s;
+    return KG_OK;
+}
+
+kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
+    if (!s || !cols) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    for (uint32_t i = 0; i < s->n; i++) {
+        kg_status st = build_row(ctx, s->cfg, cols, i, &s->h_nodes[i], &s->h_zones[i]);
+        if (st != KG_OK) return st;
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    s->uploaded = true;
+    return KG_OK;
+}
+
+kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, const kg_node_columns* cols) {
+    if (!s || (!rows && n) || !cols) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (uint32_t k = 0; k < n; k++) {
+        if (rows[k] >= s->n) return fail(ctx, KG_INVALID_ARG, "row %u >= %u", rows[k], s->n);
+        NodeRec rec;
+        ZoneRec zr;
+        kg_status st = build_row(ctx, s->cfg, cols, k, &rec, &zr);
+        if (st != KG_OK) return st;
+        s->h_nodes[rows[k]] = rec;
+        s->h_zones[rows[k]] = zr;
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes + rows[k], &s->h_nodes[rows[k]], sizeof(NodeRec), hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_zones + rows[k], &s->h_zones[rows[k]], sizeof(ZoneRec), hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
+kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
+    if (!s || !o) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<NodeRec> h(s->n);
+    std::vector<ZoneRec> z(s->n);
+    HIP_TRY(ctx, hipMemcpyAsync(h.data(), s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(z.data(), s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t i = 0; i < s->n; i++) {
+        const int64_t* v = h[i].v;
+        if (o->req_cpu) o->req_cpu[i] = v[N_REQ_CPU];
+        if (o->req_mem) o->req_mem[i] = v[N_REQ_MEM];
+        if (o->req_eph) o->req_eph[i] = v[N_REQ_EPH];
+        if (o->num_pods) o->num_pods[i] = v[N_NUM_PODS];
+        if (o->nz_cpu) o->nz_cpu[i] = v[N_NZ_CPU];
+        if (o->nz_mem) o->nz_mem[i] = v[N_NZ_MEM];
+        if (o->sc_req[0]) o->sc_req[0][i] = v[N_SC_REQ0];
+        if (o->sc_req[1]) o->sc_req[1][i] = v[N_SC_REQ1];
+        const int fb_np[2] = {N_LA_FBASE_NP0, N_LA_FBASE_NP1}, fb_p[2] = {N_LA_FBASE_PROD0, N_LA_FBASE_PROD1};
+        const int sb_np[2] = {N_LA_SBASE_NP0, N_LA_SBASE_NP1}, sb_p[2] = {N_LA_SBASE_PROD0, N_LA_SBASE_PROD1};
+        for (int r = 0; r < KG_LA_R; r++) {
+            if (o->la_fbase_np[r]) o->la_fbase_np[r][i] = v[fb_np[r]];
+            if (o->la_fbase_prod[r]) o->la_fbase_prod[r][i] = v[fb_p[r]];
+            if (o->la_sbase_np[r]) o->la_sbase_np[r][i] = v[sb_np[r]];
+            if (o->la_sbase_prod[r]) o->la_sbase_prod[r][i] = v[sb_p[r]];
+        }
+        for (int zz = 0; zz < KG_MAX_ZONES; zz++) {
+            if (o->zone_cpu_used[zz]) o->zone_cpu_used[zz][i] = z[i].cpu_used[zz];
+            if (o->zone_mem_used[zz]) o->zone_mem_used[zz][i] = z[i].mem_used[zz];
+        }
+    }
+    return KG_OK;
+}
+
+kg_status kg_snapshot_destroy(kg_snap* s) {
+    if (!s) return KG_INVALID_ARG;
+    hipSetDevice(s->ctx->device);
+    hipStreamSynchronize(s->ctx->stream);
+    hipFree(s->d_nodes);
+    hipFree(s->d_zones);
+    delete s;
+    return KG_OK;
+}
+
+kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
+    if (!ctx || !out || capacity == 0) return KG_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    *out = nullptr;
+    kg_pods* p = new kg_pods();
+    p->ctx = ctx;
+    p->cap = capacity;
+    hipSetDevice(ctx->device);
+    bool ok = hipMalloc(&p->d_cols, sizeof(int64_t) * 9 * capacity) == hipSuccess &&
+              hipMalloc(&p->d_flags, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_keys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
+              hipMalloc(&p->d_winners, sizeof(uint64_t) * (capacity + 1)) == hipSuccess &&
+              hipMalloc(&p->d_step, sizeof(uint32_t) * 64) == hipSuccess;
+    if (!ok) {
+        hipFree(p->d_cols);
+        hipFree(p->d_flags);
+        hipFree(p->d_keys);
+        hipFree(p->d_winners);
+        hipFree(p->d_step);
+        delete p;
+        return fail(ctx, KG_OOM, "pod batch of %u", capacity);
+    }
+    int64_t* c = p->d_cols;
+    p->dev.req_cpu = c + 0 * (size_t)capacity;
+    p->dev.req_mem = c + 1 * (size_t)capacity;
+    p->dev.req_eph = c + 2 * (size_t)capacity;
+    p->dev.sc_req0 = c + 3 * (size_t)capacity;
+    p->dev.sc_req1 = c + 4 * (size_t)capacity;
+    p->dev.nz_cpu = c + 5 * (size_t)capacity;
+    p->dev.nz_mem = c + 6 * (size_t)capacity;
+    p->dev.la_est0 = c + 7 * (size_t)capacity;
+    p->dev.la_est1 = c + 8 * (size_t)capacity;
+    p->dev.flags = p->d_flags;
+    *out = p;
+    return KG_OK;
+}
+
+kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
+    if (!p || !cols) return KG_INVALID_ARG;
+    kg_ctx* ctx = p->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n > p->cap) return fail(ctx, KG_INVALID_ARG, "%u pods > capacity %u", n, p->cap);
+    std::vector<int64_t> h((size_t)9 * std::max<uint32_t>(n, 1));
+    std::vector<uint32_t> f(std::max<uint32_t>(n, 1));
+    const int64_t* src[9] = {cols->req_cpu, cols->req_mem, cols->req_eph, cols->sc_req[0], cols->sc_req[1],
+                             cols->nz_cpu, cols->nz_mem, cols->la_est[0], cols->la_est[1]};
+    for (int c = 0; c < 9; c++)
+        for (uint32_t j = 0; j < n; j++) h[(size_t)c * n + j] = src[c] ? src[c][j] : 0;
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t pol = cols->numa_policy ? cols->numa_policy[j] : 0;
+        if (pol > KG_NUMA_SINGLE_NODE) return fail(ctx, KG_INVALID_ARG, "pod %u: NUMA policy %u", j, pol);
+        f[j] = (cols->flags ? (cols->flags[j] & 0xFFFFu) : 0u) | (pol << 16);
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (int c = 0; c < 9; c++)
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_cols + (size_t)c * p->cap, h.data() + (size_t)c * n, sizeof(int64_t) * n,
+                                    hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(p->d_flags, f.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    p->n = n;
+    return KG_OK;
+}
+
+kg_status kg_pods_destroy(kg_pods* p) {
+    if (!p) return KG_INVALID_ARG;
+    hipSetDevice(p->ctx->device);
+    hipStreamSynchronize(p->ctx->stream);
+    hipFree(p->d_cols);
+    hipFree(p->d_flags);
+    hipFree(p->d_keys);
+    hipFree(p->d_winners);
+    hipFree(p->d_step);
+    hipFree(p->d_partial);
+    hipFree(p->d_gather);
+    delete p;
+    return KG_OK;
+}
+
+static kg_status check_pair(kg_snap* s, kg_pods* p) {
+    if (!s || !p) return KG_INVALID_ARG;
+    if (s->ctx != p->ctx) return fail(s->ctx, KG_INVALID_ARG, "snapshot and pods belong to different contexts");
+    if (!s->uploaded) return fail(s->ctx, KG_INVALID_ARG, "snapshot not uploaded");
+    return KG_OK;
+}
+
+kg_status kg_eval_verify(kg_snap* s, kg_pods* p, kg_verify_out* out) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    if (!out) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const size_t pairs = (size_t)p->n * s->n;
+    if (pairs == 0) return KG_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    VerifyDev d{};
+    void* buf = nullptr;
+    const size_t bytes = pairs * (4 + 8 * 4 + 1);
+    HIP_TRY(ctx, hipMalloc(&buf, bytes));
+    char* b = (char*)buf;
+    d.s_nrf = (int64_t*)b;
+    d.s_la = d.s_nrf + pairs;
+    d.s_numa = d.s_la + pairs;
+    d.total = d.s_numa + pairs;
+    d.status = (uint32_t*)(d.total + pairs);
+    d.zone = (int8_t*)(d.status + pairs);
+    hipError_t e = launch_verify(s->d_nodes, s->d_zones, p->dev, p->n, s->n, s->kcfg, force_exact(), d, ctx->stream);
+    if (e == hipSuccess) {
+        struct {
+            void* dst;
+            const void* src;
+            size_t sz;
+        } cp[] = {{out->status, d.status, 4}, {out->score_nrf, d.s_nrf, 8}, {out->score_la, d.s_la, 8},
+                  {out->score_numa, d.s_numa, 8}, {out->total, d.total, 8}, {out->numa_zone, d.zone, 1}};
+        for (auto& c : cp)
+            if (c.dst && e == hipSuccess) e = hipMemcpyAsync(c.dst, c.src, c.sz * pairs, hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    }
+    hipFree(buf);
+    HIP_TRY(ctx, e);
+    return KG_OK;
+}
+
+static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_out) {
+    kg_ctx* ctx = s->ctx;
+    if (k == 0 || k > (uint32_t)KG_TOPK_MAX) return fail(ctx, KG_INVALID_ARG, "k=%u outside [1, %d]", k, KG_TOPK_MAX);
+    const uint32_t kk = k == 1 ? 1 : KG_TOPK_MAX;
+    LaunchSelect a{};
+    a.nodes = s->d_nodes;
+    a.zones = s->d_zones;
+    a.pods = p->dev;
+    a.n_pods = p->n;
+    a.n_nodes = s->n;
+    a.chunk = select_chunk(s->n, p->n);
+    a.n_chunks = s->n ? (s->n + a.chunk - 1) / a.chunk : 1;
+    a.index_base = s->base;
+    a.k = kk;
+    a.exact = force_exact();
+    a.cfg = s->kcfg;
+    const size_t need = (size_t)a.n_chunks * p->n * kk;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (need > p->partial_cap) {
+        if (p->d_partial) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(p->d_partial));
+            p->d_partial = nullptr;
+        }
+        HIP_TRY(ctx, hipMalloc(&p->d_partial, sizeof(uint64_t) * need));
+        p->partial_cap = need;
+    }
+    a.partial = p->d_partial;
+    p->k_last = k;
+    p->kk_last = kk;
+    if (p->n == 0) return KG_OK;
+    if (s->n == 0) {
+        HIP_TRY(ctx, hipMemsetAsync(d_out, 0, sizeof(uint64_t) * kk * p->n, ctx->stream));
+        return KG_OK;
+    }
+    hipEvent_t e0, e1;
+    kg_status st = record_begin(ctx, &e0, &e1);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, launch_select(a, ctx->stream));
+    st = record_end(ctx, e0, e1);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, launch_merge(p->d_partial, a.n_chunks, p->n, kk, d_out, ctx->stream));
+    return KG_OK;
+}
+
+kg_status kg_eval_select(kg_snap* s, kg_pods* p, uint32_t k) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    std::lock_guard<std::mutex> g(s->ctx->mu);
+    return select_local(s, p, k, p->d_keys);
+}
+
+kg_status kg_result_keys(kg_pods* p, uint64_t* out) {
+    if (!p || !out) return KG_INVALID_ARG;
+    kg_ctx* ctx = p->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (p->k_last == 0) return fail(ctx, KG_INVALID_ARG, "no selection result");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<uint64_t> h((size_t)p->kk_last * std::max<uint32_t>(p->n, 1));
+    HIP_TRY(ctx, hipMemcpyAsync(h.data(), p->d_keys, sizeof(uint64_t) * p->kk_last * p->n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t j = 0; j < p->n; j++)
+        for (uint32_t t = 0; t < p->k_last; t++) out[(size_t)j * p->k_last + t] = h[(size_t)j * p->kk_last + t];
+    return KG_OK;
+}
+
+kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint32_t n = p->n;
+    HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
+    const bool exact = force_exact();
+    hipEvent_t e0, e1;
+    st = record_begin(ctx, &e0, &e1);
+    if (st != KG_OK) return st;
+    // Steps 0..n: step i Assumes pod i-1 and evaluates pod i. Launched as captured hipGraphs of
+    // G steps that read their base step from device memory (bumped by the graph's last node).
+    const uint32_t G = 256;
+    HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = hipSuccess;
+    for (uint32_t t = 0; t < G && e == hipSuccess; t++)
+        e = launch_replay_step(s->d_nodes, s->d_zones, p->dev, n, s->n, s->base, s->kcfg, exact, p->d_step, t,
+                               p->d_winners, ctx->stream);
+    if (e == hipSuccess) e = launch_bump(p->d_step, G, ctx->stream);
+    hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    HIP_TRY(ctx, e);
+    HIP_TRY(ctx, ec);
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    if (e == hipSuccess) {
+        for (uint32_t done = 0; done <= n && e == hipSuccess; done += G) e = hipGraphLaunch(exec, ctx->stream);
+    }
+    if (exec) hipGraphExecDestroy(exec);
+    hipGraphDestroy(graph);
+    HIP_TRY(ctx, e);
+    st = record_end(ctx, e0, e1);
+    if (st != KG_OK) return st;
+    std::vector<uint64_t> w(std::max<uint32_t>(n, 1));
+    HIP_TRY(ctx, hipMemcpyAsync(w.data(), p->d_winners, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t j = 0; j < n; j++) {
+        if (out_node) out_node[j] = kg_key_node(w[j]);
+        if (out_total) out_total[j] = kg_key_total(w[j]);
+    }
+    return KG_OK;
+}
+
+kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, node, -1, 1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
+kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, node, zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
+kg_status kg_profile_enable(kg_ctx* ctx, int enable) {
+    if (!ctx) return KG_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->profiling = enable != 0;
+    return KG_OK;
+}
+
+kg_status kg_profile_read(kg_ctx* ctx, double* total_ms, uint64_t* launches, int reset) {
+    if (!ctx) return KG_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (auto& e : ctx->ev_live) {
+        HIP_TRY(ctx, hipEventSynchronize(e.second));
+        float ms = 0.f;
+        HIP_TRY(ctx, hipEventElapsedTime(&ms, e.first, e.second));
+        ctx->prof_ms += ms;
+        ctx->prof_launches++;
+        ctx->ev_free.push_back(e);
+    }
+    ctx->ev_live.clear();
+    if (total_ms) *total_ms = ctx->prof_ms;
+    if (launches) *launches = ctx->prof_launches;
+    if (reset) {
+        ctx->prof_ms = 0.0;
+        ctx->prof_launches = 0;
+    }
+    return KG_OK;
+}
+
+kg_status kg_shard_unique_id(uint8_t out[128]) {
+    if (!out) return KG_INVALID_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return KG_DEVICE_ERROR;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(out, &id, 128);
+    return KG_OK;
+}
+
+kg_status kg_shard_init(kg_ctx* ctx, const uint8_t id[128], int rank, int world) {
+    if (!ctx || !id || world < 1 || rank < 0 || rank >= world) return KG_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    if (ctx->comm) {
+        ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    }
+    NCCL_TRY(ctx, ncclCommInitRank(&ctx->comm, world, uid, rank));
+    ctx->rank = rank;
+    ctx->world = world;
+    return KG_OK;
+}
+
+kg_status kg_shard_select(kg_snap* s, kg_pods* p, uint64_t* out_keys) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!ctx->comm) return fail(ctx, KG_INVALID_ARG, "kg_shard_init not called");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint32_t n = p->n;
+    const size_t need = (size_t)n * (ctx->world + 1);
+    if (need > p->gather_cap) {
+        if (p->d_gather) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(p->d_gather));
+            p->d_gather = nullptr;
+        }
+        HIP_TRY(ctx, hipMalloc(&p->d_gather, sizeof(uint64_t) * std::max<size_t>(need, 1)));
+        p->gather_cap = need;
+    }
+    uint64_t* local = p->d_gather + (size_t)n * ctx->world;  // this shard's per-pod best key
+    st = select_local(s, p, 1, local);
+    if (st != KG_OK) return st;
+    // exchange per-shard best keys (8 B per pod per shard) and run the same global selectHost
+    NCCL_TRY(ctx, ncclAllGather(local, p->d_gather, n, ncclUint64, ctx->comm, ctx->stream));
+    HIP_TRY(ctx, launch_merge(p->d_gather, (uint32_t)ctx->world, n, 1, p->d_keys, ctx->stream));
+    p->k_last = 1;
+    p->kk_last = 1;
+    if (out_keys) {
+        HIP_TRY(ctx, hipMemcpyAsync(out_keys, p->d_keys, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return KG_OK;
+}
+
+uint64_t kg_make_key(int64_t total, uint32_t node) {
+    return ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - node);
+}
+
+int32_t kg_key_node(uint64_t key) { return key ? (int32_t)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull)) : -1; }
+
+int64_t kg_key_total(uint64_t key) { return key ? (int64_t)(key >> 32) : -1; }
+
+kg_status kg_merge_keys(const uint64_t* keys, uint32_t n_shards, uint32_t n_pods, uint32_t k, uint64_t* out) {
+    if ((!keys && n_shards && n_pods) || (!out && n_pods) || k == 0) return KG_INVALID_ARG;
+    std::vector<uint64_t> top(k);
+    for (uint32_t j = 0; j < n_pods; j++) {
+        std::fill(top.begin(), top.end(), 0ull);
+        for (uint32_t sh = 0; sh < n_shards; sh++) {
+            const uint64_t* src = keys + ((size_t)sh * n_pods + j) * k;
+            for (uint32_t t = 0; t < k; t++) {
+                uint64_t key = src[t];
+                for (uint32_t u = 0; u < k; u++) {
+                    if (key > top[u]) std::swap(key, top[u]);
+                }
+            }
+        }
+        for (uint32_t t = 0; t < k; t++) out[(size_t)j * k + t] = top[t];
+    }
+    return KG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,297 @@
+"""Python binding of libkoordgpu.so (the C ABI of include/koordgpu.h) over ctypes.
+
+This is the product path: every evaluation runs the HIP kernels through the library. There is no
+CPU fallback — if the library is missing or no device is present the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import weakref
+from typing import Optional
+
+import numpy as np
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkoordgpu.so")
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"koordgpu: {msg} (status {status})")
+        self.status = status
+
+
+class Unsupported(EngineError):
+    pass
+
+
+def lib():
+    """Load libkoordgpu.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    P, u32, i32, i64, u64, vp = C.POINTER, C.c_uint32, C.c_int32, C.c_int64, C.c_uint64, C.c_void_p
+    st = C.c_int
+    L.kg_abi_version.restype = C.c_int
+    L.kg_status_string.argtypes = [st]
+    L.kg_status_string.restype = C.c_char_p
+    L.kg_device_count.restype = C.c_int
+    L.kg_open.argtypes = [C.c_int, P(vp)]
+    L.kg_open.restype = st
+    L.kg_close.argtypes = [vp]
+    L.kg_close.restype = st
+    L.kg_last_error.argtypes = [vp]
+    L.kg_last_error.restype = C.c_char_p
+    L.kg_sync.argtypes = [vp]
+    L.kg_sync.restype = st
+    L.kg_snapshot_create.argtypes = [vp, P(abi.KgConfig), u32, u32, P(vp)]
+    L.kg_snapshot_create.restype = st
+    L.kg_snapshot_upload.argtypes = [vp, P(abi.KgNodeColumns)]
+    L.kg_snapshot_upload.restype = st
+    L.kg_snapshot_update_rows.argtypes = [vp, P(u32), u32, P(abi.KgNodeColumns)]
+    L.kg_snapshot_update_rows.restype = st
+    L.kg_snapshot_read_state.argtypes = [vp, P(abi.KgNodeState)]
+    L.kg_snapshot_read_state.restype = st
+    L.kg_snapshot_destroy.argtypes = [vp]
+    L.kg_snapshot_destroy.restype = st
+    L.kg_pods_create.argtypes = [vp, u32, P(vp)]
+    L.kg_pods_create.restype = st
+    L.kg_pods_upload.argtypes = [vp, P(abi.KgPodColumns), u32]
+    L.kg_pods_upload.restype = st
+    L.kg_pods_destroy.argtypes = [vp]
+    L.kg_pods_destroy.restype = st
+    L.kg_eval_verify.argtypes = [vp, vp, P(abi.KgVerifyOut)]
+    L.kg_eval_verify.restype = st
+    L.kg_eval_select.argtypes = [vp, vp, u32]
+    L.kg_eval_select.restype = st
+    L.kg_result_keys.argtypes = [vp, P(u64)]
+    L.kg_result_keys.restype = st
+    L.kg_replay.argtypes = [vp, vp, P(i32), P(i64)]
+    L.kg_replay.restype = st
+    L.kg_assume.argtypes = [vp, vp, u32, u32]
+    L.kg_assume.restype = st
+    L.kg_forget.argtypes = [vp, vp, u32, u32, i32]
+    L.kg_forget.restype = st
+    L.kg_profile_enable.argtypes = [vp, C.c_int]
+    L.kg_profile_enable.restype = st
+    L.kg_profile_read.argtypes = [vp, P(C.c_double), P(u64), C.c_int]
+    L.kg_profile_read.restype = st
+    L.kg_shard_unique_id.argtypes = [P(C.c_uint8)]
+    L.kg_shard_unique_id.restype = st
+    L.kg_shard_init.argtypes = [vp, P(C.c_uint8), C.c_int, C.c_int]
+    L.kg_shard_init.restype = st
+    L.kg_shard_select.argtypes = [vp, vp, P(u64)]
+    L.kg_shard_select.restype = st
+    L.kg_make_key.argtypes = [i64, u32]
+    L.kg_make_key.restype = u64
+    L.kg_key_node.argtypes = [u64]
+    L.kg_key_node.restype = i32
+    L.kg_key_total.argtypes = [u64]
+    L.kg_key_total.restype = i64
+    L.kg_merge_keys.argtypes = [P(u64), u32, u32, u32, P(u64)]
+    L.kg_merge_keys.restype = st
+    if L.kg_abi_version() != abi.KG_ABI_VERSION:
+        raise ImportError(f"libkoordgpu ABI {L.kg_abi_version()} != {abi.KG_ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def device_count() -> int:
+    return lib().kg_device_count()
+
+
+def _u64p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint64))
+
+
+class Context:
+    """kg_ctx: one HIP device + stream (+ RCCL communicator when sharded)."""
+
+    def __init__(self, device: int = 0):
+        self.L = lib()
+        h = C.c_void_p()
+        s = self.L.kg_open(device, C.byref(h))
+        if s != abi.KG_OK:
+            raise EngineError(s, f"kg_open(device={device}) failed: {self.L.kg_status_string(s).decode()}")
+        self.h = h
+        self.device = device
+        self._children = weakref.WeakSet()  # snapshots / pod batches, closed before the context
+
+    def check(self, s: int, what: str):
+        if s == abi.KG_OK:
+            return
+        msg = self.L.kg_last_error(self.h).decode() or self.L.kg_status_string(s).decode()
+        cls = Unsupported if s == abi.KG_UNSUPPORTED else EngineError
+        raise cls(s, f"{what}: {msg}")
+
+    def sync(self):
+        self.check(self.L.kg_sync(self.h), "kg_sync")
+
+    def profile(self, enable: bool = True):
+        self.check(self.L.kg_profile_enable(self.h, int(enable)), "kg_profile_enable")
+
+    def profile_read(self, reset: bool = False):
+        ms, n = C.c_double(), C.c_uint64()
+        self.check(self.L.kg_profile_read(self.h, C.byref(ms), C.byref(n), int(reset)), "kg_profile_read")
+        return ms.value, n.value
+
+    def shard_init(self, uid: bytes, rank: int, world: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self.check(self.L.kg_shard_init(self.h, buf, rank, world), "kg_shard_init")
+
+    def close(self):
+        if getattr(self, "h", None):
+            for child in list(self._children):
+                child.close()
+            self.L.kg_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def shard_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    s = lib().kg_shard_unique_id(buf)
+    if s != abi.KG_OK:
+        raise EngineError(s, "kg_shard_unique_id failed")
+    return bytes(buf)
+
+
+class Snapshot:
+    """kg_snap: device-resident node snapshot (one shard)."""
+
+    def __init__(self, ctx: Context, cfg: abi.KgConfig, nodes: abi.Table, index_base: int = 0):
+        self.ctx = ctx
+        self.cfg = cfg
+        self.n = abi.table_len(nodes)
+        self.index_base = index_base
+        h = C.c_void_p()
+        ctx.check(ctx.L.kg_snapshot_create(ctx.h, C.byref(cfg), self.n, index_base, C.byref(h)), "kg_snapshot_create")
+        self.h = h
+        ctx._children.add(self)
+        self.upload(nodes)
+
+    def upload(self, nodes: abi.Table):
+        cols = abi.node_columns(nodes)
+        self.ctx.check(self.ctx.L.kg_snapshot_upload(self.h, C.byref(cols)), "kg_snapshot_upload")
+
+    def update_rows(self, rows, nodes: abi.Table):
+        rows = np.ascontiguousarray(rows, np.uint32)
+        cols = abi.node_columns(nodes)
+        self.ctx.check(self.ctx.L.kg_snapshot_update_rows(self.h, rows.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                          len(rows), C.byref(cols)), "kg_snapshot_update_rows")
+
+    def read_state(self) -> abi.Table:
+        t = abi.empty_node_state(self.n)
+        s = abi.node_state_struct(t)
+        self.ctx.check(self.ctx.L.kg_snapshot_read_state(self.h, C.byref(s)), "kg_snapshot_read_state")
+        return t
+
+    def close(self):
+        if getattr(self, "h", None) and getattr(self.ctx, "h", None):
+            self.ctx.L.kg_snapshot_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PodBatch:
+    """kg_pods: device-resident pending pods + result buffers."""
+
+    def __init__(self, ctx: Context, pods: abi.Table, capacity: Optional[int] = None):
+        self.ctx = ctx
+        n = abi.table_len(pods)
+        cap = max(1, capacity or n)
+        h = C.c_void_p()
+        ctx.check(ctx.L.kg_pods_create(ctx.h, cap, C.byref(h)), "kg_pods_create")
+        self.h = h
+        ctx._children.add(self)
+        self.capacity = cap
+        self.upload(pods)
+
+    def upload(self, pods: abi.Table):
+        self.n = abi.table_len(pods)
+        cols = abi.pod_columns(pods)
+        self.ctx.check(self.ctx.L.kg_pods_upload(self.h, C.byref(cols), self.n), "kg_pods_upload")
+
+    def close(self):
+        if getattr(self, "h", None) and getattr(self.ctx, "h", None):
+            self.ctx.L.kg_pods_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def eval_verify(snap: Snapshot, pods: PodBatch) -> abi.VerifyResult:
+    res = abi.VerifyResult(pods.n, snap.n)
+    s = res.struct()
+    snap.ctx.check(snap.ctx.L.kg_eval_verify(snap.h, pods.h, C.byref(s)), "kg_eval_verify")
+    return res
+
+
+def eval_select_async(snap: Snapshot, pods: PodBatch, k: int = 1):
+    snap.ctx.check(snap.ctx.L.kg_eval_select(snap.h, pods.h, k), "kg_eval_select")
+
+
+def result_keys(pods: PodBatch, k: int) -> np.ndarray:
+    out = np.zeros((pods.n, k), np.uint64)
+    pods.ctx.check(pods.ctx.L.kg_result_keys(pods.h, _u64p(out)), "kg_result_keys")
+    return out
+
+
+def eval_select(snap: Snapshot, pods: PodBatch, k: int = 1) -> np.ndarray:
+    eval_select_async(snap, pods, k)
+    return result_keys(pods, k)
+
+
+def replay(snap: Snapshot, pods: PodBatch):
+    node = np.zeros(pods.n, np.int32)
+    total = np.zeros(pods.n, np.int64)
+    snap.ctx.check(snap.ctx.L.kg_replay(snap.h, pods.h, node.ctypes.data_as(C.POINTER(C.c_int32)),
+                                        total.ctypes.data_as(C.POINTER(C.c_int64))), "kg_replay")
+    return node, total
+
+
+def assume(snap: Snapshot, pods: PodBatch, pod: int, node: int):
+    snap.ctx.check(snap.ctx.L.kg_assume(snap.h, pods.h, pod, node), "kg_assume")
+
+
+def forget(snap: Snapshot, pods: PodBatch, pod: int, node: int, zone: int):
+    snap.ctx.check(snap.ctx.L.kg_forget(snap.h, pods.h, pod, node, zone), "kg_forget")
+
+
+def shard_select(snap: Snapshot, pods: PodBatch, download: bool = True) -> Optional[np.ndarray]:
+    out = np.zeros(pods.n, np.uint64) if download else None
+    snap.ctx.check(snap.ctx.L.kg_shard_select(snap.h, pods.h, _u64p(out) if download else None), "kg_shard_select")
+    return out
+
+
+def merge_keys(keys: np.ndarray) -> np.ndarray:
+    """Host selectHost over gathered shard keys, keys[shard][pod][k] -> [pod][k] (no device needed)."""
+    keys = np.ascontiguousarray(keys, np.uint64)
+    n_shards, n_pods, k = keys.shape
+    out = np.zeros((n_pods, k), np.uint64)
+    s = lib().kg_merge_keys(_u64p(keys), n_shards, n_pods, k, _u64p(out))
+    if s != abi.KG_OK:
+        raise EngineError(s, "kg_merge_keys failed")
+    return out

@@ -1,0 +1,170 @@
+"""CPU-side tests: the C-ABI library loads and exports the header's symbols, host-only helpers,
+host decode known answers, oracle self-consistency."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import kat
+import oracle_lib
+from koordinator_amd import abi, decode, engine, synth
+from koordinator_amd.config import LoadAwareArgs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "koordgpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kg_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    L = engine.lib()
+    names = header_functions()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert L.kg_abi_version() == abi.KG_ABI_VERSION
+
+
+def test_struct_layouts_match_header():
+    # pointer-per-column structs: sizes follow from the field lists of include/koordgpu.h
+    ptr = C.sizeof(C.c_void_p)
+    n_node_ptrs = 10 + 2 * abi.KG_NSCALAR + 1 + 8 * abi.KG_LA_R + 4 + 4 * abi.KG_MAX_ZONES
+    assert C.sizeof(abi.KgNodeColumns) == n_node_ptrs * ptr
+    assert C.sizeof(abi.KgPodColumns) == (7 + abi.KG_LA_R + 2) * ptr
+    assert C.sizeof(abi.KgVerifyOut) == 6 * ptr
+
+
+def test_keys_host_helpers():
+    L = engine.lib()
+    for total, node in [(0, 0), (190, 5), (500_000, 99_999), (1, 0x7FFFFFFE)]:
+        key = L.kg_make_key(total, node)
+        assert key == abi.make_key(total, node)
+        assert L.kg_key_node(key) == node and L.kg_key_total(key) == total
+    assert L.kg_key_node(0) == -1 and L.kg_key_total(0) == -1
+    # higher total wins, then lower index
+    assert abi.make_key(10, 7) > abi.make_key(9, 0)
+    assert abi.make_key(10, 3) > abi.make_key(10, 4)
+
+
+def test_merge_keys_is_global_select_host():
+    rng = np.random.default_rng(3)
+    keys = np.zeros((4, 100, 3), np.uint64)
+    for s in range(4):
+        for j in range(100):
+            ks = sorted((abi.make_key(int(rng.integers(0, 300)), s * 1000 + int(i)) for i in rng.choice(1000, 3, False)),
+                        reverse=True)
+            keys[s, j] = ks
+    keys[2, 10] = 0  # shard with no feasible node
+    out = engine.merge_keys(keys)
+    flat = np.sort(keys.transpose(1, 0, 2).reshape(100, -1), axis=1)[:, ::-1][:, :3]
+    assert np.array_equal(out, flat)
+
+
+def test_device_count_without_gpu_is_safe():
+    assert engine.device_count() >= 0
+
+
+def test_oracle_parallel_baseline_equals_sequential():
+    cfg, nodes, pods = synth.small(800, 120, seed=21)
+    kc = cfg.kg_config()
+    seq = oracle_lib.select(kc, nodes, pods, 1)[:, 0]
+    for workers in (1, 3, 16):
+        par = oracle_lib.select_parallel(kc, nodes, pods, workers)
+        assert np.array_equal(seq, par)
+
+
+def test_oracle_replay_consistent_with_assume():
+    cfg, nodes, pods = synth.small(120, 200, seed=22, scale=3.0)
+    kc = cfg.kg_config()
+    st = oracle_lib.OracleState(kc, nodes)
+    node, total = st.replay(pods)
+    st2 = oracle_lib.OracleState(kc, nodes)
+    for j in range(200):
+        view = st2.table()
+        keys = oracle_lib.select(kc, view, abi.take(pods, [j]), 1)[0, 0]
+        assert abi.key_node(keys) == node[j]
+        if node[j] >= 0:
+            st2.assume(int(node[j]), pods, j)
+    assert (node < 0).any()
+
+
+EST_CASES = [
+    # default_estimator_test.go:33-283 (TestDefaultEstimatorEstimatePod)
+    ("estimate empty pod", {"containers": [{}]}, None, False, [250, 200 * 1024 * 1024]),
+    ("estimate guaranteed pod", {"containers": [{"requests": {"cpu": "4", "memory": "8Gi"}, "limits": {"cpu": "4", "memory": "8Gi"}}]},
+     None, False, [3400, 6012954214]),
+    ("estimate burstable pod", {"containers": [{"requests": {"cpu": "4", "memory": "8Gi"}, "limits": {"cpu": "8", "memory": "8Gi"}}]},
+     None, False, [6800, 6012954214]),
+    ("zoomed cpu factors", {"containers": [{"requests": {"cpu": "4", "memory": "8Gi"}, "limits": {"cpu": "4", "memory": "8Gi"}}]},
+     {"cpu": 110}, False, [4000, 6012954214]),
+    ("zoomed memory factors", {"containers": [{"requests": {"cpu": "4", "memory": "8Gi"}, "limits": {"cpu": "4", "memory": "8Gi"}}]},
+     {"memory": 110}, False, [3400, 8589934592]),
+    ("estimate Batch pod", {"labels": {"koordinator.sh/qosClass": "BE"}, "priority": 5000,
+                            "containers": [{"requests": {"kubernetes.io/batch-cpu": "4000", "kubernetes.io/batch-memory": "8Gi"},
+                                            "limits": {"kubernetes.io/batch-cpu": "4000", "kubernetes.io/batch-memory": "8Gi"}}]},
+     None, False, [3400, 6012954214]),
+    ("estimate pod only has request", {"labels": {"koordinator.sh/qosClass": "LS"}, "priority": 9999,
+                                       "containers": [{"requests": {"cpu": "4", "memory": "8Gi"}}]},
+     {"cpu": 80, "memory": 80}, False, [3200, 6871947674]),
+    ("estimate pod with customized factors", {"labels": {"koordinator.sh/qosClass": "LS"}, "priority": 9999,
+                                              "annotations": {"scheduling.koordinator.sh/load-estimated-scaling-factors": '{"cpu":100}'},
+                                              "containers": [{"requests": {"cpu": "4", "memory": "8Gi"}}]},
+     {"cpu": 80, "memory": 80}, True, [4000, 6871947674]),
+]
+
+
+@pytest.mark.parametrize("name,pod,factors,custom,want", EST_CASES, ids=[c[0] for c in EST_CASES])
+def test_estimator_known_answers(name, pod, factors, custom, want):
+    la = LoadAwareArgs(estimated_scaling_factors=dict(factors) if factors else None,
+                       allow_customize_estimation=custom).defaulted()
+    assert decode.estimate_pod(kat.make_pod(pod), la) == want
+
+
+@pytest.mark.parametrize("ann,alloc,want", [
+    # default_estimator_test.go:291-360 (TestDefaultEstimatorEstimateNode)
+    (None, {"cpu": "32"}, {"cpu": 32000}),
+    ('{"cpu":28,"memory":"32Gi"}', {"cpu": "32", "memory": "42Gi"}, {"cpu": 28000, "memory": 32 << 30}),
+    ('{"cpu":32,"memory":"42Gi"}', {"cpu": "32", "memory": "42Gi"}, {"cpu": 32000, "memory": 42 << 30}),
+])
+def test_estimate_node_known_answers(ann, alloc, want):
+    node = {"metadata": {"annotations": {decode.ANN_RAW_ALLOCATABLE: ann} if ann else {}}, "status": {"allocatable": alloc}}
+    got = {k: decode.vec_value(k, v) for k, v in decode.estimate_node_allocatable(node).items()}
+    assert got == want
+
+
+@pytest.mark.parametrize("q,value,milli", [
+    ("1", 1, 1000), ("100m", 1, 100), ("0.5", 1, 500), ("1Gi", 1 << 30, 1000 << 30), ("20k", 20000, 20_000_000),
+    ("1.5Mi", 1572864, 1572864000), ("2e3", 2000, 2_000_000), ("0", 0, 0), ("250m", 1, 250)])
+def test_quantity(q, value, milli):
+    assert decode.value(q) == value and decode.milli_value(q) == milli
+
+
+def test_pod_requests_sidecars_and_overhead():
+    pod = kat.make_pod({"containers": [{"requests": {"cpu": "1", "memory": "1Gi"}}],
+                        "init_containers": [{"requests": {"cpu": "3"}},
+                                            {"requests": {"cpu": "500m", "memory": "2Gi"}, "restartPolicy": "Always"},
+                                            {"requests": {"cpu": "2"}}],
+                        "overhead": {"cpu": "100m"}})
+    r = decode.pod_requests(pod)
+    # containers 1 + sidecar 0.5 = 1.5 cpu; init max(3, 2 + 0.5) = 3 -> max(1.5, 3) = 3; + overhead
+    assert decode.milli_value(r["cpu"]) == 3100
+    assert decode.value(r["memory"]) == 3 << 30
+    nz = decode.pod_requests(kat.make_pod({"containers": [{"requests": {"cpu": "1"}}, {}]}), decode.NON_MISSING)
+    assert decode.milli_value(nz["cpu"]) == 1100 and decode.value(nz["memory"]) == 400 << 20
+
+
+@pytest.mark.parametrize("spec,want", [
+    ({}, "koord-batch"),                                                        # BestEffort -> BE -> batch
+    ({"containers": [{"requests": {"cpu": "1"}}]}, "koord-prod"),               # Burstable -> LS -> prod
+    ({"priority": 7000}, "koord-mid"),
+    ({"priority": 100, "containers": [{"requests": {"cpu": "1"}}]}, "koord-prod"),
+    ({"labels": {"koordinator.sh/priority-class": "koord-free"}}, "koord-free"),
+    ({"labels": {"koordinator.sh/qosClass": "BE"}, "containers": [{"requests": {"cpu": "1"}}]}, "koord-batch"),
+])
+def test_priority_class_with_default(spec, want):
+    assert decode.priority_class(kat.make_pod(spec)) == want
