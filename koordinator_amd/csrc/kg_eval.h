@@ -295,6 +295,194 @@ __device__ __forceinline__ void apply_assume(const KCfg& c, int64_t* n, ZoneRec*
         zr->cpu_used[zone] += sign * p.req_cpu;
         zr->mem_used[zone] += sign * p.req_mem;
     }
+    derive_node(*reinterpret_cast<NodeRec*>(n), *zr);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fast path of the select kernel. Node values come from the record's fast block (wave-uniform, in
+// SGPRs); pod values are scaled by 100 once per lane. Every quotient is exact by construction, so
+// results equal eval_pair's bit for bit; nodes or pods outside the fast domain (F_BIG, host pod
+// check) take eval_pair instead.
+//
+// leastRequestedScore(requested, capacity) = (capacity - requested) * 100 / capacity (0 if the
+// request exceeds capacity or capacity is 0): with F = capacity - node requested (0 <= F <= capacity
+// < 2^44, node-side, x100) and r the pod request (x100), t = F100 - r100 is exact and
+//   y = RN(t * rcp_up),  rcp_up = 1/capacity rounded toward +inf,
+// satisfies floor(t/c) <= y < floor(t/c) + 1 for t >= 0: y >= t/c because rcp_up >= 1/c and rounding
+// is monotone; y - t/c <= (t/c) 2^-52 + ulp(y)/2 <= 100 * 2^-52 + 2^-46 < 1/c <= distance from t/c
+// to the next integer. A saturating float->uint convert truncates y and maps t < 0 to 0. Capacity 0
+// has rcp_up = 0, so y = 0.
+//
+// Weighted mean Σ s_i w_i / Σ w_i (s_i <= 100, host-checked w_i <= 4096, Σ w_i <= 16384): with
+// doubled weights, trunc((2 Σ s_i w_i + 1) * (0.5 / Σ w_i)) in float32: the exact value sits at least
+// 0.5/Σw (>= 3.05e-5) away from any integer and the float error is <= 101 * 1.5 * 2^-23 (1.8e-5).
+
+struct PodF {
+    double cpu, mem, eph, sc0, sc1, nzc, nzm, e0, e1;  // x100
+    double la_sprod;   // 1.0 when the LoadAware score uses the prod profile (la_score_prod && prod pod)
+    double has_cpu;    // 1.0 when the cpu request is non-zero (amplified-cpu score)
+    uint32_t sc0_on, sc1_on;  // 1 when the scalar request is non-zero (LeastAllocated counts it)
+    uint32_t flags;
+};
+
+__device__ __forceinline__ PodF to_podf(const PodV& p, const KCfg& c) {
+    PodF q;
+    q.la_sprod = (c.la_score_prod && (p.flags & KG_POD_PROD)) ? 1.0 : 0.0;
+    q.has_cpu = p.req_cpu != 0 ? 1.0 : 0.0;
+    q.sc0_on = p.sc0 != 0 ? 1u : 0u;
+    q.sc1_on = p.sc1 != 0 ? 1u : 0u;
+    q.cpu = x100(p.req_cpu);
+    q.mem = x100(p.req_mem);
+    q.eph = x100(p.req_eph);
+    q.sc0 = x100(p.sc0);
+    q.sc1 = x100(p.sc1);
+    q.nzc = x100(p.nz_cpu);
+    q.nzm = x100(p.nz_mem);
+    q.e0 = x100(p.est0);
+    q.e1 = x100(p.est1);
+    q.flags = p.flags;
+    return q;
+}
+
+// saturating float64 -> uint32 (v_cvt_u32_f64 clamps negatives to 0)
+__device__ __forceinline__ uint32_t cvt_sat_u32(double y) {
+    uint32_t r;
+    asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(y));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t lr100(double f100, double r100, double rcp_up) {
+    return cvt_sat_u32((f100 - r100) * rcp_up);
+}
+
+// trunc(sum2 * hw) for sum2 = 2 Σ s_i w_i + 1, hw = 0.5 / Σ w_i
+__device__ __forceinline__ uint32_t wq(uint32_t sum2, float hw) { return (uint32_t)((float)sum2 * hw); }
+
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) { return __umul24(a, b) + c; }
+
+__device__ __forceinline__ uint32_t u16(uint64_t pack, int k) { return (uint32_t)(pack >> (16 * k)) & 0xFFFFu; }
+
+__device__ __forceinline__ float f32hi(uint64_t pack) { return __uint_as_float((uint32_t)(pack >> 32)); }
+
+__device__ __forceinline__ float f32lo(uint64_t pack) { return __uint_as_float((uint32_t)pack); }
+
+// Copy a wave-uniform kernel argument into a VGPR: keeps the select loop's SGPRs for the node
+// record (the compiler would otherwise pin the configuration in SGPRs and spill the record).
+__device__ __forceinline__ int32_t in_vgpr(int32_t x) {
+    int32_t y;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "s"(x));
+    return y;
+}
+
+__device__ __forceinline__ KCfg cfg_in_vgprs(const KCfg& c) {
+    KCfg v = c;
+    v.w_nrf = in_vgpr(c.w_nrf);
+    v.w_la = in_vgpr(c.w_la);
+    v.w_numa = in_vgpr(c.w_numa);
+    v.la_w[0] = in_vgpr(2 * c.la_w[0]);  // doubled for wq
+    v.la_w[1] = in_vgpr(2 * c.la_w[1]);
+    v.la_dom_w = in_vgpr(2 * c.la_dom_w);
+    v.la_hw = __int_as_float(in_vgpr(__float_as_int(c.la_hw)));
+    return v;
+}
+
+// Selection key of one (pod, node) pair on the fast path. `r` is the node's fast block (by value:
+// wide scalar loads, one wait); plugin arithmetic is branch-free except for the SingleNUMANode
+// zone walk. `c` comes from cfg_in_vgprs (LoadAware weights doubled).
+// PM: enabled plugins (KG_PLUGIN_* mask); CLS: node storage class (node_class), both compile-time.
+template <uint32_t PM, int CLS>
+__device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr,
+                                                  const PodF& p, uint32_t gidx) {
+    const uint32_t f = (uint32_t)r.flags;
+    bool ok = true;
+    uint32_t total = 0;
+
+    if constexpr ((PM & KG_PLUGIN_NRF) != 0) {
+        // Fits: request r fails iff r > 0 and r > alloc - requested, i.e. 100 r > 100 max(0, headroom)
+        const bool fit_fail = (p.cpu > r.fit_cpu) | (p.mem > r.fit_mem) | (p.eph > r.fit_eph) |
+                              (p.sc0 > r.fit_sc0) | (p.sc1 > r.fit_sc1);
+        ok = ok & !fit_fail & !(f & F_PODS_FULL);
+        // LeastAllocated (NonZeroRequested for cpu / memory, Requested for scalars the pod requests)
+        const uint64_t wp = r.wpack_nrf;
+        const uint32_t w0 = u16(wp, 0), w1 = u16(wp, 1);
+        const uint32_t w2 = __umul24(u16(wp, 2), p.sc0_on), w3 = __umul24(u16(wp, 3), p.sc1_on);
+        uint32_t sum2 = mad24(lr100(r.lr_nz_cpu, p.nzc, r.rcp_cpu), w0, 1u);
+        sum2 = mad24(lr100(r.lr_nz_mem, p.nzm, r.rcp_mem), w1, sum2);
+        sum2 = mad24(lr100(r.lr_sc0, p.sc0, r.rcp_sc0), w2, sum2);
+        sum2 = mad24(lr100(r.lr_sc1, p.sc1, r.rcp_sc1), w3, sum2);
+        // Σ 2w = 0 -> sum2 = 1, and max(.., 2) gives trunc(1 * 0.5) = 0
+        const float wsum = (float)max(w0 + w1 + w2 + w3, 2u);
+        float h = __builtin_amdgcn_rcpf(wsum);
+        h = fmaf(h, fmaf(-wsum, h, 1.0f), h);  // one Newton step: 1/(Σ 2w) = 0.5/Σw, <= 1 ulp
+        total = mad24(c.w_nrf, wq(sum2, h), total);
+    }
+
+    if constexpr ((PM & KG_PLUGIN_LA) != 0) {
+        // Filter: usage cut-offs of the pod's profile (100 * (cut - base) vs 100 * estimate)
+        const bool pod_prod = (p.flags & KG_POD_PROD) != 0;
+        const bool fprod = (f & F_LA_PROD_THR) && pod_prod;
+        const uint32_t mode_np = (f >> F_LA_FMODE_NP_SHIFT) & 3u, mode_pr = (f >> F_LA_FMODE_PROD_SHIFT) & 3u;
+        const bool over_np = (p.e0 > r.la_head_np0) | (p.e1 > r.la_head_np1);
+        const bool over_pr = (p.e0 > r.la_head_prod0) | (p.e1 > r.la_head_prod1);
+        const bool fail_np = (mode_np == FMODE_FAIL_EXPIRED) | ((mode_np == FMODE_CHECK) & over_np);
+        const bool fail_pr = (mode_pr == FMODE_FAIL_EXPIRED) | ((mode_pr == FMODE_CHECK) & over_pr);
+        const bool la_fail = ((p.flags & KG_POD_DAEMONSET) == 0) & (fprod ? fail_pr : fail_np);
+        ok = ok & !la_fail;
+        // Score: least-used over the estimated usage
+        // profile select as an exact fma: (free_np - e) + delta * {0, 1}
+        const uint32_t s0 = cvt_sat_u32(fma(r.la_sdelta0, p.la_sprod, r.la_sfree_np0 - p.e0) * r.rcp_la0);
+        const uint32_t s1 = cvt_sat_u32(fma(r.la_sdelta1, p.la_sprod, r.la_sfree_np1 - p.e1) * r.rcp_la1);
+        const uint32_t dom = min(min(s0, s1), 100u);
+        uint32_t sum2 = mad24(s0, (uint32_t)c.la_w[0], 1u);
+        sum2 = mad24(s1, (uint32_t)c.la_w[1], sum2);
+        sum2 = mad24(dom, (uint32_t)c.la_dom_w, sum2);
+        const bool zero = !c.la_score_enabled || (f & F_LA_SCORE_ZERO);
+        total = mad24(c.w_la, zero ? 0u : wq(sum2, c.la_hw), total);
+    }
+
+    if constexpr ((PM & KG_PLUGIN_NUMA) != 0) {
+        const bool skip = (p.flags & KG_POD_NUMA_SKIP) != 0;
+        const uint32_t pol = (f >> F_NUMA_POLICY_SHIFT) & 15u;  // pod policies take eval_pair (host check)
+        bool nok = !(p.flags & KG_POD_CPU_BIND) && pol != KG_NUMA_RESTRICTED && pol != KG_NUMA_BEST_EFFORT;
+        nok = nok & !(p.cpu > r.amp_fit);  // amp_fit is 2^62 without amplification
+        const uint64_t wn = r.wpack_numa;
+        uint32_t s_numa;
+        if constexpr (CLS == 1) {  // SingleNUMANode nodes (their own storage class): zone walk
+            const uint32_t Z = (f >> F_NUMA_ZONES_SHIFT) & 15u;
+            const bool has_cpu = (p.flags & KG_POD_HAS_CPU) != 0, has_mem = (p.flags & KG_POD_HAS_MEM) != 0;
+            const bool has_any = has_cpu | has_mem;
+            int32_t best = -1;
+            uint32_t best_hint = 0, best_score = 0;
+#pragma unroll 1
+            for (uint32_t z = 0; z < Z; z++) {
+                const ZoneFast q = zr->zf[z];
+                const bool elig = (!has_cpu | (p.cpu <= q.avail_cpu)) & (!has_mem | (p.mem <= q.avail_mem));
+                const uint32_t hc = lr100(q.hint_cpu, p.cpu, q.rcp_cpu), hm = lr100(q.hint_mem, p.mem, q.rcp_mem);
+                const uint32_t fc = lr100(q.free_cpu, p.cpu, q.rcp_cpu), fm = lr100(q.free_mem, p.mem, q.rcp_mem);
+                const uint32_t hint = wq(mad24(hm, u16(q.wpack, 1), mad24(hc, u16(q.wpack, 0), 1u)), f32lo(q.hpack));
+                const uint32_t fin = wq(mad24(fm, u16(q.wpack, 3), mad24(fc, u16(q.wpack, 2), 1u)), f32hi(q.hpack));
+                const bool take = elig & ((best < 0) | (hint > best_hint));
+                best = take ? (int32_t)z : best;
+                best_hint = take ? hint : best_hint;
+                best_score = take ? fin : best_score;
+            }
+            nok &= (Z != 0) & !(has_any & (best < 0));
+            // a best hint equal to the default affinity (no request on NUMA resources, or one zone)
+            // carries no affinity: node-level score without amplification
+            const uint32_t sc = lr100(r.numa_free_cpu, p.cpu, r.rcp_cpu), sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
+            const uint32_t node_level = wq(mad24(sm, u16(wn, 1), mad24(sc, u16(wn, 0), 1u)), f32hi(wn));
+            s_numa = (!has_any || Z == 1) ? node_level : best_score;
+        } else {
+            // amplified requested for pods with a cpu request: (free - r) + delta * {0, 1}
+            const uint32_t sc = cvt_sat_u32(fma(r.amp_delta, p.has_cpu, r.numa_free_cpu - p.cpu) * r.rcp_cpu);
+            const uint32_t sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
+            s_numa = wq(mad24(sm, u16(wn, 1), mad24(sc, u16(wn, 0), 1u)), f32hi(wn));
+        }
+        ok &= skip || nok;
+        total = mad24(c.w_numa, skip ? 0u : s_numa, total);
+    }
+    const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - gidx);
+    return ok ? key : 0ull;
 }
 
 }  // namespace kg

@@ -8,12 +8,19 @@ namespace kg {
 
 constexpr int KG_TOPK_MAX = 4;  // select kernels are instantiated for K = 1 and K = 4 (k <= 4)
 
+// One storage class of node records: [begin, end) walked in n_chunks chunks of `chunk` records,
+// written to partial rows [part0, part0 + n_chunks).
+struct SelectRange {
+    uint32_t begin, end, chunk, n_chunks, part0;
+};
+
 struct LaunchSelect {
     const NodeRec* nodes;
     const ZoneRec* zones;
     PodsDev pods;
-    uint32_t n_pods, n_nodes, chunk, n_chunks, index_base, k;
-    bool exact;
+    uint32_t n_pods, index_base, k;
+    SelectRange range[2];
+    bool exact, fast;
     KCfg cfg;
     uint64_t* partial;
 };
@@ -27,6 +34,12 @@ struct VerifyDev {
 hipError_t launch_select(const LaunchSelect& a, hipStream_t s);
 hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k, uint64_t* out,
                         hipStream_t s);
+hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k,
+                            const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, const uint32_t* big_list,
+                            const uint32_t* big_count, uint32_t index_base, const KCfg& cfg, uint64_t* out,
+                            hipStream_t s);
+hipError_t launch_big_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t* big_list, uint32_t* big_count,
+                           hipStream_t s);
 hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, uint32_t n_pods,
                          uint32_t n_nodes, const KCfg& cfg, bool exact, const VerifyDev& o, hipStream_t s);
 hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t n_pods, uint32_t n_nodes,

@@ -1,14 +1,15 @@
 // kg_kernels.hip — CDNA4 (gfx950) kernels of the Filter/Score evaluation engine.
 //
-//   k_select   matrix mode: lane = pending pod, wave walks a chunk of nodes in uniform order
-//              (node records arrive through the scalar cache into SGPRs), running top-K per lane;
-//              per-(chunk, pod) partial keys -> k_merge.
-//   k_merge    per pod: top-K over the chunks' partial keys (global selectHost of one shard or of
-//              the all-gathered shards).
-//   k_verify   lane = (pod, node) pair: every plugin's status / score (FilterPlugin / ScorePlugin
+//   k_select   matrix mode: lane = pending pod, wave walks a chunk of node records in uniform order
+//              (each record's 256-byte fast block arrives by wide scalar loads into SGPRs), running
+//              top-K per lane; per-(chunk, pod) partial keys. Specialised per node storage class
+//              (records are stored grouped by class) and per enabled-plugin set.
+//   k_merge    per pod: top-K over partial keys (global selectHost of one shard or of the
+//              all-gathered shards); k_merge_big adds the nodes outside the float64 fast path.
+//   k_verify   lane = (pod, node record): every plugin's status / score (FilterPlugin / ScorePlugin
 //              results) for parity dumps.
-//   k_replay   one pod per launch, lane = node: applies the previous pod's Assume to the winning
-//              node in place, evaluates the pod on every node, block max -> atomicMax.
+//   k_replay   one pod per launch, lane = node record: applies the previous pod's Assume to the
+//              winning node in place, evaluates the pod on every node, block max -> atomicMax.
 //   k_assume   Reserve / Unreserve of one pod on one node.
 // No MFMA: this is integer / IEEE-double scalar work bound by VALU issue and on-chip bandwidth.
 #include <hip/hip_runtime.h>
@@ -33,10 +34,18 @@ __device__ __forceinline__ void topk_insert(uint64_t (&top)[K], uint64_t key) {
     }
 }
 
-template <int K, bool EXACT>
+__device__ __forceinline__ uint32_t rec_gidx(const NodeRec& r, uint32_t index_base) {
+    return index_base + node_index(r);
+}
+
+// Records [begin, end) are walked in chunks of `chunk`; blockIdx.y = chunk, partial row = part0 + chunk.
+// FAST: pods and weights fit the float64 fast path (host check); records flagged F_BIG are skipped
+// and evaluated on the integer path by k_merge_big.
+template <int K, bool EXACT, bool FAST, uint32_t PM, int CLS>
 __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
-                                                PodsDev pods, uint32_t n_pods, uint32_t n_nodes, uint32_t chunk,
-                                                uint32_t index_base, KCfg cfg, uint64_t* __restrict__ partial) {
+                                                PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
+                                                uint32_t chunk, uint32_t part0, uint32_t index_base, KCfg cfg,
+                                                uint64_t* __restrict__ partial) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t c = blockIdx.y;
     const bool live = j < n_pods;
@@ -44,15 +53,26 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
     uint64_t top[K];
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
-    const uint32_t lo = c * chunk;
-    const uint32_t hi = min(n_nodes, lo + chunk);
-    for (uint32_t i = lo; i < hi; i++) {
-        const int64_t* n = nodes[i].v;
-        const PairOut o = eval_pair<EXACT>(cfg, n, zones + i, p);
-        topk_insert<K>(top, pair_key(cfg, o, index_base + i));
+    const uint32_t lo = begin + c * chunk;
+    const uint32_t hi = min(end, lo + chunk);
+    if constexpr (FAST) {
+        const PodF pf = to_podf(p, cfg);
+        const KCfg cv = cfg_in_vgprs(cfg);
+        for (uint32_t i = lo; i < hi; i++) {
+            const FastRec r = *reinterpret_cast<const FastRec*>(&nodes[i].v[FAST_BEGIN]);
+            const uint64_t key = eval_fast_key<PM, CLS>(cv, r, zones + i, pf, index_base + (uint32_t)((uint64_t)r.flags >> 32));
+            // F_BIG records (integer path in k_merge_big) are masked, not branched around: one wait
+            // for the whole record
+            topk_insert<K>(top, ((uint32_t)r.flags & F_BIG) ? 0ull : key);
+        }
+    } else {
+        for (uint32_t i = lo; i < hi; i++) {
+            const PairOut o = eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p);
+            topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
+        }
     }
     if (live) {
-        uint64_t* dst = partial + ((size_t)c * n_pods + j) * K;
+        uint64_t* dst = partial + ((size_t)(part0 + c) * n_pods + j) * K;
 #pragma unroll
         for (int t = 0; t < K; t++) dst[t] = top[t];
     }
@@ -75,6 +95,50 @@ __global__ __launch_bounds__(256) void k_merge(const uint64_t* __restrict__ part
     for (int t = 0; t < K; t++) out[(size_t)j * K + t] = top[t];
 }
 
+// Merge of the fast select: top-K over the chunk partials plus the BIG records (integer path) listed
+// by k_big_scan.
+template <int K>
+__global__ __launch_bounds__(256) void k_merge_big(const uint64_t* __restrict__ partial, uint32_t n_parts,
+                                                   uint32_t n_pods, const NodeRec* __restrict__ nodes,
+                                                   const ZoneRec* __restrict__ zones, PodsDev pods,
+                                                   const uint32_t* __restrict__ big_list,
+                                                   const uint32_t* __restrict__ big_count, uint32_t index_base,
+                                                   KCfg cfg, uint64_t* __restrict__ out) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_pods) return;
+    uint64_t top[K];
+#pragma unroll
+    for (int t = 0; t < K; t++) top[t] = 0;
+    for (uint32_t c = 0; c < n_parts; c++) {
+        const uint64_t* src = partial + ((size_t)c * n_pods + j) * K;
+#pragma unroll
+        for (int t = 0; t < K; t++) topk_insert<K>(top, src[t]);
+    }
+    const uint32_t nb = *big_count;
+    if (nb) {
+        const PodV p = load_pod(pods, j);
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint32_t i = big_list[b];
+            const PairOut o = eval_pair<false>(cfg, nodes[i].v, zones + i, p);
+            topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < K; t++) out[(size_t)j * K + t] = top[t];
+}
+
+// Rebuild the list of F_BIG records (after any change of node state).
+__global__ __launch_bounds__(256) void k_big_scan(const NodeRec* __restrict__ nodes, uint32_t n_nodes,
+                                                  uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_nodes) return;
+    if ((uint32_t)nodes[i].v[N_FLAGS] & F_BIG) {
+        const uint32_t slot = atomicAdd(big_count, 1u);
+        big_list[slot] = i;
+    }
+}
+
+// Outputs are indexed by the node's snapshot index (record orig), [pod][node].
 template <bool EXACT>
 __global__ __launch_bounds__(256) void k_verify(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                 PodsDev pods, uint32_t n_pods, uint32_t n_nodes, KCfg cfg,
@@ -86,12 +150,13 @@ __global__ __launch_bounds__(256) void k_verify(const NodeRec* __restrict__ node
     const uint32_t j = (uint32_t)(x / n_nodes), i = (uint32_t)(x % n_nodes);
     const PodV p = load_pod(pods, j);
     const PairOut o = eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p);
-    status[x] = o.status;
-    s_nrf[x] = o.s_nrf;
-    s_la[x] = o.s_la;
-    s_numa[x] = o.s_numa;
-    total[x] = o.status ? -1 : pair_total(cfg, o);
-    zone[x] = (int8_t)o.zone;
+    const size_t y = (size_t)j * n_nodes + node_index(nodes[i]);
+    status[y] = o.status;
+    s_nrf[y] = o.s_nrf;
+    s_la[y] = o.s_la;
+    s_numa[y] = o.s_numa;
+    total[y] = o.status ? -1 : pair_total(cfg, o);
+    zone[y] = (int8_t)o.zone;
 }
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
@@ -118,7 +183,7 @@ __global__ __launch_bounds__(256) void k_replay(NodeRec* __restrict__ nodes, Zon
         const uint64_t prev = winners[step - 1];
         if (prev != 0ull) {
             const uint32_t g = 0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull);
-            if (g - index_base == i) {
+            if (g == rec_gidx(nodes[i], index_base)) {
                 const PodV q = load_pod(pods, step - 1);
                 int64_t* n = nodes[i].v;
                 const PairOut o = eval_pair<EXACT>(cfg, n, zones + i, q);
@@ -131,7 +196,7 @@ __global__ __launch_bounds__(256) void k_replay(NodeRec* __restrict__ nodes, Zon
     if (live) {
         const PodV p = load_pod(pods, step);
         const PairOut o = eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p);
-        key = pair_key(cfg, o, index_base + i);
+        key = pair_key(cfg, o, rec_gidx(nodes[i], index_base));
     }
     key = wave_max_u64(key);
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -168,22 +233,46 @@ __global__ void k_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zone
 
 #define KG_LAUNCH_CHECK() (hipGetLastError())
 
+template <int K, bool EXACT, bool FAST, uint32_t PM, int CLS>
+static void select_instance(const LaunchSelect& a, const SelectRange& r, hipStream_t s) {
+    dim3 grid((a.n_pods + 255) / 256, r.n_chunks), block(256);
+    k_select<K, EXACT, FAST, PM, CLS><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end,
+                                                             r.chunk, r.part0, a.index_base, a.cfg, a.partial);
+}
+
+template <int K, int CLS>
+static void select_fast(const LaunchSelect& a, const SelectRange& r, hipStream_t s) {
+    switch (a.cfg.plugins & 7u) {
+        case 0: select_instance<K, false, true, 0, CLS>(a, r, s); break;
+        case 1: select_instance<K, false, true, 1, CLS>(a, r, s); break;
+        case 2: select_instance<K, false, true, 2, CLS>(a, r, s); break;
+        case 3: select_instance<K, false, true, 3, CLS>(a, r, s); break;
+        case 4: select_instance<K, false, true, 4, CLS>(a, r, s); break;
+        case 5: select_instance<K, false, true, 5, CLS>(a, r, s); break;
+        case 6: select_instance<K, false, true, 6, CLS>(a, r, s); break;
+        default: select_instance<K, false, true, 7, CLS>(a, r, s); break;
+    }
+}
+
 hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
-    dim3 grid((a.n_pods + 255) / 256, a.n_chunks), block(256);
-    if (a.exact) {
-        if (a.k == 1)
-            k_select<1, true><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, a.n_nodes, a.chunk,
-                                                    a.index_base, a.cfg, a.partial);
-        else
-            k_select<KG_TOPK_MAX, true><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, a.n_nodes, a.chunk,
-                                                              a.index_base, a.cfg, a.partial);
-    } else {
-        if (a.k == 1)
-            k_select<1, false><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, a.n_nodes, a.chunk,
-                                                     a.index_base, a.cfg, a.partial);
-        else
-            k_select<KG_TOPK_MAX, false><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, a.n_nodes,
-                                                               a.chunk, a.index_base, a.cfg, a.partial);
+    for (int cls = 0; cls < 2; cls++) {
+        const SelectRange& r = a.range[cls];
+        if (r.n_chunks == 0) continue;
+        if (a.exact) {
+            if (a.k == 1) select_instance<1, true, false, 0, 0>(a, r, s);
+            else select_instance<KG_TOPK_MAX, true, false, 0, 0>(a, r, s);
+        } else if (a.fast) {
+            if (a.k == 1) {
+                if (cls == 0) select_fast<1, 0>(a, r, s);
+                else select_fast<1, 1>(a, r, s);
+            } else {
+                if (cls == 0) select_fast<KG_TOPK_MAX, 0>(a, r, s);
+                else select_fast<KG_TOPK_MAX, 1>(a, r, s);
+            }
+        } else {
+            if (a.k == 1) select_instance<1, false, false, 0, 0>(a, r, s);
+            else select_instance<KG_TOPK_MAX, false, false, 0, 0>(a, r, s);
+        }
     }
     return KG_LAUNCH_CHECK();
 }
@@ -195,6 +284,28 @@ hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_po
         k_merge<1><<<grid, block, 0, s>>>(partial, n_parts, n_pods, out);
     else
         k_merge<KG_TOPK_MAX><<<grid, block, 0, s>>>(partial, n_parts, n_pods, out);
+    return KG_LAUNCH_CHECK();
+}
+
+hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k,
+                            const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, const uint32_t* big_list,
+                            const uint32_t* big_count, uint32_t index_base, const KCfg& cfg, uint64_t* out,
+                            hipStream_t s) {
+    dim3 grid((n_pods + 255) / 256), block(256);
+    if (k == 1)
+        k_merge_big<1><<<grid, block, 0, s>>>(partial, n_parts, n_pods, nodes, zones, pods, big_list, big_count,
+                                              index_base, cfg, out);
+    else
+        k_merge_big<KG_TOPK_MAX><<<grid, block, 0, s>>>(partial, n_parts, n_pods, nodes, zones, pods, big_list,
+                                                        big_count, index_base, cfg, out);
+    return KG_LAUNCH_CHECK();
+}
+
+hipError_t launch_big_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t* big_list, uint32_t* big_count,
+                           hipStream_t s) {
+    hipError_t e = hipMemsetAsync(big_count, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n_nodes == 0) return e;
+    k_big_scan<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, n_nodes, big_list, big_count);
     return KG_LAUNCH_CHECK();
 }
 

@@ -1,12 +1,22 @@
 // kg_layout.h — device-resident layout of the node snapshot and pod batch (host + device view).
 //
-// Node snapshot: one 320-byte record per node (array of records, 256-byte aligned array base).
-// The select kernel walks nodes in wave-uniform order, so a record is fetched with a handful of
-// scalar (s_load_dwordx16) loads and every field lives in SGPRs while the 64 lanes evaluate 64
-// different pods; NUMA zone tables are kept in a side array read only for NUMA-policy nodes.
-// Pods: struct-of-arrays, one lane per pod (coalesced dwordx2 loads, loaded once per kernel).
+// Node snapshot: one 512-byte record per node. Slots [0, 40) are the authoritative int64 state
+// (what Assume/Forget change); slots [40, 64) are exact float64 derivations of it ("headroom"
+// values such as allocatable - requested) recomputed by derive_node() whenever the int state
+// changes — on the host at upload and on the device after every Assume. The select kernel walks
+// nodes in wave-uniform order, so a record arrives through the scalar cache (s_load_dwordx16) and
+// lives in SGPRs while 64 lanes evaluate 64 different pods; NUMA zone tables are a side array read
+// only for SingleNUMANode nodes.
+// Pods: struct-of-arrays, one lane per pod (coalesced loads, once per kernel).
 #pragma once
 #include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__)
+#define KG_HD __host__ __device__
+#else
+#define KG_HD
+#endif
 
 namespace kg {
 
@@ -19,13 +29,53 @@ enum NodeSlot : int {
     N_LA_FCUT_NP0, N_LA_FCUT_NP1, N_LA_FCUT_PROD0, N_LA_FCUT_PROD1,
     N_LA_FBASE_NP0, N_LA_FBASE_NP1, N_LA_FBASE_PROD0, N_LA_FBASE_PROD1,
     N_LA_SBASE_NP0, N_LA_SBASE_NP1, N_LA_SBASE_PROD0, N_LA_SBASE_PROD1,
-    N_FLAGS, N_CPUSET, N_AMP_CPUSET, N_SPARE0,
-    // reciprocals (IEEE double bit patterns) of the static divisors
+    N_CPUSET, N_AMP_CPUSET, N_SPARE0, N_SPARE1,
+    N_INT_SLOTS,
+    // ---- fast block [32, 64): read by the select kernel with wide scalar loads per node ----
+    //  * N_FLAGS: low 32 bits device flags, high 32 bits the node's snapshot index (records are
+    //    stored grouped by storage class, see node_class);
+    //  * static slots (host, at upload; never touched by derive_node): upward-rounded reciprocals
+    //    of the divisors and the plugin weights already masked by "capacity != 0";
+    //  * derived slots (derive_node): headrooms x100 as exact float64 integers.
+    FAST_BEGIN = 32,
+    N_FLAGS = 32,
+    // 1/capacity rounded toward +inf (0 for capacity 0): floor((F*100 - x*100) * rcp) is the exact
+    // truncating quotient for 0 <= F <= capacity < 2^44 (see lr100 in kg_eval.h)
     N_RCP_CPU, N_RCP_MEM, N_RCP_SC0, N_RCP_SC1, N_RCP_LA0, N_RCP_LA1,
-    N_SPARE1, N_SPARE2,
+    N_WPACK_NRF,          // 4 x uint16: 2 x LeastAllocated weight of cpu, memory, scalar0, scalar1 (0 if capacity 0)
+    N_WPACK_NUMA,         // uint16 2*w_cpu, uint16 2*w_mem (0 if capacity 0), float 0.5 / (w_cpu + w_mem)
+    D_FIT_CPU,            // 100 * max(0, alloc - requested): Fits (pod request r fails iff 100 r > this)
+    D_FIT_MEM, D_FIT_EPH, D_FIT_SC0, D_FIT_SC1,
+    D_LR_NZ_CPU,          // 100 * (alloc - nonzero requested): LeastAllocated cpu
+    D_LR_NZ_MEM,
+    D_LR_SC0, D_LR_SC1,   // 100 * (alloc - requested) of the scalar resources
+    D_LA_HEAD_NP0, D_LA_HEAD_NP1,      // 100 * (usage cut-off - filter base), non-prod / prod profile
+    D_LA_HEAD_PROD0, D_LA_HEAD_PROD1,
+    D_LA_SFREE_NP0, D_LA_SFREE_NP1,    // 100 * (LoadAware allocatable - non-prod score base)
+    D_LA_SDELTA0, D_LA_SDELTA1,        // 100 * (non-prod score base - prod score base)
+    D_NUMA_FREE_CPU,      // 100 * (alloc_cpu - requested_cpu): NodeNUMAResource score, no amplification
+    D_NUMA_FREE_MEM,
+    D_AMP_FIT,            // 100 * max(0, alloc_cpu - amplified requested): filterAmplifiedCPUs (2^62 if no amplification)
+    D_AMP_DELTA,          // 100 * (requested - amplified requested): scoreWithAmplifiedCPUs (0 if no amplification)
+    N_SPARE2, N_SPARE3,
     N_SLOTS
 };
-static_assert(N_SLOTS == 40, "node record is 40 x 8 bytes");
+static_assert(N_INT_SLOTS == 32, "int section is 32 x 8 bytes");
+static_assert(N_SLOTS == 64, "node record is 64 x 8 bytes");
+
+// The fast block as the select kernel sees it (a by-value copy -> wide scalar loads).
+struct alignas(64) FastRec {
+    int64_t flags;  // low: flags, high: snapshot index
+    double rcp_cpu, rcp_mem, rcp_sc0, rcp_sc1, rcp_la0, rcp_la1;
+    uint64_t wpack_nrf, wpack_numa;
+    double fit_cpu, fit_mem, fit_eph, fit_sc0, fit_sc1;
+    double lr_nz_cpu, lr_nz_mem, lr_sc0, lr_sc1;
+    double la_head_np0, la_head_np1, la_head_prod0, la_head_prod1;
+    double la_sfree_np0, la_sfree_np1, la_sdelta0, la_sdelta1;
+    double numa_free_cpu, numa_free_mem, amp_fit, amp_delta;
+    int64_t spare2, spare3;
+};
+static_assert(sizeof(FastRec) == 8 * (N_SLOTS - FAST_BEGIN), "fast block layout");
 
 struct alignas(64) NodeRec {
     int64_t v[N_SLOTS];
@@ -42,14 +92,113 @@ enum : uint32_t {
     F_NUMA_POLICY_SHIFT = 8,   // 4 bits KG_NUMA_*
     F_NUMA_ZONES_SHIFT = 12,   // 4 bits zone count
     F_AMP = 1u << 16,          // cpu amplification ratio > 1
+    F_PODS_FULL = 1u << 17,    // len(Pods) + 1 > AllowedPodNumber (derived)
+    F_BIG = 1u << 18,          // some value is outside the exact float64 fast path (derived)
+    F_DERIVED_MASK = F_PODS_FULL | F_BIG,
 };
 enum : uint32_t { FMODE_CHECK = 0, FMODE_PASS = 1, FMODE_FAIL_EXPIRED = 2 };
 
 constexpr int MAX_ZONES = 4;
+// Fast view of one NUMA zone (select kernel, SingleNUMANode class): derived headrooms x100 plus
+// static reciprocals / masked weights set by the host at upload.
+struct alignas(16) ZoneFast {
+    double avail_cpu, avail_mem;  // 100 * max(0, total - used); -1 when that is 0 (never eligible)
+    double hint_cpu, hint_mem;    // 100 * (total - max(0, total - available)): hint-score headroom
+    double free_cpu, free_mem;    // 100 * (total - used): allocation-score headroom
+    double rcp_cpu, rcp_mem;      // static: 1/total rounded toward +inf (0 if total 0)
+    uint64_t wpack;               // static: uint16 2*hint_w_cpu, 2*hint_w_mem, 2*w_cpu, 2*w_mem (0 if total 0)
+    uint64_t hpack;               // static: float 0.5/(hint weights), float 0.5/(score weights)
+};
 struct alignas(64) ZoneRec {
     int64_t cpu[MAX_ZONES], mem[MAX_ZONES], cpu_used[MAX_ZONES], mem_used[MAX_ZONES];
     double rcp_cpu[MAX_ZONES], rcp_mem[MAX_ZONES];
+    ZoneFast zf[MAX_ZONES];
 };
+
+// Magnitude bound of the float64 fast path: operands below 2^44 keep 100 * headroom below 2^51
+// (exact) and make the upward-rounded reciprocal's quotient exact after truncation.
+constexpr int64_t FAST_LIMIT = (int64_t)1 << 44;
+
+KG_HD inline bool kg_big(int64_t x) { return x >= FAST_LIMIT || x <= -FAST_LIMIT; }
+
+KG_HD inline int64_t kg_bits(double d) {
+    int64_t b;
+    memcpy(&b, &d, 8);
+    return b;
+}
+
+KG_HD inline double x100(int64_t x) { return (double)x * 100.0; }  // exact for |x| < 2^46
+
+KG_HD inline uint32_t node_index(const NodeRec& r) { return (uint32_t)((uint64_t)r.v[N_FLAGS] >> 32); }
+
+// Recompute the derived section of a node record (flags F_PODS_FULL / F_BIG, headrooms, zone
+// headrooms) from its int section. Used by the host runtime at upload and by the device after
+// Assume/Forget, so both sides produce identical bits. Static slots are left alone.
+KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
+    int64_t* v = r.v;
+    uint32_t f = (uint32_t)v[N_FLAGS] & ~(uint32_t)F_DERIVED_MASK;
+    if (v[N_NUM_PODS] + 1 > v[N_ALLOC_PODS]) f |= F_PODS_FULL;
+    // F_BIG: some operand is outside the fast path (magnitude >= 2^44, or a negative quantity,
+    // which could push a headroom above its capacity); such nodes take the integer path
+    bool big = false;
+    for (int s = N_ALLOC_CPU; s <= N_LA_SBASE_PROD1; s++) {
+        if (s == N_ALLOC_PODS || s == N_NUM_PODS) continue;
+        if (s >= N_LA_FCUT_NP0 && s <= N_LA_FCUT_PROD1) continue;  // cut-offs may be INT64_MAX or -1
+        big = big || kg_big(v[s]) || v[s] < 0;
+    }
+    big = big || kg_big(v[N_CPUSET]) || kg_big(v[N_AMP_CPUSET]) || v[N_CPUSET] < 0 || v[N_AMP_CPUSET] < v[N_CPUSET];
+    for (uint32_t q = 0; q < (uint32_t)MAX_ZONES; q++) {
+        const int64_t tc = z.cpu[q], tm = z.mem[q], uc = z.cpu_used[q], um = z.mem_used[q];
+        big = big || kg_big(tc) || kg_big(tm) || kg_big(uc) || kg_big(um) || uc < 0 || um < 0;
+        const int64_t ac = tc - uc < 0 ? 0 : tc - uc, am = tm - um < 0 ? 0 : tm - um;
+        const int64_t rc = tc - ac < 0 ? 0 : tc - ac, rm = tm - am < 0 ? 0 : tm - am;
+        ZoneFast& zf = z.zf[q];
+        zf.avail_cpu = ac != 0 ? x100(ac) : -1.0;
+        zf.avail_mem = am != 0 ? x100(am) : -1.0;
+        zf.hint_cpu = x100(tc - rc);
+        zf.hint_mem = x100(tm - rm);
+        zf.free_cpu = x100(tc - uc);
+        zf.free_mem = x100(tm - um);
+    }
+    if (big) f |= F_BIG;
+    v[N_FLAGS] = (int64_t)(((uint64_t)v[N_FLAGS] & 0xFFFFFFFF00000000ull) | f);
+    auto fit = [](int64_t x) { return kg_bits(x100(x < 0 ? 0 : x)); };
+    v[D_FIT_CPU] = fit(v[N_ALLOC_CPU] - v[N_REQ_CPU]);
+    v[D_FIT_MEM] = fit(v[N_ALLOC_MEM] - v[N_REQ_MEM]);
+    v[D_FIT_EPH] = fit(v[N_ALLOC_EPH] - v[N_REQ_EPH]);
+    v[D_FIT_SC0] = fit(v[N_SC_ALLOC0] - v[N_SC_REQ0]);
+    v[D_FIT_SC1] = fit(v[N_SC_ALLOC1] - v[N_SC_REQ1]);
+    v[D_LR_NZ_CPU] = kg_bits(x100(v[N_ALLOC_CPU] - v[N_NZ_CPU]));
+    v[D_LR_NZ_MEM] = kg_bits(x100(v[N_ALLOC_MEM] - v[N_NZ_MEM]));
+    v[D_LR_SC0] = kg_bits(x100(v[N_SC_ALLOC0] - v[N_SC_REQ0]));
+    v[D_LR_SC1] = kg_bits(x100(v[N_SC_ALLOC1] - v[N_SC_REQ1]));
+    // cut-offs may be INT64_MAX ("no check"): the float64 difference stays >= 2^53 there, above any
+    // fast-path estimate, and is exact everywhere else
+    auto head = [](int64_t cut, int64_t base) { return kg_bits(((double)cut - (double)base) * 100.0); };
+    v[D_LA_HEAD_NP0] = head(v[N_LA_FCUT_NP0], v[N_LA_FBASE_NP0]);
+    v[D_LA_HEAD_NP1] = head(v[N_LA_FCUT_NP1], v[N_LA_FBASE_NP1]);
+    v[D_LA_HEAD_PROD0] = head(v[N_LA_FCUT_PROD0], v[N_LA_FBASE_PROD0]);
+    v[D_LA_HEAD_PROD1] = head(v[N_LA_FCUT_PROD1], v[N_LA_FBASE_PROD1]);
+    v[D_LA_SFREE_NP0] = kg_bits(x100(v[N_LA_ALLOC0] - v[N_LA_SBASE_NP0]));
+    v[D_LA_SFREE_NP1] = kg_bits(x100(v[N_LA_ALLOC1] - v[N_LA_SBASE_NP1]));
+    v[D_LA_SDELTA0] = kg_bits(x100(v[N_LA_SBASE_NP0] - v[N_LA_SBASE_PROD0]));
+    v[D_LA_SDELTA1] = kg_bits(x100(v[N_LA_SBASE_NP1] - v[N_LA_SBASE_PROD1]));
+    v[D_NUMA_FREE_CPU] = kg_bits(x100(v[N_ALLOC_CPU] - v[N_REQ_CPU]));
+    v[D_NUMA_FREE_MEM] = kg_bits(x100(v[N_ALLOC_MEM] - v[N_REQ_MEM]));
+    // filterAmplifiedCPUs: requested' = requested - cs + Amplify(cs) when requested >= cs > 0
+    const int64_t req = v[N_REQ_CPU], cs = v[N_CPUSET], acs = v[N_AMP_CPUSET];
+    const int64_t req_f = (req >= cs && cs > 0) ? req - cs + acs : req;
+    const bool amp = (f & F_AMP) != 0;
+    v[D_AMP_FIT] = amp ? fit(v[N_ALLOC_CPU] - req_f) : kg_bits(4611686018427387904.0);
+    // scoreWithAmplifiedCPUs: requested - cs + Amplify(cs) unconditionally
+    v[D_AMP_DELTA] = kg_bits(amp ? x100(cs - acs) : 0.0);
+}
+
+// Storage class of a node record: the select kernel is specialised per class and the snapshot is
+// stored grouped by class (class 0 first), each group in ascending snapshot order.
+KG_HD inline int node_class(const NodeRec& r) {
+    return (((uint32_t)r.v[N_FLAGS] >> F_NUMA_POLICY_SHIFT) & 15u) == 3u /* KG_NUMA_SINGLE_NODE */ ? 1 : 0;
+}
 
 // Pod batch (device pointers, SoA). flags: low 16 bits KG_POD_*, bits 16..19 pod NUMA policy.
 struct PodsDev {
@@ -66,15 +215,17 @@ struct PodsDev {
 };
 
 // Scoring / filtering configuration passed by value to every kernel.
+// Weights are host-validated to [0, 2^20] so int32 holds them (fewer SGPRs in the select loop).
 struct KCfg {
     uint32_t plugins;
-    uint32_t la_score_enabled, la_score_prod, pad0;
-    int64_t w_nrf, w_la, w_numa;
-    int64_t nrf_w[4];  // cpu, memory, scalar0, scalar1
-    int64_t la_w[2];
-    int64_t la_dom_w;
-    int64_t la_wsum;   // Σ la_w (+ dominant) — constant per profile
-    int64_t numa_w_cpu, numa_w_mem, numa_hint_w_cpu, numa_hint_w_mem;
+    uint32_t la_score_enabled, la_score_prod;
+    int32_t w_nrf, w_la, w_numa;
+    int32_t nrf_w[4];  // cpu, memory, scalar0, scalar1
+    int32_t la_w[2];
+    int32_t la_dom_w;
+    int32_t la_wsum;   // Σ la_w + dominant weight — constant per profile
+    int32_t numa_w_cpu, numa_w_mem, numa_hint_w_cpu, numa_hint_w_mem;
+    float la_hw;       // 0.5 / la_wsum (0 when la_wsum is 0): fast-path weighted quotient
 };
 
 }  // namespace kg

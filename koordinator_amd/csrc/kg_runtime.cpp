@@ -52,9 +52,15 @@ struct kg_snap {
     uint32_t n = 0, base = 0;
     NodeRec* d_nodes = nullptr;
     ZoneRec* d_zones = nullptr;
-    std::vector<NodeRec> h_nodes;
+    uint32_t* d_big = nullptr;  // [0] = count, [1..] = list of F_BIG records (k_big_scan)
+    // Records are stored grouped by storage class (node_class: 0 = no per-zone scoring, 1 = NUMA
+    // SingleNUMANode), each group in ascending snapshot index; the high half of v[N_FLAGS] holds the snapshot index.
+    std::vector<NodeRec> h_nodes;  // device order
     std::vector<ZoneRec> h_zones;
+    std::vector<uint32_t> pos;     // snapshot index -> record position
+    uint32_t n0 = 0;               // records of class 0 (positions [0, n0))
     bool uploaded = false;
+    bool weights_small = false;  // per-resource weights <= 2^12: float64 fast path allowed
 };
 
 struct kg_pods {
@@ -73,6 +79,7 @@ struct kg_pods {
     uint32_t* d_step = nullptr;
     uint64_t* d_gather = nullptr;
     size_t gather_cap = 0;
+    bool fast_ok = false;  // every value below FAST_LIMIT and no pod NUMA policy
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -135,11 +142,36 @@ int64_t la_cut(int64_t thr, int64_t total) {
     return lo;
 }
 
+// 1/x rounded toward +inf (0 for x == 0): with it, trunc((F*100 - r*100) * rcp) is the exact
+// truncating quotient of the fast path (kg_eval.h lr100)
+double rcp_up(int64_t x) {
+    if (x == 0) return 0.0;
+    const double d = (double)x;
+    double r = 1.0 / d;
+    if (std::fma(r, d, -1.0) < 0.0) r = std::nextafter(r, std::numeric_limits<double>::infinity());
+    return r;
+}
+
 int64_t rcp_bits(int64_t x) {
-    double r = x != 0 ? 1.0 / (double)x : 0.0;
+    const double r = rcp_up(x);
     int64_t b;
     std::memcpy(&b, &r, 8);
     return b;
+}
+
+// 0.5 / w as float (0 for w == 0): the fast path's weighted quotient is trunc((2 sum + 1) * this)
+float half_rcp(int64_t w) { return w > 0 ? 0.5f * (1.0f / (float)w) : 0.0f; }
+
+uint64_t pack16(int64_t a, int64_t b, int64_t c, int64_t d) {
+    return ((uint64_t)(a & 0xFFFF)) | ((uint64_t)(b & 0xFFFF) << 16) | ((uint64_t)(c & 0xFFFF) << 32) |
+           ((uint64_t)(d & 0xFFFF) << 48);
+}
+
+uint64_t pack_f32(float lo, float hi) {
+    uint32_t a, b;
+    std::memcpy(&a, &lo, 4);
+    std::memcpy(&b, &hi, 4);
+    return (uint64_t)a | ((uint64_t)b << 32);
 }
 
 bool valid_weight(int64_t w) { return w >= 0 && w <= (1 << 20); }
@@ -171,6 +203,7 @@ kg_status build_kcfg(kg_ctx* ctx, const kg_config* c, KCfg* k) {
     k->numa_w_mem = c->numa_w_mem;
     k->numa_hint_w_cpu = c->numa_hint_w_cpu;
     k->numa_hint_w_mem = c->numa_hint_w_mem;
+    k->la_hw = half_rcp(k->la_wsum);
     return KG_OK;
 }
 
@@ -255,15 +288,31 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     v[N_RCP_SC1] = rcp_bits(v[N_SC_ALLOC1]);
     v[N_RCP_LA0] = rcp_bits(la_alloc[0]);
     v[N_RCP_LA1] = rcp_bits(la_alloc[1]);
+    // weights masked by "capacity != 0" (the LeastAllocated loops skip such resources), doubled
+    auto on = [](int64_t w, int64_t cap) { return (w != 0 && cap != 0) ? 2 * w : 0; };
+    v[N_WPACK_NRF] = (int64_t)pack16(on(c.nrf_w_cpu, v[N_ALLOC_CPU]), on(c.nrf_w_mem, v[N_ALLOC_MEM]),
+                                     on(c.nrf_w_sc[0], v[N_SC_ALLOC0]), on(c.nrf_w_sc[1], v[N_SC_ALLOC1]));
+    {
+        const int64_t wc = on(c.numa_w_cpu, v[N_ALLOC_CPU]), wm = on(c.numa_w_mem, v[N_ALLOC_MEM]);
+        v[N_WPACK_NUMA] = (int64_t)(pack16(wc, wm, 0, 0) | ((uint64_t)pack_f32(0.f, half_rcp((wc + wm) / 2)) & 0xFFFFFFFF00000000ull));
+    }
     for (int z = 0; z < KG_MAX_ZONES; z++) {
         zr->cpu[z] = COL(s->zone_cpu[z], i);
         zr->mem[z] = COL(s->zone_mem[z], i);
         zr->cpu_used[z] = COL(s->zone_cpu_used[z], i);
         zr->mem_used[z] = COL(s->zone_mem_used[z], i);
         if (zr->cpu[z] < 0 || zr->mem[z] < 0) return fail(ctx, KG_INVALID_ARG, "node %u: negative zone total", i);
-        zr->rcp_cpu[z] = zr->cpu[z] ? 1.0 / (double)zr->cpu[z] : 0.0;
-        zr->rcp_mem[z] = zr->mem[z] ? 1.0 / (double)zr->mem[z] : 0.0;
+        zr->rcp_cpu[z] = rcp_up(zr->cpu[z]);
+        zr->rcp_mem[z] = rcp_up(zr->mem[z]);
+        ZoneFast& zf = zr->zf[z];
+        zf.rcp_cpu = zr->rcp_cpu[z];
+        zf.rcp_mem = zr->rcp_mem[z];
+        const int64_t hc = on(c.numa_hint_w_cpu, zr->cpu[z]), hm = on(c.numa_hint_w_mem, zr->mem[z]);
+        const int64_t fc = on(c.numa_w_cpu, zr->cpu[z]), fm = on(c.numa_w_mem, zr->mem[z]);
+        zf.wpack = pack16(hc, hm, fc, fm);
+        zf.hpack = pack_f32(half_rcp((hc + hm) / 2), half_rcp((fc + fm) / 2));
     }
+    derive_node(*rec, *zr);
     return KG_OK;
 }
 
@@ -271,6 +320,16 @@ bool force_exact() {
     static int v = -1;
     if (v < 0) {
         const char* e = std::getenv("KG_FORCE_EXACT");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
+// KG_SELECT_INT=1: select kernel on the integer path only (A/B and parity checks of the fast path)
+bool force_int() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("KG_SELECT_INT");
         v = (e && e[0] == '1') ? 1 : 0;
     }
     return v == 1;
@@ -285,6 +344,26 @@ uint32_t select_chunk(uint32_t n_nodes, uint32_t n_pods) {
     uint32_t chunk = (n_nodes + n_chunks - 1) / n_chunks;
     chunk = std::max<uint32_t>(chunk, 32);
     return std::max<uint32_t>(1, std::min<uint32_t>(chunk, std::max<uint32_t>(n_nodes, 1)));
+}
+
+void set_node_index(NodeRec& r, uint32_t i) {
+    r.v[N_FLAGS] = (int64_t)(((uint64_t)r.v[N_FLAGS] & 0xFFFFFFFFull) | ((uint64_t)i << 32));
+}
+
+// Place records (indexed by snapshot index) in device order: class 0 then class 1, each ascending.
+void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>& zrs) {
+    const uint32_t n = s->n;
+    s->pos.resize(n);
+    uint32_t n0 = 0;
+    for (uint32_t i = 0; i < n; i++) n0 += node_class(recs[i]) == 0;
+    uint32_t a = 0, b = n0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t p = node_class(recs[i]) == 0 ? a++ : b++;
+        s->pos[i] = p;
+        s->h_nodes[p] = recs[i];
+        s->h_zones[p] = zrs[i];
+    }
+    s->n0 = n0;
 }
 
 kg_status record_begin(kg_ctx* ctx, hipEvent_t* a, hipEvent_t* b) {
@@ -391,14 +470,25 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
         delete s;
         return st;
     }
+    {
+        const int64_t rw[] = {cfg->nrf_w_cpu, cfg->nrf_w_mem, cfg->nrf_w_sc[0], cfg->nrf_w_sc[1], cfg->la_w[0],
+                              cfg->la_w[1], cfg->la_dominant_w, cfg->numa_w_cpu, cfg->numa_w_mem,
+                              cfg->numa_hint_w_cpu, cfg->numa_hint_w_mem};
+        s->weights_small = true;
+        for (int64_t w : rw) s->weights_small &= (w >= 0 && w <= 4096);
+        s->weights_small &= (cfg->la_w[0] + cfg->la_w[1] + cfg->la_dominant_w) <= 4096;
+    }
     s->n = n_nodes;
     s->base = index_base;
     s->h_nodes.resize(n_nodes);
     s->h_zones.resize(n_nodes);
     hipSetDevice(ctx->device);
     const size_t nb = sizeof(NodeRec) * std::max<uint32_t>(n_nodes, 1), zb = sizeof(ZoneRec) * std::max<uint32_t>(n_nodes, 1);
-    if (hipMalloc(&s->d_nodes, nb) != hipSuccess || hipMalloc(&s->d_zones, zb) != hipSuccess) {
+    if (hipMalloc(&s->d_nodes, nb) != hipSuccess || hipMalloc(&s->d_zones, zb) != hipSuccess ||
+        hipMalloc(&s->d_big, sizeof(uint32_t) * ((size_t)n_nodes + 1)) != hipSuccess ||
+        hipMemset(s->d_big, 0, sizeof(uint32_t)) != hipSuccess) {
         hipFree(s->d_nodes);
+        hipFree(s->d_zones);
         delete s;
         return fail(ctx, KG_OOM, "snapshot of %u nodes", n_nodes);
     }
@@ -410,13 +500,18 @@ kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
     if (!s || !cols) return KG_INVALID_ARG;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
+    std::vector<NodeRec> recs(s->n);
+    std::vector<ZoneRec> zrs(s->n);
     for (uint32_t i = 0; i < s->n; i++) {
-        kg_status st = build_row(ctx, s->cfg, cols, i, &s->h_nodes[i], &s->h_zones[i]);
+        kg_status st = build_row(ctx, s->cfg, cols, i, &recs[i], &zrs[i]);
         if (st != KG_OK) return st;
+        set_node_index(recs[i], i);
     }
+    place_records(s, recs, zrs);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->uploaded = true;
     return KG_OK;
@@ -426,18 +521,47 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
     if (!s || (!rows && n) || !cols) return KG_INVALID_ARG;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
+    if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<NodeRec> recs(n);
+    std::vector<ZoneRec> zrs(n);
+    bool moved = false;  // a row changes storage class: the record groups are rebuilt
     for (uint32_t k = 0; k < n; k++) {
         if (rows[k] >= s->n) return fail(ctx, KG_INVALID_ARG, "row %u >= %u", rows[k], s->n);
-        NodeRec rec;
-        ZoneRec zr;
-        kg_status st = build_row(ctx, s->cfg, cols, k, &rec, &zr);
+        kg_status st = build_row(ctx, s->cfg, cols, k, &recs[k], &zrs[k]);
         if (st != KG_OK) return st;
-        s->h_nodes[rows[k]] = rec;
-        s->h_zones[rows[k]] = zr;
-        HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes + rows[k], &s->h_nodes[rows[k]], sizeof(NodeRec), hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(s->d_zones + rows[k], &s->h_zones[rows[k]], sizeof(ZoneRec), hipMemcpyHostToDevice, ctx->stream));
+        set_node_index(recs[k], rows[k]);
+        moved |= node_class(recs[k]) != (s->pos[rows[k]] < s->n0 ? 0u : 1u);
     }
+    if (moved) {
+        // device records carry Assume state: read them back, replace the rows, regroup, re-upload
+        HIP_TRY(ctx, hipMemcpyAsync(s->h_nodes.data(), s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(s->h_zones.data(), s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        std::vector<NodeRec> all(s->n);
+        std::vector<ZoneRec> allz(s->n);
+        for (uint32_t p = 0; p < s->n; p++) {
+            const uint32_t i = node_index(s->h_nodes[p]);
+            all[i] = s->h_nodes[p];
+            allz[i] = s->h_zones[p];
+        }
+        for (uint32_t k = 0; k < n; k++) {
+            all[rows[k]] = recs[k];
+            allz[rows[k]] = zrs[k];
+        }
+        place_records(s, all, allz);
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t p = s->pos[rows[k]];
+            s->h_nodes[p] = recs[k];
+            s->h_zones[p] = zrs[k];
+            HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes + p, &s->h_nodes[p], sizeof(NodeRec), hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(s->d_zones + p, &s->h_zones[p], sizeof(ZoneRec), hipMemcpyHostToDevice, ctx->stream));
+        }
+    }
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return KG_OK;
 }
@@ -452,8 +576,10 @@ kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
     HIP_TRY(ctx, hipMemcpyAsync(h.data(), s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(z.data(), s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    for (uint32_t i = 0; i < s->n; i++) {
-        const int64_t* v = h[i].v;
+    for (uint32_t pp = 0; pp < s->n; pp++) {
+        const int64_t* v = h[pp].v;
+        const ZoneRec& zr = z[pp];
+        const uint32_t i = node_index(h[pp]);
         if (o->req_cpu) o->req_cpu[i] = v[N_REQ_CPU];
         if (o->req_mem) o->req_mem[i] = v[N_REQ_MEM];
         if (o->req_eph) o->req_eph[i] = v[N_REQ_EPH];
@@ -471,8 +597,8 @@ kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
             if (o->la_sbase_prod[r]) o->la_sbase_prod[r][i] = v[sb_p[r]];
         }
         for (int zz = 0; zz < KG_MAX_ZONES; zz++) {
-            if (o->zone_cpu_used[zz]) o->zone_cpu_used[zz][i] = z[i].cpu_used[zz];
-            if (o->zone_mem_used[zz]) o->zone_mem_used[zz][i] = z[i].mem_used[zz];
+            if (o->zone_cpu_used[zz]) o->zone_cpu_used[zz][i] = zr.cpu_used[zz];
+            if (o->zone_mem_used[zz]) o->zone_mem_used[zz][i] = zr.mem_used[zz];
         }
     }
     return KG_OK;
@@ -484,6 +610,7 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipStreamSynchronize(s->ctx->stream);
     hipFree(s->d_nodes);
     hipFree(s->d_zones);
+    hipFree(s->d_big);
     delete s;
     return KG_OK;
 }
@@ -534,13 +661,20 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     std::vector<uint32_t> f(std::max<uint32_t>(n, 1));
     const int64_t* src[9] = {cols->req_cpu, cols->req_mem, cols->req_eph, cols->sc_req[0], cols->sc_req[1],
                              cols->nz_cpu, cols->nz_mem, cols->la_est[0], cols->la_est[1]};
+    bool fast = true;
     for (int c = 0; c < 9; c++)
-        for (uint32_t j = 0; j < n; j++) h[(size_t)c * n + j] = src[c] ? src[c][j] : 0;
+        for (uint32_t j = 0; j < n; j++) {
+            const int64_t x = src[c] ? src[c][j] : 0;
+            h[(size_t)c * n + j] = x;
+            fast &= !kg_big(x) && x >= 0;  // fast path: non-negative requests below 2^44
+        }
     for (uint32_t j = 0; j < n; j++) {
         const uint32_t pol = cols->numa_policy ? cols->numa_policy[j] : 0;
         if (pol > KG_NUMA_SINGLE_NODE) return fail(ctx, KG_INVALID_ARG, "pod %u: NUMA policy %u", j, pol);
         f[j] = (cols->flags ? (cols->flags[j] & 0xFFFFu) : 0u) | (pol << 16);
+        fast &= pol == KG_NUMA_NONE;
     }
+    p->fast_ok = fast;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     for (int c = 0; c < 9; c++)
         HIP_TRY(ctx, hipMemcpyAsync(p->d_cols + (size_t)c * p->cap, h.data() + (size_t)c * n, sizeof(int64_t) * n,
@@ -619,14 +753,23 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     a.zones = s->d_zones;
     a.pods = p->dev;
     a.n_pods = p->n;
-    a.n_nodes = s->n;
-    a.chunk = select_chunk(s->n, p->n);
-    a.n_chunks = s->n ? (s->n + a.chunk - 1) / a.chunk : 1;
+    uint32_t n_parts = 0;
+    const uint32_t bounds[3] = {0, s->n0, s->n};
+    for (int c = 0; c < 2; c++) {
+        SelectRange& r = a.range[c];
+        r.begin = bounds[c];
+        r.end = bounds[c + 1];
+        r.chunk = select_chunk(r.end - r.begin, p->n);  // each class launch fills the chip on its own
+        r.n_chunks = (r.end - r.begin + r.chunk - 1) / r.chunk;
+        r.part0 = n_parts;
+        n_parts += r.n_chunks;
+    }
     a.index_base = s->base;
     a.k = kk;
     a.exact = force_exact();
+    a.fast = !a.exact && !force_int() && s->weights_small && p->fast_ok;
     a.cfg = s->kcfg;
-    const size_t need = (size_t)a.n_chunks * p->n * kk;
+    const size_t need = (size_t)std::max<uint32_t>(n_parts, 1) * p->n * kk;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     if (need > p->partial_cap) {
         if (p->d_partial) {
@@ -651,7 +794,11 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
-    HIP_TRY(ctx, launch_merge(p->d_partial, a.n_chunks, p->n, kk, d_out, ctx->stream));
+    if (a.fast)
+        HIP_TRY(ctx, launch_merge_big(p->d_partial, n_parts, p->n, kk, s->d_nodes, s->d_zones, p->dev, s->d_big + 1,
+                                      s->d_big, s->base, s->kcfg, d_out, ctx->stream));
+    else
+        HIP_TRY(ctx, launch_merge(p->d_partial, n_parts, p->n, kk, d_out, ctx->stream));
     return KG_OK;
 }
 
@@ -710,6 +857,7 @@ kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_tota
     if (exec) hipGraphExecDestroy(exec);
     hipGraphDestroy(graph);
     HIP_TRY(ctx, e);
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
     std::vector<uint64_t> w(std::max<uint32_t>(n, 1));
@@ -729,7 +877,8 @@ kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) {
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, node, -1, 1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], -1, 1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return KG_OK;
 }
@@ -741,7 +890,8 @@ kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, node, zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return KG_OK;
 }

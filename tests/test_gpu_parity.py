@@ -123,6 +123,22 @@ def test_large_values_take_exact_integer_path(ctx):
     snap = engine.Snapshot(ctx, kc, big)
     batch = engine.PodBatch(ctx, pods)
     assert_verify_equal(engine.eval_verify(snap, batch), oracle_lib.eval_verify(kc, big, pods), "big values")
+    # select: the float64 fast path skips these nodes and the merge evaluates them on the integer path
+    for k in (1, 4):
+        assert np.array_equal(engine.eval_select(snap, batch, k), oracle_lib.select(kc, big, pods, k))
+
+
+def test_select_after_replay_uses_device_state(ctx):
+    cfg, nodes, pods = synth.small(600, 1200, seed=17, scale=6.0)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    first = abi.take(pods, np.arange(800))
+    engine.replay(snap, engine.PodBatch(ctx, first))
+    st = oracle_lib.OracleState(kc, nodes)
+    st.replay(first)
+    rest = abi.take(pods, np.arange(800, 1200))
+    got = engine.eval_select(snap, engine.PodBatch(ctx, rest), 4)
+    assert np.array_equal(got, oracle_lib.select(kc, st.table(), rest, 4))
 
 
 @pytest.mark.parametrize("seed,n_nodes,n_pods,scale", [(12, 400, 900, 10.0), (13, 1000, 3000, 8.0)])
@@ -193,6 +209,34 @@ def test_update_rows(ctx):
     assert_verify_equal(engine.eval_verify(snap, batch), oracle_lib.eval_verify(kc, merged, pods), "update_rows")
 
 
+def test_update_rows_changing_numa_policy_keeps_assumed_state(ctx):
+    """Rows that switch between the None and SingleNUMANode policies move between record groups;
+    the Assume state of every other node must survive the regrouping."""
+    cfg, nodes, pods = synth.small(300, 400, seed=18, scale=6.0)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    first = abi.take(pods, np.arange(200))
+    engine.replay(snap, engine.PodBatch(ctx, first))
+    st = oracle_lib.OracleState(kc, nodes)
+    st.replay(first)
+    state = st.table()
+    single = np.flatnonzero(nodes["numa_policy"] == abi.KG_NUMA_SINGLE_NODE)
+    plain = np.flatnonzero(nodes["numa_policy"] != abi.KG_NUMA_SINGLE_NODE)
+    assert len(single) and len(plain)
+    rows = np.array(sorted({int(single[0]), int(plain[0]), int(plain[-1])}), np.uint32)
+    upd = abi.take(nodes, rows.astype(np.int64))
+    upd["numa_policy"] = np.where(upd["numa_policy"] == abi.KG_NUMA_SINGLE_NODE, abi.KG_NUMA_NONE,
+                                  abi.KG_NUMA_SINGLE_NODE).astype(np.uint32)
+    snap.update_rows(rows, upd)
+    merged = {k: v.copy() for k, v in state.items()}
+    for k in merged:
+        merged[k][rows] = upd[k]
+    rest = abi.take(pods, np.arange(200, 400))
+    batch = engine.PodBatch(ctx, rest)
+    assert_verify_equal(engine.eval_verify(snap, batch), oracle_lib.eval_verify(kc, merged, rest), "regroup")
+    assert np.array_equal(engine.eval_select(snap, batch, 4), oracle_lib.select(kc, merged, rest, 4))
+
+
 def test_config2_full_size_properties(ctx):
     """10k nodes x 10k pods (config 2): sampled bit-exact selection + whole-matrix invariants."""
     cfg, nodes, pods = synth.cluster(2)
@@ -213,3 +257,98 @@ def test_config2_full_size_properties(ctx):
     # same batch evaluated again is bit-identical (deterministic reductions)
     again = engine.eval_select(snap, batch, 4)
     assert np.array_equal(keys, again)
+
+
+def _boundary_cluster(seed: int, n_nodes: int, n_pods: int):
+    """Nodes whose headrooms put 100 * (capacity - requested) / capacity exactly on, just above and just
+    below integers for the pod request they are tuned to, with capacities up to just below 2^44 (the
+    edge of the fast path), for every scored resource (NodeResourcesFit cpu/memory/scalars, LoadAware,
+    NodeNUMAResource node level and zones)."""
+    rng = np.random.default_rng(seed)
+    cfg, nodes, pods = synth.small(n_nodes, n_pods, seed=seed, numa=True)
+    # pod request variants: every pod requests everything (scalars too), a few distinct sizes
+    variants = np.array([1, 999, 1000, 7 * 1024 ** 3, 123456789], np.int64)
+    vj = rng.integers(0, len(variants), n_pods)
+    x = variants[vj]
+    for col in ("req_cpu", "req_mem", "req_eph", "sc_req0", "sc_req1", "nz_cpu", "nz_mem", "la_est0", "la_est1"):
+        pods[col] = x.copy()
+    pods["flags"] = pods["flags"] | abi.KG_POD_HAS_CPU | abi.KG_POD_HAS_MEM
+    caps_pool = np.array([100, 101, 1000, 32000, 96000, (1 << 44) - 1, (1 << 44) - 100, 17592186044399,
+                          (1 << 37), 3 * (1 << 40) + 7], np.int64)
+    tgt = variants[rng.integers(0, len(variants), n_nodes)]
+
+    def tuned(cap):
+        """node-side requested making (cap - req - x) * 100 / cap land on a boundary for pod size x = tgt"""
+        k = rng.integers(0, 101, len(cap))
+        mode = rng.integers(0, 3, len(cap))
+        out = np.zeros(len(cap), np.int64)
+        for i in range(len(cap)):
+            c, kk = int(cap[i]), int(k[i])
+            m0 = (-kk * c) % 100
+            m = [m0, m0 + 100 * ((c - 1 - m0) // 100), m0 + 100][mode[i]]
+            m = min(m, c - 1) if c > 1 else 0
+            if (kk * c + m) % 100:
+                m = m0
+            head = (kk * c + m) // 100  # cap - req - x
+            req = c - head - int(tgt[i])
+            out[i] = max(req, 0)
+        return out
+
+    for a, r in (("alloc_cpu", "req_cpu"), ("alloc_mem", "req_mem"), ("sc_alloc0", "sc_req0"),
+                 ("sc_alloc1", "sc_req1")):
+        cap = caps_pool[rng.integers(0, len(caps_pool), n_nodes)]
+        nodes[a] = cap
+        nodes[r] = tuned(cap)
+    nodes["nz_cpu"] = nodes["req_cpu"].copy()
+    nodes["nz_mem"] = nodes["req_mem"].copy()
+    nodes["alloc_eph"] = np.full(n_nodes, 1 << 43, np.int64)
+    nodes["req_eph"] = np.zeros(n_nodes, np.int64)
+    for k in range(2):
+        cap = caps_pool[rng.integers(0, len(caps_pool), n_nodes)]
+        nodes[f"la_alloc{k}"] = cap
+        nodes[f"la_thr_usage{k}"] = np.zeros(n_nodes, np.int64)
+        nodes[f"la_thr_prod{k}"] = np.zeros(n_nodes, np.int64)
+        nodes[f"la_sbase_np{k}"] = tuned(cap)
+        nodes[f"la_sbase_prod{k}"] = tuned(cap)
+        nodes[f"la_fbase_np{k}"] = nodes[f"la_sbase_np{k}"].copy()
+        nodes[f"la_fbase_prod{k}"] = nodes[f"la_sbase_prod{k}"].copy()
+    nodes["la_flags"] = np.full(n_nodes, abi.KG_LA_HAS_METRIC, np.uint32)
+    for z in range(2):
+        cap = caps_pool[rng.integers(0, len(caps_pool), n_nodes)]
+        nodes[f"zone_cpu{z}"] = cap
+        nodes[f"zone_cpu_used{z}"] = tuned(cap)
+        cap = caps_pool[rng.integers(0, len(caps_pool), n_nodes)]
+        nodes[f"zone_mem{z}"] = cap
+        nodes[f"zone_mem_used{z}"] = tuned(cap)
+    nodes["numa_zones"] = np.full(n_nodes, 2, np.uint32)
+    nodes["num_pods"] = np.zeros(n_nodes, np.int64)
+    return cfg, nodes, pods
+
+
+def _all_totals_via_select(ctx, kc, nodes, pods):
+    """Every (pod, node) total of the select kernel: snapshots of 4 nodes, top-4 keys expose all 4."""
+    n = abi.table_len(nodes)
+    batch = engine.PodBatch(ctx, pods)
+    out = np.full((abi.table_len(pods), n), -1, np.int64)
+    for g in range(0, n, 4):
+        idx = np.arange(g, min(n, g + 4))
+        snap = engine.Snapshot(ctx, kc, abi.take(nodes, idx), index_base=g)
+        keys = engine.eval_select(snap, batch, 4)
+        for t in range(4):
+            nz = keys[:, t] != 0
+            out[np.flatnonzero(nz), abi.key_node(keys[nz, t])] = abi.key_total(keys[nz, t])
+        snap.close()
+    return out
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_fast_path_quotient_boundaries(ctx, seed):
+    """The select kernel's fast path (upward-rounded reciprocals, float32 weighted means) must give
+    the integer path's totals on quotients sitting exactly on / next to integers up to 2^44."""
+    cfg, nodes, pods = _boundary_cluster(seed, 96, 64)
+    kc = cfg.kg_config()
+    got = _all_totals_via_select(ctx, kc, nodes, pods)
+    want = oracle_lib.eval_verify(kc, nodes, pods)
+    assert (want.total >= 0).mean() > 0.2
+    bad = np.argwhere(got != want.total)
+    assert len(bad) == 0, f"{len(bad)} totals differ, first {bad[0]}: gpu={got[tuple(bad[0])]} oracle={want.total[tuple(bad[0])]}"
