@@ -360,7 +360,9 @@ __device__ __forceinline__ uint32_t wq(uint32_t sum2, float hw) { return (uint32
 
 __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) { return __umul24(a, b) + c; }
 
-__device__ __forceinline__ uint32_t u16(uint64_t pack, int k) { return (uint32_t)(pack >> (16 * k)) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t lo32(uint64_t pack) { return (uint32_t)pack; }
+
+__device__ __forceinline__ uint32_t hi32(uint64_t pack) { return (uint32_t)(pack >> 32); }
 
 __device__ __forceinline__ float f32hi(uint64_t pack) { return __uint_as_float((uint32_t)(pack >> 32)); }
 
@@ -377,7 +379,7 @@ __device__ __forceinline__ int32_t in_vgpr(int32_t x) {
 __device__ __forceinline__ KCfg cfg_in_vgprs(const KCfg& c) {
     KCfg v = c;
     v.w_nrf = in_vgpr(c.w_nrf);
-    v.w_la = in_vgpr(c.w_la);
+    v.w_la = in_vgpr(c.la_score_enabled ? c.w_la : 0);
     v.w_numa = in_vgpr(c.w_numa);
     v.la_w[0] = in_vgpr(2 * c.la_w[0]);  // doubled for wq
     v.la_w[1] = in_vgpr(2 * c.la_w[1]);
@@ -399,54 +401,50 @@ __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& 
 
     if constexpr ((PM & KG_PLUGIN_NRF) != 0) {
         // Fits: request r fails iff r > 0 and r > alloc - requested, i.e. 100 r > 100 max(0, headroom)
+        // ("Too many pods" is folded into fit_cpu by derive_node)
         const bool fit_fail = (p.cpu > r.fit_cpu) | (p.mem > r.fit_mem) | (p.eph > r.fit_eph) |
                               (p.sc0 > r.fit_sc0) | (p.sc1 > r.fit_sc1);
-        ok = ok & !fit_fail & !(f & F_PODS_FULL);
+        ok = ok & !fit_fail;
         // LeastAllocated (NonZeroRequested for cpu / memory, Requested for scalars the pod requests)
-        const uint64_t wp = r.wpack_nrf;
-        const uint32_t w0 = u16(wp, 0), w1 = u16(wp, 1);
-        const uint32_t w2 = __umul24(u16(wp, 2), p.sc0_on), w3 = __umul24(u16(wp, 3), p.sc1_on);
+        const uint32_t w0 = lo32(r.w_nrf01), w1 = hi32(r.w_nrf01);
+        const uint32_t w2 = __umul24(lo32(r.w_nrf23), p.sc0_on), w3 = __umul24(hi32(r.w_nrf23), p.sc1_on);
         uint32_t sum2 = mad24(lr100(r.lr_nz_cpu, p.nzc, r.rcp_cpu), w0, 1u);
         sum2 = mad24(lr100(r.lr_nz_mem, p.nzm, r.rcp_mem), w1, sum2);
         sum2 = mad24(lr100(r.lr_sc0, p.sc0, r.rcp_sc0), w2, sum2);
         sum2 = mad24(lr100(r.lr_sc1, p.sc1, r.rcp_sc1), w3, sum2);
         // Σ 2w = 0 -> sum2 = 1, and max(.., 2) gives trunc(1 * 0.5) = 0
-        const float wsum = (float)max(w0 + w1 + w2 + w3, 2u);
+        const float wsum = (float)max(hi32(r.w_aux) + w2 + w3, 2u);
         float h = __builtin_amdgcn_rcpf(wsum);
         h = fmaf(h, fmaf(-wsum, h, 1.0f), h);  // one Newton step: 1/(Σ 2w) = 0.5/Σw, <= 1 ulp
         total = mad24(c.w_nrf, wq(sum2, h), total);
     }
 
     if constexpr ((PM & KG_PLUGIN_LA) != 0) {
-        // Filter: usage cut-offs of the pod's profile (100 * (cut - base) vs 100 * estimate)
+        // Filter: usage cut-offs of the pod's profile (100 * (cut - base) vs 100 * estimate); the
+        // node's filter modes and profile choice are folded into the heads by derive_node
         const bool pod_prod = (p.flags & KG_POD_PROD) != 0;
-        const bool fprod = (f & F_LA_PROD_THR) && pod_prod;
-        const uint32_t mode_np = (f >> F_LA_FMODE_NP_SHIFT) & 3u, mode_pr = (f >> F_LA_FMODE_PROD_SHIFT) & 3u;
         const bool over_np = (p.e0 > r.la_head_np0) | (p.e1 > r.la_head_np1);
         const bool over_pr = (p.e0 > r.la_head_prod0) | (p.e1 > r.la_head_prod1);
-        const bool fail_np = (mode_np == FMODE_FAIL_EXPIRED) | ((mode_np == FMODE_CHECK) & over_np);
-        const bool fail_pr = (mode_pr == FMODE_FAIL_EXPIRED) | ((mode_pr == FMODE_CHECK) & over_pr);
-        const bool la_fail = ((p.flags & KG_POD_DAEMONSET) == 0) & (fprod ? fail_pr : fail_np);
+        const bool la_fail = ((p.flags & KG_POD_DAEMONSET) == 0) & (pod_prod ? over_pr : over_np);
         ok = ok & !la_fail;
-        // Score: least-used over the estimated usage
-        // profile select as an exact fma: (free_np - e) + delta * {0, 1}
+        // Score: least-used over the estimated usage; profile select as an exact fma:
+        // (free_np - e) + delta * {0, 1}. Nodes whose score is 0 carry rcp_la = 0.
         const uint32_t s0 = cvt_sat_u32(fma(r.la_sdelta0, p.la_sprod, r.la_sfree_np0 - p.e0) * r.rcp_la0);
         const uint32_t s1 = cvt_sat_u32(fma(r.la_sdelta1, p.la_sprod, r.la_sfree_np1 - p.e1) * r.rcp_la1);
         const uint32_t dom = min(min(s0, s1), 100u);
         uint32_t sum2 = mad24(s0, (uint32_t)c.la_w[0], 1u);
         sum2 = mad24(s1, (uint32_t)c.la_w[1], sum2);
         sum2 = mad24(dom, (uint32_t)c.la_dom_w, sum2);
-        const bool zero = !c.la_score_enabled || (f & F_LA_SCORE_ZERO);
-        total = mad24(c.w_la, zero ? 0u : wq(sum2, c.la_hw), total);
+        total = mad24(c.w_la, wq(sum2, c.la_hw), total);  // c.w_la is 0 when the score is disabled
     }
 
     if constexpr ((PM & KG_PLUGIN_NUMA) != 0) {
         const bool skip = (p.flags & KG_POD_NUMA_SKIP) != 0;
-        const uint32_t pol = (f >> F_NUMA_POLICY_SHIFT) & 15u;  // pod policies take eval_pair (host check)
-        bool nok = !(p.flags & KG_POD_CPU_BIND) && pol != KG_NUMA_RESTRICTED && pol != KG_NUMA_BEST_EFFORT;
-        nok = nok & !(p.cpu > r.amp_fit);  // amp_fit is 2^62 without amplification
-        const uint64_t wn = r.wpack_numa;
+        // filterAmplifiedCPUs (amp_fit is 2^62 without amplification, -1 on Restricted / BestEffort
+        // nodes, which leave the device path)
+        const bool nok0 = ((p.flags & KG_POD_CPU_BIND) == 0) & !(p.cpu > r.amp_fit);
         uint32_t s_numa;
+        bool nok = nok0;
         if constexpr (CLS == 1) {  // SingleNUMANode nodes (their own storage class): zone walk
             const uint32_t Z = (f >> F_NUMA_ZONES_SHIFT) & 15u;
             const bool has_cpu = (p.flags & KG_POD_HAS_CPU) != 0, has_mem = (p.flags & KG_POD_HAS_MEM) != 0;
@@ -459,26 +457,26 @@ __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& 
                 const bool elig = (!has_cpu | (p.cpu <= q.avail_cpu)) & (!has_mem | (p.mem <= q.avail_mem));
                 const uint32_t hc = lr100(q.hint_cpu, p.cpu, q.rcp_cpu), hm = lr100(q.hint_mem, p.mem, q.rcp_mem);
                 const uint32_t fc = lr100(q.free_cpu, p.cpu, q.rcp_cpu), fm = lr100(q.free_mem, p.mem, q.rcp_mem);
-                const uint32_t hint = wq(mad24(hm, u16(q.wpack, 1), mad24(hc, u16(q.wpack, 0), 1u)), f32lo(q.hpack));
-                const uint32_t fin = wq(mad24(fm, u16(q.wpack, 3), mad24(fc, u16(q.wpack, 2), 1u)), f32hi(q.hpack));
+                const uint32_t hint = wq(mad24(hm, hi32(q.w_hint), mad24(hc, lo32(q.w_hint), 1u)), f32lo(q.hpack));
+                const uint32_t fin = wq(mad24(fm, hi32(q.w_score), mad24(fc, lo32(q.w_score), 1u)), f32hi(q.hpack));
                 const bool take = elig & ((best < 0) | (hint > best_hint));
                 best = take ? (int32_t)z : best;
                 best_hint = take ? hint : best_hint;
                 best_score = take ? fin : best_score;
             }
-            nok &= (Z != 0) & !(has_any & (best < 0));
+            nok = nok & (Z != 0) & !(has_any & (best < 0));
             // a best hint equal to the default affinity (no request on NUMA resources, or one zone)
             // carries no affinity: node-level score without amplification
             const uint32_t sc = lr100(r.numa_free_cpu, p.cpu, r.rcp_cpu), sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
-            const uint32_t node_level = wq(mad24(sm, u16(wn, 1), mad24(sc, u16(wn, 0), 1u)), f32hi(wn));
+            const uint32_t node_level = wq(mad24(sm, hi32(r.w_numa), mad24(sc, lo32(r.w_numa), 1u)), f32lo(r.w_aux));
             s_numa = (!has_any || Z == 1) ? node_level : best_score;
         } else {
             // amplified requested for pods with a cpu request: (free - r) + delta * {0, 1}
             const uint32_t sc = cvt_sat_u32(fma(r.amp_delta, p.has_cpu, r.numa_free_cpu - p.cpu) * r.rcp_cpu);
             const uint32_t sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
-            s_numa = wq(mad24(sm, u16(wn, 1), mad24(sc, u16(wn, 0), 1u)), f32hi(wn));
+            s_numa = wq(mad24(sm, hi32(r.w_numa), mad24(sc, lo32(r.w_numa), 1u)), f32lo(r.w_aux));
         }
-        ok &= skip || nok;
+        ok = ok & (skip | nok);
         total = mad24(c.w_numa, skip ? 0u : s_numa, total);
     }
     const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - gidx);

@@ -42,8 +42,10 @@ enum NodeSlot : int {
     // 1/capacity rounded toward +inf (0 for capacity 0): floor((F*100 - x*100) * rcp) is the exact
     // truncating quotient for 0 <= F <= capacity < 2^44 (see lr100 in kg_eval.h)
     N_RCP_CPU, N_RCP_MEM, N_RCP_SC0, N_RCP_SC1, N_RCP_LA0, N_RCP_LA1,
-    N_WPACK_NRF,          // 4 x uint16: 2 x LeastAllocated weight of cpu, memory, scalar0, scalar1 (0 if capacity 0)
-    N_WPACK_NUMA,         // uint16 2*w_cpu, uint16 2*w_mem (0 if capacity 0), float 0.5 / (w_cpu + w_mem)
+    N_W_NRF01,            // uint32 x 2: 2 x LeastAllocated weight of cpu, memory (0 if capacity 0)
+    N_W_NRF23,            // uint32 x 2: same for scalar0, scalar1
+    N_W_NUMA,             // uint32 2*w_cpu, uint32 2*w_mem of the NodeNUMAResource score (0 if capacity 0)
+    N_W_AUX,              // float 0.5 / (w_cpu + w_mem) of the NUMA score | uint32 N_W_NRF01 sum
     D_FIT_CPU,            // 100 * max(0, alloc - requested): Fits (pod request r fails iff 100 r > this)
     D_FIT_MEM, D_FIT_EPH, D_FIT_SC0, D_FIT_SC1,
     D_LR_NZ_CPU,          // 100 * (alloc - nonzero requested): LeastAllocated cpu
@@ -57,7 +59,6 @@ enum NodeSlot : int {
     D_NUMA_FREE_MEM,
     D_AMP_FIT,            // 100 * max(0, alloc_cpu - amplified requested): filterAmplifiedCPUs (2^62 if no amplification)
     D_AMP_DELTA,          // 100 * (requested - amplified requested): scoreWithAmplifiedCPUs (0 if no amplification)
-    N_SPARE2, N_SPARE3,
     N_SLOTS
 };
 static_assert(N_INT_SLOTS == 32, "int section is 32 x 8 bytes");
@@ -67,13 +68,12 @@ static_assert(N_SLOTS == 64, "node record is 64 x 8 bytes");
 struct alignas(64) FastRec {
     int64_t flags;  // low: flags, high: snapshot index
     double rcp_cpu, rcp_mem, rcp_sc0, rcp_sc1, rcp_la0, rcp_la1;
-    uint64_t wpack_nrf, wpack_numa;
+    uint64_t w_nrf01, w_nrf23, w_numa, w_aux;
     double fit_cpu, fit_mem, fit_eph, fit_sc0, fit_sc1;
     double lr_nz_cpu, lr_nz_mem, lr_sc0, lr_sc1;
     double la_head_np0, la_head_np1, la_head_prod0, la_head_prod1;
     double la_sfree_np0, la_sfree_np1, la_sdelta0, la_sdelta1;
     double numa_free_cpu, numa_free_mem, amp_fit, amp_delta;
-    int64_t spare2, spare3;
 };
 static_assert(sizeof(FastRec) == 8 * (N_SLOTS - FAST_BEGIN), "fast block layout");
 
@@ -106,7 +106,8 @@ struct alignas(16) ZoneFast {
     double hint_cpu, hint_mem;    // 100 * (total - max(0, total - available)): hint-score headroom
     double free_cpu, free_mem;    // 100 * (total - used): allocation-score headroom
     double rcp_cpu, rcp_mem;      // static: 1/total rounded toward +inf (0 if total 0)
-    uint64_t wpack;               // static: uint16 2*hint_w_cpu, 2*hint_w_mem, 2*w_cpu, 2*w_mem (0 if total 0)
+    uint64_t w_hint;              // static: uint32 2*hint_w_cpu, 2*hint_w_mem (0 if total 0)
+    uint64_t w_score;             // static: uint32 2*w_cpu, 2*w_mem (0 if total 0)
     uint64_t hpack;               // static: float 0.5/(hint weights), float 0.5/(score weights)
 };
 struct alignas(64) ZoneRec {
@@ -163,7 +164,10 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
     if (big) f |= F_BIG;
     v[N_FLAGS] = (int64_t)(((uint64_t)v[N_FLAGS] & 0xFFFFFFFF00000000ull) | f);
     auto fit = [](int64_t x) { return kg_bits(x100(x < 0 ? 0 : x)); };
-    v[D_FIT_CPU] = fit(v[N_ALLOC_CPU] - v[N_REQ_CPU]);
+    const int64_t always_fail = kg_bits(-1.0);  // below every fast-path request (requests are >= 0)
+    const int64_t never_fail = kg_bits(4611686018427387904.0);  // 2^62: above every fast-path request
+    // "Too many pods" folded into the cpu check: every pod then fails it
+    v[D_FIT_CPU] = (f & F_PODS_FULL) ? always_fail : fit(v[N_ALLOC_CPU] - v[N_REQ_CPU]);
     v[D_FIT_MEM] = fit(v[N_ALLOC_MEM] - v[N_REQ_MEM]);
     v[D_FIT_EPH] = fit(v[N_ALLOC_EPH] - v[N_REQ_EPH]);
     v[D_FIT_SC0] = fit(v[N_SC_ALLOC0] - v[N_SC_REQ0]);
@@ -174,11 +178,18 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
     v[D_LR_SC1] = kg_bits(x100(v[N_SC_ALLOC1] - v[N_SC_REQ1]));
     // cut-offs may be INT64_MAX ("no check"): the float64 difference stays >= 2^53 there, above any
     // fast-path estimate, and is exact everywhere else
-    auto head = [](int64_t cut, int64_t base) { return kg_bits(((double)cut - (double)base) * 100.0); };
-    v[D_LA_HEAD_NP0] = head(v[N_LA_FCUT_NP0], v[N_LA_FBASE_NP0]);
-    v[D_LA_HEAD_NP1] = head(v[N_LA_FCUT_NP1], v[N_LA_FBASE_NP1]);
-    v[D_LA_HEAD_PROD0] = head(v[N_LA_FCUT_PROD0], v[N_LA_FBASE_PROD0]);
-    v[D_LA_HEAD_PROD1] = head(v[N_LA_FCUT_PROD1], v[N_LA_FBASE_PROD1]);
+    // The profile's filter mode is folded into the heads: PASS -> 2^62 (never over), FAIL_EXPIRED -> -1
+    // (always over); nodes without prod thresholds give prod pods the non-prod heads.
+    auto head = [&](uint32_t mode, int64_t cut, int64_t base) {
+        return mode == FMODE_PASS ? never_fail
+             : mode == FMODE_FAIL_EXPIRED ? always_fail : kg_bits(((double)cut - (double)base) * 100.0);
+    };
+    const uint32_t m_np = (f >> F_LA_FMODE_NP_SHIFT) & 3u, m_pr = (f >> F_LA_FMODE_PROD_SHIFT) & 3u;
+    v[D_LA_HEAD_NP0] = head(m_np, v[N_LA_FCUT_NP0], v[N_LA_FBASE_NP0]);
+    v[D_LA_HEAD_NP1] = head(m_np, v[N_LA_FCUT_NP1], v[N_LA_FBASE_NP1]);
+    const bool prod_thr = (f & F_LA_PROD_THR) != 0;
+    v[D_LA_HEAD_PROD0] = prod_thr ? head(m_pr, v[N_LA_FCUT_PROD0], v[N_LA_FBASE_PROD0]) : v[D_LA_HEAD_NP0];
+    v[D_LA_HEAD_PROD1] = prod_thr ? head(m_pr, v[N_LA_FCUT_PROD1], v[N_LA_FBASE_PROD1]) : v[D_LA_HEAD_NP1];
     v[D_LA_SFREE_NP0] = kg_bits(x100(v[N_LA_ALLOC0] - v[N_LA_SBASE_NP0]));
     v[D_LA_SFREE_NP1] = kg_bits(x100(v[N_LA_ALLOC1] - v[N_LA_SBASE_NP1]));
     v[D_LA_SDELTA0] = kg_bits(x100(v[N_LA_SBASE_NP0] - v[N_LA_SBASE_PROD0]));
@@ -189,7 +200,11 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
     const int64_t req = v[N_REQ_CPU], cs = v[N_CPUSET], acs = v[N_AMP_CPUSET];
     const int64_t req_f = (req >= cs && cs > 0) ? req - cs + acs : req;
     const bool amp = (f & F_AMP) != 0;
-    v[D_AMP_FIT] = amp ? fit(v[N_ALLOC_CPU] - req_f) : kg_bits(4611686018427387904.0);
+    // Restricted / BestEffort nodes are outside the device NUMA path: every non-skipped pod fails here
+    // (the verify path reports them KG_ST_UNSUPPORTED)
+    const uint32_t pol = (f >> F_NUMA_POLICY_SHIFT) & 15u;
+    const bool pol_host = pol == 1u /* KG_NUMA_BEST_EFFORT */ || pol == 2u /* KG_NUMA_RESTRICTED */;
+    v[D_AMP_FIT] = pol_host ? always_fail : amp ? fit(v[N_ALLOC_CPU] - req_f) : never_fail;
     // scoreWithAmplifiedCPUs: requested - cs + Amplify(cs) unconditionally
     v[D_AMP_DELTA] = kg_bits(amp ? x100(cs - acs) : 0.0);
 }

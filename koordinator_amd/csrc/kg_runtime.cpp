@@ -162,10 +162,7 @@ int64_t rcp_bits(int64_t x) {
 // 0.5 / w as float (0 for w == 0): the fast path's weighted quotient is trunc((2 sum + 1) * this)
 float half_rcp(int64_t w) { return w > 0 ? 0.5f * (1.0f / (float)w) : 0.0f; }
 
-uint64_t pack16(int64_t a, int64_t b, int64_t c, int64_t d) {
-    return ((uint64_t)(a & 0xFFFF)) | ((uint64_t)(b & 0xFFFF) << 16) | ((uint64_t)(c & 0xFFFF) << 32) |
-           ((uint64_t)(d & 0xFFFF) << 48);
-}
+uint64_t pack32(int64_t lo, int64_t hi) { return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32); }
 
 uint64_t pack_f32(float lo, float hi) {
     uint32_t a, b;
@@ -286,15 +283,23 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     v[N_RCP_MEM] = rcp_bits(v[N_ALLOC_MEM]);
     v[N_RCP_SC0] = rcp_bits(v[N_SC_ALLOC0]);
     v[N_RCP_SC1] = rcp_bits(v[N_SC_ALLOC1]);
-    v[N_RCP_LA0] = rcp_bits(la_alloc[0]);
-    v[N_RCP_LA1] = rcp_bits(la_alloc[1]);
+    // LoadAware Score is 0 on this node (no / expired / nil NodeMetric): the fast path's leastUsed
+    // terms vanish with a zero reciprocal (the integer path checks F_LA_SCORE_ZERO itself)
+    const bool la_zero = (f & F_LA_SCORE_ZERO) != 0;
+    v[N_RCP_LA0] = la_zero ? 0 : rcp_bits(la_alloc[0]);
+    v[N_RCP_LA1] = la_zero ? 0 : rcp_bits(la_alloc[1]);
     // weights masked by "capacity != 0" (the LeastAllocated loops skip such resources), doubled
     auto on = [](int64_t w, int64_t cap) { return (w != 0 && cap != 0) ? 2 * w : 0; };
-    v[N_WPACK_NRF] = (int64_t)pack16(on(c.nrf_w_cpu, v[N_ALLOC_CPU]), on(c.nrf_w_mem, v[N_ALLOC_MEM]),
-                                     on(c.nrf_w_sc[0], v[N_SC_ALLOC0]), on(c.nrf_w_sc[1], v[N_SC_ALLOC1]));
     {
+        const int64_t w0 = on(c.nrf_w_cpu, v[N_ALLOC_CPU]), w1 = on(c.nrf_w_mem, v[N_ALLOC_MEM]);
+        v[N_W_NRF01] = (int64_t)pack32(w0, w1);
+        v[N_W_NRF23] = (int64_t)pack32(on(c.nrf_w_sc[0], v[N_SC_ALLOC0]), on(c.nrf_w_sc[1], v[N_SC_ALLOC1]));
         const int64_t wc = on(c.numa_w_cpu, v[N_ALLOC_CPU]), wm = on(c.numa_w_mem, v[N_ALLOC_MEM]);
-        v[N_WPACK_NUMA] = (int64_t)(pack16(wc, wm, 0, 0) | ((uint64_t)pack_f32(0.f, half_rcp((wc + wm) / 2)) & 0xFFFFFFFF00000000ull));
+        v[N_W_NUMA] = (int64_t)pack32(wc, wm);
+        uint32_t hb;
+        const float hw = half_rcp((wc + wm) / 2);
+        std::memcpy(&hb, &hw, 4);
+        v[N_W_AUX] = (int64_t)pack32(hb, w0 + w1);
     }
     for (int z = 0; z < KG_MAX_ZONES; z++) {
         zr->cpu[z] = COL(s->zone_cpu[z], i);
@@ -309,7 +314,8 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
         zf.rcp_mem = zr->rcp_mem[z];
         const int64_t hc = on(c.numa_hint_w_cpu, zr->cpu[z]), hm = on(c.numa_hint_w_mem, zr->mem[z]);
         const int64_t fc = on(c.numa_w_cpu, zr->cpu[z]), fm = on(c.numa_w_mem, zr->mem[z]);
-        zf.wpack = pack16(hc, hm, fc, fm);
+        zf.w_hint = pack32(hc, hm);
+        zf.w_score = pack32(fc, fm);
         zf.hpack = pack_f32(half_rcp((hc + hm) / 2), half_rcp((fc + fm) / 2));
     }
     derive_node(*rec, *zr);
