@@ -26,7 +26,7 @@ from koordinator_amd import abi, engine, synth  # noqa: E402
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak B/s (MI355X_MICROARCH.md, chip-level parameters)
 # Algorithmic bytes per (pod, node) eval, SURVEY.md §8d (scan model, node row read once per eval):
 # NodeResourcesFit 120 B + LoadAware 52 B + NodeNUMAResource 4 B + 0.2 x 64 B zone table = 188.8 B.
-B_EVAL = {1: 172.0, 2: 188.8}
+B_EVAL = {1: 172.0, 2: 188.8, 4: 188.8}
 METRIC = "Filter+Score pod-node evals/sec"
 
 
@@ -35,7 +35,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2])
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4],
+                    help="2: 10k nodes per GPU x 10k pods (weak scaling, default); 4: 100k nodes split over "
+                         "the GPUs x 10k pods (strong scaling); 1: the 1k x 500 CPU-harness case")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-replay", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
@@ -78,7 +80,7 @@ def cpu_baseline(cfg, nodes, pods, target_s):
                       f"{workers} workers, chunked like pkg/util/parallelize/parallelism.go:29-49"}
 
 
-def replay_rate(ctx, cfg):
+def replay_rate(ctx, cfg, with_cpu):
     """Config 3: 50k pods placed one by one on 10k nodes with device-resident Assume."""
     _, nodes, pods = synth.cluster(3)
     kc = cfg.kg_config()
@@ -91,9 +93,24 @@ def replay_rate(ctx, cfg):
     node, _ = engine.replay(snap, batch)
     dt = time.perf_counter() - t0
     placed = int((node >= 0).sum())
-    return {"pods_placed_per_s": batch.n / dt, "pods": batch.n, "placed": placed,
-            "unschedulable": batch.n - placed, "seconds": round(dt, 4),
-            "workload": "config3: 10k nodes x 50k pods, one pod per cycle, Assume on device"}
+    out = {"pods_placed_per_s": batch.n / dt, "pods": batch.n, "placed": placed,
+           "unschedulable": batch.n - placed, "seconds": round(dt, 4),
+           "workload": "config3: 10k nodes x 50k pods, one pod per cycle, Assume on device"}
+    if with_cpu:
+        # CPU baseline: the oracle's sequential replay (one thread) of the first pods of the same sequence
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib  # test infrastructure: the CPU baseline leg only
+
+        n = 1500
+        st = oracle_lib.OracleState(kc, nodes)
+        t0 = time.perf_counter()
+        want, _ = st.replay(abi.take(pods, np.arange(n)))
+        cdt = time.perf_counter() - t0
+        assert np.array_equal(want, node[:n])  # same placements as the device replay
+        out["cpu_baseline"] = {"value": n / cdt, "unit": "pods/s", "cores": 1, "kind": "port",
+                               "sample": f"first {n} pods of the config-3 sequence, oracle/kg_oracle.c kgo_replay "
+                                         f"(sequential Filter+Score over all nodes + Assume), {cdt:.2f} s"}
+    return out
 
 
 def main():
@@ -108,17 +125,28 @@ def main():
         dist.init_process_group("gloo")
     ctx = engine.Context(local)
     cfg, nodes, pods = synth.cluster(a.config)
-    n_local = abi.table_len(nodes)
+    if a.config == 4:
+        # one 100k-node cluster, contiguous shard per rank (strong scaling)
+        bounds = np.linspace(0, abi.table_len(nodes), world + 1).astype(np.int64)
+        base = int(bounds[rank])
+        nodes = abi.take(nodes, np.arange(bounds[rank], bounds[rank + 1]))
+        n_local = abi.table_len(nodes)
+        n_total = int(bounds[-1])
+    else:
+        # one 10k-node shard per rank (weak scaling)
+        n_local = abi.table_len(nodes)
+        if world > 1:
+            nodes = synth.nodes(n_local, a.config + 10 * rank, numa=(a.config == 2))
+        base = rank * n_local
+        n_total = n_local * world
     if world > 1:
-        nodes = synth.nodes(n_local, a.config + 10 * rank, numa=(a.config == 2))
         uid = [engine.shard_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.shard_init(uid[0], rank, world)
     kc = cfg.kg_config()
-    snap = engine.Snapshot(ctx, kc, nodes, index_base=rank * n_local)
+    snap = engine.Snapshot(ctx, kc, nodes, index_base=base)
     batch = engine.PodBatch(ctx, pods)
     n_pods = batch.n
-    n_total = n_local * world
 
     def step():
         if world > 1:
@@ -168,12 +196,12 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.config == 4 else "weak",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (PCG64 seed 0x6B6F6F7264, SURVEY.md §8d distributions)",
         "config": {"workload": f"config{a.config}: {n_local} nodes/GPU x {n_pods} pods, Filter+Score+selectHost "
-                               f"(NodeResourcesFit{'+LoadAware+NodeNUMAResource' if a.config == 2 else '+LoadAware'})",
+                               f"(NodeResourcesFit{'+LoadAware' if a.config == 1 else '+LoadAware+NodeNUMAResource'})",
                    "nodes_per_gpu": n_local, "nodes_total": n_total, "pods": n_pods,
                    "parallelism": f"node-shard x{world}" + (" + RCCL all-gather of per-pod best keys" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
@@ -184,7 +212,7 @@ def main():
     }
     if rank == 0 and world == 1:
         if not a.no_replay:
-            out["replay"] = replay_rate(ctx, cfg)
+            out["replay"] = replay_rate(ctx, cfg, not a.no_cpu_baseline)
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, nodes, pods, a.cpu_seconds)
     if rank == 0:

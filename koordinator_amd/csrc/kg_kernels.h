@@ -44,7 +44,7 @@ hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsD
                          uint32_t n_nodes, const KCfg& cfg, bool exact, const VerifyDev& o, hipStream_t s);
 hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t n_pods, uint32_t n_nodes,
                               uint32_t index_base, const KCfg& cfg, bool exact, const uint32_t* step_base,
-                              uint32_t step_off, uint64_t* winners, hipStream_t s);
+                              uint32_t step_off, uint64_t* winners, int8_t* zsel, hipStream_t s);
 hipError_t launch_bump(uint32_t* step_base, uint32_t by, hipStream_t s);
 hipError_t launch_assume(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t pod, uint32_t node,
                          int32_t zone, int64_t sign, const KCfg& cfg, bool exact, int32_t* zone_out, hipStream_t s);

@@ -169,44 +169,35 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 }
 
 // Step `step` of the sequential replay: Assume(pod step-1 -> its winner), then evaluate pod `step`.
+// One wave per workgroup (no LDS, no barrier): lane = node record. The zone each lane chose for its
+// node in the previous step is kept in zsel, so the winner's Reserve needs no re-evaluation; the
+// winner key and both pods are loaded up front, independently of each other.
 template <bool EXACT>
-__global__ __launch_bounds__(256) void k_replay(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, PodsDev pods,
-                                                uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, KCfg cfg,
-                                                const uint32_t* __restrict__ step_base, uint32_t step_off,
-                                                uint64_t* __restrict__ winners) {
-    __shared__ uint64_t red[4];
+__global__ __launch_bounds__(64) void k_replay(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, PodsDev pods,
+                                               uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, KCfg cfg,
+                                               const uint32_t* __restrict__ step_base, uint32_t step_off,
+                                               uint64_t* __restrict__ winners, int8_t* __restrict__ zsel) {
     const uint32_t step = (step_base ? *step_base : 0u) + step_off;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (step > n_pods) return;  // uniform: past the end of the batch
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     const bool live = i < n_nodes;
-    if (step > 0 && live) {
-        const uint64_t prev = winners[step - 1];
-        if (prev != 0ull) {
-            const uint32_t g = 0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull);
-            if (g == rec_gidx(nodes[i], index_base)) {
-                const PodV q = load_pod(pods, step - 1);
-                int64_t* n = nodes[i].v;
-                const PairOut o = eval_pair<EXACT>(cfg, n, zones + i, q);
-                apply_assume(cfg, n, zones + i, q, o.zone, 1);
-            }
-        }
+    const bool has_next = step < n_pods;
+    const uint64_t prev = step > 0 ? __hip_atomic_load(&winners[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const PodV q = load_pod(pods, step > 0 ? step - 1 : 0);
+    const PodV p = load_pod(pods, has_next ? step : 0);
+    if (live && prev != 0ull) {
+        const uint32_t g = 0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull);
+        if (g == rec_gidx(nodes[i], index_base)) apply_assume(cfg, nodes[i].v, zones + i, q, zsel[i], 1);
     }
-    if (step == n_pods) return;  // uniform: final step only applies the last Assume
+    if (!has_next) return;  // uniform: the final step only applies the last Assume
     uint64_t key = 0;
     if (live) {
-        const PodV p = load_pod(pods, step);
         const PairOut o = eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p);
         key = pair_key(cfg, o, rec_gidx(nodes[i], index_base));
+        zsel[i] = (int8_t)o.zone;
     }
     key = wave_max_u64(key);
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    if (lane == 0) red[wave] = key;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t m = red[0];
-        for (uint32_t w = 1; w < (blockDim.x >> 6); w++) m = red[w] > m ? red[w] : m;
-        if (m) atomicMax((unsigned long long*)&winners[step], (unsigned long long)m);
-    }
+    if (threadIdx.x == 0 && key) atomicMax((unsigned long long*)&winners[step], (unsigned long long)key);
 }
 
 __global__ void k_bump(uint32_t* step_base, uint32_t by) {
@@ -324,14 +315,14 @@ hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsD
 
 hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t n_pods, uint32_t n_nodes,
                               uint32_t index_base, const KCfg& cfg, bool exact, const uint32_t* step_base,
-                              uint32_t step_off, uint64_t* winners, hipStream_t s) {
-    dim3 grid((n_nodes + 255) / 256), block(256);
+                              uint32_t step_off, uint64_t* winners, int8_t* zsel, hipStream_t s) {
+    dim3 grid((n_nodes + 63) / 64), block(64);
     if (exact)
         k_replay<true><<<grid, block, 0, s>>>(nodes, zones, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                              step_off, winners);
+                                              step_off, winners, zsel);
     else
         k_replay<false><<<grid, block, 0, s>>>(nodes, zones, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                               step_off, winners);
+                                               step_off, winners, zsel);
     return KG_LAUNCH_CHECK();
 }
 

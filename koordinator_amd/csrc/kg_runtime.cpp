@@ -53,6 +53,7 @@ struct kg_snap {
     NodeRec* d_nodes = nullptr;
     ZoneRec* d_zones = nullptr;
     uint32_t* d_big = nullptr;  // [0] = count, [1..] = list of F_BIG records (k_big_scan)
+    int8_t* d_zsel = nullptr;   // replay: NUMA zone each record chose for the current pod
     // Records are stored grouped by storage class (node_class: 0 = no per-zone scoring, 1 = NUMA
     // SingleNUMANode), each group in ascending snapshot index; the high half of v[N_FLAGS] holds the snapshot index.
     std::vector<NodeRec> h_nodes;  // device order
@@ -80,6 +81,9 @@ struct kg_pods {
     uint64_t* d_gather = nullptr;
     size_t gather_cap = 0;
     bool fast_ok = false;  // every value below FAST_LIMIT and no pod NUMA policy
+    // replay graph (G steps) cached for the (snapshot buffers, batch size, configuration) it captured
+    hipGraphExec_t rexec = nullptr;
+    std::vector<uint8_t> rkey;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -492,6 +496,7 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
     const size_t nb = sizeof(NodeRec) * std::max<uint32_t>(n_nodes, 1), zb = sizeof(ZoneRec) * std::max<uint32_t>(n_nodes, 1);
     if (hipMalloc(&s->d_nodes, nb) != hipSuccess || hipMalloc(&s->d_zones, zb) != hipSuccess ||
         hipMalloc(&s->d_big, sizeof(uint32_t) * ((size_t)n_nodes + 1)) != hipSuccess ||
+        hipMalloc(&s->d_zsel, std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
         hipMemset(s->d_big, 0, sizeof(uint32_t)) != hipSuccess) {
         hipFree(s->d_nodes);
         hipFree(s->d_zones);
@@ -617,6 +622,7 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_nodes);
     hipFree(s->d_zones);
     hipFree(s->d_big);
+    hipFree(s->d_zsel);
     delete s;
     return KG_OK;
 }
@@ -702,6 +708,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     hipFree(p->d_step);
     hipFree(p->d_partial);
     hipFree(p->d_gather);
+    if (p->rexec) hipGraphExecDestroy(p->rexec);
     delete p;
     return KG_OK;
 }
@@ -829,6 +836,54 @@ kg_status kg_result_keys(kg_pods* p, uint64_t* out) {
     return KG_OK;
 }
 
+}  // extern "C"
+
+namespace {
+constexpr uint32_t REPLAY_G = 256;  // replay steps per captured graph
+
+std::vector<uint8_t> replay_key(const kg_snap* s, const kg_pods* p, bool exact) {
+    std::vector<uint8_t> k;
+    auto put = [&k](const void* x, size_t n) { k.insert(k.end(), (const uint8_t*)x, (const uint8_t*)x + n); };
+    put(&s->d_nodes, sizeof(s->d_nodes));
+    put(&s->d_zones, sizeof(s->d_zones));
+    put(&s->d_zsel, sizeof(s->d_zsel));
+    put(&s->n, sizeof(s->n));
+    put(&s->base, sizeof(s->base));
+    put(&s->kcfg, sizeof(s->kcfg));
+    put(&p->n, sizeof(p->n));
+    put(&exact, sizeof(exact));
+    return k;
+}
+
+// Capture REPLAY_G steps that read their base step from device memory, plus the bump of that base.
+kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact) {
+    kg_ctx* ctx = s->ctx;
+    std::vector<uint8_t> key = replay_key(s, p, exact);
+    if (p->rexec && key == p->rkey) return KG_OK;
+    if (p->rexec) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        hipGraphExecDestroy(p->rexec);
+        p->rexec = nullptr;
+    }
+    hipGraph_t graph = nullptr;
+    HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = hipSuccess;
+    for (uint32_t t = 0; t < REPLAY_G && e == hipSuccess; t++)
+        e = launch_replay_step(s->d_nodes, s->d_zones, p->dev, p->n, s->n, s->base, s->kcfg, exact, p->d_step, t,
+                               p->d_winners, s->d_zsel, ctx->stream);
+    if (e == hipSuccess) e = launch_bump(p->d_step, REPLAY_G, ctx->stream);
+    hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    if (e == hipSuccess) e = ec;
+    if (e == hipSuccess) e = hipGraphInstantiate(&p->rexec, graph, nullptr, nullptr, 0);
+    if (graph) hipGraphDestroy(graph);
+    HIP_TRY(ctx, e);
+    p->rkey = std::move(key);
+    return KG_OK;
+}
+}  // namespace
+
+extern "C" {
+
 kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
@@ -836,33 +891,16 @@ kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_tota
     std::lock_guard<std::mutex> g(ctx->mu);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint32_t n = p->n;
-    HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
     const bool exact = force_exact();
+    st = replay_graph(s, p, exact);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
-    // Steps 0..n: step i Assumes pod i-1 and evaluates pod i. Launched as captured hipGraphs of
-    // G steps that read their base step from device memory (bumped by the graph's last node).
-    const uint32_t G = 256;
-    HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-    hipError_t e = hipSuccess;
-    for (uint32_t t = 0; t < G && e == hipSuccess; t++)
-        e = launch_replay_step(s->d_nodes, s->d_zones, p->dev, n, s->n, s->base, s->kcfg, exact, p->d_step, t,
-                               p->d_winners, ctx->stream);
-    if (e == hipSuccess) e = launch_bump(p->d_step, G, ctx->stream);
-    hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
-    HIP_TRY(ctx, e);
-    HIP_TRY(ctx, ec);
-    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    if (e == hipSuccess) {
-        for (uint32_t done = 0; done <= n && e == hipSuccess; done += G) e = hipGraphLaunch(exec, ctx->stream);
-    }
-    if (exec) hipGraphExecDestroy(exec);
-    hipGraphDestroy(graph);
-    HIP_TRY(ctx, e);
+    // steps 0..n: step i Assumes pod i-1 and evaluates pod i
+    for (uint32_t done = 0; done <= n; done += REPLAY_G) HIP_TRY(ctx, hipGraphLaunch(p->rexec, ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;

@@ -129,14 +129,17 @@ def pods(p: int, config: int = 1, scale: float = 1.0, rng=None, la_factors=(85, 
 
 def cluster(config: int):
     """(SchedulerConfig, nodes, pods) of a BASELINE configuration (1: 1k x 500, 2: 10k x 10k,
-    3: 10k nodes x 50k replay pods)."""
+    3: 10k nodes x 50k replay pods, 4: 100k nodes x 10k pods)."""
     if config == 1:
         return bench_profile(numa=False), nodes(1000, 1), pods(500, 1)
     if config == 2:
         return bench_profile(numa=True), nodes(10_000, 2, numa=True), pods(10_000, 2)
     if config == 3:
-        # pods scaled so that 50k placements drive the cluster to ~90% cpu requested (§8d cfg3)
-        return bench_profile(numa=True), nodes(10_000, 3, numa=True), pods(50_000, 3, scale=1.6)
+        # pods scaled so that the 50k placements saturate the cluster: LoadAware usage thresholds bind first
+        # (cpu requested levels off near 51%), the last ~1.3k pods are unschedulable (SURVEY §8d cfg3)
+        return bench_profile(numa=True), nodes(10_000, 3, numa=True), pods(50_000, 3, scale=2.5)
+    if config == 4:
+        return bench_profile(numa=True), nodes(100_000, 4, numa=True), pods(10_000, 4)
     raise ValueError(config)
 
 

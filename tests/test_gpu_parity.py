@@ -352,3 +352,25 @@ def test_fast_path_quotient_boundaries(ctx, seed):
     assert (want.total >= 0).mean() > 0.2
     bad = np.argwhere(got != want.total)
     assert len(bad) == 0, f"{len(bad)} totals differ, first {bad[0]}: gpu={got[tuple(bad[0])]} oracle={want.total[tuple(bad[0])]}"
+
+
+def test_config4_100k_nodes_sampled(ctx):
+    """Config 4 cluster (100k nodes) on one GPU: sampled bit-exact selection, and the same keys when
+    the nodes are split into 4 contiguous shards merged with kg_merge_keys (the sharded path's merge)."""
+    cfg, nodes, pods = synth.cluster(4)
+    kc = cfg.kg_config()
+    n = abi.table_len(nodes)
+    rng = np.random.default_rng(4)
+    sub = abi.take(pods, rng.choice(abi.table_len(pods), 48, replace=False))
+    batch = engine.PodBatch(ctx, sub)
+    snap = engine.Snapshot(ctx, kc, nodes)
+    keys = engine.eval_select(snap, batch, 2)
+    snap.close()
+    assert np.array_equal(keys, oracle_lib.select(kc, nodes, sub, 2))
+    bounds = np.linspace(0, n, 5).astype(np.int64)
+    parts = []
+    for s in range(4):
+        sh = engine.Snapshot(ctx, kc, abi.take(nodes, np.arange(bounds[s], bounds[s + 1])), index_base=int(bounds[s]))
+        parts.append(engine.eval_select(sh, batch, 2))
+        sh.close()
+    assert np.array_equal(engine.merge_keys(np.stack(parts)), keys)
