@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 1
+#define KG_ABI_VERSION 2
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -48,6 +48,19 @@ extern "C" {
 #define KG_NSCALAR 2
 /* NUMA zones per node supported on device (nodenumaresource/node_allocation.go:221-243). */
 #define KG_MAX_ZONES 4
+/* DeviceShare: GPU minors per node and per-minor resources {gpu-core, gpu-memory-ratio, gpu-memory}
+ * (deviceshare/device_cache.go nodeDevice.deviceTotal / deviceFree, apis/extension/device_share.go). */
+#define KG_DEV_MINORS 8
+#define KG_DEV_R 3
+#define KG_DEV_CORE 0
+#define KG_DEV_RATIO 1
+#define KG_DEV_MEM 2
+/* ElasticQuota resource dimensions {cpu, memory, scalar0, scalar1}: the pod request columns
+ * req_cpu, req_mem, sc_req[0], sc_req[1] (elasticquota/plugin.go:279-281). */
+#define KG_QUOTA_R 4
+/* Reservation resource dimensions {cpu, memory, ephemeral-storage, scalar0, scalar1}
+ * (framework.Resource fields used by reservation/plugin.go:915-965). */
+#define KG_RSV_R 5
 
 typedef enum kg_status {
     KG_OK = 0,
@@ -62,6 +75,10 @@ typedef enum kg_status {
 #define KG_PLUGIN_NRF 0x1u  /* upstream NodeResourcesFit: Fits + LeastAllocated score          */
 #define KG_PLUGIN_LA 0x2u   /* LoadAwareScheduling (loadaware/load_aware.go)                     */
 #define KG_PLUGIN_NUMA 0x4u /* NodeNUMAResource (nodenumaresource/plugin.go, scoring.go)         */
+#define KG_PLUGIN_DEV 0x8u  /* DeviceShare GPU fit + score (deviceshare/plugin.go, scoring.go)      */
+#define KG_PLUGIN_RSV 0x10u /* Reservation restore / filter / score (reservation/plugin.go, scoring.go) */
+#define KG_PLUGIN_QUOTA 0x20u /* ElasticQuota PreFilter gate + Reserve (elasticquota/plugin.go)     */
+#define KG_PLUGIN_EXT (KG_PLUGIN_DEV | KG_PLUGIN_RSV | KG_PLUGIN_QUOTA)
 
 /* Node LoadAware flags (kg_node_columns.la_flags). Computed by the host at a frozen snapshot time. */
 #define KG_LA_HAS_METRIC 0x1u /* podAssignCache holds a NodeMetric for the node (pod_assign_cache.go:169-172) */
@@ -83,6 +100,14 @@ typedef enum kg_status {
 #define KG_POD_HAS_CPU 0x8u   /* "cpu" key present in PodRequests                                       */
 #define KG_POD_HAS_MEM 0x10u  /* "memory" key present in PodRequests                                    */
 #define KG_POD_CPU_BIND 0x20u /* LSE/LSR prod pod requesting cpuset binding: not on the device path      */
+#define KG_POD_NON_PREEMPTIBLE 0x40u /* extension.IsPodNonPreemptible (elasticquota/plugin.go:288)     */
+#define KG_POD_RSV_REQUIRED 0x80u    /* pod has a reservation affinity (reservation/transformer.go:148,
+                                      * stateData.hasAffinity): must allocate from a reservation      */
+
+/* Reservation allocate policies (apis/scheduling/v1alpha1 ReservationAllocatePolicy). */
+#define KG_RSV_DEFAULT 0u
+#define KG_RSV_ALIGNED 1u
+#define KG_RSV_RESTRICTED 2u
 
 /* Per-(pod,node) filter status bits (kg_verify_out.status). Plugin order follows the framework's
  * filter order: NodeResourcesFit, LoadAwareScheduling, NodeNUMAResource. */
@@ -103,6 +128,16 @@ typedef enum kg_status {
 #define KG_ST_NUMA_NO_RES 0x40000u   /* "node(s) missing NUMA resources"                      */
 #define KG_ST_NUMA_ALIGN 0x80000u    /* ErrNUMAHintCannotAligned                              */
 #define KG_ST_NUMA_MASK 0xFF0000u
+#define KG_ST_DEV_INSUFFICIENT 0x01000000u /* "Insufficient gpu devices" (Unschedulable, device_allocator.go:432) */
+#define KG_ST_DEV_NO_DEVICE 0x02000000u    /* no GPU minors on the node's Device (UnschedulableAndUnresolvable,
+                                              devicehandler_gpu.go:41-44)                              */
+#define KG_ST_DEV_MASK 0x03000000u
+#define KG_ST_RSV_AFFINITY 0x04000000u     /* ErrReasonReservationAffinity (reservation/plugin.go:366-368)  */
+#define KG_ST_RSV_NODE 0x08000000u         /* "Insufficient <r> by node" (reservation/plugin.go:498-525)    */
+#define KG_ST_RSV_RESERVATION 0x10000000u  /* reservation-level reasons / no reservation meets the pod      */
+#define KG_ST_RSV_MASK 0x1C000000u
+#define KG_ST_QUOTA 0x20000000u            /* ElasticQuota PreFilter: "Insufficient quotas" / non-preemptible
+                                              (pod-level, reported on every node)                       */
 #define KG_ST_UNSUPPORTED 0x80000000u /* pair needs the host path (e.g. cpuset binding)        */
 
 typedef struct kg_ctx kg_ctx;   /* one per device per scheduler profile */
@@ -129,6 +164,12 @@ typedef struct kg_config {
     /* NodeNUMAResource LeastAllocated ScoringStrategy (node score) and NUMAScoringStrategy (hints). */
     int64_t numa_w_cpu, numa_w_mem;
     int64_t numa_hint_w_cpu, numa_hint_w_mem;
+    /* DeviceShare / Reservation score plugin weights (config/manager/scheduler-config.yaml:91-96) and
+     * DeviceShare LeastAllocated weights over {gpu-core, gpu-memory-ratio, gpu-memory}, 0 = resource
+     * not listed (defaults ratio 1, memory 1: pkg/scheduler/apis/config/v1/defaults.go:254-277). */
+    int64_t weight_dev;
+    int64_t weight_rsv;
+    int64_t dev_w[KG_DEV_R];
 } kg_config;
 
 /* Node snapshot, struct-of-arrays host columns, n_nodes entries each (caller-owned, copied). */
@@ -160,6 +201,13 @@ typedef struct kg_node_columns {
     const int64_t* zone_mem[KG_MAX_ZONES];
     const int64_t* zone_cpu_used[KG_MAX_ZONES]; /* zone allocated                                     */
     const int64_t* zone_mem_used[KG_MAX_ZONES];
+    /* DeviceShare: the node's GPU minors (nodeDevice of deviceshare/device_cache.go). dev_minors < 0:
+     * the node has no Device object (Filter passes, Score 0: deviceshare/plugin.go:398-401,
+     * scoring.go:58-61); otherwise minors 0..dev_minors-1. dev_total / dev_free are row-major
+     * [node][KG_DEV_R][KG_DEV_MINORS] with 0 <= free <= total (NULL = no DeviceShare data). */
+    const int32_t* dev_minors;
+    const int64_t* dev_total;
+    const int64_t* dev_free;
 } kg_node_columns;
 
 /* Mutable node state that Assume/Forget change; used to read a snapshot back after kg_replay. */
@@ -169,6 +217,7 @@ typedef struct kg_node_state {
     int64_t *la_fbase_np[KG_LA_R], *la_fbase_prod[KG_LA_R];
     int64_t *la_sbase_np[KG_LA_R], *la_sbase_prod[KG_LA_R];
     int64_t *zone_cpu_used[KG_MAX_ZONES], *zone_mem_used[KG_MAX_ZONES];
+    int64_t* dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
 } kg_node_state;
 
 /* Pending pods, struct-of-arrays host columns (caller-owned, copied). */
@@ -179,6 +228,19 @@ typedef struct kg_pod_columns {
     const int64_t* la_est[KG_LA_R];             /* DefaultEstimator.EstimatePod (estimator/default_estimator.go:57-120) */
     const uint32_t* flags;                      /* KG_POD_*                                         */
     const uint32_t* numa_policy;                /* pod NUMA topology policy annotation, KG_NUMA_*   */
+    /* DeviceShare GPURequirements (deviceshare/utils.go:516-545, devicehandler_gpu.go:53-96):
+     * per-instance request [pod][KG_DEV_R], number of GPUs (0 = no GPU request: PreFilter Skip) and
+     * the keys present in requestsPerGPU (bit KG_DEV_*). */
+    const int64_t* dev_req;
+    const uint32_t* dev_count;
+    const uint32_t* dev_keys;
+    /* ElasticQuota: quota index (-1 = none: PreFilter Skip) and the keys of PodRequests masked by the
+     * quota's Max names (bit r of KG_QUOTA_R), elasticquota/plugin.go:279-281. */
+    const int32_t* quota;
+    const uint32_t* quota_keys;
+    /* Reservation owner-match class (-1 = the pod matches no reservation): pods of one class match
+     * the same reservations (reservation/transformer.go:233-240, checkReservationMatchedOrIgnored). */
+    const int32_t* rsv_class;
 } kg_pod_columns;
 
 /* Verify-mode outputs, [n_pods][n_nodes] row-major, caller-allocated host buffers (NULL = skip). */
@@ -189,7 +251,46 @@ typedef struct kg_verify_out {
     int64_t* score_numa;  /* NodeNUMAResource score                                         */
     int64_t* total;       /* Σ weight·score, -1 when infeasible                             */
     int8_t* numa_zone;    /* zone the NUMA Reserve would allocate from, -1 = none           */
+    int64_t* score_dev;   /* DeviceShare Score before NormalizeScore (0 when infeasible)    */
+    int64_t* score_rsv;   /* Reservation Score before NormalizeScore (1000 on the preferred
+                             node, reservation/scoring.go:40,191-198; 0 when infeasible)     */
 } kg_verify_out;
+
+/* ElasticQuota table, [quota][KG_QUOTA_R] values with per-quota key masks (bit r = key present).
+ * used / used_limit: the PreFilter's state.used / state.usedLimit (runtime when EnableRuntimeQuota,
+ * else max; elasticquota/plugin.go:274-284); min / np_used: CalculateInfo.Min and the non-preemptible
+ * used (:286-293). Quotas are flat (no parent check: EnableCheckParentQuota=false). */
+typedef struct kg_quota_columns {
+    const int64_t *used, *used_limit, *min, *np_used;
+    const uint32_t *used_keys, *limit_keys, *min_keys, *np_used_keys;
+} kg_quota_columns;
+
+/* Restored NodeInfo of one node as pods of one owner class see it, after the Reservation transformer
+ * (reservation/transformer.go:740-811): the unmatched reservations' double-counted Allocated returned
+ * (updateNodeInfoRequestedForUnmatched :918-935) and the matched reserve pods removed
+ * (restoreMatchedReservation :855-878). The snapshot columns hold the view of pods that match nothing
+ * on the node (every reservation unmatched). */
+typedef struct kg_rsv_view {
+    uint32_t node;                       /* local node index                                         */
+    uint32_t cls;                        /* owner-match class (kg_pod_columns.rsv_class)             */
+    uint32_t first, count;               /* matched reservations: kg_rsv_info[first, first + count)  */
+    int64_t req[KG_RSV_R];               /* restored Requested                                       */
+    int64_t nz_cpu, nz_mem, num_pods;    /* restored NonZeroRequested and len(Pods)                  */
+    int64_t pod_requested[KG_RSV_R];     /* nodeRState.podRequested (after the unmatched correction) */
+    int64_t r_allocated[KG_RSV_R];       /* nodeRState.rAllocated: Σ Allocated of matched reservations */
+} kg_rsv_view;
+
+/* One matched reservation (frameworkext.ReservationInfo). */
+typedef struct kg_rsv_info {
+    uint32_t policy;                     /* KG_RSV_*                                                 */
+    uint32_t names;                      /* bit r: resource r in ResourceNames (keys of Allocatable) */
+    uint32_t allocate_once;              /* IsAllocateOnce (apis/extension/reservation.go:167)       */
+    uint32_t pad_;
+    int64_t order;                       /* LabelReservationOrder, 0 = none; |order| < 2^31          */
+    int64_t allocatable[KG_RSV_R], allocated[KG_RSV_R], reserved[KG_RSV_R];
+    int64_t max_pods;                    /* "pods" in Allocatable, -1 = absent                       */
+    int64_t allocated_pods;              /* len(AssignedPods)                                        */
+} kg_rsv_info;
 
 /* ------------------------------------------------------------------------------------------------ */
 int kg_abi_version(void);
@@ -211,6 +312,15 @@ kg_status kg_snapshot_upload(kg_snap* snap, const kg_node_columns* cols);
 /* Replace rows[i] (local index) with entry i of cols (each column has n entries). */
 kg_status kg_snapshot_update_rows(kg_snap* snap, const uint32_t* rows, uint32_t n, const kg_node_columns* cols);
 kg_status kg_snapshot_read_state(kg_snap* snap, kg_node_state* out);
+/* ElasticQuota table (KG_PLUGIN_QUOTA): n_quotas entries, copied; Reserve updates used / np_used. */
+kg_status kg_snapshot_upload_quotas(kg_snap* snap, const kg_quota_columns* cols, uint32_t n_quotas);
+/* Read back used / np_used (and their key masks) after kg_replay / kg_assume_ext. */
+kg_status kg_snapshot_read_quotas(kg_snap* snap, int64_t* used, uint32_t* used_keys, int64_t* np_used,
+                                  uint32_t* np_used_keys);
+/* Reservation views of this snapshot (KG_PLUGIN_RSV), replacing any earlier upload. Views of one
+ * class must name distinct nodes; at most 64 classes and 8 reservations per view. */
+kg_status kg_snapshot_upload_reservations(kg_snap* snap, const kg_rsv_view* views, uint32_t n_views,
+                                          const kg_rsv_info* infos, uint32_t n_infos);
 kg_status kg_snapshot_destroy(kg_snap* snap);
 
 kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out);
@@ -231,6 +341,13 @@ kg_status kg_replay(kg_snap* snap, kg_pods* pods, int32_t* out_node, int64_t* ou
 /* Reserve/Unreserve of pod `pod` (batch index) on local node `node`. */
 kg_status kg_assume(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node);
 kg_status kg_forget(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t numa_zone);
+/* Reserve with every enabled plugin's state (NodeInfo, LoadAware, NUMA zone, DeviceShare minors via
+ * defaultAllocateDevices order, ElasticQuota used); returns the NUMA zone and the GPU minor bitmask
+ * the Unreserve needs (deviceshare/plugin.go:507-569, elasticquota/plugin.go:622-636). */
+kg_status kg_assume_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t* out_zone,
+                        uint32_t* out_minors);
+kg_status kg_forget_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t numa_zone,
+                        uint32_t minors);
 
 /* Timing of the dominant kernel with HIP events on the launch stream. */
 kg_status kg_profile_enable(kg_ctx* ctx, int enable);

@@ -11,16 +11,25 @@ from typing import Dict
 
 import numpy as np
 
-KG_ABI_VERSION = 1
+KG_ABI_VERSION = 2
 KG_LA_R = 2
 KG_NSCALAR = 2
 KG_MAX_ZONES = 4
+KG_DEV_MINORS = 8
+KG_DEV_R = 3
+KG_DEV_CORE, KG_DEV_RATIO, KG_DEV_MEM = 0, 1, 2
+KG_QUOTA_R = 4
+KG_RSV_R = 5
 
 KG_OK, KG_INVALID_ARG, KG_DEVICE_ERROR, KG_OOM, KG_UNSUPPORTED, KG_NO_DEVICE = range(6)
 
 KG_PLUGIN_NRF = 0x1
 KG_PLUGIN_LA = 0x2
 KG_PLUGIN_NUMA = 0x4
+KG_PLUGIN_DEV = 0x8
+KG_PLUGIN_RSV = 0x10
+KG_PLUGIN_QUOTA = 0x20
+KG_PLUGIN_EXT = KG_PLUGIN_DEV | KG_PLUGIN_RSV | KG_PLUGIN_QUOTA
 
 KG_LA_HAS_METRIC = 0x1
 KG_LA_NM_NIL = 0x2
@@ -39,6 +48,10 @@ KG_POD_NUMA_SKIP = 0x4
 KG_POD_HAS_CPU = 0x8
 KG_POD_HAS_MEM = 0x10
 KG_POD_CPU_BIND = 0x20
+KG_POD_NON_PREEMPTIBLE = 0x40
+KG_POD_RSV_REQUIRED = 0x80
+
+KG_RSV_DEFAULT, KG_RSV_ALIGNED, KG_RSV_RESTRICTED = 0, 1, 2
 
 KG_ST_NRF_PODS = 0x1
 KG_ST_NRF_CPU = 0x2
@@ -57,11 +70,20 @@ KG_ST_NUMA_CONFLICT = 0x20000
 KG_ST_NUMA_NO_RES = 0x40000
 KG_ST_NUMA_ALIGN = 0x80000
 KG_ST_NUMA_MASK = 0xFF0000
+KG_ST_DEV_INSUFFICIENT = 0x01000000
+KG_ST_DEV_NO_DEVICE = 0x02000000
+KG_ST_DEV_MASK = 0x03000000
+KG_ST_RSV_AFFINITY = 0x04000000
+KG_ST_RSV_NODE = 0x08000000
+KG_ST_RSV_RESERVATION = 0x10000000
+KG_ST_RSV_MASK = 0x1C000000
+KG_ST_QUOTA = 0x20000000
 KG_ST_UNSUPPORTED = 0x80000000
 
 _p64 = C.POINTER(C.c_int64)
 _pu32 = C.POINTER(C.c_uint32)
 _pf64 = C.POINTER(C.c_double)
+_pi32 = C.POINTER(C.c_int32)
 
 
 class KgConfig(C.Structure):
@@ -83,6 +105,9 @@ class KgConfig(C.Structure):
         ("numa_w_mem", C.c_int64),
         ("numa_hint_w_cpu", C.c_int64),
         ("numa_hint_w_mem", C.c_int64),
+        ("weight_dev", C.c_int64),
+        ("weight_rsv", C.c_int64),
+        ("dev_w", C.c_int64 * KG_DEV_R),
     ]
 
 
@@ -109,6 +134,7 @@ class KgNodeColumns(C.Structure):
         ("zone_mem", _p64 * KG_MAX_ZONES),
         ("zone_cpu_used", _p64 * KG_MAX_ZONES),
         ("zone_mem_used", _p64 * KG_MAX_ZONES),
+        ("dev_minors", _pi32), ("dev_total", _p64), ("dev_free", _p64),
     ]
 
 
@@ -120,6 +146,7 @@ class KgNodeState(C.Structure):
         ("la_fbase_np", _p64 * KG_LA_R), ("la_fbase_prod", _p64 * KG_LA_R),
         ("la_sbase_np", _p64 * KG_LA_R), ("la_sbase_prod", _p64 * KG_LA_R),
         ("zone_cpu_used", _p64 * KG_MAX_ZONES), ("zone_mem_used", _p64 * KG_MAX_ZONES),
+        ("dev_free", _p64),
     ]
 
 
@@ -131,6 +158,9 @@ class KgPodColumns(C.Structure):
         ("la_est", _p64 * KG_LA_R),
         ("flags", _pu32),
         ("numa_policy", _pu32),
+        ("dev_req", _p64), ("dev_count", _pu32), ("dev_keys", _pu32),
+        ("quota", _pi32), ("quota_keys", _pu32),
+        ("rsv_class", _pi32),
     ]
 
 
@@ -142,7 +172,26 @@ class KgVerifyOut(C.Structure):
         ("score_numa", _p64),
         ("total", _p64),
         ("numa_zone", C.POINTER(C.c_int8)),
+        ("score_dev", _p64),
+        ("score_rsv", _p64),
     ]
+
+
+class KgQuotaColumns(C.Structure):
+    _fields_ = [("used", _p64), ("used_limit", _p64), ("min", _p64), ("np_used", _p64),
+                ("used_keys", _pu32), ("limit_keys", _pu32), ("min_keys", _pu32), ("np_used_keys", _pu32)]
+
+
+class KgRsvView(C.Structure):
+    _fields_ = [("node", C.c_uint32), ("cls", C.c_uint32), ("first", C.c_uint32), ("count", C.c_uint32),
+                ("req", C.c_int64 * KG_RSV_R), ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("num_pods", C.c_int64),
+                ("pod_requested", C.c_int64 * KG_RSV_R), ("r_allocated", C.c_int64 * KG_RSV_R)]
+
+
+class KgRsvInfo(C.Structure):
+    _fields_ = [("policy", C.c_uint32), ("names", C.c_uint32), ("allocate_once", C.c_uint32), ("pad_", C.c_uint32),
+                ("order", C.c_int64), ("allocatable", C.c_int64 * KG_RSV_R), ("allocated", C.c_int64 * KG_RSV_R),
+                ("reserved", C.c_int64 * KG_RSV_R), ("max_pods", C.c_int64), ("allocated_pods", C.c_int64)]
 
 
 # ----------------------------------------------------------------------------------------------
@@ -165,6 +214,7 @@ NODE_I64 = (
 )
 NODE_U32 = ["la_flags", "numa_policy", "numa_zones"]
 NODE_F64 = ["cpu_amp_ratio"]
+NODE_DEV = ["dev_total", "dev_free"]  # int64 [n][KG_DEV_R][KG_DEV_MINORS]
 
 NODE_STATE = (
     ["req_cpu", "req_mem", "req_eph", "num_pods", "nz_cpu", "nz_mem"] + _indexed("sc_req", KG_NSCALAR)
@@ -175,7 +225,8 @@ NODE_STATE = (
 
 POD_I64 = (["req_cpu", "req_mem", "req_eph"] + _indexed("sc_req", KG_NSCALAR) + ["nz_cpu", "nz_mem"]
            + _indexed("la_est", KG_LA_R))
-POD_U32 = ["flags", "numa_policy"]
+POD_U32 = ["flags", "numa_policy", "dev_count", "dev_keys", "quota_keys"]
+POD_I32 = ["quota", "rsv_class"]
 
 Table = Dict[str, np.ndarray]
 
@@ -184,12 +235,17 @@ def empty_nodes(n: int) -> Table:
     t: Table = {k: np.zeros(n, np.int64) for k in NODE_I64}
     t.update({k: np.zeros(n, np.uint32) for k in NODE_U32})
     t["cpu_amp_ratio"] = np.zeros(n, np.float64)
+    t["dev_minors"] = np.full(n, -1, np.int32)  # no Device object
+    for k in NODE_DEV:
+        t[k] = np.zeros((n, KG_DEV_R, KG_DEV_MINORS), np.int64)
     return t
 
 
 def empty_pods(n: int) -> Table:
     t: Table = {k: np.zeros(n, np.int64) for k in POD_I64}
     t.update({k: np.zeros(n, np.uint32) for k in POD_U32})
+    t.update({k: np.full(n, -1, np.int32) for k in POD_I32})
+    t["dev_req"] = np.zeros((n, KG_DEV_R), np.int64)
     return t
 
 
@@ -241,6 +297,13 @@ def node_columns(t: Table) -> KgNodeColumns:
     s.numa_policy = _ptr(t["numa_policy"], C.c_uint32)
     s.numa_zones = _ptr(t["numa_zones"], C.c_uint32)
     s.cpu_amp_ratio = _ptr(t["cpu_amp_ratio"], C.c_double)
+    if "dev_minors" in t:
+        t["dev_minors"] = np.ascontiguousarray(t["dev_minors"], np.int32)
+        for k in NODE_DEV:
+            t[k] = np.ascontiguousarray(t[k], np.int64)
+        s.dev_minors = _ptr(t["dev_minors"], C.c_int32)
+        s.dev_total = _ptr(t["dev_total"], C.c_int64)
+        s.dev_free = _ptr(t["dev_free"], C.c_int64)
     s._keep = t  # keep the buffers alive with the struct
     return s
 
@@ -259,12 +322,16 @@ def node_state_struct(t: Table) -> KgNodeState:
         arr = getattr(s, name)
         for z in range(KG_MAX_ZONES):
             arr[z] = _ptr(t[f"{name}{z}"], C.c_int64)
+    if "dev_free" in t:
+        s.dev_free = _ptr(t["dev_free"], C.c_int64)
     s._keep = t
     return s
 
 
 def empty_node_state(n: int) -> Table:
-    return {k: np.zeros(n, np.int64) for k in NODE_STATE}
+    t = {k: np.zeros(n, np.int64) for k in NODE_STATE}
+    t["dev_free"] = np.zeros((n, KG_DEV_R, KG_DEV_MINORS), np.int64)
+    return t
 
 
 def pod_columns(t: Table) -> KgPodColumns:
@@ -279,8 +346,63 @@ def pod_columns(t: Table) -> KgPodColumns:
         s.la_est[r] = _ptr(t[f"la_est{r}"], C.c_int64)
     s.flags = _ptr(t["flags"], C.c_uint32)
     s.numa_policy = _ptr(t["numa_policy"], C.c_uint32)
+    if "dev_req" in t:
+        _check(t, [k for k in POD_U32 if k in t], np.uint32)
+        _check(t, [k for k in POD_I32 if k in t], np.int32)
+        t["dev_req"] = np.ascontiguousarray(t["dev_req"], np.int64)
+        s.dev_req = _ptr(t["dev_req"], C.c_int64)
+        s.dev_count = _ptr(t["dev_count"], C.c_uint32)
+        s.dev_keys = _ptr(t["dev_keys"], C.c_uint32)
+        s.quota = _ptr(t["quota"], C.c_int32)
+        s.quota_keys = _ptr(t["quota_keys"], C.c_uint32)
+        s.rsv_class = _ptr(t["rsv_class"], C.c_int32)
     s._keep = t
     return s
+
+
+QUOTA_I64 = ["used", "used_limit", "min", "np_used"]     # [q][KG_QUOTA_R]
+QUOTA_U32 = ["used_keys", "limit_keys", "min_keys", "np_used_keys"]
+
+
+def empty_quotas(q: int) -> Table:
+    t: Table = {k: np.zeros((q, KG_QUOTA_R), np.int64) for k in QUOTA_I64}
+    t.update({k: np.zeros(q, np.uint32) for k in QUOTA_U32})
+    return t
+
+
+def quota_columns(t: Table) -> KgQuotaColumns:
+    for k in QUOTA_I64:
+        t[k] = np.ascontiguousarray(t[k], np.int64)
+    for k in QUOTA_U32:
+        t[k] = np.ascontiguousarray(t[k], np.uint32)
+    s = KgQuotaColumns()
+    for k in QUOTA_I64:
+        setattr(s, k, _ptr(t[k], C.c_int64))
+    for k in QUOTA_U32:
+        setattr(s, k, _ptr(t[k], C.c_uint32))
+    s._keep = t
+    return s
+
+
+class Reservations:
+    """Reservation restore views and matched reservations (kg_rsv_view / kg_rsv_info arrays)."""
+
+    def __init__(self, views, infos):
+        self.views = (KgRsvView * max(1, len(views)))()
+        self.infos = (KgRsvInfo * max(1, len(infos)))()
+        self.n_views, self.n_infos = len(views), len(infos)
+        for a, rows in ((self.views, views), (self.infos, infos)):
+            for x, row in enumerate(rows):
+                for k, v in row.items():
+                    f = getattr(a[x], k)
+                    if isinstance(f, int):
+                        setattr(a[x], k, int(v))
+                    else:
+                        for q, y in enumerate(v):
+                            f[q] = int(y)
+
+    def view_list(self):
+        return [self.views[x] for x in range(self.n_views)]
 
 
 class VerifyResult:
@@ -294,6 +416,8 @@ class VerifyResult:
         self.score_numa = np.zeros(shape, np.int64)
         self.total = np.zeros(shape, np.int64)
         self.numa_zone = np.zeros(shape, np.int8)
+        self.score_dev = np.zeros(shape, np.int64)
+        self.score_rsv = np.zeros(shape, np.int64)
 
     def struct(self) -> KgVerifyOut:
         s = KgVerifyOut()
@@ -303,6 +427,8 @@ class VerifyResult:
         s.score_numa = _ptr(self.score_numa, C.c_int64)
         s.total = _ptr(self.total, C.c_int64)
         s.numa_zone = _ptr(self.numa_zone, C.c_int8)
+        s.score_dev = _ptr(self.score_dev, C.c_int64)
+        s.score_rsv = _ptr(self.score_rsv, C.c_int64)
         return s
 
     @property

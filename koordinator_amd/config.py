@@ -21,6 +21,10 @@ BATCH_CPU = "kubernetes.io/batch-cpu"
 BATCH_MEMORY = "kubernetes.io/batch-memory"
 MID_CPU = "kubernetes.io/mid-cpu"
 MID_MEMORY = "kubernetes.io/mid-memory"
+GPU_CORE = "koordinator.sh/gpu-core"
+GPU_MEMORY_RATIO = "koordinator.sh/gpu-memory-ratio"
+GPU_MEMORY = "koordinator.sh/gpu-memory"
+DEV_RESOURCES = (GPU_CORE, GPU_MEMORY_RATIO, GPU_MEMORY)  # KG_DEV_CORE, KG_DEV_RATIO, KG_DEV_MEM
 
 # LoadAware vectorizer (loadaware/helper.go:162-173): cpu and memory, sorted by name.
 LA_RESOURCES = (CPU, MEMORY)
@@ -95,6 +99,13 @@ class SchedulerConfig:
     # NodeNUMAResource ScoringStrategy / NUMAScoringStrategy (v1/defaults.go:128-162).
     numa_scoring: List[Tuple[str, int]] = field(default_factory=lambda: [(CPU, 1), (MEMORY, 1)])
     numa_hint_scoring: List[Tuple[str, int]] = field(default_factory=lambda: [(CPU, 1), (MEMORY, 1)])
+    # DeviceShare (score weight 1) and Reservation (score weight 5000) of the shipped profile
+    # (config/manager/scheduler-config.yaml:91-96); DeviceShare LeastAllocated resources
+    # (v1/defaults.go:254-277: gpu-memory-ratio 1, gpu-memory 1; rdma / fpga are not GPU minors).
+    weight_dev: int = 1
+    weight_rsv: int = 5000
+    dev_scoring: List[Tuple[str, int]] = field(
+        default_factory=lambda: [(GPU_MEMORY_RATIO, 1), (GPU_MEMORY, 1)])
 
     def la(self) -> LoadAwareArgs:
         return self.loadaware.defaulted()
@@ -128,6 +139,11 @@ class SchedulerConfig:
         c.numa_w_cpu, c.numa_w_mem = ns.get(CPU, 0), ns.get(MEMORY, 0)
         nh = dict(self.numa_hint_scoring)
         c.numa_hint_w_cpu, c.numa_hint_w_mem = nh.get(CPU, 0), nh.get(MEMORY, 0)
+        c.weight_dev = self.weight_dev
+        c.weight_rsv = self.weight_rsv
+        ds = dict(self.dev_scoring)
+        for r, name in enumerate(DEV_RESOURCES):
+            c.dev_w[r] = ds.get(name, 0)
         return c
 
 
@@ -137,6 +153,13 @@ def shipped_profile() -> SchedulerConfig:
         loadaware=LoadAwareArgs(filter_expired_node_metrics=False, node_metric_expiration_seconds=300,
                                 resource_weights={CPU: 1, MEMORY: 1}, usage_thresholds={CPU: 0, MEMORY: 0},
                                 estimated_scaling_factors={CPU: 85, MEMORY: 70}))
+
+
+def config5_profile() -> SchedulerConfig:
+    """Config 5 of BASELINE.md: configs 1-2's plugins plus DeviceShare, Reservation and ElasticQuota."""
+    plugins = (abi.KG_PLUGIN_NRF | abi.KG_PLUGIN_LA | abi.KG_PLUGIN_NUMA | abi.KG_PLUGIN_DEV | abi.KG_PLUGIN_RSV
+               | abi.KG_PLUGIN_QUOTA)
+    return SchedulerConfig(plugins=plugins, loadaware=LoadAwareArgs())
 
 
 def bench_profile(numa: bool = True) -> SchedulerConfig:

@@ -721,3 +721,134 @@ def nodes_table(nodes: Sequence[NodeInput], cfg: SchedulerConfig) -> abi.Table:
         for k, v in node_row(ni, cfg).items():
             t[k][i] = v
     return t
+
+
+# ------------------------------------------------------------------------------------------------
+# DeviceShare / Reservation / ElasticQuota host decode (config 5)
+
+def gpu_requirements(requests: Dict[str, int]) -> Tuple[List[int], int, int, bool]:
+    """calcDesiredRequestsAndCountForGPU (deviceshare/devicehandler_gpu.go:53-96) on the koordinator
+    GPU resources of a pod (after the nvidia.com/gpu conversion): per-instance request vector
+    [gpu-core, gpu-memory-ratio, gpu-memory], the key mask of requestsPerGPU, numberOfGPUs and whether
+    the request is shared. Go integer division (all values non-negative)."""
+    from .config import GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO
+    gpu_shared = requests.get("koordinator.sh/gpu.shared")
+    desired = 1
+    ratio = requests.get(GPU_MEMORY_RATIO)
+    if gpu_shared is not None and gpu_shared > 0:
+        desired = gpu_shared
+    elif ratio is not None and ratio > 100 and ratio % 100 == 0:
+        desired = ratio // 100
+    req = [0, 0, 0]
+    keys = 0
+    shared = False
+    if GPU_CORE in requests:
+        req[abi.KG_DEV_CORE] = requests[GPU_CORE] // desired
+        keys |= 1 << abi.KG_DEV_CORE
+    if ratio is not None:
+        per = ratio // desired
+        shared = per < 100
+        req[abi.KG_DEV_RATIO] = per
+        keys |= 1 << abi.KG_DEV_RATIO
+    elif GPU_MEMORY in requests:
+        shared = True
+        req[abi.KG_DEV_MEM] = requests[GPU_MEMORY] // desired
+        keys |= 1 << abi.KG_DEV_MEM
+    return req, keys, desired, shared
+
+
+RSV_DIMS = ("cpu", "memory", "ephemeral-storage", "scalar0", "scalar1")  # KG_RSV_R order
+
+
+def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
+    """Host restatement of the Reservation transformer (reservation/transformer.go:147-350,740-935).
+
+    `nodes` is the true NodeInfo view (reserve pods and the pods allocated to reservations both
+    counted, as NodeInfo accounts them). Each reservation is a dict: node, cls (owner-match class),
+    allocatable / allocated / reserved (KG_RSV_R vectors, allocated None when no pod is assigned),
+    allocated_pods, policy, order, allocate_once, max_pods.
+
+    Returns (nodes_default, views, infos): the snapshot columns as seen by pods matching nothing on
+    the node (every reservation with assigned pods corrected by updateNodeInfoRequestedForUnmatched),
+    and per (class, node) the restored view with its matched reservations (kg_rsv_view / kg_rsv_info
+    dicts for abi.Reservations). Reserve pods request their Allocatable; the non-zero request of a
+    present cpu / memory key is the value itself (GetNonZeroRequestForResource,
+    frameworkext/reservation_info.go:581-605)."""
+    out = {k: np.array(v, copy=True) for k, v in nodes.items()}
+    req_cols = ["req_cpu", "req_mem", "req_eph", "sc_req0", "sc_req1"]
+    by_node: Dict[int, List[int]] = {}
+    for x, r in enumerate(reservations):
+        by_node.setdefault(int(r["node"]), []).append(x)
+
+    def vec(r, key):
+        v = r.get(key)
+        return [0] * abi.KG_RSV_R if v is None else [int(a) for a in v]
+
+    def nz(v, present):
+        cpu = v[0] if present else 100           # DefaultMilliCPURequest
+        mem = v[1] if present else 200 * 1024 * 1024  # DefaultMemoryRequest
+        return cpu, mem
+
+    for i, xs in by_node.items():
+        for x in xs:  # default view: every reservation with assigned pods is unmatched
+            r = reservations[x]
+            if int(r.get("allocated_pods", 0)) > 0:
+                a = vec(r, "allocated")
+                for k, c in enumerate(req_cols):
+                    out[c][i] -= a[k]
+                ncpu, nmem = nz(a, r.get("allocated") is not None)
+                out["nz_cpu"][i] -= ncpu
+                out["nz_mem"][i] -= nmem
+    views, infos = [], []
+    for i in sorted(by_node):
+        classes = sorted({int(reservations[x]["cls"]) for x in by_node[i]})
+        for c in classes:
+            matched = [x for x in by_node[i] if int(reservations[x]["cls"]) == c]
+            req = [int(out[col][i]) for col in req_cols]
+            nzc, nzm = int(out["nz_cpu"][i]), int(out["nz_mem"][i])
+            pod_requested = list(req)
+            r_alloc = [0] * abi.KG_RSV_R
+            for x in matched:
+                r = reservations[x]
+                a = vec(r, "allocated")
+                if int(r.get("allocated_pods", 0)) > 0:  # its unmatched correction is undone
+                    for k in range(abi.KG_RSV_R):
+                        req[k] += a[k]
+                        pod_requested[k] += a[k]
+                    ncpu, nmem = nz(a, r.get("allocated") is not None)
+                    nzc += ncpu
+                    nzm += nmem
+                rp = vec(r, "allocatable")  # restoreMatchedReservation: RemovePod(reserve pod)
+                for k in range(abi.KG_RSV_R):
+                    req[k] -= rp[k]
+                    r_alloc[k] += a[k]
+                ncpu, nmem = nz(rp, True)
+                nzc -= ncpu
+                nzm -= nmem
+            first = len(infos)
+            for x in matched:
+                r = reservations[x]
+                alloc = vec(r, "allocatable")
+                names = 0
+                for k in range(abi.KG_RSV_R):
+                    if alloc[k] != 0 or (r.get("names") is not None and (int(r["names"]) >> k) & 1):
+                        names |= 1 << k
+                infos.append(dict(policy=int(r.get("policy", abi.KG_RSV_DEFAULT)), names=names,
+                                  allocate_once=int(bool(r.get("allocate_once", True))), order=int(r.get("order", 0)),
+                                  allocatable=alloc, allocated=vec(r, "allocated"), reserved=vec(r, "reserved"),
+                                  max_pods=int(r.get("max_pods", -1)), allocated_pods=int(r.get("allocated_pods", 0))))
+            views.append(dict(node=i, cls=c, first=first, count=len(matched), req=req, nz_cpu=nzc, nz_mem=nzm,
+                              num_pods=int(out["num_pods"][i]) - len(matched), pod_requested=pod_requested,
+                              r_allocated=r_alloc))
+    return out, views, infos
+
+
+def quota_keys(pods: abi.Table, max_keys: np.ndarray) -> np.ndarray:
+    """Keys of quotav1.Mask(PodRequests, Max names) over KG_QUOTA_R = {cpu, memory, scalar0, scalar1}
+    (elasticquota/plugin.go:279-280): a key is present when the pod requests it."""
+    f = pods["flags"]
+    have = (np.where(f & abi.KG_POD_HAS_CPU, 1, 0) | np.where(f & abi.KG_POD_HAS_MEM, 2, 0)
+            | np.where(pods["sc_req0"] != 0, 4, 0) | np.where(pods["sc_req1"] != 0, 8, 0))
+    q = pods["quota"]
+    mk = np.where(q >= 0, max_keys[np.maximum(q, 0)], 0)
+    return (have & mk).astype(np.uint32)

@@ -8,8 +8,8 @@ from __future__ import annotations
 import numpy as np
 
 from . import abi
-from .config import SchedulerConfig, bench_profile
-from .decode import amplify
+from .config import GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, SchedulerConfig, bench_profile, config5_profile
+from .decode import amplify, gpu_requirements, quota_keys, reservation_restore
 
 SEED = 0x6B6F6F7264
 GI = 1 << 30
@@ -125,6 +125,103 @@ def pods(p: int, config: int = 1, scale: float = 1.0, rng=None, la_factors=(85, 
     flags |= np.where(empty, abi.KG_POD_NUMA_SKIP, 0)
     t["flags"] = flags.astype(np.uint32)
     return t
+
+
+GPU_MEM_PER_MINOR = 192 * GI
+N_RSV_CLASSES = 8
+
+
+def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 100, rsv_frac: float = 0.05):
+    """Config 5: configs 1-2's plugins plus DeviceShare (8 GPU minors per node: gpu-core
+    100, gpu-memory-ratio 100, gpu-memory 192Gi; minors 40% idle, 30% fully used, 30% partially used),
+    Reservation (5% of nodes hold 1-4 reservations of one of 8 owner classes; 20% of the non-GPU pods
+    match one class, a quarter of them with a required reservation affinity) and ElasticQuota (100
+    flat quotas, every pod in one; 10% non-preemptible pods). 30% of the pods request GPUs: 60% whole
+    GPUs (1/2/4/8), 40% shared (gpu-core 50 + gpu-memory-ratio 50, or gpu-core 50 + gpu-memory 24Gi).
+    NUMA policy None on every node (GPU and reservation NUMA restore stay on the host path).
+
+    Returns (cfg, nodes, pods, quotas, reservations): nodes already restored to the view of pods that
+    match no reservation (decode.reservation_restore), reservations = abi.Reservations."""
+    cfg = config5_profile()
+    r = _rng(seed_config)
+    t = nodes(n_nodes, seed_config, numa=True, rng=r)
+    n = n_nodes
+    t["numa_policy"][:] = abi.KG_NUMA_NONE
+    # DeviceShare minors
+    t["dev_minors"] = np.full(n, abi.KG_DEV_MINORS, np.int32)
+    tot = np.zeros((n, abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
+    tot[:, abi.KG_DEV_CORE, :] = 100
+    tot[:, abi.KG_DEV_RATIO, :] = 100
+    tot[:, abi.KG_DEV_MEM, :] = GPU_MEM_PER_MINOR
+    state = r.random((n, abi.KG_DEV_MINORS))
+    used_pct = np.where(state < 0.4, 0, np.where(state < 0.7, 100, (r.random((n, abi.KG_DEV_MINORS)) * 20).astype(np.int64) * 5))
+    free = tot.copy()
+    free[:, abi.KG_DEV_CORE, :] -= used_pct
+    free[:, abi.KG_DEV_RATIO, :] -= used_pct
+    free[:, abi.KG_DEV_MEM, :] -= used_pct * GPU_MEM_PER_MINOR // 100
+    t["dev_total"], t["dev_free"] = tot, free
+    # Reservations on 5% of the nodes (counted in the true NodeInfo: reserve pod + assigned pods)
+    resv = []
+    holders = np.nonzero(r.random(n) < rsv_frac)[0]
+    for i in holders:
+        for _ in range(int(r.integers(1, 5))):
+            cpu = int(r.choice([2000, 4000, 8000]))
+            mem = int(r.choice([4, 8, 16])) * GI
+            alloc = [cpu, mem, 0, 0, 0]
+            ap = int(r.integers(1, 3)) if r.random() < 0.5 else 0
+            allocated = None
+            if ap:
+                f = float(r.choice([0.25, 0.5, 0.75]))
+                allocated = [int(cpu * f), int(mem * f), 0, 0, 0]
+            pol = r.random()
+            policy = abi.KG_RSV_DEFAULT if pol < 0.6 else (abi.KG_RSV_ALIGNED if pol < 0.8 else abi.KG_RSV_RESTRICTED)
+            order = int(r.integers(1, 11)) if r.random() < 0.3 else 0
+            resv.append(dict(node=int(i), cls=int(r.integers(0, N_RSV_CLASSES)), allocatable=alloc,
+                             allocated=allocated, reserved=None, allocated_pods=ap, policy=policy, order=order,
+                             allocate_once=ap == 0, max_pods=-1))
+            t["req_cpu"][i] += cpu + (allocated[0] if allocated else 0)
+            t["req_mem"][i] += mem + (allocated[1] if allocated else 0)
+            t["nz_cpu"][i] += cpu + (allocated[0] if allocated else 0)
+            t["nz_mem"][i] += mem + (allocated[1] if allocated else 0)
+            t["num_pods"][i] += 1 + ap
+    t, views, infos = reservation_restore(t, resv)
+    # Pods
+    pr = _rng(seed_config, 1)
+    p = pods(n_pods, seed_config, rng=pr)
+    gpu = pr.random(n_pods) < 0.30
+    whole = pr.random(n_pods) < 0.60
+    count = pr.choice([1, 2, 4, 8], n_pods, p=[0.5, 0.25, 0.15, 0.10])
+    by_mem = pr.random(n_pods) < 0.25
+    for j in np.nonzero(gpu)[0]:
+        if whole[j]:
+            req = {GPU_CORE: 100 * int(count[j]), GPU_MEMORY_RATIO: 100 * int(count[j])}
+        elif by_mem[j]:
+            req = {GPU_CORE: 50, GPU_MEMORY: 24 * GI}
+        else:
+            req = {GPU_CORE: 50, GPU_MEMORY_RATIO: 50}
+        vec, keys, cnt, _ = gpu_requirements(req)
+        p["dev_req"][j] = vec
+        p["dev_keys"][j] = keys
+        p["dev_count"][j] = cnt
+    # reservation owner classes (non-GPU pods only: GPU pods with reservations leave the device path)
+    cls_on = (~gpu) & (pr.random(n_pods) < 0.20 / 0.70)
+    p["rsv_class"] = np.where(cls_on, pr.integers(0, N_RSV_CLASSES, n_pods), -1).astype(np.int32)
+    p["flags"] |= np.where(cls_on & (pr.random(n_pods) < 0.25), abi.KG_POD_RSV_REQUIRED, 0).astype(np.uint32)
+    # ElasticQuota: flat quotas with Max over cpu + memory (10%: also the batch resources)
+    q = abi.empty_quotas(n_quotas)
+    maxk = np.where(pr.random(n_quotas) < 0.10, 0b1111, 0b0011).astype(np.uint32)
+    lim = np.stack([pr.integers(50, 500, n_quotas) * 1000, pr.integers(100, 2000, n_quotas) * GI,
+                    pr.integers(50, 500, n_quotas) * 1000, pr.integers(100, 2000, n_quotas) * GI], 1).astype(np.int64)
+    used = (lim * pr.uniform(0.5, 1.0, (n_quotas, 1))).astype(np.int64)
+    q["used_limit"], q["used"] = lim, used
+    q["limit_keys"], q["used_keys"] = maxk, maxk
+    q["min"] = (lim * 0.6).astype(np.int64)
+    q["np_used"] = (q["min"] * pr.uniform(0.0, 1.1, (n_quotas, 1))).astype(np.int64)
+    q["min_keys"], q["np_used_keys"] = maxk, maxk
+    p["quota"] = pr.integers(0, n_quotas, n_pods).astype(np.int32)
+    p["flags"] |= np.where(pr.random(n_pods) < 0.10, abi.KG_POD_NON_PREEMPTIBLE, 0).astype(np.uint32)
+    p["quota_keys"] = quota_keys(p, maxk)
+    return cfg, t, p, q, abi.Reservations(views, infos)
 
 
 def cluster(config: int):

@@ -41,21 +41,37 @@ int64_t kgo_la_usage_percent(int64_t estimated, int64_t total) {
     return (int64_t)round(p);
 }
 
+/* Node quantities a Reservation restore changes for the pods of one owner class (kg_rsv_view):
+ * NodeResourcesFit and NodeNUMAResource read the restored NodeInfo, LoadAware and DeviceShare do not. */
+typedef struct kgo_over {
+    int64_t req[KG_RSV_R]; /* cpu, memory, ephemeral-storage, scalar0, scalar1 */
+    int64_t nz_cpu, nz_mem, num_pods;
+} kgo_over;
+
+#define N_REQ_CPU(n, i, ov) ((ov) ? (ov)->req[0] : (n)->req_cpu[i])
+#define N_REQ_MEM(n, i, ov) ((ov) ? (ov)->req[1] : (n)->req_mem[i])
+#define N_REQ_EPH(n, i, ov) ((ov) ? (ov)->req[2] : (n)->req_eph[i])
+#define N_REQ_SC(n, k, i, ov) ((ov) ? (ov)->req[3 + (k)] : (n)->sc_req[k][i])
+#define N_NZ_CPU(n, i, ov) ((ov) ? (ov)->nz_cpu : (n)->nz_cpu[i])
+#define N_NZ_MEM(n, i, ov) ((ov) ? (ov)->nz_mem : (n)->nz_mem[i])
+#define N_NUM_PODS(n, i, ov) ((ov) ? (ov)->num_pods : (n)->num_pods[i])
+
 /* ---------------------------------------------------------------------------------------------- */
 /* NodeResourcesFit (upstream v1.35.6)                                              */
 
-static uint32_t nrf_filter(const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j) {
+static uint32_t nrf_filter(const kg_node_columns* n, uint32_t i, const kgo_over* ov, const kg_pod_columns* p,
+                           uint32_t j) {
     uint32_t st = 0;
     /* fitsRequest: len(nodeInfo.Pods)+1 > allowedPodNumber */
-    if (n->num_pods[i] + 1 > n->alloc_pods[i]) st |= KG_ST_NRF_PODS;
+    if (N_NUM_PODS(n, i, ov) + 1 > n->alloc_pods[i]) st |= KG_ST_NRF_PODS;
     /* (the all-zero early return yields the same verdict as the guarded checks below) */
-    if (p->req_cpu[j] > 0 && p->req_cpu[j] > n->alloc_cpu[i] - n->req_cpu[i]) st |= KG_ST_NRF_CPU;
-    if (p->req_mem[j] > 0 && p->req_mem[j] > n->alloc_mem[i] - n->req_mem[i]) st |= KG_ST_NRF_MEM;
-    if (p->req_eph[j] > 0 && p->req_eph[j] > n->alloc_eph[i] - n->req_eph[i]) st |= KG_ST_NRF_EPH;
+    if (p->req_cpu[j] > 0 && p->req_cpu[j] > n->alloc_cpu[i] - N_REQ_CPU(n, i, ov)) st |= KG_ST_NRF_CPU;
+    if (p->req_mem[j] > 0 && p->req_mem[j] > n->alloc_mem[i] - N_REQ_MEM(n, i, ov)) st |= KG_ST_NRF_MEM;
+    if (p->req_eph[j] > 0 && p->req_eph[j] > n->alloc_eph[i] - N_REQ_EPH(n, i, ov)) st |= KG_ST_NRF_EPH;
     for (int k = 0; k < KG_NSCALAR; k++) {
         int64_t q = p->sc_req[k][j];
         if (q == 0) continue; /* "Skip in case request quantity is zero" */
-        if (q > n->sc_alloc[k][i] - n->sc_req[k][i]) st |= (k == 0 ? KG_ST_NRF_SC0 : KG_ST_NRF_SC1);
+        if (q > n->sc_alloc[k][i] - N_REQ_SC(n, k, i, ov)) st |= (k == 0 ? KG_ST_NRF_SC0 : KG_ST_NRF_SC1);
     }
     return st;
 }
@@ -63,14 +79,14 @@ static uint32_t nrf_filter(const kg_node_columns* n, uint32_t i, const kg_pod_co
 /* resourceAllocationScorer.score + leastResourceScorer with NonZeroRequested for cpu/memory and
  * Requested for scalars; scalars the pod does not request are bypassed (0, 0); resources with
  * allocatable 0 are skipped (mirrors noderesourcefitplus/node_resource_fit_plus_utils.go:114-139). */
-static int64_t nrf_score(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
-                         uint32_t j) {
+static int64_t nrf_score(const kg_config* c, const kg_node_columns* n, uint32_t i, const kgo_over* ov,
+                         const kg_pod_columns* p, uint32_t j) {
     int64_t alloc[2 + KG_NSCALAR], req[2 + KG_NSCALAR], w[2 + KG_NSCALAR];
     alloc[0] = n->alloc_cpu[i];
-    req[0] = n->nz_cpu[i] + p->nz_cpu[j];
+    req[0] = N_NZ_CPU(n, i, ov) + p->nz_cpu[j];
     w[0] = c->nrf_w_cpu;
     alloc[1] = n->alloc_mem[i];
-    req[1] = n->nz_mem[i] + p->nz_mem[j];
+    req[1] = N_NZ_MEM(n, i, ov) + p->nz_mem[j];
     w[1] = c->nrf_w_mem;
     for (int k = 0; k < KG_NSCALAR; k++) {
         int64_t q = p->sc_req[k][j];
@@ -79,7 +95,7 @@ static int64_t nrf_score(const kg_config* c, const kg_node_columns* n, uint32_t 
             req[2 + k] = 0;
         } else {
             alloc[2 + k] = n->sc_alloc[k][i];
-            req[2 + k] = n->sc_req[k][i] + q;
+            req[2 + k] = N_REQ_SC(n, k, i, ov) + q;
         }
         w[2 + k] = c->nrf_w_sc[k];
     }
@@ -237,8 +253,8 @@ static uint32_t numa_merge_policy(uint32_t node_policy, uint32_t pod_policy, int
 
 /* Filter (plugin.go:363-459) + Score (scoring.go:67-151) of one pair. zone_out: -2 = node scored
  * at node level (no NUMA allocation), >=0 zone allocation. */
-static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
-                          uint32_t j, int64_t* score_out, int32_t* zone_out) {
+static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t i, const kgo_over* ov,
+                          const kg_pod_columns* p, uint32_t j, int64_t* score_out, int32_t* zone_out) {
     *score_out = 0;
     *zone_out = -1;
     if (p->flags[j] & KG_POD_NUMA_SKIP) return 0; /* PreFilter Skip: no Filter, no Score */
@@ -252,7 +268,7 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
     /* filterAmplifiedCPUs: plugin.go:461-498 (requestCPUBind == false) */
     if (pod_cpu != 0 && ratio > 1) {
         int64_t allocated = n->cpuset_alloc_milli[i];
-        int64_t requested = n->req_cpu[i];
+        int64_t requested = N_REQ_CPU(n, i, ov);
         if (requested >= allocated && allocated > 0) {
             requested = requested - allocated;
             requested += kgo_amplify(allocated, ratio);
@@ -274,8 +290,8 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
          * (policy_single_numa_node.go:79-84): no NUMA allocation, node-level score */
         if (!has_any || Z == 1) {
             *zone_out = -1;
-            *score_out = numa_least_score(c->numa_w_cpu, c->numa_w_mem, n->alloc_cpu[i], n->req_cpu[i] + pod_cpu,
-                                          n->alloc_mem[i], n->req_mem[i] + p->req_mem[j]);
+            *score_out = numa_least_score(c->numa_w_cpu, c->numa_w_mem, n->alloc_cpu[i], N_REQ_CPU(n, i, ov) + pod_cpu,
+                                          n->alloc_mem[i], N_REQ_MEM(n, i, ov) + p->req_mem[j]);
             return 0;
         }
         /* Score with the zone allocation: calculateAllocatableAndRequested, scoring.go:153-199 */
@@ -286,13 +302,13 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
         return 0;
     }
     /* policy None: scoreWithAmplifiedCPUs, scoring.go:132-151 */
-    int64_t req_cpu = n->req_cpu[i];
+    int64_t req_cpu = N_REQ_CPU(n, i, ov);
     if (!(pod_cpu == 0 || ratio <= 1)) {
         int64_t allocated = n->cpuset_alloc_milli[i];
         req_cpu = req_cpu - allocated + kgo_amplify(allocated, ratio);
     }
     *score_out = numa_least_score(c->numa_w_cpu, c->numa_w_mem, n->alloc_cpu[i], req_cpu + pod_cpu, n->alloc_mem[i],
-                                  n->req_mem[i] + p->req_mem[j]);
+                                  N_REQ_MEM(n, i, ov) + p->req_mem[j]);
     return 0;
 }
 
@@ -303,13 +319,13 @@ void kgo_eval_pair(const kg_config* c, const kg_node_columns* n, uint32_t i, con
     uint32_t st = 0;
     int64_t s_numa = 0;
     int32_t zone = -1;
-    if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(n, i, p, j);
+    if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(n, i, NULL, p, j);
     if (c->plugins & KG_PLUGIN_LA) st |= la_filter(c, n, i, p, j);
-    if (c->plugins & KG_PLUGIN_NUMA) st |= numa_eval(c, n, i, p, j, &s_numa, &zone);
+    if (c->plugins & KG_PLUGIN_NUMA) st |= numa_eval(c, n, i, NULL, p, j, &s_numa, &zone);
     out->status = st;
     /* Score functions are defined for every node (the Go ScorePlugin.Score can be called on any
      * node); the NUMA score exists only where its Filter admitted the pod (it needs the hint). */
-    out->s_nrf = (c->plugins & KG_PLUGIN_NRF) ? nrf_score(c, n, i, p, j) : 0;
+    out->s_nrf = (c->plugins & KG_PLUGIN_NRF) ? nrf_score(c, n, i, NULL, p, j) : 0;
     out->s_la = (c->plugins & KG_PLUGIN_LA) ? la_score(c, n, i, p, j) : 0;
     out->s_numa = (c->plugins & KG_PLUGIN_NUMA) && !(st & (KG_ST_NUMA_MASK | KG_ST_UNSUPPORTED)) ? s_numa : 0;
     if (st) {
@@ -403,12 +419,12 @@ static void par_run(par_job* jb) {
             if (jb->phase == 0) {
                 uint32_t st = 0;
                 uint32_t i = (uint32_t)x;
-                if (jb->c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(jb->n, i, jb->p, jb->pod);
+                if (jb->c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(jb->n, i, NULL, jb->p, jb->pod);
                 if (jb->c->plugins & KG_PLUGIN_LA) st |= la_filter(jb->c, jb->n, i, jb->p, jb->pod);
                 int64_t s;
                 int32_t z;
                 if (jb->c->plugins & KG_PLUGIN_NUMA) {
-                    st |= numa_eval(jb->c, jb->n, i, jb->p, jb->pod, &s, &z);
+                    st |= numa_eval(jb->c, jb->n, i, NULL, jb->p, jb->pod, &s, &z);
                     jb->total[i] = s; /* NUMA score is produced by the same resource-manager walk */
                 }
                 jb->feasible[i] = st == 0;
@@ -416,7 +432,7 @@ static void par_run(par_job* jb) {
                 uint32_t i = jb->items[x];
                 int64_t t = 0;
                 const kg_config* c = jb->c;
-                if (c->plugins & KG_PLUGIN_NRF) t += c->weight_nrf * nrf_score(c, jb->n, i, jb->p, jb->pod);
+                if (c->plugins & KG_PLUGIN_NRF) t += c->weight_nrf * nrf_score(c, jb->n, i, NULL, jb->p, jb->pod);
                 if (c->plugins & KG_PLUGIN_LA) t += c->weight_la * la_score(c, jb->n, i, jb->p, jb->pod);
                 if (c->plugins & KG_PLUGIN_NUMA) t += c->weight_numa * jb->total[i];
                 jb->total[i] = t;
@@ -535,6 +551,8 @@ struct kgo_state {
     int64_t* col[C_NCOLS];
     uint32_t *la_flags, *numa_policy, *numa_zones;
     double* amp;
+    int32_t* dev_minors;          /* DeviceShare (NULL when the snapshot has no device tables) */
+    int64_t *dev_total, *dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
 };
 
 static int64_t* dup64(const int64_t* s, uint32_t n) {
@@ -585,6 +603,15 @@ kgo_state* kgo_state_new(const kg_node_columns* s, uint32_t n) {
     if (s->numa_policy) memcpy(st->numa_policy, s->numa_policy, 4 * (size_t)n);
     if (s->numa_zones) memcpy(st->numa_zones, s->numa_zones, 4 * (size_t)n);
     if (s->cpu_amp_ratio) memcpy(st->amp, s->cpu_amp_ratio, 8 * (size_t)n);
+    if (s->dev_minors && s->dev_total && s->dev_free) {
+        size_t m = (size_t)(n ? n : 1) * KG_DEV_R * KG_DEV_MINORS;
+        st->dev_minors = (int32_t*)calloc(n ? n : 1, 4);
+        st->dev_total = (int64_t*)calloc(m, 8);
+        st->dev_free = (int64_t*)calloc(m, 8);
+        memcpy(st->dev_minors, s->dev_minors, 4 * (size_t)n);
+        memcpy(st->dev_total, s->dev_total, 8 * (size_t)n * KG_DEV_R * KG_DEV_MINORS);
+        memcpy(st->dev_free, s->dev_free, 8 * (size_t)n * KG_DEV_R * KG_DEV_MINORS);
+    }
     return st;
 }
 
@@ -595,6 +622,9 @@ void kgo_state_free(kgo_state* st) {
     free(st->numa_policy);
     free(st->numa_zones);
     free(st->amp);
+    free(st->dev_minors);
+    free(st->dev_total);
+    free(st->dev_free);
     free(st);
 }
 
@@ -635,6 +665,9 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
         v->zone_cpu_used[z] = st->col[C_ZONE_CPU_USED + z];
         v->zone_mem_used[z] = st->col[C_ZONE_MEM_USED + z];
     }
+    v->dev_minors = st->dev_minors;
+    v->dev_total = st->dev_total;
+    v->dev_free = st->dev_free;
 }
 
 static void apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,
@@ -709,4 +742,637 @@ void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_c
         if (out_total) out_total[j] = (int64_t)(best >> 32);
         apply(c, st, g - base, p, j, best_zone, 1);
     }
+}
+
+/* ============================================================================================== */
+/* Config-5 plugins: DeviceShare (a12-a13), Reservation (a10-a11), ElasticQuota (a14)              */
+
+#define DEVX(tab, i, r, m) ((tab)[((size_t)(i) * KG_DEV_R + (size_t)(r)) * KG_DEV_MINORS + (size_t)(m)])
+
+/* resourceAllocationScorer.scoreNode / scoreDevice + leastResourceScorer (deviceshare/scoring.go:197-281):
+ * resources with a zero total are skipped; requested = total >= free ? total - free + podRequest : total. */
+static int64_t dev_least(const int64_t* w, const int64_t* total, const int64_t* free_, const int64_t* preq) {
+    int64_t score = 0, wsum = 0;
+    for (int r = 0; r < KG_DEV_R; r++) {
+        if (w[r] == 0 || total[r] == 0) continue;
+        int64_t req = total[r] >= free_[r] ? total[r] - free_[r] + preq[r] : total[r];
+        score += least_requested_score(req, total[r]) * w[r];
+        wsum += w[r];
+    }
+    return wsum == 0 ? 0 : score / wsum;
+}
+
+static void dev_pod_req(const kg_pod_columns* p, uint32_t j, int64_t* preq, uint32_t* keys) {
+    *keys = p->dev_keys ? p->dev_keys[j] : 0;
+    for (int r = 0; r < KG_DEV_R; r++)
+        preq[r] = ((*keys >> r) & 1u) && p->dev_req ? p->dev_req[(size_t)j * KG_DEV_R + r] : 0;
+}
+
+/* defaultAllocateDevices predicate (device_allocator.go:391-402): skip minors whose free resources are
+ * all zero; quotav1.LessThanOrEqual(requestPerInstance, free) over the request's keys. */
+static int dev_minor_fits(const int64_t* fr, const int64_t* preq, uint32_t keys) {
+    if (fr[0] == 0 && fr[1] == 0 && fr[2] == 0) return 0;
+    for (int r = 0; r < KG_DEV_R; r++)
+        if (((keys >> r) & 1u) && preq[r] > fr[r]) return 0;
+    return 1;
+}
+
+/* DeviceShare Filter (deviceshare/plugin.go:345-421 -> AutopilotAllocator.Allocate, GPUAllocator
+ * generalAllocate -> defaultAllocateDevices) for a node without GPU topology tree or partition table,
+ * and the node Score (scoring.go:45-104 -> AutopilotAllocator.score -> scoreNode). */
+static uint32_t dev_eval(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                         uint32_t j, int64_t* raw) {
+    *raw = 0;
+    uint32_t cnt = p->dev_count ? p->dev_count[j] : 0;
+    if (cnt == 0) return 0;                                 /* PreFilter Skip */
+    int32_t D = n->dev_minors ? n->dev_minors[i] : -1;
+    if (D < 0) return 0;                                    /* no Device object: pass, Score 0 */
+    if (D == 0) return KG_ST_DEV_NO_DEVICE;                 /* devicehandler_gpu.go:41-44 */
+    int64_t preq[KG_DEV_R], T[KG_DEV_R] = {0, 0, 0}, F[KG_DEV_R] = {0, 0, 0};
+    uint32_t keys;
+    dev_pod_req(p, j, preq, &keys);
+    uint32_t fit = 0;
+    for (int32_t m = 0; m < D; m++) {
+        int64_t fr[KG_DEV_R];
+        for (int r = 0; r < KG_DEV_R; r++) {
+            fr[r] = DEVX(n->dev_free, i, r, m);
+            T[r] += DEVX(n->dev_total, i, r, m);
+            F[r] += fr[r];
+        }
+        fit += (uint32_t)dev_minor_fits(fr, preq, keys);
+    }
+    if (fit < cnt) return KG_ST_DEV_INSUFFICIENT;
+    *raw = dev_least(c->dev_w, T, F, preq);
+    return 0;
+}
+
+/* Reserve-time minor choice: scoreDevices + sortDeviceResourcesByMinor (score desc, minor asc,
+ * device_resources.go:171-209), first numberOfGPUs minors that fit. Returns the minor bitmask. */
+static uint32_t dev_choose(const kg_config* c, const int64_t* total_tab, const int64_t* free_tab, uint32_t i,
+                           int32_t D, const int64_t* preq, uint32_t keys, uint32_t cnt) {
+    int64_t sc[KG_DEV_MINORS];
+    int order[KG_DEV_MINORS];
+    for (int32_t m = 0; m < D; m++) {
+        int64_t t[KG_DEV_R], f[KG_DEV_R];
+        for (int r = 0; r < KG_DEV_R; r++) {
+            t[r] = DEVX(total_tab, i, r, m);
+            f[r] = DEVX(free_tab, i, r, m);
+        }
+        sc[m] = dev_least(c->dev_w, t, f, preq);
+        order[m] = m;
+    }
+    for (int32_t a = 1; a < D; a++) { /* stable insertion sort by score desc (minor asc on ties) */
+        int x = order[a];
+        int32_t b = a;
+        while (b > 0 && sc[order[b - 1]] < sc[x]) {
+            order[b] = order[b - 1];
+            b--;
+        }
+        order[b] = x;
+    }
+    uint32_t mask = 0, got = 0;
+    for (int32_t t = 0; t < D && got < cnt; t++) {
+        int m = order[t];
+        int64_t fr[KG_DEV_R];
+        for (int r = 0; r < KG_DEV_R; r++) fr[r] = DEVX(free_tab, i, r, m);
+        if (!dev_minor_fits(fr, preq, keys)) continue;
+        mask |= 1u << m;
+        got++;
+    }
+    return got < cnt ? 0 : mask;
+}
+
+/* Per-minor allocation after fillGPUTotalMem (devicehandler_gpu.go:98-135): gpu-memory from the ratio
+ * (ratio * total / 100) or the ratio from gpu-memory (int64(float64(mem)/float64(total)*100)). */
+int64_t kgo_mem_bytes_to_ratio(int64_t bytes, int64_t total) {
+    volatile double q = (double)bytes / (double)total;
+    volatile double r = q * 100.0;
+    return (int64_t)r;
+}
+
+static void dev_alloc_of(const int64_t* preq, uint32_t keys, int64_t total_mem, int64_t* alloc) {
+    alloc[KG_DEV_CORE] = (keys & (1u << KG_DEV_CORE)) ? preq[KG_DEV_CORE] : 0;
+    int has_r = (keys & (1u << KG_DEV_RATIO)) != 0, has_m = (keys & (1u << KG_DEV_MEM)) != 0;
+    if (has_r && has_m) {
+        alloc[KG_DEV_RATIO] = preq[KG_DEV_RATIO];
+        alloc[KG_DEV_MEM] = preq[KG_DEV_MEM];
+    } else if (has_m) {
+        alloc[KG_DEV_MEM] = preq[KG_DEV_MEM];
+        alloc[KG_DEV_RATIO] = kgo_mem_bytes_to_ratio(preq[KG_DEV_MEM], total_mem);
+    } else {
+        int64_t ratio = has_r ? preq[KG_DEV_RATIO] : 0;
+        alloc[KG_DEV_RATIO] = ratio;
+        alloc[KG_DEV_MEM] = ratio * total_mem / 100;
+    }
+}
+
+static void dev_apply(const int64_t* total_tab, int64_t* free_tab, uint32_t i, uint32_t mask, const int64_t* preq,
+                      uint32_t keys, int64_t sign) {
+    for (int m = 0; m < KG_DEV_MINORS; m++) {
+        if (!((mask >> m) & 1u)) continue;
+        int64_t a[KG_DEV_R];
+        dev_alloc_of(preq, keys, DEVX(total_tab, i, KG_DEV_MEM, m), a);
+        for (int r = 0; r < KG_DEV_R; r++) DEVX(free_tab, i, r, m) -= sign * a[r];
+    }
+}
+
+/* ---- ElasticQuota ----------------------------------------------------------------------------- */
+
+typedef struct kgo_quota_state {
+    uint32_t n;
+    const kg_quota_columns* lim;
+    int64_t *used, *np_used;
+    uint32_t *used_keys, *np_keys;
+} kgo_quota_state;
+
+static void quota_pod_req(const kg_pod_columns* p, uint32_t j, int64_t* req, uint32_t* keys) {
+    *keys = p->quota_keys ? p->quota_keys[j] : 0;
+    const int64_t v[KG_QUOTA_R] = {p->req_cpu[j], p->req_mem[j], p->sc_req[0][j], p->sc_req[1][j]};
+    for (int r = 0; r < KG_QUOTA_R; r++) req[r] = ((*keys >> r) & 1u) ? v[r] : 0;
+}
+
+/* quotav1.LessThanOrEqual(a, b): every key of b that a also has must satisfy a <= b. */
+static int quota_le(const int64_t* a, uint32_t akeys, const int64_t* b, uint32_t bkeys) {
+    for (int r = 0; r < KG_QUOTA_R; r++)
+        if (((bkeys & akeys) >> r) & 1u)
+            if (a[r] > b[r]) return 0;
+    return 1;
+}
+
+/* ElasticQuota PreFilter (elasticquota/plugin.go:257-309), flat quotas. */
+static uint32_t quota_gate(const kgo_quota_state* q, const kg_pod_columns* p, uint32_t j) {
+    int32_t qi = p->quota ? p->quota[j] : -1;
+    if (qi < 0 || !q || (uint32_t)qi >= q->n) return 0;
+    int64_t req[KG_QUOTA_R], a[KG_QUOTA_R];
+    uint32_t rk;
+    quota_pod_req(p, j, req, &rk);
+    const size_t o = (size_t)qi * KG_QUOTA_R;
+    for (int r = 0; r < KG_QUOTA_R; r++) a[r] = req[r] + q->used[o + r];
+    if (!quota_le(a, rk | q->used_keys[qi], q->lim->used_limit + o, q->lim->limit_keys[qi])) return KG_ST_QUOTA;
+    if (p->flags[j] & KG_POD_NON_PREEMPTIBLE) {
+        for (int r = 0; r < KG_QUOTA_R; r++) a[r] = req[r] + q->np_used[o + r];
+        if (!quota_le(a, rk | q->np_keys[qi], q->lim->min + o, q->lim->min_keys[qi])) return KG_ST_QUOTA;
+    }
+    return 0;
+}
+
+/* Reserve / Unreserve: GroupQuotaManager.updatePodUsedNoLock adds Mask(PodRequests, Max names) to used
+ * (and non-preemptible used), never below zero (core/group_quota_manager.go:765-805,1008-1046). */
+static void quota_apply(kgo_quota_state* q, const kg_pod_columns* p, uint32_t j, int64_t sign) {
+    int32_t qi = p->quota ? p->quota[j] : -1;
+    if (qi < 0 || !q || (uint32_t)qi >= q->n) return;
+    int64_t req[KG_QUOTA_R];
+    uint32_t rk;
+    quota_pod_req(p, j, req, &rk);
+    const size_t o = (size_t)qi * KG_QUOTA_R;
+    int np = (p->flags[j] & KG_POD_NON_PREEMPTIBLE) != 0;
+    for (int r = 0; r < KG_QUOTA_R; r++) {
+        if (!((rk >> r) & 1u)) continue;
+        int64_t u = q->used[o + r] + sign * req[r];
+        q->used[o + r] = u < 0 ? 0 : u;
+        if (np) {
+            int64_t v = q->np_used[o + r] + sign * req[r];
+            q->np_used[o + r] = v < 0 ? 0 : v;
+        }
+    }
+    q->used_keys[qi] |= rk;
+    if (np) q->np_keys[qi] |= rk;
+}
+
+static kgo_quota_state* quota_state_new(const kg_quota_columns* cols, uint32_t n) {
+    if (!cols || n == 0) return NULL;
+    kgo_quota_state* q = (kgo_quota_state*)calloc(1, sizeof(*q));
+    q->n = n;
+    q->lim = cols;
+    q->used = (int64_t*)calloc((size_t)n * KG_QUOTA_R, 8);
+    q->np_used = (int64_t*)calloc((size_t)n * KG_QUOTA_R, 8);
+    q->used_keys = (uint32_t*)calloc(n, 4);
+    q->np_keys = (uint32_t*)calloc(n, 4);
+    memcpy(q->used, cols->used, (size_t)n * KG_QUOTA_R * 8);
+    memcpy(q->np_used, cols->np_used, (size_t)n * KG_QUOTA_R * 8);
+    memcpy(q->used_keys, cols->used_keys, (size_t)n * 4);
+    memcpy(q->np_keys, cols->np_used_keys, (size_t)n * 4);
+    return q;
+}
+
+static void quota_state_free(kgo_quota_state* q) {
+    if (!q) return;
+    free(q->used);
+    free(q->np_used);
+    free(q->used_keys);
+    free(q->np_keys);
+    free(q);
+}
+
+/* ---- Reservation ------------------------------------------------------------------------------ */
+
+/* quotav1.ResourceNames(PodRequests) over the KG_RSV_R dimensions (keys present; scalar / ephemeral
+ * requests are present when non-zero). */
+static uint32_t rsv_pod_names(const kg_pod_columns* p, uint32_t j) {
+    uint32_t m = 0;
+    if (p->flags[j] & KG_POD_HAS_CPU) m |= 1u;
+    if (p->flags[j] & KG_POD_HAS_MEM) m |= 2u;
+    if (p->req_eph[j] != 0) m |= 4u;
+    if (p->sc_req[0][j] != 0) m |= 8u;
+    if (p->sc_req[1][j] != 0) m |= 16u;
+    return m;
+}
+
+static void rsv_pod_req(const kg_pod_columns* p, uint32_t j, int64_t* r) {
+    r[0] = p->req_cpu[j];
+    r[1] = p->req_mem[j];
+    r[2] = p->req_eph[j];
+    r[3] = p->sc_req[0][j];
+    r[4] = p->sc_req[1][j];
+}
+
+/* ReservationInfo.GetAvailable: max(0, Allocatable - Allocated - Reserved), reservation_info.go:516-519. */
+static void rsv_remained(const kg_rsv_info* r, int64_t* out) {
+    for (int k = 0; k < KG_RSV_R; k++) {
+        int64_t v = r->allocatable[k] - r->allocated[k] - r->reserved[k];
+        out[k] = v < 0 ? 0 : v;
+    }
+}
+
+/* fitsNode (reservation/plugin.go:915-965); returns a bitmask of insufficient resources (bit 5 = pods). */
+static uint32_t rsv_fits_node(const int64_t* preq, uint32_t pnames, const int64_t* alloc, int64_t allowed,
+                              const int64_t* requested, const int64_t* r_alloc, const int64_t* rem, int64_t matched,
+                              int64_t pods) {
+    uint32_t bad = 0;
+    if (pods - matched + 1 > allowed) bad |= 1u << 5;
+    if (preq[0] == 0 && preq[1] == 0 && preq[2] == 0 && !(pnames & 0x18u)) return bad;
+    for (int k = 0; k < KG_RSV_R; k++) {
+        if (k >= 3 && !((pnames >> k) & 1u)) continue; /* scalar resources the pod requests */
+        if (preq[k] > alloc[k] - (requested[k] - rem[k] - r_alloc[k])) bad |= 1u << k;
+    }
+    return bad;
+}
+
+/* fitsReservation (reservation/plugin.go:973-1057). */
+static uint32_t rsv_fits_reservation(const int64_t* preq, uint32_t pnames, const kg_rsv_info* r) {
+    uint32_t bad = 0;
+    if (r->max_pods >= 0 && r->allocated_pods + 1 > r->max_pods) bad |= 1u << 5;
+    for (int k = 0; k < KG_RSV_R; k++) {
+        if (!((r->names >> k) & 1u)) continue;
+        if (!((pnames >> k) & 1u) || preq[k] == 0) continue;
+        int64_t used = r->allocated[k] < 0 ? 0 : r->allocated[k];
+        int64_t cap = r->allocatable[k] - r->reserved[k];
+        if (preq[k] <= cap - used) continue;
+        bad |= 1u << k;
+    }
+    return bad;
+}
+
+typedef struct rsv_ctx {
+    const kg_node_columns* n;
+    uint32_t i;
+    const kg_rsv_view* v;
+    const kg_rsv_info* infos;
+    int64_t preq[KG_RSV_R], alloc[KG_RSV_R];
+    uint32_t pnames;
+    int required;
+} rsv_ctx;
+
+static void rsv_ctx_init(rsv_ctx* x, const kg_node_columns* n, uint32_t i, const kg_rsv_view* v,
+                         const kg_rsv_info* infos, const kg_pod_columns* p, uint32_t j) {
+    x->n = n;
+    x->i = i;
+    x->v = v;
+    x->infos = infos;
+    rsv_pod_req(p, j, x->preq);
+    x->pnames = rsv_pod_names(p, j);
+    x->required = (p->flags[j] & KG_POD_RSV_REQUIRED) != 0;
+    x->alloc[0] = n->alloc_cpu[i];
+    x->alloc[1] = n->alloc_mem[i];
+    x->alloc[2] = n->alloc_eph[i];
+    x->alloc[3] = n->sc_alloc[0][i];
+    x->alloc[4] = n->sc_alloc[1][i];
+}
+
+/* fitsNodeAndReservation (reservation/plugin.go:858-895) for matched reservation r: 0 = fits. */
+static int rsv_fits_one(const rsv_ctx* x, const kg_rsv_info* r, uint32_t* bn, uint32_t* br) {
+    int64_t rem[KG_RSV_R];
+    rsv_remained(r, rem);
+    *bn = rsv_fits_node(x->preq, x->pnames, x->alloc, x->n->alloc_pods[x->i], x->v->pod_requested,
+                        x->v->r_allocated, rem, (int64_t)x->v->count, x->v->num_pods);
+    *br = 0;
+    if (r->policy == KG_RSV_RESTRICTED) {
+        *br = rsv_fits_reservation(x->preq, x->pnames, r);
+        return (*bn == 0 && *br == 0) ? 0 : 1;
+    }
+    return *bn == 0 ? 0 : 1;
+}
+
+/* Reservation Filter for a normal pod (reservation/plugin.go:319-409) -> filterWithReservations
+ * (:411-527); RunReservationFilterPlugins passes for cpu/memory reservations. */
+static uint32_t rsv_filter(const rsv_ctx* x) {
+    if (!x->v) return x->required ? KG_ST_RSV_AFFINITY : 0;
+    uint32_t any_node = 0, any_resv = 0;
+    for (uint32_t t = 0; t < x->v->count; t++) {
+        const kg_rsv_info* r = &x->infos[x->v->first + t];
+        if (!x->required && !(r->names & x->pnames)) continue;
+        uint32_t bn, br;
+        if (rsv_fits_one(x, r, &bn, &br) == 0) return 0;
+        any_node |= bn;
+        any_resv |= br;
+    }
+    if (x->required) return KG_ST_RSV_RESERVATION * (any_resv != 0 || any_node == 0) | (any_node ? KG_ST_RSV_NODE : 0);
+    if (any_node) return KG_ST_RSV_NODE;
+    int64_t zero[KG_RSV_R] = {0, 0, 0, 0, 0};
+    uint32_t bn = rsv_fits_node(x->preq, x->pnames, x->alloc, x->n->alloc_pods[x->i], x->v->pod_requested,
+                                x->v->r_allocated, zero, (int64_t)x->v->count, x->v->num_pods);
+    return bn ? KG_ST_RSV_NODE : 0;
+}
+
+/* findMostPreferredReservationByOrder (reservation/scoring.go:295-314): index of the smallest non-zero
+ * order among infos[first, first+count) passing `ok` (NULL = all), -1 if none. */
+static int rsv_most_preferred(const kg_rsv_info* infos, uint32_t first, uint32_t count, const int* ok) {
+    int best = -1;
+    int64_t sel = INT64_MAX;
+    for (uint32_t t = 0; t < count; t++) {
+        if (ok && !ok[t]) continue;
+        int64_t o = infos[first + t].order;
+        if (o != 0 && sel > o) {
+            sel = o;
+            best = (int)t;
+        }
+    }
+    return best;
+}
+
+/* ScoreReservation (reservation/scoring.go:262-289): MostAllocated over RemoveZeros(Allocatable),
+ * requested = PodRequests + Allocated, MilliValue arithmetic (cpu is milli already). */
+static int64_t rsv_score_reservation(const rsv_ctx* x, const kg_rsv_info* r) {
+    int64_t w = 0, s = 0;
+    for (int k = 0; k < KG_RSV_R; k++) {
+        int64_t cap = r->allocatable[k];
+        if (cap == 0) continue;
+        w++;
+        int64_t req = x->preq[k] + r->allocated[k];
+        if (req <= cap) {
+            int64_t m = k == 0 ? 1 : 1000;
+            s += (int64_t)((uint64_t)MAX_NODE_SCORE * (uint64_t)(req * m)) / (cap * m);
+        }
+    }
+    if (r->max_pods > 0) w++; /* "pods" in Allocatable: requested pods 0 -> contributes 0 */
+    if (w <= 0) return 0;
+    return s / w;
+}
+
+/* Nominated reservation's score for a feasible pair (NominateReservation nominator.go:348-419 with
+ * FilterNominateReservation plugin.go:1195-1212), and the node's order for preferredNode. */
+static int64_t rsv_nominate_score(const rsv_ctx* x, int64_t* node_order) {
+    *node_order = 0;
+    if (!x->v || x->v->count == 0) return 0;
+    const kg_rsv_info* infos = x->infos;
+    const uint32_t first = x->v->first, count = x->v->count;
+    int bi = rsv_most_preferred(infos, first, count, NULL);
+    if (bi >= 0) *node_order = infos[first + bi].order;
+    const kg_rsv_info* nom = NULL;
+    if (count == 1 && x->required) {
+        nom = &infos[first];
+    } else {
+        int ok[64];
+        uint32_t nc = 0;
+        int last = -1;
+        for (uint32_t t = 0; t < count; t++) {
+            const kg_rsv_info* r = &infos[first + t];
+            ok[t] = 0;
+            if (r->allocate_once && r->allocated_pods > 0) continue;
+            if (!x->required && !(r->names & x->pnames)) continue;
+            uint32_t bn, br;
+            if (rsv_fits_one(x, r, &bn, &br) != 0) continue;
+            ok[t] = 1;
+            nc++;
+            last = (int)t;
+        }
+        if (nc == 1) {
+            nom = &infos[first + last];
+        } else if (nc > 1) {
+            int o = rsv_most_preferred(infos, first, count, ok);
+            if (o >= 0) {
+                nom = &infos[first + o];
+            } else {
+                int64_t best = -1;
+                for (uint32_t t = 0; t < count; t++) {
+                    if (!ok[t]) continue;
+                    int64_t sc = rsv_score_reservation(x, &infos[first + t]);
+                    if (sc > best) { /* stable sort by score desc: first of the maxima */
+                        best = sc;
+                        nom = &infos[first + t];
+                    }
+                }
+            }
+        }
+    }
+    return nom ? rsv_score_reservation(x, nom) : 0;
+}
+
+/* ---- one pod against every node --------------------------------------------------------------- */
+
+/* view index per node for one class: built per call (views are few). */
+static const kg_rsv_view* find_view(const kgo_ext* e, int32_t cls, uint32_t i) {
+    if (!e || cls < 0) return NULL;
+    for (uint32_t v = 0; v < e->n_views; v++)
+        if (e->views[v].node == i && e->views[v].cls == (uint32_t)cls) return &e->views[v];
+    return NULL;
+}
+
+static int64_t normalize(int64_t s, int64_t max) { return max == 0 ? s : s * MAX_NODE_SCORE / max; }
+
+typedef struct ext_row {
+    uint32_t* st;
+    int64_t *nrf, *la, *numa, *dev, *rsv, *total, *order;
+    int32_t* zone;
+} ext_row;
+
+static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t nn, const kg_pod_columns* p,
+                         uint32_t j, const kgo_ext* e, const kgo_quota_state* q, ext_row* o) {
+    uint32_t qst = (c->plugins & KG_PLUGIN_QUOTA) ? quota_gate(q, p, j) : 0;
+    const int32_t cls = (c->plugins & KG_PLUGIN_RSV) && p->rsv_class ? p->rsv_class[j] : -1;
+    const int gpu_pod = (c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0;
+    for (uint32_t i = 0; i < nn; i++) {
+        o->nrf[i] = o->la[i] = o->numa[i] = o->dev[i] = o->rsv[i] = o->order[i] = 0;
+        o->zone[i] = -1;
+        o->total[i] = -1;
+        if (qst) { /* PreFilter rejected the pod: no node is evaluated */
+            o->st[i] = qst;
+            continue;
+        }
+        const kg_rsv_view* v = (c->plugins & KG_PLUGIN_RSV) ? find_view(e, cls, i) : NULL;
+        kgo_over ov, *ovp = NULL;
+        if (v) {
+            for (int k = 0; k < KG_RSV_R; k++) ov.req[k] = v->req[k];
+            ov.nz_cpu = v->nz_cpu;
+            ov.nz_mem = v->nz_mem;
+            ov.num_pods = v->num_pods;
+            ovp = &ov;
+        }
+        uint32_t st = 0;
+        int64_t s_numa = 0;
+        int32_t zone = -1;
+        if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(n, i, ovp, p, j);
+        if (c->plugins & KG_PLUGIN_LA) st |= la_filter(c, n, i, p, j);
+        if (c->plugins & KG_PLUGIN_NUMA) {
+            if (v && n->numa_policy[i] != KG_NUMA_NONE && !(p->flags[j] & KG_POD_NUMA_SKIP))
+                st |= KG_ST_UNSUPPORTED; /* NUMA zone restore of reservations: host path */
+            else
+                st |= numa_eval(c, n, i, ovp, p, j, &s_numa, &zone);
+        }
+        int64_t dev_raw = 0;
+        if (c->plugins & KG_PLUGIN_DEV) st |= dev_eval(c, n, i, p, j, &dev_raw);
+        if (gpu_pod && v) st |= KG_ST_UNSUPPORTED; /* DeviceShare reservation restore: host path */
+        rsv_ctx x;
+        if (c->plugins & KG_PLUGIN_RSV) {
+            rsv_ctx_init(&x, n, i, v, e ? e->infos : NULL, p, j);
+            st |= rsv_filter(&x);
+        }
+        o->st[i] = st;
+        o->nrf[i] = (c->plugins & KG_PLUGIN_NRF) ? nrf_score(c, n, i, ovp, p, j) : 0;
+        o->la[i] = (c->plugins & KG_PLUGIN_LA) ? la_score(c, n, i, p, j) : 0;
+        o->numa[i] = (c->plugins & KG_PLUGIN_NUMA) && !(st & (KG_ST_NUMA_MASK | KG_ST_UNSUPPORTED)) ? s_numa : 0;
+        if (st) continue;
+        o->zone[i] = zone;
+        o->dev[i] = dev_raw;
+        if ((c->plugins & KG_PLUGIN_RSV) && v) o->rsv[i] = rsv_nominate_score(&x, &o->order[i]);
+    }
+    if (qst) return;
+    /* PreScore preferredNode (reservation/scoring.go:113-121) and NormalizeScore maxima over the
+     * feasible nodes (DefaultNormalizeScore, frameworkext/normalize_score.go:24-52) */
+    int64_t dev_max = 0, rsv_max = 0, pref_order = INT64_MAX;
+    int64_t pref = -1;
+    for (uint32_t i = 0; i < nn; i++) {
+        if (o->st[i]) continue;
+        if (o->dev[i] > dev_max) dev_max = o->dev[i];
+        if (o->order[i] != 0 && pref_order > o->order[i]) {
+            pref_order = o->order[i];
+            pref = i;
+        }
+    }
+    if (pref >= 0) o->rsv[pref] = 1000; /* mostPreferredScore */
+    for (uint32_t i = 0; i < nn; i++)
+        if (!o->st[i] && o->rsv[i] > rsv_max) rsv_max = o->rsv[i];
+    for (uint32_t i = 0; i < nn; i++) {
+        if (o->st[i]) continue;
+        o->total[i] = c->weight_nrf * o->nrf[i] + c->weight_la * o->la[i] + c->weight_numa * o->numa[i] +
+                      c->weight_dev * normalize(o->dev[i], dev_max) + c->weight_rsv * normalize(o->rsv[i], rsv_max);
+    }
+}
+
+typedef struct ext_buf {
+    ext_row r;
+    void* mem;
+} ext_buf;
+
+static int ext_buf_new(ext_buf* b, uint32_t nn) {
+    size_t m = nn ? nn : 1;
+    b->mem = calloc(m, 4 + 8 * 8 + 4);
+    if (!b->mem) return -1;
+    int64_t* q = (int64_t*)b->mem;
+    b->r.nrf = q;
+    b->r.la = q + m;
+    b->r.numa = q + 2 * m;
+    b->r.dev = q + 3 * m;
+    b->r.rsv = q + 4 * m;
+    b->r.total = q + 5 * m;
+    b->r.order = q + 6 * m;
+    b->r.st = (uint32_t*)(q + 8 * m);
+    b->r.zone = (int32_t*)(b->r.st + m);
+    return 0;
+}
+
+int kgo_ext_verify(const kg_config* c, const kg_node_columns* n, uint32_t nn, const kg_pod_columns* p, uint32_t np,
+                   const kgo_ext* e, kg_verify_out* out) {
+    ext_buf b;
+    if (ext_buf_new(&b, nn)) return -1;
+    kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    for (uint32_t j = 0; j < np; j++) {
+        ext_eval_pod(c, n, nn, p, j, e, q, &b.r);
+        for (uint32_t i = 0; i < nn; i++) {
+            size_t x = (size_t)j * nn + i;
+            if (out->status) out->status[x] = b.r.st[i];
+            if (out->score_nrf) out->score_nrf[x] = b.r.nrf[i];
+            if (out->score_la) out->score_la[x] = b.r.la[i];
+            if (out->score_numa) out->score_numa[x] = b.r.numa[i];
+            if (out->score_dev) out->score_dev[x] = b.r.dev[i];
+            if (out->score_rsv) out->score_rsv[x] = b.r.rsv[i];
+            if (out->total) out->total[x] = b.r.total[i];
+            if (out->numa_zone) out->numa_zone[x] = (int8_t)b.r.zone[i];
+        }
+    }
+    quota_state_free(q);
+    free(b.mem);
+    return 0;
+}
+
+int kgo_ext_select(const kg_config* c, const kg_node_columns* n, uint32_t nn, uint32_t base, const kg_pod_columns* p,
+                   uint32_t np, const kgo_ext* e, uint32_t k, uint64_t* keys) {
+    ext_buf b;
+    if (ext_buf_new(&b, nn)) return -1;
+    kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    for (uint32_t j = 0; j < np; j++) {
+        uint64_t* top = keys + (size_t)j * k;
+        memset(top, 0, sizeof(uint64_t) * k);
+        ext_eval_pod(c, n, nn, p, j, e, q, &b.r);
+        for (uint32_t i = 0; i < nn; i++)
+            if (!b.r.st[i]) topk_insert(top, k, make_key(b.r.total[i], base + i));
+    }
+    quota_state_free(q);
+    free(b.mem);
+    return 0;
+}
+
+/* Sequential scheduling with every Reserve applied before the next pod (DeviceShare minors,
+ * ElasticQuota used, NodeInfo / LoadAware / NUMA). Reservation views are not replayed (their restore
+ * changes with every placement): returns -1 when KG_PLUGIN_RSV is enabled. out_minors may be NULL. */
+int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
+                   const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
+                   int64_t* quota_used_out, int64_t* quota_np_used_out) {
+    if (c->plugins & KG_PLUGIN_RSV) return -1;
+    kg_node_columns v;
+    kgo_state_view(st, &v);
+    ext_buf b;
+    if (ext_buf_new(&b, st->n)) return -1;
+    kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    for (uint32_t j = 0; j < np; j++) {
+        ext_eval_pod(c, &v, st->n, p, j, e, q, &b.r);
+        uint64_t best = 0;
+        int32_t best_zone = -1;
+        for (uint32_t i = 0; i < st->n; i++) {
+            if (b.r.st[i]) continue;
+            uint64_t key = make_key(b.r.total[i], base + i);
+            if (key > best) {
+                best = key;
+                best_zone = b.r.zone[i];
+            }
+        }
+        if (out_minors) out_minors[j] = 0;
+        if (!best) {
+            out_node[j] = -1;
+            if (out_total) out_total[j] = -1;
+            continue;
+        }
+        uint32_t g = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
+        uint32_t i = g - base;
+        out_node[j] = (int32_t)g;
+        if (out_total) out_total[j] = (int64_t)(best >> 32);
+        apply(c, st, i, p, j, best_zone, 1);
+        if ((c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0 && st->dev_minors &&
+            st->dev_minors[i] > 0) {
+            int64_t preq[KG_DEV_R];
+            uint32_t keys;
+            dev_pod_req(p, j, preq, &keys);
+            uint32_t mask = dev_choose(c, st->dev_total, st->dev_free, i, st->dev_minors[i], preq, keys, p->dev_count[j]);
+            dev_apply(st->dev_total, st->dev_free, i, mask, preq, keys, 1);
+            if (out_minors) out_minors[j] = mask;
+        }
+        quota_apply(q, p, j, 1);
+    }
+    if (q) {
+        if (quota_used_out) memcpy(quota_used_out, q->used, (size_t)q->n * KG_QUOTA_R * 8);
+        if (quota_np_used_out) memcpy(quota_np_used_out, q->np_used, (size_t)q->n * KG_QUOTA_R * 8);
+    }
+    quota_state_free(q);
+    free(b.mem);
+    return 0;
 }

@@ -60,6 +60,30 @@ void kgo_forget(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod
 void kgo_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, const kg_pod_columns* pods,
                 uint32_t n_pods, int32_t* out_node, int64_t* out_total);
 
+/* Config-5 plugins (DeviceShare, Reservation, ElasticQuota): the tables the plugins read besides the
+ * node columns. quotas: state at the start of the batch; views / infos: Reservation restore views. */
+typedef struct kgo_ext {
+    const kg_quota_columns* quotas;
+    uint32_t n_quotas;
+    const kg_rsv_view* views;
+    uint32_t n_views;
+    const kg_rsv_info* infos;
+    uint32_t n_infos;
+} kgo_ext;
+
+/* Verify matrix with every enabled plugin incl. KG_PLUGIN_DEV / RSV / QUOTA: raw Score values, totals
+ * after NormalizeScore (DeviceShare, Reservation) and the weights. */
+int kgo_ext_verify(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes, const kg_pod_columns* pods,
+                   uint32_t n_pods, const kgo_ext* ext, kg_verify_out* out);
+int kgo_ext_select(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes, uint32_t index_base,
+                   const kg_pod_columns* pods, uint32_t n_pods, const kgo_ext* ext, uint32_t k, uint64_t* keys);
+/* Replay with DeviceShare / ElasticQuota Reserve between pods; out_minors: GPU minors chosen per pod;
+ * quota_*_out: final used / non-preemptible used [quota][KG_QUOTA_R]. -1 with KG_PLUGIN_RSV. */
+int kgo_ext_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, const kg_pod_columns* pods,
+                   uint32_t n_pods, const kgo_ext* ext, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
+                   int64_t* quota_used_out, int64_t* quota_np_used_out);
+int64_t kgo_mem_bytes_to_ratio(int64_t bytes, int64_t total);
+
 /* Helpers shared with tests. */
 int64_t kgo_amplify(int64_t origin, double ratio);
 int64_t kgo_la_usage_percent(int64_t estimated, int64_t total);

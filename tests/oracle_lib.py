@@ -21,6 +21,30 @@ class KgoPair(C.Structure):
                 ("total", C.c_int64), ("zone", C.c_int32)]
 
 
+class KgoExt(C.Structure):
+    _fields_ = [("quotas", C.POINTER(abi.KgQuotaColumns)), ("n_quotas", C.c_uint32),
+                ("views", C.POINTER(abi.KgRsvView)), ("n_views", C.c_uint32),
+                ("infos", C.POINTER(abi.KgRsvInfo)), ("n_infos", C.c_uint32)]
+
+
+def make_ext(quotas=None, rsv=None) -> KgoExt:
+    e = KgoExt()
+    keep = []
+    if quotas is not None:
+        qc = abi.quota_columns(quotas)
+        keep.append(qc)
+        e.quotas = C.pointer(qc)
+        e.n_quotas = len(quotas["used"])
+    if rsv is not None:
+        e.views = C.cast(rsv.views, C.POINTER(abi.KgRsvView))
+        e.n_views = rsv.n_views
+        e.infos = C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo))
+        e.n_infos = rsv.n_infos
+        keep.append(rsv)
+    e._keep = keep
+    return e
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -45,6 +69,18 @@ def lib():
         L.kgo_forget.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32, C.c_int32]
         L.kgo_replay.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
                                  P(C.c_int32), P(C.c_int64)]
+        L.kgo_ext_verify.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns),
+                                     C.c_uint32, P(KgoExt), P(abi.KgVerifyOut)]
+        L.kgo_ext_verify.restype = C.c_int
+        L.kgo_ext_select.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
+                                     P(abi.KgPodColumns), C.c_uint32, P(KgoExt), C.c_uint32, P(C.c_uint64)]
+        L.kgo_ext_select.restype = C.c_int
+        L.kgo_ext_replay.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
+                                     P(KgoExt), P(C.c_int32), P(C.c_int64), P(C.c_uint32), P(C.c_int64),
+                                     P(C.c_int64)]
+        L.kgo_ext_replay.restype = C.c_int
+        L.kgo_mem_bytes_to_ratio.argtypes = [C.c_int64, C.c_int64]
+        L.kgo_mem_bytes_to_ratio.restype = C.c_int64
         L.kgo_amplify.argtypes = [C.c_int64, C.c_double]
         L.kgo_amplify.restype = C.c_int64
         L.kgo_la_usage_percent.argtypes = [C.c_int64, C.c_int64]
@@ -87,6 +123,24 @@ def select_parallel(cfg, nodes: abi.Table, pods: abi.Table, workers: int = 16, i
     return keys
 
 
+def ext_verify(cfg, nodes: abi.Table, pods: abi.Table, quotas=None, rsv=None) -> abi.VerifyResult:
+    nn, np_ = abi.table_len(nodes), abi.table_len(pods)
+    res = abi.VerifyResult(np_, nn)
+    nc, pc, vo, e = abi.node_columns(nodes), abi.pod_columns(pods), res.struct(), make_ext(quotas, rsv)
+    assert lib().kgo_ext_verify(C.byref(cfg), C.byref(nc), nn, C.byref(pc), np_, C.byref(e), C.byref(vo)) == 0
+    return res
+
+
+def ext_select(cfg, nodes: abi.Table, pods: abi.Table, k: int = 1, index_base: int = 0, quotas=None,
+               rsv=None) -> np.ndarray:
+    nn, np_ = abi.table_len(nodes), abi.table_len(pods)
+    keys = np.zeros((np_, k), np.uint64)
+    nc, pc, e = abi.node_columns(nodes), abi.pod_columns(pods), make_ext(quotas, rsv)
+    assert lib().kgo_ext_select(C.byref(cfg), C.byref(nc), nn, index_base, C.byref(pc), np_, C.byref(e), k,
+                                keys.ctypes.data_as(C.POINTER(C.c_uint64))) == 0
+    return keys
+
+
 class OracleState:
     """Mutable oracle snapshot for Assume / replay."""
 
@@ -117,6 +171,30 @@ class OracleState:
         lib().kgo_replay(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_,
                          out_node.ctypes.data_as(C.POINTER(C.c_int32)), out_total.ctypes.data_as(C.POINTER(C.c_int64)))
         return out_node, out_total
+
+    def ext_replay(self, pods: abi.Table, quotas=None, index_base: int = 0):
+        np_ = abi.table_len(pods)
+        out_node = np.zeros(np_, np.int32)
+        out_total = np.zeros(np_, np.int64)
+        out_minors = np.zeros(np_, np.uint32)
+        nq = len(quotas["used"]) if quotas is not None else 0
+        qu = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
+        qn = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
+        pc, e = abi.pod_columns(pods), make_ext(quotas, None)
+        P = C.POINTER
+        rc = lib().kgo_ext_replay(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_, C.byref(e),
+                                  out_node.ctypes.data_as(P(C.c_int32)), out_total.ctypes.data_as(P(C.c_int64)),
+                                  out_minors.ctypes.data_as(P(C.c_uint32)), qu.ctypes.data_as(P(C.c_int64)),
+                                  qn.ctypes.data_as(P(C.c_int64)))
+        assert rc == 0
+        return out_node, out_total, out_minors, qu[:nq], qn[:nq]
+
+    def dev_free(self) -> np.ndarray:
+        v = abi.KgNodeColumns()
+        lib().kgo_state_view(self.h, C.byref(v))
+        if not v.dev_free:
+            return None
+        return np.ctypeslib.as_array(v.dev_free, shape=(self.n, abi.KG_DEV_R, abi.KG_DEV_MINORS)).copy()
 
     def table(self) -> abi.Table:
         """Copy of the current node columns."""
