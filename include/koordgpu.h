@@ -348,6 +348,8 @@ kg_status kg_assume_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t nod
                         uint32_t* out_minors);
 kg_status kg_forget_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t numa_zone,
                         uint32_t minors);
+/* GPU minors chosen for each pod by the last kg_replay (bitmask; 0 = none), n_pods entries. */
+kg_status kg_replay_minors(kg_pods* pods, uint32_t* out);
 
 /* Timing of the dominant kernel with HIP events on the launch stream. */
 kg_status kg_profile_enable(kg_ctx* ctx, int enable);

@@ -85,6 +85,33 @@ __device__ __forceinline__ int64_t numa_least(int64_t w_cpu, int64_t w_mem, int6
     return wdiv(sum, wsum);
 }
 
+// Node quantities a Reservation restore changes for pods of one owner class (kg_rsv_view): the
+// NodeResourcesFit and NodeNUMAResource terms read these instead of the record's int section.
+struct Over {
+    int64_t req[5];  // cpu, memory, ephemeral-storage, scalar0, scalar1
+    int64_t nz_cpu, nz_mem, num_pods;
+};
+
+// record slot s, or its restored value when a view applies
+template <bool OV>
+__device__ __forceinline__ int64_t nv(const int64_t* __restrict__ n, const Over* ov, int s) {
+    if constexpr (OV) {
+        switch (s) {
+            case N_REQ_CPU: return ov->req[0];
+            case N_REQ_MEM: return ov->req[1];
+            case N_REQ_EPH: return ov->req[2];
+            case N_SC_REQ0: return ov->req[3];
+            case N_SC_REQ1: return ov->req[4];
+            case N_NZ_CPU: return ov->nz_cpu;
+            case N_NZ_MEM: return ov->nz_mem;
+            case N_NUM_PODS: return ov->num_pods;
+            default: return n[s];
+        }
+    } else {
+        return n[s];
+    }
+}
+
 struct PairOut {
     uint32_t status;
     int64_t s_nrf, s_la, s_numa;
@@ -92,9 +119,9 @@ struct PairOut {
 };
 
 // NodeNUMAResource Filter + Score for a SingleNUMANode / None node.
-template <bool EXACT>
+template <bool EXACT, bool OV = false>
 __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restrict__ n, const ZoneRec* __restrict__ zr,
-                                          const PodV& p, uint32_t flags, PairOut& o) {
+                                          const PodV& p, uint32_t flags, PairOut& o, const Over* ov = nullptr) {
     if (p.flags & KG_POD_NUMA_SKIP) return;
     if (p.flags & KG_POD_CPU_BIND) {
         o.status |= KG_ST_UNSUPPORTED;
@@ -115,7 +142,7 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
     const int64_t pod_cpu = p.req_cpu;
     // filterAmplifiedCPUs
     if (pod_cpu != 0 && amp) {
-        int64_t requested = n[N_REQ_CPU];
+        int64_t requested = nv<OV>(n, ov, N_REQ_CPU);
         const int64_t cs = n[N_CPUSET];
         if (requested >= cs && cs > 0) requested = requested - cs + n[N_AMP_CPUSET];
         if (pod_cpu > n[N_ALLOC_CPU] - requested) {
@@ -155,8 +182,8 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
         }
         if (best < 0 || Z == 1) {  // best hint == default affinity: no NUMA allocation
             o.zone = -1;
-            o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], n[N_REQ_CPU] + pod_cpu, rcp_cpu,
-                                         n[N_ALLOC_MEM], n[N_REQ_MEM] + p.req_mem, rcp_mem);
+            o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
+                                         rcp_cpu, n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
             return;
         }
         o.zone = best;
@@ -166,15 +193,15 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
         return;
     }
     // policy None: scoreWithAmplifiedCPUs
-    int64_t req_cpu = n[N_REQ_CPU];
+    int64_t req_cpu = nv<OV>(n, ov, N_REQ_CPU);
     if (pod_cpu != 0 && amp) req_cpu = req_cpu - n[N_CPUSET] + n[N_AMP_CPUSET];
     o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], req_cpu + pod_cpu, rcp_cpu,
-                                 n[N_ALLOC_MEM], n[N_REQ_MEM] + p.req_mem, rcp_mem);
+                                 n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
 }
 
-template <bool EXACT>
+template <bool EXACT, bool OV = false>
 __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __restrict__ n,
-                                             const ZoneRec* __restrict__ zr, const PodV& p) {
+                                             const ZoneRec* __restrict__ zr, const PodV& p, const Over* ov = nullptr) {
     PairOut o;
     o.status = 0;
     o.s_nrf = o.s_la = o.s_numa = 0;
@@ -184,37 +211,37 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
     if (c.plugins & KG_PLUGIN_NRF) {
         // Fits
         uint32_t st = 0;
-        st |= (n[N_NUM_PODS] + 1 > n[N_ALLOC_PODS]) ? KG_ST_NRF_PODS : 0u;
-        st |= (p.req_cpu > 0 && p.req_cpu > n[N_ALLOC_CPU] - n[N_REQ_CPU]) ? KG_ST_NRF_CPU : 0u;
-        st |= (p.req_mem > 0 && p.req_mem > n[N_ALLOC_MEM] - n[N_REQ_MEM]) ? KG_ST_NRF_MEM : 0u;
-        st |= (p.req_eph > 0 && p.req_eph > n[N_ALLOC_EPH] - n[N_REQ_EPH]) ? KG_ST_NRF_EPH : 0u;
-        st |= (p.sc0 != 0 && p.sc0 > n[N_SC_ALLOC0] - n[N_SC_REQ0]) ? KG_ST_NRF_SC0 : 0u;
-        st |= (p.sc1 != 0 && p.sc1 > n[N_SC_ALLOC1] - n[N_SC_REQ1]) ? KG_ST_NRF_SC1 : 0u;
+        st |= (nv<OV>(n, ov, N_NUM_PODS) + 1 > n[N_ALLOC_PODS]) ? KG_ST_NRF_PODS : 0u;
+        st |= (p.req_cpu > 0 && p.req_cpu > n[N_ALLOC_CPU] - nv<OV>(n, ov, N_REQ_CPU)) ? KG_ST_NRF_CPU : 0u;
+        st |= (p.req_mem > 0 && p.req_mem > n[N_ALLOC_MEM] - nv<OV>(n, ov, N_REQ_MEM)) ? KG_ST_NRF_MEM : 0u;
+        st |= (p.req_eph > 0 && p.req_eph > n[N_ALLOC_EPH] - nv<OV>(n, ov, N_REQ_EPH)) ? KG_ST_NRF_EPH : 0u;
+        st |= (p.sc0 != 0 && p.sc0 > n[N_SC_ALLOC0] - nv<OV>(n, ov, N_SC_REQ0)) ? KG_ST_NRF_SC0 : 0u;
+        st |= (p.sc1 != 0 && p.sc1 > n[N_SC_ALLOC1] - nv<OV>(n, ov, N_SC_REQ1)) ? KG_ST_NRF_SC1 : 0u;
         o.status |= st;
         // LeastAllocated over {cpu, memory, scalar0, scalar1}
         int64_t sum = 0, wsum = 0;
         {
             const int64_t cap = n[N_ALLOC_CPU], w = c.nrf_w[0];
             const bool on = (w != 0) & (cap != 0);
-            sum += on ? least_req<EXACT>(n[N_NZ_CPU] + p.nz_cpu, cap, as_f64(n[N_RCP_CPU])) * w : 0;
+            sum += on ? least_req<EXACT>(nv<OV>(n, ov, N_NZ_CPU) + p.nz_cpu, cap, as_f64(n[N_RCP_CPU])) * w : 0;
             wsum += on ? w : 0;
         }
         {
             const int64_t cap = n[N_ALLOC_MEM], w = c.nrf_w[1];
             const bool on = (w != 0) & (cap != 0);
-            sum += on ? least_req<EXACT>(n[N_NZ_MEM] + p.nz_mem, cap, as_f64(n[N_RCP_MEM])) * w : 0;
+            sum += on ? least_req<EXACT>(nv<OV>(n, ov, N_NZ_MEM) + p.nz_mem, cap, as_f64(n[N_RCP_MEM])) * w : 0;
             wsum += on ? w : 0;
         }
         {
             const int64_t cap = n[N_SC_ALLOC0], w = c.nrf_w[2];
             const bool on = (w != 0) & (cap != 0) & (p.sc0 != 0);
-            sum += on ? least_req<EXACT>(n[N_SC_REQ0] + p.sc0, cap, as_f64(n[N_RCP_SC0])) * w : 0;
+            sum += on ? least_req<EXACT>(nv<OV>(n, ov, N_SC_REQ0) + p.sc0, cap, as_f64(n[N_RCP_SC0])) * w : 0;
             wsum += on ? w : 0;
         }
         {
             const int64_t cap = n[N_SC_ALLOC1], w = c.nrf_w[3];
             const bool on = (w != 0) & (cap != 0) & (p.sc1 != 0);
-            sum += on ? least_req<EXACT>(n[N_SC_REQ1] + p.sc1, cap, as_f64(n[N_RCP_SC1])) * w : 0;
+            sum += on ? least_req<EXACT>(nv<OV>(n, ov, N_SC_REQ1) + p.sc1, cap, as_f64(n[N_RCP_SC1])) * w : 0;
             wsum += on ? w : 0;
         }
         o.s_nrf = wdiv(sum, wsum);
@@ -251,7 +278,7 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
         }
     }
 
-    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT>(c, n, zr, p, flags, o);
+    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT, OV>(c, n, zr, p, flags, o, ov);
     if (o.status & (KG_ST_NUMA_MASK | KG_ST_UNSUPPORTED)) o.s_numa = 0;
     if (o.status) o.zone = -1;
     return o;

@@ -1,0 +1,463 @@
+// kg_ext.h — device arithmetic of the config-5 plugins (integer path, one (pod, node) pair per lane):
+//   DeviceShare  Filter / Score / Reserve   deviceshare/plugin.go:345-421,507-569, scoring.go:45-112,197-281,
+//                                           device_allocator.go:98-141,331-437, devicehandler_gpu.go:53-135
+//   Reservation  Filter / nominate / Score  reservation/plugin.go:319-527,858-1057,1195-1212,
+//                                           nominator.go:348-419, scoring.go:113-121,180-314
+//   ElasticQuota PreFilter / Reserve        elasticquota/plugin.go:257-309,622-636,
+//                                           core/group_quota_manager.go:765-805,1008-1046
+// The CPU restatement these must equal bit for bit is oracle/kg_oracle.c (ext section).
+#pragma once
+#include "kg_eval.h"
+
+namespace kg {
+
+struct PodX {
+    int64_t dreq[DEV_R];  // per-instance GPU request (keys in dkeys)
+    uint32_t dcount, dkeys;
+    int32_t quota;
+    uint32_t qkeys;
+    int32_t cls;
+};
+
+__device__ __forceinline__ PodX load_podx(const PodsDev& P, uint32_t j) {
+    PodX x;
+    x.dcount = P.dev_count ? P.dev_count[j] : 0u;
+    x.dkeys = P.dev_keys ? P.dev_keys[j] : 0u;
+    for (int r = 0; r < DEV_R; r++) x.dreq[r] = (P.dev_req && ((x.dkeys >> r) & 1u)) ? P.dev_req[(size_t)j * DEV_R + r] : 0;
+    x.quota = P.quota ? P.quota[j] : -1;
+    x.qkeys = P.quota_keys ? P.quota_keys[j] : 0u;
+    x.cls = P.rsv_class ? P.rsv_class[j] : -1;
+    return x;
+}
+
+// ---- DeviceShare ------------------------------------------------------------------------------------
+
+__device__ __forceinline__ int64_t least_score_i64(int64_t requested, int64_t capacity) {
+    if (capacity == 0 || requested > capacity) return 0;
+    return ((capacity - requested) * 100) / capacity;
+}
+
+// leastResourceScorer over {gpu-core, gpu-memory-ratio, gpu-memory}: zero totals skipped, requested =
+// total >= free ? total - free + request : total (scoreNode / scoreDevice).
+__device__ __forceinline__ int64_t dev_least(const KCfg& c, const int64_t* total, const int64_t* fr, const int64_t* preq) {
+    int64_t score = 0, wsum = 0;
+#pragma unroll
+    for (int r = 0; r < DEV_R; r++) {
+        const int64_t w = c.dev_w[r];
+        if (w == 0 || total[r] == 0) continue;
+        const int64_t req = total[r] >= fr[r] ? total[r] - fr[r] + preq[r] : total[r];
+        score += least_score_i64(req, total[r]) * w;
+        wsum += w;
+    }
+    return wsum == 0 ? 0 : score / wsum;
+}
+
+__device__ __forceinline__ bool dev_minor_fits(const int64_t* fr, const PodX& x) {
+    if (fr[0] == 0 && fr[1] == 0 && fr[2] == 0) return false;  // unhealthy / exhausted minor
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < DEV_R; r++) ok &= !(((x.dkeys >> r) & 1u) && x.dreq[r] > fr[r]);
+    return ok;
+}
+
+// Filter (count of minors that fit >= numberOfGPUs) + node Score before NormalizeScore.
+__device__ __forceinline__ uint32_t dev_eval(const KCfg& c, const int64_t* __restrict__ n, const DevRec* __restrict__ d,
+                                             const PodX& x, int64_t& raw) {
+    raw = 0;
+    if (x.dcount == 0) return 0;  // PreFilter Skip
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    if (D < 0) return 0;  // no Device object
+    if (D == 0) return KG_ST_DEV_NO_DEVICE;
+    int64_t T[DEV_R] = {0, 0, 0}, F[DEV_R] = {0, 0, 0};
+    uint32_t fit = 0;
+    for (int32_t m = 0; m < D; m++) {
+        int64_t fr[DEV_R];
+#pragma unroll
+        for (int r = 0; r < DEV_R; r++) {
+            fr[r] = d->free_[r][m];
+            T[r] += d->total[r][m];
+            F[r] += fr[r];
+        }
+        fit += dev_minor_fits(fr, x) ? 1u : 0u;
+    }
+    if (fit < x.dcount) return KG_ST_DEV_INSUFFICIENT;
+    raw = dev_least(c, T, F, x.dreq);
+    return 0;
+}
+
+// Reserve: minors by (per-minor score desc, minor asc), the first numberOfGPUs that fit.
+__device__ __forceinline__ uint32_t dev_choose(const KCfg& c, const int64_t* __restrict__ n, const DevRec* __restrict__ d,
+                                               const PodX& x) {
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    if (x.dcount == 0 || D <= 0) return 0;
+    int64_t sc[DEV_MINORS];
+    int ord[DEV_MINORS];
+    for (int32_t m = 0; m < D; m++) {
+        int64_t t[DEV_R], f[DEV_R];
+#pragma unroll
+        for (int r = 0; r < DEV_R; r++) {
+            t[r] = d->total[r][m];
+            f[r] = d->free_[r][m];
+        }
+        sc[m] = dev_least(c, t, f, x.dreq);
+        ord[m] = m;
+    }
+    for (int32_t a = 1; a < D; a++) {
+        const int v = ord[a];
+        int32_t b = a;
+        while (b > 0 && sc[ord[b - 1]] < sc[v]) {
+            ord[b] = ord[b - 1];
+            b--;
+        }
+        ord[b] = v;
+    }
+    uint32_t mask = 0, got = 0;
+    for (int32_t t = 0; t < D && got < x.dcount; t++) {
+        const int m = ord[t];
+        const int64_t fr[DEV_R] = {d->free_[0][m], d->free_[1][m], d->free_[2][m]};
+        if (!dev_minor_fits(fr, x)) continue;
+        mask |= 1u << m;
+        got++;
+    }
+    return got < x.dcount ? 0u : mask;
+}
+
+// fillGPUTotalMem: gpu-memory from the ratio, or the ratio from gpu-memory in float64 like Go.
+__device__ __forceinline__ void dev_alloc_of(const PodX& x, int64_t total_mem, int64_t* a) {
+    a[0] = ((x.dkeys >> 0) & 1u) ? x.dreq[0] : 0;
+    const bool hr = ((x.dkeys >> 1) & 1u) != 0, hm = ((x.dkeys >> 2) & 1u) != 0;
+    if (hr && hm) {
+        a[1] = x.dreq[1];
+        a[2] = x.dreq[2];
+    } else if (hm) {
+        a[2] = x.dreq[2];
+        const double q = __ddiv_rn((double)x.dreq[2], (double)total_mem);
+        a[1] = (int64_t)__dmul_rn(q, 100.0);
+    } else {
+        const int64_t ratio = hr ? x.dreq[1] : 0;
+        a[1] = ratio;
+        a[2] = ratio * total_mem / 100;
+    }
+}
+
+__device__ __forceinline__ void dev_apply(DevRec* __restrict__ d, uint32_t mask, const PodX& x, int64_t sign) {
+    for (int m = 0; m < DEV_MINORS; m++) {
+        if (!((mask >> m) & 1u)) continue;
+        int64_t a[DEV_R];
+        dev_alloc_of(x, d->total[2][m], a);
+#pragma unroll
+        for (int r = 0; r < DEV_R; r++) d->free_[r][m] -= sign * a[r];
+    }
+}
+
+// ---- ElasticQuota -----------------------------------------------------------------------------------
+
+__device__ __forceinline__ void quota_req(const PodV& p, const PodX& x, int64_t* q) {
+    const int64_t v[QUOTA_R] = {p.req_cpu, p.req_mem, p.sc0, p.sc1};
+#pragma unroll
+    for (int r = 0; r < QUOTA_R; r++) q[r] = ((x.qkeys >> r) & 1u) ? v[r] : 0;
+}
+
+// quotav1.LessThanOrEqual(a, b) over the keys of b that a has
+__device__ __forceinline__ bool quota_le(const int64_t* a, uint32_t ak, const int64_t* b, uint32_t bk) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < QUOTA_R; r++) ok &= !((((ak & bk) >> r) & 1u) && a[r] > b[r]);
+    return ok;
+}
+
+// PreFilter of the pod's quota given that quota's current state
+__device__ __forceinline__ uint32_t quota_gate(const QuotaLim& L, const QuotaState& S, const PodV& p, const PodX& x) {
+    int64_t q[QUOTA_R], a[QUOTA_R];
+    quota_req(p, x, q);
+#pragma unroll
+    for (int r = 0; r < QUOTA_R; r++) a[r] = q[r] + S.used[r];
+    if (!quota_le(a, x.qkeys | S.used_keys, L.limit, L.limit_keys)) return KG_ST_QUOTA;
+    if (p.flags & KG_POD_NON_PREEMPTIBLE) {
+#pragma unroll
+        for (int r = 0; r < QUOTA_R; r++) a[r] = q[r] + S.np_used[r];
+        if (!quota_le(a, x.qkeys | S.np_keys, L.min, L.min_keys)) return KG_ST_QUOTA;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ void quota_add(QuotaState& S, const PodV& p, const PodX& x, int64_t sign) {
+    int64_t q[QUOTA_R];
+    quota_req(p, x, q);
+    const bool np = (p.flags & KG_POD_NON_PREEMPTIBLE) != 0;
+#pragma unroll
+    for (int r = 0; r < QUOTA_R; r++) {
+        if (!((x.qkeys >> r) & 1u)) continue;
+        const int64_t u = S.used[r] + sign * q[r];
+        S.used[r] = u < 0 ? 0 : u;
+        if (np) {
+            const int64_t v = S.np_used[r] + sign * q[r];
+            S.np_used[r] = v < 0 ? 0 : v;
+        }
+    }
+    S.used_keys |= x.qkeys;
+    if (np) S.np_keys |= x.qkeys;
+}
+
+// ---- Reservation ------------------------------------------------------------------------------------
+
+__device__ __forceinline__ const RsvView* find_view(const ExtDev& e, int32_t cls, uint32_t rec) {
+    uint32_t lo = e.cls_begin[cls], hi = e.cls_begin[cls + 1];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint32_t r = e.views[mid].rec;
+        if (r == rec) return &e.views[mid];
+        if (r < rec)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return nullptr;
+}
+
+struct RsvPod {
+    int64_t preq[RSV_R];
+    uint32_t names;
+    bool required;
+};
+
+__device__ __forceinline__ RsvPod rsv_pod(const PodV& p) {
+    RsvPod r;
+    r.preq[0] = p.req_cpu;
+    r.preq[1] = p.req_mem;
+    r.preq[2] = p.req_eph;
+    r.preq[3] = p.sc0;
+    r.preq[4] = p.sc1;
+    r.names = ((p.flags & KG_POD_HAS_CPU) ? 1u : 0u) | ((p.flags & KG_POD_HAS_MEM) ? 2u : 0u) |
+              (p.req_eph != 0 ? 4u : 0u) | (p.sc0 != 0 ? 8u : 0u) | (p.sc1 != 0 ? 16u : 0u);
+    r.required = (p.flags & KG_POD_RSV_REQUIRED) != 0;
+    return r;
+}
+
+// fitsNode: bitmask of insufficient resources (bit 5 = pods); rem == nullptr -> zero remained
+__device__ __forceinline__ uint32_t rsv_fits_node(const RsvPod& q, const int64_t* __restrict__ n, const RsvView& v,
+                                                  const int64_t* rem) {
+    uint32_t bad = 0;
+    if (v.num_pods - (int64_t)v.count + 1 > n[N_ALLOC_PODS]) bad |= 1u << 5;
+    if (q.preq[0] == 0 && q.preq[1] == 0 && q.preq[2] == 0 && !(q.names & 0x18u)) return bad;
+    const int64_t alloc[RSV_R] = {n[N_ALLOC_CPU], n[N_ALLOC_MEM], n[N_ALLOC_EPH], n[N_SC_ALLOC0], n[N_SC_ALLOC1]};
+#pragma unroll
+    for (int k = 0; k < RSV_R; k++) {
+        if (k >= 3 && !((q.names >> k) & 1u)) continue;
+        const int64_t rk = rem ? rem[k] : 0;
+        if (q.preq[k] > alloc[k] - (v.pod_requested[k] - rk - v.r_allocated[k])) bad |= 1u << k;
+    }
+    return bad;
+}
+
+__device__ __forceinline__ uint32_t rsv_fits_reservation(const RsvPod& q, const RsvInfo& r) {
+    uint32_t bad = 0;
+    if (r.max_pods >= 0 && r.allocated_pods + 1 > r.max_pods) bad |= 1u << 5;
+#pragma unroll
+    for (int k = 0; k < RSV_R; k++) {
+        if (!((r.names >> k) & 1u)) continue;
+        if (!((q.names >> k) & 1u) || q.preq[k] == 0) continue;
+        const int64_t used = r.allocated[k] < 0 ? 0 : r.allocated[k];
+        const int64_t cap = r.allocatable[k] - r.reserved[k];
+        if (q.preq[k] <= cap - used) continue;
+        bad |= 1u << k;
+    }
+    return bad;
+}
+
+// fitsNodeAndReservation: true when the pod fits node + reservation r
+__device__ __forceinline__ bool rsv_fits_one(const RsvPod& q, const int64_t* __restrict__ n, const RsvView& v,
+                                             const RsvInfo& r, uint32_t& bn, uint32_t& br) {
+    int64_t rem[RSV_R];
+#pragma unroll
+    for (int k = 0; k < RSV_R; k++) {
+        const int64_t x = r.allocatable[k] - r.allocated[k] - r.reserved[k];
+        rem[k] = x < 0 ? 0 : x;
+    }
+    bn = rsv_fits_node(q, n, v, rem);
+    br = 0;
+    if (r.policy == KG_RSV_RESTRICTED) {
+        br = rsv_fits_reservation(q, r);
+        return bn == 0 && br == 0;
+    }
+    return bn == 0;
+}
+
+__device__ __forceinline__ uint32_t rsv_filter(const RsvPod& q, const int64_t* __restrict__ n, const RsvView* v,
+                                               const RsvInfo* __restrict__ infos) {
+    if (!v) return q.required ? KG_ST_RSV_AFFINITY : 0u;
+    uint32_t any_node = 0, any_resv = 0;
+    for (uint32_t t = 0; t < v->count; t++) {
+        const RsvInfo& r = infos[v->first + t];
+        if (!q.required && !(r.names & q.names)) continue;
+        uint32_t bn, br;
+        if (rsv_fits_one(q, n, *v, r, bn, br)) return 0;
+        any_node |= bn;
+        any_resv |= br;
+    }
+    if (q.required)
+        return ((any_resv != 0 || any_node == 0) ? KG_ST_RSV_RESERVATION : 0u) | (any_node ? KG_ST_RSV_NODE : 0u);
+    if (any_node) return KG_ST_RSV_NODE;
+    return rsv_fits_node(q, n, *v, nullptr) ? KG_ST_RSV_NODE : 0u;
+}
+
+__device__ __forceinline__ int64_t rsv_score_reservation(const RsvPod& q, const RsvInfo& r) {
+    int64_t w = 0, s = 0;
+#pragma unroll
+    for (int k = 0; k < RSV_R; k++) {
+        const int64_t cap = r.allocatable[k];
+        if (cap == 0) continue;
+        w++;
+        const int64_t req = q.preq[k] + r.allocated[k];
+        if (req <= cap) {
+            const int64_t m = k == 0 ? 1 : 1000;
+            s += (int64_t)(100ull * (uint64_t)(req * m)) / (cap * m);
+        }
+    }
+    if (r.max_pods > 0) w++;
+    return w <= 0 ? 0 : s / w;
+}
+
+// nominated reservation's ScoreReservation and the node's most-preferred order (0 = none)
+__device__ __forceinline__ int64_t rsv_nominate_score(const RsvPod& q, const int64_t* __restrict__ n, const RsvView& v,
+                                                      const RsvInfo* __restrict__ infos, int64_t& node_order) {
+    node_order = 0;
+    int64_t sel = INT64_MAX;
+    for (uint32_t t = 0; t < v.count; t++) {
+        const int64_t o = infos[v.first + t].order;
+        if (o != 0 && sel > o) {
+            sel = o;
+            node_order = o;
+        }
+    }
+    if (v.count == 0) return 0;
+    int nom = -1;
+    if (v.count == 1 && q.required) {
+        nom = 0;
+    } else {
+        uint32_t okm = 0, nc = 0;
+        int last = -1;
+        for (uint32_t t = 0; t < v.count; t++) {
+            const RsvInfo& r = infos[v.first + t];
+            if (r.allocate_once && r.allocated_pods > 0) continue;
+            if (!q.required && !(r.names & q.names)) continue;
+            uint32_t bn, br;
+            if (!rsv_fits_one(q, n, v, r, bn, br)) continue;
+            okm |= 1u << t;
+            nc++;
+            last = (int)t;
+        }
+        if (nc == 1) {
+            nom = last;
+        } else if (nc > 1) {
+            int64_t so = INT64_MAX;
+            for (uint32_t t = 0; t < v.count; t++) {
+                if (!((okm >> t) & 1u)) continue;
+                const int64_t o = infos[v.first + t].order;
+                if (o != 0 && so > o) {
+                    so = o;
+                    nom = (int)t;
+                }
+            }
+            if (nom < 0) {
+                int64_t best = -1;
+                for (uint32_t t = 0; t < v.count; t++) {
+                    if (!((okm >> t) & 1u)) continue;
+                    const int64_t sc = rsv_score_reservation(q, infos[v.first + t]);
+                    if (sc > best) {
+                        best = sc;
+                        nom = (int)t;
+                    }
+                }
+            }
+        }
+    }
+    return nom >= 0 ? rsv_score_reservation(q, infos[v.first + nom]) : 0;
+}
+
+// ---- one pair with every plugin ---------------------------------------------------------------------
+
+struct PairX {
+    uint32_t status;
+    int32_t zone;
+    int64_t s_nrf, s_la, s_numa, s_dev, s_rsv, order;
+};
+
+template <bool EXACT>
+__device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                               const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
+                                               uint32_t rec, const PodV& p, const PodX& x, uint32_t qst) {
+    PairX o;
+    o.status = 0;
+    o.zone = -1;
+    o.s_nrf = o.s_la = o.s_numa = o.s_dev = o.s_rsv = o.order = 0;
+    if (qst) {  // ElasticQuota PreFilter rejected the pod: no node is evaluated
+        o.status = qst;
+        return o;
+    }
+    const uint32_t flags = (uint32_t)n[N_FLAGS];
+    const RsvView* v = nullptr;
+    if ((c.plugins & KG_PLUGIN_RSV) && x.cls >= 0 && x.cls < RSV_MAX_CLASSES &&
+        (((uint64_t)n[N_RSV_CLASSES] >> x.cls) & 1ull))
+        v = find_view(e, x.cls, rec);
+    PairOut b;
+    if (v) {
+        Over ov;
+#pragma unroll
+        for (int k = 0; k < RSV_R; k++) ov.req[k] = v->req[k];
+        ov.nz_cpu = v->nz_cpu;
+        ov.nz_mem = v->nz_mem;
+        ov.num_pods = v->num_pods;
+        b = eval_pair<EXACT, true>(c, n, zr, p, &ov);
+        const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u;
+        if ((c.plugins & KG_PLUGIN_NUMA) && node_pol != KG_NUMA_NONE && !(p.flags & KG_POD_NUMA_SKIP))
+            b.status = (b.status & ~(uint32_t)KG_ST_NUMA_MASK) | KG_ST_UNSUPPORTED;  // NUMA restore: host path
+    } else {
+        b = eval_pair<EXACT, false>(c, n, zr, p);
+    }
+    uint32_t st = b.status;
+    int64_t dev_raw = 0;
+    if (c.plugins & KG_PLUGIN_DEV) {
+        st |= dev_eval(c, n, d, x, dev_raw);
+        if (x.dcount > 0) {
+            const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (p.flags >> 16) & 15u;
+            if (v || ((c.plugins & KG_PLUGIN_NUMA) && (node_pol != KG_NUMA_NONE || pod_pol != KG_NUMA_NONE)))
+                st |= KG_ST_UNSUPPORTED;  // device NUMA hints / device reservation restore: host path
+        }
+    }
+    RsvPod q;
+    if (c.plugins & KG_PLUGIN_RSV) {
+        q = rsv_pod(p);
+        st |= rsv_filter(q, n, v, e.infos);
+    }
+    o.status = st;
+    o.s_nrf = b.s_nrf;
+    o.s_la = b.s_la;
+    o.s_numa = (st & (KG_ST_NUMA_MASK | KG_ST_UNSUPPORTED)) ? 0 : b.s_numa;
+    if (st) return o;
+    o.zone = b.zone;
+    o.s_dev = dev_raw;
+    if (v) o.s_rsv = rsv_nominate_score(q, n, *v, e.infos, o.order);
+    return o;
+}
+
+// per-pod NormalizeScore inputs: max DeviceShare raw score, max nominated Reservation score, and the
+// preferred node key ((order + 2^31) << 32 | snapshot index, minimum; ~0 = none)
+constexpr uint64_t PREF_NONE = ~0ull;
+
+__device__ __forceinline__ uint64_t pref_key(int64_t order, uint32_t gidx) {
+    return ((uint64_t)(uint32_t)(order + 0x80000000ll) << 32) | gidx;
+}
+
+__device__ __forceinline__ int64_t norm100(int64_t s, int64_t mx) { return mx == 0 ? s : s * 100 / mx; }
+
+__device__ __forceinline__ int64_t total_ext(const KCfg& c, const PairX& o, uint32_t gidx, uint32_t dev_max,
+                                             uint32_t rsv_max, uint64_t pref) {
+    const bool has_pref = pref != PREF_NONE;
+    const int64_t rsv = (has_pref && (uint32_t)pref == gidx) ? 1000 : o.s_rsv;
+    const int64_t rmax = has_pref ? 1000 : (int64_t)rsv_max;
+    return (int64_t)c.w_nrf * o.s_nrf + (int64_t)c.w_la * o.s_la + (int64_t)c.w_numa * o.s_numa +
+           (int64_t)c.w_dev * norm100(o.s_dev, dev_max) + (int64_t)c.w_rsv * norm100(rsv, rmax);
+}
+
+}  // namespace kg

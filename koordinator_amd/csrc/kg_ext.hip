@@ -1,0 +1,407 @@
+// kg_ext.hip — CDNA4 (gfx950) kernels of the config-5 plugin set (DeviceShare, Reservation,
+// ElasticQuota on top of NodeResourcesFit / LoadAware / NodeNUMAResource), integer path.
+//
+// DeviceShare and Reservation normalise their scores by the per-pod maximum over the feasible nodes
+// (DefaultNormalizeScore, frameworkext/normalize_score.go:24-52) and Reservation gives its PreScore
+// preferredNode 1000 (reservation/scoring.go:113-121,191-198), so matrix mode runs in two passes:
+//   k_ext_stats   lane = pod (of the pods that carry a GPU request or a reservation class), wave walks
+//                 a chunk of node records: feasibility + raw DeviceShare score, nominated reservation
+//                 score and the node order -> per-pod max / min by atomics;
+//   k_ext_select  lane = pod, wave walks a chunk of records: weighted total with the normalised terms,
+//                 running top-K per lane -> per-(chunk, pod) partials (merged by k_merge).
+// Between the passes the multi-GPU path all-reduces the per-pod maxima over RCCL.
+// k_ext_replay   one pod per launch (lane = node record): applies the previous pod's Reserve in place
+//                (NodeInfo, LoadAware, NUMA zone, GPU minors, quota used), gates the next pod on its
+//                quota, evaluates it, and reduces per DeviceShare raw score bucket so that the next
+//                launch can normalise without another grid-wide pass.
+#include <hip/hip_runtime.h>
+
+#include "kg_ext.h"
+#include "kg_kernels.h"
+
+namespace kg {
+
+__device__ __forceinline__ uint64_t wmax_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(v, off, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int32_t wmax_i32(int32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+__device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) { return e.dev ? e.dev + rec : nullptr; }
+
+// ElasticQuota PreFilter of every pod against the batch-start quota state (matrix mode).
+__global__ __launch_bounds__(256) void k_ext_gate(PodsDev pods, uint32_t n_pods, ExtDev e, uint32_t plugins,
+                                                  uint32_t* __restrict__ qst) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_pods) return;
+    uint32_t s = 0;
+    if (plugins & KG_PLUGIN_QUOTA) {
+        const PodX x = load_podx(pods, j);
+        if (x.quota >= 0 && (uint32_t)x.quota < e.n_quotas)
+            s = quota_gate(e.qlim[x.quota], e.qstate[x.quota], load_pod(pods, j), x);
+    }
+    qst[j] = s;
+}
+
+// Verify: raw per-plugin results of every (pod, record) pair, [pod][snapshot index].
+template <bool EXACT>
+__global__ __launch_bounds__(256) void k_ext_verify_raw(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                        ExtDev e, PodsDev pods, uint32_t n_pods, uint32_t n_nodes, KCfg cfg,
+                                                        const uint32_t* __restrict__ qst, ExtVerifyDev o) {
+    const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= (size_t)n_pods * n_nodes) return;
+    const uint32_t j = (uint32_t)(x / n_nodes), rec = (uint32_t)(x % n_nodes);
+    const PodV p = load_pod(pods, j);
+    const PodX px = load_podx(pods, j);
+    const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, qst[j]);
+    const size_t y = (size_t)j * n_nodes + node_index(nodes[rec]);
+    o.status[y] = r.status;
+    o.s_nrf[y] = r.s_nrf;
+    o.s_la[y] = r.s_la;
+    o.s_numa[y] = r.s_numa;
+    o.s_dev[y] = r.s_dev;
+    o.s_rsv[y] = r.s_rsv;
+    o.order[y] = r.order;
+    o.zone[y] = (int8_t)r.zone;
+}
+
+// Verify: per pod, PreScore preferredNode + NormalizeScore maxima, then the weighted totals.
+__global__ __launch_bounds__(256) void k_ext_verify_fin(uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, KCfg cfg,
+                                                        ExtVerifyDev o) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_pods) return;
+    const size_t row = (size_t)j * n_nodes;
+    uint32_t dmax = 0, rmax = 0;
+    uint64_t pref = PREF_NONE;
+    for (uint32_t i = 0; i < n_nodes; i++) {
+        if (o.status[row + i]) continue;
+        dmax = max(dmax, (uint32_t)o.s_dev[row + i]);
+        rmax = max(rmax, (uint32_t)o.s_rsv[row + i]);
+        if (o.order[row + i] != 0) {
+            const uint64_t k = pref_key(o.order[row + i], index_base + i);
+            pref = k < pref ? k : pref;
+        }
+    }
+    for (uint32_t i = 0; i < n_nodes; i++) {
+        PairX r;
+        r.status = o.status[row + i];
+        if (r.status) {
+            o.total[row + i] = -1;
+            continue;
+        }
+        r.s_nrf = o.s_nrf[row + i];
+        r.s_la = o.s_la[row + i];
+        r.s_numa = o.s_numa[row + i];
+        r.s_dev = o.s_dev[row + i];
+        r.s_rsv = o.s_rsv[row + i];
+        o.total[row + i] = total_ext(cfg, r, index_base + i, dmax, rmax, pref);
+        if (pref != PREF_NONE && (uint32_t)pref == index_base + i) o.s_rsv[row + i] = 1000;
+    }
+}
+
+// Pass 1: per-pod NormalizeScore inputs over the feasible nodes of records [lo, hi) of chunk blockIdx.y.
+template <bool EXACT>
+__global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                   ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
+                                                   uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
+                                                   KCfg cfg, const uint32_t* __restrict__ qst, uint32_t* __restrict__ dev_max,
+                                                   uint32_t* __restrict__ rsv_max, uint64_t* __restrict__ pref) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = t < n_list;
+    const uint32_t j = live ? list[t] : 0;
+    const PodV p = load_pod(pods, j);
+    const PodX px = load_podx(pods, j);
+    const uint32_t q = live ? qst[j] : 1u;
+    const uint32_t lo = blockIdx.y * chunk, hi = min(n_nodes, lo + chunk);
+    uint32_t dmax = 0, rmax = 0;
+    uint64_t pk = PREF_NONE;
+    for (uint32_t rec = lo; rec < hi; rec++) {
+        const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        if (r.status) continue;
+        dmax = max(dmax, (uint32_t)r.s_dev);
+        rmax = max(rmax, (uint32_t)r.s_rsv);
+        if (r.order != 0) {
+            const uint64_t k = pref_key(r.order, index_base + node_index(nodes[rec]));
+            pk = k < pk ? k : pk;
+        }
+    }
+    if (!live) return;
+    if (dmax) atomicMax(dev_max + j, dmax);
+    if (rmax) atomicMax(rsv_max + j, rmax);
+    if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
+}
+
+template <int K>
+__device__ __forceinline__ void topk_ins(uint64_t (&top)[K], uint64_t key) {
+#pragma unroll
+    for (int t = 0; t < K; t++) {
+        const uint64_t cur = top[t];
+        const bool gt = key > cur;
+        top[t] = gt ? key : cur;
+        key = gt ? cur : key;
+    }
+}
+
+// Pass 2: weighted totals with the normalised DeviceShare / Reservation terms, top-K per (chunk, pod).
+template <int K, bool EXACT>
+__global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                    ExtDev e, PodsDev pods, uint32_t n_pods, uint32_t n_nodes,
+                                                    uint32_t chunk, uint32_t index_base, KCfg cfg,
+                                                    const uint32_t* __restrict__ qst, const uint32_t* __restrict__ dev_max,
+                                                    const uint32_t* __restrict__ rsv_max, const uint64_t* __restrict__ pref,
+                                                    uint64_t* __restrict__ partial) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = j < n_pods;
+    const uint32_t jj = live ? j : 0;
+    const PodV p = load_pod(pods, jj);
+    const PodX px = load_podx(pods, jj);
+    const uint32_t q = live ? qst[jj] : 1u;
+    const uint32_t dm = dev_max[jj], rm = rsv_max[jj];
+    const uint64_t pf = pref[jj];
+    uint64_t top[K];
+#pragma unroll
+    for (int t = 0; t < K; t++) top[t] = 0;
+    const uint32_t lo = blockIdx.y * chunk, hi = min(n_nodes, lo + chunk);
+    for (uint32_t rec = lo; rec < hi; rec++) {
+        const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const uint32_t g = index_base + node_index(nodes[rec]);
+        const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
+        topk_ins<K>(top, r.status ? 0ull : key);
+    }
+    if (live) {
+        uint64_t* dst = partial + ((size_t)blockIdx.y * n_pods + j) * K;
+#pragma unroll
+        for (int t = 0; t < K; t++) dst[t] = top[t];
+    }
+}
+
+// One replay step (see file header). buckets: [3][128] ring of per-DeviceShare-score best keys.
+template <bool EXACT>
+__global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
+                                                   DevRec* __restrict__ devs, ExtDev e, PodsDev pods, uint32_t n_pods,
+                                                   uint32_t n_nodes, uint32_t index_base, KCfg cfg,
+                                                   const uint32_t* __restrict__ step_base, uint32_t step_off,
+                                                   uint64_t* __restrict__ winners, uint32_t* __restrict__ minors,
+                                                   uint64_t* __restrict__ buckets, int8_t* __restrict__ zsel) {
+    const uint32_t step = (step_base ? *step_base : 0u) + step_off;
+    if (step > n_pods) return;  // uniform
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * 64u + lane;
+    const bool live = i < n_nodes;
+    const bool has_next = step < n_pods;
+    // winner of the previous step from its score buckets: M = highest DeviceShare raw score among the
+    // feasible nodes; key = (base + w_dev * 100 s / M) << 32 | index
+    uint64_t prev = 0;
+    if (step > 0) {
+        const uint64_t* B = buckets + (size_t)((step - 1) % 3) * 128;
+        const uint64_t b0 = B[lane], b1 = B[lane + 64];
+        const int32_t M = wmax_i32(max(b0 ? (int32_t)lane : -1, b1 ? (int32_t)lane + 64 : -1));
+        if (M >= 0) {
+            auto cand = [&](uint64_t b, int64_t s) -> uint64_t {
+                if (!b) return 0ull;
+                const int64_t tot = (int64_t)(b >> 32) + (int64_t)cfg.w_dev * norm100(s, M);
+                return ((uint64_t)tot << 32) | (b & 0xFFFFFFFFull);
+            };
+            const uint64_t c0 = cand(b0, lane), c1 = cand(b1, lane + 64);
+            prev = wmax_u64(c0 > c1 ? c0 : c1);
+        }
+    }
+    if (blockIdx.x == 0) {
+        uint64_t* Z = buckets + (size_t)((step + 1) % 3) * 128;  // last read at step - 1
+        Z[lane] = 0;
+        Z[lane + 64] = 0;
+        if (lane == 0 && step > 0) winners[step - 1] = prev;
+    }
+    // Reserve of pod step-1 on its winner
+    if (live && prev != 0ull) {
+        const uint32_t g = 0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull);
+        if (g == index_base + node_index(nodes[i])) {
+            const PodV q = load_pod(pods, step - 1);
+            const PodX qx = load_podx(pods, step - 1);
+            apply_assume(cfg, nodes[i].v, zones + i, q, zsel[i], 1);
+            if ((cfg.plugins & KG_PLUGIN_DEV) && qx.dcount > 0) {
+                const uint32_t mask = dev_choose(cfg, nodes[i].v, devs + i, qx);
+                dev_apply(devs + i, mask, qx, 1);
+                minors[step - 1] = mask;
+            }
+        }
+    }
+    // ElasticQuota: buffer (step-1)&1 holds the state after pods < step-1; buffer step&1 becomes the
+    // state after pods < step (block 0, nobody reads it during this launch)
+    uint32_t qst = 0;
+    PodV p = load_pod(pods, has_next ? step : 0);
+    PodX px = load_podx(pods, has_next ? step : 0);
+    if (cfg.plugins & KG_PLUGIN_QUOTA) {
+        const uint32_t nq = e.n_quotas;
+        const QuotaState* rd = e.qstate + (size_t)((step - 1) & 1u) * nq;
+        PodX x1;
+        PodV p1;
+        bool placed1 = false;
+        if (step > 0) {
+            p1 = load_pod(pods, step - 1);
+            x1 = load_podx(pods, step - 1);
+            placed1 = prev != 0ull;
+        }
+        if (has_next && px.quota >= 0 && (uint32_t)px.quota < nq) {
+            QuotaState S = rd[px.quota];
+            if (placed1 && x1.quota == px.quota) quota_add(S, p1, x1, 1);
+            qst = quota_gate(e.qlim[px.quota], S, p, px);
+        }
+        if (blockIdx.x == 0 && lane == 0) {
+            QuotaState* wr = e.qstate + (size_t)(step & 1u) * nq;
+            if (step > 1 && winners[step - 2] != 0ull) {
+                const PodV p2 = load_pod(pods, step - 2);
+                const PodX x2 = load_podx(pods, step - 2);
+                if (x2.quota >= 0 && (uint32_t)x2.quota < nq) quota_add(wr[x2.quota], p2, x2, 1);
+            }
+            if (placed1 && x1.quota >= 0 && (uint32_t)x1.quota < nq) quota_add(wr[x1.quota], p1, x1, 1);
+        }
+    }
+    if (!has_next) return;  // the final step only applies the last Reserve
+    uint64_t kb = 0;
+    int32_t s = 0;
+    if (live) {
+        const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, qst);
+        zsel[i] = (int8_t)r.zone;
+        if (!r.status) {
+            const int64_t base = (int64_t)cfg.w_nrf * r.s_nrf + (int64_t)cfg.w_la * r.s_la + (int64_t)cfg.w_numa * r.s_numa;
+            kb = ((uint64_t)base << 32) | (uint64_t)(0xFFFFFFFFu - (index_base + node_index(nodes[i])));
+            s = (int32_t)r.s_dev;
+        }
+    }
+    // per-score-bucket wave max, one atomic per distinct score in the wave
+    uint64_t* B = buckets + (size_t)(step % 3) * 128;
+    bool pending = kb != 0ull;
+    uint64_t m = __ballot(pending);
+    while (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        const int32_t sl = __shfl(s, leader, 64);
+        const bool mine = pending && s == sl;
+        const uint64_t v = wmax_u64(mine ? kb : 0ull);
+        if ((int)lane == leader) atomicMax((unsigned long long*)(B + sl), (unsigned long long)v);
+        pending = pending && !mine;
+        m = __ballot(pending);
+    }
+}
+
+// Reserve (sign +1: zone and minors chosen here) / Unreserve (sign -1: the given zone and minors).
+template <bool EXACT>
+__global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, DevRec* __restrict__ devs, ExtDev e,
+                             PodsDev pods, uint32_t pod, uint32_t rec, int32_t zone_in, uint32_t minors_in, int64_t sign,
+                             KCfg cfg, int32_t* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const PodV q = load_pod(pods, pod);
+    const PodX qx = load_podx(pods, pod);
+    int64_t* n = nodes[rec].v;
+    int32_t zone = zone_in;
+    uint32_t mask = minors_in;
+    if (sign > 0) {
+        const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, 0u);
+        zone = r.status ? -1 : r.zone;
+        mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, n, devs + rec, qx) : 0u;
+    }
+    apply_assume(cfg, n, zones + rec, q, zone, sign);
+    if ((cfg.plugins & KG_PLUGIN_DEV) && devs && qx.dcount > 0) dev_apply(devs + rec, mask, qx, sign);
+    if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
+        quota_add(e.qstate[qx.quota], q, qx, sign);
+        quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, sign);
+    }
+    if (out) {
+        out[0] = zone;
+        out[1] = (int32_t)mask;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+
+hipError_t launch_ext_gate(const PodsDev& pods, uint32_t n_pods, const ExtDev& e, uint32_t plugins, uint32_t* qst,
+                           hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    k_ext_gate<<<(n_pods + 255) / 256, 256, 0, s>>>(pods, n_pods, e, plugins, qst);
+    return hipGetLastError();
+}
+
+hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                             uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
+                             const uint32_t* qst, const ExtVerifyDev& o, hipStream_t s) {
+    const size_t pairs = (size_t)n_pods * n_nodes;
+    if (pairs == 0) return hipSuccess;
+    dim3 grid((unsigned)((pairs + 255) / 256));
+    if (exact)
+        k_ext_verify_raw<true><<<grid, 256, 0, s>>>(nodes, zones, e, pods, n_pods, n_nodes, cfg, qst, o);
+    else
+        k_ext_verify_raw<false><<<grid, 256, 0, s>>>(nodes, zones, e, pods, n_pods, n_nodes, cfg, qst, o);
+    k_ext_verify_fin<<<(n_pods + 255) / 256, 256, 0, s>>>(n_pods, n_nodes, index_base, cfg, o);
+    return hipGetLastError();
+}
+
+hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                            const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
+                            const KCfg& cfg, bool exact, const uint32_t* qst, uint32_t* dev_max, uint32_t* rsv_max,
+                            uint64_t* pref, hipStream_t s) {
+    if (n_list == 0 || n_nodes == 0) return hipSuccess;
+    dim3 grid((n_list + 255) / 256, (n_nodes + chunk - 1) / chunk);
+    if (exact)
+        k_ext_stats<true><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, chunk, index_base, cfg, qst,
+                                               dev_max, rsv_max, pref);
+    else
+        k_ext_stats<false><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, chunk, index_base, cfg, qst,
+                                                dev_max, rsv_max, pref);
+    return hipGetLastError();
+}
+
+hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                             uint32_t n_pods, uint32_t n_nodes, uint32_t chunk, uint32_t k, uint32_t index_base,
+                             const KCfg& cfg, bool exact, const uint32_t* qst, const uint32_t* dev_max,
+                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, hipStream_t s) {
+    if (n_pods == 0 || n_nodes == 0) return hipSuccess;
+    dim3 grid((n_pods + 255) / 256, (n_nodes + chunk - 1) / chunk);
+#define KG_EXT_SEL(KK, EX)                                                                                          \
+    k_ext_select<KK, EX><<<grid, 256, 0, s>>>(nodes, zones, e, pods, n_pods, n_nodes, chunk, index_base, cfg, qst, \
+                                              dev_max, rsv_max, pref, partial)
+    if (k == 1) {
+        if (exact) KG_EXT_SEL(1, true);
+        else KG_EXT_SEL(1, false);
+    } else {
+        if (exact) KG_EXT_SEL(KG_TOPK_MAX, true);
+        else KG_EXT_SEL(KG_TOPK_MAX, false);
+    }
+#undef KG_EXT_SEL
+    return hipGetLastError();
+}
+
+hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
+                                  uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
+                                  const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
+                                  uint64_t* buckets, int8_t* zsel, hipStream_t s) {
+    dim3 grid((n_nodes + 63) / 64), block(64);
+    if (exact)
+        k_ext_replay<true><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
+                                                  step_off, winners, minors, buckets, zsel);
+    else
+        k_ext_replay<false><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
+                                                   step_off, winners, minors, buckets, zsel);
+    return hipGetLastError();
+}
+
+hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
+                             uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
+                             bool exact, int32_t* out, hipStream_t s) {
+    if (exact)
+        k_ext_assume<true><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, pod, rec, zone, minors, sign, cfg, out);
+    else
+        k_ext_assume<false><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, pod, rec, zone, minors, sign, cfg, out);
+    return hipGetLastError();
+}
+
+}  // namespace kg

@@ -31,7 +31,35 @@ struct VerifyDev {
     int8_t* zone;
 };
 
+struct ExtVerifyDev {
+    uint32_t* status;
+    int64_t *s_nrf, *s_la, *s_numa, *s_dev, *s_rsv, *order, *total;
+    int8_t* zone;
+};
+
 hipError_t launch_select(const LaunchSelect& a, hipStream_t s);
+
+// config-5 plugin set (kg_ext.hip)
+hipError_t launch_ext_gate(const PodsDev& pods, uint32_t n_pods, const ExtDev& e, uint32_t plugins, uint32_t* qst,
+                           hipStream_t s);
+hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                             uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
+                             const uint32_t* qst, const ExtVerifyDev& o, hipStream_t s);
+hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                            const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
+                            const KCfg& cfg, bool exact, const uint32_t* qst, uint32_t* dev_max, uint32_t* rsv_max,
+                            uint64_t* pref, hipStream_t s);
+hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                             uint32_t n_pods, uint32_t n_nodes, uint32_t chunk, uint32_t k, uint32_t index_base,
+                             const KCfg& cfg, bool exact, const uint32_t* qst, const uint32_t* dev_max,
+                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, hipStream_t s);
+hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
+                                  uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
+                                  const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
+                                  uint64_t* buckets, int8_t* zsel, hipStream_t s);
+hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
+                             uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
+                             bool exact, int32_t* out, hipStream_t s);
 hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k, uint64_t* out,
                         hipStream_t s);
 hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k,

@@ -29,7 +29,9 @@ enum NodeSlot : int {
     N_LA_FCUT_NP0, N_LA_FCUT_NP1, N_LA_FCUT_PROD0, N_LA_FCUT_PROD1,
     N_LA_FBASE_NP0, N_LA_FBASE_NP1, N_LA_FBASE_PROD0, N_LA_FBASE_PROD1,
     N_LA_SBASE_NP0, N_LA_SBASE_NP1, N_LA_SBASE_PROD0, N_LA_SBASE_PROD1,
-    N_CPUSET, N_AMP_CPUSET, N_SPARE0, N_SPARE1,
+    N_CPUSET, N_AMP_CPUSET,
+    N_RSV_CLASSES,        // Reservation: bit c set when the node has a restore view for owner class c
+    N_DEV_MINORS,         // DeviceShare: GPU minors of the node's Device (-1: no Device object)
     N_INT_SLOTS,
     // ---- fast block [32, 64): read by the select kernel with wide scalar loads per node ----
     //  * N_FLAGS: low 32 bits device flags, high 32 bits the node's snapshot index (records are
@@ -217,6 +219,13 @@ KG_HD inline int node_class(const NodeRec& r) {
 
 // Pod batch (device pointers, SoA). flags: low 16 bits KG_POD_*, bits 16..19 pod NUMA policy.
 struct PodsDev {
+    // config-5 columns (nullptr unless the snapshot enables DeviceShare / Reservation / ElasticQuota)
+    const int64_t* dev_req;     // [pod][KG_DEV_R]
+    const uint32_t* dev_count;
+    const uint32_t* dev_keys;
+    const int32_t* quota;
+    const uint32_t* quota_keys;
+    const int32_t* rsv_class;
     const int64_t* req_cpu;
     const int64_t* req_mem;
     const int64_t* req_eph;
@@ -241,6 +250,56 @@ struct KCfg {
     int32_t la_wsum;   // Σ la_w + dominant weight — constant per profile
     int32_t numa_w_cpu, numa_w_mem, numa_hint_w_cpu, numa_hint_w_mem;
     float la_hw;       // 0.5 / la_wsum (0 when la_wsum is 0): fast-path weighted quotient
+    int32_t w_dev, w_rsv;
+    int32_t dev_w[3];  // DeviceShare LeastAllocated weights {gpu-core, gpu-memory-ratio, gpu-memory}
+};
+
+// ---- config-5 side tables (integer path) -----------------------------------------------------------
+constexpr int DEV_MINORS = 8, DEV_R = 3;
+// DeviceShare minors of one node record (side array in record order).
+struct alignas(64) DevRec {
+    int64_t total[DEV_R][DEV_MINORS];
+    int64_t free_[DEV_R][DEV_MINORS];
+};
+
+constexpr int QUOTA_R = 4;
+// ElasticQuota mutable state (double-buffered during replay) and static limits.
+struct alignas(16) QuotaState {
+    int64_t used[QUOTA_R], np_used[QUOTA_R];
+    uint32_t used_keys, np_keys;
+    uint64_t pad_;
+};
+struct alignas(16) QuotaLim {
+    int64_t limit[QUOTA_R], min[QUOTA_R];
+    uint32_t limit_keys, min_keys;
+    uint64_t pad_;
+};
+
+constexpr int RSV_R = 5, RSV_MAX_CLASSES = 64, RSV_MAX_PER_VIEW = 8;
+// Reservation restore view (kg_rsv_view with the node's record position).
+struct alignas(16) RsvView {
+    uint32_t rec, first, count, cls;
+    int64_t req[RSV_R];
+    int64_t nz_cpu, nz_mem, num_pods;
+    int64_t pod_requested[RSV_R];
+    int64_t r_allocated[RSV_R];
+};
+struct alignas(16) RsvInfo {
+    uint32_t policy, names, allocate_once, pad_;
+    int64_t order;
+    int64_t allocatable[RSV_R], allocated[RSV_R], reserved[RSV_R];
+    int64_t max_pods, allocated_pods;
+};
+
+// Device pointers of the config-5 tables of a snapshot (nullptr when the plugin is off).
+struct ExtDev {
+    const DevRec* dev;             // [record]
+    const QuotaLim* qlim;          // [quota]
+    QuotaState* qstate;            // [2][quota] (replay double buffer; outside replay both agree)
+    uint32_t n_quotas;
+    const RsvView* views;          // sorted by class, then record position
+    const RsvInfo* infos;
+    const uint32_t* cls_begin;     // [RSV_MAX_CLASSES + 1] view range per class
 };
 
 }  // namespace kg

@@ -62,6 +62,31 @@ struct kg_snap {
     uint32_t n0 = 0;               // records of class 0 (positions [0, n0))
     bool uploaded = false;
     bool weights_small = false;  // per-resource weights <= 2^12: float64 fast path allowed
+    // config-5 tables (KG_PLUGIN_DEV / RSV / QUOTA)
+    DevRec* d_dev = nullptr;       // [record]
+    std::vector<DevRec> h_dev;     // device order
+    QuotaLim* d_qlim = nullptr;
+    QuotaState* d_qstate = nullptr;  // [2][n_quotas]
+    uint32_t n_quotas = 0;
+    RsvView* d_views = nullptr;
+    RsvInfo* d_infos = nullptr;
+    uint32_t* d_cls_begin = nullptr;  // [RSV_MAX_CLASSES + 1]
+    uint32_t n_views = 0;
+    std::vector<kg_rsv_view> h_views;  // as uploaded (local snapshot indices)
+    std::vector<kg_rsv_info> h_infos;
+    std::vector<uint64_t> cls_mask;  // per snapshot index: classes with a view on the node
+    bool ext() const { return (cfg.plugins & KG_PLUGIN_EXT) != 0; }
+    ExtDev ext_dev() const {
+        ExtDev e{};
+        e.dev = d_dev;
+        e.qlim = d_qlim;
+        e.qstate = d_qstate;
+        e.n_quotas = n_quotas;
+        e.views = d_views;
+        e.infos = d_infos;
+        e.cls_begin = d_cls_begin;
+        return e;
+    }
 };
 
 struct kg_pods {
@@ -81,6 +106,20 @@ struct kg_pods {
     uint64_t* d_gather = nullptr;
     size_t gather_cap = 0;
     bool fast_ok = false;  // every value below FAST_LIMIT and no pod NUMA policy
+    // config-5 columns and scratch
+    int64_t* d_dev_req = nullptr;     // [cap][KG_DEV_R]
+    uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32): 5 x cap
+    uint32_t* d_stat_list = nullptr;  // pods carrying a GPU request or a reservation class
+    uint32_t n_stat = 0;
+    uint32_t* d_qst = nullptr;        // ElasticQuota PreFilter status per pod
+    uint32_t* d_dev_max = nullptr;    // [cap] pass-1 NormalizeScore maxima
+    uint32_t* d_rsv_max = nullptr;
+    uint64_t* d_pref = nullptr;
+    uint32_t* d_minors = nullptr;     // replay: GPU minors chosen per pod
+    uint64_t* d_buckets = nullptr;    // replay: [3][128] per-score best keys
+    int32_t* d_aout = nullptr;        // kg_assume_ext outputs
+    hipGraphExec_t xexec = nullptr;   // ext replay graph
+    std::vector<uint8_t> xkey;
     // replay graph (G steps) cached for the (snapshot buffers, batch size, configuration) it captured
     hipGraphExec_t rexec = nullptr;
     std::vector<uint8_t> rkey;
@@ -184,8 +223,19 @@ kg_status build_kcfg(kg_ctx* ctx, const kg_config* c, KCfg* k) {
                           c->numa_hint_w_cpu, c->numa_hint_w_mem};
     for (int64_t w : ws)
         if (!valid_weight(w)) return fail(ctx, KG_INVALID_ARG, "weight %lld outside [0, 2^20]", (long long)w);
-    if (c->plugins & ~(KG_PLUGIN_NRF | KG_PLUGIN_LA | KG_PLUGIN_NUMA))
+    if (c->plugins & ~(KG_PLUGIN_NRF | KG_PLUGIN_LA | KG_PLUGIN_NUMA | KG_PLUGIN_EXT))
         return fail(ctx, KG_UNSUPPORTED, "plugins mask 0x%x", c->plugins);
+    if (c->plugins & KG_PLUGIN_EXT) {
+        const int64_t xs[] = {c->weight_dev, c->weight_rsv, c->dev_w[0], c->dev_w[1], c->dev_w[2]};
+        for (int64_t w : xs)
+            if (!valid_weight(w)) return fail(ctx, KG_INVALID_ARG, "weight %lld outside [0, 2^20]", (long long)w);
+        // totals must stay below 2^31 for the packed selection key: Σ weight x 100 per plugin
+        const int64_t wsum = c->weight_nrf + c->weight_la + c->weight_numa + c->weight_dev + c->weight_rsv;
+        if (wsum * 100 >= (1ll << 31)) return fail(ctx, KG_INVALID_ARG, "score weights too large for the packed key");
+        k->w_dev = (c->plugins & KG_PLUGIN_DEV) ? (int32_t)c->weight_dev : 0;
+        k->w_rsv = (c->plugins & KG_PLUGIN_RSV) ? (int32_t)c->weight_rsv : 0;
+        for (int r = 0; r < DEV_R; r++) k->dev_w[r] = (int32_t)c->dev_w[r];
+    }
     k->plugins = c->plugins;
     k->la_score_enabled = c->la_score_enabled;
     k->la_score_prod = c->la_score_prod;
@@ -281,6 +331,9 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     const double ratio = s->cpu_amp_ratio ? s->cpu_amp_ratio[i] : 0.0;
     if (ratio > 1) f |= F_AMP;
     v[N_FLAGS] = f;
+    v[N_RSV_CLASSES] = 0;  // set by kg_snapshot_upload_reservations
+    v[N_DEV_MINORS] = s->dev_minors ? (int64_t)s->dev_minors[i] : -1;
+    if (v[N_DEV_MINORS] > DEV_MINORS) return fail(ctx, KG_UNSUPPORTED, "node %u: %lld GPU minors > %d", i, (long long)v[N_DEV_MINORS], DEV_MINORS);
     v[N_CPUSET] = COL(s->cpuset_alloc_milli, i);
     v[N_AMP_CPUSET] = amplify(v[N_CPUSET], ratio);
     v[N_RCP_CPU] = rcp_bits(v[N_ALLOC_CPU]);
@@ -326,6 +379,17 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     return KG_OK;
 }
 
+void build_dev(const kg_node_columns* s, uint32_t i, DevRec* d) {
+    std::memset(d, 0, sizeof(*d));
+    if (!s->dev_total || !s->dev_free) return;
+    for (int r = 0; r < DEV_R; r++)
+        for (int m = 0; m < DEV_MINORS; m++) {
+            const size_t x = ((size_t)i * DEV_R + r) * DEV_MINORS + m;
+            d->total[r][m] = s->dev_total[x];
+            d->free_[r][m] = s->dev_free[x];
+        }
+}
+
 bool force_exact() {
     static int v = -1;
     if (v < 0) {
@@ -361,9 +425,10 @@ void set_node_index(NodeRec& r, uint32_t i) {
 }
 
 // Place records (indexed by snapshot index) in device order: class 0 then class 1, each ascending.
-void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>& zrs) {
+void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>& zrs, std::vector<DevRec>* devs = nullptr) {
     const uint32_t n = s->n;
     s->pos.resize(n);
+    if (devs) s->h_dev.resize(n);
     uint32_t n0 = 0;
     for (uint32_t i = 0; i < n; i++) n0 += node_class(recs[i]) == 0;
     uint32_t a = 0, b = n0;
@@ -372,6 +437,7 @@ void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>&
         s->pos[i] = p;
         s->h_nodes[p] = recs[i];
         s->h_zones[p] = zrs[i];
+        if (devs) s->h_dev[p] = (*devs)[i];
     }
     s->n0 = n0;
 }
@@ -503,6 +569,13 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
         delete s;
         return fail(ctx, KG_OOM, "snapshot of %u nodes", n_nodes);
     }
+    if ((cfg->plugins & KG_PLUGIN_DEV) && hipMalloc(&s->d_dev, sizeof(DevRec) * std::max<uint32_t>(n_nodes, 1)) != hipSuccess) {
+        hipFree(s->d_nodes);
+        hipFree(s->d_zones);
+        delete s;
+        return fail(ctx, KG_OOM, "device tables of %u nodes", n_nodes);
+    }
+    s->cls_mask.assign(n_nodes, 0);
     *out = s;
     return KG_OK;
 }
@@ -513,15 +586,20 @@ kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
     std::lock_guard<std::mutex> g(ctx->mu);
     std::vector<NodeRec> recs(s->n);
     std::vector<ZoneRec> zrs(s->n);
+    const bool dev = s->d_dev != nullptr;
+    std::vector<DevRec> devs(dev ? s->n : 0);
     for (uint32_t i = 0; i < s->n; i++) {
         kg_status st = build_row(ctx, s->cfg, cols, i, &recs[i], &zrs[i]);
         if (st != KG_OK) return st;
         set_node_index(recs[i], i);
+        recs[i].v[N_RSV_CLASSES] = (int64_t)s->cls_mask[i];
+        if (dev) build_dev(cols, i, &devs[i]);
     }
-    place_records(s, recs, zrs);
+    place_records(s, recs, zrs, dev ? &devs : nullptr);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+    if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, s->h_dev.data(), sizeof(DevRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->uploaded = true;
@@ -536,33 +614,43 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     std::vector<NodeRec> recs(n);
     std::vector<ZoneRec> zrs(n);
+    const bool dev = s->d_dev != nullptr;
+    std::vector<DevRec> devs(dev ? n : 0);
     bool moved = false;  // a row changes storage class: the record groups are rebuilt
     for (uint32_t k = 0; k < n; k++) {
         if (rows[k] >= s->n) return fail(ctx, KG_INVALID_ARG, "row %u >= %u", rows[k], s->n);
         kg_status st = build_row(ctx, s->cfg, cols, k, &recs[k], &zrs[k]);
         if (st != KG_OK) return st;
         set_node_index(recs[k], rows[k]);
+        recs[k].v[N_RSV_CLASSES] = (int64_t)s->cls_mask[rows[k]];
+        if (dev) build_dev(cols, k, &devs[k]);
         moved |= node_class(recs[k]) != (s->pos[rows[k]] < s->n0 ? 0u : 1u);
     }
+    if (moved && s->n_views) return fail(ctx, KG_UNSUPPORTED, "row update moves a record while reservation views are uploaded");
     if (moved) {
         // device records carry Assume state: read them back, replace the rows, regroup, re-upload
         HIP_TRY(ctx, hipMemcpyAsync(s->h_nodes.data(), s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->h_zones.data(), s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
+        if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->h_dev.data(), s->d_dev, sizeof(DevRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         std::vector<NodeRec> all(s->n);
         std::vector<ZoneRec> allz(s->n);
+        std::vector<DevRec> alld(dev ? s->n : 0);
         for (uint32_t p = 0; p < s->n; p++) {
             const uint32_t i = node_index(s->h_nodes[p]);
             all[i] = s->h_nodes[p];
             allz[i] = s->h_zones[p];
+            if (dev) alld[i] = s->h_dev[p];
         }
         for (uint32_t k = 0; k < n; k++) {
             all[rows[k]] = recs[k];
             allz[rows[k]] = zrs[k];
+            if (dev) alld[rows[k]] = devs[k];
         }
-        place_records(s, all, allz);
+        place_records(s, all, allz, dev ? &alld : nullptr);
         HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+        if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, s->h_dev.data(), sizeof(DevRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
     } else {
         for (uint32_t k = 0; k < n; k++) {
             const uint32_t p = s->pos[rows[k]];
@@ -570,6 +658,10 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
             s->h_zones[p] = zrs[k];
             HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes + p, &s->h_nodes[p], sizeof(NodeRec), hipMemcpyHostToDevice, ctx->stream));
             HIP_TRY(ctx, hipMemcpyAsync(s->d_zones + p, &s->h_zones[p], sizeof(ZoneRec), hipMemcpyHostToDevice, ctx->stream));
+            if (dev) {
+                s->h_dev[p] = devs[k];
+                HIP_TRY(ctx, hipMemcpyAsync(s->d_dev + p, &s->h_dev[p], sizeof(DevRec), hipMemcpyHostToDevice, ctx->stream));
+            }
         }
     }
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
@@ -584,8 +676,10 @@ kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     std::vector<NodeRec> h(s->n);
     std::vector<ZoneRec> z(s->n);
+    std::vector<DevRec> dv(s->d_dev ? s->n : 0);
     HIP_TRY(ctx, hipMemcpyAsync(h.data(), s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(z.data(), s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
+    if (s->d_dev) HIP_TRY(ctx, hipMemcpyAsync(dv.data(), s->d_dev, sizeof(DevRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (uint32_t pp = 0; pp < s->n; pp++) {
         const int64_t* v = h[pp].v;
@@ -611,6 +705,9 @@ kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
             if (o->zone_cpu_used[zz]) o->zone_cpu_used[zz][i] = zr.cpu_used[zz];
             if (o->zone_mem_used[zz]) o->zone_mem_used[zz][i] = zr.mem_used[zz];
         }
+        if (o->dev_free && s->d_dev)
+            for (int r = 0; r < DEV_R; r++)
+                for (int m = 0; m < DEV_MINORS; m++) o->dev_free[((size_t)i * DEV_R + r) * DEV_MINORS + m] = dv[pp].free_[r][m];
     }
     return KG_OK;
 }
@@ -623,6 +720,12 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_zones);
     hipFree(s->d_big);
     hipFree(s->d_zsel);
+    hipFree(s->d_dev);
+    hipFree(s->d_qlim);
+    hipFree(s->d_qstate);
+    hipFree(s->d_views);
+    hipFree(s->d_infos);
+    hipFree(s->d_cls_begin);
     delete s;
     return KG_OK;
 }
@@ -639,13 +742,27 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_flags, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_keys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
               hipMalloc(&p->d_winners, sizeof(uint64_t) * (capacity + 1)) == hipSuccess &&
-              hipMalloc(&p->d_step, sizeof(uint32_t) * 64) == hipSuccess;
+              hipMalloc(&p->d_step, sizeof(uint32_t) * 64) == hipSuccess &&
+              hipMalloc(&p->d_dev_req, sizeof(int64_t) * DEV_R * capacity) == hipSuccess &&
+              hipMalloc(&p->d_xcols, sizeof(uint32_t) * 5 * capacity) == hipSuccess &&
+              hipMalloc(&p->d_stat_list, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_qst, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_dev_max, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_rsv_max, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_pref, sizeof(uint64_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_minors, sizeof(uint32_t) * (capacity + 1)) == hipSuccess &&
+              hipMalloc(&p->d_buckets, sizeof(uint64_t) * 3 * 128) == hipSuccess &&
+              hipMalloc(&p->d_aout, sizeof(int32_t) * 2) == hipSuccess;
     if (!ok) {
         hipFree(p->d_cols);
         hipFree(p->d_flags);
         hipFree(p->d_keys);
         hipFree(p->d_winners);
         hipFree(p->d_step);
+        for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst,
+                        (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors,
+                        (void*)p->d_buckets, (void*)p->d_aout})
+            hipFree(b);
         delete p;
         return fail(ctx, KG_OOM, "pod batch of %u", capacity);
     }
@@ -660,6 +777,12 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
     p->dev.la_est0 = c + 7 * (size_t)capacity;
     p->dev.la_est1 = c + 8 * (size_t)capacity;
     p->dev.flags = p->d_flags;
+    p->dev.dev_req = p->d_dev_req;
+    p->dev.dev_count = p->d_xcols;
+    p->dev.dev_keys = p->d_xcols + (size_t)capacity;
+    p->dev.quota = (const int32_t*)(p->d_xcols + 2 * (size_t)capacity);
+    p->dev.quota_keys = p->d_xcols + 3 * (size_t)capacity;
+    p->dev.rsv_class = (const int32_t*)(p->d_xcols + 4 * (size_t)capacity);
     *out = p;
     return KG_OK;
 }
@@ -687,7 +810,36 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         fast &= pol == KG_NUMA_NONE;
     }
     p->fast_ok = fast;
+    // config-5 columns (absent columns: no GPU request, no quota, no reservation class)
+    std::vector<int64_t> dreq((size_t)DEV_R * std::max<uint32_t>(n, 1), 0);
+    std::vector<uint32_t> xc((size_t)5 * std::max<uint32_t>(n, 1), 0);
+    std::vector<uint32_t> stat;
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t cnt = cols->dev_count ? cols->dev_count[j] : 0u;
+        const uint32_t keys = cols->dev_keys ? cols->dev_keys[j] : 0u;
+        for (int r = 0; r < DEV_R; r++) {
+            const int64_t v = cols->dev_req ? cols->dev_req[(size_t)j * DEV_R + r] : 0;
+            if (v < 0) return fail(ctx, KG_INVALID_ARG, "pod %u: negative GPU request", j);
+            dreq[(size_t)j * DEV_R + r] = v;
+        }
+        const int32_t q = cols->quota ? cols->quota[j] : -1;
+        const int32_t cls = cols->rsv_class ? cols->rsv_class[j] : -1;
+        if (cls >= RSV_MAX_CLASSES) return fail(ctx, KG_UNSUPPORTED, "pod %u: reservation class %d >= %d", j, cls, RSV_MAX_CLASSES);
+        xc[j] = cnt;
+        xc[(size_t)n + j] = keys;
+        xc[2 * (size_t)n + j] = (uint32_t)q;
+        xc[3 * (size_t)n + j] = cols->quota_keys ? cols->quota_keys[j] : 0u;
+        xc[4 * (size_t)n + j] = (uint32_t)cls;
+        if (cnt > 0 || cls >= 0) stat.push_back(j);
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemcpyAsync(p->d_dev_req, dreq.data(), sizeof(int64_t) * DEV_R * n, hipMemcpyHostToDevice, ctx->stream));
+    for (int c = 0; c < 5; c++)
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_xcols + (size_t)c * p->cap, xc.data() + (size_t)c * n, sizeof(uint32_t) * n,
+                                    hipMemcpyHostToDevice, ctx->stream));
+    if (!stat.empty())
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_stat_list, stat.data(), sizeof(uint32_t) * stat.size(), hipMemcpyHostToDevice, ctx->stream));
+    p->n_stat = (uint32_t)stat.size();
     for (int c = 0; c < 9; c++)
         HIP_TRY(ctx, hipMemcpyAsync(p->d_cols + (size_t)c * p->cap, h.data() + (size_t)c * n, sizeof(int64_t) * n,
                                     hipMemcpyHostToDevice, ctx->stream));
@@ -708,7 +860,11 @@ kg_status kg_pods_destroy(kg_pods* p) {
     hipFree(p->d_step);
     hipFree(p->d_partial);
     hipFree(p->d_gather);
+    for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst, (void*)p->d_dev_max,
+                    (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout})
+        hipFree(b);
     if (p->rexec) hipGraphExecDestroy(p->rexec);
+    if (p->xexec) hipGraphExecDestroy(p->xexec);
     delete p;
     return KG_OK;
 }
@@ -720,12 +876,62 @@ static kg_status check_pair(kg_snap* s, kg_pods* p) {
     return KG_OK;
 }
 
+static kg_status check_ext(kg_snap* s) {
+    kg_ctx* ctx = s->ctx;
+    if ((s->cfg.plugins & KG_PLUGIN_QUOTA) && s->n_quotas == 0 && !s->d_qstate)
+        return fail(ctx, KG_INVALID_ARG, "KG_PLUGIN_QUOTA without kg_snapshot_upload_quotas");
+    return KG_OK;
+}
+
+static kg_status ext_verify(kg_snap* s, kg_pods* p, kg_verify_out* out) {
+    kg_ctx* ctx = s->ctx;
+    kg_status st0 = check_ext(s);
+    if (st0 != KG_OK) return st0;
+    const size_t pairs = (size_t)p->n * s->n;
+    if (pairs == 0) return KG_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    ExtVerifyDev d{};
+    void* buf = nullptr;
+    HIP_TRY(ctx, hipMalloc(&buf, pairs * (4 + 8 * 7 + 1)));
+    char* b = (char*)buf;
+    d.s_nrf = (int64_t*)b;
+    d.s_la = d.s_nrf + pairs;
+    d.s_numa = d.s_la + pairs;
+    d.s_dev = d.s_numa + pairs;
+    d.s_rsv = d.s_dev + pairs;
+    d.order = d.s_rsv + pairs;
+    d.total = d.order + pairs;
+    d.status = (uint32_t*)(d.total + pairs);
+    d.zone = (int8_t*)(d.status + pairs);
+    const ExtDev e = s->ext_dev();
+    hipError_t err = launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, ctx->stream);
+    if (err == hipSuccess)
+        err = launch_ext_verify(s->d_nodes, s->d_zones, e, p->dev, p->n, s->n, s->base, s->kcfg, force_exact(), p->d_qst,
+                                d, ctx->stream);
+    if (err == hipSuccess) {
+        struct {
+            void* dst;
+            const void* src;
+            size_t sz;
+        } cp[] = {{out->status, d.status, 4},     {out->score_nrf, d.s_nrf, 8}, {out->score_la, d.s_la, 8},
+                  {out->score_numa, d.s_numa, 8}, {out->total, d.total, 8},     {out->numa_zone, d.zone, 1},
+                  {out->score_dev, d.s_dev, 8},   {out->score_rsv, d.s_rsv, 8}};
+        for (auto& c : cp)
+            if (c.dst && err == hipSuccess) err = hipMemcpyAsync(c.dst, c.src, c.sz * pairs, hipMemcpyDeviceToHost, ctx->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(ctx->stream);
+    }
+    hipFree(buf);
+    HIP_TRY(ctx, err);
+    return KG_OK;
+}
+
 kg_status kg_eval_verify(kg_snap* s, kg_pods* p, kg_verify_out* out) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
     if (!out) return KG_INVALID_ARG;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
+    if (s->ext()) return ext_verify(s, p, out);
     const size_t pairs = (size_t)p->n * s->n;
     if (pairs == 0) return KG_OK;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -752,8 +958,58 @@ kg_status kg_eval_verify(kg_snap* s, kg_pods* p, kg_verify_out* out) {
             if (c.dst && e == hipSuccess) e = hipMemcpyAsync(c.dst, c.src, c.sz * pairs, hipMemcpyDeviceToHost, ctx->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     }
+    if (e == hipSuccess && out->score_dev) std::memset(out->score_dev, 0, 8 * pairs);
+    if (e == hipSuccess && out->score_rsv) std::memset(out->score_rsv, 0, 8 * pairs);
     hipFree(buf);
     HIP_TRY(ctx, e);
+    return KG_OK;
+}
+
+static kg_status ensure_partial(kg_pods* p, size_t need) {
+    kg_ctx* ctx = p->ctx;
+    if (need <= p->partial_cap) return KG_OK;
+    if (p->d_partial) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(p->d_partial));
+        p->d_partial = nullptr;
+    }
+    HIP_TRY(ctx, hipMalloc(&p->d_partial, sizeof(uint64_t) * need));
+    p->partial_cap = need;
+    return KG_OK;
+}
+
+// config-5 matrix mode, pass 1: quota gate + per-pod NormalizeScore inputs of this shard
+static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
+    kg_ctx* ctx = s->ctx;
+    const ExtDev e = s->ext_dev();
+    HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_dev_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_pref, 0xFF, sizeof(uint64_t) * p->n, ctx->stream));
+    if (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) {
+        const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(p->n_stat, 1));
+        HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list, p->n_stat, s->n, chunk, s->base,
+                                      s->kcfg, force_exact(), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, ctx->stream));
+    }
+    return KG_OK;
+}
+
+// config-5 matrix mode, pass 2: totals with the normalised terms -> per-pod top-k in d_out
+static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out) {
+    kg_ctx* ctx = s->ctx;
+    const uint32_t chunk = select_chunk(s->n, p->n);
+    const uint32_t n_parts = (s->n + chunk - 1) / chunk;
+    kg_status st = ensure_partial(p, (size_t)std::max<uint32_t>(n_parts, 1) * p->n * kk);
+    if (st != KG_OK) return st;
+    hipEvent_t e0, e1;
+    st = record_begin(ctx, &e0, &e1);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, p->n, s->n, chunk, kk, s->base, s->kcfg,
+                                   force_exact(), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, p->d_partial,
+                                   ctx->stream));
+    st = record_end(ctx, e0, e1);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, launch_merge(p->d_partial, n_parts, p->n, kk, d_out, ctx->stream));
     return KG_OK;
 }
 
@@ -761,6 +1017,21 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     kg_ctx* ctx = s->ctx;
     if (k == 0 || k > (uint32_t)KG_TOPK_MAX) return fail(ctx, KG_INVALID_ARG, "k=%u outside [1, %d]", k, KG_TOPK_MAX);
     const uint32_t kk = k == 1 ? 1 : KG_TOPK_MAX;
+    if (s->ext()) {
+        kg_status st0 = check_ext(s);
+        if (st0 != KG_OK) return st0;
+        HIP_TRY(ctx, hipSetDevice(ctx->device));
+        p->k_last = k;
+        p->kk_last = kk;
+        if (p->n == 0) return KG_OK;
+        if (s->n == 0) {
+            HIP_TRY(ctx, hipMemsetAsync(d_out, 0, sizeof(uint64_t) * kk * p->n, ctx->stream));
+            return KG_OK;
+        }
+        st0 = ext_stats_local(s, p);
+        if (st0 != KG_OK) return st0;
+        return ext_select_local(s, p, kk, d_out);
+    }
     LaunchSelect a{};
     a.nodes = s->d_nodes;
     a.zones = s->d_zones;
@@ -880,15 +1151,49 @@ kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact) {
     p->rkey = std::move(key);
     return KG_OK;
 }
+
+// config-5 replay steps (DeviceShare minors, ElasticQuota used, NormalizeScore via score buckets)
+kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact) {
+    kg_ctx* ctx = s->ctx;
+    std::vector<uint8_t> key = replay_key(s, p, exact);
+    auto put = [&key](const void* x, size_t n) { key.insert(key.end(), (const uint8_t*)x, (const uint8_t*)x + n); };
+    put(&s->d_dev, sizeof(s->d_dev));
+    put(&s->d_qstate, sizeof(s->d_qstate));
+    put(&s->n_quotas, sizeof(s->n_quotas));
+    if (p->xexec && key == p->xkey) return KG_OK;
+    if (p->xexec) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        hipGraphExecDestroy(p->xexec);
+        p->xexec = nullptr;
+    }
+    hipGraph_t graph = nullptr;
+    const ExtDev e = s->ext_dev();
+    HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t err = hipSuccess;
+    for (uint32_t t = 0; t < REPLAY_G && err == hipSuccess; t++)
+        err = launch_ext_replay_step(s->d_nodes, s->d_zones, s->d_dev, e, p->dev, p->n, s->n, s->base, s->kcfg, exact,
+                                     p->d_step, t, p->d_winners, p->d_minors, p->d_buckets, s->d_zsel, ctx->stream);
+    if (err == hipSuccess) err = launch_bump(p->d_step, REPLAY_G, ctx->stream);
+    hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    if (err == hipSuccess) err = ec;
+    if (err == hipSuccess) err = hipGraphInstantiate(&p->xexec, graph, nullptr, nullptr, 0);
+    if (graph) hipGraphDestroy(graph);
+    HIP_TRY(ctx, err);
+    p->xkey = std::move(key);
+    return KG_OK;
+}
 }  // namespace
 
 extern "C" {
+
+static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total);
 
 kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
+    if (s->ext()) return ext_replay(s, p, out_node, out_total);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint32_t n = p->n;
     const bool exact = force_exact();
@@ -937,6 +1242,235 @@ kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
+static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total) {
+    kg_ctx* ctx = s->ctx;
+    if (s->cfg.plugins & KG_PLUGIN_RSV)
+        return fail(ctx, KG_UNSUPPORTED, "replay with Reservation views (their restore changes with every placement)");
+    kg_status st = check_ext(s);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint32_t n = p->n;
+    const bool exact = force_exact();
+    st = ext_replay_graph(s, p, exact);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_minors, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_buckets, 0, sizeof(uint64_t) * 3 * 128, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
+    hipEvent_t e0, e1;
+    st = record_begin(ctx, &e0, &e1);
+    if (st != KG_OK) return st;
+    for (uint32_t done = 0; done <= n; done += REPLAY_G) HIP_TRY(ctx, hipGraphLaunch(p->xexec, ctx->stream));
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
+    st = record_end(ctx, e0, e1);
+    if (st != KG_OK) return st;
+    if ((s->cfg.plugins & KG_PLUGIN_QUOTA) && s->n_quotas) {
+        // the final state sits in buffer n & 1; make both buffers agree again
+        const size_t qb = sizeof(QuotaState) * s->n_quotas;
+        QuotaState* fin = s->d_qstate + (size_t)(n & 1u) * s->n_quotas;
+        QuotaState* other = s->d_qstate + (size_t)((n & 1u) ^ 1u) * s->n_quotas;
+        HIP_TRY(ctx, hipMemcpyAsync(other, fin, qb, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    std::vector<uint64_t> w(std::max<uint32_t>(n, 1));
+    HIP_TRY(ctx, hipMemcpyAsync(w.data(), p->d_winners, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t j = 0; j < n; j++) {
+        if (out_node) out_node[j] = kg_key_node(w[j]);
+        if (out_total) out_total[j] = kg_key_total(w[j]);
+    }
+    return KG_OK;
+}
+
+kg_status kg_replay_minors(kg_pods* p, uint32_t* out) {
+    if (!p || !out) return KG_INVALID_ARG;
+    kg_ctx* ctx = p->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (p->n) HIP_TRY(ctx, hipMemcpyAsync(out, p->d_minors, sizeof(uint32_t) * p->n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
+static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone, uint32_t minors,
+                            int64_t sign, int32_t* out_zone, uint32_t* out_minors) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
+    st = check_ext(s);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone, minors,
+                                   sign, s->kcfg, force_exact(), p->d_aout, ctx->stream));
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
+    int32_t o[2] = {-1, 0};
+    HIP_TRY(ctx, hipMemcpyAsync(o, p->d_aout, sizeof(o), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (out_zone) *out_zone = o[0];
+    if (out_minors) *out_minors = (uint32_t)o[1];
+    return KG_OK;
+}
+
+kg_status kg_assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t* out_zone, uint32_t* out_minors) {
+    return assume_ext(s, p, pod, node, -1, 0, 1, out_zone, out_minors);
+}
+
+kg_status kg_forget_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone, uint32_t minors) {
+    return assume_ext(s, p, pod, node, zone, minors, -1, nullptr, nullptr);
+}
+
+kg_status kg_snapshot_upload_quotas(kg_snap* s, const kg_quota_columns* c, uint32_t nq) {
+    if (!s || (!c && nq)) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<QuotaLim> lim(std::max<uint32_t>(nq, 1));
+    std::vector<QuotaState> qs(2 * (size_t)std::max<uint32_t>(nq, 1));
+    for (uint32_t q = 0; q < nq; q++) {
+        QuotaLim& L = lim[q];
+        QuotaState& S = qs[q];
+        std::memset(&L, 0, sizeof(L));
+        std::memset(&S, 0, sizeof(S));
+        for (int r = 0; r < QUOTA_R; r++) {
+            const size_t x = (size_t)q * QUOTA_R + r;
+            L.limit[r] = c->used_limit ? c->used_limit[x] : 0;
+            L.min[r] = c->min ? c->min[x] : 0;
+            S.used[r] = c->used ? c->used[x] : 0;
+            S.np_used[r] = c->np_used ? c->np_used[x] : 0;
+        }
+        L.limit_keys = c->limit_keys ? c->limit_keys[q] : 0u;
+        L.min_keys = c->min_keys ? c->min_keys[q] : 0u;
+        S.used_keys = c->used_keys ? c->used_keys[q] : 0u;
+        S.np_keys = c->np_used_keys ? c->np_used_keys[q] : 0u;
+        qs[nq + q] = S;
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    hipFree(s->d_qlim);
+    hipFree(s->d_qstate);
+    s->d_qlim = nullptr;
+    s->d_qstate = nullptr;
+    HIP_TRY(ctx, hipMalloc(&s->d_qlim, sizeof(QuotaLim) * lim.size()));
+    HIP_TRY(ctx, hipMalloc(&s->d_qstate, sizeof(QuotaState) * qs.size()));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_qlim, lim.data(), sizeof(QuotaLim) * lim.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_qstate, qs.data(), sizeof(QuotaState) * qs.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    s->n_quotas = nq;
+    return KG_OK;
+}
+
+kg_status kg_snapshot_read_quotas(kg_snap* s, int64_t* used, uint32_t* used_keys, int64_t* np_used, uint32_t* np_keys) {
+    if (!s) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!s->n_quotas) return KG_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::vector<QuotaState> qs(s->n_quotas);
+    HIP_TRY(ctx, hipMemcpyAsync(qs.data(), s->d_qstate, sizeof(QuotaState) * s->n_quotas, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t q = 0; q < s->n_quotas; q++) {
+        for (int r = 0; r < QUOTA_R; r++) {
+            if (used) used[(size_t)q * QUOTA_R + r] = qs[q].used[r];
+            if (np_used) np_used[(size_t)q * QUOTA_R + r] = qs[q].np_used[r];
+        }
+        if (used_keys) used_keys[q] = qs[q].used_keys;
+        if (np_keys) np_keys[q] = qs[q].np_keys;
+    }
+    return KG_OK;
+}
+
+kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, uint32_t nv, const kg_rsv_info* infos,
+                                          uint32_t ni) {
+    if (!s || (!views && nv) || (!infos && ni)) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
+    // views sorted by (class, record position); node class masks
+    std::vector<uint32_t> order(nv);
+    std::vector<uint64_t> mask(s->n, 0);
+    for (uint32_t v = 0; v < nv; v++) {
+        const kg_rsv_view& x = views[v];
+        if (x.node >= s->n) return fail(ctx, KG_INVALID_ARG, "view %u: node %u >= %u", v, x.node, s->n);
+        if (x.cls >= (uint32_t)RSV_MAX_CLASSES) return fail(ctx, KG_UNSUPPORTED, "view %u: class %u >= %d", v, x.cls, RSV_MAX_CLASSES);
+        if (x.count > (uint32_t)RSV_MAX_PER_VIEW || (uint64_t)x.first + x.count > ni)
+            return fail(ctx, KG_INVALID_ARG, "view %u: reservations [%u, %u+%u) invalid", v, x.first, x.first, x.count);
+        if ((mask[x.node] >> x.cls) & 1ull) return fail(ctx, KG_INVALID_ARG, "view %u: duplicate (class %u, node %u)", v, x.cls, x.node);
+        mask[x.node] |= 1ull << x.cls;
+        order[v] = v;
+    }
+    for (uint32_t t = 0; t < ni; t++) {
+        const int64_t o = infos[t].order;
+        if (o <= -(1ll << 31) || o >= (1ll << 31)) return fail(ctx, KG_INVALID_ARG, "reservation %u: order outside int32", t);
+    }
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        if (views[a].cls != views[b].cls) return views[a].cls < views[b].cls;
+        return s->pos[views[a].node] < s->pos[views[b].node];
+    });
+    std::vector<RsvView> dv(std::max<uint32_t>(nv, 1));
+    std::vector<uint32_t> cb(RSV_MAX_CLASSES + 1, 0);
+    for (uint32_t t = 0; t < nv; t++) {
+        const kg_rsv_view& x = views[order[t]];
+        RsvView& d = dv[t];
+        std::memset(&d, 0, sizeof(d));
+        d.rec = s->pos[x.node];
+        d.first = x.first;
+        d.count = x.count;
+        d.cls = x.cls;
+        for (int k = 0; k < RSV_R; k++) {
+            d.req[k] = x.req[k];
+            d.pod_requested[k] = x.pod_requested[k];
+            d.r_allocated[k] = x.r_allocated[k];
+        }
+        d.nz_cpu = x.nz_cpu;
+        d.nz_mem = x.nz_mem;
+        d.num_pods = x.num_pods;
+        cb[x.cls + 1]++;
+    }
+    for (int c = 0; c < RSV_MAX_CLASSES; c++) cb[c + 1] += cb[c];
+    std::vector<RsvInfo> di(std::max<uint32_t>(ni, 1));
+    for (uint32_t t = 0; t < ni; t++) {
+        const kg_rsv_info& x = infos[t];
+        RsvInfo& d = di[t];
+        std::memset(&d, 0, sizeof(d));
+        d.policy = x.policy;
+        d.names = x.names;
+        d.allocate_once = x.allocate_once;
+        d.order = x.order;
+        for (int k = 0; k < RSV_R; k++) {
+            d.allocatable[k] = x.allocatable[k];
+            d.allocated[k] = x.allocated[k];
+            d.reserved[k] = x.reserved[k];
+        }
+        d.max_pods = x.max_pods;
+        d.allocated_pods = x.allocated_pods;
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (void* b : {(void*)s->d_views, (void*)s->d_infos, (void*)s->d_cls_begin}) hipFree(b);
+    s->d_views = nullptr;
+    s->d_infos = nullptr;
+    s->d_cls_begin = nullptr;
+    HIP_TRY(ctx, hipMalloc(&s->d_views, sizeof(RsvView) * dv.size()));
+    HIP_TRY(ctx, hipMalloc(&s->d_infos, sizeof(RsvInfo) * di.size()));
+    HIP_TRY(ctx, hipMalloc(&s->d_cls_begin, sizeof(uint32_t) * cb.size()));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_views, dv.data(), sizeof(RsvView) * dv.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_infos, di.data(), sizeof(RsvInfo) * di.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_cls_begin, cb.data(), sizeof(uint32_t) * cb.size(), hipMemcpyHostToDevice, ctx->stream));
+    // class masks into slot N_RSV_CLASSES of every record (a strided 8-byte column copy)
+    s->cls_mask = mask;
+    std::vector<int64_t> col(s->n);
+    for (uint32_t i = 0; i < s->n; i++) {
+        col[s->pos[i]] = (int64_t)mask[i];
+        s->h_nodes[s->pos[i]].v[N_RSV_CLASSES] = (int64_t)mask[i];
+    }
+    if (s->n)
+        HIP_TRY(ctx, hipMemcpy2DAsync(&s->d_nodes[0].v[N_RSV_CLASSES], sizeof(NodeRec), col.data(), sizeof(int64_t),
+                                      sizeof(int64_t), s->n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    s->n_views = nv;
     return KG_OK;
 }
 
@@ -1013,7 +1547,25 @@ kg_status kg_shard_select(kg_snap* s, kg_pods* p, uint64_t* out_keys) {
         p->gather_cap = need;
     }
     uint64_t* local = p->d_gather + (size_t)n * ctx->world;  // this shard's per-pod best key
-    st = select_local(s, p, 1, local);
+    if (s->ext()) {
+        // NormalizeScore maxima and the Reservation preferred node are global over all shards: one
+        // all-reduce per statistic between the two passes (a real exchange step)
+        st = check_ext(s);
+        if (st != KG_OK) return st;
+        p->k_last = p->kk_last = 1;
+        if (n == 0) return KG_OK;
+        st = ext_stats_local(s, p);
+        if (st != KG_OK) return st;
+        NCCL_TRY(ctx, ncclAllReduce(p->d_dev_max, p->d_dev_max, n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
+        NCCL_TRY(ctx, ncclAllReduce(p->d_rsv_max, p->d_rsv_max, n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
+        NCCL_TRY(ctx, ncclAllReduce(p->d_pref, p->d_pref, n, ncclUint64, ncclMin, ctx->comm, ctx->stream));
+        if (s->n == 0)
+            HIP_TRY(ctx, hipMemsetAsync(local, 0, sizeof(uint64_t) * n, ctx->stream));
+        else
+            st = ext_select_local(s, p, 1, local);
+    } else {
+        st = select_local(s, p, 1, local);
+    }
     if (st != KG_OK) return st;
     // exchange per-shard best keys (8 B per pod per shard) and run the same global selectHost
     NCCL_TRY(ctx, ncclAllGather(local, p->d_gather, n, ncclUint64, ctx->comm, ctx->stream));

@@ -98,6 +98,18 @@ def lib():
     L.kg_key_total.restype = i64
     L.kg_merge_keys.argtypes = [P(u64), u32, u32, u32, P(u64)]
     L.kg_merge_keys.restype = st
+    L.kg_snapshot_upload_quotas.argtypes = [vp, P(abi.KgQuotaColumns), u32]
+    L.kg_snapshot_upload_quotas.restype = st
+    L.kg_snapshot_read_quotas.argtypes = [vp, P(i64), P(u32), P(i64), P(u32)]
+    L.kg_snapshot_read_quotas.restype = st
+    L.kg_snapshot_upload_reservations.argtypes = [vp, P(abi.KgRsvView), u32, P(abi.KgRsvInfo), u32]
+    L.kg_snapshot_upload_reservations.restype = st
+    L.kg_assume_ext.argtypes = [vp, vp, u32, u32, P(i32), P(u32)]
+    L.kg_assume_ext.restype = st
+    L.kg_forget_ext.argtypes = [vp, vp, u32, u32, i32, u32]
+    L.kg_forget_ext.restype = st
+    L.kg_replay_minors.argtypes = [vp, P(u32)]
+    L.kg_replay_minors.restype = st
     if L.kg_abi_version() != abi.KG_ABI_VERSION:
         raise ImportError(f"libkoordgpu ABI {L.kg_abi_version()} != {abi.KG_ABI_VERSION}")
     _lib = L
@@ -199,6 +211,30 @@ class Snapshot:
         self.ctx.check(self.ctx.L.kg_snapshot_read_state(self.h, C.byref(s)), "kg_snapshot_read_state")
         return t
 
+    def upload_quotas(self, quotas: abi.Table):
+        self.n_quotas = len(quotas["used"])
+        qc = abi.quota_columns(quotas)
+        self.ctx.check(self.ctx.L.kg_snapshot_upload_quotas(self.h, C.byref(qc), self.n_quotas),
+                       "kg_snapshot_upload_quotas")
+
+    def read_quotas(self):
+        nq = getattr(self, "n_quotas", 0)
+        used = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
+        npu = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
+        uk = np.zeros(max(nq, 1), np.uint32)
+        nk = np.zeros(max(nq, 1), np.uint32)
+        P = C.POINTER
+        self.ctx.check(self.ctx.L.kg_snapshot_read_quotas(self.h, used.ctypes.data_as(P(C.c_int64)),
+                                                          uk.ctypes.data_as(P(C.c_uint32)),
+                                                          npu.ctypes.data_as(P(C.c_int64)),
+                                                          nk.ctypes.data_as(P(C.c_uint32))), "kg_snapshot_read_quotas")
+        return used[:nq], uk[:nq], npu[:nq], nk[:nq]
+
+    def upload_reservations(self, rsv: abi.Reservations):
+        self.ctx.check(self.ctx.L.kg_snapshot_upload_reservations(
+            self.h, C.cast(rsv.views, C.POINTER(abi.KgRsvView)), rsv.n_views,
+            C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos), "kg_snapshot_upload_reservations")
+
     def close(self):
         if getattr(self, "h", None) and getattr(self.ctx, "h", None):
             self.ctx.L.kg_snapshot_destroy(self.h)
@@ -278,6 +314,22 @@ def assume(snap: Snapshot, pods: PodBatch, pod: int, node: int):
 
 def forget(snap: Snapshot, pods: PodBatch, pod: int, node: int, zone: int):
     snap.ctx.check(snap.ctx.L.kg_forget(snap.h, pods.h, pod, node, zone), "kg_forget")
+
+
+def replay_minors(pods: PodBatch) -> np.ndarray:
+    out = np.zeros(pods.n, np.uint32)
+    pods.ctx.check(pods.ctx.L.kg_replay_minors(pods.h, out.ctypes.data_as(C.POINTER(C.c_uint32))), "kg_replay_minors")
+    return out
+
+
+def assume_ext(snap: Snapshot, pods: PodBatch, pod: int, node: int):
+    zone, minors = C.c_int32(), C.c_uint32()
+    snap.ctx.check(snap.ctx.L.kg_assume_ext(snap.h, pods.h, pod, node, C.byref(zone), C.byref(minors)), "kg_assume_ext")
+    return zone.value, minors.value
+
+
+def forget_ext(snap: Snapshot, pods: PodBatch, pod: int, node: int, zone: int, minors: int):
+    snap.ctx.check(snap.ctx.L.kg_forget_ext(snap.h, pods.h, pod, node, zone, minors), "kg_forget_ext")
 
 
 def shard_select(snap: Snapshot, pods: PodBatch, download: bool = True) -> Optional[np.ndarray]:

@@ -1170,12 +1170,30 @@ static int64_t rsv_nominate_score(const rsv_ctx* x, int64_t* node_order) {
 
 /* ---- one pod against every node --------------------------------------------------------------- */
 
-/* view index per node for one class: built per call (views are few). */
-static const kg_rsv_view* find_view(const kgo_ext* e, int32_t cls, uint32_t i) {
-    if (!e || cls < 0) return NULL;
+/* (class, node) -> view lookup table, built once per call: vidx[cls * nn + node] = view or -1. */
+typedef struct view_index {
+    int32_t* v;
+    uint32_t nn, ncls;
+} view_index;
+
+static void view_index_build(view_index* x, const kgo_ext* e, uint32_t nn) {
+    x->v = NULL;
+    x->nn = nn;
+    x->ncls = 0;
+    if (!e || !e->views) return;
     for (uint32_t v = 0; v < e->n_views; v++)
-        if (e->views[v].node == i && e->views[v].cls == (uint32_t)cls) return &e->views[v];
-    return NULL;
+        if (e->views[v].cls + 1 > x->ncls) x->ncls = e->views[v].cls + 1;
+    if (!x->ncls) return;
+    x->v = (int32_t*)malloc(sizeof(int32_t) * (size_t)x->ncls * (nn ? nn : 1));
+    for (size_t t = 0; t < (size_t)x->ncls * nn; t++) x->v[t] = -1;
+    for (uint32_t v = 0; v < e->n_views; v++)
+        if (e->views[v].node < nn) x->v[(size_t)e->views[v].cls * nn + e->views[v].node] = (int32_t)v;
+}
+
+static const kg_rsv_view* find_view(const view_index* x, const kgo_ext* e, int32_t cls, uint32_t i) {
+    if (!x || !x->v || cls < 0 || (uint32_t)cls >= x->ncls) return NULL;
+    int32_t v = x->v[(size_t)cls * x->nn + i];
+    return v < 0 ? NULL : &e->views[v];
 }
 
 static int64_t normalize(int64_t s, int64_t max) { return max == 0 ? s : s * MAX_NODE_SCORE / max; }
@@ -1187,7 +1205,7 @@ typedef struct ext_row {
 } ext_row;
 
 static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t nn, const kg_pod_columns* p,
-                         uint32_t j, const kgo_ext* e, const kgo_quota_state* q, ext_row* o) {
+                         uint32_t j, const kgo_ext* e, const view_index* vx, const kgo_quota_state* q, ext_row* o) {
     uint32_t qst = (c->plugins & KG_PLUGIN_QUOTA) ? quota_gate(q, p, j) : 0;
     const int32_t cls = (c->plugins & KG_PLUGIN_RSV) && p->rsv_class ? p->rsv_class[j] : -1;
     const int gpu_pod = (c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0;
@@ -1199,7 +1217,7 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
             o->st[i] = qst;
             continue;
         }
-        const kg_rsv_view* v = (c->plugins & KG_PLUGIN_RSV) ? find_view(e, cls, i) : NULL;
+        const kg_rsv_view* v = (c->plugins & KG_PLUGIN_RSV) ? find_view(vx, e, cls, i) : NULL;
         kgo_over ov, *ovp = NULL;
         if (v) {
             for (int k = 0; k < KG_RSV_R; k++) ov.req[k] = v->req[k];
@@ -1221,7 +1239,11 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
         }
         int64_t dev_raw = 0;
         if (c->plugins & KG_PLUGIN_DEV) st |= dev_eval(c, n, i, p, j, &dev_raw);
-        if (gpu_pod && v) st |= KG_ST_UNSUPPORTED; /* DeviceShare reservation restore: host path */
+        /* GPU pods on reservation views (device reservation restore) or under a NUMA policy (DeviceShare
+         * joins the NUMA hint merge, topology_hint.go): host path */
+        if (gpu_pod && (v || ((c->plugins & KG_PLUGIN_NUMA) &&
+                              (n->numa_policy[i] != KG_NUMA_NONE || p->numa_policy[j] != KG_NUMA_NONE))))
+            st |= KG_ST_UNSUPPORTED;
         rsv_ctx x;
         if (c->plugins & KG_PLUGIN_RSV) {
             rsv_ctx_init(&x, n, i, v, e ? e->infos : NULL, p, j);
@@ -1286,8 +1308,10 @@ int kgo_ext_verify(const kg_config* c, const kg_node_columns* n, uint32_t nn, co
     ext_buf b;
     if (ext_buf_new(&b, nn)) return -1;
     kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    view_index vx;
+    view_index_build(&vx, e, nn);
     for (uint32_t j = 0; j < np; j++) {
-        ext_eval_pod(c, n, nn, p, j, e, q, &b.r);
+        ext_eval_pod(c, n, nn, p, j, e, &vx, q, &b.r);
         for (uint32_t i = 0; i < nn; i++) {
             size_t x = (size_t)j * nn + i;
             if (out->status) out->status[x] = b.r.st[i];
@@ -1301,6 +1325,7 @@ int kgo_ext_verify(const kg_config* c, const kg_node_columns* n, uint32_t nn, co
         }
     }
     quota_state_free(q);
+    free(vx.v);
     free(b.mem);
     return 0;
 }
@@ -1310,13 +1335,16 @@ int kgo_ext_select(const kg_config* c, const kg_node_columns* n, uint32_t nn, ui
     ext_buf b;
     if (ext_buf_new(&b, nn)) return -1;
     kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    view_index vx;
+    view_index_build(&vx, e, nn);
     for (uint32_t j = 0; j < np; j++) {
         uint64_t* top = keys + (size_t)j * k;
         memset(top, 0, sizeof(uint64_t) * k);
-        ext_eval_pod(c, n, nn, p, j, e, q, &b.r);
+        ext_eval_pod(c, n, nn, p, j, e, &vx, q, &b.r);
         for (uint32_t i = 0; i < nn; i++)
             if (!b.r.st[i]) topk_insert(top, k, make_key(b.r.total[i], base + i));
     }
+    free(vx.v);
     quota_state_free(q);
     free(b.mem);
     return 0;
@@ -1335,7 +1363,7 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
     if (ext_buf_new(&b, st->n)) return -1;
     kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
     for (uint32_t j = 0; j < np; j++) {
-        ext_eval_pod(c, &v, st->n, p, j, e, q, &b.r);
+        ext_eval_pod(c, &v, st->n, p, j, e, NULL, q, &b.r);
         uint64_t best = 0;
         int32_t best_zone = -1;
         for (uint32_t i = 0; i < st->n; i++) {

@@ -1,0 +1,166 @@
+"""Config-5 parity of the HIP engine (through the C ABI) with the CPU oracle: DeviceShare GPU fit /
+score / Reserve, Reservation restore / filter / nominate / score, ElasticQuota gate / Reserve, on top
+of NodeResourcesFit + LoadAware + NodeNUMAResource.
+
+Bar: bit-exact — filter status bits, int64 per-plugin raw scores, weighted totals after NormalizeScore,
+selected hosts (deterministic tie-break), replay placements, GPU minors and final device / quota state.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+from koordinator_amd import abi, engine, synth
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("status", "score_nrf", "score_la", "score_numa", "score_dev", "score_rsv", "total", "numa_zone")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = engine.Context(0)
+    yield c
+    c.close()
+
+
+def assert_equal(got, ref, what=""):
+    for name in FIELDS:
+        a, b = getattr(got, name), getattr(ref, name)
+        if not np.array_equal(a, b):
+            bad = np.argwhere(a != b)
+            j, i = bad[0]
+            raise AssertionError(f"{what}: {name} differs at {len(bad)} pairs, first pod {j} node {i}: "
+                                 f"gpu={a[j, i]} oracle={b[j, i]}")
+
+
+def make(ctx, kc, nodes, pods, quotas, rsv):
+    snap = engine.Snapshot(ctx, kc, nodes)
+    if kc.plugins & abi.KG_PLUGIN_QUOTA:
+        snap.upload_quotas(quotas)
+    if kc.plugins & abi.KG_PLUGIN_RSV:
+        snap.upload_reservations(rsv)
+    return snap, engine.PodBatch(ctx, pods)
+
+
+SUBSETS = {
+    "all": abi.KG_PLUGIN_NRF | abi.KG_PLUGIN_LA | abi.KG_PLUGIN_NUMA | abi.KG_PLUGIN_EXT,
+    "dev": abi.KG_PLUGIN_NRF | abi.KG_PLUGIN_DEV,
+    "rsv": abi.KG_PLUGIN_NRF | abi.KG_PLUGIN_LA | abi.KG_PLUGIN_RSV,
+    "quota": abi.KG_PLUGIN_NRF | abi.KG_PLUGIN_QUOTA,
+    "dev_quota_numa": abi.KG_PLUGIN_NRF | abi.KG_PLUGIN_LA | abi.KG_PLUGIN_NUMA | abi.KG_PLUGIN_DEV | abi.KG_PLUGIN_QUOTA,
+}
+
+
+@pytest.mark.parametrize("subset", list(SUBSETS))
+@pytest.mark.parametrize("seed,n_nodes,n_pods,rsv_frac", [(11, 1200, 192, 0.05), (12, 600, 256, 0.4)])
+def test_ext_verify(ctx, subset, seed, n_nodes, n_pods, rsv_frac):
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(n_nodes, n_pods, seed_config=seed, rsv_frac=rsv_frac)
+    kc = cfg.kg_config()
+    kc.plugins = SUBSETS[subset]
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_verify(snap, batch)
+    ref = oracle_lib.ext_verify(kc, nodes, pods, quotas if kc.plugins & abi.KG_PLUGIN_QUOTA else None,
+                                rsv if kc.plugins & abi.KG_PLUGIN_RSV else None)
+    assert_equal(got, ref, subset)
+    # the workload exercises every plugin's outcomes
+    st = ref.status
+    if kc.plugins & abi.KG_PLUGIN_DEV:
+        assert (st & abi.KG_ST_DEV_INSUFFICIENT).any() and (ref.score_dev > 0).any()
+    if kc.plugins & abi.KG_PLUGIN_RSV:
+        assert (ref.score_rsv > 0).any() and (st & abi.KG_ST_RSV_AFFINITY).any()
+    if kc.plugins & abi.KG_PLUGIN_QUOTA:
+        assert (st & abi.KG_ST_QUOTA).any()
+    assert (st == 0).any()
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_ext_select(ctx, k):
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(2500, 300, seed_config=21, rsv_frac=0.2)
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_select(snap, batch, k)
+    want = oracle_lib.ext_select(kc, nodes, pods, k, 0, quotas, rsv)
+    assert np.array_equal(got, want)
+    assert (want[:, 0] == 0).any() and (want[:, 0] != 0).any()
+
+
+def test_ext_select_preferred_reservation_wins(ctx):
+    """Reservation weight 5000 with the preferred (ordered) reservation node normalised to 100."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(800, 200, seed_config=31, rsv_frac=0.5)
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_select(snap, batch, 1)[:, 0]
+    want = oracle_lib.ext_select(kc, nodes, pods, 1, 0, quotas, rsv)[:, 0]
+    assert np.array_equal(got, want)
+    tot = abi.key_total(want)
+    assert (tot >= 5000 * 100).any()  # some pods land on their preferred reservation node
+
+
+def test_ext_replay(ctx):
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(1500, 3000, seed_config=41)
+    kc = cfg.kg_config()
+    kc.plugins &= ~abi.KG_PLUGIN_RSV
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    node, total = engine.replay(snap, batch)
+    minors = engine.replay_minors(batch)
+    ost = oracle_lib.OracleState(kc, nodes)
+    onode, ototal, ominors, oused, onp = ost.ext_replay(pods, quotas)
+    assert np.array_equal(node, onode)
+    assert np.array_equal(total, ototal)
+    assert np.array_equal(minors, ominors)
+    state = snap.read_state()
+    assert np.array_equal(state["dev_free"], ost.dev_free())
+    want = ost.table()
+    for k in ("req_cpu", "req_mem", "num_pods", "nz_cpu", "nz_mem"):
+        assert np.array_equal(state[k], want[k]), k
+    used, _, npu, _ = snap.read_quotas()
+    assert np.array_equal(used, oused) and np.array_equal(npu, onp)
+    assert (node < 0).any() and (minors != 0).any()
+
+
+def test_ext_replay_rejects_reservations(ctx):
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(300, 20, seed_config=42)
+    snap, batch = make(ctx, cfg.kg_config(), nodes, pods, quotas, rsv)
+    with pytest.raises(engine.Unsupported):
+        engine.replay(snap, batch)
+
+
+def test_ext_assume_forget_roundtrip(ctx):
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(400, 64, seed_config=43)
+    kc = cfg.kg_config()
+    kc.plugins &= ~abi.KG_PLUGIN_RSV
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    before = snap.read_state()
+    qb = snap.read_quotas()
+    keys = engine.eval_select(snap, batch, 1)[:, 0]
+    gpu = np.nonzero((pods["dev_count"] > 0) & (keys != 0))[0][:4]
+    assert len(gpu) > 0
+    done = []
+    for j in gpu:
+        i = int(abi.key_node(keys[j]))
+        zone, minors = engine.assume_ext(snap, batch, int(j), i)
+        assert bin(minors).count("1") == int(pods["dev_count"][j])
+        done.append((int(j), i, zone, minors))
+    mid = snap.read_state()
+    assert not np.array_equal(mid["dev_free"], before["dev_free"])
+    for j, i, zone, minors in reversed(done):
+        engine.forget_ext(snap, batch, j, i, zone, minors)
+    after = snap.read_state()
+    for k in before:
+        assert np.array_equal(before[k], after[k]), k
+    qa = snap.read_quotas()
+    for a, b in zip(qb, qa):
+        assert np.array_equal(a, b)
+
+
+def test_config5_full_size_sampled(ctx):
+    """Config 5 at 100k nodes x 10k pods: select on the device, a pod sample re-checked on the oracle."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(100_000, 10_000)
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    keys = engine.eval_select(snap, batch, 1)[:, 0]
+    idx = np.random.default_rng(5).choice(10_000, 24, replace=False)
+    sample = abi.take(pods, idx)
+    want = oracle_lib.ext_select(kc, nodes, sample, 1, 0, quotas, rsv)[:, 0]
+    assert np.array_equal(keys[idx], want)
+    assert (keys != 0).mean() > 0.5

@@ -30,13 +30,22 @@ def test_library_exports_every_header_symbol():
     assert L.kg_abi_version() == abi.KG_ABI_VERSION
 
 
-def test_struct_layouts_match_header():
-    # pointer-per-column structs: sizes follow from the field lists of include/koordgpu.h
-    ptr = C.sizeof(C.c_void_p)
-    n_node_ptrs = 10 + 2 * abi.KG_NSCALAR + 1 + 8 * abi.KG_LA_R + 4 + 4 * abi.KG_MAX_ZONES
-    assert C.sizeof(abi.KgNodeColumns) == n_node_ptrs * ptr
-    assert C.sizeof(abi.KgPodColumns) == (7 + abi.KG_LA_R + 2) * ptr
-    assert C.sizeof(abi.KgVerifyOut) == 6 * ptr
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors have the C sizes of include/koordgpu.h (compiled with gcc here)."""
+    import subprocess
+    names = ["kg_config", "kg_node_columns", "kg_node_state", "kg_pod_columns", "kg_verify_out",
+             "kg_quota_columns", "kg_rsv_view", "kg_rsv_info"]
+    src = tmp_path / "sz.c"
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "koordgpu.h")
+    src.write_text(f'#include "{hdr}"\n#include <stdio.h>\nint main(void){{' +
+                   "".join(f'printf("%zu\\n", sizeof({n}));' for n in names) + "return 0;}\n")
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", str(src), "-o", str(exe)])
+    sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    mirrors = [abi.KgConfig, abi.KgNodeColumns, abi.KgNodeState, abi.KgPodColumns, abi.KgVerifyOut,
+               abi.KgQuotaColumns, abi.KgRsvView, abi.KgRsvInfo]
+    for n, c_size, m in zip(names, sizes, mirrors):
+        assert C.sizeof(m) == c_size, n
 
 
 def test_keys_host_helpers():
