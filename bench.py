@@ -26,8 +26,12 @@ from koordinator_amd import abi, engine, synth  # noqa: E402
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak B/s (MI355X_MICROARCH.md, chip-level parameters)
 # Algorithmic bytes per (pod, node) eval, SURVEY.md §8d (scan model, node row read once per eval):
 # NodeResourcesFit 120 B + LoadAware 52 B + NodeNUMAResource 4 B + 0.2 x 64 B zone table = 188.8 B.
-B_EVAL = {1: 172.0, 2: 188.8, 4: 188.8}
+B_EVAL = {1: 172.0, 2: 188.8, 4: 188.8,
+          # config 5: + DeviceShare 384 B x 30% GPU pods + Reservation 4 B node flag (308 B)
+          5: 308.0}
 METRIC = "Filter+Score pod-node evals/sec"
+PLUGINS = {1: "+LoadAware", 2: "+LoadAware+NodeNUMAResource", 4: "+LoadAware+NodeNUMAResource",
+           5: "+LoadAware+NodeNUMAResource+DeviceShare+Reservation+ElasticQuota"}
 
 
 def parse():
@@ -35,9 +39,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4],
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4, 5],
                     help="2: 10k nodes per GPU x 10k pods (weak scaling, default); 4: 100k nodes split over "
-                         "the GPUs x 10k pods (strong scaling); 1: the 1k x 500 CPU-harness case")
+                         "the GPUs x 10k pods (strong scaling); 5: config 4 + DeviceShare / Reservation / "
+                         "ElasticQuota; 1: the 1k x 500 CPU-harness case")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-replay", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
@@ -78,6 +83,25 @@ def cpu_baseline(cfg, nodes, pods, target_s):
             "sample": f"{n} pods x {n_nodes} nodes ({n * n_nodes} evals) in {dt:.2f} s; oracle/kg_oracle.c "
                       f"kgo_select_parallel: per pod parallel Filter then parallel Score over nodes, "
                       f"{workers} workers, chunked like pkg/util/parallelize/parallelism.go:29-49"}
+
+
+def cpu_baseline_ext(kc, nodes, pods, quotas, rsv, target_s):
+    """Config 5: the oracle's restatement (one thread) on a bounded pod sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib  # test infrastructure: the CPU baseline leg only
+
+    n_nodes = abi.table_len(nodes)
+    probe = 4
+    t0 = time.perf_counter()
+    oracle_lib.ext_select(kc, nodes, abi.take(pods, np.arange(probe)), 1, 0, quotas, rsv)
+    dt = max(time.perf_counter() - t0, 1e-6)
+    n = int(min(abi.table_len(pods), max(probe, target_s / (dt / probe))))
+    t0 = time.perf_counter()
+    oracle_lib.ext_select(kc, nodes, abi.take(pods, np.arange(n)), 1, 0, quotas, rsv)
+    dt = time.perf_counter() - t0
+    return {"value": n * n_nodes / dt, "unit": "evals/s", "cores": 1, "kind": "port",
+            "sample": f"{n} pods x {n_nodes} nodes ({n * n_nodes} evals) in {dt:.2f} s; oracle/kg_oracle.c "
+                      f"kgo_ext_select (all six plugins, NormalizeScore, selectHost), one thread"}
 
 
 def replay_rate(ctx, cfg, with_cpu):
@@ -124,12 +148,18 @@ def main():
 
         dist.init_process_group("gloo")
     ctx = engine.Context(local)
-    cfg, nodes, pods = synth.cluster(a.config)
-    if a.config == 4:
+    quotas = rsv = None
+    if a.config == 5:
+        cfg, nodes, pods, quotas, rsv = synth.cluster5(100_000, 10_000)
+    else:
+        cfg, nodes, pods = synth.cluster(a.config)
+    if a.config in (4, 5):
         # one 100k-node cluster, contiguous shard per rank (strong scaling)
         bounds = np.linspace(0, abi.table_len(nodes), world + 1).astype(np.int64)
         base = int(bounds[rank])
         nodes = abi.take(nodes, np.arange(bounds[rank], bounds[rank + 1]))
+        if rsv is not None:
+            rsv = rsv.shard(int(bounds[rank]), int(bounds[rank + 1]))
         n_local = abi.table_len(nodes)
         n_total = int(bounds[-1])
     else:
@@ -145,6 +175,10 @@ def main():
         ctx.shard_init(uid[0], rank, world)
     kc = cfg.kg_config()
     snap = engine.Snapshot(ctx, kc, nodes, index_base=base)
+    if quotas is not None:
+        snap.upload_quotas(quotas)
+    if rsv is not None:
+        snap.upload_reservations(rsv)
     batch = engine.PodBatch(ctx, pods)
     n_pods = batch.n
 
@@ -196,25 +230,30 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if a.config == 4 else "weak",
+        "scaling": "strong" if a.config in (4, 5) else "weak",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (PCG64 seed 0x6B6F6F7264, SURVEY.md §8d distributions)",
         "config": {"workload": f"config{a.config}: {n_local} nodes/GPU x {n_pods} pods, Filter+Score+selectHost "
-                               f"(NodeResourcesFit{'+LoadAware' if a.config == 1 else '+LoadAware+NodeNUMAResource'})",
+                               f"(NodeResourcesFit{PLUGINS[a.config]})",
                    "nodes_per_gpu": n_local, "nodes_total": n_total, "pods": n_pods,
                    "parallelism": f"node-shard x{world}" + (" + RCCL all-gather of per-pod best keys" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK) if achieved else None,
-                     "traffic": load_traffic(), "kernel": "k_select", "kernel_avg_ms": avg_kernel_s * 1e3,
+                     "traffic": load_traffic() if a.config != 5 else None,
+                     "kernel": "k_select" if a.config != 5 else "k_ext_select", "kernel_avg_ms": avg_kernel_s * 1e3,
                      "bytes_per_eval": B_EVAL[a.config], "evals_per_launch": n_pods * n_local},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
-        if not a.no_replay:
-            out["replay"] = replay_rate(ctx, cfg, not a.no_cpu_baseline)
-        if not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cfg, nodes, pods, a.cpu_seconds)
+        if a.config == 5:
+            if not a.no_cpu_baseline:
+                out["cpu_baseline"] = cpu_baseline_ext(kc, nodes, pods, quotas, rsv, a.cpu_seconds)
+        else:
+            if not a.no_replay:
+                out["replay"] = replay_rate(ctx, cfg, not a.no_cpu_baseline)
+            if not a.no_cpu_baseline:
+                out["cpu_baseline"] = cpu_baseline(cfg, nodes, pods, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -404,6 +404,18 @@ class Reservations:
     def view_list(self):
         return [self.views[x] for x in range(self.n_views)]
 
+    def shard(self, lo: int, hi: int) -> "Reservations":
+        """Views of nodes [lo, hi) re-indexed to the shard (matched reservations are shared)."""
+        r = Reservations([], [])
+        keep = [self.views[x] for x in range(self.n_views) if lo <= self.views[x].node < hi]
+        r.views = (KgRsvView * max(1, len(keep)))()
+        for x, v in enumerate(keep):
+            C.pointer(r.views[x])[0] = v
+            r.views[x].node = v.node - lo
+        r.n_views = len(keep)
+        r.infos, r.n_infos = self.infos, self.n_infos
+        return r
+
 
 class VerifyResult:
     """Host buffers of a verify-mode evaluation, [n_pods][n_nodes]."""

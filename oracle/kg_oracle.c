@@ -1258,27 +1258,49 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
         o->dev[i] = dev_raw;
         if ((c->plugins & KG_PLUGIN_RSV) && v) o->rsv[i] = rsv_nominate_score(&x, &o->order[i]);
     }
-    if (qst) return;
-    /* PreScore preferredNode (reservation/scoring.go:113-121) and NormalizeScore maxima over the
-     * feasible nodes (DefaultNormalizeScore, frameworkext/normalize_score.go:24-52) */
-    int64_t dev_max = 0, rsv_max = 0, pref_order = INT64_MAX;
-    int64_t pref = -1;
+}
+
+/* PreScore preferredNode (reservation/scoring.go:113-121: smallest non-zero order among the feasible
+ * nodes, first in node order) and the NormalizeScore maxima (DefaultNormalizeScore,
+ * frameworkext/normalize_score.go:24-52) over this pod's feasible nodes. pref: (order + 2^31) << 32 |
+ * global node index, UINT64_MAX = none; the Reservation maximum excludes the preferred node's 1000. */
+static void ext_pod_stats(const ext_row* o, uint32_t nn, uint32_t base, int64_t* dev_max, int64_t* rsv_max,
+                          uint64_t* pref) {
+    *dev_max = 0;
+    *rsv_max = 0;
+    *pref = UINT64_MAX;
     for (uint32_t i = 0; i < nn; i++) {
         if (o->st[i]) continue;
-        if (o->dev[i] > dev_max) dev_max = o->dev[i];
-        if (o->order[i] != 0 && pref_order > o->order[i]) {
-            pref_order = o->order[i];
-            pref = i;
+        if (o->dev[i] > *dev_max) *dev_max = o->dev[i];
+        if (o->rsv[i] > *rsv_max) *rsv_max = o->rsv[i];
+        if (o->order[i] != 0) {
+            uint64_t k = ((uint64_t)(uint32_t)(o->order[i] + 0x80000000ll) << 32) | (uint64_t)(base + i);
+            if (k < *pref) *pref = k;
         }
     }
-    if (pref >= 0) o->rsv[pref] = 1000; /* mostPreferredScore */
-    for (uint32_t i = 0; i < nn; i++)
-        if (!o->st[i] && o->rsv[i] > rsv_max) rsv_max = o->rsv[i];
+}
+
+/* Score of the preferred node (mostPreferredScore 1000) and the weighted totals after NormalizeScore. */
+static void ext_pod_totals(const kg_config* c, ext_row* o, uint32_t nn, uint32_t base, int64_t dev_max, int64_t rsv_max,
+                           uint64_t pref) {
+    const int has_pref = pref != UINT64_MAX;
+    if (has_pref) {
+        uint32_t g = (uint32_t)pref;
+        if (g >= base && g - base < nn) o->rsv[g - base] = 1000;
+        rsv_max = 1000;
+    }
     for (uint32_t i = 0; i < nn; i++) {
         if (o->st[i]) continue;
         o->total[i] = c->weight_nrf * o->nrf[i] + c->weight_la * o->la[i] + c->weight_numa * o->numa[i] +
                       c->weight_dev * normalize(o->dev[i], dev_max) + c->weight_rsv * normalize(o->rsv[i], rsv_max);
     }
+}
+
+static void ext_pod_finish(const kg_config* c, ext_row* o, uint32_t nn, uint32_t base) {
+    int64_t dm, rm;
+    uint64_t pf;
+    ext_pod_stats(o, nn, base, &dm, &rm, &pf);
+    ext_pod_totals(c, o, nn, base, dm, rm, pf);
 }
 
 typedef struct ext_buf {
@@ -1312,6 +1334,7 @@ int kgo_ext_verify(const kg_config* c, const kg_node_columns* n, uint32_t nn, co
     view_index_build(&vx, e, nn);
     for (uint32_t j = 0; j < np; j++) {
         ext_eval_pod(c, n, nn, p, j, e, &vx, q, &b.r);
+        ext_pod_finish(c, &b.r, nn, 0);
         for (uint32_t i = 0; i < nn; i++) {
             size_t x = (size_t)j * nn + i;
             if (out->status) out->status[x] = b.r.st[i];
@@ -1341,6 +1364,52 @@ int kgo_ext_select(const kg_config* c, const kg_node_columns* n, uint32_t nn, ui
         uint64_t* top = keys + (size_t)j * k;
         memset(top, 0, sizeof(uint64_t) * k);
         ext_eval_pod(c, n, nn, p, j, e, &vx, q, &b.r);
+        ext_pod_finish(c, &b.r, nn, base);
+        for (uint32_t i = 0; i < nn; i++)
+            if (!b.r.st[i]) topk_insert(top, k, make_key(b.r.total[i], base + i));
+    }
+    free(vx.v);
+    quota_state_free(q);
+    free(b.mem);
+    return 0;
+}
+
+/* Node-sharded two-pass selection (kg_shard_select): per-shard NormalizeScore inputs ... */
+int kgo_ext_shard_stats(const kg_config* c, const kg_node_columns* n, uint32_t nn, uint32_t base,
+                        const kg_pod_columns* p, uint32_t np, const kgo_ext* e, uint32_t* dev_max, uint32_t* rsv_max,
+                        uint64_t* pref) {
+    ext_buf b;
+    if (ext_buf_new(&b, nn)) return -1;
+    kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    view_index vx;
+    view_index_build(&vx, e, nn);
+    for (uint32_t j = 0; j < np; j++) {
+        ext_eval_pod(c, n, nn, p, j, e, &vx, q, &b.r);
+        int64_t dm, rm;
+        ext_pod_stats(&b.r, nn, base, &dm, &rm, &pref[j]);
+        dev_max[j] = (uint32_t)dm;
+        rsv_max[j] = (uint32_t)rm;
+    }
+    free(vx.v);
+    quota_state_free(q);
+    free(b.mem);
+    return 0;
+}
+
+/* ... and the shard's top-k with the global (all-reduced) inputs. */
+int kgo_ext_shard_select(const kg_config* c, const kg_node_columns* n, uint32_t nn, uint32_t base,
+                         const kg_pod_columns* p, uint32_t np, const kgo_ext* e, const uint32_t* dev_max,
+                         const uint32_t* rsv_max, const uint64_t* pref, uint32_t k, uint64_t* keys) {
+    ext_buf b;
+    if (ext_buf_new(&b, nn)) return -1;
+    kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    view_index vx;
+    view_index_build(&vx, e, nn);
+    for (uint32_t j = 0; j < np; j++) {
+        uint64_t* top = keys + (size_t)j * k;
+        memset(top, 0, sizeof(uint64_t) * k);
+        ext_eval_pod(c, n, nn, p, j, e, &vx, q, &b.r);
+        ext_pod_totals(c, &b.r, nn, base, dev_max[j], rsv_max[j], pref[j]);
         for (uint32_t i = 0; i < nn; i++)
             if (!b.r.st[i]) topk_insert(top, k, make_key(b.r.total[i], base + i));
     }
@@ -1364,6 +1433,7 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
     kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
     for (uint32_t j = 0; j < np; j++) {
         ext_eval_pod(c, &v, st->n, p, j, e, NULL, q, &b.r);
+        ext_pod_finish(c, &b.r, st->n, base);
         uint64_t best = 0;
         int32_t best_zone = -1;
         for (uint32_t i = 0; i < st->n; i++) {

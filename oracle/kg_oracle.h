@@ -83,6 +83,14 @@ int kgo_ext_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, con
                    uint32_t n_pods, const kgo_ext* ext, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
                    int64_t* quota_used_out, int64_t* quota_np_used_out);
 int64_t kgo_mem_bytes_to_ratio(int64_t bytes, int64_t total);
+/* Node-sharded two-pass selection: per-shard NormalizeScore inputs (to be max / min all-reduced over
+ * the shards), then the shard's top-k with the global inputs. */
+int kgo_ext_shard_stats(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes, uint32_t index_base,
+                        const kg_pod_columns* pods, uint32_t n_pods, const kgo_ext* ext, uint32_t* dev_max,
+                        uint32_t* rsv_max, uint64_t* pref);
+int kgo_ext_shard_select(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes, uint32_t index_base,
+                         const kg_pod_columns* pods, uint32_t n_pods, const kgo_ext* ext, const uint32_t* dev_max,
+                         const uint32_t* rsv_max, const uint64_t* pref, uint32_t k, uint64_t* keys);
 
 /* Helpers shared with tests. */
 int64_t kgo_amplify(int64_t origin, double ratio);

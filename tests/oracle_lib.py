@@ -79,6 +79,14 @@ def lib():
                                      P(KgoExt), P(C.c_int32), P(C.c_int64), P(C.c_uint32), P(C.c_int64),
                                      P(C.c_int64)]
         L.kgo_ext_replay.restype = C.c_int
+        L.kgo_ext_shard_stats.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
+                                          P(abi.KgPodColumns), C.c_uint32, P(KgoExt), P(C.c_uint32), P(C.c_uint32),
+                                          P(C.c_uint64)]
+        L.kgo_ext_shard_stats.restype = C.c_int
+        L.kgo_ext_shard_select.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
+                                           P(abi.KgPodColumns), C.c_uint32, P(KgoExt), P(C.c_uint32), P(C.c_uint32),
+                                           P(C.c_uint64), C.c_uint32, P(C.c_uint64)]
+        L.kgo_ext_shard_select.restype = C.c_int
         L.kgo_mem_bytes_to_ratio.argtypes = [C.c_int64, C.c_int64]
         L.kgo_mem_bytes_to_ratio.restype = C.c_int64
         L.kgo_amplify.argtypes = [C.c_int64, C.c_double]
@@ -138,6 +146,30 @@ def ext_select(cfg, nodes: abi.Table, pods: abi.Table, k: int = 1, index_base: i
     nc, pc, e = abi.node_columns(nodes), abi.pod_columns(pods), make_ext(quotas, rsv)
     assert lib().kgo_ext_select(C.byref(cfg), C.byref(nc), nn, index_base, C.byref(pc), np_, C.byref(e), k,
                                 keys.ctypes.data_as(C.POINTER(C.c_uint64))) == 0
+    return keys
+
+
+def ext_shard_stats(cfg, nodes: abi.Table, pods: abi.Table, index_base: int, quotas=None, rsv=None):
+    nn, np_ = abi.table_len(nodes), abi.table_len(pods)
+    dm, rm, pf = np.zeros(np_, np.uint32), np.zeros(np_, np.uint32), np.zeros(np_, np.uint64)
+    nc, pc, e = abi.node_columns(nodes), abi.pod_columns(pods), make_ext(quotas, rsv)
+    P = C.POINTER
+    assert lib().kgo_ext_shard_stats(C.byref(cfg), C.byref(nc), nn, index_base, C.byref(pc), np_, C.byref(e),
+                                     dm.ctypes.data_as(P(C.c_uint32)), rm.ctypes.data_as(P(C.c_uint32)),
+                                     pf.ctypes.data_as(P(C.c_uint64))) == 0
+    return dm, rm, pf
+
+
+def ext_shard_select(cfg, nodes: abi.Table, pods: abi.Table, index_base: int, dm, rm, pf, k: int = 1, quotas=None,
+                     rsv=None) -> np.ndarray:
+    nn, np_ = abi.table_len(nodes), abi.table_len(pods)
+    keys = np.zeros((np_, k), np.uint64)
+    nc, pc, e = abi.node_columns(nodes), abi.pod_columns(pods), make_ext(quotas, rsv)
+    P = C.POINTER
+    dm, rm, pf = (np.ascontiguousarray(x) for x in (dm, rm, pf))
+    assert lib().kgo_ext_shard_select(C.byref(cfg), C.byref(nc), nn, index_base, C.byref(pc), np_, C.byref(e),
+                                      dm.ctypes.data_as(P(C.c_uint32)), rm.ctypes.data_as(P(C.c_uint32)),
+                                      pf.ctypes.data_as(P(C.c_uint64)), k, keys.ctypes.data_as(P(C.c_uint64))) == 0
     return keys
 
 

@@ -164,3 +164,19 @@ def test_config5_full_size_sampled(ctx):
     want = oracle_lib.ext_select(kc, nodes, sample, 1, 0, quotas, rsv)[:, 0]
     assert np.array_equal(keys[idx], want)
     assert (keys != 0).mean() > 0.5
+
+
+def test_ext_shard_select_single_rank(ctx):
+    """kg_shard_select's config-5 path (stats pass, RCCL all-reduce of the NormalizeScore inputs,
+    select pass, all-gather, merge) with one rank equals the global selection."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(1500, 256, seed_config=61, rsv_frac=0.3)
+    kc = cfg.kg_config()
+    sctx = engine.Context(0)
+    try:
+        sctx.shard_init(engine.shard_unique_id(), 0, 1)
+        snap, batch = make(sctx, kc, nodes, pods, quotas, rsv)
+        got = engine.shard_select(snap, batch)
+    finally:
+        sctx.close()
+    want = oracle_lib.ext_select(kc, nodes, pods, 1, 0, quotas, rsv)[:, 0]
+    assert np.array_equal(got, want)
