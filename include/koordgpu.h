@@ -127,6 +127,8 @@ typedef enum kg_status {
 #define KG_ST_NUMA_CONFLICT 0x20000u /* ErrNotMatchNUMATopology (UnschedulableAndUnresolvable) */
 #define KG_ST_NUMA_NO_RES 0x40000u   /* "node(s) missing NUMA resources"                      */
 #define KG_ST_NUMA_ALIGN 0x80000u    /* ErrNUMAHintCannotAligned                              */
+#define KG_ST_NUMA_UNSATISFIED 0x100000u /* ErrUnsatisfiedNUMAResource: a requested resource has no NUMA hint
+                                            (frameworkext/topologymanager/policy.go:166-173)     */
 #define KG_ST_NUMA_MASK 0xFF0000u
 #define KG_ST_DEV_INSUFFICIENT 0x01000000u /* "Insufficient gpu devices" (Unschedulable, device_allocator.go:432) */
 #define KG_ST_DEV_NO_DEVICE 0x02000000u    /* no GPU minors on the node's Device (UnschedulableAndUnresolvable,
@@ -170,6 +172,12 @@ typedef struct kg_config {
     int64_t weight_dev;
     int64_t weight_rsv;
     int64_t dev_w[KG_DEV_R];
+    /* ScoringStrategy type MostAllocated instead of LeastAllocated (nodenumaresource/most_allocated.go,
+     * deviceshare/scoring.go:283-308): NodeNUMAResource node score, its NUMA hint score, DeviceShare. */
+    uint32_t numa_most_allocated;
+    uint32_t numa_hint_most_allocated;
+    uint32_t dev_most_allocated;
+    uint32_t pad_;
 } kg_config;
 
 /* Node snapshot, struct-of-arrays host columns, n_nodes entries each (caller-owned, copied). */
@@ -208,6 +216,10 @@ typedef struct kg_node_columns {
     const int32_t* dev_minors;
     const int64_t* dev_total;
     const int64_t* dev_free;
+    /* NUMA node shared status per zone, 2 bits each (0 idle, 1 single, 2 shared; NUMANodeSharedStatus,
+     * nodenumaresource/node_allocation.go:52-68) for the Required exclusive policy of pods with a
+     * pod-level NUMA policy (NULL = all idle). */
+    const uint32_t* numa_zone_status;
 } kg_node_columns;
 
 /* Mutable node state that Assume/Forget change; used to read a snapshot back after kg_replay. */
@@ -250,7 +262,8 @@ typedef struct kg_verify_out {
     int64_t* score_la;    /* LoadAwareScheduling score                                      */
     int64_t* score_numa;  /* NodeNUMAResource score                                         */
     int64_t* total;       /* Σ weight·score, -1 when infeasible                             */
-    int8_t* numa_zone;    /* zone the NUMA Reserve would allocate from, -1 = none           */
+    int8_t* numa_zone;    /* NUMA allocation the Reserve would make: -1 none, 0..3 one zone,
+                             0x40 | zone mask for a split over several zones                 */
     int64_t* score_dev;   /* DeviceShare Score before NormalizeScore (0 when infeasible)    */
     int64_t* score_rsv;   /* Reservation Score before NormalizeScore (1000 on the preferred
                              node, reservation/scoring.go:40,191-198; 0 when infeasible)     */

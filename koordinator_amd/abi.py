@@ -69,6 +69,7 @@ KG_ST_NUMA_AMP_CPU = 0x10000
 KG_ST_NUMA_CONFLICT = 0x20000
 KG_ST_NUMA_NO_RES = 0x40000
 KG_ST_NUMA_ALIGN = 0x80000
+KG_ST_NUMA_UNSATISFIED = 0x100000
 KG_ST_NUMA_MASK = 0xFF0000
 KG_ST_DEV_INSUFFICIENT = 0x01000000
 KG_ST_DEV_NO_DEVICE = 0x02000000
@@ -108,6 +109,10 @@ class KgConfig(C.Structure):
         ("weight_dev", C.c_int64),
         ("weight_rsv", C.c_int64),
         ("dev_w", C.c_int64 * KG_DEV_R),
+        ("numa_most_allocated", C.c_uint32),
+        ("numa_hint_most_allocated", C.c_uint32),
+        ("dev_most_allocated", C.c_uint32),
+        ("pad_", C.c_uint32),
     ]
 
 
@@ -135,6 +140,7 @@ class KgNodeColumns(C.Structure):
         ("zone_cpu_used", _p64 * KG_MAX_ZONES),
         ("zone_mem_used", _p64 * KG_MAX_ZONES),
         ("dev_minors", _pi32), ("dev_total", _p64), ("dev_free", _p64),
+        ("numa_zone_status", _pu32),
     ]
 
 
@@ -212,7 +218,7 @@ NODE_I64 = (
     + _indexed("zone_cpu", KG_MAX_ZONES) + _indexed("zone_mem", KG_MAX_ZONES)
     + _indexed("zone_cpu_used", KG_MAX_ZONES) + _indexed("zone_mem_used", KG_MAX_ZONES)
 )
-NODE_U32 = ["la_flags", "numa_policy", "numa_zones"]
+NODE_U32 = ["la_flags", "numa_policy", "numa_zones", "numa_zone_status"]
 NODE_F64 = ["cpu_amp_ratio"]
 NODE_DEV = ["dev_total", "dev_free"]  # int64 [n][KG_DEV_R][KG_DEV_MINORS]
 
@@ -274,6 +280,8 @@ def _check(t: Table, names, dtype):
 
 
 def node_columns(t: Table) -> KgNodeColumns:
+    if "numa_zone_status" not in t:
+        t["numa_zone_status"] = np.zeros(table_len(t), np.uint32)
     _check(t, NODE_I64, np.int64)
     _check(t, NODE_U32, np.uint32)
     _check(t, NODE_F64, np.float64)
@@ -296,6 +304,8 @@ def node_columns(t: Table) -> KgNodeColumns:
     s.la_flags = _ptr(t["la_flags"], C.c_uint32)
     s.numa_policy = _ptr(t["numa_policy"], C.c_uint32)
     s.numa_zones = _ptr(t["numa_zones"], C.c_uint32)
+    if "numa_zone_status" in t:
+        s.numa_zone_status = _ptr(t["numa_zone_status"], C.c_uint32)
     s.cpu_amp_ratio = _ptr(t["cpu_amp_ratio"], C.c_double)
     if "dev_minors" in t:
         t["dev_minors"] = np.ascontiguousarray(t["dev_minors"], np.int32)

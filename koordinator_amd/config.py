@@ -106,6 +106,10 @@ class SchedulerConfig:
     weight_rsv: int = 5000
     dev_scoring: List[Tuple[str, int]] = field(
         default_factory=lambda: [(GPU_MEMORY_RATIO, 1), (GPU_MEMORY, 1)])
+    # ScoringStrategy types ("LeastAllocated" default / "MostAllocated")
+    numa_strategy: str = "LeastAllocated"
+    numa_hint_strategy: str = "LeastAllocated"
+    dev_strategy: str = "LeastAllocated"
 
     def la(self) -> LoadAwareArgs:
         return self.loadaware.defaulted()
@@ -141,6 +145,9 @@ class SchedulerConfig:
         c.numa_hint_w_cpu, c.numa_hint_w_mem = nh.get(CPU, 0), nh.get(MEMORY, 0)
         c.weight_dev = self.weight_dev
         c.weight_rsv = self.weight_rsv
+        c.numa_most_allocated = int(self.numa_strategy == "MostAllocated")
+        c.numa_hint_most_allocated = int(self.numa_hint_strategy == "MostAllocated")
+        c.dev_most_allocated = int(self.dev_strategy == "MostAllocated")
         ds = dict(self.dev_scoring)
         for r, name in enumerate(DEV_RESOURCES):
             c.dev_w[r] = ds.get(name, 0)

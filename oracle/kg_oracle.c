@@ -192,53 +192,39 @@ static int64_t la_score(const kg_config* c, const kg_node_columns* n, uint32_t i
 /* ---------------------------------------------------------------------------------------------- */
 /* NodeNUMAResource                                                                                */
 
-/* leastResourceScorer over {cpu, memory} with resources of allocatable 0 dropped
- * (nodenumaresource/scoring.go:222-238, least_allocated.go:30-48). */
-static int64_t numa_least_score(int64_t w_cpu, int64_t w_mem, int64_t alloc_cpu, int64_t req_cpu, int64_t alloc_mem,
-                                int64_t req_mem) {
+/* leastResourceScorer / mostResourceScorer over {cpu, memory} with resources of allocatable 0 dropped
+ * (nodenumaresource/scoring.go:222-238, least_allocated.go:30-58, most_allocated.go:30-62). */
+static int64_t most_requested_score(int64_t requested, int64_t capacity) {
+    if (capacity == 0) return 0;
+    if (requested > capacity) requested = capacity;
+    return (requested * MAX_NODE_SCORE) / capacity;
+}
+
+static int64_t numa_scorer(int most, int64_t w_cpu, int64_t w_mem, int64_t alloc_cpu, int64_t req_cpu, int64_t alloc_mem,
+                           int64_t req_mem) {
     int64_t score = 0, wsum = 0;
     if (alloc_cpu != 0 && w_cpu != 0) {
-        score += least_requested_score(req_cpu, alloc_cpu) * w_cpu;
+        score += (most ? most_requested_score(req_cpu, alloc_cpu) : least_requested_score(req_cpu, alloc_cpu)) * w_cpu;
         wsum += w_cpu;
     }
     if (alloc_mem != 0 && w_mem != 0) {
-        score += least_requested_score(req_mem, alloc_mem) * w_mem;
+        score += (most ? most_requested_score(req_mem, alloc_mem) : least_requested_score(req_mem, alloc_mem)) * w_mem;
         wsum += w_mem;
     }
     if (wsum == 0) return 0;
     return score / wsum;
 }
 
-static int64_t sub_nonneg(int64_t a, int64_t b) { return a - b < 0 ? 0 : a - b; }
-
-/* Best single-NUMA-node hint for a non-cpuset pod on a SingleNUMANode node: a zone is usable when
- * tryBestToDistributeEvenly fits the pod's requests into it (resource_manager.go:272-318) and it does
- * not lack any requested resource (generateResourceHints, resource_manager.go:529-626); among usable
- * zones mergeFilteredHints keeps the highest hint score, ties to the lowest zone (policy.go:198-256,
- * bitmask IsNarrowerThan). Returns zone or -1. */
-static int32_t numa_best_zone(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
-                              uint32_t j) {
-    uint32_t Z = n->numa_zones[i];
-    int has_cpu = (p->flags[j] & KG_POD_HAS_CPU) != 0, has_mem = (p->flags[j] & KG_POD_HAS_MEM) != 0;
-    int32_t best = -1;
-    int64_t best_score = 0;
-    for (uint32_t z = 0; z < Z; z++) {
-        int64_t tc = n->zone_cpu[z][i], tm = n->zone_mem[z][i];
-        int64_t uc = n->zone_cpu_used[z][i], um = n->zone_mem_used[z][i];
-        int64_t ac = sub_nonneg(tc, uc), am = sub_nonneg(tm, um); /* node_allocation.go:240 */
-        if (has_cpu && (ac == 0 || p->req_cpu[j] > ac)) continue;
-        if (has_mem && (am == 0 || p->req_mem[j] > am)) continue;
-        /* hint score: numaScorer over requested = total - available (resource_manager.go:575-579) */
-        int64_t rc = sub_nonneg(tc, ac), rm = sub_nonneg(tm, am);
-        int64_t s = numa_least_score(c->numa_hint_w_cpu, c->numa_hint_w_mem, tc, rc + p->req_cpu[j], tm,
-                                     rm + p->req_mem[j]);
-        if (best < 0 || s > best_score) {
-            best = (int32_t)z;
-            best_score = s;
-        }
-    }
-    return best;
+/* the plugin's node score (ScoringStrategy) and its NUMA hint score (NUMAScoringStrategy) */
+static int64_t numa_node_score(const kg_config* c, int64_t ac, int64_t rc, int64_t am, int64_t rm) {
+    return numa_scorer(c->numa_most_allocated != 0, c->numa_w_cpu, c->numa_w_mem, ac, rc, am, rm);
 }
+
+static int64_t numa_hint_score(const kg_config* c, int64_t ac, int64_t rc, int64_t am, int64_t rm) {
+    return numa_scorer(c->numa_hint_most_allocated != 0, c->numa_hint_w_cpu, c->numa_hint_w_mem, ac, rc, am, rm);
+}
+
+static int64_t sub_nonneg(int64_t a, int64_t b) { return a - b < 0 ? 0 : a - b; }
 
 static uint32_t numa_merge_policy(uint32_t node_policy, uint32_t pod_policy, int* conflict) {
     /* mergeTopologyPolicy: nodenumaresource/util.go:58-66 */
@@ -251,8 +237,249 @@ static uint32_t numa_merge_policy(uint32_t node_policy, uint32_t pod_policy, int
     return node_policy;
 }
 
-/* Filter (plugin.go:363-459) + Score (scoring.go:67-151) of one pair. zone_out: -2 = node scored
- * at node level (no NUMA allocation), >=0 zone allocation. */
+/* ---- NUMA topology manager: hints (resource_manager.go:529-657) and policy merge
+ *      (frameworkext/topologymanager/policy*.go) for non-cpuset pods ---------------------------------- */
+
+/* bitmask.IterateBitMasks order (pkg/util/bitmask/bitmask.go:206-221): by size, then lexicographic */
+static const uint8_t NUMA_MASKS[KG_MAX_ZONES][15] = {
+    {1},
+    {1, 2, 3},
+    {1, 2, 4, 3, 5, 6, 7},
+    {1, 2, 4, 8, 3, 5, 9, 6, 10, 12, 7, 11, 13, 14, 15},
+};
+static const uint32_t NUMA_NMASKS[KG_MAX_ZONES] = {1, 3, 7, 15};
+
+static int popcount32(uint32_t x) { return __builtin_popcount(x); }
+
+typedef struct numa_zones {
+    uint32_t Z, status;
+    int64_t tot[2][KG_MAX_ZONES], used[2][KG_MAX_ZONES], avail[2][KG_MAX_ZONES];
+} numa_zones;
+
+static void numa_zones_load(const kg_node_columns* n, uint32_t i, numa_zones* x) {
+    memset(x, 0, sizeof(*x));
+    x->Z = n->numa_zones[i];
+    x->status = n->numa_zone_status ? n->numa_zone_status[i] : 0;
+    for (uint32_t z = 0; z < x->Z && z < KG_MAX_ZONES; z++) {
+        x->tot[0][z] = n->zone_cpu[z][i];
+        x->tot[1][z] = n->zone_mem[z][i];
+        x->used[0][z] = n->zone_cpu_used[z][i];
+        x->used[1][z] = n->zone_mem_used[z][i];
+        for (int r = 0; r < 2; r++) x->avail[r][z] = sub_nonneg(x->tot[r][z], x->used[r][z]); /* node_allocation.go:240 */
+    }
+}
+
+/* tryBestToDistributeEvenly (resource_manager.go:264-318) of the pod's cpu / memory requests over the
+ * zones of `mask`. The per-resource zone order comes from sort.Slice whose less(i, j) reads
+ * totalAvailable by the positions i, j rather than by the zone ids being sorted (:276-279); sort.Slice
+ * runs insertion sort for n <= 12, so the swaps depend only on the availability of zones 0..n-1. */
+static int numa_split(const numa_zones* x, uint32_t mask, const int64_t* req, const int* has,
+                      int64_t alloc[2][KG_MAX_ZONES]) {
+    int nodes[KG_MAX_ZONES], n = 0;
+    for (uint32_t z = 0; z < x->Z; z++)
+        if ((mask >> z) & 1u) nodes[n++] = (int)z;
+    memset(alloc, 0, sizeof(int64_t) * 2 * KG_MAX_ZONES);
+    for (int r = 0; r < 2; r++) {
+        if (!has[r]) continue;
+        int s[KG_MAX_ZONES];
+        memcpy(s, nodes, sizeof(nodes));
+        for (int a = 1; a < n; a++)
+            for (int b = a; b > 0 && x->avail[r][b] < x->avail[r][b - 1]; b--) {
+                int t = s[b];
+                s[b] = s[b - 1];
+                s[b - 1] = t;
+            }
+        int64_t q = req[r];
+        for (int t = 0; t < n; t++) {
+            int64_t split = q / (n - t); /* splitQuantity :320-334 (milli-cpu / bytes) */
+            int64_t av = x->avail[r][s[t]];
+            int64_t got = av > split ? split : av; /* allocateRes :336-355 */
+            if (got != 0) {
+                alloc[r][s[t]] = got;
+                q -= got;
+            }
+        }
+        if (q != 0) return 0; /* "Insufficient NUMA <resource>" */
+    }
+    return 1;
+}
+
+typedef struct numa_hint {
+    uint32_t mask; /* 0 = nil affinity */
+    int pref, unsat;
+    int64_t score;
+} numa_hint;
+
+typedef struct numa_lists {
+    int n_lists;
+    int len[2];
+    numa_hint h[2][15];
+    int reasons;
+} numa_lists;
+
+/* generateResourceHints + filterProvidersHints: per requested resource (cpu, then memory) the hints of
+ * the masks whose allocation succeeds and that avoid zones lacking the resource; Preferred = narrowest
+ * size, or every hint under Restricted. A requested resource without hints contributes one unsatisfied
+ * nil hint and a reason (policy.go:166-173). */
+static void numa_hints(const kg_config* c, const numa_zones* x, const int64_t* req, const int* has, uint32_t policy,
+                       numa_lists* L) {
+    const uint32_t Z = x->Z;
+    uint32_t lack[2] = {0, 0};
+    for (uint32_t z = 0; z < Z; z++)
+        for (int r = 0; r < 2; r++)
+            if (x->avail[r][z] == 0) lack[r] |= 1u << z;
+    int minsize[2] = {(int)Z, (int)Z};
+    uint32_t okm[2] = {0, 0};
+    int64_t score[15];
+    const uint8_t* masks = NUMA_MASKS[Z - 1];
+    for (uint32_t k = 0; k < NUMA_NMASKS[Z - 1]; k++) {
+        uint32_t m = masks[k];
+        int64_t T[2] = {0, 0}, A[2] = {0, 0};
+        for (uint32_t z = 0; z < Z; z++)
+            if ((m >> z) & 1u)
+                for (int r = 0; r < 2; r++) {
+                    T[r] += x->tot[r][z];
+                    A[r] += x->avail[r][z];
+                }
+        /* numaScorer over requested = SubtractWithNonNegativeResult(total, available) */
+        score[k] = numa_hint_score(c, T[0], sub_nonneg(T[0], A[0]) + req[0], T[1], sub_nonneg(T[1], A[1]) + req[1]);
+        int64_t al[2][KG_MAX_ZONES];
+        if (!numa_split(x, m, req, has, al)) continue;
+        for (int r = 0; r < 2; r++) {
+            if (!has[r] || (m & lack[r])) continue;
+            if (popcount32(m) < minsize[r]) minsize[r] = popcount32(m);
+            okm[r] |= 1u << k;
+        }
+    }
+    L->n_lists = 0;
+    L->reasons = 0;
+    for (int r = 0; r < 2; r++) {
+        if (!has[r]) continue;
+        int li = L->n_lists++;
+        int len = 0;
+        for (uint32_t k = 0; k < NUMA_NMASKS[Z - 1]; k++) {
+            if (!((okm[r] >> k) & 1u)) continue;
+            numa_hint* h = &L->h[li][len++];
+            h->mask = masks[k];
+            h->pref = popcount32(masks[k]) == minsize[r] || policy == KG_NUMA_RESTRICTED;
+            h->unsat = 0;
+            h->score = score[k];
+        }
+        if (len == 0) {
+            L->reasons++;
+            numa_hint* h = &L->h[li][len++];
+            h->mask = 0;
+            h->pref = 0;
+            h->unsat = 1;
+            h->score = 0;
+        }
+        L->len[li] = len;
+    }
+}
+
+/* checkExclusivePolicy with NumaTopologyExclusiveRequired (policy.go:73-93) */
+static int numa_excl_ok(uint32_t mask, uint32_t status) {
+    if (popcount32(mask) > 1) {
+        for (uint32_t z = 0; z < KG_MAX_ZONES; z++)
+            if (((mask >> z) & 1u) && ((status >> (2 * z)) & 3u) == 1u) return 0;
+        return 1;
+    }
+    uint32_t z = (uint32_t)__builtin_ctz(mask);
+    return ((status >> (2 * z)) & 3u) != 2u;
+}
+
+/* mergePermutation + the bestHint update of mergeFilteredHints (policy.go:98-137,198-260) */
+static void numa_merge_one(uint32_t all, int excl, uint32_t status, const numa_hint* perm, int np, numa_hint* best) {
+    uint32_t merged = all, first = 0;
+    int pref = 1, unsat = 0, naff = 0, maxc = 0;
+    for (int t = 0; t < np; t++) {
+        const numa_hint* v = &perm[t];
+        if (v->mask) {
+            if (naff == 0) first = v->mask;
+            else if (v->mask != first) pref = 0;
+            naff++;
+            merged &= v->mask;
+            if (popcount32(v->mask) > maxc) maxc = popcount32(v->mask);
+        }
+        if (!v->pref) pref = 0;
+        if (v->unsat) unsat = 1;
+    }
+    int satisfied = (naff == 0 || maxc == popcount32(merged)) && !unsat;
+    if (popcount32(merged) == 0) return;
+    if (excl && !numa_excl_ok(merged, status)) pref = 0;
+    int64_t score = 0;
+    for (int t = 0; t < np; t++)
+        if (perm[t].mask && perm[t].mask == merged) score += perm[t].score;
+    numa_hint m = {merged, pref, !satisfied, score};
+    if (m.pref && !best->pref) {
+        *best = m;
+        return;
+    }
+    if (!m.pref && best->pref) return;
+    int cm = popcount32(m.mask), cb = popcount32(best->mask);
+    int narrower = cm == cb ? m.mask < best->mask : cm < cb;
+    if (!narrower) {
+        if (cm == cb && m.score > best->score) *best = m;
+        return;
+    }
+    *best = m;
+}
+
+/* Policy Merge (policy_single_numa_node.go:69-90, policy_restricted.go:50-62, policy_best_effort.go:48-60).
+ * Returns 0 admitted (affinity mask in *mask_out, 0 = none), else a KG_ST_NUMA_* reason. Permutations
+ * run cpu-major; the reference iterates Go map order here, which matters only for BestEffort when no
+ * merged hint is preferred (parity unpinned there). */
+static uint32_t numa_admit(const kg_config* c, const numa_zones* x, const int64_t* req, const int* has, uint32_t policy,
+                           int excl, uint32_t* mask_out) {
+    numa_lists L;
+    numa_hints(c, x, req, has, policy, &L);
+    const uint32_t all = (1u << x->Z) - 1u;
+    *mask_out = 0;
+    if (L.reasons && policy != KG_NUMA_BEST_EFFORT) return KG_ST_NUMA_UNSATISFIED;
+    if (policy == KG_NUMA_SINGLE_NODE) { /* filterSingleNumaHints */
+        for (int li = 0; li < L.n_lists; li++) {
+            int w = 0;
+            for (int t = 0; t < L.len[li]; t++) {
+                numa_hint h = L.h[li][t];
+                if (h.pref && (h.mask == 0 || popcount32(h.mask) == 1)) L.h[li][w++] = h;
+            }
+            L.len[li] = w;
+        }
+    }
+    numa_hint best = {all, 0, 0, 0};
+    if (L.n_lists == 0) {
+        /* no NUMA resource requested: the providers' "no preference" hints */
+        numa_merge_one(all, excl, x->status, NULL, 0, &best);
+    } else if (L.n_lists == 1) {
+        for (int a = 0; a < L.len[0]; a++) numa_merge_one(all, excl, x->status, &L.h[0][a], 1, &best);
+    } else {
+        for (int a = 0; a < L.len[0]; a++)
+            for (int b = 0; b < L.len[1]; b++) {
+                numa_hint perm[2] = {L.h[0][a], L.h[1][b]};
+                numa_merge_one(all, excl, x->status, perm, 2, &best);
+            }
+    }
+    if (policy == KG_NUMA_BEST_EFFORT) {
+        *mask_out = best.unsat ? all : best.mask;
+        return 0;
+    }
+    if (!best.pref) return KG_ST_NUMA_ALIGN;
+    *mask_out = (policy == KG_NUMA_SINGLE_NODE && best.mask == all) ? 0 : best.mask;
+    return 0;
+}
+
+/* zone code of an allocation: -1 none, the zone for one zone, 0x40 | mask for several */
+static int32_t numa_code(uint32_t mask) {
+    if (!mask) return -1;
+    return popcount32(mask) == 1 ? (int32_t)__builtin_ctz(mask) : (int32_t)(0x40u | mask);
+}
+
+static uint32_t numa_code_mask(int32_t code) {
+    if (code < 0) return 0;
+    return code >= 0x40 ? (uint32_t)code & 0xFu : 1u << code;
+}
+
+/* Filter (plugin.go:363-459) + Score (scoring.go:67-151,153-199) of one pair. */
 static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t i, const kgo_over* ov,
                           const kg_pod_columns* p, uint32_t j, int64_t* score_out, int32_t* zone_out) {
     *score_out = 0;
@@ -262,7 +489,6 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
     int conflict;
     uint32_t policy = numa_merge_policy(n->numa_policy[i], p->numa_policy[j], &conflict);
     if (conflict) return KG_ST_NUMA_CONFLICT;
-    if (policy == KG_NUMA_RESTRICTED || policy == KG_NUMA_BEST_EFFORT) return KG_ST_UNSUPPORTED;
     double ratio = n->cpu_amp_ratio[i];
     int64_t pod_cpu = p->req_cpu[j];
     /* filterAmplifiedCPUs: plugin.go:461-498 (requestCPUBind == false) */
@@ -275,40 +501,55 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
         }
         if (pod_cpu > n->alloc_cpu[i] - requested) return KG_ST_NUMA_AMP_CPU;
     }
-    if (policy == KG_NUMA_SINGLE_NODE) {
-        /* FilterByNUMANode: topology_hint.go:31-41 -> singleNumaNodePolicy.Merge
-         * (frameworkext/topologymanager/policy_single_numa_node.go:69-90) */
-        uint32_t Z = n->numa_zones[i];
-        if (Z == 0) return KG_ST_NUMA_NO_RES;
-        int has_any = (p->flags[j] & (KG_POD_HAS_CPU | KG_POD_HAS_MEM)) != 0;
-        int32_t z = -1;
-        if (has_any) {
-            z = numa_best_zone(c, n, i, p, j);
-            if (z < 0) return KG_ST_NUMA_ALIGN;
+    if (policy == KG_NUMA_NONE) {
+        /* scoreWithAmplifiedCPUs, scoring.go:132-151 */
+        int64_t req_cpu = N_REQ_CPU(n, i, ov);
+        if (!(pod_cpu == 0 || ratio <= 1)) {
+            int64_t allocated = n->cpuset_alloc_milli[i];
+            req_cpu = req_cpu - allocated + kgo_amplify(allocated, ratio);
         }
-        /* a best hint equal to the default affinity (all zones) is returned without affinity
-         * (policy_single_numa_node.go:79-84): no NUMA allocation, node-level score */
-        if (!has_any || Z == 1) {
-            *zone_out = -1;
-            *score_out = numa_least_score(c->numa_w_cpu, c->numa_w_mem, n->alloc_cpu[i], N_REQ_CPU(n, i, ov) + pod_cpu,
-                                          n->alloc_mem[i], N_REQ_MEM(n, i, ov) + p->req_mem[j]);
-            return 0;
-        }
-        /* Score with the zone allocation: calculateAllocatableAndRequested, scoring.go:153-199 */
-        *zone_out = z;
-        *score_out = numa_least_score(c->numa_w_cpu, c->numa_w_mem, n->zone_cpu[z][i],
-                                      n->zone_cpu_used[z][i] + pod_cpu, n->zone_mem[z][i],
-                                      n->zone_mem_used[z][i] + p->req_mem[j]);
+        *score_out = numa_node_score(c, n->alloc_cpu[i], req_cpu + pod_cpu, n->alloc_mem[i],
+                                     N_REQ_MEM(n, i, ov) + p->req_mem[j]);
         return 0;
     }
-    /* policy None: scoreWithAmplifiedCPUs, scoring.go:132-151 */
-    int64_t req_cpu = N_REQ_CPU(n, i, ov);
-    if (!(pod_cpu == 0 || ratio <= 1)) {
-        int64_t allocated = n->cpuset_alloc_milli[i];
-        req_cpu = req_cpu - allocated + kgo_amplify(allocated, ratio);
+    /* FilterByNUMANode (topology_hint.go:31-41): SingleNUMANode / Restricted admit in Filter; BestEffort
+     * admits at Reserve only (plugin.go:448,612-623), its Score sees no affinity */
+    numa_zones x;
+    numa_zones_load(n, i, &x);
+    const int64_t req[2] = {p->req_cpu[j], p->req_mem[j]};
+    const int has[2] = {(p->flags[j] & KG_POD_HAS_CPU) != 0, (p->flags[j] & KG_POD_HAS_MEM) != 0};
+    /* podNUMAExclusive defaults to Required when the pod carries its own NUMA policy (plugin.go:449-454) */
+    const int excl = p->numa_policy[j] != KG_NUMA_NONE;
+    uint32_t mask = 0;
+    if (x.Z == 0) {
+        if (policy != KG_NUMA_BEST_EFFORT) return KG_ST_NUMA_NO_RES;
+        return KG_ST_UNSUPPORTED; /* the BestEffort Reserve fails on a node without NUMA resources */
     }
-    *score_out = numa_least_score(c->numa_w_cpu, c->numa_w_mem, n->alloc_cpu[i], req_cpu + pod_cpu, n->alloc_mem[i],
-                                  N_REQ_MEM(n, i, ov) + p->req_mem[j]);
+    uint32_t st = numa_admit(c, &x, req, has, policy, excl, &mask);
+    if (st) return st;
+    int64_t al[2][KG_MAX_ZONES];
+    if (mask && !numa_split(&x, mask, req, has, al)) {
+        /* only a non-preferred / unsatisfied BestEffort hint can fail its allocation: the reference
+         * fails the Reserve, the device path hands the pair back to the host */
+        return KG_ST_UNSUPPORTED;
+    }
+    *zone_out = numa_code(mask);
+    if (policy == KG_NUMA_BEST_EFFORT || !mask) {
+        /* calculateAllocatableAndRequested without NUMA allocation: node allocatable / requested */
+        *score_out = numa_node_score(c, n->alloc_cpu[i], N_REQ_CPU(n, i, ov) + pod_cpu, n->alloc_mem[i],
+                                     N_REQ_MEM(n, i, ov) + p->req_mem[j]);
+        return 0;
+    }
+    /* the zones that received an allocation: their totals and their allocated */
+    int64_t T[2] = {0, 0}, U[2] = {0, 0};
+    for (uint32_t z = 0; z < x.Z; z++) {
+        if (al[0][z] == 0 && al[1][z] == 0) continue;
+        for (int r = 0; r < 2; r++) {
+            T[r] += x.tot[r][z];
+            U[r] += x.used[r][z];
+        }
+    }
+    *score_out = numa_node_score(c, T[0], U[0] + pod_cpu, T[1], U[1] + p->req_mem[j]);
     return 0;
 }
 
@@ -549,7 +790,7 @@ enum {
 struct kgo_state {
     uint32_t n;
     int64_t* col[C_NCOLS];
-    uint32_t *la_flags, *numa_policy, *numa_zones;
+    uint32_t *la_flags, *numa_policy, *numa_zones, *zone_status;
     double* amp;
     int32_t* dev_minors;          /* DeviceShare (NULL when the snapshot has no device tables) */
     int64_t *dev_total, *dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
@@ -599,6 +840,8 @@ kgo_state* kgo_state_new(const kg_node_columns* s, uint32_t n) {
     st->numa_policy = (uint32_t*)calloc(n ? n : 1, 4);
     st->numa_zones = (uint32_t*)calloc(n ? n : 1, 4);
     st->amp = (double*)calloc(n ? n : 1, 8);
+    st->zone_status = (uint32_t*)calloc(n ? n : 1, 4);
+    if (s->numa_zone_status) memcpy(st->zone_status, s->numa_zone_status, 4 * (size_t)n);
     if (s->la_flags) memcpy(st->la_flags, s->la_flags, 4 * (size_t)n);
     if (s->numa_policy) memcpy(st->numa_policy, s->numa_policy, 4 * (size_t)n);
     if (s->numa_zones) memcpy(st->numa_zones, s->numa_zones, 4 * (size_t)n);
@@ -622,6 +865,7 @@ void kgo_state_free(kgo_state* st) {
     free(st->numa_policy);
     free(st->numa_zones);
     free(st->amp);
+    free(st->zone_status);
     free(st->dev_minors);
     free(st->dev_total);
     free(st->dev_free);
@@ -665,6 +909,7 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
         v->zone_cpu_used[z] = st->col[C_ZONE_CPU_USED + z];
         v->zone_mem_used[z] = st->col[C_ZONE_MEM_USED + z];
     }
+    v->numa_zone_status = st->zone_status;
     v->dev_minors = st->dev_minors;
     v->dev_total = st->dev_total;
     v->dev_free = st->dev_free;
@@ -695,10 +940,30 @@ static void apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_co
             }
         }
     }
-    /* NodeNUMAResource Reserve -> resourceManager.Update (plugin.go:585-635) */
+    /* NodeNUMAResource Reserve -> resourceManager.Update (plugin.go:585-635): the allocation split of
+     * the affinity, recomputed from the zone state the pair was evaluated on (Reserve runs right after) */
     if ((c->plugins & KG_PLUGIN_NUMA) && zone >= 0) {
-        st->col[C_ZONE_CPU_USED + zone][i] += sign * p->req_cpu[j];
-        st->col[C_ZONE_MEM_USED + zone][i] += sign * p->req_mem[j];
+        uint32_t mask = numa_code_mask(zone);
+        int64_t al[2][KG_MAX_ZONES];
+        memset(al, 0, sizeof(al));
+        if (popcount32(mask) == 1) {
+            int z = __builtin_ctz(mask);
+            al[0][z] = p->req_cpu[j];
+            al[1][z] = p->req_mem[j];
+        } else {
+            kg_node_columns v;
+            kgo_state_view(st, &v);
+            numa_zones x;
+            numa_zones_load(&v, i, &x);
+            const int64_t req[2] = {p->req_cpu[j], p->req_mem[j]};
+            const int has[2] = {(p->flags[j] & KG_POD_HAS_CPU) != 0, (p->flags[j] & KG_POD_HAS_MEM) != 0};
+            /* a multi-zone split is only reproducible before the Reserve: Unreserve of one is not restated */
+            if (sign > 0) numa_split(&x, mask, req, has, al);
+        }
+        for (uint32_t z = 0; z < KG_MAX_ZONES; z++) {
+            st->col[C_ZONE_CPU_USED + z][i] += sign * al[0][z];
+            st->col[C_ZONE_MEM_USED + z][i] += sign * al[1][z];
+        }
     }
 }
 

@@ -254,6 +254,7 @@ class OracleState:
         t["la_flags"] = grab(v.la_flags, np.uint32)
         t["numa_policy"] = grab(v.numa_policy, np.uint32)
         t["numa_zones"] = grab(v.numa_zones, np.uint32)
+        t["numa_zone_status"] = grab(v.numa_zone_status, np.uint32)
         t["cpu_amp_ratio"] = grab(v.cpu_amp_ratio, np.float64)
         df = self.dev_free()
         t["dev_free"] = df if df is not None else np.zeros((n, abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
