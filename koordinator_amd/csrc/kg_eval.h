@@ -85,6 +85,229 @@ __device__ __forceinline__ int64_t numa_least(int64_t w_cpu, int64_t w_mem, int6
     return wdiv(sum, wsum);
 }
 
+__device__ __forceinline__ int64_t most_req(int64_t requested, int64_t capacity) {
+    if (capacity == 0) return 0;
+    if (requested > capacity) requested = capacity;
+    return (requested * 100) / capacity;
+}
+
+// LeastAllocated / MostAllocated over {cpu, memory} (nodenumaresource least_allocated.go / most_allocated.go)
+template <bool EXACT>
+__device__ __forceinline__ int64_t numa_score(bool most, int64_t w_cpu, int64_t w_mem, int64_t alloc_cpu, int64_t req_cpu,
+                                              double rcp_cpu, int64_t alloc_mem, int64_t req_mem, double rcp_mem) {
+    if (!most) return numa_least<EXACT>(w_cpu, w_mem, alloc_cpu, req_cpu, rcp_cpu, alloc_mem, req_mem, rcp_mem);
+    int64_t sum = 0, wsum = 0;
+    if (alloc_cpu != 0 && w_cpu != 0) {
+        sum += most_req(req_cpu, alloc_cpu) * w_cpu;
+        wsum += w_cpu;
+    }
+    if (alloc_mem != 0 && w_mem != 0) {
+        sum += most_req(req_mem, alloc_mem) * w_mem;
+        wsum += w_mem;
+    }
+    return wsum == 0 ? 0 : sum / wsum;
+}
+
+// ---- NUMA topology manager for non-cpuset pods: hints (resource_manager.go:529-657) and the
+//      SingleNUMANode / Restricted / BestEffort merge (frameworkext/topologymanager/policy*.go).
+//      Mirrors oracle/kg_oracle.c numa_hints / numa_admit.
+
+__device__ __constant__ const uint8_t NUMA_MASKS[4][15] = {
+    {1},
+    {1, 2, 3},
+    {1, 2, 4, 3, 5, 6, 7},
+    {1, 2, 4, 8, 3, 5, 9, 6, 10, 12, 7, 11, 13, 14, 15},
+};
+__device__ __constant__ const uint8_t NUMA_NMASKS[4] = {1, 3, 7, 15};
+
+struct NumaZ {
+    uint32_t Z, status;
+    int64_t tot[2][MAX_ZONES], used[2][MAX_ZONES], avail[2][MAX_ZONES];
+};
+
+__device__ __forceinline__ void numa_load(const ZoneRec* __restrict__ zr, uint32_t Z, NumaZ& x) {
+    x.Z = Z;
+    x.status = zr->status;
+    for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++) {
+        const bool on = z < Z;
+        x.tot[0][z] = on ? zr->cpu[z] : 0;
+        x.tot[1][z] = on ? zr->mem[z] : 0;
+        x.used[0][z] = on ? zr->cpu_used[z] : 0;
+        x.used[1][z] = on ? zr->mem_used[z] : 0;
+        for (int r = 0; r < 2; r++) x.avail[r][z] = x.tot[r][z] - x.used[r][z] < 0 ? 0 : x.tot[r][z] - x.used[r][z];
+    }
+}
+
+// tryBestToDistributeEvenly with the position-indexed sort comparator (see the oracle)
+__device__ __forceinline__ bool numa_split(const NumaZ& x, uint32_t mask, const int64_t* req, const bool* has,
+                                           int64_t (&al)[2][MAX_ZONES]) {
+    int nodes[MAX_ZONES], n = 0;
+    for (uint32_t z = 0; z < x.Z; z++)
+        if ((mask >> z) & 1u) nodes[n++] = (int)z;
+    for (int r = 0; r < 2; r++)
+        for (int z = 0; z < MAX_ZONES; z++) al[r][z] = 0;
+    for (int r = 0; r < 2; r++) {
+        if (!has[r]) continue;
+        int s[MAX_ZONES];
+        for (int t = 0; t < n; t++) s[t] = nodes[t];
+        for (int a = 1; a < n; a++)
+            for (int b = a; b > 0 && x.avail[r][b] < x.avail[r][b - 1]; b--) {
+                const int t = s[b];
+                s[b] = s[b - 1];
+                s[b - 1] = t;
+            }
+        int64_t q = req[r];
+        for (int t = 0; t < n; t++) {
+            const int64_t split = q / (n - t);
+            const int64_t av = x.avail[r][s[t]];
+            const int64_t got = av > split ? split : av;
+            if (got != 0) {
+                al[r][s[t]] = got;
+                q -= got;
+            }
+        }
+        if (q != 0) return false;
+    }
+    return true;
+}
+
+struct NumaHint {
+    uint32_t mask;  // 0 = nil affinity
+    bool pref, unsat;
+    int64_t score;
+};
+
+__device__ __forceinline__ int popc(uint32_t x) { return __popc(x); }
+
+__device__ __forceinline__ bool numa_excl_ok(uint32_t mask, uint32_t status) {
+    if (popc(mask) > 1) {
+        for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++)
+            if (((mask >> z) & 1u) && ((status >> (2 * z)) & 3u) == 1u) return false;
+        return true;
+    }
+    const uint32_t z = (uint32_t)(__ffs(mask) - 1);
+    return ((status >> (2 * z)) & 3u) != 2u;
+}
+
+__device__ __forceinline__ void numa_merge_one(uint32_t all, bool excl, uint32_t status, const NumaHint* perm, int np,
+                                               NumaHint& best) {
+    uint32_t merged = all, first = 0;
+    bool pref = true, unsat = false;
+    int naff = 0, maxc = 0;
+    for (int t = 0; t < np; t++) {
+        const NumaHint& v = perm[t];
+        if (v.mask) {
+            if (naff == 0) first = v.mask;
+            else if (v.mask != first) pref = false;
+            naff++;
+            merged &= v.mask;
+            maxc = max(maxc, popc(v.mask));
+        }
+        pref = pref && v.pref;
+        unsat = unsat || v.unsat;
+    }
+    const bool satisfied = (naff == 0 || maxc == popc(merged)) && !unsat;
+    if (popc(merged) == 0) return;
+    if (excl && !numa_excl_ok(merged, status)) pref = false;
+    int64_t score = 0;
+    for (int t = 0; t < np; t++)
+        if (perm[t].mask && perm[t].mask == merged) score += perm[t].score;
+    NumaHint m{merged, pref, !satisfied, score};
+    if (m.pref && !best.pref) {
+        best = m;
+        return;
+    }
+    if (!m.pref && best.pref) return;
+    const int cm = popc(m.mask), cb = popc(best.mask);
+    const bool narrower = cm == cb ? m.mask < best.mask : cm < cb;
+    if (!narrower) {
+        if (cm == cb && m.score > best.score) best = m;
+        return;
+    }
+    best = m;
+}
+
+// Policy merge: 0 = admitted with affinity `mask` (0 = none), else a KG_ST_NUMA_* reason.
+template <bool EXACT>
+__device__ __forceinline__ uint32_t numa_admit(const KCfg& c, const NumaZ& x, const int64_t* req, const bool* has,
+                                              uint32_t policy, bool excl, uint32_t& mask_out) {
+    const uint32_t Z = x.Z;
+    const uint8_t* masks = NUMA_MASKS[Z - 1];
+    const uint32_t nm = NUMA_NMASKS[Z - 1];
+    uint32_t lack[2] = {0, 0};
+    for (uint32_t z = 0; z < Z; z++)
+        for (int r = 0; r < 2; r++)
+            if (x.avail[r][z] == 0) lack[r] |= 1u << z;
+    int minsize[2] = {(int)Z, (int)Z};
+    uint32_t okm[2] = {0, 0};
+    int64_t score[15];
+    for (uint32_t k = 0; k < nm; k++) {
+        const uint32_t m = masks[k];
+        int64_t T[2] = {0, 0}, A[2] = {0, 0};
+        for (uint32_t z = 0; z < Z; z++)
+            if ((m >> z) & 1u)
+                for (int r = 0; r < 2; r++) {
+                    T[r] += x.tot[r][z];
+                    A[r] += x.avail[r][z];
+                }
+        const int64_t rq0 = (T[0] - A[0] < 0 ? 0 : T[0] - A[0]) + req[0];
+        const int64_t rq1 = (T[1] - A[1] < 0 ? 0 : T[1] - A[1]) + req[1];
+        score[k] = numa_score<true>((c.most & MOST_NUMA_HINT) != 0, c.numa_hint_w_cpu, c.numa_hint_w_mem, T[0], rq0, 0.0,
+                                    T[1], rq1, 0.0);
+        int64_t al[2][MAX_ZONES];
+        if (!numa_split(x, m, req, has, al)) continue;
+        for (int r = 0; r < 2; r++) {
+            if (!has[r] || (m & lack[r])) continue;
+            minsize[r] = min(minsize[r], popc(m));
+            okm[r] |= 1u << k;
+        }
+    }
+    NumaHint L[2][15];
+    int len[2] = {0, 0}, nl = 0, reasons = 0;
+    for (int r = 0; r < 2; r++) {
+        if (!has[r]) continue;
+        const int li = nl++;
+        for (uint32_t k = 0; k < nm; k++) {
+            if (!((okm[r] >> k) & 1u)) continue;
+            const bool pref = popc(masks[k]) == minsize[r] || policy == KG_NUMA_RESTRICTED;
+            if (policy == KG_NUMA_SINGLE_NODE && !(pref && popc(masks[k]) == 1)) continue;  // filterSingleNumaHints
+            L[li][len[li]++] = NumaHint{masks[k], pref, false, score[k]};
+        }
+        if (okm[r] == 0) {
+            reasons++;
+            L[li][len[li]++] = NumaHint{0u, false, true, 0};
+            if (policy == KG_NUMA_SINGLE_NODE) len[li] = 0;  // not preferred: filtered out
+        }
+    }
+    mask_out = 0;
+    if (reasons && policy != KG_NUMA_BEST_EFFORT) return KG_ST_NUMA_UNSATISFIED;
+    const uint32_t all = (1u << Z) - 1u;
+    NumaHint best{all, false, false, 0};
+    if (nl == 0) {
+        numa_merge_one(all, excl, x.status, nullptr, 0, best);
+    } else if (nl == 1) {
+        for (int a = 0; a < len[0]; a++) numa_merge_one(all, excl, x.status, &L[0][a], 1, best);
+    } else {
+        for (int a = 0; a < len[0]; a++)
+            for (int b = 0; b < len[1]; b++) {
+                const NumaHint perm[2] = {L[0][a], L[1][b]};
+                numa_merge_one(all, excl, x.status, perm, 2, best);
+            }
+    }
+    if (policy == KG_NUMA_BEST_EFFORT) {
+        mask_out = best.unsat ? all : best.mask;
+        return 0;
+    }
+    if (!best.pref) return KG_ST_NUMA_ALIGN;
+    mask_out = (policy == KG_NUMA_SINGLE_NODE && best.mask == all) ? 0u : best.mask;
+    return 0;
+}
+
+__device__ __forceinline__ int32_t numa_code(uint32_t mask) {
+    if (!mask) return -1;
+    return popc(mask) == 1 ? (int32_t)(__ffs(mask) - 1) : (int32_t)(0x40u | mask);
+}
+
 // Node quantities a Reservation restore changes for pods of one owner class (kg_rsv_view): the
 // NodeResourcesFit and NodeNUMAResource terms read these instead of the record's int section.
 struct Over {
@@ -134,10 +357,6 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
         return;
     }
     const uint32_t pol = pod_pol != KG_NUMA_NONE ? pod_pol : node_pol;
-    if (pol == KG_NUMA_RESTRICTED || pol == KG_NUMA_BEST_EFFORT) {
-        o.status |= KG_ST_UNSUPPORTED;
-        return;
-    }
     const bool amp = (flags & F_AMP) != 0;
     const int64_t pod_cpu = p.req_cpu;
     // filterAmplifiedCPUs
@@ -151,6 +370,47 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
         }
     }
     const double rcp_cpu = as_f64(n[N_RCP_CPU]), rcp_mem = as_f64(n[N_RCP_MEM]);
+    const bool most = (c.most & MOST_NUMA) != 0;
+    // pods with their own NUMA policy default to the Required exclusive policy (plugin.go:449-454)
+    const bool excl = pod_pol != KG_NUMA_NONE;
+    if (pol == KG_NUMA_RESTRICTED || pol == KG_NUMA_BEST_EFFORT || (pol == KG_NUMA_SINGLE_NODE && excl)) {
+        const uint32_t Z = (flags >> F_NUMA_ZONES_SHIFT) & 15u;
+        if (Z == 0) {
+            o.status |= pol == KG_NUMA_BEST_EFFORT ? KG_ST_UNSUPPORTED : KG_ST_NUMA_NO_RES;
+            return;
+        }
+        NumaZ x;
+        numa_load(zr, Z, x);
+        const int64_t req[2] = {p.req_cpu, p.req_mem};
+        const bool has[2] = {(p.flags & KG_POD_HAS_CPU) != 0, (p.flags & KG_POD_HAS_MEM) != 0};
+        uint32_t mask = 0;
+        const uint32_t st = numa_admit<EXACT>(c, x, req, has, pol, excl, mask);
+        if (st) {
+            o.status |= st;
+            return;
+        }
+        int64_t al[2][MAX_ZONES];
+        if (mask && !numa_split(x, mask, req, has, al)) {
+            o.status |= KG_ST_UNSUPPORTED;  // a BestEffort Reserve that would fail: host path
+            return;
+        }
+        o.zone = numa_code(mask);
+        if (pol == KG_NUMA_BEST_EFFORT || !mask) {
+            o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
+                                         rcp_cpu, n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
+            return;
+        }
+        int64_t T[2] = {0, 0}, U[2] = {0, 0};
+        for (uint32_t z = 0; z < Z; z++) {
+            if (al[0][z] == 0 && al[1][z] == 0) continue;
+            for (int r = 0; r < 2; r++) {
+                T[r] += x.tot[r][z];
+                U[r] += x.used[r][z];
+            }
+        }
+        o.s_numa = numa_score<true>(most, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + pod_cpu, 0.0, T[1], U[1] + p.req_mem, 0.0);
+        return;
+    }
     if (pol == KG_NUMA_SINGLE_NODE) {
         const uint32_t Z = (flags >> F_NUMA_ZONES_SHIFT) & 15u;
         if (Z == 0) {
@@ -169,7 +429,7 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
                 const bool ok = (!has_cpu || (ac != 0 && p.req_cpu <= ac)) && (!has_mem || (am != 0 && p.req_mem <= am));
                 const int64_t rc = tc - ac < 0 ? 0 : tc - ac;
                 const int64_t rm = tm - am < 0 ? 0 : tm - am;
-                const int64_t s = numa_least<EXACT>(c.numa_hint_w_cpu, c.numa_hint_w_mem, tc, rc + p.req_cpu,
+                const int64_t s = numa_score<EXACT>((c.most & MOST_NUMA_HINT) != 0, c.numa_hint_w_cpu, c.numa_hint_w_mem, tc, rc + p.req_cpu,
                                                     zr->rcp_cpu[z], tm, rm + p.req_mem, zr->rcp_mem[z]);
                 const bool take = ok && (best < 0 || s > best_score);
                 best = take ? (int32_t)z : best;
@@ -182,12 +442,12 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
         }
         if (best < 0 || Z == 1) {  // best hint == default affinity: no NUMA allocation
             o.zone = -1;
-            o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
+            o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
                                          rcp_cpu, n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
             return;
         }
         o.zone = best;
-        o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, zr->cpu[best], zr->cpu_used[best] + pod_cpu,
+        o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, zr->cpu[best], zr->cpu_used[best] + pod_cpu,
                                      zr->rcp_cpu[best], zr->mem[best], zr->mem_used[best] + p.req_mem,
                                      zr->rcp_mem[best]);
         return;
@@ -195,7 +455,7 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
     // policy None: scoreWithAmplifiedCPUs
     int64_t req_cpu = nv<OV>(n, ov, N_REQ_CPU);
     if (pod_cpu != 0 && amp) req_cpu = req_cpu - n[N_CPUSET] + n[N_AMP_CPUSET];
-    o.s_numa = numa_least<EXACT>(c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], req_cpu + pod_cpu, rcp_cpu,
+    o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], req_cpu + pod_cpu, rcp_cpu,
                                  n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
 }
 
@@ -321,6 +581,18 @@ __device__ __forceinline__ void apply_assume(const KCfg& c, int64_t* n, ZoneRec*
     if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES) {
         zr->cpu_used[zone] += sign * p.req_cpu;
         zr->mem_used[zone] += sign * p.req_mem;
+    } else if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0x40 && sign > 0) {
+        // a split over several zones, recomputed on the zone state the pair was evaluated on
+        NumaZ x;
+        numa_load(zr, (flags >> F_NUMA_ZONES_SHIFT) & 15u, x);
+        const int64_t req[2] = {p.req_cpu, p.req_mem};
+        const bool has[2] = {(p.flags & KG_POD_HAS_CPU) != 0, (p.flags & KG_POD_HAS_MEM) != 0};
+        int64_t al[2][MAX_ZONES];
+        if (numa_split(x, (uint32_t)zone & 0xFu, req, has, al))
+            for (int z = 0; z < MAX_ZONES; z++) {
+                zr->cpu_used[z] += al[0][z];
+                zr->mem_used[z] += al[1][z];
+            }
     }
     derive_node(*reinterpret_cast<NodeRec*>(n), *zr);
 }

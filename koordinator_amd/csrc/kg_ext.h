@@ -37,8 +37,9 @@ __device__ __forceinline__ int64_t least_score_i64(int64_t requested, int64_t ca
     return ((capacity - requested) * 100) / capacity;
 }
 
-// leastResourceScorer over {gpu-core, gpu-memory-ratio, gpu-memory}: zero totals skipped, requested =
-// total >= free ? total - free + request : total (scoreNode / scoreDevice).
+// leastResourceScorer / mostResourceScorer (deviceshare/scoring.go:263-323) over {gpu-core,
+// gpu-memory-ratio, gpu-memory}: zero totals skipped, requested = total >= free ? total - free +
+// request : total (scoreNode / scoreDevice).
 __device__ __forceinline__ int64_t dev_least(const KCfg& c, const int64_t* total, const int64_t* fr, const int64_t* preq) {
     int64_t score = 0, wsum = 0;
 #pragma unroll
@@ -46,7 +47,7 @@ __device__ __forceinline__ int64_t dev_least(const KCfg& c, const int64_t* total
         const int64_t w = c.dev_w[r];
         if (w == 0 || total[r] == 0) continue;
         const int64_t req = total[r] >= fr[r] ? total[r] - fr[r] + preq[r] : total[r];
-        score += least_score_i64(req, total[r]) * w;
+        score += ((c.most & MOST_DEV) ? most_req(req, total[r]) : least_score_i64(req, total[r])) * w;
         wsum += w;
     }
     return wsum == 0 ? 0 : score / wsum;

@@ -116,6 +116,7 @@ struct alignas(64) ZoneRec {
     int64_t cpu[MAX_ZONES], mem[MAX_ZONES], cpu_used[MAX_ZONES], mem_used[MAX_ZONES];
     double rcp_cpu[MAX_ZONES], rcp_mem[MAX_ZONES];
     ZoneFast zf[MAX_ZONES];
+    uint32_t status;  // NUMANodeSharedStatus, 2 bits per zone (0 idle, 1 single, 2 shared)
 };
 
 // Magnitude bound of the float64 fast path: operands below 2^44 keep 100 * headroom below 2^51
@@ -163,6 +164,9 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
         zf.free_cpu = x100(tc - uc);
         zf.free_mem = x100(tm - um);
     }
+    // Restricted / BestEffort nodes run the general NUMA topology manager on the integer path
+    const uint32_t pol0 = (f >> F_NUMA_POLICY_SHIFT) & 15u;
+    big = big || pol0 == 1u /* KG_NUMA_BEST_EFFORT */ || pol0 == 2u /* KG_NUMA_RESTRICTED */;
     if (big) f |= F_BIG;
     v[N_FLAGS] = (int64_t)(((uint64_t)v[N_FLAGS] & 0xFFFFFFFF00000000ull) | f);
     auto fit = [](int64_t x) { return kg_bits(x100(x < 0 ? 0 : x)); };
@@ -252,7 +256,9 @@ struct KCfg {
     float la_hw;       // 0.5 / la_wsum (0 when la_wsum is 0): fast-path weighted quotient
     int32_t w_dev, w_rsv;
     int32_t dev_w[3];  // DeviceShare LeastAllocated weights {gpu-core, gpu-memory-ratio, gpu-memory}
+    uint32_t most;     // MostAllocated strategies: bit 0 NUMA score, bit 1 NUMA hint score, bit 2 DeviceShare
 };
+enum : uint32_t { MOST_NUMA = 1u, MOST_NUMA_HINT = 2u, MOST_DEV = 4u };
 
 // ---- config-5 side tables (integer path) -----------------------------------------------------------
 constexpr int DEV_MINORS = 8, DEV_R = 3;

@@ -255,6 +255,8 @@ kg_status build_kcfg(kg_ctx* ctx, const kg_config* c, KCfg* k) {
     k->numa_hint_w_cpu = c->numa_hint_w_cpu;
     k->numa_hint_w_mem = c->numa_hint_w_mem;
     k->la_hw = half_rcp(k->la_wsum);
+    k->most = (c->numa_most_allocated ? MOST_NUMA : 0u) | (c->numa_hint_most_allocated ? MOST_NUMA_HINT : 0u) |
+              (c->dev_most_allocated ? MOST_DEV : 0u);
     return KG_OK;
 }
 
@@ -375,6 +377,8 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
         zf.w_score = pack32(fc, fm);
         zf.hpack = pack_f32(half_rcp((hc + hm) / 2), half_rcp((fc + fm) / 2));
     }
+    zr->status = COL(s->numa_zone_status, i);
+    if (zr->status >> (2 * KG_MAX_ZONES)) return fail(ctx, KG_INVALID_ARG, "node %u: zone status 0x%x", i, zr->status);
     derive_node(*rec, *zr);
     return KG_OK;
 }
@@ -553,6 +557,7 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
         s->weights_small = true;
         for (int64_t w : rw) s->weights_small &= (w >= 0 && w <= 4096);
         s->weights_small &= (cfg->la_w[0] + cfg->la_w[1] + cfg->la_dominant_w) <= 4096;
+        s->weights_small &= !cfg->numa_most_allocated && !cfg->numa_hint_most_allocated;  // fast path: LeastAllocated
     }
     s->n = n_nodes;
     s->base = index_base;
@@ -1238,6 +1243,7 @@ kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
+    if (zone >= KG_MAX_ZONES) return fail(ctx, KG_UNSUPPORTED, "Unreserve of a multi-zone NUMA allocation (zone code 0x%x)", zone);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
@@ -1320,6 +1326,8 @@ kg_status kg_assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int
 }
 
 kg_status kg_forget_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone, uint32_t minors) {
+    if (s && zone >= KG_MAX_ZONES)
+        return fail(s->ctx, KG_UNSUPPORTED, "Unreserve of a multi-zone NUMA allocation (zone code 0x%x)", zone);
     return assume_ext(s, p, pod, node, zone, minors, -1, nullptr, nullptr);
 }
 

@@ -224,6 +224,46 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     return cfg, t, p, q, abi.Reservations(views, infos)
 
 
+def topology(n_nodes: int, n_pods: int, seed: int = 0, pod_policy_frac: float = 0.3):
+    """NUMA topology-manager workload: nodes with 1-4 zones under every policy
+    (None / BestEffort / Restricted / SingleNUMANode), zone statuses (idle / single / shared), pods
+    with and without their own NUMA policy and large enough that multi-zone hints are needed."""
+    r = _rng(900 + seed, 0)
+    t = nodes(n_nodes, 900 + seed, numa=True, rng=r)
+    n = n_nodes
+    Z = r.integers(1, 5, n).astype(np.uint32)
+    Z[r.random(n) < 0.03] = 0  # a few nodes without NUMA resources
+    t["numa_zones"] = Z
+    t["numa_policy"] = r.choice([abi.KG_NUMA_NONE, abi.KG_NUMA_BEST_EFFORT, abi.KG_NUMA_RESTRICTED,
+                                 abi.KG_NUMA_SINGLE_NODE], n, p=[0.25, 0.25, 0.25, 0.25]).astype(np.uint32)
+    zs = np.maximum(Z, 1).astype(np.int64)
+    status = np.zeros(n, np.uint32)
+    for z in range(abi.KG_MAX_ZONES):
+        on = z < Z
+        zc = np.where(on, t["alloc_cpu"] // zs, 0)
+        zm = np.where(on, t["alloc_mem"] // zs, 0)
+        t[f"zone_cpu{z}"] = zc
+        t[f"zone_mem{z}"] = zm
+        lvl = r.choice([0.0, 0.3, 0.6, 0.9, 1.0], n)
+        t[f"zone_cpu_used{z}"] = (zc * lvl * r.random(n)).astype(np.int64)
+        t[f"zone_mem_used{z}"] = (zm * lvl * r.random(n)).astype(np.int64)
+        full = r.random(n) < 0.05  # a zone with no cpu left
+        t[f"zone_cpu_used{z}"] = np.where(full & on, zc, t[f"zone_cpu_used{z}"])
+        status |= (np.where(on, r.choice([0, 1, 2], n, p=[0.6, 0.2, 0.2]), 0).astype(np.uint32) << (2 * z))
+    t["numa_zone_status"] = status
+    used_cpu = sum(t[f"zone_cpu_used{z}"] for z in range(abi.KG_MAX_ZONES))
+    used_mem = sum(t[f"zone_mem_used{z}"] for z in range(abi.KG_MAX_ZONES))
+    t["req_cpu"] = np.maximum(t["req_cpu"], used_cpu)
+    t["req_mem"] = np.maximum(t["req_mem"], used_mem)
+    t["nz_cpu"] = np.maximum(t["nz_cpu"], t["req_cpu"])
+    t["nz_mem"] = np.maximum(t["nz_mem"], t["req_mem"])
+    pr = _rng(900 + seed, 1)
+    p = pods(n_pods, 900 + seed, scale=4.0, rng=pr)
+    pol = pr.choice([abi.KG_NUMA_BEST_EFFORT, abi.KG_NUMA_RESTRICTED, abi.KG_NUMA_SINGLE_NODE], n_pods)
+    p["numa_policy"] = np.where(pr.random(n_pods) < pod_policy_frac, pol, abi.KG_NUMA_NONE).astype(np.uint32)
+    return bench_profile(numa=True), t, p
+
+
 def cluster(config: int):
     """(SchedulerConfig, nodes, pods) of a BASELINE configuration (1: 1k x 500, 2: 10k x 10k,
     3: 10k nodes x 50k replay pods, 4: 100k nodes x 10k pods)."""

@@ -1016,12 +1016,14 @@ void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_c
 
 /* resourceAllocationScorer.scoreNode / scoreDevice + leastResourceScorer (deviceshare/scoring.go:197-281):
  * resources with a zero total are skipped; requested = total >= free ? total - free + podRequest : total. */
-static int64_t dev_least(const int64_t* w, const int64_t* total, const int64_t* free_, const int64_t* preq) {
+static int64_t dev_least(const kg_config* c, const int64_t* total, const int64_t* free_, const int64_t* preq) {
+    const int64_t* w = c->dev_w;
     int64_t score = 0, wsum = 0;
     for (int r = 0; r < KG_DEV_R; r++) {
         if (w[r] == 0 || total[r] == 0) continue;
         int64_t req = total[r] >= free_[r] ? total[r] - free_[r] + preq[r] : total[r];
-        score += least_requested_score(req, total[r]) * w[r];
+        /* ScoringStrategy LeastAllocated / MostAllocated (deviceshare/scoring.go:164-181,263-323) */
+        score += (c->dev_most_allocated ? most_requested_score(req, total[r]) : least_requested_score(req, total[r])) * w[r];
         wsum += w[r];
     }
     return wsum == 0 ? 0 : score / wsum;
@@ -1067,7 +1069,7 @@ static uint32_t dev_eval(const kg_config* c, const kg_node_columns* n, uint32_t 
         fit += (uint32_t)dev_minor_fits(fr, preq, keys);
     }
     if (fit < cnt) return KG_ST_DEV_INSUFFICIENT;
-    *raw = dev_least(c->dev_w, T, F, preq);
+    *raw = dev_least(c, T, F, preq);
     return 0;
 }
 
@@ -1083,7 +1085,7 @@ static uint32_t dev_choose(const kg_config* c, const int64_t* total_tab, const i
             t[r] = DEVX(total_tab, i, r, m);
             f[r] = DEVX(free_tab, i, r, m);
         }
-        sc[m] = dev_least(c->dev_w, t, f, preq);
+        sc[m] = dev_least(c, t, f, preq);
         order[m] = m;
     }
     for (int32_t a = 1; a < D; a++) { /* stable insertion sort by score desc (minor asc on ties) */
