@@ -436,7 +436,14 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
                 best_score = take ? s : best_score;
             }
             if (best < 0) {
-                o.status |= KG_ST_NUMA_ALIGN;
+                // no single zone fits: the reason is ErrUnsatisfiedNUMAResource when some requested
+                // resource has no hint at all, else the alignment failure (general merge decides)
+                NumaZ x;
+                numa_load(zr, Z, x);
+                const int64_t req[2] = {p.req_cpu, p.req_mem};
+                const bool has[2] = {has_cpu, has_mem};
+                uint32_t mask = 0;
+                o.status |= numa_admit<EXACT>(c, x, req, has, KG_NUMA_SINGLE_NODE, false, mask);
                 return;
             }
         }
