@@ -308,6 +308,41 @@ __device__ __forceinline__ int32_t numa_code(uint32_t mask) {
     return popc(mask) == 1 ? (int32_t)(__ffs(mask) - 1) : (int32_t)(0x40u | mask);
 }
 
+// The topology manager for one (pod, node) pair: hints, policy merge, the allocation's zone code and
+// the NUMA score (score_node when no allocation is made). Returns 0 or KG_ST_* bits. Out of line: its
+// hint tables are private arrays that would otherwise sit in the frame of every kernel inlining
+// eval_pair.
+__device__ __forceinline__ uint32_t numa_topology(const KCfg* cp, const ZoneRec* zr, uint32_t Z, int64_t req_cpu,
+                                               int64_t req_mem, uint32_t pflags, uint32_t pol, bool excl,
+                                               int64_t score_node, int32_t* zone_out, int64_t* score_out) {
+    const KCfg& c = *cp;
+    NumaZ x;
+    numa_load(zr, Z, x);
+    const int64_t req[2] = {req_cpu, req_mem};
+    const bool has[2] = {(pflags & KG_POD_HAS_CPU) != 0, (pflags & KG_POD_HAS_MEM) != 0};
+    uint32_t mask = 0;
+    const uint32_t st = numa_admit<true>(c, x, req, has, pol, excl, mask);
+    if (st) return st;
+    int64_t al[2][MAX_ZONES];
+    if (mask && !numa_split(x, mask, req, has, al)) return KG_ST_UNSUPPORTED;  // a BestEffort Reserve that would fail: host path
+    *zone_out = numa_code(mask);
+    if (pol == KG_NUMA_BEST_EFFORT || !mask) {
+        *score_out = score_node;
+        return 0;
+    }
+    int64_t T[2] = {0, 0}, U[2] = {0, 0};
+    for (uint32_t z = 0; z < Z; z++) {
+        if (al[0][z] == 0 && al[1][z] == 0) continue;
+        for (int r = 0; r < 2; r++) {
+            T[r] += x.tot[r][z];
+            U[r] += x.used[r][z];
+        }
+    }
+    *score_out = numa_score<true>((c.most & MOST_NUMA) != 0, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + req_cpu, 0.0, T[1],
+                                  U[1] + req_mem, 0.0);
+    return 0;
+}
+
 // Node quantities a Reservation restore changes for pods of one owner class (kg_rsv_view): the
 // NodeResourcesFit and NodeNUMAResource terms read these instead of the record's int section.
 struct Over {
@@ -379,36 +414,18 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             o.status |= pol == KG_NUMA_BEST_EFFORT ? KG_ST_UNSUPPORTED : KG_ST_NUMA_NO_RES;
             return;
         }
-        NumaZ x;
-        numa_load(zr, Z, x);
-        const int64_t req[2] = {p.req_cpu, p.req_mem};
-        const bool has[2] = {(p.flags & KG_POD_HAS_CPU) != 0, (p.flags & KG_POD_HAS_MEM) != 0};
-        uint32_t mask = 0;
-        const uint32_t st = numa_admit<EXACT>(c, x, req, has, pol, excl, mask);
+        const int64_t score_node = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU],
+                                                     nv<OV>(n, ov, N_REQ_CPU) + pod_cpu, rcp_cpu, n[N_ALLOC_MEM],
+                                                     nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
+        int32_t zone = -1;
+        int64_t s = 0;
+        const uint32_t st = numa_topology(&c, zr, Z, p.req_cpu, p.req_mem, p.flags, pol, excl, score_node, &zone, &s);
         if (st) {
             o.status |= st;
             return;
         }
-        int64_t al[2][MAX_ZONES];
-        if (mask && !numa_split(x, mask, req, has, al)) {
-            o.status |= KG_ST_UNSUPPORTED;  // a BestEffort Reserve that would fail: host path
-            return;
-        }
-        o.zone = numa_code(mask);
-        if (pol == KG_NUMA_BEST_EFFORT || !mask) {
-            o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
-                                         rcp_cpu, n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
-            return;
-        }
-        int64_t T[2] = {0, 0}, U[2] = {0, 0};
-        for (uint32_t z = 0; z < Z; z++) {
-            if (al[0][z] == 0 && al[1][z] == 0) continue;
-            for (int r = 0; r < 2; r++) {
-                T[r] += x.tot[r][z];
-                U[r] += x.used[r][z];
-            }
-        }
-        o.s_numa = numa_score<true>(most, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + pod_cpu, 0.0, T[1], U[1] + p.req_mem, 0.0);
+        o.zone = zone;
+        o.s_numa = s;
         return;
     }
     if (pol == KG_NUMA_SINGLE_NODE) {
@@ -438,12 +455,9 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             if (best < 0) {
                 // no single zone fits: the reason is ErrUnsatisfiedNUMAResource when some requested
                 // resource has no hint at all, else the alignment failure (general merge decides)
-                NumaZ x;
-                numa_load(zr, Z, x);
-                const int64_t req[2] = {p.req_cpu, p.req_mem};
-                const bool has[2] = {has_cpu, has_mem};
-                uint32_t mask = 0;
-                o.status |= numa_admit<EXACT>(c, x, req, has, KG_NUMA_SINGLE_NODE, false, mask);
+                int32_t zone = -1;
+                int64_t s = 0;
+                o.status |= numa_topology(&c, zr, Z, p.req_cpu, p.req_mem, p.flags, KG_NUMA_SINGLE_NODE, false, 0, &zone, &s);
                 return;
             }
         }
@@ -560,6 +574,22 @@ __device__ __forceinline__ uint64_t pair_key(const KCfg& c, const PairOut& o, ui
     return o.status ? 0ull : key;
 }
 
+// Reserve of a multi-zone NUMA allocation: the split recomputed on the zone state the pair was
+// evaluated on. Out of line, so that its private arrays stay out of the callers' frames.
+__device__ __forceinline__ void numa_reserve_split(ZoneRec* zr, uint32_t Z, int64_t req_cpu, int64_t req_mem, uint32_t pflags,
+                                                uint32_t mask) {
+    NumaZ x;
+    numa_load(zr, Z, x);
+    const int64_t req[2] = {req_cpu, req_mem};
+    const bool has[2] = {(pflags & KG_POD_HAS_CPU) != 0, (pflags & KG_POD_HAS_MEM) != 0};
+    int64_t al[2][MAX_ZONES];
+    if (numa_split(x, mask, req, has, al))
+        for (int z = 0; z < MAX_ZONES; z++) {
+            zr->cpu_used[z] += al[0][z];
+            zr->mem_used[z] += al[1][z];
+        }
+}
+
 // Reserve (sign = +1) / Unreserve (sign = -1) of pod p on node record n (a16).
 __device__ __forceinline__ void apply_assume(const KCfg& c, int64_t* n, ZoneRec* zr, const PodV& p, int32_t zone,
                                              int64_t sign) {
@@ -589,17 +619,7 @@ __device__ __forceinline__ void apply_assume(const KCfg& c, int64_t* n, ZoneRec*
         zr->cpu_used[zone] += sign * p.req_cpu;
         zr->mem_used[zone] += sign * p.req_mem;
     } else if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0x40 && sign > 0) {
-        // a split over several zones, recomputed on the zone state the pair was evaluated on
-        NumaZ x;
-        numa_load(zr, (flags >> F_NUMA_ZONES_SHIFT) & 15u, x);
-        const int64_t req[2] = {p.req_cpu, p.req_mem};
-        const bool has[2] = {(p.flags & KG_POD_HAS_CPU) != 0, (p.flags & KG_POD_HAS_MEM) != 0};
-        int64_t al[2][MAX_ZONES];
-        if (numa_split(x, (uint32_t)zone & 0xFu, req, has, al))
-            for (int z = 0; z < MAX_ZONES; z++) {
-                zr->cpu_used[z] += al[0][z];
-                zr->mem_used[z] += al[1][z];
-            }
+        numa_reserve_split(zr, (flags >> F_NUMA_ZONES_SHIFT) & 15u, p.req_cpu, p.req_mem, p.flags, (uint32_t)zone & 0xFu);
     }
     derive_node(*reinterpret_cast<NodeRec*>(n), *zr);
 }
@@ -700,7 +720,7 @@ __device__ __forceinline__ KCfg cfg_in_vgprs(const KCfg& c) {
 // PM: enabled plugins (KG_PLUGIN_* mask); CLS: node storage class (node_class), both compile-time.
 template <uint32_t PM, int CLS>
 __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr,
-                                                  const PodF& p, uint32_t gidx) {
+                                                  const PodF& p, uint32_t gidx, int32_t* zone_out = nullptr) {
     const uint32_t f = (uint32_t)r.flags;
     bool ok = true;
     uint32_t total = 0;
@@ -776,6 +796,7 @@ __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& 
             const uint32_t sc = lr100(r.numa_free_cpu, p.cpu, r.rcp_cpu), sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
             const uint32_t node_level = wq(mad24(sm, hi32(r.w_numa), mad24(sc, lo32(r.w_numa), 1u)), f32lo(r.w_aux));
             s_numa = (!has_any || Z == 1) ? node_level : best_score;
+            if (zone_out) *zone_out = (skip || !has_any || Z == 1) ? -1 : best;  // the Reserve's zone (eval_pair o.zone)
         } else {
             // amplified requested for pods with a cpu request: (free - r) + delta * {0, 1}
             const uint32_t sc = cvt_sat_u32(fma(r.amp_delta, p.has_cpu, r.numa_free_cpu - p.cpu) * r.rcp_cpu);

@@ -25,6 +25,30 @@ struct LaunchSelect {
     uint64_t* partial;
 };
 
+// Block replay (k_rb_top / k_rb_merge / k_rb_fix): window of RB_W pods, RB_K keys kept per pod,
+// changed-row bitmap in LDS (snapshots up to 32 x RB_BITMAP_WORDS records).
+constexpr int RB_W = 64;
+constexpr int RB_K = 16;
+constexpr int RB_BITMAP_WORDS = 8192;
+constexpr int RB_CHUNK = 32;  // records per k_rb_top wave (fast blocks staged in LDS)
+
+struct LaunchRb {
+    const NodeRec* nodes;
+    const ZoneRec* zones;
+    NodeRec* nodes_rw;
+    ZoneRec* zones_rw;
+    PodsDev pods;
+    uint32_t n_pods, n_nodes, index_base, n_parts;
+    SelectRange range[2];
+    bool exact, fast;
+    KCfg cfg;
+    const uint32_t* pos;  // snapshot index -> record
+    uint32_t* step;       // next pod to place
+    uint64_t* partial;    // [n_parts][RB_W][RB_K]
+    uint64_t* tops;       // [RB_W][RB_K]
+    uint64_t* winners;
+};
+
 struct VerifyDev {
     uint32_t* status;
     int64_t *s_nrf, *s_la, *s_numa, *total;
@@ -74,6 +98,7 @@ hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pod
                               uint32_t index_base, const KCfg& cfg, bool exact, const uint32_t* step_base,
                               uint32_t step_off, uint64_t* winners, int8_t* zsel, hipStream_t s);
 hipError_t launch_bump(uint32_t* step_base, uint32_t by, hipStream_t s);
+hipError_t launch_rb_window(const LaunchRb& a, hipStream_t s);
 hipError_t launch_assume(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t pod, uint32_t node,
                          int32_t zone, int64_t sign, const KCfg& cfg, bool exact, int32_t* zone_out, hipStream_t s);
 

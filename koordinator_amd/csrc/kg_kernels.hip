@@ -168,6 +168,30 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return v;
 }
 
+// Ordering of LDS accesses between the lanes of a one-wave workgroup: the LDS serves a wave's
+// operations in order, so waiting for this wave's own LDS operations is enough. Unlike
+// __syncthreads(), it leaves the wave's global loads (row prefetches) and stores in flight.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Wave max by DPP (row-local steps, then row broadcasts; result read from lane 63). Call with all
+// 64 lanes active.
+__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));  // row_mirror
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// max of 64-bit selection keys: the high halves (totals), then the low halves of the lanes that hold it
+__device__ __forceinline__ uint64_t wave_max_key(uint64_t k) {
+    const uint32_t hi = wave_max_u32_dpp((uint32_t)(k >> 32));
+    const uint32_t lo = wave_max_u32_dpp((uint32_t)(k >> 32) == hi ? (uint32_t)k : 0u);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Step `step` of the sequential replay: Assume(pod step-1 -> its winner), then evaluate pod `step`.
 // One wave per workgroup (no LDS, no barrier): lane = node record. The zone each lane chose for its
 // node in the previous step is kept in zsel, so the winner's Reserve needs no re-evaluation; the
@@ -217,6 +241,311 @@ __global__ void k_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zone
     }
     apply_assume(cfg, n, zones + node, q, zone, sign);
     if (zone_out) *zone_out = zone;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Block replay (config 3): the pods of a window [base, base + RB_W) are placed one by one, exactly as
+// the sequential replay places them, from one matrix pass over the window. A placement changes the
+// row of its winner only, and every config-3 plugin scores a pair from that pair's row alone, so for
+// pod base + t only the nodes already chosen in the window (the set C, at most t rows) can have new
+// keys; every other node keeps the key the window pass computed. The pass keeps each pod's top RB_K
+// keys; pod base + t's best unchanged node is the first of them outside C, unless all RB_K are in C
+// (the window ends before that pod: the next window starts there). k_rb_fix re-evaluates C plus
+// that candidate on the updated rows, staged in LDS, and applies the Assume.
+
+// Integer-path key of one pair, out of line: keeps the fast loops' register allocation free of the
+// integer path's (records flagged F_BIG are rare).
+template <bool EXACT>
+__device__ __forceinline__ uint64_t int_key(const KCfg& cfg, const int64_t* n, const ZoneRec* zr, const PodV& p, uint32_t g) {
+    return pair_key(cfg, eval_pair<EXACT>(cfg, n, zr, p), g);
+}
+
+// Pass 1: per-(chunk, pod) top-RB_K over node records [begin, end); lane = pod of the window. Each
+// wave first stages its chunk's fast blocks (and zone tables for SingleNUMANode records) in LDS with
+// all lanes, so the walk pays one memory latency instead of one per record.
+template <bool EXACT, bool FAST, int CLS>
+__global__ __launch_bounds__(64) void k_rb_top(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                               PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
+                                               uint32_t chunk, uint32_t part0, uint32_t index_base, KCfg cfg,
+                                               const uint32_t* __restrict__ step, uint64_t* __restrict__ partial) {
+    __shared__ FastRec sfr[FAST ? RB_CHUNK : 1];
+    __shared__ ZoneRec szr[(FAST && CLS == 1) ? RB_CHUNK : 1];
+    const uint32_t base = *step;
+    if (base >= n_pods) return;  // uniform: batch done
+    const uint32_t t = threadIdx.x, j = base + t;
+    const bool live = j < n_pods;
+    const PodV p = load_pod(pods, live ? j : base);
+    uint64_t top[RB_K];
+#pragma unroll
+    for (int k = 0; k < RB_K; k++) top[k] = 0;
+    const uint32_t lo = begin + blockIdx.x * chunk;
+    const uint32_t hi = min(end, lo + chunk);
+    if constexpr (FAST) {
+        const uint32_t n = hi - lo;  // <= RB_CHUNK (host)
+        constexpr uint32_t QF = sizeof(FastRec) / 16, QZ = sizeof(ZoneRec) / 16;
+        for (uint32_t q = t; q < n * QF; q += 64u)
+            reinterpret_cast<uint4*>(sfr)[q] = reinterpret_cast<const uint4*>(&nodes[lo + q / QF].v[FAST_BEGIN])[q % QF];
+        if constexpr (CLS == 1)
+            for (uint32_t q = t; q < n * QZ; q += 64u)
+                reinterpret_cast<uint4*>(szr)[q] = reinterpret_cast<const uint4*>(&zones[lo + q / QZ])[q % QZ];
+        __syncthreads();
+        const PodF pf = to_podf(p, cfg);
+        const KCfg cv = cfg_in_vgprs(cfg);
+        for (uint32_t x = 0; x < n; x++) {
+            const FastRec& r = sfr[x];
+            const uint32_t f = (uint32_t)r.flags;
+            const uint32_t g = index_base + (uint32_t)((uint64_t)r.flags >> 32);
+            uint64_t key;
+            if (f & F_BIG)  // uniform branch: lane = pod, the record is the wave's
+                key = int_key<false>(cfg, nodes[lo + x].v, zones + lo + x, p, g);
+            else
+                key = eval_fast_key<7u, CLS>(cv, r, CLS == 1 ? &szr[x] : zones + lo + x, pf, g);
+            if (key > top[RB_K - 1]) topk_insert<RB_K>(top, key);
+        }
+    } else {
+        for (uint32_t i = lo; i < hi; i++) {
+            const uint64_t key = pair_key(cfg, eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p), rec_gidx(nodes[i], index_base));
+            if (key > top[RB_K - 1]) topk_insert<RB_K>(top, key);
+        }
+    }
+    uint64_t* dst = partial + ((size_t)(part0 + blockIdx.x) * RB_W + t) * RB_K;
+#pragma unroll
+    for (int k = 0; k < RB_K; k++) dst[k] = live ? top[k] : 0ull;
+}
+
+// Pass 2: per pod of the window (one workgroup each), top-RB_K over the chunk lists.
+__global__ __launch_bounds__(256) void k_rb_merge(const uint64_t* __restrict__ partial, uint32_t n_parts, uint32_t n_pods,
+                                                  const uint32_t* __restrict__ step, uint64_t* __restrict__ tops) {
+    __shared__ uint64_t cand[4 * RB_K];
+    const uint32_t base = *step;
+    if (base >= n_pods) return;
+    const uint32_t t = blockIdx.x, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint64_t top[RB_K];
+#pragma unroll
+    for (int k = 0; k < RB_K; k++) top[k] = 0;
+    for (uint32_t c = threadIdx.x; c < n_parts; c += blockDim.x) {
+        const uint64_t* src = partial + ((size_t)c * RB_W + t) * RB_K;
+        uint64_t in[RB_K];
+#pragma unroll
+        for (int k = 0; k < RB_K; k++) in[k] = src[k];  // one wait for the whole list
+#pragma unroll
+        for (int k = 0; k < RB_K; k++) {
+            if (in[k] <= top[RB_K - 1]) break;  // lists are sorted: the rest is smaller
+            topk_insert<RB_K>(top, in[k]);
+        }
+    }
+    // wave: RB_K rounds of max extraction (keys are unique: the node index is in the low half)
+    for (int r = 0; r < RB_K; r++) {
+        const uint64_t m = wave_max_key(top[0]);
+        if (m != 0 && top[0] == m) {
+#pragma unroll
+            for (int k = 0; k < RB_K - 1; k++) top[k] = top[k + 1];
+            top[RB_K - 1] = 0;
+        }
+        if (lane == 0) cand[w * RB_K + r] = m;
+    }
+    __syncthreads();
+    if (w == 0) {
+        uint64_t v = cand[lane];  // 4 waves x RB_K = 64 candidates
+        for (int r = 0; r < RB_K; r++) {
+            const uint64_t m = wave_max_key(v);
+            if (m != 0 && v == m) v = 0;
+            if (lane == 0) tops[t * RB_K + r] = m;
+        }
+    }
+}
+
+// Integer-path key and zone of one pair, out of line: rows flagged F_BIG and the integer variant.
+// Keeps the integer path's registers and private arrays out of the window loop.
+template <bool EXACT>
+__device__ __forceinline__ uint64_t rb_int_eval(const KCfg* cfg, const NodeRec* n, const ZoneRec* zr, PodV p, uint32_t g,
+                                             int32_t* zone) {
+    const PairOut o = eval_pair<EXACT>(*cfg, n->v, zr, p);
+    *zone = o.zone;
+    return pair_key(*cfg, o, g);
+}
+
+// Pass 3 (one wave, lane = pod base + lane of the window): the sequential placements of the window.
+// Rows of C (the nodes placed on so far in this window) live in LDS slots [0, nc), and ckey[c][t] holds
+// pod t's key on slot c as the row is now. Pod t's winner is the larger of its best key over C (a
+// column read and a DPP max) and its candidate: the first entry of its list outside C, whose key the
+// window pass computed on an unchanged row. After the Assume, the one changed row is re-evaluated
+// for every later pod of the window at once (lane = pod, row uniform). While pod t is placed, the
+// rows of the first two entries of pod t+1's list outside C are loaded into registers: whichever
+// node pod t takes, pod t+1's candidate is one of them. FAST: keys from the float64 fast path (rows
+// not flagged F_BIG), else the integer path. Ends by writing the rows of C back and advancing *step.
+template <bool EXACT, bool FAST>
+__global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, PodsDev pods,
+                                               uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, KCfg cfg,
+                                               const uint32_t* __restrict__ pos, const uint64_t* __restrict__ tops,
+                                               uint32_t* __restrict__ step, uint64_t* __restrict__ winners) {
+    __shared__ NodeRec snode[RB_W];
+    __shared__ ZoneRec szone[RB_W];
+    __shared__ uint32_t changed[RB_BITMAP_WORDS];
+    __shared__ uint32_t crec[RB_W];
+    __shared__ uint64_t skey[RB_W * RB_K];
+    __shared__ uint32_t srec[RB_W * RB_K];
+    __shared__ uint64_t ckey[RB_W][RB_W];  // [slot][pod]
+    __shared__ int8_t czone[RB_W][RB_W];
+    __shared__ KCfg scfg;  // for the out-of-line integer path
+    constexpr uint32_t NN = sizeof(NodeRec) / 16, NZ = sizeof(ZoneRec) / 16, NQ = NN + NZ;  // 16-B pieces
+    static_assert(NQ <= 128, "row staging: two pieces per lane");
+    const uint32_t lane = threadIdx.x;
+    const uint32_t base = *step;
+    if (base >= n_pods) return;  // uniform
+    const uint32_t words = (n_nodes + 31u) >> 5;
+    for (uint32_t w = lane; w < words; w += 64u) changed[w] = 0;
+    const bool live = base + lane < n_pods;
+    const PodV mp = load_pod(pods, live ? base + lane : base);  // this lane's pod
+    {
+        uint64_t kk[RB_K];
+#pragma unroll
+        for (int k = 0; k < RB_K; k++) kk[k] = tops[lane * RB_K + k];
+        uint32_t rr[RB_K];
+#pragma unroll
+        for (int k = 0; k < RB_K; k++)  // branch-free index: the RB_K loads are in flight together
+            rr[k] = pos[kk[k] ? 0xFFFFFFFFu - (uint32_t)(kk[k] & 0xFFFFFFFFull) - index_base : 0u];
+#pragma unroll
+        for (int k = 0; k < RB_K; k++) {
+            skey[lane * RB_K + k] = kk[k];
+            srec[lane * RB_K + k] = kk[k] ? rr[k] : 0u;
+        }
+    }
+    if (lane == 0) scfg = cfg;
+    __syncthreads();
+    const KCfg cv = cfg_in_vgprs(cfg);
+    const PodF mpf = to_podf(mp, cfg);
+    // key and zone of this lane's pod on slot s (row uniform across the wave)
+    auto eval_slot = [&](uint32_t s, int32_t* zone) -> uint64_t {
+        const uint32_t f = (uint32_t)snode[s].v[N_FLAGS];
+        const uint32_t g = index_base + node_index(snode[s]);
+        if (FAST && !(f & F_BIG)) {
+            const FastRec& r = *reinterpret_cast<const FastRec*>(&snode[s].v[FAST_BEGIN]);
+            *zone = -1;
+            if (node_class(snode[s]) == 1) return eval_fast_key<7u, 1>(cv, r, &szone[s], mpf, g, zone);
+            return eval_fast_key<7u, 0>(cv, r, &szone[s], mpf, g);
+        }
+        return rb_int_eval<EXACT>(&scfg, &snode[s], &szone[s], mp, g, zone);
+    };
+    auto piece = [&](uint32_t r, uint32_t q) -> uint4 {
+        return q < NN ? reinterpret_cast<const uint4*>(&nodes[r])[q] : reinterpret_cast<const uint4*>(&zones[r])[q - NN];
+    };
+    auto put = [&](uint32_t slot, uint32_t q, uint4 v) {
+        if (q < NN) reinterpret_cast<uint4*>(&snode[slot])[q] = v;
+        else reinterpret_cast<uint4*>(&szone[slot])[q - NN] = v;
+    };
+    // prefetched rows: two candidates (e1, e2) of the next pod, two pieces per lane each
+    // (named registers, not arrays: a dynamically indexed private array would live in scratch)
+    uint32_t rec1 = 0, rec2 = 0;
+    int k1 = -1, k2 = -1;
+    uint4 pa1 = {}, pb1 = {}, pa2 = {}, pb2 = {};
+    auto prefetch = [&](uint32_t t) {
+        const uint64_t ck = lane < (uint32_t)RB_K ? skey[t * RB_K + lane] : 0ull;
+        const uint32_t rec = lane < (uint32_t)RB_K ? srec[t * RB_K + lane] : 0u;
+        uint64_t m = __ballot(ck != 0ull && ((changed[rec >> 5] >> (rec & 31u)) & 1u) == 0u);
+        k1 = m ? (int)(__ffsll((long long)m) - 1) : -1;
+        if (m) m &= m - 1;
+        k2 = m ? (int)(__ffsll((long long)m) - 1) : -1;
+        rec1 = (uint32_t)__builtin_amdgcn_readlane((int)rec, k1 >= 0 ? k1 : 0);
+        rec2 = (uint32_t)__builtin_amdgcn_readlane((int)rec, k2 >= 0 ? k2 : 0);
+        if (k1 >= 0) {
+            pa1 = piece(rec1, lane);
+            if (lane + 64u < NQ) pb1 = piece(rec1, lane + 64u);
+        }
+        if (k2 >= 0) {
+            pa2 = piece(rec2, lane);
+            if (lane + 64u < NQ) pb2 = piece(rec2, lane + 64u);
+        }
+    };
+#ifdef KG_RB_CLOCKS
+    uint64_t ck_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t ck_prev = wall_clock64();
+#define RB_TICK(i) do { const uint64_t now_ = wall_clock64(); ck_t[i] += now_ - ck_prev; ck_prev = now_; } while (0)
+#else
+#define RB_TICK(i) do { } while (0)
+#endif
+    prefetch(0);
+    RB_TICK(7);
+    uint32_t nc = 0, done = 0, last = 0xFFFFFFFFu;  // last: the record the previous pod added to C
+    for (uint32_t t = 0; t < (uint32_t)RB_W && base + t < n_pods; t++) {
+        const uint32_t j = base + t;
+        // candidate: e1 unless the previous pod just took it
+        const bool second = k1 >= 0 && rec1 == last;
+        const int ck_k = second ? k2 : k1;
+        const bool has_cand = ck_k >= 0;
+        const bool full = skey[t * RB_K + RB_K - 1] != 0ull;
+        if (!has_cand && full) break;  // every listed node changed: this pod starts the next window
+        const uint32_t cand = second ? rec2 : rec1;
+        const uint64_t cand_key = has_cand ? skey[t * RB_K + ck_k] : 0ull;
+        const uint4 cpre0 = second ? pa2 : pa1, cpre1 = second ? pb2 : pb1;
+        // pod t+1's first two entries outside C_t: their rows load while pod t is placed
+        if (t + 1 < (uint32_t)RB_W && j + 1 < n_pods) prefetch(t + 1);
+        RB_TICK(0);
+        // best key over C
+        const uint64_t kc = lane < nc ? ckey[lane][t] : 0ull;
+        const uint64_t best_c = wave_max_key(kc);
+        const uint64_t best = best_c > cand_key ? best_c : cand_key;
+        last = 0xFFFFFFFFu;
+        RB_TICK(1);
+        if (best != 0ull) {
+            uint32_t slot;
+            int32_t zone;
+            if (best == cand_key) {  // the candidate wins: it joins C in slot nc
+                slot = nc;
+                put(slot, lane, cpre0);
+                if (lane + 64u < NQ) put(slot, lane + 64u, cpre1);
+                if (lane == 0) {
+                    crec[slot] = cand;
+                    changed[cand >> 5] |= 1u << (cand & 31u);
+                }
+                wave_lds_sync();
+                // pod t's zone on the candidate (class-0 rows on the fast path never allocate one)
+                const uint32_t cf = (uint32_t)snode[slot].v[N_FLAGS];
+                int32_t z = -1;
+                if (!(FAST && !(cf & F_BIG) && node_class(snode[slot]) == 0) && lane == t) eval_slot(slot, &z);
+                zone = __shfl(z, (int)t, 64);
+                last = cand;
+                nc++;
+            } else {
+                slot = (uint32_t)(__ffsll((long long)__ballot(lane < nc && kc == best)) - 1);
+                zone = czone[slot][t];
+            }
+            RB_TICK(2);
+            if (lane == t) apply_assume(cfg, snode[slot].v, &szone[slot], mp, zone, 1);  // lane t holds pod t
+            wave_lds_sync();
+            RB_TICK(3);
+            // later pods of the window on the changed row
+            if (lane > t && live) {
+                int32_t z = -1;
+                ckey[slot][lane] = eval_slot(slot, &z);
+                czone[slot][lane] = (int8_t)z;
+            }
+            RB_TICK(4);
+        }
+        if (lane == 0) winners[j] = best;
+        wave_lds_sync();
+        RB_TICK(5);
+        done = t + 1;
+    }
+    // write the changed rows back
+    for (uint32_t s2 = 0; s2 < nc; s2++) {
+        const uint32_t r = crec[s2];
+        uint4* dn = reinterpret_cast<uint4*>(&nodes[r]);
+        uint4* dz = reinterpret_cast<uint4*>(&zones[r]);
+        const uint4* sn = reinterpret_cast<const uint4*>(&snode[s2]);
+        const uint4* sz = reinterpret_cast<const uint4*>(&szone[s2]);
+        for (uint32_t q = lane; q < NQ; q += 64u) {
+            if (q < NN) dn[q] = sn[q];
+            else dz[q - NN] = sz[q - NN];
+        }
+    }
+    if (lane == 0) *step = base + done;
+#ifdef KG_RB_CLOCKS
+    RB_TICK(6);
+    if (lane == 0 && base < 400)
+        printf("rb_fix base %u done %u nc %u ticks pick %lu max %lu stage %lu apply %lu reeval %lu book %lu tail %lu head %lu\n",
+               base, done, nc, ck_t[0], ck_t[1], ck_t[2], ck_t[3], ck_t[4], ck_t[5], ck_t[6], ck_t[7]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -323,6 +652,34 @@ hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pod
     else
         k_replay<false><<<grid, block, 0, s>>>(nodes, zones, pods, n_pods, n_nodes, index_base, cfg, step_base,
                                                step_off, winners, zsel);
+    return KG_LAUNCH_CHECK();
+}
+
+template <bool EXACT, bool FAST, int CLS>
+static void rb_top_instance(const LaunchRb& a, const SelectRange& r, hipStream_t s) {
+    k_rb_top<EXACT, FAST, CLS><<<r.n_chunks, 64, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end, r.chunk,
+                                                         r.part0, a.index_base, a.cfg, a.step, a.partial);
+}
+
+hipError_t launch_rb_window(const LaunchRb& a, hipStream_t s) {
+    for (int cls = 0; cls < 2; cls++) {
+        const SelectRange& r = a.range[cls];
+        if (r.n_chunks == 0) continue;
+        if (a.exact) rb_top_instance<true, false, 0>(a, r, s);
+        else if (a.fast && cls == 0) rb_top_instance<false, true, 0>(a, r, s);
+        else if (a.fast) rb_top_instance<false, true, 1>(a, r, s);
+        else rb_top_instance<false, false, 0>(a, r, s);
+    }
+    k_rb_merge<<<RB_W, 256, 0, s>>>(a.partial, a.n_parts, a.n_pods, a.step, a.tops);
+    if (a.exact)
+        k_rb_fix<true, false><<<1, 64, 0, s>>>(a.nodes_rw, a.zones_rw, a.pods, a.n_pods, a.n_nodes, a.index_base, a.cfg,
+                                               a.pos, a.tops, a.step, a.winners);
+    else if (a.fast)
+        k_rb_fix<false, true><<<1, 64, 0, s>>>(a.nodes_rw, a.zones_rw, a.pods, a.n_pods, a.n_nodes, a.index_base, a.cfg,
+                                               a.pos, a.tops, a.step, a.winners);
+    else
+        k_rb_fix<false, false><<<1, 64, 0, s>>>(a.nodes_rw, a.zones_rw, a.pods, a.n_pods, a.n_nodes, a.index_base, a.cfg,
+                                                a.pos, a.tops, a.step, a.winners);
     return KG_LAUNCH_CHECK();
 }
 

@@ -54,6 +54,7 @@ struct kg_snap {
     ZoneRec* d_zones = nullptr;
     uint32_t* d_big = nullptr;  // [0] = count, [1..] = list of F_BIG records (k_big_scan)
     int8_t* d_zsel = nullptr;   // replay: NUMA zone each record chose for the current pod
+    uint32_t* d_pos = nullptr;  // snapshot index -> record position (block replay)
     // Records are stored grouped by storage class (node_class: 0 = no per-zone scoring, 1 = NUMA
     // SingleNUMANode), each group in ascending snapshot index; the high half of v[N_FLAGS] holds the snapshot index.
     std::vector<NodeRec> h_nodes;  // device order
@@ -123,6 +124,13 @@ struct kg_pods {
     // replay graph (G steps) cached for the (snapshot buffers, batch size, configuration) it captured
     hipGraphExec_t rexec = nullptr;
     std::vector<uint8_t> rkey;
+    // block replay: per-window chunk lists and merged lists, graph of RB_R windows
+    uint64_t* d_rbpart = nullptr;
+    size_t rbpart_cap = 0;  // entries
+    uint64_t* d_rbtops = nullptr;
+    hipGraphExec_t bexec = nullptr;
+    std::vector<uint8_t> bkey;
+    LaunchRb rb_args{};
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -403,6 +411,18 @@ bool force_exact() {
     return v == 1;
 }
 
+// KG_REPLAY_STEP=1: replay one pod per launch (k_replay) instead of by windows (k_rb_*)
+bool force_step_replay() {
+    const char* e = std::getenv("KG_REPLAY_STEP");  // read per call: tests switch it per case
+    return e && e[0] == '1';
+}
+
+// KG_REPLAY_NOGRAPH=1: window replay by direct launches (kernel tracers that cannot follow graphs)
+bool replay_no_graph() {
+    const char* e = std::getenv("KG_REPLAY_NOGRAPH");
+    return e && e[0] == '1';
+}
+
 // KG_SELECT_INT=1: select kernel on the integer path only (A/B and parity checks of the fast path)
 bool force_int() {
     static int v = -1;
@@ -568,6 +588,7 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
     if (hipMalloc(&s->d_nodes, nb) != hipSuccess || hipMalloc(&s->d_zones, zb) != hipSuccess ||
         hipMalloc(&s->d_big, sizeof(uint32_t) * ((size_t)n_nodes + 1)) != hipSuccess ||
         hipMalloc(&s->d_zsel, std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
+        hipMalloc(&s->d_pos, sizeof(uint32_t) * std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
         hipMemset(s->d_big, 0, sizeof(uint32_t)) != hipSuccess) {
         hipFree(s->d_nodes);
         hipFree(s->d_zones);
@@ -602,6 +623,7 @@ kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
     }
     place_records(s, recs, zrs, dev ? &devs : nullptr);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_pos, s->pos.data(), sizeof(uint32_t) * s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
     if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, s->h_dev.data(), sizeof(DevRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
@@ -653,6 +675,7 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
             if (dev) alld[rows[k]] = devs[k];
         }
         place_records(s, all, allz, dev ? &alld : nullptr);
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_pos, s->pos.data(), sizeof(uint32_t) * s->n, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, s->h_dev.data(), sizeof(DevRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
@@ -725,6 +748,7 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_zones);
     hipFree(s->d_big);
     hipFree(s->d_zsel);
+    hipFree(s->d_pos);
     hipFree(s->d_dev);
     hipFree(s->d_qlim);
     hipFree(s->d_qstate);
@@ -868,8 +892,11 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst, (void*)p->d_dev_max,
                     (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout})
         hipFree(b);
+    hipFree(p->d_rbpart);
+    hipFree(p->d_rbtops);
     if (p->rexec) hipGraphExecDestroy(p->rexec);
     if (p->xexec) hipGraphExecDestroy(p->xexec);
+    if (p->bexec) hipGraphExecDestroy(p->bexec);
     delete p;
     return KG_OK;
 }
@@ -1157,6 +1184,79 @@ kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact) {
     return KG_OK;
 }
 
+constexpr uint32_t RB_R = 8;  // replay windows per captured graph
+
+// Window replay: RB_R windows of (k_rb_top per storage class, k_rb_merge, k_rb_fix) per graph; each
+// window reads the next pod to place from p->d_step and advances it by 1..RB_W pods.
+kg_status rb_graph(kg_snap* s, kg_pods* p, bool exact) {
+    kg_ctx* ctx = s->ctx;
+    LaunchRb a{};
+    a.nodes = s->d_nodes;
+    a.zones = s->d_zones;
+    a.nodes_rw = s->d_nodes;
+    a.zones_rw = s->d_zones;
+    a.pods = p->dev;
+    a.n_pods = p->n;
+    a.n_nodes = s->n;
+    a.index_base = s->base;
+    const uint32_t bounds[3] = {0, s->n0, s->n};
+    const uint32_t chunk = RB_CHUNK;
+    uint32_t n_parts = 0;
+    for (int c = 0; c < 2; c++) {
+        SelectRange& r = a.range[c];
+        r.begin = bounds[c];
+        r.end = bounds[c + 1];
+        r.chunk = chunk;
+        r.n_chunks = (r.end - r.begin + chunk - 1) / chunk;
+        r.part0 = n_parts;
+        n_parts += r.n_chunks;
+    }
+    a.n_parts = n_parts;
+    a.exact = exact;
+    a.fast = !exact && !force_int() && s->weights_small && p->fast_ok && (s->kcfg.plugins & 7u) == 7u;
+    a.cfg = s->kcfg;
+    a.pos = s->d_pos;
+    a.step = p->d_step;
+    a.winners = p->d_winners;
+    const size_t need = (size_t)std::max<uint32_t>(n_parts, 1) * RB_W * RB_K;
+    if (p->rbpart_cap < need) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        hipFree(p->d_rbpart);
+        p->d_rbpart = nullptr;
+        p->rbpart_cap = 0;
+        HIP_TRY(ctx, hipMalloc(&p->d_rbpart, sizeof(uint64_t) * need));
+        p->rbpart_cap = need;
+    }
+    if (!p->d_rbtops) HIP_TRY(ctx, hipMalloc(&p->d_rbtops, sizeof(uint64_t) * RB_W * RB_K));
+    a.partial = p->d_rbpart;
+    a.tops = p->d_rbtops;
+    p->rb_args = a;
+    std::vector<uint8_t> key = replay_key(s, p, exact);
+    auto put = [&key](const void* x, size_t n) { key.insert(key.end(), (const uint8_t*)x, (const uint8_t*)x + n); };
+    put(&s->d_pos, sizeof(s->d_pos));
+    put(&s->n0, sizeof(s->n0));
+    put(&a.fast, sizeof(a.fast));
+    put(&p->d_rbpart, sizeof(p->d_rbpart));
+    put(&p->d_rbtops, sizeof(p->d_rbtops));
+    if (p->bexec && key == p->bkey) return KG_OK;
+    if (p->bexec) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        hipGraphExecDestroy(p->bexec);
+        p->bexec = nullptr;
+    }
+    hipGraph_t graph = nullptr;
+    HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = hipSuccess;
+    for (uint32_t t = 0; t < RB_R && e == hipSuccess; t++) e = launch_rb_window(a, ctx->stream);
+    hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    if (e == hipSuccess) e = ec;
+    if (e == hipSuccess) e = hipGraphInstantiate(&p->bexec, graph, nullptr, nullptr, 0);
+    if (graph) hipGraphDestroy(graph);
+    HIP_TRY(ctx, e);
+    p->bkey = std::move(key);
+    return KG_OK;
+}
+
 // config-5 replay steps (DeviceShare minors, ElasticQuota used, NormalizeScore via score buckets)
 kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact) {
     kg_ctx* ctx = s->ctx;
@@ -1193,6 +1293,27 @@ extern "C" {
 
 static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total);
 
+// Test aid (not part of include/koordgpu.h): run ONE replay window from pod 0 and return its merged
+// per-pod key lists [RB_W][RB_K], the number of pods it placed and their winner keys.
+kg_status kg_debug_rb_window(kg_snap* s, kg_pods* p, uint64_t* lists, uint32_t* placed, uint64_t* winners) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    st = rb_graph(s, p, force_exact());
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (p->n + 1), ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
+    HIP_TRY(ctx, launch_rb_window(p->rb_args, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(lists, p->d_rbtops, sizeof(uint64_t) * RB_W * RB_K, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(placed, p->d_step, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(winners, p->d_winners, sizeof(uint64_t) * std::min<uint32_t>(p->n, RB_W), hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
 kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
@@ -1202,15 +1323,34 @@ kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_tota
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint32_t n = p->n;
     const bool exact = force_exact();
-    st = replay_graph(s, p, exact);
+    // window replay needs the changed-row bitmap in LDS; every config-3 plugin scores a pair from its own row
+    const bool windows = !force_step_replay() && s->n <= 32u * (uint32_t)RB_BITMAP_WORDS;
+    st = windows ? rb_graph(s, p, exact) : replay_graph(s, p, exact);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
-    // steps 0..n: step i Assumes pod i-1 and evaluates pod i
-    for (uint32_t done = 0; done <= n; done += REPLAY_G) HIP_TRY(ctx, hipGraphLaunch(p->rexec, ctx->stream));
+    if (windows) {
+        // every window places 1..RB_W pods: launch the windows the remaining pods need at least, then look
+        uint32_t placed = 0;
+        while (placed < n) {
+            const uint32_t before = placed;
+            const uint32_t windows_min = (n - placed + RB_W - 1) / RB_W;
+            if (replay_no_graph()) {  // profiling aid: the same launches, not captured
+                for (uint32_t w = 0; w < windows_min; w++) HIP_TRY(ctx, launch_rb_window(p->rb_args, ctx->stream));
+            } else {
+                for (uint32_t w = 0; w < windows_min; w += RB_R) HIP_TRY(ctx, hipGraphLaunch(p->bexec, ctx->stream));
+            }
+            HIP_TRY(ctx, hipMemcpyAsync(&placed, p->d_step, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            if (placed <= before || placed > n) return fail(ctx, KG_DEVICE_ERROR, "window replay stalled at pod %u", placed);
+        }
+    } else {
+        // steps 0..n: step i Assumes pod i-1 and evaluates pod i
+        for (uint32_t done = 0; done <= n; done += REPLAY_G) HIP_TRY(ctx, hipGraphLaunch(p->rexec, ctx->stream));
+    }
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;

@@ -141,8 +141,12 @@ def test_select_after_replay_uses_device_state(ctx):
     assert np.array_equal(got, oracle_lib.select(kc, st.table(), rest, 4))
 
 
+@pytest.mark.parametrize("mode", ["window", "step"])
 @pytest.mark.parametrize("seed,n_nodes,n_pods,scale", [(12, 400, 900, 10.0), (13, 1000, 3000, 8.0)])
-def test_replay_matches_oracle(ctx, seed, n_nodes, n_pods, scale):
+def test_replay_matches_oracle(ctx, monkeypatch, mode, seed, n_nodes, n_pods, scale):
+    """Both replay drivers: windows of 64 pods (k_rb_*) and one pod per launch (k_replay)."""
+    if mode == "step":
+        monkeypatch.setenv("KG_REPLAY_STEP", "1")
     cfg, nodes, pods = synth.small(n_nodes, n_pods, seed=seed, scale=scale)
     kc = cfg.kg_config()
     snap = engine.Snapshot(ctx, kc, nodes, index_base=7)
@@ -374,3 +378,24 @@ def test_config4_100k_nodes_sampled(ctx):
         parts.append(engine.eval_select(sh, batch, 2))
         sh.close()
     assert np.array_equal(engine.merge_keys(np.stack(parts)), keys)
+
+
+@pytest.mark.parametrize("n_nodes,n_pods,scale", [(150, 2000, 4.0), (3000, 5000, 8.0)])
+def test_window_replay_edge_cases(ctx, n_nodes, n_pods, scale):
+    """Window replay where windows end early (few nodes: every pod's top-16 list is exhausted by the
+    nodes placed earlier in the window), integer-path records (F_BIG) inside the windows, and pods
+    that become unschedulable."""
+    cfg, nodes, pods = synth.small(n_nodes, n_pods, seed=19, scale=scale)
+    nodes = {k: v.copy() for k, v in nodes.items()}
+    nodes["alloc_mem"][:n_nodes // 10] = 1 << 50
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    node, total = engine.replay(snap, engine.PodBatch(ctx, pods))
+    st = oracle_lib.OracleState(kc, nodes)
+    want_node, want_total = st.replay(pods)
+    assert np.array_equal(node, want_node)
+    assert np.array_equal(total, want_total)
+    assert (node < 0).any() and (node >= 0).any()
+    got_state, want_state = snap.read_state(), st.table()
+    for k, v in got_state.items():
+        assert np.array_equal(v, want_state[k]), k
