@@ -376,8 +376,11 @@ struct PairOut {
     int32_t zone;
 };
 
-// NodeNUMAResource Filter + Score for a SingleNUMANode / None node.
-template <bool EXACT, bool OV = false>
+// NodeNUMAResource Filter + Score for a SingleNUMANode / None node. TOPO = false drops the general
+// topology manager (numa_topology) from the instantiation: the host picks it only when no node is
+// Restricted / BestEffort and no pod carries a NUMA policy, and only for select-mode kernels, where a
+// SingleNUMANode pair without a fitting zone just needs some failure bit (the reason is unused).
+template <bool EXACT, bool OV = false, bool TOPO = true>
 __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restrict__ n, const ZoneRec* __restrict__ zr,
                                           const PodV& p, uint32_t flags, PairOut& o, const Over* ov = nullptr) {
     if (p.flags & KG_POD_NUMA_SKIP) return;
@@ -409,6 +412,10 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
     // pods with their own NUMA policy default to the Required exclusive policy (plugin.go:449-454)
     const bool excl = pod_pol != KG_NUMA_NONE;
     if (pol == KG_NUMA_RESTRICTED || pol == KG_NUMA_BEST_EFFORT || (pol == KG_NUMA_SINGLE_NODE && excl)) {
+        if constexpr (!TOPO) {
+            o.status |= KG_ST_UNSUPPORTED;  // unreachable under the host's TOPO selection
+            return;
+        }
         const uint32_t Z = (flags >> F_NUMA_ZONES_SHIFT) & 15u;
         if (Z == 0) {
             o.status |= pol == KG_NUMA_BEST_EFFORT ? KG_ST_UNSUPPORTED : KG_ST_NUMA_NO_RES;
@@ -455,6 +462,10 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             if (best < 0) {
                 // no single zone fits: the reason is ErrUnsatisfiedNUMAResource when some requested
                 // resource has no hint at all, else the alignment failure (general merge decides)
+                if constexpr (!TOPO) {
+                    o.status |= KG_ST_NUMA_ALIGN;
+                    return;
+                }
                 int32_t zone = -1;
                 int64_t s = 0;
                 o.status |= numa_topology(&c, zr, Z, p.req_cpu, p.req_mem, p.flags, KG_NUMA_SINGLE_NODE, false, 0, &zone, &s);
@@ -480,7 +491,7 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
                                  n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
 }
 
-template <bool EXACT, bool OV = false>
+template <bool EXACT, bool OV = false, bool TOPO = true>
 __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __restrict__ n,
                                              const ZoneRec* __restrict__ zr, const PodV& p, const Over* ov = nullptr) {
     PairOut o;
@@ -559,7 +570,7 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
         }
     }
 
-    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT, OV>(c, n, zr, p, flags, o, ov);
+    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT, OV, TOPO>(c, n, zr, p, flags, o, ov);
     if (o.status & (KG_ST_NUMA_MASK | KG_ST_UNSUPPORTED)) o.s_numa = 0;
     if (o.status) o.zone = -1;
     return o;

@@ -384,7 +384,7 @@ struct PairX {
     int64_t s_nrf, s_la, s_numa, s_dev, s_rsv, order;
 };
 
-template <bool EXACT>
+template <bool EXACT, bool TOPO = true>
 __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
                                                const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
                                                uint32_t rec, const PodV& p, const PodX& x, uint32_t qst) {
@@ -409,12 +409,12 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
         ov.nz_cpu = v->nz_cpu;
         ov.nz_mem = v->nz_mem;
         ov.num_pods = v->num_pods;
-        b = eval_pair<EXACT, true>(c, n, zr, p, &ov);
+        b = eval_pair<EXACT, true, TOPO>(c, n, zr, p, &ov);
         const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u;
         if ((c.plugins & KG_PLUGIN_NUMA) && node_pol != KG_NUMA_NONE && !(p.flags & KG_POD_NUMA_SKIP))
             b.status = (b.status & ~(uint32_t)KG_ST_NUMA_MASK) | KG_ST_UNSUPPORTED;  // NUMA restore: host path
     } else {
-        b = eval_pair<EXACT, false>(c, n, zr, p);
+        b = eval_pair<EXACT, false, TOPO>(c, n, zr, p);
     }
     uint32_t st = b.status;
     int64_t dev_raw = 0;

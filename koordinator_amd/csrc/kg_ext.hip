@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void k_ext_verify_fin(uint32_t n_pods, uint32_
 }
 
 // Pass 1: per-pod NormalizeScore inputs over the feasible nodes of records [lo, hi) of chunk blockIdx.y.
-template <bool EXACT>
+template <bool EXACT, bool TOPO>
 __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                    ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
                                                    uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
     uint32_t dmax = 0, rmax = 0;
     uint64_t pk = PREF_NONE;
     for (uint32_t rec = lo; rec < hi; rec++) {
-        const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
         if (r.status) continue;
         dmax = max(dmax, (uint32_t)r.s_dev);
         rmax = max(rmax, (uint32_t)r.s_rsv);
@@ -152,7 +152,7 @@ __device__ __forceinline__ void topk_ins(uint64_t (&top)[K], uint64_t key) {
 }
 
 // Pass 2: weighted totals with the normalised DeviceShare / Reservation terms, top-K per (chunk, pod).
-template <int K, bool EXACT>
+template <int K, bool EXACT, bool TOPO>
 __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                     ExtDev e, PodsDev pods, uint32_t n_pods, uint32_t n_nodes,
                                                     uint32_t chunk, uint32_t index_base, KCfg cfg,
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
     for (int t = 0; t < K; t++) top[t] = 0;
     const uint32_t lo = blockIdx.y * chunk, hi = min(n_nodes, lo + chunk);
     for (uint32_t rec = lo; rec < hi; rec++) {
-        const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
         const uint32_t g = index_base + node_index(nodes[rec]);
         const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
         topk_ins<K>(top, r.status ? 0ull : key);
@@ -347,35 +347,47 @@ hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const E
 
 hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                             const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
-                            const KCfg& cfg, bool exact, const uint32_t* qst, uint32_t* dev_max, uint32_t* rsv_max,
-                            uint64_t* pref, hipStream_t s) {
+                            const KCfg& cfg, bool exact, bool topo, const uint32_t* qst, uint32_t* dev_max,
+                            uint32_t* rsv_max, uint64_t* pref, hipStream_t s) {
     if (n_list == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_list + 255) / 256, (n_nodes + chunk - 1) / chunk);
-    if (exact)
-        k_ext_stats<true><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, chunk, index_base, cfg, qst,
-                                               dev_max, rsv_max, pref);
-    else
-        k_ext_stats<false><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, chunk, index_base, cfg, qst,
-                                                dev_max, rsv_max, pref);
+#define KG_EXT_ST(EX, TP)                                                                                           \
+    k_ext_stats<EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, chunk, index_base, cfg, qst, \
+                                             dev_max, rsv_max, pref)
+    if (exact) {
+        if (topo) KG_EXT_ST(true, true);
+        else KG_EXT_ST(true, false);
+    } else {
+        if (topo) KG_EXT_ST(false, true);
+        else KG_EXT_ST(false, false);
+    }
+#undef KG_EXT_ST
     return hipGetLastError();
 }
 
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                              uint32_t n_pods, uint32_t n_nodes, uint32_t chunk, uint32_t k, uint32_t index_base,
-                             const KCfg& cfg, bool exact, const uint32_t* qst, const uint32_t* dev_max,
+                             const KCfg& cfg, bool exact, bool topo, const uint32_t* qst, const uint32_t* dev_max,
                              const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, hipStream_t s) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_pods + 255) / 256, (n_nodes + chunk - 1) / chunk);
-#define KG_EXT_SEL(KK, EX)                                                                                          \
-    k_ext_select<KK, EX><<<grid, 256, 0, s>>>(nodes, zones, e, pods, n_pods, n_nodes, chunk, index_base, cfg, qst, \
-                                              dev_max, rsv_max, pref, partial)
-    if (k == 1) {
-        if (exact) KG_EXT_SEL(1, true);
-        else KG_EXT_SEL(1, false);
-    } else {
-        if (exact) KG_EXT_SEL(KG_TOPK_MAX, true);
-        else KG_EXT_SEL(KG_TOPK_MAX, false);
+#define KG_EXT_SEL(KK, EX, TP)                                                                                          \
+    k_ext_select<KK, EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, n_pods, n_nodes, chunk, index_base, cfg, qst, \
+                                                  dev_max, rsv_max, pref, partial)
+#define KG_EXT_SEL_K(KK)                  \
+    if (exact) {                          \
+        if (topo) KG_EXT_SEL(KK, true, true); \
+        else KG_EXT_SEL(KK, true, false);     \
+    } else {                              \
+        if (topo) KG_EXT_SEL(KK, false, true); \
+        else KG_EXT_SEL(KK, false, false);     \
     }
+    if (k == 1) {
+        KG_EXT_SEL_K(1)
+    } else {
+        KG_EXT_SEL_K(KG_TOPK_MAX)
+    }
+#undef KG_EXT_SEL_K
 #undef KG_EXT_SEL
     return hipGetLastError();
 }

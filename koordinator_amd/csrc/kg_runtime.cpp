@@ -61,6 +61,7 @@ struct kg_snap {
     std::vector<ZoneRec> h_zones;
     std::vector<uint32_t> pos;     // snapshot index -> record position
     uint32_t n0 = 0;               // records of class 0 (positions [0, n0))
+    uint32_t n_topo = 0;           // Restricted / BestEffort records (need the general NUMA topology manager)
     bool uploaded = false;
     bool weights_small = false;  // per-resource weights <= 2^12: float64 fast path allowed
     // config-5 tables (KG_PLUGIN_DEV / RSV / QUOTA)
@@ -107,6 +108,7 @@ struct kg_pods {
     uint64_t* d_gather = nullptr;
     size_t gather_cap = 0;
     bool fast_ok = false;  // every value below FAST_LIMIT and no pod NUMA policy
+    bool pod_policy = false;  // some pod carries its own NUMA policy
     // config-5 columns and scratch
     int64_t* d_dev_req = nullptr;     // [cap][KG_DEV_R]
     uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32): 5 x cap
@@ -448,6 +450,20 @@ void set_node_index(NodeRec& r, uint32_t i) {
     r.v[N_FLAGS] = (int64_t)(((uint64_t)r.v[N_FLAGS] & 0xFFFFFFFFull) | ((uint64_t)i << 32));
 }
 
+uint32_t rec_numa_policy(const NodeRec& r) { return ((uint32_t)r.v[N_FLAGS] >> F_NUMA_POLICY_SHIFT) & 15u; }
+
+void count_topo(kg_snap* s) {
+    uint32_t t = 0;
+    for (uint32_t p = 0; p < s->n; p++) {
+        const uint32_t pol = rec_numa_policy(s->h_nodes[p]);
+        t += pol == KG_NUMA_BEST_EFFORT || pol == KG_NUMA_RESTRICTED;
+    }
+    s->n_topo = t;
+}
+
+// Select-mode ext kernels may drop the general topology manager when nothing in the pair set needs it
+bool need_topo(const kg_snap* s, const kg_pods* p) { return s->n_topo != 0 || p->pod_policy; }
+
 // Place records (indexed by snapshot index) in device order: class 0 then class 1, each ascending.
 void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>& zrs, std::vector<DevRec>* devs = nullptr) {
     const uint32_t n = s->n;
@@ -464,6 +480,7 @@ void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>&
         if (devs) s->h_dev[p] = (*devs)[i];
     }
     s->n0 = n0;
+    count_topo(s);
 }
 
 kg_status record_begin(kg_ctx* ctx, hipEvent_t* a, hipEvent_t* b) {
@@ -691,6 +708,7 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
                 HIP_TRY(ctx, hipMemcpyAsync(s->d_dev + p, &s->h_dev[p], sizeof(DevRec), hipMemcpyHostToDevice, ctx->stream));
             }
         }
+        count_topo(s);
     }
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -825,7 +843,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     std::vector<uint32_t> f(std::max<uint32_t>(n, 1));
     const int64_t* src[9] = {cols->req_cpu, cols->req_mem, cols->req_eph, cols->sc_req[0], cols->sc_req[1],
                              cols->nz_cpu, cols->nz_mem, cols->la_est[0], cols->la_est[1]};
-    bool fast = true;
+    bool fast = true, any_pol = false;
     for (int c = 0; c < 9; c++)
         for (uint32_t j = 0; j < n; j++) {
             const int64_t x = src[c] ? src[c][j] : 0;
@@ -837,8 +855,10 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         if (pol > KG_NUMA_SINGLE_NODE) return fail(ctx, KG_INVALID_ARG, "pod %u: NUMA policy %u", j, pol);
         f[j] = (cols->flags ? (cols->flags[j] & 0xFFFFu) : 0u) | (pol << 16);
         fast &= pol == KG_NUMA_NONE;
+        any_pol |= pol != KG_NUMA_NONE;
     }
     p->fast_ok = fast;
+    p->pod_policy = any_pol;
     // config-5 columns (absent columns: no GPU request, no quota, no reservation class)
     std::vector<int64_t> dreq((size_t)DEV_R * std::max<uint32_t>(n, 1), 0);
     std::vector<uint32_t> xc((size_t)5 * std::max<uint32_t>(n, 1), 0);
@@ -1021,7 +1041,8 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     if (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) {
         const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(p->n_stat, 1));
         HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list, p->n_stat, s->n, chunk, s->base,
-                                      s->kcfg, force_exact(), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, ctx->stream));
+                                      s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
+                                      ctx->stream));
     }
     return KG_OK;
 }
@@ -1037,7 +1058,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, p->n, s->n, chunk, kk, s->base, s->kcfg,
-                                   force_exact(), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, p->d_partial,
+                                   force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, p->d_partial,
                                    ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
