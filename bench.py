@@ -49,17 +49,40 @@ def parse():
     return ap.parse_args()
 
 
-def load_traffic():
-    """HBM bytes per select launch from the committed rocprofv3 PMC summary (or None)."""
+# VALU issue peak in wave-instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+# instruction (MI355X_MICROARCH.md: a wave issues each VALU instruction over 2 cycles)
+VALU_PEAK = 256 * 4 * 2.4e9 / 2
+
+
+def load_pmc():
+    """The committed rocprofv3 PMC summary of the select kernels (tools/pmc_summary.py), or {}."""
     path = os.path.join(ROOT, "profiles", "select_pmc.json")
     if not os.path.exists(path):
-        return None
+        return {}
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+            return json.load(f)
     except Exception:
+        return {}
+
+
+def load_traffic():
+    """HBM bytes per select launch from the committed rocprofv3 PMC summary (or None)."""
+    return load_pmc().get("hbm_bytes_per_launch")
+
+
+def valu_issue(avg_kernel_s):
+    """The select's actual ceiling: VALU wave-instructions per launch (SQ_INSTS_VALU of the committed
+    PMC pass, summed over the k_select kernels of one step) / the live kernel time, against VALU_PEAK."""
+    ks = load_pmc().get("kernels", {})
+    insts = sum(v["counters"].get("SQ_INSTS_VALU", 0.0) for k, v in ks.items() if "k_select<" in k)
+    if not insts or not avg_kernel_s:
         return None
+    a = insts / avg_kernel_s
+    return {"bound": "valu", "achieved": a / 1e12, "peak": VALU_PEAK / 1e12, "unit": "T wave-inst/s",
+            "frac": a / VALU_PEAK, "insts_per_launch": insts,
+            "note": "pod tiling serves one node read to 64 pods, so the scan-model HBM frac exceeds 1; the "
+                    "kernel is VALU-issue bound (float64 ops issue over 4 cycles, so this frac is a lower bound)"}
 
 
 def cpu_baseline(cfg, nodes, pods, target_s):
@@ -242,7 +265,8 @@ def main():
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK) if achieved else None,
                      "traffic": load_traffic() if a.config != 5 else None,
                      "kernel": "k_select" if a.config != 5 else "k_ext_select", "kernel_avg_ms": avg_kernel_s * 1e3,
-                     "bytes_per_eval": B_EVAL[a.config], "evals_per_launch": n_pods * n_local},
+                     "bytes_per_eval": B_EVAL[a.config], "evals_per_launch": n_pods * n_local,
+                     "issue": valu_issue(avg_kernel_s) if a.config == 2 and world == 1 else None},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
