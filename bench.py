@@ -264,7 +264,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": (achieved / HBM_PEAK) if achieved else None,
                      "traffic": load_traffic() if a.config != 5 else None,
-                     "kernel": "k_select" if a.config != 5 else "k_ext_select", "kernel_avg_ms": avg_kernel_s * 1e3,
+                     "kernel": "k_select" if a.config != 5 else "k_ext_select + k_select (plain-pod split, one bracket)", "kernel_avg_ms": avg_kernel_s * 1e3,
                      "bytes_per_eval": B_EVAL[a.config], "evals_per_launch": n_pods * n_local,
                      "issue": valu_issue(avg_kernel_s) if a.config == 2 and world == 1 else None},
         "cpu_baseline": None,

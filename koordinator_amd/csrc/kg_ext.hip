@@ -154,14 +154,16 @@ __device__ __forceinline__ void topk_ins(uint64_t (&top)[K], uint64_t key) {
 // Pass 2: weighted totals with the normalised DeviceShare / Reservation terms, top-K per (chunk, pod).
 template <int K, bool EXACT, bool TOPO>
 __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
-                                                    ExtDev e, PodsDev pods, uint32_t n_pods, uint32_t n_nodes,
+                                                    ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
+                                                    uint32_t n_pods, uint32_t n_nodes,
                                                     uint32_t chunk, uint32_t index_base, KCfg cfg,
                                                     const uint32_t* __restrict__ qst, const uint32_t* __restrict__ dev_max,
                                                     const uint32_t* __restrict__ rsv_max, const uint64_t* __restrict__ pref,
                                                     uint64_t* __restrict__ partial) {
+    // lane j = row j of the output; the pod is list[j] (list == nullptr: the batch in order)
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = j < n_pods;
-    const uint32_t jj = live ? j : 0;
+    const uint32_t jj = live ? (list ? list[j] : j) : 0;
     const PodV p = load_pod(pods, jj);
     const PodX px = load_podx(pods, jj);
     const uint32_t q = live ? qst[jj] : 1u;
@@ -182,6 +184,18 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
 #pragma unroll
         for (int t = 0; t < K; t++) dst[t] = top[t];
     }
+}
+
+// Rows of a sub-batch select (plain pods / config-5 pods) back to their batch positions; a pod the
+// ElasticQuota PreFilter rejected has no feasible node.
+__global__ __launch_bounds__(256) void k_scatter_keys(const uint64_t* __restrict__ src, const uint32_t* __restrict__ map,
+                                                      uint32_t n, uint32_t k, const uint32_t* __restrict__ qst,
+                                                      uint64_t* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t j = map[t];
+    const bool rejected = qst && qst[j] != 0;
+    for (uint32_t i = 0; i < k; i++) out[(size_t)j * k + i] = rejected ? 0ull : src[(size_t)t * k + i];
 }
 
 // One replay step (see file header). buckets: [3][128] ring of per-DeviceShare-score best keys.
@@ -365,14 +379,21 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
     return hipGetLastError();
 }
 
+hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, const uint32_t* qst,
+                               uint64_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_scatter_keys<<<(n + 255) / 256, 256, 0, s>>>(src, map, n, k, qst, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
-                             uint32_t n_pods, uint32_t n_nodes, uint32_t chunk, uint32_t k, uint32_t index_base,
+                             const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t chunk, uint32_t k, uint32_t index_base,
                              const KCfg& cfg, bool exact, bool topo, const uint32_t* qst, const uint32_t* dev_max,
                              const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, hipStream_t s) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_pods + 255) / 256, (n_nodes + chunk - 1) / chunk);
 #define KG_EXT_SEL(KK, EX, TP)                                                                                          \
-    k_ext_select<KK, EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, n_pods, n_nodes, chunk, index_base, cfg, qst, \
+    k_ext_select<KK, EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n_nodes, chunk, index_base, cfg, qst, \
                                                   dev_max, rsv_max, pref, partial)
 #define KG_EXT_SEL_K(KK)                  \
     if (exact) {                          \

@@ -123,6 +123,16 @@ struct kg_pods {
     int32_t* d_aout = nullptr;        // kg_assume_ext outputs
     hipGraphExec_t xexec = nullptr;   // ext replay graph
     std::vector<uint8_t> xkey;
+    // config-5 select split: "plain" pods (no GPU request, no reservation class or affinity) see only
+    // NodeResourcesFit / LoadAware / NodeNUMAResource and take the fast k_select over a compacted copy
+    // of their columns; the rest go through k_ext_select by list
+    int64_t* d_pcols = nullptr;   // 9 int64 columns of `cap` entries (plain pods, compacted)
+    uint32_t* d_pflags = nullptr;
+    uint32_t* d_pmap = nullptr;   // plain row -> batch position
+    uint32_t* d_xlist = nullptr;  // config-5 row -> batch position
+    uint64_t* d_tkeys = nullptr;  // [KG_TOPK_MAX][cap] sub-batch keys before the scatter
+    uint32_t n_plain = 0, n_x = 0;
+    PodsDev plain{};
     // replay graph (G steps) cached for the (snapshot buffers, batch size, configuration) it captured
     hipGraphExec_t rexec = nullptr;
     std::vector<uint8_t> rkey;
@@ -426,6 +436,16 @@ bool replay_no_graph() {
 }
 
 // KG_SELECT_INT=1: select kernel on the integer path only (A/B and parity checks of the fast path)
+// KG_EXT_SPLIT=0: every config-5 pod through k_ext_select (A/B aid for the plain-pod split)
+bool ext_split_off() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("KG_EXT_SPLIT");
+        v = (e && e[0] == '0') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 bool force_int() {
     static int v = -1;
     if (v < 0) {
@@ -799,7 +819,12 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_pref, sizeof(uint64_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_minors, sizeof(uint32_t) * (capacity + 1)) == hipSuccess &&
               hipMalloc(&p->d_buckets, sizeof(uint64_t) * 3 * 128) == hipSuccess &&
-              hipMalloc(&p->d_aout, sizeof(int32_t) * 2) == hipSuccess;
+              hipMalloc(&p->d_aout, sizeof(int32_t) * 2) == hipSuccess &&
+              hipMalloc(&p->d_pcols, sizeof(int64_t) * 9 * capacity) == hipSuccess &&
+              hipMalloc(&p->d_pflags, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_pmap, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_xlist, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess;
     if (!ok) {
         hipFree(p->d_cols);
         hipFree(p->d_flags);
@@ -808,7 +833,8 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
         hipFree(p->d_step);
         for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst,
                         (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors,
-                        (void*)p->d_buckets, (void*)p->d_aout})
+                        (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_pcols, (void*)p->d_pflags,
+                        (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys})
             hipFree(b);
         delete p;
         return fail(ctx, KG_OOM, "pod batch of %u", capacity);
@@ -830,6 +856,17 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
     p->dev.quota = (const int32_t*)(p->d_xcols + 2 * (size_t)capacity);
     p->dev.quota_keys = p->d_xcols + 3 * (size_t)capacity;
     p->dev.rsv_class = (const int32_t*)(p->d_xcols + 4 * (size_t)capacity);
+    int64_t* pc = p->d_pcols;
+    p->plain.req_cpu = pc + 0 * (size_t)capacity;
+    p->plain.req_mem = pc + 1 * (size_t)capacity;
+    p->plain.req_eph = pc + 2 * (size_t)capacity;
+    p->plain.sc_req0 = pc + 3 * (size_t)capacity;
+    p->plain.sc_req1 = pc + 4 * (size_t)capacity;
+    p->plain.nz_cpu = pc + 5 * (size_t)capacity;
+    p->plain.nz_mem = pc + 6 * (size_t)capacity;
+    p->plain.la_est0 = pc + 7 * (size_t)capacity;
+    p->plain.la_est1 = pc + 8 * (size_t)capacity;
+    p->plain.flags = p->d_pflags;
     *out = p;
     return KG_OK;
 }
@@ -862,7 +899,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     // config-5 columns (absent columns: no GPU request, no quota, no reservation class)
     std::vector<int64_t> dreq((size_t)DEV_R * std::max<uint32_t>(n, 1), 0);
     std::vector<uint32_t> xc((size_t)5 * std::max<uint32_t>(n, 1), 0);
-    std::vector<uint32_t> stat;
+    std::vector<uint32_t> stat, pmap, xlist;
     for (uint32_t j = 0; j < n; j++) {
         const uint32_t cnt = cols->dev_count ? cols->dev_count[j] : 0u;
         const uint32_t keys = cols->dev_keys ? cols->dev_keys[j] : 0u;
@@ -880,6 +917,15 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         xc[3 * (size_t)n + j] = cols->quota_keys ? cols->quota_keys[j] : 0u;
         xc[4 * (size_t)n + j] = (uint32_t)cls;
         if (cnt > 0 || cls >= 0) stat.push_back(j);
+        if (cnt == 0 && cls < 0 && !(f[j] & KG_POD_RSV_REQUIRED)) pmap.push_back(j);
+        else xlist.push_back(j);
+    }
+    const uint32_t np = (uint32_t)pmap.size();
+    std::vector<int64_t> hp((size_t)9 * std::max<uint32_t>(np, 1));
+    std::vector<uint32_t> fp(std::max<uint32_t>(np, 1));
+    for (uint32_t t = 0; t < np; t++) {
+        for (int c = 0; c < 9; c++) hp[(size_t)c * np + t] = h[(size_t)c * n + pmap[t]];
+        fp[t] = f[pmap[t]];
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipMemcpyAsync(p->d_dev_req, dreq.data(), sizeof(int64_t) * DEV_R * n, hipMemcpyHostToDevice, ctx->stream));
@@ -889,6 +935,17 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     if (!stat.empty())
         HIP_TRY(ctx, hipMemcpyAsync(p->d_stat_list, stat.data(), sizeof(uint32_t) * stat.size(), hipMemcpyHostToDevice, ctx->stream));
     p->n_stat = (uint32_t)stat.size();
+    if (np) {
+        for (int c = 0; c < 9; c++)
+            HIP_TRY(ctx, hipMemcpyAsync(p->d_pcols + (size_t)c * p->cap, hp.data() + (size_t)c * np, sizeof(int64_t) * np,
+                                        hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_pflags, fp.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_pmap, pmap.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (!xlist.empty())
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_xlist, xlist.data(), sizeof(uint32_t) * xlist.size(), hipMemcpyHostToDevice, ctx->stream));
+    p->n_plain = np;
+    p->n_x = (uint32_t)xlist.size();
     for (int c = 0; c < 9; c++)
         HIP_TRY(ctx, hipMemcpyAsync(p->d_cols + (size_t)c * p->cap, h.data() + (size_t)c * n, sizeof(int64_t) * n,
                                     hipMemcpyHostToDevice, ctx->stream));
@@ -910,7 +967,8 @@ kg_status kg_pods_destroy(kg_pods* p) {
     hipFree(p->d_partial);
     hipFree(p->d_gather);
     for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst, (void*)p->d_dev_max,
-                    (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout})
+                    (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout,
+                    (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys})
         hipFree(b);
     hipFree(p->d_rbpart);
     hipFree(p->d_rbtops);
@@ -1047,22 +1105,73 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     return KG_OK;
 }
 
-// config-5 matrix mode, pass 2: totals with the normalised terms -> per-pod top-k in d_out
+// config-5 matrix mode, pass 2: totals with the normalised terms -> per-pod top-k in d_out.
+// Split: a plain pod's DeviceShare / Reservation terms are 0 and it passes their filters on every node
+// (eval_pair_ext with dcount == 0, no view, no required affinity), so its keys are exactly the base
+// select's; those pods run the fast k_select over their compacted columns, the others k_ext_select by
+// list. ElasticQuota rejections are applied in the scatter.
 static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out) {
     kg_ctx* ctx = s->ctx;
-    const uint32_t chunk = select_chunk(s->n, p->n);
-    const uint32_t n_parts = (s->n + chunk - 1) / chunk;
-    kg_status st = ensure_partial(p, (size_t)std::max<uint32_t>(n_parts, 1) * p->n * kk);
+    const bool split = !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok &&
+                       !need_topo(s, p);
+    const uint32_t n_x = split ? p->n_x : p->n;
+    const uint32_t* xl = split ? p->d_xlist : nullptr;
+    const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(n_x, 1));
+    const uint32_t xparts = n_x ? (s->n + chunk - 1) / chunk : 0;
+    const uint32_t n_plain = split ? p->n_plain : 0;
+    LaunchSelect a{};
+    uint32_t fparts = 0;
+    if (n_plain) {
+        a.nodes = s->d_nodes;
+        a.zones = s->d_zones;
+        a.pods = p->plain;
+        a.n_pods = n_plain;
+        const uint32_t bounds[3] = {0, s->n0, s->n};
+        for (int c = 0; c < 2; c++) {
+            SelectRange& r = a.range[c];
+            r.begin = bounds[c];
+            r.end = bounds[c + 1];
+            r.chunk = select_chunk(r.end - r.begin, n_plain);
+            r.n_chunks = (r.end - r.begin + r.chunk - 1) / r.chunk;
+            r.part0 = fparts;
+            fparts += r.n_chunks;
+        }
+        a.index_base = s->base;
+        a.k = kk;
+        a.exact = false;
+        a.fast = true;
+        a.cfg = s->kcfg;
+    }
+    const size_t xneed = (size_t)xparts * n_x * kk;
+    kg_status st = ensure_partial(p, std::max<size_t>(xneed + (size_t)fparts * n_plain * kk, 1));
     if (st != KG_OK) return st;
+    a.partial = p->d_partial + xneed;
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
-    HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, p->n, s->n, chunk, kk, s->base, s->kcfg,
-                                   force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, p->d_partial,
-                                   ctx->stream));
+    if (n_x)
+        HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, xl, n_x, s->n, chunk, kk, s->base,
+                                       s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
+                                       p->d_pref, p->d_partial, ctx->stream));
+    if (fparts) HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
-    HIP_TRY(ctx, launch_merge(p->d_partial, n_parts, p->n, kk, d_out, ctx->stream));
+    if (!split) {
+        HIP_TRY(ctx, launch_merge(p->d_partial, xparts, p->n, kk, d_out, ctx->stream));
+        return KG_OK;
+    }
+    if (n_x) {
+        HIP_TRY(ctx, launch_merge(p->d_partial, xparts, n_x, kk, p->d_tkeys, ctx->stream));
+        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_xlist, n_x, kk, nullptr, d_out, ctx->stream));
+    }
+    if (n_plain) {
+        if (fparts)
+            HIP_TRY(ctx, launch_merge_big(a.partial, fparts, n_plain, kk, s->d_nodes, s->d_zones, p->plain, s->d_big + 1,
+                                          s->d_big, s->base, s->kcfg, p->d_tkeys, ctx->stream));
+        else
+            HIP_TRY(ctx, hipMemsetAsync(p->d_tkeys, 0, sizeof(uint64_t) * kk * n_plain, ctx->stream));
+        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_pmap, n_plain, kk, p->d_qst, d_out, ctx->stream));
+    }
     return KG_OK;
 }
 

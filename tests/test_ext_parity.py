@@ -84,6 +84,47 @@ def test_ext_select(ctx, k):
     assert (want[:, 0] == 0).any() and (want[:, 0] != 0).any()
 
 
+def plain_pods(pods):
+    """Pods without a GPU request, reservation class or reservation affinity: the select runs them
+    through the fast k_select (kg_runtime.cpp ext_select_local split)."""
+    cls = pods.get("rsv_class", np.full(len(pods["req_cpu"]), -1))
+    return (pods["dev_count"] == 0) & (cls < 0) & ((pods["flags"] & abi.KG_POD_RSV_REQUIRED) == 0)
+
+
+@pytest.mark.parametrize("subset", list(SUBSETS))
+@pytest.mark.parametrize("k", [1, 4])
+def test_ext_select_split(ctx, subset, k):
+    """Select with the plain / config-5 pod split: both sub-batches scattered back in batch order,
+    quota-rejected plain pods without a node, every plugin subset."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(1800, 400, seed_config=71, rsv_frac=0.2)
+    kc = cfg.kg_config()
+    kc.plugins = SUBSETS[subset]
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_select(snap, batch, k)
+    want = oracle_lib.ext_select(kc, nodes, pods, k, 0, quotas if kc.plugins & abi.KG_PLUGIN_QUOTA else None,
+                                 rsv if kc.plugins & abi.KG_PLUGIN_RSV else None)
+    assert np.array_equal(got, want)
+    plain = plain_pods(pods)
+    assert plain.any() and (~plain).any()
+    if kc.plugins & abi.KG_PLUGIN_QUOTA:
+        assert (plain & (want[:, 0] == 0)).any()
+
+
+def test_ext_select_split_big_values(ctx):
+    """Plain pods on nodes outside the fast path's exact domain go through k_merge_big."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(900, 200, seed_config=72, rsv_frac=0.2)
+    nodes = {k: v.copy() for k, v in nodes.items()}
+    nodes["alloc_mem"][:40] = 1 << 50
+    nodes["la_alloc1"][:40] = 1 << 50
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    for k in (1, 4):
+        got = engine.eval_select(snap, batch, k)
+        want = oracle_lib.ext_select(kc, nodes, pods, k, 0, quotas, rsv)
+        assert np.array_equal(got, want)
+    assert (abi.key_node(want[:, 0][want[:, 0] != 0]) < 40).any()
+
+
 def test_ext_select_preferred_reservation_wins(ctx):
     """Reservation weight 5000 with the preferred (ordered) reservation node normalised to 100."""
     cfg, nodes, pods, quotas, rsv = synth.cluster5(800, 200, seed_config=31, rsv_frac=0.5)

@@ -1,5 +1,8 @@
 set -o pipefail
+TAG=${1:-r1}
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest tests/test_ext_parity.py tests/test_numa_topology.py tests/test_ext_kat.py tests/test_numa_kat.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ext_tests.log 2>&1 || exit 1
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_ext_parity.py tests/test_numa_topology.py tests/test_ext_kat.py tests/test_numa_kat.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ext_tests_$TAG.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --config 5 --steps 5 --warmup 1 > gpurun_out/bench5_$TAG.json 2> gpurun_out/bench5_$TAG.err || exit 2
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof5b -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench5b.json 2>gpurun_out/bench5b.err || exit 3
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof5_$TAG -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --config 5 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench5t_$TAG.json 2>gpurun_out/bench5t_$TAG.err || exit 3
