@@ -85,10 +85,24 @@ __device__ __forceinline__ int64_t numa_least(int64_t w_cpu, int64_t w_mem, int6
     return wdiv(sum, wsum);
 }
 
+// Go's truncating a / c for a score-sized quotient. For 0 <= a < 2^62, 0 < c < 2^62 and a / c < 2^18,
+// a * v_rcp_f64(c) is within 2^-22 relative of a / c even at single-precision reciprocal accuracy, so
+// it is within 1/16 absolute, its floor is off by at most one and the exact int64 remainder a - q*c
+// fixes it; every other operand pair takes the int64 divide.
+__device__ __forceinline__ int64_t qdiv(int64_t a, int64_t c) {
+    const bool ok = (a >= 0) & (c > 0) & (a < (1ll << 62)) & (c < (1ll << 62));
+    const double est = floor((double)a * __builtin_amdgcn_rcp((double)c));
+    if (__builtin_expect(!ok || !(est < 262144.0), 0)) return c == 0 ? 0 : a / c;
+    int64_t q = (int64_t)(int32_t)est;
+    const int64_t r = a - q * c;
+    q += (r < 0) ? -1 : ((r >= c) ? 1 : 0);
+    return q;
+}
+
 __device__ __forceinline__ int64_t most_req(int64_t requested, int64_t capacity) {
     if (capacity == 0) return 0;
     if (requested > capacity) requested = capacity;
-    return (requested * 100) / capacity;
+    return qdiv(requested * 100, capacity);
 }
 
 // LeastAllocated / MostAllocated over {cpu, memory} (nodenumaresource least_allocated.go / most_allocated.go)
@@ -105,7 +119,7 @@ __device__ __forceinline__ int64_t numa_score(bool most, int64_t w_cpu, int64_t 
         sum += most_req(req_mem, alloc_mem) * w_mem;
         wsum += w_mem;
     }
-    return wsum == 0 ? 0 : sum / wsum;
+    return wsum == 0 ? 0 : qdiv(sum, wsum);
 }
 
 // ---- NUMA topology manager for non-cpuset pods: hints (resource_manager.go:529-657) and the
@@ -380,7 +394,9 @@ struct PairOut {
 // topology manager (numa_topology) from the instantiation: the host picks it only when no node is
 // Restricted / BestEffort and no pod carries a NUMA policy, and only for select-mode kernels, where a
 // SingleNUMANode pair without a fitting zone just needs some failure bit (the reason is unused).
-template <bool EXACT, bool OV = false, bool TOPO = true>
+// SCORE = false: the filter outcome only (status bits; scores and zone choice by score not computed),
+// for the config-5 statistics pass.
+template <bool EXACT, bool OV = false, bool TOPO = true, bool SCORE = true>
 __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restrict__ n, const ZoneRec* __restrict__ zr,
                                           const PodV& p, uint32_t flags, PairOut& o, const Over* ov = nullptr) {
     if (p.flags & KG_POD_NUMA_SKIP) return;
@@ -453,8 +469,10 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
                 const bool ok = (!has_cpu || (ac != 0 && p.req_cpu <= ac)) && (!has_mem || (am != 0 && p.req_mem <= am));
                 const int64_t rc = tc - ac < 0 ? 0 : tc - ac;
                 const int64_t rm = tm - am < 0 ? 0 : tm - am;
-                const int64_t s = numa_score<EXACT>((c.most & MOST_NUMA_HINT) != 0, c.numa_hint_w_cpu, c.numa_hint_w_mem, tc, rc + p.req_cpu,
-                                                    zr->rcp_cpu[z], tm, rm + p.req_mem, zr->rcp_mem[z]);
+                int64_t s = 0;
+                if constexpr (SCORE)
+                    s = numa_score<EXACT>((c.most & MOST_NUMA_HINT) != 0, c.numa_hint_w_cpu, c.numa_hint_w_mem, tc,
+                                          rc + p.req_cpu, zr->rcp_cpu[z], tm, rm + p.req_mem, zr->rcp_mem[z]);
                 const bool take = ok && (best < 0 || s > best_score);
                 best = take ? (int32_t)z : best;
                 best_score = take ? s : best_score;
@@ -472,6 +490,7 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
                 return;
             }
         }
+        if constexpr (!SCORE) return;
         if (best < 0 || Z == 1) {  // best hint == default affinity: no NUMA allocation
             o.zone = -1;
             o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
@@ -485,13 +504,14 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
         return;
     }
     // policy None: scoreWithAmplifiedCPUs
+    if constexpr (!SCORE) return;
     int64_t req_cpu = nv<OV>(n, ov, N_REQ_CPU);
     if (pod_cpu != 0 && amp) req_cpu = req_cpu - n[N_CPUSET] + n[N_AMP_CPUSET];
     o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], req_cpu + pod_cpu, rcp_cpu,
                                  n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
 }
 
-template <bool EXACT, bool OV = false, bool TOPO = true>
+template <bool EXACT, bool OV = false, bool TOPO = true, bool SCORE = true>
 __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __restrict__ n,
                                              const ZoneRec* __restrict__ zr, const PodV& p, const Over* ov = nullptr) {
     PairOut o;
@@ -510,6 +530,7 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
         st |= (p.sc0 != 0 && p.sc0 > n[N_SC_ALLOC0] - nv<OV>(n, ov, N_SC_REQ0)) ? KG_ST_NRF_SC0 : 0u;
         st |= (p.sc1 != 0 && p.sc1 > n[N_SC_ALLOC1] - nv<OV>(n, ov, N_SC_REQ1)) ? KG_ST_NRF_SC1 : 0u;
         o.status |= st;
+        if constexpr (SCORE) {
         // LeastAllocated over {cpu, memory, scalar0, scalar1}
         int64_t sum = 0, wsum = 0;
         {
@@ -537,6 +558,7 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
             wsum += on ? w : 0;
         }
         o.s_nrf = wdiv(sum, wsum);
+        }
     }
 
     if (c.plugins & KG_PLUGIN_LA) {
@@ -556,7 +578,7 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
             }
         }
         // Score
-        if (c.la_score_enabled && !(flags & F_LA_SCORE_ZERO)) {
+        if (SCORE && c.la_score_enabled && !(flags & F_LA_SCORE_ZERO)) {
             const bool prod = c.la_score_prod && (p.flags & KG_POD_PROD);
             const int64_t u0 = (prod ? n[N_LA_SBASE_PROD0] : n[N_LA_SBASE_NP0]) + p.est0;
             const int64_t u1 = (prod ? n[N_LA_SBASE_PROD1] : n[N_LA_SBASE_NP1]) + p.est1;
@@ -570,7 +592,7 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
         }
     }
 
-    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT, OV, TOPO>(c, n, zr, p, flags, o, ov);
+    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT, OV, TOPO, SCORE>(c, n, zr, p, flags, o, ov);
     if (o.status & (KG_ST_NUMA_MASK | KG_ST_UNSUPPORTED)) o.s_numa = 0;
     if (o.status) o.zone = -1;
     return o;

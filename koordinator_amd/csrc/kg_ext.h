@@ -34,7 +34,7 @@ __device__ __forceinline__ PodX load_podx(const PodsDev& P, uint32_t j) {
 
 __device__ __forceinline__ int64_t least_score_i64(int64_t requested, int64_t capacity) {
     if (capacity == 0 || requested > capacity) return 0;
-    return ((capacity - requested) * 100) / capacity;
+    return qdiv((capacity - requested) * 100, capacity);
 }
 
 // leastResourceScorer / mostResourceScorer (deviceshare/scoring.go:263-323) over {gpu-core,
@@ -50,7 +50,7 @@ __device__ __forceinline__ int64_t dev_least(const KCfg& c, const int64_t* total
         score += ((c.most & MOST_DEV) ? most_req(req, total[r]) : least_score_i64(req, total[r])) * w;
         wsum += w;
     }
-    return wsum == 0 ? 0 : score / wsum;
+    return wsum == 0 ? 0 : qdiv(score, wsum);
 }
 
 __device__ __forceinline__ bool dev_minor_fits(const int64_t* fr, const PodX& x) {
@@ -316,7 +316,7 @@ __device__ __forceinline__ int64_t rsv_score_reservation(const RsvPod& q, const 
         }
     }
     if (r.max_pods > 0) w++;
-    return w <= 0 ? 0 : s / w;
+    return w <= 0 ? 0 : qdiv(s, w);
 }
 
 // nominated reservation's ScoreReservation and the node's most-preferred order (0 = none)
@@ -384,7 +384,9 @@ struct PairX {
     int64_t s_nrf, s_la, s_numa, s_dev, s_rsv, order;
 };
 
-template <bool EXACT, bool TOPO = true>
+// SCORE = false (statistics pass): status, raw DeviceShare score and the nominated reservation only;
+// the NodeResourcesFit / LoadAware / NodeNUMAResource scores stay 0.
+template <bool EXACT, bool TOPO = true, bool SCORE = true>
 __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
                                                const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
                                                uint32_t rec, const PodV& p, const PodX& x, uint32_t qst) {
@@ -409,12 +411,12 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
         ov.nz_cpu = v->nz_cpu;
         ov.nz_mem = v->nz_mem;
         ov.num_pods = v->num_pods;
-        b = eval_pair<EXACT, true, TOPO>(c, n, zr, p, &ov);
+        b = eval_pair<EXACT, true, TOPO, SCORE>(c, n, zr, p, &ov);
         const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u;
         if ((c.plugins & KG_PLUGIN_NUMA) && node_pol != KG_NUMA_NONE && !(p.flags & KG_POD_NUMA_SKIP))
             b.status = (b.status & ~(uint32_t)KG_ST_NUMA_MASK) | KG_ST_UNSUPPORTED;  // NUMA restore: host path
     } else {
-        b = eval_pair<EXACT, false, TOPO>(c, n, zr, p);
+        b = eval_pair<EXACT, false, TOPO, SCORE>(c, n, zr, p);
     }
     uint32_t st = b.status;
     int64_t dev_raw = 0;
@@ -450,7 +452,7 @@ __device__ __forceinline__ uint64_t pref_key(int64_t order, uint32_t gidx) {
     return ((uint64_t)(uint32_t)(order + 0x80000000ll) << 32) | gidx;
 }
 
-__device__ __forceinline__ int64_t norm100(int64_t s, int64_t mx) { return mx == 0 ? s : s * 100 / mx; }
+__device__ __forceinline__ int64_t norm100(int64_t s, int64_t mx) { return mx == 0 ? s : qdiv(s * 100, mx); }
 
 __device__ __forceinline__ int64_t total_ext(const KCfg& c, const PairX& o, uint32_t gidx, uint32_t dev_max,
                                              uint32_t rsv_max, uint64_t pref) {
