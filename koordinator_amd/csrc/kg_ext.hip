@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
     uint32_t dmax = 0, rmax = 0;
     uint64_t pk = PREF_NONE;
     for (uint32_t rec = lo; rec < hi; rec++) {
-        const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
         if (r.status) continue;
         dmax = max(dmax, (uint32_t)r.s_dev);
         rmax = max(rmax, (uint32_t)r.s_rsv);
