@@ -920,6 +920,16 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         if (cnt == 0 && cls < 0 && !(f[j] & KG_POD_RSV_REQUIRED)) pmap.push_back(j);
         else xlist.push_back(j);
     }
+    // wave-uniform work in the config-5 kernels: GPU pods (by GPU count) first, then reservation
+    // classes in order; rows are scattered back by list, so the order does not change any result
+    auto kind = [&](uint32_t j) {
+        const uint32_t cnt = xc[j];
+        const int32_t cls = (int32_t)xc[4 * (size_t)n + j];
+        return std::make_pair(cnt > 0 ? 0u - cnt : 0u, cls);
+    };
+    auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
+    std::stable_sort(stat.begin(), stat.end(), by_kind);
+    std::stable_sort(xlist.begin(), xlist.end(), by_kind);
     const uint32_t np = (uint32_t)pmap.size();
     std::vector<int64_t> hp((size_t)9 * std::max<uint32_t>(np, 1));
     std::vector<uint32_t> fp(std::max<uint32_t>(np, 1));
