@@ -16,6 +16,8 @@
 //                launch can normalise without another grid-wide pass.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kg_ext.h"
 #include "kg_kernels.h"
 
@@ -136,6 +138,41 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
     }
     if (!live) return;
     if (dmax) atomicMax(dev_max + j, dmax);
+    if (rmax) atomicMax(rsv_max + j, rmax);
+    if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
+}
+
+// Pass 1 for pods without a GPU request: only the nodes holding a view of the pod's reservation class
+// can carry a Reservation score or order, so lane t walks chunk blockIdx.y of that class's views
+// (record order) instead of every record.
+template <bool EXACT, bool TOPO>
+__global__ __launch_bounds__(256) void k_ext_stats_views(const NodeRec* __restrict__ nodes,
+                                                         const ZoneRec* __restrict__ zones, ExtDev e, PodsDev pods,
+                                                         const uint32_t* __restrict__ list, uint32_t n_list,
+                                                         uint32_t chunk, uint32_t index_base, KCfg cfg,
+                                                         const uint32_t* __restrict__ qst,
+                                                         uint32_t* __restrict__ rsv_max, uint64_t* __restrict__ pref) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_list) return;
+    const uint32_t j = list[t];
+    const PodV p = load_pod(pods, j);
+    const PodX px = load_podx(pods, j);
+    const uint32_t q = qst[j];
+    if (q || px.cls < 0 || px.cls >= RSV_MAX_CLASSES) return;
+    uint32_t rmax = 0;
+    uint64_t pk = PREF_NONE;
+    const uint32_t cb = e.cls_begin[px.cls], ce = e.cls_begin[px.cls + 1];
+    const uint32_t vb = cb + blockIdx.y * chunk, ve = min(ce, vb + chunk);
+    for (uint32_t v = vb; v < ve; v++) {
+        const uint32_t rec = e.views[v].rec;
+        const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        if (r.status) continue;
+        rmax = max(rmax, (uint32_t)r.s_rsv);
+        if (r.order != 0) {
+            const uint64_t k = pref_key(r.order, index_base + node_index(nodes[rec]));
+            pk = k < pk ? k : pk;
+        }
+    }
     if (rmax) atomicMax(rsv_max + j, rmax);
     if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
 }
@@ -383,6 +420,32 @@ hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_
                                uint64_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
     k_scatter_keys<<<(n + 255) / 256, 256, 0, s>>>(src, map, n, k, qst, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                                  const uint32_t* list, uint32_t n_list, uint32_t max_views, uint32_t index_base,
+                                  const KCfg& cfg, bool exact,
+                                  bool topo, const uint32_t* qst, uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref,
+                                  hipStream_t s) {
+    (void)dev_max;  // no GPU request: the DeviceShare maximum stays 0
+    if (n_list == 0 || max_views == 0) return hipSuccess;
+    // split every class's views over enough chunks to fill the chip (~2048 workgroups)
+    const uint32_t pod_blocks = (n_list + 255) / 256;
+    const uint32_t want = std::max<uint32_t>(1, 2048 / pod_blocks);
+    const uint32_t chunk = std::max<uint32_t>(4, (max_views + want - 1) / want);
+    dim3 grid(pod_blocks, (max_views + chunk - 1) / chunk);
+#define KG_EXT_SV(EX, TP)                                                                                        \
+    k_ext_stats_views<EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, chunk, index_base, cfg, qst, \
+                                                   rsv_max, pref)
+    if (exact) {
+        if (topo) KG_EXT_SV(true, true);
+        else KG_EXT_SV(true, false);
+    } else {
+        if (topo) KG_EXT_SV(false, true);
+        else KG_EXT_SV(false, false);
+    }
+#undef KG_EXT_SV
     return hipGetLastError();
 }
 

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <limits>
 #include <mutex>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -74,6 +75,7 @@ struct kg_snap {
     RsvInfo* d_infos = nullptr;
     uint32_t* d_cls_begin = nullptr;  // [RSV_MAX_CLASSES + 1]
     uint32_t n_views = 0;
+    uint32_t max_cls_views = 0;  // views of the largest reservation class
     std::vector<kg_rsv_view> h_views;  // as uploaded (local snapshot indices)
     std::vector<kg_rsv_info> h_infos;
     std::vector<uint64_t> cls_mask;  // per snapshot index: classes with a view on the node
@@ -114,6 +116,7 @@ struct kg_pods {
     uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32): 5 x cap
     uint32_t* d_stat_list = nullptr;  // pods carrying a GPU request or a reservation class
     uint32_t n_stat = 0;
+    uint32_t n_stat_cls = 0;          // leading d_stat_list entries without a GPU request (class views only)
     uint32_t* d_qst = nullptr;        // ElasticQuota PreFilter status per pod
     uint32_t* d_dev_max = nullptr;    // [cap] pass-1 NormalizeScore maxima
     uint32_t* d_rsv_max = nullptr;
@@ -924,12 +927,15 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     // classes in order; rows are scattered back by list, so the order does not change any result
     auto kind = [&](uint32_t j) {
         const uint32_t cnt = xc[j];
+        const uint64_t gpu = cnt > 0 ? ((uint64_t)(0u - cnt) << 8) | (xc[(size_t)n + j] & 0xFFu) : 0u;  // count, request keys
         const int32_t cls = (int32_t)xc[4 * (size_t)n + j];
-        return std::make_pair(cnt > 0 ? 0u - cnt : 0u, cls);
+        return std::make_tuple(gpu, (f[j] & KG_POD_RSV_REQUIRED) != 0, cls);
     };
     auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
     std::stable_sort(stat.begin(), stat.end(), by_kind);
     std::stable_sort(xlist.begin(), xlist.end(), by_kind);
+    uint32_t n_stat_cls = 0;
+    while (n_stat_cls < stat.size() && xc[stat[n_stat_cls]] == 0) n_stat_cls++;
     const uint32_t np = (uint32_t)pmap.size();
     std::vector<int64_t> hp((size_t)9 * std::max<uint32_t>(np, 1));
     std::vector<uint32_t> fp(std::max<uint32_t>(np, 1));
@@ -945,6 +951,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     if (!stat.empty())
         HIP_TRY(ctx, hipMemcpyAsync(p->d_stat_list, stat.data(), sizeof(uint32_t) * stat.size(), hipMemcpyHostToDevice, ctx->stream));
     p->n_stat = (uint32_t)stat.size();
+    p->n_stat_cls = n_stat_cls;
     if (np) {
         for (int c = 0; c < 9; c++)
             HIP_TRY(ctx, hipMemcpyAsync(p->d_pcols + (size_t)c * p->cap, hp.data() + (size_t)c * np, sizeof(int64_t) * np,
@@ -1107,8 +1114,15 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_pref, 0xFF, sizeof(uint64_t) * p->n, ctx->stream));
     if (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) {
-        const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(p->n_stat, 1));
-        HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list, p->n_stat, s->n, chunk, s->base,
+        // pods without a GPU request only get statistics from the nodes holding a view of their
+        // reservation class (elsewhere s_dev = s_rsv = order = 0): one lane per pod over those views
+        const uint32_t nc = p->n_stat_cls, ng = p->n_stat - nc;
+        if (nc && (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views)
+            HIP_TRY(ctx, launch_ext_stats_views(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list, nc, s->max_cls_views,
+                                                s->base, s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
+                                                p->d_pref, ctx->stream));
+        const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(ng, 1));
+        HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, chunk, s->base,
                                       s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
                                       ctx->stream));
     }
@@ -1759,6 +1773,8 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
                                       sizeof(int64_t), s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->n_views = nv;
+    s->max_cls_views = 0;
+    for (int c = 0; c < RSV_MAX_CLASSES; c++) s->max_cls_views = std::max(s->max_cls_views, cb[c + 1] - cb[c]);
     return KG_OK;
 }
 
