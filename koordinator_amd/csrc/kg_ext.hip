@@ -189,10 +189,15 @@ __device__ __forceinline__ void topk_ins(uint64_t (&top)[K], uint64_t key) {
 }
 
 // Pass 2: weighted totals with the normalised DeviceShare / Reservation terms, top-K per (chunk, pod).
-template <int K, bool EXACT, bool TOPO>
+// FB (host: fast path valid, all three base plugins, no general topology manager): on class-0 records
+// that are not F_BIG and hold no view of the lane's reservation class, the NodeResourcesFit / LoadAware
+// / NodeNUMAResource part of the pair comes from the fast block (eval_fast_key, the base select's
+// arithmetic: same feasibility and weighted total as eval_pair), and only DeviceShare, the
+// reservation-affinity check and the normalised terms are evaluated on top.
+template <int K, bool EXACT, bool TOPO, bool FB>
 __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                     ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
-                                                    uint32_t n_pods, uint32_t n_nodes,
+                                                    uint32_t n_pods, uint32_t n_nodes, uint32_t n0,
                                                     uint32_t chunk, uint32_t index_base, KCfg cfg,
                                                     const uint32_t* __restrict__ qst, const uint32_t* __restrict__ dev_max,
                                                     const uint32_t* __restrict__ rsv_max, const uint64_t* __restrict__ pref,
@@ -210,8 +215,36 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
     const uint32_t lo = blockIdx.y * chunk, hi = min(n_nodes, lo + chunk);
+    PodF pff{};
+    KCfg cv = cfg;
+    if constexpr (FB) {
+        pff = to_podf(p, cfg);
+        cv = cfg_in_vgprs(cfg);
+    }
+    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
     for (uint32_t rec = lo; rec < hi; rec++) {
-        const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const int64_t* __restrict__ n = nodes[rec].v;
+        if constexpr (FB) {
+            const uint32_t fl = (uint32_t)n[N_FLAGS];
+            const bool view = (cfg.plugins & KG_PLUGIN_RSV) && px.cls >= 0 && px.cls < RSV_MAX_CLASSES &&
+                              (((uint64_t)n[N_RSV_CLASSES] >> px.cls) & 1ull);
+            if (rec < n0 && !(fl & F_BIG) && !view) {
+                const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
+                const uint32_t g = index_base + (uint32_t)((uint64_t)fr.flags >> 32);
+                const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, g);
+                uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
+                PairX x{};
+                if (cfg.plugins & KG_PLUGIN_DEV) {
+                    st |= dev_eval(cfg, n, dev_of(e, rec), px, x.s_dev);
+                    const uint32_t node_pol = (fl >> F_NUMA_POLICY_SHIFT) & 15u;
+                    if (px.dcount > 0 && (cfg.plugins & KG_PLUGIN_NUMA) && node_pol != KG_NUMA_NONE) st |= KG_ST_UNSUPPORTED;
+                }
+                const int64_t tot = (int64_t)(bk >> 32) + total_ext(cfg, x, g, dm, rm, pf);
+                topk_ins<K>(top, st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)));
+                continue;
+            }
+        }
+        const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
         const uint32_t g = index_base + node_index(nodes[rec]);
         const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
         topk_ins<K>(top, r.status ? 0ull : key);
@@ -450,21 +483,23 @@ hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, co
 }
 
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
-                             const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t chunk, uint32_t k, uint32_t index_base,
-                             const KCfg& cfg, bool exact, bool topo, const uint32_t* qst, const uint32_t* dev_max,
+                             const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
+                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
                              const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, hipStream_t s) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_pods + 255) / 256, (n_nodes + chunk - 1) / chunk);
-#define KG_EXT_SEL(KK, EX, TP)                                                                                          \
-    k_ext_select<KK, EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n_nodes, chunk, index_base, cfg, qst, \
-                                                  dev_max, rsv_max, pref, partial)
-#define KG_EXT_SEL_K(KK)                  \
-    if (exact) {                          \
-        if (topo) KG_EXT_SEL(KK, true, true); \
-        else KG_EXT_SEL(KK, true, false);     \
-    } else {                              \
-        if (topo) KG_EXT_SEL(KK, false, true); \
-        else KG_EXT_SEL(KK, false, false);     \
+#define KG_EXT_SEL(KK, EX, TP, F)                                                                            \
+    k_ext_select<KK, EX, TP, F><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n_nodes, n0, chunk, index_base, \
+                                                     cfg, qst, dev_max, rsv_max, pref, partial)
+#define KG_EXT_SEL_K(KK)                              \
+    if (fb) {                                         \
+        KG_EXT_SEL(KK, false, false, true);           \
+    } else if (exact) {                               \
+        if (topo) KG_EXT_SEL(KK, true, true, false);  \
+        else KG_EXT_SEL(KK, true, false, false);      \
+    } else {                                          \
+        if (topo) KG_EXT_SEL(KK, false, true, false); \
+        else KG_EXT_SEL(KK, false, false, false);     \
     }
     if (k == 1) {
         KG_EXT_SEL_K(1)

@@ -79,8 +79,8 @@ hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, co
                                   bool topo, const uint32_t* qst, uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref,
                                   hipStream_t s);
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
-                             const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t chunk, uint32_t k, uint32_t index_base,
-                             const KCfg& cfg, bool exact, bool topo, const uint32_t* qst, const uint32_t* dev_max,
+                             const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
+                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
                              const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, hipStream_t s);
 // out[map[t]] = rows t of src (k keys each); rows whose pod has a nonzero qst[pod] get zero keys
 hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, const uint32_t* qst,

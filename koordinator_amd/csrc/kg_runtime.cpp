@@ -1174,8 +1174,8 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
     if (n_x)
-        HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, xl, n_x, s->n, chunk, kk, s->base,
-                                       s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
+        HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
+                                       s->kcfg, force_exact(), need_topo(s, p), split && (s->kcfg.plugins & 7u) == 7u, p->d_qst, p->d_dev_max, p->d_rsv_max,
                                        p->d_pref, p->d_partial, ctx->stream));
     if (fparts) HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
