@@ -111,10 +111,12 @@ __global__ __launch_bounds__(256) void k_ext_verify_fin(uint32_t n_pods, uint32_
 }
 
 // Pass 1: per-pod NormalizeScore inputs over the feasible nodes of records [lo, hi) of chunk blockIdx.y.
-template <bool EXACT, bool TOPO>
+// FB: base-plugin feasibility from the fast block where k_ext_select<FB> takes it (same conditions).
+template <bool EXACT, bool TOPO, bool FB>
 __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                    ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
-                                                   uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
+                                                   uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
+                                                   uint32_t index_base,
                                                    KCfg cfg, const uint32_t* __restrict__ qst, uint32_t* __restrict__ dev_max,
                                                    uint32_t* __restrict__ rsv_max, uint64_t* __restrict__ pref) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -126,8 +128,33 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
     const uint32_t lo = blockIdx.y * chunk, hi = min(n_nodes, lo + chunk);
     uint32_t dmax = 0, rmax = 0;
     uint64_t pk = PREF_NONE;
+    PodF pff{};
+    KCfg cv = cfg;
+    if constexpr (FB) {
+        pff = to_podf(p, cfg);
+        cv = cfg_in_vgprs(cfg);
+    }
+    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
     for (uint32_t rec = lo; rec < hi; rec++) {
-        const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const int64_t* __restrict__ n = nodes[rec].v;
+        if constexpr (FB) {
+            const uint32_t fl = (uint32_t)n[N_FLAGS];
+            const bool view = (cfg.plugins & KG_PLUGIN_RSV) && px.cls >= 0 && px.cls < RSV_MAX_CLASSES &&
+                              (((uint64_t)n[N_RSV_CLASSES] >> px.cls) & 1ull);
+            if (rec < n0 && !(fl & F_BIG) && !view) {
+                // no view: Reservation score and order are 0, only the DeviceShare maximum can move
+                if (!(cfg.plugins & KG_PLUGIN_DEV) || px.dcount == 0) continue;
+                const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
+                const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
+                int64_t raw = 0;
+                uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
+                st |= dev_eval(cfg, n, dev_of(e, rec), px, raw);
+                if ((cfg.plugins & KG_PLUGIN_NUMA) && ((fl >> F_NUMA_POLICY_SHIFT) & 15u) != KG_NUMA_NONE) st |= KG_ST_UNSUPPORTED;
+                if (!st) dmax = max(dmax, (uint32_t)raw);
+                continue;
+            }
+        }
+        const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
         if (r.status) continue;
         dmax = max(dmax, (uint32_t)r.s_dev);
         rmax = max(rmax, (uint32_t)r.s_rsv);
@@ -430,20 +457,22 @@ hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const E
 }
 
 hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
-                            const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
-                            const KCfg& cfg, bool exact, bool topo, const uint32_t* qst, uint32_t* dev_max,
-                            uint32_t* rsv_max, uint64_t* pref, hipStream_t s) {
+                            const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
+                            uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
+                            uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, hipStream_t s) {
     if (n_list == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_list + 255) / 256, (n_nodes + chunk - 1) / chunk);
-#define KG_EXT_ST(EX, TP)                                                                                           \
-    k_ext_stats<EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, chunk, index_base, cfg, qst, \
-                                             dev_max, rsv_max, pref)
-    if (exact) {
-        if (topo) KG_EXT_ST(true, true);
-        else KG_EXT_ST(true, false);
+#define KG_EXT_ST(EX, TP, F)                                                                                       \
+    k_ext_stats<EX, TP, F><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, n0, chunk, index_base, cfg, \
+                                                qst, dev_max, rsv_max, pref)
+    if (fb) {
+        KG_EXT_ST(false, false, true);
+    } else if (exact) {
+        if (topo) KG_EXT_ST(true, true, false);
+        else KG_EXT_ST(true, false, false);
     } else {
-        if (topo) KG_EXT_ST(false, true);
-        else KG_EXT_ST(false, false);
+        if (topo) KG_EXT_ST(false, true, false);
+        else KG_EXT_ST(false, false, false);
     }
 #undef KG_EXT_ST
     return hipGetLastError();

@@ -70,9 +70,9 @@ hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const E
                              uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                              const uint32_t* qst, const ExtVerifyDev& o, hipStream_t s);
 hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
-                            const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
-                            const KCfg& cfg, bool exact, bool topo, const uint32_t* qst, uint32_t* dev_max,
-                            uint32_t* rsv_max, uint64_t* pref, hipStream_t s);
+                            const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
+                            uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
+                            uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, hipStream_t s);
 hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                                   const uint32_t* list, uint32_t n_list, uint32_t max_views, uint32_t index_base,
                                   const KCfg& cfg, bool exact,

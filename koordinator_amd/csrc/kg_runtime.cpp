@@ -1105,6 +1105,13 @@ static kg_status ensure_partial(kg_pods* p, size_t need) {
     return KG_OK;
 }
 
+// config-5 pass 1 / pass 2 take the base plugins from the fast block where the fast path is valid:
+// same conditions as the plain-pod split, plus all three base plugins enabled (eval_fast_key<7>)
+static bool ext_fast_base(const kg_snap* s, const kg_pods* p) {
+    return !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok && !need_topo(s, p) &&
+           (s->kcfg.plugins & 7u) == 7u;
+}
+
 // config-5 matrix mode, pass 1: quota gate + per-pod NormalizeScore inputs of this shard
 static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     kg_ctx* ctx = s->ctx;
@@ -1122,8 +1129,8 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
                                                 s->base, s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
                                                 p->d_pref, ctx->stream));
         const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(ng, 1));
-        HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, chunk, s->base,
-                                      s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
+        HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, s->n0, chunk, s->base,
+                                      s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
                                       ctx->stream));
     }
     return KG_OK;
@@ -1175,7 +1182,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     if (st != KG_OK) return st;
     if (n_x)
         HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
-                                       s->kcfg, force_exact(), need_topo(s, p), split && (s->kcfg.plugins & 7u) == 7u, p->d_qst, p->d_dev_max, p->d_rsv_max,
+                                       s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
                                        p->d_pref, p->d_partial, ctx->stream));
     if (fparts) HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
