@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
                 const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
                 int64_t raw = 0;
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
-                st |= dev_eval(cfg, n, dev_of(e, rec), px, raw);
+                if (!st) st |= dev_eval(cfg, n, dev_of(e, rec), px, raw);
                 if ((cfg.plugins & KG_PLUGIN_NUMA) && ((fl >> F_NUMA_POLICY_SHIFT) & 15u) != KG_NUMA_NONE) st |= KG_ST_UNSUPPORTED;
                 if (!st) dmax = max(dmax, (uint32_t)raw);
                 continue;
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
                 const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, g);
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
                 PairX x{};
-                if (cfg.plugins & KG_PLUGIN_DEV) {
+                if ((cfg.plugins & KG_PLUGIN_DEV) && !st) {  // only the key's zero-ness matters once st != 0
                     st |= dev_eval(cfg, n, dev_of(e, rec), px, x.s_dev);
                     const uint32_t node_pol = (fl >> F_NUMA_POLICY_SHIFT) & 15u;
                     if (px.dcount > 0 && (cfg.plugins & KG_PLUGIN_NUMA) && node_pol != KG_NUMA_NONE) st |= KG_ST_UNSUPPORTED;
