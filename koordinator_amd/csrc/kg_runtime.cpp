@@ -460,9 +460,8 @@ bool force_int() {
 
 // Node chunk of the select kernel: enough (pod-block, chunk) workgroups to fill 256 CUs several
 // times over, while each wave still walks a long run of nodes.
-uint32_t select_chunk(uint32_t n_nodes, uint32_t n_pods) {
+uint32_t select_chunk(uint32_t n_nodes, uint32_t n_pods, uint32_t target_blocks = 2048) {
     const uint32_t pod_blocks = (n_pods + 255) / 256;
-    const uint32_t target_blocks = 2048;
     uint32_t n_chunks = std::max<uint32_t>(1, (target_blocks + pod_blocks - 1) / pod_blocks);
     uint32_t chunk = (n_nodes + n_chunks - 1) / n_chunks;
     chunk = std::max<uint32_t>(chunk, 32);
@@ -1128,7 +1127,8 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
             HIP_TRY(ctx, launch_ext_stats_views(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list, nc, s->max_cls_views,
                                                 s->base, s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
                                                 p->d_pref, ctx->stream));
-        const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(ng, 1));
+        // config-5 waves cost unequal amounts (GPU count, views): more, smaller chunks shorten the tail
+        const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(ng, 1), 8192);
         HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, s->n0, chunk, s->base,
                                       s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
                                       ctx->stream));
@@ -1147,7 +1147,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
                        !need_topo(s, p);
     const uint32_t n_x = split ? p->n_x : p->n;
     const uint32_t* xl = split ? p->d_xlist : nullptr;
-    const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(n_x, 1));
+    const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(n_x, 1), 8192);
     const uint32_t xparts = n_x ? (s->n + chunk - 1) / chunk : 0;
     const uint32_t n_plain = split ? p->n_plain : 0;
     LaunchSelect a{};
