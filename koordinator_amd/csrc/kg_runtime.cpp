@@ -460,7 +460,19 @@ bool force_int() {
 
 // Node chunk of the select kernel: enough (pod-block, chunk) workgroups to fill 256 CUs several
 // times over, while each wave still walks a long run of nodes.
-uint32_t select_chunk(uint32_t n_nodes, uint32_t n_pods, uint32_t target_blocks = 2048) {
+// KG_SELECT_BLOCKS: workgroup target of the base select launches (tuning aid; default 2048)
+uint32_t select_blocks() {
+    static uint32_t v = 0;
+    if (v == 0) {
+        const char* e = std::getenv("KG_SELECT_BLOCKS");
+        const long x = e ? std::strtol(e, nullptr, 10) : 0;
+        v = (x >= 64 && x <= 65536) ? (uint32_t)x : 2048u;
+    }
+    return v;
+}
+
+uint32_t select_chunk(uint32_t n_nodes, uint32_t n_pods, uint32_t target_blocks = 0) {
+    if (target_blocks == 0) target_blocks = select_blocks();
     const uint32_t pod_blocks = (n_pods + 255) / 256;
     uint32_t n_chunks = std::max<uint32_t>(1, (target_blocks + pod_blocks - 1) / pod_blocks);
     uint32_t chunk = (n_nodes + n_chunks - 1) / n_chunks;
