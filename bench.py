@@ -1,29 +1,41 @@
 """Benchmark of the MI355X Filter/Score evaluation engine (BASELINE.json metric).
 
 One step = one pass of the hot path over one batch: Filter + Score of every pending pod against
-every node of the snapshot (NodeResourcesFit + LoadAwareScheduling + NodeNUMAResource) and the
-selectHost of each pod — config 2 of BASELINE.md (10k nodes x 10k pods) per GPU. With --gpus N the
-nodes are sharded (10k per GPU, weak scaling): each rank evaluates its shard, the per-pod best keys
-are all-gathered over RCCL and every rank runs the same global selectHost.
+every node of the snapshot and the selectHost of each pod.
 
-Prints ONE JSON line on rank 0 (value = evals/s over all ranks, inputs resident in HBM).
+  N = 1 (default): config 2 of BASELINE.md — 10k nodes x 10k pods, NodeResourcesFit + LoadAware +
+          NodeNUMAResource, on one GPU.
+  N > 1 (default): config 4 — one 100k-node cluster split contiguously over the N GPUs (strong
+          scaling). Each rank evaluates its shard, the per-pod top-k keys (k = 3, upstream
+          numberOfHighestScoredNodesToReport) are all-gathered over RCCL and every rank runs the same
+          global selectHost (kg_shard_select).
+
+`python bench.py --gpus N` with no launcher environment starts N rank processes itself (RANK,
+WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT set per child) before anything touches the GPU; under
+`torch.distributed.run` each process is one rank. Prints ONE JSON line on rank 0 (value = evals/s over
+all ranks, inputs resident in HBM).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-
-from koordinator_amd import abi, engine, synth  # noqa: E402
-
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak B/s (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak in wave-instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+# instruction (MI355X_MICROARCH.md § Wave scheduling); float64 ops issue over 4 cycles, so a frac
+# computed against this peak is a lower bound on the VALU pipe's utilisation.
+VALU_PEAK = 256 * 4 * 2.4e9 / 2
+# SALU issue peak: one scalar instruction per cycle per CU.
+SALU_PEAK = 256 * 2.4e9
 # Algorithmic bytes per (pod, node) eval, SURVEY.md §8d (scan model, node row read once per eval):
 # NodeResourcesFit 120 B + LoadAware 52 B + NodeNUMAResource 4 B + 0.2 x 64 B zone table = 188.8 B.
 B_EVAL = {1: 172.0, 2: 188.8, 4: 188.8,
@@ -32,6 +44,7 @@ B_EVAL = {1: 172.0, 2: 188.8, 4: 188.8,
 METRIC = "Filter+Score pod-node evals/sec"
 PLUGINS = {1: "+LoadAware", 2: "+LoadAware+NodeNUMAResource", 4: "+LoadAware+NodeNUMAResource",
            5: "+LoadAware+NodeNUMAResource+DeviceShare+Reservation+ElasticQuota"}
+KERNEL_SOURCES = ("kg_eval.h", "kg_ext.h", "kg_kernels.h", "kg_layout.h", "kg_kernels.hip", "kg_ext.hip")
 
 
 def parse():
@@ -39,56 +52,106 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4, 5],
-                    help="2: 10k nodes per GPU x 10k pods (weak scaling, default); 4: 100k nodes split over "
-                         "the GPUs x 10k pods (strong scaling); 5: config 4 + DeviceShare / Reservation / "
+    ap.add_argument("--config", type=int, default=None, choices=[1, 2, 4, 5],
+                    help="2: 10k nodes x 10k pods (default at 1 GPU); 4: 100k nodes split over the GPUs x 10k "
+                         "pods (strong scaling, default at N > 1); 5: config 4 + DeviceShare / Reservation / "
                          "ElasticQuota; 1: the 1k x 500 CPU-harness case")
+    ap.add_argument("--k", type=int, default=None, help="per-pod top-k (default 3 for config 4, else 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-replay", action="store_true")
+    ap.add_argument("--no-cycle", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
 
 
-# VALU issue peak in wave-instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
-# instruction (MI355X_MICROARCH.md: a wave issues each VALU instruction over 2 cycles)
-VALU_PEAK = 256 * 4 * 2.4e9 / 2
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def load_pmc():
-    """The committed rocprofv3 PMC summary of the select kernels (tools/pmc_summary.py), or {}."""
-    path = os.path.join(ROOT, "profiles", "select_pmc.json")
+def launch_ranks(n: int) -> int:
+    """Start n rank processes of this script (one per GPU) and wait for them. The parent never
+    initialises the GPU: it only spawns children with the rendezvous environment."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        rc = rc or code
+    return rc
+
+
+def kernel_source_hash() -> str:
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "koordinator_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def load_pmc(name: str):
+    """A committed rocprofv3 PMC summary (tools/pmc_summary.py) if it was taken on these kernel sources."""
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
-        return {}
+        return None
     try:
         with open(path) as f:
-            return json.load(f)
+            pmc = json.load(f)
     except Exception:
-        return {}
-
-
-def load_traffic():
-    """HBM bytes per select launch from the committed rocprofv3 PMC summary (or None)."""
-    return load_pmc().get("hbm_bytes_per_launch")
-
-
-def valu_issue(avg_kernel_s):
-    """The select's actual ceiling: VALU wave-instructions per launch (SQ_INSTS_VALU of the committed
-    PMC pass, summed over the k_select kernels of one step) / the live kernel time, against VALU_PEAK."""
-    ks = load_pmc().get("kernels", {})
-    insts = sum(v["counters"].get("SQ_INSTS_VALU", 0.0) for k, v in ks.items() if "k_select<" in k)
-    if not insts or not avg_kernel_s:
         return None
-    a = insts / avg_kernel_s
-    return {"bound": "valu", "achieved": a / 1e12, "peak": VALU_PEAK / 1e12, "unit": "T wave-inst/s",
-            "frac": a / VALU_PEAK, "insts_per_launch": insts,
-            "note": "pod tiling serves one node read to 64 pods, so the scan-model HBM frac exceeds 1; the "
-                    "kernel is VALU-issue bound (float64 ops issue over 4 cycles, so this frac is a lower bound)"}
+    if pmc.get("kernel_source_hash") != kernel_source_hash():
+        return None  # stale: taken on other kernel code
+    return pmc
+
+
+def roofline(pmc, kernel_s, evals_per_launch, b_eval, kernel_name):
+    """The dominant kernel's ceiling. The select kernels are bound by instruction issue (VALU, with the
+    CU's single scalar unit as co-limit), not by HBM: pod tiling serves each node record to 64 pods, so
+    the HBM traffic is a few MB per launch. The primary figure is therefore the VALU issue fraction
+    (instructions per launch from the committed PMC pass on these kernel sources / the live average
+    kernel time); the measured HBM bytes and the SURVEY §8d scan model are reported next to it."""
+    out = {"bound": "valu-issue", "achieved": None, "peak": VALU_PEAK / 1e12, "unit": "T wave-inst/s", "frac": None,
+           "traffic": None, "kernel": kernel_name, "kernel_avg_ms": kernel_s * 1e3 if kernel_s else None,
+           "evals_per_launch": evals_per_launch}
+    scan = evals_per_launch * b_eval / kernel_s if kernel_s else None
+    out["scan_model"] = {"bytes_per_eval": b_eval, "effective_GBps": scan / 1e9 if scan else None,
+                         "note": "SURVEY §8d scan model (node row read once per eval); pod tiling reads a row "
+                                 "once per 64 pods, so this is not an HBM utilisation and may exceed 8 TB/s"}
+    if not pmc or not kernel_s:
+        out["note"] = "no PMC summary for these kernel sources: issue / HBM fractions not available"
+        return out
+    valu = pmc.get("valu_insts_per_launch")
+    salu = pmc.get("salu_insts_per_launch")
+    hbm = pmc.get("hbm_bytes_per_launch")
+    if valu:
+        out["achieved"] = valu / kernel_s / 1e12
+        out["frac"] = valu / kernel_s / VALU_PEAK
+    if salu:
+        out["salu"] = {"achieved": salu / kernel_s / 1e12, "peak": SALU_PEAK / 1e12, "unit": "T inst/s",
+                       "frac": salu / kernel_s / SALU_PEAK}
+    if hbm:
+        out["traffic"] = hbm
+        out["hbm"] = {"achieved": hbm / kernel_s / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                      "frac": hbm / kernel_s / HBM_PEAK,
+                      "note": "rocprofv3 FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE per launch"}
+    out["pmc"] = pmc.get("source")
+    return out
 
 
 def cpu_baseline(cfg, nodes, pods, target_s):
     """Oracle (C restatement, upstream-shaped 16-worker parallelizer) on a bounded pod sample."""
+    import numpy as np
+
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib  # test infrastructure: the CPU baseline leg only
+    from koordinator_amd import abi
 
     workers = 16
     kc = cfg.kg_config()
@@ -102,16 +165,21 @@ def cpu_baseline(cfg, nodes, pods, target_s):
     t0 = time.perf_counter()
     oracle_lib.select_parallel(kc, nodes, sample, workers)
     dt = time.perf_counter() - t0
-    return {"value": n * n_nodes / dt, "unit": "evals/s", "cores": workers, "kind": "port",
+    return {"value": n * n_nodes / dt, "unit": "evals/s", "cores": os.cpu_count(), "workers": workers,
+            "kind": "port",
             "sample": f"{n} pods x {n_nodes} nodes ({n * n_nodes} evals) in {dt:.2f} s; oracle/kg_oracle.c "
-                      f"kgo_select_parallel: per pod parallel Filter then parallel Score over nodes, "
-                      f"{workers} workers, chunked like pkg/util/parallelize/parallelism.go:29-49"}
+                      f"kgo_select_parallel: per pod parallel Filter then parallel Score over nodes on {workers} "
+                      f"worker threads (upstream parallelism 16, chunked like pkg/util/parallelize/"
+                      f"parallelism.go:29-49) on a host with {os.cpu_count()} logical CPUs"}
 
 
 def cpu_baseline_ext(kc, nodes, pods, quotas, rsv, target_s):
     """Config 5: the oracle's restatement (one thread) on a bounded pod sample."""
+    import numpy as np
+
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib  # test infrastructure: the CPU baseline leg only
+    from koordinator_amd import abi
 
     n_nodes = abi.table_len(nodes)
     probe = 4
@@ -122,13 +190,17 @@ def cpu_baseline_ext(kc, nodes, pods, quotas, rsv, target_s):
     t0 = time.perf_counter()
     oracle_lib.ext_select(kc, nodes, abi.take(pods, np.arange(n)), 1, 0, quotas, rsv)
     dt = time.perf_counter() - t0
-    return {"value": n * n_nodes / dt, "unit": "evals/s", "cores": 1, "kind": "port",
+    return {"value": n * n_nodes / dt, "unit": "evals/s", "cores": os.cpu_count(), "workers": 1, "kind": "port",
             "sample": f"{n} pods x {n_nodes} nodes ({n * n_nodes} evals) in {dt:.2f} s; oracle/kg_oracle.c "
                       f"kgo_ext_select (all six plugins, NormalizeScore, selectHost), one thread"}
 
 
-def replay_rate(ctx, cfg, with_cpu):
+def replay_rate(ctx, cfg, with_cpu, cpu_s):
     """Config 3: 50k pods placed one by one on 10k nodes with device-resident Assume."""
+    import numpy as np
+
+    from koordinator_amd import abi, engine, synth
+
     _, nodes, pods = synth.cluster(3)
     kc = cfg.kg_config()
     snap = engine.Snapshot(ctx, kc, nodes)
@@ -144,27 +216,65 @@ def replay_rate(ctx, cfg, with_cpu):
            "unschedulable": batch.n - placed, "seconds": round(dt, 4),
            "workload": "config3: 10k nodes x 50k pods, one pod per cycle, Assume on device"}
     if with_cpu:
-        # CPU baseline: the oracle's sequential replay (one thread) of the first pods of the same sequence
+        # CPU baseline: every cycle's Filter / Score on the upstream 16-worker parallelizer, then the
+        # Reserve, for the first pods of the same sequence (bounded sample)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib  # test infrastructure: the CPU baseline leg only
 
-        n = 1500
+        probe = 50
         st = oracle_lib.OracleState(kc, nodes)
         t0 = time.perf_counter()
-        want, _ = st.replay(abi.take(pods, np.arange(n)))
+        st.replay_parallel(abi.take(pods, np.arange(probe)), 16)
+        per = max(time.perf_counter() - t0, 1e-6) / probe
+        n = int(min(batch.n, max(probe * 2, cpu_s / per)))
+        st = oracle_lib.OracleState(kc, nodes)
+        t0 = time.perf_counter()
+        want, _ = st.replay_parallel(abi.take(pods, np.arange(n)), 16)
         cdt = time.perf_counter() - t0
         assert np.array_equal(want, node[:n])  # same placements as the device replay
-        out["cpu_baseline"] = {"value": n / cdt, "unit": "pods/s", "cores": 1, "kind": "port",
-                               "sample": f"first {n} pods of the config-3 sequence, oracle/kg_oracle.c kgo_replay "
-                                         f"(sequential Filter+Score over all nodes + Assume), {cdt:.2f} s"}
+        out["cpu_baseline"] = {"value": n / cdt, "unit": "pods/s", "cores": os.cpu_count(), "workers": 16,
+                               "kind": "port",
+                               "sample": f"first {n} pods of the config-3 sequence in {cdt:.2f} s; oracle/kg_oracle.c "
+                                         f"kgo_replay_parallel: each cycle's Filter then Score over all nodes on 16 "
+                                         f"worker threads (parallelism.go:29-49), then the Reserve"}
+    snap.close()
+    batch.close()
     return out
+
+
+def cycle_rate(ctx, snap, pods_table, steps):
+    """One end-to-end PreFilter cycle as the plugin pays it: pod batch upload (host columns -> HBM), the
+    select over every node, and the download of the per-pod keys."""
+    from koordinator_amd import engine
+
+    batch = engine.PodBatch(ctx, pods_table)
+    engine.eval_select(snap, batch, 1)  # warm-up
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        batch.upload(pods_table)
+        engine.eval_select(snap, batch, 1)  # includes kg_result_keys (device -> host)
+    dt = (time.perf_counter() - t0) / steps
+    n = batch.n
+    batch.close()
+    return {"ms_per_cycle": dt * 1e3, "evals_per_s": n * snap.n / dt, "pods": n, "nodes": snap.n,
+            "note": "kg_pods_upload + kg_eval_select + kg_result_keys per cycle, host buffers in pageable memory"}
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(a.gpus))
+
+    import numpy as np
+
+    from koordinator_amd import abi, engine, synth
+
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    config = a.config if a.config is not None else (2 if world == 1 else 4)
+    k = a.k if a.k is not None else (3 if config == 4 else 1)
     dist = None
     if world > 1:
         import torch.distributed as dist  # bootstrap + host barriers only (data path is RCCL in the library)
@@ -172,11 +282,12 @@ def main():
         dist.init_process_group("gloo")
     ctx = engine.Context(local)
     quotas = rsv = None
-    if a.config == 5:
+    if config == 5:
         cfg, nodes, pods, quotas, rsv = synth.cluster5(100_000, 10_000)
     else:
-        cfg, nodes, pods = synth.cluster(a.config)
-    if a.config in (4, 5):
+        cfg, nodes, pods = synth.cluster(config)
+    all_nodes = nodes
+    if config in (4, 5):
         # one 100k-node cluster, contiguous shard per rank (strong scaling)
         bounds = np.linspace(0, abi.table_len(nodes), world + 1).astype(np.int64)
         base = int(bounds[rank])
@@ -189,7 +300,7 @@ def main():
         # one 10k-node shard per rank (weak scaling)
         n_local = abi.table_len(nodes)
         if world > 1:
-            nodes = synth.nodes(n_local, a.config + 10 * rank, numa=(a.config == 2))
+            nodes = synth.nodes(n_local, config + 10 * rank, numa=(config == 2))
         base = rank * n_local
         n_total = n_local * world
     if world > 1:
@@ -207,9 +318,9 @@ def main():
 
     def step():
         if world > 1:
-            engine.shard_select(snap, batch, download=False)
+            engine.shard_select(snap, batch, k, download=False)
         else:
-            engine.eval_select_async(snap, batch, 1)
+            engine.eval_select_async(snap, batch, k)
 
     for _ in range(a.warmup):
         step()
@@ -235,15 +346,17 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # check the result of the last step is sane (feasible keys point into the cluster)
-    keys = engine.result_keys(batch, 1)[:, 0]
+    # the result of the last step is sane (descending keys pointing into the cluster)
+    keys = engine.result_keys(batch, k)
     idx = abi.key_node(keys)
     assert np.all(idx[keys != 0] < n_total)
+    assert np.all(keys[:, :-1] >= keys[:, 1:])
 
     evals = float(n_pods) * n_total * a.steps
     value = evals / elapsed
-    avg_kernel_s = (kern_ms / 1e3) / max(launches, 1)
-    achieved = (float(n_pods) * n_local * B_EVAL[a.config]) / avg_kernel_s if launches else None
+    avg_kernel_s = (kern_ms / 1e3) / max(launches, 1) if launches else None
+    pmc = load_pmc("select_pmc.json" if config != 5 else "ext_pmc.json") if world == 1 else None
+    kname = "k_select" if config != 5 else "k_ext_select + k_select (plain-pod split, one bracket)"
     out = {
         "metric": METRIC,
         "value": value,
@@ -253,31 +366,28 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if a.config in (4, 5) else "weak",
+        "scaling": "strong" if config in (4, 5) else "weak",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (PCG64 seed 0x6B6F6F7264, SURVEY.md §8d distributions)",
-        "config": {"workload": f"config{a.config}: {n_local} nodes/GPU x {n_pods} pods, Filter+Score+selectHost "
-                               f"(NodeResourcesFit{PLUGINS[a.config]})",
-                   "nodes_per_gpu": n_local, "nodes_total": n_total, "pods": n_pods,
-                   "parallelism": f"node-shard x{world}" + (" + RCCL all-gather of per-pod best keys" if world > 1 else "")},
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None, "peak": HBM_PEAK / 1e9,
-                     "unit": "GB/s", "frac": (achieved / HBM_PEAK) if achieved else None,
-                     "traffic": load_traffic() if a.config != 5 else None,
-                     "kernel": "k_select" if a.config != 5 else "k_ext_select + k_select (plain-pod split, one bracket)", "kernel_avg_ms": avg_kernel_s * 1e3,
-                     "bytes_per_eval": B_EVAL[a.config], "evals_per_launch": n_pods * n_local,
-                     "issue": valu_issue(avg_kernel_s) if a.config == 2 and world == 1 else None},
+        "config": {"workload": f"config{config}: {n_total} nodes ({n_local}/GPU) x {n_pods} pods, "
+                               f"Filter+Score+selectHost top-{k} (NodeResourcesFit{PLUGINS[config]})",
+                   "nodes_per_gpu": n_local, "nodes_total": n_total, "pods": n_pods, "k": k,
+                   "parallelism": f"node-shard x{world}" + (f" + RCCL all-gather of per-pod top-{k} keys" if world > 1 else "")},
+        "roofline": roofline(pmc, avg_kernel_s, n_pods * n_local, B_EVAL[config], kname),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
-        if a.config == 5:
+        if config != 5 and not a.no_cycle:
+            out["cycle"] = cycle_rate(ctx, snap, pods, 10)
+        if config == 5:
             if not a.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline_ext(kc, nodes, pods, quotas, rsv, a.cpu_seconds)
         else:
-            if not a.no_replay:
-                out["replay"] = replay_rate(ctx, cfg, not a.no_cpu_baseline)
+            if not a.no_replay and config in (1, 2):
+                out["replay"] = replay_rate(ctx, cfg, not a.no_cpu_baseline, a.cpu_seconds)
             if not a.no_cpu_baseline:
-                out["cpu_baseline"] = cpu_baseline(cfg, nodes, pods, a.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(cfg, all_nodes, pods, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

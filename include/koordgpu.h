@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 2
+#define KG_ABI_VERSION 3
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -348,9 +348,20 @@ kg_status kg_eval_verify(kg_snap* snap, kg_pods* pods, kg_verify_out* out);
  * asynchronous; results stay on the device until kg_result_keys. */
 kg_status kg_eval_select(kg_snap* snap, kg_pods* pods, uint32_t k);
 kg_status kg_result_keys(kg_pods* pods, uint64_t* out_keys /* n_pods * k */);
+/* Per-pod outcome flags of the last kg_eval_select / kg_shard_select (n_pods entries):
+ *   KG_ST_UNSUPPORTED  some (pod, node) pair needs the host path (cpuset binding, a failing BestEffort
+ *                      NUMA Reserve, DeviceShare with device NUMA hints, ...): the pod's keys cover only
+ *                      the pairs the device decided, so the caller runs the reference plugins for it;
+ *   KG_ST_QUOTA        the ElasticQuota PreFilter rejected the pod (no node evaluated, keys 0);
+ *   0                  the keys are the complete Filter/Score/selectHost result. */
+kg_status kg_result_status(kg_pods* pods, uint32_t* out_status);
 /* Sequential scheduling of pods[0..n) one at a time with Assume applied on the device between pods
- * (the reference's one-pod-per-cycle semantics). out_node[i] = global node index or -1. */
-kg_status kg_replay(kg_snap* snap, kg_pods* pods, int32_t* out_node, int64_t* out_total);
+ * (the reference's one-pod-per-cycle semantics). out_node[i] = global node index or -1.
+ * out_reason (may be NULL): per pod, the OR of the KG_ST_* filter status bits over every node of the
+ * snapshot as it stood in that pod's cycle (0 when every node passed) — the per-plugin reasons the
+ * caller turns into the FitError diagnosis of an unschedulable pod (load_aware.go:48-51,
+ * nodenumaresource/plugin.go:54-63). */
+kg_status kg_replay(kg_snap* snap, kg_pods* pods, int32_t* out_node, int64_t* out_total, uint32_t* out_reason);
 /* Reserve/Unreserve of pod `pod` (batch index) on local node `node`. */
 kg_status kg_assume(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node);
 kg_status kg_forget(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t numa_zone);
@@ -371,9 +382,11 @@ kg_status kg_profile_read(kg_ctx* ctx, double* total_ms, uint64_t* launches, int
 /* Multi-GPU node sharding over RCCL (one process per GPU). */
 kg_status kg_shard_unique_id(uint8_t out[128]);
 kg_status kg_shard_init(kg_ctx* ctx, const uint8_t id[128], int rank, int world);
-/* Local select (k=1) + RCCL all-gather of per-shard best keys + global selectHost.
- * out_keys (host, n_pods entries) may be NULL to leave the result on the device. */
-kg_status kg_shard_select(kg_snap* snap, kg_pods* pods, uint64_t* out_keys);
+/* Local select of the per-pod top k (1 <= k <= 4; k = 3 mirrors upstream
+ * numberOfHighestScoredNodesToReport) + RCCL all-gather of the P x k per-shard keys + the same global
+ * selectHost on every rank. out_keys (host, n_pods * k entries, descending per pod) may be NULL to leave
+ * the result on the device (kg_result_keys reads it). */
+kg_status kg_shard_select(kg_snap* snap, kg_pods* pods, uint32_t k, uint64_t* out_keys);
 
 /* Host-only helpers (no device needed). */
 /* Packed selection key: (total << 32) | (0xFFFFFFFF - node); max key = highest total, lowest index. */

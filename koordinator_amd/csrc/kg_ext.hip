@@ -42,7 +42,7 @@ __device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) {
 
 // ElasticQuota PreFilter of every pod against the batch-start quota state (matrix mode).
 __global__ __launch_bounds__(256) void k_ext_gate(PodsDev pods, uint32_t n_pods, ExtDev e, uint32_t plugins,
-                                                  uint32_t* __restrict__ qst) {
+                                                  uint32_t* __restrict__ qst, uint32_t* __restrict__ pstat) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_pods) return;
     uint32_t s = 0;
@@ -52,6 +52,7 @@ __global__ __launch_bounds__(256) void k_ext_gate(PodsDev pods, uint32_t n_pods,
             s = quota_gate(e.qlim[x.quota], e.qstate[x.quota], load_pod(pods, j), x);
     }
     qst[j] = s;
+    if (pstat) pstat[j] = s;  // a rejected pod is decided; the select kernels OR in KG_ST_UNSUPPORTED
 }
 
 // Verify: raw per-plugin results of every (pod, record) pair, [pod][snapshot index].
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
                                                     uint32_t chunk, uint32_t index_base, KCfg cfg,
                                                     const uint32_t* __restrict__ qst, const uint32_t* __restrict__ dev_max,
                                                     const uint32_t* __restrict__ rsv_max, const uint64_t* __restrict__ pref,
-                                                    uint64_t* __restrict__ partial) {
+                                                    uint64_t* __restrict__ partial, uint32_t* __restrict__ pstat) {
     // lane j = row j of the output; the pod is list[j] (list == nullptr: the batch in order)
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = j < n_pods;
@@ -249,6 +250,10 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
         cv = cfg_in_vgprs(cfg);
     }
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
+    // pairs that need the host path (the FB records' only sources: a cpuset-binding pod under
+    // NodeNUMAResource, and a GPU pod on a NUMA-policy node)
+    uint32_t unsup = 0;
+    const bool bind_unsup = (cfg.plugins & KG_PLUGIN_NUMA) && (p.flags & KG_POD_CPU_BIND) && !(p.flags & KG_POD_NUMA_SKIP);
     for (uint32_t rec = lo; rec < hi; rec++) {
         const int64_t* __restrict__ n = nodes[rec].v;
         if constexpr (FB) {
@@ -260,11 +265,14 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
                 const uint32_t g = index_base + (uint32_t)((uint64_t)fr.flags >> 32);
                 const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, g);
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
+                const uint32_t node_pol = (fl >> F_NUMA_POLICY_SHIFT) & 15u;
+                const bool dev_unsup = px.dcount > 0 && (cfg.plugins & KG_PLUGIN_DEV) && (cfg.plugins & KG_PLUGIN_NUMA) &&
+                                       node_pol != KG_NUMA_NONE;
+                unsup |= (q == 0u && (bind_unsup || dev_unsup)) ? KG_ST_UNSUPPORTED : 0u;
                 PairX x{};
                 if ((cfg.plugins & KG_PLUGIN_DEV) && !st) {  // only the key's zero-ness matters once st != 0
                     st |= dev_eval(cfg, n, dev_of(e, rec), px, x.s_dev);
-                    const uint32_t node_pol = (fl >> F_NUMA_POLICY_SHIFT) & 15u;
-                    if (px.dcount > 0 && (cfg.plugins & KG_PLUGIN_NUMA) && node_pol != KG_NUMA_NONE) st |= KG_ST_UNSUPPORTED;
+                    if (dev_unsup) st |= KG_ST_UNSUPPORTED;
                 }
                 const int64_t tot = (int64_t)(bk >> 32) + total_ext(cfg, x, g, dm, rm, pf);
                 topk_ins<K>(top, st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)));
@@ -272,6 +280,7 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
             }
         }
         const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
+        unsup |= r.status & KG_ST_UNSUPPORTED;
         const uint32_t g = index_base + node_index(nodes[rec]);
         const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
         topk_ins<K>(top, r.status ? 0ull : key);
@@ -280,6 +289,7 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
         uint64_t* dst = partial + ((size_t)blockIdx.y * n_pods + j) * K;
 #pragma unroll
         for (int t = 0; t < K; t++) dst[t] = top[t];
+        if (unsup) atomicOr(pstat + jj, unsup);
     }
 }
 
@@ -287,12 +297,13 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
 // ElasticQuota PreFilter rejected has no feasible node.
 __global__ __launch_bounds__(256) void k_scatter_keys(const uint64_t* __restrict__ src, const uint32_t* __restrict__ map,
                                                       uint32_t n, uint32_t k, const uint32_t* __restrict__ qst,
-                                                      uint64_t* __restrict__ out) {
+                                                      uint64_t* __restrict__ out, uint32_t* __restrict__ pstat) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const uint32_t j = map[t];
     const bool rejected = qst && qst[j] != 0;
     for (uint32_t i = 0; i < k; i++) out[(size_t)j * k + i] = rejected ? 0ull : src[(size_t)t * k + i];
+    if (rejected && pstat) pstat[j] = qst[j];
 }
 
 // One replay step (see file header). buckets: [3][128] ring of per-DeviceShare-score best keys.
@@ -302,7 +313,8 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
                                                    uint32_t n_nodes, uint32_t index_base, KCfg cfg,
                                                    const uint32_t* __restrict__ step_base, uint32_t step_off,
                                                    uint64_t* __restrict__ winners, uint32_t* __restrict__ minors,
-                                                   uint64_t* __restrict__ buckets, int8_t* __restrict__ zsel) {
+                                                   uint64_t* __restrict__ buckets, int8_t* __restrict__ zsel,
+                                                   uint32_t* __restrict__ reason) {
     const uint32_t step = (step_base ? *step_base : 0u) + step_off;
     if (step > n_pods) return;  // uniform
     const uint32_t lane = threadIdx.x;
@@ -380,14 +392,21 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
     if (!has_next) return;  // the final step only applies the last Reserve
     uint64_t kb = 0;
     int32_t s = 0;
+    uint32_t stat = 0;
     if (live) {
         const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, qst);
         zsel[i] = (int8_t)r.zone;
+        stat = r.status;
         if (!r.status) {
             const int64_t base = (int64_t)cfg.w_nrf * r.s_nrf + (int64_t)cfg.w_la * r.s_la + (int64_t)cfg.w_numa * r.s_numa;
             kb = ((uint64_t)base << 32) | (uint64_t)(0xFFFFFFFFu - (index_base + node_index(nodes[i])));
             s = (int32_t)r.s_dev;
         }
+    }
+    if (reason) {  // FitError diagnosis: OR of the filter status bits over the nodes
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) stat |= (uint32_t)__shfl_xor((int)stat, off, 64);
+        if (lane == 0 && stat) atomicOr(reason + step, stat);
     }
     // per-score-bucket wave max, one atomic per distinct score in the wave
     uint64_t* B = buckets + (size_t)(step % 3) * 128;
@@ -436,9 +455,9 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
 // launchers
 
 hipError_t launch_ext_gate(const PodsDev& pods, uint32_t n_pods, const ExtDev& e, uint32_t plugins, uint32_t* qst,
-                           hipStream_t s) {
+                           uint32_t* pstat, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
-    k_ext_gate<<<(n_pods + 255) / 256, 256, 0, s>>>(pods, n_pods, e, plugins, qst);
+    k_ext_gate<<<(n_pods + 255) / 256, 256, 0, s>>>(pods, n_pods, e, plugins, qst, pstat);
     return hipGetLastError();
 }
 
@@ -479,9 +498,9 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
 }
 
 hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, const uint32_t* qst,
-                               uint64_t* out, hipStream_t s) {
+                               uint64_t* out, uint32_t* pstat, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_scatter_keys<<<(n + 255) / 256, 256, 0, s>>>(src, map, n, k, qst, out);
+    k_scatter_keys<<<(n + 255) / 256, 256, 0, s>>>(src, map, n, k, qst, out, pstat);
     return hipGetLastError();
 }
 
@@ -514,12 +533,13 @@ hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, co
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                              const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                              uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
-                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, hipStream_t s) {
+                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
+                             hipStream_t s) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_pods + 255) / 256, (n_nodes + chunk - 1) / chunk);
 #define KG_EXT_SEL(KK, EX, TP, F)                                                                            \
     k_ext_select<KK, EX, TP, F><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n_nodes, n0, chunk, index_base, \
-                                                     cfg, qst, dev_max, rsv_max, pref, partial)
+                                                     cfg, qst, dev_max, rsv_max, pref, partial, pstat)
 #define KG_EXT_SEL_K(KK)                              \
     if (fb) {                                         \
         KG_EXT_SEL(KK, false, false, true);           \
@@ -543,14 +563,14 @@ hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const E
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
-                                  uint64_t* buckets, int8_t* zsel, hipStream_t s) {
+                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, hipStream_t s) {
     dim3 grid((n_nodes + 63) / 64), block(64);
     if (exact)
         k_ext_replay<true><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                  step_off, winners, minors, buckets, zsel);
+                                                  step_off, winners, minors, buckets, zsel, reason);
     else
         k_ext_replay<false><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                   step_off, winners, minors, buckets, zsel);
+                                                   step_off, winners, minors, buckets, zsel, reason);
     return hipGetLastError();
 }
 

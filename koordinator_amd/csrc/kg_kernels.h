@@ -23,6 +23,8 @@ struct LaunchSelect {
     bool exact, fast;
     KCfg cfg;
     uint64_t* partial;
+    const uint32_t* pmap;  // sub-batch row -> batch position (nullptr: identity)
+    uint32_t* pstat;       // per batch position: KG_ST_UNSUPPORTED when some pair needs the host path
 };
 
 // Block replay (k_rb_top / k_rb_merge / k_rb_fix): window of RB_W pods, RB_K keys kept per pod,
@@ -65,7 +67,7 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s);
 
 // config-5 plugin set (kg_ext.hip)
 hipError_t launch_ext_gate(const PodsDev& pods, uint32_t n_pods, const ExtDev& e, uint32_t plugins, uint32_t* qst,
-                           hipStream_t s);
+                           uint32_t* pstat, hipStream_t s);
 hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                              uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                              const uint32_t* qst, const ExtVerifyDev& o, hipStream_t s);
@@ -81,14 +83,16 @@ hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, co
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                              const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                              uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
-                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, hipStream_t s);
-// out[map[t]] = rows t of src (k keys each); rows whose pod has a nonzero qst[pod] get zero keys
+                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
+                             hipStream_t s);
+// out[map[t]] = rows t of src (k keys each); rows whose pod has a nonzero qst[pod] get zero keys and
+// pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the host path)
 hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, const uint32_t* qst,
-                               uint64_t* out, hipStream_t s);
+                               uint64_t* out, uint32_t* pstat, hipStream_t s);
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
-                                  uint64_t* buckets, int8_t* zsel, hipStream_t s);
+                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, hipStream_t s);
 hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                              uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
                              bool exact, int32_t* out, hipStream_t s);
@@ -97,14 +101,14 @@ hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_po
 hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k,
                             const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, const uint32_t* big_list,
                             const uint32_t* big_count, uint32_t index_base, const KCfg& cfg, uint64_t* out,
-                            hipStream_t s);
+                            const uint32_t* pmap, uint32_t* pstat, hipStream_t s);
 hipError_t launch_big_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t* big_list, uint32_t* big_count,
                            hipStream_t s);
 hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, uint32_t n_pods,
                          uint32_t n_nodes, const KCfg& cfg, bool exact, const VerifyDev& o, hipStream_t s);
 hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t n_pods, uint32_t n_nodes,
                               uint32_t index_base, const KCfg& cfg, bool exact, const uint32_t* step_base,
-                              uint32_t step_off, uint64_t* winners, int8_t* zsel, hipStream_t s);
+                              uint32_t step_off, uint64_t* winners, int8_t* zsel, uint32_t* reason, hipStream_t s);
 hipError_t launch_bump(uint32_t* step_base, uint32_t by, hipStream_t s);
 hipError_t launch_rb_window(const LaunchRb& a, hipStream_t s);
 hipError_t launch_assume(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t pod, uint32_t node,

@@ -45,7 +45,8 @@ template <int K, bool EXACT, bool FAST, uint32_t PM, int CLS>
 __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                 PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
                                                 uint32_t chunk, uint32_t part0, uint32_t index_base, KCfg cfg,
-                                                uint64_t* __restrict__ partial) {
+                                                uint64_t* __restrict__ partial, const uint32_t* __restrict__ pmap,
+                                                uint32_t* __restrict__ pstat) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t c = blockIdx.y;
     const bool live = j < n_pods;
@@ -55,7 +56,12 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
     for (int t = 0; t < K; t++) top[t] = 0;
     const uint32_t lo = begin + c * chunk;
     const uint32_t hi = min(end, lo + chunk);
+    uint32_t unsup = 0;
     if constexpr (FAST) {
+        // the fast path's only host-path pairs: a cpuset-binding pod under NodeNUMAResource (pod-level;
+        // Restricted / BestEffort records are F_BIG and flagged by k_merge_big)
+        if ((PM & KG_PLUGIN_NUMA) && (p.flags & KG_POD_CPU_BIND) && !(p.flags & KG_POD_NUMA_SKIP) && hi > lo)
+            unsup = KG_ST_UNSUPPORTED;
         const PodF pf = to_podf(p, cfg);
         const KCfg cv = cfg_in_vgprs(cfg);
         for (uint32_t i = lo; i < hi; i++) {
@@ -68,6 +74,7 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
     } else {
         for (uint32_t i = lo; i < hi; i++) {
             const PairOut o = eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p);
+            unsup |= o.status & KG_ST_UNSUPPORTED;
             topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
         }
     }
@@ -75,6 +82,7 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
         uint64_t* dst = partial + ((size_t)(part0 + c) * n_pods + j) * K;
 #pragma unroll
         for (int t = 0; t < K; t++) dst[t] = top[t];
+        if (unsup) atomicOr(pstat + (pmap ? pmap[j] : j), unsup);
     }
 }
 
@@ -103,7 +111,8 @@ __global__ __launch_bounds__(256) void k_merge_big(const uint64_t* __restrict__ 
                                                    const ZoneRec* __restrict__ zones, PodsDev pods,
                                                    const uint32_t* __restrict__ big_list,
                                                    const uint32_t* __restrict__ big_count, uint32_t index_base,
-                                                   KCfg cfg, uint64_t* __restrict__ out) {
+                                                   KCfg cfg, uint64_t* __restrict__ out,
+                                                   const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_pods) return;
     uint64_t top[K];
@@ -117,11 +126,14 @@ __global__ __launch_bounds__(256) void k_merge_big(const uint64_t* __restrict__ 
     const uint32_t nb = *big_count;
     if (nb) {
         const PodV p = load_pod(pods, j);
+        uint32_t unsup = 0;
         for (uint32_t b = 0; b < nb; b++) {
             const uint32_t i = big_list[b];
             const PairOut o = eval_pair<false>(cfg, nodes[i].v, zones + i, p);
+            unsup |= o.status & KG_ST_UNSUPPORTED;
             topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
         }
+        if (unsup) atomicOr(pstat + (pmap ? pmap[j] : j), unsup);
     }
 #pragma unroll
     for (int t = 0; t < K; t++) out[(size_t)j * K + t] = top[t];
@@ -168,6 +180,12 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off, 64);
+    return v;
+}
+
 // Ordering of LDS accesses between the lanes of a one-wave workgroup: the LDS serves a wave's
 // operations in order, so waiting for this wave's own LDS operations is enough. Unlike
 // __syncthreads(), it leaves the wave's global loads (row prefetches) and stores in flight.
@@ -200,7 +218,8 @@ template <bool EXACT>
 __global__ __launch_bounds__(64) void k_replay(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, PodsDev pods,
                                                uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, KCfg cfg,
                                                const uint32_t* __restrict__ step_base, uint32_t step_off,
-                                               uint64_t* __restrict__ winners, int8_t* __restrict__ zsel) {
+                                               uint64_t* __restrict__ winners, int8_t* __restrict__ zsel,
+                                               uint32_t* __restrict__ reason) {
     const uint32_t step = (step_base ? *step_base : 0u) + step_off;
     if (step > n_pods) return;  // uniform: past the end of the batch
     const uint32_t i = blockIdx.x * 64u + threadIdx.x;
@@ -215,13 +234,19 @@ __global__ __launch_bounds__(64) void k_replay(NodeRec* __restrict__ nodes, Zone
     }
     if (!has_next) return;  // uniform: the final step only applies the last Assume
     uint64_t key = 0;
+    uint32_t st = 0;
     if (live) {
         const PairOut o = eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p);
         key = pair_key(cfg, o, rec_gidx(nodes[i], index_base));
         zsel[i] = (int8_t)o.zone;
+        st = o.status;
     }
     key = wave_max_u64(key);
     if (threadIdx.x == 0 && key) atomicMax((unsigned long long*)&winners[step], (unsigned long long)key);
+    if (reason) {  // FitError diagnosis: OR of the filter status bits over the nodes
+        st = wave_or_u32(st);
+        if (threadIdx.x == 0 && st) atomicOr(reason + step, st);
+    }
 }
 
 __global__ void k_bump(uint32_t* step_base, uint32_t by) {
@@ -457,15 +482,7 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
             if (lane + 64u < NQ) pb2 = piece(rec2, lane + 64u);
         }
     };
-#ifdef KG_RB_CLOCKS
-    uint64_t ck_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t ck_prev = wall_clock64();
-#define RB_TICK(i) do { const uint64_t now_ = wall_clock64(); ck_t[i] += now_ - ck_prev; ck_prev = now_; } while (0)
-#else
-#define RB_TICK(i) do { } while (0)
-#endif
     prefetch(0);
-    RB_TICK(7);
     uint32_t nc = 0, done = 0, last = 0xFFFFFFFFu;  // last: the record the previous pod added to C
     for (uint32_t t = 0; t < (uint32_t)RB_W && base + t < n_pods; t++) {
         const uint32_t j = base + t;
@@ -480,13 +497,11 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
         const uint4 cpre0 = second ? pa2 : pa1, cpre1 = second ? pb2 : pb1;
         // pod t+1's first two entries outside C_t: their rows load while pod t is placed
         if (t + 1 < (uint32_t)RB_W && j + 1 < n_pods) prefetch(t + 1);
-        RB_TICK(0);
         // best key over C
         const uint64_t kc = lane < nc ? ckey[lane][t] : 0ull;
         const uint64_t best_c = wave_max_key(kc);
         const uint64_t best = best_c > cand_key ? best_c : cand_key;
         last = 0xFFFFFFFFu;
-        RB_TICK(1);
         if (best != 0ull) {
             uint32_t slot;
             int32_t zone;
@@ -510,21 +525,17 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
                 slot = (uint32_t)(__ffsll((long long)__ballot(lane < nc && kc == best)) - 1);
                 zone = czone[slot][t];
             }
-            RB_TICK(2);
             if (lane == t) apply_assume(cfg, snode[slot].v, &szone[slot], mp, zone, 1);  // lane t holds pod t
             wave_lds_sync();
-            RB_TICK(3);
             // later pods of the window on the changed row
             if (lane > t && live) {
                 int32_t z = -1;
                 ckey[slot][lane] = eval_slot(slot, &z);
                 czone[slot][lane] = (int8_t)z;
             }
-            RB_TICK(4);
         }
         if (lane == 0) winners[j] = best;
         wave_lds_sync();
-        RB_TICK(5);
         done = t + 1;
     }
     // write the changed rows back
@@ -540,12 +551,6 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
         }
     }
     if (lane == 0) *step = base + done;
-#ifdef KG_RB_CLOCKS
-    RB_TICK(6);
-    if (lane == 0 && base < 400)
-        printf("rb_fix base %u done %u nc %u ticks pick %lu max %lu stage %lu apply %lu reeval %lu book %lu tail %lu head %lu\n",
-               base, done, nc, ck_t[0], ck_t[1], ck_t[2], ck_t[3], ck_t[4], ck_t[5], ck_t[6], ck_t[7]);
-#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -557,7 +562,8 @@ template <int K, bool EXACT, bool FAST, uint32_t PM, int CLS>
 static void select_instance(const LaunchSelect& a, const SelectRange& r, hipStream_t s) {
     dim3 grid((a.n_pods + 255) / 256, r.n_chunks), block(256);
     k_select<K, EXACT, FAST, PM, CLS><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end,
-                                                             r.chunk, r.part0, a.index_base, a.cfg, a.partial);
+                                                             r.chunk, r.part0, a.index_base, a.cfg, a.partial, a.pmap,
+                                                             a.pstat);
 }
 
 template <int K, int CLS>
@@ -610,14 +616,14 @@ hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_po
 hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k,
                             const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, const uint32_t* big_list,
                             const uint32_t* big_count, uint32_t index_base, const KCfg& cfg, uint64_t* out,
-                            hipStream_t s) {
+                            const uint32_t* pmap, uint32_t* pstat, hipStream_t s) {
     dim3 grid((n_pods + 255) / 256), block(256);
     if (k == 1)
         k_merge_big<1><<<grid, block, 0, s>>>(partial, n_parts, n_pods, nodes, zones, pods, big_list, big_count,
-                                              index_base, cfg, out);
+                                              index_base, cfg, out, pmap, pstat);
     else
         k_merge_big<KG_TOPK_MAX><<<grid, block, 0, s>>>(partial, n_parts, n_pods, nodes, zones, pods, big_list,
-                                                        big_count, index_base, cfg, out);
+                                                        big_count, index_base, cfg, out, pmap, pstat);
     return KG_LAUNCH_CHECK();
 }
 
@@ -644,14 +650,14 @@ hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsD
 
 hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t n_pods, uint32_t n_nodes,
                               uint32_t index_base, const KCfg& cfg, bool exact, const uint32_t* step_base,
-                              uint32_t step_off, uint64_t* winners, int8_t* zsel, hipStream_t s) {
+                              uint32_t step_off, uint64_t* winners, int8_t* zsel, uint32_t* reason, hipStream_t s) {
     dim3 grid((n_nodes + 63) / 64), block(64);
     if (exact)
         k_replay<true><<<grid, block, 0, s>>>(nodes, zones, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                              step_off, winners, zsel);
+                                              step_off, winners, zsel, reason);
     else
         k_replay<false><<<grid, block, 0, s>>>(nodes, zones, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                               step_off, winners, zsel);
+                                               step_off, winners, zsel, reason);
     return KG_LAUNCH_CHECK();
 }
 

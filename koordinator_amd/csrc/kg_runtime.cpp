@@ -79,6 +79,10 @@ struct kg_snap {
     std::vector<kg_rsv_view> h_views;  // as uploaded (local snapshot indices)
     std::vector<kg_rsv_info> h_infos;
     std::vector<uint64_t> cls_mask;  // per snapshot index: classes with a view on the node
+    // A Reserve / Unreserve / row update on a node that holds views changes what its views restore
+    // (absolute restored Requested etc.): the caller recomputes the restore (the reference reruns the
+    // Reservation transformer every cycle) and re-uploads; until then selects on the snapshot refuse.
+    bool views_stale = false;
     bool ext() const { return (cfg.plugins & KG_PLUGIN_EXT) != 0; }
     ExtDev ext_dev() const {
         ExtDev e{};
@@ -104,6 +108,8 @@ struct kg_pods {
     size_t partial_cap = 0;  // entries
     uint64_t* d_keys = nullptr;
     uint32_t k_last = 0, kk_last = 0;
+    uint32_t* d_pstat = nullptr;   // per pod: KG_ST_UNSUPPORTED / KG_ST_QUOTA of the last select (kg_result_status)
+    uint32_t* d_reason = nullptr;  // replay: per pod OR of the filter status bits (kg_replay out_reason)
     // replay / shard scratch
     uint64_t* d_winners = nullptr;
     uint32_t* d_step = nullptr;
@@ -498,6 +504,19 @@ void count_topo(kg_snap* s) {
 // Select-mode ext kernels may drop the general topology manager when nothing in the pair set needs it
 bool need_topo(const kg_snap* s, const kg_pods* p) { return s->n_topo != 0 || p->pod_policy; }
 
+kg_status check_views(kg_snap* s) {
+    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->views_stale)
+        return fail(s->ctx, KG_UNSUPPORTED,
+                    "reservation views are stale after a state change on a node holding one: re-upload them "
+                    "(kg_snapshot_upload_reservations)");
+    return KG_OK;
+}
+
+void touch_views(kg_snap* s, uint32_t node) {
+    if (node < s->cls_mask.size() && s->cls_mask[node]) s->views_stale = true;
+}
+
+
 // Place records (indexed by snapshot index) in device order: class 0 then class 1, each ascending.
 void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>& zrs, std::vector<DevRec>* devs = nullptr) {
     const uint32_t n = s->n;
@@ -697,6 +716,7 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
     bool moved = false;  // a row changes storage class: the record groups are rebuilt
     for (uint32_t k = 0; k < n; k++) {
         if (rows[k] >= s->n) return fail(ctx, KG_INVALID_ARG, "row %u >= %u", rows[k], s->n);
+        touch_views(s, rows[k]);
         kg_status st = build_row(ctx, s->cfg, cols, k, &recs[k], &zrs[k]);
         if (st != KG_OK) return st;
         set_node_index(recs[k], rows[k]);
@@ -838,7 +858,9 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_pflags, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_pmap, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_xlist, sizeof(uint32_t) * capacity) == hipSuccess &&
-              hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess;
+              hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
+              hipMalloc(&p->d_pstat, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_reason, sizeof(uint32_t) * (capacity + 1)) == hipSuccess;
     if (!ok) {
         hipFree(p->d_cols);
         hipFree(p->d_flags);
@@ -848,7 +870,7 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
         for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst,
                         (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors,
                         (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_pcols, (void*)p->d_pflags,
-                        (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys})
+                        (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys, (void*)p->d_pstat, (void*)p->d_reason})
             hipFree(b);
         delete p;
         return fail(ctx, KG_OOM, "pod batch of %u", capacity);
@@ -996,7 +1018,8 @@ kg_status kg_pods_destroy(kg_pods* p) {
     hipFree(p->d_gather);
     for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst, (void*)p->d_dev_max,
                     (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout,
-                    (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys})
+                    (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys,
+                    (void*)p->d_pstat, (void*)p->d_reason})
         hipFree(b);
     hipFree(p->d_rbpart);
     hipFree(p->d_rbtops);
@@ -1042,7 +1065,7 @@ static kg_status ext_verify(kg_snap* s, kg_pods* p, kg_verify_out* out) {
     d.status = (uint32_t*)(d.total + pairs);
     d.zone = (int8_t*)(d.status + pairs);
     const ExtDev e = s->ext_dev();
-    hipError_t err = launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, ctx->stream);
+    hipError_t err = launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, nullptr, ctx->stream);
     if (err == hipSuccess)
         err = launch_ext_verify(s->d_nodes, s->d_zones, e, p->dev, p->n, s->n, s->base, s->kcfg, force_exact(), p->d_qst,
                                 d, ctx->stream);
@@ -1069,6 +1092,8 @@ kg_status kg_eval_verify(kg_snap* s, kg_pods* p, kg_verify_out* out) {
     if (!out) return KG_INVALID_ARG;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
+    st = check_views(s);
+    if (st != KG_OK) return st;
     if (s->ext()) return ext_verify(s, p, out);
     const size_t pairs = (size_t)p->n * s->n;
     if (pairs == 0) return KG_OK;
@@ -1127,7 +1152,7 @@ static bool ext_fast_base(const kg_snap* s, const kg_pods* p) {
 static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     kg_ctx* ctx = s->ctx;
     const ExtDev e = s->ext_dev();
-    HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, ctx->stream));
+    HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, p->d_pstat, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_dev_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_pref, 0xFF, sizeof(uint64_t) * p->n, ctx->stream));
@@ -1184,6 +1209,8 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         a.exact = false;
         a.fast = true;
         a.cfg = s->kcfg;
+        a.pmap = p->d_pmap;
+        a.pstat = p->d_pstat;
     }
     const size_t xneed = (size_t)xparts * n_x * kk;
     kg_status st = ensure_partial(p, std::max<size_t>(xneed + (size_t)fparts * n_plain * kk, 1));
@@ -1195,7 +1222,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     if (n_x)
         HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
                                        s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
-                                       p->d_pref, p->d_partial, ctx->stream));
+                                       p->d_pref, p->d_partial, p->d_pstat, ctx->stream));
     if (fparts) HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
@@ -1205,15 +1232,15 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     }
     if (n_x) {
         HIP_TRY(ctx, launch_merge(p->d_partial, xparts, n_x, kk, p->d_tkeys, ctx->stream));
-        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_xlist, n_x, kk, nullptr, d_out, ctx->stream));
+        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_xlist, n_x, kk, nullptr, d_out, nullptr, ctx->stream));
     }
     if (n_plain) {
         if (fparts)
             HIP_TRY(ctx, launch_merge_big(a.partial, fparts, n_plain, kk, s->d_nodes, s->d_zones, p->plain, s->d_big + 1,
-                                          s->d_big, s->base, s->kcfg, p->d_tkeys, ctx->stream));
+                                          s->d_big, s->base, s->kcfg, p->d_tkeys, p->d_pmap, p->d_pstat, ctx->stream));
         else
             HIP_TRY(ctx, hipMemsetAsync(p->d_tkeys, 0, sizeof(uint64_t) * kk * n_plain, ctx->stream));
-        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_pmap, n_plain, kk, p->d_qst, d_out, ctx->stream));
+        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_pmap, n_plain, kk, p->d_qst, d_out, p->d_pstat, ctx->stream));
     }
     return KG_OK;
 }
@@ -1231,6 +1258,7 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
         if (p->n == 0) return KG_OK;
         if (s->n == 0) {
             HIP_TRY(ctx, hipMemsetAsync(d_out, 0, sizeof(uint64_t) * kk * p->n, ctx->stream));
+            HIP_TRY(ctx, hipMemsetAsync(p->d_pstat, 0, sizeof(uint32_t) * p->n, ctx->stream));
             return KG_OK;
         }
         st0 = ext_stats_local(s, p);
@@ -1258,6 +1286,8 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     a.exact = force_exact();
     a.fast = !a.exact && !force_int() && s->weights_small && p->fast_ok;
     a.cfg = s->kcfg;
+    a.pmap = nullptr;
+    a.pstat = p->d_pstat;
     const size_t need = (size_t)std::max<uint32_t>(n_parts, 1) * p->n * kk;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     if (need > p->partial_cap) {
@@ -1273,6 +1303,7 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     p->k_last = k;
     p->kk_last = kk;
     if (p->n == 0) return KG_OK;
+    HIP_TRY(ctx, hipMemsetAsync(p->d_pstat, 0, sizeof(uint32_t) * p->n, ctx->stream));
     if (s->n == 0) {
         HIP_TRY(ctx, hipMemsetAsync(d_out, 0, sizeof(uint64_t) * kk * p->n, ctx->stream));
         return KG_OK;
@@ -1285,7 +1316,7 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     if (st != KG_OK) return st;
     if (a.fast)
         HIP_TRY(ctx, launch_merge_big(p->d_partial, n_parts, p->n, kk, s->d_nodes, s->d_zones, p->dev, s->d_big + 1,
-                                      s->d_big, s->base, s->kcfg, d_out, ctx->stream));
+                                      s->d_big, s->base, s->kcfg, d_out, nullptr, p->d_pstat, ctx->stream));
     else
         HIP_TRY(ctx, launch_merge(p->d_partial, n_parts, p->n, kk, d_out, ctx->stream));
     return KG_OK;
@@ -1295,6 +1326,8 @@ kg_status kg_eval_select(kg_snap* s, kg_pods* p, uint32_t k) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
     std::lock_guard<std::mutex> g(s->ctx->mu);
+    st = check_views(s);
+    if (st != KG_OK) return st;
     return select_local(s, p, k, p->d_keys);
 }
 
@@ -1312,14 +1345,26 @@ kg_status kg_result_keys(kg_pods* p, uint64_t* out) {
     return KG_OK;
 }
 
+kg_status kg_result_status(kg_pods* p, uint32_t* out) {
+    if (!p || !out) return KG_INVALID_ARG;
+    kg_ctx* ctx = p->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (p->k_last == 0) return fail(ctx, KG_INVALID_ARG, "no selection result");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (p->n) HIP_TRY(ctx, hipMemcpyAsync(out, p->d_pstat, sizeof(uint32_t) * p->n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
 }  // extern "C"
 
 namespace {
 constexpr uint32_t REPLAY_G = 256;  // replay steps per captured graph
 
-std::vector<uint8_t> replay_key(const kg_snap* s, const kg_pods* p, bool exact) {
+std::vector<uint8_t> replay_key(const kg_snap* s, const kg_pods* p, bool exact, bool reasons = false) {
     std::vector<uint8_t> k;
     auto put = [&k](const void* x, size_t n) { k.insert(k.end(), (const uint8_t*)x, (const uint8_t*)x + n); };
+    put(&reasons, sizeof(reasons));
     put(&s->d_nodes, sizeof(s->d_nodes));
     put(&s->d_zones, sizeof(s->d_zones));
     put(&s->d_zsel, sizeof(s->d_zsel));
@@ -1332,9 +1377,9 @@ std::vector<uint8_t> replay_key(const kg_snap* s, const kg_pods* p, bool exact) 
 }
 
 // Capture REPLAY_G steps that read their base step from device memory, plus the bump of that base.
-kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact) {
+kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     kg_ctx* ctx = s->ctx;
-    std::vector<uint8_t> key = replay_key(s, p, exact);
+    std::vector<uint8_t> key = replay_key(s, p, exact, reasons);
     if (p->rexec && key == p->rkey) return KG_OK;
     if (p->rexec) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1346,7 +1391,7 @@ kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact) {
     hipError_t e = hipSuccess;
     for (uint32_t t = 0; t < REPLAY_G && e == hipSuccess; t++)
         e = launch_replay_step(s->d_nodes, s->d_zones, p->dev, p->n, s->n, s->base, s->kcfg, exact, p->d_step, t,
-                               p->d_winners, s->d_zsel, ctx->stream);
+                               p->d_winners, s->d_zsel, reasons ? p->d_reason : nullptr, ctx->stream);
     if (e == hipSuccess) e = launch_bump(p->d_step, REPLAY_G, ctx->stream);
     hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
     if (e == hipSuccess) e = ec;
@@ -1431,9 +1476,9 @@ kg_status rb_graph(kg_snap* s, kg_pods* p, bool exact) {
 }
 
 // config-5 replay steps (DeviceShare minors, ElasticQuota used, NormalizeScore via score buckets)
-kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact) {
+kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     kg_ctx* ctx = s->ctx;
-    std::vector<uint8_t> key = replay_key(s, p, exact);
+    std::vector<uint8_t> key = replay_key(s, p, exact, reasons);
     auto put = [&key](const void* x, size_t n) { key.insert(key.end(), (const uint8_t*)x, (const uint8_t*)x + n); };
     put(&s->d_dev, sizeof(s->d_dev));
     put(&s->d_qstate, sizeof(s->d_qstate));
@@ -1450,7 +1495,8 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact) {
     hipError_t err = hipSuccess;
     for (uint32_t t = 0; t < REPLAY_G && err == hipSuccess; t++)
         err = launch_ext_replay_step(s->d_nodes, s->d_zones, s->d_dev, e, p->dev, p->n, s->n, s->base, s->kcfg, exact,
-                                     p->d_step, t, p->d_winners, p->d_minors, p->d_buckets, s->d_zsel, ctx->stream);
+                                     p->d_step, t, p->d_winners, p->d_minors, p->d_buckets, s->d_zsel,
+                                     reasons ? p->d_reason : nullptr, ctx->stream);
     if (err == hipSuccess) err = launch_bump(p->d_step, REPLAY_G, ctx->stream);
     hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
     if (err == hipSuccess) err = ec;
@@ -1464,43 +1510,27 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact) {
 
 extern "C" {
 
-static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total);
+static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total, uint32_t* out_reason);
 
-// Test aid (not part of include/koordgpu.h): run ONE replay window from pod 0 and return its merged
-// per-pod key lists [RB_W][RB_K], the number of pods it placed and their winner keys.
-kg_status kg_debug_rb_window(kg_snap* s, kg_pods* p, uint64_t* lists, uint32_t* placed, uint64_t* winners) {
+kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total, uint32_t* out_reason) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    st = rb_graph(s, p, force_exact());
+    st = check_views(s);
     if (st != KG_OK) return st;
-    HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (p->n + 1), ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
-    HIP_TRY(ctx, launch_rb_window(p->rb_args, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(lists, p->d_rbtops, sizeof(uint64_t) * RB_W * RB_K, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(placed, p->d_step, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(winners, p->d_winners, sizeof(uint64_t) * std::min<uint32_t>(p->n, RB_W), hipMemcpyDeviceToHost,
-                                ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return KG_OK;
-}
-
-kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total) {
-    kg_status st = check_pair(s, p);
-    if (st != KG_OK) return st;
-    kg_ctx* ctx = s->ctx;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    if (s->ext()) return ext_replay(s, p, out_node, out_total);
+    if (s->ext()) return ext_replay(s, p, out_node, out_total, out_reason);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint32_t n = p->n;
     const bool exact = force_exact();
-    // window replay needs the changed-row bitmap in LDS; every config-3 plugin scores a pair from its own row
-    const bool windows = !force_step_replay() && s->n <= 32u * (uint32_t)RB_BITMAP_WORDS;
-    st = windows ? rb_graph(s, p, exact) : replay_graph(s, p, exact);
+    const bool reasons = out_reason != nullptr;
+    // window replay needs the changed-row bitmap in LDS; every config-3 plugin scores a pair from its own row.
+    // The FitError diagnosis (out_reason) needs every node's status in each pod's cycle: one pod per launch.
+    const bool windows = !reasons && !force_step_replay() && s->n <= 32u * (uint32_t)RB_BITMAP_WORDS;
+    st = windows ? rb_graph(s, p, exact) : replay_graph(s, p, exact, reasons);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
+    if (reasons) HIP_TRY(ctx, hipMemsetAsync(p->d_reason, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
@@ -1529,6 +1559,8 @@ kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_tota
     if (st != KG_OK) return st;
     std::vector<uint64_t> w(std::max<uint32_t>(n, 1));
     HIP_TRY(ctx, hipMemcpyAsync(w.data(), p->d_winners, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    if (out_reason && n)
+        HIP_TRY(ctx, hipMemcpyAsync(out_reason, p->d_reason, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (uint32_t j = 0; j < n; j++) {
         if (out_node) out_node[j] = kg_key_node(w[j]);
@@ -1544,6 +1576,7 @@ kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) {
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    touch_views(s, node);
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], -1, 1, s->kcfg, force_exact(), nullptr, ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1558,13 +1591,14 @@ kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     if (zone >= KG_MAX_ZONES) return fail(ctx, KG_UNSUPPORTED, "Unreserve of a multi-zone NUMA allocation (zone code 0x%x)", zone);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    touch_views(s, node);
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return KG_OK;
 }
 
-static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total) {
+static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total, uint32_t* out_reason) {
     kg_ctx* ctx = s->ctx;
     if (s->cfg.plugins & KG_PLUGIN_RSV)
         return fail(ctx, KG_UNSUPPORTED, "replay with Reservation views (their restore changes with every placement)");
@@ -1573,8 +1607,9 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint32_t n = p->n;
     const bool exact = force_exact();
-    st = ext_replay_graph(s, p, exact);
+    st = ext_replay_graph(s, p, exact, out_reason != nullptr);
     if (st != KG_OK) return st;
+    if (out_reason) HIP_TRY(ctx, hipMemsetAsync(p->d_reason, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_minors, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_buckets, 0, sizeof(uint64_t) * 3 * 128, ctx->stream));
@@ -1595,6 +1630,8 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
     }
     std::vector<uint64_t> w(std::max<uint32_t>(n, 1));
     HIP_TRY(ctx, hipMemcpyAsync(w.data(), p->d_winners, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    if (out_reason && n)
+        HIP_TRY(ctx, hipMemcpyAsync(out_reason, p->d_reason, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (uint32_t j = 0; j < n; j++) {
         if (out_node) out_node[j] = kg_key_node(w[j]);
@@ -1623,6 +1660,7 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     st = check_ext(s);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    touch_views(s, node);
     HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone, minors,
                                    sign, s->kcfg, force_exact(), p->d_aout, ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
@@ -1792,6 +1830,7 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
                                       sizeof(int64_t), s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->n_views = nv;
+    s->views_stale = false;
     s->max_cls_views = 0;
     for (int c = 0; c < RSV_MAX_CLASSES; c++) s->max_cls_views = std::max(s->max_cls_views, cb[c + 1] - cb[c]);
     return KG_OK;
@@ -1851,15 +1890,19 @@ kg_status kg_shard_init(kg_ctx* ctx, const uint8_t id[128], int rank, int world)
     return KG_OK;
 }
 
-kg_status kg_shard_select(kg_snap* s, kg_pods* p, uint64_t* out_keys) {
+kg_status kg_shard_select(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* out_keys) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
     if (!ctx->comm) return fail(ctx, KG_INVALID_ARG, "kg_shard_init not called");
+    if (k == 0 || k > (uint32_t)KG_TOPK_MAX) return fail(ctx, KG_INVALID_ARG, "k=%u outside [1, %d]", k, KG_TOPK_MAX);
+    st = check_views(s);
+    if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint32_t n = p->n;
-    const size_t need = (size_t)n * (ctx->world + 1);
+    const uint32_t kk = k == 1 ? 1 : KG_TOPK_MAX;  // kernels keep 1 or KG_TOPK_MAX keys per pod
+    const size_t need = (size_t)n * kk * (ctx->world + 1);
     if (need > p->gather_cap) {
         if (p->d_gather) {
             HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1869,13 +1912,14 @@ kg_status kg_shard_select(kg_snap* s, kg_pods* p, uint64_t* out_keys) {
         HIP_TRY(ctx, hipMalloc(&p->d_gather, sizeof(uint64_t) * std::max<size_t>(need, 1)));
         p->gather_cap = need;
     }
-    uint64_t* local = p->d_gather + (size_t)n * ctx->world;  // this shard's per-pod best key
+    uint64_t* local = p->d_gather + (size_t)n * kk * ctx->world;  // this shard's per-pod top-kk keys
     if (s->ext()) {
         // NormalizeScore maxima and the Reservation preferred node are global over all shards: one
         // all-reduce per statistic between the two passes (a real exchange step)
         st = check_ext(s);
         if (st != KG_OK) return st;
-        p->k_last = p->kk_last = 1;
+        p->k_last = k;
+        p->kk_last = kk;
         if (n == 0) return KG_OK;
         st = ext_stats_local(s, p);
         if (st != KG_OK) return st;
@@ -1883,21 +1927,28 @@ kg_status kg_shard_select(kg_snap* s, kg_pods* p, uint64_t* out_keys) {
         NCCL_TRY(ctx, ncclAllReduce(p->d_rsv_max, p->d_rsv_max, n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
         NCCL_TRY(ctx, ncclAllReduce(p->d_pref, p->d_pref, n, ncclUint64, ncclMin, ctx->comm, ctx->stream));
         if (s->n == 0)
-            HIP_TRY(ctx, hipMemsetAsync(local, 0, sizeof(uint64_t) * n, ctx->stream));
+            HIP_TRY(ctx, hipMemsetAsync(local, 0, sizeof(uint64_t) * n * kk, ctx->stream));
         else
-            st = ext_select_local(s, p, 1, local);
+            st = ext_select_local(s, p, kk, local);
     } else {
-        st = select_local(s, p, 1, local);
+        st = select_local(s, p, k, local);
     }
     if (st != KG_OK) return st;
-    // exchange per-shard best keys (8 B per pod per shard) and run the same global selectHost
-    NCCL_TRY(ctx, ncclAllGather(local, p->d_gather, n, ncclUint64, ctx->comm, ctx->stream));
-    HIP_TRY(ctx, launch_merge(p->d_gather, (uint32_t)ctx->world, n, 1, p->d_keys, ctx->stream));
-    p->k_last = 1;
-    p->kk_last = 1;
+    if (n == 0) return KG_OK;
+    // per-pod outcome flags: the quota verdict is the same on every rank and KG_ST_UNSUPPORTED is the
+    // top bit, so the max over ranks is their OR
+    NCCL_TRY(ctx, ncclAllReduce(p->d_pstat, p->d_pstat, n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
+    // exchange the per-shard top-kk keys (8 B x kk per pod per shard) and run the same global selectHost
+    NCCL_TRY(ctx, ncclAllGather(local, p->d_gather, (size_t)n * kk, ncclUint64, ctx->comm, ctx->stream));
+    HIP_TRY(ctx, launch_merge(p->d_gather, (uint32_t)ctx->world, n, kk, p->d_keys, ctx->stream));
+    p->k_last = k;
+    p->kk_last = kk;
     if (out_keys) {
-        HIP_TRY(ctx, hipMemcpyAsync(out_keys, p->d_keys, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+        std::vector<uint64_t> h((size_t)n * kk);
+        HIP_TRY(ctx, hipMemcpyAsync(h.data(), p->d_keys, sizeof(uint64_t) * n * kk, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        for (uint32_t j = 0; j < n; j++)
+            for (uint32_t t = 0; t < k; t++) out_keys[(size_t)j * k + t] = h[(size_t)j * kk + t];
     }
     return KG_OK;
 }

@@ -74,7 +74,9 @@ def lib():
     L.kg_eval_select.restype = st
     L.kg_result_keys.argtypes = [vp, P(u64)]
     L.kg_result_keys.restype = st
-    L.kg_replay.argtypes = [vp, vp, P(i32), P(i64)]
+    L.kg_result_status.argtypes = [vp, P(u32)]
+    L.kg_result_status.restype = st
+    L.kg_replay.argtypes = [vp, vp, P(i32), P(i64), P(u32)]
     L.kg_replay.restype = st
     L.kg_assume.argtypes = [vp, vp, u32, u32]
     L.kg_assume.restype = st
@@ -88,7 +90,7 @@ def lib():
     L.kg_shard_unique_id.restype = st
     L.kg_shard_init.argtypes = [vp, P(C.c_uint8), C.c_int, C.c_int]
     L.kg_shard_init.restype = st
-    L.kg_shard_select.argtypes = [vp, vp, P(u64)]
+    L.kg_shard_select.argtypes = [vp, vp, u32, P(u64)]
     L.kg_shard_select.restype = st
     L.kg_make_key.argtypes = [i64, u32]
     L.kg_make_key.restype = u64
@@ -295,17 +297,30 @@ def result_keys(pods: PodBatch, k: int) -> np.ndarray:
     return out
 
 
+def result_status(pods: PodBatch) -> np.ndarray:
+    """Per-pod outcome flags of the last select: KG_ST_UNSUPPORTED (some pair needs the reference plugin on
+    the host), KG_ST_QUOTA (ElasticQuota PreFilter rejected the pod), or 0."""
+    out = np.zeros(pods.n, np.uint32)
+    pods.ctx.check(pods.ctx.L.kg_result_status(pods.h, out.ctypes.data_as(C.POINTER(C.c_uint32))), "kg_result_status")
+    return out
+
+
 def eval_select(snap: Snapshot, pods: PodBatch, k: int = 1) -> np.ndarray:
     eval_select_async(snap, pods, k)
     return result_keys(pods, k)
 
 
-def replay(snap: Snapshot, pods: PodBatch):
+def replay(snap: Snapshot, pods: PodBatch, reasons: bool = False):
+    """One pod per cycle with device-resident Assume: (node, total) or, with reasons=True, (node, total,
+    reason) where reason[j] is the OR of the KG_ST_* filter bits over the nodes in pod j's cycle."""
     node = np.zeros(pods.n, np.int32)
     total = np.zeros(pods.n, np.int64)
+    reason = np.zeros(pods.n, np.uint32) if reasons else None
     snap.ctx.check(snap.ctx.L.kg_replay(snap.h, pods.h, node.ctypes.data_as(C.POINTER(C.c_int32)),
-                                        total.ctypes.data_as(C.POINTER(C.c_int64))), "kg_replay")
-    return node, total
+                                        total.ctypes.data_as(C.POINTER(C.c_int64)),
+                                        reason.ctypes.data_as(C.POINTER(C.c_uint32)) if reasons else None),
+                   "kg_replay")
+    return (node, total, reason) if reasons else (node, total)
 
 
 def assume(snap: Snapshot, pods: PodBatch, pod: int, node: int):
@@ -332,9 +347,10 @@ def forget_ext(snap: Snapshot, pods: PodBatch, pod: int, node: int, zone: int, m
     snap.ctx.check(snap.ctx.L.kg_forget_ext(snap.h, pods.h, pod, node, zone, minors), "kg_forget_ext")
 
 
-def shard_select(snap: Snapshot, pods: PodBatch, download: bool = True) -> Optional[np.ndarray]:
-    out = np.zeros(pods.n, np.uint64) if download else None
-    snap.ctx.check(snap.ctx.L.kg_shard_select(snap.h, pods.h, _u64p(out) if download else None), "kg_shard_select")
+def shard_select(snap: Snapshot, pods: PodBatch, k: int = 1, download: bool = True) -> Optional[np.ndarray]:
+    """Node-sharded select over RCCL: per-pod global top-k keys [pods, k] (identical on every rank)."""
+    out = np.zeros((pods.n, k), np.uint64) if download else None
+    snap.ctx.check(snap.ctx.L.kg_shard_select(snap.h, pods.h, k, _u64p(out) if download else None), "kg_shard_select")
     return out
 
 

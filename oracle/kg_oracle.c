@@ -636,6 +636,7 @@ typedef struct par_job {
     int phase; /* 0 filter, 1 score */
     uint8_t* feasible;
     int64_t* total;
+    int32_t* zone; /* NUMA zone the pair's Reserve would allocate from (filter phase) */
     volatile int next_chunk;
     int chunk, n_items;
     const uint32_t* items; /* phase 1: feasible node list */
@@ -643,10 +644,12 @@ typedef struct par_job {
 
 typedef struct par_pool {
     pthread_t* th;
-    int n;
+    int n, workers;
     pthread_barrier_t start, done;
     par_job* job;
     int quit;
+    par_job jb;
+    uint32_t* items;
 } par_pool;
 
 static void par_run(par_job* jb) {
@@ -662,12 +665,13 @@ static void par_run(par_job* jb) {
                 uint32_t i = (uint32_t)x;
                 if (jb->c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(jb->n, i, NULL, jb->p, jb->pod);
                 if (jb->c->plugins & KG_PLUGIN_LA) st |= la_filter(jb->c, jb->n, i, jb->p, jb->pod);
-                int64_t s;
-                int32_t z;
+                int64_t s = 0;
+                int32_t z = -1;
                 if (jb->c->plugins & KG_PLUGIN_NUMA) {
                     st |= numa_eval(jb->c, jb->n, i, NULL, jb->p, jb->pod, &s, &z);
                     jb->total[i] = s; /* NUMA score is produced by the same resource-manager walk */
                 }
+                jb->zone[i] = st ? -1 : z;
                 jb->feasible[i] = st == 0;
             } else {
                 uint32_t i = jb->items[x];
@@ -700,76 +704,97 @@ static int chunk_size(int n, int workers) {
     return c < 1 ? 1 : c;
 }
 
+static int par_open(par_pool* pool, int workers, uint32_t nn) {
+    if (workers < 1) workers = 1;
+    memset(pool, 0, sizeof(*pool));
+    pool->workers = workers;
+    pool->n = workers - 1; /* the calling thread is worker 0 */
+    pool->th = (pthread_t*)calloc((size_t)(pool->n > 0 ? pool->n : 1), sizeof(pthread_t));
+    pool->jb.feasible = (uint8_t*)malloc(nn ? nn : 1);
+    pool->jb.total = (int64_t*)malloc(sizeof(int64_t) * (nn ? nn : 1));
+    pool->jb.zone = (int32_t*)malloc(sizeof(int32_t) * (nn ? nn : 1));
+    pool->items = (uint32_t*)malloc(sizeof(uint32_t) * (nn ? nn : 1));
+    if (!pool->th || !pool->jb.feasible || !pool->jb.total || !pool->jb.zone || !pool->items) return -1;
+    pool->job = &pool->jb;
+    pthread_barrier_init(&pool->start, NULL, (unsigned)workers);
+    pthread_barrier_init(&pool->done, NULL, (unsigned)workers);
+    for (int t = 0; t < pool->n; t++) pthread_create(&pool->th[t], NULL, par_worker, pool);
+    return 0;
+}
+
+static void par_close(par_pool* pool) {
+    pool->quit = 1;
+    pthread_barrier_wait(&pool->start);
+    for (int t = 0; t < pool->n; t++) pthread_join(pool->th[t], NULL);
+    pthread_barrier_destroy(&pool->start);
+    pthread_barrier_destroy(&pool->done);
+    free(pool->th);
+    free(pool->jb.feasible);
+    free(pool->jb.total);
+    free(pool->jb.zone);
+    free(pool->items);
+}
+
+/* One scheduling cycle of pod j on the pool: findNodesThatPassFilters (parallel Filter), then, with more
+ * than one feasible node, prioritizeNodes (parallel Score) and selectHost. Returns the best key and the
+ * NUMA zone of the chosen pair. */
+static uint64_t par_cycle(par_pool* pool, const kg_config* c, const kg_node_columns* n, uint32_t nn, uint32_t base,
+                          const kg_pod_columns* p, uint32_t j, int32_t* zone_out) {
+    par_job* jb = &pool->jb;
+    uint32_t* items = pool->items;
+    jb->c = c;
+    jb->n = n;
+    jb->p = p;
+    jb->nn = nn;
+    jb->pod = j;
+    jb->base = base;
+    jb->phase = 0;
+    jb->n_items = (int)nn;
+    jb->chunk = chunk_size((int)nn, pool->workers);
+    jb->next_chunk = 0;
+    pthread_barrier_wait(&pool->start);
+    par_run(jb);
+    pthread_barrier_wait(&pool->done);
+    uint32_t nf = 0;
+    for (uint32_t i = 0; i < nn; i++)
+        if (jb->feasible[i]) items[nf++] = i;
+    uint64_t best = 0;
+    int32_t zone = -1;
+    if (nf > 1) {
+        /* prioritizeNodes */
+        jb->phase = 1;
+        jb->items = items;
+        jb->n_items = (int)nf;
+        jb->chunk = chunk_size((int)nf, pool->workers);
+        jb->next_chunk = 0;
+        pthread_barrier_wait(&pool->start);
+        par_run(jb);
+        pthread_barrier_wait(&pool->done);
+        /* selectHost (deterministic tie-break) */
+        for (uint32_t x = 0; x < nf; x++) {
+            uint64_t key = make_key(jb->total[items[x]], base + items[x]);
+            if (key > best) {
+                best = key;
+                zone = jb->zone[items[x]];
+            }
+        }
+    } else if (nf == 1) {
+        /* exactly one feasible node: chosen without scoring; key still carries its total */
+        kgo_pair r;
+        kgo_eval_pair(c, n, items[0], p, j, &r);
+        best = make_key(r.total, base + items[0]);
+        zone = jb->zone[items[0]];
+    }
+    if (zone_out) *zone_out = zone;
+    return best;
+}
+
 int kgo_select_parallel(const kg_config* c, const kg_node_columns* n, uint32_t nn, uint32_t base,
                         const kg_pod_columns* p, uint32_t np, int workers, uint64_t* keys) {
-    if (workers < 1) workers = 1;
     par_pool pool;
-    memset(&pool, 0, sizeof(pool));
-    pool.n = workers - 1; /* the calling thread is worker 0 */
-    pool.th = (pthread_t*)calloc((size_t)(pool.n > 0 ? pool.n : 1), sizeof(pthread_t));
-    uint8_t* feasible = (uint8_t*)malloc(nn);
-    int64_t* total = (int64_t*)malloc(sizeof(int64_t) * (nn ? nn : 1));
-    uint32_t* items = (uint32_t*)malloc(sizeof(uint32_t) * (nn ? nn : 1));
-    if (!pool.th || !feasible || !total || !items) return -1;
-    par_job jb;
-    memset(&jb, 0, sizeof(jb));
-    pool.job = &jb;
-    pthread_barrier_init(&pool.start, NULL, (unsigned)workers);
-    pthread_barrier_init(&pool.done, NULL, (unsigned)workers);
-    for (int t = 0; t < pool.n; t++) pthread_create(&pool.th[t], NULL, par_worker, &pool);
-    for (uint32_t j = 0; j < np; j++) {
-        /* findNodesThatPassFilters */
-        jb.c = c;
-        jb.n = n;
-        jb.p = p;
-        jb.nn = nn;
-        jb.pod = j;
-        jb.base = base;
-        jb.feasible = feasible;
-        jb.total = total;
-        jb.phase = 0;
-        jb.n_items = (int)nn;
-        jb.chunk = chunk_size((int)nn, workers);
-        jb.next_chunk = 0;
-        pthread_barrier_wait(&pool.start);
-        par_run(&jb);
-        pthread_barrier_wait(&pool.done);
-        uint32_t nf = 0;
-        for (uint32_t i = 0; i < nn; i++)
-            if (feasible[i]) items[nf++] = i;
-        uint64_t best = 0;
-        if (nf > 1) {
-            /* prioritizeNodes */
-            jb.phase = 1;
-            jb.items = items;
-            jb.n_items = (int)nf;
-            jb.chunk = chunk_size((int)nf, workers);
-            jb.next_chunk = 0;
-            pthread_barrier_wait(&pool.start);
-            par_run(&jb);
-            pthread_barrier_wait(&pool.done);
-            /* selectHost (deterministic tie-break) */
-            for (uint32_t x = 0; x < nf; x++) {
-                uint64_t key = make_key(total[items[x]], base + items[x]);
-                if (key > best) best = key;
-            }
-        } else if (nf == 1) {
-            /* exactly one feasible node: chosen without scoring; key still carries its total */
-            kgo_pair r;
-            kgo_eval_pair(c, n, items[0], p, j, &r);
-            best = make_key(r.total, base + items[0]);
-        }
-        keys[j] = best;
-    }
-    pool.quit = 1;
-    pthread_barrier_wait(&pool.start);
-    for (int t = 0; t < pool.n; t++) pthread_join(pool.th[t], NULL);
-    pthread_barrier_destroy(&pool.start);
-    pthread_barrier_destroy(&pool.done);
-    free(pool.th);
-    free(feasible);
-    free(total);
-    free(items);
+    if (par_open(&pool, workers, nn)) return -1;
+    for (uint32_t j = 0; j < np; j++) keys[j] = par_cycle(&pool, c, n, nn, base, p, j, NULL);
+    par_close(&pool);
     return 0;
 }
 
@@ -981,15 +1006,17 @@ void kgo_forget(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_colu
 }
 
 void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
-                int32_t* out_node, int64_t* out_total) {
+                int32_t* out_node, int64_t* out_total, uint32_t* out_reason) {
     kg_node_columns v;
     kgo_state_view(st, &v);
     for (uint32_t j = 0; j < np; j++) {
         uint64_t best = 0;
         int32_t best_zone = -1;
+        uint32_t why = 0;
         for (uint32_t i = 0; i < st->n; i++) {
             kgo_pair r;
             kgo_eval_pair(c, &v, i, p, j, &r);
+            why |= r.status;
             if (r.status) continue;
             uint64_t key = make_key(r.total, base + i);
             if (key > best) {
@@ -997,6 +1024,7 @@ void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_c
                 best_zone = r.zone;
             }
         }
+        if (out_reason) out_reason[j] = why;
         if (!best) {
             out_node[j] = -1;
             if (out_total) out_total[j] = -1;
@@ -1007,6 +1035,31 @@ void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_c
         if (out_total) out_total[j] = (int64_t)(best >> 32);
         apply(c, st, g - base, p, j, best_zone, 1);
     }
+}
+
+/* The CPU baseline of replay: every pod's cycle on the upstream-shaped parallelizer (kgo_select_parallel's
+ * filter / score phases over n_workers threads), then its Reserve, sequentially across pods. */
+int kgo_replay_parallel(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
+                        int workers, int32_t* out_node, int64_t* out_total) {
+    kg_node_columns v;
+    kgo_state_view(st, &v);
+    par_pool pool;
+    if (par_open(&pool, workers, st->n)) return -1;
+    for (uint32_t j = 0; j < np; j++) {
+        int32_t zone = -1;
+        const uint64_t best = par_cycle(&pool, c, &v, st->n, base, p, j, &zone);
+        if (!best) {
+            out_node[j] = -1;
+            if (out_total) out_total[j] = -1;
+            continue;
+        }
+        const uint32_t g = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
+        out_node[j] = (int32_t)g;
+        if (out_total) out_total[j] = (int64_t)(best >> 32);
+        apply(c, st, g - base, p, j, zone, 1);
+    }
+    par_close(&pool);
+    return 0;
 }
 
 /* ============================================================================================== */
@@ -1691,7 +1744,7 @@ int kgo_ext_shard_select(const kg_config* c, const kg_node_columns* n, uint32_t 
  * changes with every placement): returns -1 when KG_PLUGIN_RSV is enabled. out_minors may be NULL. */
 int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
                    const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
-                   int64_t* quota_used_out, int64_t* quota_np_used_out) {
+                   int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason) {
     if (c->plugins & KG_PLUGIN_RSV) return -1;
     kg_node_columns v;
     kgo_state_view(st, &v);
@@ -1703,7 +1756,9 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
         ext_pod_finish(c, &b.r, st->n, base);
         uint64_t best = 0;
         int32_t best_zone = -1;
+        uint32_t why = 0;
         for (uint32_t i = 0; i < st->n; i++) {
+            why |= b.r.st[i];
             if (b.r.st[i]) continue;
             uint64_t key = make_key(b.r.total[i], base + i);
             if (key > best) {
@@ -1712,6 +1767,7 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
             }
         }
         if (out_minors) out_minors[j] = 0;
+        if (out_reason) out_reason[j] = why;
         if (!best) {
             out_node[j] = -1;
             if (out_total) out_total[j] = -1;

@@ -56,9 +56,14 @@ void kgo_assume(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod
 /* Unreserve (reverse of kgo_assume with the zone chosen at Reserve). */
 void kgo_forget(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod,
                 int32_t zone);
-/* One-pod-per-cycle scheduling with Assume between pods. */
+/* One-pod-per-cycle scheduling with Assume between pods. out_reason (may be NULL): per pod, the OR of
+ * the filter status bits over every node in that pod's cycle (the FitError diagnosis). */
 void kgo_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, const kg_pod_columns* pods,
-                uint32_t n_pods, int32_t* out_node, int64_t* out_total);
+                uint32_t n_pods, int32_t* out_node, int64_t* out_total, uint32_t* out_reason);
+
+/* Replay CPU baseline: each pod's cycle on the parallelizer (kgo_select_parallel), then its Reserve. */
+int kgo_replay_parallel(const kg_config* cfg, kgo_state* st, uint32_t index_base, const kg_pod_columns* pods,
+                        uint32_t n_pods, int n_workers, int32_t* out_node, int64_t* out_total);
 
 /* Config-5 plugins (DeviceShare, Reservation, ElasticQuota): the tables the plugins read besides the
  * node columns. quotas: state at the start of the batch; views / infos: Reservation restore views. */
@@ -81,7 +86,7 @@ int kgo_ext_select(const kg_config* cfg, const kg_node_columns* nodes, uint32_t 
  * quota_*_out: final used / non-preemptible used [quota][KG_QUOTA_R]. -1 with KG_PLUGIN_RSV. */
 int kgo_ext_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, const kg_pod_columns* pods,
                    uint32_t n_pods, const kgo_ext* ext, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
-                   int64_t* quota_used_out, int64_t* quota_np_used_out);
+                   int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason);
 int64_t kgo_mem_bytes_to_ratio(int64_t bytes, int64_t total);
 /* Node-sharded two-pass selection: per-shard NormalizeScore inputs (to be max / min all-reduced over
  * the shards), then the shard's top-k with the global inputs. */

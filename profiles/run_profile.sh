@@ -1,27 +1,35 @@
 #!/bin/bash
-# rocprofv3 collection for the select kernel (run on the GPU box from the repo root):
-#   bash profiles/run_profile.sh <tag>
+# rocprofv3 collection for the select kernels (run on the GPU box from the repo root):
+#   bash profiles/run_profile.sh <tag> [config]      (config 2 default; 5 = the config-5 plugin set)
 # 1) kernel trace + stats of a bench run (per-kernel average durations);
-# 2) separate PMC passes (gfx950 slot limits): FETCH_SIZE, WRITE_SIZE, SQ instruction mix / cycles.
+# 2) separate PMC passes (gfx950 slot limits): FETCH_SIZE, WRITE_SIZE, SQ instruction mix / cycles;
+# 3) tools/pmc_summary.py -> gpurun_out/prof_<tag>/summary.json (copy it to profiles/ to commit).
 set -uo pipefail
-TAG=${1:-r1}
+TAG=${1:-r2}
+CFG=${2:-2}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-BENCH=("$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-replay)
-PMC_BENCH=("$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --no-replay)
+BENCH=("$R/bench.py" --config "$CFG" --steps 20 --warmup 2 --no-cpu-baseline --no-replay --no-cycle)
+PMC_BENCH=("$R/bench.py" --config "$CFG" --steps 4 --warmup 1 --no-cpu-baseline --no-replay --no-cycle)
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python3 "${BENCH[@]}" > "$OUT/bench_under_trace.json" || exit $?
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
     python3 "${PMC_BENCH[@]}" > /dev/null || exit $?
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
     python3 "${PMC_BENCH[@]}" > /dev/null || exit $?
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
     SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d "$OUT/pmc_sq" -o run --output-format csv -- \
     python3 "${PMC_BENCH[@]}" > /dev/null || exit $?
-timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INST_CYCLES_VMEM -d "$OUT/pmc_clk" \
+timeout -s KILL 150 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INST_CYCLES_VMEM -d "$OUT/pmc_clk" \
     -o run --output-format csv -- python3 "${PMC_BENCH[@]}" > /dev/null || exit $?
+cd "$R" || exit 1
+if [ "$CFG" = "5" ]; then
+    python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_ext_select<" "k_select<" || exit $?
+else
+    python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_select<" || exit $?
+fi
 echo "profile done: $OUT"

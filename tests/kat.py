@@ -8,7 +8,7 @@ from __future__ import annotations
 import json
 import os
 
-from koordinator_amd import abi, decode
+from koordinator_amd import abi, decode, reasons
 from koordinator_amd.config import AggregatedArgs, LoadAwareArgs, SchedulerConfig
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -108,11 +108,4 @@ def la_case(case, default_node):
 
 def la_status(bits: int):
     """KG_ST_* bits of the LoadAware plugin -> (code, reason) of the Go Status."""
-    if bits & abi.KG_ST_LA_EXPIRED:
-        return "Unschedulable", "node(s) nodeMetric expired"
-    for bit, res in ((abi.KG_ST_LA_CPU, "cpu"), (abi.KG_ST_LA_MEM, "memory")):
-        if bits & bit:
-            if bits & abi.KG_ST_LA_AGG:
-                return "Unschedulable", f"node(s) {res} aggregated usage exceed threshold"
-            return "Unschedulable", f"node(s) {res} usage exceed threshold"
-    return "Success", None
+    return reasons.loadaware_status(bits)

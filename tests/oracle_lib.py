@@ -68,7 +68,10 @@ def lib():
         L.kgo_assume.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32]
         L.kgo_forget.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32, C.c_int32]
         L.kgo_replay.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
-                                 P(C.c_int32), P(C.c_int64)]
+                                 P(C.c_int32), P(C.c_int64), P(C.c_uint32)]
+        L.kgo_replay_parallel.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
+                                          C.c_int, P(C.c_int32), P(C.c_int64)]
+        L.kgo_replay_parallel.restype = C.c_int
         L.kgo_ext_verify.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns),
                                      C.c_uint32, P(KgoExt), P(abi.KgVerifyOut)]
         L.kgo_ext_verify.restype = C.c_int
@@ -77,7 +80,7 @@ def lib():
         L.kgo_ext_select.restype = C.c_int
         L.kgo_ext_replay.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
                                      P(KgoExt), P(C.c_int32), P(C.c_int64), P(C.c_uint32), P(C.c_int64),
-                                     P(C.c_int64)]
+                                     P(C.c_int64), P(C.c_uint32)]
         L.kgo_ext_replay.restype = C.c_int
         L.kgo_ext_shard_stats.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
                                           P(abi.KgPodColumns), C.c_uint32, P(KgoExt), P(C.c_uint32), P(C.c_uint32),
@@ -195,20 +198,35 @@ class OracleState:
         pc = abi.pod_columns(pods)
         lib().kgo_forget(C.byref(self.cfg), self.h, node, C.byref(pc), pod, zone)
 
-    def replay(self, pods: abi.Table, index_base: int = 0):
+    def replay(self, pods: abi.Table, index_base: int = 0, reasons: bool = False):
+        np_ = abi.table_len(pods)
+        out_node = np.zeros(np_, np.int32)
+        out_total = np.zeros(np_, np.int64)
+        out_reason = np.zeros(np_, np.uint32)
+        pc = abi.pod_columns(pods)
+        lib().kgo_replay(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_,
+                         out_node.ctypes.data_as(C.POINTER(C.c_int32)), out_total.ctypes.data_as(C.POINTER(C.c_int64)),
+                         out_reason.ctypes.data_as(C.POINTER(C.c_uint32)))
+        return (out_node, out_total, out_reason) if reasons else (out_node, out_total)
+
+    def replay_parallel(self, pods: abi.Table, workers: int = 16, index_base: int = 0):
+        """The replay CPU baseline: each cycle's Filter / Score on the 16-worker parallelizer."""
         np_ = abi.table_len(pods)
         out_node = np.zeros(np_, np.int32)
         out_total = np.zeros(np_, np.int64)
         pc = abi.pod_columns(pods)
-        lib().kgo_replay(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_,
-                         out_node.ctypes.data_as(C.POINTER(C.c_int32)), out_total.ctypes.data_as(C.POINTER(C.c_int64)))
+        rc = lib().kgo_replay_parallel(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_, workers,
+                                       out_node.ctypes.data_as(C.POINTER(C.c_int32)),
+                                       out_total.ctypes.data_as(C.POINTER(C.c_int64)))
+        assert rc == 0
         return out_node, out_total
 
-    def ext_replay(self, pods: abi.Table, quotas=None, index_base: int = 0):
+    def ext_replay(self, pods: abi.Table, quotas=None, index_base: int = 0, reasons: bool = False):
         np_ = abi.table_len(pods)
         out_node = np.zeros(np_, np.int32)
         out_total = np.zeros(np_, np.int64)
         out_minors = np.zeros(np_, np.uint32)
+        out_reason = np.zeros(np_, np.uint32)
         nq = len(quotas["used"]) if quotas is not None else 0
         qu = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
         qn = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
@@ -217,8 +235,10 @@ class OracleState:
         rc = lib().kgo_ext_replay(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_, C.byref(e),
                                   out_node.ctypes.data_as(P(C.c_int32)), out_total.ctypes.data_as(P(C.c_int64)),
                                   out_minors.ctypes.data_as(P(C.c_uint32)), qu.ctypes.data_as(P(C.c_int64)),
-                                  qn.ctypes.data_as(P(C.c_int64)))
+                                  qn.ctypes.data_as(P(C.c_int64)), out_reason.ctypes.data_as(P(C.c_uint32)))
         assert rc == 0
+        if reasons:
+            return out_node, out_total, out_minors, qu[:nq], qn[:nq], out_reason
         return out_node, out_total, out_minors, qu[:nq], qn[:nq]
 
     def dev_free(self) -> np.ndarray:

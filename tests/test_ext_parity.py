@@ -207,17 +207,60 @@ def test_config5_full_size_sampled(ctx):
     assert (keys != 0).mean() > 0.5
 
 
-def test_ext_shard_select_single_rank(ctx):
+@pytest.mark.parametrize("k", [1, 3])
+def test_ext_shard_select_single_rank(ctx, k):
     """kg_shard_select's config-5 path (stats pass, RCCL all-reduce of the NormalizeScore inputs,
-    select pass, all-gather, merge) with one rank equals the global selection."""
+    select pass, all-gather of the per-shard top-k, merge) with one rank equals the global selection."""
     cfg, nodes, pods, quotas, rsv = synth.cluster5(1500, 256, seed_config=61, rsv_frac=0.3)
     kc = cfg.kg_config()
     sctx = engine.Context(0)
     try:
         sctx.shard_init(engine.shard_unique_id(), 0, 1)
         snap, batch = make(sctx, kc, nodes, pods, quotas, rsv)
-        got = engine.shard_select(snap, batch)
+        got = engine.shard_select(snap, batch, k)
+        again = engine.result_keys(batch, k)
+        status = engine.result_status(batch)
     finally:
         sctx.close()
-    want = oracle_lib.ext_select(kc, nodes, pods, 1, 0, quotas, rsv)[:, 0]
+    want = oracle_lib.ext_select(kc, nodes, pods, k, 0, quotas, rsv)
     assert np.array_equal(got, want)
+    assert np.array_equal(again, want)
+    ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
+    assert np.array_equal(status, np.bitwise_or.reduce(ref.status & (abi.KG_ST_UNSUPPORTED | abi.KG_ST_QUOTA), axis=1))
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_ext_result_status(ctx, monkeypatch, split):
+    """kg_result_status on config 5: GPU pods on NUMA-policy nodes and cpuset-binding pods are flagged
+    KG_ST_UNSUPPORTED, quota-rejected pods KG_ST_QUOTA — the OR of the oracle verify rows' bits."""
+    monkeypatch.setenv("KG_EXT_SPLIT", split)
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(1200, 400, seed_config=73, rsv_frac=0.2)
+    nodes = {k: v.copy() for k, v in nodes.items()}
+    pods = {k: v.copy() for k, v in pods.items()}
+    nodes["numa_policy"][::50] = abi.KG_NUMA_SINGLE_NODE
+    nodes["numa_zones"][::50] = np.maximum(nodes["numa_zones"][::50], 1)
+    pods["flags"][1::11] |= abi.KG_POD_CPU_BIND
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_select(snap, batch, 1)
+    want = oracle_lib.ext_select(kc, nodes, pods, 1, 0, quotas, rsv)
+    assert np.array_equal(got, want)
+    ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
+    wstat = np.bitwise_or.reduce(ref.status & (abi.KG_ST_UNSUPPORTED | abi.KG_ST_QUOTA), axis=1)
+    assert np.array_equal(engine.result_status(batch), wstat)
+    assert (wstat & abi.KG_ST_UNSUPPORTED).any() and (wstat & abi.KG_ST_QUOTA).any() and (wstat == 0).any()
+
+
+def test_views_stale_after_assume_on_view_node(ctx):
+    """A Reserve on a node holding reservation views changes what the views restore: selects refuse
+    (KG_UNSUPPORTED) until the caller re-uploads the recomputed views."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(600, 64, seed_config=74, rsv_frac=0.5)
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    view_nodes = sorted({int(v.node) for v in rsv.view_list()})
+    engine.eval_select(snap, batch, 1)
+    zone, minors = engine.assume_ext(snap, batch, 0, view_nodes[0])
+    with pytest.raises(engine.Unsupported):
+        engine.eval_select(snap, batch, 1)
+    snap.upload_reservations(rsv)
+    engine.eval_select(snap, batch, 1)

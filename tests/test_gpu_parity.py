@@ -399,3 +399,58 @@ def test_window_replay_edge_cases(ctx, n_nodes, n_pods, scale):
     got_state, want_state = snap.read_state(), st.table()
     for k, v in got_state.items():
         assert np.array_equal(v, want_state[k]), k
+
+
+@pytest.mark.parametrize("ext", [False, True])
+def test_replay_reasons_match_oracle(ctx, ext):
+    """kg_replay's out_reason: per pod the OR of the filter status bits over every node in its cycle,
+    equal to the oracle's, and rebuilt into the reference's FitError reason strings."""
+    from koordinator_amd import reasons
+
+    if ext:
+        cfg, nodes, pods, quotas, _ = synth.cluster5(700, 1500, seed_config=44)
+        kc = cfg.kg_config()
+        kc.plugins &= ~abi.KG_PLUGIN_RSV
+        snap = engine.Snapshot(ctx, kc, nodes)
+        snap.upload_quotas(quotas)
+        batch = engine.PodBatch(ctx, pods)
+        node, total, why = engine.replay(snap, batch, reasons=True)
+        onode, ototal, _, _, _, owhy = oracle_lib.OracleState(kc, nodes).ext_replay(pods, quotas, reasons=True)
+    else:
+        cfg, nodes, pods = synth.small(400, 900, seed=12, scale=10.0)
+        kc = cfg.kg_config()
+        snap = engine.Snapshot(ctx, kc, nodes)
+        node, total, why = engine.replay(snap, engine.PodBatch(ctx, pods), reasons=True)
+        onode, ototal, owhy = oracle_lib.OracleState(kc, nodes).replay(pods, reasons=True)
+    assert np.array_equal(node, onode)
+    assert np.array_equal(total, ototal)
+    assert np.array_equal(why, owhy)
+    unsched = node < 0
+    assert unsched.any() and np.all(why[unsched] != 0)
+    msgs = reasons.reasons(int(why[np.flatnonzero(unsched)[0]]))
+    assert msgs and all(isinstance(m, str) for m in msgs)
+    assert any(m.startswith("Insufficient") or m == "Too many pods" for m in
+               (x for w in why[unsched] for x in reasons.reasons(int(w))))
+
+
+def test_result_status_flags_host_path_pods(ctx):
+    """kg_result_status: pods with a pair the device cannot decide (cpuset binding under
+    NodeNUMAResource; a BestEffort node without zones) are flagged KG_ST_UNSUPPORTED, exactly the pods
+    whose oracle verify row carries the bit; every other pod's keys are complete."""
+    cfg, nodes, pods = synth.small(900, 300, seed=23, numa=True)
+    pods = {k: v.copy() for k, v in pods.items()}
+    pods["flags"][::7] |= abi.KG_POD_CPU_BIND
+    nodes = {k: v.copy() for k, v in nodes.items()}
+    nodes["numa_policy"][5:9] = abi.KG_NUMA_BEST_EFFORT
+    nodes["numa_zones"][5:7] = 0
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    batch = engine.PodBatch(ctx, pods)
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    want = np.bitwise_or.reduce(ref.status & abi.KG_ST_UNSUPPORTED, axis=1)
+    for k in (1, 4):
+        keys = engine.eval_select(snap, batch, k)
+        assert np.array_equal(keys, oracle_lib.select(kc, nodes, pods, k))
+        got = engine.result_status(batch)
+        assert np.array_equal(got, want)
+    assert (want != 0).any() and (want == 0).any()

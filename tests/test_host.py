@@ -177,3 +177,25 @@ def test_pod_requests_sidecars_and_overhead():
 ])
 def test_priority_class_with_default(spec, want):
     assert decode.priority_class(kat.make_pod(spec)) == want
+
+
+def test_oracle_parallel_replay_equals_sequential():
+    """The replay CPU baseline (each cycle on the 16-worker parallelizer) places exactly like kgo_replay."""
+    cfg, nodes, pods = synth.small(300, 400, seed=24, scale=6.0, numa=True)
+    kc = cfg.kg_config()
+    want, wtot = oracle_lib.OracleState(kc, nodes).replay(pods)
+    for workers in (1, 5, 16):
+        got, gtot = oracle_lib.OracleState(kc, nodes).replay_parallel(pods, workers)
+        assert np.array_equal(got, want) and np.array_equal(gtot, wtot)
+    assert (want < 0).any() and (want >= 0).any()
+
+
+def test_reason_strings():
+    from koordinator_amd import reasons
+    bits = abi.KG_ST_NRF_CPU | abi.KG_ST_LA_MEM | abi.KG_ST_LA_AGG | abi.KG_ST_NUMA_AMP_CPU
+    got = reasons.plugin_reasons(bits)
+    assert got["NodeResourcesFit"] == ["Insufficient cpu"]
+    assert got["LoadAwareScheduling"] == ["node(s) memory aggregated usage exceed threshold"]
+    assert got["NodeNUMAResource"] == ["Insufficient amplified cpu"]
+    assert reasons.reasons(0) == []
+    assert reasons.loadaware_status(abi.KG_ST_LA_EXPIRED) == ("Unschedulable", "node(s) nodeMetric expired")

@@ -51,9 +51,12 @@ def _worker(rank, world, port, n_nodes, n_pods, k, bounds, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bounds,k", [((0, 500, 1000), 1), ((0, 333, 1000), 3), ((0, 1, 1000), 2)])
+@pytest.mark.parametrize("bounds,k", [((0, 500, 1000), 1), ((0, 333, 1000), 3), ((0, 1, 1000), 2),
+                                     ((0, 250, 500, 750, 1000), 3), ((0, 100, 101, 600, 1000), 3)])
 def test_sharded_select_matches_global(bounds, k):
-    world = 2
+    """P x k per-shard keys all-gathered (world 2 and 4, k up to 3 = numberOfHighestScoredNodesToReport)
+    and merged: the global top-k, including an empty shard's contribution."""
+    world = len(bounds) - 1
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -107,9 +110,9 @@ def _ext_worker(rank, world, port, n_nodes, n_pods, k, bounds, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bounds,k", [((0, 400, 900), 1), ((0, 450, 900), 3)])
+@pytest.mark.parametrize("bounds,k", [((0, 400, 900), 1), ((0, 450, 900), 3), ((0, 200, 450, 700, 900), 3)])
 def test_sharded_ext_select_matches_global(bounds, k):
-    world = 2
+    world = len(bounds) - 1
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
