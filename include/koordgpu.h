@@ -177,7 +177,15 @@ typedef struct kg_config {
     uint32_t numa_most_allocated;
     uint32_t numa_hint_most_allocated;
     uint32_t dev_most_allocated;
-    uint32_t pad_;
+    /* NodeResourcesFit scoringStrategy per resource: bit r set = MostAllocated for resource r of {cpu,
+     * memory, scalar0, scalar1} (all bits: upstream's MostAllocated strategy; a mix: the per-resource
+     * types of NodeResourcesFitPlus, noderesourcefitplus/node_resource_fit_plus_utils.go:58-86). */
+    uint32_t nrf_most_allocated;
+    /* Scalar resources left out of the fit checks (bit k: scalar k), from NodeResourcesFitArgs
+     * IgnoredResources / IgnoredResourceGroups and the Reservation plugin's ignored resources
+     * (reservation/plugin.go:897-909: extended resources only, never the native ones). */
+    uint32_t nrf_ignored_scalars;
+    uint32_t rsv_ignored_scalars;
 } kg_config;
 
 /* Node snapshot, struct-of-arrays host columns, n_nodes entries each (caller-owned, copied). */

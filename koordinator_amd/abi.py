@@ -112,7 +112,9 @@ class KgConfig(C.Structure):
         ("numa_most_allocated", C.c_uint32),
         ("numa_hint_most_allocated", C.c_uint32),
         ("dev_most_allocated", C.c_uint32),
-        ("pad_", C.c_uint32),
+        ("nrf_most_allocated", C.c_uint32),
+        ("nrf_ignored_scalars", C.c_uint32),
+        ("rsv_ignored_scalars", C.c_uint32),
     ]
 
 

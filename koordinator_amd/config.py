@@ -110,6 +110,22 @@ class SchedulerConfig:
     numa_strategy: str = "LeastAllocated"
     numa_hint_strategy: str = "LeastAllocated"
     dev_strategy: str = "LeastAllocated"
+    # NodeResourcesFit per-resource MostAllocated (upstream MostAllocated strategy = every resource;
+    # NodeResourcesFitPlus allows a mix)
+    nrf_most: Tuple[str, ...] = ()
+    # IgnoredResources / IgnoredResourceGroups of NodeResourcesFit and of the Reservation plugin (extended
+    # resources only; a group is the name's prefix before "/")
+    nrf_ignored: Tuple[str, ...] = ()
+    nrf_ignored_groups: Tuple[str, ...] = ()
+    rsv_ignored: Tuple[str, ...] = ()
+    rsv_ignored_groups: Tuple[str, ...] = ()
+
+    def _ignore_mask(self, names, groups) -> int:
+        m = 0
+        for k, name in enumerate(self.scalar_resources):
+            if name in names or (name.split("/", 1)[0] in groups and "/" in name):
+                m |= 1 << k
+        return m
 
     def la(self) -> LoadAwareArgs:
         return self.loadaware.defaulted()
@@ -148,6 +164,10 @@ class SchedulerConfig:
         c.numa_most_allocated = int(self.numa_strategy == "MostAllocated")
         c.numa_hint_most_allocated = int(self.numa_hint_strategy == "MostAllocated")
         c.dev_most_allocated = int(self.dev_strategy == "MostAllocated")
+        names = (CPU, MEMORY) + tuple(self.scalar_resources)
+        c.nrf_most_allocated = sum(1 << r for r, name in enumerate(names) if name in self.nrf_most)
+        c.nrf_ignored_scalars = self._ignore_mask(self.nrf_ignored, self.nrf_ignored_groups)
+        c.rsv_ignored_scalars = self._ignore_mask(self.rsv_ignored, self.rsv_ignored_groups)
         ds = dict(self.dev_scoring)
         for r, name in enumerate(DEV_RESOURCES):
             c.dev_w[r] = ds.get(name, 0)

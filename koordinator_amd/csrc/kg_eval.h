@@ -400,10 +400,6 @@ template <bool EXACT, bool OV = false, bool TOPO = true, bool SCORE = true>
 __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restrict__ n, const ZoneRec* __restrict__ zr,
                                           const PodV& p, uint32_t flags, PairOut& o, const Over* ov = nullptr) {
     if (p.flags & KG_POD_NUMA_SKIP) return;
-    if (p.flags & KG_POD_CPU_BIND) {
-        o.status |= KG_ST_UNSUPPORTED;
-        return;
-    }
     const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u;
     const uint32_t pod_pol = (p.flags >> 16) & 15u;
     if (node_pol != KG_NUMA_NONE && pod_pol != KG_NUMA_NONE && pod_pol != node_pol) {
@@ -412,16 +408,23 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
     }
     const uint32_t pol = pod_pol != KG_NUMA_NONE ? pod_pol : node_pol;
     const bool amp = (flags & F_AMP) != 0;
+    const bool cpu_bind = (p.flags & KG_POD_CPU_BIND) != 0;
     const int64_t pod_cpu = p.req_cpu;
-    // filterAmplifiedCPUs
+    // filterAmplifiedCPUs (plugin.go:461-498): a cpuset-binding pod's request is amplified too
     if (pod_cpu != 0 && amp) {
         int64_t requested = nv<OV>(n, ov, N_REQ_CPU);
         const int64_t cs = n[N_CPUSET];
         if (requested >= cs && cs > 0) requested = requested - cs + n[N_AMP_CPUSET];
-        if (pod_cpu > n[N_ALLOC_CPU] - requested) {
+        const int64_t need = cpu_bind ? (int64_t)ceil(__dmul_rn((double)pod_cpu, zr->amp_ratio)) : pod_cpu;
+        if (need > n[N_ALLOC_CPU] - requested) {
             o.status |= KG_ST_NUMA_AMP_CPU;
             return;
         }
+    }
+    // the cpuset allocation (cpu_accumulator.go) runs on the host (plugin.go:396-440)
+    if (cpu_bind) {
+        o.status |= KG_ST_UNSUPPORTED;
+        return;
     }
     const double rcp_cpu = as_f64(n[N_RCP_CPU]), rcp_mem = as_f64(n[N_RCP_MEM]);
     const bool most = (c.most & MOST_NUMA) != 0;
@@ -527,34 +530,37 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
         st |= (p.req_cpu > 0 && p.req_cpu > n[N_ALLOC_CPU] - nv<OV>(n, ov, N_REQ_CPU)) ? KG_ST_NRF_CPU : 0u;
         st |= (p.req_mem > 0 && p.req_mem > n[N_ALLOC_MEM] - nv<OV>(n, ov, N_REQ_MEM)) ? KG_ST_NRF_MEM : 0u;
         st |= (p.req_eph > 0 && p.req_eph > n[N_ALLOC_EPH] - nv<OV>(n, ov, N_REQ_EPH)) ? KG_ST_NRF_EPH : 0u;
-        st |= (p.sc0 != 0 && p.sc0 > n[N_SC_ALLOC0] - nv<OV>(n, ov, N_SC_REQ0)) ? KG_ST_NRF_SC0 : 0u;
-        st |= (p.sc1 != 0 && p.sc1 > n[N_SC_ALLOC1] - nv<OV>(n, ov, N_SC_REQ1)) ? KG_ST_NRF_SC1 : 0u;
+        st |= (p.sc0 != 0 && !(c.nrf_ign & 1u) && p.sc0 > n[N_SC_ALLOC0] - nv<OV>(n, ov, N_SC_REQ0)) ? KG_ST_NRF_SC0 : 0u;
+        st |= (p.sc1 != 0 && !(c.nrf_ign & 2u) && p.sc1 > n[N_SC_ALLOC1] - nv<OV>(n, ov, N_SC_REQ1)) ? KG_ST_NRF_SC1 : 0u;
         o.status |= st;
         if constexpr (SCORE) {
-        // LeastAllocated over {cpu, memory, scalar0, scalar1}
+        // LeastAllocated (or, per resource, MostAllocated) over {cpu, memory, scalar0, scalar1}
         int64_t sum = 0, wsum = 0;
+        auto term = [&](int r, int64_t req, int64_t cap, double rcp) -> int64_t {
+            return ((c.nrf_most >> r) & 1u) ? most_req(req, cap) : least_req<EXACT>(req, cap, rcp);
+        };
         {
             const int64_t cap = n[N_ALLOC_CPU], w = c.nrf_w[0];
             const bool on = (w != 0) & (cap != 0);
-            sum += on ? least_req<EXACT>(nv<OV>(n, ov, N_NZ_CPU) + p.nz_cpu, cap, as_f64(n[N_RCP_CPU])) * w : 0;
+            sum += on ? term(0, nv<OV>(n, ov, N_NZ_CPU) + p.nz_cpu, cap, as_f64(n[N_RCP_CPU])) * w : 0;
             wsum += on ? w : 0;
         }
         {
             const int64_t cap = n[N_ALLOC_MEM], w = c.nrf_w[1];
             const bool on = (w != 0) & (cap != 0);
-            sum += on ? least_req<EXACT>(nv<OV>(n, ov, N_NZ_MEM) + p.nz_mem, cap, as_f64(n[N_RCP_MEM])) * w : 0;
+            sum += on ? term(1, nv<OV>(n, ov, N_NZ_MEM) + p.nz_mem, cap, as_f64(n[N_RCP_MEM])) * w : 0;
             wsum += on ? w : 0;
         }
         {
             const int64_t cap = n[N_SC_ALLOC0], w = c.nrf_w[2];
             const bool on = (w != 0) & (cap != 0) & (p.sc0 != 0);
-            sum += on ? least_req<EXACT>(nv<OV>(n, ov, N_SC_REQ0) + p.sc0, cap, as_f64(n[N_RCP_SC0])) * w : 0;
+            sum += on ? term(2, nv<OV>(n, ov, N_SC_REQ0) + p.sc0, cap, as_f64(n[N_RCP_SC0])) * w : 0;
             wsum += on ? w : 0;
         }
         {
             const int64_t cap = n[N_SC_ALLOC1], w = c.nrf_w[3];
             const bool on = (w != 0) & (cap != 0) & (p.sc1 != 0);
-            sum += on ? least_req<EXACT>(nv<OV>(n, ov, N_SC_REQ1) + p.sc1, cap, as_f64(n[N_RCP_SC1])) * w : 0;
+            sum += on ? term(3, nv<OV>(n, ov, N_SC_REQ1) + p.sc1, cap, as_f64(n[N_RCP_SC1])) * w : 0;
             wsum += on ? w : 0;
         }
         o.s_nrf = wdiv(sum, wsum);

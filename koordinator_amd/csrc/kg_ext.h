@@ -237,7 +237,7 @@ __device__ __forceinline__ RsvPod rsv_pod(const PodV& p) {
 
 // fitsNode: bitmask of insufficient resources (bit 5 = pods); rem == nullptr -> zero remained
 __device__ __forceinline__ uint32_t rsv_fits_node(const RsvPod& q, const int64_t* __restrict__ n, const RsvView& v,
-                                                  const int64_t* rem) {
+                                                  const int64_t* rem, uint32_t ign) {
     uint32_t bad = 0;
     if (v.num_pods - (int64_t)v.count + 1 > n[N_ALLOC_PODS]) bad |= 1u << 5;
     if (q.preq[0] == 0 && q.preq[1] == 0 && q.preq[2] == 0 && !(q.names & 0x18u)) return bad;
@@ -245,18 +245,20 @@ __device__ __forceinline__ uint32_t rsv_fits_node(const RsvPod& q, const int64_t
 #pragma unroll
     for (int k = 0; k < RSV_R; k++) {
         if (k >= 3 && !((q.names >> k) & 1u)) continue;
+        if (k >= 3 && ((ign >> (k - 3)) & 1u)) continue;  // isResourceIgnored (reservation/plugin.go:951-953)
         const int64_t rk = rem ? rem[k] : 0;
         if (q.preq[k] > alloc[k] - (v.pod_requested[k] - rk - v.r_allocated[k])) bad |= 1u << k;
     }
     return bad;
 }
 
-__device__ __forceinline__ uint32_t rsv_fits_reservation(const RsvPod& q, const RsvInfo& r) {
+__device__ __forceinline__ uint32_t rsv_fits_reservation(const RsvPod& q, const RsvInfo& r, uint32_t ign) {
     uint32_t bad = 0;
     if (r.max_pods >= 0 && r.allocated_pods + 1 > r.max_pods) bad |= 1u << 5;
 #pragma unroll
     for (int k = 0; k < RSV_R; k++) {
         if (!((r.names >> k) & 1u)) continue;
+        if (k >= 3 && ((ign >> (k - 3)) & 1u)) continue;
         if (!((q.names >> k) & 1u) || q.preq[k] == 0) continue;
         const int64_t used = r.allocated[k] < 0 ? 0 : r.allocated[k];
         const int64_t cap = r.allocatable[k] - r.reserved[k];
@@ -268,38 +270,38 @@ __device__ __forceinline__ uint32_t rsv_fits_reservation(const RsvPod& q, const 
 
 // fitsNodeAndReservation: true when the pod fits node + reservation r
 __device__ __forceinline__ bool rsv_fits_one(const RsvPod& q, const int64_t* __restrict__ n, const RsvView& v,
-                                             const RsvInfo& r, uint32_t& bn, uint32_t& br) {
+                                             const RsvInfo& r, uint32_t& bn, uint32_t& br, uint32_t ign) {
     int64_t rem[RSV_R];
 #pragma unroll
     for (int k = 0; k < RSV_R; k++) {
         const int64_t x = r.allocatable[k] - r.allocated[k] - r.reserved[k];
         rem[k] = x < 0 ? 0 : x;
     }
-    bn = rsv_fits_node(q, n, v, rem);
+    bn = rsv_fits_node(q, n, v, rem, ign);
     br = 0;
     if (r.policy == KG_RSV_RESTRICTED) {
-        br = rsv_fits_reservation(q, r);
+        br = rsv_fits_reservation(q, r, ign);
         return bn == 0 && br == 0;
     }
     return bn == 0;
 }
 
 __device__ __forceinline__ uint32_t rsv_filter(const RsvPod& q, const int64_t* __restrict__ n, const RsvView* v,
-                                               const RsvInfo* __restrict__ infos) {
+                                               const RsvInfo* __restrict__ infos, uint32_t ign) {
     if (!v) return q.required ? KG_ST_RSV_AFFINITY : 0u;
     uint32_t any_node = 0, any_resv = 0;
     for (uint32_t t = 0; t < v->count; t++) {
         const RsvInfo& r = infos[v->first + t];
         if (!q.required && !(r.names & q.names)) continue;
         uint32_t bn, br;
-        if (rsv_fits_one(q, n, *v, r, bn, br)) return 0;
+        if (rsv_fits_one(q, n, *v, r, bn, br, ign)) return 0;
         any_node |= bn;
         any_resv |= br;
     }
     if (q.required)
         return ((any_resv != 0 || any_node == 0) ? KG_ST_RSV_RESERVATION : 0u) | (any_node ? KG_ST_RSV_NODE : 0u);
     if (any_node) return KG_ST_RSV_NODE;
-    return rsv_fits_node(q, n, *v, nullptr) ? KG_ST_RSV_NODE : 0u;
+    return rsv_fits_node(q, n, *v, nullptr, ign) ? KG_ST_RSV_NODE : 0u;
 }
 
 __device__ __forceinline__ int64_t rsv_score_reservation(const RsvPod& q, const RsvInfo& r) {
@@ -321,7 +323,8 @@ __device__ __forceinline__ int64_t rsv_score_reservation(const RsvPod& q, const 
 
 // nominated reservation's ScoreReservation and the node's most-preferred order (0 = none)
 __device__ __forceinline__ int64_t rsv_nominate_score(const RsvPod& q, const int64_t* __restrict__ n, const RsvView& v,
-                                                      const RsvInfo* __restrict__ infos, int64_t& node_order) {
+                                                      const RsvInfo* __restrict__ infos, int64_t& node_order,
+                                                      uint32_t ign) {
     node_order = 0;
     int64_t sel = INT64_MAX;
     for (uint32_t t = 0; t < v.count; t++) {
@@ -343,7 +346,7 @@ __device__ __forceinline__ int64_t rsv_nominate_score(const RsvPod& q, const int
             if (r.allocate_once && r.allocated_pods > 0) continue;
             if (!q.required && !(r.names & q.names)) continue;
             uint32_t bn, br;
-            if (!rsv_fits_one(q, n, v, r, bn, br)) continue;
+            if (!rsv_fits_one(q, n, v, r, bn, br, ign)) continue;
             okm |= 1u << t;
             nc++;
             last = (int)t;
@@ -431,7 +434,7 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     RsvPod q;
     if (c.plugins & KG_PLUGIN_RSV) {
         q = rsv_pod(p);
-        st |= rsv_filter(q, n, v, e.infos);
+        st |= rsv_filter(q, n, v, e.infos, c.rsv_ign);
     }
     o.status = st;
     o.s_nrf = b.s_nrf;
@@ -440,7 +443,7 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     if (st) return o;
     o.zone = b.zone;
     o.s_dev = dev_raw;
-    if (v) o.s_rsv = rsv_nominate_score(q, n, *v, e.infos, o.order);
+    if (v) o.s_rsv = rsv_nominate_score(q, n, *v, e.infos, o.order, c.rsv_ign);
     return o;
 }
 

@@ -150,7 +150,6 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
                 int64_t raw = 0;
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
                 if (!st) st |= dev_eval(cfg, n, dev_of(e, rec), px, raw);
-                if ((cfg.plugins & KG_PLUGIN_NUMA) && ((fl >> F_NUMA_POLICY_SHIFT) & 15u) != KG_NUMA_NONE) st |= KG_ST_UNSUPPORTED;
                 if (!st) dmax = max(dmax, (uint32_t)raw);
                 continue;
             }
@@ -223,7 +222,7 @@ __device__ __forceinline__ void topk_ins(uint64_t (&top)[K], uint64_t key) {
 // arithmetic: same feasibility and weighted total as eval_pair), and only DeviceShare, the
 // reservation-affinity check and the normalised terms are evaluated on top.
 template <int K, bool EXACT, bool TOPO, bool FB>
-__global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+__global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                     ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
                                                     uint32_t n_pods, uint32_t n_nodes, uint32_t n0,
                                                     uint32_t chunk, uint32_t index_base, KCfg cfg,
@@ -250,10 +249,11 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
         cv = cfg_in_vgprs(cfg);
     }
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
-    // pairs that need the host path (the FB records' only sources: a cpuset-binding pod under
-    // NodeNUMAResource, and a GPU pod on a NUMA-policy node)
-    uint32_t unsup = 0;
-    const bool bind_unsup = (cfg.plugins & KG_PLUGIN_NUMA) && (p.flags & KG_POD_CPU_BIND) && !(p.flags & KG_POD_NUMA_SKIP);
+    // pairs that need the host path: a cpuset-binding pod under NodeNUMAResource has one on every node
+    // (numa_eval), whatever path the record takes; FB records (class 0, not F_BIG: NUMA policy None) have
+    // no other source
+    uint32_t unsup = ((cfg.plugins & KG_PLUGIN_NUMA) && (p.flags & KG_POD_CPU_BIND) && !(p.flags & KG_POD_NUMA_SKIP) &&
+                      q == 0u && hi > lo) ? KG_ST_UNSUPPORTED : 0u;
     for (uint32_t rec = lo; rec < hi; rec++) {
         const int64_t* __restrict__ n = nodes[rec].v;
         if constexpr (FB) {
@@ -265,15 +265,9 @@ __global__ __launch_bounds__(256) void k_ext_select(const NodeRec* __restrict__ 
                 const uint32_t g = index_base + (uint32_t)((uint64_t)fr.flags >> 32);
                 const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, g);
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
-                const uint32_t node_pol = (fl >> F_NUMA_POLICY_SHIFT) & 15u;
-                const bool dev_unsup = px.dcount > 0 && (cfg.plugins & KG_PLUGIN_DEV) && (cfg.plugins & KG_PLUGIN_NUMA) &&
-                                       node_pol != KG_NUMA_NONE;
-                unsup |= (q == 0u && (bind_unsup || dev_unsup)) ? KG_ST_UNSUPPORTED : 0u;
                 PairX x{};
-                if ((cfg.plugins & KG_PLUGIN_DEV) && !st) {  // only the key's zero-ness matters once st != 0
+                if ((cfg.plugins & KG_PLUGIN_DEV) && !st)  // only the key's zero-ness matters once st != 0
                     st |= dev_eval(cfg, n, dev_of(e, rec), px, x.s_dev);
-                    if (dev_unsup) st |= KG_ST_UNSUPPORTED;
-                }
                 const int64_t tot = (int64_t)(bk >> 32) + total_ext(cfg, x, g, dm, rm, pf);
                 topk_ins<K>(top, st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)));
                 continue;

@@ -117,6 +117,8 @@ struct alignas(64) ZoneRec {
     double rcp_cpu[MAX_ZONES], rcp_mem[MAX_ZONES];
     ZoneFast zf[MAX_ZONES];
     uint32_t status;  // NUMANodeSharedStatus, 2 bits per zone (0 idle, 1 single, 2 shared)
+    uint32_t pad_;
+    double amp_ratio;  // cpu amplification ratio (filterAmplifiedCPUs amplifies a cpuset-binding pod's request)
 };
 
 // Magnitude bound of the float64 fast path: operands below 2^44 keep 100 * headroom below 2^51
@@ -257,6 +259,8 @@ struct KCfg {
     int32_t w_dev, w_rsv;
     int32_t dev_w[3];  // DeviceShare LeastAllocated weights {gpu-core, gpu-memory-ratio, gpu-memory}
     uint32_t most;     // MostAllocated strategies: bit 0 NUMA score, bit 1 NUMA hint score, bit 2 DeviceShare
+    uint32_t nrf_most; // NodeResourcesFit MostAllocated resources: bit r of {cpu, memory, scalar0, scalar1}
+    uint32_t nrf_ign, rsv_ign;  // scalars left out of NodeResourcesFit Fits / Reservation fitsNode (bit k)
 };
 enum : uint32_t { MOST_NUMA = 1u, MOST_NUMA_HINT = 2u, MOST_DEV = 4u };
 

@@ -286,6 +286,11 @@ kg_status build_kcfg(kg_ctx* ctx, const kg_config* c, KCfg* k) {
     k->la_hw = half_rcp(k->la_wsum);
     k->most = (c->numa_most_allocated ? MOST_NUMA : 0u) | (c->numa_hint_most_allocated ? MOST_NUMA_HINT : 0u) |
               (c->dev_most_allocated ? MOST_DEV : 0u);
+    if (c->nrf_most_allocated & ~0xFu) return fail(ctx, KG_INVALID_ARG, "nrf_most_allocated 0x%x", c->nrf_most_allocated);
+    k->nrf_most = c->nrf_most_allocated;
+    if ((c->nrf_ignored_scalars | c->rsv_ignored_scalars) & ~3u) return fail(ctx, KG_INVALID_ARG, "ignored scalar mask");
+    k->nrf_ign = c->nrf_ignored_scalars;
+    k->rsv_ign = c->rsv_ignored_scalars;
     return KG_OK;
 }
 
@@ -407,6 +412,7 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
         zf.hpack = pack_f32(half_rcp((hc + hm) / 2), half_rcp((fc + fm) / 2));
     }
     zr->status = COL(s->numa_zone_status, i);
+    zr->amp_ratio = ratio > 1 ? ratio : 1.0;
     if (zr->status >> (2 * KG_MAX_ZONES)) return fail(ctx, KG_INVALID_ARG, "node %u: zone status 0x%x", i, zr->status);
     derive_node(*rec, *zr);
     return KG_OK;
@@ -647,7 +653,9 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
         s->weights_small = true;
         for (int64_t w : rw) s->weights_small &= (w >= 0 && w <= 4096);
         s->weights_small &= (cfg->la_w[0] + cfg->la_w[1] + cfg->la_dominant_w) <= 4096;
-        s->weights_small &= !cfg->numa_most_allocated && !cfg->numa_hint_most_allocated;  // fast path: LeastAllocated
+        s->weights_small &= !cfg->numa_most_allocated && !cfg->numa_hint_most_allocated &&
+                            !cfg->nrf_most_allocated &&  // fast path: LeastAllocated
+                            !cfg->nrf_ignored_scalars;     // fast path: every requested scalar is checked
     }
     s->n = n_nodes;
     s->base = index_base;

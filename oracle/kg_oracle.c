@@ -59,8 +59,8 @@ typedef struct kgo_over {
 /* ---------------------------------------------------------------------------------------------- */
 /* NodeResourcesFit (upstream v1.35.6)                                              */
 
-static uint32_t nrf_filter(const kg_node_columns* n, uint32_t i, const kgo_over* ov, const kg_pod_columns* p,
-                           uint32_t j) {
+static uint32_t nrf_filter(const kg_config* c, const kg_node_columns* n, uint32_t i, const kgo_over* ov,
+                           const kg_pod_columns* p, uint32_t j) {
     uint32_t st = 0;
     /* fitsRequest: len(nodeInfo.Pods)+1 > allowedPodNumber */
     if (N_NUM_PODS(n, i, ov) + 1 > n->alloc_pods[i]) st |= KG_ST_NRF_PODS;
@@ -71,6 +71,7 @@ static uint32_t nrf_filter(const kg_node_columns* n, uint32_t i, const kgo_over*
     for (int k = 0; k < KG_NSCALAR; k++) {
         int64_t q = p->sc_req[k][j];
         if (q == 0) continue; /* "Skip in case request quantity is zero" */
+        if ((c->nrf_ignored_scalars >> k) & 1u) continue; /* NodeResourcesFitArgs IgnoredResources(Groups) */
         if (q > n->sc_alloc[k][i] - N_REQ_SC(n, k, i, ov)) st |= (k == 0 ? KG_ST_NRF_SC0 : KG_ST_NRF_SC1);
     }
     return st;
@@ -79,6 +80,8 @@ static uint32_t nrf_filter(const kg_node_columns* n, uint32_t i, const kgo_over*
 /* resourceAllocationScorer.score + leastResourceScorer with NonZeroRequested for cpu/memory and
  * Requested for scalars; scalars the pod does not request are bypassed (0, 0); resources with
  * allocatable 0 are skipped (mirrors noderesourcefitplus/node_resource_fit_plus_utils.go:114-139). */
+static int64_t most_requested_score(int64_t requested, int64_t capacity);
+
 static int64_t nrf_score(const kg_config* c, const kg_node_columns* n, uint32_t i, const kgo_over* ov,
                          const kg_pod_columns* p, uint32_t j) {
     int64_t alloc[2 + KG_NSCALAR], req[2 + KG_NSCALAR], w[2 + KG_NSCALAR];
@@ -103,7 +106,10 @@ static int64_t nrf_score(const kg_config* c, const kg_node_columns* n, uint32_t 
     for (int r = 0; r < 2 + KG_NSCALAR; r++) {
         if (w[r] == 0) continue; /* resource not in the scoring strategy */
         if (alloc[r] == 0) continue;
-        score += least_requested_score(req[r], alloc[r]) * w[r];
+        /* per-resource strategy: LeastAllocated, or MostAllocated (mostRequestedScore,
+         * noderesourcefitplus/node_resource_fit_plus_utils.go:36-45) */
+        const int most = (c->nrf_most_allocated >> r) & 1u;
+        score += (most ? most_requested_score(req[r], alloc[r]) : least_requested_score(req[r], alloc[r])) * w[r];
         wsum += w[r];
     }
     if (wsum == 0) return 0;
@@ -485,13 +491,13 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
     *score_out = 0;
     *zone_out = -1;
     if (p->flags[j] & KG_POD_NUMA_SKIP) return 0; /* PreFilter Skip: no Filter, no Score */
-    if (p->flags[j] & KG_POD_CPU_BIND) return KG_ST_UNSUPPORTED;
     int conflict;
     uint32_t policy = numa_merge_policy(n->numa_policy[i], p->numa_policy[j], &conflict);
-    if (conflict) return KG_ST_NUMA_CONFLICT;
+    if (conflict) return KG_ST_NUMA_CONFLICT; /* plugin.go:377-381 */
+    const int cpu_bind = (p->flags[j] & KG_POD_CPU_BIND) != 0;
     double ratio = n->cpu_amp_ratio[i];
     int64_t pod_cpu = p->req_cpu[j];
-    /* filterAmplifiedCPUs: plugin.go:461-498 (requestCPUBind == false) */
+    /* filterAmplifiedCPUs: plugin.go:461-498; a cpuset-binding pod's request is amplified too (:477-479) */
     if (pod_cpu != 0 && ratio > 1) {
         int64_t allocated = n->cpuset_alloc_milli[i];
         int64_t requested = N_REQ_CPU(n, i, ov);
@@ -499,8 +505,11 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
             requested = requested - allocated;
             requested += kgo_amplify(allocated, ratio);
         }
-        if (pod_cpu > n->alloc_cpu[i] - requested) return KG_ST_NUMA_AMP_CPU;
+        const int64_t need = cpu_bind ? kgo_amplify(pod_cpu, ratio) : pod_cpu;
+        if (need > n->alloc_cpu[i] - requested) return KG_ST_NUMA_AMP_CPU;
     }
+    /* the cpuset allocation itself (cpu_accumulator.go) is the host's: plugin.go:396-440 */
+    if (cpu_bind) return KG_ST_UNSUPPORTED;
     if (policy == KG_NUMA_NONE) {
         /* scoreWithAmplifiedCPUs, scoring.go:132-151 */
         int64_t req_cpu = N_REQ_CPU(n, i, ov);
@@ -560,7 +569,7 @@ void kgo_eval_pair(const kg_config* c, const kg_node_columns* n, uint32_t i, con
     uint32_t st = 0;
     int64_t s_numa = 0;
     int32_t zone = -1;
-    if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(n, i, NULL, p, j);
+    if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(c, n, i, NULL, p, j);
     if (c->plugins & KG_PLUGIN_LA) st |= la_filter(c, n, i, p, j);
     if (c->plugins & KG_PLUGIN_NUMA) st |= numa_eval(c, n, i, NULL, p, j, &s_numa, &zone);
     out->status = st;
@@ -663,7 +672,7 @@ static void par_run(par_job* jb) {
             if (jb->phase == 0) {
                 uint32_t st = 0;
                 uint32_t i = (uint32_t)x;
-                if (jb->c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(jb->n, i, NULL, jb->p, jb->pod);
+                if (jb->c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(jb->c, jb->n, i, NULL, jb->p, jb->pod);
                 if (jb->c->plugins & KG_PLUGIN_LA) st |= la_filter(jb->c, jb->n, i, jb->p, jb->pod);
                 int64_t s = 0;
                 int32_t z = -1;
@@ -1317,23 +1326,25 @@ static void rsv_remained(const kg_rsv_info* r, int64_t* out) {
 /* fitsNode (reservation/plugin.go:915-965); returns a bitmask of insufficient resources (bit 5 = pods). */
 static uint32_t rsv_fits_node(const int64_t* preq, uint32_t pnames, const int64_t* alloc, int64_t allowed,
                               const int64_t* requested, const int64_t* r_alloc, const int64_t* rem, int64_t matched,
-                              int64_t pods) {
+                              int64_t pods, uint32_t ign) {
     uint32_t bad = 0;
     if (pods - matched + 1 > allowed) bad |= 1u << 5;
     if (preq[0] == 0 && preq[1] == 0 && preq[2] == 0 && !(pnames & 0x18u)) return bad;
     for (int k = 0; k < KG_RSV_R; k++) {
         if (k >= 3 && !((pnames >> k) & 1u)) continue; /* scalar resources the pod requests */
+        if (k >= 3 && ((ign >> (k - 3)) & 1u)) continue; /* isResourceIgnored (plugin.go:897-909,951-953) */
         if (preq[k] > alloc[k] - (requested[k] - rem[k] - r_alloc[k])) bad |= 1u << k;
     }
     return bad;
 }
 
 /* fitsReservation (reservation/plugin.go:973-1057). */
-static uint32_t rsv_fits_reservation(const int64_t* preq, uint32_t pnames, const kg_rsv_info* r) {
+static uint32_t rsv_fits_reservation(const int64_t* preq, uint32_t pnames, const kg_rsv_info* r, uint32_t ign) {
     uint32_t bad = 0;
     if (r->max_pods >= 0 && r->allocated_pods + 1 > r->max_pods) bad |= 1u << 5;
     for (int k = 0; k < KG_RSV_R; k++) {
         if (!((r->names >> k) & 1u)) continue;
+        if (k >= 3 && ((ign >> (k - 3)) & 1u)) continue; /* isResourceIgnored (:1014-1016) */
         if (!((pnames >> k) & 1u) || preq[k] == 0) continue;
         int64_t used = r->allocated[k] < 0 ? 0 : r->allocated[k];
         int64_t cap = r->allocatable[k] - r->reserved[k];
@@ -1351,10 +1362,12 @@ typedef struct rsv_ctx {
     int64_t preq[KG_RSV_R], alloc[KG_RSV_R];
     uint32_t pnames;
     int required;
+    uint32_t ign; /* ReservationArgs ignored scalar resources (bit k: scalar k) */
 } rsv_ctx;
 
-static void rsv_ctx_init(rsv_ctx* x, const kg_node_columns* n, uint32_t i, const kg_rsv_view* v,
+static void rsv_ctx_init(rsv_ctx* x, const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_rsv_view* v,
                          const kg_rsv_info* infos, const kg_pod_columns* p, uint32_t j) {
+    x->ign = c->rsv_ignored_scalars;
     x->n = n;
     x->i = i;
     x->v = v;
@@ -1374,10 +1387,10 @@ static int rsv_fits_one(const rsv_ctx* x, const kg_rsv_info* r, uint32_t* bn, ui
     int64_t rem[KG_RSV_R];
     rsv_remained(r, rem);
     *bn = rsv_fits_node(x->preq, x->pnames, x->alloc, x->n->alloc_pods[x->i], x->v->pod_requested,
-                        x->v->r_allocated, rem, (int64_t)x->v->count, x->v->num_pods);
+                        x->v->r_allocated, rem, (int64_t)x->v->count, x->v->num_pods, x->ign);
     *br = 0;
     if (r->policy == KG_RSV_RESTRICTED) {
-        *br = rsv_fits_reservation(x->preq, x->pnames, r);
+        *br = rsv_fits_reservation(x->preq, x->pnames, r, x->ign);
         return (*bn == 0 && *br == 0) ? 0 : 1;
     }
     return *bn == 0 ? 0 : 1;
@@ -1400,7 +1413,7 @@ static uint32_t rsv_filter(const rsv_ctx* x) {
     if (any_node) return KG_ST_RSV_NODE;
     int64_t zero[KG_RSV_R] = {0, 0, 0, 0, 0};
     uint32_t bn = rsv_fits_node(x->preq, x->pnames, x->alloc, x->n->alloc_pods[x->i], x->v->pod_requested,
-                                x->v->r_allocated, zero, (int64_t)x->v->count, x->v->num_pods);
+                                x->v->r_allocated, zero, (int64_t)x->v->count, x->v->num_pods, x->ign);
     return bn ? KG_ST_RSV_NODE : 0;
 }
 
@@ -1549,7 +1562,7 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
         uint32_t st = 0;
         int64_t s_numa = 0;
         int32_t zone = -1;
-        if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(n, i, ovp, p, j);
+        if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(c, n, i, ovp, p, j);
         if (c->plugins & KG_PLUGIN_LA) st |= la_filter(c, n, i, p, j);
         if (c->plugins & KG_PLUGIN_NUMA) {
             if (v && n->numa_policy[i] != KG_NUMA_NONE && !(p->flags[j] & KG_POD_NUMA_SKIP))
@@ -1566,7 +1579,7 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
             st |= KG_ST_UNSUPPORTED;
         rsv_ctx x;
         if (c->plugins & KG_PLUGIN_RSV) {
-            rsv_ctx_init(&x, n, i, v, e ? e->infos : NULL, p, j);
+            rsv_ctx_init(&x, c, n, i, v, e ? e->infos : NULL, p, j);
             st |= rsv_filter(&x);
         }
         o->st[i] = st;

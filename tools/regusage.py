@@ -3,7 +3,7 @@ import re
 import subprocess
 import sys
 
-SRC = "koordinator_amd/csrc/kg_kernels.hip"
+SRC = sys.argv[2] if len(sys.argv) > 2 else "koordinator_amd/csrc/kg_kernels.hip"
 
 
 def main(pattern=""):
