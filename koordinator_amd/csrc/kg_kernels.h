@@ -25,6 +25,12 @@ struct LaunchSelect {
     uint64_t* partial;
     const uint32_t* pmap;  // sub-batch row -> batch position (nullptr: identity)
     uint32_t* pstat;       // per batch position: KG_ST_UNSUPPORTED when some pair needs the host path
+    // fused top-1 (k == 1 on the fast path): one launch over both storage classes, per-pod keys by
+    // atomicMax straight into `out`, which k_big_init has seeded with the F_BIG records' best keys
+    bool fused;
+    uint64_t* out;
+    const uint32_t* big_list;
+    const uint32_t* big_count;
 };
 
 // Block replay (k_rb_top / k_rb_merge / k_rb_fix): window of RB_W pods, RB_K keys kept per pod,

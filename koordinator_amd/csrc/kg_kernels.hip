@@ -86,6 +86,63 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
     }
 }
 
+// Fused top-1 select of one storage class: lane = pod, blockIdx.y = chunk of records [begin, end); the
+// lane's best key goes to out[pod] by atomicMax. out was seeded by k_big_init with the pod's best key
+// over the F_BIG records (integer path), or 0; no per-chunk partials, no merge pass.
+template <uint32_t PM, int CLS>
+__global__ __launch_bounds__(256) void k_select1(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                 PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
+                                                 uint32_t chunk, uint32_t index_base, KCfg cfg,
+                                                 uint64_t* __restrict__ out, const uint32_t* __restrict__ pmap,
+                                                 uint32_t* __restrict__ pstat) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = j < n_pods;
+    const PodV p = load_pod(pods, live ? j : 0);
+    const uint32_t lo = begin + blockIdx.y * chunk;
+    const uint32_t hi = min(end, lo + chunk);
+    const PodF pf = to_podf(p, cfg);
+    const KCfg cv = cfg_in_vgprs(cfg);
+    uint64_t top = 0;
+    for (uint32_t i = lo; i < hi; i++) {
+        const FastRec r = *reinterpret_cast<const FastRec*>(&nodes[i].v[FAST_BEGIN]);
+        const uint64_t key = eval_fast_key<PM, CLS>(cv, r, zones + i, pf, index_base + (uint32_t)((uint64_t)r.flags >> 32));
+        const uint64_t k2 = ((uint32_t)r.flags & F_BIG) ? 0ull : key;  // F_BIG records: k_big_init
+        top = k2 > top ? k2 : top;
+    }
+    if (live) {
+        if (top) atomicMax((unsigned long long*)(out + j), (unsigned long long)top);
+        // the fast path's only host-path pairs: a cpuset-binding pod under NodeNUMAResource (pod-level)
+        if ((PM & KG_PLUGIN_NUMA) && (p.flags & KG_POD_CPU_BIND) && !(p.flags & KG_POD_NUMA_SKIP) && hi > lo)
+            atomicOr(pstat + (pmap ? pmap[j] : j), (uint32_t)KG_ST_UNSUPPORTED);
+    }
+}
+
+// Seeds the fused select's output: per pod, the best key over the F_BIG records (integer path), 0 if none.
+__global__ __launch_bounds__(256) void k_big_init(uint32_t n_pods, const NodeRec* __restrict__ nodes,
+                                                  const ZoneRec* __restrict__ zones, PodsDev pods,
+                                                  const uint32_t* __restrict__ big_list,
+                                                  const uint32_t* __restrict__ big_count, uint32_t index_base,
+                                                  KCfg cfg, uint64_t* __restrict__ out,
+                                                  const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_pods) return;
+    uint64_t top = 0;
+    const uint32_t nb = *big_count;
+    if (nb) {
+        const PodV p = load_pod(pods, j);
+        uint32_t unsup = 0;
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint32_t i = big_list[b];
+            const PairOut o = eval_pair<false>(cfg, nodes[i].v, zones + i, p);
+            unsup |= o.status & KG_ST_UNSUPPORTED;
+            const uint64_t key = pair_key(cfg, o, rec_gidx(nodes[i], index_base));
+            top = key > top ? key : top;
+        }
+        if (unsup) atomicOr(pstat + (pmap ? pmap[j] : j), unsup);
+    }
+    out[j] = top;
+}
+
 template <int K>
 __global__ __launch_bounds__(256) void k_merge(const uint64_t* __restrict__ partial, uint32_t n_parts, uint32_t n_pods,
                                                uint64_t* __restrict__ out) {
@@ -581,6 +638,37 @@ static void select_fast(const LaunchSelect& a, const SelectRange& r, hipStream_t
 }
 
 hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
+    if (a.fused) {
+        const uint32_t pod_blocks = (a.n_pods + 255) / 256;
+        k_big_init<<<pod_blocks, 256, 0, s>>>(a.n_pods, a.nodes, a.zones, a.pods, a.big_list, a.big_count, a.index_base,
+                                               a.cfg, a.out, a.pmap, a.pstat);
+        for (int cls = 0; cls < 2; cls++) {
+            const SelectRange& r = a.range[cls];
+            if (r.n_chunks == 0) continue;
+            dim3 grid(pod_blocks, r.n_chunks), block(256);
+#define KG_SEL1(PMV)                                                                                               \
+    do {                                                                                                           \
+        if (cls == 0)                                                                                              \
+            k_select1<PMV, 0><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end, r.chunk,  \
+                                                     a.index_base, a.cfg, a.out, a.pmap, a.pstat);                 \
+        else                                                                                                       \
+            k_select1<PMV, 1><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end, r.chunk,  \
+                                                     a.index_base, a.cfg, a.out, a.pmap, a.pstat);                 \
+    } while (0)
+            switch (a.cfg.plugins & 7u) {
+                case 0: KG_SEL1(0); break;
+                case 1: KG_SEL1(1); break;
+                case 2: KG_SEL1(2); break;
+                case 3: KG_SEL1(3); break;
+                case 4: KG_SEL1(4); break;
+                case 5: KG_SEL1(5); break;
+                case 6: KG_SEL1(6); break;
+                default: KG_SEL1(7); break;
+            }
+#undef KG_SEL1
+        }
+        return KG_LAUNCH_CHECK();
+    }
     for (int cls = 0; cls < 2; cls++) {
         const SelectRange& r = a.range[cls];
         if (r.n_chunks == 0) continue;

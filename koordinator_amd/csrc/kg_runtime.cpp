@@ -461,6 +461,16 @@ bool ext_split_off() {
     return v == 1;
 }
 
+// KG_SELECT_UNFUSED=1: k == 1 selects through per-chunk partials + merge (A/B aid for the fused top-1)
+bool unfused() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("KG_SELECT_UNFUSED");
+        v = (e && e[0] == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 bool force_int() {
     static int v = -1;
     if (v < 0) {
@@ -472,13 +482,13 @@ bool force_int() {
 
 // Node chunk of the select kernel: enough (pod-block, chunk) workgroups to fill 256 CUs several
 // times over, while each wave still walks a long run of nodes.
-// KG_SELECT_BLOCKS: workgroup target of the base select launches (tuning aid; default 2048)
+// KG_SELECT_BLOCKS: workgroup target of the base select launches (tuning aid; default 8192)
 uint32_t select_blocks() {
     static uint32_t v = 0;
     if (v == 0) {
         const char* e = std::getenv("KG_SELECT_BLOCKS");
         const long x = e ? std::strtol(e, nullptr, 10) : 0;
-        v = (x >= 64 && x <= 65536) ? (uint32_t)x : 2048u;
+        v = (x >= 64 && x <= 65536) ? (uint32_t)x : 8192u;
     }
     return v;
 }
@@ -1219,6 +1229,12 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         a.cfg = s->kcfg;
         a.pmap = p->d_pmap;
         a.pstat = p->d_pstat;
+        a.fused = kk == 1 && !unfused();
+        if (a.fused) {
+            a.out = p->d_tkeys + p->cap;  // the x sub-batch's merge reuses d_tkeys[0, cap) before the scatters
+            a.big_list = s->d_big + 1;
+            a.big_count = s->d_big;
+        }
     }
     const size_t xneed = (size_t)xparts * n_x * kk;
     kg_status st = ensure_partial(p, std::max<size_t>(xneed + (size_t)fparts * n_plain * kk, 1));
@@ -1231,7 +1247,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
                                        s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
                                        p->d_pref, p->d_partial, p->d_pstat, ctx->stream));
-    if (fparts) HIP_TRY(ctx, launch_select(a, ctx->stream));
+    if (fparts || a.fused) HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
     if (!split) {
@@ -1243,12 +1259,15 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_xlist, n_x, kk, nullptr, d_out, nullptr, ctx->stream));
     }
     if (n_plain) {
-        if (fparts)
+        if (a.fused) {
+            // keys already in d_tkeys (k_big_init + k_select1)
+        } else if (fparts)
             HIP_TRY(ctx, launch_merge_big(a.partial, fparts, n_plain, kk, s->d_nodes, s->d_zones, p->plain, s->d_big + 1,
                                           s->d_big, s->base, s->kcfg, p->d_tkeys, p->d_pmap, p->d_pstat, ctx->stream));
         else
             HIP_TRY(ctx, hipMemsetAsync(p->d_tkeys, 0, sizeof(uint64_t) * kk * n_plain, ctx->stream));
-        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_pmap, n_plain, kk, p->d_qst, d_out, p->d_pstat, ctx->stream));
+        HIP_TRY(ctx, launch_scatter_keys(a.fused ? a.out : p->d_tkeys, p->d_pmap, n_plain, kk, p->d_qst, d_out, p->d_pstat,
+                                         ctx->stream));
     }
     return KG_OK;
 }
@@ -1296,6 +1315,12 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     a.cfg = s->kcfg;
     a.pmap = nullptr;
     a.pstat = p->d_pstat;
+    a.fused = a.fast && kk == 1 && !unfused();
+    if (a.fused) {
+        a.out = d_out;
+        a.big_list = s->d_big + 1;
+        a.big_count = s->d_big;
+    }
     const size_t need = (size_t)std::max<uint32_t>(n_parts, 1) * p->n * kk;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     if (need > p->partial_cap) {
@@ -1322,6 +1347,7 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
+    if (a.fused) return KG_OK;
     if (a.fast)
         HIP_TRY(ctx, launch_merge_big(p->d_partial, n_parts, p->n, kk, s->d_nodes, s->d_zones, p->dev, s->d_big + 1,
                                       s->d_big, s->base, s->kcfg, d_out, nullptr, p->d_pstat, ctx->stream));

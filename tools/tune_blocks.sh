@@ -1,7 +1,8 @@
-# Sweep KG_SELECT_BLOCKS (base select workgroup target) on config 2, then the GPU suite once.
-cd $GRAFT_REPO_ROOT
+#!/bin/bash
+# Sweep KG_SELECT_BLOCKS (workgroup target of the base select launches) on config 2.
+cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-for b in 2048 4096 8192 1024; do
-  KG_SELECT_BLOCKS=$b timeout -k 10 120 python bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-replay > gpurun_out/tune_$b.json 2>gpurun_out/tune_$b.err || exit 1
+for b in ${*:-2048 4096 8192 16384}; do
+  KG_SELECT_BLOCKS=$b timeout -k 10 120 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-replay --no-cycle > gpurun_out/tune_$b.json 2>gpurun_out/tune_$b.err || exit 1
+  python -c "import json;d=json.loads(open('gpurun_out/tune_$b.json').read().strip().splitlines()[-1]);print($b, round(d['ms_per_step'],4), d['roofline'].get('kernel_avg_ms'))"
 done
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_tune.log 2>&1 || exit 2
