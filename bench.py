@@ -356,7 +356,9 @@ def main():
     value = evals / elapsed
     avg_kernel_s = (kern_ms / 1e3) / max(launches, 1) if launches else None
     pmc = load_pmc("select_pmc.json" if config != 5 else "ext_pmc.json") if world == 1 else None
-    kname = "k_select" if config != 5 else "k_ext_select + k_select (plain-pod split, one bracket)"
+    fused = k == 1 and os.environ.get("KG_SELECT_UNFUSED", "0") in ("", "0")
+    base = "k_big_init + k_select1 (fused top-1)" if fused else "k_select"
+    kname = base if config != 5 else f"k_ext_select + {base} (plain-pod split, one bracket)"
     out = {
         "metric": METRIC,
         "value": value,

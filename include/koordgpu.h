@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 3
+#define KG_ABI_VERSION 4
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -330,8 +330,14 @@ kg_status kg_sync(kg_ctx* ctx);
 kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes, uint32_t index_base,
                              kg_snap** out);
 kg_status kg_snapshot_upload(kg_snap* snap, const kg_node_columns* cols);
-/* Replace rows[i] (local index) with entry i of cols (each column has n entries). */
+/* Replace rows[i] (local index) with entry i of cols (each column has n entries): the informer-event
+ * deltas of one scheduling cycle in one call (one staged copy + one scatter launch on the device). */
 kg_status kg_snapshot_update_rows(kg_snap* snap, const uint32_t* rows, uint32_t n, const kg_node_columns* cols);
+/* Generation of the snapshot: bumped by every call that changes its contents (upload, update_rows,
+ * kg_assume / kg_forget and their _ext forms, kg_replay, quota and reservation uploads). A caller that
+ * stamps its host cache with it can tell whether the device has seen every delta (k8s UpdateSnapshot's
+ * NodeInfo.Generation scheme; the host side is koordinator_amd.cluster). */
+kg_status kg_snapshot_generation(kg_snap* snap, uint64_t* out);
 kg_status kg_snapshot_read_state(kg_snap* snap, kg_node_state* out);
 /* ElasticQuota table (KG_PLUGIN_QUOTA): n_quotas entries, copied; Reserve updates used / np_used. */
 kg_status kg_snapshot_upload_quotas(kg_snap* snap, const kg_quota_columns* cols, uint32_t n_quotas);

@@ -1,0 +1,663 @@
+"""Event-driven snapshot maintenance: the scheduler-side caches that turn informer
+events into snapshot row deltas, and the sync that ships those deltas to a device snapshot.
+
+The reference keeps one cache per plugin, each fed by its own informer handlers:
+  * framework NodeInfo (k8s scheduler cache): Requested / NonZeroRequested / pod count of assigned pods,
+    AssumePod / ForgetPod for the scheduler's own placements;
+  * LoadAware podAssignCache (loadaware/pod_assign_cache.go:89-707): OnAdd / OnUpdate / OnDelete (:365-413),
+    AddOrUpdateNodeMetric / DeleteNodeMetric (:498-616), assign / unAssign from Reserve / Unreserve
+    (load_aware.go:226-233);
+  * NodeNUMAResource resourceManager (nodenumaresource/pod_eventhandler.go:53-149, node_allocation.go):
+    per-node pod allocations (cpuset, NUMA zone resources) from the resource-status annotation;
+  * DeviceShare nodeDeviceCache (deviceshare/device_cache.go:518-548 updateNodeDevice,
+    eventhandler_pod.go updatePod / deletePod): per-minor total, used and free.
+ClusterState mirrors all four over one set of nodes, bumps a generation counter per event and stamps each
+node it touched with it (the NodeInfo.Generation scheme of the k8s cache's UpdateSnapshot); SnapshotSync
+then sends every row newer than the snapshot's last sync in ONE batched kg_snapshot_update_rows call.
+
+Times are seconds on the cache clock (`clock()`), None being Go's zero time. The node set is fixed for a
+snapshot's life: adding or removing a node is a new snapshot (kg_snapshot_create + upload)."""
+from __future__ import annotations
+
+import json
+from fractions import Fraction
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple
+
+import numpy as np
+
+from . import abi
+from .config import CPU, DEV_RESOURCES, MEMORY, SchedulerConfig
+from .decode import (ANN_AMPLIFICATION, LoadAwareNodeCache, NODEINFO_KEYS, Unsupported, _is_terminated, _rl, amplify,
+                     assign_info, is_reserve_pod, la_cols, milli_value, node_static_cols, nodeinfo_cols,
+                     pod_request_vec, value, zone_used_cols)
+
+ANN_RESOURCE_STATUS = "scheduling.koordinator.sh/resource-status"
+ANN_DEVICE_ALLOCATED = "scheduling.koordinator.sh/device-allocated"
+
+
+def _md(obj) -> dict:
+    return obj.get("metadata") or {}
+
+
+def _uid(pod) -> str:
+    md = _md(pod)
+    return md.get("uid") or f"{md.get('namespace', '')}/{md.get('name', '')}"
+
+
+def _node_name(pod) -> str:
+    return (pod.get("spec") or {}).get("nodeName") or ""
+
+
+def _nn(pod) -> Tuple[str, str]:
+    md = _md(pod)
+    return md.get("namespace", ""), md.get("name", "")
+
+
+# ------------------------------------------------------------------------------------------------
+# LoadAware podAssignCache
+
+class PodAssignCache:
+    """podAssignCache (loadaware/pod_assign_cache.go:89-707): nodeInfo entries by node name, created on the
+    first object for a node and removed when both its metric and its pods are gone (tryCleanup, :281-288).
+    Single-threaded here: the reference's lock protocol (:42-88) orders concurrent handlers, and the event
+    stream this cache sees is already serialised. `on_change(node)` is called for every node an event
+    touches."""
+
+    def __init__(self, la, clock: Callable[[], float] = lambda: 0.0,
+                 on_change: Callable[[str], None] = lambda name: None):
+        self.la = la
+        self.clock = clock
+        self.items: Dict[str, LoadAwareNodeCache] = {}
+        self.on_change = on_change
+
+    def get(self, name: str) -> Optional[LoadAwareNodeCache]:
+        return self.items.get(name)
+
+    def _get_or_create(self, name: str) -> LoadAwareNodeCache:
+        n = self.items.get(name)
+        if n is None:
+            n = LoadAwareNodeCache(la=self.la)
+            self.items[name] = n
+        return n
+
+    def _try_cleanup(self, name: str, n: LoadAwareNodeCache):
+        if n.empty():
+            self.items.pop(name, None)
+
+    def pod_info(self, name: str, pod):
+        """getPodAssignInfo (:215-226)."""
+        if not name:
+            return None
+        n = self.items.get(name)
+        return None if n is None else n.pod_infos.get(_uid(pod))
+
+    def assign(self, name: str, pod):
+        """assign (:291-327): terminated and reserve pods are not cached."""
+        if not name or _is_terminated(pod) or is_reserve_pod(pod):
+            return
+        info = assign_info(pod, self.la, now=self.clock())
+        self._get_or_create(name).add_or_update_pod(_uid(pod), info)
+        self.on_change(name)
+
+    def unassign(self, name: str, pod):
+        """unAssign (:356-363) -> nodeInfo.DeletePod (:449-466)."""
+        if not name:
+            return
+        n = self.items.get(name)
+        if n is not None:
+            n.delete_pod(_uid(pod))
+            self._try_cleanup(name, n)
+            self.on_change(name)
+
+    def on_add(self, pod):
+        """OnAdd (:365-371)."""
+        self.assign(_node_name(pod), pod)
+
+    def on_update(self, old, pod):
+        """OnUpdate (:373-396): a pod moved off a node is removed there first; an uncached pod is assigned,
+        a terminated one removed, and a cached one renewed only when its spec or conditions changed."""
+        if pod is None:
+            return
+        if old is not None and _node_name(old) and _node_name(old) != _node_name(pod):
+            self.unassign(_node_name(old), pod)
+        cached = self.pod_info(_node_name(pod), pod)
+        if cached is None:
+            self.assign(_node_name(pod), pod)
+        elif _is_terminated(pod):
+            self.unassign(_node_name(pod), pod)
+        elif (pod.get("spec") != cached.pod.get("spec")
+              or (pod.get("status") or {}).get("conditions") != (cached.pod.get("status") or {}).get("conditions")):
+            self.assign(_node_name(pod), pod)
+
+    def on_delete(self, pod):
+        """OnDelete (:398-413)."""
+        self.unassign(_node_name(pod), pod)
+
+    def add_or_update_node_metric(self, metric: dict):
+        """AddOrUpdateNodeMetric (:498-509, nodeInfo side :520-603)."""
+        name = _md(metric).get("name", "")
+        self._get_or_create(name).set_metric(metric)
+        self.on_change(name)
+
+    def delete_node_metric(self, name: str):
+        """DeleteNodeMetric (:511-516, :605-616)."""
+        n = self.items.get(name)
+        if n is not None:
+            n.clear_metric()
+            self._try_cleanup(name, n)
+            self.on_change(name)
+
+
+# ------------------------------------------------------------------------------------------------
+# NodeNUMAResource resourceManager allocations
+
+def parse_cpuset(s: str) -> Set[int]:
+    """cpuset.Parse: Linux CPU list format ("0-3,8,10-11")."""
+    out: Set[int] = set()
+    s = (s or "").strip()
+    if not s:
+        return out
+    for part in s.split(","):
+        part = part.strip()
+        if "-" in part:
+            a, b = part.split("-", 1)
+            lo, hi = int(a), int(b)
+            if hi < lo:
+                raise ValueError(f"invalid cpuset range {part!r}")
+            out.update(range(lo, hi + 1))
+        else:
+            out.add(int(part))
+    return out
+
+
+@dataclass
+class _PodAllocation:
+    cpus: Set[int]
+    numa: List[Tuple[int, Dict[str, object]]]  # (zone, ResourceList)
+
+
+@dataclass
+class NodeAllocation:
+    """NodeAllocation (nodenumaresource/node_allocation.go:33-243) restricted to what the snapshot reads:
+    allocated cpus with reference counts, allocated resources per zone and the per-zone shared status."""
+    pods: Dict[str, _PodAllocation] = field(default_factory=dict)
+    cpu_refs: Dict[int, int] = field(default_factory=dict)
+    zone_res: Dict[int, Dict[str, object]] = field(default_factory=dict)
+    single: Dict[int, Set[str]] = field(default_factory=dict)
+    shared: Dict[int, Set[str]] = field(default_factory=dict)
+
+    def add(self, uid: str, a: _PodAllocation, cpu_zone: Dict[int, int]):
+        """addPodAllocation (:111-156); an existing allocation of the uid is kept."""
+        if uid in self.pods:
+            return
+        self.pods[uid] = a
+        used = set()
+        for c in a.cpus:
+            self.cpu_refs[c] = self.cpu_refs.get(c, 0) + 1
+            used.add(cpu_zone.get(c, 0))
+        if len(used) > 1:
+            for z in used:
+                self.shared.setdefault(z, set()).add(uid)
+        elif len(used) == 1:
+            self.single.setdefault(next(iter(used)), set()).add(uid)
+        for z, res in a.numa:
+            cur = self.zone_res.setdefault(z, {})
+            for k, q in _rl(res).items():
+                cur[k] = cur.get(k, 0) + q
+
+    def release(self, uid: str, cpu_zone: Dict[int, int]):
+        """release (:158-190)."""
+        a = self.pods.pop(uid, None)
+        if a is None:
+            return
+        used = set()
+        for c in a.cpus:
+            if c not in self.cpu_refs:
+                continue
+            self.cpu_refs[c] -= 1
+            if self.cpu_refs[c] == 0:
+                del self.cpu_refs[c]
+            used.add(cpu_zone.get(c, 0))
+        for z in used:
+            self.shared.get(z, set()).discard(uid)
+            self.single.get(z, set()).discard(uid)
+        for z, res in a.numa:
+            cur = self.zone_res.get(z)
+            if cur is not None:  # quotav1.SubtractWithNonNegativeResult
+                for k, q in _rl(res).items():
+                    cur[k] = max(cur.get(k, 0) - q, 0)
+
+    def zone_status(self, n_zones: int) -> int:
+        """NUMANodeSharedStatus per zone (:52-68), 2 bits each."""
+        st = 0
+        for z in range(n_zones):
+            s = 0
+            if self.single.get(z) and not self.shared.get(z):
+                s = 1
+            elif self.single.get(z) or self.shared.get(z):
+                s = 2
+            st |= s << (2 * z)
+        return st
+
+
+def pod_numa_allocation(pod) -> Optional[_PodAllocation]:
+    """podEventHandler.updatePod (pod_eventhandler.go:108-139): the resource-status annotation's cpuset and
+    NUMA zone resources; None when it carries neither (or does not parse)."""
+    ann = _md(pod).get("annotations") or {}
+    raw = ann.get(ANN_RESOURCE_STATUS)
+    if not raw:
+        return None
+    try:
+        st = json.loads(raw)
+        cpus = parse_cpuset(st.get("cpuset", ""))
+    except (ValueError, TypeError):
+        return None
+    numa = [(int(r.get("node", 0)), r.get("resources") or {}) for r in st.get("numaNodeResources") or []]
+    if not numa and not cpus:
+        return None
+    return _PodAllocation(cpus, numa)
+
+
+# ------------------------------------------------------------------------------------------------
+# DeviceShare nodeDeviceCache (GPU minors)
+
+GPU = "gpu"
+
+
+@dataclass
+class NodeDevice:
+    """nodeDevice (deviceshare/device_cache.go:44-130): deviceTotal / deviceUsed per type and minor, and the
+    allocateSet that keeps one pod's allocation from being counted twice (isValid, :209-228)."""
+    total: Dict[str, Dict[int, Dict[str, int]]] = field(default_factory=dict)
+    used: Dict[str, Dict[int, Dict[str, int]]] = field(default_factory=dict)
+    allocate_set: Dict[str, Dict[Tuple[str, str], list]] = field(default_factory=dict)
+    has_device: bool = False
+
+    def reset_total(self, resources: Dict[str, Dict[int, Dict[str, int]]]):
+        """resetDeviceTotal (:119-130): a type absent from the new Device keeps an empty table."""
+        for t in self.total:
+            resources.setdefault(t, {})
+        self.total = resources
+
+    def free(self, t: str) -> Dict[int, Dict[str, int]]:
+        """resetDeviceFree (:101-117): total minus used, clamped at zero, per minor."""
+        out = {m: dict(r) for m, r in self.total.get(t, {}).items()}
+        for m, u in self.used.get(t, {}).items():
+            tot = self.total.get(t, {}).get(m, {})
+            out[m] = {k: max(tot.get(k, 0) - u.get(k, 0), 0) for k in set(tot) | set(u)}
+            out[m] = {k: v for k, v in out[m].items() if k in tot or v != 0}
+        return out
+
+    def update_cache_used(self, allocations: Dict[str, list], pod, add: bool):
+        """updateCacheUsed (:132-143) with updateDeviceUsed (:184-210) and updateAllocateSet."""
+        key = _nn(pod)
+        for t, allocs in allocations.items():
+            aset = self.allocate_set.setdefault(t, {})
+            if add and key in aset:
+                continue  # already counted (e.g. after Reserve)
+            if not add and key not in aset:
+                continue
+            used = self.used.setdefault(t, {})
+            for a in allocs:
+                m = int(a.get("minor", 0))
+                res = {k: value(q) for k, q in (a.get("resources") or {}).items()}
+                cur = used.setdefault(m, {})
+                if add:
+                    for k, v in res.items():
+                        cur[k] = cur.get(k, 0) + v
+                else:
+                    for k, v in res.items():
+                        cur[k] = max(cur.get(k, 0) - v, 0)
+                    if all(v == 0 for v in cur.values()):
+                        del used[m]
+            if not add and not used:
+                del self.used[t]
+            if add:
+                aset[key] = allocs
+            else:
+                del aset[key]
+
+
+def device_resources(device: dict) -> Dict[str, Dict[int, Dict[str, int]]]:
+    """buildDeviceResources (device_cache.go:550-568): an unhealthy device reports no resources."""
+    out: Dict[str, Dict[int, Dict[str, int]]] = {}
+    for d in (device.get("spec") or {}).get("devices") or []:
+        t = d.get("type", "")
+        res = {} if not d.get("health", False) else {k: value(q) for k, q in (d.get("resources") or {}).items()}
+        out.setdefault(t, {})[int(d.get("minor", 0))] = res
+    return out
+
+
+def pod_device_allocations(pod) -> Dict[str, list]:
+    """apiext.GetDeviceAllocations: the device-allocated annotation ({} when absent or unparsable)."""
+    raw = (_md(pod).get("annotations") or {}).get(ANN_DEVICE_ALLOCATED)
+    if not raw:
+        return {}
+    try:
+        d = json.loads(raw)
+    except ValueError:
+        return {}
+    return {t: list(v or []) for t, v in d.items()} if isinstance(d, dict) else {}
+
+
+class NodeDeviceCache:
+    """nodeDeviceCache (device_cache.go:455-548) with the pod handlers of eventhandler_pod.go."""
+
+    def __init__(self, on_change: Callable[[str], None] = lambda name: None):
+        self.infos: Dict[str, NodeDevice] = {}
+        self.on_change = on_change
+
+    def update_node_device(self, device: dict):
+        """updateNodeDevice (:518-548), GPU partition / topology-scope state aside (row f4)."""
+        name = _md(device).get("name", "")
+        if not name:
+            return
+        info = self.infos.setdefault(name, NodeDevice())
+        info.reset_total(device_resources(device))
+        info.has_device = True
+        self.on_change(name)
+
+    def remove_node_device(self, name: str):
+        """removeNodeDevice (:486-494)."""
+        if self.infos.pop(name, None) is not None:
+            self.on_change(name)
+
+    def update_pod(self, old, pod):
+        """updatePod (eventhandler_pod.go): note that an old allocation is released through the NEW node's
+        entry, as the reference does."""
+        if not _node_name(pod):
+            if old is not None and _node_name(old):
+                self.delete_pod(old)
+            return
+        if _is_terminated(pod):
+            self.delete_pod(pod)
+            return
+        allocs = pod_device_allocations(pod)
+        old_allocs = pod_device_allocations(old) if old is not None else {}
+        if not allocs and not old_allocs:
+            return
+        name = _node_name(pod)
+        info = self.infos.setdefault(name, NodeDevice())
+        if old is not None and _node_name(old) and old_allocs:
+            info.update_cache_used(old_allocs, old, False)
+        if allocs:
+            info.update_cache_used(allocs, pod, True)
+        self.on_change(name)
+
+    def delete_pod(self, pod):
+        """deletePod (eventhandler_pod.go)."""
+        name = _node_name(pod)
+        if not name:
+            return
+        allocs = pod_device_allocations(pod)
+        if not allocs:
+            return
+        info = self.infos.get(name)
+        if info is None:
+            return
+        info.update_cache_used(allocs, pod, False)
+        self.on_change(name)
+
+    def columns(self, name: str):
+        """(dev_minors, dev_total[R][M], dev_free[R][M]) of the node's GPU minors (kg_node_columns)."""
+        tot = np.zeros((abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
+        free = np.zeros_like(tot)
+        info = self.infos.get(name)
+        if info is None or not info.has_device:
+            return -1, tot, free
+        t = info.total.get(GPU, {})
+        f = info.free(GPU)
+        minors = sorted(set(t) | set(f))
+        if minors != list(range(len(minors))) or len(minors) > abi.KG_DEV_MINORS:
+            raise Unsupported(f"GPU minors {minors} of node {name} are not 0..{abi.KG_DEV_MINORS - 1}")
+        for m in minors:
+            for r, key in enumerate(DEV_RESOURCES):
+                tot[r, m] = t.get(m, {}).get(key, 0)
+                free[r, m] = f.get(m, {}).get(key, 0)
+        return len(minors), tot, free
+
+
+# ------------------------------------------------------------------------------------------------
+# The cluster state and its sync to a device snapshot
+
+@dataclass
+class _NodeTopology:
+    zones: List[Dict[str, str]] = field(default_factory=list)
+    kubelet_policy: str = ""
+    cpu_zone: Dict[int, int] = field(default_factory=dict)  # cpu id -> NUMA node (CPUTopology); {} = none
+
+
+class ClusterState:
+    """Every cache the device path's plugins read, kept per node from informer events, with generations.
+
+    Event entry points (each the fan-out of one informer event to the caches that register for it):
+      on_pod_add / on_pod_update / on_pod_delete   Pod events (NodeInfo, podAssignCache, NUMA, DeviceShare)
+      on_node_update                               Node events (allocatable, labels, annotations)
+      on_node_metric / on_node_metric_delete       NodeMetric events (podAssignCache)
+      on_topology                                  NodeResourceTopology events (zones, kubelet policy, cpus)
+      on_device / on_device_delete                 Device events (nodeDeviceCache)
+      assume / forget                              the scheduler's own Reserve / Unreserve of a placement
+    """
+
+    def __init__(self, cfg: SchedulerConfig, nodes: Sequence[dict], clock: Callable[[], float] = lambda: 0.0):
+        self.cfg = cfg
+        self.la = cfg.la()
+        self.clock = clock
+        self.nodes = [dict(n) for n in nodes]
+        self.names = [_md(n).get("name", "") for n in self.nodes]
+        self.index = {name: i for i, name in enumerate(self.names)}
+        if len(self.index) != len(self.names):
+            raise ValueError("node names must be unique")
+        n = len(self.nodes)
+        width = len(NODEINFO_KEYS) + abi.KG_NSCALAR
+        self.req = np.zeros((n, width), np.int64)
+        self.num_pods = np.zeros(n, np.int64)
+        self.node_pods: Dict[str, Tuple[int, List[int]]] = {}  # uid -> (node row, request vector)
+        self.topo = [_NodeTopology() for _ in range(n)]
+        self.numa = [NodeAllocation() for _ in range(n)]
+        self.generation = 0
+        self.row_gen = np.zeros(n, np.uint64)
+        self.assign_cache = PodAssignCache(self.la, clock, self._touch_name)
+        self.devices = NodeDeviceCache(self._touch_name)
+
+    # -- generations -----------------------------------------------------------------------------
+    def _touch(self, i: int):
+        self.generation += 1
+        self.row_gen[i] = self.generation
+
+    def _touch_name(self, name: str):
+        i = self.index.get(name)
+        if i is not None:
+            self._touch(i)
+
+    def rows_since(self, generation: int) -> np.ndarray:
+        """Snapshot rows changed after `generation` (UpdateSnapshot's NodeInfo.Generation test)."""
+        return np.nonzero(self.row_gen > np.uint64(generation))[0].astype(np.uint32)
+
+    # -- NodeInfo (k8s scheduler cache) ---------------------------------------------------------
+    def _nodeinfo_remove(self, uid: str):
+        ent = self.node_pods.pop(uid, None)
+        if ent is None:
+            return
+        i, vec = ent
+        self.req[i] -= vec
+        self.num_pods[i] -= 1
+        self._touch(i)
+
+    def _nodeinfo_add(self, pod):
+        i = self.index.get(_node_name(pod))
+        if i is None:
+            return
+        vec = pod_request_vec(pod, self.cfg)
+        self.node_pods[_uid(pod)] = (i, vec)
+        self.req[i] += vec
+        self.num_pods[i] += 1
+        self._touch(i)
+
+    def _nodeinfo_update(self, pod):
+        """addPod / updatePod / removePod of the scheduler cache: assigned, non-terminated pods only, keyed
+        by UID (so a binding that confirms an assumed pod replaces it rather than adding it twice)."""
+        self._nodeinfo_remove(_uid(pod))
+        if _node_name(pod) and not _is_terminated(pod):
+            self._nodeinfo_add(pod)
+
+    # -- NUMA resourceManager --------------------------------------------------------------------
+    def _numa_release(self, name: str, uid: str):
+        i = self.index.get(name)
+        if i is None:
+            return
+        if uid in self.numa[i].pods:
+            self.numa[i].release(uid, self.topo[i].cpu_zone)
+            self._touch(i)
+
+    def _numa_update(self, old, pod):
+        """podEventHandler.updatePod / deletePod (pod_eventhandler.go:95-149); Update = release + add."""
+        if not _node_name(pod):
+            if old is not None and _node_name(old):
+                self._numa_release(_node_name(old), _uid(old))
+            return
+        if _is_terminated(pod):
+            self._numa_release(_node_name(pod), _uid(pod))
+            return
+        a = pod_numa_allocation(pod)
+        if a is None:
+            return
+        i = self.index.get(_node_name(pod))
+        if i is None:
+            return
+        self.numa[i].release(_uid(pod), self.topo[i].cpu_zone)
+        self.numa[i].add(_uid(pod), a, self.topo[i].cpu_zone)
+        self._touch(i)
+
+    # -- events ----------------------------------------------------------------------------------
+    def on_pod_add(self, pod):
+        self._nodeinfo_update(pod)
+        self.assign_cache.on_add(pod)
+        self._numa_update(None, pod)
+        self.devices.update_pod(None, pod)
+
+    def on_pod_update(self, old, pod):
+        self._nodeinfo_update(pod)
+        self.assign_cache.on_update(old, pod)
+        self._numa_update(old, pod)
+        self.devices.update_pod(old, pod)
+
+    def on_pod_delete(self, pod):
+        self._nodeinfo_remove(_uid(pod))
+        self.assign_cache.on_delete(pod)
+        self._numa_release(_node_name(pod), _uid(pod))
+        self.devices.delete_pod(pod)
+
+    def assume(self, pod, node_name: str):
+        """The scheduler's Reserve of a placement: cache AssumePod (NodeInfo) and LoadAware Reserve
+        (podAssignCache.assign, load_aware.go:226-229)."""
+        p = dict(pod)
+        p["spec"] = dict(pod.get("spec") or {}, nodeName=node_name)
+        self._nodeinfo_update(p)
+        self.assign_cache.assign(node_name, p)
+        return p
+
+    def forget(self, pod, node_name: str):
+        """Unreserve: ForgetPod and podAssignCache.unAssign (load_aware.go:231-233)."""
+        self._nodeinfo_remove(_uid(pod))
+        self.assign_cache.unassign(node_name, pod)
+
+    def on_node_update(self, node: dict):
+        i = self.index[_md(node).get("name", "")]
+        self.nodes[i] = dict(node)
+        self._touch(i)
+
+    def on_node_metric(self, metric: dict):
+        self.assign_cache.add_or_update_node_metric(metric)
+
+    def on_node_metric_delete(self, name: str):
+        self.assign_cache.delete_node_metric(name)
+
+    def on_topology(self, name: str, zones: List[Dict[str, str]], kubelet_policy: str = "",
+                    cpu_zone: Optional[Dict[int, int]] = None):
+        i = self.index[name]
+        t = self.topo[i]
+        t.zones = list(zones)
+        t.kubelet_policy = kubelet_policy
+        if cpu_zone is not None and cpu_zone != t.cpu_zone:
+            t.cpu_zone = dict(cpu_zone)
+            old = self.numa[i]
+            self.numa[i] = NodeAllocation()
+            for uid, a in old.pods.items():  # re-place the allocations on the new topology
+                self.numa[i].add(uid, a, t.cpu_zone)
+        self._touch(i)
+
+    def on_device(self, device: dict):
+        self.devices.update_node_device(device)
+
+    def on_device_delete(self, name: str):
+        self.devices.remove_node_device(name)
+
+    # -- rows ------------------------------------------------------------------------------------
+    def _zone_used(self, i: int) -> Tuple[List[Dict[str, object]], int]:
+        """getAvailableNUMANodeResources' totalAllocated (node_allocation.go:221-243, no reusable
+        reservations) and the node's allocated cpuset size (plugin.go:485-490)."""
+        t = self.topo[i]
+        alloc = self.numa[i]
+        ratio = float(json.loads((_md(self.nodes[i]).get("annotations") or {}).get(ANN_AMPLIFICATION) or "{}")
+                      .get(CPU, 1.0))
+        used: List[Dict[str, object]] = []
+        for z in range(len(t.zones)):
+            res = dict(alloc.zone_res.get(z, {}))
+            if z in alloc.zone_res and ratio > 1 and t.cpu_zone:
+                cs = sum(1 for c in alloc.cpu_refs if t.cpu_zone.get(c, 0) == z) * 1000
+                cpu = milli_value(res.get(CPU, 0))
+                res[CPU] = Fraction(cpu - cs + amplify(cs, ratio), 1000)
+            used.append(res)
+        cpuset_milli = len(alloc.cpu_refs) * 1000 if t.cpu_zone else 0
+        return used, cpuset_milli
+
+    def row(self, i: int) -> Dict[str, object]:
+        """Snapshot row of node i from the incrementally maintained caches."""
+        name = self.names[i]
+        t = self.topo[i]
+        row = node_static_cols(self.nodes[i], self.cfg, t.zones, t.kubelet_policy)
+        row.update(nodeinfo_cols(self.req[i], int(self.num_pods[i])))
+        cache = self.assign_cache.get(name) or LoadAwareNodeCache(la=self.la)
+        row.update(la_cols(self.nodes[i], cache.metric, cache, self.la, self.clock()))
+        used, cpuset_milli = self._zone_used(i)
+        row.update(zone_used_cols(used, cpuset_milli))
+        row["numa_zone_status"] = self.numa[i].zone_status(len(t.zones)) if t.cpu_zone else 0
+        row["dev_minors"], row["dev_total"], row["dev_free"] = self.devices.columns(name)
+        return row
+
+    def table(self, rows: Optional[Iterable[int]] = None) -> abi.Table:
+        rows = range(len(self.nodes)) if rows is None else list(rows)
+        t = abi.empty_nodes(len(rows))
+        for k, i in enumerate(rows):
+            for key, v in self.row(int(i)).items():
+                t[key][k] = v
+        return t
+
+
+class SnapshotSync:
+    """Keeps device snapshots of a ClusterState current: each sync() sends the rows whose generation is
+    newer than the last sync, as one batched kg_snapshot_update_rows per shard (a shard owns the global
+    rows [index_base, index_base + n)). Rows are rebuilt from the caches, so a row the device changed by
+    kg_assume is overwritten with the host's view of the same placement once its events arrive."""
+
+    def __init__(self, state: ClusterState, snaps):
+        self.state = state
+        self.snaps = list(snaps) if isinstance(snaps, (list, tuple)) else [snaps]
+        self.synced = state.generation
+        self.last_rows = 0
+
+    def sync(self) -> int:
+        rows = self.state.rows_since(self.synced)
+        self.synced = self.state.generation
+        self.last_rows = len(rows)
+        if len(rows) == 0:
+            return 0
+        table = self.state.table(rows)
+        for s in self.snaps:
+            lo, hi = s.index_base, s.index_base + s.n
+            sel = np.nonzero((rows >= lo) & (rows < hi))[0]
+            if len(sel):
+                s.update_rows(rows[sel] - lo, abi.take(table, sel))
+        return len(rows)

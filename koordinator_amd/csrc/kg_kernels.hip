@@ -715,6 +715,40 @@ hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t 
     return KG_LAUNCH_CHECK();
 }
 
+// Batched row update (kg_snapshot_update_rows): record r of the staged block (NodeRec, ZoneRec and, with
+// DeviceShare, DevRec of each row back to back) goes to record position pos[r]. One 16-byte word per lane:
+// a 512-B node record is 32 consecutive lanes, so each wave writes two whole records with full-line stores.
+__global__ __launch_bounds__(256) void k_scatter_rows(const uint4* __restrict__ stage, const uint32_t* __restrict__ pos,
+                                                      uint32_t n, uint32_t dev_words, uint4* __restrict__ nodes,
+                                                      uint4* __restrict__ zones, uint4* __restrict__ devs) {
+    constexpr uint32_t NW = sizeof(NodeRec) / 16, ZW = sizeof(ZoneRec) / 16;
+    const uint32_t rw = NW + ZW + dev_words;
+    const size_t total = (size_t)n * rw;
+    for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t r = (uint32_t)(x / rw), w = (uint32_t)(x % rw);
+        const size_t p = pos[r];
+        const uint4 v = stage[x];
+        if (w < NW)
+            nodes[p * NW + w] = v;
+        else if (w < NW + ZW)
+            zones[p * ZW + (w - NW)] = v;
+        else
+            devs[p * dev_words + (w - NW - ZW)] = v;
+    }
+}
+
+hipError_t launch_scatter_rows(const void* stage, const uint32_t* pos, uint32_t n, bool dev, NodeRec* nodes,
+                               ZoneRec* zones, DevRec* devs, hipStream_t s) {
+    static_assert(sizeof(NodeRec) % 16 == 0 && sizeof(ZoneRec) % 16 == 0 && sizeof(DevRec) % 16 == 0, "16-B words");
+    if (n == 0) return hipSuccess;
+    const uint32_t dw = dev ? (uint32_t)(sizeof(DevRec) / 16) : 0u;
+    const size_t words = (size_t)n * (sizeof(NodeRec) / 16 + sizeof(ZoneRec) / 16 + dw);
+    const unsigned grid = (unsigned)std::min<size_t>((words + 255) / 256, 4096);
+    k_scatter_rows<<<grid, 256, 0, s>>>(static_cast<const uint4*>(stage), pos, n, dw, reinterpret_cast<uint4*>(nodes),
+                                        reinterpret_cast<uint4*>(zones), reinterpret_cast<uint4*>(devs));
+    return KG_LAUNCH_CHECK();
+}
+
 hipError_t launch_big_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t* big_list, uint32_t* big_count,
                            hipStream_t s) {
     hipError_t e = hipMemsetAsync(big_count, 0, sizeof(uint32_t), s);

@@ -83,6 +83,14 @@ struct kg_snap {
     // (absolute restored Requested etc.): the caller recomputes the restore (the reference reruns the
     // Reservation transformer every cycle) and re-uploads; until then selects on the snapshot refuse.
     bool views_stale = false;
+    // Generation: bumped by every call that changes what the snapshot holds (upload, row update, Assume /
+    // Forget, replay, quota / reservation upload); kg_snapshot_generation reads it.
+    uint64_t gen = 0;
+    // batched row updates: staged records (NodeRec, ZoneRec[, DevRec] per row) and their positions
+    uint8_t* d_stage = nullptr;
+    uint32_t* d_stage_pos = nullptr;
+    size_t stage_cap = 0;  // rows
+    std::vector<uint8_t> h_stage;
     bool ext() const { return (cfg.plugins & KG_PLUGIN_EXT) != 0; }
     ExtDev ext_dev() const {
         ExtDev e{};
@@ -718,6 +726,7 @@ kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->uploaded = true;
+    s->gen++;
     return KG_OK;
 }
 
@@ -768,22 +777,52 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
         HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, s->h_dev.data(), sizeof(DevRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
-    } else {
+    } else if (n) {
+        // one staged copy of every changed record, then one scatter launch to their positions
+        const size_t rb = sizeof(NodeRec) + sizeof(ZoneRec) + (dev ? sizeof(DevRec) : 0);
+        if (n > s->stage_cap) {
+            hipFree(s->d_stage);
+            hipFree(s->d_stage_pos);
+            s->d_stage = nullptr;
+            s->d_stage_pos = nullptr;
+            s->stage_cap = 0;
+            const size_t cap = std::max<size_t>(n, 256);
+            if (hipMalloc(&s->d_stage, (sizeof(NodeRec) + sizeof(ZoneRec) + sizeof(DevRec)) * cap) != hipSuccess ||
+                hipMalloc(&s->d_stage_pos, sizeof(uint32_t) * cap) != hipSuccess)
+                return fail(ctx, KG_OOM, "row-update staging for %u rows", n);
+            s->stage_cap = cap;
+        }
+        s->h_stage.resize(rb * n + sizeof(uint32_t) * n);
+        uint8_t* h = s->h_stage.data();
+        uint32_t* hpos = reinterpret_cast<uint32_t*>(h + rb * n);
         for (uint32_t k = 0; k < n; k++) {
             const uint32_t p = s->pos[rows[k]];
             s->h_nodes[p] = recs[k];
             s->h_zones[p] = zrs[k];
-            HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes + p, &s->h_nodes[p], sizeof(NodeRec), hipMemcpyHostToDevice, ctx->stream));
-            HIP_TRY(ctx, hipMemcpyAsync(s->d_zones + p, &s->h_zones[p], sizeof(ZoneRec), hipMemcpyHostToDevice, ctx->stream));
+            uint8_t* o = h + rb * k;
+            std::memcpy(o, &recs[k], sizeof(NodeRec));
+            std::memcpy(o + sizeof(NodeRec), &zrs[k], sizeof(ZoneRec));
             if (dev) {
                 s->h_dev[p] = devs[k];
-                HIP_TRY(ctx, hipMemcpyAsync(s->d_dev + p, &s->h_dev[p], sizeof(DevRec), hipMemcpyHostToDevice, ctx->stream));
+                std::memcpy(o + sizeof(NodeRec) + sizeof(ZoneRec), &devs[k], sizeof(DevRec));
             }
+            hpos[k] = p;
         }
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_stage, h, rb * n, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_stage_pos, hpos, sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, launch_scatter_rows(s->d_stage, s->d_stage_pos, n, dev, s->d_nodes, s->d_zones, s->d_dev, ctx->stream));
         count_topo(s);
     }
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    s->gen++;
+    return KG_OK;
+}
+
+kg_status kg_snapshot_generation(kg_snap* s, uint64_t* out) {
+    if (!s || !out) return KG_INVALID_ARG;
+    std::lock_guard<std::mutex> g(s->ctx->mu);
+    *out = s->gen;
     return KG_OK;
 }
 
@@ -845,6 +884,8 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_views);
     hipFree(s->d_infos);
     hipFree(s->d_cls_begin);
+    hipFree(s->d_stage);
+    hipFree(s->d_stage_pos);
     delete s;
     return KG_OK;
 }
@@ -1565,6 +1606,7 @@ kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_tota
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
     if (reasons) HIP_TRY(ctx, hipMemsetAsync(p->d_reason, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
+    s->gen++;
     HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
@@ -1612,6 +1654,7 @@ kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     touch_views(s, node);
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], -1, 1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return KG_OK;
@@ -1627,6 +1670,7 @@ kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     touch_views(s, node);
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return KG_OK;
@@ -1646,6 +1690,7 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
     if (out_reason) HIP_TRY(ctx, hipMemsetAsync(p->d_reason, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_minors, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
+    s->gen++;
     HIP_TRY(ctx, hipMemsetAsync(p->d_buckets, 0, sizeof(uint64_t) * 3 * 128, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
     hipEvent_t e0, e1;
@@ -1697,6 +1742,7 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     touch_views(s, node);
     HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone, minors,
                                    sign, s->kcfg, force_exact(), p->d_aout, ctx->stream));
+    s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     int32_t o[2] = {-1, 0};
     HIP_TRY(ctx, hipMemcpyAsync(o, p->d_aout, sizeof(o), hipMemcpyDeviceToHost, ctx->stream));
@@ -1742,6 +1788,7 @@ kg_status kg_snapshot_upload_quotas(kg_snap* s, const kg_quota_columns* c, uint3
         qs[nq + q] = S;
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    s->gen++;
     hipFree(s->d_qlim);
     hipFree(s->d_qstate);
     s->d_qlim = nullptr;
@@ -1865,6 +1912,7 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->n_views = nv;
     s->views_stale = false;
+    s->gen++;
     s->max_cls_views = 0;
     for (int c = 0; c < RSV_MAX_CLASSES; c++) s->max_cls_views = std::max(s->max_cls_views, cb[c + 1] - cb[c]);
     return KG_OK;

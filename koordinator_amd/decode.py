@@ -477,31 +477,165 @@ class AssignedPod:
     timestamp: float  # podAssignInfo.timestamp, seconds relative to now
 
 
-class LoadAwareNodeCache:
-    """nodeInfo of loadaware/pod_assign_cache.go:93-125 for one node at a frozen time."""
+ANN_CUSTOM_EST_SECONDS_AFTER_SCHEDULED = "scheduling.koordinator.sh/load-estimated-seconds-after-pod-scheduled"
+ANN_CUSTOM_EST_SECONDS_AFTER_INITIALIZED = "scheduling.koordinator.sh/load-estimated-seconds-after-initialized"
+ANN_RESERVE_POD = "scheduling.koordinator.sh/reserve-pod"
+DEFAULT_NODE_METRIC_REPORT_INTERVAL = 60.0  # loadaware DefaultNodeMetricReportInterval
 
-    def __init__(self, metric: Optional[dict], assigned: Iterable[AssignedPod], la: LoadAwareArgs):
-        self.metric = metric
+
+def pod_condition(pod, ctype: str) -> Optional[dict]:
+    """podutil.GetPodCondition: the condition of that type, or None. lastTransitionTime is seconds (None = zero)."""
+    for c in (pod.get("status") or {}).get("conditions") or []:
+        if c.get("type") == ctype:
+            return c
+    return None
+
+
+def is_reserve_pod(pod) -> bool:
+    """reservationutil.IsReservePod (pkg/util/reservation/reservation.go:197-199)."""
+    return ((pod.get("metadata") or {}).get("annotations") or {}).get(ANN_RESERVE_POD) == "true"
+
+
+def _custom_seconds(pod, key: str) -> int:
+    """extension.GetCustomEstimatedSecondsAfter* (apis/extension/load_aware.go:84-100): -1 when absent."""
+    s = ((pod.get("metadata") or {}).get("annotations") or {}).get(key, "")
+    if s:
+        try:
+            return int(s, 10)
+        except ValueError:
+            pass
+    return -1
+
+
+def estimated_deadline(pod, timestamp: float, la: LoadAwareArgs) -> Optional[float]:
+    """podAssignCache.shouldEstimatePodDeadline (pod_assign_cache.go:329-354); None is the zero time."""
+    after_sched = after_init = -1
+    if la.allow_customize_estimation:
+        after_sched = _custom_seconds(pod, ANN_CUSTOM_EST_SECONDS_AFTER_SCHEDULED)
+        after_init = _custom_seconds(pod, ANN_CUSTOM_EST_SECONDS_AFTER_INITIALIZED)
+    if la.estimated_seconds_after_pod_scheduled is not None and after_sched < 0:
+        after_sched = la.estimated_seconds_after_pod_scheduled
+    if la.estimated_seconds_after_initialized is not None and after_init < 0:
+        after_init = la.estimated_seconds_after_initialized
+    if after_init > 0:
+        c = pod_condition(pod, "PodInitialized")
+        if c is not None and c.get("status") == "True" and c.get("lastTransitionTime") is not None:
+            return float(c["lastTransitionTime"]) + after_init
+    if after_sched > 0 and timestamp is not None:
+        return timestamp + after_sched
+    return None
+
+
+@dataclass
+class PodAssignInfo:
+    """podAssignInfo (pod_assign_cache.go:127-132)."""
+    pod: dict
+    timestamp: float
+    estimated: Optional[List[int]]   # None: the estimator returned nothing (assign(): empty vector)
+    deadline: Optional[float] = None  # estimatedDeadline, None = zero time
+
+
+def assign_info(pod, la: LoadAwareArgs, now: float = 0.0, timestamp: Optional[float] = None) -> PodAssignInfo:
+    """The podAssignInfo podAssignCache.assign builds (pod_assign_cache.go:291-315): the PodScheduled
+    condition's transition time when True, else the cache clock (or an explicit `timestamp`)."""
+    e = estimate_pod(pod, la)
+    est = None if all(x == 0 for x in e) else e
+    if timestamp is None:
+        c = pod_condition(pod, "PodScheduled")
+        if c is not None and c.get("status") == "True" and c.get("lastTransitionTime") is not None:
+            timestamp = float(c["lastTransitionTime"])
+        else:
+            timestamp = now
+    return PodAssignInfo(pod, timestamp, est, estimated_deadline(pod, timestamp, la))
+
+
+def _vadd(v, x):
+    for i, a in enumerate(x):
+        v[i] += a
+
+
+def _vsub(v, x):
+    for i, a in enumerate(x):
+        v[i] -= a
+
+
+def _add_delta(v, x, y) -> bool:
+    """ResourceVector.AddDelta (loadaware/helper.go:231-242): v += max(0, x - y) per entry (in place)."""
+    changed = False
+    for i, val in enumerate(x):
+        if y is not None:
+            val -= y[i]
+        if val > 0:
+            v[i] += val
+            changed = True
+    return changed
+
+
+def _sub_delta(v, x, y) -> bool:
+    """ResourceVector.SubDelta (loadaware/helper.go:251-262)."""
+    changed = False
+    for i, val in enumerate(x):
+        if y is not None:
+            val -= y[i]
+        if val > 0:
+            v[i] -= val
+            changed = True
+    return changed
+
+
+class LoadAwareNodeCache:
+    """nodeInfo of loadaware/pod_assign_cache.go:101-125 for one node, maintained incrementally:
+    AddOrUpdateNodeMetric (:520-603), DeleteNodeMetric (:605-616), AddOrUpdatePod (:418-447) and
+    DeletePod (:449-466) with addPod / deletePod (:618-707). Times are seconds on the cache clock;
+    None is Go's zero time.
+
+    LoadAwareNodeCache(metric, assigned, la) builds the node at a frozen time from a NodeMetric and the
+    pods assigned to it, which is what the incremental path reaches by any order of the same events."""
+
+    def __init__(self, metric: Optional[dict] = None, assigned: Iterable[AssignedPod] = (),
+                 la: Optional[LoadAwareArgs] = None):
         self.la = la
+        self.pod_infos: Dict[str, PodAssignInfo] = {}
+        self.update_time: Optional[float] = None  # kept across metric updates that carry none (:586-588)
+        self._clear_metric_state()
+        self.metric = None
+        if metric is not None:
+            self.set_metric(metric)
+        for i, ap in enumerate(assigned):
+            uid = (ap.pod.get("metadata") or {}).get("uid") or f"#{i}"
+            self.add_or_update_pod(uid, assign_info(ap.pod, la, timestamp=ap.timestamp))
+
+    def _clear_metric_state(self):
         zero = [0] * abi.KG_LA_R
-        self.node_usage = None
+        self.report_interval = DEFAULT_NODE_METRIC_REPORT_INTERVAL
+        self.node_usage: Optional[List[int]] = None
         self.prod_usage = list(zero)
         self.agg_usages: Dict[Tuple[str, float], List[int]] = {}
         self.pod_usages: Dict[Tuple[str, str], List[int]] = {}
         self.prod_pods = set()
-        self.update_time = -math.inf
-        self.report_interval = 60.0
         self.node_delta, self.prod_delta, self.node_estimated = list(zero), list(zero), list(zero)
-        if metric is None:
-            return
+        self.node_delta_pods, self.prod_delta_pods, self.node_estimated_pods = set(), set(), set()
+
+    @staticmethod
+    def _vec(resources) -> List[int]:
+        res = resources or {}
+        return [vec_value(r, res[r]) if r in res else 0 for r in LA_RESOURCES]
+
+    def empty(self) -> bool:
+        return self.metric is None and not self.pod_infos
+
+    # -- NodeMetric events -------------------------------------------------------------------------
+    def set_metric(self, metric: dict):
+        """nodeInfo.AddOrUpdateNodeMetric (pod_assign_cache.go:520-603): every derived vector is rebuilt
+        and every cached pod re-added."""
+        self._clear_metric_state()
         st = metric.get("status") or {}
         spec = metric.get("spec") or {}
         info = st.get("nodeMetric")
         if info is not None:
             self.node_usage = self._vec((info.get("nodeUsage") or {}).get("resources"))
-            aggs = info.get("aggregatedNodeUsages") or []
             max_d: Dict[str, float] = {}
-            for agg in aggs:
+            for agg in info.get("aggregatedNodeUsages") or []:
                 d = _duration(agg.get("duration"))
                 for t, u in (agg.get("usage") or {}).items():
                     res = (u or {}).get("resources") or {}
@@ -512,9 +646,8 @@ class LoadAwareNodeCache:
                         max_d[t] = d
             for t, d in max_d.items():
                 self.agg_usages[(t, 0.0)] = self.agg_usages[(t, d)]
-            if la.prod_usage_include_sys:
-                sysu = self._vec((info.get("systemUsage") or {}).get("resources"))
-                self.prod_usage = [a + b for a, b in zip(self.prod_usage, sysu)]
+            if self.la.prod_usage_include_sys:
+                _vadd(self.prod_usage, self._vec((info.get("systemUsage") or {}).get("resources")))
         for pm in st.get("podsMetric") or []:
             if pm is None:
                 continue
@@ -525,42 +658,89 @@ class LoadAwareNodeCache:
             self.pod_usages[key] = self._vec(res)
             if pm.get("priority") == PROD:
                 self.prod_pods.add(key)
-        ut = st.get("updateTime")
-        if ut is not None:
-            self.update_time = float(ut)
+        self.metric = metric
         ri = (spec.get("collectPolicy") or {}).get("reportIntervalSeconds")
         if ri is not None:
             self.report_interval = float(ri)
-        for ap in assigned:
-            self._add_pod(ap)
+        ut = st.get("updateTime")
+        if ut is not None:
+            self.update_time = float(ut)
+        for info_ in self.pod_infos.values():
+            self._add_pod(info_)
 
-    @staticmethod
-    def _vec(resources) -> List[int]:
-        res = resources or {}
-        return [vec_value(r, res[r]) if r in res else 0 for r in LA_RESOURCES]
+    def clear_metric(self):
+        """nodeInfo.DeleteNodeMetric (pod_assign_cache.go:605-616): only the metric pointer is dropped."""
+        self.metric = None
 
-    def _add_pod(self, ap: AssignedPod):
+    # -- pod events ------------------------------------------------------------------------------
+    def add_or_update_pod(self, uid: str, info: PodAssignInfo):
+        """nodeInfo.AddOrUpdatePod (pod_assign_cache.go:418-447)."""
+        old = self.pod_infos.get(uid)
+        self.pod_infos[uid] = info
+        if self.metric is not None:
+            if old is not None:
+                self._delete_pod(old)
+            self._add_pod(info)
+
+    def delete_pod(self, uid: str):
+        """nodeInfo.DeletePod (pod_assign_cache.go:449-466)."""
+        old = self.pod_infos.pop(uid, None)
+        if self.metric is not None and old is not None:
+            self._delete_pod(old)
+
+    def _should(self, info: PodAssignInfo, u) -> bool:
+        # u == nil || updateTime - reportInterval < timestamp || (deadline set && deadline > updateTime)
+        if u is None:
+            return True
+        if self.update_time is None or self.update_time - self.report_interval < info.timestamp:
+            return True
+        return info.deadline is not None and info.deadline > self.update_time
+
+    def _add_pod(self, info: PodAssignInfo):
         """nodeInfo.addPod (pod_assign_cache.go:618-662)."""
-        pod = ap.pod
-        key = _pod_key(pod)
+        key = _pod_key(info.pod)
         u = self.pod_usages.get(key)
-        prod = priority_class(pod) == PROD
+        prod = priority_class(info.pod) == PROD
         active_prod = prod and key in self.prod_pods
         if active_prod:
-            self.prod_usage = [a + b for a, b in zip(self.prod_usage, u)]
-        e = estimate_pod(pod, self.la)
-        if all(x == 0 for x in e):  # assign(): empty estimate vector -> nil
+            _vadd(self.prod_usage, u)
+        e = info.estimated
+        if e is None:
             return
-        should = u is None or (self.update_time - self.report_interval) < ap.timestamp
-        if should:
-            self.node_delta = _add_delta(self.node_delta, e, u)
-        self.node_estimated = [a + b for a, b in zip(self.node_estimated, e)]
+        should = self._should(info, u)
+        if should and _add_delta(self.node_delta, e, u):
+            self.node_delta_pods.add(key)
+        _vadd(self.node_estimated, e)
+        self.node_estimated_pods.add(key)
         if not prod:
             return
         if not active_prod and u is not None:
             u, should = None, True
-        if should:
-            self.prod_delta = _add_delta(self.prod_delta, e, u)
+        if should and _add_delta(self.prod_delta, e, u):
+            self.prod_delta_pods.add(key)
+
+    def _delete_pod(self, info: PodAssignInfo):
+        """nodeInfo.deletePod (pod_assign_cache.go:669-707), the reverse of addPod."""
+        key = _pod_key(info.pod)
+        u = self.pod_usages.get(key)
+        prod = priority_class(info.pod) == PROD
+        active_prod = prod and key in self.prod_pods
+        if active_prod:
+            _vsub(self.prod_usage, u)
+        e = info.estimated
+        if e is None:
+            return
+        should = self._should(info, u)
+        if should and _sub_delta(self.node_delta, e, u):
+            self.node_delta_pods.discard(key)
+        _vsub(self.node_estimated, e)
+        self.node_estimated_pods.discard(key)
+        if not prod:
+            return
+        if not active_prod and u is not None:
+            u, should = None, True
+        if should and _sub_delta(self.prod_delta, e, u):
+            self.prod_delta_pods.discard(key)
 
     def estimated_of_existing(self, prod_pod: bool, agg_type: str = "", agg_duration: float = 0.0):
         """GetNodeMetricAndEstimatedOfExisting (pod_assign_cache.go:163-201); None = NotFound."""
@@ -579,16 +759,6 @@ class LoadAwareNodeCache:
         return list(self.node_estimated)
 
 
-def _add_delta(v, x, y):
-    out = list(v)
-    for i, val in enumerate(x):
-        if y is not None:
-            val -= y[i]
-        if val > 0:
-            out[i] += val
-    return out
-
-
 @dataclass
 class NodeInput:
     """Everything the snapshot needs about one node."""
@@ -603,9 +773,35 @@ class NodeInput:
     cpuset_allocated_milli: int = 0
 
 
-def node_row(ni: NodeInput, cfg: SchedulerConfig) -> Dict[str, object]:
+NODEINFO_KEYS = ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem")
+
+
+def pod_request_vec(pod, cfg: SchedulerConfig) -> List[int]:
+    """What framework.NodeInfo.AddPod adds for one pod: Requested (cpu, memory, ephemeral-storage, the
+    snapshot's scalar slots) and NonZeroRequested (cpu, memory), in NODEINFO_KEYS + sc_req order."""
+    r = pod_requests(pod)
+    nz = pod_requests(pod, NON_MISSING)
+    v = [milli_value(r.get(CPU, 0)), value(r.get(MEMORY, 0)), value(r.get(EPHEMERAL, 0)),
+         milli_value(nz.get(CPU, 0)), value(nz.get(MEMORY, 0))]
+    v += [value(r.get(name, 0)) for name in cfg.scalar_resources]
+    v += [0] * (abi.KG_NSCALAR - len(cfg.scalar_resources))
+    return v
+
+
+def nodeinfo_cols(requested: Sequence[int], num_pods: int) -> Dict[str, object]:
+    """Requested / NonZeroRequested / pod count columns from the sum of pod_request_vec over the node's pods."""
+    row: Dict[str, object] = {k: int(requested[i]) for i, k in enumerate(NODEINFO_KEYS)}
+    for k in range(abi.KG_NSCALAR):
+        row[f"sc_req{k}"] = int(requested[len(NODEINFO_KEYS) + k])
+    row["num_pods"] = num_pods
+    return row
+
+
+def node_static_cols(node: dict, cfg: SchedulerConfig, zones: Optional[List[Dict[str, str]]] = None,
+                     kubelet_numa_policy: str = "") -> Dict[str, object]:
+    """Columns that follow the Node object (allocatable, LoadAware thresholds, NUMA policy and amplification)
+    and the NodeResourceTopology zones."""
     la = cfg.la()
-    node = ni.node
     alloc = _rl((node.get("status") or {}).get("allocatable"))
     row: Dict[str, object] = {
         "alloc_cpu": milli_value(alloc.get(CPU, 0)),
@@ -613,28 +809,8 @@ def node_row(ni: NodeInput, cfg: SchedulerConfig) -> Dict[str, object]:
         "alloc_eph": value(alloc.get(EPHEMERAL, 0)),
         "alloc_pods": value(alloc.get(PODS, 0)),
     }
-    for k, name in enumerate(cfg.scalar_resources):
-        row[f"sc_alloc{k}"] = value(alloc.get(name, 0))
-    # NodeInfo.AddPod for every pod on the node
-    req = {"cpu": 0, "mem": 0, "eph": 0}
-    sc = [0] * abi.KG_NSCALAR
-    nzc = nzm = 0
-    for p in ni.pods:
-        r = pod_requests(p)
-        nz = pod_requests(p, NON_MISSING)
-        req["cpu"] += milli_value(r.get(CPU, 0))
-        req["mem"] += value(r.get(MEMORY, 0))
-        req["eph"] += value(r.get(EPHEMERAL, 0))
-        for k, name in enumerate(cfg.scalar_resources):
-            sc[k] += value(r.get(name, 0))
-        nzc += milli_value(nz.get(CPU, 0))
-        nzm += value(nz.get(MEMORY, 0))
-    row.update(req_cpu=req["cpu"], req_mem=req["mem"], req_eph=req["eph"], num_pods=len(ni.pods),
-               nz_cpu=nzc, nz_mem=nzm)
     for k in range(abi.KG_NSCALAR):
-        row[f"sc_req{k}"] = sc[k]
-
-    # LoadAwareScheduling
+        row[f"sc_alloc{k}"] = value(alloc.get(cfg.scalar_resources[k], 0)) if k < len(cfg.scalar_resources) else 0
     est_alloc = estimate_node_allocatable(node)
     for r, name in enumerate(LA_RESOURCES):
         row[f"la_alloc{r}"] = vec_value(name, est_alloc[name]) if name in est_alloc else 0
@@ -643,11 +819,37 @@ def node_row(ni: NodeInput, cfg: SchedulerConfig) -> Dict[str, object]:
         row[f"la_thr_usage{r}"] = prof.usage[r]
         row[f"la_thr_prod{r}"] = prof.prod[r]
         row[f"la_thr_agg{r}"] = prof.agg[0][r] if prof.agg else 0
-    assigned = ni.assigned
-    if assigned is None:
-        assigned = [AssignedPod(p, 0.0) for p in ni.pods]
-    assigned = [a for a in assigned if not _is_terminated(a.pod)]
-    cache = LoadAwareNodeCache(ni.node_metric, assigned, la)
+    md = node.get("metadata") or {}
+    labels = md.get("labels") or {}
+    policy_name = labels.get(LABEL_NUMA_POLICY, "") or kubelet_numa_policy
+    if policy_name not in NUMA_POLICIES:
+        raise Unsupported(f"NUMA topology policy {policy_name!r}")
+    row["numa_policy"] = NUMA_POLICIES[policy_name]
+    ratio = 1.0
+    ann = (md.get("annotations") or {}).get(ANN_AMPLIFICATION)
+    if ann:
+        ratio = float(json.loads(ann).get(CPU, 1.0))
+    row["cpu_amp_ratio"] = ratio
+    zones = zones or []
+    if len(zones) > abi.KG_MAX_ZONES:
+        raise Unsupported(f"{len(zones)} NUMA zones > {abi.KG_MAX_ZONES}")
+    row["numa_zones"] = len(zones)
+    for z in range(abi.KG_MAX_ZONES):
+        if z < len(zones):
+            zr = _rl(zones[z])
+            # amplifyNUMANodeResources (nodenumaresource/util.go:101-124)
+            row[f"zone_cpu{z}"] = amplify(milli_value(zr.get(CPU, 0)), ratio)
+            row[f"zone_mem{z}"] = value(zr.get(MEMORY, 0))
+        else:
+            row[f"zone_cpu{z}"] = row[f"zone_mem{z}"] = 0
+    return row
+
+
+def la_cols(node: dict, metric: Optional[dict], cache: LoadAwareNodeCache, la: LoadAwareArgs,
+            now: float = 0.0) -> Dict[str, object]:
+    """LoadAware flags and the Filter / Score bases GetNodeMetricAndEstimatedOfExisting returns for the node
+    (load_aware.go:150-376 reads them per pod; they depend only on the node and the pod's prod-ness)."""
+    prof = filter_profile(node, la)
     flags = 0
     if any(x != 0 for x in prof.prod):
         flags |= abi.KG_LA_PROD_THR
@@ -655,15 +857,15 @@ def node_row(ni: NodeInput, cfg: SchedulerConfig) -> Dict[str, object]:
         flags |= abi.KG_LA_AGG_THR
     zero = [0] * abi.KG_LA_R
     fb_np = fb_prod = sb_np = sb_prod = zero
-    if ni.node_metric is not None:
+    if metric is not None:
         flags |= abi.KG_LA_HAS_METRIC
-        st = ni.node_metric.get("status") or {}
+        st = metric.get("status") or {}
         if st.get("nodeMetric") is None:
             flags |= abi.KG_LA_NM_NIL
         secs = la.node_metric_expiration_seconds
         if secs is not None:
             ut = st.get("updateTime")
-            if ut is None or (secs > 0 and (0.0 - float(ut)) >= secs):
+            if ut is None or (secs > 0 and (now - float(ut)) >= secs):
                 flags |= abi.KG_LA_EXPIRED
         if prof.agg is not None:
             fb_np = cache.estimated_of_existing(False, prof.agg[1], prof.agg[2])
@@ -676,42 +878,41 @@ def node_row(ni: NodeInput, cfg: SchedulerConfig) -> Dict[str, object]:
         else:
             sb_np = cache.estimated_of_existing(False)
         sb_prod = cache.estimated_of_existing(True)
-    row["la_flags"] = flags
+    row: Dict[str, object] = {"la_flags": flags}
     for r in range(abi.KG_LA_R):
         row[f"la_fbase_np{r}"] = fb_np[r]
         row[f"la_fbase_prod{r}"] = fb_prod[r]
         row[f"la_sbase_np{r}"] = sb_np[r]
         row[f"la_sbase_prod{r}"] = sb_prod[r]
+    return row
 
-    # NodeNUMAResource
-    md = node.get("metadata") or {}
-    labels = md.get("labels") or {}
-    policy_name = labels.get(LABEL_NUMA_POLICY, "") or ni.kubelet_numa_policy
-    if policy_name not in NUMA_POLICIES:
-        raise Unsupported(f"NUMA topology policy {policy_name!r}")
-    row["numa_policy"] = NUMA_POLICIES[policy_name]
-    ratio = 1.0
-    ann = (md.get("annotations") or {}).get(ANN_AMPLIFICATION)
-    if ann:
-        ratio = float(json.loads(ann).get(CPU, 1.0))
-    row["cpu_amp_ratio"] = ratio
-    row["cpuset_alloc_milli"] = ni.cpuset_allocated_milli
-    zones = ni.numa_zones or []
-    if len(zones) > abi.KG_MAX_ZONES:
-        raise Unsupported(f"{len(zones)} NUMA zones > {abi.KG_MAX_ZONES}")
-    row["numa_zones"] = len(zones)
-    used = ni.numa_used or [{} for _ in zones]
+
+def zone_used_cols(used: Optional[List[Dict[str, str]]], cpuset_allocated_milli: int = 0) -> Dict[str, object]:
+    """resourceManager allocations per NUMA zone (node_allocation.go:221-243) and the node's cpuset total."""
+    used = used or []
+    row: Dict[str, object] = {"cpuset_alloc_milli": int(cpuset_allocated_milli)}
     for z in range(abi.KG_MAX_ZONES):
-        if z < len(zones):
-            zr = _rl(zones[z])
-            # amplifyNUMANodeResources (nodenumaresource/util.go:101-124)
-            row[f"zone_cpu{z}"] = amplify(milli_value(zr.get(CPU, 0)), ratio)
-            row[f"zone_mem{z}"] = value(zr.get(MEMORY, 0))
-            ur = _rl(used[z])
-            row[f"zone_cpu_used{z}"] = milli_value(ur.get(CPU, 0))
-            row[f"zone_mem_used{z}"] = value(ur.get(MEMORY, 0))
-        else:
-            row[f"zone_cpu{z}"] = row[f"zone_mem{z}"] = row[f"zone_cpu_used{z}"] = row[f"zone_mem_used{z}"] = 0
+        ur = _rl(used[z]) if z < len(used) else {}
+        row[f"zone_cpu_used{z}"] = milli_value(ur.get(CPU, 0))
+        row[f"zone_mem_used{z}"] = value(ur.get(MEMORY, 0))
+    return row
+
+
+def node_row(ni: NodeInput, cfg: SchedulerConfig, now: float = 0.0) -> Dict[str, object]:
+    """Snapshot row of one node built from scratch (the incremental path is cluster.ClusterState)."""
+    la = cfg.la()
+    row = node_static_cols(ni.node, cfg, ni.numa_zones, ni.kubelet_numa_policy)
+    req = [0] * (len(NODEINFO_KEYS) + abi.KG_NSCALAR)
+    for p in ni.pods:  # NodeInfo.AddPod for every pod on the node
+        for i, x in enumerate(pod_request_vec(p, cfg)):
+            req[i] += x
+    row.update(nodeinfo_cols(req, len(ni.pods)))
+    assigned = ni.assigned
+    if assigned is None:
+        assigned = [AssignedPod(p, 0.0) for p in ni.pods]
+    assigned = [a for a in assigned if not _is_terminated(a.pod) and not is_reserve_pod(a.pod)]  # assign(): :292
+    row.update(la_cols(ni.node, ni.node_metric, LoadAwareNodeCache(ni.node_metric, assigned, la), la, now))
+    row.update(zone_used_cols(ni.numa_used, ni.cpuset_allocated_milli))
     return row
 
 

@@ -58,6 +58,8 @@ def lib():
     L.kg_snapshot_upload.restype = st
     L.kg_snapshot_update_rows.argtypes = [vp, P(u32), u32, P(abi.KgNodeColumns)]
     L.kg_snapshot_update_rows.restype = st
+    L.kg_snapshot_generation.argtypes = [vp, P(C.c_uint64)]
+    L.kg_snapshot_generation.restype = st
     L.kg_snapshot_read_state.argtypes = [vp, P(abi.KgNodeState)]
     L.kg_snapshot_read_state.restype = st
     L.kg_snapshot_destroy.argtypes = [vp]
@@ -206,6 +208,11 @@ class Snapshot:
         cols = abi.node_columns(nodes)
         self.ctx.check(self.ctx.L.kg_snapshot_update_rows(self.h, rows.ctypes.data_as(C.POINTER(C.c_uint32)),
                                                           len(rows), C.byref(cols)), "kg_snapshot_update_rows")
+
+    def generation(self) -> int:
+        g = C.c_uint64()
+        self.ctx.check(self.ctx.L.kg_snapshot_generation(self.h, C.byref(g)), "kg_snapshot_generation")
+        return int(g.value)
 
     def read_state(self) -> abi.Table:
         t = abi.empty_node_state(self.n)

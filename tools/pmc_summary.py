@@ -61,6 +61,7 @@ def main(prof, out, names):
         "kernels": {k: {"trace": stats.get(k), "counters": v} for k, v in sel.items()},
         "select_avg_ns_sum": sum((stats.get(k) or {}).get("avg_ns", 0.0) for k in sel),
         "all_kernels_trace": stats,
+        "all_kernels_counters": counters,
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)

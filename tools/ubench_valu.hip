@@ -14,6 +14,7 @@ __global__ void kern(unsigned long long* out, double* dsink, float* fsink, unsig
     unsigned u0 = threadIdx.x + 1, u1 = u0 + 1, u2 = u0 + 2, u3 = u0 + 3, u4 = u0 + 4, u5 = u0 + 5, u6 = u0 + 6, u7 = u0 + 7;
     unsigned long long x0 = threadIdx.x * 77ull + 1, y = 12345678901ull;
     unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < 16; it++) {
         if constexpr (OP == 0) {  // v_add_f64
             REP64(asm volatile("v_add_f64 %0, %0, %8\n v_add_f64 %1, %1, %8\n v_add_f64 %2, %2, %8\n v_add_f64 %3, %3, %8\n v_add_f64 %4, %4, %8\n v_add_f64 %5, %5, %8\n v_add_f64 %6, %6, %8\n v_add_f64 %7, %7, %8" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));)
@@ -46,24 +47,65 @@ __global__ void kern(unsigned long long* out, double* dsink, float* fsink, unsig
         }
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0;
+    unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = t1 - t0;
+        out[2 * blockIdx.x + 1] = r1 - r0;
+    }
     dsink[threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
     usink[threadIdx.x] = u0 + u1 + u2 + u3 + u4 + u5 + u6 + u7 + (unsigned)x0;
 }
 
 template <int OP>
 void run(const char* name, unsigned long long* d, double* ds, float* fs, unsigned* us) {
-    for (int waves : {1, 4}) {
+    for (int waves : {1, 4, 8, 16}) {
         // one workgroup of `waves` waves per CU x 256 CUs: waves per SIMD = waves / 4 rounded up
         hipLaunchKernelGGL(kern<OP>, dim3(256), dim3(64 * waves), 0, 0, d, ds, fs, us);
         hipDeviceSynchronize();
-        unsigned long long h[256];
+        unsigned long long h[512];
         hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-        double avg = 0;
-        for (int i = 0; i < 256; i++) avg += h[i];
+        double avg = 0, rt = 0;
+        for (int i = 0; i < 256; i++) {
+            avg += h[2 * i];
+            rt += h[2 * i + 1];
+        }
         avg /= 256;
-        printf("%-16s waves/CU=%d  %.2f memtime ticks per wave-instruction\n", name, waves, avg / (16.0 * 512));
+        rt /= 256;
+        const double per_simd = waves < 4 ? 1.0 : waves / 4.0;  // waves sharing one SIMD's issue
+        printf("%-16s waves/CU=%2d  %.2f ticks per wave-instruction per SIMD (clock %.0f MHz)\n", name, waves,
+               avg / (16.0 * 512 * per_simd), avg / rt * 100.0);
     }
+}
+
+// Chip-wide rate: a grid far larger than the chip (4096 x 256 threads = 16 waves per SIMD over time),
+// timed by events; cycles per wave-instruction per SIMD at the in-kernel clock.
+template <int OP>
+void run_grid(const char* name, unsigned long long* d, double* ds, float* fs, unsigned* us) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    const int blocks = 4096, threads = 256;
+    hipLaunchKernelGGL(kern<OP>, dim3(blocks), dim3(threads), 0, 0, d, ds, fs, us);  // warm
+    hipEventRecord(a);
+    for (int r = 0; r < 10; r++) hipLaunchKernelGGL(kern<OP>, dim3(blocks), dim3(threads), 0, 0, d, ds, fs, us);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    unsigned long long h[512];
+    hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    double tk = 0, rt = 0;
+    for (int i = 0; i < 256; i++) {
+        tk += h[2 * i];
+        rt += h[2 * i + 1];
+    }
+    const double mhz = tk / rt * 100.0;
+    const double insts = 10.0 * blocks * (threads / 64) * 16.0 * 512;
+    const double cyc = (ms * 1e-3) * mhz * 1e6 * 1024.0 / insts;
+    printf("%-16s grid: %.3f ms for %.3g wave-inst = %.3g T/s; %.2f cycles per wave-instruction per SIMD at %.0f MHz\n",
+           name, ms / 10, insts / 10, insts / (ms * 1e-3) / 1e12, cyc, mhz);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
 }
 
 int main() {
@@ -71,10 +113,10 @@ int main() {
     double* ds;
     float* fs;
     unsigned* us;
-    hipMalloc(&d, 256 * 8);
-    hipMalloc(&ds, 4096 * 8);
-    hipMalloc(&fs, 4096 * 4);
-    hipMalloc(&us, 4096 * 4);
+    hipMalloc(&d, 512 * 8);
+    hipMalloc(&ds, 8192 * 8);
+    hipMalloc(&fs, 8192 * 4);
+    hipMalloc(&us, 8192 * 4);
     run<0>("v_add_f64", d, ds, fs, us);
     run<1>("v_cmp_lt_f64", d, ds, fs, us);
     run<2>("v_cmp_lt_u64", d, ds, fs, us);
@@ -87,5 +129,16 @@ int main() {
     run<9>("v_cmp_lt_f32", d, ds, fs, us);
     run<10>("v_cndmask_b32", d, ds, fs, us);
     run<11>("v_cvt_f64_u32", d, ds, fs, us);
+    hipMalloc(&d, 8192 * 8);
+    run_grid<0>("v_add_f64", d, ds, fs, us);
+    run_grid<1>("v_cmp_lt_f64", d, ds, fs, us);
+    run_grid<2>("v_cmp_lt_u64", d, ds, fs, us);
+    run_grid<3>("v_cvt_u32_f64", d, ds, fs, us);
+    run_grid<4>("v_mul_u32_u24", d, ds, fs, us);
+    run_grid<5>("v_cmp_lt_u32", d, ds, fs, us);
+    run_grid<6>("v_fma_f64", d, ds, fs, us);
+    run_grid<7>("v_mul_f32", d, ds, fs, us);
+    run_grid<8>("v_mul_hi_u32", d, ds, fs, us);
+    run_grid<10>("v_cndmask_b32", d, ds, fs, us);
     return 0;
 }
