@@ -140,6 +140,8 @@ typedef enum kg_status {
 #define KG_ST_RSV_MASK 0x1C000000u
 #define KG_ST_QUOTA 0x20000000u            /* ElasticQuota PreFilter: "Insufficient quotas" / non-preemptible
                                               (pod-level, reported on every node)                       */
+#define KG_ST_DEV_RSV 0x40000000u          /* "Reservation(s) Insufficient gpu devices": the pod must allocate from a
+                                            * matched reservation and none fits (deviceshare/reservation.go:404-406) */
 #define KG_ST_UNSUPPORTED 0x80000000u /* pair needs the host path (e.g. cpuset binding)        */
 
 typedef struct kg_ctx kg_ctx;   /* one per device per scheduler profile */
@@ -299,6 +301,11 @@ typedef struct kg_rsv_view {
     int64_t nz_cpu, nz_mem, num_pods;    /* restored NonZeroRequested and len(Pods)                  */
     int64_t pod_requested[KG_RSV_R];     /* nodeRState.podRequested (after the unmatched correction) */
     int64_t r_allocated[KG_RSV_R];       /* nodeRState.rAllocated: Σ Allocated of matched reservations */
+    /* DeviceShare: kg_rsv_dev index of the GPU minors a pod of this class allocates from outside its
+     * reservations (unmatched reservations' used and matched reservations' allocatable given back:
+     * deviceshare/plugin.go:397-419, reservation.go:94-117); -1 = the node's own minors. */
+    int32_t dev_base;
+    uint32_t pad_;
 } kg_rsv_view;
 
 /* One matched reservation (frameworkext.ReservationInfo). */
@@ -306,12 +313,22 @@ typedef struct kg_rsv_info {
     uint32_t policy;                     /* KG_RSV_*                                                 */
     uint32_t names;                      /* bit r: resource r in ResourceNames (keys of Allocatable) */
     uint32_t allocate_once;              /* IsAllocateOnce (apis/extension/reservation.go:167)       */
-    uint32_t pad_;
+    int32_t dev;                         /* kg_rsv_dev index of the GPU minors a pod allocates from this
+                                          * reservation (tryAllocateFromReusable, deviceshare/reservation.go
+                                          * :344-410); -1 = it reserves no GPU                         */
     int64_t order;                       /* LabelReservationOrder, 0 = none; |order| < 2^31          */
     int64_t allocatable[KG_RSV_R], allocated[KG_RSV_R], reserved[KG_RSV_R];
     int64_t max_pods;                    /* "pods" in Allocatable, -1 = absent                       */
     int64_t allocated_pods;              /* len(AssignedPods)                                        */
 } kg_rsv_info;
+
+/* GPU minors as one restore sees them (nodeDevice.calcFreeWithPreemptible / filter, deviceshare/
+ * device_cache.go:322-410): total and free per resource (KG_DEV_CORE / _RATIO / _MEM) and minor; a minor
+ * outside the allocation's reach has total 0 and free 0. */
+typedef struct kg_rsv_dev {
+    int64_t total[KG_DEV_R][KG_DEV_MINORS];
+    int64_t free[KG_DEV_R][KG_DEV_MINORS];
+} kg_rsv_dev;
 
 /* ------------------------------------------------------------------------------------------------ */
 int kg_abi_version(void);
@@ -347,7 +364,8 @@ kg_status kg_snapshot_read_quotas(kg_snap* snap, int64_t* used, uint32_t* used_k
 /* Reservation views of this snapshot (KG_PLUGIN_RSV), replacing any earlier upload. Views of one
  * class must name distinct nodes; at most 64 classes and 8 reservations per view. */
 kg_status kg_snapshot_upload_reservations(kg_snap* snap, const kg_rsv_view* views, uint32_t n_views,
-                                          const kg_rsv_info* infos, uint32_t n_infos);
+                                          const kg_rsv_info* infos, uint32_t n_infos, const kg_rsv_dev* devs,
+                                          uint32_t n_devs);
 kg_status kg_snapshot_destroy(kg_snap* snap);
 
 kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out);

@@ -79,6 +79,7 @@ KG_ST_RSV_NODE = 0x08000000
 KG_ST_RSV_RESERVATION = 0x10000000
 KG_ST_RSV_MASK = 0x1C000000
 KG_ST_QUOTA = 0x20000000
+KG_ST_DEV_RSV = 0x40000000  # "Reservation(s) Insufficient gpu devices"
 KG_ST_UNSUPPORTED = 0x80000000
 
 _p64 = C.POINTER(C.c_int64)
@@ -193,13 +194,18 @@ class KgQuotaColumns(C.Structure):
 class KgRsvView(C.Structure):
     _fields_ = [("node", C.c_uint32), ("cls", C.c_uint32), ("first", C.c_uint32), ("count", C.c_uint32),
                 ("req", C.c_int64 * KG_RSV_R), ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("num_pods", C.c_int64),
-                ("pod_requested", C.c_int64 * KG_RSV_R), ("r_allocated", C.c_int64 * KG_RSV_R)]
+                ("pod_requested", C.c_int64 * KG_RSV_R), ("r_allocated", C.c_int64 * KG_RSV_R),
+                ("dev_base", C.c_int32), ("pad_", C.c_uint32)]
 
 
 class KgRsvInfo(C.Structure):
-    _fields_ = [("policy", C.c_uint32), ("names", C.c_uint32), ("allocate_once", C.c_uint32), ("pad_", C.c_uint32),
+    _fields_ = [("policy", C.c_uint32), ("names", C.c_uint32), ("allocate_once", C.c_uint32), ("dev", C.c_int32),
                 ("order", C.c_int64), ("allocatable", C.c_int64 * KG_RSV_R), ("allocated", C.c_int64 * KG_RSV_R),
                 ("reserved", C.c_int64 * KG_RSV_R), ("max_pods", C.c_int64), ("allocated_pods", C.c_int64)]
+
+
+class KgRsvDev(C.Structure):
+    _fields_ = [("total", (C.c_int64 * KG_DEV_MINORS) * KG_DEV_R), ("free", (C.c_int64 * KG_DEV_MINORS) * KG_DEV_R)]
 
 
 # ----------------------------------------------------------------------------------------------
@@ -399,10 +405,22 @@ def quota_columns(t: Table) -> KgQuotaColumns:
 class Reservations:
     """Reservation restore views and matched reservations (kg_rsv_view / kg_rsv_info arrays)."""
 
-    def __init__(self, views, infos):
+    def __init__(self, views, infos, devs=()):
         self.views = (KgRsvView * max(1, len(views)))()
         self.infos = (KgRsvInfo * max(1, len(infos)))()
-        self.n_views, self.n_infos = len(views), len(infos)
+        self.devs = (KgRsvDev * max(1, len(devs)))()
+        self.n_views, self.n_infos, self.n_devs = len(views), len(infos), len(devs)
+        for x in range(len(views)):
+            self.views[x].dev_base = -1
+        for x in range(len(infos)):
+            self.infos[x].dev = -1
+        for x, (tot, fr) in enumerate(devs):
+            t = np.asarray(tot, np.int64).reshape(KG_DEV_R, KG_DEV_MINORS)
+            f = np.asarray(fr, np.int64).reshape(KG_DEV_R, KG_DEV_MINORS)
+            for r in range(KG_DEV_R):
+                for m in range(KG_DEV_MINORS):
+                    self.devs[x].total[r][m] = int(t[r, m])
+                    self.devs[x].free[r][m] = int(f[r, m])
         for a, rows in ((self.views, views), (self.infos, infos)):
             for x, row in enumerate(rows):
                 for k, v in row.items():
@@ -426,6 +444,7 @@ class Reservations:
             r.views[x].node = v.node - lo
         r.n_views = len(keep)
         r.infos, r.n_infos = self.infos, self.n_infos
+        r.devs, r.n_devs = self.devs, self.n_devs
         return r
 
 

@@ -19,6 +19,7 @@ Times are seconds on the cache clock (`clock()`), None being Go's zero time. The
 snapshot's life: adding or removing a node is a new snapshot (kg_snapshot_create + upload)."""
 from __future__ import annotations
 
+import heapq
 import json
 from fractions import Fraction
 from dataclasses import dataclass, field
@@ -460,6 +461,10 @@ class ClusterState:
         self.row_gen = np.zeros(n, np.uint64)
         self.assign_cache = PodAssignCache(self.la, clock, self._touch_name)
         self.devices = NodeDeviceCache(self._touch_name)
+        # NodeMetric expiry is a function of time (isNodeMetricExpired, loadaware/helper.go:35-40): a timer per
+        # metric marks the row when its deadline passes (tick), as an event would
+        self._expiry: List[Tuple[float, int, int]] = []  # (deadline, row, metric token)
+        self._metric_token = [0] * n
 
     # -- generations -----------------------------------------------------------------------------
     def _touch(self, i: int):
@@ -470,6 +475,14 @@ class ClusterState:
         i = self.index.get(name)
         if i is not None:
             self._touch(i)
+
+    def tick(self):
+        """Mark the rows whose NodeMetric expired since the last tick (the clock's time events)."""
+        now = self.clock()
+        while self._expiry and self._expiry[0][0] <= now:
+            _, i, token = heapq.heappop(self._expiry)
+            if token == self._metric_token[i]:
+                self._touch(i)
 
     def rows_since(self, generation: int) -> np.ndarray:
         """Snapshot rows changed after `generation` (UpdateSnapshot's NodeInfo.Generation test)."""
@@ -570,9 +583,19 @@ class ClusterState:
 
     def on_node_metric(self, metric: dict):
         self.assign_cache.add_or_update_node_metric(metric)
+        i = self.index.get(_md(metric).get("name", ""))
+        if i is not None:
+            self._metric_token[i] += 1
+            secs = self.la.node_metric_expiration_seconds
+            ut = (metric.get("status") or {}).get("updateTime")
+            if secs is not None and secs > 0 and ut is not None:
+                heapq.heappush(self._expiry, (float(ut) + secs, i, self._metric_token[i]))
 
     def on_node_metric_delete(self, name: str):
         self.assign_cache.delete_node_metric(name)
+        i = self.index.get(name)
+        if i is not None:
+            self._metric_token[i] += 1
 
     def on_topology(self, name: str, zones: List[Dict[str, str]], kubelet_policy: str = "",
                     cpu_zone: Optional[Dict[int, int]] = None):
@@ -649,6 +672,7 @@ class SnapshotSync:
         self.last_rows = 0
 
     def sync(self) -> int:
+        self.state.tick()
         rows = self.state.rows_since(self.synced)
         self.synced = self.state.generation
         self.last_rows = len(rows)

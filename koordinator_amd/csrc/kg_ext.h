@@ -86,6 +86,22 @@ __device__ __forceinline__ uint32_t dev_eval(const KCfg& c, const int64_t* __res
     return 0;
 }
 
+// DeviceShare Score on a restore table (AutopilotAllocator.score, device_allocator.go:486-508): a table
+// whose free is zero everywhere leaves the GPU type out (nodeDevice.filter skips it): score 0.
+__device__ __forceinline__ int64_t dev_score(const KCfg& c, const DevRec* __restrict__ d, const PodX& x) {
+    int64_t T[DEV_R] = {0, 0, 0}, F[DEV_R] = {0, 0, 0};
+    bool any = false;
+    for (int m = 0; m < DEV_MINORS; m++) {
+#pragma unroll
+        for (int r = 0; r < DEV_R; r++) {
+            T[r] += d->total[r][m];
+            F[r] += d->free_[r][m];
+            any |= d->free_[r][m] != 0;
+        }
+    }
+    return any ? dev_least(c, T, F, x.dreq) : 0;
+}
+
 // Reserve: minors by (per-minor score desc, minor asc), the first numberOfGPUs that fit.
 __device__ __forceinline__ uint32_t dev_choose(const KCfg& c, const int64_t* __restrict__ n, const DevRec* __restrict__ d,
                                                const PodX& x) {
@@ -324,8 +340,9 @@ __device__ __forceinline__ int64_t rsv_score_reservation(const RsvPod& q, const 
 // nominated reservation's ScoreReservation and the node's most-preferred order (0 = none)
 __device__ __forceinline__ int64_t rsv_nominate_score(const RsvPod& q, const int64_t* __restrict__ n, const RsvView& v,
                                                       const RsvInfo* __restrict__ infos, int64_t& node_order,
-                                                      uint32_t ign) {
+                                                      uint32_t ign, int& nom_out) {
     node_order = 0;
+    nom_out = -1;
     int64_t sel = INT64_MAX;
     for (uint32_t t = 0; t < v.count; t++) {
         const int64_t o = infos[v.first + t].order;
@@ -376,7 +393,31 @@ __device__ __forceinline__ int64_t rsv_nominate_score(const RsvPod& q, const int
             }
         }
     }
+    nom_out = nom;
     return nom >= 0 ? rsv_score_reservation(q, infos[v.first + nom]) : 0;
+}
+
+// DeviceShare Filter of a GPU pod on a node where its class has a restore view (plugin.go:397-419):
+// tryAllocateFromReusable over the matched reservations that reserve GPUs, in view order (reservation.go
+// :344-410); if none fits, a pod with a reservation affinity fails there, any other pod allocates outside
+// the reservations (the view's base table).
+__device__ __forceinline__ uint32_t dev_filter_view(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                                    const DevRec* __restrict__ d, const RsvView& v, const PodX& x,
+                                                    bool required) {
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    if (D < 0) return 0;  // no Device object
+    if (D == 0) return KG_ST_DEV_NO_DEVICE;
+    bool any = false;
+    for (uint32_t t = 0; t < v.count; t++) {
+        const int32_t di = e.infos[v.first + t].dev;
+        if (di < 0) continue;
+        any = true;
+        int64_t raw;
+        if (dev_eval(c, n, e.rdev + di, x, raw) == 0) return 0;
+    }
+    if (any && required) return KG_ST_DEV_RSV;
+    int64_t raw;
+    return dev_eval(c, n, v.dev_base >= 0 ? e.rdev + v.dev_base : d, x, raw);
 }
 
 // ---- one pair with every plugin ---------------------------------------------------------------------
@@ -423,12 +464,16 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     }
     uint32_t st = b.status;
     int64_t dev_raw = 0;
+    const bool dev_view = (c.plugins & KG_PLUGIN_DEV) && v && x.dcount > 0;
     if (c.plugins & KG_PLUGIN_DEV) {
-        st |= dev_eval(c, n, d, x, dev_raw);
+        if (dev_view)
+            st |= dev_filter_view(c, e, n, d, *v, x, (p.flags & KG_POD_RSV_REQUIRED) != 0);
+        else
+            st |= dev_eval(c, n, d, x, dev_raw);
         if (x.dcount > 0) {
             const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (p.flags >> 16) & 15u;
-            if (v || ((c.plugins & KG_PLUGIN_NUMA) && (node_pol != KG_NUMA_NONE || pod_pol != KG_NUMA_NONE)))
-                st |= KG_ST_UNSUPPORTED;  // device NUMA hints / device reservation restore: host path
+            if ((c.plugins & KG_PLUGIN_NUMA) && (node_pol != KG_NUMA_NONE || pod_pol != KG_NUMA_NONE))
+                st |= KG_ST_UNSUPPORTED;  // device NUMA hints (topology_hint.go): host path
         }
     }
     RsvPod q;
@@ -443,7 +488,18 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     if (st) return o;
     o.zone = b.zone;
     o.s_dev = dev_raw;
-    if (v) o.s_rsv = rsv_nominate_score(q, n, *v, e.infos, o.order, c.rsv_ign);
+    int nom = -1;
+    if (v) o.s_rsv = rsv_nominate_score(q, n, *v, e.infos, o.order, c.rsv_ign, nom);
+    if (dev_view) {
+        // Score (scoring.go:77-103): with a nominated reservation, its table, or 0 when it reserves no GPU
+        // (scoreWithNominatedReservation, reservation.go:492-520); without one, the view's base table
+        if (nom >= 0) {
+            const int32_t di = e.infos[v->first + nom].dev;
+            o.s_dev = di >= 0 ? dev_score(c, e.rdev + di, x) : 0;
+        } else {
+            o.s_dev = dev_score(c, v->dev_base >= 0 ? e.rdev + v->dev_base : d, x);
+        }
+    }
     return o;
 }
 

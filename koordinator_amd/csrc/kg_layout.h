@@ -293,9 +293,12 @@ struct alignas(16) RsvView {
     int64_t nz_cpu, nz_mem, num_pods;
     int64_t pod_requested[RSV_R];
     int64_t r_allocated[RSV_R];
+    int32_t dev_base;  // DevRec of the restore's allocation outside the reservations (-1: the node's)
+    uint32_t pad_;
 };
 struct alignas(16) RsvInfo {
-    uint32_t policy, names, allocate_once, pad_;
+    uint32_t policy, names, allocate_once;
+    int32_t dev;  // DevRec a pod allocates from this reservation (-1: it reserves no GPU)
     int64_t order;
     int64_t allocatable[RSV_R], allocated[RSV_R], reserved[RSV_R];
     int64_t max_pods, allocated_pods;
@@ -310,6 +313,7 @@ struct ExtDev {
     const RsvView* views;          // sorted by class, then record position
     const RsvInfo* infos;
     const uint32_t* cls_begin;     // [RSV_MAX_CLASSES + 1] view range per class
+    const DevRec* rdev;            // GPU restore tables of views / reservations (kg_rsv_dev)
 };
 
 }  // namespace kg

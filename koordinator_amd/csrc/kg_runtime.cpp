@@ -74,6 +74,7 @@ struct kg_snap {
     RsvView* d_views = nullptr;
     RsvInfo* d_infos = nullptr;
     uint32_t* d_cls_begin = nullptr;  // [RSV_MAX_CLASSES + 1]
+    DevRec* d_rdev = nullptr;         // kg_rsv_dev tables
     uint32_t n_views = 0;
     uint32_t max_cls_views = 0;  // views of the largest reservation class
     std::vector<kg_rsv_view> h_views;  // as uploaded (local snapshot indices)
@@ -101,6 +102,7 @@ struct kg_snap {
         e.views = d_views;
         e.infos = d_infos;
         e.cls_begin = d_cls_begin;
+        e.rdev = d_rdev;
         return e;
     }
 };
@@ -884,6 +886,7 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_views);
     hipFree(s->d_infos);
     hipFree(s->d_cls_begin);
+    hipFree(s->d_rdev);
     hipFree(s->d_stage);
     hipFree(s->d_stage_pos);
     delete s;
@@ -1823,8 +1826,8 @@ kg_status kg_snapshot_read_quotas(kg_snap* s, int64_t* used, uint32_t* used_keys
 }
 
 kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, uint32_t nv, const kg_rsv_info* infos,
-                                          uint32_t ni) {
-    if (!s || (!views && nv) || (!infos && ni)) return KG_INVALID_ARG;
+                                          uint32_t ni, const kg_rsv_dev* devs, uint32_t nd) {
+    if (!s || (!views && nv) || (!infos && ni) || (!devs && nd)) return KG_INVALID_ARG;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
     if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
@@ -1838,12 +1841,15 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
         if (x.count > (uint32_t)RSV_MAX_PER_VIEW || (uint64_t)x.first + x.count > ni)
             return fail(ctx, KG_INVALID_ARG, "view %u: reservations [%u, %u+%u) invalid", v, x.first, x.first, x.count);
         if ((mask[x.node] >> x.cls) & 1ull) return fail(ctx, KG_INVALID_ARG, "view %u: duplicate (class %u, node %u)", v, x.cls, x.node);
+        if (x.dev_base < -1 || x.dev_base >= (int64_t)nd) return fail(ctx, KG_INVALID_ARG, "view %u: GPU table %d of %u", v, x.dev_base, nd);
         mask[x.node] |= 1ull << x.cls;
         order[v] = v;
     }
     for (uint32_t t = 0; t < ni; t++) {
         const int64_t o = infos[t].order;
         if (o <= -(1ll << 31) || o >= (1ll << 31)) return fail(ctx, KG_INVALID_ARG, "reservation %u: order outside int32", t);
+        if (infos[t].dev < -1 || infos[t].dev >= (int64_t)nd)
+            return fail(ctx, KG_INVALID_ARG, "reservation %u: GPU table %d of %u", t, infos[t].dev, nd);
     }
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
         if (views[a].cls != views[b].cls) return views[a].cls < views[b].cls;
@@ -1867,6 +1873,7 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
         d.nz_cpu = x.nz_cpu;
         d.nz_mem = x.nz_mem;
         d.num_pods = x.num_pods;
+        d.dev_base = x.dev_base;
         cb[x.cls + 1]++;
     }
     for (int c = 0; c < RSV_MAX_CLASSES; c++) cb[c + 1] += cb[c];
@@ -1878,6 +1885,7 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
         d.policy = x.policy;
         d.names = x.names;
         d.allocate_once = x.allocate_once;
+        d.dev = x.dev;
         d.order = x.order;
         for (int k = 0; k < RSV_R; k++) {
             d.allocatable[k] = x.allocatable[k];
@@ -1889,10 +1897,14 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    for (void* b : {(void*)s->d_views, (void*)s->d_infos, (void*)s->d_cls_begin}) hipFree(b);
+    for (void* b : {(void*)s->d_views, (void*)s->d_infos, (void*)s->d_cls_begin, (void*)s->d_rdev}) hipFree(b);
     s->d_views = nullptr;
     s->d_infos = nullptr;
     s->d_cls_begin = nullptr;
+    s->d_rdev = nullptr;
+    static_assert(sizeof(DevRec) == sizeof(kg_rsv_dev), "kg_rsv_dev is a DevRec");
+    HIP_TRY(ctx, hipMalloc(&s->d_rdev, sizeof(DevRec) * std::max<uint32_t>(nd, 1)));
+    if (nd) HIP_TRY(ctx, hipMemcpyAsync(s->d_rdev, devs, sizeof(DevRec) * nd, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMalloc(&s->d_views, sizeof(RsvView) * dv.size()));
     HIP_TRY(ctx, hipMalloc(&s->d_infos, sizeof(RsvInfo) * di.size()));
     HIP_TRY(ctx, hipMalloc(&s->d_cls_begin, sizeof(uint32_t) * cb.size()));

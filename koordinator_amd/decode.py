@@ -961,6 +961,95 @@ def gpu_requirements(requests: Dict[str, int]) -> Tuple[List[int], int, int, boo
 RSV_DIMS = ("cpu", "memory", "ephemeral-storage", "scalar0", "scalar1")  # KG_RSV_R order
 
 
+# ---- DeviceShare reservation restore (GPU minors) ----------------------------------------------------
+# A device table here is int64 [KG_DEV_R][KG_DEV_MINORS] (gpu-core, gpu-memory-ratio, gpu-memory per minor)
+# with a presence mask over minors (a deviceResources map holds a minor or not).
+
+def _dz():
+    return np.zeros((abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
+
+
+def _dtab(v):
+    return _dz() if v is None else np.asarray(v, np.int64).reshape(abi.KG_DEV_R, abi.KG_DEV_MINORS).copy()
+
+
+def _dmask(a) -> np.ndarray:
+    return np.any(a != 0, axis=0)
+
+
+def dev_effective(total, used, free, pre, pre_mask, req=None, req_mask=None):
+    """The (total, free) an allocation sees (nodeDevice.calcFreeWithPreemptible, device_cache.go:322-364, and
+    nodeDevice.filter, :366-410): a minor holding preemptible resources frees them from its used (never below
+    zero), and if any such minor then has something left, the other minors keep their free; allocating
+    from a reservation's required resources keeps only those minors, each capped by them
+    (util.MinResourceList). Minors outside the result have total and free 0."""
+    total, used, free = _dtab(total), _dtab(used), _dtab(free)
+    F = free.copy()
+    merged = {}
+    for m in range(abi.KG_DEV_MINORS):
+        if pre_mask[m]:
+            u = np.maximum(used[:, m] - pre[:, m], 0)
+            rem = np.maximum(total[:, m] - u, 0)
+            if np.any(rem != 0):
+                merged[m] = rem
+    for m, rem in merged.items():
+        F[:, m] = rem
+    T = total.copy()
+    if req_mask is not None:
+        for m in range(abi.KG_DEV_MINORS):
+            if req_mask[m]:
+                F[:, m] = np.minimum(F[:, m], req[:, m])
+            else:
+                F[:, m] = 0
+                T[:, m] = 0
+    return T, F
+
+
+def dev_reusable(total, used, free, unmatched_used, matched_allocated, matched_allocatable, matched):
+    """Effective device tables of one node for one pod's restore state (deviceshare/reservation.go):
+      matched[i] = (policy, allocatable, remained) of the i-th matched reservation holding GPUs, each a
+      (table, mask) pair; unmatched_used / matched_allocated / matched_allocatable are the merged tables
+      (mergeReservationAllocations, :94-117).
+    Returns (per_matched, base): per_matched[i] = (total, free) that tryAllocateFromReusable (:344-410)
+    allocates from for reservation i (preemptible = unmatched used + matched allocated + its remained; the
+    Restricted policy only its minors, capped by calcRequiredDeviceResources :436-455), and base = (total,
+    free) of the allocation outside the reservations (plugin.go:417-419: unmatched used + matched
+    allocatable)."""
+    uu, uum = unmatched_used
+    ma, mam = matched_allocated
+    mal, malm = matched_allocatable
+    out = []
+    for policy, (alloc, alloc_mask), (rem, rem_mask) in matched:
+        pre = uu + ma + rem
+        pm = uum | mam | rem_mask
+        if policy == abi.KG_RSV_RESTRICTED:
+            req_mask = rem_mask.copy() if rem_mask.any() else alloc_mask.copy()
+            req = np.where(rem_mask[None, :], rem, 0)
+            out.append(dev_effective(total, used, free, pre, pm, req, req_mask & alloc_mask))
+        else:
+            out.append(dev_effective(total, used, free, pre, pm))
+    base = dev_effective(total, used, free, uu + mal, uum | malm)
+    return out, base
+
+
+def dev_reservation_parts(r: dict):
+    """(allocatable, allocated, remained, used-when-unmatched) of one reservation's GPUs (RestoreReservation's
+    filterFn, reservation.go:163-186): `dev_alloc` is the reserve pod's allocation (nodeDevice.getUsed),
+    `dev_allocated` its assigned pods' allocations on those minors (appendAllocatedByHints). Each part is
+    a (table, mask) pair; None when the reservation holds no GPU."""
+    alloc = _dtab(r.get("dev_alloc"))
+    amask = _dmask(alloc)
+    if not amask.any():
+        return None
+    allocated = np.where(amask[None, :], _dtab(r.get("dev_allocated")), 0)
+    almask = _dmask(allocated)
+    rem = alloc - allocated  # subtractAllocated(.., false): negative kept, zero minors dropped
+    rmask = _dmask(rem)
+    used = np.where(_dmask(np.maximum(allocated, 0))[None, :], np.maximum(allocated, 0), 0)
+    return (alloc, amask), (allocated, almask), (rem, rmask), (used, _dmask(used))
+
+
+
 def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
     """Host restatement of the Reservation transformer (reservation/transformer.go:147-350,740-935).
 
@@ -969,12 +1058,18 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
     allocatable / allocated / reserved (KG_RSV_R vectors, allocated None when no pod is assigned),
     allocated_pods, policy, order, allocate_once, max_pods.
 
-    Returns (nodes_default, views, infos): the snapshot columns as seen by pods matching nothing on
+    Returns (nodes_default, views, infos, devs): the snapshot columns as seen by pods matching nothing on
     the node (every reservation with assigned pods corrected by updateNodeInfoRequestedForUnmatched),
     and per (class, node) the restored view with its matched reservations (kg_rsv_view / kg_rsv_info
     dicts for abi.Reservations). Reserve pods request their Allocatable; the non-zero request of a
     present cpu / memory key is the value itself (GetNonZeroRequestForResource,
-    frameworkext/reservation_info.go:581-605)."""
+    frameworkext/reservation_info.go:581-605).
+
+    DeviceShare (nodes with dev_minors >= 0): a reservation may carry `dev_alloc` (its reserve pod's GPU
+    allocation, [KG_DEV_R][KG_DEV_MINORS]) and `dev_allocated` (its pods' allocations on those minors);
+    `nodes["dev_used"]` (optional, default total - free) is the node's used per minor. The default
+    columns' dev_free then give back what pods use inside unmatched reservations, and `devs` holds the
+    (total, free) tables views (dev_base) and matched reservations (dev) allocate from (dev_reusable)."""
     out = {k: np.array(v, copy=True) for k, v in nodes.items()}
     req_cols = ["req_cpu", "req_mem", "req_eph", "sc_req0", "sc_req1"]
     by_node: Dict[int, List[int]] = {}
@@ -1000,7 +1095,31 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
                 ncpu, nmem = nz(a, r.get("allocated") is not None)
                 out["nz_cpu"][i] -= ncpu
                 out["nz_mem"][i] -= nmem
-    views, infos = [], []
+    views, infos, devs = [], [], []
+    dev_on = "dev_minors" in nodes and "dev_total" in nodes
+    parts = [dev_reservation_parts(r) for r in reservations]
+
+    def node_dev(i):
+        tot = np.asarray(nodes["dev_total"][i], np.int64)
+        fr = np.asarray(nodes["dev_free"][i], np.int64)
+        used = np.asarray(nodes["dev_used"][i], np.int64) if "dev_used" in nodes else tot - fr
+        return tot, used, fr
+
+    def merged(xs, part):
+        t, m = _dz(), np.zeros(abi.KG_DEV_MINORS, bool)
+        for x in xs:
+            if parts[x] is not None:
+                t += parts[x][part][0]
+                m |= parts[x][part][1]
+        return t, m
+
+    for i, xs in by_node.items():  # default view: unmatched = the reservations with assigned pods
+        if dev_on and int(nodes["dev_minors"][i]) >= 0:
+            gx = [x for x in xs if parts[x] is not None and int(reservations[x].get("allocated_pods", 0)) > 0]
+            if gx:
+                tot, used, fr = node_dev(i)
+                uu = merged(gx, 3)
+                out["dev_free"][i] = dev_effective(tot, used, fr, uu[0], uu[1])[1]
     for i in sorted(by_node):
         classes = sorted({int(reservations[x]["cls"]) for x in by_node[i]})
         for c in classes:
@@ -1026,6 +1145,22 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
                 ncpu, nmem = nz(rp, True)
                 nzc -= ncpu
                 nzm -= nmem
+            dev_base, dev_idx = -1, {}
+            if dev_on and int(nodes["dev_minors"][i]) >= 0 and any(parts[x] is not None for x in by_node[i]):
+                # RestoreReservation (deviceshare/reservation.go:149-200): matched = the class's reservations
+                # holding GPUs, unmatched = the node's others that hold GPUs and have assigned pods
+                tot, used, fr = node_dev(i)
+                gm = [x for x in matched if parts[x] is not None]
+                gu = [x for x in by_node[i] if x not in matched and parts[x] is not None
+                      and int(reservations[x].get("allocated_pods", 0)) > 0]
+                per, base = dev_reusable(tot, used, fr, merged(gu, 3), merged(gm, 1), merged(gm, 0),
+                                         [(int(reservations[x].get("policy", abi.KG_RSV_DEFAULT)), parts[x][0],
+                                           parts[x][2]) for x in gm])
+                dev_base = len(devs)
+                devs.append(base)
+                for x, tf in zip(gm, per):
+                    dev_idx[x] = len(devs)
+                    devs.append(tf)
             first = len(infos)
             for x in matched:
                 r = reservations[x]
@@ -1037,11 +1172,12 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
                 infos.append(dict(policy=int(r.get("policy", abi.KG_RSV_DEFAULT)), names=names,
                                   allocate_once=int(bool(r.get("allocate_once", True))), order=int(r.get("order", 0)),
                                   allocatable=alloc, allocated=vec(r, "allocated"), reserved=vec(r, "reserved"),
-                                  max_pods=int(r.get("max_pods", -1)), allocated_pods=int(r.get("allocated_pods", 0))))
+                                  max_pods=int(r.get("max_pods", -1)), allocated_pods=int(r.get("allocated_pods", 0)),
+                                  dev=dev_idx.get(x, -1)))
             views.append(dict(node=i, cls=c, first=first, count=len(matched), req=req, nz_cpu=nzc, nz_mem=nzm,
                               num_pods=int(out["num_pods"][i]) - len(matched), pod_requested=pod_requested,
-                              r_allocated=r_alloc))
-    return out, views, infos
+                              r_allocated=r_alloc, dev_base=dev_base))
+    return out, views, infos, devs
 
 
 def quota_keys(pods: abi.Table, max_keys: np.ndarray) -> np.ndarray:

@@ -106,7 +106,7 @@ def lib():
     L.kg_snapshot_upload_quotas.restype = st
     L.kg_snapshot_read_quotas.argtypes = [vp, P(i64), P(u32), P(i64), P(u32)]
     L.kg_snapshot_read_quotas.restype = st
-    L.kg_snapshot_upload_reservations.argtypes = [vp, P(abi.KgRsvView), u32, P(abi.KgRsvInfo), u32]
+    L.kg_snapshot_upload_reservations.argtypes = [vp, P(abi.KgRsvView), u32, P(abi.KgRsvInfo), u32, P(abi.KgRsvDev), u32]
     L.kg_snapshot_upload_reservations.restype = st
     L.kg_assume_ext.argtypes = [vp, vp, u32, u32, P(i32), P(u32)]
     L.kg_assume_ext.restype = st
@@ -242,7 +242,8 @@ class Snapshot:
     def upload_reservations(self, rsv: abi.Reservations):
         self.ctx.check(self.ctx.L.kg_snapshot_upload_reservations(
             self.h, C.cast(rsv.views, C.POINTER(abi.KgRsvView)), rsv.n_views,
-            C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos), "kg_snapshot_upload_reservations")
+            C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos,
+            C.cast(rsv.devs, C.POINTER(abi.KgRsvDev)), rsv.n_devs), "kg_snapshot_upload_reservations")
 
     def close(self):
         if getattr(self, "h", None) and getattr(self.ctx, "h", None):

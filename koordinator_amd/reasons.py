@@ -62,6 +62,8 @@ def plugin_reasons(bits: int, scalar_names=DEFAULT_SCALARS) -> dict:
             add("NodeNUMAResource", msg)
     if bits & (abi.KG_ST_DEV_INSUFFICIENT | abi.KG_ST_DEV_NO_DEVICE):
         add("DeviceShare", "Insufficient gpu devices")
+    if bits & abi.KG_ST_DEV_RSV:  # makeReasonsByReservation (deviceshare/plugin.go)
+        add("DeviceShare", "Reservation(s) Insufficient gpu devices")
     if bits & abi.KG_ST_RSV_AFFINITY:
         add("Reservation", "node(s) no reservations match reservation affinity")
     if bits & abi.KG_ST_RSV_NODE:

@@ -134,11 +134,13 @@ N_RSV_CLASSES = 8
 def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 100, rsv_frac: float = 0.05):
     """Config 5: configs 1-2's plugins plus DeviceShare (8 GPU minors per node: gpu-core
     100, gpu-memory-ratio 100, gpu-memory 192Gi; minors 40% idle, 30% fully used, 30% partially used),
-    Reservation (5% of nodes hold 1-4 reservations of one of 8 owner classes; 20% of the non-GPU pods
-    match one class, a quarter of them with a required reservation affinity) and ElasticQuota (100
-    flat quotas, every pod in one; 10% non-preemptible pods). 30% of the pods request GPUs: 60% whole
-    GPUs (1/2/4/8), 40% shared (gpu-core 50 + gpu-memory-ratio 50, or gpu-core 50 + gpu-memory 24Gi).
-    NUMA policy None on every node (GPU and reservation NUMA restore stay on the host path).
+    Reservation (5% of nodes hold 1-4 reservations of one of 8 owner classes, a third of them reserving
+    1-2 whole GPUs of the node's idle minors, their assigned pods using part of them; 20% of all pods, GPU
+    pods included, match one class, a quarter of them with a required reservation affinity) and
+    ElasticQuota (100 flat quotas, every pod in one; 10% non-preemptible pods). 30% of the pods request
+    GPUs: 60% whole GPUs (1/2/4/8), 40% shared (gpu-core 50 + gpu-memory-ratio 50, or gpu-core 50 +
+    gpu-memory 24Gi). NUMA policy None on every node (the NUMA zone restore of reservations and the
+    DeviceShare NUMA hints stay on the host path).
 
     Returns (cfg, nodes, pods, quotas, reservations): nodes already restored to the view of pods that
     match no reservation (decode.reservation_restore), reservations = abi.Reservations."""
@@ -159,11 +161,12 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     free[:, abi.KG_DEV_CORE, :] -= used_pct
     free[:, abi.KG_DEV_RATIO, :] -= used_pct
     free[:, abi.KG_DEV_MEM, :] -= used_pct * GPU_MEM_PER_MINOR // 100
-    t["dev_total"], t["dev_free"] = tot, free
+    used = tot - free
     # Reservations on 5% of the nodes (counted in the true NodeInfo: reserve pod + assigned pods)
     resv = []
     holders = np.nonzero(r.random(n) < rsv_frac)[0]
     for i in holders:
+        idle = [m for m in range(abi.KG_DEV_MINORS) if used_pct[i, m] == 0]
         for _ in range(int(r.integers(1, 5))):
             cpu = int(r.choice([2000, 4000, 8000]))
             mem = int(r.choice([4, 8, 16])) * GI
@@ -176,15 +179,33 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
             pol = r.random()
             policy = abi.KG_RSV_DEFAULT if pol < 0.6 else (abi.KG_RSV_ALIGNED if pol < 0.8 else abi.KG_RSV_RESTRICTED)
             order = int(r.integers(1, 11)) if r.random() < 0.3 else 0
+            # GPUs: the reserve pod holds whole idle minors; assigned pods use part of them (both counted
+            # in the node's used, as nodeDevice.deviceUsed counts every allocation)
+            dev_alloc = dev_allocated = None
+            if idle and r.random() < 1 / 3:
+                k = min(len(idle), int(r.integers(1, 3)))
+                ms = [idle.pop(int(r.integers(0, len(idle)))) for _ in range(k)]
+                dev_alloc = np.zeros((abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
+                dev_alloc[:, ms] = tot[i][:, ms]
+                used[i] += dev_alloc
+                if ap:
+                    part = int(r.choice([25, 50, 100]))
+                    dev_allocated = np.zeros_like(dev_alloc)
+                    m0 = ms[0]
+                    dev_allocated[abi.KG_DEV_CORE, m0] = part
+                    dev_allocated[abi.KG_DEV_RATIO, m0] = part
+                    dev_allocated[abi.KG_DEV_MEM, m0] = part * GPU_MEM_PER_MINOR // 100
+                    used[i] += dev_allocated
             resv.append(dict(node=int(i), cls=int(r.integers(0, N_RSV_CLASSES)), allocatable=alloc,
                              allocated=allocated, reserved=None, allocated_pods=ap, policy=policy, order=order,
-                             allocate_once=ap == 0, max_pods=-1))
+                             allocate_once=ap == 0, max_pods=-1, dev_alloc=dev_alloc, dev_allocated=dev_allocated))
             t["req_cpu"][i] += cpu + (allocated[0] if allocated else 0)
             t["req_mem"][i] += mem + (allocated[1] if allocated else 0)
             t["nz_cpu"][i] += cpu + (allocated[0] if allocated else 0)
             t["nz_mem"][i] += mem + (allocated[1] if allocated else 0)
             t["num_pods"][i] += 1 + ap
-    t, views, infos = reservation_restore(t, resv)
+    t["dev_total"], t["dev_free"], t["dev_used"] = tot, np.maximum(tot - used, 0), used
+    t, views, infos, devs = reservation_restore(t, resv)
     # Pods
     pr = _rng(seed_config, 1)
     p = pods(n_pods, seed_config, rng=pr)
@@ -203,8 +224,8 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
         p["dev_req"][j] = vec
         p["dev_keys"][j] = keys
         p["dev_count"][j] = cnt
-    # reservation owner classes (non-GPU pods only: GPU pods with reservations leave the device path)
-    cls_on = (~gpu) & (pr.random(n_pods) < 0.20 / 0.70)
+    # reservation owner classes
+    cls_on = pr.random(n_pods) < 0.20
     p["rsv_class"] = np.where(cls_on, pr.integers(0, N_RSV_CLASSES, n_pods), -1).astype(np.int32)
     p["flags"] |= np.where(cls_on & (pr.random(n_pods) < 0.25), abi.KG_POD_RSV_REQUIRED, 0).astype(np.uint32)
     # ElasticQuota: flat quotas with Max over cpu + memory (10%: also the batch resources)
@@ -221,7 +242,7 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     p["quota"] = pr.integers(0, n_quotas, n_pods).astype(np.int32)
     p["flags"] |= np.where(pr.random(n_pods) < 0.10, abi.KG_POD_NON_PREEMPTIBLE, 0).astype(np.uint32)
     p["quota_keys"] = quota_keys(p, maxk)
-    return cfg, t, p, q, abi.Reservations(views, infos)
+    return cfg, t, p, q, abi.Reservations(views, infos, devs)
 
 
 def topology(n_nodes: int, n_pods: int, seed: int = 0, pod_policy_frac: float = 0.3):

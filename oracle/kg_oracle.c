@@ -1135,6 +1135,53 @@ static uint32_t dev_eval(const kg_config* c, const kg_node_columns* n, uint32_t 
     return 0;
 }
 
+/* The same Filter and Score on one GPU restore table (kg_rsv_dev: the free / total a reservation restore
+ * hands the allocator, device_cache.go:322-410). Score: AutopilotAllocator.score (device_allocator.go
+ * :486-508) leaves the GPU type out when every free value is zero (nodeDevice.filter), giving 0. */
+static uint32_t dev_eval_tab(const kg_config* c, const kg_rsv_dev* t, int32_t D, const kg_pod_columns* p, uint32_t j,
+                             int64_t* raw) {
+    *raw = 0;
+    int64_t preq[KG_DEV_R], T[KG_DEV_R] = {0, 0, 0}, F[KG_DEV_R] = {0, 0, 0};
+    uint32_t keys, cnt = p->dev_count[j], fit = 0;
+    dev_pod_req(p, j, preq, &keys);
+    for (int32_t m = 0; m < D; m++) {
+        int64_t fr[KG_DEV_R];
+        for (int r = 0; r < KG_DEV_R; r++) fr[r] = t->free[r][m];
+        fit += (uint32_t)dev_minor_fits(fr, preq, keys);
+    }
+    int any = 0;
+    for (int m = 0; m < KG_DEV_MINORS; m++)
+        for (int r = 0; r < KG_DEV_R; r++) {
+            T[r] += t->total[r][m];
+            F[r] += t->free[r][m];
+            any |= t->free[r][m] != 0;
+        }
+    *raw = any ? dev_least(c, T, F, preq) : 0;
+    return fit < cnt ? KG_ST_DEV_INSUFFICIENT : 0u;
+}
+
+/* DeviceShare Filter of a GPU pod on a reservation view (deviceshare/plugin.go:397-419):
+ * tryAllocateFromReusable (reservation.go:344-410) over the matched reservations reserving GPUs in view
+ * order, the first that fits wins; none fitting fails a pod with a reservation affinity ("Reservation(s)
+ * Insufficient gpu devices") and sends any other pod to the allocation outside the reservations. */
+static uint32_t dev_filter_view(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                                uint32_t j, const kgo_ext* e, const kg_rsv_view* v) {
+    int32_t D = n->dev_minors ? n->dev_minors[i] : -1;
+    if (D < 0) return 0;
+    if (D == 0) return KG_ST_DEV_NO_DEVICE;
+    int any = 0;
+    int64_t raw;
+    for (uint32_t t = 0; t < v->count; t++) {
+        int32_t di = e->infos[v->first + t].dev;
+        if (di < 0) continue;
+        any = 1;
+        if (dev_eval_tab(c, &e->devs[di], D, p, j, &raw) == 0) return 0;
+    }
+    if (any && (p->flags[j] & KG_POD_RSV_REQUIRED)) return KG_ST_DEV_RSV;
+    if (v->dev_base >= 0) return dev_eval_tab(c, &e->devs[v->dev_base], D, p, j, &raw);
+    return dev_eval(c, n, i, p, j, &raw);
+}
+
 /* Reserve-time minor choice: scoreDevices + sortDeviceResourcesByMinor (score desc, minor asc,
  * device_resources.go:171-209), first numberOfGPUs minors that fit. Returns the minor bitmask. */
 static uint32_t dev_choose(const kg_config* c, const int64_t* total_tab, const int64_t* free_tab, uint32_t i,
@@ -1454,8 +1501,9 @@ static int64_t rsv_score_reservation(const rsv_ctx* x, const kg_rsv_info* r) {
 
 /* Nominated reservation's score for a feasible pair (NominateReservation nominator.go:348-419 with
  * FilterNominateReservation plugin.go:1195-1212), and the node's order for preferredNode. */
-static int64_t rsv_nominate_score(const rsv_ctx* x, int64_t* node_order) {
+static int64_t rsv_nominate_score(const rsv_ctx* x, int64_t* node_order, int* nom_index) {
     *node_order = 0;
+    *nom_index = -1;
     if (!x->v || x->v->count == 0) return 0;
     const kg_rsv_info* infos = x->infos;
     const uint32_t first = x->v->first, count = x->v->count;
@@ -1498,6 +1546,7 @@ static int64_t rsv_nominate_score(const rsv_ctx* x, int64_t* node_order) {
             }
         }
     }
+    if (nom) *nom_index = (int)(nom - &infos[first]);
     return nom ? rsv_score_reservation(x, nom) : 0;
 }
 
@@ -1571,11 +1620,12 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
                 st |= numa_eval(c, n, i, ovp, p, j, &s_numa, &zone);
         }
         int64_t dev_raw = 0;
-        if (c->plugins & KG_PLUGIN_DEV) st |= dev_eval(c, n, i, p, j, &dev_raw);
-        /* GPU pods on reservation views (device reservation restore) or under a NUMA policy (DeviceShare
-         * joins the NUMA hint merge, topology_hint.go): host path */
-        if (gpu_pod && (v || ((c->plugins & KG_PLUGIN_NUMA) &&
-                              (n->numa_policy[i] != KG_NUMA_NONE || p->numa_policy[j] != KG_NUMA_NONE))))
+        const int dev_view = gpu_pod && v;
+        if (c->plugins & KG_PLUGIN_DEV)
+            st |= dev_view ? dev_filter_view(c, n, i, p, j, e, v) : dev_eval(c, n, i, p, j, &dev_raw);
+        /* GPU pods under a NUMA policy (DeviceShare joins the NUMA hint merge, topology_hint.go): host path */
+        if (gpu_pod && (c->plugins & KG_PLUGIN_NUMA) &&
+            (n->numa_policy[i] != KG_NUMA_NONE || p->numa_policy[j] != KG_NUMA_NONE))
             st |= KG_ST_UNSUPPORTED;
         rsv_ctx x;
         if (c->plugins & KG_PLUGIN_RSV) {
@@ -1589,7 +1639,23 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
         if (st) continue;
         o->zone[i] = zone;
         o->dev[i] = dev_raw;
-        if ((c->plugins & KG_PLUGIN_RSV) && v) o->rsv[i] = rsv_nominate_score(&x, &o->order[i]);
+        int nom = -1;
+        if ((c->plugins & KG_PLUGIN_RSV) && v) o->rsv[i] = rsv_nominate_score(&x, &o->order[i], &nom);
+        if (dev_view) {
+            /* DeviceShare Score (scoring.go:77-103): the nominated reservation's table (0 when it reserves no
+             * GPU: scoreWithNominatedReservation, reservation.go:492-520), else the view's base table */
+            int32_t D = n->dev_minors[i];
+            int64_t raw = 0;
+            if (nom >= 0) {
+                int32_t di = e->infos[v->first + (uint32_t)nom].dev;
+                if (di >= 0) dev_eval_tab(c, &e->devs[di], D, p, j, &raw);
+            } else if (v->dev_base >= 0) {
+                dev_eval_tab(c, &e->devs[v->dev_base], D, p, j, &raw);
+            } else {
+                dev_eval(c, n, i, p, j, &raw);
+            }
+            o->dev[i] = raw;
+        }
     }
 }
 

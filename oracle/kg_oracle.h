@@ -74,6 +74,8 @@ typedef struct kgo_ext {
     uint32_t n_views;
     const kg_rsv_info* infos;
     uint32_t n_infos;
+    const kg_rsv_dev* devs; /* GPU restore tables named by kg_rsv_view.dev_base / kg_rsv_info.dev */
+    uint32_t n_devs;
 } kgo_ext;
 
 /* Verify matrix with every enabled plugin incl. KG_PLUGIN_DEV / RSV / QUOTA: raw Score values, totals

@@ -24,7 +24,8 @@ class KgoPair(C.Structure):
 class KgoExt(C.Structure):
     _fields_ = [("quotas", C.POINTER(abi.KgQuotaColumns)), ("n_quotas", C.c_uint32),
                 ("views", C.POINTER(abi.KgRsvView)), ("n_views", C.c_uint32),
-                ("infos", C.POINTER(abi.KgRsvInfo)), ("n_infos", C.c_uint32)]
+                ("infos", C.POINTER(abi.KgRsvInfo)), ("n_infos", C.c_uint32),
+                ("devs", C.POINTER(abi.KgRsvDev)), ("n_devs", C.c_uint32)]
 
 
 def make_ext(quotas=None, rsv=None) -> KgoExt:
@@ -40,6 +41,8 @@ def make_ext(quotas=None, rsv=None) -> KgoExt:
         e.n_views = rsv.n_views
         e.infos = C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo))
         e.n_infos = rsv.n_infos
+        e.devs = C.cast(rsv.devs, C.POINTER(abi.KgRsvDev))
+        e.n_devs = rsv.n_devs
         keep.append(rsv)
     e._keep = keep
     return e

@@ -73,6 +73,31 @@ def test_ext_verify(ctx, subset, seed, n_nodes, n_pods, rsv_frac):
     assert (st == 0).any()
 
 
+def test_gpu_pods_on_reservation_views(ctx):
+    """GPU pods of a reservation class on nodes where reservations hold GPUs: the DeviceShare restore
+    (tryAllocateFromReusable over the matched reservations, the base allocation outside them, the nominated
+    reservation's table for the Score) on the device equals the oracle over every pair."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(500, 384, seed_config=13, rsv_frac=0.6)
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_verify(snap, batch)
+    ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
+    assert_equal(got, ref, "gpu+views")
+    st = ref.status
+    gpu_cls = (pods["dev_count"] > 0) & (pods["rsv_class"] >= 0)
+    assert gpu_cls.sum() >= 10
+    assert not (st & abi.KG_ST_UNSUPPORTED).any()
+    assert (st[gpu_cls] & abi.KG_ST_DEV_RSV).any()  # required affinity, no matched reservation's GPUs fit
+    view_nodes = np.zeros(len(nodes["req_cpu"]), bool)
+    for v in rsv.view_list():
+        if v.dev_base >= 0:
+            view_nodes[v.node] = True
+    ok = (st == 0) & gpu_cls[:, None] & view_nodes[None, :]
+    assert ok.any() and (ref.score_dev[ok] > 0).any()
+    keys = engine.eval_select(snap, batch, 2)
+    assert np.array_equal(keys, oracle_lib.ext_select(kc, nodes, pods, 2, 0, quotas, rsv))
+
+
 @pytest.mark.parametrize("k", [1, 3])
 def test_ext_select(ctx, k):
     cfg, nodes, pods, quotas, rsv = synth.cluster5(2500, 300, seed_config=21, rsv_frac=0.2)
