@@ -86,6 +86,36 @@ __device__ __forceinline__ uint32_t dev_eval(const KCfg& c, const int64_t* __res
     return 0;
 }
 
+// DeviceShare Filter + node Score from the record's DevSum for a pod of GPU request class cls (same
+// results as dev_eval; a pod outside the batch's classes walks the minors).
+__device__ __forceinline__ uint32_t dev_eval_sum(const KCfg& c, const int64_t* __restrict__ n, const DevRec* __restrict__ d,
+                                                 const DevSum* __restrict__ ds, const PodX& x, uint32_t cls,
+                                                 int64_t& raw) {
+    raw = 0;
+    if (x.dcount == 0) return 0;
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    if (D < 0) return 0;
+    if (D == 0) return KG_ST_DEV_NO_DEVICE;
+    if (cls >= (uint32_t)DEV_CLASSES) return dev_eval(c, n, d, x, raw);
+    const uint32_t fit = (uint32_t)(ds->fit >> (4u * cls)) & 15u;
+    if (fit < x.dcount) return KG_ST_DEV_INSUFFICIENT;
+    if (c.most & MOST_DEV) {
+        raw = dev_least(c, ds->T, ds->F, x.dreq);
+        return 0;
+    }
+    int64_t score = 0, wsum = 0;
+#pragma unroll
+    for (int r = 0; r < DEV_R; r++) {
+        const int64_t w = c.dev_w[r], T = ds->T[r], F = ds->F[r];
+        if (w == 0 || T == 0) continue;
+        const int64_t req = T >= F ? T - F + x.dreq[r] : T;
+        score += least_req<false>(req, T, ds->rcp[r]) * w;
+        wsum += w;
+    }
+    raw = wdiv(score, wsum);
+    return 0;
+}
+
 // DeviceShare Score on a restore table (AutopilotAllocator.score, device_allocator.go:486-508): a table
 // whose free is zero everywhere leaves the GPU type out (nodeDevice.filter skips it): score 0.
 __device__ __forceinline__ int64_t dev_score(const KCfg& c, const DevRec* __restrict__ d, const PodX& x) {

@@ -40,6 +40,56 @@ __device__ __forceinline__ int32_t wmax_i32(int32_t v) {
 
 __device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) { return e.dev ? e.dev + rec : nullptr; }
 
+// DevSum of every record for the pod batch's GPU request classes (one thread per record).
+__global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nodes, const DevRec* __restrict__ devs,
+                                                 uint32_t n_nodes, const DevClass* __restrict__ cls, uint32_t n_cls,
+                                                 DevSum* __restrict__ out) {
+    const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
+    if (rec >= n_nodes) return;
+    const DevRec& d = devs[rec];
+    const int32_t D = (int32_t)nodes[rec].v[N_DEV_MINORS];
+    DevSum o;
+    o.fit = 0;
+    for (int r = 0; r < DEV_R; r++) {
+        int64_t t = 0, f = 0;
+        for (int m = 0; m < DEV_MINORS; m++) {
+            t += d.total[r][m];
+            f += d.free_[r][m];
+        }
+        o.T[r] = t;
+        o.F[r] = f;
+        o.rcp[r] = t != 0 ? 1.0 / (double)t : 0.0;
+    }
+    for (uint32_t k = 0; k < n_cls; k++) {
+        PodX x{};
+        x.dkeys = cls[k].dkeys;
+        for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
+        uint64_t fit = 0;
+        for (int32_t m = 0; m < D; m++) {
+            const int64_t fr[DEV_R] = {d.free_[0][m], d.free_[1][m], d.free_[2][m]};
+            fit += dev_minor_fits(fr, x) ? 1u : 0u;
+        }
+        o.fit |= fit << (4u * k);
+    }
+    out[rec] = o;
+}
+
+// Weighted total of a fast-base pair (FB paths): base total from the fast block + the normalised
+// DeviceShare term + the Reservation term, which off a view is 0 or the preferred node's 100 (total_ext
+// with s_rsv = 0). mag = ceil(2^32 / dev_max) for dev_max >= 2: floor(s * 100 / dev_max) exactly for
+// s * 100 <= 10^4 (the error term s * 100 * (mag * dev_max - 2^32) stays below 2^32).
+__device__ __forceinline__ int64_t total_fb(const KCfg& c, uint64_t base_key, int64_t s_dev, uint32_t dm, uint32_t mag,
+                                            uint32_t g, uint64_t pf) {
+    const uint32_t n100 = (uint32_t)s_dev * 100u;
+    const uint32_t nd = dm == 0 ? (uint32_t)s_dev : (dm == 1 ? n100 : __umulhi(n100, mag));
+    const int64_t rsv = (pf != PREF_NONE && (uint32_t)pf == g) ? (int64_t)c.w_rsv * 100 : 0;
+    return (int64_t)(base_key >> 32) + (int64_t)c.w_dev * nd + rsv;
+}
+
+__device__ __forceinline__ uint32_t norm_magic(uint32_t dm) {
+    return dm >= 2 ? (uint32_t)(((1ull << 32) + dm - 1) / dm) : 0u;
+}
+
 // ElasticQuota PreFilter of every pod against the batch-start quota state (matrix mode).
 __global__ __launch_bounds__(256) void k_ext_gate(PodsDev pods, uint32_t n_pods, ExtDev e, uint32_t plugins,
                                                   uint32_t* __restrict__ qst, uint32_t* __restrict__ pstat) {
@@ -136,6 +186,7 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
         cv = cfg_in_vgprs(cfg);
     }
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
+    const uint32_t dcls = pods.dev_cls ? pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
     for (uint32_t rec = lo; rec < hi; rec++) {
         const int64_t* __restrict__ n = nodes[rec].v;
         if constexpr (FB) {
@@ -149,7 +200,7 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
                 const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
                 int64_t raw = 0;
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
-                if (!st) st |= dev_eval(cfg, n, dev_of(e, rec), px, raw);
+                if (!st) st |= dev_eval_sum(cfg, n, dev_of(e, rec), e.dsum + rec, px, dcls, raw);
                 if (!st) dmax = max(dmax, (uint32_t)raw);
                 continue;
             }
@@ -249,6 +300,8 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
         cv = cfg_in_vgprs(cfg);
     }
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
+    const uint32_t dcls = pods.dev_cls ? pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
+    const uint32_t mag = norm_magic(dm);
     // pairs that need the host path: a cpuset-binding pod under NodeNUMAResource has one on every node
     // (numa_eval), whatever path the record takes; FB records (class 0, not F_BIG: NUMA policy None) have
     // no other source
@@ -265,10 +318,10 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
                 const uint32_t g = index_base + (uint32_t)((uint64_t)fr.flags >> 32);
                 const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, g);
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
-                PairX x{};
+                int64_t s_dev = 0;
                 if ((cfg.plugins & KG_PLUGIN_DEV) && !st)  // only the key's zero-ness matters once st != 0
-                    st |= dev_eval(cfg, n, dev_of(e, rec), px, x.s_dev);
-                const int64_t tot = (int64_t)(bk >> 32) + total_ext(cfg, x, g, dm, rm, pf);
+                    st |= dev_eval_sum(cfg, n, dev_of(e, rec), e.dsum + rec, px, dcls, s_dev);
+                const int64_t tot = total_fb(cfg, bk, s_dev, dm, mag, g, pf);
                 topk_ins<K>(top, st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)));
                 continue;
             }
@@ -488,6 +541,13 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
         else KG_EXT_ST(false, false, false);
     }
 #undef KG_EXT_ST
+    return hipGetLastError();
+}
+
+hipError_t launch_dev_sum(const NodeRec* nodes, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
+                          DevSum* out, hipStream_t s) {
+    if (n_nodes == 0) return hipSuccess;
+    k_dev_sum<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, devs, n_nodes, cls, n_cls, out);
     return hipGetLastError();
 }
 

@@ -110,6 +110,8 @@ hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t 
                             const uint32_t* pmap, uint32_t* pstat, hipStream_t s);
 hipError_t launch_big_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t* big_list, uint32_t* big_count,
                            hipStream_t s);
+hipError_t launch_dev_sum(const NodeRec* nodes, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
+                          DevSum* out, hipStream_t s);
 hipError_t launch_scatter_rows(const void* stage, const uint32_t* pos, uint32_t n, bool dev, NodeRec* nodes,
                                ZoneRec* zones, DevRec* devs, hipStream_t s);
 hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, uint32_t n_pods,

@@ -242,6 +242,7 @@ struct PodsDev {
     const int64_t* la_est0;
     const int64_t* la_est1;
     const uint32_t* flags;
+    const uint8_t* dev_cls;     // GPU request class of the pod (DevSum.fit nibble), DEV_CLASSES = none
 };
 
 // Scoring / filtering configuration passed by value to every kernel.
@@ -270,6 +271,21 @@ constexpr int DEV_MINORS = 8, DEV_R = 3;
 struct alignas(64) DevRec {
     int64_t total[DEV_R][DEV_MINORS];
     int64_t free_[DEV_R][DEV_MINORS];
+};
+
+// Per-(pod batch, node record) DeviceShare summary (k_dev_sum): the pod batch's distinct GPU requests
+// (at most DEV_CLASSES, host-assigned per pod) each get a nibble of `fit` holding the number of the
+// record's minors that fit one instance (defaultAllocateDevices' predicate), and the minor sums the
+// node Score reads, so that the config-5 fast path does not walk the minors per pair.
+constexpr int DEV_CLASSES = 15;
+struct DevClass {
+    int64_t dreq[DEV_R];
+    uint32_t dkeys, pad_;
+};
+struct alignas(16) DevSum {
+    uint64_t fit;
+    int64_t T[DEV_R], F[DEV_R];
+    double rcp[DEV_R];  // 1 / T (least_req's exact-quotient path)
 };
 
 constexpr int QUOTA_R = 4;
@@ -314,6 +330,7 @@ struct ExtDev {
     const RsvInfo* infos;
     const uint32_t* cls_begin;     // [RSV_MAX_CLASSES + 1] view range per class
     const DevRec* rdev;            // GPU restore tables of views / reservations (kg_rsv_dev)
+    const DevSum* dsum;            // [record] of the current pod batch (fast-base select / stats only)
 };
 
 }  // namespace kg

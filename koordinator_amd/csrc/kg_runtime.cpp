@@ -120,6 +120,12 @@ struct kg_pods {
     uint32_t k_last = 0, kk_last = 0;
     uint32_t* d_pstat = nullptr;   // per pod: KG_ST_UNSUPPORTED / KG_ST_QUOTA of the last select (kg_result_status)
     uint32_t* d_reason = nullptr;  // replay: per pod OR of the filter status bits (kg_replay out_reason)
+    // GPU request classes of the batch (DevSum nibbles) and the per-record DevSum of the last config-5 select
+    uint8_t* d_dcls = nullptr;
+    DevClass* d_dclass = nullptr;
+    uint32_t n_dclass = 0;
+    DevSum* d_devsum = nullptr;
+    size_t devsum_cap = 0;
     // replay / shard scratch
     uint64_t* d_winners = nullptr;
     uint32_t* d_step = nullptr;
@@ -922,7 +928,9 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_xlist, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
               hipMalloc(&p->d_pstat, sizeof(uint32_t) * capacity) == hipSuccess &&
-              hipMalloc(&p->d_reason, sizeof(uint32_t) * (capacity + 1)) == hipSuccess;
+              hipMalloc(&p->d_reason, sizeof(uint32_t) * (capacity + 1)) == hipSuccess &&
+              hipMalloc(&p->d_dcls, capacity) == hipSuccess &&
+              hipMalloc(&p->d_dclass, sizeof(DevClass) * DEV_CLASSES) == hipSuccess;
     if (!ok) {
         hipFree(p->d_cols);
         hipFree(p->d_flags);
@@ -932,7 +940,8 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
         for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst,
                         (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors,
                         (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_pcols, (void*)p->d_pflags,
-                        (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys, (void*)p->d_pstat, (void*)p->d_reason})
+                        (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys, (void*)p->d_pstat, (void*)p->d_reason,
+                        (void*)p->d_dcls, (void*)p->d_dclass})
             hipFree(b);
         delete p;
         return fail(ctx, KG_OOM, "pod batch of %u", capacity);
@@ -954,6 +963,7 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
     p->dev.quota = (const int32_t*)(p->d_xcols + 2 * (size_t)capacity);
     p->dev.quota_keys = p->d_xcols + 3 * (size_t)capacity;
     p->dev.rsv_class = (const int32_t*)(p->d_xcols + 4 * (size_t)capacity);
+    p->dev.dev_cls = p->d_dcls;
     int64_t* pc = p->d_pcols;
     p->plain.req_cpu = pc + 0 * (size_t)capacity;
     p->plain.req_mem = pc + 1 * (size_t)capacity;
@@ -998,6 +1008,8 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     std::vector<int64_t> dreq((size_t)DEV_R * std::max<uint32_t>(n, 1), 0);
     std::vector<uint32_t> xc((size_t)5 * std::max<uint32_t>(n, 1), 0);
     std::vector<uint32_t> stat, pmap, xlist;
+    std::vector<uint8_t> dcls(std::max<uint32_t>(n, 1), (uint8_t)DEV_CLASSES);
+    std::vector<DevClass> classes;
     for (uint32_t j = 0; j < n; j++) {
         const uint32_t cnt = cols->dev_count ? cols->dev_count[j] : 0u;
         const uint32_t keys = cols->dev_keys ? cols->dev_keys[j] : 0u;
@@ -1005,6 +1017,17 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             const int64_t v = cols->dev_req ? cols->dev_req[(size_t)j * DEV_R + r] : 0;
             if (v < 0) return fail(ctx, KG_INVALID_ARG, "pod %u: negative GPU request", j);
             dreq[(size_t)j * DEV_R + r] = v;
+        }
+        if (cnt > 0) {  // GPU request class: the per-instance request the minor predicate reads
+            DevClass c{};
+            c.dkeys = keys & 7u;
+            for (int r = 0; r < DEV_R; r++) c.dreq[r] = ((c.dkeys >> r) & 1u) ? dreq[(size_t)j * DEV_R + r] : 0;
+            size_t k = 0;
+            while (k < classes.size() && !(classes[k].dkeys == c.dkeys && classes[k].dreq[0] == c.dreq[0] &&
+                                           classes[k].dreq[1] == c.dreq[1] && classes[k].dreq[2] == c.dreq[2]))
+                k++;
+            if (k == classes.size() && classes.size() < (size_t)DEV_CLASSES) classes.push_back(c);
+            if (k < classes.size()) dcls[j] = (uint8_t)k;
         }
         const int32_t q = cols->quota ? cols->quota[j] : -1;
         const int32_t cls = cols->rsv_class ? cols->rsv_class[j] : -1;
@@ -1062,6 +1085,11 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         HIP_TRY(ctx, hipMemcpyAsync(p->d_cols + (size_t)c * p->cap, h.data() + (size_t)c * n, sizeof(int64_t) * n,
                                     hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(p->d_flags, f.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(p->d_dcls, dcls.data(), n, hipMemcpyHostToDevice, ctx->stream));
+    if (!classes.empty())
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_dclass, classes.data(), sizeof(DevClass) * classes.size(), hipMemcpyHostToDevice,
+                                    ctx->stream));
+    p->n_dclass = (uint32_t)classes.size();
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     p->n = n;
     return KG_OK;
@@ -1081,7 +1109,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst, (void*)p->d_dev_max,
                     (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout,
                     (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys,
-                    (void*)p->d_pstat, (void*)p->d_reason})
+                    (void*)p->d_pstat, (void*)p->d_reason, (void*)p->d_dcls, (void*)p->d_dclass, (void*)p->d_devsum})
         hipFree(b);
     hipFree(p->d_rbpart);
     hipFree(p->d_rbtops);
@@ -1211,9 +1239,29 @@ static bool ext_fast_base(const kg_snap* s, const kg_pods* p) {
 }
 
 // config-5 matrix mode, pass 1: quota gate + per-pod NormalizeScore inputs of this shard
+// The batch's DevSum table over this snapshot's records (fast-base config-5 select with DeviceShare).
+static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
+    kg_ctx* ctx = s->ctx;
+    e.dsum = nullptr;
+    if (!s->d_dev || !ext_fast_base(s, p)) return KG_OK;
+    if (p->devsum_cap < s->n) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(p->d_devsum));
+        p->d_devsum = nullptr;
+        p->devsum_cap = 0;
+        HIP_TRY(ctx, hipMalloc(&p->d_devsum, sizeof(DevSum) * std::max<uint32_t>(s->n, 1)));
+        p->devsum_cap = s->n;
+    }
+    HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_dev, s->n, p->d_dclass, p->n_dclass, p->d_devsum, ctx->stream));
+    e.dsum = p->d_devsum;
+    return KG_OK;
+}
+
 static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     kg_ctx* ctx = s->ctx;
-    const ExtDev e = s->ext_dev();
+    ExtDev e = s->ext_dev();
+    kg_status dst = ext_dev_sum(s, p, e);
+    if (dst != KG_OK) return dst;
     HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, p->d_pstat, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_dev_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
@@ -1287,8 +1335,10 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
+    ExtDev xe = s->ext_dev();
+    xe.dsum = (s->d_dev && ext_fast_base(s, p)) ? p->d_devsum : nullptr;  // ext_stats_local built it for this batch
     if (n_x)
-        HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, s->ext_dev(), p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
+        HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
                                        s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
                                        p->d_pref, p->d_partial, p->d_pstat, ctx->stream));
     if (fparts || a.fused) HIP_TRY(ctx, launch_select(a, ctx->stream));
