@@ -30,10 +30,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E peak B/s (MI355X_MICROARCH.md, chip-level parameters)
-# VALU issue peak in wave-instructions/s: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
-# instruction (MI355X_MICROARCH.md § Wave scheduling); float64 ops issue over 4 cycles, so a frac
-# computed against this peak is a lower bound on the VALU pipe's utilisation.
-VALU_PEAK = 256 * 4 * 2.4e9 / 2
+# VALU issue: 256 CUs x 4 SIMDs at 2.4 GHz. A wave64 instruction holds its SIMD for 2 cycles when it is
+# f32 arithmetic and 4 cycles when it is f64, 64-bit or 32-bit integer, a compare, a conversion or a
+# v_cndmask (chip-wide measurement, tools/ubench_valu.hip -> profiles/r2/ubench_valu.txt); the select
+# kernels' loops are ~95 % of the latter, so the peak is priced per kernel from its ISA mix (roofline).
+SIMD_CYCLES = 256 * 4 * 2.4e9
+VALU_PEAK = SIMD_CYCLES / 2  # the all-f32 ceiling, for reference
 # SALU issue peak: one scalar instruction per cycle per CU.
 SALU_PEAK = 256 * 2.4e9
 # Algorithmic bytes per (pod, node) eval, SURVEY.md §8d (scan model, node row read once per eval):
@@ -131,8 +133,28 @@ def roofline(pmc, kernel_s, evals_per_launch, b_eval, kernel_name):
     salu = pmc.get("salu_insts_per_launch")
     hbm = pmc.get("hbm_bytes_per_launch")
     if valu:
+        # price each kernel's VALU count with its loop's issue cost (profiles/valu_mix.json: 2 cycles per f32
+        # wave64 instruction, 4 for f64 / integer / compare / convert, measured by tools/ubench_valu.hip)
+        mix = load_pmc("valu_mix.json")
+        cyc = None
+        if mix:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            from valu_mix import canon_demangled
+
+            cyc = 0.0
+            for name, k in (pmc.get("kernels") or {}).items():
+                v = (k.get("counters") or {}).get("SQ_INSTS_VALU", 0.0)
+                m = mix["kernels"].get(canon_demangled(name) or "")
+                cyc += v * (m["cyc_per_valu"] if m else 4.0)
+        cpi = cyc / valu if cyc else 4.0
+        peak = SIMD_CYCLES / cpi
         out["achieved"] = valu / kernel_s / 1e12
-        out["frac"] = valu / kernel_s / VALU_PEAK
+        out["peak"] = peak / 1e12
+        out["frac"] = valu / kernel_s / peak
+        out["issue_model"] = {"cycles_per_valu": cpi, "simd_cycles_per_s": SIMD_CYCLES,
+                              "source": "profiles/valu_mix.json (ISA mix) x profiles/r2/ubench_valu.txt (costs)"
+                                        if mix else "4 cycles per VALU (no ISA mix for these sources)",
+                              "frac_at_2_cycles": valu / kernel_s / (SIMD_CYCLES / 2)}
     if salu:
         out["salu"] = {"achieved": salu / kernel_s / 1e12, "peak": SALU_PEAK / 1e12, "unit": "T inst/s",
                        "frac": salu / kernel_s / SALU_PEAK}

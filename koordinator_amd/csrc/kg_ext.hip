@@ -74,6 +74,16 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
     out[rec] = o;
 }
 
+// Records the fast-base kernels (PART 1) take for no pod: F_BIG or storage class 1. special[0] = count,
+// special[1..] = records (any order: keys are order-free).
+__global__ __launch_bounds__(256) void k_special_scan(const NodeRec* __restrict__ nodes, uint32_t n_nodes, uint32_t n0,
+                                                      uint32_t* __restrict__ special) {
+    const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
+    if (rec >= n_nodes) return;
+    const int64_t* n = nodes[rec].v;
+    if (rec >= n0 || ((uint32_t)n[N_FLAGS] & F_BIG)) special[1 + atomicAdd(special, 1u)] = rec;
+}
+
 // Weighted total of a fast-base pair (FB paths): base total from the fast block + the normalised
 // DeviceShare term + the Reservation term, which off a view is 0 or the preferred node's 100 (total_ext
 // with s_rsv = 0). mag = ceil(2^32 / dev_max) for dev_max >= 2: floor(s * 100 / dev_max) exactly for
@@ -163,7 +173,9 @@ __global__ __launch_bounds__(256) void k_ext_verify_fin(uint32_t n_pods, uint32_
 
 // Pass 1: per-pod NormalizeScore inputs over the feasible nodes of records [lo, hi) of chunk blockIdx.y.
 // FB: base-plugin feasibility from the fast block where k_ext_select<FB> takes it (same conditions).
-template <bool EXACT, bool TOPO, bool FB>
+// PART (FB launches split the records so that the fast kernel stays small): 1 = the fast-base records
+// only (the others are k_ext_stats_sp's), 0 = all records.
+template <bool EXACT, bool TOPO, bool FB, int PART = 0>
 __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                    ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
                                                    uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
@@ -193,27 +205,86 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
             const uint32_t fl = (uint32_t)n[N_FLAGS];
             const bool view = (cfg.plugins & KG_PLUGIN_RSV) && px.cls >= 0 && px.cls < RSV_MAX_CLASSES &&
                               (((uint64_t)n[N_RSV_CLASSES] >> px.cls) & 1ull);
-            if (rec < n0 && !(fl & F_BIG) && !view) {
+            const bool fbrec = rec < n0 && !(fl & F_BIG) && !view;
+            if (fbrec) {
                 // no view: Reservation score and order are 0, only the DeviceShare maximum can move
-                if (!(cfg.plugins & KG_PLUGIN_DEV) || px.dcount == 0) continue;
-                const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
-                const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
-                int64_t raw = 0;
-                uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
-                if (!st) st |= dev_eval_sum(cfg, n, dev_of(e, rec), e.dsum + rec, px, dcls, raw);
-                if (!st) dmax = max(dmax, (uint32_t)raw);
+                uint32_t pv = 0;
+                if ((cfg.plugins & KG_PLUGIN_DEV) && px.dcount != 0) {
+                    const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
+                    const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
+                    int64_t raw = 0;
+                    uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
+                    if (!st) st |= dev_eval_sum(cfg, n, dev_of(e, rec), e.dsum + rec, px, dcls, raw);
+                    if (!st) dmax = max(dmax, (uint32_t)raw);
+                    pv = 0x80000000u | (st ? 0u : (0x40000000u | ((uint32_t)(bk >> 32) << 7) | (uint32_t)raw));
+                }
+                if (e.pairs && live) e.pairs[(size_t)rec * e.pairs_ld + t] = pv;
                 continue;
             }
+            if (e.pairs && live) e.pairs[(size_t)rec * e.pairs_ld + t] = 0u;
         }
-        const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
-        if (r.status) continue;
+        if constexpr (PART != 1) {
+            const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
+            if (r.status) continue;
+            dmax = max(dmax, (uint32_t)r.s_dev);
+            rmax = max(rmax, (uint32_t)r.s_rsv);
+            if (r.order != 0) {
+                const uint64_t k = pref_key(r.order, index_base + node_index(nodes[rec]));
+                pk = k < pk ? k : pk;
+            }
+        }
+    }
+    if (!live) return;
+    if (dmax) atomicMax(dev_max + j, dmax);
+    if (rmax) atomicMax(rsv_max + j, rmax);
+    if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
+}
+
+// The records a fast-base pass leaves to the general path for lane t: the special records (F_BIG, class
+// 1; grid-stride over chunks of `chunk`) for every lane, then the views of the lane's reservation class
+// that are not special. fn(rec) evaluates one pair.
+template <typename Fn>
+__device__ __forceinline__ void for_general_records(const NodeRec* __restrict__ nodes, const ExtDev& e,
+                                                    const uint32_t* __restrict__ special, uint32_t n0, uint32_t chunk,
+                                                    int32_t cls, Fn&& fn) {
+    const uint32_t nsp = special[0], step = gridDim.y * chunk;
+    for (uint32_t x = blockIdx.y * chunk; x < nsp; x += step)
+        for (uint32_t y = x, ye = min(x + chunk, nsp); y < ye; y++) fn(special[1 + y]);
+    if (cls < 0 || cls >= RSV_MAX_CLASSES || !e.cls_begin) return;
+    const uint32_t cb = e.cls_begin[cls], ce = e.cls_begin[cls + 1];
+    for (uint32_t x = cb + blockIdx.y * chunk; x < ce; x += step)
+        for (uint32_t v = x, ve = min(x + chunk, ce); v < ve; v++) {
+            const uint32_t rec = e.views[v].rec;
+            if (rec >= n0 || ((uint32_t)nodes[rec].v[N_FLAGS] & F_BIG)) continue;  // special: done above
+            fn(rec);
+        }
+}
+
+// Pass 1, general records of a fast-base launch (the complement of k_ext_stats<.., 1>).
+__global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                      ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
+                                                      uint32_t n_list, uint32_t n0, uint32_t chunk, uint32_t index_base,
+                                                      KCfg cfg, const uint32_t* __restrict__ qst,
+                                                      uint32_t* __restrict__ dev_max, uint32_t* __restrict__ rsv_max,
+                                                      uint64_t* __restrict__ pref, const uint32_t* __restrict__ special) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = t < n_list;
+    const uint32_t j = live ? list[t] : 0;
+    const PodV p = load_pod(pods, j);
+    const PodX px = load_podx(pods, j);
+    const uint32_t q = live ? qst[j] : 1u;
+    uint32_t dmax = 0, rmax = 0;
+    uint64_t pk = PREF_NONE;
+    for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, [&](uint32_t rec) {
+        const PairX r = eval_pair_ext<false, false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        if (r.status) return;
         dmax = max(dmax, (uint32_t)r.s_dev);
         rmax = max(rmax, (uint32_t)r.s_rsv);
         if (r.order != 0) {
             const uint64_t k = pref_key(r.order, index_base + node_index(nodes[rec]));
             pk = k < pk ? k : pk;
         }
-    }
+    });
     if (!live) return;
     if (dmax) atomicMax(dev_max + j, dmax);
     if (rmax) atomicMax(rsv_max + j, rmax);
@@ -272,7 +343,7 @@ __device__ __forceinline__ void topk_ins(uint64_t (&top)[K], uint64_t key) {
 // / NodeNUMAResource part of the pair comes from the fast block (eval_fast_key, the base select's
 // arithmetic: same feasibility and weighted total as eval_pair), and only DeviceShare, the
 // reservation-affinity check and the normalised terms are evaluated on top.
-template <int K, bool EXACT, bool TOPO, bool FB>
+template <int K, bool EXACT, bool TOPO, bool FB, int PART = 0>
 __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                     ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
                                                     uint32_t n_pods, uint32_t n_nodes, uint32_t n0,
@@ -302,6 +373,7 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
     const uint32_t dcls = pods.dev_cls ? pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
     const uint32_t mag = norm_magic(dm);
+    const int64_t prow = (FB && e.pairs && live && j >= e.pairs_row0) ? (int64_t)(j - e.pairs_row0) : -1;
     // pairs that need the host path: a cpuset-binding pod under NodeNUMAResource has one on every node
     // (numa_eval), whatever path the record takes; FB records (class 0, not F_BIG: NUMA policy None) have
     // no other source
@@ -313,7 +385,19 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
             const uint32_t fl = (uint32_t)n[N_FLAGS];
             const bool view = (cfg.plugins & KG_PLUGIN_RSV) && px.cls >= 0 && px.cls < RSV_MAX_CLASSES &&
                               (((uint64_t)n[N_RSV_CLASSES] >> px.cls) & 1ull);
-            if (rec < n0 && !(fl & F_BIG) && !view) {
+            const bool fbrec = rec < n0 && !(fl & F_BIG) && !view;
+            if (PART == 1 && !fbrec) continue;
+            if (fbrec) {
+                if (prow >= 0) {  // pass 1 evaluated this pair: only the normalised terms are added
+                    const uint32_t pv = e.pairs[(size_t)rec * e.pairs_ld + prow];
+                    if (pv & 0x80000000u) {
+                        const uint32_t g = index_base + (uint32_t)((uint64_t)n[N_FLAGS] >> 32);
+                        const int64_t tot = total_fb(cfg, (uint64_t)((pv >> 7) & 0x7FFFFFu) << 32, (int64_t)(pv & 127u),
+                                                     dm, mag, g, pf);
+                        topk_ins<K>(top, (pv & 0x40000000u) ? (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)) : 0ull);
+                        continue;
+                    }
+                }
                 const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
                 const uint32_t g = index_base + (uint32_t)((uint64_t)fr.flags >> 32);
                 const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, g);
@@ -326,14 +410,55 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
                 continue;
             }
         }
-        const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
+        if constexpr (PART != 1) {
+            const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
+            unsup |= r.status & KG_ST_UNSUPPORTED;
+            const uint32_t g = index_base + node_index(nodes[rec]);
+            const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
+            topk_ins<K>(top, r.status ? 0ull : key);
+        }
+    }
+    if (live) {
+        uint64_t* dst = partial + ((size_t)blockIdx.y * n_pods + j) * K;
+#pragma unroll
+        for (int t = 0; t < K; t++) dst[t] = top[t];
+        if (unsup) atomicOr(pstat + jj, unsup);
+    }
+}
+
+// Pass 2, general records of a fast-base launch (the complement of k_ext_select<.., 1>): partials of
+// chunk blockIdx.y go after the fast kernel's (part_off).
+template <int K>
+__global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                       ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
+                                                       uint32_t n_pods, uint32_t n0, uint32_t chunk, uint32_t index_base,
+                                                       KCfg cfg, const uint32_t* __restrict__ qst,
+                                                       const uint32_t* __restrict__ dev_max,
+                                                       const uint32_t* __restrict__ rsv_max,
+                                                       const uint64_t* __restrict__ pref, uint64_t* __restrict__ partial,
+                                                       uint32_t* __restrict__ pstat, const uint32_t* __restrict__ special,
+                                                       uint32_t part_off) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = j < n_pods;
+    const uint32_t jj = live ? (list ? list[j] : j) : 0;
+    const PodV p = load_pod(pods, jj);
+    const PodX px = load_podx(pods, jj);
+    const uint32_t q = live ? qst[jj] : 1u;
+    const uint32_t dm = dev_max[jj], rm = rsv_max[jj];
+    const uint64_t pf = pref[jj];
+    uint64_t top[K];
+#pragma unroll
+    for (int t = 0; t < K; t++) top[t] = 0;
+    uint32_t unsup = 0;
+    for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, [&](uint32_t rec) {
+        const PairX r = eval_pair_ext<false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
         unsup |= r.status & KG_ST_UNSUPPORTED;
         const uint32_t g = index_base + node_index(nodes[rec]);
         const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
         topk_ins<K>(top, r.status ? 0ull : key);
-    }
+    });
     if (live) {
-        uint64_t* dst = partial + ((size_t)blockIdx.y * n_pods + j) * K;
+        uint64_t* dst = partial + (((size_t)blockIdx.y + part_off) * n_pods + j) * K;
 #pragma unroll
         for (int t = 0; t < K; t++) dst[t] = top[t];
         if (unsup) atomicOr(pstat + jj, unsup);
@@ -525,14 +650,19 @@ hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const E
 hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                             const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
-                            uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, hipStream_t s) {
+                            uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, const uint32_t* special,
+                            uint32_t special_est, hipStream_t s) {
     if (n_list == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_list + 255) / 256, (n_nodes + chunk - 1) / chunk);
-#define KG_EXT_ST(EX, TP, F)                                                                                       \
-    k_ext_stats<EX, TP, F><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, n0, chunk, index_base, cfg, \
+    uint32_t chunk2, y2;
+    ext_part2_grid(special_est, grid.x, &chunk2, &y2);
+#define KG_EXT_ST(EX, TP, F, ...)                                                                                  \
+    k_ext_stats<EX, TP, F, ##__VA_ARGS__><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, n0, chunk, index_base, cfg, \
                                                 qst, dev_max, rsv_max, pref)
     if (fb) {
-        KG_EXT_ST(false, false, true);
+        KG_EXT_ST(false, false, true, 1);
+        k_ext_stats_sp<<<dim3(grid.x, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n0, chunk2, index_base, cfg,
+                                                        qst, dev_max, rsv_max, pref, special);
     } else if (exact) {
         if (topo) KG_EXT_ST(true, true, false);
         else KG_EXT_ST(true, false, false);
@@ -541,6 +671,13 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
         else KG_EXT_ST(false, false, false);
     }
 #undef KG_EXT_ST
+    return hipGetLastError();
+}
+
+hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(special, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n_nodes == 0) return e;
+    k_special_scan<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, n_nodes, n0, special);
     return hipGetLastError();
 }
 
@@ -588,15 +725,20 @@ hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const E
                              const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                              uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
                              const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
-                             hipStream_t s) {
+                             const uint32_t* special, uint32_t special_est, hipStream_t s) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_pods + 255) / 256, (n_nodes + chunk - 1) / chunk);
-#define KG_EXT_SEL(KK, EX, TP, F)                                                                            \
-    k_ext_select<KK, EX, TP, F><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n_nodes, n0, chunk, index_base, \
+    const uint32_t y1 = grid.y;
+    uint32_t chunk2, y2;
+    ext_part2_grid(special_est, grid.x, &chunk2, &y2);
+#define KG_EXT_SEL(KK, EX, TP, F, ...)                                                                       \
+    k_ext_select<KK, EX, TP, F, ##__VA_ARGS__><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n_nodes, n0, chunk, index_base, \
                                                      cfg, qst, dev_max, rsv_max, pref, partial, pstat)
 #define KG_EXT_SEL_K(KK)                              \
     if (fb) {                                         \
-        KG_EXT_SEL(KK, false, false, true);           \
+        KG_EXT_SEL(KK, false, false, true, 1);        \
+        k_ext_select_sp<KK><<<dim3(grid.x, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, \
+            index_base, cfg, qst, dev_max, rsv_max, pref, partial, pstat, special, y1); \
     } else if (exact) {                               \
         if (topo) KG_EXT_SEL(KK, true, true, false);  \
         else KG_EXT_SEL(KK, true, false, false);      \

@@ -80,7 +80,8 @@ hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const E
 hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                             const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
-                            uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, hipStream_t s);
+                            uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, const uint32_t* special,
+                            uint32_t special_est, hipStream_t s);
 hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                                   const uint32_t* list, uint32_t n_list, uint32_t max_views, uint32_t index_base,
                                   const KCfg& cfg, bool exact,
@@ -89,8 +90,8 @@ hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, co
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                              const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                              uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
-                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
-                             hipStream_t s);
+                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat, const uint32_t* special,
+                             uint32_t special_est, hipStream_t s);
 // out[map[t]] = rows t of src (k keys each); rows whose pod has a nonzero qst[pod] get zero keys and
 // pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the host path)
 hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, const uint32_t* qst,
@@ -110,6 +111,15 @@ hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t 
                             const uint32_t* pmap, uint32_t* pstat, hipStream_t s);
 hipError_t launch_big_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t* big_list, uint32_t* big_count,
                            hipStream_t s);
+// Grid of the PART 2 ext kernels (special records, grid-stride): chunk and chunk count for an estimate
+// of the special-record count and the pod blocks of the launch (~2048 workgroups in all).
+inline void ext_part2_grid(uint32_t special_est, uint32_t pod_blocks, uint32_t* chunk, uint32_t* n_chunks) {
+    const uint32_t want = pod_blocks ? (2048u + pod_blocks - 1) / pod_blocks : 1u;
+    const uint32_t est = special_est ? special_est : 1u;
+    *chunk = est / want < 4u ? 4u : (est + want - 1) / want;
+    *n_chunks = (est + *chunk - 1) / *chunk;
+}
+hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, hipStream_t s);
 hipError_t launch_dev_sum(const NodeRec* nodes, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
                           DevSum* out, hipStream_t s);
 hipError_t launch_scatter_rows(const void* stage, const uint32_t* pos, uint32_t n, bool dev, NodeRec* nodes,

@@ -331,6 +331,11 @@ struct ExtDev {
     const uint32_t* cls_begin;     // [RSV_MAX_CLASSES + 1] view range per class
     const DevRec* rdev;            // GPU restore tables of views / reservations (kg_rsv_dev)
     const DevSum* dsum;            // [record] of the current pod batch (fast-base select / stats only)
+    // Pair results of pass 1 kept for pass 2 (fast-base records of the GPU pods): [record][pairs_ld], lane
+    // row t of the stats list; bit 31 stored, bit 30 feasible, bits 7..29 base total, bits 0..6 DeviceShare
+    // raw score. pairs_row0: select-list row of stats row 0. nullptr = pass 2 evaluates every pair.
+    uint32_t* pairs;
+    uint32_t pairs_ld, pairs_row0;
 };
 
 }  // namespace kg

@@ -75,6 +75,10 @@ struct kg_snap {
     RsvInfo* d_infos = nullptr;
     uint32_t* d_cls_begin = nullptr;  // [RSV_MAX_CLASSES + 1]
     DevRec* d_rdev = nullptr;         // kg_rsv_dev tables
+    uint32_t* d_special = nullptr;    // [0] = count, [1..]: records the fast-base ext kernels leave to PART 2
+    uint32_t n_view_nodes = 0;        // nodes holding a reservation view
+    // PART 2 grid: the class-1 records and the largest reservation class's views (F_BIG records come on top)
+    uint32_t special_est() const { return std::max(n - n0, max_cls_views); }
     uint32_t n_views = 0;
     uint32_t max_cls_views = 0;  // views of the largest reservation class
     std::vector<kg_rsv_view> h_views;  // as uploaded (local snapshot indices)
@@ -126,6 +130,10 @@ struct kg_pods {
     uint32_t n_dclass = 0;
     DevSum* d_devsum = nullptr;
     size_t devsum_cap = 0;
+    // pass-1 pair results kept for pass 2 (ExtDev.pairs)
+    uint32_t* d_pairs = nullptr;
+    size_t pairs_cap = 0;  // entries
+    bool pairs_on = false;
     // replay / shard scratch
     uint64_t* d_winners = nullptr;
     uint32_t* d_step = nullptr;
@@ -893,6 +901,7 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_infos);
     hipFree(s->d_cls_begin);
     hipFree(s->d_rdev);
+    hipFree(s->d_special);
     hipFree(s->d_stage);
     hipFree(s->d_stage_pos);
     delete s;
@@ -1109,7 +1118,8 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst, (void*)p->d_dev_max,
                     (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout,
                     (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys,
-                    (void*)p->d_pstat, (void*)p->d_reason, (void*)p->d_dcls, (void*)p->d_dclass, (void*)p->d_devsum})
+                    (void*)p->d_pstat, (void*)p->d_reason, (void*)p->d_dcls, (void*)p->d_dclass, (void*)p->d_devsum,
+                    (void*)p->d_pairs})
         hipFree(b);
     hipFree(p->d_rbpart);
     hipFree(p->d_rbtops);
@@ -1257,11 +1267,50 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     return KG_OK;
 }
 
+// Pass 1 keeps each fast-base pair of the GPU pods (base total, feasibility, DeviceShare raw score) for
+// pass 2 when the weighted base total fits 23 bits and the table fits the budget (KG_PAIRS_GB, default 16).
+static kg_status ext_pairs(kg_snap* s, kg_pods* p, ExtDev& e) {
+    kg_ctx* ctx = s->ctx;
+    e.pairs = nullptr;
+    e.pairs_ld = e.pairs_row0 = 0;
+    p->pairs_on = false;
+    const uint32_t ng = p->n_stat - p->n_stat_cls;
+    const KCfg& c = s->kcfg;
+    if (!e.dsum || ng == 0 || 100ll * ((int64_t)c.w_nrf + c.w_la + c.w_numa) >= (1ll << 23)) return KG_OK;
+    const char* env = std::getenv("KG_PAIRS_GB");
+    const double budget = (env ? std::atof(env) : 16.0) * 1e9;
+    const uint32_t ld = (ng + 63u) & ~63u;
+    const size_t need = (size_t)ld * s->n;
+    if ((double)need * sizeof(uint32_t) > budget) return KG_OK;
+    if (need > p->pairs_cap) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(p->d_pairs));
+        p->d_pairs = nullptr;
+        p->pairs_cap = 0;
+        if (hipMalloc(&p->d_pairs, sizeof(uint32_t) * need) != hipSuccess) {
+            (void)hipGetLastError();
+            return KG_OK;  // no room: pass 2 evaluates every pair
+        }
+        p->pairs_cap = need;
+    }
+    e.pairs = p->d_pairs;
+    e.pairs_ld = ld;
+    e.pairs_row0 = p->n_x - ng;  // GPU pods close both lists in the same order (kg_pods_upload)
+    p->pairs_on = true;
+    return KG_OK;
+}
+
 static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     kg_ctx* ctx = s->ctx;
     ExtDev e = s->ext_dev();
     kg_status dst = ext_dev_sum(s, p, e);
     if (dst != KG_OK) return dst;
+    dst = ext_pairs(s, p, e);
+    if (dst != KG_OK) return dst;
+    if (ext_fast_base(s, p)) {  // records for the PART 2 kernels (pass 1 and pass 2 of this batch)
+        if (!s->d_special) HIP_TRY(ctx, hipMalloc(&s->d_special, sizeof(uint32_t) * ((size_t)s->n + 1)));
+        HIP_TRY(ctx, launch_special_scan(s->d_nodes, s->n, s->n0, s->d_special, ctx->stream));
+    }
     HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, p->d_pstat, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_dev_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
@@ -1278,7 +1327,7 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
         const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(ng, 1), 8192);
         HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, s->n0, chunk, s->base,
                                       s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
-                                      ctx->stream));
+                                      s->d_special, s->special_est(), ctx->stream));
     }
     return KG_OK;
 }
@@ -1295,7 +1344,13 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     const uint32_t n_x = split ? p->n_x : p->n;
     const uint32_t* xl = split ? p->d_xlist : nullptr;
     const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(n_x, 1), 8192);
-    const uint32_t xparts = n_x ? (s->n + chunk - 1) / chunk : 0;
+    // a fast-base launch writes the fast-record kernel's chunks, then the special-record kernel's
+    uint32_t xparts = n_x ? (s->n + chunk - 1) / chunk : 0;
+    if (n_x && ext_fast_base(s, p)) {
+        uint32_t c2, y2;
+        ext_part2_grid(s->special_est(), (n_x + 255) / 256, &c2, &y2);
+        xparts += y2;
+    }
     const uint32_t n_plain = split ? p->n_plain : 0;
     LaunchSelect a{};
     uint32_t fparts = 0;
@@ -1337,10 +1392,15 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     if (st != KG_OK) return st;
     ExtDev xe = s->ext_dev();
     xe.dsum = (s->d_dev && ext_fast_base(s, p)) ? p->d_devsum : nullptr;  // ext_stats_local built it for this batch
+    if (p->pairs_on && xe.dsum) {  // and the pass-1 pair table
+        xe.pairs = p->d_pairs;
+        xe.pairs_ld = (p->n_stat - p->n_stat_cls + 63u) & ~63u;
+        xe.pairs_row0 = p->n_x - (p->n_stat - p->n_stat_cls);
+    }
     if (n_x)
         HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
                                        s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
-                                       p->d_pref, p->d_partial, p->d_pstat, ctx->stream));
+                                       p->d_pref, p->d_partial, p->d_pstat, s->d_special, s->special_est(), ctx->stream));
     if (fparts || a.fused) HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
@@ -1963,6 +2023,8 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
     HIP_TRY(ctx, hipMemcpyAsync(s->d_cls_begin, cb.data(), sizeof(uint32_t) * cb.size(), hipMemcpyHostToDevice, ctx->stream));
     // class masks into slot N_RSV_CLASSES of every record (a strided 8-byte column copy)
     s->cls_mask = mask;
+    s->n_view_nodes = 0;
+    for (uint32_t i = 0; i < s->n; i++) s->n_view_nodes += mask[i] != 0;
     std::vector<int64_t> col(s->n);
     for (uint32_t i = 0; i < s->n; i++) {
         col[s->pos[i]] = (int64_t)mask[i];
