@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 4
+#define KG_ABI_VERSION 5
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -406,6 +406,33 @@ kg_status kg_forget_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t nod
                         uint32_t minors);
 /* GPU minors chosen for each pod by the last kg_replay (bitmask; 0 = none), n_pods entries. */
 kg_status kg_replay_minors(kg_pods* pods, uint32_t* out);
+
+/* ---- whole-job placement (FindOneNodePlugin slot, frameworkext/interface.go:118-127) ----------------
+ * Checkpoint / rollback of everything Reserve changes (node records, NUMA zones, GPU minors, quota used):
+ * a planner replays the job on the live snapshot and rolls back, so the plan costs no copy of the cluster
+ * (the reference clones NodeInfos per plan, coscheduling/core/network_topology_workflow.go:98-118). One
+ * checkpoint per snapshot; a new checkpoint replaces the old. Rollback fails if the snapshot was re-uploaded
+ * or had rows updated since the checkpoint (its records may have moved). Both bump the generation. */
+kg_status kg_snapshot_checkpoint(kg_snap* snap);
+kg_status kg_snapshot_rollback(kg_snap* snap);
+
+/* kg_batch_schedule result codes, per pod */
+#define KG_BATCH_ASSUMED 0u     /* PreFilter + Filter passed on the planned node; Reserve applied          */
+#define KG_BATCH_FAILED 1u      /* PreFilter / Filter failed on the planned node: status holds the bits    */
+#define KG_BATCH_SIBLING 2u     /* after a failed pod of the same node (engine.go:188-192): its status     */
+#define KG_BATCH_ROLLED_BACK 3u /* was assumed, undone because the job failed (CleanupAssumedPods)         */
+#define KG_BATCH_NO_PLAN 4u     /* plan_node < 0: the job fails before any pod is assumed (batch_scheduler.go:96-101) */
+/* Inline batch scheduling cycle for a planned job (batch/batch_scheduler.go:74-185 BatchSchedule,
+ * batch/engine.go:92-294 RunSchedulingCycle): plan_node[j] = local node of pod j. Pods are grouped by
+ * planned node; each group runs in batch order (the caller orders a node's pods by name, engine.go
+ * :357-359): PreFilter (ElasticQuota gate on the current used) + Filter on that node, then Reserve. If every
+ * pod is assumed the state stays committed and the call returns KG_OK; otherwise every assumed pod is
+ * undone (result KG_BATCH_ROLLED_BACK, CleanupAssumedPods) and the call still returns KG_OK, the per-pod
+ * codes telling which pod failed and why. out_zone / out_minors (may be NULL): NUMA zone and GPU minors
+ * of each assumed pod. KG_UNSUPPORTED when some pair needs the host path (the state is rolled back) or
+ * when reservation views are uploaded (a Reserve into a view changes its restore). */
+kg_status kg_batch_schedule(kg_snap* snap, kg_pods* pods, const int32_t* plan_node, uint32_t* out_result,
+                            uint32_t* out_status, int32_t* out_zone, uint32_t* out_minors);
 
 /* Timing of the dominant kernel with HIP events on the launch stream. */
 kg_status kg_profile_enable(kg_ctx* ctx, int enable);

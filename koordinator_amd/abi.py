@@ -11,7 +11,7 @@ from typing import Dict
 
 import numpy as np
 
-KG_ABI_VERSION = 4
+KG_ABI_VERSION = 5
 KG_LA_R = 2
 KG_NSCALAR = 2
 KG_MAX_ZONES = 4
@@ -81,6 +81,8 @@ KG_ST_RSV_MASK = 0x1C000000
 KG_ST_QUOTA = 0x20000000
 KG_ST_DEV_RSV = 0x40000000  # "Reservation(s) Insufficient gpu devices"
 KG_ST_UNSUPPORTED = 0x80000000
+# kg_batch_schedule per-pod result codes
+KG_BATCH_ASSUMED, KG_BATCH_FAILED, KG_BATCH_SIBLING, KG_BATCH_ROLLED_BACK, KG_BATCH_NO_PLAN = range(5)
 
 _p64 = C.POINTER(C.c_int64)
 _pu32 = C.POINTER(C.c_uint32)

@@ -103,6 +103,11 @@ hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, 
 hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                              uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
                              bool exact, int32_t* out, hipStream_t s);
+// inline batch cycle of a whole-job plan (k_batch); ext = the snapshot carries the config-5 tables
+hipError_t launch_batch(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
+                        const uint32_t* grp_begin, const uint32_t* grp_pods, const uint32_t* grp_rec, uint32_t n_groups,
+                        bool ext, const KCfg& cfg, bool exact, uint32_t* result, uint32_t* status, int32_t* zone,
+                        uint32_t* minors, hipStream_t s);
 hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k, uint64_t* out,
                         hipStream_t s);
 hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k,

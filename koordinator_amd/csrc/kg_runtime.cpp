@@ -96,6 +96,17 @@ struct kg_snap {
     uint32_t* d_stage_pos = nullptr;
     size_t stage_cap = 0;  // rows
     std::vector<uint8_t> h_stage;
+    // Saved Reserve state: `ck` for kg_snapshot_checkpoint / rollback (planners), `bk` for the cleanup of a
+    // failed kg_batch_schedule. Invalidated by anything that may move records or replace tables.
+    struct Saved {
+        NodeRec* nodes = nullptr;
+        ZoneRec* zones = nullptr;
+        DevRec* dev = nullptr;
+        QuotaState* q = nullptr;
+        uint32_t nq = 0;
+        bool valid = false, views_stale = false;
+    } ck, bk;
+    void invalidate_saved() { ck.valid = bk.valid = false; }
     bool ext() const { return (cfg.plugins & KG_PLUGIN_EXT) != 0; }
     ExtDev ext_dev() const {
         ExtDev e{};
@@ -154,6 +165,7 @@ struct kg_pods {
     uint32_t* d_minors = nullptr;     // replay: GPU minors chosen per pod
     uint64_t* d_buckets = nullptr;    // replay: [3][128] per-score best keys
     int32_t* d_aout = nullptr;        // kg_assume_ext outputs
+    uint32_t* d_batch = nullptr;      // kg_batch_schedule: groups + per-pod outputs (7 x cap + 1 words)
     hipGraphExec_t xexec = nullptr;   // ext replay graph
     std::vector<uint8_t> xkey;
     // config-5 select split: "plain" pods (no GPU request, no reservation class or affinity) see only
@@ -743,6 +755,7 @@ kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->uploaded = true;
     s->gen++;
+    s->invalidate_saved();
     return KG_OK;
 }
 
@@ -832,6 +845,7 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->gen++;
+    s->invalidate_saved();
     return KG_OK;
 }
 
@@ -904,6 +918,12 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_special);
     hipFree(s->d_stage);
     hipFree(s->d_stage_pos);
+    for (kg_snap::Saved* k : {&s->ck, &s->bk}) {
+        hipFree(k->nodes);
+        hipFree(k->zones);
+        hipFree(k->dev);
+        hipFree(k->q);
+    }
     delete s;
     return KG_OK;
 }
@@ -1119,7 +1139,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
                     (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout,
                     (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys,
                     (void*)p->d_pstat, (void*)p->d_reason, (void*)p->d_dcls, (void*)p->d_dclass, (void*)p->d_devsum,
-                    (void*)p->d_pairs})
+                    (void*)p->d_pairs, (void*)p->d_batch})
         hipFree(b);
     hipFree(p->d_rbpart);
     hipFree(p->d_rbtops);
@@ -1875,6 +1895,170 @@ kg_status kg_forget_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int
     return assume_ext(s, p, pod, node, zone, minors, -1, nullptr, nullptr);
 }
 
+// ---- checkpoint / rollback and the inline batch cycle ------------------------------------------------
+
+static kg_status save_state(kg_snap* s, kg_snap::Saved& k) {
+    kg_ctx* ctx = s->ctx;
+    const size_t n = std::max<uint32_t>(s->n, 1);
+    if (!k.nodes) {
+        HIP_TRY(ctx, hipMalloc(&k.nodes, sizeof(NodeRec) * n));
+        HIP_TRY(ctx, hipMalloc(&k.zones, sizeof(ZoneRec) * n));
+        if (s->d_dev) HIP_TRY(ctx, hipMalloc(&k.dev, sizeof(DevRec) * n));
+    }
+    if (k.nq < s->n_quotas || (s->n_quotas && !k.q)) {
+        hipFree(k.q);
+        k.q = nullptr;
+        HIP_TRY(ctx, hipMalloc(&k.q, sizeof(QuotaState) * 2 * (size_t)s->n_quotas));
+    }
+    k.nq = s->n_quotas;
+    HIP_TRY(ctx, hipMemcpyAsync(k.nodes, s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(k.zones, s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
+    if (s->d_dev) HIP_TRY(ctx, hipMemcpyAsync(k.dev, s->d_dev, sizeof(DevRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
+    if (s->n_quotas && s->d_qstate)
+        HIP_TRY(ctx, hipMemcpyAsync(k.q, s->d_qstate, sizeof(QuotaState) * 2 * (size_t)s->n_quotas, hipMemcpyDeviceToDevice,
+                                    ctx->stream));
+    k.views_stale = s->views_stale;
+    k.valid = true;
+    return KG_OK;
+}
+
+static kg_status restore_state(kg_snap* s, kg_snap::Saved& k) {
+    kg_ctx* ctx = s->ctx;
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, k.nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, k.zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
+    if (s->d_dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, k.dev, sizeof(DevRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
+    if (k.nq && s->d_qstate)
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_qstate, k.q, sizeof(QuotaState) * 2 * (size_t)k.nq, hipMemcpyDeviceToDevice,
+                                    ctx->stream));
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
+    s->views_stale = k.views_stale;
+    s->gen++;
+    return KG_OK;
+}
+
+kg_status kg_snapshot_checkpoint(kg_snap* s) {
+    if (!s) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    kg_status st = save_state(s, s->ck);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    s->gen++;
+    return KG_OK;
+}
+
+kg_status kg_snapshot_rollback(kg_snap* s) {
+    if (!s) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!s->ck.valid)
+        return fail(ctx, KG_INVALID_ARG, "no checkpoint (none taken, or the snapshot / its tables were re-uploaded since)");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    kg_status st = restore_state(s, s->ck);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KG_OK;
+}
+
+kg_status kg_batch_schedule(kg_snap* s, kg_pods* p, const int32_t* plan_node, uint32_t* out_result, uint32_t* out_status,
+                            int32_t* out_zone, uint32_t* out_minors) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    if ((!plan_node || !out_result || !out_status) && p->n) return fail(ctx, KG_INVALID_ARG, "null plan / result buffer");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views)
+        return fail(ctx, KG_UNSUPPORTED, "batch schedule with Reservation views (a Reserve into a view changes its restore)");
+    if (s->ext()) {
+        st = check_ext(s);
+        if (st != KG_OK) return st;
+    }
+    const uint32_t n = p->n;
+    for (uint32_t j = 0; j < n; j++)
+        if (plan_node[j] >= (int32_t)s->n) return fail(ctx, KG_INVALID_ARG, "pod %u: planned node %d >= %u", j, plan_node[j], s->n);
+    auto set_all = [&](uint32_t code) {
+        for (uint32_t j = 0; j < n; j++) {
+            out_result[j] = code;
+            out_status[j] = 0;
+            if (out_zone) out_zone[j] = -1;
+            if (out_minors) out_minors[j] = 0;
+        }
+    };
+    for (uint32_t j = 0; j < n; j++)
+        if (plan_node[j] < 0) {  // "batch schedule plan missing node for pod": nothing is assumed
+            set_all(KG_BATCH_NO_PLAN);
+            return KG_OK;
+        }
+    if (n == 0) return KG_OK;
+    // podRequestsByNode: groups in order of first appearance, each in batch order
+    std::vector<uint32_t> gid(s->n, UINT32_MAX), begin, rec, count;
+    for (uint32_t j = 0; j < n; j++) {
+        uint32_t& x = gid[plan_node[j]];
+        if (x == UINT32_MAX) {
+            x = (uint32_t)rec.size();
+            rec.push_back(s->pos[plan_node[j]]);
+            count.push_back(0);
+        }
+        count[x]++;
+    }
+    const uint32_t G = (uint32_t)rec.size();
+    begin.assign(G + 1, 0);
+    for (uint32_t q = 0; q < G; q++) begin[q + 1] = begin[q] + count[q];
+    std::vector<uint32_t> fill(begin.begin(), begin.end() - 1), order(n);
+    for (uint32_t j = 0; j < n; j++) order[fill[gid[plan_node[j]]]++] = j;
+    // device scratch: [begin G+1][pods n][rec G] + outputs [result n][status n][zone n][minors n]
+    const size_t words = (size_t)G + 1 + n + G + 4 * (size_t)n;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!p->d_batch) HIP_TRY(ctx, hipMalloc(&p->d_batch, sizeof(uint32_t) * (7 * (size_t)p->cap + 1)));
+    uint32_t* d = p->d_batch;
+    if (words > 7 * (size_t)p->cap + 1) return fail(ctx, KG_INVALID_ARG, "batch scratch");
+    std::vector<uint32_t> h(G + 1 + n + G);
+    std::copy(begin.begin(), begin.end(), h.begin());
+    std::copy(order.begin(), order.end(), h.begin() + G + 1);
+    std::copy(rec.begin(), rec.end(), h.begin() + G + 1 + n);
+    uint32_t* d_res = d + G + 1 + n + G;
+    HIP_TRY(ctx, hipMemcpyAsync(d, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice, ctx->stream));
+    st = save_state(s, s->bk);  // CleanupAssumedPods restores this
+    if (st != KG_OK) return st;
+    hipEvent_t e0, e1;
+    st = record_begin(ctx, &e0, &e1);
+    if (st != KG_OK) return st;
+    HIP_TRY(ctx, launch_batch(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, d, d + G + 1, d + G + 1 + n, G, s->ext(),
+                              s->kcfg, force_exact(), d_res, d_res + n, (int32_t*)(d_res + 2 * n), d_res + 3 * n, ctx->stream));
+    st = record_end(ctx, e0, e1);
+    if (st != KG_OK) return st;
+    std::vector<uint32_t> out(4 * (size_t)n);
+    HIP_TRY(ctx, hipMemcpyAsync(out.data(), d_res, sizeof(uint32_t) * 4 * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    s->gen++;
+    bool failed = false, unsup = false;
+    for (uint32_t j = 0; j < n; j++) {
+        failed |= out[j] != KG_BATCH_ASSUMED;
+        unsup |= (out[n + j] & KG_ST_UNSUPPORTED) != 0;
+    }
+    if (failed) {  // the job failed: Unreserve + ForgetPod every assumed pod
+        st = restore_state(s, s->bk);
+        if (st != KG_OK) return st;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        for (uint32_t j = 0; j < n; j++)
+            if (out[j] == KG_BATCH_ASSUMED) out[j] = KG_BATCH_ROLLED_BACK;
+    } else {
+        HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    s->bk.valid = false;
+    for (uint32_t j = 0; j < n; j++) {
+        out_result[j] = out[j];
+        out_status[j] = out[n + j];
+        if (out_zone) out_zone[j] = (int32_t)out[2 * (size_t)n + j];
+        if (out_minors) out_minors[j] = out[3 * (size_t)n + j];
+    }
+    if (unsup) return fail(ctx, KG_UNSUPPORTED, "a pod of the plan needs the host path on its planned node");
+    return KG_OK;
+}
+
 kg_status kg_snapshot_upload_quotas(kg_snap* s, const kg_quota_columns* c, uint32_t nq) {
     if (!s || (!c && nq)) return KG_INVALID_ARG;
     kg_ctx* ctx = s->ctx;
@@ -1912,6 +2096,7 @@ kg_status kg_snapshot_upload_quotas(kg_snap* s, const kg_quota_columns* c, uint3
     HIP_TRY(ctx, hipMemcpyAsync(s->d_qstate, qs.data(), sizeof(QuotaState) * qs.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->n_quotas = nq;
+    s->invalidate_saved();
     return KG_OK;
 }
 
@@ -2037,6 +2222,7 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
     s->n_views = nv;
     s->views_stale = false;
     s->gen++;
+    s->invalidate_saved();
     s->max_cls_views = 0;
     for (int c = 0; c < RSV_MAX_CLASSES; c++) s->max_cls_views = std::max(s->max_cls_views, cb[c + 1] - cb[c]);
     return KG_OK;

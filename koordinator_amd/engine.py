@@ -114,6 +114,12 @@ def lib():
     L.kg_forget_ext.restype = st
     L.kg_replay_minors.argtypes = [vp, P(u32)]
     L.kg_replay_minors.restype = st
+    L.kg_snapshot_checkpoint.argtypes = [vp]
+    L.kg_snapshot_checkpoint.restype = st
+    L.kg_snapshot_rollback.argtypes = [vp]
+    L.kg_snapshot_rollback.restype = st
+    L.kg_batch_schedule.argtypes = [vp, vp, P(i32), P(u32), P(u32), P(i32), P(u32)]
+    L.kg_batch_schedule.restype = st
     if L.kg_abi_version() != abi.KG_ABI_VERSION:
         raise ImportError(f"libkoordgpu ABI {L.kg_abi_version()} != {abi.KG_ABI_VERSION}")
     _lib = L
@@ -219,6 +225,13 @@ class Snapshot:
         s = abi.node_state_struct(t)
         self.ctx.check(self.ctx.L.kg_snapshot_read_state(self.h, C.byref(s)), "kg_snapshot_read_state")
         return t
+
+    def checkpoint(self):
+        """Save the Reserve state (records, zones, GPU minors, quota used) for rollback()."""
+        self.ctx.check(self.ctx.L.kg_snapshot_checkpoint(self.h), "kg_snapshot_checkpoint")
+
+    def rollback(self):
+        self.ctx.check(self.ctx.L.kg_snapshot_rollback(self.h), "kg_snapshot_rollback")
 
     def upload_quotas(self, quotas: abi.Table):
         self.n_quotas = len(quotas["used"])
@@ -353,6 +366,24 @@ def assume_ext(snap: Snapshot, pods: PodBatch, pod: int, node: int):
 
 def forget_ext(snap: Snapshot, pods: PodBatch, pod: int, node: int, zone: int, minors: int):
     snap.ctx.check(snap.ctx.L.kg_forget_ext(snap.h, pods.h, pod, node, zone, minors), "kg_forget_ext")
+
+
+def batch_schedule(snap: Snapshot, pods: PodBatch, plan_node):
+    """Inline batch cycle of a planned job (kg_batch_schedule): per pod (result code KG_BATCH_*, filter
+    status bits, NUMA zone, GPU minors). Raises Unsupported when a pod needs the host path (state rolled back)."""
+    plan = np.ascontiguousarray(plan_node, np.int32)
+    if len(plan) != pods.n:
+        raise ValueError(f"plan has {len(plan)} entries for {pods.n} pods")
+    res = np.zeros(pods.n, np.uint32)
+    stat = np.zeros(pods.n, np.uint32)
+    zone = np.zeros(pods.n, np.int32)
+    minors = np.zeros(pods.n, np.uint32)
+    P = C.POINTER
+    snap.ctx.check(snap.ctx.L.kg_batch_schedule(snap.h, pods.h, plan.ctypes.data_as(P(C.c_int32)),
+                                                res.ctypes.data_as(P(C.c_uint32)), stat.ctypes.data_as(P(C.c_uint32)),
+                                                zone.ctypes.data_as(P(C.c_int32)), minors.ctypes.data_as(P(C.c_uint32))),
+                   "kg_batch_schedule")
+    return res, stat, zone, minors
 
 
 def shard_select(snap: Snapshot, pods: PodBatch, k: int = 1, download: bool = True) -> Optional[np.ndarray]:

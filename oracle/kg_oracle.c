@@ -1876,3 +1876,110 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
     free(b.mem);
     return 0;
 }
+
+/* Inline batch scheduling cycle of a planned job: batch/engine.go:92-294 RunSchedulingCycle with the
+ * grouping of ValidateAndGroupByRequest (:348-371) and the cleanup of batch_scheduler.go:146-152.
+ * Pods are grouped by plan_node (groups in order of first appearance, each in batch order; the caller
+ * orders a node's pods by name). Per pod: PreFilter (ElasticQuota gate on the current used,
+ * elasticquota/plugin.go:257-309) and Filter on the planned node (every enabled plugin), then Reserve
+ * (NodeInfo / LoadAware / NUMA, DeviceShare minors in scoreDevice order, quota used). The first failure
+ * of a group gives its later pods the same status (engine.go:188-192). If any pod failed, every Reserve is
+ * undone (CleanupAssumedPods): here by restoring the state copied before the cycle. Codes are the ABI's
+ * KG_BATCH_*. Groups run one after another, as lane 0 of k_batch does when ElasticQuota is on; without
+ * quota the groups touch disjoint nodes, so their order changes nothing. -1 with KG_PLUGIN_RSV. */
+int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* p, uint32_t np, const kgo_ext* e,
+                       const int32_t* plan_node, uint32_t* out_result, uint32_t* out_status, int32_t* out_zone,
+                       uint32_t* out_minors, int64_t* quota_used_out, int64_t* quota_np_used_out) {
+    if (c->plugins & KG_PLUGIN_RSV) return -1;
+    for (uint32_t j = 0; j < np; j++) {
+        out_zone[j] = -1;
+        out_minors[j] = 0;
+        out_status[j] = 0;
+    }
+    for (uint32_t j = 0; j < np; j++)
+        if (plan_node[j] < 0) { /* batch_scheduler.go:96-101: nothing is assumed */
+            for (uint32_t k = 0; k < np; k++) out_result[k] = KG_BATCH_NO_PLAN;
+            return 0;
+        }
+    const int ext = (c->plugins & KG_PLUGIN_EXT) != 0;
+    kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    /* the state before the cycle, for the cleanup */
+    kg_node_columns v;
+    kgo_state_view(st, &v);
+    kgo_state* saved = kgo_state_new(&v, st->n);
+    ext_buf b;
+    if (ext_buf_new(&b, st->n)) return -1;
+    uint8_t* done = (uint8_t*)calloc(np ? np : 1, 1);
+    int failed_any = 0;
+    for (uint32_t j0 = 0; j0 < np; j0++) {
+        if (done[j0]) continue;
+        const int32_t node = plan_node[j0];
+        uint32_t failed = 0;
+        for (uint32_t j = j0; j < np; j++) {
+            if (done[j] || plan_node[j] != node) continue;
+            done[j] = 1;
+            if (failed) {
+                out_result[j] = KG_BATCH_SIBLING;
+                out_status[j] = failed;
+                continue;
+            }
+            kgo_state_view(st, &v);
+            uint32_t s;
+            int32_t zone;
+            if (ext) {
+                ext_eval_pod(c, &v, st->n, p, j, e, NULL, q, &b.r);
+                s = b.r.st[node];
+                zone = b.r.zone[node];
+            } else {
+                kgo_pair o;
+                kgo_eval_pair(c, &v, (uint32_t)node, p, j, &o);
+                s = o.status;
+                zone = o.zone;
+            }
+            if (s) {
+                failed = s;
+                failed_any = 1;
+                out_result[j] = KG_BATCH_FAILED;
+                out_status[j] = s;
+                continue;
+            }
+            apply(c, st, (uint32_t)node, p, j, zone, 1);
+            if ((c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0 && st->dev_minors &&
+                st->dev_minors[node] > 0) {
+                int64_t preq[KG_DEV_R];
+                uint32_t keys;
+                dev_pod_req(p, j, preq, &keys);
+                uint32_t mask = dev_choose(c, st->dev_total, st->dev_free, (uint32_t)node, st->dev_minors[node], preq, keys,
+                                           p->dev_count[j]);
+                dev_apply(st->dev_total, st->dev_free, (uint32_t)node, mask, preq, keys, 1);
+                out_minors[j] = mask;
+            }
+            quota_apply(q, p, j, 1);
+            out_result[j] = KG_BATCH_ASSUMED;
+            out_zone[j] = zone;
+        }
+    }
+    if (failed_any) {
+        kgo_state_view(saved, &v);
+        kgo_state* fresh = kgo_state_new(&v, st->n);
+        kgo_state tmp = *st;
+        *st = *fresh;
+        *fresh = tmp;
+        kgo_state_free(fresh);
+        for (uint32_t j = 0; j < np; j++)
+            if (out_result[j] == KG_BATCH_ASSUMED) out_result[j] = KG_BATCH_ROLLED_BACK;
+        if (q) {
+            quota_state_free(q);
+            q = quota_state_new(e->quotas, e->n_quotas);
+        }
+    }
+    if (q) {
+        if (quota_used_out) memcpy(quota_used_out, q->used, (size_t)q->n * KG_QUOTA_R * 8);
+        if (quota_np_used_out) memcpy(quota_np_used_out, q->np_used, (size_t)q->n * KG_QUOTA_R * 8);
+    }
+    quota_state_free(q);
+    kgo_state_free(saved);
+    free(done);
+    free(b.mem);
+    return 0;
+}

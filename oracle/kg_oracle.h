@@ -90,6 +90,11 @@ int kgo_ext_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, con
                    uint32_t n_pods, const kgo_ext* ext, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
                    int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason);
 int64_t kgo_mem_bytes_to_ratio(int64_t bytes, int64_t total);
+/* Inline batch cycle of a planned job (batch/engine.go:92-294): per-pod KG_BATCH_* codes, status bits, NUMA
+ * zone and GPU minors; a failed job leaves the state as it was. -1 with KG_PLUGIN_RSV. */
+int kgo_batch_schedule(const kg_config* cfg, kgo_state* st, const kg_pod_columns* pods, uint32_t n_pods,
+                       const kgo_ext* ext, const int32_t* plan_node, uint32_t* out_result, uint32_t* out_status,
+                       int32_t* out_zone, uint32_t* out_minors, int64_t* quota_used_out, int64_t* quota_np_used_out);
 /* Node-sharded two-pass selection: per-shard NormalizeScore inputs (to be max / min all-reduced over
  * the shards), then the shard's top-k with the global inputs. */
 int kgo_ext_shard_stats(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes, uint32_t index_base,

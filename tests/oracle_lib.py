@@ -85,6 +85,10 @@ def lib():
                                      P(KgoExt), P(C.c_int32), P(C.c_int64), P(C.c_uint32), P(C.c_int64),
                                      P(C.c_int64), P(C.c_uint32)]
         L.kgo_ext_replay.restype = C.c_int
+        L.kgo_batch_schedule.argtypes = [P(abi.KgConfig), C.c_void_p, P(abi.KgPodColumns), C.c_uint32, P(KgoExt),
+                                         P(C.c_int32), P(C.c_uint32), P(C.c_uint32), P(C.c_int32), P(C.c_uint32),
+                                         P(C.c_int64), P(C.c_int64)]
+        L.kgo_batch_schedule.restype = C.c_int
         L.kgo_ext_shard_stats.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
                                           P(abi.KgPodColumns), C.c_uint32, P(KgoExt), P(C.c_uint32), P(C.c_uint32),
                                           P(C.c_uint64)]
@@ -243,6 +247,27 @@ class OracleState:
         if reasons:
             return out_node, out_total, out_minors, qu[:nq], qn[:nq], out_reason
         return out_node, out_total, out_minors, qu[:nq], qn[:nq]
+
+    def batch_schedule(self, pods: abi.Table, plan_node, quotas=None):
+        """kgo_batch_schedule: (result codes, status bits, zone, minors, quota used, quota np_used)."""
+        np_ = abi.table_len(pods)
+        plan = np.ascontiguousarray(plan_node, np.int32)
+        res = np.zeros(np_, np.uint32)
+        stat = np.zeros(np_, np.uint32)
+        zone = np.zeros(np_, np.int32)
+        minors = np.zeros(np_, np.uint32)
+        nq = len(quotas["used"]) if quotas is not None else 0
+        qu = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
+        qn = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
+        pc, e = abi.pod_columns(pods), make_ext(quotas, None)
+        P = C.POINTER
+        rc = lib().kgo_batch_schedule(C.byref(self.cfg), self.h, C.byref(pc), np_, C.byref(e),
+                                      plan.ctypes.data_as(P(C.c_int32)), res.ctypes.data_as(P(C.c_uint32)),
+                                      stat.ctypes.data_as(P(C.c_uint32)), zone.ctypes.data_as(P(C.c_int32)),
+                                      minors.ctypes.data_as(P(C.c_uint32)), qu.ctypes.data_as(P(C.c_int64)),
+                                      qn.ctypes.data_as(P(C.c_int64)))
+        assert rc == 0
+        return res, stat, zone, minors, qu[:nq], qn[:nq]
 
     def dev_free(self) -> np.ndarray:
         v = abi.KgNodeColumns()
