@@ -191,6 +191,34 @@ typedef struct kg_config {
 } kg_config;
 
 /* Node snapshot, struct-of-arrays host columns, n_nodes entries each (caller-owned, copied). */
+/* ---- cpuset binding (NodeNUMAResource with LSE/LSR pods) ----------------------- */
+#define KG_MAX_CPUS 256
+/* CPU bind policies (apis/scheduling/config CPUBindPolicy) and exclusive policies (CPUExclusivePolicy). */
+#define KG_CPU_BIND_NONE 0u
+#define KG_CPU_BIND_FULL_PCPUS 1u
+#define KG_CPU_BIND_SPREAD_BY_PCPUS 2u
+#define KG_CPU_EXCL_NONE 0u
+#define KG_CPU_EXCL_PCPU_LEVEL 1u
+#define KG_CPU_EXCL_NUMA_NODE_LEVEL 2u
+/* NUMA allocate strategy of the accumulator (NUMAMostAllocated / NUMALeastAllocated). */
+#define KG_NUMA_MOST_ALLOCATED 0u
+#define KG_NUMA_LEAST_ALLOCATED 1u
+/* CPU topology of one node (nodenumaresource/cpu_topology.go CPUTopology). CPU ids are 0..n_cpus-1; core,
+ * NUMA node and socket ids are dense ranks of the reference's ids (order preserved: the accumulator breaks
+ * ties by id). n_sockets == 0 (or any count 0): no valid topology (CPUTopology.IsValid). */
+typedef struct kg_cpu_topo {
+    uint16_t n_cpus, n_cores, n_nodes, n_sockets;
+    uint8_t core[KG_MAX_CPUS];
+    uint8_t numa[KG_MAX_CPUS];
+    uint8_t socket[KG_MAX_CPUS];
+} kg_cpu_topo;
+/* CPUs already allocated on a node (NodeAllocation.allocatedCPUs): per CPU its RefCount (0 = free) and the
+ * CPUExclusivePolicy of the allocation that holds it. */
+typedef struct kg_cpu_alloc {
+    uint8_t ref[KG_MAX_CPUS];
+    uint8_t excl[KG_MAX_CPUS];
+} kg_cpu_alloc;
+
 typedef struct kg_node_columns {
     /* upstream NodeInfo (k8s v1.35.6): Allocatable / Requested / NonZeroRequested / len(Pods) */
     const int64_t *alloc_cpu, *alloc_mem, *alloc_eph, *alloc_pods;

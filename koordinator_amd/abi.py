@@ -210,6 +210,65 @@ class KgRsvDev(C.Structure):
     _fields_ = [("total", (C.c_int64 * KG_DEV_MINORS) * KG_DEV_R), ("free", (C.c_int64 * KG_DEV_MINORS) * KG_DEV_R)]
 
 
+KG_MAX_CPUS = 256
+KG_CPU_BIND = {"": 0, "None": 0, "FullPCPUs": 1, "SpreadByPCPUs": 2}
+KG_CPU_EXCL = {"": 0, "None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}
+KG_NUMA_STRATEGY = {"MostAllocated": 0, "LeastAllocated": 1}
+
+
+class KgCpuTopo(C.Structure):
+    _fields_ = [("n_cpus", C.c_uint16), ("n_cores", C.c_uint16), ("n_nodes", C.c_uint16), ("n_sockets", C.c_uint16),
+                ("core", C.c_uint8 * KG_MAX_CPUS), ("numa", C.c_uint8 * KG_MAX_CPUS),
+                ("socket", C.c_uint8 * KG_MAX_CPUS)]
+
+
+class KgCpuAlloc(C.Structure):
+    _fields_ = [("ref", C.c_uint8 * KG_MAX_CPUS), ("excl", C.c_uint8 * KG_MAX_CPUS)]
+
+
+def cpu_topo(core, numa, socket) -> KgCpuTopo:
+    """kg_cpu_topo from per-CPU ids (any integers): dense ranks in id order (the accumulator's tie-breaks)."""
+    t = KgCpuTopo()
+    n = len(core)
+    if n > KG_MAX_CPUS:
+        raise ValueError(f"{n} CPUs > {KG_MAX_CPUS}")
+    for name, ids in (("core", core), ("numa", numa), ("socket", socket)):
+        rank = {v: r for r, v in enumerate(sorted(set(ids)))}
+        arr = getattr(t, name)
+        for i, v in enumerate(ids):
+            arr[i] = rank[v]
+        setattr(t, {"core": "n_cores", "numa": "n_nodes", "socket": "n_sockets"}[name], len(rank))
+    t.n_cpus = n
+    return t
+
+
+def cpu_topo_for_test(sockets, nodes_per_socket, cores_per_node, cpus_per_core) -> KgCpuTopo:
+    """nodenumaresource/cpu_accumulator_test.go:30-57 buildCPUTopologyForTest."""
+    core, numa, socket = [], [], []
+    nid = cid = 0
+    for s in range(sockets):
+        for _ in range(nodes_per_socket):
+            for _ in range(cores_per_node):
+                for _ in range(cpus_per_core):
+                    core.append(cid)
+                    numa.append(nid)
+                    socket.append(s)
+                cid += 1
+            nid += 1
+    return cpu_topo(core, numa, socket)
+
+
+def cpu_mask(cpus) -> np.ndarray:
+    m = np.zeros(4, np.uint64)
+    for c in cpus:
+        m[c >> 6] |= np.uint64(1) << np.uint64(c & 63)
+    return m
+
+
+def mask_cpus(m) -> list:
+    return [w * 64 + b for w in range(4) for b in range(64) if (int(m[w]) >> b) & 1]
+
+
 # ----------------------------------------------------------------------------------------------
 # column tables
 

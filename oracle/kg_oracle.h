@@ -104,6 +104,14 @@ int kgo_ext_shard_select(const kg_config* cfg, const kg_node_columns* nodes, uin
                          const kg_pod_columns* pods, uint32_t n_pods, const kgo_ext* ext, const uint32_t* dev_max,
                          const uint32_t* rsv_max, const uint64_t* pref, uint32_t k, uint64_t* keys);
 
+/* cpuset accumulator (nodenumaresource/cpu_accumulator.go takeCPUs / takePreferredCPUs, kg_cpuset.c):
+ * 0 = ok (out = the chosen CPUs), -1 = ErrNotEnoughCPUs, -2 = "failed to allocate cpus". */
+int kgo_take_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t avail[4], const kg_cpu_alloc* allocated,
+                  int needed, int bind_policy, int excl_policy, int strategy, uint64_t out[4]);
+int kgo_take_preferred_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t avail[4], const uint64_t preferred[4],
+                            const kg_cpu_alloc* allocated, int needed, int bind_policy, int excl_policy, int strategy,
+                            uint64_t out[4]);
+
 /* Helpers shared with tests. */
 int64_t kgo_amplify(int64_t origin, double ratio);
 int64_t kgo_la_usage_percent(int64_t estimated, int64_t total);

@@ -89,6 +89,12 @@ def lib():
                                          P(C.c_int32), P(C.c_uint32), P(C.c_uint32), P(C.c_int32), P(C.c_uint32),
                                          P(C.c_int64), P(C.c_int64)]
         L.kgo_batch_schedule.restype = C.c_int
+        L.kgo_take_cpus.argtypes = [P(abi.KgCpuTopo), C.c_int, P(C.c_uint64), P(abi.KgCpuAlloc), C.c_int, C.c_int,
+                                    C.c_int, C.c_int, P(C.c_uint64)]
+        L.kgo_take_cpus.restype = C.c_int
+        L.kgo_take_preferred_cpus.argtypes = [P(abi.KgCpuTopo), C.c_int, P(C.c_uint64), P(C.c_uint64),
+                                              P(abi.KgCpuAlloc), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_uint64)]
+        L.kgo_take_preferred_cpus.restype = C.c_int
         L.kgo_ext_shard_stats.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
                                           P(abi.KgPodColumns), C.c_uint32, P(KgoExt), P(C.c_uint32), P(C.c_uint32),
                                           P(C.c_uint64)]
@@ -105,6 +111,24 @@ def lib():
         L.kgo_la_usage_percent.restype = C.c_int64
         _lib = L
     return _lib
+
+
+def take_cpus(topo, max_ref, avail, alloc, needed, bind, excl, strategy, preferred=None):
+    """kgo_take_cpus / kgo_take_preferred_cpus: (rc, cpus)."""
+    out = np.zeros(4, np.uint64)
+    av = np.ascontiguousarray(avail, np.uint64)
+    P = C.POINTER
+    if preferred is None:
+        rc = lib().kgo_take_cpus(C.byref(topo), max_ref, av.ctypes.data_as(P(C.c_uint64)),
+                                 C.byref(alloc) if alloc is not None else None, needed, bind, excl, strategy,
+                                 out.ctypes.data_as(P(C.c_uint64)))
+    else:
+        pf = np.ascontiguousarray(preferred, np.uint64)
+        rc = lib().kgo_take_preferred_cpus(C.byref(topo), max_ref, av.ctypes.data_as(P(C.c_uint64)),
+                                           pf.ctypes.data_as(P(C.c_uint64)),
+                                           C.byref(alloc) if alloc is not None else None, needed, bind, excl, strategy,
+                                           out.ctypes.data_as(P(C.c_uint64)))
+    return rc, abi.mask_cpus(out)
 
 
 def eval_pair(cfg, nodes: abi.Table, i: int, pods: abi.Table, j: int) -> KgoPair:
