@@ -219,6 +219,20 @@ typedef struct kg_cpu_alloc {
     uint8_t excl[KG_MAX_CPUS];
 } kg_cpu_alloc;
 
+/* One takeCPUs / takePreferredCPUs request (nodenumaresource/cpu_accumulator.go:30-246). */
+typedef struct kg_cpuset_request {
+    uint32_t topo;          /* index into the topologies of the call                                   */
+    int32_t alloc;          /* index into the allocations of the call, -1 = nothing allocated          */
+    uint64_t avail[4];      /* allocatable CPUs (NodeAllocation.getAvailableCPUs)                       */
+    uint64_t preferred[4];  /* preferred CPUs (takePreferredCPUs); used when has_preferred               */
+    int32_t needed;         /* numCPUsNeeded                                                            */
+    int32_t max_ref;        /* TopologyOptions.MaxRefCount (>= 1)                                       */
+    int32_t bind;           /* KG_CPU_BIND_*                                                            */
+    int32_t excl;           /* the pod's KG_CPU_EXCL_*                                                  */
+    int32_t strategy;       /* KG_NUMA_MOST_ALLOCATED / KG_NUMA_LEAST_ALLOCATED                         */
+    int32_t has_preferred;
+} kg_cpuset_request;
+
 typedef struct kg_node_columns {
     /* upstream NodeInfo (k8s v1.35.6): Allocatable / Requested / NonZeroRequested / len(Pods) */
     const int64_t *alloc_cpu, *alloc_mem, *alloc_eph, *alloc_pods;
@@ -434,6 +448,12 @@ kg_status kg_forget_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t nod
                         uint32_t minors);
 /* GPU minors chosen for each pod by the last kg_replay (bitmask; 0 = none), n_pods entries. */
 kg_status kg_replay_minors(kg_pods* pods, uint32_t* out);
+
+/* Device cpuset accumulator, one request per workgroup: out[4 * i] = the CPUs chosen for request i,
+ * rc[i] = 0, -1 (ErrNotEnoughCPUs: fewer allocatable CPUs than needed) or -2 ("failed to allocate cpus").
+ * Topologies need <= 8 NUMA nodes, <= 8 sockets and <= 8 CPUs per core (KG_UNSUPPORTED otherwise). */
+kg_status kg_cpuset_take(kg_ctx* ctx, const kg_cpu_topo* topos, uint32_t n_topos, const kg_cpu_alloc* allocs,
+                         uint32_t n_allocs, const kg_cpuset_request* reqs, uint32_t n, uint64_t* out, int32_t* rc);
 
 /* ---- whole-job placement (FindOneNodePlugin slot, frameworkext/interface.go:118-127) ----------------
  * Checkpoint / rollback of everything Reserve changes (node records, NUMA zones, GPU minors, quota used):

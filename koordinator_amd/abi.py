@@ -226,6 +226,12 @@ class KgCpuAlloc(C.Structure):
     _fields_ = [("ref", C.c_uint8 * KG_MAX_CPUS), ("excl", C.c_uint8 * KG_MAX_CPUS)]
 
 
+class KgCpusetRequest(C.Structure):
+    _fields_ = [("topo", C.c_uint32), ("alloc", C.c_int32), ("avail", C.c_uint64 * 4), ("preferred", C.c_uint64 * 4),
+                ("needed", C.c_int32), ("max_ref", C.c_int32), ("bind", C.c_int32), ("excl", C.c_int32),
+                ("strategy", C.c_int32), ("has_preferred", C.c_int32)]
+
+
 def cpu_topo(core, numa, socket) -> KgCpuTopo:
     """kg_cpu_topo from per-CPU ids (any integers): dense ranks in id order (the accumulator's tie-breaks)."""
     t = KgCpuTopo()

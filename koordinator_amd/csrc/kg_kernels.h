@@ -3,6 +3,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "kg_layout.h"
+#include "../../include/koordgpu.h"
 
 namespace kg {
 
@@ -103,6 +104,9 @@ hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, 
 hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                              uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
                              bool exact, int32_t* out, hipStream_t s);
+// batch of cpuset accumulator requests (kg_cpuset.hip)
+hipError_t launch_cpuset_take(const kg_cpu_topo* topos, const kg_cpu_alloc* allocs, const kg_cpuset_request* reqs,
+                              uint32_t n, uint64_t* out, int32_t* rc, hipStream_t s);
 // inline batch cycle of a whole-job plan (k_batch); ext = the snapshot carries the config-5 tables
 hipError_t launch_batch(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                         const uint32_t* grp_begin, const uint32_t* grp_pods, const uint32_t* grp_rec, uint32_t n_groups,

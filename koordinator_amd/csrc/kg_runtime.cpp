@@ -1895,6 +1895,63 @@ kg_status kg_forget_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int
     return assume_ext(s, p, pod, node, zone, minors, -1, nullptr, nullptr);
 }
 
+// ---- cpuset accumulator (batch entry) -----------------------------------------------------------------
+
+static const char* cpu_topo_problem(const kg_cpu_topo& t) {
+    if (t.n_cpus > KG_MAX_CPUS) return "more than 256 CPUs";
+    if (t.n_nodes > 8 || t.n_sockets > 8) return "more than 8 NUMA nodes or sockets";
+    int per_core[KG_MAX_CPUS] = {0};
+    for (int c = 0; c < t.n_cpus; c++) {
+        if (t.core[c] >= t.n_cores || t.numa[c] >= t.n_nodes || t.socket[c] >= t.n_sockets) return "id out of range";
+        if (++per_core[t.core[c]] > 8) return "more than 8 CPUs per core";
+    }
+    return nullptr;
+}
+
+kg_status kg_cpuset_take(kg_ctx* ctx, const kg_cpu_topo* topos, uint32_t n_topos, const kg_cpu_alloc* allocs,
+                         uint32_t n_allocs, const kg_cpuset_request* reqs, uint32_t n, uint64_t* out, int32_t* rc) {
+    if (!ctx || (n && (!topos || !reqs || !out || !rc))) return KG_INVALID_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    for (uint32_t t = 0; t < n_topos; t++)
+        if (const char* why = cpu_topo_problem(topos[t])) return fail(ctx, KG_UNSUPPORTED, "CPU topology %u: %s", t, why);
+    for (uint32_t i = 0; i < n; i++) {
+        const kg_cpuset_request& q = reqs[i];
+        if (q.topo >= n_topos || (q.alloc >= 0 && (!allocs || (uint32_t)q.alloc >= n_allocs)))
+            return fail(ctx, KG_INVALID_ARG, "request %u: topology / allocation index out of range", i);
+        if (q.needed < 0 || q.needed > KG_MAX_CPUS || q.max_ref < 1 || q.bind < 0 || q.bind > 2 || q.excl < 0 ||
+            q.excl > 2 || q.strategy < 0 || q.strategy > 1)
+            return fail(ctx, KG_INVALID_ARG, "request %u: bad arguments", i);
+    }
+    if (n == 0) return KG_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const size_t bt = sizeof(kg_cpu_topo) * n_topos, ba = sizeof(kg_cpu_alloc) * (allocs ? n_allocs : 0),
+                 bq = sizeof(kg_cpuset_request) * n, bo = sizeof(uint64_t) * 4 * n, br = sizeof(int32_t) * n;
+    uint8_t* d = nullptr;
+    HIP_TRY(ctx, hipMalloc(&d, bt + ba + bq + bo + br + 64));
+    kg_status st = KG_OK;
+    uint8_t* p = d;
+    auto* d_topo = reinterpret_cast<kg_cpu_topo*>(p);
+    p += bt;
+    auto* d_alloc = ba ? reinterpret_cast<kg_cpu_alloc*>(p) : nullptr;
+    p += ba;
+    p = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(p) + 7) & ~(uintptr_t)7);
+    auto* d_req = reinterpret_cast<kg_cpuset_request*>(p);
+    p += bq;
+    auto* d_out = reinterpret_cast<uint64_t*>(p);
+    p += bo;
+    auto* d_rc = reinterpret_cast<int32_t*>(p);
+    hipError_t e = hipMemcpyAsync(d_topo, topos, bt, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess && ba) e = hipMemcpyAsync(d_alloc, allocs, ba, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_req, reqs, bq, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = launch_cpuset_take(d_topo, d_alloc, d_req, n, d_out, d_rc, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, bo, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(rc, d_rc, br, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) st = fail(ctx, KG_DEVICE_ERROR, "kg_cpuset_take: %s", hipGetErrorString(e));
+    hipFree(d);
+    return st;
+}
+
 // ---- checkpoint / rollback and the inline batch cycle ------------------------------------------------
 
 static kg_status save_state(kg_snap* s, kg_snap::Saved& k) {

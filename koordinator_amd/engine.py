@@ -120,6 +120,9 @@ def lib():
     L.kg_snapshot_rollback.restype = st
     L.kg_batch_schedule.argtypes = [vp, vp, P(i32), P(u32), P(u32), P(i32), P(u32)]
     L.kg_batch_schedule.restype = st
+    L.kg_cpuset_take.argtypes = [vp, P(abi.KgCpuTopo), u32, P(abi.KgCpuAlloc), u32, P(abi.KgCpusetRequest), u32,
+                                 P(u64), P(i32)]
+    L.kg_cpuset_take.restype = st
     if L.kg_abi_version() != abi.KG_ABI_VERSION:
         raise ImportError(f"libkoordgpu ABI {L.kg_abi_version()} != {abi.KG_ABI_VERSION}")
     _lib = L
@@ -384,6 +387,19 @@ def batch_schedule(snap: Snapshot, pods: PodBatch, plan_node):
                                                 zone.ctypes.data_as(P(C.c_int32)), minors.ctypes.data_as(P(C.c_uint32))),
                    "kg_batch_schedule")
     return res, stat, zone, minors
+
+
+def cpuset_take(ctx: Context, topos, allocs, reqs):
+    """kg_cpuset_take: device cpuset accumulator over a list of KgCpusetRequest -> (masks [n, 4], rc [n])."""
+    n = len(reqs)
+    T = (abi.KgCpuTopo * max(len(topos), 1))(*topos)
+    A = (abi.KgCpuAlloc * max(len(allocs), 1))(*allocs) if allocs else None
+    R = (abi.KgCpusetRequest * max(n, 1))(*reqs)
+    out = np.zeros((max(n, 1), 4), np.uint64)
+    rc = np.zeros(max(n, 1), np.int32)
+    ctx.check(ctx.L.kg_cpuset_take(ctx.h, T, len(topos), A, len(allocs) if allocs else 0, R, n, _u64p(out),
+                                   rc.ctypes.data_as(C.POINTER(C.c_int32))), "kg_cpuset_take")
+    return out[:n], rc[:n]
 
 
 def shard_select(snap: Snapshot, pods: PodBatch, k: int = 1, download: bool = True) -> Optional[np.ndarray]:
