@@ -99,8 +99,13 @@ typedef enum kg_status {
 #define KG_POD_NUMA_SKIP 0x4u /* PodRequests all zero -> NodeNUMAResource Skip (nodenumaresource/plugin.go:277-283) */
 #define KG_POD_HAS_CPU 0x8u   /* "cpu" key present in PodRequests                                       */
 #define KG_POD_HAS_MEM 0x10u  /* "memory" key present in PodRequests                                    */
-#define KG_POD_CPU_BIND 0x20u /* LSE/LSR prod pod requesting cpuset binding: not on the device path      */
+#define KG_POD_CPU_BIND 0x20u /* state.requestCPUBind: LSE/LSR pod with a Full/Spread cpuset bind policy */
 #define KG_POD_NON_PREEMPTIBLE 0x40u /* extension.IsPodNonPreemptible (elasticquota/plugin.go:288)     */
+/* cpuset binding request of a KG_POD_CPU_BIND pod (plugin.go:319-349: requestCPUBind, the resolved
+ * preferred/required CPUBindPolicy, the preferred CPUExclusivePolicy); numCPUsNeeded = req_cpu / 1000. */
+#define KG_POD_CPU_POLICY_SHIFT 8    /* 2 bits KG_CPU_BIND_*: cpuBindPolicy (required one if set)        */
+#define KG_POD_CPU_REQUIRED 0x400u   /* the policy is RequiredCPUBindPolicy                              */
+#define KG_POD_CPU_EXCL_SHIFT 11     /* 2 bits KG_CPU_EXCL_*                                             */
 #define KG_POD_RSV_REQUIRED 0x80u    /* pod has a reservation affinity (reservation/transformer.go:148,
                                       * stateData.hasAffinity): must allocate from a reservation      */
 
@@ -129,6 +134,10 @@ typedef enum kg_status {
 #define KG_ST_NUMA_ALIGN 0x80000u    /* ErrNUMAHintCannotAligned                              */
 #define KG_ST_NUMA_UNSATISFIED 0x100000u /* ErrUnsatisfiedNUMAResource: a requested resource has no NUMA hint
                                             (frameworkext/topologymanager/policy.go:166-173)     */
+#define KG_ST_NUMA_CPU_TOPO 0x200000u /* ErrInvalidCPUTopology (UnschedulableAndUnresolvable)              */
+#define KG_ST_NUMA_CPU_BIND 0x400000u /* ErrCPUBindPolicyConflict / ErrSMTAlignmentError / ErrInvalidRequestedCPUs
+                                       * (UnschedulableAndUnresolvable, plugin.go:388-418, util.go:131-135) */
+#define KG_ST_NUMA_CPUS 0x800000u     /* ErrNotEnoughCPUs: the required bind policy's CPUs do not cover the pod */
 #define KG_ST_NUMA_MASK 0xFF0000u
 #define KG_ST_DEV_INSUFFICIENT 0x01000000u /* "Insufficient gpu devices" (Unschedulable, device_allocator.go:432) */
 #define KG_ST_DEV_NO_DEVICE 0x02000000u    /* no GPU minors on the node's Device (UnschedulableAndUnresolvable,
@@ -200,6 +209,10 @@ typedef struct kg_config {
 #define KG_CPU_EXCL_NONE 0u
 #define KG_CPU_EXCL_PCPU_LEVEL 1u
 #define KG_CPU_EXCL_NUMA_NODE_LEVEL 2u
+/* Node CPU bind policy (apis/extension NodeCPUBindPolicy via GetNodeCPUBindPolicy). */
+#define KG_NODE_CPU_BIND_NONE 0u
+#define KG_NODE_CPU_BIND_FULL_PCPUS_ONLY 1u
+#define KG_NODE_CPU_BIND_SPREAD_BY_PCPUS 2u
 /* NUMA allocate strategy of the accumulator (NUMAMostAllocated / NUMALeastAllocated). */
 #define KG_NUMA_MOST_ALLOCATED 0u
 #define KG_NUMA_LEAST_ALLOCATED 1u
@@ -272,6 +285,19 @@ typedef struct kg_node_columns {
      * nodenumaresource/node_allocation.go:52-68) for the Required exclusive policy of pods with a
      * pod-level NUMA policy (NULL = all idle). */
     const uint32_t* numa_zone_status;
+    /* cpuset binding (NodeNUMAResource, LSE/LSR pods; all may be NULL = no CPU topology anywhere):
+     * cpu_topo[i] indexes cpu_topos (-1 = the node has no CPU topology: ErrInvalidCPUTopology for a
+     * cpuset-binding pod); cpu_alloc[i] = the node's allocated CPUs (NULL = none). cpuset_alloc_milli must
+     * then equal 1000 x the CPUs with RefCount > 0. cpu_max_ref (NULL = 1), cpu_bind_policy
+     * (KG_NODE_CPU_BIND_*, GetNodeCPUBindPolicy) and cpu_strategy (KG_NUMA_MOST/LEAST_ALLOCATED,
+     * GetNUMAAllocateStrategy) are per node. */
+    const int32_t* cpu_topo;
+    const kg_cpu_topo* cpu_topos;
+    uint32_t n_cpu_topos;
+    const kg_cpu_alloc* cpu_alloc;
+    const uint8_t* cpu_max_ref;
+    const uint8_t* cpu_bind_policy;
+    const uint8_t* cpu_strategy;
 } kg_node_columns;
 
 /* Mutable node state that Assume/Forget change; used to read a snapshot back after kg_replay. */
@@ -282,6 +308,8 @@ typedef struct kg_node_state {
     int64_t *la_sbase_np[KG_LA_R], *la_sbase_prod[KG_LA_R];
     int64_t *zone_cpu_used[KG_MAX_ZONES], *zone_mem_used[KG_MAX_ZONES];
     int64_t* dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
+    int64_t* cpuset_alloc_milli;
+    kg_cpu_alloc* cpu_alloc; /* [node] (nodes without a CPU topology: zeros) */
 } kg_node_state;
 
 /* Pending pods, struct-of-arrays host columns (caller-owned, copied). */

@@ -48,6 +48,10 @@ KG_POD_NUMA_SKIP = 0x4
 KG_POD_HAS_CPU = 0x8
 KG_POD_HAS_MEM = 0x10
 KG_POD_CPU_BIND = 0x20
+KG_POD_CPU_POLICY_SHIFT = 8
+KG_POD_CPU_REQUIRED = 0x400
+KG_POD_CPU_EXCL_SHIFT = 11
+KG_NODE_CPU_BIND_NONE, KG_NODE_CPU_BIND_FULL_PCPUS_ONLY, KG_NODE_CPU_BIND_SPREAD_BY_PCPUS = 0, 1, 2
 KG_POD_NON_PREEMPTIBLE = 0x40
 KG_POD_RSV_REQUIRED = 0x80
 
@@ -70,6 +74,9 @@ KG_ST_NUMA_CONFLICT = 0x20000
 KG_ST_NUMA_NO_RES = 0x40000
 KG_ST_NUMA_ALIGN = 0x80000
 KG_ST_NUMA_UNSATISFIED = 0x100000
+KG_ST_NUMA_CPU_TOPO = 0x200000
+KG_ST_NUMA_CPU_BIND = 0x400000
+KG_ST_NUMA_CPUS = 0x800000
 KG_ST_NUMA_MASK = 0xFF0000
 KG_ST_DEV_INSUFFICIENT = 0x01000000
 KG_ST_DEV_NO_DEVICE = 0x02000000
@@ -146,6 +153,10 @@ class KgNodeColumns(C.Structure):
         ("zone_mem_used", _p64 * KG_MAX_ZONES),
         ("dev_minors", _pi32), ("dev_total", _p64), ("dev_free", _p64),
         ("numa_zone_status", _pu32),
+        # cpuset binding: cpu_topo (int32 per node), cpu_topos (kg_cpu_topo[]), cpu_alloc (kg_cpu_alloc per node)
+        ("cpu_topo", _pi32), ("cpu_topos", C.c_void_p), ("n_cpu_topos", C.c_uint32), ("cpu_alloc", C.c_void_p),
+        ("cpu_max_ref", C.POINTER(C.c_uint8)), ("cpu_bind_policy", C.POINTER(C.c_uint8)),
+        ("cpu_strategy", C.POINTER(C.c_uint8)),
     ]
 
 
@@ -158,6 +169,7 @@ class KgNodeState(C.Structure):
         ("la_sbase_np", _p64 * KG_LA_R), ("la_sbase_prod", _p64 * KG_LA_R),
         ("zone_cpu_used", _p64 * KG_MAX_ZONES), ("zone_mem_used", _p64 * KG_MAX_ZONES),
         ("dev_free", _p64),
+        ("cpuset_alloc_milli", _p64), ("cpu_alloc", C.c_void_p),
     ]
 
 
@@ -230,6 +242,14 @@ class KgCpusetRequest(C.Structure):
     _fields_ = [("topo", C.c_uint32), ("alloc", C.c_int32), ("avail", C.c_uint64 * 4), ("preferred", C.c_uint64 * 4),
                 ("needed", C.c_int32), ("max_ref", C.c_int32), ("bind", C.c_int32), ("excl", C.c_int32),
                 ("strategy", C.c_int32), ("has_preferred", C.c_int32)]
+
+
+def cpu_topos_array(topos) -> np.ndarray:
+    """list of KgCpuTopo -> uint8 [T, sizeof(kg_cpu_topo)] (the node table's cpu_topos column)."""
+    out = np.zeros((len(topos), C.sizeof(KgCpuTopo)), np.uint8)
+    for k, t in enumerate(topos):
+        out[k] = np.frombuffer(bytes(t), np.uint8)
+    return out
 
 
 def cpu_topo(core, numa, socket) -> KgCpuTopo:
@@ -389,6 +409,20 @@ def node_columns(t: Table) -> KgNodeColumns:
         s.dev_minors = _ptr(t["dev_minors"], C.c_int32)
         s.dev_total = _ptr(t["dev_total"], C.c_int64)
         s.dev_free = _ptr(t["dev_free"], C.c_int64)
+    if "cpu_topo" in t:
+        # cpuset tables: cpu_topos uint8 [T, sizeof kg_cpu_topo]; cpu_alloc uint8 [n, 512]
+        t["cpu_topo"] = np.ascontiguousarray(t["cpu_topo"], np.int32)
+        t["cpu_topos"] = np.ascontiguousarray(t["cpu_topos"], np.uint8)
+        s.cpu_topo = _ptr(t["cpu_topo"], C.c_int32)
+        s.cpu_topos = t["cpu_topos"].ctypes.data
+        s.n_cpu_topos = len(t["cpu_topos"])
+        if "cpu_alloc" in t:
+            t["cpu_alloc"] = np.ascontiguousarray(t["cpu_alloc"], np.uint8)
+            s.cpu_alloc = t["cpu_alloc"].ctypes.data
+        for k in ("cpu_max_ref", "cpu_bind_policy", "cpu_strategy"):
+            if k in t:
+                t[k] = np.ascontiguousarray(t[k], np.uint8)
+                setattr(s, k, t[k].ctypes.data_as(C.POINTER(C.c_uint8)))
     s._keep = t  # keep the buffers alive with the struct
     return s
 
@@ -409,6 +443,10 @@ def node_state_struct(t: Table) -> KgNodeState:
             arr[z] = _ptr(t[f"{name}{z}"], C.c_int64)
     if "dev_free" in t:
         s.dev_free = _ptr(t["dev_free"], C.c_int64)
+    if "cpuset_alloc_milli" in t:
+        s.cpuset_alloc_milli = _ptr(t["cpuset_alloc_milli"], C.c_int64)
+    if "cpu_alloc" in t:
+        s.cpu_alloc = t["cpu_alloc"].ctypes.data
     s._keep = t
     return s
 
@@ -416,6 +454,8 @@ def node_state_struct(t: Table) -> KgNodeState:
 def empty_node_state(n: int) -> Table:
     t = {k: np.zeros(n, np.int64) for k in NODE_STATE}
     t["dev_free"] = np.zeros((n, KG_DEV_R, KG_DEV_MINORS), np.int64)
+    t["cpuset_alloc_milli"] = np.zeros(n, np.int64)
+    t["cpu_alloc"] = np.zeros((n, 2 * KG_MAX_CPUS), np.uint8)
     return t
 
 

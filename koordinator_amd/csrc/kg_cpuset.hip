@@ -54,3 +54,108 @@ hipError_t launch_cpuset_take(const kg_cpu_topo* topos, const kg_cpu_alloc* allo
 }
 
 }  // namespace kg
+
+namespace kg {
+
+// NodeNUMAResource Reserve of a cpuset-binding pod on a NUMA-policy-None node (plugin.go:585-635 ->
+// resourceManager.Allocate/Update): the accumulator's CPUs enter the node's allocation (RefCount++, the
+// pod's exclusive policy, node_allocation.go:111-130), the Filter counts and cpuset_alloc_milli follow.
+// Runs before the Reserve of the NodeInfo columns (apply_assume, which re-derives the record). The pod
+// and record come from (pod, rec), or in replay from the previous step's winner.
+__global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
+                                                       kg_cpu_alloc* __restrict__ allocs,
+                                                       const kg_cpu_topo* __restrict__ topos, PodsDev pods, KCfg cfg,
+                                                       uint32_t pod, uint32_t rec, const uint64_t* __restrict__ winners,
+                                                       const uint32_t* __restrict__ step_base, uint32_t step_off,
+                                                       const uint32_t* __restrict__ pos, uint32_t index_base) {
+    __shared__ kg_cpu_topo st;
+    __shared__ CpuAccLds acc;
+    __shared__ kg_cpu_alloc sa;
+    if (!(cfg.plugins & KG_PLUGIN_NUMA)) return;
+    if (winners) {  // replay: Reserve of pod step-1 on its winner
+        const uint32_t step = *step_base + step_off;
+        if (step == 0) return;
+        const uint64_t prev = __hip_atomic_load(&winners[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == 0ull) return;
+        pod = step - 1;
+        rec = pos[(0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull)) - index_base];
+    }
+    const uint32_t pf = pods.flags[pod];
+    const int64_t req_cpu = pods.req_cpu[pod];
+    ZoneRec& z = zones[rec];
+    int64_t* n = nodes[rec].v;
+    if (z.cpu_topo < 0 || (pf & KG_POD_NUMA_SKIP)) return;
+    const uint32_t node_bind = (z.cpu_meta >> CPU_META_BIND_SHIFT) & 3u;
+    if (!((pf & KG_POD_CPU_BIND) || (node_bind != KG_NODE_CPU_BIND_NONE && req_cpu != 0))) return;
+    const uint32_t node_pol = ((uint32_t)n[N_FLAGS] >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (pf >> 16) & 15u;
+    if ((pod_pol != KG_NUMA_NONE ? pod_pol : node_pol) != KG_NUMA_NONE) return;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(topos + z.cpu_topo);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&st);
+    for (uint32_t k = threadIdx.x; k < sizeof(kg_cpu_topo) / 4; k += 64) dst[k] = src[k];
+    const uint32_t* as = reinterpret_cast<const uint32_t*>(allocs + rec);
+    uint32_t* ad = reinterpret_cast<uint32_t*>(&sa);
+    for (uint32_t k = threadIdx.x; k < sizeof(kg_cpu_alloc) / 4; k += 64) ad[k] = as[k];
+    __syncthreads();
+    // getCPUBindPolicy (util.go:101-119): the pod's required policy, else the node's, else the preferred one
+    const bool pod_req = (pf & KG_POD_CPU_REQUIRED) != 0;
+    uint32_t bind = (pf >> KG_POD_CPU_POLICY_SHIFT) & 3u;
+    bool required = pod_req;
+    if (!pod_req && node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) bind = KG_CPU_BIND_SPREAD_BY_PCPUS, required = true;
+    if (!pod_req && node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) bind = KG_CPU_BIND_FULL_PCPUS, required = true;
+    const int max_ref = (int)(z.cpu_meta & 0xFFu);
+    CpuTake q;
+    for (int w = 0; w < 4; w++) q.avail[w] = q.preferred[w] = 0;
+    // getAvailableCPUs, then filterCPUsByRequiredCPUBindPolicy for a required policy (lane 0)
+    if (threadIdx.x == 0) {
+        const int cpc = st.n_cores ? st.n_cpus / st.n_cores : 1;
+        for (int c = 0; c < st.n_cpus; c++) {
+            if (sa.ref[c] >= max_ref) continue;
+            bool keep = true;
+            if (required) {
+                int cnt = 0, first = -1;
+                for (int d = 0; d < st.n_cpus; d++)
+                    if (st.core[d] == st.core[c] && sa.ref[d] < max_ref) {
+                        cnt++;
+                        if (first < 0) first = d;
+                    }
+                keep = bind == KG_CPU_BIND_FULL_PCPUS ? cnt == cpc : first == c;
+            }
+            if (keep) q.avail[c >> 6] |= 1ull << (c & 63);
+        }
+    }
+    __shared__ uint64_t s_avail[4];
+    if (threadIdx.x == 0)
+        for (int w = 0; w < 4; w++) s_avail[w] = q.avail[w];
+    __syncthreads();
+    for (int w = 0; w < 4; w++) q.avail[w] = s_avail[w];
+    q.needed = (int32_t)(req_cpu / 1000);
+    q.max_ref = max_ref;
+    q.bind = (int32_t)bind;
+    q.excl = (int32_t)((pf >> KG_POD_CPU_EXCL_SHIFT) & 3u);
+    q.strategy = (int32_t)((z.cpu_meta >> CPU_META_STRATEGY_SHIFT) & 1u);
+    q.has_preferred = 0;
+    uint64_t res[4];
+    const int code = cpuset_take(&st, &sa, q, &acc, res);
+    __syncthreads();
+    if (code != 0 || threadIdx.x != 0) return;
+    kg_cpu_alloc& A = allocs[rec];
+    for (int c = 0; c < st.n_cpus; c++)
+        if ((res[c >> 6] >> (c & 63)) & 1ull) {
+            A.ref[c] = (uint8_t)(A.ref[c] + 1);
+            A.excl[c] = (uint8_t)q.excl;
+        }
+    cpu_counts(st, &A, max_ref, z);
+    n[N_CPUSET] = 1000 * (int64_t)z.cpu_allocated;
+    n[N_AMP_CPUSET] = z.amp_ratio > 1.0 ? (int64_t)ceil(__dmul_rn((double)n[N_CPUSET], z.amp_ratio)) : n[N_CPUSET];
+}
+
+hipError_t launch_cpuset_reserve(NodeRec* nodes, ZoneRec* zones, kg_cpu_alloc* allocs, const kg_cpu_topo* topos,
+                                 const PodsDev& pods, const KCfg& cfg, uint32_t pod, uint32_t rec, const uint64_t* winners,
+                                 const uint32_t* step_base, uint32_t step_off, const uint32_t* pos, uint32_t index_base,
+                                 hipStream_t s) {
+    k_cpuset_reserve<<<1, 64, 0, s>>>(nodes, zones, allocs, topos, pods, cfg, pod, rec, winners, step_base, step_off, pos,
+                                      index_base);
+    return hipGetLastError();
+}
+
+}  // namespace kg

@@ -408,8 +408,17 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
     }
     const uint32_t pol = pod_pol != KG_NUMA_NONE ? pod_pol : node_pol;
     const bool amp = (flags & F_AMP) != 0;
-    const bool cpu_bind = (p.flags & KG_POD_CPU_BIND) != 0;
     const int64_t pod_cpu = p.req_cpu;
+    // requestCPUBind (util.go:121-138): the pod's own cpuset request, or a node CPU bind policy and a cpu request
+    const uint32_t node_bind = (zr->cpu_meta >> CPU_META_BIND_SHIFT) & 3u;
+    bool cpu_bind = (p.flags & KG_POD_CPU_BIND) != 0;
+    if (!cpu_bind && pod_cpu != 0 && node_bind != KG_NODE_CPU_BIND_NONE) {
+        if (pod_cpu % 1000 != 0) {  // ErrInvalidRequestedCPUs
+            o.status |= KG_ST_NUMA_CPU_BIND;
+            return;
+        }
+        cpu_bind = true;
+    }
     // filterAmplifiedCPUs (plugin.go:461-498): a cpuset-binding pod's request is amplified too
     if (pod_cpu != 0 && amp) {
         int64_t requested = nv<OV>(n, ov, N_REQ_CPU);
@@ -421,10 +430,39 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             return;
         }
     }
-    // the cpuset allocation (cpu_accumulator.go) runs on the host (plugin.go:396-440)
-    if (cpu_bind) {
-        o.status |= KG_ST_UNSUPPORTED;
-        return;
+    if (cpu_bind) {  // plugin.go:396-440
+        if (zr->cpu_topo < 0) {
+            o.status |= KG_ST_NUMA_CPU_TOPO;
+            return;
+        }
+        const uint32_t cpu_pol = (p.flags >> KG_POD_CPU_POLICY_SHIFT) & 3u;
+        const bool pod_required = (p.flags & KG_POD_CPU_REQUIRED) != 0;
+        uint32_t required = pod_required ? cpu_pol : KG_CPU_BIND_NONE;
+        if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KG_CPU_BIND_FULL_PCPUS;
+        else if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KG_CPU_BIND_SPREAD_BY_PCPUS;
+        const int64_t needed = pod_cpu / 1000;
+        const int64_t cpc = (zr->cpu_meta >> CPU_META_CPC_SHIFT) & 15u;
+        if ((pod_required && cpu_pol != required) || (required == KG_CPU_BIND_FULL_PCPUS && (cpc == 0 || needed % cpc != 0))) {
+            o.status |= KG_ST_NUMA_CPU_BIND;  // ErrCPUBindPolicyConflict / ErrSMTAlignmentError
+            return;
+        }
+        if (pol != KG_NUMA_NONE) {  // cpusets inside NUMA hints (resource_manager.go:357-499): host path
+            o.status |= KG_ST_UNSUPPORTED;
+            return;
+        }
+        if (required != KG_CPU_BIND_NONE) {
+            // tryAllocateFromNode: the required policy's CPUs (filterCPUsByRequiredCPUBindPolicy) must cover the
+            // pod; takeCPUs then always succeeds on them and the result satisfies the policy
+            const int64_t have = required == KG_CPU_BIND_FULL_PCPUS ? zr->cpu_free_full : zr->cpu_free_cores;
+            if (needed > have) {
+                o.status |= KG_ST_NUMA_CPUS;
+                return;
+            }
+        } else if (needed > zr->cpu_free) {
+            // no Filter check: the Reserve would fail (ErrNotEnoughCPUs) and the reference retries the pod
+            o.status |= KG_ST_UNSUPPORTED;
+            return;
+        }
     }
     const double rcp_cpu = as_f64(n[N_RCP_CPU]), rcp_mem = as_f64(n[N_RCP_MEM]);
     const bool most = (c.most & MOST_NUMA) != 0;
@@ -506,11 +544,13 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
                                      zr->rcp_mem[best]);
         return;
     }
-    // policy None: scoreWithAmplifiedCPUs
+    // policy None: scoreWithAmplifiedCPUs; a cpuset-binding pod's own request is amplified (getResourceOptions,
+    // plugin.go:772-778)
     if constexpr (!SCORE) return;
     int64_t req_cpu = nv<OV>(n, ov, N_REQ_CPU);
     if (pod_cpu != 0 && amp) req_cpu = req_cpu - n[N_CPUSET] + n[N_AMP_CPUSET];
-    o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], req_cpu + pod_cpu, rcp_cpu,
+    const int64_t own_cpu = (cpu_bind && amp) ? (int64_t)ceil(__dmul_rn((double)pod_cpu, zr->amp_ratio)) : pod_cpu;
+    o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], req_cpu + own_cpu, rcp_cpu,
                                  n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
 }
 

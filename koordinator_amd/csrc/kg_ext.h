@@ -487,8 +487,9 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
         ov.num_pods = v->num_pods;
         b = eval_pair<EXACT, true, TOPO, SCORE>(c, n, zr, p, &ov);
         const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u;
-        if ((c.plugins & KG_PLUGIN_NUMA) && node_pol != KG_NUMA_NONE && !(p.flags & KG_POD_NUMA_SKIP))
-            b.status = (b.status & ~(uint32_t)KG_ST_NUMA_MASK) | KG_ST_UNSUPPORTED;  // NUMA restore: host path
+        const bool binds = (p.flags & KG_POD_CPU_BIND) || ((zr->cpu_meta >> CPU_META_BIND_SHIFT) & 3u);
+        if ((c.plugins & KG_PLUGIN_NUMA) && (node_pol != KG_NUMA_NONE || binds) && !(p.flags & KG_POD_NUMA_SKIP))
+            b.status = (b.status & ~(uint32_t)KG_ST_NUMA_MASK) | KG_ST_UNSUPPORTED;  // NUMA / cpuset restore: host path
     } else {
         b = eval_pair<EXACT, false, TOPO, SCORE>(c, n, zr, p);
     }

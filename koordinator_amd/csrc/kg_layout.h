@@ -12,6 +12,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include "../../include/koordgpu.h"
+
 #if defined(__HIPCC__)
 #define KG_HD __host__ __device__
 #else
@@ -119,7 +121,46 @@ struct alignas(64) ZoneRec {
     uint32_t status;  // NUMANodeSharedStatus, 2 bits per zone (0 idle, 1 single, 2 shared)
     uint32_t pad_;
     double amp_ratio;  // cpu amplification ratio (filterAmplifiedCPUs amplifies a cpuset-binding pod's request)
+    // cpuset binding (kg_cpuset.h): topology index (-1: none), packed meta (CPU_META_*), and the counts the
+    // Filter compares numCPUsNeeded with, derived from the node's kg_cpu_alloc (cpu_counts)
+    int32_t cpu_topo;
+    uint32_t cpu_meta;
+    int32_t cpu_free;        // CPUs with RefCount < maxRefCount (getAvailableCPUs)
+    int32_t cpu_free_full;   // of those, the CPUs of cores whose every CPU is free (required FullPCPUs)
+    int32_t cpu_free_cores;  // cores with a free CPU (required SpreadByPCPUs: one CPU per core)
+    int32_t cpu_allocated;   // CPUs with RefCount > 0 (cpuset_alloc_milli / 1000)
 };
+static_assert(sizeof(ZoneRec) == 640, "the cpuset fields live in ZoneRec's tail padding");
+// ZoneRec.cpu_meta: bits 0-7 maxRefCount, 8-9 node CPU bind policy (KG_NODE_CPU_BIND_*), 10 NUMA allocate
+// strategy, 11-14 CPUs per core
+constexpr uint32_t CPU_META_BIND_SHIFT = 8, CPU_META_STRATEGY_SHIFT = 10, CPU_META_CPC_SHIFT = 11;
+
+// The Filter's view of a node's allocated CPUs (ZoneRec.cpu_free / cpu_free_full / cpu_free_cores /
+// cpu_allocated), recomputed on the host at upload and on the device after a cpuset Reserve.
+KG_HD inline void cpu_counts(const kg_cpu_topo& t, const kg_cpu_alloc* a, int max_ref, ZoneRec& z) {
+    int free_core[KG_MAX_CPUS];
+    for (int k = 0; k < t.n_cores; k++) free_core[k] = 0;
+    int fr = 0, al = 0;
+    for (int c = 0; c < t.n_cpus; c++) {
+        const int ref = a ? a->ref[c] : 0;
+        if (ref < max_ref) {
+            fr++;
+            free_core[t.core[c]]++;
+        }
+        al += ref > 0;
+    }
+    // filterCPUsByRequiredCPUBindPolicy counts a core for FullPCPUs when its free CPUs number CPUsPerCore()
+    const int cpc = t.n_cores ? t.n_cpus / t.n_cores : 0;
+    int full = 0, cores = 0;
+    for (int k = 0; k < t.n_cores; k++) {
+        full += free_core[k] == cpc ? cpc : 0;
+        cores += free_core[k] > 0;
+    }
+    z.cpu_free = fr;
+    z.cpu_free_full = full;
+    z.cpu_free_cores = cores;
+    z.cpu_allocated = al;
+}
 
 // Magnitude bound of the float64 fast path: operands below 2^44 keep 100 * headroom below 2^51
 // (exact) and make the upward-rounded reciprocal's quotient exact after truncation.
@@ -169,6 +210,8 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
     // Restricted / BestEffort nodes run the general NUMA topology manager on the integer path
     const uint32_t pol0 = (f >> F_NUMA_POLICY_SHIFT) & 15u;
     big = big || pol0 == 1u /* KG_NUMA_BEST_EFFORT */ || pol0 == 2u /* KG_NUMA_RESTRICTED */;
+    // a node CPU bind policy makes every pod with a cpu request bind cpusets there (util.go:121-138)
+    big = big || ((z.cpu_meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
     if (big) f |= F_BIG;
     v[N_FLAGS] = (int64_t)(((uint64_t)v[N_FLAGS] & 0xFFFFFFFF00000000ull) | f);
     auto fit = [](int64_t x) { return kg_bits(x100(x < 0 ? 0 : x)); };

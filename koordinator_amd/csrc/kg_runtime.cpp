@@ -102,11 +102,19 @@ struct kg_snap {
         NodeRec* nodes = nullptr;
         ZoneRec* zones = nullptr;
         DevRec* dev = nullptr;
+        kg_cpu_alloc* cpu = nullptr;
         QuotaState* q = nullptr;
         uint32_t nq = 0;
         bool valid = false, views_stale = false;
     } ck, bk;
     void invalidate_saved() { ck.valid = bk.valid = false; }
+    // cpuset binding: CPU topology table, per-record allocations (device order, like h_dev)
+    kg_cpu_topo* d_cpu_topos = nullptr;
+    uint32_t n_cpu_topos = 0;
+    kg_cpu_alloc* d_cpu_alloc = nullptr;
+    std::vector<kg_cpu_alloc> h_cpu_alloc;
+    bool has_cpu = false;   // the snapshot carries CPU topologies
+    bool node_bind = false; // some node has a CPU bind policy (every pod with a cpu request binds there)
     bool ext() const { return (cfg.plugins & KG_PLUGIN_EXT) != 0; }
     ExtDev ext_dev() const {
         ExtDev e{};
@@ -152,6 +160,9 @@ struct kg_pods {
     size_t gather_cap = 0;
     bool fast_ok = false;  // every value below FAST_LIMIT and no pod NUMA policy
     bool pod_policy = false;  // some pod carries its own NUMA policy
+    bool any_cpu_bind = false;  // some pod binds cpusets (KG_POD_CPU_BIND)
+    std::vector<uint32_t> h_flags;  // host copies for argument checks (kg_forget of a cpuset pod)
+    std::vector<int64_t> h_req_cpu;
     // config-5 columns and scratch
     int64_t* d_dev_req = nullptr;     // [cap][KG_DEV_R]
     uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32): 5 x cap
@@ -449,6 +460,29 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     }
     zr->status = COL(s->numa_zone_status, i);
     zr->amp_ratio = ratio > 1 ? ratio : 1.0;
+    zr->cpu_topo = -1;
+    zr->cpu_meta = 1u;
+    if (s->cpu_topo && s->cpu_topos) {
+        const int32_t ti = s->cpu_topo[i];
+        const uint32_t mr = s->cpu_max_ref ? std::max<uint32_t>(1u, s->cpu_max_ref[i]) : 1u;
+        const uint32_t nb = s->cpu_bind_policy ? s->cpu_bind_policy[i] : 0u;
+        const uint32_t sg = s->cpu_strategy ? s->cpu_strategy[i] : 0u;
+        if (ti >= (int32_t)s->n_cpu_topos || nb > 2 || sg > 1 || mr > 255)
+            return fail(ctx, KG_INVALID_ARG, "node %u: CPU topology %d / bind policy %u / strategy %u", i, ti, nb, sg);
+        uint32_t cpc = 0;
+        if (ti >= 0) {
+            const kg_cpu_topo& t = s->cpu_topos[ti];
+            if (t.n_sockets && t.n_nodes && t.n_cores && t.n_cpus) {  // CPUTopology.IsValid
+                zr->cpu_topo = ti;
+                cpc = t.n_cpus / t.n_cores;
+                cpu_counts(t, s->cpu_alloc ? &s->cpu_alloc[i] : nullptr, (int)mr, *zr);
+            }
+        }
+        zr->cpu_meta = mr | nb << CPU_META_BIND_SHIFT | sg << CPU_META_STRATEGY_SHIFT | cpc << CPU_META_CPC_SHIFT;
+        if (zr->cpu_topo >= 0 && v[N_CPUSET] != 1000 * (int64_t)zr->cpu_allocated)
+            return fail(ctx, KG_INVALID_ARG, "node %u: cpuset_alloc_milli %lld != 1000 x %d allocated CPUs", i,
+                        (long long)v[N_CPUSET], zr->cpu_allocated);
+    }
     if (zr->status >> (2 * KG_MAX_ZONES)) return fail(ctx, KG_INVALID_ARG, "node %u: zone status 0x%x", i, zr->status);
     derive_node(*rec, *zr);
     return KG_OK;
@@ -570,10 +604,12 @@ void touch_views(kg_snap* s, uint32_t node) {
 
 
 // Place records (indexed by snapshot index) in device order: class 0 then class 1, each ascending.
-void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>& zrs, std::vector<DevRec>* devs = nullptr) {
+void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>& zrs, std::vector<DevRec>* devs = nullptr,
+                   std::vector<kg_cpu_alloc>* cpus = nullptr) {
     const uint32_t n = s->n;
     s->pos.resize(n);
     if (devs) s->h_dev.resize(n);
+    if (cpus) s->h_cpu_alloc.resize(n);
     uint32_t n0 = 0;
     for (uint32_t i = 0; i < n; i++) n0 += node_class(recs[i]) == 0;
     uint32_t a = 0, b = n0;
@@ -583,6 +619,7 @@ void place_records(kg_snap* s, std::vector<NodeRec>& recs, std::vector<ZoneRec>&
         s->h_nodes[p] = recs[i];
         s->h_zones[p] = zrs[i];
         if (devs) s->h_dev[p] = (*devs)[i];
+        if (cpus) s->h_cpu_alloc[p] = (*cpus)[i];
     }
     s->n0 = n0;
     count_topo(s);
@@ -730,6 +767,28 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
     return KG_OK;
 }
 
+static const char* cpu_topo_problem(const kg_cpu_topo& t);
+
+// Replace the CPU topology table (kg_node_columns.cpu_topos) on the device.
+static kg_status upload_cpu_topos(kg_snap* s, const kg_node_columns* cols, uint32_t n_rows) {
+    kg_ctx* ctx = s->ctx;
+    for (uint32_t t = 0; t < cols->n_cpu_topos; t++)
+        if (const char* why = cpu_topo_problem(cols->cpu_topos[t])) return fail(ctx, KG_UNSUPPORTED, "CPU topology %u: %s", t, why);
+    if (cols->n_cpu_topos > s->n_cpu_topos || !s->d_cpu_topos) {
+        hipFree(s->d_cpu_topos);
+        s->d_cpu_topos = nullptr;
+        HIP_TRY(ctx, hipMalloc(&s->d_cpu_topos, sizeof(kg_cpu_topo) * std::max<uint32_t>(cols->n_cpu_topos, 1)));
+    }
+    if (cols->n_cpu_topos)
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_cpu_topos, cols->cpu_topos, sizeof(kg_cpu_topo) * cols->n_cpu_topos,
+                                    hipMemcpyHostToDevice, ctx->stream));
+    s->n_cpu_topos = std::max(s->n_cpu_topos, cols->n_cpu_topos);
+    if (!s->d_cpu_alloc) HIP_TRY(ctx, hipMalloc(&s->d_cpu_alloc, sizeof(kg_cpu_alloc) * std::max<uint32_t>(s->n, 1)));
+    s->has_cpu = true;
+    for (uint32_t i = 0; cols->cpu_bind_policy && i < n_rows; i++) s->node_bind |= cols->cpu_bind_policy[i] != 0;
+    return KG_OK;
+}
+
 kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
     if (!s || !cols) return KG_INVALID_ARG;
     kg_ctx* ctx = s->ctx;
@@ -745,12 +804,28 @@ kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
         recs[i].v[N_RSV_CLASSES] = (int64_t)s->cls_mask[i];
         if (dev) build_dev(cols, i, &devs[i]);
     }
-    place_records(s, recs, zrs, dev ? &devs : nullptr);
+    const bool cpu = cols->cpu_topo && cols->cpu_topos;
+    std::vector<kg_cpu_alloc> cpus(cpu ? s->n : 0);
+    for (uint32_t i = 0; cpu && i < s->n; i++) {
+        if (cols->cpu_alloc) cpus[i] = cols->cpu_alloc[i];
+        else std::memset(&cpus[i], 0, sizeof(kg_cpu_alloc));
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    s->node_bind = false;
+    if (cpu) {
+        kg_status st = upload_cpu_topos(s, cols, s->n);
+        if (st != KG_OK) return st;
+    } else {
+        s->has_cpu = false;
+    }
+    place_records(s, recs, zrs, dev ? &devs : nullptr, cpu ? &cpus : nullptr);
     HIP_TRY(ctx, hipMemcpyAsync(s->d_pos, s->pos.data(), sizeof(uint32_t) * s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
     if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, s->h_dev.data(), sizeof(DevRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+    if (cpu)
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_cpu_alloc, s->h_cpu_alloc.data(), sizeof(kg_cpu_alloc) * s->n, hipMemcpyHostToDevice,
+                                    ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->uploaded = true;
@@ -781,27 +856,50 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
         moved |= node_class(recs[k]) != (s->pos[rows[k]] < s->n0 ? 0u : 1u);
     }
     if (moved && s->n_views) return fail(ctx, KG_UNSUPPORTED, "row update moves a record while reservation views are uploaded");
+    const bool cpu = s->has_cpu;
+    if (cpu && !(cols->cpu_topo && cols->cpu_topos))
+        return fail(ctx, KG_INVALID_ARG, "the snapshot carries CPU topologies: row updates must carry them too");
+    std::vector<kg_cpu_alloc> cpus(cpu ? n : 0);
+    for (uint32_t k = 0; cpu && k < n; k++) {
+        if (cols->cpu_alloc) cpus[k] = cols->cpu_alloc[k];
+        else std::memset(&cpus[k], 0, sizeof(kg_cpu_alloc));
+    }
+    if (cpu) {
+        kg_status st = upload_cpu_topos(s, cols, n);
+        if (st != KG_OK) return st;
+    }
     if (moved) {
         // device records carry Assume state: read them back, replace the rows, regroup, re-upload
         HIP_TRY(ctx, hipMemcpyAsync(s->h_nodes.data(), s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->h_zones.data(), s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
         if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->h_dev.data(), s->d_dev, sizeof(DevRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
+        if (cpu) {
+            s->h_cpu_alloc.resize(s->n);
+            HIP_TRY(ctx, hipMemcpyAsync(s->h_cpu_alloc.data(), s->d_cpu_alloc, sizeof(kg_cpu_alloc) * s->n,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+        }
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         std::vector<NodeRec> all(s->n);
         std::vector<ZoneRec> allz(s->n);
         std::vector<DevRec> alld(dev ? s->n : 0);
+        std::vector<kg_cpu_alloc> allc(cpu ? s->n : 0);
         for (uint32_t p = 0; p < s->n; p++) {
             const uint32_t i = node_index(s->h_nodes[p]);
             all[i] = s->h_nodes[p];
             allz[i] = s->h_zones[p];
             if (dev) alld[i] = s->h_dev[p];
+            if (cpu) allc[i] = s->h_cpu_alloc[p];
         }
         for (uint32_t k = 0; k < n; k++) {
             all[rows[k]] = recs[k];
             allz[rows[k]] = zrs[k];
             if (dev) alld[rows[k]] = devs[k];
+            if (cpu) allc[rows[k]] = cpus[k];
         }
-        place_records(s, all, allz, dev ? &alld : nullptr);
+        place_records(s, all, allz, dev ? &alld : nullptr, cpu ? &allc : nullptr);
+        if (cpu)
+            HIP_TRY(ctx, hipMemcpyAsync(s->d_cpu_alloc, s->h_cpu_alloc.data(), sizeof(kg_cpu_alloc) * s->n,
+                                        hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_pos, s->pos.data(), sizeof(uint32_t) * s->n, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
@@ -836,6 +934,11 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
                 std::memcpy(o + sizeof(NodeRec) + sizeof(ZoneRec), &devs[k], sizeof(DevRec));
             }
             hpos[k] = p;
+            if (cpu) {
+                s->h_cpu_alloc[p] = cpus[k];
+                HIP_TRY(ctx, hipMemcpyAsync(s->d_cpu_alloc + p, &s->h_cpu_alloc[p], sizeof(kg_cpu_alloc),
+                                            hipMemcpyHostToDevice, ctx->stream));
+            }
         }
         HIP_TRY(ctx, hipMemcpyAsync(s->d_stage, h, rb * n, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_stage_pos, hpos, sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
@@ -864,6 +967,9 @@ kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
     std::vector<NodeRec> h(s->n);
     std::vector<ZoneRec> z(s->n);
     std::vector<DevRec> dv(s->d_dev ? s->n : 0);
+    std::vector<kg_cpu_alloc> ca(s->d_cpu_alloc && s->has_cpu ? s->n : 0);
+    if (!ca.empty())
+        HIP_TRY(ctx, hipMemcpyAsync(ca.data(), s->d_cpu_alloc, sizeof(kg_cpu_alloc) * s->n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(h.data(), s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(z.data(), s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
     if (s->d_dev) HIP_TRY(ctx, hipMemcpyAsync(dv.data(), s->d_dev, sizeof(DevRec) * s->n, hipMemcpyDeviceToHost, ctx->stream));
@@ -891,6 +997,11 @@ kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
         for (int zz = 0; zz < KG_MAX_ZONES; zz++) {
             if (o->zone_cpu_used[zz]) o->zone_cpu_used[zz][i] = zr.cpu_used[zz];
             if (o->zone_mem_used[zz]) o->zone_mem_used[zz][i] = zr.mem_used[zz];
+        }
+        if (o->cpuset_alloc_milli) o->cpuset_alloc_milli[i] = v[N_CPUSET];
+        if (o->cpu_alloc) {
+            if (!ca.empty()) o->cpu_alloc[i] = ca[pp];
+            else std::memset(&o->cpu_alloc[i], 0, sizeof(kg_cpu_alloc));
         }
         if (o->dev_free && s->d_dev)
             for (int r = 0; r < DEV_R; r++)
@@ -922,8 +1033,11 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
         hipFree(k->nodes);
         hipFree(k->zones);
         hipFree(k->dev);
+        hipFree(k->cpu);
         hipFree(k->q);
     }
+    hipFree(s->d_cpu_topos);
+    hipFree(s->d_cpu_alloc);
     delete s;
     return KG_OK;
 }
@@ -1031,8 +1145,16 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         fast &= pol == KG_NUMA_NONE;
         any_pol |= pol != KG_NUMA_NONE;
     }
-    p->fast_ok = fast;
+    bool any_bind = false;
+    for (uint32_t j = 0; j < n; j++) any_bind |= (f[j] & KG_POD_CPU_BIND) != 0;
+    // cpuset-binding pods take the integer path (the fast block has no CPU counts); nodes with a CPU bind
+    // policy are F_BIG and take it for every pod
+    p->fast_ok = fast && !any_bind;
     p->pod_policy = any_pol;
+    p->any_cpu_bind = any_bind;
+    p->h_flags.assign(f.begin(), f.begin() + n);
+    p->h_req_cpu.assign(n, 0);
+    for (uint32_t j = 0; j < n; j++) p->h_req_cpu[j] = cols->req_cpu ? cols->req_cpu[j] : 0;
     // config-5 columns (absent columns: no GPU request, no quota, no reservation class)
     std::vector<int64_t> dreq((size_t)DEV_R * std::max<uint32_t>(n, 1), 0);
     std::vector<uint32_t> xc((size_t)5 * std::max<uint32_t>(n, 1), 0);
@@ -1569,6 +1691,19 @@ kg_status kg_result_status(kg_pods* p, uint32_t* out) {
 namespace {
 constexpr uint32_t REPLAY_G = 256;  // replay steps per captured graph
 
+// pod binds cpusets on (local) node: its Reserve allocated CPUs the Unreserve would have to know
+bool cpuset_bound(const kg_snap* s, const kg_pods* p, uint32_t pod, uint32_t node) {
+    if (!s->has_cpu || !(s->kcfg.plugins & KG_PLUGIN_NUMA) || pod >= p->h_flags.size()) return false;
+    const ZoneRec& z = s->h_zones[s->pos[node]];
+    const bool node_bind = ((z.cpu_meta >> CPU_META_BIND_SHIFT) & 3u) != 0;
+    return z.cpu_topo >= 0 && ((p->h_flags[pod] & KG_POD_CPU_BIND) || (node_bind && p->h_req_cpu[pod] != 0));
+}
+
+// cpuset Reserves happen in this (snapshot, batch): the replay runs the device accumulator between steps
+bool cpuset_active(const kg_snap* s, const kg_pods* p) {
+    return s->has_cpu && (s->kcfg.plugins & KG_PLUGIN_NUMA) && (p->any_cpu_bind || s->node_bind);
+}
+
 std::vector<uint8_t> replay_key(const kg_snap* s, const kg_pods* p, bool exact, bool reasons = false) {
     std::vector<uint8_t> k;
     auto put = [&k](const void* x, size_t n) { k.insert(k.end(), (const uint8_t*)x, (const uint8_t*)x + n); };
@@ -1581,6 +1716,11 @@ std::vector<uint8_t> replay_key(const kg_snap* s, const kg_pods* p, bool exact, 
     put(&s->kcfg, sizeof(s->kcfg));
     put(&p->n, sizeof(p->n));
     put(&exact, sizeof(exact));
+    const bool cs = cpuset_active(s, p);
+    put(&cs, sizeof(cs));
+    put(&s->d_cpu_alloc, sizeof(s->d_cpu_alloc));
+    put(&s->d_cpu_topos, sizeof(s->d_cpu_topos));
+    put(&s->d_pos, sizeof(s->d_pos));
     return k;
 }
 
@@ -1597,9 +1737,16 @@ kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     hipGraph_t graph = nullptr;
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
     hipError_t e = hipSuccess;
-    for (uint32_t t = 0; t < REPLAY_G && e == hipSuccess; t++)
-        e = launch_replay_step(s->d_nodes, s->d_zones, p->dev, p->n, s->n, s->base, s->kcfg, exact, p->d_step, t,
-                               p->d_winners, s->d_zsel, reasons ? p->d_reason : nullptr, ctx->stream);
+    const bool cs = cpuset_active(s, p);
+    for (uint32_t t = 0; t < REPLAY_G && e == hipSuccess; t++) {
+        // the previous pod's cpuset Reserve runs before the step that applies its other Reserves
+        if (cs)
+            e = launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, 0, 0,
+                                      p->d_winners, p->d_step, t, s->d_pos, s->base, ctx->stream);
+        if (e == hipSuccess)
+            e = launch_replay_step(s->d_nodes, s->d_zones, p->dev, p->n, s->n, s->base, s->kcfg, exact, p->d_step, t,
+                                   p->d_winners, s->d_zsel, reasons ? p->d_reason : nullptr, ctx->stream);
+    }
     if (e == hipSuccess) e = launch_bump(p->d_step, REPLAY_G, ctx->stream);
     hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
     if (e == hipSuccess) e = ec;
@@ -1734,7 +1881,7 @@ kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_tota
     const bool reasons = out_reason != nullptr;
     // window replay needs the changed-row bitmap in LDS; every config-3 plugin scores a pair from its own row.
     // The FitError diagnosis (out_reason) needs every node's status in each pod's cycle: one pod per launch.
-    const bool windows = !reasons && !force_step_replay() && s->n <= 32u * (uint32_t)RB_BITMAP_WORDS;
+    const bool windows = !reasons && !force_step_replay() && !cpuset_active(s, p) && s->n <= 32u * (uint32_t)RB_BITMAP_WORDS;
     st = windows ? rb_graph(s, p, exact) : replay_graph(s, p, exact, reasons);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
@@ -1786,6 +1933,9 @@ kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) {
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     touch_views(s, node);
+    if (s->has_cpu)
+        HIP_TRY(ctx, launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, pod,
+                                           s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, ctx->stream));
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], -1, 1, s->kcfg, force_exact(), nullptr, ctx->stream));
     s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
@@ -1800,6 +1950,7 @@ kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     if (zone >= KG_MAX_ZONES) return fail(ctx, KG_UNSUPPORTED, "Unreserve of a multi-zone NUMA allocation (zone code 0x%x)", zone);
+    if (cpuset_bound(s, p, pod, node)) return fail(ctx, KG_UNSUPPORTED, "Unreserve of a cpuset allocation");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     touch_views(s, node);
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
@@ -1813,6 +1964,7 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
     kg_ctx* ctx = s->ctx;
     if (s->cfg.plugins & KG_PLUGIN_RSV)
         return fail(ctx, KG_UNSUPPORTED, "replay with Reservation views (their restore changes with every placement)");
+    if (cpuset_active(s, p)) return fail(ctx, KG_UNSUPPORTED, "config-5 replay with cpuset-binding pods");
     kg_status st = check_ext(s);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -1873,6 +2025,9 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     touch_views(s, node);
+    if (sign > 0 && s->has_cpu)
+        HIP_TRY(ctx, launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, pod,
+                                           s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, ctx->stream));
     HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone, minors,
                                    sign, s->kcfg, force_exact(), p->d_aout, ctx->stream));
     s->gen++;
@@ -1892,6 +2047,8 @@ kg_status kg_assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int
 kg_status kg_forget_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone, uint32_t minors) {
     if (s && zone >= KG_MAX_ZONES)
         return fail(s->ctx, KG_UNSUPPORTED, "Unreserve of a multi-zone NUMA allocation (zone code 0x%x)", zone);
+    if (s && p && node < s->n && cpuset_bound(s, p, pod, node))
+        return fail(s->ctx, KG_UNSUPPORTED, "Unreserve of a cpuset allocation");
     return assume_ext(s, p, pod, node, zone, minors, -1, nullptr, nullptr);
 }
 
@@ -1962,6 +2119,7 @@ static kg_status save_state(kg_snap* s, kg_snap::Saved& k) {
         HIP_TRY(ctx, hipMalloc(&k.zones, sizeof(ZoneRec) * n));
         if (s->d_dev) HIP_TRY(ctx, hipMalloc(&k.dev, sizeof(DevRec) * n));
     }
+    if (s->d_cpu_alloc && !k.cpu) HIP_TRY(ctx, hipMalloc(&k.cpu, sizeof(kg_cpu_alloc) * n));
     if (k.nq < s->n_quotas || (s->n_quotas && !k.q)) {
         hipFree(k.q);
         k.q = nullptr;
@@ -1971,6 +2129,8 @@ static kg_status save_state(kg_snap* s, kg_snap::Saved& k) {
     HIP_TRY(ctx, hipMemcpyAsync(k.nodes, s->d_nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(k.zones, s->d_zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
     if (s->d_dev) HIP_TRY(ctx, hipMemcpyAsync(k.dev, s->d_dev, sizeof(DevRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
+    if (s->d_cpu_alloc)
+        HIP_TRY(ctx, hipMemcpyAsync(k.cpu, s->d_cpu_alloc, sizeof(kg_cpu_alloc) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
     if (s->n_quotas && s->d_qstate)
         HIP_TRY(ctx, hipMemcpyAsync(k.q, s->d_qstate, sizeof(QuotaState) * 2 * (size_t)s->n_quotas, hipMemcpyDeviceToDevice,
                                     ctx->stream));
@@ -1984,6 +2144,8 @@ static kg_status restore_state(kg_snap* s, kg_snap::Saved& k) {
     HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, k.nodes, sizeof(NodeRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, k.zones, sizeof(ZoneRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
     if (s->d_dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, k.dev, sizeof(DevRec) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
+    if (s->d_cpu_alloc && k.cpu)
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_cpu_alloc, k.cpu, sizeof(kg_cpu_alloc) * s->n, hipMemcpyDeviceToDevice, ctx->stream));
     if (k.nq && s->d_qstate)
         HIP_TRY(ctx, hipMemcpyAsync(s->d_qstate, k.q, sizeof(QuotaState) * 2 * (size_t)k.nq, hipMemcpyDeviceToDevice,
                                     ctx->stream));
@@ -2028,6 +2190,7 @@ kg_status kg_batch_schedule(kg_snap* s, kg_pods* p, const int32_t* plan_node, ui
     std::lock_guard<std::mutex> g(ctx->mu);
     if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views)
         return fail(ctx, KG_UNSUPPORTED, "batch schedule with Reservation views (a Reserve into a view changes its restore)");
+    if (cpuset_active(s, p)) return fail(ctx, KG_UNSUPPORTED, "batch schedule with cpuset-binding pods");
     if (s->ext()) {
         st = check_ext(s);
         if (st != KG_OK) return st;

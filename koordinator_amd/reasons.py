@@ -56,6 +56,9 @@ def plugin_reasons(bits: int, scalar_names=DEFAULT_SCALARS) -> dict:
         (abi.KG_ST_NUMA_NO_RES, "node(s) missing NUMA resources"),
         (abi.KG_ST_NUMA_ALIGN, "Unaligned NUMA Hint cause <hints>"),
         (abi.KG_ST_NUMA_UNSATISFIED, "Unsatisfied NUMA <resource>"),
+        (abi.KG_ST_NUMA_CPU_TOPO, "node(s) invalid CPU Topology"),
+        (abi.KG_ST_NUMA_CPU_BIND, "node(s) cpu bind policy conflicts / SMT alignment / invalid requested cpus"),
+        (abi.KG_ST_NUMA_CPUS, "not enough cpus available to satisfy request"),
     )
     for bit, msg in numa:
         if bits & bit:

@@ -301,6 +301,63 @@ def cluster(config: int):
     raise ValueError(config)
 
 
+CPU_SHAPES = ((1, 1, 16, 2), (2, 1, 16, 2), (2, 2, 12, 2), (2, 2, 8, 1))  # buildCPUTopologyForTest shapes
+
+
+def cpuset_cluster(n_nodes: int, n_pods: int, seed: int = 0, bind_frac: float = 0.3, node_bind_frac: float = 0.06,
+                   no_topo_frac: float = 0.08):
+    """A small cluster with cpuset binding: CPU topologies of CPU_SHAPES on most nodes, an
+    existing allocation per node (cpuset_alloc_milli = 1000 x allocated CPUs, RefCount up to maxRefCount 1 or
+    2, random exclusive policies), node CPU bind policies on a few nodes, both NUMA allocate strategies; pods
+    from pods() with a share turned into LSE/LSR cpuset pods (whole cores, Full/Spread policy, required or
+    preferred, random exclusive policy)."""
+    cfg, t, pt = small(n_nodes, n_pods, seed=seed, numa=True)
+    r = _rng(200 + seed, 7)
+    topos = [abi.cpu_topo_for_test(*sh) for sh in CPU_SHAPES]
+    n = n_nodes
+    ti = r.integers(0, len(topos), n).astype(np.int32)
+    ti[r.random(n) < no_topo_frac] = -1
+    max_ref = np.where(r.random(n) < 0.15, 2, 1).astype(np.uint8)
+    alloc = np.zeros((n, 2 * abi.KG_MAX_CPUS), np.uint8)
+    cs = np.zeros(n, np.int64)
+    for i in range(n):
+        if ti[i] < 0:
+            continue
+        nc = topos[ti[i]].n_cpus
+        k = int(r.integers(0, int(nc * 0.6) + 1))
+        k = min(k, int(t["req_cpu"][i] // 1000))
+        cpus = r.choice(nc, size=k, replace=False)
+        for c in cpus:
+            alloc[i, c] = 1 if max_ref[i] == 1 else int(r.integers(1, 3))
+            alloc[i, abi.KG_MAX_CPUS + c] = int(r.integers(0, 3))
+        cs[i] = 1000 * k
+    t["cpu_topo"] = ti
+    t["cpu_topos"] = abi.cpu_topos_array(topos)
+    t["cpu_alloc"] = alloc
+    t["cpu_max_ref"] = max_ref
+    nb = np.zeros(n, np.uint8)
+    u = r.random(n)
+    nb[u < node_bind_frac / 2] = abi.KG_NODE_CPU_BIND_FULL_PCPUS_ONLY
+    nb[(u >= node_bind_frac / 2) & (u < node_bind_frac)] = abi.KG_NODE_CPU_BIND_SPREAD_BY_PCPUS
+    t["cpu_bind_policy"] = nb
+    t["cpu_strategy"] = r.integers(0, 2, n).astype(np.uint8)
+    t["cpuset_alloc_milli"] = cs
+    # cpuset pods: prod pods with whole-core requests
+    m = len(pt["req_cpu"])
+    bind = (r.random(m) < bind_frac) & ((pt["flags"] & abi.KG_POD_PROD) != 0)
+    cores = r.choice([1, 2, 4, 6, 8, 16], m)
+    pt["req_cpu"] = np.where(bind, cores * 1000, pt["req_cpu"]).astype(np.int64)
+    pt["nz_cpu"] = np.where(bind, cores * 1000, pt["nz_cpu"]).astype(np.int64)
+    pol = r.integers(1, 3, m).astype(np.uint32)
+    req = r.random(m) < 0.35
+    excl = r.integers(0, 3, m).astype(np.uint32)
+    f = pt["flags"].astype(np.uint32)
+    f = np.where(bind, f | abi.KG_POD_CPU_BIND | (pol << abi.KG_POD_CPU_POLICY_SHIFT) |
+                 np.where(req, abi.KG_POD_CPU_REQUIRED, 0).astype(np.uint32) | (excl << abi.KG_POD_CPU_EXCL_SHIFT), f)
+    pt["flags"] = f.astype(np.uint32)
+    return cfg, t, pt
+
+
 def small(n_nodes: int, n_pods: int, seed: int = 0, numa: bool = True, scale: float = 1.0) -> tuple:
     """Small synthetic cluster for parity tests."""
     cfg: SchedulerConfig = bench_profile(numa=numa)

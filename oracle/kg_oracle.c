@@ -485,6 +485,129 @@ static uint32_t numa_code_mask(int32_t code) {
     return code >= 0x40 ? (uint32_t)code & 0xFu : 1u << code;
 }
 
+/* ---- cpuset binding (plugin.go:396-440, resource_manager.go:357-499,659-722) ---------------------- */
+
+static const kg_cpu_topo* cpu_topology(const kg_node_columns* n, uint32_t i) {
+    if (!n->cpu_topo || !n->cpu_topos || n->cpu_topo[i] < 0 || (uint32_t)n->cpu_topo[i] >= n->n_cpu_topos) return NULL;
+    const kg_cpu_topo* t = &n->cpu_topos[n->cpu_topo[i]];
+    /* CPUTopology.IsValid (cpu_topology.go:79-81) */
+    return (t->n_sockets && t->n_nodes && t->n_cores && t->n_cpus) ? t : NULL;
+}
+
+static int cpu_max_ref(const kg_node_columns* n, uint32_t i) {
+    const int m = n->cpu_max_ref ? n->cpu_max_ref[i] : 1;
+    return m < 1 ? 1 : m;
+}
+
+/* NodeAllocation.getAvailableCPUs (node_allocation.go:192-220), no reserved / preferred CPUs */
+static void cpu_available(const kg_node_columns* n, uint32_t i, const kg_cpu_topo* t, uint64_t m[4]) {
+    memset(m, 0, 4 * sizeof(uint64_t));
+    const int mr = cpu_max_ref(n, i);
+    for (int c = 0; c < t->n_cpus; c++) {
+        const int ref = n->cpu_alloc ? n->cpu_alloc[i].ref[c] : 0;
+        if (ref < mr) m[c >> 6] |= 1ull << (c & 63);
+    }
+}
+
+static int mask_count(const uint64_t m[4]) {
+    return __builtin_popcountll(m[0]) + __builtin_popcountll(m[1]) + __builtin_popcountll(m[2]) + __builtin_popcountll(m[3]);
+}
+
+/* filterCPUsByRequiredCPUBindPolicy (resource_manager.go:659-699): FullPCPUs keeps the cores whose every CPU
+ * is available, SpreadByPCPUs the smallest available CPU of each core */
+static void cpu_filter_required(const kg_cpu_topo* t, uint32_t policy, uint64_t m[4]) {
+    const int cpc = t->n_cpus / t->n_cores;
+    int cnt[KG_MAX_CPUS] = {0}, first[KG_MAX_CPUS];
+    for (int k = 0; k < KG_MAX_CPUS; k++) first[k] = -1;
+    for (int c = 0; c < t->n_cpus; c++)
+        if ((m[c >> 6] >> (c & 63)) & 1ull) {
+            cnt[t->core[c]]++;
+            if (first[t->core[c]] < 0) first[t->core[c]] = c;
+        }
+    uint64_t o[4] = {0, 0, 0, 0};
+    for (int c = 0; c < t->n_cpus; c++) {
+        if (!((m[c >> 6] >> (c & 63)) & 1ull)) continue;
+        const int keep = policy == KG_CPU_BIND_FULL_PCPUS ? cnt[t->core[c]] == cpc : first[t->core[c]] == c;
+        if (keep) o[c >> 6] |= 1ull << (c & 63);
+    }
+    memcpy(m, o, sizeof(o));
+}
+
+/* the pod's resolved bind policy on node i (getCPUBindPolicy, util.go:101-119): required or preferred, the
+ * node policy overriding both; *required tells whether it is required */
+static uint32_t cpu_bind_policy(const kg_pod_columns* p, uint32_t j, uint32_t node_bind, int* required) {
+    const uint32_t pol = (p->flags[j] >> KG_POD_CPU_POLICY_SHIFT) & 3u;
+    const int pod_req = (p->flags[j] & KG_POD_CPU_REQUIRED) != 0;
+    *required = pod_req;
+    if (pod_req) return pol;
+    if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) {
+        *required = 1;
+        return KG_CPU_BIND_SPREAD_BY_PCPUS;
+    }
+    if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) {
+        *required = 1;
+        return KG_CPU_BIND_FULL_PCPUS;
+    }
+    return pol;
+}
+
+/* resourceManager.allocateCPUSet on NUMA policy None (no hint): 0 and the CPUs, or -1 */
+static int cpuset_allocate(const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j, uint32_t node_bind,
+                           uint64_t out[4]) {
+    const kg_cpu_topo* t = cpu_topology(n, i);
+    if (!t) return -1;
+    int required;
+    const uint32_t bind = cpu_bind_policy(p, j, node_bind, &required);
+    uint64_t avail[4];
+    cpu_available(n, i, t, avail);
+    if (required) cpu_filter_required(t, bind, avail);
+    const int needed = (int)(p->req_cpu[j] / 1000);
+    if (mask_count(avail) < needed) return -1; /* ErrNotEnoughCPUs */
+    const uint32_t excl = (p->flags[j] >> KG_POD_CPU_EXCL_SHIFT) & 3u;
+    const uint32_t strategy = n->cpu_strategy ? n->cpu_strategy[i] : KG_NUMA_MOST_ALLOCATED;
+    if (kgo_take_cpus(t, cpu_max_ref(n, i), avail, n->cpu_alloc ? &n->cpu_alloc[i] : NULL, needed, (int)bind, (int)excl,
+                      (int)strategy, out))
+        return -1;
+    if (required) { /* satisfiedRequiredCPUBindPolicy (resource_manager.go:701-722) */
+        int cores = 0;
+        uint8_t seen[KG_MAX_CPUS] = {0};
+        for (int c = 0; c < t->n_cpus; c++)
+            if (((out[c >> 6] >> (c & 63)) & 1ull) && !seen[t->core[c]]) {
+                seen[t->core[c]] = 1;
+                cores++;
+            }
+        const int size = mask_count(out), cpc = t->n_cpus / t->n_cores;
+        if (bind == KG_CPU_BIND_FULL_PCPUS ? cores * cpc != size : cores != size) return -1;
+    }
+    return 0;
+}
+
+/* the cpuset part of Filter for a pod that binds CPUs on node i (plugin.go:396-440) */
+static uint32_t cpuset_filter(const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j, uint32_t policy,
+                              uint32_t node_bind) {
+    const kg_cpu_topo* t = cpu_topology(n, i);
+    if (!t) return KG_ST_NUMA_CPU_TOPO; /* ErrInvalidCPUTopology */
+    const uint32_t pod_pol = (p->flags[j] >> KG_POD_CPU_POLICY_SHIFT) & 3u;
+    const int pod_req = (p->flags[j] & KG_POD_CPU_REQUIRED) != 0;
+    uint32_t required = pod_req ? pod_pol : KG_CPU_BIND_NONE;
+    if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KG_CPU_BIND_FULL_PCPUS;
+    else if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KG_CPU_BIND_SPREAD_BY_PCPUS;
+    if (pod_req && pod_pol != required) return KG_ST_NUMA_CPU_BIND; /* ErrCPUBindPolicyConflict */
+    const int64_t needed = p->req_cpu[j] / 1000;
+    if (required == KG_CPU_BIND_FULL_PCPUS && needed % (t->n_cpus / t->n_cores) != 0)
+        return KG_ST_NUMA_CPU_BIND; /* ErrSMTAlignmentError */
+    if (policy != KG_NUMA_NONE) return KG_ST_UNSUPPORTED; /* cpusets inside NUMA hints: host path */
+    uint64_t out[4];
+    if (required != KG_CPU_BIND_NONE) {
+        if (cpuset_allocate(n, i, p, j, node_bind, out)) return KG_ST_NUMA_CPUS; /* tryAllocateFromNode */
+        return 0;
+    }
+    /* no allocation in Filter; the Reserve's allocateCPUSet fails when the node has too few CPUs left, which
+     * the device path hands back to the host */
+    if (cpuset_allocate(n, i, p, j, node_bind, out)) return KG_ST_UNSUPPORTED;
+    return 0;
+}
+
 /* Filter (plugin.go:363-459) + Score (scoring.go:67-151,153-199) of one pair. */
 static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t i, const kgo_over* ov,
                           const kg_pod_columns* p, uint32_t j, int64_t* score_out, int32_t* zone_out) {
@@ -494,9 +617,15 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
     int conflict;
     uint32_t policy = numa_merge_policy(n->numa_policy[i], p->numa_policy[j], &conflict);
     if (conflict) return KG_ST_NUMA_CONFLICT; /* plugin.go:377-381 */
-    const int cpu_bind = (p->flags[j] & KG_POD_CPU_BIND) != 0;
+    int cpu_bind = (p->flags[j] & KG_POD_CPU_BIND) != 0;
     double ratio = n->cpu_amp_ratio[i];
     int64_t pod_cpu = p->req_cpu[j];
+    /* requestCPUBind (util.go:121-138): a node CPU bind policy binds every pod with a cpu request */
+    const uint32_t node_bind = n->cpu_bind_policy ? n->cpu_bind_policy[i] : KG_NODE_CPU_BIND_NONE;
+    if (!cpu_bind && pod_cpu != 0 && node_bind != KG_NODE_CPU_BIND_NONE) {
+        if (pod_cpu % 1000 != 0) return KG_ST_NUMA_CPU_BIND; /* ErrInvalidRequestedCPUs */
+        cpu_bind = 1;
+    }
     /* filterAmplifiedCPUs: plugin.go:461-498; a cpuset-binding pod's request is amplified too (:477-479) */
     if (pod_cpu != 0 && ratio > 1) {
         int64_t allocated = n->cpuset_alloc_milli[i];
@@ -508,8 +637,10 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
         const int64_t need = cpu_bind ? kgo_amplify(pod_cpu, ratio) : pod_cpu;
         if (need > n->alloc_cpu[i] - requested) return KG_ST_NUMA_AMP_CPU;
     }
-    /* the cpuset allocation itself (cpu_accumulator.go) is the host's: plugin.go:396-440 */
-    if (cpu_bind) return KG_ST_UNSUPPORTED;
+    if (cpu_bind) {
+        const uint32_t st = cpuset_filter(n, i, p, j, policy, node_bind);
+        if (st) return st;
+    }
     if (policy == KG_NUMA_NONE) {
         /* scoreWithAmplifiedCPUs, scoring.go:132-151 */
         int64_t req_cpu = N_REQ_CPU(n, i, ov);
@@ -517,7 +648,9 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
             int64_t allocated = n->cpuset_alloc_milli[i];
             req_cpu = req_cpu - allocated + kgo_amplify(allocated, ratio);
         }
-        *score_out = numa_node_score(c, n->alloc_cpu[i], req_cpu + pod_cpu, n->alloc_mem[i],
+        /* getResourceOptions (plugin.go:772-778): a cpuset-binding pod's request is amplified */
+        const int64_t own = cpu_bind && ratio > 1 ? kgo_amplify(pod_cpu, ratio) : pod_cpu;
+        *score_out = numa_node_score(c, n->alloc_cpu[i], req_cpu + own, n->alloc_mem[i],
                                      N_REQ_MEM(n, i, ov) + p->req_mem[j]);
         return 0;
     }
@@ -828,6 +961,12 @@ struct kgo_state {
     double* amp;
     int32_t* dev_minors;          /* DeviceShare (NULL when the snapshot has no device tables) */
     int64_t *dev_total, *dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
+    /* cpuset binding (NULL when no node has a CPU topology) */
+    int32_t* cpu_topo;
+    kg_cpu_topo* cpu_topos;
+    uint32_t n_cpu_topos;
+    kg_cpu_alloc* cpu_alloc;
+    uint8_t *cpu_max_ref, *cpu_bind, *cpu_strategy;
 };
 
 static int64_t* dup64(const int64_t* s, uint32_t n) {
@@ -889,6 +1028,23 @@ kgo_state* kgo_state_new(const kg_node_columns* s, uint32_t n) {
         memcpy(st->dev_total, s->dev_total, 8 * (size_t)n * KG_DEV_R * KG_DEV_MINORS);
         memcpy(st->dev_free, s->dev_free, 8 * (size_t)n * KG_DEV_R * KG_DEV_MINORS);
     }
+    if (s->cpu_topo && s->cpu_topos) {
+        const size_t m = n ? n : 1;
+        st->cpu_topo = (int32_t*)calloc(m, 4);
+        memcpy(st->cpu_topo, s->cpu_topo, 4 * (size_t)n);
+        st->n_cpu_topos = s->n_cpu_topos;
+        st->cpu_topos = (kg_cpu_topo*)calloc(s->n_cpu_topos ? s->n_cpu_topos : 1, sizeof(kg_cpu_topo));
+        memcpy(st->cpu_topos, s->cpu_topos, sizeof(kg_cpu_topo) * s->n_cpu_topos);
+        st->cpu_alloc = (kg_cpu_alloc*)calloc(m, sizeof(kg_cpu_alloc));
+        if (s->cpu_alloc) memcpy(st->cpu_alloc, s->cpu_alloc, sizeof(kg_cpu_alloc) * (size_t)n);
+        st->cpu_max_ref = (uint8_t*)calloc(m, 1);
+        st->cpu_bind = (uint8_t*)calloc(m, 1);
+        st->cpu_strategy = (uint8_t*)calloc(m, 1);
+        for (uint32_t i = 0; i < n; i++) st->cpu_max_ref[i] = 1;
+        if (s->cpu_max_ref) memcpy(st->cpu_max_ref, s->cpu_max_ref, n);
+        if (s->cpu_bind_policy) memcpy(st->cpu_bind, s->cpu_bind_policy, n);
+        if (s->cpu_strategy) memcpy(st->cpu_strategy, s->cpu_strategy, n);
+    }
     return st;
 }
 
@@ -903,6 +1059,12 @@ void kgo_state_free(kgo_state* st) {
     free(st->dev_minors);
     free(st->dev_total);
     free(st->dev_free);
+    free(st->cpu_topo);
+    free(st->cpu_topos);
+    free(st->cpu_alloc);
+    free(st->cpu_max_ref);
+    free(st->cpu_bind);
+    free(st->cpu_strategy);
     free(st);
 }
 
@@ -947,10 +1109,45 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
     v->dev_minors = st->dev_minors;
     v->dev_total = st->dev_total;
     v->dev_free = st->dev_free;
+    v->cpu_topo = st->cpu_topo;
+    v->cpu_topos = st->cpu_topos;
+    v->n_cpu_topos = st->n_cpu_topos;
+    v->cpu_alloc = st->cpu_alloc;
+    v->cpu_max_ref = st->cpu_max_ref;
+    v->cpu_bind_policy = st->cpu_bind;
+    v->cpu_strategy = st->cpu_strategy;
+}
+
+/* NodeNUMAResource Reserve of a cpuset-binding pod on a NUMA-policy-None node: the accumulator's CPUs
+ * enter NodeAllocation.allocatedCPUs (addPodAllocation, node_allocation.go:111-130: RefCount++, the pod's
+ * exclusive policy), and cpuset_alloc_milli follows the allocated CPU count */
+static void cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j) {
+    if (!(c->plugins & KG_PLUGIN_NUMA) || !st->cpu_topo || (p->flags[j] & KG_POD_NUMA_SKIP)) return;
+    const uint32_t node_bind = st->cpu_bind[i];
+    const int bind = (p->flags[j] & KG_POD_CPU_BIND) || (node_bind != KG_NODE_CPU_BIND_NONE && p->req_cpu[j] != 0);
+    if (!bind) return;
+    int conflict;
+    if (numa_merge_policy(st->numa_policy[i], p->numa_policy[j], &conflict) != KG_NUMA_NONE) return;
+    kg_node_columns v;
+    kgo_state_view(st, &v);
+    uint64_t out[4];
+    if (cpuset_allocate(&v, i, p, j, node_bind, out)) return;
+    const uint32_t excl = (p->flags[j] >> KG_POD_CPU_EXCL_SHIFT) & 3u;
+    const kg_cpu_topo* t = cpu_topology(&v, i);
+    int allocated = 0;
+    for (int cc = 0; cc < t->n_cpus; cc++) {
+        if ((out[cc >> 6] >> (cc & 63)) & 1ull) {
+            st->cpu_alloc[i].ref[cc]++;
+            st->cpu_alloc[i].excl[cc] = (uint8_t)excl;
+        }
+        allocated += st->cpu_alloc[i].ref[cc] > 0;
+    }
+    st->col[C_CPUSET][i] = 1000 * (int64_t)allocated;
 }
 
 static void apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,
                   int64_t sign) {
+    if (sign > 0) cpuset_reserve(c, st, i, p, j);
     /* upstream NodeInfo.AddPod / RemovePod: Requested, NonZeroRequested, len(Pods) */
     st->col[C_REQ_CPU][i] += sign * p->req_cpu[j];
     st->col[C_REQ_MEM][i] += sign * p->req_mem[j];
@@ -1614,8 +1811,10 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
         if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(c, n, i, ovp, p, j);
         if (c->plugins & KG_PLUGIN_LA) st |= la_filter(c, n, i, p, j);
         if (c->plugins & KG_PLUGIN_NUMA) {
-            if (v && n->numa_policy[i] != KG_NUMA_NONE && !(p->flags[j] & KG_POD_NUMA_SKIP))
-                st |= KG_ST_UNSUPPORTED; /* NUMA zone restore of reservations: host path */
+            const int binds = (p->flags[j] & KG_POD_CPU_BIND) ||
+                              (n->cpu_bind_policy && n->cpu_bind_policy[i] != KG_NODE_CPU_BIND_NONE);
+            if (v && (n->numa_policy[i] != KG_NUMA_NONE || binds) && !(p->flags[j] & KG_POD_NUMA_SKIP))
+                st |= KG_ST_UNSUPPORTED; /* NUMA zone / cpuset restore of reservations: host path */
             else
                 st |= numa_eval(c, n, i, ovp, p, j, &s_numa, &zone);
         }

@@ -84,9 +84,8 @@ cases = {
          "want": ["Insufficient amplified cpu"]},
     ],
     # nodenumaresource/scoring_test.go:726-1008 TestScoreWithAmplifiedCPUs (default resources cpu 1,
-    # memory 1); every node's topology is buildCPUTopologyForTest(2, 1, 8, 2) (32 CPUs). Requests of a
-    # cpuset-binding pod are placed by the CPU accumulator on the host (device: KG_ST_UNSUPPORTED), so
-    # those cases carry the reference's scores for the record only (host_path).
+    # memory 1); the nodes in nodeHasNRT carry the CPU topology buildCPUTopologyForTest(2, 1, 8, 2) (32 CPUs).
+    # A cpuset-binding pod's request is amplified in its Score (getResourceOptions, plugin.go:772-778).
     "numa_amp_score": [
         {"name": "ScoringStrategy MostAllocated, non-cpuset pod", "ref": "nodenumaresource/scoring_test.go:739",
          "strategy": "MostAllocated", "nodes": [[32, 40, 1.0], [64, 60, 2.0], [32, 40, 2.0]], "nrt": [],
@@ -94,7 +93,7 @@ cases = {
         {"name": "ScoringStrategy MostAllocated, cpuset pod", "ref": "nodenumaresource/scoring_test.go:756",
          "strategy": "MostAllocated", "nodes": [[32, 40, 1.0], [64, 60, 2.0], [32, 40, 2.0]],
          "nrt": ["node1", "node2", "node3"], "existing": [], "pod": {"cpu": 8, "mem": 16, "cpuset": True},
-         "want": [32, 19, 32], "host_path": True},
+         "want": [32, 19, 32]},
         {"name": "ScoringStrategy MostAllocated, non-cpuset pods, and existing cpuset pod on node",
          "ref": "nodenumaresource/scoring_test.go:779",
          "strategy": "MostAllocated", "nodes": [[32, 40, 1.0], [64, 60, 2.0]], "nrt": ["node1", "node2"],
@@ -104,12 +103,12 @@ cases = {
          "ref": "nodenumaresource/scoring_test.go:804",
          "strategy": "MostAllocated", "nodes": [[32, 40, 1.0], [64, 60, 2.0]], "nrt": ["node1", "node2"],
          "existing": [["node1", 20, 4, False], ["node2", 20, 4, False]], "pod": {"cpu": 8, "mem": 16, "cpuset": True},
-         "want": [68, 30], "host_path": True},
+         "want": [68, 30]},
         {"name": "ScoringStrategy MostAllocated, cpuset pods on node, scheduling cpuset pod",
          "ref": "nodenumaresource/scoring_test.go:829",
          "strategy": "MostAllocated", "nodes": [[32, 40, 1.0], [64, 60, 2.0]], "nrt": ["node1", "node2"],
          "existing": [["node1", 20, 4, True], ["node2", 20, 4, True]], "pod": {"cpu": 8, "mem": 16, "cpuset": True},
-         "want": [68, 38], "host_path": True},
+         "want": [68, 38]},
         {"name": "ScoringStrategy LeastAllocated, no cpuset pod", "ref": "nodenumaresource/scoring_test.go:854",
          "strategy": "LeastAllocated", "nodes": [[32, 40, 1.0], [64, 60, 2.0]], "nrt": [],
          "existing": [["node1", 20, 4, False], ["node2", 20, 4, False]], "pod": {"cpu": 8, "mem": 16, "cpuset": False},
@@ -123,12 +122,12 @@ cases = {
          "ref": "nodenumaresource/scoring_test.go:899",
          "strategy": "LeastAllocated", "nodes": [[32, 40, 1.0], [64, 60, 2.0]], "nrt": ["node1", "node2"],
          "existing": [["node1", 20, 4, False], ["node2", 20, 4, False]], "pod": {"cpu": 8, "mem": 16, "cpuset": True},
-         "want": [31, 68], "host_path": True},
+         "want": [31, 68]},
         {"name": "ScoringStrategy LeastAllocated, cpuset pods on node,scheduling cpuset pod",
          "ref": "nodenumaresource/scoring_test.go:924",
          "strategy": "LeastAllocated", "nodes": [[32, 40, 1.0], [64, 60, 2.0]], "nrt": ["node1", "node2"],
          "existing": [["node1", 20, 4, True], ["node2", 20, 4, True]], "pod": {"cpu": 8, "mem": 16, "cpuset": True},
-         "want": [31, 61], "host_path": True},
+         "want": [31, 61]},
     ],
     # reservation/plugin_test.go:1090-2546 Test_filterWithReservations: test-node allocatable cpu 32,
     # memory 32Gi, pods 100, batch-cpu 7500, batch-memory 10Gi (:1162-1174), no pods in the NodeInfo

@@ -330,4 +330,7 @@ class OracleState:
         t["cpu_amp_ratio"] = grab(v.cpu_amp_ratio, np.float64)
         df = self.dev_free()
         t["dev_free"] = df if df is not None else np.zeros((n, abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
+        if v.cpu_alloc:
+            raw = C.string_at(v.cpu_alloc, n * 2 * abi.KG_MAX_CPUS)
+            t["cpu_alloc"] = np.frombuffer(raw, np.uint8).reshape(n, 2 * abi.KG_MAX_CPUS).copy()
         return t

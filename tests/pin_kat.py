@@ -177,14 +177,20 @@ def numa_amp_score(case):
         t["alloc_cpu"][i] = decode.amplify(cpu * 1000, ratio)
         t["alloc_mem"][i] = mem * GI
         t["cpu_amp_ratio"][i] = ratio
+    # nodes in nodeHasNRT carry the CPU topology buildCPUTopologyForTest(2, 1, 8, 2) (scoring_test.go:982-996);
+    # an existing cpuset pod holds that many CPUs in the resource manager (the count is what the Score reads)
+    t["cpu_topo"] = np.array([0 if nm in case["nrt"] else -1 for nm in names], np.int32)
+    t["cpu_topos"] = abi.cpu_topos_array([abi.cpu_topo_for_test(2, 1, 8, 2)])
+    t["cpu_alloc"] = np.zeros((n, 2 * abi.KG_MAX_CPUS), np.uint8)
+    held = [0] * n
     for node, cpu, mem, cpuset in case["existing"]:
         i = names.index(node)
         _add_existing(t, i, cpu_m=cpu * 1000, mem_b=mem * GI)
         if cpuset and node in case["nrt"]:
             t["cpuset_alloc_milli"][i] += cpu * 1000
+            t["cpu_alloc"][i, held[i]:held[i] + cpu] = 1
+            held[i] += cpu
     pods = _amp_pod(case["pod"])
-    if case.get("host_path"):
-        return kc, t, pods, None, {"host_path": True}
     return kc, t, pods, None, {"score_numa": case["want"]}
 
 

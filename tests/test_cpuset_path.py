@@ -1,0 +1,135 @@
+"""cpuset binding on the device path: NodeNUMAResource Filter / Score of LSE/LSR pods and
+of pods on nodes with a CPU bind policy (plugin.go:388-440, util.go:101-138, scoring.go:132-151), and the
+Reserve through the device accumulator (resource_manager.go:197-499, node_allocation.go:103-130), against the
+oracle (oracle/kg_oracle.c cpuset_filter / cpuset_reserve over oracle/kg_cpuset.c). Bit-exact: status bits,
+scores, keys, replay placements, allocated CPUs per node (RefCount and exclusive policy) and
+cpuset_alloc_milli."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from koordinator_amd import abi, synth
+
+
+# ---------------------------------------------------------------------------------------------- CPU
+
+def test_oracle_cpuset_verify_outcomes():
+    cfg, nodes, pods = synth.cpuset_cluster(300, 160, seed=1)
+    kc = cfg.kg_config()
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    bind = (pods["flags"] & abi.KG_POD_CPU_BIND) != 0
+    st = ref.status
+    assert (st[bind] & abi.KG_ST_NUMA_CPU_TOPO).any()   # nodes without a CPU topology
+    assert (st & abi.KG_ST_NUMA_CPU_BIND).any()          # conflicts / SMT / fractional cpus on bind-policy nodes
+    assert (st[bind] & abi.KG_ST_NUMA_CPUS).any()        # the required policy's CPUs do not cover the pod
+    assert ((st[bind] == 0)).any()                        # and cpuset pods that fit
+
+
+def test_oracle_cpuset_replay_allocations_respect_policies():
+    """Every Reserve of the oracle replay hands out free CPUs (RefCount < maxRefCount), counted into
+    cpuset_alloc_milli; required FullPCPUs allocations are whole cores."""
+    cfg, nodes, pods = synth.cpuset_cluster(120, 200, seed=2)
+    kc = cfg.kg_config()
+    st = oracle_lib.OracleState(kc, nodes)
+    node, _ = st.replay(pods)
+    t = st.table()
+    ref = t["cpu_alloc"][:, :abi.KG_MAX_CPUS].astype(np.int64)
+    before = nodes["cpu_alloc"][:, :abi.KG_MAX_CPUS].astype(np.int64)
+    assert (ref >= before).all()
+    assert (ref <= nodes["cpu_max_ref"][:, None]).all()
+    assert np.array_equal(t["cpuset_alloc_milli"], 1000 * (ref > 0).sum(axis=1))
+    bind = (pods["flags"] & abi.KG_POD_CPU_BIND) != 0
+    placed = bind & (node >= 0) & (nodes["numa_policy"][np.maximum(node, 0)] == abi.KG_NUMA_NONE)
+    assert placed.sum() > 10
+    assert (ref.sum() - before.sum()) == int((pods["req_cpu"][placed] // 1000).sum()) + \
+        int(sum(pods["req_cpu"][j] // 1000 for j in range(len(node)) if not bind[j] and node[j] >= 0
+                and nodes["cpu_bind_policy"][node[j]] != 0 and nodes["cpu_topo"][node[j]] >= 0
+                and nodes["numa_policy"][node[j]] == abi.KG_NUMA_NONE and pods["req_cpu"][j] > 0))
+
+
+# ---------------------------------------------------------------------------------------------- GPU
+
+@pytest.fixture(scope="module")
+def ctx():
+    from koordinator_amd import engine
+    c = engine.Context(0)
+    yield c
+    c.close()
+
+
+FIELDS = ("status", "score_nrf", "score_la", "score_numa", "total", "numa_zone")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [3, 4])
+def test_cpuset_verify_select(ctx, seed):
+    from koordinator_amd import engine
+    cfg, nodes, pods = synth.cpuset_cluster(700, 256, seed=seed)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    batch = engine.PodBatch(ctx, pods)
+    got = engine.eval_verify(snap, batch)
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    for f in FIELDS:
+        a, b = getattr(got, f), getattr(ref, f)
+        if not np.array_equal(a, b):
+            j, i = np.argwhere(a != b)[0]
+            raise AssertionError(f"{f} pod {j} node {i}: gpu {a[j, i]} oracle {b[j, i]} status {ref.status[j, i]:#x}")
+    for k in (1, 3):
+        assert np.array_equal(engine.eval_select(snap, batch, k), oracle_lib.select(kc, nodes, pods, k))
+    want = np.bitwise_or.reduce(ref.status & abi.KG_ST_UNSUPPORTED, axis=1)
+    assert np.array_equal(engine.result_status(batch), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [5, 6])
+def test_cpuset_replay(ctx, seed):
+    """One pod per cycle with the cpuset Reserve on the device between steps (k_cpuset_reserve before each
+    k_replay step): placements, reasons, NodeInfo columns, allocated CPUs and cpuset_alloc_milli."""
+    from koordinator_amd import engine
+    cfg, nodes, pods = synth.cpuset_cluster(500, 600, seed=seed)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    batch = engine.PodBatch(ctx, pods)
+    node, total, why = engine.replay(snap, batch, reasons=True)
+    st = oracle_lib.OracleState(kc, nodes)
+    rn, rt, rwhy = st.replay(pods, reasons=True)
+    bad = np.flatnonzero(node != rn)
+    assert not len(bad), (bad[:5], node[bad[:5]], rn[bad[:5]])
+    assert np.array_equal(total, rt) and np.array_equal(why, rwhy)
+    got, want = snap.read_state(), st.table()
+    for k in ("req_cpu", "req_mem", "num_pods", "nz_cpu", "cpuset_alloc_milli"):
+        assert np.array_equal(got[k], want[k]), k
+    assert np.array_equal(got["cpu_alloc"], want["cpu_alloc"])
+    moved = (got["cpu_alloc"][:, :abi.KG_MAX_CPUS] != nodes["cpu_alloc"][:, :abi.KG_MAX_CPUS]).any(axis=1)
+    assert moved.sum() > 20
+
+
+@pytest.mark.gpu
+def test_cpuset_assume_and_forget(ctx):
+    from koordinator_amd import engine
+    cfg, nodes, pods = synth.cpuset_cluster(200, 64, seed=7)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    batch = engine.PodBatch(ctx, pods)
+    st = oracle_lib.OracleState(kc, nodes)
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    bind = np.flatnonzero((pods["flags"] & abi.KG_POD_CPU_BIND) != 0)
+    done = 0
+    for j in bind:
+        ok = np.flatnonzero((ref.status[j] == 0) & (nodes["cpu_topo"] >= 0) & (nodes["numa_policy"] == 0))
+        if not len(ok):
+            continue
+        i = int(ok[j % len(ok)])
+        engine.assume(snap, batch, int(j), i)
+        st.assume(i, pods, int(j))
+        with pytest.raises(engine.Unsupported):
+            engine.forget(snap, batch, int(j), i, -1)
+        done += 1
+        if done == 12:
+            break
+    assert done >= 8
+    got, want = snap.read_state(), st.table()
+    assert np.array_equal(got["cpu_alloc"], want["cpu_alloc"])
+    assert np.array_equal(got["cpuset_alloc_milli"], want["cpuset_alloc_milli"])
+    assert np.array_equal(got["req_cpu"], want["req_cpu"])

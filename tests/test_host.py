@@ -34,7 +34,8 @@ def test_struct_layouts_match_header(tmp_path):
     """ctypes mirrors have the C sizes of include/koordgpu.h (compiled with gcc here)."""
     import subprocess
     names = ["kg_config", "kg_node_columns", "kg_node_state", "kg_pod_columns", "kg_verify_out",
-             "kg_quota_columns", "kg_rsv_view", "kg_rsv_info"]
+             "kg_quota_columns", "kg_rsv_view", "kg_rsv_info", "kg_rsv_dev", "kg_cpu_topo", "kg_cpu_alloc",
+             "kg_cpuset_request"]
     src = tmp_path / "sz.c"
     hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "koordgpu.h")
     src.write_text(f'#include "{hdr}"\n#include <stdio.h>\nint main(void){{' +
@@ -43,7 +44,8 @@ def test_struct_layouts_match_header(tmp_path):
     subprocess.check_call(["gcc", str(src), "-o", str(exe)])
     sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     mirrors = [abi.KgConfig, abi.KgNodeColumns, abi.KgNodeState, abi.KgPodColumns, abi.KgVerifyOut,
-               abi.KgQuotaColumns, abi.KgRsvView, abi.KgRsvInfo]
+               abi.KgQuotaColumns, abi.KgRsvView, abi.KgRsvInfo, abi.KgRsvDev, abi.KgCpuTopo, abi.KgCpuAlloc,
+               abi.KgCpusetRequest]
     for n, c_size, m in zip(names, sizes, mirrors):
         assert C.sizeof(m) == c_size, n
 
