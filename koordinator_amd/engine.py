@@ -15,7 +15,8 @@ import numpy as np
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkoordgpu.so")
+# KG_LIB_PATH: A/B measurements of alternative builds (tools/); the product loads the in-tree library
+LIB_PATH = os.environ.get("KG_LIB_PATH") or os.path.join(HERE, "libkoordgpu.so")
 
 _lib = None
 

@@ -1,0 +1,59 @@
+"""Regression guard for the round-1 miscompile (commit f4efa99): with the NUMA topology manager
+(`numa_topology`) and the multi-zone Reserve split (`numa_reserve_split`) compiled as out-of-line device
+functions, the round-1 build's device results stopped matching the oracle on gfx950 (ROCm 7.2 hipcc / clang).
+The fault was not isolated to a smaller reproducer; the functions were made __forceinline__ and the results
+matched again. This CPU test compiles the integer evaluation path (eval_pair + apply_assume, which contain both
+functions) for gfx950 to assembly and fails if any out-of-line call (s_swappc_b64 / s_setpc_b64) appears in
+it, so a toolchain or source change cannot bring the out-of-line form back silently. A self-check compiles a
+deliberately __noinline__ helper and expects the call to show up."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "koordinator_amd", "csrc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", f"-I{CSRC}",
+         "--cuda-device-only", "-S"]
+
+PROBE = r"""
+#include <hip/hip_runtime.h>
+#include "kg_eval.h"
+namespace kg {
+%s
+__global__ void probe(NodeRec* nodes, ZoneRec* zones, PodsDev pods, KCfg cfg, uint64_t* out) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    const PodV p = load_pod(pods, 0);
+    const PairOut o = eval_pair<false>(cfg, nodes[i].v, zones + i, p);
+    apply_assume(cfg, nodes[i].v, zones + i, p, o.zone, 1);
+    out[i] = pair_key(cfg, o, i) %s;
+}
+}
+"""
+
+
+def _compile(tmp_path, extra_fn="", extra_use=""):
+    src = tmp_path / "probe.hip"
+    src.write_text(PROBE % (extra_fn, extra_use))
+    asm = tmp_path / "probe.s"
+    subprocess.check_call([HIPCC, *FLAGS, str(src), "-o", str(asm)], stderr=subprocess.DEVNULL)
+    return asm.read_text()
+
+
+def _calls(asm: str) -> int:
+    return sum(1 for line in asm.splitlines() if line.strip().startswith(("s_swappc_b64", "s_setpc_b64")))
+
+
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not in this image")
+def test_eval_path_has_no_out_of_line_calls(tmp_path):
+    asm = _compile(tmp_path)
+    ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.splitlines()[:1]
+    assert _calls(asm) == 0, f"out-of-line device call in the evaluation path ({ver})"
+
+
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not in this image")
+def test_guard_detects_a_call(tmp_path):
+    asm = _compile(tmp_path, "__device__ __attribute__((noinline)) uint64_t twist(uint64_t x) { return x * 3 + 1; }",
+                   "^ twist(i)")
+    assert _calls(asm) >= 1
