@@ -320,6 +320,36 @@ ANN_NUMA_TOPOLOGY_SPEC = "scheduling.koordinator.sh/numa-topology-spec"
 ANN_RESOURCE_SPEC = "scheduling.koordinator.sh/resource-spec"
 
 
+ANN_RESOURCE_SPEC = "scheduling.koordinator.sh/resource-spec"
+DEFAULT_CPU_BIND_POLICY = "FullPCPUs"
+
+
+def cpu_bind_flags(pod, req_cpu_milli: int) -> int:
+    """KG_POD_CPU_* bits of an AllowUseCPUSet pod (nodenumaresource/plugin.go:331-349,
+    apis/extension/numa_aware.go:63-71,231-244). A Full/Spread policy with a fractional cpu request is
+    ErrInvalidRequestedCPUs at PreFilter: Unsupported here (the pod never reaches Filter)."""
+    ann = (pod.get("metadata") or {}).get("annotations") or {}
+    spec = json.loads(ann[ANN_RESOURCE_SPEC]) if ann.get(ANN_RESOURCE_SPEC) else {}
+    preferred = spec.get("preferredCPUBindPolicy") or ""
+    if preferred in ("", "Default"):
+        preferred = DEFAULT_CPU_BIND_POLICY
+    required = spec.get("requiredCPUBindPolicy") or ""
+    if required == "Default":
+        required = DEFAULT_CPU_BIND_POLICY
+    policy = required or preferred
+    if policy not in ("FullPCPUs", "SpreadByPCPUs"):
+        return 0
+    if req_cpu_milli % 1000 != 0:
+        raise Unsupported("cpuset-binding pod with a fractional cpu request (ErrInvalidRequestedCPUs at PreFilter)")
+    if req_cpu_milli <= 0:
+        return 0
+    flags = abi.KG_POD_CPU_BIND | (abi.KG_CPU_BIND[policy] << abi.KG_POD_CPU_POLICY_SHIFT)
+    if required:
+        flags |= abi.KG_POD_CPU_REQUIRED
+    flags |= abi.KG_CPU_EXCL.get(spec.get("preferredCPUExclusivePolicy") or "", 0) << abi.KG_POD_CPU_EXCL_SHIFT
+    return flags
+
+
 def pod_row(pod, cfg: SchedulerConfig) -> Dict[str, int]:
     """Pod columns (kg_pod_columns) for one pending pod."""
     la = cfg.la()
@@ -355,11 +385,11 @@ def pod_row(pod, cfg: SchedulerConfig) -> Dict[str, int]:
         flags |= abi.KG_POD_HAS_CPU
     if MEMORY in req:
         flags |= abi.KG_POD_HAS_MEM
-    # AllowUseCPUSet (nodenumaresource/util.go:49-56): LSE/LSR prod pods bind cpusets by default
-    # (DefaultCPUBindPolicy FullPCPUs) -> host path.
+    # AllowUseCPUSet (nodenumaresource/util.go:49-56) and the PreFilter's bind request (plugin.go:319-349):
+    # LSE/LSR prod pods bind cpusets with the resource-spec annotation's policies, DefaultCPUBindPolicy
+    # (FullPCPUs, v1/defaults.go:50) filling in "" / "Default"; a required policy wins
     if koord_qos_raw(pod) in ("LSE", "LSR") and pc == PROD and (cfg.plugins & abi.KG_PLUGIN_NUMA):
-        if row["req_cpu"] > 0:
-            flags |= abi.KG_POD_CPU_BIND
+        flags |= cpu_bind_flags(pod, row["req_cpu"])
     ann = (pod.get("metadata") or {}).get("annotations") or {}
     if ann.get(ANN_NUMA_TOPOLOGY_SPEC):
         raise Unsupported("pod NUMA topology spec (exclusive-policy admission) is not on the device path")
