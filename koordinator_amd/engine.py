@@ -212,6 +212,7 @@ class Snapshot:
     def upload(self, nodes: abi.Table):
         cols = abi.node_columns(nodes)
         self.ctx.check(self.ctx.L.kg_snapshot_upload(self.h, C.byref(cols)), "kg_snapshot_upload")
+        self.has_cpu = "cpu_topo" in nodes
 
     def update_rows(self, rows, nodes: abi.Table):
         rows = np.ascontiguousarray(rows, np.uint32)
@@ -228,6 +229,8 @@ class Snapshot:
         t = abi.empty_node_state(self.n)
         s = abi.node_state_struct(t)
         self.ctx.check(self.ctx.L.kg_snapshot_read_state(self.h, C.byref(s)), "kg_snapshot_read_state")
+        if not getattr(self, "has_cpu", False):
+            t.pop("cpu_alloc")  # no CPU topologies in this snapshot
         return t
 
     def checkpoint(self):
