@@ -67,14 +67,15 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
                                                        const kg_cpu_topo* __restrict__ topos, PodsDev pods, KCfg cfg,
                                                        uint32_t pod, uint32_t rec, const uint64_t* __restrict__ winners,
                                                        const uint32_t* __restrict__ step_base, uint32_t step_off,
-                                                       const uint32_t* __restrict__ pos, uint32_t index_base) {
+                                                       const uint32_t* __restrict__ pos, uint32_t index_base,
+                                                       uint32_t n_pods) {
     __shared__ kg_cpu_topo st;
     __shared__ CpuAccLds acc;
     __shared__ kg_cpu_alloc sa;
     if (!(cfg.plugins & KG_PLUGIN_NUMA)) return;
     if (winners) {  // replay: Reserve of pod step-1 on its winner
         const uint32_t step = *step_base + step_off;
-        if (step == 0) return;
+        if (step == 0 || step > n_pods) return;  // the graph runs whole blocks of steps past the batch
         const uint64_t prev = __hip_atomic_load(&winners[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == 0ull) return;
         pod = step - 1;
@@ -152,9 +153,9 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
 hipError_t launch_cpuset_reserve(NodeRec* nodes, ZoneRec* zones, kg_cpu_alloc* allocs, const kg_cpu_topo* topos,
                                  const PodsDev& pods, const KCfg& cfg, uint32_t pod, uint32_t rec, const uint64_t* winners,
                                  const uint32_t* step_base, uint32_t step_off, const uint32_t* pos, uint32_t index_base,
-                                 hipStream_t s) {
+                                 uint32_t n_pods, hipStream_t s) {
     k_cpuset_reserve<<<1, 64, 0, s>>>(nodes, zones, allocs, topos, pods, cfg, pod, rec, winners, step_base, step_off, pos,
-                                      index_base);
+                                      index_base, n_pods);
     return hipGetLastError();
 }
 
