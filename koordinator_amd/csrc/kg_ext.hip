@@ -374,11 +374,9 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
     const uint32_t dcls = pods.dev_cls ? pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
     const uint32_t mag = norm_magic(dm);
     const int64_t prow = (FB && e.pairs && live && j >= e.pairs_row0) ? (int64_t)(j - e.pairs_row0) : -1;
-    // pairs that need the host path: a cpuset-binding pod under NodeNUMAResource has one on every node
-    // (numa_eval), whatever path the record takes; FB records (class 0, not F_BIG: NUMA policy None) have
-    // no other source
-    uint32_t unsup = ((cfg.plugins & KG_PLUGIN_NUMA) && (p.flags & KG_POD_CPU_BIND) && !(p.flags & KG_POD_NUMA_SKIP) &&
-                      q == 0u && hi > lo) ? KG_ST_UNSUPPORTED : 0u;
+    // pairs that need the host path come from eval_pair_ext only: FB records never do (a batch with a
+    // cpuset-binding pod is not fast_ok, nodes with a CPU bind policy are F_BIG)
+    uint32_t unsup = 0;
     for (uint32_t rec = lo; rec < hi; rec++) {
         const int64_t* __restrict__ n = nodes[rec].v;
         if constexpr (FB) {

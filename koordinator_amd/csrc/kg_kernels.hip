@@ -58,10 +58,8 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
     const uint32_t hi = min(end, lo + chunk);
     uint32_t unsup = 0;
     if constexpr (FAST) {
-        // the fast path's only host-path pairs: a cpuset-binding pod under NodeNUMAResource (pod-level;
-        // Restricted / BestEffort records are F_BIG and flagged by k_merge_big)
-        if ((PM & KG_PLUGIN_NUMA) && (p.flags & KG_POD_CPU_BIND) && !(p.flags & KG_POD_NUMA_SKIP) && hi > lo)
-            unsup = KG_ST_UNSUPPORTED;
+        // no host-path pairs on the fast path: Restricted / BestEffort records and nodes with a CPU bind
+        // policy are F_BIG (flagged by k_merge_big), a batch with a cpuset-binding pod is not fast_ok
         const PodF pf = to_podf(p, cfg);
         const KCfg cv = cfg_in_vgprs(cfg);
         for (uint32_t i = lo; i < hi; i++) {
@@ -111,9 +109,6 @@ __global__ __launch_bounds__(256) void k_select1(const NodeRec* __restrict__ nod
     }
     if (live) {
         if (top) atomicMax((unsigned long long*)(out + j), (unsigned long long)top);
-        // the fast path's only host-path pairs: a cpuset-binding pod under NodeNUMAResource (pod-level)
-        if ((PM & KG_PLUGIN_NUMA) && (p.flags & KG_POD_CPU_BIND) && !(p.flags & KG_POD_NUMA_SKIP) && hi > lo)
-            atomicOr(pstat + (pmap ? pmap[j] : j), (uint32_t)KG_ST_UNSUPPORTED);
     }
 }
 

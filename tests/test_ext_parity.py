@@ -256,8 +256,9 @@ def test_ext_shard_select_single_rank(ctx, k):
 
 @pytest.mark.parametrize("split", ["1", "0"])
 def test_ext_result_status(ctx, monkeypatch, split):
-    """kg_result_status on config 5: GPU pods on NUMA-policy nodes and cpuset-binding pods are flagged
-    KG_ST_UNSUPPORTED, quota-rejected pods KG_ST_QUOTA — the OR of the oracle verify rows' bits."""
+    """kg_result_status on config 5: GPU pods on NUMA-policy nodes and pairs of cpuset-binding pods on
+    reservation views are flagged KG_ST_UNSUPPORTED, quota-rejected pods KG_ST_QUOTA — the OR of the
+    oracle verify rows' bits (a cpuset-binding pod on a node without CPU topology fails its Filter)."""
     monkeypatch.setenv("KG_EXT_SPLIT", split)
     cfg, nodes, pods, quotas, rsv = synth.cluster5(1200, 400, seed_config=73, rsv_frac=0.2)
     nodes = {k: v.copy() for k, v in nodes.items()}
@@ -271,8 +272,16 @@ def test_ext_result_status(ctx, monkeypatch, split):
     want = oracle_lib.ext_select(kc, nodes, pods, 1, 0, quotas, rsv)
     assert np.array_equal(got, want)
     ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
+    vg = engine.eval_verify(snap, batch)
+    badp = np.argwhere(vg.status != ref.status)
+    assert not len(badp), [(int(j), int(i), hex(vg.status[j, i]), hex(ref.status[j, i])) for j, i in badp[:8]]
+    engine.eval_select(snap, batch, 1)
     wstat = np.bitwise_or.reduce(ref.status & (abi.KG_ST_UNSUPPORTED | abi.KG_ST_QUOTA), axis=1)
-    assert np.array_equal(engine.result_status(batch), wstat)
+    gstat = engine.result_status(batch)
+    bad = np.flatnonzero(gstat != wstat)
+    assert not len(bad), [(int(j), hex(gstat[j]), hex(wstat[j]), hex(pods["flags"][j]),
+                           [(int(i), hex(ref.status[j, i])) for i in np.flatnonzero(ref.status[j] & abi.KG_ST_UNSUPPORTED)[:4]])
+                          for j in bad[:6]]
     assert (wstat & abi.KG_ST_UNSUPPORTED).any() and (wstat & abi.KG_ST_QUOTA).any() and (wstat == 0).any()
 
 
