@@ -856,7 +856,9 @@ __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& 
             const bool has_any = has_cpu | has_mem;
             int32_t best = -1;
             uint32_t best_hint = 0, best_score = 0;
-            auto zone_step = [&](const ZoneFast& q, uint32_t z) {
+#pragma unroll 1
+            for (uint32_t z = 0; z < Z; z++) {
+                const ZoneFast q = zr->zf[z];
                 const bool elig = (!has_cpu | (p.cpu <= q.avail_cpu)) & (!has_mem | (p.mem <= q.avail_mem));
                 const uint32_t hc = lr100(q.hint_cpu, p.cpu, q.rcp_cpu), hm = lr100(q.hint_mem, p.mem, q.rcp_mem);
                 const uint32_t fc = lr100(q.free_cpu, p.cpu, q.rcp_cpu), fm = lr100(q.free_mem, p.mem, q.rcp_mem);
@@ -866,15 +868,6 @@ __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& 
                 best = take ? (int32_t)z : best;
                 best_hint = take ? hint : best_hint;
                 best_score = take ? fin : best_score;
-            };
-            if (Z == 2) {
-                // the common two-zone node: both zone blocks issued before either is used (one wait)
-                const ZoneFast q0 = zr->zf[0], q1 = zr->zf[1];
-                zone_step(q0, 0);
-                zone_step(q1, 1);
-            } else {
-#pragma unroll 1
-                for (uint32_t z = 0; z < Z; z++) zone_step(zr->zf[z], z);
             }
             nok = nok & (Z != 0) & !(has_any & (best < 0));
             // a best hint equal to the default affinity (no request on NUMA resources, or one zone)
