@@ -797,28 +797,60 @@ __device__ __forceinline__ KCfg cfg_in_vgprs(const KCfg& c) {
 // wide scalar loads, one wait); plugin arithmetic is branch-free except for the SingleNUMANode
 // zone walk. `c` comes from cfg_in_vgprs (LoadAware weights doubled).
 // PM: enabled plugins (KG_PLUGIN_* mask); CLS: node storage class (node_class), both compile-time.
-template <uint32_t PM, int CLS>
-__device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr,
-                                                  const PodF& p, uint32_t gidx, int32_t* zone_out = nullptr) {
+// Wave kinds of the fast select (a wave whose 64 pods all share one of these shapes runs a loop
+// specialised for it; the host groups a batch's pods by kind, kg_pods_upload):
+//   FK_PROD  - prod pods (KG_POD_PROD), no DaemonSet, no scalar (batch) requests, NodeNUMAResource not
+//              skipped, no cpuset binding: the LoadAware prod profile, no scalar Fits / LeastAllocated terms;
+//   FK_BATCH - non-prod pods with both scalar requests and no cpu / memory request (koord-batch pods),
+//              no DaemonSet, no HAS_CPU / HAS_MEM, not skipped, no cpuset binding: the non-prod profile, both scalar terms,
+//              the cpu / memory Fits reduce to the node's "Too many pods" bit, no NUMA zone walk.
+// Every kind computes exactly what the general loop (FK_ANY) computes for those pods.
+enum : int { FK_ANY = 0, FK_PROD = 1, FK_BATCH = 2 };
+
+__device__ __forceinline__ bool fast_kind_match(int kind, const PodV& p) {
+    const uint32_t f = p.flags;
+    if (kind == FK_PROD)
+        return (f & (KG_POD_PROD | KG_POD_DAEMONSET | KG_POD_NUMA_SKIP | KG_POD_CPU_BIND)) == KG_POD_PROD && p.sc0 == 0 &&
+               p.sc1 == 0;
+    return (f & (KG_POD_PROD | KG_POD_DAEMONSET | KG_POD_NUMA_SKIP | KG_POD_CPU_BIND | KG_POD_HAS_CPU | KG_POD_HAS_MEM)) == 0 &&
+           p.req_cpu == 0 && p.req_mem == 0 && p.sc0 != 0 && p.sc1 != 0;
+}
+
+// sign of a fast-block double from its high word (a scalar test: fit values are +x or -1.0)
+__device__ __forceinline__ bool neg_bits(double x) { return (int32_t)((uint64_t)__double_as_longlong(x) >> 32) < 0; }
+
+// fast_eval: the weighted total in `total`, feasibility as the return value (select loops fold it into
+// their top-key update); eval_fast_key: the selection key, 0 when infeasible.
+template <uint32_t PM, int CLS, int KIND = FK_ANY>
+__device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr, const PodF& p,
+                                          uint32_t& total_out, int32_t* zone_out = nullptr) {
+    constexpr bool KP = KIND == FK_PROD, KB = KIND == FK_BATCH;
     const uint32_t f = (uint32_t)r.flags;
     bool ok = true;
     uint32_t total = 0;
 
     if constexpr ((PM & KG_PLUGIN_NRF) != 0) {
         // Fits: request r fails iff r > 0 and r > alloc - requested, i.e. 100 r > 100 max(0, headroom)
-        // ("Too many pods" is folded into fit_cpu by derive_node)
-        const bool fit_fail = (p.cpu > r.fit_cpu) | (p.mem > r.fit_mem) | (p.eph > r.fit_eph) |
-                              (p.sc0 > r.fit_sc0) | (p.sc1 > r.fit_sc1);
+        // ("Too many pods" is folded into fit_cpu by derive_node: -1.0, the only negative fit value)
+        bool fit_fail = p.eph > r.fit_eph;
+        if constexpr (KB) fit_fail = fit_fail | neg_bits(r.fit_cpu);
+        else fit_fail = fit_fail | (p.cpu > r.fit_cpu) | (p.mem > r.fit_mem);
+        if constexpr (!KP) fit_fail = fit_fail | (p.sc0 > r.fit_sc0) | (p.sc1 > r.fit_sc1);
         ok = ok & !fit_fail;
         // LeastAllocated (NonZeroRequested for cpu / memory, Requested for scalars the pod requests)
         const uint32_t w0 = lo32(r.w_nrf01), w1 = hi32(r.w_nrf01);
-        const uint32_t w2 = __umul24(lo32(r.w_nrf23), p.sc0_on), w3 = __umul24(hi32(r.w_nrf23), p.sc1_on);
         uint32_t sum2 = mad24(lr100(r.lr_nz_cpu, p.nzc, r.rcp_cpu), w0, 1u);
         sum2 = mad24(lr100(r.lr_nz_mem, p.nzm, r.rcp_mem), w1, sum2);
-        sum2 = mad24(lr100(r.lr_sc0, p.sc0, r.rcp_sc0), w2, sum2);
-        sum2 = mad24(lr100(r.lr_sc1, p.sc1, r.rcp_sc1), w3, sum2);
+        uint32_t wsum_u = hi32(r.w_aux);
+        if constexpr (!KP) {
+            const uint32_t w2 = KB ? lo32(r.w_nrf23) : (p.sc0_on ? lo32(r.w_nrf23) : 0u);
+            const uint32_t w3 = KB ? hi32(r.w_nrf23) : (p.sc1_on ? hi32(r.w_nrf23) : 0u);
+            sum2 = mad24(lr100(r.lr_sc0, p.sc0, r.rcp_sc0), w2, sum2);
+            sum2 = mad24(lr100(r.lr_sc1, p.sc1, r.rcp_sc1), w3, sum2);
+            wsum_u = wsum_u + w2 + w3;
+        }
         // Σ 2w = 0 -> sum2 = 1, and max(.., 2) gives trunc(1 * 0.5) = 0
-        const float wsum = (float)max(hi32(r.w_aux) + w2 + w3, 2u);
+        const float wsum = (float)max(wsum_u, 2u);
         float h = __builtin_amdgcn_rcpf(wsum);
         h = fmaf(h, fmaf(-wsum, h, 1.0f), h);  // one Newton step: 1/(Σ 2w) = 0.5/Σw, <= 1 ulp
         total = mad24(c.w_nrf, wq(sum2, h), total);
@@ -827,15 +859,28 @@ __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& 
     if constexpr ((PM & KG_PLUGIN_LA) != 0) {
         // Filter: usage cut-offs of the pod's profile (100 * (cut - base) vs 100 * estimate); the
         // node's filter modes and profile choice are folded into the heads by derive_node
-        const bool pod_prod = (p.flags & KG_POD_PROD) != 0;
-        const bool over_np = (p.e0 > r.la_head_np0) | (p.e1 > r.la_head_np1);
-        const bool over_pr = (p.e0 > r.la_head_prod0) | (p.e1 > r.la_head_prod1);
-        const bool la_fail = ((p.flags & KG_POD_DAEMONSET) == 0) & (pod_prod ? over_pr : over_np);
+        bool la_fail;
+        if constexpr (KP) {
+            la_fail = (p.e0 > r.la_head_prod0) | (p.e1 > r.la_head_prod1);
+        } else if constexpr (KB) {
+            la_fail = (p.e0 > r.la_head_np0) | (p.e1 > r.la_head_np1);
+        } else {
+            const bool pod_prod = (p.flags & KG_POD_PROD) != 0;
+            const bool over_np = (p.e0 > r.la_head_np0) | (p.e1 > r.la_head_np1);
+            const bool over_pr = (p.e0 > r.la_head_prod0) | (p.e1 > r.la_head_prod1);
+            la_fail = ((p.flags & KG_POD_DAEMONSET) == 0) & (pod_prod ? over_pr : over_np);
+        }
         ok = ok & !la_fail;
         // Score: least-used over the estimated usage; profile select as an exact fma:
         // (free_np - e) + delta * {0, 1}. Nodes whose score is 0 carry rcp_la = 0.
-        const uint32_t s0 = cvt_sat_u32(fma(r.la_sdelta0, p.la_sprod, r.la_sfree_np0 - p.e0) * r.rcp_la0);
-        const uint32_t s1 = cvt_sat_u32(fma(r.la_sdelta1, p.la_sprod, r.la_sfree_np1 - p.e1) * r.rcp_la1);
+        uint32_t s0, s1;
+        if constexpr (KB) {  // non-prod pods: la_sprod = 0
+            s0 = cvt_sat_u32((r.la_sfree_np0 - p.e0) * r.rcp_la0);
+            s1 = cvt_sat_u32((r.la_sfree_np1 - p.e1) * r.rcp_la1);
+        } else {
+            s0 = cvt_sat_u32(fma(r.la_sdelta0, p.la_sprod, r.la_sfree_np0 - p.e0) * r.rcp_la0);
+            s1 = cvt_sat_u32(fma(r.la_sdelta1, p.la_sprod, r.la_sfree_np1 - p.e1) * r.rcp_la1);
+        }
         const uint32_t dom = min(min(s0, s1), 100u);
         uint32_t sum2 = mad24(s0, (uint32_t)c.la_w[0], 1u);
         sum2 = mad24(s1, (uint32_t)c.la_w[1], sum2);
@@ -844,30 +889,34 @@ __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& 
     }
 
     if constexpr ((PM & KG_PLUGIN_NUMA) != 0) {
-        const bool skip = (p.flags & KG_POD_NUMA_SKIP) != 0;
+        const bool skip = (KP || KB) ? false : (p.flags & KG_POD_NUMA_SKIP) != 0;
         // filterAmplifiedCPUs (amp_fit is 2^62 without amplification, -1 on Restricted / BestEffort
-        // nodes, which leave the device path)
-        const bool nok0 = ((p.flags & KG_POD_CPU_BIND) == 0) & !(p.cpu > r.amp_fit);
+        // nodes, which are F_BIG and leave the fast path; FK_BATCH pods request no cpu)
+        const bool nok0 = KB ? true : ((p.flags & KG_POD_CPU_BIND) == 0) & !(p.cpu > r.amp_fit);
         uint32_t s_numa;
         bool nok = nok0;
         if constexpr (CLS == 1) {  // SingleNUMANode nodes (their own storage class): zone walk
             const uint32_t Z = (f >> F_NUMA_ZONES_SHIFT) & 15u;
-            const bool has_cpu = (p.flags & KG_POD_HAS_CPU) != 0, has_mem = (p.flags & KG_POD_HAS_MEM) != 0;
+            const bool has_cpu = KB ? false : (p.flags & KG_POD_HAS_CPU) != 0;
+            const bool has_mem = KB ? false : (p.flags & KG_POD_HAS_MEM) != 0;
             const bool has_any = has_cpu | has_mem;
             int32_t best = -1;
-            uint32_t best_hint = 0, best_score = 0;
+            uint32_t best_score = 0;
+            if constexpr (!KB) {
+                uint32_t best_hint = 0;
 #pragma unroll 1
-            for (uint32_t z = 0; z < Z; z++) {
-                const ZoneFast q = zr->zf[z];
-                const bool elig = (!has_cpu | (p.cpu <= q.avail_cpu)) & (!has_mem | (p.mem <= q.avail_mem));
-                const uint32_t hc = lr100(q.hint_cpu, p.cpu, q.rcp_cpu), hm = lr100(q.hint_mem, p.mem, q.rcp_mem);
-                const uint32_t fc = lr100(q.free_cpu, p.cpu, q.rcp_cpu), fm = lr100(q.free_mem, p.mem, q.rcp_mem);
-                const uint32_t hint = wq(mad24(hm, hi32(q.w_hint), mad24(hc, lo32(q.w_hint), 1u)), f32lo(q.hpack));
-                const uint32_t fin = wq(mad24(fm, hi32(q.w_score), mad24(fc, lo32(q.w_score), 1u)), f32hi(q.hpack));
-                const bool take = elig & ((best < 0) | (hint > best_hint));
-                best = take ? (int32_t)z : best;
-                best_hint = take ? hint : best_hint;
-                best_score = take ? fin : best_score;
+                for (uint32_t z = 0; z < Z; z++) {
+                    const ZoneFast q = zr->zf[z];
+                    const bool elig = (!has_cpu | (p.cpu <= q.avail_cpu)) & (!has_mem | (p.mem <= q.avail_mem));
+                    const uint32_t hc = lr100(q.hint_cpu, p.cpu, q.rcp_cpu), hm = lr100(q.hint_mem, p.mem, q.rcp_mem);
+                    const uint32_t fc = lr100(q.free_cpu, p.cpu, q.rcp_cpu), fm = lr100(q.free_mem, p.mem, q.rcp_mem);
+                    const uint32_t hint = wq(mad24(hm, hi32(q.w_hint), mad24(hc, lo32(q.w_hint), 1u)), f32lo(q.hpack));
+                    const uint32_t fin = wq(mad24(fm, hi32(q.w_score), mad24(fc, lo32(q.w_score), 1u)), f32hi(q.hpack));
+                    const bool take = elig & ((best < 0) | (hint > best_hint));
+                    best = take ? (int32_t)z : best;
+                    best_hint = take ? hint : best_hint;
+                    best_score = take ? fin : best_score;
+                }
             }
             nok = nok & (Z != 0) & !(has_any & (best < 0));
             // a best hint equal to the default affinity (no request on NUMA resources, or one zone)
@@ -878,13 +927,23 @@ __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& 
             if (zone_out) *zone_out = (skip || !has_any || Z == 1) ? -1 : best;  // the Reserve's zone (eval_pair o.zone)
         } else {
             // amplified requested for pods with a cpu request: (free - r) + delta * {0, 1}
-            const uint32_t sc = cvt_sat_u32(fma(r.amp_delta, p.has_cpu, r.numa_free_cpu - p.cpu) * r.rcp_cpu);
+            const uint32_t sc = KB ? cvt_sat_u32(r.numa_free_cpu * r.rcp_cpu)
+                                   : cvt_sat_u32(fma(r.amp_delta, p.has_cpu, r.numa_free_cpu - p.cpu) * r.rcp_cpu);
             const uint32_t sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
             s_numa = wq(mad24(sm, hi32(r.w_numa), mad24(sc, lo32(r.w_numa), 1u)), f32lo(r.w_aux));
         }
         ok = ok & (skip | nok);
         total = mad24(c.w_numa, skip ? 0u : s_numa, total);
     }
+    total_out = total;
+    return ok;
+}
+
+template <uint32_t PM, int CLS>
+__device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr,
+                                                  const PodF& p, uint32_t gidx, int32_t* zone_out = nullptr) {
+    uint32_t total;
+    const bool ok = fast_eval<PM, CLS>(c, r, zr, p, total, zone_out);
     const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - gidx);
     return ok ? key : 0ull;
 }

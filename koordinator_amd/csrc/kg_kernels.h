@@ -32,6 +32,7 @@ struct LaunchSelect {
     uint64_t* out;
     const uint32_t* big_list;
     const uint32_t* big_count;
+    const uint32_t* order;  // fused select: the batch grouped by wave kind (nullptr: batch order)
 };
 
 // Block replay (k_rb_top / k_rb_merge / k_rb_fix): window of RB_W pods, RB_K keys kept per pod,

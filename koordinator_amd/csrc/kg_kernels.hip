@@ -41,16 +41,36 @@ __device__ __forceinline__ uint32_t rec_gidx(const NodeRec& r, uint32_t index_ba
 // Records [begin, end) are walked in chunks of `chunk`; blockIdx.y = chunk, partial row = part0 + chunk.
 // FAST: pods and weights fit the float64 fast path (host check); records flagged F_BIG are skipped
 // and evaluated on the integer path by k_merge_big.
+template <int K, uint32_t PM, int CLS, int KIND>
+__device__ __forceinline__ void select_fast_loop(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                 uint32_t lo, uint32_t hi, uint32_t index_base, const KCfg& cv,
+                                                 const PodF& pf, uint64_t (&top)[K]) {
+    for (uint32_t i = lo; i < hi; i++) {
+        const FastRec r = *reinterpret_cast<const FastRec*>(&nodes[i].v[FAST_BEGIN]);
+        uint32_t total;
+        const bool ok = fast_eval<PM, CLS, KIND>(cv, r, zones + i, pf, total);
+        const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - (index_base + (uint32_t)((uint64_t)r.flags >> 32)));
+        // F_BIG records (integer path in k_merge_big) are masked, not branched around: one wait
+        // for the whole record
+        topk_insert<K>(top, (ok & !((uint32_t)r.flags & F_BIG)) ? key : 0ull);
+    }
+}
+
+// Records [begin, end) are walked in chunks of `chunk`; blockIdx.y = chunk, partial row = part0 + chunk.
+// FAST: pods and weights fit the float64 fast path (host check); records flagged F_BIG are skipped
+// and evaluated on the integer path by k_merge_big. `order` (nullable): lane -> pod, the batch grouped
+// by wave kind (kg_pods_upload); partial rows stay indexed by pod.
 template <int K, bool EXACT, bool FAST, uint32_t PM, int CLS>
 __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                 PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
                                                 uint32_t chunk, uint32_t part0, uint32_t index_base, KCfg cfg,
                                                 uint64_t* __restrict__ partial, const uint32_t* __restrict__ pmap,
-                                                uint32_t* __restrict__ pstat) {
+                                                uint32_t* __restrict__ pstat, const uint32_t* __restrict__ order) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t c = blockIdx.y;
     const bool live = j < n_pods;
-    const PodV p = load_pod(pods, live ? j : 0);
+    const uint32_t row = live ? (order ? order[j] : j) : 0u;
+    const PodV p = load_pod(pods, row);
     uint64_t top[K];
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
@@ -62,13 +82,12 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
         // policy are F_BIG (flagged by k_merge_big), a batch with a cpuset-binding pod is not fast_ok
         const PodF pf = to_podf(p, cfg);
         const KCfg cv = cfg_in_vgprs(cfg);
-        for (uint32_t i = lo; i < hi; i++) {
-            const FastRec r = *reinterpret_cast<const FastRec*>(&nodes[i].v[FAST_BEGIN]);
-            const uint64_t key = eval_fast_key<PM, CLS>(cv, r, zones + i, pf, index_base + (uint32_t)((uint64_t)r.flags >> 32));
-            // F_BIG records (integer path in k_merge_big) are masked, not branched around: one wait
-            // for the whole record
-            topk_insert<K>(top, ((uint32_t)r.flags & F_BIG) ? 0ull : key);
-        }
+        if (__all(!live || fast_kind_match(FK_PROD, p)))
+            select_fast_loop<K, PM, CLS, FK_PROD>(nodes, zones, lo, hi, index_base, cv, pf, top);
+        else if (__all(!live || fast_kind_match(FK_BATCH, p)))
+            select_fast_loop<K, PM, CLS, FK_BATCH>(nodes, zones, lo, hi, index_base, cv, pf, top);
+        else
+            select_fast_loop<K, PM, CLS, FK_ANY>(nodes, zones, lo, hi, index_base, cv, pf, top);
     } else {
         for (uint32_t i = lo; i < hi; i++) {
             const PairOut o = eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p);
@@ -77,39 +96,56 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
         }
     }
     if (live) {
-        uint64_t* dst = partial + ((size_t)(part0 + c) * n_pods + j) * K;
+        uint64_t* dst = partial + ((size_t)(part0 + c) * n_pods + row) * K;
 #pragma unroll
         for (int t = 0; t < K; t++) dst[t] = top[t];
-        if (unsup) atomicOr(pstat + (pmap ? pmap[j] : j), unsup);
+        if (unsup) atomicOr(pstat + (pmap ? pmap[row] : row), unsup);
     }
 }
 
 // Fused top-1 select of one storage class: lane = pod, blockIdx.y = chunk of records [begin, end); the
 // lane's best key goes to out[pod] by atomicMax. out was seeded by k_big_init with the pod's best key
-// over the F_BIG records (integer path), or 0; no per-chunk partials, no merge pass.
+// over the F_BIG records (integer path), or 0; no per-chunk partials, no merge pass. `order` (nullable)
+// lists the batch grouped by wave kind (kg_pods_upload), so most waves run a kind-specialised loop.
+template <uint32_t PM, int CLS, int KIND>
+__device__ __forceinline__ uint64_t select1_loop(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                 uint32_t lo, uint32_t hi, uint32_t index_base, const KCfg& cv,
+                                                 const PodF& pf) {
+    uint64_t top = 0;
+    for (uint32_t i = lo; i < hi; i++) {
+        const FastRec r = *reinterpret_cast<const FastRec*>(&nodes[i].v[FAST_BEGIN]);
+        uint32_t total;
+        const bool ok = fast_eval<PM, CLS, KIND>(cv, r, zones + i, pf, total);
+        const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - (index_base + (uint32_t)((uint64_t)r.flags >> 32)));
+        // F_BIG records: k_big_init; feasibility and the record test fold into the update's lane mask
+        const bool better = ok & !((uint32_t)r.flags & F_BIG) & (key > top);
+        top = better ? key : top;
+    }
+    return top;
+}
+
 template <uint32_t PM, int CLS>
 __global__ __launch_bounds__(256) void k_select1(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                  PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
                                                  uint32_t chunk, uint32_t index_base, KCfg cfg,
-                                                 uint64_t* __restrict__ out, const uint32_t* __restrict__ pmap,
-                                                 uint32_t* __restrict__ pstat) {
+                                                 uint64_t* __restrict__ out, const uint32_t* __restrict__ order) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = j < n_pods;
-    const PodV p = load_pod(pods, live ? j : 0);
+    const uint32_t o = live ? (order ? order[j] : j) : 0u;
+    const PodV p = load_pod(pods, o);
     const uint32_t lo = begin + blockIdx.y * chunk;
     const uint32_t hi = min(end, lo + chunk);
     const PodF pf = to_podf(p, cfg);
     const KCfg cv = cfg_in_vgprs(cfg);
-    uint64_t top = 0;
-    for (uint32_t i = lo; i < hi; i++) {
-        const FastRec r = *reinterpret_cast<const FastRec*>(&nodes[i].v[FAST_BEGIN]);
-        const uint64_t key = eval_fast_key<PM, CLS>(cv, r, zones + i, pf, index_base + (uint32_t)((uint64_t)r.flags >> 32));
-        const uint64_t k2 = ((uint32_t)r.flags & F_BIG) ? 0ull : key;  // F_BIG records: k_big_init
-        top = k2 > top ? k2 : top;
-    }
-    if (live) {
-        if (top) atomicMax((unsigned long long*)(out + j), (unsigned long long)top);
-    }
+    uint64_t top;
+    // wave-uniform dispatch (idle lanes match any kind)
+    if (__all(!live || fast_kind_match(FK_PROD, p)))
+        top = select1_loop<PM, CLS, FK_PROD>(nodes, zones, lo, hi, index_base, cv, pf);
+    else if (__all(!live || fast_kind_match(FK_BATCH, p)))
+        top = select1_loop<PM, CLS, FK_BATCH>(nodes, zones, lo, hi, index_base, cv, pf);
+    else
+        top = select1_loop<PM, CLS, FK_ANY>(nodes, zones, lo, hi, index_base, cv, pf);
+    if (live && top) atomicMax((unsigned long long*)(out + o), (unsigned long long)top);
 }
 
 // Seeds the fused select's output: per pod, the best key over the F_BIG records (integer path), 0 if none.
@@ -615,7 +651,7 @@ static void select_instance(const LaunchSelect& a, const SelectRange& r, hipStre
     dim3 grid((a.n_pods + 255) / 256, r.n_chunks), block(256);
     k_select<K, EXACT, FAST, PM, CLS><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end,
                                                              r.chunk, r.part0, a.index_base, a.cfg, a.partial, a.pmap,
-                                                             a.pstat);
+                                                             a.pstat, a.fast ? a.order : nullptr);
 }
 
 template <int K, int CLS>
@@ -645,10 +681,10 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
     do {                                                                                                           \
         if (cls == 0)                                                                                              \
             k_select1<PMV, 0><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end, r.chunk,  \
-                                                     a.index_base, a.cfg, a.out, a.pmap, a.pstat);                 \
+                                                     a.index_base, a.cfg, a.out, a.order);                         \
         else                                                                                                       \
             k_select1<PMV, 1><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end, r.chunk,  \
-                                                     a.index_base, a.cfg, a.out, a.pmap, a.pstat);                 \
+                                                     a.index_base, a.cfg, a.out, a.order);                         \
     } while (0)
             switch (a.cfg.plugins & 7u) {
                 case 0: KG_SEL1(0); break;

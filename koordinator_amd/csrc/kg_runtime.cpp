@@ -185,6 +185,7 @@ struct kg_pods {
     int64_t* d_pcols = nullptr;   // 9 int64 columns of `cap` entries (plain pods, compacted)
     uint32_t* d_pflags = nullptr;
     uint32_t* d_pmap = nullptr;   // plain row -> batch position
+    uint32_t* d_order = nullptr;  // batch positions grouped by wave kind (fast select lanes)
     uint32_t* d_xlist = nullptr;  // config-5 row -> batch position
     uint64_t* d_tkeys = nullptr;  // [KG_TOPK_MAX][cap] sub-batch keys before the scatter
     uint32_t n_plain = 0, n_x = 0;
@@ -1068,6 +1069,7 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_pcols, sizeof(int64_t) * 9 * capacity) == hipSuccess &&
               hipMalloc(&p->d_pflags, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_pmap, sizeof(uint32_t) * capacity) == hipSuccess &&
+              hipMalloc(&p->d_order, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_xlist, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
               hipMalloc(&p->d_pstat, sizeof(uint32_t) * capacity) == hipSuccess &&
@@ -1083,8 +1085,8 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
         for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst,
                         (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors,
                         (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_pcols, (void*)p->d_pflags,
-                        (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys, (void*)p->d_pstat, (void*)p->d_reason,
-                        (void*)p->d_dcls, (void*)p->d_dclass})
+                        (void*)p->d_pmap, (void*)p->d_order, (void*)p->d_xlist, (void*)p->d_tkeys, (void*)p->d_pstat,
+                        (void*)p->d_reason, (void*)p->d_dcls, (void*)p->d_dclass})
             hipFree(b);
         delete p;
         return fail(ctx, KG_OOM, "pod batch of %u", capacity);
@@ -1203,6 +1205,21 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
     std::stable_sort(stat.begin(), stat.end(), by_kind);
     std::stable_sort(xlist.begin(), xlist.end(), by_kind);
+    // fast select: pods grouped by wave kind (fast_kind_match in kg_eval.h), so whole waves run a
+    // kind-specialised loop; keys are written per pod, so the order changes no result
+    auto wave_kind = [&](uint32_t j) {
+        const uint32_t fl = f[j];
+        const int64_t cpu = h[j], mem = h[(size_t)n + j], sc0 = h[3 * (size_t)n + j], sc1 = h[4 * (size_t)n + j];
+        const uint32_t excl = KG_POD_DAEMONSET | KG_POD_NUMA_SKIP | KG_POD_CPU_BIND;
+        if ((fl & (KG_POD_PROD | excl)) == KG_POD_PROD && sc0 == 0 && sc1 == 0) return 0;
+        if ((fl & (KG_POD_PROD | excl | KG_POD_HAS_CPU | KG_POD_HAS_MEM)) == 0 && cpu == 0 && mem == 0 && sc0 != 0 && sc1 != 0)
+            return 1;
+        return 2;
+    };
+    std::vector<uint32_t> order(n);
+    for (uint32_t j = 0; j < n; j++) order[j] = j;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return wave_kind(a) < wave_kind(b); });
+    std::stable_sort(pmap.begin(), pmap.end(), [&](uint32_t a, uint32_t b) { return wave_kind(a) < wave_kind(b); });
     uint32_t n_stat_cls = 0;
     while (n_stat_cls < stat.size() && xc[stat[n_stat_cls]] == 0) n_stat_cls++;
     const uint32_t np = (uint32_t)pmap.size();
@@ -1230,6 +1247,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     }
     if (!xlist.empty())
         HIP_TRY(ctx, hipMemcpyAsync(p->d_xlist, xlist.data(), sizeof(uint32_t) * xlist.size(), hipMemcpyHostToDevice, ctx->stream));
+    if (n) HIP_TRY(ctx, hipMemcpyAsync(p->d_order, order.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
     p->n_plain = np;
     p->n_x = (uint32_t)xlist.size();
     for (int c = 0; c < 9; c++)
@@ -1259,7 +1277,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     hipFree(p->d_gather);
     for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst, (void*)p->d_dev_max,
                     (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout,
-                    (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_xlist, (void*)p->d_tkeys,
+                    (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_order, (void*)p->d_xlist, (void*)p->d_tkeys,
                     (void*)p->d_pstat, (void*)p->d_reason, (void*)p->d_dcls, (void*)p->d_dclass, (void*)p->d_devsum,
                     (void*)p->d_pairs, (void*)p->d_batch})
         hipFree(b);
@@ -1611,6 +1629,7 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     a.cfg = s->kcfg;
     a.pmap = nullptr;
     a.pstat = p->d_pstat;
+    a.order = p->d_order;
     a.fused = a.fast && kk == 1 && !unfused();
     if (a.fused) {
         a.out = d_out;
