@@ -816,9 +816,6 @@ __device__ __forceinline__ bool fast_kind_match(int kind, const PodV& p) {
            p.req_cpu == 0 && p.req_mem == 0 && p.sc0 != 0 && p.sc1 != 0;
 }
 
-// sign of a fast-block double from its high word (a scalar test: fit values are +x or -1.0)
-__device__ __forceinline__ bool neg_bits(double x) { return (int32_t)((uint64_t)__double_as_longlong(x) >> 32) < 0; }
-
 // fast_eval: the weighted total in `total`, feasibility as the return value (select loops fold it into
 // their top-key update); eval_fast_key: the selection key, 0 when infeasible.
 template <uint32_t PM, int CLS, int KIND = FK_ANY>
@@ -833,7 +830,7 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
         // Fits: request r fails iff r > 0 and r > alloc - requested, i.e. 100 r > 100 max(0, headroom)
         // ("Too many pods" is folded into fit_cpu by derive_node: -1.0, the only negative fit value)
         bool fit_fail = p.eph > r.fit_eph;
-        if constexpr (KB) fit_fail = fit_fail | neg_bits(r.fit_cpu);
+        if constexpr (KB) fit_fail = fit_fail | ((f & F_PODS_FULL) != 0);  // 0 > fit_cpu: only the folded bit
         else fit_fail = fit_fail | (p.cpu > r.fit_cpu) | (p.mem > r.fit_mem);
         if constexpr (!KP) fit_fail = fit_fail | (p.sc0 > r.fit_sc0) | (p.sc1 > r.fit_sc1);
         ok = ok & !fit_fail;
@@ -841,18 +838,24 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
         const uint32_t w0 = lo32(r.w_nrf01), w1 = hi32(r.w_nrf01);
         uint32_t sum2 = mad24(lr100(r.lr_nz_cpu, p.nzc, r.rcp_cpu), w0, 1u);
         sum2 = mad24(lr100(r.lr_nz_mem, p.nzm, r.rcp_mem), w1, sum2);
-        uint32_t wsum_u = hi32(r.w_aux);
-        if constexpr (!KP) {
-            const uint32_t w2 = KB ? lo32(r.w_nrf23) : (p.sc0_on ? lo32(r.w_nrf23) : 0u);
-            const uint32_t w3 = KB ? hi32(r.w_nrf23) : (p.sc1_on ? hi32(r.w_nrf23) : 0u);
+        // h = 1 / max(Σ 2w, 2) (Σ 2w = 0 -> sum2 = 1 and trunc(1 * 0.5) = 0): set by the host for the two
+        // kinds (correctly rounded), else rcp + one Newton step (<= 1 ulp)
+        float h;
+        if constexpr (KP) {
+            h = f32hi(r.w_aux);
+        } else {
+            const uint32_t w23 = lo32(r.w_nrf23), w2s = w23 & 0xFFFFu, w3s = w23 >> 16;
+            const uint32_t w2 = KB ? w2s : (p.sc0_on ? w2s : 0u), w3 = KB ? w3s : (p.sc1_on ? w3s : 0u);
             sum2 = mad24(lr100(r.lr_sc0, p.sc0, r.rcp_sc0), w2, sum2);
             sum2 = mad24(lr100(r.lr_sc1, p.sc1, r.rcp_sc1), w3, sum2);
-            wsum_u = wsum_u + w2 + w3;
+            if constexpr (KB) {
+                h = f32hi(r.w_nrf23);
+            } else {
+                const float wsum = (float)max(w0 + w1 + w2 + w3, 2u);
+                h = __builtin_amdgcn_rcpf(wsum);
+                h = fmaf(h, fmaf(-wsum, h, 1.0f), h);
+            }
         }
-        // Σ 2w = 0 -> sum2 = 1, and max(.., 2) gives trunc(1 * 0.5) = 0
-        const float wsum = (float)max(wsum_u, 2u);
-        float h = __builtin_amdgcn_rcpf(wsum);
-        h = fmaf(h, fmaf(-wsum, h, 1.0f), h);  // one Newton step: 1/(Σ 2w) = 0.5/Σw, <= 1 ulp
         total = mad24(c.w_nrf, wq(sum2, h), total);
     }
 

@@ -47,9 +47,9 @@ enum NodeSlot : int {
     // truncating quotient for 0 <= F <= capacity < 2^44 (see lr100 in kg_eval.h)
     N_RCP_CPU, N_RCP_MEM, N_RCP_SC0, N_RCP_SC1, N_RCP_LA0, N_RCP_LA1,
     N_W_NRF01,            // uint32 x 2: 2 x LeastAllocated weight of cpu, memory (0 if capacity 0)
-    N_W_NRF23,            // uint32 x 2: same for scalar0, scalar1
+    N_W_NRF23,            // uint16 x 2: same for scalar0, scalar1 | float 1 / max(Σ 2w of all four, 2)
     N_W_NUMA,             // uint32 2*w_cpu, uint32 2*w_mem of the NodeNUMAResource score (0 if capacity 0)
-    N_W_AUX,              // float 0.5 / (w_cpu + w_mem) of the NUMA score | uint32 N_W_NRF01 sum
+    N_W_AUX,              // float 0.5 / (w_cpu + w_mem) of the NUMA score | float 1 / max(N_W_NRF01 sum, 2)
     D_FIT_CPU,            // 100 * max(0, alloc - requested): Fits (pod request r fails iff 100 r > this)
     D_FIT_MEM, D_FIT_EPH, D_FIT_SC0, D_FIT_SC1,
     D_LR_NZ_CPU,          // 100 * (alloc - nonzero requested): LeastAllocated cpu

@@ -434,13 +434,19 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     {
         const int64_t w0 = on(c.nrf_w_cpu, v[N_ALLOC_CPU]), w1 = on(c.nrf_w_mem, v[N_ALLOC_MEM]);
         v[N_W_NRF01] = (int64_t)pack32(w0, w1);
-        v[N_W_NRF23] = (int64_t)pack32(on(c.nrf_w_sc[0], v[N_SC_ALLOC0]), on(c.nrf_w_sc[1], v[N_SC_ALLOC1]));
+        // scalar weights as 16-bit halves (the fast path requires weights <= 4096) and 1 / max(Σ 2w, 2) over
+        // all four resources, the reciprocal of pods requesting both scalars
+        const int64_t w2 = on(c.nrf_w_sc[0], v[N_SC_ALLOC0]), w3 = on(c.nrf_w_sc[1], v[N_SC_ALLOC1]);
+        uint32_t hb4;
+        const float h4 = 1.0f / (float)std::max<int64_t>(w0 + w1 + w2 + w3, 2);
+        std::memcpy(&hb4, &h4, 4);
+        v[N_W_NRF23] = (int64_t)pack32((w2 & 0xFFFF) | ((w3 & 0xFFFF) << 16), hb4);
         const int64_t wc = on(c.numa_w_cpu, v[N_ALLOC_CPU]), wm = on(c.numa_w_mem, v[N_ALLOC_MEM]);
         v[N_W_NUMA] = (int64_t)pack32(wc, wm);
-        uint32_t hb;
-        const float hw = half_rcp((wc + wm) / 2);
-        std::memcpy(&hb, &hw, 4);
-        v[N_W_AUX] = (int64_t)pack32(hb, w0 + w1);
+        // NUMA score 0.5 / (w_cpu + w_mem); LeastAllocated 1 / max(Σ 2w, 2) over cpu / memory (correctly
+        // rounded: within the weighted-mean error bound of kg_eval.h, so pods without scalar requests
+        // need no reciprocal in the select loop)
+        v[N_W_AUX] = (int64_t)pack_f32(half_rcp((wc + wm) / 2), 1.0f / (float)std::max<int64_t>(w0 + w1, 2));
     }
     for (int z = 0; z < KG_MAX_ZONES; z++) {
         zr->cpu[z] = COL(s->zone_cpu[z], i);
