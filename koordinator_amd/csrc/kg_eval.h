@@ -942,28 +942,13 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
     return ok;
 }
 
-template <uint32_t PM, int CLS, int KIND = FK_ANY>
+template <uint32_t PM, int CLS>
 __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr,
                                                   const PodF& p, uint32_t gidx, int32_t* zone_out = nullptr) {
     uint32_t total;
-    const bool ok = fast_eval<PM, CLS, KIND>(c, r, zr, p, total, zone_out);
+    const bool ok = fast_eval<PM, CLS>(c, r, zr, p, total, zone_out);
     const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - gidx);
     return ok ? key : 0ull;
-}
-
-// The wave's kind (wave-uniform; idle lanes match any kind) and eval_fast_key dispatched on it.
-__device__ __forceinline__ int wave_fast_kind(bool live, const PodV& p) {
-    if (__all(!live || fast_kind_match(FK_PROD, p))) return FK_PROD;
-    if (__all(!live || fast_kind_match(FK_BATCH, p))) return FK_BATCH;
-    return FK_ANY;
-}
-
-template <uint32_t PM, int CLS>
-__device__ __forceinline__ uint64_t eval_fast_key_wk(int wk, const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr,
-                                                     const PodF& p, uint32_t gidx) {
-    if (wk == FK_PROD) return eval_fast_key<PM, CLS, FK_PROD>(c, r, zr, p, gidx);
-    if (wk == FK_BATCH) return eval_fast_key<PM, CLS, FK_BATCH>(c, r, zr, p, gidx);
-    return eval_fast_key<PM, CLS, FK_ANY>(c, r, zr, p, gidx);
 }
 
 }  // namespace kg

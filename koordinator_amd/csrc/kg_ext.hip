@@ -193,11 +193,9 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
     uint64_t pk = PREF_NONE;
     PodF pff{};
     KCfg cv = cfg;
-    int wk = FK_ANY;
     if constexpr (FB) {
         pff = to_podf(p, cfg);
         cv = cfg_in_vgprs(cfg);
-        wk = wave_fast_kind(live, p);
     }
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
     const uint32_t dcls = pods.dev_cls ? pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
@@ -213,7 +211,7 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
                 uint32_t pv = 0;
                 if ((cfg.plugins & KG_PLUGIN_DEV) && px.dcount != 0) {
                     const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
-                    const uint64_t bk = eval_fast_key_wk<7u, 0>(wk, cv, fr, zones + rec, pff, 0u);
+                    const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
                     int64_t raw = 0;
                     uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
                     if (!st) st |= dev_eval_sum(cfg, n, dev_of(e, rec), e.dsum + rec, px, dcls, raw);
@@ -368,11 +366,9 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
     const uint32_t lo = blockIdx.y * chunk, hi = min(n_nodes, lo + chunk);
     PodF pff{};
     KCfg cv = cfg;
-    int wk = FK_ANY;
     if constexpr (FB) {
         pff = to_podf(p, cfg);
         cv = cfg_in_vgprs(cfg);
-        wk = wave_fast_kind(live, p);
     }
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
     const uint32_t dcls = pods.dev_cls ? pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
@@ -402,7 +398,7 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
                 }
                 const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
                 const uint32_t g = index_base + (uint32_t)((uint64_t)fr.flags >> 32);
-                const uint64_t bk = eval_fast_key_wk<7u, 0>(wk, cv, fr, zones + rec, pff, g);
+                const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, g);
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
                 int64_t s_dev = 0;
                 if ((cfg.plugins & KG_PLUGIN_DEV) && !st)  // only the key's zero-ness matters once st != 0

@@ -1200,6 +1200,17 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         if (cnt == 0 && cls < 0 && !(f[j] & KG_POD_RSV_REQUIRED)) pmap.push_back(j);
         else xlist.push_back(j);
     }
+    // wave-uniform work in the config-5 kernels: GPU pods (by GPU count) first, then reservation
+    // classes in order; rows are scattered back by list, so the order does not change any result
+    auto kind = [&](uint32_t j) {
+        const uint32_t cnt = xc[j];
+        const uint64_t gpu = cnt > 0 ? ((uint64_t)(0u - cnt) << 8) | (xc[(size_t)n + j] & 0xFFu) : 0u;  // count, request keys
+        const int32_t cls = (int32_t)xc[4 * (size_t)n + j];
+        return std::make_tuple(gpu, (f[j] & KG_POD_RSV_REQUIRED) != 0, cls);
+    };
+    auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
+    std::stable_sort(stat.begin(), stat.end(), by_kind);
+    std::stable_sort(xlist.begin(), xlist.end(), by_kind);
     // fast select: pods grouped by wave kind (fast_kind_match in kg_eval.h), so whole waves run a
     // kind-specialised loop; keys are written per pod, so the order changes no result
     auto wave_kind = [&](uint32_t j) {
@@ -1211,18 +1222,6 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             return 1;
         return 2;
     };
-    // wave-uniform work in the config-5 kernels: GPU pods (by GPU count) first, then reservation
-    // classes in order, then the wave kind; rows are scattered back by list, so the order does not
-    // change any result
-    auto kind = [&](uint32_t j) {
-        const uint32_t cnt = xc[j];
-        const uint64_t gpu = cnt > 0 ? ((uint64_t)(0u - cnt) << 8) | (xc[(size_t)n + j] & 0xFFu) : 0u;  // count, request keys
-        const int32_t cls = (int32_t)xc[4 * (size_t)n + j];
-        return std::make_tuple(gpu, (f[j] & KG_POD_RSV_REQUIRED) != 0, cls, wave_kind(j));
-    };
-    auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
-    std::stable_sort(stat.begin(), stat.end(), by_kind);
-    std::stable_sort(xlist.begin(), xlist.end(), by_kind);
     std::vector<uint32_t> order(n);
     for (uint32_t j = 0; j < n; j++) order[j] = j;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return wave_kind(a) < wave_kind(b); });
