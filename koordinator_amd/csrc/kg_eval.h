@@ -799,8 +799,9 @@ __device__ __forceinline__ KCfg cfg_in_vgprs(const KCfg& c) {
 // PM: enabled plugins (KG_PLUGIN_* mask); CLS: node storage class (node_class), both compile-time.
 // Wave kinds of the fast select (a wave whose 64 pods all share one of these shapes runs a loop
 // specialised for it; the host groups a batch's pods by kind, kg_pods_upload):
-//   FK_PROD  - prod pods (KG_POD_PROD), no DaemonSet, no scalar (batch) requests, NodeNUMAResource not
-//              skipped, no cpuset binding: the LoadAware prod profile, no scalar Fits / LeastAllocated terms;
+//   FK_PROD  - prod pods (KG_POD_PROD) requesting cpu or memory, no DaemonSet, no scalar (batch) requests,
+//              NodeNUMAResource not skipped, no cpuset binding: the LoadAware prod profile, no scalar Fits /
+//              LeastAllocated terms, no node-level NUMA score on multi-zone SingleNUMANode nodes;
 //   FK_BATCH - non-prod pods with both scalar requests and no cpu / memory request (koord-batch pods),
 //              no DaemonSet, no HAS_CPU / HAS_MEM, not skipped, no cpuset binding: the non-prod profile, both scalar terms,
 //              the cpu / memory Fits reduce to the node's "Too many pods" bit, no NUMA zone walk.
@@ -810,8 +811,8 @@ enum : int { FK_ANY = 0, FK_PROD = 1, FK_BATCH = 2 };
 __device__ __forceinline__ bool fast_kind_match(int kind, const PodV& p) {
     const uint32_t f = p.flags;
     if (kind == FK_PROD)
-        return (f & (KG_POD_PROD | KG_POD_DAEMONSET | KG_POD_NUMA_SKIP | KG_POD_CPU_BIND)) == KG_POD_PROD && p.sc0 == 0 &&
-               p.sc1 == 0;
+        return (f & (KG_POD_PROD | KG_POD_DAEMONSET | KG_POD_NUMA_SKIP | KG_POD_CPU_BIND)) == KG_POD_PROD &&
+               (f & (KG_POD_HAS_CPU | KG_POD_HAS_MEM)) != 0 && p.sc0 == 0 && p.sc1 == 0;
     return (f & (KG_POD_PROD | KG_POD_DAEMONSET | KG_POD_NUMA_SKIP | KG_POD_CPU_BIND | KG_POD_HAS_CPU | KG_POD_HAS_MEM)) == 0 &&
            p.req_cpu == 0 && p.req_mem == 0 && p.sc0 != 0 && p.sc1 != 0;
 }
@@ -902,7 +903,7 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
             const uint32_t Z = (f >> F_NUMA_ZONES_SHIFT) & 15u;
             const bool has_cpu = KB ? false : (p.flags & KG_POD_HAS_CPU) != 0;
             const bool has_mem = KB ? false : (p.flags & KG_POD_HAS_MEM) != 0;
-            const bool has_any = has_cpu | has_mem;
+            const bool has_any = KP ? true : has_cpu | has_mem;
             int32_t best = -1;
             uint32_t best_score = 0;
             if constexpr (!KB) {
@@ -924,8 +925,11 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
             nok = nok & (Z != 0) & !(has_any & (best < 0));
             // a best hint equal to the default affinity (no request on NUMA resources, or one zone)
             // carries no affinity: node-level score without amplification
-            const uint32_t sc = lr100(r.numa_free_cpu, p.cpu, r.rcp_cpu), sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
-            const uint32_t node_level = wq(mad24(sm, hi32(r.w_numa), mad24(sc, lo32(r.w_numa), 1u)), f32lo(r.w_aux));
+            uint32_t node_level = 0;
+            if (!KP || Z == 1) {  // FK_PROD: a wave-uniform branch on the record's zone count
+                const uint32_t sc = lr100(r.numa_free_cpu, p.cpu, r.rcp_cpu), sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
+                node_level = wq(mad24(sm, hi32(r.w_numa), mad24(sc, lo32(r.w_numa), 1u)), f32lo(r.w_aux));
+            }
             s_numa = (!has_any || Z == 1) ? node_level : best_score;
             if (zone_out) *zone_out = (skip || !has_any || Z == 1) ? -1 : best;  // the Reserve's zone (eval_pair o.zone)
         } else {

@@ -1217,7 +1217,8 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         const uint32_t fl = f[j];
         const int64_t cpu = h[j], mem = h[(size_t)n + j], sc0 = h[3 * (size_t)n + j], sc1 = h[4 * (size_t)n + j];
         const uint32_t excl = KG_POD_DAEMONSET | KG_POD_NUMA_SKIP | KG_POD_CPU_BIND;
-        if ((fl & (KG_POD_PROD | excl)) == KG_POD_PROD && sc0 == 0 && sc1 == 0) return 0;
+        if ((fl & (KG_POD_PROD | excl)) == KG_POD_PROD && (fl & (KG_POD_HAS_CPU | KG_POD_HAS_MEM)) && sc0 == 0 && sc1 == 0)
+            return 0;
         if ((fl & (KG_POD_PROD | excl | KG_POD_HAS_CPU | KG_POD_HAS_MEM)) == 0 && cpu == 0 && mem == 0 && sc0 != 0 && sc1 != 0)
             return 1;
         return 2;

@@ -17,7 +17,7 @@ def wave_kind(pods, j):
     """Host restatement of the kind predicate (0 prod, 1 koord-batch, 2 general)."""
     f = int(pods["flags"][j])
     sc0, sc1 = int(pods["sc_req0"][j]), int(pods["sc_req1"][j])
-    if (f & (PROD | DS | SKIP | BIND)) == PROD and sc0 == 0 and sc1 == 0:
+    if (f & (PROD | DS | SKIP | BIND)) == PROD and f & (abi.KG_POD_HAS_CPU | abi.KG_POD_HAS_MEM) and sc0 == 0 and sc1 == 0:
         return 0
     if (f & (PROD | DS | SKIP | BIND | abi.KG_POD_HAS_CPU | abi.KG_POD_HAS_MEM)) == 0 and \
             pods["req_cpu"][j] == 0 and pods["req_mem"][j] == 0 and sc0 != 0 and sc1 != 0:
@@ -38,6 +38,8 @@ def edge_cluster(seed, n_nodes=1500, n_pods=900):
     nodes["alloc_cpu"][zero_cpu] = 0
     nodes["req_cpu"][zero_cpu] = 0
     nodes["nz_cpu"][zero_cpu] = 0
+    one_zone = (nodes["numa_policy"] == abi.KG_NUMA_SINGLE_NODE) & (r.random(n_nodes) < 0.3)
+    nodes["numa_zones"][one_zone] = 1  # node-level NUMA score on single-zone SingleNUMANode nodes
     # pods: DaemonSet prod pods, prod pods with one scalar request, batch pods with one scalar only
     ds = r.random(n_pods) < 0.05
     pods["flags"][ds] |= DS
@@ -47,6 +49,8 @@ def edge_cluster(seed, n_nodes=1500, n_pods=900):
     batch = ~prod & (pods["sc_req0"] > 0)
     half = batch & (r.random(n_pods) < 0.05)
     pods["sc_req1"][half] = 0
+    nohas = prod & (r.random(n_pods) < 0.03)  # prod pods without HAS_CPU / HAS_MEM: the general loop
+    pods["flags"][nohas] &= ~np.uint32(abi.KG_POD_HAS_CPU | abi.KG_POD_HAS_MEM)
     return cfg, nodes, pods
 
 
