@@ -478,6 +478,146 @@ __device__ __forceinline__ uint64_t rb_int_eval(const KCfg* cfg, const NodeRec* 
     return pair_key(*cfg, o, g);
 }
 
+// Lane-parallel Reserve of pod j on one LDS-staged row for the window replay's serial loop: the same
+// bits as apply_assume (sign +1; kg_eval.h) followed by derive_node (kg_layout.h), with the int-slot
+// updates, the F_BIG checks, the four zone headrooms and the derived fast slots spread over the
+// wave's lanes instead of one lane's chain of dependent LDS accesses. Multi-zone NUMA splits
+// (zone >= 0x40) keep the one-lane apply_assume. Call with all 64 lanes active.
+enum : uint8_t { DER_FIT = 0, DER_DIFF = 1, DER_HEAD = 2, DER_AMP_FIT = 3, DER_AMP_DELTA = 4 };
+constexpr int N_DER = 21;
+__constant__ uint8_t DER_DST[N_DER] = {D_FIT_CPU, D_FIT_MEM, D_FIT_EPH, D_FIT_SC0, D_FIT_SC1, D_LR_NZ_CPU, D_LR_NZ_MEM,
+                                      D_LR_SC0, D_LR_SC1, D_LA_HEAD_NP0, D_LA_HEAD_NP1, D_LA_HEAD_PROD0, D_LA_HEAD_PROD1,
+                                      D_LA_SFREE_NP0, D_LA_SFREE_NP1, D_LA_SDELTA0, D_LA_SDELTA1, D_NUMA_FREE_CPU,
+                                      D_NUMA_FREE_MEM, D_AMP_FIT, D_AMP_DELTA};
+__constant__ uint8_t DER_A[N_DER] = {N_ALLOC_CPU, N_ALLOC_MEM, N_ALLOC_EPH, N_SC_ALLOC0, N_SC_ALLOC1, N_ALLOC_CPU,
+                                    N_ALLOC_MEM, N_SC_ALLOC0, N_SC_ALLOC1, N_LA_FCUT_NP0, N_LA_FCUT_NP1, N_LA_FCUT_PROD0,
+                                    N_LA_FCUT_PROD1, N_LA_ALLOC0, N_LA_ALLOC1, N_LA_SBASE_NP0, N_LA_SBASE_NP1, N_ALLOC_CPU,
+                                    N_ALLOC_MEM, N_ALLOC_CPU, N_CPUSET};
+__constant__ uint8_t DER_B[N_DER] = {N_REQ_CPU, N_REQ_MEM, N_REQ_EPH, N_SC_REQ0, N_SC_REQ1, N_NZ_CPU, N_NZ_MEM,
+                                    N_SC_REQ0, N_SC_REQ1, N_LA_FBASE_NP0, N_LA_FBASE_NP1, N_LA_FBASE_PROD0,
+                                    N_LA_FBASE_PROD1, N_LA_SBASE_NP0, N_LA_SBASE_NP1, N_LA_SBASE_PROD0, N_LA_SBASE_PROD1,
+                                    N_REQ_CPU, N_REQ_MEM, N_REQ_CPU, N_AMP_CPUSET};
+__constant__ uint8_t DER_OP[N_DER] = {DER_FIT, DER_FIT, DER_FIT, DER_FIT, DER_FIT, DER_DIFF, DER_DIFF, DER_DIFF, DER_DIFF,
+                                     DER_HEAD, DER_HEAD, DER_HEAD, DER_HEAD, DER_DIFF, DER_DIFF, DER_DIFF, DER_DIFF,
+                                     DER_DIFF, DER_DIFF, DER_AMP_FIT, DER_AMP_DELTA};
+
+__device__ __forceinline__ void derive_node_wave(NodeRec& r, ZoneRec& z, uint32_t lane) {
+    int64_t* v = r.v;
+    const uint64_t hi = (uint64_t)v[N_FLAGS] & 0xFFFFFFFF00000000ull;
+    const uint32_t f0 = (uint32_t)v[N_FLAGS] & ~(uint32_t)F_DERIVED_MASK;
+    const bool full = v[N_NUM_PODS] + 1 > v[N_ALLOC_PODS];
+    const int64_t always_fail = kg_bits(-1.0), never_fail = kg_bits(4611686018427387904.0);
+    // F_BIG checks: int slot `lane`, the cpuset pair (lane 63), zone lane - 32
+    bool big = false;
+    if (lane <= (uint32_t)N_LA_SBASE_PROD1 && lane != (uint32_t)N_ALLOC_PODS && lane != (uint32_t)N_NUM_PODS &&
+        !(lane >= (uint32_t)N_LA_FCUT_NP0 && lane <= (uint32_t)N_LA_FCUT_PROD1)) {
+        const int64_t x = v[lane];
+        big = kg_big(x) || x < 0;
+    }
+    if (lane == 63) {
+        const int64_t cs = v[N_CPUSET], acs = v[N_AMP_CPUSET];
+        big = kg_big(cs) || kg_big(acs) || cs < 0 || acs < cs;
+    }
+    const bool zl = lane >= 32u && lane < 32u + (uint32_t)MAX_ZONES;
+    const uint32_t q = zl ? lane - 32u : 0u;
+    double zv[6] = {0, 0, 0, 0, 0, 0};
+    if (zl) {
+        const int64_t tc = z.cpu[q], tm = z.mem[q], uc = z.cpu_used[q], um = z.mem_used[q];
+        big = kg_big(tc) || kg_big(tm) || kg_big(uc) || kg_big(um) || uc < 0 || um < 0;
+        const int64_t ac = tc - uc < 0 ? 0 : tc - uc, am = tm - um < 0 ? 0 : tm - um;
+        const int64_t rc = tc - ac < 0 ? 0 : tc - ac, rm = tm - am < 0 ? 0 : tm - am;
+        zv[0] = ac != 0 ? x100(ac) : -1.0;
+        zv[1] = am != 0 ? x100(am) : -1.0;
+        zv[2] = x100(tc - rc);
+        zv[3] = x100(tm - rm);
+        zv[4] = x100(tc - uc);
+        zv[5] = x100(tm - um);
+    }
+    const uint32_t pol0 = (f0 >> F_NUMA_POLICY_SHIFT) & 15u;
+    const bool pol_host = pol0 == 1u /* KG_NUMA_BEST_EFFORT */ || pol0 == 2u /* KG_NUMA_RESTRICTED */;
+    const bool big_all = (__ballot(big) != 0ull) || pol_host || ((z.cpu_meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
+    const uint32_t f = f0 | (full ? (uint32_t)F_PODS_FULL : 0u) | (big_all ? (uint32_t)F_BIG : 0u);
+    // derived slot DER_DST[lane]
+    int64_t val = 0;
+    uint32_t dst = 0;
+    const bool dl = lane < (uint32_t)N_DER;
+    if (dl) {
+        dst = DER_DST[lane];
+        uint32_t a = DER_A[lane], b = DER_B[lane];
+        const uint32_t op = DER_OP[lane];
+        const uint32_t m_np = (f >> F_LA_FMODE_NP_SHIFT) & 3u, m_pr = (f >> F_LA_FMODE_PROD_SHIFT) & 3u;
+        uint32_t mode = m_np;
+        if (op == DER_HEAD && a >= (uint32_t)N_LA_FCUT_PROD0) {  // prod heads: the non-prod ones without prod thresholds
+            if (f & F_LA_PROD_THR) mode = m_pr;
+            else a -= 2u, b -= 2u;
+        }
+        const int64_t va = v[a], vb = v[b];
+        const bool amp = (f & F_AMP) != 0;
+        if (op == DER_FIT) {
+            const int64_t d = va - vb;
+            val = (lane == 0 && full) ? always_fail : kg_bits(x100(d < 0 ? 0 : d));
+        } else if (op == DER_DIFF) {
+            val = kg_bits(x100(va - vb));
+        } else if (op == DER_HEAD) {
+            val = mode == FMODE_PASS ? never_fail
+                : mode == FMODE_FAIL_EXPIRED ? always_fail : kg_bits(((double)va - (double)vb) * 100.0);
+        } else if (op == DER_AMP_FIT) {
+            const int64_t cs = v[N_CPUSET], acs = v[N_AMP_CPUSET];
+            const int64_t req_f = (vb >= cs && cs > 0) ? vb - cs + acs : vb;
+            const int64_t d = va - req_f;
+            val = pol_host ? always_fail : amp ? kg_bits(x100(d < 0 ? 0 : d)) : never_fail;
+        } else {
+            val = kg_bits(amp ? x100(va - vb) : 0.0);
+        }
+    }
+    wave_lds_sync();  // every read above before any write below
+    if (dl) v[dst] = val;
+    if (zl) {
+        ZoneFast& zf = z.zf[q];
+        zf.avail_cpu = zv[0];
+        zf.avail_mem = zv[1];
+        zf.hint_cpu = zv[2];
+        zf.hint_mem = zv[3];
+        zf.free_cpu = zv[4];
+        zf.free_mem = zv[5];
+    }
+    if (lane == 63) v[N_FLAGS] = (int64_t)(hi | f);
+    wave_lds_sync();
+}
+
+__device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& z, const PodsDev& pods, uint32_t j,
+                                            int32_t zone, uint32_t lane) {
+    int64_t* v = r.v;
+    const uint32_t flags = (uint32_t)v[N_FLAGS];
+    const bool la = (c.plugins & KG_PLUGIN_LA) && (flags & F_LA_HAS_METRIC);
+    const bool prod = (pods.flags[j] & KG_POD_PROD) != 0;
+    if (lane < (uint32_t)N_INT_SLOTS) {
+        int64_t add = 0;
+        switch (lane) {
+            case N_REQ_CPU: add = pods.req_cpu[j]; break;
+            case N_REQ_MEM: add = pods.req_mem[j]; break;
+            case N_REQ_EPH: add = pods.req_eph[j]; break;
+            case N_SC_REQ0: add = pods.sc_req0[j]; break;
+            case N_SC_REQ1: add = pods.sc_req1[j]; break;
+            case N_NZ_CPU: add = pods.nz_cpu[j]; break;
+            case N_NZ_MEM: add = pods.nz_mem[j]; break;
+            case N_NUM_PODS: add = 1; break;
+            case N_LA_FBASE_NP0: case N_LA_SBASE_NP0: add = la ? max(pods.la_est0[j], (int64_t)0) : 0; break;
+            case N_LA_FBASE_NP1: case N_LA_SBASE_NP1: add = la ? max(pods.la_est1[j], (int64_t)0) : 0; break;
+            case N_LA_FBASE_PROD0: case N_LA_SBASE_PROD0: add = la && prod ? max(pods.la_est0[j], (int64_t)0) : 0; break;
+            case N_LA_FBASE_PROD1: case N_LA_SBASE_PROD1: add = la && prod ? max(pods.la_est1[j], (int64_t)0) : 0; break;
+            default: break;
+        }
+        if (add) v[lane] += add;
+    }
+    if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES) {
+        if (lane == 32) z.cpu_used[zone] += pods.req_cpu[j];
+        if (lane == 33) z.mem_used[zone] += pods.req_mem[j];
+    }
+    wave_lds_sync();
+    derive_node_wave(r, z, lane);
+}
+
 // Pass 3 (one wave, lane = pod base + lane of the window): the sequential placements of the window.
 // Rows of C (the nodes placed on so far in this window) live in LDS slots [0, nc), and ckey[c][t] holds
 // pod t's key on slot c as the row is now. Pod t's winner is the larger of its best key over C (a
@@ -613,7 +753,11 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
                 slot = (uint32_t)(__ffsll((long long)__ballot(lane < nc && kc == best)) - 1);
                 zone = czone[slot][t];
             }
-            if (lane == t) apply_assume(cfg, snode[slot].v, &szone[slot], mp, zone, 1);  // lane t holds pod t
+            if (zone >= 0x40) {  // multi-zone NUMA split: one lane (lane t holds pod t)
+                if (lane == t) apply_assume(cfg, snode[slot].v, &szone[slot], mp, zone, 1);
+            } else {
+                assume_wave(cfg, snode[slot], szone[slot], pods, j, zone, lane);
+            }
             wave_lds_sync();
             // later pods of the window on the changed row
             if (lane > t && live) {
