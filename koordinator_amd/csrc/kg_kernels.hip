@@ -501,7 +501,18 @@ __constant__ uint8_t DER_OP[N_DER] = {DER_FIT, DER_FIT, DER_FIT, DER_FIT, DER_FI
                                      DER_HEAD, DER_HEAD, DER_HEAD, DER_HEAD, DER_DIFF, DER_DIFF, DER_DIFF, DER_DIFF,
                                      DER_DIFF, DER_DIFF, DER_AMP_FIT, DER_AMP_DELTA};
 
-__device__ __forceinline__ void derive_node_wave(NodeRec& r, ZoneRec& z, uint32_t lane) {
+// The lane's derived-slot operation (DER_* tables), loaded once per kernel.
+struct DerLane {
+    uint32_t dst, a, b, op;
+};
+
+__device__ __forceinline__ DerLane der_lane(uint32_t lane) {
+    DerLane d{0, 0, 0, 0};
+    if (lane < (uint32_t)N_DER) d = {DER_DST[lane], DER_A[lane], DER_B[lane], DER_OP[lane]};
+    return d;
+}
+
+__device__ __forceinline__ void derive_node_wave(NodeRec& r, ZoneRec& z, uint32_t lane, const DerLane& dl_op) {
     int64_t* v = r.v;
     const uint64_t hi = (uint64_t)v[N_FLAGS] & 0xFFFFFFFF00000000ull;
     const uint32_t f0 = (uint32_t)v[N_FLAGS] & ~(uint32_t)F_DERIVED_MASK;
@@ -542,9 +553,9 @@ __device__ __forceinline__ void derive_node_wave(NodeRec& r, ZoneRec& z, uint32_
     uint32_t dst = 0;
     const bool dl = lane < (uint32_t)N_DER;
     if (dl) {
-        dst = DER_DST[lane];
-        uint32_t a = DER_A[lane], b = DER_B[lane];
-        const uint32_t op = DER_OP[lane];
+        dst = dl_op.dst;
+        uint32_t a = dl_op.a, b = dl_op.b;
+        const uint32_t op = dl_op.op;
         const uint32_t m_np = (f >> F_LA_FMODE_NP_SHIFT) & 3u, m_pr = (f >> F_LA_FMODE_PROD_SHIFT) & 3u;
         uint32_t mode = m_np;
         if (op == DER_HEAD && a >= (uint32_t)N_LA_FCUT_PROD0) {  // prod heads: the non-prod ones without prod thresholds
@@ -585,37 +596,45 @@ __device__ __forceinline__ void derive_node_wave(NodeRec& r, ZoneRec& z, uint32_
     wave_lds_sync();
 }
 
-__device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& z, const PodsDev& pods, uint32_t j,
-                                            int32_t zone, uint32_t lane) {
+// 64-bit lane broadcast
+__device__ __forceinline__ int64_t readlane64(int64_t x, uint32_t src) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), (int)src);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// pt: the placed pod's columns, broadcast from the lane that holds it (no memory access)
+__device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& z, const PodV& pt, int32_t zone,
+                                            uint32_t lane, const DerLane& dl) {
     int64_t* v = r.v;
     const uint32_t flags = (uint32_t)v[N_FLAGS];
     const bool la = (c.plugins & KG_PLUGIN_LA) && (flags & F_LA_HAS_METRIC);
-    const bool prod = (pods.flags[j] & KG_POD_PROD) != 0;
-    if (lane < (uint32_t)N_INT_SLOTS) {
-        int64_t add = 0;
-        switch (lane) {
-            case N_REQ_CPU: add = pods.req_cpu[j]; break;
-            case N_REQ_MEM: add = pods.req_mem[j]; break;
-            case N_REQ_EPH: add = pods.req_eph[j]; break;
-            case N_SC_REQ0: add = pods.sc_req0[j]; break;
-            case N_SC_REQ1: add = pods.sc_req1[j]; break;
-            case N_NZ_CPU: add = pods.nz_cpu[j]; break;
-            case N_NZ_MEM: add = pods.nz_mem[j]; break;
-            case N_NUM_PODS: add = 1; break;
-            case N_LA_FBASE_NP0: case N_LA_SBASE_NP0: add = la ? max(pods.la_est0[j], (int64_t)0) : 0; break;
-            case N_LA_FBASE_NP1: case N_LA_SBASE_NP1: add = la ? max(pods.la_est1[j], (int64_t)0) : 0; break;
-            case N_LA_FBASE_PROD0: case N_LA_SBASE_PROD0: add = la && prod ? max(pods.la_est0[j], (int64_t)0) : 0; break;
-            case N_LA_FBASE_PROD1: case N_LA_SBASE_PROD1: add = la && prod ? max(pods.la_est1[j], (int64_t)0) : 0; break;
-            default: break;
+    const bool prod = (pt.flags & KG_POD_PROD) != 0;
+    const int64_t e0 = pt.est0 > 0 ? pt.est0 : 0, e1 = pt.est1 > 0 ? pt.est1 : 0;
+    int64_t add = 0;
+    add = lane == (uint32_t)N_REQ_CPU ? pt.req_cpu : add;
+    add = lane == (uint32_t)N_REQ_MEM ? pt.req_mem : add;
+    add = lane == (uint32_t)N_REQ_EPH ? pt.req_eph : add;
+    add = lane == (uint32_t)N_SC_REQ0 ? pt.sc0 : add;
+    add = lane == (uint32_t)N_SC_REQ1 ? pt.sc1 : add;
+    add = lane == (uint32_t)N_NZ_CPU ? pt.nz_cpu : add;
+    add = lane == (uint32_t)N_NZ_MEM ? pt.nz_mem : add;
+    add = lane == (uint32_t)N_NUM_PODS ? 1 : add;
+    if (la) {
+        add = (lane == (uint32_t)N_LA_FBASE_NP0 || lane == (uint32_t)N_LA_SBASE_NP0) ? e0 : add;
+        add = (lane == (uint32_t)N_LA_FBASE_NP1 || lane == (uint32_t)N_LA_SBASE_NP1) ? e1 : add;
+        if (prod) {
+            add = (lane == (uint32_t)N_LA_FBASE_PROD0 || lane == (uint32_t)N_LA_SBASE_PROD0) ? e0 : add;
+            add = (lane == (uint32_t)N_LA_FBASE_PROD1 || lane == (uint32_t)N_LA_SBASE_PROD1) ? e1 : add;
         }
-        if (add) v[lane] += add;
     }
+    if (lane < (uint32_t)N_INT_SLOTS && add) v[lane] += add;
     if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES) {
-        if (lane == 32) z.cpu_used[zone] += pods.req_cpu[j];
-        if (lane == 33) z.mem_used[zone] += pods.req_mem[j];
+        if (lane == 32) z.cpu_used[zone] += pt.req_cpu;
+        if (lane == 33) z.mem_used[zone] += pt.req_mem;
     }
     wave_lds_sync();
-    derive_node_wave(r, z, lane);
+    derive_node_wave(r, z, lane, dl);
 }
 
 // Pass 3 (one wave, lane = pod base + lane of the window): the sequential placements of the window.
@@ -668,6 +687,7 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
     __syncthreads();
     const KCfg cv = cfg_in_vgprs(cfg);
     const PodF mpf = to_podf(mp, cfg);
+    const DerLane der = der_lane(lane);
     // key and zone of this lane's pod on slot s (row uniform across the wave)
     auto eval_slot = [&](uint32_t s, int32_t* zone) -> uint64_t {
         const uint32_t f = (uint32_t)snode[s].v[N_FLAGS];
@@ -756,7 +776,18 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
             if (zone >= 0x40) {  // multi-zone NUMA split: one lane (lane t holds pod t)
                 if (lane == t) apply_assume(cfg, snode[slot].v, &szone[slot], mp, zone, 1);
             } else {
-                assume_wave(cfg, snode[slot], szone[slot], pods, j, zone, lane);
+                PodV pt;
+                pt.req_cpu = readlane64(mp.req_cpu, t);
+                pt.req_mem = readlane64(mp.req_mem, t);
+                pt.req_eph = readlane64(mp.req_eph, t);
+                pt.sc0 = readlane64(mp.sc0, t);
+                pt.sc1 = readlane64(mp.sc1, t);
+                pt.nz_cpu = readlane64(mp.nz_cpu, t);
+                pt.nz_mem = readlane64(mp.nz_mem, t);
+                pt.est0 = readlane64(mp.est0, t);
+                pt.est1 = readlane64(mp.est1, t);
+                pt.flags = (uint32_t)__builtin_amdgcn_readlane((int)mp.flags, (int)t);
+                assume_wave(cfg, snode[slot], szone[slot], pt, zone, lane, der);
             }
             wave_lds_sync();
             // later pods of the window on the changed row
