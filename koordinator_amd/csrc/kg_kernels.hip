@@ -512,102 +512,34 @@ __device__ __forceinline__ DerLane der_lane(uint32_t lane) {
     return d;
 }
 
-__device__ __forceinline__ void derive_node_wave(NodeRec& r, ZoneRec& z, uint32_t lane, const DerLane& dl_op) {
-    int64_t* v = r.v;
-    const uint64_t hi = (uint64_t)v[N_FLAGS] & 0xFFFFFFFF00000000ull;
-    const uint32_t f0 = (uint32_t)v[N_FLAGS] & ~(uint32_t)F_DERIVED_MASK;
-    const bool full = v[N_NUM_PODS] + 1 > v[N_ALLOC_PODS];
-    const int64_t always_fail = kg_bits(-1.0), never_fail = kg_bits(4611686018427387904.0);
-    // F_BIG checks: int slot `lane`, the cpuset pair (lane 63), zone lane - 32
-    bool big = false;
-    if (lane <= (uint32_t)N_LA_SBASE_PROD1 && lane != (uint32_t)N_ALLOC_PODS && lane != (uint32_t)N_NUM_PODS &&
-        !(lane >= (uint32_t)N_LA_FCUT_NP0 && lane <= (uint32_t)N_LA_FCUT_PROD1)) {
-        const int64_t x = v[lane];
-        big = kg_big(x) || x < 0;
-    }
-    if (lane == 63) {
-        const int64_t cs = v[N_CPUSET], acs = v[N_AMP_CPUSET];
-        big = kg_big(cs) || kg_big(acs) || cs < 0 || acs < cs;
-    }
-    const bool zl = lane >= 32u && lane < 32u + (uint32_t)MAX_ZONES;
-    const uint32_t q = zl ? lane - 32u : 0u;
-    double zv[6] = {0, 0, 0, 0, 0, 0};
-    if (zl) {
-        const int64_t tc = z.cpu[q], tm = z.mem[q], uc = z.cpu_used[q], um = z.mem_used[q];
-        big = kg_big(tc) || kg_big(tm) || kg_big(uc) || kg_big(um) || uc < 0 || um < 0;
-        const int64_t ac = tc - uc < 0 ? 0 : tc - uc, am = tm - um < 0 ? 0 : tm - um;
-        const int64_t rc = tc - ac < 0 ? 0 : tc - ac, rm = tm - am < 0 ? 0 : tm - am;
-        zv[0] = ac != 0 ? x100(ac) : -1.0;
-        zv[1] = am != 0 ? x100(am) : -1.0;
-        zv[2] = x100(tc - rc);
-        zv[3] = x100(tm - rm);
-        zv[4] = x100(tc - uc);
-        zv[5] = x100(tm - um);
-    }
-    const uint32_t pol0 = (f0 >> F_NUMA_POLICY_SHIFT) & 15u;
-    const bool pol_host = pol0 == 1u /* KG_NUMA_BEST_EFFORT */ || pol0 == 2u /* KG_NUMA_RESTRICTED */;
-    const bool big_all = (__ballot(big) != 0ull) || pol_host || ((z.cpu_meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
-    const uint32_t f = f0 | (full ? (uint32_t)F_PODS_FULL : 0u) | (big_all ? (uint32_t)F_BIG : 0u);
-    // derived slot DER_DST[lane]
-    int64_t val = 0;
-    uint32_t dst = 0;
-    const bool dl = lane < (uint32_t)N_DER;
-    if (dl) {
-        dst = dl_op.dst;
-        uint32_t a = dl_op.a, b = dl_op.b;
-        const uint32_t op = dl_op.op;
-        const uint32_t m_np = (f >> F_LA_FMODE_NP_SHIFT) & 3u, m_pr = (f >> F_LA_FMODE_PROD_SHIFT) & 3u;
-        uint32_t mode = m_np;
-        if (op == DER_HEAD && a >= (uint32_t)N_LA_FCUT_PROD0) {  // prod heads: the non-prod ones without prod thresholds
-            if (f & F_LA_PROD_THR) mode = m_pr;
-            else a -= 2u, b -= 2u;
-        }
-        const int64_t va = v[a], vb = v[b];
-        const bool amp = (f & F_AMP) != 0;
-        if (op == DER_FIT) {
-            const int64_t d = va - vb;
-            val = (lane == 0 && full) ? always_fail : kg_bits(x100(d < 0 ? 0 : d));
-        } else if (op == DER_DIFF) {
-            val = kg_bits(x100(va - vb));
-        } else if (op == DER_HEAD) {
-            val = mode == FMODE_PASS ? never_fail
-                : mode == FMODE_FAIL_EXPIRED ? always_fail : kg_bits(((double)va - (double)vb) * 100.0);
-        } else if (op == DER_AMP_FIT) {
-            const int64_t cs = v[N_CPUSET], acs = v[N_AMP_CPUSET];
-            const int64_t req_f = (vb >= cs && cs > 0) ? vb - cs + acs : vb;
-            const int64_t d = va - req_f;
-            val = pol_host ? always_fail : amp ? kg_bits(x100(d < 0 ? 0 : d)) : never_fail;
-        } else {
-            val = kg_bits(amp ? x100(va - vb) : 0.0);
-        }
-    }
-    wave_lds_sync();  // every read above before any write below
-    if (dl) v[dst] = val;
-    if (zl) {
-        ZoneFast& zf = z.zf[q];
-        zf.avail_cpu = zv[0];
-        zf.avail_mem = zv[1];
-        zf.hint_cpu = zv[2];
-        zf.hint_mem = zv[3];
-        zf.free_cpu = zv[4];
-        zf.free_mem = zv[5];
-    }
-    if (lane == 63) v[N_FLAGS] = (int64_t)(hi | f);
-    wave_lds_sync();
-}
-
-// 64-bit lane broadcast
+// 64-bit lane broadcast / gather
 __device__ __forceinline__ int64_t readlane64(int64_t x, uint32_t src) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)src);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), (int)src);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// pt: the placed pod's columns, broadcast from the lane that holds it (no memory access)
+__device__ __forceinline__ int64_t shfl64(int64_t x, uint32_t src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, (int)src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)x >> 32), (int)src, 64);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Reserve of pod pt (its columns broadcast from the lane that holds it) on an LDS-staged row, then
+// derive_node: one round of LDS reads (lane k: int slot k; lanes 32..35: zone k - 32), the new int
+// values exchanged between lanes by shuffles, one round of writes.
 __device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& z, const PodV& pt, int32_t zone,
                                             uint32_t lane, const DerLane& dl) {
     int64_t* v = r.v;
-    const uint32_t flags = (uint32_t)v[N_FLAGS];
+    const uint64_t fl = (uint64_t)v[N_FLAGS];
+    const int64_t old = lane < (uint32_t)N_INT_SLOTS ? v[lane] : 0;
+    const bool zl = lane >= 32u && lane < 32u + (uint32_t)MAX_ZONES;
+    const uint32_t q = zl ? lane - 32u : 0u;
+    int64_t tc = 0, tm = 0, uc = 0, um = 0;
+    if (zl) tc = z.cpu[q], tm = z.mem[q], uc = z.cpu_used[q], um = z.mem_used[q];
+    const uint32_t meta = z.cpu_meta;
+    // apply_assume (sign +1): the int slot updates
+    const uint32_t flags = (uint32_t)fl;
     const bool la = (c.plugins & KG_PLUGIN_LA) && (flags & F_LA_HAS_METRIC);
     const bool prod = (pt.flags & KG_POD_PROD) != 0;
     const int64_t e0 = pt.est0 > 0 ? pt.est0 : 0, e1 = pt.est1 > 0 ? pt.est1 : 0;
@@ -628,13 +560,74 @@ __device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& 
             add = (lane == (uint32_t)N_LA_FBASE_PROD1 || lane == (uint32_t)N_LA_SBASE_PROD1) ? e1 : add;
         }
     }
-    if (lane < (uint32_t)N_INT_SLOTS && add) v[lane] += add;
-    if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES) {
-        if (lane == 32) z.cpu_used[zone] += pt.req_cpu;
-        if (lane == 33) z.mem_used[zone] += pt.req_mem;
+    const int64_t nv = old + add;
+    const bool zone_hit = zl && (c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES && (uint32_t)zone == q;
+    if (zone_hit) uc += pt.req_cpu, um += pt.req_mem;
+    // derive_node on the new values
+    const int64_t always_fail = kg_bits(-1.0), never_fail = kg_bits(4611686018427387904.0);
+    const uint32_t f0 = flags & ~(uint32_t)F_DERIVED_MASK;
+    const bool full = shfl64(nv, N_NUM_PODS) + 1 > shfl64(nv, N_ALLOC_PODS);
+    const int64_t cs = shfl64(nv, N_CPUSET), acs = shfl64(nv, N_AMP_CPUSET);
+    bool big = false;
+    if (lane <= (uint32_t)N_LA_SBASE_PROD1 && lane != (uint32_t)N_ALLOC_PODS && lane != (uint32_t)N_NUM_PODS &&
+        !(lane >= (uint32_t)N_LA_FCUT_NP0 && lane <= (uint32_t)N_LA_FCUT_PROD1))
+        big = kg_big(nv) || nv < 0;
+    if (lane == 63) big = kg_big(cs) || kg_big(acs) || cs < 0 || acs < cs;
+    double zv[6] = {0, 0, 0, 0, 0, 0};
+    if (zl) {
+        big = kg_big(tc) || kg_big(tm) || kg_big(uc) || kg_big(um) || uc < 0 || um < 0;
+        const int64_t ac = tc - uc < 0 ? 0 : tc - uc, am = tm - um < 0 ? 0 : tm - um;
+        const int64_t rc = tc - ac < 0 ? 0 : tc - ac, rm = tm - am < 0 ? 0 : tm - am;
+        zv[0] = ac != 0 ? x100(ac) : -1.0;
+        zv[1] = am != 0 ? x100(am) : -1.0;
+        zv[2] = x100(tc - rc);
+        zv[3] = x100(tm - rm);
+        zv[4] = x100(tc - uc);
+        zv[5] = x100(tm - um);
     }
+    const uint32_t pol0 = (f0 >> F_NUMA_POLICY_SHIFT) & 15u;
+    const bool pol_host = pol0 == 1u /* KG_NUMA_BEST_EFFORT */ || pol0 == 2u /* KG_NUMA_RESTRICTED */;
+    const bool big_all = (__ballot(big) != 0ull) || pol_host || ((meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
+    const uint32_t f = f0 | (full ? (uint32_t)F_PODS_FULL : 0u) | (big_all ? (uint32_t)F_BIG : 0u);
+    // derived slot dl.dst of this lane (lanes < N_DER)
+    uint32_t a = dl.a, b = dl.b, mode = (f >> F_LA_FMODE_NP_SHIFT) & 3u;
+    if (dl.op == DER_HEAD && a >= (uint32_t)N_LA_FCUT_PROD0) {  // prod heads: the non-prod ones without prod thresholds
+        if (f & F_LA_PROD_THR) mode = (f >> F_LA_FMODE_PROD_SHIFT) & 3u;
+        else a -= 2u, b -= 2u;
+    }
+    const int64_t va = shfl64(nv, a), vb = shfl64(nv, b);
+    const bool amp = (f & F_AMP) != 0;
+    int64_t val;
+    if (dl.op == DER_FIT) {
+        const int64_t d = va - vb;
+        val = (lane == 0 && full) ? always_fail : kg_bits(x100(d < 0 ? 0 : d));
+    } else if (dl.op == DER_DIFF) {
+        val = kg_bits(x100(va - vb));
+    } else if (dl.op == DER_HEAD) {
+        val = mode == FMODE_PASS ? never_fail
+            : mode == FMODE_FAIL_EXPIRED ? always_fail : kg_bits(((double)va - (double)vb) * 100.0);
+    } else if (dl.op == DER_AMP_FIT) {
+        const int64_t req_f = (vb >= cs && cs > 0) ? vb - cs + acs : vb;
+        const int64_t d = va - req_f;
+        val = pol_host ? always_fail : amp ? kg_bits(x100(d < 0 ? 0 : d)) : never_fail;
+    } else {
+        val = kg_bits(amp ? x100(va - vb) : 0.0);
+    }
+    // writes
+    if (lane < (uint32_t)N_INT_SLOTS && add) v[lane] = nv;
+    if (lane < (uint32_t)N_DER) v[dl.dst] = val;
+    if (zl) {
+        if (zone_hit) z.cpu_used[q] = uc, z.mem_used[q] = um;
+        ZoneFast& zf = z.zf[q];
+        zf.avail_cpu = zv[0];
+        zf.avail_mem = zv[1];
+        zf.hint_cpu = zv[2];
+        zf.hint_mem = zv[3];
+        zf.free_cpu = zv[4];
+        zf.free_mem = zv[5];
+    }
+    if (lane == 63) v[N_FLAGS] = (int64_t)((fl & 0xFFFFFFFF00000000ull) | f);
     wave_lds_sync();
-    derive_node_wave(r, z, lane, dl);
 }
 
 // Pass 3 (one wave, lane = pod base + lane of the window): the sequential placements of the window.
