@@ -1223,10 +1223,21 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             return 1;
         return 2;
     };
+    // stable bucket order by kind (three kinds): the batch, and the plain sub-batch's row map
+    std::vector<uint8_t> wk(std::max<uint32_t>(n, 1));
+    for (uint32_t j = 0; j < n; j++) wk[j] = (uint8_t)wave_kind(j);
+    auto by_wave_kind = [&](const std::vector<uint32_t>& in) {
+        std::vector<uint32_t> out;
+        out.reserve(in.size());
+        for (uint8_t k = 0; k < 3; k++)
+            for (uint32_t j : in)
+                if (wk[j] == k) out.push_back(j);
+        return out;
+    };
     std::vector<uint32_t> order(n);
     for (uint32_t j = 0; j < n; j++) order[j] = j;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return wave_kind(a) < wave_kind(b); });
-    std::stable_sort(pmap.begin(), pmap.end(), [&](uint32_t a, uint32_t b) { return wave_kind(a) < wave_kind(b); });
+    order = by_wave_kind(order);
+    pmap = by_wave_kind(pmap);
     uint32_t n_stat_cls = 0;
     while (n_stat_cls < stat.size() && xc[stat[n_stat_cls]] == 0) n_stat_cls++;
     const uint32_t np = (uint32_t)pmap.size();
@@ -1237,10 +1248,22 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         fp[t] = f[pmap[t]];
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    HIP_TRY(ctx, hipMemcpyAsync(p->d_dev_req, dreq.data(), sizeof(int64_t) * DEV_R * n, hipMemcpyHostToDevice, ctx->stream));
-    for (int c = 0; c < 5; c++)
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_xcols + (size_t)c * p->cap, xc.data() + (size_t)c * n, sizeof(uint32_t) * n,
-                                    hipMemcpyHostToDevice, ctx->stream));
+    // absent config-5 columns: their defaults (no GPU request, no quota, no reservation class) set on the
+    // device instead of copied from pageable host memory
+    if (cols->dev_req)
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_dev_req, dreq.data(), sizeof(int64_t) * DEV_R * n, hipMemcpyHostToDevice, ctx->stream));
+    else if (n)
+        HIP_TRY(ctx, hipMemsetAsync(p->d_dev_req, 0, sizeof(int64_t) * DEV_R * n, ctx->stream));
+    const void* xsrc[5] = {cols->dev_count, cols->dev_keys, cols->quota, cols->quota_keys, cols->rsv_class};
+    const int xdef[5] = {0, 0, 0xFF, 0, 0xFF};  // -1 quota / class
+    for (int c = 0; c < 5; c++) {
+        if (!n) break;
+        if (xsrc[c])
+            HIP_TRY(ctx, hipMemcpyAsync(p->d_xcols + (size_t)c * p->cap, xc.data() + (size_t)c * n, sizeof(uint32_t) * n,
+                                        hipMemcpyHostToDevice, ctx->stream));
+        else
+            HIP_TRY(ctx, hipMemsetAsync(p->d_xcols + (size_t)c * p->cap, xdef[c], sizeof(uint32_t) * n, ctx->stream));
+    }
     if (!stat.empty())
         HIP_TRY(ctx, hipMemcpyAsync(p->d_stat_list, stat.data(), sizeof(uint32_t) * stat.size(), hipMemcpyHostToDevice, ctx->stream));
     p->n_stat = (uint32_t)stat.size();
@@ -1261,7 +1284,10 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         HIP_TRY(ctx, hipMemcpyAsync(p->d_cols + (size_t)c * p->cap, h.data() + (size_t)c * n, sizeof(int64_t) * n,
                                     hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(p->d_flags, f.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(p->d_dcls, dcls.data(), n, hipMemcpyHostToDevice, ctx->stream));
+    if (!classes.empty())
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_dcls, dcls.data(), n, hipMemcpyHostToDevice, ctx->stream));
+    else if (n)
+        HIP_TRY(ctx, hipMemsetAsync(p->d_dcls, DEV_CLASSES, n, ctx->stream));
     if (!classes.empty())
         HIP_TRY(ctx, hipMemcpyAsync(p->d_dclass, classes.data(), sizeof(DevClass) * classes.size(), hipMemcpyHostToDevice,
                                     ctx->stream));
