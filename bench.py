@@ -127,7 +127,8 @@ def roofline(pmc, kernel_s, evals_per_launch, b_eval, kernel_name):
                          "note": "SURVEY §8d scan model (node row read once per eval); pod tiling reads a row "
                                  "once per 64 pods, so this is not an HBM utilisation and may exceed 8 TB/s"}
     if not pmc or not kernel_s:
-        out["note"] = "no PMC summary for these kernel sources: issue / HBM fractions not available"
+        out["note"] = ("no PMC summary for these kernel sources and this configuration (N = 1, configs 2 and 5): "
+                       "issue / HBM fractions not available")
         return out
     valu = pmc.get("valu_insts_per_launch")
     salu = pmc.get("salu_insts_per_launch")
@@ -377,7 +378,8 @@ def main():
     evals = float(n_pods) * n_total * a.steps
     value = evals / elapsed
     avg_kernel_s = (kern_ms / 1e3) / max(launches, 1) if launches else None
-    pmc = load_pmc("select_pmc.json" if config != 5 else "ext_pmc.json") if world == 1 else None
+    # the committed PMC passes are per launch of one configuration (profiles/run_profile.sh: 2 and 5)
+    pmc = load_pmc({2: "select_pmc.json", 5: "ext_pmc.json"}[config]) if world == 1 and config in (2, 5) else None
     fused = k == 1 and os.environ.get("KG_SELECT_UNFUSED", "0") in ("", "0")
     base = "k_big_init + k_select1 (fused top-1)" if fused else "k_select"
     kname = base if config != 5 else f"k_ext_select + {base} (plain-pod split, one bracket)"
