@@ -461,7 +461,7 @@ def empty_node_state(n: int) -> Table:
 
 def pod_columns(t: Table) -> KgPodColumns:
     _check(t, POD_I64, np.int64)
-    _check(t, POD_U32, np.uint32)
+    _check(t, ["flags", "numa_policy"], np.uint32)
     s = KgPodColumns()
     for k in ["req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem"]:
         setattr(s, k, _ptr(t[k], C.c_int64))
@@ -471,16 +471,16 @@ def pod_columns(t: Table) -> KgPodColumns:
         s.la_est[r] = _ptr(t[f"la_est{r}"], C.c_int64)
     s.flags = _ptr(t["flags"], C.c_uint32)
     s.numa_policy = _ptr(t["numa_policy"], C.c_uint32)
+    # config-5 columns are optional, each on its own (absent: no GPU request / quota / reservation class)
+    _check(t, [k for k in POD_U32 if k in t], np.uint32)
+    _check(t, [k for k in POD_I32 if k in t], np.int32)
     if "dev_req" in t:
-        _check(t, [k for k in POD_U32 if k in t], np.uint32)
-        _check(t, [k for k in POD_I32 if k in t], np.int32)
         t["dev_req"] = np.ascontiguousarray(t["dev_req"], np.int64)
         s.dev_req = _ptr(t["dev_req"], C.c_int64)
-        s.dev_count = _ptr(t["dev_count"], C.c_uint32)
-        s.dev_keys = _ptr(t["dev_keys"], C.c_uint32)
-        s.quota = _ptr(t["quota"], C.c_int32)
-        s.quota_keys = _ptr(t["quota_keys"], C.c_uint32)
-        s.rsv_class = _ptr(t["rsv_class"], C.c_int32)
+    for k, ct in (("dev_count", C.c_uint32), ("dev_keys", C.c_uint32), ("quota", C.c_int32),
+                  ("quota_keys", C.c_uint32), ("rsv_class", C.c_int32)):
+        if k in t:
+            setattr(s, k, _ptr(t[k], ct))
     s._keep = t
     return s
 

@@ -298,3 +298,20 @@ def test_views_stale_after_assume_on_view_node(ctx):
         engine.eval_select(snap, batch, 1)
     snap.upload_reservations(rsv)
     engine.eval_select(snap, batch, 1)
+
+
+def test_pod_batch_without_config5_columns(ctx):
+    """A pod batch uploaded without the config-5 columns (no GPU request, quota or reservation class) onto
+    a batch object that held config-5 pods: kg_pods_upload sets their defaults on the device (memsets),
+    so nothing of the previous upload survives."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(1500, 300, seed_config=23, rsv_frac=0.2)
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    engine.eval_select(snap, batch, 1)
+    plain = {k: v for k, v in pods.items() if k not in ("dev_req", "dev_count", "dev_keys", "quota", "quota_keys",
+                                                        "rsv_class")}
+    batch.upload(plain)
+    for k in (1, 3):
+        got = engine.eval_select(snap, batch, k)
+        assert np.array_equal(got, oracle_lib.ext_select(kc, nodes, plain, k, 0, quotas, rsv)), k
+    assert not (engine.result_status(batch) & abi.KG_ST_QUOTA).any()
