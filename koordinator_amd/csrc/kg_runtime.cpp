@@ -1811,6 +1811,20 @@ kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
 
 constexpr uint32_t RB_R = 8;  // replay windows per captured graph
 
+// Records per k_rb_top wave of storage class c (one wave per chunk: the pass is latency-bound, so the
+// costlier SingleNUMANode records take shorter chunks and more waves). KG_RB_CHUNK0 / KG_RB_CHUNK1:
+// tuning aids, 1..RB_CHUNK.
+uint32_t rb_chunk(int c) {
+    static uint32_t v[2] = {0, 0};
+    if (v[c] == 0) {
+        const char* e = std::getenv(c == 0 ? "KG_RB_CHUNK0" : "KG_RB_CHUNK1");
+        const long x = e ? std::strtol(e, nullptr, 10) : 0;
+        // defaults from a sweep on config 3 (MI355X, 32/32 .. 8/4): 12 / 6 records, 165k -> 191k pods/s
+        v[c] = (x >= 1 && x <= (long)RB_CHUNK) ? (uint32_t)x : (c == 0 ? 12u : 6u);
+    }
+    return v[c];
+}
+
 // Window replay: RB_R windows of (k_rb_top per storage class, k_rb_merge, k_rb_fix) per graph; each
 // window reads the next pod to place from p->d_step and advances it by 1..RB_W pods.
 kg_status rb_graph(kg_snap* s, kg_pods* p, bool exact) {
@@ -1825,9 +1839,9 @@ kg_status rb_graph(kg_snap* s, kg_pods* p, bool exact) {
     a.n_nodes = s->n;
     a.index_base = s->base;
     const uint32_t bounds[3] = {0, s->n0, s->n};
-    const uint32_t chunk = RB_CHUNK;
     uint32_t n_parts = 0;
     for (int c = 0; c < 2; c++) {
+        const uint32_t chunk = rb_chunk(c);
         SelectRange& r = a.range[c];
         r.begin = bounds[c];
         r.end = bounds[c + 1];
