@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 5
+#define KG_ABI_VERSION 6
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -310,6 +310,7 @@ typedef struct kg_node_state {
     int64_t* dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
     int64_t* cpuset_alloc_milli;
     kg_cpu_alloc* cpu_alloc; /* [node] (nodes without a CPU topology: zeros) */
+    uint32_t* numa_zone_status; /* NUMANodeSharedStatus, 2 bits per zone (a cpuset Reserve changes it) */
 } kg_node_state;
 
 /* Pending pods, struct-of-arrays host columns (caller-owned, copied). */

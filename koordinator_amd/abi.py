@@ -11,7 +11,7 @@ from typing import Dict
 
 import numpy as np
 
-KG_ABI_VERSION = 5
+KG_ABI_VERSION = 6
 KG_LA_R = 2
 KG_NSCALAR = 2
 KG_MAX_ZONES = 4
@@ -170,6 +170,7 @@ class KgNodeState(C.Structure):
         ("zone_cpu_used", _p64 * KG_MAX_ZONES), ("zone_mem_used", _p64 * KG_MAX_ZONES),
         ("dev_free", _p64),
         ("cpuset_alloc_milli", _p64), ("cpu_alloc", C.c_void_p),
+        ("numa_zone_status", C.POINTER(C.c_uint32)),
     ]
 
 
@@ -447,6 +448,8 @@ def node_state_struct(t: Table) -> KgNodeState:
         s.cpuset_alloc_milli = _ptr(t["cpuset_alloc_milli"], C.c_int64)
     if "cpu_alloc" in t:
         s.cpu_alloc = t["cpu_alloc"].ctypes.data
+    if "numa_zone_status" in t:
+        s.numa_zone_status = _ptr(t["numa_zone_status"], C.c_uint32)
     s._keep = t
     return s
 
@@ -456,6 +459,7 @@ def empty_node_state(n: int) -> Table:
     t["dev_free"] = np.zeros((n, KG_DEV_R, KG_DEV_MINORS), np.int64)
     t["cpuset_alloc_milli"] = np.zeros(n, np.int64)
     t["cpu_alloc"] = np.zeros((n, 2 * KG_MAX_CPUS), np.uint8)
+    t["numa_zone_status"] = np.zeros(n, np.uint32)
     return t
 
 

@@ -182,6 +182,7 @@ class BatchScheduler:
         pod_status: Dict[str, Status] = {}
         assumed: Dict[str, Tuple[str, int, int]] = {}
         n_assumed, failed = 0, []
+        node_msg: Dict[str, str] = {}  # the failing pod's message, set on it and every later pod of its node
         for t, (node_name, p) in enumerate(batch):
             r = int(res[t])
             if r in (abi.KG_BATCH_ASSUMED, abi.KG_BATCH_ROLLED_BACK):
@@ -191,12 +192,18 @@ class BatchScheduler:
                     assumed[p.key] = (node_name, int(zone[t]), int(minors[t]))
             elif r in (abi.KG_BATCH_FAILED, abi.KG_BATCH_SIBLING):
                 bits = int(stat[t])
-                if bits & abi.KG_ST_QUOTA:  # the ElasticQuota gate runs in PreFilter
+                if r == abi.KG_BATCH_SIBLING and node_name in node_msg:
+                    # engine.go:188-219: errMsg is formatted once, from the pod that failed, and set on
+                    # every pod k >= j of the node group
+                    msg = node_msg[node_name]
+                elif bits & abi.KG_ST_QUOTA:  # the ElasticQuota gate runs in PreFilter
                     msg = ERR_PRE_FILTER_FAILED.format(ns=p.namespace, name=p.name, uid=p.uid,
                                                       msg=reasons.plugin_reasons(bits)["ElasticQuota"][0])
                 else:
                     msg = ERR_FILTER_POD_FAILED.format(ns=p.namespace, name=p.name, uid=p.uid, node=node_name,
                                                       msg=filter_message(bits))
+                if r == abi.KG_BATCH_FAILED:
+                    node_msg[node_name] = msg
                 pod_status[p.key] = Status(UNSCHEDULABLE, msg)
                 failed.append((p.key, node_name))
         if not failed:

@@ -140,11 +140,14 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
     __syncthreads();
     if (code != 0 || threadIdx.x != 0) return;
     kg_cpu_alloc& A = allocs[rec];
+    uint32_t used = 0;  // NUMA nodes of the CPUs taken (addPodAllocation's usedNUMA)
     for (int c = 0; c < st.n_cpus; c++)
         if ((res[c >> 6] >> (c & 63)) & 1ull) {
             A.ref[c] = (uint8_t)(A.ref[c] + 1);
             A.excl[c] = (uint8_t)q.excl;
+            used |= 1u << st.numa[c];
         }
+    z.status = cpuset_zone_status(z.status, used);
     cpu_counts(st, &A, max_ref, z);
     n[N_CPUSET] = 1000 * (int64_t)z.cpu_allocated;
     n[N_AMP_CPUSET] = z.amp_ratio > 1.0 ? (int64_t)ceil(__dmul_rn((double)n[N_CPUSET], z.amp_ratio)) : n[N_CPUSET];

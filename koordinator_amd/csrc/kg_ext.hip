@@ -465,14 +465,15 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
 
 // Rows of a sub-batch select (plain pods / config-5 pods) back to their batch positions; a pod the
 // ElasticQuota PreFilter rejected has no feasible node.
-__global__ __launch_bounds__(256) void k_scatter_keys(const uint64_t* __restrict__ src, const uint32_t* __restrict__ map,
-                                                      uint32_t n, uint32_t k, const uint32_t* __restrict__ qst,
-                                                      uint64_t* __restrict__ out, uint32_t* __restrict__ pstat) {
+__global__ __launch_bounds__(256) void k_scatter_keys(const uint64_t* src, const uint32_t* __restrict__ map,
+                                                      uint32_t n, uint32_t k, bool src_by_map, const uint32_t* __restrict__ qst,
+                                                      uint64_t* out, uint32_t* __restrict__ pstat) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const uint32_t j = map[t];
     const bool rejected = qst && qst[j] != 0;
-    for (uint32_t i = 0; i < k; i++) out[(size_t)j * k + i] = rejected ? 0ull : src[(size_t)t * k + i];
+    const size_t r = src_by_map ? j : t;
+    for (uint32_t i = 0; i < k; i++) out[(size_t)j * k + i] = rejected ? 0ull : src[r * k + i];
     if (rejected && pstat) pstat[j] = qst[j];
 }
 
@@ -775,10 +776,10 @@ hipError_t launch_dev_sum(const NodeRec* nodes, const DevRec* devs, uint32_t n_n
     return hipGetLastError();
 }
 
-hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, const uint32_t* qst,
-                               uint64_t* out, uint32_t* pstat, hipStream_t s) {
+hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, bool src_by_map,
+                               const uint32_t* qst, uint64_t* out, uint32_t* pstat, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_scatter_keys<<<(n + 255) / 256, 256, 0, s>>>(src, map, n, k, qst, out, pstat);
+    k_scatter_keys<<<(n + 255) / 256, 256, 0, s>>>(src, map, n, k, src_by_map, qst, out, pstat);
     return hipGetLastError();
 }
 

@@ -15,25 +15,36 @@ struct SelectRange {
     uint32_t begin, end, chunk, n_chunks, part0;
 };
 
+// Matrix-mode select of one pod batch against one snapshot (launch_select). The batch is split per pod:
+// lanes [0, n_fast) of `order` take the float64 fast path (k_select1 / k_select<FAST>) on the records of
+// each storage class plus the integer path on the F_BIG records (k_big_sel, chunked over the device's
+// F_BIG list); lanes [n_fast, n_pods) — pods outside the fast domain (a NUMA policy of their own, cpuset
+// binding, values >= 2^44) — take the integer path on every record (k_select<!FAST>). Final keys go to
+// out[row][K] (row = the lane's pod; K = 1 or KG_TOPK_MAX); K > 1 (and the unfused top-1 fast path)
+// goes through per-chunk partial rows [part][ld][K] and list merges.
 struct LaunchSelect {
     const NodeRec* nodes;
     const ZoneRec* zones;
     PodsDev pods;
-    uint32_t n_pods, index_base, k;
-    SelectRange range[2];
+    uint32_t n_pods;       // lanes: fast lanes then integer lanes
+    uint32_t n_rows;       // row space of out / partial (the pod batch): row stride of the partials
+    uint32_t index_base, k;
+    SelectRange range[2];  // fast sub-batch: records of storage class 0 / 1
+    SelectRange irange;    // integer sub-batch: every record
     bool exact, fast;
     KCfg cfg;
-    uint64_t* partial;
-    const uint32_t* pmap;  // sub-batch row -> batch position (nullptr: identity)
+    uint64_t* partial;     // [parts][n_rows][K]
+    const uint32_t* pmap;  // sub-batch row -> batch position for pstat (nullptr: identity)
     uint32_t* pstat;       // per batch position: KG_ST_UNSUPPORTED when some pair needs the host path
-    // fused top-1 (k == 1 on the fast path): one launch over both storage classes, per-pod keys by
-    // atomicMax straight into `out`, which k_big_init has seeded with the F_BIG records' best keys
-    bool fused;
+    bool fused;            // K == 1 fast path: atomicMax straight into out, no partials
     uint64_t* out;
     const uint32_t* big_list;
     const uint32_t* big_count;
-    const uint32_t* order;  // fused select: the batch grouped by wave kind (nullptr: batch order)
+    uint32_t big_y, big_part0;  // F_BIG chunks (blockIdx.y) and their first partial row (unfused)
+    const uint32_t* order;  // lane -> row: fast lanes (grouped by wave kind) then integer lanes; nullptr: identity
+    uint32_t n_fast;        // fast lanes (0 unless `fast`)
 };
+inline uint32_t select_fparts(const LaunchSelect& a) { return a.big_part0 + a.big_y; }
 
 // Block replay (k_rb_top / k_rb_merge / k_rb_fix): window of RB_W pods, RB_K keys kept per pod,
 // changed-row bitmap in LDS (snapshots up to 32 x RB_BITMAP_WORDS records).
@@ -94,10 +105,11 @@ hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const E
                              uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
                              const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat, const uint32_t* special,
                              uint32_t special_est, hipStream_t s);
-// out[map[t]] = rows t of src (k keys each); rows whose pod has a nonzero qst[pod] get zero keys and
-// pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the host path)
-hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, const uint32_t* qst,
-                               uint64_t* out, uint32_t* pstat, hipStream_t s);
+// out[map[t]] = rows t of src (k keys each; row map[t] with src_by_map, src may then be out); rows whose pod
+// has a nonzero qst[pod] get zero keys and pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the
+// host path)
+hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, bool src_by_map,
+                               const uint32_t* qst, uint64_t* out, uint32_t* pstat, hipStream_t s);
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
@@ -120,10 +132,9 @@ hipError_t launch_batch(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtD
                         uint32_t* minors, hipStream_t s);
 hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k, uint64_t* out,
                         hipStream_t s);
-hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k,
-                            const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, const uint32_t* big_list,
-                            const uint32_t* big_count, uint32_t index_base, const KCfg& cfg, uint64_t* out,
-                            const uint32_t* pmap, uint32_t* pstat, hipStream_t s);
+// merge of partial rows [part0, part0 + n_parts) (row stride ld pods) for the rows list[0..n) (nullptr: 0..n)
+hipError_t launch_merge_list(const uint64_t* partial, uint32_t part0, uint32_t n_parts, uint32_t ld, const uint32_t* list,
+                             uint32_t n, uint32_t k, uint64_t* out, hipStream_t s);
 hipError_t launch_big_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t* big_list, uint32_t* big_count,
                            hipStream_t s);
 // Grid of the PART 2 ext kernels (special records, grid-stride): chunk and chunk count for an estimate

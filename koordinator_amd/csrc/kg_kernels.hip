@@ -4,8 +4,10 @@
 //              (each record's 256-byte fast block arrives by wide scalar loads into SGPRs), running
 //              top-K per lane; per-(chunk, pod) partial keys. Specialised per node storage class
 //              (records are stored grouped by class) and per enabled-plugin set.
+//   k_big_sel  the nodes outside the float64 fast path (F_BIG records) for the fast lanes, on the
+//              integer path, chunked over the device's F_BIG list.
 //   k_merge    per pod: top-K over partial keys (global selectHost of one shard or of the
-//              all-gathered shards); k_merge_big adds the nodes outside the float64 fast path.
+//              all-gathered shards).
 //   k_verify   lane = (pod, node record): every plugin's status / score (FilterPlugin / ScorePlugin
 //              results) for parity dumps.
 //   k_replay   one pod per launch, lane = node record: applies the previous pod's Assume to the
@@ -40,7 +42,7 @@ __device__ __forceinline__ uint32_t rec_gidx(const NodeRec& r, uint32_t index_ba
 
 // Records [begin, end) are walked in chunks of `chunk`; blockIdx.y = chunk, partial row = part0 + chunk.
 // FAST: pods and weights fit the float64 fast path (host check); records flagged F_BIG are skipped
-// and evaluated on the integer path by k_merge_big.
+// and evaluated on the integer path by k_big_sel.
 template <int K, uint32_t PM, int CLS, int KIND>
 __device__ __forceinline__ void select_fast_loop(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                  uint32_t lo, uint32_t hi, uint32_t index_base, const KCfg& cv,
@@ -50,25 +52,28 @@ __device__ __forceinline__ void select_fast_loop(const NodeRec* __restrict__ nod
         uint32_t total;
         const bool ok = fast_eval<PM, CLS, KIND>(cv, r, zones + i, pf, total);
         const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - (index_base + (uint32_t)((uint64_t)r.flags >> 32)));
-        // F_BIG records (integer path in k_merge_big) are masked, not branched around: one wait
+        // F_BIG records (integer path in k_big_sel) are masked, not branched around: one wait
         // for the whole record
         topk_insert<K>(top, (ok & !((uint32_t)r.flags & F_BIG)) ? key : 0ull);
     }
 }
 
-// Records [begin, end) are walked in chunks of `chunk`; blockIdx.y = chunk, partial row = part0 + chunk.
-// FAST: pods and weights fit the float64 fast path (host check); records flagged F_BIG are skipped
-// and evaluated on the integer path by k_merge_big. `order` (nullable): lane -> pod, the batch grouped
-// by wave kind (kg_pods_upload); partial rows stay indexed by pod.
+// Records [begin, end) are walked in chunks of `chunk`; blockIdx.y = chunk. Lane j serves pod
+// row = order[j] (order nullable: row j). FAST: the pod is in the float64 fast domain (host check) and
+// records flagged F_BIG are masked out (k_big_sel evaluates them on the integer path); otherwise every
+// record is evaluated on the integer path. K == 1 with `out`: atomicMax of the lane's best key into
+// out[row] (zeroed by the launcher); else the lane's top-K goes to partial row part0 + chunk (row
+// stride ld pods).
 template <int K, bool EXACT, bool FAST, uint32_t PM, int CLS>
 __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
-                                                PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
+                                                PodsDev pods, uint32_t n_lanes, uint32_t ld, uint32_t begin, uint32_t end,
                                                 uint32_t chunk, uint32_t part0, uint32_t index_base, KCfg cfg,
-                                                uint64_t* __restrict__ partial, const uint32_t* __restrict__ pmap,
-                                                uint32_t* __restrict__ pstat, const uint32_t* __restrict__ order) {
+                                                uint64_t* __restrict__ partial, uint64_t* __restrict__ out,
+                                                const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat,
+                                                const uint32_t* __restrict__ order) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t c = blockIdx.y;
-    const bool live = j < n_pods;
+    const bool live = j < n_lanes;
     const uint32_t row = live ? (order ? order[j] : j) : 0u;
     const PodV p = load_pod(pods, row);
     uint64_t top[K];
@@ -78,8 +83,6 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
     const uint32_t hi = min(end, lo + chunk);
     uint32_t unsup = 0;
     if constexpr (FAST) {
-        // no host-path pairs on the fast path: Restricted / BestEffort records and nodes with a CPU bind
-        // policy are F_BIG (flagged by k_merge_big), a batch with a cpuset-binding pod is not fast_ok
         const PodF pf = to_podf(p, cfg);
         const KCfg cv = cfg_in_vgprs(cfg);
         if (__all(!live || fast_kind_match(FK_PROD, p)))
@@ -96,17 +99,21 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
         }
     }
     if (live) {
-        uint64_t* dst = partial + ((size_t)(part0 + c) * n_pods + row) * K;
+        if (K == 1 && out) {
+            if (top[0]) atomicMax((unsigned long long*)(out + row), (unsigned long long)top[0]);
+        } else {
+            uint64_t* dst = partial + ((size_t)(part0 + c) * ld + row) * K;
 #pragma unroll
-        for (int t = 0; t < K; t++) dst[t] = top[t];
+            for (int t = 0; t < K; t++) dst[t] = top[t];
+        }
         if (unsup) atomicOr(pstat + (pmap ? pmap[row] : row), unsup);
     }
 }
 
 // Fused top-1 select of one storage class: lane = pod, blockIdx.y = chunk of records [begin, end); the
-// lane's best key goes to out[pod] by atomicMax. out was seeded by k_big_init with the pod's best key
-// over the F_BIG records (integer path), or 0; no per-chunk partials, no merge pass. `order` (nullable)
-// lists the batch grouped by wave kind (kg_pods_upload), so most waves run a kind-specialised loop.
+// lane's best key goes to out[pod] by atomicMax (out zeroed by the launcher; the F_BIG records come from
+// k_big_sel); no per-chunk partials, no merge pass. `order` (nullable) lists the fast lanes grouped by
+// wave kind (kg_pods_upload), so most waves run a kind-specialised loop.
 template <uint32_t PM, int CLS, int KIND>
 __device__ __forceinline__ uint64_t select1_loop(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                  uint32_t lo, uint32_t hi, uint32_t index_base, const KCfg& cv,
@@ -117,7 +124,7 @@ __device__ __forceinline__ uint64_t select1_loop(const NodeRec* __restrict__ nod
         uint32_t total;
         const bool ok = fast_eval<PM, CLS, KIND>(cv, r, zones + i, pf, total);
         const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - (index_base + (uint32_t)((uint64_t)r.flags >> 32)));
-        // F_BIG records: k_big_init; feasibility and the record test fold into the update's lane mask
+        // F_BIG records: k_big_sel; feasibility and the record test fold into the update's lane mask
         const bool better = ok & !((uint32_t)r.flags & F_BIG) & (key > top);
         top = better ? key : top;
     }
@@ -148,83 +155,67 @@ __global__ __launch_bounds__(256) void k_select1(const NodeRec* __restrict__ nod
     if (live && top) atomicMax((unsigned long long*)(out + o), (unsigned long long)top);
 }
 
-// Seeds the fused select's output: per pod, the best key over the F_BIG records (integer path), 0 if none.
-__global__ __launch_bounds__(256) void k_big_init(uint32_t n_pods, const NodeRec* __restrict__ nodes,
-                                                  const ZoneRec* __restrict__ zones, PodsDev pods,
-                                                  const uint32_t* __restrict__ big_list,
-                                                  const uint32_t* __restrict__ big_count, uint32_t index_base,
-                                                  KCfg cfg, uint64_t* __restrict__ out,
-                                                  const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n_pods) return;
-    uint64_t top = 0;
-    const uint32_t nb = *big_count;
-    if (nb) {
-        const PodV p = load_pod(pods, j);
-        uint32_t unsup = 0;
-        for (uint32_t b = 0; b < nb; b++) {
-            const uint32_t i = big_list[b];
-            const PairOut o = eval_pair<false>(cfg, nodes[i].v, zones + i, p);
-            unsup |= o.status & KG_ST_UNSUPPORTED;
-            const uint64_t key = pair_key(cfg, o, rec_gidx(nodes[i], index_base));
-            top = key > top ? key : top;
-        }
-        if (unsup) atomicOr(pstat + (pmap ? pmap[j] : j), unsup);
-    }
-    out[j] = top;
-}
-
+// The F_BIG records (integer path) for the fast lanes: lane = pod (via order), blockIdx.y = chunk of the
+// device's F_BIG list (k_big_scan), whose length is only known on the device: gridDim.y chunks of
+// ceil(count / gridDim.y) records each. K == 1 with `out`: atomicMax into out[row]; else the lane's top-K
+// into partial row part0 + blockIdx.y (empty chunks write zeros).
 template <int K>
-__global__ __launch_bounds__(256) void k_merge(const uint64_t* __restrict__ partial, uint32_t n_parts, uint32_t n_pods,
-                                               uint64_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_big_sel(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                 PodsDev pods, uint32_t n_lanes, uint32_t ld,
+                                                 const uint32_t* __restrict__ big_list,
+                                                 const uint32_t* __restrict__ big_count, uint32_t index_base, KCfg cfg,
+                                                 uint64_t* __restrict__ partial, uint32_t part0, uint64_t* __restrict__ out,
+                                                 const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat,
+                                                 const uint32_t* __restrict__ order) {
+    const uint32_t nb = *big_count;
+    const bool direct = K == 1 && out;
+    if (nb == 0 && direct) return;  // uniform
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n_pods) return;
+    if (j >= n_lanes) return;
+    const uint32_t row = order ? order[j] : j;
+    const uint32_t chunk = (nb + gridDim.y - 1) / gridDim.y;
+    const uint32_t lo = blockIdx.y * chunk, hi = min(nb, lo + chunk);
     uint64_t top[K];
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
-    for (uint32_t c = 0; c < n_parts; c++) {
-        const uint64_t* src = partial + ((size_t)c * n_pods + j) * K;
-#pragma unroll
-        for (int t = 0; t < K; t++) topk_insert<K>(top, src[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < K; t++) out[(size_t)j * K + t] = top[t];
-}
-
-// Merge of the fast select: top-K over the chunk partials plus the BIG records (integer path) listed
-// by k_big_scan.
-template <int K>
-__global__ __launch_bounds__(256) void k_merge_big(const uint64_t* __restrict__ partial, uint32_t n_parts,
-                                                   uint32_t n_pods, const NodeRec* __restrict__ nodes,
-                                                   const ZoneRec* __restrict__ zones, PodsDev pods,
-                                                   const uint32_t* __restrict__ big_list,
-                                                   const uint32_t* __restrict__ big_count, uint32_t index_base,
-                                                   KCfg cfg, uint64_t* __restrict__ out,
-                                                   const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n_pods) return;
-    uint64_t top[K];
-#pragma unroll
-    for (int t = 0; t < K; t++) top[t] = 0;
-    for (uint32_t c = 0; c < n_parts; c++) {
-        const uint64_t* src = partial + ((size_t)c * n_pods + j) * K;
-#pragma unroll
-        for (int t = 0; t < K; t++) topk_insert<K>(top, src[t]);
-    }
-    const uint32_t nb = *big_count;
-    if (nb) {
-        const PodV p = load_pod(pods, j);
-        uint32_t unsup = 0;
-        for (uint32_t b = 0; b < nb; b++) {
+    uint32_t unsup = 0;
+    if (lo < hi) {
+        const PodV p = load_pod(pods, row);
+        for (uint32_t b = lo; b < hi; b++) {
             const uint32_t i = big_list[b];
             const PairOut o = eval_pair<false>(cfg, nodes[i].v, zones + i, p);
             unsup |= o.status & KG_ST_UNSUPPORTED;
             topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
         }
-        if (unsup) atomicOr(pstat + (pmap ? pmap[j] : j), unsup);
+    }
+    if (direct) {
+        if (top[0]) atomicMax((unsigned long long*)(out + row), (unsigned long long)top[0]);
+    } else {
+        uint64_t* dst = partial + ((size_t)(part0 + blockIdx.y) * ld + row) * K;
+#pragma unroll
+        for (int t = 0; t < K; t++) dst[t] = top[t];
+    }
+    if (unsup) atomicOr(pstat + (pmap ? pmap[row] : row), unsup);
+}
+
+// Per pod row (lane j -> list[j], or j): top-K over partial rows [part0, part0 + n_parts) of stride ld.
+template <int K>
+__global__ __launch_bounds__(256) void k_merge(const uint64_t* __restrict__ partial, uint32_t part0, uint32_t n_parts,
+                                               uint32_t ld, const uint32_t* __restrict__ list, uint32_t n,
+                                               uint64_t* __restrict__ out) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t row = list ? list[j] : j;
+    uint64_t top[K];
+#pragma unroll
+    for (int t = 0; t < K; t++) top[t] = 0;
+    for (uint32_t c = 0; c < n_parts; c++) {
+        const uint64_t* src = partial + ((size_t)(part0 + c) * ld + row) * K;
+#pragma unroll
+        for (int t = 0; t < K; t++) topk_insert<K>(top, src[t]);
     }
 #pragma unroll
-    for (int t = 0; t < K; t++) out[(size_t)j * K + t] = top[t];
+    for (int t = 0; t < K; t++) out[(size_t)row * K + t] = top[t];
 }
 
 // Rebuild the list of F_BIG records (after any change of node state).
@@ -815,103 +806,124 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
 #define KG_LAUNCH_CHECK() (hipGetLastError())
 
 template <int K, bool EXACT, bool FAST, uint32_t PM, int CLS>
-static void select_instance(const LaunchSelect& a, const SelectRange& r, hipStream_t s) {
-    dim3 grid((a.n_pods + 255) / 256, r.n_chunks), block(256);
-    k_select<K, EXACT, FAST, PM, CLS><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end,
-                                                             r.chunk, r.part0, a.index_base, a.cfg, a.partial, a.pmap,
-                                                             a.pstat, a.fast ? a.order : nullptr);
+static void select_instance(const LaunchSelect& a, const SelectRange& r, uint32_t lane0, uint32_t n_lanes, bool atom,
+                            hipStream_t s) {
+    dim3 grid((n_lanes + 255) / 256, r.n_chunks), block(256);
+    k_select<K, EXACT, FAST, PM, CLS><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_lanes, a.n_rows, r.begin, r.end,
+                                                             r.chunk, r.part0, a.index_base, a.cfg, a.partial,
+                                                             atom ? a.out : nullptr, a.pmap, a.pstat,
+                                                             a.order ? a.order + lane0 : nullptr);
 }
 
 template <int K, int CLS>
 static void select_fast(const LaunchSelect& a, const SelectRange& r, hipStream_t s) {
     switch (a.cfg.plugins & 7u) {
-        case 0: select_instance<K, false, true, 0, CLS>(a, r, s); break;
-        case 1: select_instance<K, false, true, 1, CLS>(a, r, s); break;
-        case 2: select_instance<K, false, true, 2, CLS>(a, r, s); break;
-        case 3: select_instance<K, false, true, 3, CLS>(a, r, s); break;
-        case 4: select_instance<K, false, true, 4, CLS>(a, r, s); break;
-        case 5: select_instance<K, false, true, 5, CLS>(a, r, s); break;
-        case 6: select_instance<K, false, true, 6, CLS>(a, r, s); break;
-        default: select_instance<K, false, true, 7, CLS>(a, r, s); break;
+        case 0: select_instance<K, false, true, 0, CLS>(a, r, 0, a.n_fast, false, s); break;
+        case 1: select_instance<K, false, true, 1, CLS>(a, r, 0, a.n_fast, false, s); break;
+        case 2: select_instance<K, false, true, 2, CLS>(a, r, 0, a.n_fast, false, s); break;
+        case 3: select_instance<K, false, true, 3, CLS>(a, r, 0, a.n_fast, false, s); break;
+        case 4: select_instance<K, false, true, 4, CLS>(a, r, 0, a.n_fast, false, s); break;
+        case 5: select_instance<K, false, true, 5, CLS>(a, r, 0, a.n_fast, false, s); break;
+        case 6: select_instance<K, false, true, 6, CLS>(a, r, 0, a.n_fast, false, s); break;
+        default: select_instance<K, false, true, 7, CLS>(a, r, 0, a.n_fast, false, s); break;
     }
 }
 
 hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
-    if (a.fused) {
-        const uint32_t pod_blocks = (a.n_pods + 255) / 256;
-        k_big_init<<<pod_blocks, 256, 0, s>>>(a.n_pods, a.nodes, a.zones, a.pods, a.big_list, a.big_count, a.index_base,
-                                               a.cfg, a.out, a.pmap, a.pstat);
+    const uint32_t K = a.k == 1 ? 1u : (uint32_t)KG_TOPK_MAX;
+    const uint32_t n_fast = a.fast ? a.n_fast : 0u, n_int = a.n_pods - n_fast;
+    // K == 1: the fused fast path and the integer lanes update out[row] by atomicMax
+    if (K == 1 && (a.fused || n_int)) {
+        hipError_t e = hipMemsetAsync(a.out, 0, sizeof(uint64_t) * a.n_rows, s);
+        if (e != hipSuccess) return e;
+    }
+    if (n_fast) {
+        const uint32_t pod_blocks = (n_fast + 255) / 256;
+        // F_BIG records of the fast lanes: integer path, chunked over the device's list
+        {
+            dim3 grid(pod_blocks, a.big_y), block(256);
+            if (K == 1)
+                k_big_sel<1><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, a.n_rows, a.big_list, a.big_count,
+                                                    a.index_base, a.cfg, a.partial, a.big_part0, a.fused ? a.out : nullptr,
+                                                    a.pmap, a.pstat, a.order);
+            else
+                k_big_sel<KG_TOPK_MAX><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, a.n_rows, a.big_list,
+                                                              a.big_count, a.index_base, a.cfg, a.partial, a.big_part0,
+                                                              nullptr, a.pmap, a.pstat, a.order);
+        }
         for (int cls = 0; cls < 2; cls++) {
             const SelectRange& r = a.range[cls];
             if (r.n_chunks == 0) continue;
-            dim3 grid(pod_blocks, r.n_chunks), block(256);
+            if (a.fused) {
+                dim3 grid(pod_blocks, r.n_chunks), block(256);
 #define KG_SEL1(PMV)                                                                                               \
     do {                                                                                                           \
         if (cls == 0)                                                                                              \
-            k_select1<PMV, 0><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end, r.chunk,  \
+            k_select1<PMV, 0><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, r.begin, r.end, r.chunk,    \
                                                      a.index_base, a.cfg, a.out, a.order);                         \
         else                                                                                                       \
-            k_select1<PMV, 1><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, a.n_pods, r.begin, r.end, r.chunk,  \
+            k_select1<PMV, 1><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, r.begin, r.end, r.chunk,    \
                                                      a.index_base, a.cfg, a.out, a.order);                         \
     } while (0)
-            switch (a.cfg.plugins & 7u) {
-                case 0: KG_SEL1(0); break;
-                case 1: KG_SEL1(1); break;
-                case 2: KG_SEL1(2); break;
-                case 3: KG_SEL1(3); break;
-                case 4: KG_SEL1(4); break;
-                case 5: KG_SEL1(5); break;
-                case 6: KG_SEL1(6); break;
-                default: KG_SEL1(7); break;
-            }
+                switch (a.cfg.plugins & 7u) {
+                    case 0: KG_SEL1(0); break;
+                    case 1: KG_SEL1(1); break;
+                    case 2: KG_SEL1(2); break;
+                    case 3: KG_SEL1(3); break;
+                    case 4: KG_SEL1(4); break;
+                    case 5: KG_SEL1(5); break;
+                    case 6: KG_SEL1(6); break;
+                    default: KG_SEL1(7); break;
+                }
 #undef KG_SEL1
-        }
-        return KG_LAUNCH_CHECK();
-    }
-    for (int cls = 0; cls < 2; cls++) {
-        const SelectRange& r = a.range[cls];
-        if (r.n_chunks == 0) continue;
-        if (a.exact) {
-            if (a.k == 1) select_instance<1, true, false, 0, 0>(a, r, s);
-            else select_instance<KG_TOPK_MAX, true, false, 0, 0>(a, r, s);
-        } else if (a.fast) {
-            if (a.k == 1) {
+            } else if (K == 1) {
                 if (cls == 0) select_fast<1, 0>(a, r, s);
                 else select_fast<1, 1>(a, r, s);
             } else {
                 if (cls == 0) select_fast<KG_TOPK_MAX, 0>(a, r, s);
                 else select_fast<KG_TOPK_MAX, 1>(a, r, s);
             }
-        } else {
-            if (a.k == 1) select_instance<1, false, false, 0, 0>(a, r, s);
-            else select_instance<KG_TOPK_MAX, false, false, 0, 0>(a, r, s);
+        }
+        if (!a.fused) {
+            hipError_t e = launch_merge_list(a.partial, 0, select_fparts(a), a.n_rows, a.order, n_fast, K, a.out, s);
+            if (e != hipSuccess) return e;
         }
     }
+    if (n_int && a.irange.n_chunks) {
+        const SelectRange& r = a.irange;
+        if (a.exact) {
+            if (K == 1) select_instance<1, true, false, 0, 0>(a, r, n_fast, n_int, true, s);
+            else select_instance<KG_TOPK_MAX, true, false, 0, 0>(a, r, n_fast, n_int, false, s);
+        } else {
+            if (K == 1) select_instance<1, false, false, 0, 0>(a, r, n_fast, n_int, true, s);
+            else select_instance<KG_TOPK_MAX, false, false, 0, 0>(a, r, n_fast, n_int, false, s);
+        }
+        if (K > 1) {
+            hipError_t e = launch_merge_list(a.partial, r.part0, r.n_chunks, a.n_rows, a.order ? a.order + n_fast : nullptr,
+                                             n_int, K, a.out, s);
+            if (e != hipSuccess) return e;
+        }
+    } else if (n_int && K > 1) {  // no records: no feasible node
+        hipError_t e = launch_merge_list(a.partial, 0, 0, a.n_rows, a.order ? a.order + n_fast : nullptr, n_int, K, a.out, s);
+        if (e != hipSuccess) return e;
+    }
+    return KG_LAUNCH_CHECK();
+}
+
+hipError_t launch_merge_list(const uint64_t* partial, uint32_t part0, uint32_t n_parts, uint32_t ld, const uint32_t* list,
+                             uint32_t n, uint32_t k, uint64_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    dim3 grid((n + 255) / 256), block(256);
+    if (k == 1)
+        k_merge<1><<<grid, block, 0, s>>>(partial, part0, n_parts, ld, list, n, out);
+    else
+        k_merge<KG_TOPK_MAX><<<grid, block, 0, s>>>(partial, part0, n_parts, ld, list, n, out);
     return KG_LAUNCH_CHECK();
 }
 
 hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k, uint64_t* out,
                         hipStream_t s) {
-    dim3 grid((n_pods + 255) / 256), block(256);
-    if (k == 1)
-        k_merge<1><<<grid, block, 0, s>>>(partial, n_parts, n_pods, out);
-    else
-        k_merge<KG_TOPK_MAX><<<grid, block, 0, s>>>(partial, n_parts, n_pods, out);
-    return KG_LAUNCH_CHECK();
-}
-
-hipError_t launch_merge_big(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k,
-                            const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, const uint32_t* big_list,
-                            const uint32_t* big_count, uint32_t index_base, const KCfg& cfg, uint64_t* out,
-                            const uint32_t* pmap, uint32_t* pstat, hipStream_t s) {
-    dim3 grid((n_pods + 255) / 256), block(256);
-    if (k == 1)
-        k_merge_big<1><<<grid, block, 0, s>>>(partial, n_parts, n_pods, nodes, zones, pods, big_list, big_count,
-                                              index_base, cfg, out, pmap, pstat);
-    else
-        k_merge_big<KG_TOPK_MAX><<<grid, block, 0, s>>>(partial, n_parts, n_pods, nodes, zones, pods, big_list,
-                                                        big_count, index_base, cfg, out, pmap, pstat);
-    return KG_LAUNCH_CHECK();
+    return launch_merge_list(partial, 0, n_parts, n_pods, nullptr, n_pods, k, out, s);
 }
 
 // Batched row update (kg_snapshot_update_rows): record r of the staged block (NodeRec, ZoneRec and, with

@@ -162,6 +162,21 @@ KG_HD inline void cpu_counts(const kg_cpu_topo& t, const kg_cpu_alloc* a, int ma
     z.cpu_allocated = al;
 }
 
+// NUMANodeSharedStatus after a cpuset allocation over the NUMA nodes `used` (bit per node): the pod's uid
+// joins singleNUMANode of its one node, or sharedNode of each of several (node_allocation.go:111-143);
+// a zone's status is then shared if any shared pod is there, single if only single pods, idle if none
+// (NUMANodeSharedStatus :60-68). Status bits cover zones < MAX_ZONES.
+KG_HD inline uint32_t cpuset_zone_status(uint32_t status, uint32_t used) {
+    const bool multi = (used & (used - 1)) != 0;
+    for (uint32_t q = 0; q < 4u; q++) {
+        if (!((used >> q) & 1u)) continue;
+        const uint32_t s = (status >> (2 * q)) & 3u;
+        const uint32_t ns = multi ? 2u : (s == 0u ? 1u : s);
+        status = (status & ~(3u << (2 * q))) | (ns << (2 * q));
+    }
+    return status;
+}
+
 // Magnitude bound of the float64 fast path: operands below 2^44 keep 100 * headroom below 2^51
 // (exact) and make the upward-rounded reciprocal's quotient exact after truncation.
 constexpr int64_t FAST_LIMIT = (int64_t)1 << 44;

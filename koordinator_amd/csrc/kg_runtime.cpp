@@ -63,6 +63,7 @@ struct kg_snap {
     std::vector<uint32_t> pos;     // snapshot index -> record position
     uint32_t n0 = 0;               // records of class 0 (positions [0, n0))
     uint32_t n_topo = 0;           // Restricted / BestEffort records (need the general NUMA topology manager)
+    uint32_t n_big_est = 0;        // F_BIG records at the last upload / row update (grid sizing of k_big_sel)
     bool uploaded = false;
     bool weights_small = false;  // per-resource weights <= 2^12: float64 fast path allowed
     // config-5 tables (KG_PLUGIN_DEV / RSV / QUOTA)
@@ -133,21 +134,34 @@ struct kg_snap {
 struct kg_pods {
     kg_ctx* ctx = nullptr;
     uint32_t cap = 0, n = 0;
-    int64_t* d_cols = nullptr;  // 9 int64 columns of `cap` entries
-    uint32_t* d_flags = nullptr;
+    // Inputs of the batch: one device blob filled from pinned staging by one copy per upload, regions in
+    // pod_layout(n) order; the PodsDev and list pointers below point into it for the current batch.
+    uint8_t* d_in = nullptr;
+    uint8_t* h_in = nullptr;  // pinned host staging of the same size
+    size_t in_bytes = 0;
     PodsDev dev{};
+    uint32_t* d_order = nullptr;  // lanes of the base select: fast pods grouped by wave kind, then integer-path pods
+    uint32_t n_fast = 0;          // pods in the float64 fast domain (the leading d_order entries)
+    uint32_t* d_pmap = nullptr;   // config-5 "plain" pods (batch positions) grouped by wave kind
+    uint32_t* d_xlist = nullptr;  // config-5 pods through k_ext_select (batch positions)
+    uint32_t* d_stat_list = nullptr;  // pods carrying a GPU request or a reservation class
+    int64_t* d_dev_req = nullptr;     // [n][KG_DEV_R]
+    uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32): 5 x n
+    uint8_t* d_dcls = nullptr;        // GPU request class per pod (DevSum nibble), DEV_CLASSES = none
+    DevClass* d_dclass = nullptr;
+    uint32_t n_dclass = 0;
+    uint32_t n_stat = 0;
+    uint32_t n_stat_cls = 0;          // leading d_stat_list entries without a GPU request (class views only)
+    uint32_t n_plain = 0, n_x = 0;
     // select results
     uint64_t* d_partial = nullptr;
     size_t partial_cap = 0;  // entries
     uint64_t* d_keys = nullptr;
     uint32_t k_last = 0, kk_last = 0;
+    uint64_t* h_keys = nullptr;    // pinned download staging of the keys [cap][KG_TOPK_MAX]
     uint32_t* d_pstat = nullptr;   // per pod: KG_ST_UNSUPPORTED / KG_ST_QUOTA of the last select (kg_result_status)
     uint32_t* d_reason = nullptr;  // replay: per pod OR of the filter status bits (kg_replay out_reason)
-    // GPU request classes of the batch (DevSum nibbles) and the per-record DevSum of the last config-5 select
-    uint8_t* d_dcls = nullptr;
-    DevClass* d_dclass = nullptr;
-    uint32_t n_dclass = 0;
-    DevSum* d_devsum = nullptr;
+    DevSum* d_devsum = nullptr;    // per record DevSum of the last config-5 select
     size_t devsum_cap = 0;
     // pass-1 pair results kept for pass 2 (ExtDev.pairs)
     uint32_t* d_pairs = nullptr;
@@ -158,17 +172,12 @@ struct kg_pods {
     uint32_t* d_step = nullptr;
     uint64_t* d_gather = nullptr;
     size_t gather_cap = 0;
-    bool fast_ok = false;  // every value below FAST_LIMIT and no pod NUMA policy
+    bool fast_ok = false;  // every pod in the fast domain (no value >= 2^44, no pod NUMA policy, no cpuset binding)
     bool pod_policy = false;  // some pod carries its own NUMA policy
     bool any_cpu_bind = false;  // some pod binds cpusets (KG_POD_CPU_BIND)
     std::vector<uint32_t> h_flags;  // host copies for argument checks (kg_forget of a cpuset pod)
     std::vector<int64_t> h_req_cpu;
-    // config-5 columns and scratch
-    int64_t* d_dev_req = nullptr;     // [cap][KG_DEV_R]
-    uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32): 5 x cap
-    uint32_t* d_stat_list = nullptr;  // pods carrying a GPU request or a reservation class
-    uint32_t n_stat = 0;
-    uint32_t n_stat_cls = 0;          // leading d_stat_list entries without a GPU request (class views only)
+    // config-5 scratch
     uint32_t* d_qst = nullptr;        // ElasticQuota PreFilter status per pod
     uint32_t* d_dev_max = nullptr;    // [cap] pass-1 NormalizeScore maxima
     uint32_t* d_rsv_max = nullptr;
@@ -179,17 +188,7 @@ struct kg_pods {
     uint32_t* d_batch = nullptr;      // kg_batch_schedule: groups + per-pod outputs (7 x cap + 1 words)
     hipGraphExec_t xexec = nullptr;   // ext replay graph
     std::vector<uint8_t> xkey;
-    // config-5 select split: "plain" pods (no GPU request, no reservation class or affinity) see only
-    // NodeResourcesFit / LoadAware / NodeNUMAResource and take the fast k_select over a compacted copy
-    // of their columns; the rest go through k_ext_select by list
-    int64_t* d_pcols = nullptr;   // 9 int64 columns of `cap` entries (plain pods, compacted)
-    uint32_t* d_pflags = nullptr;
-    uint32_t* d_pmap = nullptr;   // plain row -> batch position
-    uint32_t* d_order = nullptr;  // batch positions grouped by wave kind (fast select lanes)
-    uint32_t* d_xlist = nullptr;  // config-5 row -> batch position
-    uint64_t* d_tkeys = nullptr;  // [KG_TOPK_MAX][cap] sub-batch keys before the scatter
-    uint32_t n_plain = 0, n_x = 0;
-    PodsDev plain{};
+    uint64_t* d_tkeys = nullptr;  // [KG_TOPK_MAX][cap] config-5 sub-batch keys before the scatter
     // replay graph (G steps) cached for the (snapshot buffers, batch size, configuration) it captured
     hipGraphExec_t rexec = nullptr;
     std::vector<uint8_t> rkey;
@@ -586,12 +585,14 @@ void set_node_index(NodeRec& r, uint32_t i) {
 uint32_t rec_numa_policy(const NodeRec& r) { return ((uint32_t)r.v[N_FLAGS] >> F_NUMA_POLICY_SHIFT) & 15u; }
 
 void count_topo(kg_snap* s) {
-    uint32_t t = 0;
+    uint32_t t = 0, b = 0;
     for (uint32_t p = 0; p < s->n; p++) {
         const uint32_t pol = rec_numa_policy(s->h_nodes[p]);
         t += pol == KG_NUMA_BEST_EFFORT || pol == KG_NUMA_RESTRICTED;
+        b += ((uint32_t)s->h_nodes[p].v[N_FLAGS] & F_BIG) != 0;
     }
     s->n_topo = t;
+    s->n_big_est = b;
 }
 
 // Select-mode ext kernels may drop the general topology manager when nothing in the pair set needs it
@@ -1006,6 +1007,7 @@ kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
             if (o->zone_mem_used[zz]) o->zone_mem_used[zz][i] = zr.mem_used[zz];
         }
         if (o->cpuset_alloc_milli) o->cpuset_alloc_milli[i] = v[N_CPUSET];
+        if (o->numa_zone_status) o->numa_zone_status[i] = zr.status;
         if (o->cpu_alloc) {
             if (!ca.empty()) o->cpu_alloc[i] = ca[pp];
             else std::memset(&o->cpu_alloc[i], 0, sizeof(kg_cpu_alloc));
@@ -1049,6 +1051,77 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     return KG_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Regions of a pod batch's input blob for n pods (256-byte aligned). The regions every select reads come
+// first; the config-5 regions after `ext` are copied only when the batch carries config-5 data (else they
+// are set on the device). The layout depends on n only, so cached replay graphs keyed on n stay valid.
+struct PodLayout {
+    size_t cols, flags, order, pmap, ext, xlist, stat, dev_req, xcols, dclass, dcls, total;
+};
+
+PodLayout pod_layout(uint32_t n) {
+    PodLayout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o = (o + bytes + 255) & ~(size_t)255;
+        return at;
+    };
+    L.cols = take(sizeof(int64_t) * 9 * (size_t)n);
+    L.flags = take(sizeof(uint32_t) * (size_t)n);
+    L.order = take(sizeof(uint32_t) * (size_t)n);
+    L.pmap = take(sizeof(uint32_t) * (size_t)n);
+    L.ext = o;
+    L.xlist = take(sizeof(uint32_t) * (size_t)n);
+    L.stat = take(sizeof(uint32_t) * (size_t)n);
+    L.dev_req = take(sizeof(int64_t) * DEV_R * (size_t)n);
+    L.xcols = take(sizeof(uint32_t) * 5 * (size_t)n);
+    L.dclass = take(sizeof(DevClass) * DEV_CLASSES);
+    L.dcls = take((size_t)n);
+    L.total = o;
+    return L;
+}
+
+// Point the batch's device views at the regions of pod_layout(n).
+void pod_views(kg_pods* p, uint32_t n) {
+    const PodLayout L = pod_layout(n);
+    uint8_t* d = p->d_in;
+    int64_t* c = reinterpret_cast<int64_t*>(d + L.cols);
+    PodsDev& v = p->dev;
+    v.req_cpu = c + 0 * (size_t)n;
+    v.req_mem = c + 1 * (size_t)n;
+    v.req_eph = c + 2 * (size_t)n;
+    v.sc_req0 = c + 3 * (size_t)n;
+    v.sc_req1 = c + 4 * (size_t)n;
+    v.nz_cpu = c + 5 * (size_t)n;
+    v.nz_mem = c + 6 * (size_t)n;
+    v.la_est0 = c + 7 * (size_t)n;
+    v.la_est1 = c + 8 * (size_t)n;
+    v.flags = reinterpret_cast<uint32_t*>(d + L.flags);
+    p->d_order = reinterpret_cast<uint32_t*>(d + L.order);
+    p->d_pmap = reinterpret_cast<uint32_t*>(d + L.pmap);
+    p->d_xlist = reinterpret_cast<uint32_t*>(d + L.xlist);
+    p->d_stat_list = reinterpret_cast<uint32_t*>(d + L.stat);
+    p->d_dev_req = reinterpret_cast<int64_t*>(d + L.dev_req);
+    p->d_xcols = reinterpret_cast<uint32_t*>(d + L.xcols);
+    p->d_dclass = reinterpret_cast<DevClass*>(d + L.dclass);
+    p->d_dcls = d + L.dcls;
+    v.dev_req = p->d_dev_req;
+    v.dev_count = p->d_xcols;
+    v.dev_keys = p->d_xcols + (size_t)n;
+    v.quota = reinterpret_cast<const int32_t*>(p->d_xcols + 2 * (size_t)n);
+    v.quota_keys = p->d_xcols + 3 * (size_t)n;
+    v.rsv_class = reinterpret_cast<const int32_t*>(p->d_xcols + 4 * (size_t)n);
+    v.dev_cls = p->d_dcls;
+}
+
+}  // namespace
+
+extern "C" {
+
 kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
     if (!ctx || !out || capacity == 0) return KG_INVALID_ARG;
     std::lock_guard<std::mutex> g(ctx->mu);
@@ -1056,15 +1129,14 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
     kg_pods* p = new kg_pods();
     p->ctx = ctx;
     p->cap = capacity;
+    p->in_bytes = pod_layout(capacity).total;
     hipSetDevice(ctx->device);
-    bool ok = hipMalloc(&p->d_cols, sizeof(int64_t) * 9 * capacity) == hipSuccess &&
-              hipMalloc(&p->d_flags, sizeof(uint32_t) * capacity) == hipSuccess &&
+    bool ok = hipMalloc(&p->d_in, p->in_bytes) == hipSuccess &&
+              hipHostMalloc(&p->h_in, p->in_bytes, hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&p->d_keys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
+              hipHostMalloc(&p->h_keys, sizeof(uint64_t) * KG_TOPK_MAX * capacity, hipHostMallocDefault) == hipSuccess &&
               hipMalloc(&p->d_winners, sizeof(uint64_t) * (capacity + 1)) == hipSuccess &&
               hipMalloc(&p->d_step, sizeof(uint32_t) * 64) == hipSuccess &&
-              hipMalloc(&p->d_dev_req, sizeof(int64_t) * DEV_R * capacity) == hipSuccess &&
-              hipMalloc(&p->d_xcols, sizeof(uint32_t) * 5 * capacity) == hipSuccess &&
-              hipMalloc(&p->d_stat_list, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_qst, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_dev_max, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_rsv_max, sizeof(uint32_t) * capacity) == hipSuccess &&
@@ -1072,60 +1144,20 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_minors, sizeof(uint32_t) * (capacity + 1)) == hipSuccess &&
               hipMalloc(&p->d_buckets, sizeof(uint64_t) * 3 * 128) == hipSuccess &&
               hipMalloc(&p->d_aout, sizeof(int32_t) * 2) == hipSuccess &&
-              hipMalloc(&p->d_pcols, sizeof(int64_t) * 9 * capacity) == hipSuccess &&
-              hipMalloc(&p->d_pflags, sizeof(uint32_t) * capacity) == hipSuccess &&
-              hipMalloc(&p->d_pmap, sizeof(uint32_t) * capacity) == hipSuccess &&
-              hipMalloc(&p->d_order, sizeof(uint32_t) * capacity) == hipSuccess &&
-              hipMalloc(&p->d_xlist, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
               hipMalloc(&p->d_pstat, sizeof(uint32_t) * capacity) == hipSuccess &&
-              hipMalloc(&p->d_reason, sizeof(uint32_t) * (capacity + 1)) == hipSuccess &&
-              hipMalloc(&p->d_dcls, capacity) == hipSuccess &&
-              hipMalloc(&p->d_dclass, sizeof(DevClass) * DEV_CLASSES) == hipSuccess;
+              hipMalloc(&p->d_reason, sizeof(uint32_t) * (capacity + 1)) == hipSuccess;
     if (!ok) {
-        hipFree(p->d_cols);
-        hipFree(p->d_flags);
-        hipFree(p->d_keys);
-        hipFree(p->d_winners);
-        hipFree(p->d_step);
-        for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst,
-                        (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors,
-                        (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_pcols, (void*)p->d_pflags,
-                        (void*)p->d_pmap, (void*)p->d_order, (void*)p->d_xlist, (void*)p->d_tkeys, (void*)p->d_pstat,
-                        (void*)p->d_reason, (void*)p->d_dcls, (void*)p->d_dclass})
+        for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_qst,
+                        (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets,
+                        (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat, (void*)p->d_reason})
             hipFree(b);
+        hipHostFree(p->h_in);
+        hipHostFree(p->h_keys);
         delete p;
         return fail(ctx, KG_OOM, "pod batch of %u", capacity);
     }
-    int64_t* c = p->d_cols;
-    p->dev.req_cpu = c + 0 * (size_t)capacity;
-    p->dev.req_mem = c + 1 * (size_t)capacity;
-    p->dev.req_eph = c + 2 * (size_t)capacity;
-    p->dev.sc_req0 = c + 3 * (size_t)capacity;
-    p->dev.sc_req1 = c + 4 * (size_t)capacity;
-    p->dev.nz_cpu = c + 5 * (size_t)capacity;
-    p->dev.nz_mem = c + 6 * (size_t)capacity;
-    p->dev.la_est0 = c + 7 * (size_t)capacity;
-    p->dev.la_est1 = c + 8 * (size_t)capacity;
-    p->dev.flags = p->d_flags;
-    p->dev.dev_req = p->d_dev_req;
-    p->dev.dev_count = p->d_xcols;
-    p->dev.dev_keys = p->d_xcols + (size_t)capacity;
-    p->dev.quota = (const int32_t*)(p->d_xcols + 2 * (size_t)capacity);
-    p->dev.quota_keys = p->d_xcols + 3 * (size_t)capacity;
-    p->dev.rsv_class = (const int32_t*)(p->d_xcols + 4 * (size_t)capacity);
-    p->dev.dev_cls = p->d_dcls;
-    int64_t* pc = p->d_pcols;
-    p->plain.req_cpu = pc + 0 * (size_t)capacity;
-    p->plain.req_mem = pc + 1 * (size_t)capacity;
-    p->plain.req_eph = pc + 2 * (size_t)capacity;
-    p->plain.sc_req0 = pc + 3 * (size_t)capacity;
-    p->plain.sc_req1 = pc + 4 * (size_t)capacity;
-    p->plain.nz_cpu = pc + 5 * (size_t)capacity;
-    p->plain.nz_mem = pc + 6 * (size_t)capacity;
-    p->plain.la_est0 = pc + 7 * (size_t)capacity;
-    p->plain.la_est1 = pc + 8 * (size_t)capacity;
-    p->plain.flags = p->d_pflags;
+    pod_views(p, 0);
     *out = p;
     return KG_OK;
 }
@@ -1135,87 +1167,50 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     kg_ctx* ctx = p->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
     if (n > p->cap) return fail(ctx, KG_INVALID_ARG, "%u pods > capacity %u", n, p->cap);
-    std::vector<int64_t> h((size_t)9 * std::max<uint32_t>(n, 1));
-    std::vector<uint32_t> f(std::max<uint32_t>(n, 1));
-    const int64_t* src[9] = {cols->req_cpu, cols->req_mem, cols->req_eph, cols->sc_req[0], cols->sc_req[1],
-                             cols->nz_cpu, cols->nz_mem, cols->la_est[0], cols->la_est[1]};
-    bool fast = true, any_pol = false;
-    for (int c = 0; c < 9; c++)
-        for (uint32_t j = 0; j < n; j++) {
-            const int64_t x = src[c] ? src[c][j] : 0;
-            h[(size_t)c * n + j] = x;
-            fast &= !kg_big(x) && x >= 0;  // fast path: non-negative requests below 2^44
-        }
+    // ---- validation: nothing of the batch object changes before every check has passed
     for (uint32_t j = 0; j < n; j++) {
         const uint32_t pol = cols->numa_policy ? cols->numa_policy[j] : 0;
         if (pol > KG_NUMA_SINGLE_NODE) return fail(ctx, KG_INVALID_ARG, "pod %u: NUMA policy %u", j, pol);
-        f[j] = (cols->flags ? (cols->flags[j] & 0xFFFFu) : 0u) | (pol << 16);
-        fast &= pol == KG_NUMA_NONE;
-        any_pol |= pol != KG_NUMA_NONE;
-    }
-    bool any_bind = false;
-    for (uint32_t j = 0; j < n; j++) any_bind |= (f[j] & KG_POD_CPU_BIND) != 0;
-    // cpuset-binding pods take the integer path (the fast block has no CPU counts); nodes with a CPU bind
-    // policy are F_BIG and take it for every pod
-    p->fast_ok = fast && !any_bind;
-    p->pod_policy = any_pol;
-    p->any_cpu_bind = any_bind;
-    p->h_flags.assign(f.begin(), f.begin() + n);
-    p->h_req_cpu.assign(n, 0);
-    for (uint32_t j = 0; j < n; j++) p->h_req_cpu[j] = cols->req_cpu ? cols->req_cpu[j] : 0;
-    // config-5 columns (absent columns: no GPU request, no quota, no reservation class)
-    std::vector<int64_t> dreq((size_t)DEV_R * std::max<uint32_t>(n, 1), 0);
-    std::vector<uint32_t> xc((size_t)5 * std::max<uint32_t>(n, 1), 0);
-    std::vector<uint32_t> stat, pmap, xlist;
-    std::vector<uint8_t> dcls(std::max<uint32_t>(n, 1), (uint8_t)DEV_CLASSES);
-    std::vector<DevClass> classes;
-    for (uint32_t j = 0; j < n; j++) {
-        const uint32_t cnt = cols->dev_count ? cols->dev_count[j] : 0u;
-        const uint32_t keys = cols->dev_keys ? cols->dev_keys[j] : 0u;
-        for (int r = 0; r < DEV_R; r++) {
-            const int64_t v = cols->dev_req ? cols->dev_req[(size_t)j * DEV_R + r] : 0;
-            if (v < 0) return fail(ctx, KG_INVALID_ARG, "pod %u: negative GPU request", j);
-            dreq[(size_t)j * DEV_R + r] = v;
-        }
-        if (cnt > 0) {  // GPU request class: the per-instance request the minor predicate reads
-            DevClass c{};
-            c.dkeys = keys & 7u;
-            for (int r = 0; r < DEV_R; r++) c.dreq[r] = ((c.dkeys >> r) & 1u) ? dreq[(size_t)j * DEV_R + r] : 0;
-            size_t k = 0;
-            while (k < classes.size() && !(classes[k].dkeys == c.dkeys && classes[k].dreq[0] == c.dreq[0] &&
-                                           classes[k].dreq[1] == c.dreq[1] && classes[k].dreq[2] == c.dreq[2]))
-                k++;
-            if (k == classes.size() && classes.size() < (size_t)DEV_CLASSES) classes.push_back(c);
-            if (k < classes.size()) dcls[j] = (uint8_t)k;
-        }
-        const int32_t q = cols->quota ? cols->quota[j] : -1;
+        for (int r = 0; cols->dev_req && r < DEV_R; r++)
+            if (cols->dev_req[(size_t)j * DEV_R + r] < 0) return fail(ctx, KG_INVALID_ARG, "pod %u: negative GPU request", j);
         const int32_t cls = cols->rsv_class ? cols->rsv_class[j] : -1;
         if (cls >= RSV_MAX_CLASSES) return fail(ctx, KG_UNSUPPORTED, "pod %u: reservation class %d >= %d", j, cls, RSV_MAX_CLASSES);
-        xc[j] = cnt;
-        xc[(size_t)n + j] = keys;
-        xc[2 * (size_t)n + j] = (uint32_t)q;
-        xc[3 * (size_t)n + j] = cols->quota_keys ? cols->quota_keys[j] : 0u;
-        xc[4 * (size_t)n + j] = (uint32_t)cls;
-        if (cnt > 0 || cls >= 0) stat.push_back(j);
-        if (cnt == 0 && cls < 0 && !(f[j] & KG_POD_RSV_REQUIRED)) pmap.push_back(j);
-        else xlist.push_back(j);
     }
-    // wave-uniform work in the config-5 kernels: GPU pods (by GPU count) first, then reservation
-    // classes in order; rows are scattered back by list, so the order does not change any result
-    auto kind = [&](uint32_t j) {
-        const uint32_t cnt = xc[j];
-        const uint64_t gpu = cnt > 0 ? ((uint64_t)(0u - cnt) << 8) | (xc[(size_t)n + j] & 0xFFu) : 0u;  // count, request keys
-        const int32_t cls = (int32_t)xc[4 * (size_t)n + j];
-        return std::make_tuple(gpu, (f[j] & KG_POD_RSV_REQUIRED) != 0, cls);
-    };
-    auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
-    std::stable_sort(stat.begin(), stat.end(), by_kind);
-    std::stable_sort(xlist.begin(), xlist.end(), by_kind);
-    // fast select: pods grouped by wave kind (fast_kind_match in kg_eval.h), so whole waves run a
-    // kind-specialised loop; keys are written per pod, so the order changes no result
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    // the previous upload's copy has completed (every upload ends with a stream synchronisation), so the
+    // pinned staging can be rewritten
+    const PodLayout L = pod_layout(n);
+    uint8_t* h = p->h_in;
+    int64_t* hc = reinterpret_cast<int64_t*>(h + L.cols);
+    const int64_t* src[9] = {cols->req_cpu, cols->req_mem, cols->req_eph, cols->sc_req[0], cols->sc_req[1],
+                             cols->nz_cpu, cols->nz_mem, cols->la_est[0], cols->la_est[1]};
+    // per pod: outside the fast domain (a value < 0 or >= 2^44: one unsigned compare)
+    std::vector<uint8_t> slow(std::max<uint32_t>(n, 1), 0);
+    for (int c = 0; c < 9; c++) {
+        int64_t* dst = hc + (size_t)c * n;
+        if (!src[c]) {
+            std::memset(dst, 0, sizeof(int64_t) * n);
+            continue;
+        }
+        std::memcpy(dst, src[c], sizeof(int64_t) * n);
+        for (uint32_t j = 0; j < n; j++) slow[j] |= (uint64_t)src[c][j] >= (uint64_t)FAST_LIMIT;
+    }
+    uint32_t* f = reinterpret_cast<uint32_t*>(h + L.flags);
+    bool any_pol = false, any_bind = false, any_rsv_req = false;
+    for (uint32_t j = 0; j < n; j++) {
+        const uint32_t pol = cols->numa_policy ? cols->numa_policy[j] : 0;
+        f[j] = (cols->flags ? (cols->flags[j] & 0xFFFFu) : 0u) | (pol << 16);
+        any_pol |= pol != KG_NUMA_NONE;
+        any_bind |= (f[j] & KG_POD_CPU_BIND) != 0;
+        any_rsv_req |= (f[j] & KG_POD_RSV_REQUIRED) != 0;
+        // the fast block has no CPU counts and no pod-level NUMA policy: such pods take the integer path
+        slow[j] |= pol != KG_NUMA_NONE || (f[j] & KG_POD_CPU_BIND) != 0;
+    }
+    // fast select lanes: the fast pods grouped by wave kind (fast_kind_match in kg_eval.h; keys are written
+    // per pod, so the order changes no result), then the integer-path pods in batch order
     auto wave_kind = [&](uint32_t j) {
         const uint32_t fl = f[j];
-        const int64_t cpu = h[j], mem = h[(size_t)n + j], sc0 = h[3 * (size_t)n + j], sc1 = h[4 * (size_t)n + j];
+        const int64_t cpu = hc[j], mem = hc[(size_t)n + j], sc0 = hc[3 * (size_t)n + j], sc1 = hc[4 * (size_t)n + j];
         const uint32_t excl = KG_POD_DAEMONSET | KG_POD_NUMA_SKIP | KG_POD_CPU_BIND;
         if ((fl & (KG_POD_PROD | excl)) == KG_POD_PROD && (fl & (KG_POD_HAS_CPU | KG_POD_HAS_MEM)) && sc0 == 0 && sc1 == 0)
             return 0;
@@ -1223,77 +1218,109 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             return 1;
         return 2;
     };
-    // stable bucket order by kind (three kinds): the batch, and the plain sub-batch's row map
     std::vector<uint8_t> wk(std::max<uint32_t>(n, 1));
-    for (uint32_t j = 0; j < n; j++) wk[j] = (uint8_t)wave_kind(j);
-    auto by_wave_kind = [&](const std::vector<uint32_t>& in) {
-        std::vector<uint32_t> out;
-        out.reserve(in.size());
-        for (uint8_t k = 0; k < 3; k++)
-            for (uint32_t j : in)
-                if (wk[j] == k) out.push_back(j);
-        return out;
-    };
-    std::vector<uint32_t> order(n);
-    for (uint32_t j = 0; j < n; j++) order[j] = j;
-    order = by_wave_kind(order);
-    pmap = by_wave_kind(pmap);
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < n; j++) {
+        wk[j] = slow[j] ? 3 : (uint8_t)wave_kind(j);
+        cnt[wk[j]]++;
+    }
+    uint32_t* order = reinterpret_cast<uint32_t*>(h + L.order);
+    {
+        uint32_t at[4] = {0, cnt[0], cnt[0] + cnt[1], cnt[0] + cnt[1] + cnt[2]};
+        for (uint32_t j = 0; j < n; j++) order[at[wk[j]]++] = j;
+    }
+    const uint32_t n_fast = cnt[0] + cnt[1] + cnt[2];
+    // config-5 columns (absent columns: no GPU request, no quota, no reservation class)
+    const bool ext_cols = cols->dev_req || cols->dev_count || cols->dev_keys || cols->quota || cols->quota_keys ||
+                          cols->rsv_class;
+    uint32_t* xc = reinterpret_cast<uint32_t*>(h + L.xcols);
+    uint32_t* pmap = reinterpret_cast<uint32_t*>(h + L.pmap);
+    uint32_t* xlist = reinterpret_cast<uint32_t*>(h + L.xlist);
+    uint32_t* stat = reinterpret_cast<uint32_t*>(h + L.stat);
+    uint32_t np = 0, nx = 0, ns = 0;
+    std::vector<DevClass> classes;
+    if (!ext_cols && !any_rsv_req) {
+        // every pod is "plain": the plain lanes are the wave-kind order of every pod
+        std::memcpy(pmap, order, sizeof(uint32_t) * n);
+        np = n;
+    } else {
+        int64_t* dreq = reinterpret_cast<int64_t*>(h + L.dev_req);
+        uint8_t* dcls = h + L.dcls;
+        for (uint32_t j = 0; j < n; j++) {
+            const uint32_t cntj = cols->dev_count ? cols->dev_count[j] : 0u;
+            const uint32_t keys = cols->dev_keys ? cols->dev_keys[j] : 0u;
+            for (int r = 0; r < DEV_R; r++) dreq[(size_t)j * DEV_R + r] = cols->dev_req ? cols->dev_req[(size_t)j * DEV_R + r] : 0;
+            dcls[j] = (uint8_t)DEV_CLASSES;
+            if (cntj > 0) {  // GPU request class: the per-instance request the minor predicate reads
+                DevClass c{};
+                c.dkeys = keys & 7u;
+                for (int r = 0; r < DEV_R; r++) c.dreq[r] = ((c.dkeys >> r) & 1u) ? dreq[(size_t)j * DEV_R + r] : 0;
+                size_t k = 0;
+                while (k < classes.size() && !(classes[k].dkeys == c.dkeys && classes[k].dreq[0] == c.dreq[0] &&
+                                               classes[k].dreq[1] == c.dreq[1] && classes[k].dreq[2] == c.dreq[2]))
+                    k++;
+                if (k == classes.size() && classes.size() < (size_t)DEV_CLASSES) classes.push_back(c);
+                if (k < classes.size()) dcls[j] = (uint8_t)k;
+            }
+            const int32_t q = cols->quota ? cols->quota[j] : -1;
+            const int32_t cls = cols->rsv_class ? cols->rsv_class[j] : -1;
+            xc[j] = cntj;
+            xc[(size_t)n + j] = keys;
+            xc[2 * (size_t)n + j] = (uint32_t)q;
+            xc[3 * (size_t)n + j] = cols->quota_keys ? cols->quota_keys[j] : 0u;
+            xc[4 * (size_t)n + j] = (uint32_t)cls;
+            if (cntj > 0 || cls >= 0) stat[ns++] = j;
+            if (cntj == 0 && cls < 0 && !(f[j] & KG_POD_RSV_REQUIRED)) pmap[np++] = j;
+            else xlist[nx++] = j;
+        }
+        // wave-uniform work in the config-5 kernels: GPU pods (by GPU count) first, then reservation
+        // classes in order; rows are scattered back by list, so the order does not change any result
+        auto kind = [&](uint32_t j) {
+            const uint32_t c = xc[j];
+            const uint64_t gpu = c > 0 ? ((uint64_t)(0u - c) << 8) | (xc[(size_t)n + j] & 0xFFu) : 0u;  // count, request keys
+            const int32_t cls = (int32_t)xc[4 * (size_t)n + j];
+            return std::make_tuple(gpu, (f[j] & KG_POD_RSV_REQUIRED) != 0, cls);
+        };
+        auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
+        std::stable_sort(stat, stat + ns, by_kind);
+        std::stable_sort(xlist, xlist + nx, by_kind);
+        // plain lanes grouped by wave kind (stable buckets)
+        std::vector<uint32_t> by;
+        by.reserve(np);
+        for (uint8_t k = 0; k < 4; k++)
+            for (uint32_t t = 0; t < np; t++)
+                if (wk[pmap[t]] == k) by.push_back(pmap[t]);
+        std::memcpy(pmap, by.data(), sizeof(uint32_t) * np);
+        if (!classes.empty()) std::memcpy(h + L.dclass, classes.data(), sizeof(DevClass) * classes.size());
+    }
     uint32_t n_stat_cls = 0;
-    while (n_stat_cls < stat.size() && xc[stat[n_stat_cls]] == 0) n_stat_cls++;
-    const uint32_t np = (uint32_t)pmap.size();
-    std::vector<int64_t> hp((size_t)9 * std::max<uint32_t>(np, 1));
-    std::vector<uint32_t> fp(std::max<uint32_t>(np, 1));
-    for (uint32_t t = 0; t < np; t++) {
-        for (int c = 0; c < 9; c++) hp[(size_t)c * np + t] = h[(size_t)c * n + pmap[t]];
-        fp[t] = f[pmap[t]];
-    }
-    HIP_TRY(ctx, hipSetDevice(ctx->device));
-    // absent config-5 columns: their defaults (no GPU request, no quota, no reservation class) set on the
-    // device instead of copied from pageable host memory
-    if (cols->dev_req)
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_dev_req, dreq.data(), sizeof(int64_t) * DEV_R * n, hipMemcpyHostToDevice, ctx->stream));
-    else if (n)
+    while (n_stat_cls < ns && xc[stat[n_stat_cls]] == 0) n_stat_cls++;
+    // ---- one copy of the regions this batch needs; absent config-5 columns set on the device
+    pod_views(p, n);
+    const bool ext_copy = ext_cols || any_rsv_req;
+    const size_t bytes = n ? (ext_copy ? L.total : L.ext) : 0;
+    if (bytes) HIP_TRY(ctx, hipMemcpyAsync(p->d_in, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (n && !ext_copy) {
         HIP_TRY(ctx, hipMemsetAsync(p->d_dev_req, 0, sizeof(int64_t) * DEV_R * n, ctx->stream));
-    const void* xsrc[5] = {cols->dev_count, cols->dev_keys, cols->quota, cols->quota_keys, cols->rsv_class};
-    const int xdef[5] = {0, 0, 0xFF, 0, 0xFF};  // -1 quota / class
-    for (int c = 0; c < 5; c++) {
-        if (!n) break;
-        if (xsrc[c])
-            HIP_TRY(ctx, hipMemcpyAsync(p->d_xcols + (size_t)c * p->cap, xc.data() + (size_t)c * n, sizeof(uint32_t) * n,
-                                        hipMemcpyHostToDevice, ctx->stream));
-        else
-            HIP_TRY(ctx, hipMemsetAsync(p->d_xcols + (size_t)c * p->cap, xdef[c], sizeof(uint32_t) * n, ctx->stream));
-    }
-    if (!stat.empty())
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_stat_list, stat.data(), sizeof(uint32_t) * stat.size(), hipMemcpyHostToDevice, ctx->stream));
-    p->n_stat = (uint32_t)stat.size();
-    p->n_stat_cls = n_stat_cls;
-    if (np) {
-        for (int c = 0; c < 9; c++)
-            HIP_TRY(ctx, hipMemcpyAsync(p->d_pcols + (size_t)c * p->cap, hp.data() + (size_t)c * np, sizeof(int64_t) * np,
-                                        hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_pflags, fp.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_pmap, pmap.data(), sizeof(uint32_t) * np, hipMemcpyHostToDevice, ctx->stream));
-    }
-    if (!xlist.empty())
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_xlist, xlist.data(), sizeof(uint32_t) * xlist.size(), hipMemcpyHostToDevice, ctx->stream));
-    if (n) HIP_TRY(ctx, hipMemcpyAsync(p->d_order, order.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-    p->n_plain = np;
-    p->n_x = (uint32_t)xlist.size();
-    for (int c = 0; c < 9; c++)
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_cols + (size_t)c * p->cap, h.data() + (size_t)c * n, sizeof(int64_t) * n,
-                                    hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(p->d_flags, f.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-    if (!classes.empty())
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_dcls, dcls.data(), n, hipMemcpyHostToDevice, ctx->stream));
-    else if (n)
+        const int xdef[5] = {0, 0, 0xFF, 0, 0xFF};  // -1 quota / class
+        for (int c = 0; c < 5; c++)
+            HIP_TRY(ctx, hipMemsetAsync(p->d_xcols + (size_t)c * n, xdef[c], sizeof(uint32_t) * n, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(p->d_dcls, DEV_CLASSES, n, ctx->stream));
-    if (!classes.empty())
-        HIP_TRY(ctx, hipMemcpyAsync(p->d_dclass, classes.data(), sizeof(DevClass) * classes.size(), hipMemcpyHostToDevice,
-                                    ctx->stream));
-    p->n_dclass = (uint32_t)classes.size();
+    }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    // ---- commit
     p->n = n;
+    p->n_fast = n_fast;
+    p->fast_ok = n_fast == n;
+    p->pod_policy = any_pol;
+    p->any_cpu_bind = any_bind;
+    p->h_flags.assign(f, f + n);
+    p->h_req_cpu.assign(hc, hc + n);
+    p->n_stat = ns;
+    p->n_stat_cls = n_stat_cls;
+    p->n_plain = np;
+    p->n_x = nx;
+    p->n_dclass = (uint32_t)classes.size();
     return KG_OK;
 }
 
@@ -1301,19 +1328,13 @@ kg_status kg_pods_destroy(kg_pods* p) {
     if (!p) return KG_INVALID_ARG;
     hipSetDevice(p->ctx->device);
     hipStreamSynchronize(p->ctx->stream);
-    hipFree(p->d_cols);
-    hipFree(p->d_flags);
-    hipFree(p->d_keys);
-    hipFree(p->d_winners);
-    hipFree(p->d_step);
-    hipFree(p->d_partial);
-    hipFree(p->d_gather);
-    for (void* b : {(void*)p->d_dev_req, (void*)p->d_xcols, (void*)p->d_stat_list, (void*)p->d_qst, (void*)p->d_dev_max,
-                    (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout,
-                    (void*)p->d_pcols, (void*)p->d_pflags, (void*)p->d_pmap, (void*)p->d_order, (void*)p->d_xlist, (void*)p->d_tkeys,
-                    (void*)p->d_pstat, (void*)p->d_reason, (void*)p->d_dcls, (void*)p->d_dclass, (void*)p->d_devsum,
-                    (void*)p->d_pairs, (void*)p->d_batch})
+    for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
+                    (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
+                    (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
+                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_pairs, (void*)p->d_batch})
         hipFree(b);
+    hipHostFree(p->h_in);
+    hipHostFree(p->h_keys);
     hipFree(p->d_rbpart);
     hipFree(p->d_rbtops);
     if (p->rexec) hipGraphExecDestroy(p->rexec);
@@ -1525,11 +1546,70 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     return KG_OK;
 }
 
+// Launch description of a matrix-mode select of n_lanes pods (order: the n_fast fast lanes, then the
+// integer-path lanes) whose keys go to out[row][kk] for rows (pod positions) [0, n_rows); *parts = the
+// partial rows it needs (row stride n_rows). F_BIG records are spread over big_y chunks sized for ~2048
+// workgroups from the snapshot's F_BIG count at its last upload (the device list may have grown since:
+// the chunks then just get longer).
+static LaunchSelect make_select(const kg_snap* s, const PodsDev& pods, const uint32_t* order, uint32_t n_lanes,
+                                uint32_t n_fast, uint32_t n_rows, uint32_t kk, bool fast, uint64_t* out,
+                                const uint32_t* pmap, uint32_t* pstat, uint32_t* parts) {
+    LaunchSelect a{};
+    a.nodes = s->d_nodes;
+    a.zones = s->d_zones;
+    a.pods = pods;
+    a.n_pods = n_lanes;
+    a.n_rows = n_rows;
+    a.index_base = s->base;
+    a.k = kk;
+    a.exact = force_exact();
+    a.fast = fast && !a.exact && !force_int() && s->weights_small;
+    a.n_fast = a.fast ? n_fast : 0;
+    a.cfg = s->kcfg;
+    a.pmap = pmap;
+    a.pstat = pstat;
+    a.out = out;
+    a.order = order;
+    a.big_list = s->d_big + 1;
+    a.big_count = s->d_big;
+    a.fused = a.fast && kk == 1 && !unfused();
+    uint32_t np = 0;
+    if (a.n_fast) {
+        const uint32_t bounds[3] = {0, s->n0, s->n};
+        for (int c = 0; c < 2; c++) {
+            SelectRange& r = a.range[c];
+            r.begin = bounds[c];
+            r.end = bounds[c + 1];
+            r.chunk = select_chunk(r.end - r.begin, a.n_fast);  // each class launch fills the chip on its own
+            r.n_chunks = (r.end - r.begin + r.chunk - 1) / r.chunk;
+            r.part0 = np;
+            if (!a.fused) np += r.n_chunks;
+        }
+        const uint32_t pod_blocks = (a.n_fast + 255) / 256;
+        const uint32_t want = std::max<uint32_t>(1, (2048 + pod_blocks - 1) / pod_blocks);
+        a.big_y = std::max<uint32_t>(1, std::min<uint32_t>(want, (s->n_big_est + 7) / 8));
+        a.big_part0 = np;
+        if (!a.fused) np += a.big_y;
+    }
+    const uint32_t n_int = n_lanes - a.n_fast;
+    if (n_int && s->n) {
+        SelectRange& r = a.irange;
+        r.begin = 0;
+        r.end = s->n;
+        r.chunk = select_chunk(s->n, n_int);
+        r.n_chunks = (s->n + r.chunk - 1) / r.chunk;
+        r.part0 = np;
+        if (kk > 1) np += r.n_chunks;  // top-1 of the integer lanes: atomicMax into out
+    }
+    *parts = np;
+    return a;
+}
+
 // config-5 matrix mode, pass 2: totals with the normalised terms -> per-pod top-k in d_out.
 // Split: a plain pod's DeviceShare / Reservation terms are 0 and it passes their filters on every node
 // (eval_pair_ext with dcount == 0, no view, no required affinity), so its keys are exactly the base
-// select's; those pods run the fast k_select over their compacted columns, the others k_ext_select by
-// list. ElasticQuota rejections are applied in the scatter.
+// select's; those pods run the fast select through their lane list (d_pmap) straight into d_out, the
+// others k_ext_select by list. ElasticQuota rejections are applied by the scatters.
 static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out) {
     kg_ctx* ctx = s->ctx;
     const bool split = !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok &&
@@ -1545,39 +1625,10 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         xparts += y2;
     }
     const uint32_t n_plain = split ? p->n_plain : 0;
-    LaunchSelect a{};
     uint32_t fparts = 0;
-    if (n_plain) {
-        a.nodes = s->d_nodes;
-        a.zones = s->d_zones;
-        a.pods = p->plain;
-        a.n_pods = n_plain;
-        const uint32_t bounds[3] = {0, s->n0, s->n};
-        for (int c = 0; c < 2; c++) {
-            SelectRange& r = a.range[c];
-            r.begin = bounds[c];
-            r.end = bounds[c + 1];
-            r.chunk = select_chunk(r.end - r.begin, n_plain);
-            r.n_chunks = (r.end - r.begin + r.chunk - 1) / r.chunk;
-            r.part0 = fparts;
-            fparts += r.n_chunks;
-        }
-        a.index_base = s->base;
-        a.k = kk;
-        a.exact = false;
-        a.fast = true;
-        a.cfg = s->kcfg;
-        a.pmap = p->d_pmap;
-        a.pstat = p->d_pstat;
-        a.fused = kk == 1 && !unfused();
-        if (a.fused) {
-            a.out = p->d_tkeys + p->cap;  // the x sub-batch's merge reuses d_tkeys[0, cap) before the scatters
-            a.big_list = s->d_big + 1;
-            a.big_count = s->d_big;
-        }
-    }
+    LaunchSelect a = make_select(s, p->dev, p->d_pmap, n_plain, n_plain, p->n, kk, true, d_out, nullptr, p->d_pstat, &fparts);
     const size_t xneed = (size_t)xparts * n_x * kk;
-    kg_status st = ensure_partial(p, std::max<size_t>(xneed + (size_t)fparts * n_plain * kk, 1));
+    kg_status st = ensure_partial(p, std::max<size_t>(xneed + (size_t)fparts * p->n * kk, 1));
     if (st != KG_OK) return st;
     a.partial = p->d_partial + xneed;
     hipEvent_t e0, e1;
@@ -1590,11 +1641,11 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         xe.pairs_ld = (p->n_stat - p->n_stat_cls + 63u) & ~63u;
         xe.pairs_row0 = p->n_x - (p->n_stat - p->n_stat_cls);
     }
+    if (n_plain) HIP_TRY(ctx, launch_select(a, ctx->stream));  // zeroes d_out first at k = 1: before the x scatter
     if (n_x)
         HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
                                        s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
                                        p->d_pref, p->d_partial, p->d_pstat, s->d_special, s->special_est(), ctx->stream));
-    if (fparts || a.fused) HIP_TRY(ctx, launch_select(a, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
     if (!split) {
@@ -1603,19 +1654,10 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     }
     if (n_x) {
         HIP_TRY(ctx, launch_merge(p->d_partial, xparts, n_x, kk, p->d_tkeys, ctx->stream));
-        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_xlist, n_x, kk, nullptr, d_out, nullptr, ctx->stream));
+        HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_xlist, n_x, kk, false, nullptr, d_out, nullptr, ctx->stream));
     }
-    if (n_plain) {
-        if (a.fused) {
-            // keys already in d_tkeys (k_big_init + k_select1)
-        } else if (fparts)
-            HIP_TRY(ctx, launch_merge_big(a.partial, fparts, n_plain, kk, s->d_nodes, s->d_zones, p->plain, s->d_big + 1,
-                                          s->d_big, s->base, s->kcfg, p->d_tkeys, p->d_pmap, p->d_pstat, ctx->stream));
-        else
-            HIP_TRY(ctx, hipMemsetAsync(p->d_tkeys, 0, sizeof(uint64_t) * kk * n_plain, ctx->stream));
-        HIP_TRY(ctx, launch_scatter_keys(a.fused ? a.out : p->d_tkeys, p->d_pmap, n_plain, kk, p->d_qst, d_out, p->d_pstat,
-                                         ctx->stream));
-    }
+    if (n_plain)  // the plain keys are in place: apply the ElasticQuota rejections
+        HIP_TRY(ctx, launch_scatter_keys(d_out, p->d_pmap, n_plain, kk, true, p->d_qst, d_out, p->d_pstat, ctx->stream));
     return KG_OK;
 }
 
@@ -1639,48 +1681,7 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
         if (st0 != KG_OK) return st0;
         return ext_select_local(s, p, kk, d_out);
     }
-    LaunchSelect a{};
-    a.nodes = s->d_nodes;
-    a.zones = s->d_zones;
-    a.pods = p->dev;
-    a.n_pods = p->n;
-    uint32_t n_parts = 0;
-    const uint32_t bounds[3] = {0, s->n0, s->n};
-    for (int c = 0; c < 2; c++) {
-        SelectRange& r = a.range[c];
-        r.begin = bounds[c];
-        r.end = bounds[c + 1];
-        r.chunk = select_chunk(r.end - r.begin, p->n);  // each class launch fills the chip on its own
-        r.n_chunks = (r.end - r.begin + r.chunk - 1) / r.chunk;
-        r.part0 = n_parts;
-        n_parts += r.n_chunks;
-    }
-    a.index_base = s->base;
-    a.k = kk;
-    a.exact = force_exact();
-    a.fast = !a.exact && !force_int() && s->weights_small && p->fast_ok;
-    a.cfg = s->kcfg;
-    a.pmap = nullptr;
-    a.pstat = p->d_pstat;
-    a.order = p->d_order;
-    a.fused = a.fast && kk == 1 && !unfused();
-    if (a.fused) {
-        a.out = d_out;
-        a.big_list = s->d_big + 1;
-        a.big_count = s->d_big;
-    }
-    const size_t need = (size_t)std::max<uint32_t>(n_parts, 1) * p->n * kk;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    if (need > p->partial_cap) {
-        if (p->d_partial) {
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-            HIP_TRY(ctx, hipFree(p->d_partial));
-            p->d_partial = nullptr;
-        }
-        HIP_TRY(ctx, hipMalloc(&p->d_partial, sizeof(uint64_t) * need));
-        p->partial_cap = need;
-    }
-    a.partial = p->d_partial;
     p->k_last = k;
     p->kk_last = kk;
     if (p->n == 0) return KG_OK;
@@ -1689,19 +1690,17 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
         HIP_TRY(ctx, hipMemsetAsync(d_out, 0, sizeof(uint64_t) * kk * p->n, ctx->stream));
         return KG_OK;
     }
+    // per pod: fast lanes (float64 fast path + F_BIG records on the integer path), then the integer lanes
+    uint32_t parts = 0;
+    LaunchSelect a = make_select(s, p->dev, p->d_order, p->n, p->n_fast, p->n, kk, true, d_out, nullptr, p->d_pstat, &parts);
+    kg_status st = ensure_partial(p, std::max<size_t>((size_t)parts * p->n * kk, 1));
+    if (st != KG_OK) return st;
+    a.partial = p->d_partial;
     hipEvent_t e0, e1;
-    kg_status st = record_begin(ctx, &e0, &e1);
+    st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, launch_select(a, ctx->stream));
-    st = record_end(ctx, e0, e1);
-    if (st != KG_OK) return st;
-    if (a.fused) return KG_OK;
-    if (a.fast)
-        HIP_TRY(ctx, launch_merge_big(p->d_partial, n_parts, p->n, kk, s->d_nodes, s->d_zones, p->dev, s->d_big + 1,
-                                      s->d_big, s->base, s->kcfg, d_out, nullptr, p->d_pstat, ctx->stream));
-    else
-        HIP_TRY(ctx, launch_merge(p->d_partial, n_parts, p->n, kk, d_out, ctx->stream));
-    return KG_OK;
+    return record_end(ctx, e0, e1);
 }
 
 kg_status kg_eval_select(kg_snap* s, kg_pods* p, uint32_t k) {
@@ -1719,9 +1718,13 @@ kg_status kg_result_keys(kg_pods* p, uint64_t* out) {
     std::lock_guard<std::mutex> g(ctx->mu);
     if (p->k_last == 0) return fail(ctx, KG_INVALID_ARG, "no selection result");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    std::vector<uint64_t> h((size_t)p->kk_last * std::max<uint32_t>(p->n, 1));
-    HIP_TRY(ctx, hipMemcpyAsync(h.data(), p->d_keys, sizeof(uint64_t) * p->kk_last * p->n, hipMemcpyDeviceToHost, ctx->stream));
+    const uint64_t* h = p->h_keys;  // pinned staging
+    HIP_TRY(ctx, hipMemcpyAsync(p->h_keys, p->d_keys, sizeof(uint64_t) * p->kk_last * p->n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (p->k_last == p->kk_last) {
+        std::memcpy(out, h, sizeof(uint64_t) * p->k_last * p->n);
+        return KG_OK;
+    }
     for (uint32_t j = 0; j < p->n; j++)
         for (uint32_t t = 0; t < p->k_last; t++) out[(size_t)j * p->k_last + t] = h[(size_t)j * p->kk_last + t];
     return KG_OK;

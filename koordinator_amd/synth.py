@@ -358,6 +358,67 @@ def cpuset_cluster(n_nodes: int, n_pods: int, seed: int = 0, bind_frac: float = 
     return cfg, t, pt
 
 
+def mixed(n_nodes: int = 10_000, n_pods: int = 10_000, seed: int = 6):
+    """A realistic mixed cluster (bench config 6): config 2's nodes and pods, plus
+    - kubelet topology-manager policies: 20% SingleNUMANode (as config 2), 10% Restricted, 10% BestEffort;
+    - CPU topologies on every node (2 sockets x 1 NUMA node x cores/2 cores x 2 threads, matching the node's
+      cpu allocatable before amplification), existing cpuset allocations as nodes() sets them;
+    - 5% of the nodes (NUMA policy None) with a node CPU bind policy (FullPCPUsOnly / SpreadByPCPUs), where
+      every pod with a cpu request binds cpusets;
+    - 5% LSR pods: prod pods with whole-core cpu requests binding cpusets (Full / Spread, a third required).
+    Restricted / BestEffort nodes and CPU-bind-policy nodes are outside the float64 fast path (F_BIG: the
+    integer path with the general NUMA topology manager / cpuset checks); LSR pods take the integer path on
+    every node."""
+    cfg = bench_profile(numa=True)
+    r = _rng(seed)
+    t = nodes(n_nodes, seed, numa=True, rng=r)
+    n = n_nodes
+    pol = t["numa_policy"].copy()
+    u = r.random(n)
+    none = pol == abi.KG_NUMA_NONE
+    pol[none & (u < 0.125)] = abi.KG_NUMA_RESTRICTED  # 0.8 x 0.125 = 10% of all nodes
+    pol[none & (u >= 0.125) & (u < 0.25)] = abi.KG_NUMA_BEST_EFFORT
+    t["numa_policy"] = pol.astype(np.uint32)
+    # CPU topologies by core count (alloc before amplification: 32 / 64 / 96 cores)
+    cores = np.rint(t["alloc_cpu"] / np.where(t["cpu_amp_ratio"] > 1, t["cpu_amp_ratio"], 1.0) / 1000).astype(np.int64)
+    shapes = {32: 0, 64: 1, 96: 2}
+    topos = [abi.cpu_topo_for_test(2, 1, c // 4, 2) for c in (32, 64, 96)]
+    ti = np.array([shapes.get(int(c), 0) for c in cores], np.int32)
+    alloc = np.zeros((n, 2 * abi.KG_MAX_CPUS), np.uint8)
+    cs = np.zeros(n, np.int64)
+    ncpu = np.array([32, 64, 96])[ti]
+    for i in np.nonzero(t["cpuset_alloc_milli"] > 0)[0]:
+        k = int(min(t["cpuset_alloc_milli"][i] // 1000, ncpu[i] // 2))
+        cpus = r.choice(int(ncpu[i]), size=k, replace=False)
+        alloc[i, cpus] = 1
+        cs[i] = 1000 * k
+    t["cpu_topo"] = ti
+    t["cpu_topos"] = abi.cpu_topos_array(topos)
+    t["cpu_alloc"] = alloc
+    t["cpu_max_ref"] = np.ones(n, np.uint8)
+    t["cpuset_alloc_milli"] = cs
+    nb = np.zeros(n, np.uint8)
+    v = r.random(n)
+    pick = (t["numa_policy"] == abi.KG_NUMA_NONE) & (v < 0.05 / 0.6)  # policy None is 60% of the nodes
+    nb[pick & (r.random(n) < 0.5)] = abi.KG_NODE_CPU_BIND_FULL_PCPUS_ONLY
+    nb[pick & (nb == 0)] = abi.KG_NODE_CPU_BIND_SPREAD_BY_PCPUS
+    t["cpu_bind_policy"] = nb
+    t["cpu_strategy"] = r.integers(0, 2, n).astype(np.uint8)
+    pr = _rng(seed, 1)
+    p = pods(n_pods, seed, rng=pr)
+    m = n_pods
+    bind = (pr.random(m) < 0.05 / 0.7) & ((p["flags"] & abi.KG_POD_PROD) != 0)
+    whole = pr.choice([1, 2, 4, 8], m)
+    p["req_cpu"] = np.where(bind, whole * 1000, p["req_cpu"]).astype(np.int64)
+    p["nz_cpu"] = np.where(bind, whole * 1000, p["nz_cpu"]).astype(np.int64)
+    cpol = pr.integers(1, 3, m).astype(np.uint32)
+    req = pr.random(m) < 1 / 3
+    f = p["flags"].astype(np.uint32)
+    p["flags"] = np.where(bind, f | abi.KG_POD_CPU_BIND | (cpol << abi.KG_POD_CPU_POLICY_SHIFT) |
+                          np.where(req, abi.KG_POD_CPU_REQUIRED, 0).astype(np.uint32), f).astype(np.uint32)
+    return cfg, t, p
+
+
 def small(n_nodes: int, n_pods: int, seed: int = 0, numa: bool = True, scale: float = 1.0) -> tuple:
     """Small synthetic cluster for parity tests."""
     cfg: SchedulerConfig = bench_profile(numa=numa)

@@ -1135,14 +1135,25 @@ static void cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const 
     const uint32_t excl = (p->flags[j] >> KG_POD_CPU_EXCL_SHIFT) & 3u;
     const kg_cpu_topo* t = cpu_topology(&v, i);
     int allocated = 0;
+    uint32_t used = 0; /* usedNUMA: NUMA nodes of the CPUs taken */
     for (int cc = 0; cc < t->n_cpus; cc++) {
         if ((out[cc >> 6] >> (cc & 63)) & 1ull) {
             st->cpu_alloc[i].ref[cc]++;
             st->cpu_alloc[i].excl[cc] = (uint8_t)excl;
+            used |= 1u << t->numa[cc];
         }
         allocated += st->cpu_alloc[i].ref[cc] > 0;
     }
     st->col[C_CPUSET][i] = 1000 * (int64_t)allocated;
+    /* addPodAllocation (node_allocation.go:111-143): the uid joins singleNUMANode of its one NUMA node or
+     * sharedNode of each of several; NUMANodeSharedStatus (:60-68) follows (2 bits per zone < 4) */
+    const int multi = (used & (used - 1)) != 0;
+    for (uint32_t q = 0; q < KG_MAX_ZONES; q++) {
+        if (!((used >> q) & 1u)) continue;
+        const uint32_t s = (st->zone_status[i] >> (2 * q)) & 3u;
+        const uint32_t ns = multi ? 2u : (s == 0u ? 1u : s);
+        st->zone_status[i] = (st->zone_status[i] & ~(3u << (2 * q))) | (ns << (2 * q));
+    }
 }
 
 static void apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,

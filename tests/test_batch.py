@@ -279,6 +279,9 @@ def test_planner_and_batch_scheduler_end_to_end(ctx):
     assert out3.status.code == batch.UNSCHEDULABLE
     assert out3.status.message.startswith("job failed due to job batch schedule failed, assumed ")
     assert f"@{names[5]} failed due to filter pod team/" in out3.status.message
+    # the failing pod's message is set on it and on every later pod of its node (engine.go:212-217)
+    failing = [k for k, st in out3.pod_status.items() if "filter pod" in st.message]
+    assert len(failing) >= 2 and len({out3.pod_status[k].message for k in failing}) == 1
     got2 = gpu_state_cols(snap)
     for k in STATE_COLS:
         assert np.array_equal(got2[k], got[k]), k

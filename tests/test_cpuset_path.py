@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
-from koordinator_amd import abi, synth
+from koordinator_amd import abi, cluster, synth
 
 
 # ---------------------------------------------------------------------------------------------- CPU
@@ -45,6 +45,39 @@ def test_oracle_cpuset_replay_allocations_respect_policies():
         int(sum(pods["req_cpu"][j] // 1000 for j in range(len(node)) if not bind[j] and node[j] >= 0
                 and nodes["cpu_bind_policy"][node[j]] != 0 and nodes["cpu_topo"][node[j]] >= 0
                 and nodes["numa_policy"][node[j]] == abi.KG_NUMA_NONE and pods["req_cpu"][j] > 0))
+
+
+def _cpu_zone(nodes, i):
+    topo = abi.KgCpuTopo.from_buffer_copy(nodes["cpu_topos"][nodes["cpu_topo"][i]].tobytes())
+    return {c: int(topo.numa[c]) for c in range(int(topo.n_cpus))}
+
+
+def test_oracle_cpuset_reserve_updates_zone_status():
+    """A cpuset Reserve puts the pod's uid in singleNUMANode / sharedNode of the NUMA nodes of its CPUs
+    (node_allocation.go:111-143): the oracle's per-zone status after every Reserve equals a host
+    NodeAllocation (cluster.py) fed the same allocations, seeded with the node's existing pods."""
+    cfg, nodes, pods = synth.cpuset_cluster(60, 120, seed=8)
+    nodes["numa_zone_status"] = np.zeros(60, np.uint32)
+    kc = cfg.kg_config()
+    st = oracle_lib.OracleState(kc, nodes)
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    host = {}
+    changed = 0
+    for j in np.flatnonzero((pods["flags"] & abi.KG_POD_CPU_BIND) != 0):
+        ok = np.flatnonzero((ref.status[j] == 0) & (nodes["cpu_topo"] >= 0) & (nodes["numa_policy"] == 0))
+        if not len(ok):
+            continue
+        i = int(ok[j % len(ok)])
+        before = st.table()
+        st.assume(i, pods, int(j))
+        after = st.table()
+        took = np.flatnonzero(after["cpu_alloc"][i, :abi.KG_MAX_CPUS] != before["cpu_alloc"][i, :abi.KG_MAX_CPUS])
+        alloc = host.setdefault(i, cluster.NodeAllocation())
+        alloc.add(f"pod-{j}", cluster._PodAllocation(set(int(c) for c in took), []), _cpu_zone(nodes, i))
+        want = alloc.zone_status(abi.KG_MAX_ZONES)
+        assert after["numa_zone_status"][i] == want, (j, i, after["numa_zone_status"][i], want)
+        changed += int(before["numa_zone_status"][i] != want)
+    assert changed >= 3
 
 
 # ---------------------------------------------------------------------------------------------- GPU
@@ -98,7 +131,7 @@ def test_cpuset_replay(ctx, seed):
     assert not len(bad), (bad[:5], node[bad[:5]], rn[bad[:5]])
     assert np.array_equal(total, rt) and np.array_equal(why, rwhy)
     got, want = snap.read_state(), st.table()
-    for k in ("req_cpu", "req_mem", "num_pods", "nz_cpu", "cpuset_alloc_milli"):
+    for k in ("req_cpu", "req_mem", "num_pods", "nz_cpu", "cpuset_alloc_milli", "numa_zone_status"):
         assert np.array_equal(got[k], want[k]), k
     assert np.array_equal(got["cpu_alloc"], want["cpu_alloc"])
     moved = (got["cpu_alloc"][:, :abi.KG_MAX_CPUS] != nodes["cpu_alloc"][:, :abi.KG_MAX_CPUS]).any(axis=1)
@@ -133,3 +166,42 @@ def test_cpuset_assume_and_forget(ctx):
     assert np.array_equal(got["cpu_alloc"], want["cpu_alloc"])
     assert np.array_equal(got["cpuset_alloc_milli"], want["cpuset_alloc_milli"])
     assert np.array_equal(got["req_cpu"], want["req_cpu"])
+    assert np.array_equal(got["numa_zone_status"], want["numa_zone_status"])
+
+
+@pytest.mark.gpu
+def test_cpuset_then_pod_numa_policy_sees_zone_status(ctx):
+    """A cpuset pod Reserved on a policy-None node marks the zones of its CPUs single / shared; a later pod
+    with its own SingleNUMANode policy on that node (exclusive Required by default) reads the new status in
+    its Filter. Device and oracle agree on the statuses and on the later pods' whole verify matrix."""
+    from koordinator_amd import engine
+    cfg, nodes, pods = synth.cpuset_cluster(120, 96, seed=9)
+    nodes["numa_zone_status"] = np.zeros(120, np.uint32)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    batch = engine.PodBatch(ctx, pods)
+    st = oracle_lib.OracleState(kc, nodes)
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    done = 0
+    for j in np.flatnonzero((pods["flags"] & abi.KG_POD_CPU_BIND) != 0):
+        ok = np.flatnonzero((ref.status[j] == 0) & (nodes["cpu_topo"] >= 0) & (nodes["numa_policy"] == 0))
+        if not len(ok):
+            continue
+        i = int(ok[j % len(ok)])
+        engine.assume(snap, batch, int(j), i)
+        st.assume(i, pods, int(j))
+        done += 1
+    assert done >= 8
+    got, want = snap.read_state(), st.table()
+    assert np.array_equal(got["numa_zone_status"], want["numa_zone_status"])
+    assert (want["numa_zone_status"] != 0).sum() >= 5
+    # later pods: plain (no cpuset) pods carrying their own SingleNUMANode / Restricted policy
+    later = synth.pods(160, 77, scale=2.0)
+    later["numa_policy"] = np.where(np.arange(160) % 2 == 0, abi.KG_NUMA_SINGLE_NODE,
+                                    abi.KG_NUMA_RESTRICTED).astype(np.uint32)
+    lb = engine.PodBatch(ctx, later)
+    gv = engine.eval_verify(snap, lb)
+    rv = oracle_lib.eval_verify(kc, {**nodes, **want}, later)
+    for f in FIELDS:
+        a, b = getattr(gv, f), getattr(rv, f)
+        assert np.array_equal(a, b), f
