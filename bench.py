@@ -40,11 +40,13 @@ VALU_PEAK = SIMD_CYCLES / 2  # the all-f32 ceiling, for reference
 SALU_PEAK = 256 * 2.4e9
 # Algorithmic bytes per (pod, node) eval, SURVEY.md §8d (scan model, node row read once per eval):
 # NodeResourcesFit 120 B + LoadAware 52 B + NodeNUMAResource 4 B + 0.2 x 64 B zone table = 188.8 B.
-B_EVAL = {1: 172.0, 2: 188.8, 4: 188.8,
+B_EVAL = {1: 172.0, 2: 188.8, 4: 188.8, 6: 188.8,
           # config 5: + DeviceShare 384 B x 30% GPU pods + Reservation 4 B node flag (308 B)
           5: 308.0}
 METRIC = "Filter+Score pod-node evals/sec"
 PLUGINS = {1: "+LoadAware", 2: "+LoadAware+NodeNUMAResource", 4: "+LoadAware+NodeNUMAResource",
+           6: "+LoadAware+NodeNUMAResource; mixed: 20% SingleNUMANode, 10% Restricted, 10% BestEffort, 5% CPU-bind-"
+              "policy nodes, 5% LSR cpuset pods",
            5: "+LoadAware+NodeNUMAResource+DeviceShare+Reservation+ElasticQuota"}
 KERNEL_SOURCES = ("kg_eval.h", "kg_ext.h", "kg_kernels.h", "kg_layout.h", "kg_kernels.hip", "kg_ext.hip")
 
@@ -54,10 +56,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=None, choices=[1, 2, 4, 5],
+    ap.add_argument("--config", type=int, default=None, choices=[1, 2, 4, 5, 6],
                     help="2: 10k nodes x 10k pods (default at 1 GPU); 4: 100k nodes split over the GPUs x 10k "
                          "pods (strong scaling, default at N > 1); 5: config 4 + DeviceShare / Reservation / "
-                         "ElasticQuota; 1: the 1k x 500 CPU-harness case")
+                         "ElasticQuota; 1: the 1k x 500 CPU-harness case; 6: config 2 on a mixed cluster "
+                         "(Restricted / BestEffort / CPU-bind-policy nodes, LSR pods: synth.mixed)")
     ap.add_argument("--k", type=int, default=None, help="per-pod top-k (default 3 for config 4, else 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-replay", action="store_true")
@@ -307,6 +310,8 @@ def main():
     quotas = rsv = None
     if config == 5:
         cfg, nodes, pods, quotas, rsv = synth.cluster5(100_000, 10_000)
+    elif config == 6:
+        cfg, nodes, pods = synth.mixed()
     else:
         cfg, nodes, pods = synth.cluster(config)
     all_nodes = nodes
@@ -323,7 +328,8 @@ def main():
         # one 10k-node shard per rank (weak scaling)
         n_local = abi.table_len(nodes)
         if world > 1:
-            nodes = synth.nodes(n_local, config + 10 * rank, numa=(config == 2))
+            nodes = synth.mixed(n_local, 1, seed=6 + 10 * rank)[1] if config == 6 else \
+                synth.nodes(n_local, config + 10 * rank, numa=(config == 2))
         base = rank * n_local
         n_total = n_local * world
     if world > 1:
@@ -381,7 +387,9 @@ def main():
     # the committed PMC passes are per launch of one configuration (profiles/run_profile.sh: 2 and 5)
     pmc = load_pmc({2: "select_pmc.json", 5: "ext_pmc.json"}[config]) if world == 1 and config in (2, 5) else None
     fused = k == 1 and os.environ.get("KG_SELECT_UNFUSED", "0") in ("", "0")
-    base = "k_big_init + k_select1 (fused top-1)" if fused else "k_select"
+    base = "k_big_sel + k_select1 (fused top-1)" if fused else "k_select + k_big_sel + k_merge"
+    if config == 6:
+        base += " + k_select<integer path> (LSR lanes)"
     kname = base if config != 5 else f"k_ext_select + {base} (plain-pod split, one bracket)"
     out = {
         "metric": METRIC,

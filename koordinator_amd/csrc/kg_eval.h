@@ -124,15 +124,17 @@ __device__ __forceinline__ int64_t numa_score(bool most, int64_t w_cpu, int64_t 
 
 // ---- NUMA topology manager for non-cpuset pods: hints (resource_manager.go:529-657) and the
 //      SingleNUMANode / Restricted / BestEffort merge (frameworkext/topologymanager/policy*.go).
-//      Mirrors oracle/kg_oracle.c numa_hints / numa_admit.
+//      Same results as oracle/kg_oracle.c numa_hints / numa_admit, restated for registers: the hint lists
+//      are bitmasks over the mask index k (IterateBitMasks order), the per-mask hint scores (0..100) are
+//      packed 8 bits each, zone-indexed values are read through select chains. No private arrays, so no
+//      scratch memory on the integer path.
 
-__device__ __constant__ const uint8_t NUMA_MASKS[4][15] = {
-    {1},
-    {1, 2, 3},
-    {1, 2, 4, 3, 5, 6, 7},
-    {1, 2, 4, 8, 3, 5, 9, 6, 10, 12, 7, 11, 13, 14, 15},
-};
-__device__ __constant__ const uint8_t NUMA_NMASKS[4] = {1, 3, 7, 15};
+// NUMA masks of IterateBitMasks (pkg/util/bitmask/bitmask.go:206-221) for Z = 1..4 zones, 4 bits per mask index
+constexpr uint64_t NUMA_MASK_NIB[4] = {0x1ull, 0x321ull, 0x7653421ull, 0xfedb7ca69538421ull};
+
+__device__ __forceinline__ uint64_t numa_mask_nib(uint32_t Z) {
+    return Z <= 1 ? NUMA_MASK_NIB[0] : Z == 2 ? NUMA_MASK_NIB[1] : Z == 3 ? NUMA_MASK_NIB[2] : NUMA_MASK_NIB[3];
+}
 
 struct NumaZ {
     uint32_t Z, status;
@@ -152,37 +154,82 @@ __device__ __forceinline__ void numa_load(const ZoneRec* __restrict__ zr, uint32
     }
 }
 
-// tryBestToDistributeEvenly with the position-indexed sort comparator (see the oracle)
-__device__ __forceinline__ bool numa_split(const NumaZ& x, uint32_t mask, const int64_t* req, const bool* has,
-                                           int64_t (&al)[2][MAX_ZONES]) {
-    int nodes[MAX_ZONES], n = 0;
-    for (uint32_t z = 0; z < x.Z; z++)
-        if ((mask >> z) & 1u) nodes[n++] = (int)z;
-    for (int r = 0; r < 2; r++)
-        for (int z = 0; z < MAX_ZONES; z++) al[r][z] = 0;
-    for (int r = 0; r < 2; r++) {
-        if (!has[r]) continue;
-        int s[MAX_ZONES];
-        for (int t = 0; t < n; t++) s[t] = nodes[t];
-        for (int a = 1; a < n; a++)
-            for (int b = a; b > 0 && x.avail[r][b] < x.avail[r][b - 1]; b--) {
-                const int t = s[b];
-                s[b] = s[b - 1];
-                s[b - 1] = t;
-            }
-        int64_t q = req[r];
-        for (int t = 0; t < n; t++) {
-            const int64_t split = q / (n - t);
-            const int64_t av = x.avail[r][s[t]];
-            const int64_t got = av > split ? split : av;
-            if (got != 0) {
-                al[r][s[t]] = got;
-                q -= got;
+__device__ __forceinline__ int64_t sel4(const int64_t (&a)[MAX_ZONES], uint32_t i) {
+    return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+
+// Go's truncating q / d for the split divisor d in 1..4 (constant divisions, no int64 divide loop)
+__device__ __forceinline__ int64_t div_small(int64_t q, uint32_t d) {
+    return d == 1 ? q : d == 2 ? q / 2 : d == 3 ? q / 3 : q / 4;
+}
+
+// tryBestToDistributeEvenly of one resource over the zones of `mask` (resource_manager.go:264-318): the
+// zone order comes from sort.Slice whose less(i, j) reads the availability by the positions i, j rather
+// than by the zone ids being sorted (insertion sort for n <= 12, so the swaps depend only on the
+// availability of zones 0..n-1); each zone in turn takes min(available, remaining / zones left).
+// Returns whether the whole request was placed; AL: the per-zone amounts into al (added).
+template <bool AL>
+__device__ __forceinline__ bool numa_split_r(const NumaZ& x, uint32_t mask, const int64_t (&av)[MAX_ZONES], int64_t req,
+                                             int64_t (&al)[MAX_ZONES]) {
+    uint32_t s = 0, n = 0;  // the mask's zones, ascending, 4 bits per position
+#pragma unroll
+    for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++) {
+        const bool in = z < x.Z && ((mask >> z) & 1u);
+        s |= in ? z << (4 * n) : 0u;
+        n += in ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t a = 1; a < (uint32_t)MAX_ZONES; a++) {
+        bool go = a < n;
+#pragma unroll
+        for (uint32_t b = a; b > 0; b--) {
+            go = go && av[b] < av[b - 1];
+            if (go) {  // swap positions b and b - 1
+                const uint32_t hi = (s >> (4 * b)) & 15u, lo = (s >> (4 * (b - 1))) & 15u;
+                s = (s & ~(0xFFu << (4 * (b - 1)))) | (hi << (4 * (b - 1))) | (lo << (4 * b));
             }
         }
-        if (q != 0) return false;
     }
-    return true;
+    int64_t q = req;
+#pragma unroll
+    for (uint32_t t = 0; t < (uint32_t)MAX_ZONES; t++) {
+        if (t >= n) break;
+        const int64_t split = div_small(q, n - t);
+        const uint32_t zone = (s >> (4 * t)) & 15u;
+        const int64_t a0 = sel4(av, zone);
+        const int64_t got = a0 > split ? split : a0;
+        if constexpr (AL) {
+#pragma unroll
+            for (uint32_t zz = 0; zz < (uint32_t)MAX_ZONES; zz++) al[zz] += (zz == zone) ? got : 0;
+        }
+        q -= got;
+    }
+    return q == 0;
+}
+
+__device__ __forceinline__ int popc(uint32_t x) { return __popc(x); }
+
+// leastRequestedScore with an exact truncating quotient (qdiv), the integer path's arithmetic
+__device__ __forceinline__ int64_t least_req_q(int64_t requested, int64_t capacity) {
+    const int64_t x = capacity - requested;
+    if (capacity == 0 || x < 0) return 0;
+    return qdiv(x * 100, capacity);
+}
+
+// NUMA LeastAllocated / MostAllocated over {cpu, memory} with exact integer quotients
+__device__ __forceinline__ int64_t numa_score_q(bool most, int64_t w_cpu, int64_t w_mem, int64_t alloc_cpu, int64_t req_cpu,
+                                                int64_t alloc_mem, int64_t req_mem) {
+    int64_t sum = 0, wsum = 0;
+    if (alloc_cpu != 0 && w_cpu != 0) {
+        sum += (most ? most_req(req_cpu, alloc_cpu) : least_req_q(req_cpu, alloc_cpu)) * w_cpu;
+        wsum += w_cpu;
+    }
+    if (alloc_mem != 0 && w_mem != 0) {
+        sum += (most ? most_req(req_mem, alloc_mem) : least_req_q(req_mem, alloc_mem)) * w_mem;
+        wsum += w_mem;
+    }
+    if (wsum == 0) return 0;
+    return most ? qdiv(sum, wsum) : wdiv(sum, wsum);
 }
 
 struct NumaHint {
@@ -190,8 +237,6 @@ struct NumaHint {
     bool pref, unsat;
     int64_t score;
 };
-
-__device__ __forceinline__ int popc(uint32_t x) { return __popc(x); }
 
 __device__ __forceinline__ bool numa_excl_ok(uint32_t mask, uint32_t status) {
     if (popc(mask) > 1) {
@@ -203,13 +248,17 @@ __device__ __forceinline__ bool numa_excl_ok(uint32_t mask, uint32_t status) {
     return ((status >> (2 * z)) & 3u) != 2u;
 }
 
-__device__ __forceinline__ void numa_merge_one(uint32_t all, bool excl, uint32_t status, const NumaHint* perm, int np,
-                                               NumaHint& best) {
+// mergePermutation + the bestHint update of mergeFilteredHints (policy.go:98-137,198-260) for a
+// permutation of np = 0, 1 or 2 hints (a, b)
+__device__ __forceinline__ void numa_merge_perm(uint32_t all, bool excl, uint32_t status, int np, const NumaHint& a,
+                                                const NumaHint& b, NumaHint& best) {
     uint32_t merged = all, first = 0;
     bool pref = true, unsat = false;
     int naff = 0, maxc = 0;
-    for (int t = 0; t < np; t++) {
-        const NumaHint& v = perm[t];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        if (t >= np) break;
+        const NumaHint& v = t == 0 ? a : b;
         if (v.mask) {
             if (naff == 0) first = v.mask;
             else if (v.mask != first) pref = false;
@@ -224,9 +273,9 @@ __device__ __forceinline__ void numa_merge_one(uint32_t all, bool excl, uint32_t
     if (popc(merged) == 0) return;
     if (excl && !numa_excl_ok(merged, status)) pref = false;
     int64_t score = 0;
-    for (int t = 0; t < np; t++)
-        if (perm[t].mask && perm[t].mask == merged) score += perm[t].score;
-    NumaHint m{merged, pref, !satisfied, score};
+    if (np >= 1 && a.mask && a.mask == merged) score += a.score;
+    if (np >= 2 && b.mask && b.mask == merged) score += b.score;
+    const NumaHint m{merged, pref, !satisfied, score};
     if (m.pref && !best.pref) {
         best = m;
         return;
@@ -241,72 +290,104 @@ __device__ __forceinline__ void numa_merge_one(uint32_t all, bool excl, uint32_t
     best = m;
 }
 
+constexpr uint32_t NUMA_NIL_K = 15u;  // hint-list bit of the unsatisfied nil hint (filterProvidersHints)
+
+__device__ __forceinline__ NumaHint numa_hint_at(uint64_t nib, uint32_t k, uint32_t pref_bits, uint64_t sc_lo, uint64_t sc_hi) {
+    if (k == NUMA_NIL_K) return NumaHint{0u, false, true, 0};
+    const uint32_t m = (uint32_t)(nib >> (4 * k)) & 15u;
+    const uint64_t sc = k < 8 ? (sc_lo >> (8 * k)) : (sc_hi >> (8 * (k - 8)));
+    return NumaHint{m, ((pref_bits >> k) & 1u) != 0, false, (int64_t)(sc & 0xFFu)};
+}
+
 // Policy merge: 0 = admitted with affinity `mask` (0 = none), else a KG_ST_NUMA_* reason.
 template <bool EXACT>
 __device__ __forceinline__ uint32_t numa_admit(const KCfg& c, const NumaZ& x, const int64_t* req, const bool* has,
                                               uint32_t policy, bool excl, uint32_t& mask_out) {
     const uint32_t Z = x.Z;
-    const uint8_t* masks = NUMA_MASKS[Z - 1];
-    const uint32_t nm = NUMA_NMASKS[Z - 1];
-    uint32_t lack[2] = {0, 0};
-    for (uint32_t z = 0; z < Z; z++)
-        for (int r = 0; r < 2; r++)
-            if (x.avail[r][z] == 0) lack[r] |= 1u << z;
-    int minsize[2] = {(int)Z, (int)Z};
-    uint32_t okm[2] = {0, 0};
-    int64_t score[15];
-    for (uint32_t k = 0; k < nm; k++) {
-        const uint32_t m = masks[k];
-        int64_t T[2] = {0, 0}, A[2] = {0, 0};
-        for (uint32_t z = 0; z < Z; z++)
-            if ((m >> z) & 1u)
-                for (int r = 0; r < 2; r++) {
-                    T[r] += x.tot[r][z];
-                    A[r] += x.avail[r][z];
-                }
-        const int64_t rq0 = (T[0] - A[0] < 0 ? 0 : T[0] - A[0]) + req[0];
-        const int64_t rq1 = (T[1] - A[1] < 0 ? 0 : T[1] - A[1]) + req[1];
-        score[k] = numa_score<true>((c.most & MOST_NUMA_HINT) != 0, c.numa_hint_w_cpu, c.numa_hint_w_mem, T[0], rq0, 0.0,
-                                    T[1], rq1, 0.0);
-        int64_t al[2][MAX_ZONES];
-        if (!numa_split(x, m, req, has, al)) continue;
-        for (int r = 0; r < 2; r++) {
-            if (!has[r] || (m & lack[r])) continue;
-            minsize[r] = min(minsize[r], popc(m));
-            okm[r] |= 1u << k;
-        }
+    const uint64_t nib = numa_mask_nib(Z);
+    const uint32_t nm = (1u << Z) - 1u;
+    uint32_t lack0 = 0, lack1 = 0;
+#pragma unroll
+    for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++) {
+        if (z >= Z) break;
+        lack0 |= x.avail[0][z] == 0 ? 1u << z : 0u;
+        lack1 |= x.avail[1][z] == 0 ? 1u << z : 0u;
     }
-    NumaHint L[2][15];
-    int len[2] = {0, 0}, nl = 0, reasons = 0;
-    for (int r = 0; r < 2; r++) {
-        if (!has[r]) continue;
-        const int li = nl++;
-        for (uint32_t k = 0; k < nm; k++) {
-            if (!((okm[r] >> k) & 1u)) continue;
-            const bool pref = popc(masks[k]) == minsize[r] || policy == KG_NUMA_RESTRICTED;
-            if (policy == KG_NUMA_SINGLE_NODE && !(pref && popc(masks[k]) == 1)) continue;  // filterSingleNumaHints
-            L[li][len[li]++] = NumaHint{masks[k], pref, false, score[k]};
+    uint32_t okm0 = 0, okm1 = 0;
+    int min0 = (int)Z, min1 = (int)Z;
+    uint64_t sc_lo = 0, sc_hi = 0;  // hint score of mask k (0..100), 8 bits each
+    const bool most_hint = (c.most & MOST_NUMA_HINT) != 0;
+    int64_t dummy[MAX_ZONES] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < nm; k++) {
+        const uint32_t m = (uint32_t)(nib >> (4 * k)) & 15u;
+        int64_t T0 = 0, T1 = 0, A0 = 0, A1 = 0;
+#pragma unroll
+        for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++) {
+            const bool in = (m >> z) & 1u;
+            T0 += in ? x.tot[0][z] : 0;
+            T1 += in ? x.tot[1][z] : 0;
+            A0 += in ? x.avail[0][z] : 0;
+            A1 += in ? x.avail[1][z] : 0;
         }
-        if (okm[r] == 0) {
-            reasons++;
-            L[li][len[li]++] = NumaHint{0u, false, true, 0};
-            if (policy == KG_NUMA_SINGLE_NODE) len[li] = 0;  // not preferred: filtered out
+        // numaScorer over requested = SubtractWithNonNegativeResult(total, available) + the pod's request
+        const int64_t sc = numa_score_q(most_hint, c.numa_hint_w_cpu, c.numa_hint_w_mem, T0,
+                                        (T0 - A0 < 0 ? 0 : T0 - A0) + req[0], T1, (T1 - A1 < 0 ? 0 : T1 - A1) + req[1]);
+        if (k < 8) sc_lo |= (uint64_t)(sc & 0xFF) << (8 * k);
+        else sc_hi |= (uint64_t)(sc & 0xFF) << (8 * (k - 8));
+        // tryAllocateFromNode under the mask: every requested resource must be placed
+        bool ok = true;
+        if (has[0]) ok = numa_split_r<false>(x, m, x.avail[0], req[0], dummy);
+        if (ok && has[1]) ok = numa_split_r<false>(x, m, x.avail[1], req[1], dummy);
+        if (!ok) continue;
+        const int pc = popc(m);
+        if (has[0] && !(m & lack0)) {
+            okm0 |= 1u << k;
+            min0 = min(min0, pc);
+        }
+        if (has[1] && !(m & lack1)) {
+            okm1 |= 1u << k;
+            min1 = min(min1, pc);
         }
     }
     mask_out = 0;
-    if (reasons && policy != KG_NUMA_BEST_EFFORT) return KG_ST_NUMA_UNSATISFIED;
+    const bool nil0 = has[0] && okm0 == 0, nil1 = has[1] && okm1 == 0;
+    if ((nil0 || nil1) && policy != KG_NUMA_BEST_EFFORT) return KG_ST_NUMA_UNSATISFIED;
+    // Preferred: the narrowest size, or every hint under Restricted
+    uint32_t pref0 = 0, pref1 = 0;
+    for (uint32_t k = 0; k < nm; k++) {
+        const int pc = popc((uint32_t)(nib >> (4 * k)) & 15u);
+        const bool r = policy == KG_NUMA_RESTRICTED;
+        pref0 |= (pc == min0 || r) ? 1u << k : 0u;
+        pref1 |= (pc == min1 || r) ? 1u << k : 0u;
+    }
+    uint32_t L0 = okm0, L1 = okm1;
+    if (policy == KG_NUMA_SINGLE_NODE) {  // filterSingleNumaHints: preferred single-zone hints (the first Z masks)
+        const uint32_t single = (1u << Z) - 1u;
+        L0 &= pref0 & single;
+        L1 &= pref1 & single;
+    }
+    if (nil0) L0 = 1u << NUMA_NIL_K;
+    if (nil1) L1 = 1u << NUMA_NIL_K;
     const uint32_t all = (1u << Z) - 1u;
     NumaHint best{all, false, false, 0};
+    const NumaHint none{0u, false, false, 0};
+    const int nl = (has[0] ? 1 : 0) + (has[1] ? 1 : 0);
     if (nl == 0) {
-        numa_merge_one(all, excl, x.status, nullptr, 0, best);
+        numa_merge_perm(all, excl, x.status, 0, none, none, best);
     } else if (nl == 1) {
-        for (int a = 0; a < len[0]; a++) numa_merge_one(all, excl, x.status, &L[0][a], 1, best);
+        const uint32_t L = has[0] ? L0 : L1, P = has[0] ? pref0 : pref1;
+        for (uint32_t l = L; l; l &= l - 1u) {
+            const NumaHint h = numa_hint_at(nib, (uint32_t)(__ffs(l) - 1), P, sc_lo, sc_hi);
+            numa_merge_perm(all, excl, x.status, 1, h, none, best);
+        }
     } else {
-        for (int a = 0; a < len[0]; a++)
-            for (int b = 0; b < len[1]; b++) {
-                const NumaHint perm[2] = {L[0][a], L[1][b]};
-                numa_merge_one(all, excl, x.status, perm, 2, best);
+        for (uint32_t la = L0; la; la &= la - 1u) {
+            const NumaHint ha = numa_hint_at(nib, (uint32_t)(__ffs(la) - 1), pref0, sc_lo, sc_hi);
+            for (uint32_t lb = L1; lb; lb &= lb - 1u) {
+                const NumaHint hb = numa_hint_at(nib, (uint32_t)(__ffs(lb) - 1), pref1, sc_lo, sc_hi);
+                numa_merge_perm(all, excl, x.status, 2, ha, hb, best);
             }
+        }
     }
     if (policy == KG_NUMA_BEST_EFFORT) {
         mask_out = best.unsat ? all : best.mask;
@@ -322,10 +403,22 @@ __device__ __forceinline__ int32_t numa_code(uint32_t mask) {
     return popc(mask) == 1 ? (int32_t)(__ffs(mask) - 1) : (int32_t)(0x40u | mask);
 }
 
+// tryBestToDistributeEvenly of the pod's cpu / memory over `mask`: the allocation and a failure bit per
+// resource (bit 0 cpu, bit 1 memory: "Insufficient NUMA <resource>", resource_manager.go:300-309)
+__device__ __forceinline__ uint32_t numa_split(const NumaZ& x, uint32_t mask, const int64_t* req, const bool* has,
+                                               int64_t (&al)[2][MAX_ZONES]) {
+    uint32_t fail = 0;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+#pragma unroll
+        for (int z = 0; z < MAX_ZONES; z++) al[r][z] = 0;
+        if (has[r] && !numa_split_r<true>(x, mask, x.avail[r], req[r], al[r])) fail |= 1u << r;
+    }
+    return fail;
+}
+
 // The topology manager for one (pod, node) pair: hints, policy merge, the allocation's zone code and
-// the NUMA score (score_node when no allocation is made). Returns 0 or KG_ST_* bits. Out of line: its
-// hint tables are private arrays that would otherwise sit in the frame of every kernel inlining
-// eval_pair.
+// the NUMA score (score_node when no allocation is made). Returns 0 or KG_ST_* bits.
 __device__ __forceinline__ uint32_t numa_topology(const KCfg* cp, const ZoneRec* zr, uint32_t Z, int64_t req_cpu,
                                                int64_t req_mem, uint32_t pflags, uint32_t pol, bool excl,
                                                int64_t score_node, int32_t* zone_out, int64_t* score_out) {
@@ -338,22 +431,23 @@ __device__ __forceinline__ uint32_t numa_topology(const KCfg* cp, const ZoneRec*
     const uint32_t st = numa_admit<true>(c, x, req, has, pol, excl, mask);
     if (st) return st;
     int64_t al[2][MAX_ZONES];
-    if (mask && !numa_split(x, mask, req, has, al)) return KG_ST_UNSUPPORTED;  // a BestEffort Reserve that would fail: host path
+    if (mask && numa_split(x, mask, req, has, al)) return KG_ST_UNSUPPORTED;  // a BestEffort Reserve that would fail: host path
     *zone_out = numa_code(mask);
     if (pol == KG_NUMA_BEST_EFFORT || !mask) {
         *score_out = score_node;
         return 0;
     }
     int64_t T[2] = {0, 0}, U[2] = {0, 0};
-    for (uint32_t z = 0; z < Z; z++) {
-        if (al[0][z] == 0 && al[1][z] == 0) continue;
+#pragma unroll
+    for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++) {
+        if (z >= Z || (al[0][z] == 0 && al[1][z] == 0)) continue;
         for (int r = 0; r < 2; r++) {
             T[r] += x.tot[r][z];
             U[r] += x.used[r][z];
         }
     }
-    *score_out = numa_score<true>((c.most & MOST_NUMA) != 0, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + req_cpu, 0.0, T[1],
-                                  U[1] + req_mem, 0.0);
+    *score_out = numa_score_q((c.most & MOST_NUMA) != 0, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + req_cpu, T[1],
+                              U[1] + req_mem);
     return 0;
 }
 
@@ -662,7 +756,7 @@ __device__ __forceinline__ void numa_reserve_split(ZoneRec* zr, uint32_t Z, int6
     const int64_t req[2] = {req_cpu, req_mem};
     const bool has[2] = {(pflags & KG_POD_HAS_CPU) != 0, (pflags & KG_POD_HAS_MEM) != 0};
     int64_t al[2][MAX_ZONES];
-    if (numa_split(x, mask, req, has, al))
+    if (!numa_split(x, mask, req, has, al))
         for (int z = 0; z < MAX_ZONES; z++) {
             zr->cpu_used[z] += al[0][z];
             zr->mem_used[z] += al[1][z];

@@ -149,7 +149,7 @@ static int free_cores(const acc_t* a, int by_node, int filter_full, int filter_e
         in[i] = 1;
         sock_free[t->socket[i]]++;
     }
-    static cores_t g;
+    static _Thread_local cores_t g;
     group_cores(a, in, &g);
     const int ng = by_node ? t->n_nodes : t->n_sockets;
     int* cores_of = (int*)calloc((size_t)ng * MAXC, sizeof(int));
@@ -192,7 +192,7 @@ static int free_cores(const acc_t* a, int by_node, int filter_full, int filter_e
         }
         order[y + 1] = v;
     }
-    static list_t tmp[64];
+    static _Thread_local list_t tmp[64]; /* per thread: the oracle runs on worker threads */
     for (int k = 0; k < n; k++) tmp[k] = out[order[k]];
     for (int k = 0; k < n; k++) out[k] = tmp[k];
     free(cores_of);
@@ -243,7 +243,7 @@ static int free_cpus_grouped(const acc_t* a, int by_node, int filter_excl, list_
         }
         order[y + 1] = v;
     }
-    static list_t tmp[64];
+    static _Thread_local list_t tmp[64]; /* per thread: the oracle runs on worker threads */
     for (int k = 0; k < n; k++) tmp[k] = out[order[k]];
     for (int k = 0; k < n; k++) out[k] = tmp[k];
     return n;
@@ -264,7 +264,7 @@ static void free_cpus(const acc_t* a, int filter_excl, list_t* out) {
     }
     for (int i = 0; i < t->n_cpus; i++)
         if (a->result[i]) colo[t->socket[i]]++;
-    static cores_t g;
+    static _Thread_local cores_t g;
     group_cores(a, in, &g);
     int cores[MAXC], n = 0;
     for (int core = 0; core < t->n_cores; core++)
@@ -326,7 +326,7 @@ static int mask_has(const uint64_t* m, int c) { return (int)((m[c >> 6] >> (c & 
 
 int kgo_take_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t avail[4], const kg_cpu_alloc* allocated,
                   int needed, int bind_policy, int excl_policy, int strategy, uint64_t out[4]) {
-    static acc_t A;
+    static _Thread_local acc_t A;
     acc_t* a = &A;
     memset(a, 0, sizeof(*a));
     memset(out, 0, 4 * sizeof(uint64_t));
@@ -344,7 +344,7 @@ int kgo_take_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t avail[4], co
             if (max_ref > 1 && a->avail[i]) a->ref[i] = allocated->ref[i];
         }
     }
-    static list_t L[64];
+    static _Thread_local list_t L[64];
     if (satisfied(a)) return 0;
     if (a->needed > count_avail(a)) return -1; /* ErrNotEnoughCPUs */
     const int full = bind_policy == KG_CPU_BIND_FULL_PCPUS;
@@ -382,7 +382,7 @@ int kgo_take_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t avail[4], co
                 }
                 L[y + 1] = v;
             }
-            static list_t U[64];
+            static _Thread_local list_t U[64];
             int nu = 0;
             for (int k = 0; k < n && !done; k++) {
                 if (!needs(a, L[k].n)) {
@@ -443,7 +443,7 @@ int kgo_take_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t avail[4], co
         }
     }
     for (int fe = 1; fe >= 0 && !done; fe--) {
-        static list_t F;
+        static _Thread_local list_t F;
         free_cpus(a, fe, &F);
         spread(a, &F);
         for (int k = 0; k < F.n; k++) {

@@ -5,12 +5,14 @@ BASELINE configurations that are evaluated in matrix mode:
   config 2  synth.cluster(2):  10k nodes x 10k pods, NodeResourcesFit + LoadAware + NodeNUMAResource
   config 4  synth.cluster(4):  100k nodes x 10k pods, same plugins
   config 5  synth.cluster5(100_000, 10_000): + DeviceShare, Reservation, ElasticQuota
+  config 6  synth.mixed():     config 2 with Restricted / BestEffort nodes, node CPU bind policies and LSR
+                               (cpuset-binding) pods (bench config 6)
 
 plus a digest of the generated cluster (make_config3_golden.digest), so a generator change is detected
 and the GPU box only compares (tests/test_select_golden.py). Top-1 is the first column (keys are unique:
 the node index sits in the low half). The oracle (oracle/kg_oracle.c kgo_select / kgo_ext_select) is the
 checker; pods are independent in matrix mode, so the batch is cut into pod ranges evaluated on a thread
-pool (ctypes drops the GIL for the call). Usage: python tests/golden/make_select_golden.py [2 4 5]"""
+pool (ctypes drops the GIL for the call). Usage: python tests/golden/make_select_golden.py [2 4 5 6]"""
 import ctypes
 import os
 import sys
@@ -40,6 +42,9 @@ def workload(config: int):
     if config == 5:
         cfg, nodes, pods, quotas, rsv = synth.cluster5(100_000, 10_000)
         return cfg.kg_config(), nodes, pods, quotas, rsv
+    if config == 6:
+        cfg, nodes, pods = synth.mixed()
+        return cfg.kg_config(), nodes, pods, None, None
     cfg, nodes, pods = synth.cluster(config)
     return cfg.kg_config(), nodes, pods, None, None
 
@@ -86,5 +91,5 @@ def load(config: int):
 
 
 if __name__ == "__main__":
-    for c in [int(a) for a in sys.argv[1:]] or [2, 4, 5]:
+    for c in [int(a) for a in sys.argv[1:]] or [2, 4, 5, 6]:
         make(c)
