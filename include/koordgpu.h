@@ -69,6 +69,8 @@ typedef enum kg_status {
     KG_OOM = 3,
     KG_UNSUPPORTED = 4, /* feature not on the device path: caller runs the reference plugin */
     KG_NO_DEVICE = 5,
+    KG_RESERVE_FAILED = 6, /* kg_assume / kg_assume_ext: the pod's Reserve failed (a BestEffort NUMA allocation,
+                            * nodenumaresource/plugin.go:612-623): nothing was applied, the pod stays unscheduled */
 } kg_status;
 
 /* Enabled plugins (kg_config.plugins). */
@@ -127,7 +129,13 @@ typedef enum kg_status {
 #define KG_ST_LA_CPU 0x200u     /* ErrReasonUsageExceedThreshold, cpu                */
 #define KG_ST_LA_MEM 0x400u     /* ErrReasonUsageExceedThreshold, memory             */
 #define KG_ST_LA_AGG 0x800u     /* set with LA_CPU/LA_MEM: "aggregated usage" reason */
-#define KG_ST_LA_MASK 0xFF00u
+#define KG_ST_LA_MASK 0x0F00u
+/* NodeNUMAResource Reserve failures of a BestEffort node (the Filter does not admit there, plugin.go:446-455;
+ * Reserve runs the topology manager, plugin.go:612-623, and the allocation of its best hint,
+ * resource_manager.go:300-309). Reported by kg_replay's out_reason and kg_batch_schedule's status. */
+#define KG_ST_NUMA_INSUF_CPU 0x1000u  /* "Insufficient NUMA cpu"                              */
+#define KG_ST_NUMA_INSUF_MEM 0x2000u  /* "Insufficient NUMA memory"                           */
+#define KG_ST_NUMA_INSUF_NODE 0x4000u /* "node(s) Insufficient NUMA Node resources" (no zones)  */
 #define KG_ST_NUMA_AMP_CPU 0x10000u  /* ErrInsufficientAmplifiedCPU                          */
 #define KG_ST_NUMA_CONFLICT 0x20000u /* ErrNotMatchNUMATopology (UnschedulableAndUnresolvable) */
 #define KG_ST_NUMA_NO_RES 0x40000u   /* "node(s) missing NUMA resources"                      */
@@ -138,7 +146,7 @@ typedef enum kg_status {
 #define KG_ST_NUMA_CPU_BIND 0x400000u /* ErrCPUBindPolicyConflict / ErrSMTAlignmentError / ErrInvalidRequestedCPUs
                                        * (UnschedulableAndUnresolvable, plugin.go:388-418, util.go:131-135) */
 #define KG_ST_NUMA_CPUS 0x800000u     /* ErrNotEnoughCPUs: the required bind policy's CPUs do not cover the pod */
-#define KG_ST_NUMA_MASK 0xFF0000u
+#define KG_ST_NUMA_MASK 0xFF7000u
 #define KG_ST_DEV_INSUFFICIENT 0x01000000u /* "Insufficient gpu devices" (Unschedulable, device_allocator.go:432) */
 #define KG_ST_DEV_NO_DEVICE 0x02000000u    /* no GPU minors on the node's Device (UnschedulableAndUnresolvable,
                                               devicehandler_gpu.go:41-44)                              */
@@ -344,7 +352,8 @@ typedef struct kg_verify_out {
     int64_t* score_numa;  /* NodeNUMAResource score                                         */
     int64_t* total;       /* Σ weight·score, -1 when infeasible                             */
     int8_t* numa_zone;    /* NUMA allocation the Reserve would make: -1 none, 0..3 one zone,
-                             0x40 | zone mask for a split over several zones                 */
+                             0x40 | zone mask for a split over several zones, 0x20 | bits when
+                             the Reserve fails (BestEffort: bits = KG_ST_NUMA_INSUF_* >> 12) */
     int64_t* score_dev;   /* DeviceShare Score before NormalizeScore (0 when infeasible)    */
     int64_t* score_rsv;   /* Reservation Score before NormalizeScore (1000 on the preferred
                              node, reservation/scoring.go:40,191-198; 0 when infeasible)     */
@@ -459,13 +468,15 @@ kg_status kg_result_keys(kg_pods* pods, uint64_t* out_keys /* n_pods * k */);
  *   0                  the keys are the complete Filter/Score/selectHost result. */
 kg_status kg_result_status(kg_pods* pods, uint32_t* out_status);
 /* Sequential scheduling of pods[0..n) one at a time with Assume applied on the device between pods
- * (the reference's one-pod-per-cycle semantics). out_node[i] = global node index or -1.
+ * (the reference's one-pod-per-cycle semantics). out_node[i] = global node index or -1 (no feasible node,
+ * or the selected node's Reserve failed: KG_ST_NUMA_INSUF_* in out_reason).
  * out_reason (may be NULL): per pod, the OR of the KG_ST_* filter status bits over every node of the
  * snapshot as it stood in that pod's cycle (0 when every node passed) — the per-plugin reasons the
  * caller turns into the FitError diagnosis of an unschedulable pod (load_aware.go:48-51,
  * nodenumaresource/plugin.go:54-63). */
 kg_status kg_replay(kg_snap* snap, kg_pods* pods, int32_t* out_node, int64_t* out_total, uint32_t* out_reason);
-/* Reserve/Unreserve of pod `pod` (batch index) on local node `node`. */
+/* Reserve/Unreserve of pod `pod` (batch index) on local node `node`. KG_RESERVE_FAILED: the NodeNUMAResource
+ * Reserve fails on that node (BestEffort allocation), nothing applied. */
 kg_status kg_assume(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node);
 kg_status kg_forget(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t numa_zone);
 /* Reserve with every enabled plugin's state (NodeInfo, LoadAware, NUMA zone, DeviceShare minors via

@@ -21,7 +21,7 @@ KG_DEV_CORE, KG_DEV_RATIO, KG_DEV_MEM = 0, 1, 2
 KG_QUOTA_R = 4
 KG_RSV_R = 5
 
-KG_OK, KG_INVALID_ARG, KG_DEVICE_ERROR, KG_OOM, KG_UNSUPPORTED, KG_NO_DEVICE = range(6)
+KG_OK, KG_INVALID_ARG, KG_DEVICE_ERROR, KG_OOM, KG_UNSUPPORTED, KG_NO_DEVICE, KG_RESERVE_FAILED = range(7)
 
 KG_PLUGIN_NRF = 0x1
 KG_PLUGIN_LA = 0x2
@@ -68,7 +68,12 @@ KG_ST_LA_EXPIRED = 0x100
 KG_ST_LA_CPU = 0x200
 KG_ST_LA_MEM = 0x400
 KG_ST_LA_AGG = 0x800
-KG_ST_LA_MASK = 0xFF00
+KG_ST_LA_MASK = 0x0F00
+KG_ST_NUMA_INSUF_CPU = 0x1000   # BestEffort Reserve: "Insufficient NUMA cpu"
+KG_ST_NUMA_INSUF_MEM = 0x2000   # "Insufficient NUMA memory"
+KG_ST_NUMA_INSUF_NODE = 0x4000  # "node(s) Insufficient NUMA Node resources"
+KG_ST_NUMA_RESERVE = KG_ST_NUMA_INSUF_CPU | KG_ST_NUMA_INSUF_MEM | KG_ST_NUMA_INSUF_NODE
+ZONE_RESERVE_FAIL = 0x20        # numa_zone code | (KG_ST_NUMA_INSUF_* >> 12): the pair's Reserve fails
 KG_ST_NUMA_AMP_CPU = 0x10000
 KG_ST_NUMA_CONFLICT = 0x20000
 KG_ST_NUMA_NO_RES = 0x40000
@@ -77,7 +82,7 @@ KG_ST_NUMA_UNSATISFIED = 0x100000
 KG_ST_NUMA_CPU_TOPO = 0x200000
 KG_ST_NUMA_CPU_BIND = 0x400000
 KG_ST_NUMA_CPUS = 0x800000
-KG_ST_NUMA_MASK = 0xFF0000
+KG_ST_NUMA_MASK = 0xFF7000
 KG_ST_DEV_INSUFFICIENT = 0x01000000
 KG_ST_DEV_NO_DEVICE = 0x02000000
 KG_ST_DEV_MASK = 0x03000000

@@ -37,6 +37,7 @@ SKIP = "Skip"
 # batch/engine.go:55-68, batch_scheduler.go:96-101, network_topology_workflow.go:37-38
 ERR_PRE_FILTER_FAILED = "pre-filter failed for pod {ns}/{name}/{uid}, {msg}"
 ERR_FILTER_POD_FAILED = "filter pod {ns}/{name}/{uid} on node {node} failed, err: {msg}"
+ERR_RESERVE_POD_FAILED = "reserve pod {ns}/{name}/{uid} on node {node} failed, err: {msg}"
 ERR_PLAN_MISSING_NODE = "batch schedule plan missing node for pod {key}"
 ERR_NO_PENDING_PODS = "no pending pods"
 JOB_SCHEDULE_FAILED = "job batch schedule failed"
@@ -182,7 +183,7 @@ class BatchScheduler:
         pod_status: Dict[str, Status] = {}
         assumed: Dict[str, Tuple[str, int, int]] = {}
         n_assumed, failed = 0, []
-        node_msg: Dict[str, str] = {}  # the failing pod's message, set on it and every later pod of its node
+        node_msg: Dict[str, Tuple[int, str]] = {}  # the failing pod's status, set on it and every later pod of its node
         for t, (node_name, p) in enumerate(batch):
             r = int(res[t])
             if r in (abi.KG_BATCH_ASSUMED, abi.KG_BATCH_ROLLED_BACK):
@@ -192,10 +193,16 @@ class BatchScheduler:
                     assumed[p.key] = (node_name, int(zone[t]), int(minors[t]))
             elif r in (abi.KG_BATCH_FAILED, abi.KG_BATCH_SIBLING):
                 bits = int(stat[t])
+                code = UNSCHEDULABLE
                 if r == abi.KG_BATCH_SIBLING and node_name in node_msg:
                     # engine.go:188-219: errMsg is formatted once, from the pod that failed, and set on
                     # every pod k >= j of the node group
-                    msg = node_msg[node_name]
+                    code, msg = node_msg[node_name]
+                elif bits & abi.KG_ST_NUMA_RESERVE:
+                    code = ERROR  # fwktype.Error (engine.go:278-280)  # Filter passed, the NodeNUMAResource Reserve failed (engine.go:275-283)
+                    msg = ERR_RESERVE_POD_FAILED.format(ns=p.namespace, name=p.name, uid=p.uid, node=node_name,
+                                                       msg=", ".join(reasons.plugin_reasons(bits & abi.KG_ST_NUMA_RESERVE)
+                                                                     ["NodeNUMAResource"]))
                 elif bits & abi.KG_ST_QUOTA:  # the ElasticQuota gate runs in PreFilter
                     msg = ERR_PRE_FILTER_FAILED.format(ns=p.namespace, name=p.name, uid=p.uid,
                                                       msg=reasons.plugin_reasons(bits)["ElasticQuota"][0])
@@ -203,8 +210,8 @@ class BatchScheduler:
                     msg = ERR_FILTER_POD_FAILED.format(ns=p.namespace, name=p.name, uid=p.uid, node=node_name,
                                                       msg=filter_message(bits))
                 if r == abi.KG_BATCH_FAILED:
-                    node_msg[node_name] = msg
-                pod_status[p.key] = Status(UNSCHEDULABLE, msg)
+                    node_msg[node_name] = (code, msg)
+                pod_status[p.key] = Status(code, msg)
                 failed.append((p.key, node_name))
         if not failed:
             return JobOutcome(Status(SUCCESS), pod_status, assumed)

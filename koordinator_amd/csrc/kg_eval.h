@@ -490,7 +490,27 @@ struct PairOut {
 // SingleNUMANode pair without a fitting zone just needs some failure bit (the reason is unused).
 // SCORE = false: the filter outcome only (status bits; scores and zone choice by score not computed),
 // for the config-5 statistics pass.
-template <bool EXACT, bool OV = false, bool TOPO = true, bool SCORE = true>
+// The Reserve of a BestEffort node (plugin.go:612-623): FilterByNUMANode under BestEffort (the merge always
+// admits) and the allocation of its best hint; the zone code of the allocation, or ZONE_RESERVE_FAIL | bits
+// when the topology hints fail ("node(s) Insufficient NUMA Node resources", no zones) or the allocation does
+// ("Insufficient NUMA <resource>", resource_manager.go:300-309).
+__device__ __forceinline__ int32_t numa_reserve_best_effort(const KCfg& c, const ZoneRec* zr, uint32_t Z, const PodV& p,
+                                                            bool excl) {
+    if (Z == 0) return ZONE_RESERVE_FAIL | (int32_t)(KG_ST_NUMA_INSUF_NODE >> 12);
+    NumaZ x;
+    numa_load(zr, Z, x);
+    const int64_t req[2] = {p.req_cpu, p.req_mem};
+    const bool has[2] = {(p.flags & KG_POD_HAS_CPU) != 0, (p.flags & KG_POD_HAS_MEM) != 0};
+    uint32_t mask = 0;
+    numa_admit<true>(c, x, req, has, KG_NUMA_BEST_EFFORT, excl, mask);
+    int64_t al[2][MAX_ZONES];
+    const uint32_t fail = mask ? numa_split(x, mask, req, has, al) : 0u;
+    return fail ? ZONE_RESERVE_FAIL | (int32_t)fail : numa_code(mask);
+}
+
+// ZONE = false (select kernels): the pair's Reserve zone is not needed, so a BestEffort node skips its
+// topology manager entirely (the Filter / Score do not depend on it).
+template <bool EXACT, bool OV = false, bool TOPO = true, bool SCORE = true, bool ZONE = true>
 __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restrict__ n, const ZoneRec* __restrict__ zr,
                                           const PodV& p, uint32_t flags, PairOut& o, const Over* ov = nullptr) {
     if (p.flags & KG_POD_NUMA_SKIP) return;
@@ -562,14 +582,23 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
     const bool most = (c.most & MOST_NUMA) != 0;
     // pods with their own NUMA policy default to the Required exclusive policy (plugin.go:449-454)
     const bool excl = pod_pol != KG_NUMA_NONE;
-    if (pol == KG_NUMA_RESTRICTED || pol == KG_NUMA_BEST_EFFORT || (pol == KG_NUMA_SINGLE_NODE && excl)) {
+    if (pol == KG_NUMA_BEST_EFFORT) {
+        // no FilterByNUMANode under BestEffort (plugin.go:446-455); Score without an allocation: node
+        // allocatable / requested as they are (scoring.go:184-189); the Reserve's zone from the topology manager
+        if constexpr (SCORE)
+            o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
+                                         rcp_cpu, n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
+        if constexpr (ZONE && TOPO) o.zone = numa_reserve_best_effort(c, zr, (flags >> F_NUMA_ZONES_SHIFT) & 15u, p, excl);
+        return;
+    }
+    if (pol == KG_NUMA_RESTRICTED || (pol == KG_NUMA_SINGLE_NODE && excl)) {
         if constexpr (!TOPO) {
             o.status |= KG_ST_UNSUPPORTED;  // unreachable under the host's TOPO selection
             return;
         }
         const uint32_t Z = (flags >> F_NUMA_ZONES_SHIFT) & 15u;
         if (Z == 0) {
-            o.status |= pol == KG_NUMA_BEST_EFFORT ? KG_ST_UNSUPPORTED : KG_ST_NUMA_NO_RES;
+            o.status |= KG_ST_NUMA_NO_RES;
             return;
         }
         const int64_t score_node = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU],
@@ -648,7 +677,7 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
                                  n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
 }
 
-template <bool EXACT, bool OV = false, bool TOPO = true, bool SCORE = true>
+template <bool EXACT, bool OV = false, bool TOPO = true, bool SCORE = true, bool ZONE = true>
 __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __restrict__ n,
                                              const ZoneRec* __restrict__ zr, const PodV& p, const Over* ov = nullptr) {
     PairOut o;
@@ -732,7 +761,7 @@ __device__ __forceinline__ PairOut eval_pair(const KCfg& c, const int64_t* __res
         }
     }
 
-    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT, OV, TOPO, SCORE>(c, n, zr, p, flags, o, ov);
+    if (c.plugins & KG_PLUGIN_NUMA) numa_eval<EXACT, OV, TOPO, SCORE, ZONE>(c, n, zr, p, flags, o, ov);
     if (o.status & (KG_ST_NUMA_MASK | KG_ST_UNSUPPORTED)) o.s_numa = 0;
     if (o.status) o.zone = -1;
     return o;

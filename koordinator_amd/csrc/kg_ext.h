@@ -99,9 +99,15 @@ __device__ __forceinline__ uint32_t dev_eval_sum(const KCfg& c, const int64_t* _
     if (cls >= (uint32_t)DEV_CLASSES) return dev_eval(c, n, d, x, raw);
     const uint32_t fit = (uint32_t)(ds->fit >> (4u * cls)) & 15u;
     if (fit < x.dcount) return KG_ST_DEV_INSUFFICIENT;
+    raw = ds->score[cls];  // k_dev_sum: dev_sum_score of the class
+    return 0;
+}
+
+// The node Score of one GPU instance of a class from the record's minor sums (dev_eval's arithmetic).
+__device__ __forceinline__ int64_t dev_sum_score(const KCfg& c, const DevSum* __restrict__ ds, const PodX& x) {
+    int64_t raw = 0;
     if (c.most & MOST_DEV) {
-        raw = dev_least(c, ds->T, ds->F, x.dreq);
-        return 0;
+        return dev_least(c, ds->T, ds->F, x.dreq);
     }
     int64_t score = 0, wsum = 0;
 #pragma unroll
@@ -113,7 +119,7 @@ __device__ __forceinline__ uint32_t dev_eval_sum(const KCfg& c, const int64_t* _
         wsum += w;
     }
     raw = wdiv(score, wsum);
-    return 0;
+    return raw;
 }
 
 // DeviceShare Score on a restore table (AutopilotAllocator.score, device_allocator.go:486-508): a table

@@ -43,7 +43,7 @@ __device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) {
 // DevSum of every record for the pod batch's GPU request classes (one thread per record).
 __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nodes, const DevRec* __restrict__ devs,
                                                  uint32_t n_nodes, const DevClass* __restrict__ cls, uint32_t n_cls,
-                                                 DevSum* __restrict__ out) {
+                                                 KCfg cfg, DevSum* __restrict__ out) {
     const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
     if (rec >= n_nodes) return;
     const DevRec& d = devs[rec];
@@ -70,6 +70,13 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
             fit += dev_minor_fits(fr, x) ? 1u : 0u;
         }
         o.fit |= fit << (4u * k);
+    }
+    for (uint32_t k = 0; k < 16u; k++) o.score[k] = 0;
+    for (uint32_t k = 0; k < n_cls; k++) {  // the node Score per class (every pair of the class reads it)
+        PodX x{};
+        x.dkeys = cls[k].dkeys;
+        for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
+        o.score[k] = (uint8_t)dev_sum_score(cfg, &o, x);
     }
     out[rec] = o;
 }
@@ -485,7 +492,7 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
                                                    const uint32_t* __restrict__ step_base, uint32_t step_off,
                                                    uint64_t* __restrict__ winners, uint32_t* __restrict__ minors,
                                                    uint64_t* __restrict__ buckets, int8_t* __restrict__ zsel,
-                                                   uint32_t* __restrict__ reason) {
+                                                   uint32_t* __restrict__ reason, const uint32_t* __restrict__ pos) {
     const uint32_t step = (step_base ? *step_base : 0u) + step_off;
     if (step > n_pods) return;  // uniform
     const uint32_t lane = threadIdx.x;
@@ -509,6 +516,17 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
             prev = wmax_u64(c0 > c1 ? c0 : c1);
         }
     }
+    // the winner's Reserve fails (BestEffort NUMA allocation: zone code of its pair): the pod stays unscheduled.
+    // zsel is double-buffered by step parity: every block reads the previous step's codes while this step's
+    // are written
+    int32_t prev_zone = -1;
+    if (prev != 0ull) {
+        prev_zone = zsel[(size_t)((step - 1) & 1u) * n_nodes + pos[(0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull)) - index_base]];
+        if (zone_reserve_fails(prev_zone)) {
+            if (blockIdx.x == 0 && lane == 0 && reason) atomicOr(reason + step - 1, zone_fail_status(prev_zone));
+            prev = 0ull;
+        }
+    }
     if (blockIdx.x == 0) {
         uint64_t* Z = buckets + (size_t)((step + 1) % 3) * 128;  // last read at step - 1
         Z[lane] = 0;
@@ -521,7 +539,7 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
         if (g == index_base + node_index(nodes[i])) {
             const PodV q = load_pod(pods, step - 1);
             const PodX qx = load_podx(pods, step - 1);
-            apply_assume(cfg, nodes[i].v, zones + i, q, zsel[i], 1);
+            apply_assume(cfg, nodes[i].v, zones + i, q, prev_zone, 1);
             if ((cfg.plugins & KG_PLUGIN_DEV) && qx.dcount > 0) {
                 const uint32_t mask = dev_choose(cfg, nodes[i].v, devs + i, qx);
                 dev_apply(devs + i, mask, qx, 1);
@@ -566,7 +584,7 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
     uint32_t stat = 0;
     if (live) {
         const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, qst);
-        zsel[i] = (int8_t)r.zone;
+        zsel[(size_t)(step & 1u) * n_nodes + i] = (int8_t)r.zone;
         stat = r.status;
         if (!r.status) {
             const int64_t base = (int64_t)cfg.w_nrf * r.s_nrf + (int64_t)cfg.w_la * r.s_la + (int64_t)cfg.w_numa * r.s_numa;
@@ -608,6 +626,13 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     if (sign > 0) {
         const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, 0u);
         zone = r.status ? -1 : r.zone;
+        if (zone_reserve_fails(zone)) {  // the NodeNUMAResource Reserve fails: nothing is applied
+            if (out) {
+                out[0] = zone;
+                out[1] = 0;
+            }
+            return;
+        }
         mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, n, devs + rec, qx) : 0u;
     }
     apply_assume(cfg, n, zones + rec, q, zone, sign);
@@ -671,6 +696,7 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
                 st = r.status;
                 zone = r.zone;
             }
+            if (!st && zone_reserve_fails(zone)) st = zone_fail_status(zone);  // Reserve fails (engine.go:270-280)
             if (st) {
                 failed = st;
                 result[j] = KG_BATCH_FAILED;
@@ -770,9 +796,10 @@ hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t 
 }
 
 hipError_t launch_dev_sum(const NodeRec* nodes, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
+                          const KCfg& cfg,
                           DevSum* out, hipStream_t s) {
     if (n_nodes == 0) return hipSuccess;
-    k_dev_sum<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, devs, n_nodes, cls, n_cls, out);
+    k_dev_sum<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, devs, n_nodes, cls, n_cls, cfg, out);
     return hipGetLastError();
 }
 
@@ -847,14 +874,14 @@ hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const E
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
-                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, hipStream_t s) {
+                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, hipStream_t s) {
     dim3 grid((n_nodes + 63) / 64), block(64);
     if (exact)
         k_ext_replay<true><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                  step_off, winners, minors, buckets, zsel, reason);
+                                                  step_off, winners, minors, buckets, zsel, reason, pos);
     else
         k_ext_replay<false><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                   step_off, winners, minors, buckets, zsel, reason);
+                                                   step_off, winners, minors, buckets, zsel, reason, pos);
     return hipGetLastError();
 }
 

@@ -113,7 +113,7 @@ hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
-                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, hipStream_t s);
+                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, hipStream_t s);
 hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                              uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
                              bool exact, int32_t* out, hipStream_t s);
@@ -147,6 +147,7 @@ inline void ext_part2_grid(uint32_t special_est, uint32_t pod_blocks, uint32_t* 
 }
 hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, hipStream_t s);
 hipError_t launch_dev_sum(const NodeRec* nodes, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
+                          const KCfg& cfg,
                           DevSum* out, hipStream_t s);
 hipError_t launch_scatter_rows(const void* stage, const uint32_t* pos, uint32_t n, bool dev, NodeRec* nodes,
                                ZoneRec* zones, DevRec* devs, hipStream_t s);

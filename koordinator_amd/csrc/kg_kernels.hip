@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
             select_fast_loop<K, PM, CLS, FK_ANY>(nodes, zones, lo, hi, index_base, cv, pf, top);
     } else {
         for (uint32_t i = lo; i < hi; i++) {
-            const PairOut o = eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p);
+            const PairOut o = eval_pair<EXACT, false, true, true, false>(cfg, nodes[i].v, zones + i, p);
             unsup |= o.status & KG_ST_UNSUPPORTED;
             topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
         }
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void k_big_sel(const NodeRec* __restrict__ nod
         const PodV p = load_pod(pods, row);
         for (uint32_t b = lo; b < hi; b++) {
             const uint32_t i = big_list[b];
-            const PairOut o = eval_pair<false>(cfg, nodes[i].v, zones + i, p);
+            const PairOut o = eval_pair<false, false, true, true, false>(cfg, nodes[i].v, zones + i, p);
             unsup |= o.status & KG_ST_UNSUPPORTED;
             topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
         }
@@ -309,7 +309,15 @@ __global__ __launch_bounds__(64) void k_replay(NodeRec* __restrict__ nodes, Zone
     const PodV p = load_pod(pods, has_next ? step : 0);
     if (live && prev != 0ull) {
         const uint32_t g = 0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull);
-        if (g == rec_gidx(nodes[i], index_base)) apply_assume(cfg, nodes[i].v, zones + i, q, zsel[i], 1);
+        if (g == rec_gidx(nodes[i], index_base)) {
+            const int32_t z = zsel[i];
+            if (zone_reserve_fails(z)) {  // the Reserve fails (BestEffort allocation): the pod stays unscheduled
+                winners[step - 1] = 0ull;
+                if (reason) atomicOr(reason + step - 1, zone_fail_status(z));
+            } else {
+                apply_assume(cfg, nodes[i].v, zones + i, q, z, 1);
+            }
+        }
     }
     if (!has_next) return;  // uniform: the final step only applies the last Assume
     uint64_t key = 0;
@@ -343,7 +351,7 @@ __global__ void k_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zone
         const PairOut o = eval_pair<EXACT>(cfg, n, zones + node, q);
         zone = o.zone;
     }
-    apply_assume(cfg, n, zones + node, q, zone, sign);
+    if (!zone_reserve_fails(zone)) apply_assume(cfg, n, zones + node, q, zone, sign);  // else nothing is applied
     if (zone_out) *zone_out = zone;
 }
 
@@ -361,7 +369,7 @@ __global__ void k_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zone
 // integer path's (records flagged F_BIG are rare).
 template <bool EXACT>
 __device__ __forceinline__ uint64_t int_key(const KCfg& cfg, const int64_t* n, const ZoneRec* zr, const PodV& p, uint32_t g) {
-    return pair_key(cfg, eval_pair<EXACT>(cfg, n, zr, p), g);
+    return pair_key(cfg, eval_pair<EXACT, false, true, true, false>(cfg, n, zr, p), g);
 }
 
 // Pass 1: per-(chunk, pod) top-RB_K over node records [begin, end); lane = pod of the window. Each
@@ -408,7 +416,8 @@ __global__ __launch_bounds__(64) void k_rb_top(const NodeRec* __restrict__ nodes
         }
     } else {
         for (uint32_t i = lo; i < hi; i++) {
-            const uint64_t key = pair_key(cfg, eval_pair<EXACT>(cfg, nodes[i].v, zones + i, p), rec_gidx(nodes[i], index_base));
+            const uint64_t key = pair_key(cfg, eval_pair<EXACT, false, true, true, false>(cfg, nodes[i].v, zones + i, p),
+                                          rec_gidx(nodes[i], index_base));
             if (key > top[RB_K - 1]) topk_insert<RB_K>(top, key);
         }
     }
@@ -577,7 +586,7 @@ __device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& 
         zv[5] = x100(tm - um);
     }
     const uint32_t pol0 = (f0 >> F_NUMA_POLICY_SHIFT) & 15u;
-    const bool pol_host = pol0 == 1u /* KG_NUMA_BEST_EFFORT */ || pol0 == 2u /* KG_NUMA_RESTRICTED */;
+    const bool pol_host = pol0 == 2u /* KG_NUMA_RESTRICTED */;
     const bool big_all = (__ballot(big) != 0ull) || pol_host || ((meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
     const uint32_t f = f0 | (full ? (uint32_t)F_PODS_FULL : 0u) | (big_all ? (uint32_t)F_BIG : 0u);
     // derived slot dl.dst of this lane (lanes < N_DER)
@@ -601,8 +610,8 @@ __device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& 
         const int64_t req_f = (vb >= cs && cs > 0) ? vb - cs + acs : vb;
         const int64_t d = va - req_f;
         val = pol_host ? always_fail : amp ? kg_bits(x100(d < 0 ? 0 : d)) : never_fail;
-    } else {
-        val = kg_bits(amp ? x100(va - vb) : 0.0);
+    } else {  // DER_AMP_DELTA: 0 on BestEffort nodes (node-level score without amplification)
+        val = kg_bits((amp && pol0 != 1u) ? x100(va - vb) : 0.0);
     }
     // writes
     if (lane < (uint32_t)N_INT_SLOTS && add) v[lane] = nv;
@@ -676,7 +685,7 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
     auto eval_slot = [&](uint32_t s, int32_t* zone) -> uint64_t {
         const uint32_t f = (uint32_t)snode[s].v[N_FLAGS];
         const uint32_t g = index_base + node_index(snode[s]);
-        if (FAST && !(f & F_BIG)) {
+        if (FAST && !(f & (F_BIG | F_TOPO))) {
             const FastRec& r = *reinterpret_cast<const FastRec*>(&snode[s].v[FAST_BEGIN]);
             *zone = -1;
             if (node_class(snode[s]) == 1) return eval_fast_key<7u, 1>(cv, r, &szone[s], mpf, g, zone);
@@ -734,30 +743,36 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
         const uint64_t best_c = wave_max_key(kc);
         const uint64_t best = best_c > cand_key ? best_c : cand_key;
         last = 0xFFFFFFFFu;
+        uint64_t placed = best;
         if (best != 0ull) {
             uint32_t slot;
             int32_t zone;
-            if (best == cand_key) {  // the candidate wins: it joins C in slot nc
+            if (best == cand_key) {  // the candidate wins: it joins C in slot nc (unless its Reserve fails)
                 slot = nc;
                 put(slot, lane, cpre0);
                 if (lane + 64u < NQ) put(slot, lane + 64u, cpre1);
-                if (lane == 0) {
-                    crec[slot] = cand;
-                    changed[cand >> 5] |= 1u << (cand & 31u);
-                }
                 wave_lds_sync();
-                // pod t's zone on the candidate (class-0 rows on the fast path never allocate one)
+                // pod t's zone on the candidate (class-0 rows on the fast path never allocate one; BestEffort
+                // rows take the integer path for their Reserve's zone)
                 const uint32_t cf = (uint32_t)snode[slot].v[N_FLAGS];
                 int32_t z = -1;
-                if (!(FAST && !(cf & F_BIG) && node_class(snode[slot]) == 0) && lane == t) eval_slot(slot, &z);
+                if (!(FAST && !(cf & (F_BIG | F_TOPO)) && node_class(snode[slot]) == 0) && lane == t) eval_slot(slot, &z);
                 zone = __shfl(z, (int)t, 64);
-                last = cand;
-                nc++;
+                if (!zone_reserve_fails(zone)) {
+                    if (lane == 0) {
+                        crec[slot] = cand;
+                        changed[cand >> 5] |= 1u << (cand & 31u);
+                    }
+                    last = cand;
+                    nc++;
+                }
             } else {
                 slot = (uint32_t)(__ffsll((long long)__ballot(lane < nc && kc == best)) - 1);
                 zone = czone[slot][t];
             }
-            if (zone >= 0x40) {  // multi-zone NUMA split: one lane (lane t holds pod t)
+            if (zone_reserve_fails(zone)) {
+                placed = 0ull;  // the Reserve fails (BestEffort allocation): nothing changes, the pod stays unscheduled
+            } else if (zone >= 0x40) {  // multi-zone NUMA split: one lane (lane t holds pod t)
                 if (lane == t) apply_assume(cfg, snode[slot].v, &szone[slot], mp, zone, 1);
             } else {
                 PodV pt;
@@ -775,13 +790,13 @@ __global__ __launch_bounds__(64) void k_rb_fix(NodeRec* __restrict__ nodes, Zone
             }
             wave_lds_sync();
             // later pods of the window on the changed row
-            if (lane > t && live) {
+            if (placed && lane > t && live) {
                 int32_t z = -1;
                 ckey[slot][lane] = eval_slot(slot, &z);
                 czone[slot][lane] = (int8_t)z;
             }
         }
-        if (lane == 0) winners[j] = best;
+        if (lane == 0) winners[j] = placed;
         wave_lds_sync();
         done = t + 1;
     }

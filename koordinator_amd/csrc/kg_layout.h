@@ -98,6 +98,8 @@ enum : uint32_t {
     F_AMP = 1u << 16,          // cpu amplification ratio > 1
     F_PODS_FULL = 1u << 17,    // len(Pods) + 1 > AllowedPodNumber (derived)
     F_BIG = 1u << 18,          // some value is outside the exact float64 fast path (derived)
+    F_TOPO = 1u << 19,         // BestEffort node: Filter / Score like policy None, the Reserve runs the topology
+                               // manager (window replay takes the integer path for the Reserve's zone)
     F_DERIVED_MASK = F_PODS_FULL | F_BIG,
 };
 enum : uint32_t { FMODE_CHECK = 0, FMODE_PASS = 1, FMODE_FAIL_EXPIRED = 2 };
@@ -177,6 +179,11 @@ KG_HD inline uint32_t cpuset_zone_status(uint32_t status, uint32_t used) {
     return status;
 }
 
+// Zone code of a pair whose Reserve fails (BestEffort allocation): 0x20 | KG_ST_NUMA_INSUF_* >> 12.
+constexpr int32_t ZONE_RESERVE_FAIL = 0x20;
+KG_HD inline bool zone_reserve_fails(int32_t z) { return z >= 0x20 && z < 0x40; }
+KG_HD inline uint32_t zone_fail_status(int32_t z) { return ((uint32_t)z & 7u) << 12; }
+
 // Magnitude bound of the float64 fast path: operands below 2^44 keep 100 * headroom below 2^51
 // (exact) and make the upward-rounded reciprocal's quotient exact after truncation.
 constexpr int64_t FAST_LIMIT = (int64_t)1 << 44;
@@ -222,9 +229,10 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
         zf.free_cpu = x100(tc - uc);
         zf.free_mem = x100(tm - um);
     }
-    // Restricted / BestEffort nodes run the general NUMA topology manager on the integer path
+    // Restricted nodes run the general NUMA topology manager in Filter, on the integer path (BestEffort
+    // nodes do not admit in Filter, plugin.go:446-455: their Filter / Score fit the fast path)
     const uint32_t pol0 = (f >> F_NUMA_POLICY_SHIFT) & 15u;
-    big = big || pol0 == 1u /* KG_NUMA_BEST_EFFORT */ || pol0 == 2u /* KG_NUMA_RESTRICTED */;
+    big = big || pol0 == 2u /* KG_NUMA_RESTRICTED */;
     // a node CPU bind policy makes every pod with a cpu request bind cpusets there (util.go:121-138)
     big = big || ((z.cpu_meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
     if (big) f |= F_BIG;
@@ -266,13 +274,13 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
     const int64_t req = v[N_REQ_CPU], cs = v[N_CPUSET], acs = v[N_AMP_CPUSET];
     const int64_t req_f = (req >= cs && cs > 0) ? req - cs + acs : req;
     const bool amp = (f & F_AMP) != 0;
-    // Restricted / BestEffort nodes are outside the device NUMA path: every non-skipped pod fails here
-    // (the verify path reports them KG_ST_UNSUPPORTED)
+    // Restricted nodes are outside the fast path (F_BIG): every non-skipped pod fails here
     const uint32_t pol = (f >> F_NUMA_POLICY_SHIFT) & 15u;
-    const bool pol_host = pol == 1u /* KG_NUMA_BEST_EFFORT */ || pol == 2u /* KG_NUMA_RESTRICTED */;
+    const bool pol_host = pol == 2u /* KG_NUMA_RESTRICTED */;
     v[D_AMP_FIT] = pol_host ? always_fail : amp ? fit(v[N_ALLOC_CPU] - req_f) : never_fail;
-    // scoreWithAmplifiedCPUs: requested - cs + Amplify(cs) unconditionally
-    v[D_AMP_DELTA] = kg_bits(amp ? x100(cs - acs) : 0.0);
+    // scoreWithAmplifiedCPUs: requested - cs + Amplify(cs) unconditionally under policy None; a BestEffort
+    // node scores node allocatable / requested as they are (calculateAllocatableAndRequested, scoring.go:184-189)
+    v[D_AMP_DELTA] = kg_bits((amp && pol != 1u /* KG_NUMA_BEST_EFFORT */) ? x100(cs - acs) : 0.0);
 }
 
 // Storage class of a node record: the select kernel is specialised per class and the snapshot is
@@ -344,6 +352,7 @@ struct alignas(16) DevSum {
     uint64_t fit;
     int64_t T[DEV_R], F[DEV_R];
     double rcp[DEV_R];  // 1 / T (least_req's exact-quotient path)
+    uint8_t score[16];  // per class: the node Score (scoreNode over the minor sums, 0..100) of one instance
 };
 
 constexpr int QUOTA_R = 4;

@@ -411,6 +411,7 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     if (Z > KG_MAX_ZONES) return fail(ctx, KG_UNSUPPORTED, "node %u: %u NUMA zones > %d", i, Z, KG_MAX_ZONES);
     f |= pol << F_NUMA_POLICY_SHIFT;
     f |= Z << F_NUMA_ZONES_SHIFT;
+    if (pol == KG_NUMA_BEST_EFFORT) f |= F_TOPO;  // the Reserve runs the topology manager (window replay: integer path)
     const double ratio = s->cpu_amp_ratio ? s->cpu_amp_ratio[i] : 0.0;
     if (ratio > 1) f |= F_AMP;
     v[N_FLAGS] = f;
@@ -670,6 +671,7 @@ const char* kg_status_string(kg_status s) {
         case KG_OOM: return "out of device memory";
         case KG_UNSUPPORTED: return "unsupported on the device path";
         case KG_NO_DEVICE: return "no device";
+        case KG_RESERVE_FAILED: return "reserve failed";
     }
     return "unknown";
 }
@@ -756,7 +758,7 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
     const size_t nb = sizeof(NodeRec) * std::max<uint32_t>(n_nodes, 1), zb = sizeof(ZoneRec) * std::max<uint32_t>(n_nodes, 1);
     if (hipMalloc(&s->d_nodes, nb) != hipSuccess || hipMalloc(&s->d_zones, zb) != hipSuccess ||
         hipMalloc(&s->d_big, sizeof(uint32_t) * ((size_t)n_nodes + 1)) != hipSuccess ||
-        hipMalloc(&s->d_zsel, std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
+        hipMalloc(&s->d_zsel, 2 * (size_t)std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
         hipMalloc(&s->d_pos, sizeof(uint32_t) * std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
         hipMemset(s->d_big, 0, sizeof(uint32_t)) != hipSuccess) {
         hipFree(s->d_nodes);
@@ -1251,10 +1253,10 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             const uint32_t keys = cols->dev_keys ? cols->dev_keys[j] : 0u;
             for (int r = 0; r < DEV_R; r++) dreq[(size_t)j * DEV_R + r] = cols->dev_req ? cols->dev_req[(size_t)j * DEV_R + r] : 0;
             dcls[j] = (uint8_t)DEV_CLASSES;
-            if (cntj > 0) {  // GPU request class: the per-instance request the minor predicate reads
+            if (cntj > 0) {  // GPU request class: the per-instance request the minor predicate and the Score read
                 DevClass c{};
                 c.dkeys = keys & 7u;
-                for (int r = 0; r < DEV_R; r++) c.dreq[r] = ((c.dkeys >> r) & 1u) ? dreq[(size_t)j * DEV_R + r] : 0;
+                for (int r = 0; r < DEV_R; r++) c.dreq[r] = dreq[(size_t)j * DEV_R + r];
                 size_t k = 0;
                 while (k < classes.size() && !(classes[k].dkeys == c.dkeys && classes[k].dreq[0] == c.dreq[0] &&
                                                classes[k].dreq[1] == c.dreq[1] && classes[k].dreq[2] == c.dreq[2]))
@@ -1476,7 +1478,7 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
         HIP_TRY(ctx, hipMalloc(&p->d_devsum, sizeof(DevSum) * std::max<uint32_t>(s->n, 1)));
         p->devsum_cap = s->n;
     }
-    HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_dev, s->n, p->d_dclass, p->n_dclass, p->d_devsum, ctx->stream));
+    HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_dev, s->n, p->d_dclass, p->n_dclass, s->kcfg, p->d_devsum, ctx->stream));
     e.dsum = p->d_devsum;
     return KG_OK;
 }
@@ -1920,7 +1922,7 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     for (uint32_t t = 0; t < REPLAY_G && err == hipSuccess; t++)
         err = launch_ext_replay_step(s->d_nodes, s->d_zones, s->d_dev, e, p->dev, p->n, s->n, s->base, s->kcfg, exact,
                                      p->d_step, t, p->d_winners, p->d_minors, p->d_buckets, s->d_zsel,
-                                     reasons ? p->d_reason : nullptr, ctx->stream);
+                                     reasons ? p->d_reason : nullptr, s->d_pos, ctx->stream);
     if (err == hipSuccess) err = launch_bump(p->d_step, REPLAY_G, ctx->stream);
     hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
     if (err == hipSuccess) err = ec;
@@ -2005,10 +2007,15 @@ kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) {
     if (s->has_cpu)
         HIP_TRY(ctx, launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, pod,
                                            s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, p->n, ctx->stream));
-    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], -1, 1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], -1, 1, s->kcfg, force_exact(), p->d_aout,
+                               ctx->stream));
     s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
+    int32_t zone = -1;
+    HIP_TRY(ctx, hipMemcpyAsync(&zone, p->d_aout, sizeof(zone), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (zone_reserve_fails(zone))
+        return fail(ctx, KG_RESERVE_FAILED, "Reserve of pod %u on node %u failed: NUMA status 0x%x", pod, node, zone_fail_status(zone));
     return KG_OK;
 }
 
@@ -2106,6 +2113,8 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (out_zone) *out_zone = o[0];
     if (out_minors) *out_minors = (uint32_t)o[1];
+    if (sign > 0 && zone_reserve_fails(o[0]))
+        return fail(ctx, KG_RESERVE_FAILED, "Reserve of pod %u on node %u failed: NUMA status 0x%x", pod, node, zone_fail_status(o[0]));
     return KG_OK;
 }
 

@@ -31,6 +31,10 @@ class Unsupported(EngineError):
     pass
 
 
+class ReserveFailed(EngineError):
+    """kg_assume / kg_assume_ext: the NodeNUMAResource Reserve fails on that node (BestEffort allocation)."""
+
+
 def lib():
     """Load libkoordgpu.so (built in-tree by __graft_entry__.build())."""
     global _lib
@@ -155,7 +159,7 @@ class Context:
         if s == abi.KG_OK:
             return
         msg = self.L.kg_last_error(self.h).decode() or self.L.kg_status_string(s).decode()
-        cls = Unsupported if s == abi.KG_UNSUPPORTED else EngineError
+        cls = Unsupported if s == abi.KG_UNSUPPORTED else ReserveFailed if s == abi.KG_RESERVE_FAILED else EngineError
         raise cls(s, f"{what}: {msg}")
 
     def sync(self):

@@ -59,6 +59,10 @@ def plugin_reasons(bits: int, scalar_names=DEFAULT_SCALARS) -> dict:
         (abi.KG_ST_NUMA_CPU_TOPO, "node(s) invalid CPU Topology"),
         (abi.KG_ST_NUMA_CPU_BIND, "node(s) cpu bind policy conflicts / SMT alignment / invalid requested cpus"),
         (abi.KG_ST_NUMA_CPUS, "not enough cpus available to satisfy request"),
+        # Reserve of a BestEffort node (plugin.go:612-623, resource_manager.go:135,300-309)
+        (abi.KG_ST_NUMA_INSUF_CPU, "Insufficient NUMA cpu"),
+        (abi.KG_ST_NUMA_INSUF_MEM, "Insufficient NUMA memory"),
+        (abi.KG_ST_NUMA_INSUF_NODE, "node(s) Insufficient NUMA Node resources"),
     )
     for bit, msg in numa:
         if bits & bit:

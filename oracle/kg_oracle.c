@@ -474,7 +474,11 @@ static uint32_t numa_admit(const kg_config* c, const numa_zones* x, const int64_
     return 0;
 }
 
-/* zone code of an allocation: -1 none, the zone for one zone, 0x40 | mask for several */
+/* zone code of an allocation: -1 none, the zone for one zone, 0x40 | mask for several; a BestEffort Reserve
+ * that fails: KGO_ZONE_RESERVE_FAIL | KG_ST_NUMA_INSUF_* >> 12 (the ABI's numa_zone codes) */
+#define KGO_ZONE_RESERVE_FAIL 0x20
+static int zone_fails(int32_t z) { return z >= 0x20 && z < 0x40; }
+static uint32_t zone_fail_bits(int32_t z) { return ((uint32_t)z & 7u) << 12; }
 static int32_t numa_code(uint32_t mask) {
     if (!mask) return -1;
     return popcount32(mask) == 1 ? (int32_t)__builtin_ctz(mask) : (int32_t)(0x40u | mask);
@@ -655,7 +659,7 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
         return 0;
     }
     /* FilterByNUMANode (topology_hint.go:31-41): SingleNUMANode / Restricted admit in Filter; BestEffort
-     * admits at Reserve only (plugin.go:448,612-623), its Score sees no affinity */
+     * admits at Reserve only (plugin.go:446-455,612-623), its Score sees no affinity */
     numa_zones x;
     numa_zones_load(n, i, &x);
     const int64_t req[2] = {p->req_cpu[j], p->req_mem[j]};
@@ -663,20 +667,35 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
     /* podNUMAExclusive defaults to Required when the pod carries its own NUMA policy (plugin.go:449-454) */
     const int excl = p->numa_policy[j] != KG_NUMA_NONE;
     uint32_t mask = 0;
-    if (x.Z == 0) {
-        if (policy != KG_NUMA_BEST_EFFORT) return KG_ST_NUMA_NO_RES;
-        return KG_ST_UNSUPPORTED; /* the BestEffort Reserve fails on a node without NUMA resources */
+    if (policy == KG_NUMA_BEST_EFFORT) {
+        /* Filter: nothing more; Score: node allocatable / requested without an allocation (scoring.go:184-189).
+         * The zone is what the Reserve would do: FilterByNUMANode under BestEffort (always admits) and the
+         * allocation of its best hint; a failure is reported as the zone code ZONE_RESERVE_FAIL | bits:
+         * GetTopologyHints without NUMA resources -> "node(s) Insufficient NUMA Node resources"
+         * (resource_manager.go:133-136), tryBestToDistributeEvenly -> "Insufficient NUMA <r>" (:300-309) */
+        *score_out = numa_node_score(c, n->alloc_cpu[i], N_REQ_CPU(n, i, ov) + pod_cpu, n->alloc_mem[i],
+                                     N_REQ_MEM(n, i, ov) + p->req_mem[j]);
+        if (x.Z == 0) {
+            *zone_out = KGO_ZONE_RESERVE_FAIL | (int32_t)(KG_ST_NUMA_INSUF_NODE >> 12);
+            return 0;
+        }
+        numa_admit(c, &x, req, has, policy, excl, &mask);
+        int64_t al[2][KG_MAX_ZONES];
+        int32_t fail = 0;
+        for (int r = 0; r < 2 && mask; r++) {
+            const int one[2] = {r == 0 && has[0], r == 1 && has[1]};
+            if (one[r] && !numa_split(&x, mask, req, one, al)) fail |= 1 << r;
+        }
+        *zone_out = fail ? KGO_ZONE_RESERVE_FAIL | fail : numa_code(mask);
+        return 0;
     }
+    if (x.Z == 0) return KG_ST_NUMA_NO_RES;
     uint32_t st = numa_admit(c, &x, req, has, policy, excl, &mask);
     if (st) return st;
     int64_t al[2][KG_MAX_ZONES];
-    if (mask && !numa_split(&x, mask, req, has, al)) {
-        /* only a non-preferred / unsatisfied BestEffort hint can fail its allocation: the reference
-         * fails the Reserve, the device path hands the pair back to the host */
-        return KG_ST_UNSUPPORTED;
-    }
+    if (mask && !numa_split(&x, mask, req, has, al)) return KG_ST_UNSUPPORTED; /* not reached: preferred hints place */
     *zone_out = numa_code(mask);
-    if (policy == KG_NUMA_BEST_EFFORT || !mask) {
+    if (!mask) {
         /* calculateAllocatableAndRequested without NUMA allocation: node allocatable / requested */
         *score_out = numa_node_score(c, n->alloc_cpu[i], N_REQ_CPU(n, i, ov) + pod_cpu, n->alloc_mem[i],
                                      N_REQ_MEM(n, i, ov) + p->req_mem[j]);
@@ -1209,13 +1228,16 @@ static void apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_co
     }
 }
 
-void kgo_assume(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j) {
+/* Reserve of pod j on node i: 0, or 1 when the NodeNUMAResource Reserve fails (nothing applied) */
+int kgo_assume(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j) {
     kg_node_columns v;
     kgo_state_view(st, &v);
     kgo_pair r;
     kgo_eval_pair(c, &v, i, p, j, &r);
     int32_t zone = r.status ? -1 : r.zone;
+    if (zone_fails(zone)) return 1;
     apply(c, st, i, p, j, zone, 1);
+    return 0;
 }
 
 void kgo_forget(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone) {
@@ -1242,7 +1264,8 @@ void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_c
             }
         }
         if (out_reason) out_reason[j] = why;
-        if (!best) {
+        if (!best || zone_fails(best_zone)) { /* no feasible node, or the selected node's Reserve fails */
+            if (best && out_reason) out_reason[j] |= zone_fail_bits(best_zone);
             out_node[j] = -1;
             if (out_total) out_total[j] = -1;
             continue;
@@ -1265,7 +1288,7 @@ int kgo_replay_parallel(const kg_config* c, kgo_state* st, uint32_t base, const 
     for (uint32_t j = 0; j < np; j++) {
         int32_t zone = -1;
         const uint64_t best = par_cycle(&pool, c, &v, st->n, base, p, j, &zone);
-        if (!best) {
+        if (!best || zone_fails(zone)) {
             out_node[j] = -1;
             if (out_total) out_total[j] = -1;
             continue;
@@ -2057,7 +2080,8 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
         }
         if (out_minors) out_minors[j] = 0;
         if (out_reason) out_reason[j] = why;
-        if (!best) {
+        if (!best || zone_fails(best_zone)) { /* no feasible node, or the selected node's Reserve fails */
+            if (best && out_reason) out_reason[j] |= zone_fail_bits(best_zone);
             out_node[j] = -1;
             if (out_total) out_total[j] = -1;
             continue;
@@ -2146,6 +2170,7 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                 s = o.status;
                 zone = o.zone;
             }
+            if (!s && zone_fails(zone)) s = zone_fail_bits(zone); /* the Reserve fails (engine.go:275-283) */
             if (s) {
                 failed = s;
                 failed_any = 1;

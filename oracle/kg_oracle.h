@@ -52,7 +52,8 @@ void kgo_state_free(kgo_state* st);
 /* Column view of the state (pointers stay valid until kgo_state_free). */
 void kgo_state_view(kgo_state* st, kg_node_columns* view);
 /* Reserve of pod on node (a16: NodeInfo.AddPod, podAssignCache.assign, NUMA Reserve). */
-void kgo_assume(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod);
+/* Reserve: 0, or 1 when the NodeNUMAResource Reserve fails (BestEffort allocation; nothing applied). */
+int kgo_assume(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod);
 /* Unreserve (reverse of kgo_assume with the zone chosen at Reserve). */
 void kgo_forget(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod,
                 int32_t zone);

@@ -69,6 +69,7 @@ def lib():
         L.kgo_state_free.argtypes = [C.c_void_p]
         L.kgo_state_view.argtypes = [C.c_void_p, P(abi.KgNodeColumns)]
         L.kgo_assume.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32]
+        L.kgo_assume.restype = C.c_int
         L.kgo_forget.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32, C.c_int32]
         L.kgo_replay.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
                                  P(C.c_int32), P(C.c_int64), P(C.c_uint32)]
@@ -221,9 +222,10 @@ class OracleState:
             lib().kgo_state_free(self.h)
             self.h = None
 
-    def assume(self, node: int, pods: abi.Table, pod: int):
+    def assume(self, node: int, pods: abi.Table, pod: int) -> bool:
+        """Reserve; False when the NodeNUMAResource Reserve fails (nothing applied)."""
         pc = abi.pod_columns(pods)
-        lib().kgo_assume(C.byref(self.cfg), self.h, node, C.byref(pc), pod)
+        return lib().kgo_assume(C.byref(self.cfg), self.h, node, C.byref(pc), pod) == 0
 
     def forget(self, node: int, pods: abi.Table, pod: int, zone: int):
         pc = abi.pod_columns(pods)

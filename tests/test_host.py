@@ -201,3 +201,25 @@ def test_reason_strings():
     assert got["NodeNUMAResource"] == ["Insufficient amplified cpu"]
     assert reasons.reasons(0) == []
     assert reasons.loadaware_status(abi.KG_ST_LA_EXPIRED) == ("Unschedulable", "node(s) nodeMetric expired")
+
+
+def test_non_zero_requests_rule():
+    """NonZeroRequested's rule, as koordinator restates it in GetNonZeroRequestForResource
+    (frameworkext/reservation_info.go:579-600, pinned by reservation_info_test.go:934-1003 where a reserve pod
+    without requests gets Non0AllocatedMilliCPU / Non0AllocatedMem = schedutil's defaults): a cpu / memory key
+    that is absent takes the default, one explicitly set to zero stays zero; per container, so a pod's
+    non-zero request is the sum over containers. The default values themselves (100m, 200Mi) are upstream
+    constants (k8s.io/kubernetes v1.35.6 pkg/scheduler/util) not present in the reference tree: parity of the
+    values is unpinned."""
+    from koordinator_amd.config import SchedulerConfig
+
+    def pod(*reqs):
+        return {"metadata": {"name": "p", "namespace": "d"},
+                "spec": {"containers": [{"name": f"c{k}", "resources": {"requests": r}} for k, r in enumerate(reqs)]}}
+
+    cfg = SchedulerConfig()
+    row = decode.pod_row(pod({}, {"cpu": "0", "memory": "0"}, {"cpu": "250m"}), cfg)
+    assert (row["req_cpu"], row["req_mem"]) == (250, 0)
+    # container 0: both defaults; container 1: explicit zeros; container 2: its cpu, the memory default
+    assert row["nz_cpu"] == 100 + 0 + 250
+    assert row["nz_mem"] == 2 * 200 * 1024 * 1024

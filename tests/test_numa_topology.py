@@ -24,7 +24,9 @@ def workload(seed, n_nodes, n_pods, score="LeastAllocated", hint="LeastAllocated
 
 
 def zone_mask(code):
-    return 0 if code < 0 else (code & 0xF if code >= 0x40 else 1 << code)
+    if code < 0 or abi.ZONE_RESERVE_FAIL <= code < 0x40:  # none, or a BestEffort Reserve that fails
+        return 0
+    return code & 0xF if code >= 0x40 else 1 << code
 
 
 # ---- oracle properties (CPU) -----------------------------------------------------------------------
@@ -37,6 +39,9 @@ def test_oracle_affinities_are_consistent():
     ok = ref.status == 0
     for j, i in zip(*np.nonzero(ok)):
         pol = ppol[j] if ppol[j] != abi.KG_NUMA_NONE else npol[i]
+        if abi.ZONE_RESERVE_FAIL <= int(ref.numa_zone[j, i]) < 0x40:
+            assert pol == abi.KG_NUMA_BEST_EFFORT, (j, i)  # only a BestEffort Reserve can fail after Filter
+            continue
         m = zone_mask(int(ref.numa_zone[j, i]))
         assert m >> int(Z[i]) == 0, (j, i)
         if pol == abi.KG_NUMA_NONE:
@@ -56,6 +61,45 @@ def test_oracle_affinities_are_consistent():
         assert (st & bit).any(), hex(bit)
     codes = ref.numa_zone[ok]
     assert (codes >= 0x40).any() and ((codes >= 0) & (codes < 4)).any()
+
+
+def best_effort_workload(seed=7, n_nodes=600, n_pods=200):
+    """synth.topology plus a few BestEffort two-zone nodes whose zones are fuller than the node-level
+    requested (the NRT view can lag the NodeInfo): pods pass their Filter, score them high, and the
+    allocation over their zones falls short at Reserve."""
+    kc, nodes, pods = workload(seed, n_nodes, n_pods)
+    tight = np.flatnonzero((nodes["numa_policy"] == abi.KG_NUMA_BEST_EFFORT) & (nodes["numa_zones"] == 2))[:40]
+    for z in range(2):
+        nodes[f"zone_cpu_used{z}"][tight] = nodes[f"zone_cpu{z}"][tight] - 1500
+        nodes[f"zone_mem_used{z}"][tight[::2]] = nodes[f"zone_mem{z}"][tight[::2]] - (1 << 30)
+    nodes["req_cpu"][tight] = nodes["alloc_cpu"][tight] // 4
+    nodes["nz_cpu"][tight] = np.maximum(nodes["nz_cpu"][tight], nodes["req_cpu"][tight])
+    return kc, nodes, pods
+
+
+def test_oracle_best_effort_admits_in_reserve_only():
+    """BestEffort runs no FilterByNUMANode in Filter (plugin.go:446-455): its pairs carry no NUMA admit
+    reason and score node allocatable / requested; the Reserve's topology manager decides the zone, and
+    a failing allocation ("Insufficient NUMA cpu / memory") or a node without NUMA resources ("node(s)
+    Insufficient NUMA Node resources") shows as a Reserve-failure zone code on a feasible pair."""
+    kc, nodes, pods = best_effort_workload()
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    npol, ppol = nodes["numa_policy"], pods["numa_policy"]
+    be = (npol[None, :] == abi.KG_NUMA_BEST_EFFORT) & ((ppol[:, None] == abi.KG_NUMA_NONE) |
+                                                       (ppol[:, None] == abi.KG_NUMA_BEST_EFFORT))
+    admit = abi.KG_ST_NUMA_UNSATISFIED | abi.KG_ST_NUMA_ALIGN | abi.KG_ST_NUMA_NO_RES
+    assert not (ref.status[be] & admit).any()
+    codes = ref.numa_zone[be & (ref.status == 0)]
+    fails = codes[(codes >= abi.ZONE_RESERVE_FAIL) & (codes < 0x40)]
+    assert len(fails) > 0 and ((fails & 4) != 0).any() and ((fails & 3) != 0).any()
+    # the Reserve of a failing pair fails in the oracle too, and nothing changes
+    st = oracle_lib.OracleState(kc, nodes)
+    j, i = np.argwhere(be & (ref.status == 0) & (ref.numa_zone >= abi.ZONE_RESERVE_FAIL) & (ref.numa_zone < 0x40))[0]
+    before = st.table()
+    assert not st.assume(int(i), pods, int(j))
+    after = st.table()
+    for k in before:
+        assert np.array_equal(before[k], after[k]), k
 
 
 def test_oracle_exclusive_policy_respects_zone_status():
@@ -180,3 +224,32 @@ def test_topology_assume_forget(ctx):
     j, i = multi[0]
     with pytest.raises(engine.Unsupported):
         engine.forget(snap, batch, int(j), int(i), int(ref.numa_zone[j, i]))
+
+
+@pytest.mark.gpu
+def test_best_effort_reserve_failures(ctx):
+    """The BestEffort semantics on the device: Filter / Score / select without the topology manager, the
+    Reserve's zone (or failure) in verify, replays that leave a pod unscheduled when its selected node's
+    Reserve fails (reasons carry KG_ST_NUMA_INSUF_*), and kg_assume refusing with KG_RESERVE_FAILED."""
+    kc, nodes, pods = best_effort_workload(8, 700, 400)
+    snap, batch = engine.Snapshot(ctx, kc, nodes), engine.PodBatch(ctx, pods)
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    assert_equal(engine.eval_verify(snap, batch), ref, "verify")
+    for k in (1, 3):
+        assert np.array_equal(engine.eval_select(snap, batch, k), oracle_lib.select(kc, nodes, pods, k)), k
+    onode, ototal, owhy = oracle_lib.OracleState(kc, nodes).replay(pods, reasons=True)
+    failed = (onode < 0) & ((owhy & abi.KG_ST_NUMA_RESERVE) != 0)
+    assert failed.any()
+    node, total, why = engine.replay(snap, batch, reasons=True)
+    assert np.array_equal(node, onode) and np.array_equal(total, ototal) and np.array_equal(why, owhy)
+    snap.upload(nodes)
+    node2, total2 = engine.replay(snap, batch)  # window replay (no reasons)
+    assert np.array_equal(node2, onode) and np.array_equal(total2, ototal)
+    snap.upload(nodes)
+    j, i = np.argwhere((ref.status == 0) & (ref.numa_zone >= abi.ZONE_RESERVE_FAIL) & (ref.numa_zone < 0x40))[0]
+    before = snap.read_state()
+    with pytest.raises(engine.ReserveFailed):
+        engine.assume(snap, batch, int(j), int(i))
+    after = snap.read_state()
+    for k in before:
+        assert np.array_equal(before[k], after[k]), k
