@@ -119,6 +119,9 @@ class SchedulerConfig:
     nrf_ignored_groups: Tuple[str, ...] = ()
     rsv_ignored: Tuple[str, ...] = ()
     rsv_ignored_groups: Tuple[str, ...] = ()
+    # NodeNUMAResourceArgs.DefaultCPUBindPolicy (v1/defaults.go:50, plugin.go:327-334): fills in a pod's
+    # "" / "Default" bind policy
+    default_cpu_bind_policy: str = "FullPCPUs"
 
     def _ignore_mask(self, names, groups) -> int:
         m = 0

@@ -68,7 +68,8 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
                                                        uint32_t pod, uint32_t rec, const uint64_t* __restrict__ winners,
                                                        const uint32_t* __restrict__ step_base, uint32_t step_off,
                                                        const uint32_t* __restrict__ pos, uint32_t index_base,
-                                                       uint32_t n_pods) {
+                                                       uint32_t n_pods, int8_t* __restrict__ zsel,
+                                                       int32_t* __restrict__ fail_out) {
     __shared__ kg_cpu_topo st;
     __shared__ CpuAccLds acc;
     __shared__ kg_cpu_alloc sa;
@@ -138,7 +139,12 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
     uint64_t res[4];
     const int code = cpuset_take(&st, &sa, q, &acc, res);
     __syncthreads();
-    if (code != 0 || threadIdx.x != 0) return;
+    if (threadIdx.x != 0) return;
+    if (code != 0) {  // Allocate fails (ErrNotEnoughCPUs): the Reserve fails, nothing of the pod is applied
+        if (winners) zsel[rec] = (int8_t)ZONE_CPUSET_FAIL;  // read by the replay step that applies the pod
+        else if (fail_out) *fail_out = ZONE_CPUSET_FAIL;  // read by k_assume / k_ext_assume
+        return;
+    }
     kg_cpu_alloc& A = allocs[rec];
     uint32_t used = 0;  // NUMA nodes of the CPUs taken (addPodAllocation's usedNUMA)
     for (int c = 0; c < st.n_cpus; c++)
@@ -156,9 +162,9 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
 hipError_t launch_cpuset_reserve(NodeRec* nodes, ZoneRec* zones, kg_cpu_alloc* allocs, const kg_cpu_topo* topos,
                                  const PodsDev& pods, const KCfg& cfg, uint32_t pod, uint32_t rec, const uint64_t* winners,
                                  const uint32_t* step_base, uint32_t step_off, const uint32_t* pos, uint32_t index_base,
-                                 uint32_t n_pods, hipStream_t s) {
+                                 uint32_t n_pods, int8_t* zsel, int32_t* fail_out, hipStream_t s) {
     k_cpuset_reserve<<<1, 64, 0, s>>>(nodes, zones, allocs, topos, pods, cfg, pod, rec, winners, step_base, step_off, pos,
-                                      index_base, n_pods);
+                                      index_base, n_pods, zsel, fail_out);
     return hipGetLastError();
 }
 

@@ -624,6 +624,7 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     int32_t zone = zone_in;
     uint32_t mask = minors_in;
     if (sign > 0) {
+        if (out && zone_reserve_fails(out[0])) return;  // the cpuset Reserve that ran first failed (out[0] preset)
         const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, 0u);
         zone = r.status ? -1 : r.zone;
         if (zone_reserve_fails(zone)) {  // the NodeNUMAResource Reserve fails: nothing is applied

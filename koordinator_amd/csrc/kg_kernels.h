@@ -124,7 +124,7 @@ hipError_t launch_cpuset_take(const kg_cpu_topo* topos, const kg_cpu_alloc* allo
 hipError_t launch_cpuset_reserve(NodeRec* nodes, ZoneRec* zones, kg_cpu_alloc* allocs, const kg_cpu_topo* topos,
                                  const PodsDev& pods, const KCfg& cfg, uint32_t pod, uint32_t rec, const uint64_t* winners,
                                  const uint32_t* step_base, uint32_t step_off, const uint32_t* pos, uint32_t index_base,
-                                 uint32_t n_pods, hipStream_t s);
+                                 uint32_t n_pods, int8_t* zsel, int32_t* fail_out, hipStream_t s);
 // inline batch cycle of a whole-job plan (k_batch); ext = the snapshot carries the config-5 tables
 hipError_t launch_batch(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                         const uint32_t* grp_begin, const uint32_t* grp_pods, const uint32_t* grp_rec, uint32_t n_groups,

@@ -348,6 +348,7 @@ __global__ void k_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zone
     int64_t* n = nodes[node].v;
     int32_t zone = zone_in;
     if (sign > 0) {
+        if (zone_out && zone_reserve_fails(*zone_out)) return;  // the cpuset Reserve that ran first failed
         const PairOut o = eval_pair<EXACT>(cfg, n, zones + node, q);
         zone = o.zone;
     }

@@ -182,7 +182,11 @@ KG_HD inline uint32_t cpuset_zone_status(uint32_t status, uint32_t used) {
 // Zone code of a pair whose Reserve fails (BestEffort allocation): 0x20 | KG_ST_NUMA_INSUF_* >> 12.
 constexpr int32_t ZONE_RESERVE_FAIL = 0x20;
 KG_HD inline bool zone_reserve_fails(int32_t z) { return z >= 0x20 && z < 0x40; }
-KG_HD inline uint32_t zone_fail_status(int32_t z) { return ((uint32_t)z & 7u) << 12; }
+// a cpuset-binding pod whose accumulator finds no CPUs at Reserve (resource_manager.go:385,427 ErrNotEnoughCPUs)
+constexpr int32_t ZONE_CPUSET_FAIL = ZONE_RESERVE_FAIL | 8;
+KG_HD inline uint32_t zone_fail_status(int32_t z) {
+    return (((uint32_t)z & 7u) << 12) | (((uint32_t)z & 8u) ? KG_ST_NUMA_CPUS : 0u);
+}
 
 // Magnitude bound of the float64 fast path: operands below 2^44 keep 100 * headroom below 2^51
 // (exact) and make the upward-rounded reciprocal's quotient exact after truncation.

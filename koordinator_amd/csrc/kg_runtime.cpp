@@ -1799,7 +1799,8 @@ kg_status replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
         // the previous pod's cpuset Reserve runs before the step that applies its other Reserves
         if (cs)
             e = launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, 0, 0,
-                                      p->d_winners, p->d_step, t, s->d_pos, s->base, p->n, ctx->stream);
+                                      p->d_winners, p->d_step, t, s->d_pos, s->base, p->n, s->d_zsel, nullptr,
+                                      ctx->stream);
         if (e == hipSuccess)
             e = launch_replay_step(s->d_nodes, s->d_zones, p->dev, p->n, s->n, s->base, s->kcfg, exact, p->d_step, t,
                                    p->d_winners, s->d_zsel, reasons ? p->d_reason : nullptr, ctx->stream);
@@ -2004,9 +2005,11 @@ kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) {
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     touch_views(s, node);
+    HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 2, ctx->stream));
     if (s->has_cpu)
         HIP_TRY(ctx, launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, pod,
-                                           s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, p->n, ctx->stream));
+                                           s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, p->n, nullptr, p->d_aout,
+                                           ctx->stream));
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], -1, 1, s->kcfg, force_exact(), p->d_aout,
                                ctx->stream));
     s->gen++;
@@ -2101,9 +2104,11 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     touch_views(s, node);
+    HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 2, ctx->stream));
     if (sign > 0 && s->has_cpu)
         HIP_TRY(ctx, launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, pod,
-                                           s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, p->n, ctx->stream));
+                                           s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, p->n, nullptr, p->d_aout,
+                                           ctx->stream));
     HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone, minors,
                                    sign, s->kcfg, force_exact(), p->d_aout, ctx->stream));
     s->gen++;

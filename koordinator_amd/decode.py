@@ -318,13 +318,10 @@ def is_daemonset_pod(pod) -> bool:
 
 ANN_NUMA_TOPOLOGY_SPEC = "scheduling.koordinator.sh/numa-topology-spec"
 ANN_RESOURCE_SPEC = "scheduling.koordinator.sh/resource-spec"
+DEFAULT_CPU_BIND_POLICY = "FullPCPUs"  # NodeNUMAResourceArgs default (v1/defaults.go:50)
 
 
-ANN_RESOURCE_SPEC = "scheduling.koordinator.sh/resource-spec"
-DEFAULT_CPU_BIND_POLICY = "FullPCPUs"
-
-
-def cpu_bind_flags(pod, req_cpu_milli: int) -> int:
+def cpu_bind_flags(pod, req_cpu_milli: int, default_policy: str = DEFAULT_CPU_BIND_POLICY) -> int:
     """KG_POD_CPU_* bits of an AllowUseCPUSet pod (nodenumaresource/plugin.go:331-349,
     apis/extension/numa_aware.go:63-71,231-244). A Full/Spread policy with a fractional cpu request is
     ErrInvalidRequestedCPUs at PreFilter: Unsupported here (the pod never reaches Filter)."""
@@ -332,10 +329,10 @@ def cpu_bind_flags(pod, req_cpu_milli: int) -> int:
     spec = json.loads(ann[ANN_RESOURCE_SPEC]) if ann.get(ANN_RESOURCE_SPEC) else {}
     preferred = spec.get("preferredCPUBindPolicy") or ""
     if preferred in ("", "Default"):
-        preferred = DEFAULT_CPU_BIND_POLICY
+        preferred = default_policy or DEFAULT_CPU_BIND_POLICY
     required = spec.get("requiredCPUBindPolicy") or ""
     if required == "Default":
-        required = DEFAULT_CPU_BIND_POLICY
+        required = default_policy or DEFAULT_CPU_BIND_POLICY
     policy = required or preferred
     if policy not in ("FullPCPUs", "SpreadByPCPUs"):
         return 0
@@ -389,7 +386,7 @@ def pod_row(pod, cfg: SchedulerConfig) -> Dict[str, int]:
     # LSE/LSR prod pods bind cpusets with the resource-spec annotation's policies, DefaultCPUBindPolicy
     # (FullPCPUs, v1/defaults.go:50) filling in "" / "Default"; a required policy wins
     if koord_qos_raw(pod) in ("LSE", "LSR") and pc == PROD and (cfg.plugins & abi.KG_PLUGIN_NUMA):
-        flags |= cpu_bind_flags(pod, row["req_cpu"])
+        flags |= cpu_bind_flags(pod, row["req_cpu"], cfg.default_cpu_bind_policy)
     ann = (pod.get("metadata") or {}).get("annotations") or {}
     if ann.get(ANN_NUMA_TOPOLOGY_SPEC):
         raise Unsupported("pod NUMA topology spec (exclusive-policy admission) is not on the device path")

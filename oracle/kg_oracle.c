@@ -478,7 +478,9 @@ static uint32_t numa_admit(const kg_config* c, const numa_zones* x, const int64_
  * that fails: KGO_ZONE_RESERVE_FAIL | KG_ST_NUMA_INSUF_* >> 12 (the ABI's numa_zone codes) */
 #define KGO_ZONE_RESERVE_FAIL 0x20
 static int zone_fails(int32_t z) { return z >= 0x20 && z < 0x40; }
-static uint32_t zone_fail_bits(int32_t z) { return ((uint32_t)z & 7u) << 12; }
+static uint32_t zone_fail_bits(int32_t z) { return (((uint32_t)z & 7u) << 12) | ((z & 8) ? KG_ST_NUMA_CPUS : 0u); }
+/* the cpuset accumulator finds no CPUs at Reserve (resource_manager.go:385,427 ErrNotEnoughCPUs) */
+#define KGO_ZONE_CPUSET_FAIL (KGO_ZONE_RESERVE_FAIL | 8)
 static int32_t numa_code(uint32_t mask) {
     if (!mask) return -1;
     return popcount32(mask) == 1 ? (int32_t)__builtin_ctz(mask) : (int32_t)(0x40u | mask);
@@ -1140,17 +1142,18 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
 /* NodeNUMAResource Reserve of a cpuset-binding pod on a NUMA-policy-None node: the accumulator's CPUs
  * enter NodeAllocation.allocatedCPUs (addPodAllocation, node_allocation.go:111-130: RefCount++, the pod's
  * exclusive policy), and cpuset_alloc_milli follows the allocated CPU count */
-static void cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j) {
-    if (!(c->plugins & KG_PLUGIN_NUMA) || !st->cpu_topo || (p->flags[j] & KG_POD_NUMA_SKIP)) return;
+static int cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j) {
+    if (!(c->plugins & KG_PLUGIN_NUMA) || !st->cpu_topo || (p->flags[j] & KG_POD_NUMA_SKIP)) return 0;
     const uint32_t node_bind = st->cpu_bind[i];
     const int bind = (p->flags[j] & KG_POD_CPU_BIND) || (node_bind != KG_NODE_CPU_BIND_NONE && p->req_cpu[j] != 0);
-    if (!bind) return;
+    if (!bind) return 0;
     int conflict;
-    if (numa_merge_policy(st->numa_policy[i], p->numa_policy[j], &conflict) != KG_NUMA_NONE) return;
+    if (numa_merge_policy(st->numa_policy[i], p->numa_policy[j], &conflict) != KG_NUMA_NONE) return 0;
     kg_node_columns v;
     kgo_state_view(st, &v);
     uint64_t out[4];
-    if (cpuset_allocate(&v, i, p, j, node_bind, out)) return;
+    /* Allocate fails (Reserve returns the error, plugin.go:585-635): nothing of the pod is applied */
+    if (cpuset_allocate(&v, i, p, j, node_bind, out)) return 1;
     const uint32_t excl = (p->flags[j] >> KG_POD_CPU_EXCL_SHIFT) & 3u;
     const kg_cpu_topo* t = cpu_topology(&v, i);
     int allocated = 0;
@@ -1173,11 +1176,14 @@ static void cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const 
         const uint32_t ns = multi ? 2u : (s == 0u ? 1u : s);
         st->zone_status[i] = (st->zone_status[i] & ~(3u << (2 * q))) | (ns << (2 * q));
     }
+    return 0;
 }
 
-static void apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,
-                  int64_t sign) {
-    if (sign > 0) cpuset_reserve(c, st, i, p, j);
+/* Reserve (sign 1) / Unreserve (-1) of pod j on node i; a Reserve returns KGO_ZONE_CPUSET_FAIL when the
+ * cpuset accumulator fails (nothing applied), else 0 */
+static int apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,
+                 int64_t sign) {
+    if (sign > 0 && cpuset_reserve(c, st, i, p, j)) return KGO_ZONE_CPUSET_FAIL;
     /* upstream NodeInfo.AddPod / RemovePod: Requested, NonZeroRequested, len(Pods) */
     st->col[C_REQ_CPU][i] += sign * p->req_cpu[j];
     st->col[C_REQ_MEM][i] += sign * p->req_mem[j];
@@ -1226,6 +1232,7 @@ static void apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_co
             st->col[C_ZONE_MEM_USED + z][i] += sign * al[1][z];
         }
     }
+    return 0;
 }
 
 /* Reserve of pod j on node i: 0, or 1 when the NodeNUMAResource Reserve fails (nothing applied) */
@@ -1236,12 +1243,11 @@ int kgo_assume(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_colum
     kgo_eval_pair(c, &v, i, p, j, &r);
     int32_t zone = r.status ? -1 : r.zone;
     if (zone_fails(zone)) return 1;
-    apply(c, st, i, p, j, zone, 1);
-    return 0;
+    return apply(c, st, i, p, j, zone, 1) != 0;
 }
 
 void kgo_forget(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone) {
-    apply(c, st, i, p, j, zone, -1);
+    (void)apply(c, st, i, p, j, zone, -1);
 }
 
 void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
@@ -1271,9 +1277,15 @@ void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_c
             continue;
         }
         uint32_t g = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
+        const int32_t f = apply(c, st, g - base, p, j, best_zone, 1);
+        if (f) { /* the cpuset Reserve fails: the pod stays unscheduled */
+            if (out_reason) out_reason[j] |= zone_fail_bits(f);
+            out_node[j] = -1;
+            if (out_total) out_total[j] = -1;
+            continue;
+        }
         out_node[j] = (int32_t)g;
         if (out_total) out_total[j] = (int64_t)(best >> 32);
-        apply(c, st, g - base, p, j, best_zone, 1);
     }
 }
 
@@ -1294,9 +1306,13 @@ int kgo_replay_parallel(const kg_config* c, kgo_state* st, uint32_t base, const 
             continue;
         }
         const uint32_t g = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
+        if (apply(c, st, g - base, p, j, zone, 1)) {
+            out_node[j] = -1;
+            if (out_total) out_total[j] = -1;
+            continue;
+        }
         out_node[j] = (int32_t)g;
         if (out_total) out_total[j] = (int64_t)(best >> 32);
-        apply(c, st, g - base, p, j, zone, 1);
     }
     par_close(&pool);
     return 0;
@@ -2088,9 +2104,15 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
         }
         uint32_t g = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
         uint32_t i = g - base;
+        const int32_t f = apply(c, st, i, p, j, best_zone, 1);
+        if (f) { /* the cpuset Reserve fails: the pod stays unscheduled */
+            if (out_reason) out_reason[j] |= zone_fail_bits(f);
+            out_node[j] = -1;
+            if (out_total) out_total[j] = -1;
+            continue;
+        }
         out_node[j] = (int32_t)g;
         if (out_total) out_total[j] = (int64_t)(best >> 32);
-        apply(c, st, i, p, j, best_zone, 1);
         if ((c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0 && st->dev_minors &&
             st->dev_minors[i] > 0) {
             int64_t preq[KG_DEV_R];
@@ -2178,7 +2200,14 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                 out_status[j] = s;
                 continue;
             }
-            apply(c, st, (uint32_t)node, p, j, zone, 1);
+            const int32_t f = apply(c, st, (uint32_t)node, p, j, zone, 1);
+            if (f) { /* the cpuset Reserve fails */
+                failed = zone_fail_bits(f);
+                failed_any = 1;
+                out_result[j] = KG_BATCH_FAILED;
+                out_status[j] = failed;
+                continue;
+            }
             if ((c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0 && st->dev_minors &&
                 st->dev_minors[node] > 0) {
                 int64_t preq[KG_DEV_R];

@@ -80,6 +80,33 @@ def test_oracle_cpuset_reserve_updates_zone_status():
     assert changed >= 3
 
 
+def _unallocatable_pairs(nodes, pods, ref):
+    """(pod, node) pairs of cpuset pods on policy-None nodes with a topology whose accumulator fails
+    (Filter status NUMA_CPUS for a required policy, UNSUPPORTED for a preferred one)."""
+    bind = (pods["flags"] & abi.KG_POD_CPU_BIND) != 0
+    ok_node = (nodes["cpu_topo"] >= 0) & (nodes["numa_policy"] == abi.KG_NUMA_NONE)
+    hit = bind[:, None] & ok_node[None, :] & ((ref.status & (abi.KG_ST_NUMA_CPUS | abi.KG_ST_UNSUPPORTED)) != 0) & \
+        ((ref.status & np.uint32(~(abi.KG_ST_NUMA_CPUS | abi.KG_ST_UNSUPPORTED) & 0xFFFFFFFF)) == 0)
+    return np.argwhere(hit)
+
+
+def test_oracle_cpuset_reserve_failure_applies_nothing():
+    """Reserve of a cpuset pod whose accumulator finds too few CPUs (resource_manager.go:385,427
+    ErrNotEnoughCPUs -> the Reserve error): kgo_assume reports the failure and no column moves."""
+    cfg, nodes, pods = synth.cpuset_cluster(200, 160, seed=11)
+    kc = cfg.kg_config()
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    pairs = _unallocatable_pairs(nodes, pods, ref)
+    assert len(pairs) >= 3
+    st = oracle_lib.OracleState(kc, nodes)
+    before = st.table()
+    for j, i in pairs[:8]:
+        assert not st.assume(int(i), pods, int(j))
+    after = st.table()
+    for k in before:
+        assert np.array_equal(before[k], after[k]), k
+
+
 # ---------------------------------------------------------------------------------------------- GPU
 
 @pytest.fixture(scope="module")
@@ -205,3 +232,23 @@ def test_cpuset_then_pod_numa_policy_sees_zone_status(ctx):
     for f in FIELDS:
         a, b = getattr(gv, f), getattr(rv, f)
         assert np.array_equal(a, b), f
+
+
+@pytest.mark.gpu
+def test_cpuset_reserve_failure(ctx):
+    """kg_assume of a cpuset pod whose accumulator fails: KG_RESERVE_FAILED (ReserveFailed), nothing applied on
+    the device (k_cpuset_reserve flags the failure, k_assume skips the NodeInfo Reserve)."""
+    from koordinator_amd import engine
+    cfg, nodes, pods = synth.cpuset_cluster(200, 160, seed=11)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    batch = engine.PodBatch(ctx, pods)
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    pairs = _unallocatable_pairs(nodes, pods, ref)
+    before = snap.read_state()
+    for j, i in pairs[:8]:
+        with pytest.raises(engine.ReserveFailed):
+            engine.assume(snap, batch, int(j), int(i))
+    after = snap.read_state()
+    for k in before:
+        assert np.array_equal(before[k], after[k]), k

@@ -434,15 +434,11 @@ def test_replay_reasons_match_oracle(ctx, ext):
 
 
 def test_result_status_flags_host_path_pods(ctx):
-    """kg_result_status: pods with a pair the device cannot decide (cpuset binding under
-    NodeNUMAResource; a BestEffort node without zones) are flagged KG_ST_UNSUPPORTED, exactly the pods
-    whose oracle verify row carries the bit; every other pod's keys are complete."""
-    cfg, nodes, pods = synth.small(900, 300, seed=23, numa=True)
-    pods = {k: v.copy() for k, v in pods.items()}
-    pods["flags"][::7] |= abi.KG_POD_CPU_BIND
-    nodes = {k: v.copy() for k, v in nodes.items()}
-    nodes["numa_policy"][5:9] = abi.KG_NUMA_BEST_EFFORT
-    nodes["numa_zones"][5:7] = 0
+    """kg_result_status: pods with a pair the device cannot decide (a cpuset-binding pod on a node with a
+    NUMA topology policy, or one whose preferred-policy accumulator fails in Filter) are flagged
+    KG_ST_UNSUPPORTED, exactly the pods whose oracle verify row carries the bit; every other pod's keys
+    are complete."""
+    cfg, nodes, pods = synth.cpuset_cluster(300, 120, seed=23)
     kc = cfg.kg_config()
     snap = engine.Snapshot(ctx, kc, nodes)
     batch = engine.PodBatch(ctx, pods)

@@ -223,3 +223,31 @@ def test_non_zero_requests_rule():
     # container 0: both defaults; container 1: explicit zeros; container 2: its cpu, the memory default
     assert row["nz_cpu"] == 100 + 0 + 250
     assert row["nz_mem"] == 2 * 200 * 1024 * 1024
+
+
+def test_default_cpu_bind_policy_from_profile():
+    """A "" / "Default" bind policy takes NodeNUMAResourceArgs.DefaultCPUBindPolicy (plugin.go:327-334,
+    FullPCPUs by default, v1/defaults.go:50); an explicit policy is kept; a required policy marks REQUIRED."""
+    import json
+
+    from koordinator_amd.config import SchedulerConfig
+
+    def lsr(spec):
+        ann = {decode.ANN_RESOURCE_SPEC: json.dumps(spec)} if spec is not None else {}
+        return {"metadata": {"name": "p", "namespace": "d", "annotations": ann,
+                             "labels": {"koordinator.sh/qosClass": "LSR"}},
+                "spec": {"priority": 9500, "containers": [{"name": "c", "resources": {"requests": {"cpu": "4"}}}]}}
+
+    def policy(flags):
+        return (flags >> abi.KG_POD_CPU_POLICY_SHIFT) & 3
+
+    full, spread = abi.KG_CPU_BIND["FullPCPUs"], abi.KG_CPU_BIND["SpreadByPCPUs"]
+    for default, want in (("FullPCPUs", full), ("SpreadByPCPUs", spread)):
+        cfg = SchedulerConfig(default_cpu_bind_policy=default)
+        for spec in (None, {}, {"preferredCPUBindPolicy": "Default"}):
+            f = decode.pod_row(lsr(spec), cfg)["flags"]
+            assert f & abi.KG_POD_CPU_BIND and policy(f) == want and not f & abi.KG_POD_CPU_REQUIRED
+        f = decode.pod_row(lsr({"preferredCPUBindPolicy": "FullPCPUs"}), cfg)["flags"]
+        assert policy(f) == full
+        f = decode.pod_row(lsr({"requiredCPUBindPolicy": "Default"}), cfg)["flags"]
+        assert policy(f) == want and f & abi.KG_POD_CPU_REQUIRED
