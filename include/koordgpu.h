@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 6
+#define KG_ABI_VERSION 7
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -111,6 +111,15 @@ typedef enum kg_status {
 #define KG_POD_RSV_REQUIRED 0x80u    /* pod has a reservation affinity (reservation/transformer.go:148,
                                       * stateData.hasAffinity): must allocate from a reservation      */
 
+/* GPURequirements flags (kg_pod_columns.dev_flags). */
+#define KG_GPU_POD_SHARED 0x1u      /* gpuShared: per-GPU gpu-core / memory ratio below 100 (devicehandler_gpu.go:53-96) */
+#define KG_GPU_POD_HONOR 0x2u       /* GPUPartitionSpec annotation present: honorGPUPartition                    */
+#define KG_GPU_POD_RESTRICTED 0x4u  /* GPUPartitionSpec AllocatePolicy Restricted                                */
+#define KG_GPU_POD_RING_BW 0x8u     /* GPUPartitionSpec RingBusBandwidth set (kg_pod_columns.dev_ring_bw)          */
+#define KG_GPU_POD_SCOPE_SHIFT 4    /* 3 bits: DeviceTopologyScopeLevel of the required scope (0 none, 2 NUMANode,
+                                     * 3 PCIe, 4 Device; apis/extension/device_share.go:185-190)               */
+#define KG_GPU_POD_TEMPLATE 0x100u  /* enforceGPUSharedResourceTemplate: not on the device path (KG_ST_UNSUPPORTED) */
+
 /* Reservation allocate policies (apis/scheduling/v1alpha1 ReservationAllocatePolicy). */
 #define KG_RSV_DEFAULT 0u
 #define KG_RSV_ALIGNED 1u
@@ -124,7 +133,7 @@ typedef enum kg_status {
 #define KG_ST_NRF_EPH 0x8u    /* "Insufficient ephemeral-storage"         */
 #define KG_ST_NRF_SC0 0x10u   /* "Insufficient <scalar 0>"                */
 #define KG_ST_NRF_SC1 0x20u   /* "Insufficient <scalar 1>"                */
-#define KG_ST_NRF_MASK 0xFFu
+#define KG_ST_NRF_MASK 0x3Fu
 #define KG_ST_LA_EXPIRED 0x100u /* ErrReasonNodeMetricExpired                        */
 #define KG_ST_LA_CPU 0x200u     /* ErrReasonUsageExceedThreshold, cpu                */
 #define KG_ST_LA_MEM 0x400u     /* ErrReasonUsageExceedThreshold, memory             */
@@ -150,7 +159,20 @@ typedef enum kg_status {
 #define KG_ST_DEV_INSUFFICIENT 0x01000000u /* "Insufficient gpu devices" (Unschedulable, device_allocator.go:432) */
 #define KG_ST_DEV_NO_DEVICE 0x02000000u    /* no GPU minors on the node's Device (UnschedulableAndUnresolvable,
                                               devicehandler_gpu.go:41-44)                              */
-#define KG_ST_DEV_MASK 0x03000000u
+/* DeviceShare reasons are a 4-bit code: bits 24-25 are its low half, bits 6-7 its high half
+ * (KG_ST_DEV_CODE). Codes 3.. come from the GPU allocator (deviceshare/allocator_gpu.go:31-41). */
+#define KG_ST_DEV_MASK 0x030000C0u
+#define KG_ST_DEV_CODE(st) ((((st) >> 24) & 3u) | ((((st) >> 6) & 3u) << 2))
+#define KG_ST_DEV_MAKE(code) (((((uint32_t)(code)) & 3u) << 24) | (((((uint32_t)(code)) >> 2) & 3u) << 6))
+#define KG_DEV_CODE_INSUFFICIENT 1u      /* "Insufficient gpu devices" (defaultAllocateDevices)                 */
+#define KG_DEV_CODE_NO_DEVICE 2u         /* no GPU minors on the node's Device                                  */
+#define KG_DEV_CODE_GPU_DEVICES 3u       /* ErrInsufficientGPUDevices: the topology-tree allocation failed       */
+#define KG_DEV_CODE_TOPO_SCOPED 4u       /* ErrInsufficientTopologyScopedGPUDevices (required topology scope)    */
+#define KG_DEV_CODE_PARTITIONED 5u       /* ErrInsufficientPartitionedDevice (partitions honored)                */
+#define KG_DEV_CODE_NO_PARTITION 6u      /* ErrNodeMissingGPUPartitionTable (partitions honored)                 */
+#define KG_DEV_CODE_PART_COUNT 7u        /* ErrUnsupportedGPURequests: no partition of that GPU count (honored)  */
+#define KG_DEV_CODE_NO_TREE 8u           /* ErrNodeMissingGPUDeviceTopologyTree (required topology scope)        */
+#define KG_DEV_CODE_MULTI_SHARED 9u      /* ErrUnsupportedMultiSharedGPU (required topology scope)               */
 #define KG_ST_RSV_AFFINITY 0x04000000u     /* ErrReasonReservationAffinity (reservation/plugin.go:366-368)  */
 #define KG_ST_RSV_NODE 0x08000000u         /* "Insufficient <r> by node" (reservation/plugin.go:498-525)    */
 #define KG_ST_RSV_RESERVATION 0x10000000u  /* reservation-level reasons / no reservation meets the pod      */
@@ -254,6 +276,21 @@ typedef struct kg_cpuset_request {
     int32_t has_preferred;
 } kg_cpuset_request;
 
+/* One GPU partition (apis/extension/device_share.go:221-227 GPUPartition). */
+#define KG_GPU_NO_SCOPE 0xFFu
+#define KG_GPU_HONOR 0x100u
+#define KG_GPU_TREE 0x200u
+#define KG_GPU_MAX_TABLES 16
+#define KG_GPU_MAX_PARTS 1024
+typedef struct kg_gpu_partition {
+    uint8_t table;           /* partition table index (dev_part - 1)                                   */
+    uint8_t n_gpus;          /* the table key: number of GPUs (1..8)                                   */
+    uint8_t minors;          /* MinorsHash: bit m = minor m                                            */
+    uint8_t pad_;
+    int32_t alloc_score;     /* AllocationScore                                                        */
+    int64_t ring_bw;         /* RingBusBandwidth in bytes, -1 = none                                   */
+} kg_gpu_partition;
+
 typedef struct kg_node_columns {
     /* upstream NodeInfo (k8s v1.35.6): Allocatable / Requested / NonZeroRequested / len(Pods) */
     const int64_t *alloc_cpu, *alloc_mem, *alloc_eph, *alloc_pods;
@@ -306,6 +343,21 @@ typedef struct kg_node_columns {
     const uint8_t* cpu_max_ref;
     const uint8_t* cpu_bind_policy;
     const uint8_t* cpu_strategy;
+    /* DeviceShare GPU topology and partitions (deviceshare/allocator_gpu.go:72-451, allocator_gpu_helper.go
+     * :150-275; all may be NULL = no tree, no partition table, Prefer policy):
+     * dev_topo[i]: byte m = GPU minor m's place in the topology tree (GetGPUTopologyScope): high nibble the
+     *   rank of its NUMA node id (numeric order), low nibble the rank of its (NUMA node, PCIe id) pair
+     *   (PCIe ids in string order within a NUMA node); KG_GPU_NO_SCOPE = the minor is in no NUMA / PCIe scope;
+     * dev_part[i]: bits 0-7 = 1 + the node's partition table in gpu_parts (0 = none: GetGPUPartitionIndexer of
+     *   the Device annotation, else the designated table of the node's GPU model), KG_GPU_HONOR = the
+     *   GPUPartitionPolicy label is Honor, KG_GPU_TREE = the node has a topology tree (every GPU DeviceInfo
+     *   carries a Topology);
+     * gpu_parts: every partition of every table (kg_gpu_partition), grouped by table, then GPU count, then
+     *   AllocationScore ascending; within a group in the table's order (GetGPUPartitionIndexer). */
+    const uint64_t* dev_topo;
+    const uint32_t* dev_part;
+    const struct kg_gpu_partition* gpu_parts;
+    uint32_t n_gpu_parts;
 } kg_node_columns;
 
 /* Mutable node state that Assume/Forget change; used to read a snapshot back after kg_replay. */
@@ -342,6 +394,10 @@ typedef struct kg_pod_columns {
     /* Reservation owner-match class (-1 = the pod matches no reservation): pods of one class match
      * the same reservations (reservation/transformer.go:233-240, checkReservationMatchedOrIgnored). */
     const int32_t* rsv_class;
+    /* GPURequirements beyond the request (deviceshare/utils.go:516-545; NULL = none): KG_GPU_POD_* flags and
+     * the GPUPartitionSpec RingBusBandwidth in bytes (read when KG_GPU_POD_RING_BW is set). */
+    const uint32_t* dev_flags;
+    const int64_t* dev_ring_bw;
 } kg_pod_columns;
 
 /* Verify-mode outputs, [n_pods][n_nodes] row-major, caller-allocated host buffers (NULL = skip). */

@@ -11,7 +11,7 @@ from typing import Dict
 
 import numpy as np
 
-KG_ABI_VERSION = 6
+KG_ABI_VERSION = 7
 KG_LA_R = 2
 KG_NSCALAR = 2
 KG_MAX_ZONES = 4
@@ -63,7 +63,7 @@ KG_ST_NRF_MEM = 0x4
 KG_ST_NRF_EPH = 0x8
 KG_ST_NRF_SC0 = 0x10
 KG_ST_NRF_SC1 = 0x20
-KG_ST_NRF_MASK = 0xFF
+KG_ST_NRF_MASK = 0x3F
 KG_ST_LA_EXPIRED = 0x100
 KG_ST_LA_CPU = 0x200
 KG_ST_LA_MEM = 0x400
@@ -85,7 +85,37 @@ KG_ST_NUMA_CPUS = 0x800000
 KG_ST_NUMA_MASK = 0xFF7000
 KG_ST_DEV_INSUFFICIENT = 0x01000000
 KG_ST_DEV_NO_DEVICE = 0x02000000
-KG_ST_DEV_MASK = 0x03000000
+KG_ST_DEV_MASK = 0x030000C0  # 4-bit reason code: bits 24-25 low half, bits 6-7 high half
+KG_DEV_CODE_INSUFFICIENT, KG_DEV_CODE_NO_DEVICE, KG_DEV_CODE_GPU_DEVICES, KG_DEV_CODE_TOPO_SCOPED = 1, 2, 3, 4
+KG_DEV_CODE_PARTITIONED, KG_DEV_CODE_NO_PARTITION, KG_DEV_CODE_PART_COUNT, KG_DEV_CODE_NO_TREE = 5, 6, 7, 8
+KG_DEV_CODE_MULTI_SHARED = 9
+
+
+def dev_code(st: int) -> int:
+    """KG_ST_DEV_CODE: the DeviceShare reason code of a status word."""
+    return ((st >> 24) & 3) | (((st >> 6) & 3) << 2)
+
+
+def dev_status(code: int) -> int:
+    """KG_ST_DEV_MAKE"""
+    return ((code & 3) << 24) | (((code >> 2) & 3) << 6)
+
+
+# GPU topology / partitions (kg_node_columns.dev_topo / dev_part / gpu_parts, kg_pod_columns.dev_flags)
+KG_GPU_NO_SCOPE = 0xFF
+KG_GPU_HONOR = 0x100
+KG_GPU_TREE = 0x200
+KG_GPU_MAX_TABLES = 16
+KG_GPU_POD_SHARED = 0x1
+KG_GPU_POD_HONOR = 0x2
+KG_GPU_POD_RESTRICTED = 0x4
+KG_GPU_POD_RING_BW = 0x8
+KG_GPU_POD_SCOPE_SHIFT = 4
+KG_GPU_POD_TEMPLATE = 0x100
+# DeviceTopologyScopeLevel (apis/extension/device_share.go:185-190); 5 = a scope name without a level
+GPU_SCOPE_LEVEL = {"": 0, "Node": 1, "NUMANode": 2, "PCIe": 3, "Device": 4}
+GPU_PARTITION_DTYPE = np.dtype([("table", np.uint8), ("n_gpus", np.uint8), ("minors", np.uint8), ("pad_", np.uint8),
+                                ("alloc_score", np.int32), ("ring_bw", np.int64)])
 KG_ST_RSV_AFFINITY = 0x04000000
 KG_ST_RSV_NODE = 0x08000000
 KG_ST_RSV_RESERVATION = 0x10000000
@@ -162,6 +192,8 @@ class KgNodeColumns(C.Structure):
         ("cpu_topo", _pi32), ("cpu_topos", C.c_void_p), ("n_cpu_topos", C.c_uint32), ("cpu_alloc", C.c_void_p),
         ("cpu_max_ref", C.POINTER(C.c_uint8)), ("cpu_bind_policy", C.POINTER(C.c_uint8)),
         ("cpu_strategy", C.POINTER(C.c_uint8)),
+        # GPU topology tree / partition tables
+        ("dev_topo", C.POINTER(C.c_uint64)), ("dev_part", _pu32), ("gpu_parts", C.c_void_p), ("n_gpu_parts", C.c_uint32),
     ]
 
 
@@ -190,6 +222,7 @@ class KgPodColumns(C.Structure):
         ("dev_req", _p64), ("dev_count", _pu32), ("dev_keys", _pu32),
         ("quota", _pi32), ("quota_keys", _pu32),
         ("rsv_class", _pi32),
+        ("dev_flags", _pu32), ("dev_ring_bw", _p64),
     ]
 
 
@@ -333,6 +366,7 @@ NODE_STATE = (
 POD_I64 = (["req_cpu", "req_mem", "req_eph"] + _indexed("sc_req", KG_NSCALAR) + ["nz_cpu", "nz_mem"]
            + _indexed("la_est", KG_LA_R))
 POD_U32 = ["flags", "numa_policy", "dev_count", "dev_keys", "quota_keys"]
+# optional GPURequirements columns (absent: no partition / topology requirement): dev_flags uint32, dev_ring_bw int64
 POD_I32 = ["quota", "rsv_class"]
 
 Table = Dict[str, np.ndarray]
@@ -362,11 +396,15 @@ def table_len(t: Table) -> int:
 
 def concat(tables) -> Table:
     keys = tables[0].keys()
-    return {k: np.concatenate([t[k] for t in tables]) for k in keys}
+    return {k: (tables[0][k] if k in TABLE_KEYS else np.concatenate([t[k] for t in tables])) for k in keys}
+
+
+# table-level arrays of a node table (not one entry per node): shared by every row subset
+TABLE_KEYS = ("cpu_topos", "gpu_parts")
 
 
 def take(t: Table, idx) -> Table:
-    return {k: np.ascontiguousarray(v[idx]) for k, v in t.items()}
+    return {k: (v if k in TABLE_KEYS else np.ascontiguousarray(v[idx])) for k, v in t.items()}
 
 
 def _ptr(a: np.ndarray, ctype):
@@ -429,6 +467,16 @@ def node_columns(t: Table) -> KgNodeColumns:
             if k in t:
                 t[k] = np.ascontiguousarray(t[k], np.uint8)
                 setattr(s, k, t[k].ctypes.data_as(C.POINTER(C.c_uint8)))
+    if "dev_topo" in t:
+        t["dev_topo"] = np.ascontiguousarray(t["dev_topo"], np.uint64)
+        s.dev_topo = t["dev_topo"].ctypes.data_as(C.POINTER(C.c_uint64))
+    if "dev_part" in t:
+        t["dev_part"] = np.ascontiguousarray(t["dev_part"], np.uint32)
+        s.dev_part = _ptr(t["dev_part"], C.c_uint32)
+    if "gpu_parts" in t and len(t["gpu_parts"]):
+        t["gpu_parts"] = np.ascontiguousarray(t["gpu_parts"], GPU_PARTITION_DTYPE)
+        s.gpu_parts = t["gpu_parts"].ctypes.data
+        s.n_gpu_parts = len(t["gpu_parts"])
     s._keep = t  # keep the buffers alive with the struct
     return s
 
@@ -481,15 +529,18 @@ def pod_columns(t: Table) -> KgPodColumns:
     s.flags = _ptr(t["flags"], C.c_uint32)
     s.numa_policy = _ptr(t["numa_policy"], C.c_uint32)
     # config-5 columns are optional, each on its own (absent: no GPU request / quota / reservation class)
-    _check(t, [k for k in POD_U32 if k in t], np.uint32)
+    _check(t, [k for k in POD_U32 + ["dev_flags"] if k in t], np.uint32)
     _check(t, [k for k in POD_I32 if k in t], np.int32)
     if "dev_req" in t:
         t["dev_req"] = np.ascontiguousarray(t["dev_req"], np.int64)
         s.dev_req = _ptr(t["dev_req"], C.c_int64)
     for k, ct in (("dev_count", C.c_uint32), ("dev_keys", C.c_uint32), ("quota", C.c_int32),
-                  ("quota_keys", C.c_uint32), ("rsv_class", C.c_int32)):
+                  ("quota_keys", C.c_uint32), ("rsv_class", C.c_int32), ("dev_flags", C.c_uint32)):
         if k in t:
             setattr(s, k, _ptr(t[k], ct))
+    if "dev_ring_bw" in t:
+        t["dev_ring_bw"] = np.ascontiguousarray(t["dev_ring_bw"], np.int64)
+        s.dev_ring_bw = _ptr(t["dev_ring_bw"], C.c_int64)
     s._keep = t
     return s
 

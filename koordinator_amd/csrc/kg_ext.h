@@ -17,12 +17,16 @@ struct PodX {
     int32_t quota;
     uint32_t qkeys;
     int32_t cls;
+    uint32_t dflags;  // KG_GPU_POD_*
+    int64_t dbw;      // ring bus bandwidth request (KG_GPU_POD_RING_BW)
 };
 
 __device__ __forceinline__ PodX load_podx(const PodsDev& P, uint32_t j) {
     PodX x;
     x.dcount = P.dev_count ? P.dev_count[j] : 0u;
     x.dkeys = P.dev_keys ? P.dev_keys[j] : 0u;
+    x.dflags = (P.dev_flags && x.dcount) ? P.dev_flags[j] : 0u;
+    x.dbw = (P.dev_bw && (x.dflags & KG_GPU_POD_RING_BW)) ? P.dev_bw[j] : 0;
     for (int r = 0; r < DEV_R; r++) x.dreq[r] = (P.dev_req && ((x.dkeys >> r) & 1u)) ? P.dev_req[(size_t)j * DEV_R + r] : 0;
     x.quota = P.quota ? P.quota[j] : -1;
     x.qkeys = P.quota_keys ? P.quota_keys[j] : 0u;
@@ -61,44 +65,324 @@ __device__ __forceinline__ bool dev_minor_fits(const int64_t* fr, const PodX& x)
     return ok;
 }
 
-// Filter (count of minors that fit >= numberOfGPUs) + node Score before NormalizeScore.
-__device__ __forceinline__ uint32_t dev_eval(const KCfg& c, const int64_t* __restrict__ n, const DevRec* __restrict__ d,
-                                             const PodX& x, int64_t& raw) {
+// ---- GPU allocator (GPUAllocator.Allocate, deviceshare/allocator_gpu.go:72-133) ------------------------
+// Order of the reference: a partition table (allocateByPartition :177-237), then the topology tree
+// (allocateByDeviceTopology :312-451), then defaultAllocateDevices (device_allocator.go:355-437). Shared
+// resource templates (:135-159) are not on the device path (KG_GPU_POD_TEMPLATE -> KG_ST_UNSUPPORTED).
+
+struct GpuAlloc {
+    uint32_t code;  // KG_DEV_CODE_* (0 = allocated)
+    uint32_t mask;  // minors taken (when asked for)
+};
+
+// Minor sets of one table as the allocator's AllocateContext sees them (bit m = minor m < D):
+//   used  deviceUsedMinorsHash = hashDevices(getRealUsed(...)) (:59-70,83-86): minors with something used
+//         (free != total) in the table, plus `outside`: minors used on the node that the table leaves out
+//         (a reservation restore's filtered nodeDevice);
+//   total hashDevices(removeZeroDevice(deviceTotal)) (:87,112-120,200);
+//   sat   DeviceLevelContext.satisfied (:404-414): LessThanOrEqual(requestsPerGPU, free) and in total.
+struct GpuMinors {
+    uint32_t used, total, sat;
+};
+
+__device__ __forceinline__ GpuMinors gpu_minors(const DevRec* __restrict__ d, int32_t D, const PodX& x, uint32_t outside) {
+    GpuMinors g{outside, 0u, 0u};
+    for (int32_t m = 0; m < D; m++) {
+        bool any_t = false, diff = false, le = true;
+#pragma unroll
+        for (int r = 0; r < DEV_R; r++) {
+            const int64_t t = d->total[r][m], f = d->free_[r][m];
+            any_t |= t != 0;
+            diff |= f != t;
+            le &= !(((x.dkeys >> r) & 1u) && x.dreq[r] > f);
+        }
+        g.used |= diff ? 1u << m : 0u;
+        g.total |= any_t ? 1u << m : 0u;
+        g.sat |= (any_t && le) ? 1u << m : 0u;
+    }
+    return g;
+}
+
+// Σ AllocationScore of the partitions of the lowest-score group of (table tbl, n2 GPUs) that do not
+// overlap `allocated` (selectPartitionByBinPack's inner loop, allocator_gpu.go:275-284).
+__device__ __forceinline__ int64_t free_partitions(const ExtDev& e, uint32_t tbl, uint32_t n2, uint32_t allocated) {
+    const uint32_t r2 = e.part_rng[(tbl - 1u) * 9u + n2];
+    const uint32_t b2 = r2 & 0xFFFFu, e2 = r2 >> 16;
+    if (b2 >= e2) return 0;
+    const int32_t s0 = e.parts[b2].alloc_score;
+    int64_t sum = 0;
+    for (uint32_t u = b2; u < e2; u++) {
+        const kg_gpu_partition q = e.parts[u];
+        if (q.alloc_score != s0) break;
+        if ((uint32_t)q.minors & allocated) continue;
+        sum += (int64_t)q.alloc_score;
+    }
+    return sum;
+}
+
+__device__ __forceinline__ bool partition_ok(const kg_gpu_partition& q, const GpuMinors& g, const PodX& x) {
+    if ((uint32_t)q.minors & g.used) return false;
+    if ((g.total & (uint32_t)q.minors) != (uint32_t)q.minors) return false;
+    if (x.dflags & KG_GPU_POD_RING_BW) return q.ring_bw >= 0 && x.dbw <= q.ring_bw;
+    return true;
+}
+
+// allocateByPartition for a non-shared request on partition table `tbl` (1-based; 0 = none).
+// (An earlier form with the bin-pack weights in a local array indexed by the loop counter returned a wrong
+// partition on gfx950 at -O1 and -O3 while the same source was right on the host and right with a printf in
+// the loop: tools/dbg_part.hip keeps it as a reproducer; this form is checked by tests/test_gpu_alloc_kat.py.)
+__device__ __forceinline__ GpuAlloc gpu_partition(const ExtDev& e, uint32_t tbl, const PodX& x, const GpuMinors& g) {
+    if (tbl == 0u || !e.parts) return {KG_DEV_CODE_NO_PARTITION, 0u};
+    const uint32_t N = x.dcount;
+    if (N > 8u) return {KG_DEV_CODE_PART_COUNT, 0u};
+    const uint32_t rng = e.part_rng[(tbl - 1u) * 9u + N];
+    const uint32_t b = rng & 0xFFFFu, en = rng >> 16;
+    if (b >= en) return {KG_DEV_CODE_PART_COUNT, 0u};
+    const bool restricted = (x.dflags & KG_GPU_POD_RESTRICTED) != 0;
+    // the feasible partitions all come from one AllocationScore group: the first that has any (only the
+    // first group under the Restricted policy)
+    uint32_t gb = b, ge = b, nfeas = 0;
+    while (gb < en) {
+        const int32_t sg = e.parts[gb].alloc_score;
+        ge = gb;
+        while (ge < en && e.parts[ge].alloc_score == sg) {
+            nfeas += partition_ok(e.parts[ge], g, x) ? 1u : 0u;
+            ge++;
+        }
+        if (nfeas > 0u || restricted) break;
+        gb = ge;
+    }
+    if (nfeas == 0u) return {KG_DEV_CODE_PARTITIONED, 0u};
+    // selectPartitionByBinPack (:261-296): the first of the highest bin-pack scores (sort.Slice of <= 12
+    // elements is an insertion sort, stable); scoreOfNumOfGPUs 8: 10000, 4: 100, 2: 1
+    uint32_t best_mask = 0u;
+    int64_t best = -1;
+    for (uint32_t t = gb; t < ge; t++) {
+        const kg_gpu_partition q = e.parts[t];
+        if (!partition_ok(q, g, x)) continue;
+        if (nfeas == 1u) return {0u, (uint32_t)q.minors};
+        const uint32_t allocated = g.used | (uint32_t)q.minors;
+        int64_t score = 0;
+        if (N <= 8u) score += 10000 * free_partitions(e, tbl, 8u, allocated);
+        if (N <= 4u) score += 100 * free_partitions(e, tbl, 4u, allocated);
+        if (N <= 2u) score += free_partitions(e, tbl, 2u, allocated);
+        if (score > best) {
+            best = score;
+            best_mask = q.minors;
+        }
+    }
+    return {0u, best_mask};
+}
+
+struct ScopeRes {
+    uint32_t mask;
+    int32_t depth, cne;
+    int64_t score;
+};
+
+// allocateFromScope's take at one scope (:393-449): the first numberOfGPUs satisfied minors in minor
+// order, or for a shared GPU the satisfied minor of the highest scoreDevice (first on ties). The shared
+// score is scoreDevice(requestsPerGPU, free, total) with total and free swapped as the call site passes them
+// (:412): dev_least over (free, total).
+__device__ __forceinline__ ScopeRes scope_take(const KCfg& c, const DevRec* __restrict__ d, const PodX& x, uint32_t mask,
+                                               const GpuMinors& g, bool shared, int32_t depth, int32_t cne) {
+    ScopeRes r{0u, depth, cne, -1};
+    uint32_t cand = mask & g.sat;
+    if (!shared) {
+        uint32_t got = 0, pick = 0;
+        while (cand && got < x.dcount) {
+            const uint32_t m = __builtin_ctz(cand);
+            cand &= cand - 1u;
+            pick |= 1u << m;
+            got++;
+        }
+        if (got == x.dcount) r.mask = pick;
+        return r;
+    }
+    int32_t bm = -1;
+    while (cand) {
+        const uint32_t m = __builtin_ctz(cand);
+        cand &= cand - 1u;
+        int64_t t[DEV_R], f[DEV_R];
+#pragma unroll
+        for (int k = 0; k < DEV_R; k++) {
+            t[k] = d->total[k][m];
+            f[k] = d->free_[k][m];
+        }
+        const int64_t sc = dev_least(c, f, t, x.dreq);
+        if (sc > r.score || bm < 0) {
+            if (sc > r.score) r.score = sc;
+            bm = (int32_t)m;
+        }
+    }
+    if (bm >= 0) r.mask = 1u << bm;
+    return r;
+}
+
+// bestAllocateResult update over the child scopes in order (:372-387)
+__device__ __forceinline__ void scope_merge(ScopeRes& best, const ScopeRes& r, bool shared) {
+    if (!r.mask) return;
+    if (!best.mask) {
+        best = r;
+        return;
+    }
+    if (best.depth < r.depth || (best.depth == r.depth && best.cne < r.cne)) best = r;
+    if (shared && best.depth == r.depth && best.cne == r.cne && best.score < r.score) best = r;
+}
+
+// allocateFromScope over the node -> NUMA node -> PCIe tree of dev_topo (GetGPUTopologyScope,
+// allocator_gpu_helper.go:201-262: NUMA scopes in NUMA id order, PCIe scopes in PCIe id order). `level`:
+// DeviceTopologyScopeLevel of the required scope (0 = none). Depth: node 1, NUMA 2, PCIe 3.
+__device__ __forceinline__ uint32_t gpu_scope(const KCfg& c, const DevRec* __restrict__ d, int32_t D, uint64_t topo,
+                                              const PodX& x, const GpuMinors& g, int32_t level, bool shared) {
+    const uint32_t N = x.dcount;
+    const uint32_t root = D >= 32 ? ~0u : (1u << D) - 1u;
+    if ((uint32_t)__popc(root) < N) return 0u;
+    const int32_t cne1 = (root & g.used) ? 1 : 0;
+    ScopeRes best{0u, 0, 0, -1};
+    for (uint32_t q = 0; q < 15u; q++) {  // NUMA scopes in rank order
+        uint32_t qm = 0;
+        for (int32_t m = 0; m < D; m++) {
+            const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
+            if (b != KG_GPU_NO_SCOPE && (b >> 4) == q) qm |= 1u << m;
+        }
+        if (!qm) continue;
+        if ((uint32_t)__popc(qm) < N) continue;
+        const int32_t cne2 = cne1 + ((qm & g.used) ? 1 : 0);
+        ScopeRes bq{0u, 0, 0, -1};
+        for (uint32_t r = 0; r < 16u; r++) {
+            uint32_t rm = 0;
+            for (int32_t m = 0; m < D; m++) {
+                const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
+                if (b != KG_GPU_NO_SCOPE && (b >> 4) == q && (b & 15u) == r) rm |= 1u << m;
+            }
+            if (!rm || (uint32_t)__popc(rm) < N) continue;
+            if (level > 3) continue;  // a PCIe scope has no children; below the required level: nothing
+            scope_merge(bq, scope_take(c, d, x, rm, g, shared, 3, cne2 + ((rm & g.used) ? 1 : 0)), shared);
+        }
+        if (!bq.mask && level <= 2) bq = scope_take(c, d, x, qm, g, shared, 2, cne2);
+        scope_merge(best, bq, shared);
+    }
+    if (best.mask) return best.mask;
+    if (level > 1) return 0u;
+    return scope_take(c, d, x, root, g, shared, 1, cne1).mask;
+}
+
+// defaultAllocateDevices (device_allocator.go:355-437): minors by (scoreDevice desc, minor asc), the first
+// numberOfGPUs whose free resources are not all zero and cover the request. want_mask = false: only whether
+// enough minors fit (the Filter).
+__device__ __forceinline__ GpuAlloc dev_default(const KCfg& c, const DevRec* __restrict__ d, int32_t D, const PodX& x,
+                                                bool want_mask) {
+    uint32_t fit = 0;
+    for (int32_t m = 0; m < D; m++) {
+        const int64_t fr[DEV_R] = {d->free_[0][m], d->free_[1][m], d->free_[2][m]};
+        fit += dev_minor_fits(fr, x) ? 1u : 0u;
+    }
+    if (fit < x.dcount) return {KG_DEV_CODE_INSUFFICIENT, 0u};
+    if (!want_mask) return {0u, 0u};
+    int64_t sc[DEV_MINORS];
+    int ord[DEV_MINORS];
+    for (int32_t m = 0; m < D; m++) {
+        int64_t t[DEV_R], f[DEV_R];
+#pragma unroll
+        for (int r = 0; r < DEV_R; r++) {
+            t[r] = d->total[r][m];
+            f[r] = d->free_[r][m];
+        }
+        sc[m] = dev_least(c, t, f, x.dreq);
+        ord[m] = m;
+    }
+    for (int32_t a = 1; a < D; a++) {
+        const int v = ord[a];
+        int32_t b = a;
+        while (b > 0 && sc[ord[b - 1]] < sc[v]) {
+            ord[b] = ord[b - 1];
+            b--;
+        }
+        ord[b] = v;
+    }
+    uint32_t mask = 0, got = 0;
+    for (int32_t t = 0; t < D && got < x.dcount; t++) {
+        const int m = ord[t];
+        const int64_t fr[DEV_R] = {d->free_[0][m], d->free_[1][m], d->free_[2][m]};
+        if (!dev_minor_fits(fr, x)) continue;
+        mask |= 1u << m;
+        got++;
+    }
+    return {0u, mask};
+}
+
+// GPUAllocator.Allocate for a pod with a GPU request on a node with D > 0 minors. topo / part: the node's
+// ZoneRec.dev_topo / dev_part; outside: minors used on the node outside the table (0 for the node's own).
+__device__ __forceinline__ GpuAlloc gpu_allocate(const KCfg& c, const ExtDev& e, const DevRec* __restrict__ d, int32_t D,
+                                                 uint64_t topo, uint32_t part, const PodX& x, uint32_t outside,
+                                                 bool want_mask) {
+    const bool shared = (x.dflags & KG_GPU_POD_SHARED) != 0;
+    const uint32_t sfield = (x.dflags >> KG_GPU_POD_SCOPE_SHIFT) & 7u;
+    const bool required = sfield != 0u;
+    const int32_t level = sfield > 4u ? 0 : (int32_t)sfield;  // 5: a scope name without a level
+    const bool tree = (part & KG_GPU_TREE) != 0;
+    const uint32_t tbl = part & 0xFFu;
+    // partitions apply to whole GPUs; a node without table or a non-honored miss falls through
+    if (!shared && (tbl != 0u || (x.dflags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR))) {
+        const GpuMinors g = gpu_minors(d, D, x, outside);
+        const GpuAlloc pa = gpu_partition(e, tbl, x, g);
+        if (pa.code == 0u) return pa;
+        if ((x.dflags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR)) return pa;
+    }
+    if (tree) {
+        if (!(shared && x.dcount > 1u)) {
+            const GpuMinors g = gpu_minors(d, D, x, outside);
+            const uint32_t mask = gpu_scope(c, d, D, topo, x, g, level, shared);
+            if (mask) return {0u, mask};
+            return {required ? KG_DEV_CODE_TOPO_SCOPED : KG_DEV_CODE_GPU_DEVICES, 0u};
+        }
+        if (required) return {KG_DEV_CODE_MULTI_SHARED, 0u};
+    } else if (required) {
+        return {KG_DEV_CODE_NO_TREE, 0u};
+    }
+    return dev_default(c, d, D, x, want_mask);
+}
+
+__device__ __forceinline__ uint32_t dev_code_status(uint32_t code) { return code ? KG_ST_DEV_MAKE(code) : 0u; }
+
+// Filter (GPUAllocator.Allocate succeeds) + node Score before NormalizeScore.
+__device__ __forceinline__ uint32_t dev_eval(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                             const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
+                                             const PodX& x, int64_t& raw, uint32_t outside = 0u) {
     raw = 0;
     if (x.dcount == 0) return 0;  // PreFilter Skip
     const int32_t D = (int32_t)n[N_DEV_MINORS];
     if (D < 0) return 0;  // no Device object
     if (D == 0) return KG_ST_DEV_NO_DEVICE;
+    if (x.dflags & KG_GPU_POD_TEMPLATE) return KG_ST_UNSUPPORTED;
+    const GpuAlloc a = gpu_allocate(c, e, d, D, zr->dev_topo, zr->dev_part, x, outside, false);
+    if (a.code) return dev_code_status(a.code);
     int64_t T[DEV_R] = {0, 0, 0}, F[DEV_R] = {0, 0, 0};
-    uint32_t fit = 0;
     for (int32_t m = 0; m < D; m++) {
-        int64_t fr[DEV_R];
 #pragma unroll
         for (int r = 0; r < DEV_R; r++) {
-            fr[r] = d->free_[r][m];
             T[r] += d->total[r][m];
-            F[r] += fr[r];
+            F[r] += d->free_[r][m];
         }
-        fit += dev_minor_fits(fr, x) ? 1u : 0u;
     }
-    if (fit < x.dcount) return KG_ST_DEV_INSUFFICIENT;
     raw = dev_least(c, T, F, x.dreq);
     return 0;
 }
 
 // DeviceShare Filter + node Score from the record's DevSum for a pod of GPU request class cls (same
-// results as dev_eval; a pod outside the batch's classes walks the minors).
-__device__ __forceinline__ uint32_t dev_eval_sum(const KCfg& c, const int64_t* __restrict__ n, const DevRec* __restrict__ d,
-                                                 const DevSum* __restrict__ ds, const PodX& x, uint32_t cls,
-                                                 int64_t& raw) {
+// results as dev_eval; a pod outside the batch's classes runs the allocator).
+__device__ __forceinline__ uint32_t dev_eval_sum(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                                 const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
+                                                 const DevSum* __restrict__ ds, const PodX& x, uint32_t cls, int64_t& raw) {
     raw = 0;
     if (x.dcount == 0) return 0;
     const int32_t D = (int32_t)n[N_DEV_MINORS];
     if (D < 0) return 0;
     if (D == 0) return KG_ST_DEV_NO_DEVICE;
-    if (cls >= (uint32_t)DEV_CLASSES) return dev_eval(c, n, d, x, raw);
-    const uint32_t fit = (uint32_t)(ds->fit >> (4u * cls)) & 15u;
-    if (fit < x.dcount) return KG_ST_DEV_INSUFFICIENT;
+    if (cls >= (uint32_t)DEV_CLASSES) return dev_eval(c, e, n, zr, d, x, raw);
+    const uint32_t code = (uint32_t)(ds->fit >> (4u * cls)) & 15u;
+    if (code) return dev_code_status(code);
     raw = ds->score[cls];  // k_dev_sum: dev_sum_score of the class
     return 0;
 }
@@ -138,41 +422,14 @@ __device__ __forceinline__ int64_t dev_score(const KCfg& c, const DevRec* __rest
     return any ? dev_least(c, T, F, x.dreq) : 0;
 }
 
-// Reserve: minors by (per-minor score desc, minor asc), the first numberOfGPUs that fit.
-__device__ __forceinline__ uint32_t dev_choose(const KCfg& c, const int64_t* __restrict__ n, const DevRec* __restrict__ d,
+// Reserve: the minors GPUAllocator.Allocate takes on the node (0 when it fails).
+__device__ __forceinline__ uint32_t dev_choose(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                               const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
                                                const PodX& x) {
     const int32_t D = (int32_t)n[N_DEV_MINORS];
     if (x.dcount == 0 || D <= 0) return 0;
-    int64_t sc[DEV_MINORS];
-    int ord[DEV_MINORS];
-    for (int32_t m = 0; m < D; m++) {
-        int64_t t[DEV_R], f[DEV_R];
-#pragma unroll
-        for (int r = 0; r < DEV_R; r++) {
-            t[r] = d->total[r][m];
-            f[r] = d->free_[r][m];
-        }
-        sc[m] = dev_least(c, t, f, x.dreq);
-        ord[m] = m;
-    }
-    for (int32_t a = 1; a < D; a++) {
-        const int v = ord[a];
-        int32_t b = a;
-        while (b > 0 && sc[ord[b - 1]] < sc[v]) {
-            ord[b] = ord[b - 1];
-            b--;
-        }
-        ord[b] = v;
-    }
-    uint32_t mask = 0, got = 0;
-    for (int32_t t = 0; t < D && got < x.dcount; t++) {
-        const int m = ord[t];
-        const int64_t fr[DEV_R] = {d->free_[0][m], d->free_[1][m], d->free_[2][m]};
-        if (!dev_minor_fits(fr, x)) continue;
-        mask |= 1u << m;
-        got++;
-    }
-    return got < x.dcount ? 0u : mask;
+    const GpuAlloc a = gpu_allocate(c, e, d, D, zr->dev_topo, zr->dev_part, x, 0u, true);
+    return a.code ? 0u : a.mask;
 }
 
 // fillGPUTotalMem: gpu-memory from the ratio, or the ratio from gpu-memory in float64 like Go.
@@ -437,9 +694,26 @@ __device__ __forceinline__ int64_t rsv_nominate_score(const RsvPod& q, const int
 // tryAllocateFromReusable over the matched reservations that reserve GPUs, in view order (reservation.go
 // :344-410); if none fits, a pod with a reservation affinity fails there, any other pod allocates outside
 // the reservations (the view's base table).
+// Minors used on the node (free != total) that a restore table leaves out (total 0): getRealUsed's first
+// term (allocator_gpu.go:59-70), the node's own used minors outside the filtered nodeDevice.
+__device__ __forceinline__ uint32_t dev_outside_used(const DevRec* __restrict__ node, const DevRec* __restrict__ tab,
+                                                     int32_t D) {
+    uint32_t o = 0;
+    for (int32_t m = 0; m < D; m++) {
+        bool used = false, in_tab = false;
+#pragma unroll
+        for (int r = 0; r < DEV_R; r++) {
+            used |= node->free_[r][m] != node->total[r][m];
+            in_tab |= tab->total[r][m] != 0;
+        }
+        o |= (used && !in_tab) ? 1u << m : 0u;
+    }
+    return o;
+}
+
 __device__ __forceinline__ uint32_t dev_filter_view(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
-                                                    const DevRec* __restrict__ d, const RsvView& v, const PodX& x,
-                                                    bool required) {
+                                                    const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
+                                                    const RsvView& v, const PodX& x, bool required) {
     const int32_t D = (int32_t)n[N_DEV_MINORS];
     if (D < 0) return 0;  // no Device object
     if (D == 0) return KG_ST_DEV_NO_DEVICE;
@@ -449,11 +723,13 @@ __device__ __forceinline__ uint32_t dev_filter_view(const KCfg& c, const ExtDev&
         if (di < 0) continue;
         any = true;
         int64_t raw;
-        if (dev_eval(c, n, e.rdev + di, x, raw) == 0) return 0;
+        const DevRec* tab = e.rdev + di;
+        if (dev_eval(c, e, n, zr, tab, x, raw, dev_outside_used(d, tab, D)) == 0) return 0;
     }
     if (any && required) return KG_ST_DEV_RSV;
     int64_t raw;
-    return dev_eval(c, n, v.dev_base >= 0 ? e.rdev + v.dev_base : d, x, raw);
+    const DevRec* tab = v.dev_base >= 0 ? e.rdev + v.dev_base : d;
+    return dev_eval(c, e, n, zr, tab, x, raw, tab == d ? 0u : dev_outside_used(d, tab, D));
 }
 
 // ---- one pair with every plugin ---------------------------------------------------------------------
@@ -504,9 +780,9 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     const bool dev_view = (c.plugins & KG_PLUGIN_DEV) && v && x.dcount > 0;
     if (c.plugins & KG_PLUGIN_DEV) {
         if (dev_view)
-            st |= dev_filter_view(c, e, n, d, *v, x, (p.flags & KG_POD_RSV_REQUIRED) != 0);
+            st |= dev_filter_view(c, e, n, zr, d, *v, x, (p.flags & KG_POD_RSV_REQUIRED) != 0);
         else
-            st |= dev_eval(c, n, d, x, dev_raw);
+            st |= dev_eval(c, e, n, zr, d, x, dev_raw);
         if (x.dcount > 0) {
             const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (p.flags >> 16) & 15u;
             if ((c.plugins & KG_PLUGIN_NUMA) && (node_pol != KG_NUMA_NONE || pod_pol != KG_NUMA_NONE))

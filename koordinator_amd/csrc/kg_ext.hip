@@ -41,13 +41,15 @@ __device__ __forceinline__ int32_t wmax_i32(int32_t v) {
 __device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) { return e.dev ? e.dev + rec : nullptr; }
 
 // DevSum of every record for the pod batch's GPU request classes (one thread per record).
-__global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nodes, const DevRec* __restrict__ devs,
-                                                 uint32_t n_nodes, const DevClass* __restrict__ cls, uint32_t n_cls,
-                                                 KCfg cfg, DevSum* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                 const DevRec* __restrict__ devs, uint32_t n_nodes,
+                                                 const DevClass* __restrict__ cls, uint32_t n_cls, KCfg cfg, ExtDev e,
+                                                 DevSum* __restrict__ out) {
     const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
     if (rec >= n_nodes) return;
     const DevRec& d = devs[rec];
     const int32_t D = (int32_t)nodes[rec].v[N_DEV_MINORS];
+    const ZoneRec& zr = zones[rec];
     DevSum o;
     o.fit = 0;
     for (int r = 0; r < DEV_R; r++) {
@@ -63,13 +65,13 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
     for (uint32_t k = 0; k < n_cls; k++) {
         PodX x{};
         x.dkeys = cls[k].dkeys;
+        x.dcount = cls[k].dcount;
+        x.dflags = cls[k].dflags;
+        x.dbw = cls[k].dbw;
         for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
-        uint64_t fit = 0;
-        for (int32_t m = 0; m < D; m++) {
-            const int64_t fr[DEV_R] = {d.free_[0][m], d.free_[1][m], d.free_[2][m]};
-            fit += dev_minor_fits(fr, x) ? 1u : 0u;
-        }
-        o.fit |= fit << (4u * k);
+        // D <= 0 and template pods never read the nibble (dev_eval_sum decides them first)
+        const uint64_t code = D > 0 ? gpu_allocate(cfg, e, &d, D, zr.dev_topo, zr.dev_part, x, 0u, false).code : 0u;
+        o.fit |= code << (4u * k);
     }
     for (uint32_t k = 0; k < 16u; k++) o.score[k] = 0;
     for (uint32_t k = 0; k < n_cls; k++) {  // the node Score per class (every pair of the class reads it)
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
                     const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
                     int64_t raw = 0;
                     uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
-                    if (!st) st |= dev_eval_sum(cfg, n, dev_of(e, rec), e.dsum + rec, px, dcls, raw);
+                    if (!st) st |= dev_eval_sum(cfg, e, n, zones + rec, dev_of(e, rec), e.dsum + rec, px, dcls, raw);
                     if (!st) dmax = max(dmax, (uint32_t)raw);
                     pv = 0x80000000u | (st ? 0u : (0x40000000u | ((uint32_t)(bk >> 32) << 7) | (uint32_t)raw));
                 }
@@ -409,7 +411,8 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
                 int64_t s_dev = 0;
                 if ((cfg.plugins & KG_PLUGIN_DEV) && !st)  // only the key's zero-ness matters once st != 0
-                    st |= dev_eval_sum(cfg, n, dev_of(e, rec), e.dsum + rec, px, dcls, s_dev);
+                    st |= dev_eval_sum(cfg, e, n, zones + rec, dev_of(e, rec), e.dsum + rec, px, dcls, s_dev);
+                unsup |= st & KG_ST_UNSUPPORTED;  // a shared-resource-template pod
                 const int64_t tot = total_fb(cfg, bk, s_dev, dm, mag, g, pf);
                 topk_ins<K>(top, st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)));
                 continue;
@@ -541,7 +544,7 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
             const PodX qx = load_podx(pods, step - 1);
             apply_assume(cfg, nodes[i].v, zones + i, q, prev_zone, 1);
             if ((cfg.plugins & KG_PLUGIN_DEV) && qx.dcount > 0) {
-                const uint32_t mask = dev_choose(cfg, nodes[i].v, devs + i, qx);
+                const uint32_t mask = dev_choose(cfg, e, nodes[i].v, zones + i, devs + i, qx);
                 dev_apply(devs + i, mask, qx, 1);
                 minors[step - 1] = mask;
             }
@@ -617,7 +620,8 @@ template <bool EXACT>
 __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, DevRec* __restrict__ devs, ExtDev e,
                              PodsDev pods, uint32_t pod, uint32_t rec, int32_t zone_in, uint32_t minors_in, int64_t sign,
                              KCfg cfg, int32_t* __restrict__ out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (blockIdx.x != 0) return;
+    // the whole wave evaluates (uniform work on a full exec mask), lane 0 applies
     const PodV q = load_pod(pods, pod);
     const PodX qx = load_podx(pods, pod);
     int64_t* n = nodes[rec].v;
@@ -628,14 +632,16 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
         const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, 0u);
         zone = r.status ? -1 : r.zone;
         if (zone_reserve_fails(zone)) {  // the NodeNUMAResource Reserve fails: nothing is applied
-            if (out) {
+            if (out && threadIdx.x == 0) {
                 out[0] = zone;
                 out[1] = 0;
             }
             return;
         }
-        mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, n, devs + rec, qx) : 0u;
+        mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, e, n, zones + rec, devs + rec, qx) : 0u;
     }
+    __syncthreads();  // every lane has read the state before lane 0 changes it
+    if (threadIdx.x != 0) return;
     apply_assume(cfg, n, zones + rec, q, zone, sign);
     if ((cfg.plugins & KG_PLUGIN_DEV) && devs && qx.dcount > 0) dev_apply(devs + rec, mask, qx, sign);
     if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
@@ -691,7 +697,7 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
                 const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, qst);
                 st = r.status;
                 zone = r.zone;
-                if (!st && (cfg.plugins & KG_PLUGIN_DEV) && devs) mask = dev_choose(cfg, n, devs + rec, qx);
+                if (!st && (cfg.plugins & KG_PLUGIN_DEV) && devs) mask = dev_choose(cfg, e, n, zones + rec, devs + rec, qx);
             } else {
                 const PairOut r = eval_pair<EXACT>(cfg, n, zones + rec, q);
                 st = r.status;
@@ -796,11 +802,11 @@ hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t 
     return hipGetLastError();
 }
 
-hipError_t launch_dev_sum(const NodeRec* nodes, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
-                          const KCfg& cfg,
+hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
+                          const KCfg& cfg, const ExtDev& e,
                           DevSum* out, hipStream_t s) {
     if (n_nodes == 0) return hipSuccess;
-    k_dev_sum<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, devs, n_nodes, cls, n_cls, cfg, out);
+    k_dev_sum<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, zones, devs, n_nodes, cls, n_cls, cfg, e, out);
     return hipGetLastError();
 }
 

@@ -146,8 +146,8 @@ inline void ext_part2_grid(uint32_t special_est, uint32_t pod_blocks, uint32_t* 
     *n_chunks = (est + *chunk - 1) / *chunk;
 }
 hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, hipStream_t s);
-hipError_t launch_dev_sum(const NodeRec* nodes, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
-                          const KCfg& cfg,
+hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
+                          const KCfg& cfg, const ExtDev& e,
                           DevSum* out, hipStream_t s);
 hipError_t launch_scatter_rows(const void* stage, const uint32_t* pos, uint32_t n, bool dev, NodeRec* nodes,
                                ZoneRec* zones, DevRec* devs, hipStream_t s);

@@ -131,8 +131,12 @@ struct alignas(64) ZoneRec {
     int32_t cpu_free_full;   // of those, the CPUs of cores whose every CPU is free (required FullPCPUs)
     int32_t cpu_free_cores;  // cores with a free CPU (required SpreadByPCPUs: one CPU per core)
     int32_t cpu_allocated;   // CPUs with RefCount > 0 (cpuset_alloc_milli / 1000)
+    // DeviceShare GPU topology of the node (static; kg_node_columns.dev_topo / dev_part): per minor
+    // (NUMA rank << 4 | PCIe rank) or KG_GPU_NO_SCOPE, and the partition table / KG_GPU_HONOR / KG_GPU_TREE
+    uint64_t dev_topo;
+    uint32_t dev_part;
 };
-static_assert(sizeof(ZoneRec) == 640, "the cpuset fields live in ZoneRec's tail padding");
+static_assert(sizeof(ZoneRec) == 640, "the cpuset and GPU topology fields live in ZoneRec's tail padding");
 // ZoneRec.cpu_meta: bits 0-7 maxRefCount, 8-9 node CPU bind policy (KG_NODE_CPU_BIND_*), 10 NUMA allocate
 // strategy, 11-14 CPUs per core
 constexpr uint32_t CPU_META_BIND_SHIFT = 8, CPU_META_STRATEGY_SHIFT = 10, CPU_META_CPC_SHIFT = 11;
@@ -313,6 +317,8 @@ struct PodsDev {
     const int64_t* la_est1;
     const uint32_t* flags;
     const uint8_t* dev_cls;     // GPU request class of the pod (DevSum.fit nibble), DEV_CLASSES = none
+    const uint32_t* dev_flags;  // KG_GPU_POD_*
+    const int64_t* dev_bw;      // ring bus bandwidth request (KG_GPU_POD_RING_BW)
 };
 
 // Scoring / filtering configuration passed by value to every kernel.
@@ -344,16 +350,18 @@ struct alignas(64) DevRec {
 };
 
 // Per-(pod batch, node record) DeviceShare summary (k_dev_sum): the pod batch's distinct GPU requests
-// (at most DEV_CLASSES, host-assigned per pod) each get a nibble of `fit` holding the number of the
-// record's minors that fit one instance (defaultAllocateDevices' predicate), and the minor sums the
-// node Score reads, so that the config-5 fast path does not walk the minors per pair.
+// (at most DEV_CLASSES, host-assigned per pod) each get a nibble of `fit` holding the GPU allocator's
+// outcome on the record (gpu_allocate's reason code), and the minor sums the node Score reads, so that
+// the config-5 fast path does not walk the minors per pair.
 constexpr int DEV_CLASSES = 15;
+// A GPU request class: everything the allocator reads of a pod (GPURequirements).
 struct DevClass {
     int64_t dreq[DEV_R];
-    uint32_t dkeys, pad_;
+    uint32_t dkeys, dcount, dflags, pad_;
+    int64_t dbw;
 };
 struct alignas(16) DevSum {
-    uint64_t fit;
+    uint64_t fit;  // per class a nibble: the GPU allocator's DeviceShare reason code (0 = the pod fits)
     int64_t T[DEV_R], F[DEV_R];
     double rcp[DEV_R];  // 1 / T (least_req's exact-quotient path)
     uint8_t score[16];  // per class: the node Score (scoreNode over the minor sums, 0..100) of one instance
@@ -407,6 +415,10 @@ struct ExtDev {
     // raw score. pairs_row0: select-list row of stats row 0. nullptr = pass 2 evaluates every pair.
     uint32_t* pairs;
     uint32_t pairs_ld, pairs_row0;
+    // GPU partition tables (kg_gpu_partition, grouped by table / GPU count / AllocationScore) and per (table,
+    // GPU count) the entry range: part_rng[table * 9 + n] = begin | end << 16
+    const kg_gpu_partition* parts;
+    const uint32_t* part_rng;
 };
 
 }  // namespace kg

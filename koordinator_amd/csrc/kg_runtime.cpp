@@ -116,9 +116,15 @@ struct kg_snap {
     std::vector<kg_cpu_alloc> h_cpu_alloc;
     bool has_cpu = false;   // the snapshot carries CPU topologies
     bool node_bind = false; // some node has a CPU bind policy (every pod with a cpu request binds there)
+    // GPU partition tables (kg_node_columns.gpu_parts): entries and per (table, GPU count) ranges
+    kg_gpu_partition* d_parts = nullptr;
+    uint32_t* d_part_rng = nullptr;  // [KG_GPU_MAX_TABLES * 9]
+    uint32_t n_gpu_tables = 0;
     bool ext() const { return (cfg.plugins & KG_PLUGIN_EXT) != 0; }
     ExtDev ext_dev() const {
         ExtDev e{};
+        e.parts = n_gpu_tables ? d_parts : nullptr;
+        e.part_rng = d_part_rng;
         e.dev = d_dev;
         e.qlim = d_qlim;
         e.qstate = d_qstate;
@@ -146,7 +152,7 @@ struct kg_pods {
     uint32_t* d_xlist = nullptr;  // config-5 pods through k_ext_select (batch positions)
     uint32_t* d_stat_list = nullptr;  // pods carrying a GPU request or a reservation class
     int64_t* d_dev_req = nullptr;     // [n][KG_DEV_R]
-    uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32): 5 x n
+    uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32), dev_flags: 6 x n
     uint8_t* d_dcls = nullptr;        // GPU request class per pod (DevSum nibble), DEV_CLASSES = none
     DevClass* d_dclass = nullptr;
     uint32_t n_dclass = 0;
@@ -491,6 +497,11 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
                         (long long)v[N_CPUSET], zr->cpu_allocated);
     }
     if (zr->status >> (2 * KG_MAX_ZONES)) return fail(ctx, KG_INVALID_ARG, "node %u: zone status 0x%x", i, zr->status);
+    // GPU topology tree / partition table (static)
+    zr->dev_topo = s->dev_topo ? s->dev_topo[i] : ~0ull;
+    zr->dev_part = s->dev_part ? s->dev_part[i] : 0u;
+    if ((zr->dev_part & ~(0xFFu | KG_GPU_HONOR | KG_GPU_TREE)) || (zr->dev_part & 0xFFu) > KG_GPU_MAX_TABLES)
+        return fail(ctx, KG_INVALID_ARG, "node %u: dev_part 0x%x", i, zr->dev_part);
     derive_node(*rec, *zr);
     return KG_OK;
 }
@@ -779,6 +790,50 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
 
 static const char* cpu_topo_problem(const kg_cpu_topo& t);
 
+// Replace the GPU partition tables (kg_node_columns.gpu_parts; GetGPUPartitionIndexer order) on the device.
+static kg_status upload_gpu_parts(kg_snap* s, const kg_node_columns* cols) {
+    kg_ctx* ctx = s->ctx;
+    const uint32_t n = cols->gpu_parts ? cols->n_gpu_parts : 0u;
+    if (n > KG_GPU_MAX_PARTS) return fail(ctx, KG_UNSUPPORTED, "%u GPU partitions > %d", n, KG_GPU_MAX_PARTS);
+    std::vector<uint32_t> rng(KG_GPU_MAX_TABLES * 9, 0u);
+    uint32_t tables = 0;
+    for (uint32_t t = 0; t < n; t++) {
+        const kg_gpu_partition& q = cols->gpu_parts[t];
+        if (q.table >= KG_GPU_MAX_TABLES || q.n_gpus < 1 || q.n_gpus > 8)
+            return fail(ctx, KG_INVALID_ARG, "GPU partition %u: table %u, %u GPUs", t, q.table, q.n_gpus);
+        const uint32_t key = q.table * 9u + q.n_gpus;
+        if (t > 0) {
+            const kg_gpu_partition& pq = cols->gpu_parts[t - 1];
+            const uint32_t pkey = pq.table * 9u + pq.n_gpus;
+            if (pkey > key || (pkey == key && pq.alloc_score > q.alloc_score))
+                return fail(ctx, KG_INVALID_ARG, "GPU partition %u: not grouped by table / GPU count / score", t);
+            if (pkey != key && (rng[key] >> 16) != 0) return fail(ctx, KG_INVALID_ARG, "GPU partition %u: group split", t);
+        }
+        if ((rng[key] >> 16) == 0) rng[key] = t;
+        rng[key] = (rng[key] & 0xFFFFu) | ((t + 1u) << 16);
+        tables = std::max(tables, (uint32_t)q.table + 1u);
+    }
+    if (!s->d_part_rng) HIP_TRY(ctx, hipMalloc(&s->d_part_rng, sizeof(uint32_t) * KG_GPU_MAX_TABLES * 9));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_part_rng, rng.data(), sizeof(uint32_t) * rng.size(), hipMemcpyHostToDevice, ctx->stream));
+    if (n) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        hipFree(s->d_parts);
+        s->d_parts = nullptr;
+        HIP_TRY(ctx, hipMalloc(&s->d_parts, sizeof(kg_gpu_partition) * n));
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_parts, cols->gpu_parts, sizeof(kg_gpu_partition) * n, hipMemcpyHostToDevice, ctx->stream));
+    }
+    s->n_gpu_tables = tables;
+    return KG_OK;
+}
+
+// Node rows name partition tables that exist.
+static kg_status check_gpu_tables(kg_ctx* ctx, const kg_node_columns* cols, uint32_t n_rows, uint32_t tables) {
+    for (uint32_t i = 0; cols->dev_part && i < n_rows; i++)
+        if ((cols->dev_part[i] & 0xFFu) > tables)
+            return fail(ctx, KG_INVALID_ARG, "node row %u: GPU partition table %u of %u", i, cols->dev_part[i] & 0xFFu, tables);
+    return KG_OK;
+}
+
 // Replace the CPU topology table (kg_node_columns.cpu_topos) on the device.
 static kg_status upload_cpu_topos(kg_snap* s, const kg_node_columns* cols, uint32_t n_rows) {
     kg_ctx* ctx = s->ctx;
@@ -820,6 +875,13 @@ kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
         if (cols->cpu_alloc) cpus[i] = cols->cpu_alloc[i];
         else std::memset(&cpus[i], 0, sizeof(kg_cpu_alloc));
     }
+    {
+        uint32_t tables = 0;
+        for (uint32_t t = 0; cols->gpu_parts && t < cols->n_gpu_parts; t++)
+            tables = std::max(tables, (uint32_t)cols->gpu_parts[t].table + 1u);
+        kg_status st = check_gpu_tables(ctx, cols, s->n, tables);
+        if (st != KG_OK) return st;
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     s->node_bind = false;
     if (cpu) {
@@ -827,6 +889,10 @@ kg_status kg_snapshot_upload(kg_snap* s, const kg_node_columns* cols) {
         if (st != KG_OK) return st;
     } else {
         s->has_cpu = false;
+    }
+    if (dev) {
+        kg_status st = upload_gpu_parts(s, cols);
+        if (st != KG_OK) return st;
     }
     place_records(s, recs, zrs, dev ? &devs : nullptr, cpu ? &cpus : nullptr);
     HIP_TRY(ctx, hipMemcpyAsync(s->d_pos, s->pos.data(), sizeof(uint32_t) * s->n, hipMemcpyHostToDevice, ctx->stream));
@@ -866,6 +932,10 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
         moved |= node_class(recs[k]) != (s->pos[rows[k]] < s->n0 ? 0u : 1u);
     }
     if (moved && s->n_views) return fail(ctx, KG_UNSUPPORTED, "row update moves a record while reservation views are uploaded");
+    {
+        kg_status st = check_gpu_tables(ctx, cols, n, s->n_gpu_tables);  // rows name the uploaded tables
+        if (st != KG_OK) return st;
+    }
     const bool cpu = s->has_cpu;
     if (cpu && !(cols->cpu_topo && cols->cpu_topos))
         return fail(ctx, KG_INVALID_ARG, "the snapshot carries CPU topologies: row updates must carry them too");
@@ -1031,6 +1101,8 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_zsel);
     hipFree(s->d_pos);
     hipFree(s->d_dev);
+    hipFree(s->d_parts);
+    hipFree(s->d_part_rng);
     hipFree(s->d_qlim);
     hipFree(s->d_qstate);
     hipFree(s->d_views);
@@ -1061,7 +1133,7 @@ namespace {
 // first; the config-5 regions after `ext` are copied only when the batch carries config-5 data (else they
 // are set on the device). The layout depends on n only, so cached replay graphs keyed on n stay valid.
 struct PodLayout {
-    size_t cols, flags, order, pmap, ext, xlist, stat, dev_req, xcols, dclass, dcls, total;
+    size_t cols, flags, order, pmap, ext, xlist, stat, dev_req, dev_bw, xcols, dclass, dcls, total;
 };
 
 PodLayout pod_layout(uint32_t n) {
@@ -1080,7 +1152,8 @@ PodLayout pod_layout(uint32_t n) {
     L.xlist = take(sizeof(uint32_t) * (size_t)n);
     L.stat = take(sizeof(uint32_t) * (size_t)n);
     L.dev_req = take(sizeof(int64_t) * DEV_R * (size_t)n);
-    L.xcols = take(sizeof(uint32_t) * 5 * (size_t)n);
+    L.dev_bw = take(sizeof(int64_t) * (size_t)n);
+    L.xcols = take(sizeof(uint32_t) * 6 * (size_t)n);
     L.dclass = take(sizeof(DevClass) * DEV_CLASSES);
     L.dcls = take((size_t)n);
     L.total = o;
@@ -1117,6 +1190,8 @@ void pod_views(kg_pods* p, uint32_t n) {
     v.quota = reinterpret_cast<const int32_t*>(p->d_xcols + 2 * (size_t)n);
     v.quota_keys = p->d_xcols + 3 * (size_t)n;
     v.rsv_class = reinterpret_cast<const int32_t*>(p->d_xcols + 4 * (size_t)n);
+    v.dev_flags = p->d_xcols + 5 * (size_t)n;
+    v.dev_bw = reinterpret_cast<const int64_t*>(d + L.dev_bw);
     v.dev_cls = p->d_dcls;
 }
 
@@ -1177,6 +1252,11 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             if (cols->dev_req[(size_t)j * DEV_R + r] < 0) return fail(ctx, KG_INVALID_ARG, "pod %u: negative GPU request", j);
         const int32_t cls = cols->rsv_class ? cols->rsv_class[j] : -1;
         if (cls >= RSV_MAX_CLASSES) return fail(ctx, KG_UNSUPPORTED, "pod %u: reservation class %d >= %d", j, cls, RSV_MAX_CLASSES);
+        const uint32_t df = cols->dev_flags ? cols->dev_flags[j] : 0u;
+        if ((df & ~0x17Fu) || ((df >> KG_GPU_POD_SCOPE_SHIFT) & 7u) > 5u)
+            return fail(ctx, KG_INVALID_ARG, "pod %u: GPU requirement flags 0x%x", j, df);
+        if ((df & KG_GPU_POD_RING_BW) && !cols->dev_ring_bw)
+            return fail(ctx, KG_INVALID_ARG, "pod %u: KG_GPU_POD_RING_BW without dev_ring_bw", j);
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     // the previous upload's copy has completed (every upload ends with a stream synchronisation), so the
@@ -1234,7 +1314,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     const uint32_t n_fast = cnt[0] + cnt[1] + cnt[2];
     // config-5 columns (absent columns: no GPU request, no quota, no reservation class)
     const bool ext_cols = cols->dev_req || cols->dev_count || cols->dev_keys || cols->quota || cols->quota_keys ||
-                          cols->rsv_class;
+                          cols->rsv_class || cols->dev_flags;
     uint32_t* xc = reinterpret_cast<uint32_t*>(h + L.xcols);
     uint32_t* pmap = reinterpret_cast<uint32_t*>(h + L.pmap);
     uint32_t* xlist = reinterpret_cast<uint32_t*>(h + L.xlist);
@@ -1247,19 +1327,27 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         np = n;
     } else {
         int64_t* dreq = reinterpret_cast<int64_t*>(h + L.dev_req);
+        int64_t* dbw = reinterpret_cast<int64_t*>(h + L.dev_bw);
         uint8_t* dcls = h + L.dcls;
         for (uint32_t j = 0; j < n; j++) {
             const uint32_t cntj = cols->dev_count ? cols->dev_count[j] : 0u;
             const uint32_t keys = cols->dev_keys ? cols->dev_keys[j] : 0u;
+            const uint32_t dfl = cols->dev_flags ? cols->dev_flags[j] : 0u;
             for (int r = 0; r < DEV_R; r++) dreq[(size_t)j * DEV_R + r] = cols->dev_req ? cols->dev_req[(size_t)j * DEV_R + r] : 0;
+            dbw[j] = (dfl & KG_GPU_POD_RING_BW) ? cols->dev_ring_bw[j] : 0;
             dcls[j] = (uint8_t)DEV_CLASSES;
-            if (cntj > 0) {  // GPU request class: the per-instance request the minor predicate and the Score read
+            if (cntj > 0 && !(dfl & KG_GPU_POD_TEMPLATE)) {  // GPU request class: everything the allocator and the Score read
                 DevClass c{};
                 c.dkeys = keys & 7u;
+                c.dcount = cntj;
+                c.dflags = dfl;
+                c.dbw = dbw[j];
                 for (int r = 0; r < DEV_R; r++) c.dreq[r] = dreq[(size_t)j * DEV_R + r];
                 size_t k = 0;
                 while (k < classes.size() && !(classes[k].dkeys == c.dkeys && classes[k].dreq[0] == c.dreq[0] &&
-                                               classes[k].dreq[1] == c.dreq[1] && classes[k].dreq[2] == c.dreq[2]))
+                                               classes[k].dreq[1] == c.dreq[1] && classes[k].dreq[2] == c.dreq[2] &&
+                                               classes[k].dcount == c.dcount && classes[k].dflags == c.dflags &&
+                                               classes[k].dbw == c.dbw))
                     k++;
                 if (k == classes.size() && classes.size() < (size_t)DEV_CLASSES) classes.push_back(c);
                 if (k < classes.size()) dcls[j] = (uint8_t)k;
@@ -1271,6 +1359,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             xc[2 * (size_t)n + j] = (uint32_t)q;
             xc[3 * (size_t)n + j] = cols->quota_keys ? cols->quota_keys[j] : 0u;
             xc[4 * (size_t)n + j] = (uint32_t)cls;
+            xc[5 * (size_t)n + j] = dfl;
             if (cntj > 0 || cls >= 0) stat[ns++] = j;
             if (cntj == 0 && cls < 0 && !(f[j] & KG_POD_RSV_REQUIRED)) pmap[np++] = j;
             else xlist[nx++] = j;
@@ -1304,8 +1393,9 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     if (bytes) HIP_TRY(ctx, hipMemcpyAsync(p->d_in, h, bytes, hipMemcpyHostToDevice, ctx->stream));
     if (n && !ext_copy) {
         HIP_TRY(ctx, hipMemsetAsync(p->d_dev_req, 0, sizeof(int64_t) * DEV_R * n, ctx->stream));
-        const int xdef[5] = {0, 0, 0xFF, 0, 0xFF};  // -1 quota / class
-        for (int c = 0; c < 5; c++)
+        HIP_TRY(ctx, hipMemsetAsync(const_cast<int64_t*>(p->dev.dev_bw), 0, sizeof(int64_t) * n, ctx->stream));
+        const int xdef[6] = {0, 0, 0xFF, 0, 0xFF, 0};  // -1 quota / class
+        for (int c = 0; c < 6; c++)
             HIP_TRY(ctx, hipMemsetAsync(p->d_xcols + (size_t)c * n, xdef[c], sizeof(uint32_t) * n, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(p->d_dcls, DEV_CLASSES, n, ctx->stream));
     }
@@ -1478,7 +1568,8 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
         HIP_TRY(ctx, hipMalloc(&p->d_devsum, sizeof(DevSum) * std::max<uint32_t>(s->n, 1)));
         p->devsum_cap = s->n;
     }
-    HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_dev, s->n, p->d_dclass, p->n_dclass, s->kcfg, p->d_devsum, ctx->stream));
+    HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(), p->d_devsum,
+                                ctx->stream));
     e.dsum = p->d_devsum;
     return KG_OK;
 }

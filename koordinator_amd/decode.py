@@ -1216,3 +1216,132 @@ def quota_keys(pods: abi.Table, max_keys: np.ndarray) -> np.ndarray:
     q = pods["quota"]
     mk = np.where(q >= 0, max_keys[np.maximum(q, 0)], 0)
     return (have & mk).astype(np.uint32)
+
+
+# ---- DeviceShare GPU topology tree and partition tables (deviceshare/allocator_gpu.go, allocator_gpu_helper.go)
+
+ANN_GPU_PARTITIONS = "scheduling.koordinator.sh/gpu-partitions"          # Device: GPUPartitionTable JSON
+ANN_GPU_PARTITION_SPEC = "scheduling.koordinator.sh/gpu-partition-spec"  # Pod: GPUPartitionSpec JSON
+ANN_DEVICE_ALLOCATE_HINT = "scheduling.koordinator.sh/device-allocate-hint"
+LABEL_GPU_PARTITION_POLICY = "node.koordinator.sh/gpu-partition-policy"
+LABEL_GPU_VENDOR = "node.koordinator.sh/gpu-vendor"
+LABEL_GPU_MODEL = "node.koordinator.sh/gpu-model"
+
+
+def _hopper_table() -> Dict[int, List[dict]]:
+    """GPUPartitionIndexOfNVIDIAHopper (allocator_gpu_helper.go:28-147): NVLink pairs / quads / all eight, every
+    partition and group of AllocationScore 1."""
+    return {1: [{"minors": [m], "allocationScore": 1} for m in range(8)],
+            2: [{"minors": [2 * k, 2 * k + 1], "allocationScore": 1} for k in range(4)],
+            4: [{"minors": [0, 1, 2, 3], "allocationScore": 1}, {"minors": [4, 5, 6, 7], "allocationScore": 1}],
+            8: [{"minors": list(range(8)), "allocationScore": 1}]}
+
+
+def gpu_partition_table(device: Optional[dict], node: dict) -> Tuple[Optional[Dict[int, List[dict]]], bool]:
+    """(GPUPartitionTable, honor) of a node: the Device annotation's table with the Device's GPUPartitionPolicy
+    label (device_cache.go:536-545, apiext.GetGPUPartitionTable / GetGPUPartitionPolicy), else the designated
+    table of the node's GPU model with the Node's label (GetDesignatedGPUPartitionIndexer,
+    allocator_gpu_helper.go:149-162; an empty vendor counts as nvidia)."""
+    meta = (device or {}).get("metadata", {})
+    raw = (meta.get("annotations") or {}).get(ANN_GPU_PARTITIONS)
+    if raw:
+        table = {int(k): v for k, v in json.loads(raw).items()}
+        honor = (meta.get("labels") or {}).get(LABEL_GPU_PARTITION_POLICY) == "Honor"
+        return table, honor
+    labels = node.get("metadata", {}).get("labels") or {}
+    honor = labels.get(LABEL_GPU_PARTITION_POLICY) == "Honor"
+    if labels.get(LABEL_GPU_VENDOR, "") in ("", "nvidia") and labels.get(LABEL_GPU_MODEL) in ("H100", "H800", "H20"):
+        return _hopper_table(), honor
+    return None, honor
+
+
+def gpu_partition_entries(table: Dict[int, List[dict]], index: int) -> List[tuple]:
+    """kg_gpu_partition rows of one table in GetGPUPartitionIndexer order (allocator_gpu_helper.go:165-199):
+    per GPU count, AllocationScore groups ascending, each group in the table's order. RingBusBandwidth in
+    bytes (-1 = none)."""
+    rows = []
+    for n in sorted(table):
+        parts = table[n]
+        for score in sorted({int(p.get("allocationScore", 0)) for p in parts}):
+            for p in parts:
+                if int(p.get("allocationScore", 0)) != score:
+                    continue
+                mask = 0
+                for m in p["minors"]:
+                    mask |= 1 << int(m)
+                bw = p.get("ringBusBandwidth")
+                rows.append((index, int(n), mask, 0, score, -1 if bw is None else value(bw)))
+    return rows
+
+
+class GpuPartitionTables:
+    """Distinct partition tables of a snapshot (kg_node_columns.gpu_parts) and the dev_part of each node."""
+
+    def __init__(self):
+        self._index: Dict[str, int] = {}
+        self._rows: List[tuple] = []
+
+    def add(self, table: Optional[Dict[int, List[dict]]]) -> int:
+        """1 + the table's index (0 for None)."""
+        if table is None:
+            return 0
+        key = json.dumps({str(k): v for k, v in sorted(table.items())}, sort_keys=True)
+        if key not in self._index:
+            if len(self._index) >= abi.KG_GPU_MAX_TABLES:
+                raise Unsupported(f"more than {abi.KG_GPU_MAX_TABLES} distinct GPU partition tables")
+            self._index[key] = len(self._index)
+            self._rows += gpu_partition_entries(table, self._index[key])
+        return 1 + self._index[key]
+
+    def array(self) -> np.ndarray:
+        return np.array(self._rows, dtype=abi.GPU_PARTITION_DTYPE)
+
+
+def gpu_topology(gpu_infos: Sequence[dict]) -> Tuple[int, bool]:
+    """dev_topo of a node from its GPU DeviceInfos (minor, topology {nodeID, pcieID}) and whether the node has a
+    topology tree: GetGPUTopologyScope (allocator_gpu_helper.go:201-262) returns nil without infos or when one
+    lacks a Topology. Byte m = (rank of the NUMA node id) << 4 | rank of (NUMA node id, PCIe id), PCIe ids in
+    string order within a NUMA node (the scopes' sort order)."""
+    if not gpu_infos or any(d.get("topology") is None for d in gpu_infos):
+        return (1 << 64) - 1, False
+    numa_ids = sorted({int(d["topology"].get("nodeID", 0)) for d in gpu_infos})
+    pairs = sorted({(int(d["topology"].get("nodeID", 0)), str(d["topology"].get("pcieID", ""))) for d in gpu_infos})
+    if len(numa_ids) > 15 or len(pairs) > 16:
+        raise Unsupported("GPU topology with more than 15 NUMA nodes or 16 PCIe switches")
+    topo = (1 << 64) - 1
+    for d in gpu_infos:
+        m = int(d.get("minor", 0))
+        if m >= abi.KG_DEV_MINORS:
+            raise Unsupported(f"GPU minor {m} >= {abi.KG_DEV_MINORS}")
+        t = d["topology"]
+        q = numa_ids.index(int(t.get("nodeID", 0)))
+        r = pairs.index((int(t.get("nodeID", 0)), str(t.get("pcieID", ""))))
+        topo &= ~(0xFF << (8 * m))
+        topo |= ((q << 4) | r) << (8 * m)
+    return topo, True
+
+
+def gpu_pod_flags(pod: dict, shared: bool) -> Tuple[int, int]:
+    """(dev_flags, dev_ring_bw) of a GPU pod: parseGPURequirements (deviceshare/utils.go:516-545) beyond the
+    request: GPUPartitionSpec (apiext.GetGPUPartitionSpec: present -> honor, AllocatePolicy Restricted,
+    RingBusBandwidth) and the gpu DeviceHint's RequiredTopologyScope."""
+    ann = pod.get("metadata", {}).get("annotations") or {}
+    flags = abi.KG_GPU_POD_SHARED if shared else 0
+    bw = 0
+    raw = ann.get(ANN_GPU_PARTITION_SPEC)
+    if raw is not None:
+        spec = json.loads(raw)
+        flags |= abi.KG_GPU_POD_HONOR
+        if spec.get("allocatePolicy", "BestEffort") == "Restricted":
+            flags |= abi.KG_GPU_POD_RESTRICTED
+        if spec.get("ringBusBandwidth") is not None:
+            flags |= abi.KG_GPU_POD_RING_BW
+            bw = value(spec["ringBusBandwidth"])
+    raw = ann.get(ANN_DEVICE_ALLOCATE_HINT)
+    if raw is not None:
+        hint = (json.loads(raw) or {}).get("gpu") or {}
+        scope = hint.get("requiredTopologyScope", "")
+        if scope:
+            level = abi.GPU_SCOPE_LEVEL.get(scope, 5)
+            flags |= level << abi.KG_GPU_POD_SCOPE_SHIFT
+    return flags, bw

@@ -67,8 +67,9 @@ def plugin_reasons(bits: int, scalar_names=DEFAULT_SCALARS) -> dict:
     for bit, msg in numa:
         if bits & bit:
             add("NodeNUMAResource", msg)
-    if bits & (abi.KG_ST_DEV_INSUFFICIENT | abi.KG_ST_DEV_NO_DEVICE):
-        add("DeviceShare", "Insufficient gpu devices")
+    code = abi.dev_code(bits)
+    if code:  # GPU allocator reasons (deviceshare/allocator_gpu.go:31-41, device_allocator.go:432)
+        add("DeviceShare", DEV_CODE_REASONS.get(code, "Insufficient gpu devices"))
     if bits & abi.KG_ST_DEV_RSV:  # makeReasonsByReservation (deviceshare/plugin.go)
         add("DeviceShare", "Reservation(s) Insufficient gpu devices")
     if bits & abi.KG_ST_RSV_AFFINITY:
@@ -82,6 +83,19 @@ def plugin_reasons(bits: int, scalar_names=DEFAULT_SCALARS) -> dict:
     if bits & abi.KG_ST_UNSUPPORTED:
         add("(host path)", "pair evaluated by the reference plugin on the host")
     return out
+
+
+DEV_CODE_REASONS = {
+    abi.KG_DEV_CODE_INSUFFICIENT: "Insufficient gpu devices",
+    abi.KG_DEV_CODE_NO_DEVICE: "Insufficient gpu devices",
+    abi.KG_DEV_CODE_GPU_DEVICES: "Insufficient GPU Devices",
+    abi.KG_DEV_CODE_TOPO_SCOPED: "Insufficient Topology Scoped GPU Devices",
+    abi.KG_DEV_CODE_PARTITIONED: "Insufficient Partitioned GPU Devices",
+    abi.KG_DEV_CODE_NO_PARTITION: "node(s) missing GPU Partition Table",
+    abi.KG_DEV_CODE_PART_COUNT: "node(s) Unsupported number of GPU requests",
+    abi.KG_DEV_CODE_NO_TREE: "node(s) missing GPU Device Topology Tree",
+    abi.KG_DEV_CODE_MULTI_SHARED: "node(s) Unsupported Multi-Shared GPU",
+}
 
 
 def reasons(bits: int, scalar_names=DEFAULT_SCALARS) -> list:

@@ -9,6 +9,7 @@ import numpy as np
 
 from . import abi
 from .config import GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, SchedulerConfig, bench_profile, config5_profile
+from . import decode
 from .decode import amplify, gpu_requirements, quota_keys, reservation_restore
 
 SEED = 0x6B6F6F7264
@@ -242,7 +243,46 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     p["quota"] = pr.integers(0, n_quotas, n_pods).astype(np.int32)
     p["flags"] |= np.where(pr.random(n_pods) < 0.10, abi.KG_POD_NON_PREEMPTIBLE, 0).astype(np.uint32)
     p["quota_keys"] = quota_keys(p, maxk)
+    gpu_topology5(t, p, seed_config)
     return cfg, t, p, q, abi.Reservations(views, infos, devs)
+
+
+def gpu_topology5(t: abi.Table, p: abi.Table, seed_config: int = 5):
+    """GPU topology and partitions of a config-5 cluster (own random stream, so the other draws do not
+    move): 90% of the nodes report GPU topology (two NUMA nodes of four minors; half of them two GPUs per PCIe
+    switch, half one, like the reference's fakeDeviceCR / fakeH800DeviceCR), 30% are labelled H100 (the
+    Hopper partition table), a third of those with the Honor partition policy. GPU pods: whole-GPU pods carry a
+    GPUPartitionSpec 10% of the time (a third Restricted), and 10% of the GPU pods require a NUMANode or PCIe
+    topology scope."""
+    n, n_pods = abi.table_len(t), abi.table_len(p)
+    r = _rng(seed_config, 2)
+    has = r.random(n) < 0.90
+    pair = r.random(n) < 0.5
+    h100 = r.random(n) < 0.30
+    honor = h100 & (r.random(n) < 1 / 3)
+    layouts = [[(m // 4, str(m // 2)) for m in range(8)], [(m // 4, str(m)) for m in range(8)]]
+    topos = [decode.gpu_topology([{"minor": m, "topology": {"nodeID": q, "pcieID": pc}} for m, (q, pc) in enumerate(l)])[0]
+             for l in layouts]
+    tabs = decode.GpuPartitionTables()
+    hop = tabs.add(decode.gpu_partition_table(None, {"metadata": {"labels": {decode.LABEL_GPU_MODEL: "H100"}}})[0])
+    t["dev_topo"] = np.where(has, np.where(pair, np.uint64(topos[0]), np.uint64(topos[1])),
+                             np.uint64((1 << 64) - 1)).astype(np.uint64)
+    t["dev_part"] = (np.where(has, abi.KG_GPU_TREE, 0) | np.where(h100, hop, 0) |
+                     np.where(honor, abi.KG_GPU_HONOR, 0)).astype(np.uint32)
+    t["gpu_parts"] = tabs.array()
+    flags = np.zeros(n_pods, np.uint32)
+    gpu = p["dev_count"] > 0
+    # gpuShared as calcDesiredRequestsAndCountForGPU decides it (decode.gpu_requirements)
+    has_ratio = ((p["dev_keys"] >> abi.KG_DEV_RATIO) & 1) != 0
+    shared = gpu & np.where(has_ratio, p["dev_req"][:, abi.KG_DEV_RATIO] < 100, ((p["dev_keys"] >> abi.KG_DEV_MEM) & 1) != 0)
+    flags |= np.where(shared, abi.KG_GPU_POD_SHARED, 0).astype(np.uint32)
+    spec = gpu & ~shared & (r.random(n_pods) < 0.10)
+    flags |= np.where(spec, abi.KG_GPU_POD_HONOR, 0).astype(np.uint32)
+    flags |= np.where(spec & (r.random(n_pods) < 1 / 3), abi.KG_GPU_POD_RESTRICTED, 0).astype(np.uint32)
+    scope = np.where(r.random(n_pods) < 0.5, 2, 3)
+    req_scope = gpu & (r.random(n_pods) < 0.10)
+    flags |= np.where(req_scope, scope << abi.KG_GPU_POD_SCOPE_SHIFT, 0).astype(np.uint32)
+    p["dev_flags"] = flags
 
 
 def topology(n_nodes: int, n_pods: int, seed: int = 0, pod_policy_frac: float = 0.3):

@@ -982,6 +982,10 @@ struct kgo_state {
     double* amp;
     int32_t* dev_minors;          /* DeviceShare (NULL when the snapshot has no device tables) */
     int64_t *dev_total, *dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
+    uint64_t* dev_topo;            /* GPU topology / partition tables (static) */
+    uint32_t* dev_part;
+    kg_gpu_partition* gpu_parts;
+    uint32_t n_gpu_parts;
     /* cpuset binding (NULL when no node has a CPU topology) */
     int32_t* cpu_topo;
     kg_cpu_topo* cpu_topos;
@@ -1048,6 +1052,19 @@ kgo_state* kgo_state_new(const kg_node_columns* s, uint32_t n) {
         memcpy(st->dev_minors, s->dev_minors, 4 * (size_t)n);
         memcpy(st->dev_total, s->dev_total, 8 * (size_t)n * KG_DEV_R * KG_DEV_MINORS);
         memcpy(st->dev_free, s->dev_free, 8 * (size_t)n * KG_DEV_R * KG_DEV_MINORS);
+        if (s->dev_topo) {
+            st->dev_topo = (uint64_t*)calloc(n ? n : 1, 8);
+            memcpy(st->dev_topo, s->dev_topo, 8 * (size_t)n);
+        }
+        if (s->dev_part) {
+            st->dev_part = (uint32_t*)calloc(n ? n : 1, 4);
+            memcpy(st->dev_part, s->dev_part, 4 * (size_t)n);
+        }
+        if (s->gpu_parts && s->n_gpu_parts) {
+            st->n_gpu_parts = s->n_gpu_parts;
+            st->gpu_parts = (kg_gpu_partition*)calloc(s->n_gpu_parts, sizeof(kg_gpu_partition));
+            memcpy(st->gpu_parts, s->gpu_parts, sizeof(kg_gpu_partition) * s->n_gpu_parts);
+        }
     }
     if (s->cpu_topo && s->cpu_topos) {
         const size_t m = n ? n : 1;
@@ -1078,6 +1095,9 @@ void kgo_state_free(kgo_state* st) {
     free(st->amp);
     free(st->zone_status);
     free(st->dev_minors);
+    free(st->dev_topo);
+    free(st->dev_part);
+    free(st->gpu_parts);
     free(st->dev_total);
     free(st->dev_free);
     free(st->cpu_topo);
@@ -1130,6 +1150,10 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
     v->dev_minors = st->dev_minors;
     v->dev_total = st->dev_total;
     v->dev_free = st->dev_free;
+    v->dev_topo = st->dev_topo;
+    v->dev_part = st->dev_part;
+    v->gpu_parts = st->gpu_parts;
+    v->n_gpu_parts = st->n_gpu_parts;
     v->cpu_topo = st->cpu_topo;
     v->cpu_topos = st->cpu_topos;
     v->n_cpu_topos = st->n_cpu_topos;
@@ -1353,49 +1377,381 @@ static int dev_minor_fits(const int64_t* fr, const int64_t* preq, uint32_t keys)
     return 1;
 }
 
-/* DeviceShare Filter (deviceshare/plugin.go:345-421 -> AutopilotAllocator.Allocate, GPUAllocator
- * generalAllocate -> defaultAllocateDevices) for a node without GPU topology tree or partition table,
- * and the node Score (scoring.go:45-104 -> AutopilotAllocator.score -> scoreNode). */
+/* ---- GPUAllocator.Allocate (deviceshare/allocator_gpu.go:72-133) ------------------------------------
+ * A device table is a pair of [KG_DEV_R][KG_DEV_MINORS] blocks (total, free) over minors 0..D-1. */
+
+typedef struct gpu_req {
+    int64_t preq[KG_DEV_R];
+    uint32_t keys, n, flags;
+    int64_t ring_bw;
+} gpu_req;
+
+static void gpu_req_of(const kg_pod_columns* p, uint32_t j, gpu_req* g) {
+    dev_pod_req(p, j, g->preq, &g->keys);
+    g->n = p->dev_count ? p->dev_count[j] : 0;
+    g->flags = p->dev_flags ? p->dev_flags[j] : 0;
+    g->ring_bw = (g->flags & KG_GPU_POD_RING_BW) && p->dev_ring_bw ? p->dev_ring_bw[j] : 0;
+}
+
+#define TAB(t, r, m) ((t)[(size_t)(r) * KG_DEV_MINORS + (size_t)(m)])
+
+/* hashDevices(getRealUsed(original used, refined total, refined used)) (:59-70,239-254): the minors the table
+ * has something used on (free != total, i.e. a deviceUsed entry), plus `outside` (minors used on the node that
+ * a filtered table does not hold). */
+static uint32_t used_minors_hash(const int64_t* T, const int64_t* F, int32_t D, uint32_t outside) {
+    uint32_t h = outside;
+    for (int32_t m = 0; m < D; m++)
+        for (int r = 0; r < KG_DEV_R; r++)
+            if (TAB(F, r, m) != TAB(T, r, m)) h |= 1u << m;
+    return h;
+}
+
+/* hashDevices(removeZeroDevice(deviceTotal)) (:87,112-120) */
+static uint32_t total_minors_hash(const int64_t* T, int32_t D) {
+    uint32_t h = 0;
+    for (int32_t m = 0; m < D; m++)
+        for (int r = 0; r < KG_DEV_R; r++)
+            if (TAB(T, r, m) != 0) h |= 1u << m;
+    return h;
+}
+
+/* the partitions of table `tbl` for `ngpu` GPUs (GPUPartitionIndexer[ngpu]): entries [*b, *e) of gpu_parts */
+static int part_range(const kg_node_columns* n, uint32_t tbl, uint32_t ngpu, uint32_t* b, uint32_t* e) {
+    *b = *e = 0;
+    int found = 0;
+    for (uint32_t t = 0; n->gpu_parts && t < n->n_gpu_parts; t++) {
+        const kg_gpu_partition* q = &n->gpu_parts[t];
+        if (q->table != tbl || q->n_gpus != ngpu) continue;
+        if (!found) *b = t;
+        *e = t + 1;
+        found = 1;
+    }
+    return found;
+}
+
+static int partition_feasible(const kg_gpu_partition* q, uint32_t used, uint32_t total, const gpu_req* g) {
+    if (q->minors & used) return 0;
+    if ((total & q->minors) != q->minors) return 0;
+    if (g->flags & KG_GPU_POD_RING_BW) {
+        if (q->ring_bw < 0) return 0;
+        if (g->ring_bw > q->ring_bw) return 0;
+    }
+    return 1;
+}
+
+/* allocateByPartition (:177-237) + selectPartitionByBinPack (:261-296); returns 0 and the minors, or an
+ * allocator code. The caller applies the honor rule of the deferred status reset. */
+static uint32_t allocate_by_partition(const kg_node_columns* n, uint32_t tbl1, const gpu_req* g, uint32_t used,
+                                      uint32_t total, uint32_t* mask) {
+    *mask = 0;
+    if (tbl1 == 0) return KG_DEV_CODE_NO_PARTITION;
+    const uint32_t tbl = tbl1 - 1;
+    uint32_t b, e;
+    if (!part_range(n, tbl, g->n, &b, &e)) return KG_DEV_CODE_PART_COUNT;
+    /* feasiblePartitions over the AllocationScore groups in ascending order, stopping after the first group
+     * that adds any (or after the first group under the Restricted policy) */
+    uint32_t feas[KG_GPU_MAX_PARTS];
+    uint32_t nf = 0;
+    uint32_t t = b;
+    while (t < e) {
+        uint32_t ge = t;
+        while (ge < e && n->gpu_parts[ge].alloc_score == n->gpu_parts[t].alloc_score) ge++;
+        for (uint32_t u = t; u < ge; u++)
+            if (partition_feasible(&n->gpu_parts[u], used, total, g)) feas[nf++] = u;
+        if (nf > 0 || (g->flags & KG_GPU_POD_RESTRICTED)) break;
+        t = ge;
+    }
+    if (nf == 0) return KG_DEV_CODE_PARTITIONED;
+    if (nf == 1) {
+        *mask = n->gpu_parts[feas[0]].minors;
+        return 0;
+    }
+    static const uint32_t sizes[3] = {8, 4, 2};
+    static const int64_t score_of[3] = {10000, 100, 1};
+    int64_t sc[KG_GPU_MAX_PARTS];
+    for (uint32_t k = 0; k < nf; k++) {
+        int64_t score = 0;
+        const uint32_t allocated = used | n->gpu_parts[feas[k]].minors;
+        for (int z = 0; z < 3; z++) {
+            if (sizes[z] < g->n) continue;
+            uint32_t b2, e2;
+            if (!part_range(n, tbl, sizes[z], &b2, &e2)) continue;
+            /* indexerOfGPUNumber[0]: the lowest AllocationScore group */
+            for (uint32_t u = b2; u < e2 && n->gpu_parts[u].alloc_score == n->gpu_parts[b2].alloc_score; u++) {
+                if (n->gpu_parts[u].minors & allocated) continue;
+                score += score_of[z] * (int64_t)n->gpu_parts[u].alloc_score;
+            }
+        }
+        sc[k] = score;
+    }
+    /* sort.Slice by BinPackScore desc: an insertion sort for <= 12 elements (stable), first maximum wins */
+    uint32_t best = 0;
+    for (uint32_t k = 1; k < nf; k++)
+        if (sc[k] > sc[best]) best = k;
+    *mask = n->gpu_parts[feas[best]].minors;
+    return 0;
+}
+
+/* GPUTopologyScope (allocator_gpu_helper.go:201-262): node -> NUMA nodes (by id) -> PCIe (by id) */
+typedef struct gpu_scope {
+    int level;                 /* DeviceTopologyScopeLevel: node 1, NUMA node 2, PCIe 3 */
+    uint32_t minors;           /* bit set; scope.minors is this set in ascending order */
+    int n_children;
+    struct gpu_scope* children;
+} gpu_scope;
+
+typedef struct scope_result {
+    uint32_t mask;             /* allocations (0 = nil) */
+    int cne, depth;
+    int64_t score;
+} scope_result;
+
+typedef struct scope_ctx {
+    const kg_config* c;
+    const int64_t *T, *F;
+    const gpu_req* g;
+    int shared, level;
+    uint32_t used, total;
+} scope_ctx;
+
+/* DeviceLevelContext (:404-414): satisfied = LessThanOrEqual(requestsPerGPU, free) && minor in the refined
+ * total; the shared score is scoreDevice(requestsPerGPU, freeResources, totalResources) with the call site's
+ * argument order (free in the total slot, total in the free slot). */
+static int minor_satisfied(const scope_ctx* x, int m) {
+    if (!((x->total >> m) & 1u)) return 0;
+    for (int r = 0; r < KG_DEV_R; r++)
+        if (((x->g->keys >> r) & 1u) && x->g->preq[r] > TAB(x->F, r, m)) return 0;
+    return 1;
+}
+
+static int64_t minor_shared_score(const scope_ctx* x, int m) {
+    int64_t t[KG_DEV_R], f[KG_DEV_R];
+    for (int r = 0; r < KG_DEV_R; r++) {
+        t[r] = TAB(x->T, r, m);
+        f[r] = TAB(x->F, r, m);
+    }
+    return dev_least(x->c, f, t, x->g->preq);
+}
+
+static scope_result allocate_from_scope(const scope_ctx* x, const gpu_scope* sc, int cne, int depth) {
+    scope_result none = {0, 0, 0, -1};
+    if ((uint32_t)__builtin_popcount(sc->minors) < x->g->n) return none;
+    depth++;
+    if (sc->minors & x->used) cne++;
+    scope_result best = none;
+    int have = 0;
+    for (int k = 0; k < sc->n_children; k++) {
+        const gpu_scope* ch = &sc->children[k];
+        if ((uint32_t)__builtin_popcount(ch->minors) < x->g->n) continue;
+        scope_result r = allocate_from_scope(x, ch, cne, depth);
+        if (r.mask) {
+            if (!have) {
+                best = r;
+                have = 1;
+                continue;
+            }
+            if (best.depth < r.depth || (best.depth == r.depth && best.cne < r.cne)) best = r;
+            if (x->shared && best.depth == r.depth && best.cne == r.cne && best.score < r.score) best = r;
+        }
+    }
+    if (have) return best;
+    if (x->level > sc->level) return none;
+    uint32_t cand = 0, count = 0;
+    int best_minor = -1, satisfied = 0;
+    int64_t best_score = -1;
+    for (int m = 0; m < KG_DEV_MINORS; m++) {
+        if (!((sc->minors >> m) & 1u)) continue;
+        if (!minor_satisfied(x, m)) continue;
+        if (!x->shared) {
+            cand |= 1u << m;
+            if (++count == x->g->n) {
+                satisfied = 1;
+                break;
+            }
+            continue;
+        }
+        satisfied = 1;
+        const int64_t s = minor_shared_score(x, m);
+        if (s > best_score) {
+            best_minor = m;
+            best_score = s;
+        }
+    }
+    if (!satisfied) return none;
+    scope_result r = {x->shared ? (best_minor >= 0 ? 1u << best_minor : 0u) : cand, cne, depth, best_score};
+    return r;
+}
+
+/* build the tree of one node from dev_topo (NUMA rank in the high nibble, PCIe rank in the low one) */
+static void build_scope(uint64_t topo, int32_t D, gpu_scope* root, gpu_scope* numa, gpu_scope* pcie) {
+    root->level = 1;
+    root->minors = D >= 32 ? ~0u : (1u << D) - 1u;
+    root->n_children = 0;
+    root->children = numa;
+    int np = 0;
+    for (uint32_t q = 0; q < 15; q++) {
+        uint32_t qm = 0;
+        for (int32_t m = 0; m < D; m++) {
+            const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
+            if (b != KG_GPU_NO_SCOPE && (b >> 4) == q) qm |= 1u << m;
+        }
+        if (!qm) continue;
+        gpu_scope* ns = &numa[root->n_children++];
+        ns->level = 2;
+        ns->minors = qm;
+        ns->n_children = 0;
+        ns->children = &pcie[np];
+        for (uint32_t r = 0; r < 16; r++) {
+            uint32_t rm = 0;
+            for (int32_t m = 0; m < D; m++) {
+                const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
+                if (b != KG_GPU_NO_SCOPE && (b >> 4) == q && (b & 15u) == r) rm |= 1u << m;
+            }
+            if (!rm) continue;
+            gpu_scope* ps = &pcie[np++];
+            ps->level = 3;
+            ps->minors = rm;
+            ps->n_children = 0;
+            ps->children = NULL;
+            ns->n_children++;
+        }
+    }
+}
+
+/* defaultAllocateDevices (device_allocator.go:355-437): scoreDevices + sortDeviceResourcesByMinor (score
+ * desc, minor asc, device_resources.go:171-209), the first numberOfGPUs minors that fit. */
+static uint32_t default_allocate(const kg_config* c, const int64_t* T, const int64_t* F, int32_t D, const gpu_req* g,
+                                 uint32_t* mask) {
+    int64_t sc[KG_DEV_MINORS];
+    int order[KG_DEV_MINORS];
+    for (int32_t m = 0; m < D; m++) {
+        int64_t t[KG_DEV_R], f[KG_DEV_R];
+        for (int r = 0; r < KG_DEV_R; r++) {
+            t[r] = TAB(T, r, m);
+            f[r] = TAB(F, r, m);
+        }
+        sc[m] = dev_least(c, t, f, g->preq);
+        order[m] = m;
+    }
+    for (int32_t a = 1; a < D; a++) { /* stable insertion sort by score desc (minor asc on ties) */
+        int v = order[a];
+        int32_t b = a;
+        while (b > 0 && sc[order[b - 1]] < sc[v]) {
+            order[b] = order[b - 1];
+            b--;
+        }
+        order[b] = v;
+    }
+    uint32_t got = 0;
+    *mask = 0;
+    for (int32_t t = 0; t < D && got < g->n; t++) {
+        int m = order[t];
+        int64_t fr[KG_DEV_R];
+        for (int r = 0; r < KG_DEV_R; r++) fr[r] = TAB(F, r, m);
+        if (!dev_minor_fits(fr, g->preq, g->keys)) continue;
+        *mask |= 1u << m;
+        got++;
+    }
+    if (got < g->n) {
+        *mask = 0;
+        return KG_DEV_CODE_INSUFFICIENT;
+    }
+    return 0;
+}
+
+/* GPUAllocator.Allocate: allocateByTemplate (not restated: template pods are flagged by the caller), then
+ * allocateByPartition, then generalAllocate = allocateByDeviceTopology, then defaultAllocateDevices.
+ * Returns 0 with the minors, or a KG_DEV_CODE_*. */
+static uint32_t gpu_allocate(const kg_config* c, const kg_node_columns* n, uint32_t i, const int64_t* T,
+                             const int64_t* F, int32_t D, uint32_t outside, const gpu_req* g, uint32_t* mask) {
+    *mask = 0;
+    const uint32_t part = n->dev_part ? n->dev_part[i] : 0u;
+    const uint64_t topo = n->dev_topo ? n->dev_topo[i] : ~0ull;
+    const int shared = (g->flags & KG_GPU_POD_SHARED) != 0;
+    const uint32_t sf = (g->flags >> KG_GPU_POD_SCOPE_SHIFT) & 7u;
+    const int required = sf != 0; /* requiredTopologyScope != "" */
+    const int level = sf > 4 ? 0 : (int)sf;
+    const int honor = (g->flags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR);
+    const uint32_t used = used_minors_hash(T, F, D, outside);
+    const uint32_t total = total_minors_hash(T, D);
+    /* allocateByPartition: shared GPUs skip it; a failure stands only when partitions are honored */
+    if (!shared) {
+        uint32_t code = allocate_by_partition(n, part & 0xFFu, g, used, total, mask);
+        if (code == 0) return 0;
+        if (honor) return code;
+    }
+    /* allocateByDeviceTopology (:312-337): UnschedulableAndUnresolvable statuses vanish when no scope is
+     * required; an Unschedulable one (the tree found nothing) stands */
+    if (!(part & KG_GPU_TREE)) {
+        if (required) return KG_DEV_CODE_NO_TREE;
+    } else if (shared && g->n > 1) {
+        if (required) return KG_DEV_CODE_MULTI_SHARED;
+    } else {
+        gpu_scope root, numa[16], pcie[16 * 16];
+        build_scope(topo, D, &root, numa, pcie);
+        scope_ctx x = {c, T, F, g, shared, level, used, total};
+        scope_result r = allocate_from_scope(&x, &root, 0, 0);
+        if (r.mask) {
+            *mask = r.mask;
+            return 0;
+        }
+        return required ? KG_DEV_CODE_TOPO_SCOPED : KG_DEV_CODE_GPU_DEVICES;
+    }
+    return default_allocate(c, T, F, D, g, mask);
+}
+
+static uint32_t dev_code_status(uint32_t code) { return code ? KG_ST_DEV_MAKE(code) : 0u; }
+
+/* DeviceShare Filter (deviceshare/plugin.go:345-421 -> AutopilotAllocator.Allocate -> GPUAllocator.Allocate)
+ * and the node Score (scoring.go:45-104 -> AutopilotAllocator.score -> scoreNode over the minor sums). */
 static uint32_t dev_eval(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
                          uint32_t j, int64_t* raw) {
     *raw = 0;
-    uint32_t cnt = p->dev_count ? p->dev_count[j] : 0;
-    if (cnt == 0) return 0;                                 /* PreFilter Skip */
+    gpu_req g;
+    gpu_req_of(p, j, &g);
+    if (g.n == 0) return 0;                                 /* PreFilter Skip */
     int32_t D = n->dev_minors ? n->dev_minors[i] : -1;
     if (D < 0) return 0;                                    /* no Device object: pass, Score 0 */
     if (D == 0) return KG_ST_DEV_NO_DEVICE;                 /* devicehandler_gpu.go:41-44 */
-    int64_t preq[KG_DEV_R], T[KG_DEV_R] = {0, 0, 0}, F[KG_DEV_R] = {0, 0, 0};
-    uint32_t keys;
-    dev_pod_req(p, j, preq, &keys);
-    uint32_t fit = 0;
-    for (int32_t m = 0; m < D; m++) {
-        int64_t fr[KG_DEV_R];
+    if (g.flags & KG_GPU_POD_TEMPLATE) return KG_ST_UNSUPPORTED; /* allocateByTemplate: host path */
+    const int64_t* T = &DEVX(n->dev_total, i, 0, 0);
+    const int64_t* F = &DEVX(n->dev_free, i, 0, 0);
+    uint32_t mask;
+    const uint32_t code = gpu_allocate(c, n, i, T, F, D, 0u, &g, &mask);
+    if (code) return dev_code_status(code);
+    int64_t Ts[KG_DEV_R] = {0, 0, 0}, Fs[KG_DEV_R] = {0, 0, 0};
+    for (int32_t m = 0; m < D; m++)
         for (int r = 0; r < KG_DEV_R; r++) {
-            fr[r] = DEVX(n->dev_free, i, r, m);
-            T[r] += DEVX(n->dev_total, i, r, m);
-            F[r] += fr[r];
+            Ts[r] += TAB(T, r, m);
+            Fs[r] += TAB(F, r, m);
         }
-        fit += (uint32_t)dev_minor_fits(fr, preq, keys);
-    }
-    if (fit < cnt) return KG_ST_DEV_INSUFFICIENT;
-    *raw = dev_least(c, T, F, preq);
+    *raw = dev_least(c, Ts, Fs, g.preq);
     return 0;
+}
+
+/* minors used on node i (free != total) that a restore table leaves out (total 0 everywhere) */
+static uint32_t outside_used(const kg_node_columns* n, uint32_t i, const kg_rsv_dev* t, int32_t D) {
+    uint32_t o = 0;
+    for (int32_t m = 0; m < D; m++) {
+        int used = 0, in_tab = 0;
+        for (int r = 0; r < KG_DEV_R; r++) {
+            used |= DEVX(n->dev_free, i, r, m) != DEVX(n->dev_total, i, r, m);
+            in_tab |= t->total[r][m] != 0;
+        }
+        if (used && !in_tab) o |= 1u << m;
+    }
+    return o;
 }
 
 /* The same Filter and Score on one GPU restore table (kg_rsv_dev: the free / total a reservation restore
  * hands the allocator, device_cache.go:322-410). Score: AutopilotAllocator.score (device_allocator.go
  * :486-508) leaves the GPU type out when every free value is zero (nodeDevice.filter), giving 0. */
-static uint32_t dev_eval_tab(const kg_config* c, const kg_rsv_dev* t, int32_t D, const kg_pod_columns* p, uint32_t j,
-                             int64_t* raw) {
+static uint32_t dev_eval_tab(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_rsv_dev* t, int32_t D,
+                             const kg_pod_columns* p, uint32_t j, int64_t* raw) {
     *raw = 0;
-    int64_t preq[KG_DEV_R], T[KG_DEV_R] = {0, 0, 0}, F[KG_DEV_R] = {0, 0, 0};
-    uint32_t keys, cnt = p->dev_count[j], fit = 0;
-    dev_pod_req(p, j, preq, &keys);
-    for (int32_t m = 0; m < D; m++) {
-        int64_t fr[KG_DEV_R];
-        for (int r = 0; r < KG_DEV_R; r++) fr[r] = t->free[r][m];
-        fit += (uint32_t)dev_minor_fits(fr, preq, keys);
-    }
+    gpu_req g;
+    gpu_req_of(p, j, &g);
+    int64_t T[KG_DEV_R] = {0, 0, 0}, F[KG_DEV_R] = {0, 0, 0};
     int any = 0;
     for (int m = 0; m < KG_DEV_MINORS; m++)
         for (int r = 0; r < KG_DEV_R; r++) {
@@ -1403,8 +1759,10 @@ static uint32_t dev_eval_tab(const kg_config* c, const kg_rsv_dev* t, int32_t D,
             F[r] += t->free[r][m];
             any |= t->free[r][m] != 0;
         }
-    *raw = any ? dev_least(c, T, F, preq) : 0;
-    return fit < cnt ? KG_ST_DEV_INSUFFICIENT : 0u;
+    *raw = any ? dev_least(c, T, F, g.preq) : 0;
+    if (g.flags & KG_GPU_POD_TEMPLATE) return KG_ST_UNSUPPORTED;
+    uint32_t mask;
+    return dev_code_status(gpu_allocate(c, n, i, &t->total[0][0], &t->free[0][0], D, outside_used(n, i, t, D), &g, &mask));
 }
 
 /* DeviceShare Filter of a GPU pod on a reservation view (deviceshare/plugin.go:397-419):
@@ -1422,47 +1780,23 @@ static uint32_t dev_filter_view(const kg_config* c, const kg_node_columns* n, ui
         int32_t di = e->infos[v->first + t].dev;
         if (di < 0) continue;
         any = 1;
-        if (dev_eval_tab(c, &e->devs[di], D, p, j, &raw) == 0) return 0;
+        if (dev_eval_tab(c, n, i, &e->devs[di], D, p, j, &raw) == 0) return 0;
     }
     if (any && (p->flags[j] & KG_POD_RSV_REQUIRED)) return KG_ST_DEV_RSV;
-    if (v->dev_base >= 0) return dev_eval_tab(c, &e->devs[v->dev_base], D, p, j, &raw);
+    if (v->dev_base >= 0) return dev_eval_tab(c, n, i, &e->devs[v->dev_base], D, p, j, &raw);
     return dev_eval(c, n, i, p, j, &raw);
 }
 
-/* Reserve-time minor choice: scoreDevices + sortDeviceResourcesByMinor (score desc, minor asc,
- * device_resources.go:171-209), first numberOfGPUs minors that fit. Returns the minor bitmask. */
-static uint32_t dev_choose(const kg_config* c, const int64_t* total_tab, const int64_t* free_tab, uint32_t i,
-                           int32_t D, const int64_t* preq, uint32_t keys, uint32_t cnt) {
-    int64_t sc[KG_DEV_MINORS];
-    int order[KG_DEV_MINORS];
-    for (int32_t m = 0; m < D; m++) {
-        int64_t t[KG_DEV_R], f[KG_DEV_R];
-        for (int r = 0; r < KG_DEV_R; r++) {
-            t[r] = DEVX(total_tab, i, r, m);
-            f[r] = DEVX(free_tab, i, r, m);
-        }
-        sc[m] = dev_least(c, t, f, preq);
-        order[m] = m;
-    }
-    for (int32_t a = 1; a < D; a++) { /* stable insertion sort by score desc (minor asc on ties) */
-        int x = order[a];
-        int32_t b = a;
-        while (b > 0 && sc[order[b - 1]] < sc[x]) {
-            order[b] = order[b - 1];
-            b--;
-        }
-        order[b] = x;
-    }
-    uint32_t mask = 0, got = 0;
-    for (int32_t t = 0; t < D && got < cnt; t++) {
-        int m = order[t];
-        int64_t fr[KG_DEV_R];
-        for (int r = 0; r < KG_DEV_R; r++) fr[r] = DEVX(free_tab, i, r, m);
-        if (!dev_minor_fits(fr, preq, keys)) continue;
-        mask |= 1u << m;
-        got++;
-    }
-    return got < cnt ? 0 : mask;
+/* Reserve-time minors: the allocation GPUAllocator.Allocate makes on node i (0 when it fails). */
+static uint32_t dev_choose(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                           uint32_t j) {
+    gpu_req g;
+    gpu_req_of(p, j, &g);
+    int32_t D = n->dev_minors ? n->dev_minors[i] : -1;
+    if (g.n == 0 || D <= 0) return 0;
+    uint32_t mask;
+    const uint32_t code = gpu_allocate(c, n, i, &DEVX(n->dev_total, i, 0, 0), &DEVX(n->dev_free, i, 0, 0), D, 0u, &g, &mask);
+    return code ? 0u : mask;
 }
 
 /* Per-minor allocation after fillGPUTotalMem (devicehandler_gpu.go:98-135): gpu-memory from the ratio
@@ -1897,9 +2231,9 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
             int64_t raw = 0;
             if (nom >= 0) {
                 int32_t di = e->infos[v->first + (uint32_t)nom].dev;
-                if (di >= 0) dev_eval_tab(c, &e->devs[di], D, p, j, &raw);
+                if (di >= 0) dev_eval_tab(c, n, i, &e->devs[di], D, p, j, &raw);
             } else if (v->dev_base >= 0) {
-                dev_eval_tab(c, &e->devs[v->dev_base], D, p, j, &raw);
+                dev_eval_tab(c, n, i, &e->devs[v->dev_base], D, p, j, &raw);
             } else {
                 dev_eval(c, n, i, p, j, &raw);
             }
@@ -2118,7 +2452,7 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
             int64_t preq[KG_DEV_R];
             uint32_t keys;
             dev_pod_req(p, j, preq, &keys);
-            uint32_t mask = dev_choose(c, st->dev_total, st->dev_free, i, st->dev_minors[i], preq, keys, p->dev_count[j]);
+            uint32_t mask = dev_choose(c, &v, i, p, j);
             dev_apply(st->dev_total, st->dev_free, i, mask, preq, keys, 1);
             if (out_minors) out_minors[j] = mask;
         }
@@ -2213,8 +2547,9 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                 int64_t preq[KG_DEV_R];
                 uint32_t keys;
                 dev_pod_req(p, j, preq, &keys);
-                uint32_t mask = dev_choose(c, st->dev_total, st->dev_free, (uint32_t)node, st->dev_minors[node], preq, keys,
-                                           p->dev_count[j]);
+                kg_node_columns nv;
+                kgo_state_view(st, &nv);
+                uint32_t mask = dev_choose(c, &nv, (uint32_t)node, p, j);
                 dev_apply(st->dev_total, st->dev_free, (uint32_t)node, mask, preq, keys, 1);
                 out_minors[j] = mask;
             }
