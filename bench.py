@@ -221,13 +221,14 @@ def cpu_baseline_ext(kc, nodes, pods, quotas, rsv, target_s):
                       f"kgo_ext_select (all six plugins, NormalizeScore, selectHost), one thread"}
 
 
-def replay_rate(ctx, cfg, with_cpu, cpu_s):
-    """Config 3: 50k pods placed one by one on 10k nodes with device-resident Assume."""
+def replay_rate(ctx, cfg, with_cpu, cpu_s, config=3):
+    """Pods placed one by one with device-resident Assume: config 3 (50k pods on 10k nodes) or, for the
+    BASELINE metric's 100k-node half, the config-4 cluster (10k pods on 100k nodes, one GPU)."""
     import numpy as np
 
     from koordinator_amd import abi, engine, synth
 
-    _, nodes, pods = synth.cluster(3)
+    _, nodes, pods = synth.cluster(config)
     kc = cfg.kg_config()
     snap = engine.Snapshot(ctx, kc, nodes)
     batch = engine.PodBatch(ctx, pods)
@@ -240,14 +241,15 @@ def replay_rate(ctx, cfg, with_cpu, cpu_s):
     placed = int((node >= 0).sum())
     out = {"pods_placed_per_s": batch.n / dt, "pods": batch.n, "placed": placed,
            "unschedulable": batch.n - placed, "seconds": round(dt, 4),
-           "workload": "config3: 10k nodes x 50k pods, one pod per cycle, Assume on device"}
+           "workload": (f"config{config}: {snap.n // 1000}k nodes x {batch.n // 1000}k pods, one pod per cycle, "
+                        "Assume on device")}
     if with_cpu:
         # CPU baseline: every cycle's Filter / Score on the upstream 16-worker parallelizer, then the
         # Reserve, for the first pods of the same sequence (bounded sample)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib  # test infrastructure: the CPU baseline leg only
 
-        probe = 50
+        probe = 50 if config == 3 else 8
         st = oracle_lib.OracleState(kc, nodes)
         t0 = time.perf_counter()
         st.replay_parallel(abi.take(pods, np.arange(probe)), 16)
@@ -260,7 +262,7 @@ def replay_rate(ctx, cfg, with_cpu, cpu_s):
         assert np.array_equal(want, node[:n])  # same placements as the device replay
         out["cpu_baseline"] = {"value": n / cdt, "unit": "pods/s", "cores": os.cpu_count(), "workers": 16,
                                "kind": "port",
-                               "sample": f"first {n} pods of the config-3 sequence in {cdt:.2f} s; oracle/kg_oracle.c "
+                               "sample": f"first {n} pods of the config-{config} sequence in {cdt:.2f} s; oracle/kg_oracle.c "
                                          f"kgo_replay_parallel: each cycle's Filter then Score over all nodes on 16 "
                                          f"worker threads (parallelism.go:29-49), then the Reserve"}
     snap.close()
@@ -420,6 +422,7 @@ def main():
         else:
             if not a.no_replay and config in (1, 2):
                 out["replay"] = replay_rate(ctx, cfg, not a.no_cpu_baseline, a.cpu_seconds)
+                out["replay_100k"] = replay_rate(ctx, cfg, not a.no_cpu_baseline, a.cpu_seconds / 2, config=4)
             if not a.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline(cfg, all_nodes, pods, a.cpu_seconds)
     if rank == 0:

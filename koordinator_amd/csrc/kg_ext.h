@@ -103,21 +103,11 @@ __device__ __forceinline__ GpuMinors gpu_minors(const DevRec* __restrict__ d, in
     return g;
 }
 
-// Σ AllocationScore of the partitions of the lowest-score group of (table tbl, n2 GPUs) that do not
-// overlap `allocated` (selectPartitionByBinPack's inner loop, allocator_gpu.go:275-284).
-__device__ __forceinline__ int64_t free_partitions(const ExtDev& e, uint32_t tbl, uint32_t n2, uint32_t allocated) {
-    const uint32_t r2 = e.part_rng[(tbl - 1u) * 9u + n2];
-    const uint32_t b2 = r2 & 0xFFFFu, e2 = r2 >> 16;
-    if (b2 >= e2) return 0;
-    const int32_t s0 = e.parts[b2].alloc_score;
-    int64_t sum = 0;
-    for (uint32_t u = b2; u < e2; u++) {
-        const kg_gpu_partition q = e.parts[u];
-        if (q.alloc_score != s0) break;
-        if ((uint32_t)q.minors & allocated) continue;
-        sum += (int64_t)q.alloc_score;
-    }
-    return sum;
+// Σ AllocationScore of the partitions of the lowest-score group of (table tbl, n2 GPUs) that do not overlap
+// `allocated` (selectPartitionByBinPack's inner loop, allocator_gpu.go:275-284), tabulated by the runtime at
+// upload for every allocated mask: binpack[((tbl - 1) * 3 + k) * 256 + allocated], k = 0, 1, 2 for 8, 4, 2 GPUs.
+__device__ __forceinline__ int64_t free_partitions(const ExtDev& e, uint32_t tbl, uint32_t k, uint32_t allocated) {
+    return e.binpack[((tbl - 1u) * 3u + k) * 256u + (allocated & 0xFFu)];
 }
 
 __device__ __forceinline__ bool partition_ok(const kg_gpu_partition& q, const GpuMinors& g, const PodX& x) {
@@ -163,8 +153,8 @@ __device__ __forceinline__ GpuAlloc gpu_partition(const ExtDev& e, uint32_t tbl,
         if (nfeas == 1u) return {0u, (uint32_t)q.minors};
         const uint32_t allocated = g.used | (uint32_t)q.minors;
         int64_t score = 0;
-        if (N <= 8u) score += 10000 * free_partitions(e, tbl, 8u, allocated);
-        if (N <= 4u) score += 100 * free_partitions(e, tbl, 4u, allocated);
+        if (N <= 8u) score += 10000 * free_partitions(e, tbl, 0u, allocated);
+        if (N <= 4u) score += 100 * free_partitions(e, tbl, 1u, allocated);
         if (N <= 2u) score += free_partitions(e, tbl, 2u, allocated);
         if (score > best) {
             best = score;
@@ -238,27 +228,33 @@ __device__ __forceinline__ uint32_t gpu_scope(const KCfg& c, const DevRec* __res
     const uint32_t N = x.dcount;
     const uint32_t root = D >= 32 ? ~0u : (1u << D) - 1u;
     if ((uint32_t)__popc(root) < N) return 0u;
+    // scope minor sets from the per-minor ranks (dense: NUMA ranks 0..nq-1, PCIe ranks 0..np-1, both <= D)
+    uint32_t numa[DEV_MINORS], pcie[DEV_MINORS], pcie_numa[DEV_MINORS];
+#pragma unroll
+    for (int k = 0; k < DEV_MINORS; k++) numa[k] = pcie[k] = pcie_numa[k] = 0u;
+    for (int32_t m = 0; m < D; m++) {
+        const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
+        if (b == KG_GPU_NO_SCOPE) continue;
+        const uint32_t q = (b >> 4) & 7u, r = b & 7u;
+        numa[q] |= 1u << m;
+        pcie[r] |= 1u << m;
+        pcie_numa[r] = q;
+    }
     const int32_t cne1 = (root & g.used) ? 1 : 0;
     ScopeRes best{0u, 0, 0, -1};
-    for (uint32_t q = 0; q < 15u; q++) {  // NUMA scopes in rank order
-        uint32_t qm = 0;
-        for (int32_t m = 0; m < D; m++) {
-            const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
-            if (b != KG_GPU_NO_SCOPE && (b >> 4) == q) qm |= 1u << m;
-        }
-        if (!qm) continue;
+    for (uint32_t q = 0; q < (uint32_t)DEV_MINORS; q++) {  // NUMA scopes in rank order
+        const uint32_t qm = numa[q];
+        if (!qm) break;
         if ((uint32_t)__popc(qm) < N) continue;
         const int32_t cne2 = cne1 + ((qm & g.used) ? 1 : 0);
         ScopeRes bq{0u, 0, 0, -1};
-        for (uint32_t r = 0; r < 16u; r++) {
-            uint32_t rm = 0;
-            for (int32_t m = 0; m < D; m++) {
-                const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
-                if (b != KG_GPU_NO_SCOPE && (b >> 4) == q && (b & 15u) == r) rm |= 1u << m;
+        if (level <= 3) {  // a PCIe scope has no children; below the required level it yields nothing
+            for (uint32_t r = 0; r < (uint32_t)DEV_MINORS; r++) {  // PCIe scopes of this NUMA node in rank order
+                const uint32_t rm = pcie[r];
+                if (!rm) break;
+                if (pcie_numa[r] != q || (uint32_t)__popc(rm) < N) continue;
+                scope_merge(bq, scope_take(c, d, x, rm, g, shared, 3, cne2 + ((rm & g.used) ? 1 : 0)), shared);
             }
-            if (!rm || (uint32_t)__popc(rm) < N) continue;
-            if (level > 3) continue;  // a PCIe scope has no children; below the required level: nothing
-            scope_merge(bq, scope_take(c, d, x, rm, g, shared, 3, cne2 + ((rm & g.used) ? 1 : 0)), shared);
         }
         if (!bq.mask && level <= 2) bq = scope_take(c, d, x, qm, g, shared, 2, cne2);
         scope_merge(best, bq, shared);
@@ -381,9 +377,24 @@ __device__ __forceinline__ uint32_t dev_eval_sum(const KCfg& c, const ExtDev& e,
     if (D < 0) return 0;
     if (D == 0) return KG_ST_DEV_NO_DEVICE;
     if (cls >= (uint32_t)DEV_CLASSES) return dev_eval(c, e, n, zr, d, x, raw);
-    const uint32_t code = (uint32_t)(ds->fit >> (4u * cls)) & 15u;
+    const uint32_t code = ds->code[cls];
     if (code) return dev_code_status(code);
     raw = ds->score[cls];  // k_dev_sum: dev_sum_score of the class
+    return 0;
+}
+
+// dev_eval_sum for a pod that has a class (the fast-base kernels run only when every GPU pod of the batch has one):
+// the tabulated allocator outcome and Score, no allocator code in the kernel.
+__device__ __forceinline__ uint32_t dev_eval_cls(const int64_t* __restrict__ n, const DevSum* __restrict__ ds,
+                                                 const PodX& x, uint32_t cls, int64_t& raw) {
+    raw = 0;
+    if (x.dcount == 0) return 0;
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    if (D < 0) return 0;
+    if (D == 0) return KG_ST_DEV_NO_DEVICE;
+    const uint32_t code = ds->code[cls];
+    if (code) return dev_code_status(code);
+    raw = ds->score[cls];
     return 0;
 }
 
@@ -742,10 +753,13 @@ struct PairX {
 
 // SCORE = false (statistics pass): status, raw DeviceShare score and the nominated reservation only;
 // the NodeResourcesFit / LoadAware / NodeNUMAResource scores stay 0.
+// dcls: the pod's GPU request class; with the batch's DevSum table (e.dsum) the DeviceShare Filter / Score of a
+// pair off a reservation view read the record's tabulated allocator outcome instead of running the allocator.
 template <bool EXACT, bool TOPO = true, bool SCORE = true>
 __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
                                                const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
-                                               uint32_t rec, const PodV& p, const PodX& x, uint32_t qst) {
+                                               uint32_t rec, const PodV& p, const PodX& x, uint32_t qst,
+                                               uint32_t dcls = (uint32_t)DEV_CLASSES) {
     PairX o;
     o.status = 0;
     o.zone = -1;
@@ -781,6 +795,8 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     if (c.plugins & KG_PLUGIN_DEV) {
         if (dev_view)
             st |= dev_filter_view(c, e, n, zr, d, *v, x, (p.flags & KG_POD_RSV_REQUIRED) != 0);
+        else if (e.dsum && dcls < (uint32_t)DEV_CLASSES)
+            st |= dev_eval_sum(c, e, n, zr, d, e.dsum + rec, x, dcls, dev_raw);
         else
             st |= dev_eval(c, e, n, zr, d, x, dev_raw);
         if (x.dcount > 0) {

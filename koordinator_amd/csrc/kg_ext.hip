@@ -40,7 +40,8 @@ __device__ __forceinline__ int32_t wmax_i32(int32_t v) {
 
 __device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) { return e.dev ? e.dev + rec : nullptr; }
 
-// DevSum of every record for the pod batch's GPU request classes (one thread per record).
+// DevSum of every record for the pod batch's GPU request classes (one thread per record): the minor sums, and per
+// class the GPU allocator's outcome and the node Score.
 __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                  const DevRec* __restrict__ devs, uint32_t n_nodes,
                                                  const DevClass* __restrict__ cls, uint32_t n_cls, KCfg cfg, ExtDev e,
@@ -51,7 +52,6 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
     const int32_t D = (int32_t)nodes[rec].v[N_DEV_MINORS];
     const ZoneRec& zr = zones[rec];
     DevSum o;
-    o.fit = 0;
     for (int r = 0; r < DEV_R; r++) {
         int64_t t = 0, f = 0;
         for (int m = 0; m < DEV_MINORS; m++) {
@@ -62,23 +62,21 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
         o.F[r] = f;
         o.rcp[r] = t != 0 ? 1.0 / (double)t : 0.0;
     }
-    for (uint32_t k = 0; k < n_cls; k++) {
-        PodX x{};
-        x.dkeys = cls[k].dkeys;
-        x.dcount = cls[k].dcount;
-        x.dflags = cls[k].dflags;
-        x.dbw = cls[k].dbw;
-        for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
-        // D <= 0 and template pods never read the nibble (dev_eval_sum decides them first)
-        const uint64_t code = D > 0 ? gpu_allocate(cfg, e, &d, D, zr.dev_topo, zr.dev_part, x, 0u, false).code : 0u;
-        o.fit |= code << (4u * k);
-    }
-    for (uint32_t k = 0; k < 16u; k++) o.score[k] = 0;
-    for (uint32_t k = 0; k < n_cls; k++) {  // the node Score per class (every pair of the class reads it)
-        PodX x{};
-        x.dkeys = cls[k].dkeys;
-        for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
-        o.score[k] = (uint8_t)dev_sum_score(cfg, &o, x);
+    for (uint32_t k = 0; k < (uint32_t)DEV_CLASSES; k++) {
+        uint8_t code = 0, score = 0;
+        if (k < n_cls) {
+            PodX x{};
+            x.dkeys = cls[k].dkeys;
+            x.dcount = cls[k].dcount;
+            x.dflags = cls[k].dflags;
+            x.dbw = cls[k].dbw;
+            for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
+            // D <= 0 never reads the code (the pair is decided first)
+            code = (uint8_t)(D > 0 ? gpu_allocate(cfg, e, &d, D, zr.dev_topo, zr.dev_part, x, 0u, false).code : 0u);
+            score = (uint8_t)dev_sum_score(cfg, &o, x);
+        }
+        o.code[k] = code;
+        o.score[k] = score;
     }
     out[rec] = o;
 }
@@ -223,7 +221,7 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
                     const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
                     int64_t raw = 0;
                     uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
-                    if (!st) st |= dev_eval_sum(cfg, e, n, zones + rec, dev_of(e, rec), e.dsum + rec, px, dcls, raw);
+                    if (!st) st |= dev_eval_cls(n, e.dsum + rec, px, dcls, raw);
                     if (!st) dmax = max(dmax, (uint32_t)raw);
                     pv = 0x80000000u | (st ? 0u : (0x40000000u | ((uint32_t)(bk >> 32) << 7) | (uint32_t)raw));
                 }
@@ -233,7 +231,8 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
             if (e.pairs && live) e.pairs[(size_t)rec * e.pairs_ld + t] = 0u;
         }
         if constexpr (PART != 1) {
-            const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
+            const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q,
+                                          pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES);
             if (r.status) continue;
             dmax = max(dmax, (uint32_t)r.s_dev);
             rmax = max(rmax, (uint32_t)r.s_rsv);
@@ -285,7 +284,8 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
     uint32_t dmax = 0, rmax = 0;
     uint64_t pk = PREF_NONE;
     for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, [&](uint32_t rec) {
-        const PairX r = eval_pair_ext<false, false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const PairX r = eval_pair_ext<false, false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
+                                          pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES);
         if (r.status) return;
         dmax = max(dmax, (uint32_t)r.s_dev);
         rmax = max(rmax, (uint32_t)r.s_rsv);
@@ -323,7 +323,8 @@ __global__ __launch_bounds__(256) void k_ext_stats_views(const NodeRec* __restri
     const uint32_t vb = cb + blockIdx.y * chunk, ve = min(ce, vb + chunk);
     for (uint32_t v = vb; v < ve; v++) {
         const uint32_t rec = e.views[v].rec;
-        const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
+                                          pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES);
         if (r.status) continue;
         rmax = max(rmax, (uint32_t)r.s_rsv);
         if (r.order != 0) {
@@ -411,15 +412,15 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
                 uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
                 int64_t s_dev = 0;
                 if ((cfg.plugins & KG_PLUGIN_DEV) && !st)  // only the key's zero-ness matters once st != 0
-                    st |= dev_eval_sum(cfg, e, n, zones + rec, dev_of(e, rec), e.dsum + rec, px, dcls, s_dev);
-                unsup |= st & KG_ST_UNSUPPORTED;  // a shared-resource-template pod
+                    st |= dev_eval_cls(n, e.dsum + rec, px, dcls, s_dev);
                 const int64_t tot = total_fb(cfg, bk, s_dev, dm, mag, g, pf);
                 topk_ins<K>(top, st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)));
                 continue;
             }
         }
         if constexpr (PART != 1) {
-            const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q);
+            const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q,
+                                          pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES);
             unsup |= r.status & KG_ST_UNSUPPORTED;
             const uint32_t g = index_base + node_index(nodes[rec]);
             const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
@@ -459,7 +460,8 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
     for (int t = 0; t < K; t++) top[t] = 0;
     uint32_t unsup = 0;
     for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, [&](uint32_t rec) {
-        const PairX r = eval_pair_ext<false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q);
+        const PairX r = eval_pair_ext<false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
+                                          pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES);
         unsup |= r.status & KG_ST_UNSUPPORTED;
         const uint32_t g = index_base + node_index(nodes[rec]);
         const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);

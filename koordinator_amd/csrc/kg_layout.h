@@ -316,7 +316,7 @@ struct PodsDev {
     const int64_t* la_est0;
     const int64_t* la_est1;
     const uint32_t* flags;
-    const uint8_t* dev_cls;     // GPU request class of the pod (DevSum.fit nibble), DEV_CLASSES = none
+    const uint8_t* dev_cls;     // GPU request class of the pod (DevSum.code / score index), DEV_CLASSES = none
     const uint32_t* dev_flags;  // KG_GPU_POD_*
     const int64_t* dev_bw;      // ring bus bandwidth request (KG_GPU_POD_RING_BW)
 };
@@ -350,10 +350,10 @@ struct alignas(64) DevRec {
 };
 
 // Per-(pod batch, node record) DeviceShare summary (k_dev_sum): the pod batch's distinct GPU requests
-// (at most DEV_CLASSES, host-assigned per pod) each get a nibble of `fit` holding the GPU allocator's
-// outcome on the record (gpu_allocate's reason code), and the minor sums the node Score reads, so that
-// the config-5 fast path does not walk the minors per pair.
-constexpr int DEV_CLASSES = 15;
+// (at most DEV_CLASSES, host-assigned per pod) each get the GPU allocator's outcome on the record
+// (gpu_allocate's reason code) and the node Score, so that the config-5 fast path does not run the
+// allocator or walk the minors per pair.
+constexpr int DEV_CLASSES = 56;
 // A GPU request class: everything the allocator reads of a pod (GPURequirements).
 struct DevClass {
     int64_t dreq[DEV_R];
@@ -361,12 +361,11 @@ struct DevClass {
     int64_t dbw;
 };
 struct alignas(16) DevSum {
-    uint64_t fit;  // per class a nibble: the GPU allocator's DeviceShare reason code (0 = the pod fits)
     int64_t T[DEV_R], F[DEV_R];
-    double rcp[DEV_R];  // 1 / T (least_req's exact-quotient path)
-    uint8_t score[16];  // per class: the node Score (scoreNode over the minor sums, 0..100) of one instance
+    double rcp[DEV_R];             // 1 / T (least_req's exact-quotient path)
+    uint8_t code[DEV_CLASSES];     // per class: the GPU allocator's DeviceShare reason code (0 = the pod fits)
+    uint8_t score[DEV_CLASSES];    // per class: the node Score (scoreNode over the minor sums, 0..100) of one instance
 };
-
 constexpr int QUOTA_R = 4;
 // ElasticQuota mutable state (double-buffered during replay) and static limits.
 struct alignas(16) QuotaState {
@@ -419,6 +418,7 @@ struct ExtDev {
     // GPU count) the entry range: part_rng[table * 9 + n] = begin | end << 16
     const kg_gpu_partition* parts;
     const uint32_t* part_rng;
+    const int64_t* binpack;  // [table][8, 4, 2 GPUs][allocated minors]: free partitions' AllocationScore sum
 };
 
 }  // namespace kg

@@ -119,12 +119,14 @@ struct kg_snap {
     // GPU partition tables (kg_node_columns.gpu_parts): entries and per (table, GPU count) ranges
     kg_gpu_partition* d_parts = nullptr;
     uint32_t* d_part_rng = nullptr;  // [KG_GPU_MAX_TABLES * 9]
+    int64_t* d_binpack = nullptr;    // [KG_GPU_MAX_TABLES][3][256]
     uint32_t n_gpu_tables = 0;
     bool ext() const { return (cfg.plugins & KG_PLUGIN_EXT) != 0; }
     ExtDev ext_dev() const {
         ExtDev e{};
         e.parts = n_gpu_tables ? d_parts : nullptr;
         e.part_rng = d_part_rng;
+        e.binpack = d_binpack;
         e.dev = d_dev;
         e.qlim = d_qlim;
         e.qstate = d_qstate;
@@ -181,6 +183,7 @@ struct kg_pods {
     bool fast_ok = false;  // every pod in the fast domain (no value >= 2^44, no pod NUMA policy, no cpuset binding)
     bool pod_policy = false;  // some pod carries its own NUMA policy
     bool any_cpu_bind = false;  // some pod binds cpusets (KG_POD_CPU_BIND)
+    bool dev_unclassed = false; // some GPU pod has no GPU request class (more than DEV_CLASSES, or a template pod)
     std::vector<uint32_t> h_flags;  // host copies for argument checks (kg_forget of a cpuset pod)
     std::vector<int64_t> h_req_cpu;
     // config-5 scratch
@@ -813,8 +816,25 @@ static kg_status upload_gpu_parts(kg_snap* s, const kg_node_columns* cols) {
         rng[key] = (rng[key] & 0xFFFFu) | ((t + 1u) << 16);
         tables = std::max(tables, (uint32_t)q.table + 1u);
     }
+    // selectPartitionByBinPack's per-size sums for every allocated-minor mask (allocator_gpu.go:270-285): the
+    // partitions of the lowest AllocationScore group of (table, 8 / 4 / 2 GPUs) disjoint from the mask
+    std::vector<int64_t> bp((size_t)KG_GPU_MAX_TABLES * 3 * 256, 0);
+    const uint32_t sizes[3] = {8, 4, 2};
+    for (uint32_t tb = 0; tb < tables; tb++)
+        for (int k = 0; k < 3; k++) {
+            const uint32_t r = rng[tb * 9 + sizes[k]], b = r & 0xFFFFu, en = r >> 16;
+            for (uint32_t mask = 0; mask < 256; mask++) {
+                int64_t sum = 0;
+                for (uint32_t u = b; u < en && cols->gpu_parts[u].alloc_score == cols->gpu_parts[b].alloc_score; u++)
+                    if (!(cols->gpu_parts[u].minors & mask)) sum += cols->gpu_parts[u].alloc_score;
+                bp[((size_t)tb * 3 + k) * 256 + mask] = sum;
+            }
+        }
     if (!s->d_part_rng) HIP_TRY(ctx, hipMalloc(&s->d_part_rng, sizeof(uint32_t) * KG_GPU_MAX_TABLES * 9));
+    if (!s->d_binpack) HIP_TRY(ctx, hipMalloc(&s->d_binpack, sizeof(int64_t) * bp.size()));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_part_rng, rng.data(), sizeof(uint32_t) * rng.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_binpack, bp.data(), sizeof(int64_t) * bp.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // the staging vectors go out of scope
     if (n) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         hipFree(s->d_parts);
@@ -1103,6 +1123,7 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_dev);
     hipFree(s->d_parts);
     hipFree(s->d_part_rng);
+    hipFree(s->d_binpack);
     hipFree(s->d_qlim);
     hipFree(s->d_qstate);
     hipFree(s->d_views);
@@ -1321,6 +1342,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     uint32_t* stat = reinterpret_cast<uint32_t*>(h + L.stat);
     uint32_t np = 0, nx = 0, ns = 0;
     std::vector<DevClass> classes;
+    bool unclassed = false;
     if (!ext_cols && !any_rsv_req) {
         // every pod is "plain": the plain lanes are the wave-kind order of every pod
         std::memcpy(pmap, order, sizeof(uint32_t) * n);
@@ -1352,6 +1374,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
                 if (k == classes.size() && classes.size() < (size_t)DEV_CLASSES) classes.push_back(c);
                 if (k < classes.size()) dcls[j] = (uint8_t)k;
             }
+            unclassed |= cntj > 0 && dcls[j] == (uint8_t)DEV_CLASSES;
             const int32_t q = cols->quota ? cols->quota[j] : -1;
             const int32_t cls = cols->rsv_class ? cols->rsv_class[j] : -1;
             xc[j] = cntj;
@@ -1413,6 +1436,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     p->n_plain = np;
     p->n_x = nx;
     p->n_dclass = (uint32_t)classes.size();
+    p->dev_unclassed = unclassed;
     return KG_OK;
 }
 
@@ -1550,8 +1574,9 @@ static kg_status ensure_partial(kg_pods* p, size_t need) {
 // config-5 pass 1 / pass 2 take the base plugins from the fast block where the fast path is valid:
 // same conditions as the plain-pod split, plus all three base plugins enabled (eval_fast_key<7>)
 static bool ext_fast_base(const kg_snap* s, const kg_pods* p) {
+    // the fast-base kernels read the DeviceShare outcome from DevSum by class: every GPU pod needs one
     return !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok && !need_topo(s, p) &&
-           (s->kcfg.plugins & 7u) == 7u;
+           (s->kcfg.plugins & 7u) == 7u && !p->dev_unclassed;
 }
 
 // config-5 matrix mode, pass 1: quota gate + per-pod NormalizeScore inputs of this shard

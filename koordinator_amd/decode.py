@@ -1081,7 +1081,8 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
     """Host restatement of the Reservation transformer (reservation/transformer.go:147-350,740-935).
 
     `nodes` is the true NodeInfo view (reserve pods and the pods allocated to reservations both
-    counted, as NodeInfo accounts them). Each reservation is a dict: node, cls (owner-match class),
+    counted, as NodeInfo accounts them). Each reservation is a dict: node, cls (owner-match class, or the
+    list of classes that match it as rsvmatch.match_classes returns them),
     allocatable / allocated / reserved (KG_RSV_R vectors, allocated None when no pod is assigned),
     allocated_pods, policy, order, allocate_once, max_pods.
 
@@ -1147,10 +1148,14 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
                 tot, used, fr = node_dev(i)
                 uu = merged(gx, 3)
                 out["dev_free"][i] = dev_effective(tot, used, fr, uu[0], uu[1])[1]
+    def classes_of(r):  # one owner-match class, or the list of classes that match it (rsvmatch.match_classes)
+        c = r["cls"]
+        return {int(c)} if np.isscalar(c) else {int(v) for v in c}
+
     for i in sorted(by_node):
-        classes = sorted({int(reservations[x]["cls"]) for x in by_node[i]})
+        classes = sorted({c for x in by_node[i] for c in classes_of(reservations[x])})
         for c in classes:
-            matched = [x for x in by_node[i] if int(reservations[x]["cls"]) == c]
+            matched = [x for x in by_node[i] if c in classes_of(reservations[x])]
             req = [int(out[col][i]) for col in req_cols]
             nzc, nzm = int(out["nz_cpu"][i]), int(out["nz_mem"][i])
             pod_requested = list(req)

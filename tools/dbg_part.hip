@@ -106,9 +106,23 @@ int main() {
     hipMemcpy(dP, P, sizeof(P), hipMemcpyHostToDevice);
     hipMemcpy(dr, rng, sizeof(rng), hipMemcpyHostToDevice);
     hipMemcpy(dd, &d, sizeof(d), hipMemcpyHostToDevice);
+    static int64_t bp[3 * 256];
+    const uint32_t sizes[3] = {8, 4, 2};
+    for (int k = 0; k < 3; k++)
+        for (uint32_t mask = 0; mask < 256; mask++) {
+            const uint32_t b = rng[sizes[k]] & 0xFFFF, en = rng[sizes[k]] >> 16;
+            int64_t sum = 0;
+            for (uint32_t u = b; u < en; u++)
+                if (!(P[u].minors & mask)) sum += P[u].alloc_score;
+            bp[k * 256 + mask] = sum;
+        }
+    int64_t* dbp;
+    if (hipMalloc(&dbp, sizeof(bp))) return 1;
+    hipMemcpy(dbp, bp, sizeof(bp), hipMemcpyHostToDevice);
     ExtDev e{};
     e.parts = dP;
     e.part_rng = dr;
+    e.binpack = dbp;
     k<<<1, 64>>>(e, dd, dout);
     uint32_t o[2];
     hipMemcpy(o, dout, 8, hipMemcpyDeviceToHost);

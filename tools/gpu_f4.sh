@@ -11,3 +11,11 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_alloc_kat.py tests/test_ext
 tail -2 gpurun_out/gpu_tests_$TAG.log
 timeout -k 10 300 python bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench5_$TAG.json 2> gpurun_out/bench5_$TAG.err || exit 2
 python -c "import json;d=json.loads(open('gpurun_out/bench5_$TAG.json').read().strip().splitlines()[-1]);print('bench5', round(d['ms_per_step'],4), '%.4g'%d['value'])"
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+cd /tmp || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof5_$TAG" -o run --output-format csv -- \
+    python3 "$R/bench.py" --config 5 --steps 5 --warmup 1 --no-cpu-baseline --no-cycle > /dev/null || exit 3
+cd "$R" || exit 1
+f=$(find gpurun_out/prof5_$TAG -name "run_kernel_stats.csv" | head -1)
+head -14 "$f"
