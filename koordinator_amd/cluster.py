@@ -31,7 +31,7 @@ from . import abi
 from .config import CPU, DEV_RESOURCES, MEMORY, SchedulerConfig
 from .decode import (ANN_AMPLIFICATION, LoadAwareNodeCache, NODEINFO_KEYS, Unsupported, _is_terminated, _rl, amplify,
                      assign_info, is_reserve_pod, la_cols, milli_value, node_static_cols, nodeinfo_cols,
-                     pod_request_vec, value, zone_used_cols)
+                     pod_request_vec, pod_requests, value, zone_used_cols)
 
 ANN_RESOURCE_STATUS = "scheduling.koordinator.sh/resource-status"
 ANN_DEVICE_ALLOCATED = "scheduling.koordinator.sh/device-allocated"
@@ -461,6 +461,11 @@ class ClusterState:
         self.row_gen = np.zeros(n, np.uint64)
         self.assign_cache = PodAssignCache(self.la, clock, self._touch_name)
         self.devices = NodeDeviceCache(self._touch_name)
+        # reservation restore inputs (views) and ElasticQuota tables: their own generations, so a sync re-uploads
+        # the views of the nodes whose reservations changed and the quota table only when it changed
+        self.rsv_gen = np.zeros(n, np.uint64)
+        self.reservations = ReservationCache(cfg, self._touch_rsv)
+        self.quotas = QuotaCache(cfg)
         # NodeMetric expiry is a function of time (isNodeMetricExpired, loadaware/helper.go:35-40): a timer per
         # metric marks the row when its deadline passes (tick), as an event would
         self._expiry: List[Tuple[float, int, int]] = []  # (deadline, row, metric token)
@@ -475,6 +480,16 @@ class ClusterState:
         i = self.index.get(name)
         if i is not None:
             self._touch(i)
+
+    def _touch_rsv(self, name: str):
+        i = self.index.get(name)
+        if i is not None:
+            self.generation += 1
+            self.rsv_gen[i] = self.generation
+
+    def rsv_rows_since(self, generation: int) -> np.ndarray:
+        """Nodes whose reservations changed after `generation` (their restore views need rebuilding)."""
+        return np.nonzero(self.rsv_gen > np.uint64(generation))[0].astype(np.uint32)
 
     def tick(self):
         """Mark the rows whose NodeMetric expired since the last tick (the clock's time events)."""
@@ -549,18 +564,70 @@ class ClusterState:
         self.assign_cache.on_add(pod)
         self._numa_update(None, pod)
         self.devices.update_pod(None, pod)
+        self.reservations.add_pod(pod)
+        self.quotas.on_pod(None, pod)
 
     def on_pod_update(self, old, pod):
         self._nodeinfo_update(pod)
         self.assign_cache.on_update(old, pod)
         self._numa_update(old, pod)
         self.devices.update_pod(old, pod)
+        self.reservations.update_pod(old, pod)
+        self.quotas.on_pod(old, pod)
 
     def on_pod_delete(self, pod):
         self._nodeinfo_remove(_uid(pod))
         self.assign_cache.on_delete(pod)
         self._numa_release(_node_name(pod), _uid(pod))
         self.devices.delete_pod(pod)
+        self.reservations.delete_pod(pod)
+        self.quotas.on_pod_delete(pod)
+
+    # reservation / quota informers (reservation/eventhandler_reservation.go, elasticquota/quota_handler.go)
+    @staticmethod
+    def _reserve_pod(r: dict) -> dict:
+        """reservationutil.NewReservePod: the fake pod an Available reservation holds in NodeInfo, requesting its
+        allocatable."""
+        md, status = _md(r), r.get("status") or {}
+        alloc = {k: v for k, v in (status.get("allocatable") or {}).items() if k != "pods"}
+        return {"metadata": {"uid": "reserve-pod/" + md.get("uid", ""), "name": md.get("name", "")},
+                "spec": {"nodeName": status.get("nodeName", ""), "containers": [{"resources": {"requests": alloc}}]}}
+
+    def on_reservation(self, r: dict):
+        """Reservation add / update: the reservation cache (updateReservation) and its reserve pod in NodeInfo
+        while it is Available on a node."""
+        self.reservations.update_reservation(r)
+        rp = self._reserve_pod(r)
+        if (r.get("status") or {}).get("phase") == "Available" and _node_name(rp):
+            self._nodeinfo_update(rp)
+        else:
+            self._nodeinfo_remove(_uid(rp))
+
+    def on_reservation_delete(self, r: dict):
+        self.reservations.delete_reservation(r)
+        self._nodeinfo_remove(_uid(self._reserve_pod(r)))
+
+    def reservation_restore(self, pods: Sequence[dict], rows: Optional[abi.Table] = None):
+        """The Reservation transformer's restore for a pending batch: owner-match classes of the pods over the
+        matchable reservations (rsvmatch.match_classes), then decode.reservation_restore over the current rows.
+        Returns (rsv_class per pod, restored node table, abi.Reservations)."""
+        from . import decode, rsvmatch
+        infos = [ri for ri in self.reservations.infos.values() if ri.matchable() and ri.node in self.index]
+        infos.sort(key=lambda ri: (self.index[ri.node], ri.uid))
+        nodes_by_name = {n: self.nodes[i] for n, i in self.index.items()}
+        cls, rsv_cls, _ = rsvmatch.match_classes(list(pods), [pod_requests(p) for p in pods], [ri.obj for ri in infos],
+                                                 nodes_by_name)
+        by_uid = {ri.uid: c for ri, c in zip(infos, rsv_cls)}
+        resv = self.reservations.restore_inputs(self.index, lambda ri: by_uid.get(ri.uid, []))
+        table = self.table() if rows is None else rows
+        t, views, vinfos, devs = decode.reservation_restore(table, resv)
+        return np.array(cls, np.int32), t, abi.Reservations(views, vinfos, devs)
+
+    def on_quota(self, q: dict):
+        self.quotas.on_quota(q)
+
+    def on_quota_delete(self, name: str):
+        self.quotas.on_quota_delete(name)
 
     def assume(self, pod, node_name: str):
         """The scheduler's Reserve of a placement: cache AssumePod (NodeInfo) and LoadAware Reserve
@@ -685,3 +752,260 @@ class SnapshotSync:
             if len(sel):
                 s.update_rows(rows[sel] - lo, abi.take(table, sel))
         return len(rows)
+
+
+# ---- Reservation cache (reservation/cache.go:761-1104, frameworkext/reservation_info.go) --------------------
+
+ANN_RESERVATION_ALLOCATED = "scheduling.koordinator.sh/reservation-allocated"
+LABEL_RESERVATION_ORDER = "scheduling.koordinator.sh/reservation-order"
+RSV_VEC = (CPU, MEMORY, "ephemeral-storage")  # KG_RSV_R order: cpu, memory, ephemeral-storage, scalar0, scalar1
+
+
+class ReservationInfo:
+    """frameworkext.ReservationInfo of a Reservation object: Allocatable (status), ResourceNames (its keys),
+    Allocated = Σ Mask(requests, ResourceNames) of the assigned pods, the owners / policy / order the restore and
+    the matching read."""
+
+    def __init__(self, r: dict, cfg: SchedulerConfig):
+        self.cfg = cfg
+        self.assigned: Dict[str, List[int]] = {}  # pod uid -> masked request vector
+        self.update(r)
+
+    def update(self, r: dict):
+        self.obj = r
+        md, spec, status = _md(r), r.get("spec") or {}, r.get("status") or {}
+        self.uid = md.get("uid", "")
+        self.name = md.get("name", "")
+        self.node = status.get("nodeName", "")
+        self.phase = status.get("phase", "")
+        alloc = status.get("allocatable") or {}
+        self.names = [k for k in alloc]
+        self.allocatable = self._vec(alloc)
+        self.max_pods = value(alloc["pods"]) if "pods" in alloc else -1
+        self.policy = {"Aligned": abi.KG_RSV_ALIGNED, "Restricted": abi.KG_RSV_RESTRICTED}.get(
+            spec.get("allocatePolicy", ""), abi.KG_RSV_DEFAULT)
+        self.allocate_once = spec.get("allocateOnce", True) is not False
+        self.terminating = md.get("deletionTimestamp") is not None
+        try:
+            self.order = int((md.get("labels") or {}).get(LABEL_RESERVATION_ORDER, "0"))
+        except ValueError:
+            self.order = 0
+
+    def _vec(self, rl: dict) -> List[int]:
+        names = [self.cfg.scalar_resources[k] if k < len(self.cfg.scalar_resources) else "" for k in range(abi.KG_NSCALAR)]
+        out = []
+        for k, key in enumerate(list(RSV_VEC) + names):
+            q = rl.get(key)
+            out.append(0 if q is None else (milli_value(q) if key == CPU else value(q)))
+        return out
+
+    def mask(self, req: Dict[str, object]) -> List[int]:
+        """quotav1.Mask(requests, ResourceNames) as a KG_RSV_R vector."""
+        return self._vec({k: v for k, v in req.items() if k in self.names})
+
+    @property
+    def allocated(self) -> List[int]:
+        tot = [0] * abi.KG_RSV_R
+        for v in self.assigned.values():
+            tot = [a + b for a, b in zip(tot, v)]
+        return tot
+
+    def matchable(self) -> bool:
+        """IsMatchable (reservation_info.go:546-569): Available, and not an allocate-once reservation with pods."""
+        if self.phase != "Available":
+            return False
+        return not (self.allocate_once and len(self.assigned) > 0)
+
+
+class ReservationCache:
+    """reservationCache: reservation infos by uid, the reservations of each node, and the assigned-pod
+    bookkeeping of addPod / updatePod / deletePod (keyed by the pod's reservation-allocated annotation)."""
+
+    def __init__(self, cfg: SchedulerConfig, on_change: Callable[[str], None] = lambda node: None):
+        self.cfg = cfg
+        self.infos: Dict[str, ReservationInfo] = {}
+        self.on_node: Dict[str, Set[str]] = {}
+        self.on_change = on_change
+
+    def update_reservation(self, r: dict):
+        """updateReservation / assumeReservation (cache.go:785-844)."""
+        uid = _md(r).get("uid", "")
+        ri = self.infos.get(uid)
+        old_node = ri.node if ri else ""
+        if ri is None:
+            ri = self.infos[uid] = ReservationInfo(r, self.cfg)
+        else:
+            ri.update(r)
+        if old_node and old_node != ri.node:
+            self.on_node.get(old_node, set()).discard(uid)
+            self.on_change(old_node)
+        if ri.node:
+            self.on_node.setdefault(ri.node, set()).add(uid)
+            self.on_change(ri.node)
+
+    def delete_reservation(self, r: dict):
+        """DeleteReservation / forgetReservation (cache.go:789-791,893-918)."""
+        uid = _md(r).get("uid", "")
+        ri = self.infos.pop(uid, None)
+        node = (r.get("status") or {}).get("nodeName", "") or (ri.node if ri else "")
+        if node:
+            self.on_node.get(node, set()).discard(uid)
+            self.on_change(node)
+
+    @staticmethod
+    def reservation_of(pod) -> str:
+        raw = (_md(pod).get("annotations") or {}).get(ANN_RESERVATION_ALLOCATED)
+        return (json.loads(raw) or {}).get("uid", "") if raw else ""
+
+    def _add(self, ruid: str, pod) -> bool:
+        ri = self.infos.get(ruid)
+        if ri is None or ri.terminating or _uid(pod) in ri.assigned:
+            return False  # addPods: unknown / terminating reservation; AddAssignedPod skips repeats
+        ri.assigned[_uid(pod)] = ri.mask(pod_requests(pod))
+        self.on_change(ri.node)
+        return True
+
+    def _remove(self, ruid: str, pod):
+        ri = self.infos.get(ruid)
+        if ri is not None and ri.assigned.pop(_uid(pod), None) is not None:
+            self.on_change(ri.node)
+
+    def add_pod(self, pod):
+        ruid = self.reservation_of(pod)
+        if ruid:
+            self._add(ruid, pod)
+
+    def update_pod(self, old, pod):
+        """updatePod (cache.go:1047-1079): the old reservation forgets the pod, the new one adds it."""
+        o, n = self.reservation_of(old) if old else "", self.reservation_of(pod)
+        if o:
+            self._remove(o, old)
+        if n and not _is_terminated(pod):
+            self._add(n, pod)
+
+    def delete_pod(self, pod):
+        ruid = self.reservation_of(pod)
+        if ruid:
+            self._remove(ruid, pod)
+
+    def assume_pod(self, ruid: str, pod):
+        """assumePod (cache.go:1004-1006): the scheduler's Reserve into a reservation."""
+        return self._add(ruid, pod)
+
+    def forget_pod(self, ruid: str, pod):
+        self._remove(ruid, pod)
+
+    def restore_inputs(self, node_index: Dict[str, int], classes_of=None) -> List[dict]:
+        """The matchable reservations of every node as decode.reservation_restore reads them
+        (ForEachMatchableReservationOnNode, cache.go:1162-1180); classes_of(info) -> owner-match classes."""
+        out = []
+        for name in sorted(self.on_node, key=lambda nm: node_index.get(nm, -1)):
+            i = node_index.get(name)
+            if i is None:
+                continue
+            for uid in sorted(self.on_node[name]):
+                ri = self.infos[uid]
+                if not ri.matchable():
+                    continue
+                names = 0
+                for k, key in enumerate(list(RSV_VEC) + list(self.cfg.scalar_resources[:abi.KG_NSCALAR])):
+                    if key in ri.names:
+                        names |= 1 << k
+                out.append(dict(node=i, cls=classes_of(ri) if classes_of else [], uid=uid,
+                                allocatable=ri.allocatable, allocated=ri.allocated if ri.assigned else None,
+                                reserved=None, allocated_pods=len(ri.assigned), policy=ri.policy, order=ri.order,
+                                allocate_once=ri.allocate_once, max_pods=ri.max_pods, names=names))
+        return out
+
+
+# ---- ElasticQuota cache (elasticquota/quota_handler.go, core/group_quota_manager.go) ------------------------
+
+LABEL_QUOTA_NAME = "quota.scheduling.koordinator.sh/name"
+QUOTA_VEC = (CPU, MEMORY)  # KG_QUOTA_R order: cpu, memory, scalar0, scalar1
+
+
+class QuotaCache:
+    """Flat ElasticQuotas (EnableCheckParentQuota false, EnableRuntimeQuota false: usedLimit = max) kept from
+    quota and pod events: OnQuotaAdd / OnQuotaUpdate / OnQuotaDelete set max / min, OnPodAdd / OnPodUpdate /
+    OnPodDelete move the pod's request (Mask(requests, max names)) in and out of its quota's used, and of the
+    non-preemptible used for non-preemptible pods. Rows are quota indices (stable: a deleted quota's row is
+    cleared, not reused)."""
+
+    def __init__(self, cfg: SchedulerConfig):
+        self.cfg = cfg
+        self.index: Dict[str, int] = {}
+        self.max: List[Optional[Dict[str, object]]] = []
+        self.min: List[Dict[str, object]] = []
+        self.pods: Dict[str, Tuple[int, List[int], bool]] = {}  # uid -> (quota row, masked request, non-preemptible)
+        self.generation = 0
+
+    def _keys(self) -> List[str]:
+        return list(QUOTA_VEC) + list(self.cfg.scalar_resources[:abi.KG_NSCALAR])
+
+    def _vec(self, rl: Dict[str, object]) -> Tuple[List[int], int]:
+        v, keys = [], 0
+        for k, key in enumerate(self._keys()):
+            q = rl.get(key)
+            if q is not None:
+                keys |= 1 << k
+            v.append(0 if q is None else (milli_value(q) if key == CPU else value(q)))
+        return v, keys
+
+    def on_quota(self, q: dict):
+        name = _md(q).get("name", "")
+        spec = q.get("spec") or {}
+        if name not in self.index:
+            self.index[name] = len(self.max)
+            self.max.append(None)
+            self.min.append({})
+        i = self.index[name]
+        self.max[i] = dict(spec.get("max") or {})
+        self.min[i] = dict(spec.get("min") or {})
+        self.generation += 1
+
+    def on_quota_delete(self, name: str):
+        i = self.index.get(name)
+        if i is not None:
+            self.max[i] = None
+            self.generation += 1
+
+    def _quota_of(self, pod) -> Optional[int]:
+        name = (_md(pod).get("labels") or {}).get(LABEL_QUOTA_NAME)
+        i = self.index.get(name) if name else None
+        return i if i is not None and self.max[i] is not None else None
+
+    def on_pod(self, old, pod):
+        """OnPodAdd / OnPodUpdate: an assigned, non-terminated pod counts in its quota's used."""
+        uid = _uid(pod)
+        ent = self.pods.pop(uid, None)
+        if ent is not None:
+            self.generation += 1
+        i = self._quota_of(pod)
+        if i is None or not _node_name(pod) or _is_terminated(pod):
+            return
+        mx = self.max[i]
+        req = {k: v for k, v in pod_requests(pod).items() if k in mx}
+        vec, _ = self._vec(req)
+        np_ = (_md(pod).get("labels") or {}).get("quota.scheduling.koordinator.sh/preemptible") == "false"
+        self.pods[uid] = (i, vec, np_)
+        self.generation += 1
+
+    def on_pod_delete(self, pod):
+        if self.pods.pop(_uid(pod), None) is not None:
+            self.generation += 1
+
+    def columns(self) -> abi.Table:
+        n = len(self.max)
+        t = abi.empty_quotas(n)
+        for i in range(n):
+            if self.max[i] is None:
+                continue
+            t["used_limit"][i], t["limit_keys"][i] = self._vec(self.max[i])
+            t["min"][i], t["min_keys"][i] = self._vec(self.min[i])
+        for i, vec, np_ in self.pods.values():
+            t["used"][i] += vec
+            t["used_keys"][i] |= t["limit_keys"][i]
+            if np_:
+                t["np_used"][i] += vec
+                t["np_used_keys"][i] |= t["limit_keys"][i]
+        return t
