@@ -722,23 +722,36 @@ __device__ __forceinline__ uint32_t dev_outside_used(const DevRec* __restrict__ 
     return o;
 }
 
+// dcls < DEV_CLASSES with e.rcode: the restore tables' allocator outcomes come from k_rdev_codes, and the node's own
+// table (a view without a base table) from the batch's DevSum.
 __device__ __forceinline__ uint32_t dev_filter_view(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
                                                     const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
-                                                    const RsvView& v, const PodX& x, bool required) {
+                                                    const RsvView& v, const PodX& x, bool required, uint32_t rec,
+                                                    uint32_t dcls = (uint32_t)DEV_CLASSES) {
     const int32_t D = (int32_t)n[N_DEV_MINORS];
     if (D < 0) return 0;  // no Device object
     if (D == 0) return KG_ST_DEV_NO_DEVICE;
+    if (x.dflags & KG_GPU_POD_TEMPLATE) return KG_ST_UNSUPPORTED;
+    const bool tab_codes = e.rcode && dcls < (uint32_t)DEV_CLASSES;
     bool any = false;
     for (uint32_t t = 0; t < v.count; t++) {
         const int32_t di = e.infos[v.first + t].dev;
         if (di < 0) continue;
         any = true;
         int64_t raw;
+        if (tab_codes) {
+            if (e.rcode[(size_t)di * DEV_CLASSES + dcls] == 0) return 0;
+            continue;
+        }
         const DevRec* tab = e.rdev + di;
         if (dev_eval(c, e, n, zr, tab, x, raw, dev_outside_used(d, tab, D)) == 0) return 0;
     }
     if (any && required) return KG_ST_DEV_RSV;
     int64_t raw;
+    if (tab_codes) {
+        if (v.dev_base >= 0) return dev_code_status(e.rcode[(size_t)v.dev_base * DEV_CLASSES + dcls]);
+        if (e.dsum) return dev_code_status(e.dsum[rec].code[dcls]);
+    }
     const DevRec* tab = v.dev_base >= 0 ? e.rdev + v.dev_base : d;
     return dev_eval(c, e, n, zr, tab, x, raw, tab == d ? 0u : dev_outside_used(d, tab, D));
 }
@@ -794,7 +807,7 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     const bool dev_view = (c.plugins & KG_PLUGIN_DEV) && v && x.dcount > 0;
     if (c.plugins & KG_PLUGIN_DEV) {
         if (dev_view)
-            st |= dev_filter_view(c, e, n, zr, d, *v, x, (p.flags & KG_POD_RSV_REQUIRED) != 0);
+            st |= dev_filter_view(c, e, n, zr, d, *v, x, (p.flags & KG_POD_RSV_REQUIRED) != 0, rec, dcls);
         else if (e.dsum && dcls < (uint32_t)DEV_CLASSES)
             st |= dev_eval_sum(c, e, n, zr, d, e.dsum + rec, x, dcls, dev_raw);
         else

@@ -81,6 +81,34 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
     out[rec] = o;
 }
 
+// GPU allocator outcome of every reservation restore table for every GPU request class of the batch (thread =
+// table): the view pairs of the select / stats kernels then read a code instead of running the allocator.
+__global__ __launch_bounds__(256) void k_rdev_codes(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                    const DevRec* __restrict__ devs, const DevRec* __restrict__ rdev,
+                                                    const uint32_t* __restrict__ rdev_rec, uint32_t n_rdev,
+                                                    const DevClass* __restrict__ cls, uint32_t n_cls, KCfg cfg, ExtDev e,
+                                                    uint8_t* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_rdev) return;
+    const uint32_t rec = rdev_rec[t];
+    const int32_t D = (int32_t)nodes[rec].v[N_DEV_MINORS];
+    const DevRec* tab = rdev + t;
+    const uint32_t outside = D > 0 ? dev_outside_used(devs + rec, tab, D) : 0u;
+    for (uint32_t k = 0; k < (uint32_t)DEV_CLASSES; k++) {
+        uint8_t code = 0;
+        if (k < n_cls && D > 0) {
+            PodX x{};
+            x.dkeys = cls[k].dkeys;
+            x.dcount = cls[k].dcount;
+            x.dflags = cls[k].dflags;
+            x.dbw = cls[k].dbw;
+            for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
+            code = (uint8_t)gpu_allocate(cfg, e, tab, D, zones[rec].dev_topo, zones[rec].dev_part, x, outside, false).code;
+        }
+        out[(size_t)t * DEV_CLASSES + k] = code;
+    }
+}
+
 // Records the fast-base kernels (PART 1) take for no pod: F_BIG or storage class 1. special[0] = count,
 // special[1..] = records (any order: keys are order-free).
 __global__ __launch_bounds__(256) void k_special_scan(const NodeRec* __restrict__ nodes, uint32_t n_nodes, uint32_t n0,
@@ -801,6 +829,14 @@ hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t 
     hipError_t e = hipMemsetAsync(special, 0, sizeof(uint32_t), s);
     if (e != hipSuccess || n_nodes == 0) return e;
     k_special_scan<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, n_nodes, n0, special);
+    return hipGetLastError();
+}
+
+hipError_t launch_rdev_codes(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, const DevRec* rdev,
+                             const uint32_t* rdev_rec, uint32_t n_rdev, const DevClass* cls, uint32_t n_cls,
+                             const KCfg& cfg, const ExtDev& e, uint8_t* out, hipStream_t s) {
+    if (n_rdev == 0) return hipSuccess;
+    k_rdev_codes<<<(n_rdev + 255) / 256, 256, 0, s>>>(nodes, zones, devs, rdev, rdev_rec, n_rdev, cls, n_cls, cfg, e, out);
     return hipGetLastError();
 }
 

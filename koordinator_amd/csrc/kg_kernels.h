@@ -146,6 +146,9 @@ inline void ext_part2_grid(uint32_t special_est, uint32_t pod_blocks, uint32_t* 
     *n_chunks = (est + *chunk - 1) / *chunk;
 }
 hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, hipStream_t s);
+hipError_t launch_rdev_codes(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, const DevRec* rdev,
+                             const uint32_t* rdev_rec, uint32_t n_rdev, const DevClass* cls, uint32_t n_cls,
+                             const KCfg& cfg, const ExtDev& e, uint8_t* out, hipStream_t s);
 hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
                           const KCfg& cfg, const ExtDev& e,
                           DevSum* out, hipStream_t s);

@@ -419,6 +419,9 @@ struct ExtDev {
     const kg_gpu_partition* parts;
     const uint32_t* part_rng;
     const int64_t* binpack;  // [table][8, 4, 2 GPUs][allocated minors]: free partitions' AllocationScore sum
+    // per batch (with dsum): the GPU allocator's code of every restore table (rdev) for every GPU request class,
+    // [table][DEV_CLASSES]; nullptr = run the allocator
+    const uint8_t* rcode;
 };
 
 }  // namespace kg

@@ -76,6 +76,8 @@ struct kg_snap {
     RsvInfo* d_infos = nullptr;
     uint32_t* d_cls_begin = nullptr;  // [RSV_MAX_CLASSES + 1]
     DevRec* d_rdev = nullptr;         // kg_rsv_dev tables
+    uint32_t* d_rdev_rec = nullptr;   // record (position) of the node each kg_rsv_dev table belongs to
+    uint32_t n_rdev = 0;
     uint32_t* d_special = nullptr;    // [0] = count, [1..]: records the fast-base ext kernels leave to PART 2
     uint32_t n_view_nodes = 0;        // nodes holding a reservation view
     // PART 2 grid: the class-1 records and the largest reservation class's views (F_BIG records come on top)
@@ -171,6 +173,8 @@ struct kg_pods {
     uint32_t* d_reason = nullptr;  // replay: per pod OR of the filter status bits (kg_replay out_reason)
     DevSum* d_devsum = nullptr;    // per record DevSum of the last config-5 select
     size_t devsum_cap = 0;
+    uint8_t* d_rcode = nullptr;    // [kg_rsv_dev table][DEV_CLASSES]: GPU allocator outcome on the restore tables
+    size_t rcode_cap = 0;
     // pass-1 pair results kept for pass 2 (ExtDev.pairs)
     uint32_t* d_pairs = nullptr;
     size_t pairs_cap = 0;  // entries
@@ -1123,6 +1127,7 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_dev);
     hipFree(s->d_parts);
     hipFree(s->d_part_rng);
+    hipFree(s->d_rdev_rec);
     hipFree(s->d_binpack);
     hipFree(s->d_qlim);
     hipFree(s->d_qstate);
@@ -1387,13 +1392,14 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             if (cntj == 0 && cls < 0 && !(f[j] & KG_POD_RSV_REQUIRED)) pmap[np++] = j;
             else xlist[nx++] = j;
         }
-        // wave-uniform work in the config-5 kernels: GPU pods (by GPU count) first, then reservation
-        // classes in order; rows are scattered back by list, so the order does not change any result
+        // wave-uniform work in the config-5 kernels: pods without a GPU request first (n_stat_cls, pairs_row0 rely
+        // on it), then within each part by reservation class (the general-record kernels walk the class's views per
+        // lane), then by GPU request; rows are scattered back by list, so the order does not change any result
         auto kind = [&](uint32_t j) {
             const uint32_t c = xc[j];
             const uint64_t gpu = c > 0 ? ((uint64_t)(0u - c) << 8) | (xc[(size_t)n + j] & 0xFFu) : 0u;  // count, request keys
             const int32_t cls = (int32_t)xc[4 * (size_t)n + j];
-            return std::make_tuple(gpu, (f[j] & KG_POD_RSV_REQUIRED) != 0, cls);
+            return std::make_tuple(c > 0, cls, (f[j] & KG_POD_RSV_REQUIRED) != 0, gpu);
         };
         auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
         std::stable_sort(stat, stat + ns, by_kind);
@@ -1447,7 +1453,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
                     (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
                     (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
-                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_pairs, (void*)p->d_batch})
+                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_pairs, (void*)p->d_batch, (void*)p->d_rcode})
         hipFree(b);
     hipHostFree(p->h_in);
     hipHostFree(p->h_keys);
@@ -1596,6 +1602,21 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(), p->d_devsum,
                                 ctx->stream));
     e.dsum = p->d_devsum;
+    e.rcode = nullptr;
+    if (s->n_rdev && s->d_rdev && p->n_dclass) {  // the GPU restore tables of the reservation views, per class
+        const size_t need = (size_t)s->n_rdev * DEV_CLASSES;
+        if (p->rcode_cap < need) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(p->d_rcode));
+            p->d_rcode = nullptr;
+            p->rcode_cap = 0;
+            HIP_TRY(ctx, hipMalloc(&p->d_rcode, need));
+            p->rcode_cap = need;
+        }
+        HIP_TRY(ctx, launch_rdev_codes(s->d_nodes, s->d_zones, s->d_dev, s->d_rdev, s->d_rdev_rec, s->n_rdev, p->d_dclass,
+                                       p->n_dclass, s->kcfg, s->ext_dev(), p->d_rcode, ctx->stream));
+        e.rcode = p->d_rcode;
+    }
     return KG_OK;
 }
 
@@ -1754,6 +1775,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     if (st != KG_OK) return st;
     ExtDev xe = s->ext_dev();
     xe.dsum = (s->d_dev && ext_fast_base(s, p)) ? p->d_devsum : nullptr;  // ext_stats_local built it for this batch
+    xe.rcode = (xe.dsum && s->n_rdev && p->n_dclass) ? p->d_rcode : nullptr;   // and the restore tables' codes
     if (p->pairs_on && xe.dsum) {  // and the pass-1 pair table
         xe.pairs = p->d_pairs;
         xe.pairs_ld = (p->n_stat - p->n_stat_cls + 63u) & ~63u;
@@ -2609,13 +2631,26 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
         d.max_pods = x.max_pods;
         d.allocated_pods = x.allocated_pods;
     }
+    // the node record of every GPU restore table (a table belongs to one view: its base or one of its reservations)
+    std::vector<uint32_t> rrec(std::max<uint32_t>(nd, 1), 0u);
+    for (uint32_t v = 0; v < nv; v++) {
+        const uint32_t rec = s->pos[views[v].node];
+        if (views[v].dev_base >= 0) rrec[views[v].dev_base] = rec;
+        for (uint32_t t = views[v].first; t < views[v].first + views[v].count; t++)
+            if (infos[t].dev >= 0) rrec[infos[t].dev] = rec;
+    }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    for (void* b : {(void*)s->d_views, (void*)s->d_infos, (void*)s->d_cls_begin, (void*)s->d_rdev}) hipFree(b);
+    for (void* b : {(void*)s->d_views, (void*)s->d_infos, (void*)s->d_cls_begin, (void*)s->d_rdev, (void*)s->d_rdev_rec})
+        hipFree(b);
     s->d_views = nullptr;
     s->d_infos = nullptr;
     s->d_cls_begin = nullptr;
     s->d_rdev = nullptr;
+    s->d_rdev_rec = nullptr;
+    s->n_rdev = nd;
+    HIP_TRY(ctx, hipMalloc(&s->d_rdev_rec, sizeof(uint32_t) * rrec.size()));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_rdev_rec, rrec.data(), sizeof(uint32_t) * rrec.size(), hipMemcpyHostToDevice, ctx->stream));
     static_assert(sizeof(DevRec) == sizeof(kg_rsv_dev), "kg_rsv_dev is a DevRec");
     HIP_TRY(ctx, hipMalloc(&s->d_rdev, sizeof(DevRec) * std::max<uint32_t>(nd, 1)));
     if (nd) HIP_TRY(ctx, hipMemcpyAsync(s->d_rdev, devs, sizeof(DevRec) * nd, hipMemcpyHostToDevice, ctx->stream));
