@@ -40,8 +40,11 @@ __device__ __forceinline__ int32_t wmax_i32(int32_t v) {
 
 __device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) { return e.dev ? e.dev + rec : nullptr; }
 
-// DevSum of every record for the pod batch's GPU request classes (one thread per record): the minor sums, and per
-// class the GPU allocator's outcome and the node Score.
+constexpr uint32_t DSUM_CHUNK = 8;  // GPU request classes per thread of k_dev_sum / k_rdev_codes
+
+// DevSum of every record for the pod batch's GPU request classes: thread = (record, chunk of DSUM_CHUNK classes,
+// blockIdx.y); each thread sums the record's minors and, per class of its chunk, runs the GPU allocator and scores
+// one instance; chunk 0 also stores the sums.
 __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                  const DevRec* __restrict__ devs, uint32_t n_nodes,
                                                  const DevClass* __restrict__ cls, uint32_t n_cls, KCfg cfg, ExtDev e,
@@ -62,7 +65,16 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
         o.F[r] = f;
         o.rcp[r] = t != 0 ? 1.0 / (double)t : 0.0;
     }
-    for (uint32_t k = 0; k < (uint32_t)DEV_CLASSES; k++) {
+    DevSum& w = out[rec];
+    const uint32_t k0 = blockIdx.y * DSUM_CHUNK, k1 = min(k0 + DSUM_CHUNK, (uint32_t)DEV_CLASSES);
+    if (blockIdx.y == 0) {
+        for (int r = 0; r < DEV_R; r++) {
+            w.T[r] = o.T[r];
+            w.F[r] = o.F[r];
+            w.rcp[r] = o.rcp[r];
+        }
+    }
+    for (uint32_t k = k0; k < k1; k++) {
         uint8_t code = 0, score = 0;
         if (k < n_cls) {
             PodX x{};
@@ -75,14 +87,13 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
             code = (uint8_t)(D > 0 ? gpu_allocate(cfg, e, &d, D, zr.dev_topo, zr.dev_part, x, 0u, false).code : 0u);
             score = (uint8_t)dev_sum_score(cfg, &o, x);
         }
-        o.code[k] = code;
-        o.score[k] = score;
+        w.code[k] = code;
+        w.score[k] = score;
     }
-    out[rec] = o;
 }
 
 // GPU allocator outcome of every reservation restore table for every GPU request class of the batch (thread =
-// table): the view pairs of the select / stats kernels then read a code instead of running the allocator.
+// (table, chunk of classes)): the view pairs of the select / stats kernels then read a code instead of running the allocator.
 __global__ __launch_bounds__(256) void k_rdev_codes(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                     const DevRec* __restrict__ devs, const DevRec* __restrict__ rdev,
                                                     const uint32_t* __restrict__ rdev_rec, uint32_t n_rdev,
@@ -94,7 +105,8 @@ __global__ __launch_bounds__(256) void k_rdev_codes(const NodeRec* __restrict__ 
     const int32_t D = (int32_t)nodes[rec].v[N_DEV_MINORS];
     const DevRec* tab = rdev + t;
     const uint32_t outside = D > 0 ? dev_outside_used(devs + rec, tab, D) : 0u;
-    for (uint32_t k = 0; k < (uint32_t)DEV_CLASSES; k++) {
+    const uint32_t k0 = blockIdx.y * DSUM_CHUNK, k1 = min(k0 + DSUM_CHUNK, (uint32_t)DEV_CLASSES);
+    for (uint32_t k = k0; k < k1; k++) {
         uint8_t code = 0;
         if (k < n_cls && D > 0) {
             PodX x{};
@@ -836,7 +848,9 @@ hipError_t launch_rdev_codes(const NodeRec* nodes, const ZoneRec* zones, const D
                              const uint32_t* rdev_rec, uint32_t n_rdev, const DevClass* cls, uint32_t n_cls,
                              const KCfg& cfg, const ExtDev& e, uint8_t* out, hipStream_t s) {
     if (n_rdev == 0) return hipSuccess;
-    k_rdev_codes<<<(n_rdev + 255) / 256, 256, 0, s>>>(nodes, zones, devs, rdev, rdev_rec, n_rdev, cls, n_cls, cfg, e, out);
+    const uint32_t chunks = ((uint32_t)DEV_CLASSES + DSUM_CHUNK - 1) / DSUM_CHUNK;
+    k_rdev_codes<<<dim3((n_rdev + 63) / 64, chunks), 64, 0, s>>>(nodes, zones, devs, rdev, rdev_rec, n_rdev, cls, n_cls, cfg, e,
+                                                                 out);
     return hipGetLastError();
 }
 
@@ -844,7 +858,9 @@ hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevR
                           const KCfg& cfg, const ExtDev& e,
                           DevSum* out, hipStream_t s) {
     if (n_nodes == 0) return hipSuccess;
-    k_dev_sum<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, zones, devs, n_nodes, cls, n_cls, cfg, e, out);
+    // every chunk of DEV_CLASSES is written (classes past n_cls get code / score 0)
+    const uint32_t chunks = ((uint32_t)DEV_CLASSES + DSUM_CHUNK - 1) / DSUM_CHUNK;
+    k_dev_sum<<<dim3((n_nodes + 255) / 256, chunks), 256, 0, s>>>(nodes, zones, devs, n_nodes, cls, n_cls, cfg, e, out);
     return hipGetLastError();
 }
 
