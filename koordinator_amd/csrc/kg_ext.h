@@ -81,24 +81,27 @@ struct GpuAlloc {
 //         (a reservation restore's filtered nodeDevice);
 //   total hashDevices(removeZeroDevice(deviceTotal)) (:87,112-120,200);
 //   sat   DeviceLevelContext.satisfied (:404-414): LessThanOrEqual(requestsPerGPU, free) and in total.
+//   fit   defaultAllocateDevices' per-minor test (dev_minor_fits): free not all zero and covering the request.
 struct GpuMinors {
-    uint32_t used, total, sat;
+    uint32_t used, total, sat, fit;
 };
 
 __device__ __forceinline__ GpuMinors gpu_minors(const DevRec* __restrict__ d, int32_t D, const PodX& x, uint32_t outside) {
-    GpuMinors g{outside, 0u, 0u};
+    GpuMinors g{outside, 0u, 0u, 0u};
     for (int32_t m = 0; m < D; m++) {
-        bool any_t = false, diff = false, le = true;
+        bool any_t = false, diff = false, le = true, any_f = false;
 #pragma unroll
         for (int r = 0; r < DEV_R; r++) {
             const int64_t t = d->total[r][m], f = d->free_[r][m];
             any_t |= t != 0;
+            any_f |= f != 0;
             diff |= f != t;
             le &= !(((x.dkeys >> r) & 1u) && x.dreq[r] > f);
         }
         g.used |= diff ? 1u << m : 0u;
         g.total |= any_t ? 1u << m : 0u;
         g.sat |= (any_t && le) ? 1u << m : 0u;
+        g.fit |= (any_f && le) ? 1u << m : 0u;
     }
     return g;
 }
@@ -121,7 +124,8 @@ __device__ __forceinline__ bool partition_ok(const kg_gpu_partition& q, const Gp
 // (An earlier form with the bin-pack weights in a local array indexed by the loop counter returned a wrong
 // partition on gfx950 at -O1 and -O3 while the same source was right on the host and right with a printf in
 // the loop: tools/dbg_part.hip keeps it as a reproducer; this form is checked by tests/test_gpu_alloc_kat.py.)
-__device__ __forceinline__ GpuAlloc gpu_partition(const ExtDev& e, uint32_t tbl, const PodX& x, const GpuMinors& g) {
+__device__ __forceinline__ GpuAlloc gpu_partition(const ExtDev& e, uint32_t tbl, const PodX& x, const GpuMinors& g,
+                                                  bool want_mask = true) {
     if (tbl == 0u || !e.parts) return {KG_DEV_CODE_NO_PARTITION, 0u};
     const uint32_t N = x.dcount;
     if (N > 8u) return {KG_DEV_CODE_PART_COUNT, 0u};
@@ -143,6 +147,7 @@ __device__ __forceinline__ GpuAlloc gpu_partition(const ExtDev& e, uint32_t tbl,
         gb = ge;
     }
     if (nfeas == 0u) return {KG_DEV_CODE_PARTITIONED, 0u};
+    if (!want_mask) return {0u, 0u};  // the Filter: which partition the bin-pack picks does not matter
     // selectPartitionByBinPack (:261-296): the first of the highest bin-pack scores (sort.Slice of <= 12
     // elements is an insertion sort, stable); scoreOfNumOfGPUs 8: 10000, 4: 100, 2: 1
     uint32_t best_mask = 0u;
@@ -264,6 +269,39 @@ __device__ __forceinline__ uint32_t gpu_scope(const KCfg& c, const DevRec* __res
     return scope_take(c, d, x, root, g, shared, 1, cne1).mask;
 }
 
+// gpu_scope's outcome without the choice (the Filter): a take at a scope succeeds iff the scope holds N satisfied
+// minors, and a scope's minors include its children's, so the tree allocates iff some scope the required level
+// admits (PCIe: level <= 3, NUMA: <= 2, the node: <= 1) has N satisfied minors.
+__device__ __forceinline__ bool gpu_scope_fits(int32_t D, uint64_t topo, uint32_t N, const GpuMinors& g, int32_t level) {
+    const uint32_t root = D >= 32 ? ~0u : (1u << D) - 1u;
+    if ((uint32_t)__popc(root) < N) return false;
+    if (level <= 1) return (uint32_t)__popc(root & g.sat) >= N;
+    uint32_t numa[DEV_MINORS], pcie[DEV_MINORS], pcie_numa[DEV_MINORS];
+#pragma unroll
+    for (int k = 0; k < DEV_MINORS; k++) numa[k] = pcie[k] = pcie_numa[k] = 0u;
+    for (int32_t m = 0; m < D; m++) {
+        const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
+        if (b == KG_GPU_NO_SCOPE) continue;
+        const uint32_t q = (b >> 4) & 7u, r = b & 7u;
+        numa[q] |= 1u << m;
+        pcie[r] |= 1u << m;
+        pcie_numa[r] = q;
+    }
+    for (uint32_t q = 0; q < (uint32_t)DEV_MINORS; q++) {
+        const uint32_t qm = numa[q];
+        if (!qm) break;
+        if ((uint32_t)__popc(qm) < N) continue;
+        if (level <= 3)
+            for (uint32_t r = 0; r < (uint32_t)DEV_MINORS; r++) {
+                const uint32_t rm = pcie[r];
+                if (!rm) break;
+                if (pcie_numa[r] == q && (uint32_t)__popc(rm) >= N && (uint32_t)__popc(rm & g.sat) >= N) return true;
+            }
+        if (level <= 2 && (uint32_t)__popc(qm & g.sat) >= N) return true;
+    }
+    return false;
+}
+
 // defaultAllocateDevices (device_allocator.go:355-437): minors by (scoreDevice desc, minor asc), the first
 // numberOfGPUs whose free resources are not all zero and cover the request. want_mask = false: only whether
 // enough minors fit (the Filter).
@@ -308,11 +346,36 @@ __device__ __forceinline__ GpuAlloc dev_default(const KCfg& c, const DevRec* __r
     return {0u, mask};
 }
 
+// GPUAllocator.Allocate's outcome (the Filter: no minors chosen) from the table's minor sets.
+__device__ __forceinline__ uint32_t gpu_allocate_code(const ExtDev& e, int32_t D, uint64_t topo, uint32_t part,
+                                                      const PodX& x, const GpuMinors& g) {
+    const bool shared = (x.dflags & KG_GPU_POD_SHARED) != 0;
+    const uint32_t sfield = (x.dflags >> KG_GPU_POD_SCOPE_SHIFT) & 7u;
+    const bool required = sfield != 0u;
+    const int32_t level = sfield > 4u ? 0 : (int32_t)sfield;
+    const uint32_t tbl = part & 0xFFu;
+    const bool honor = (x.dflags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR);
+    if (!shared && (tbl != 0u || honor)) {
+        const uint32_t code = gpu_partition(e, tbl, x, g, false).code;
+        if (code == 0u || honor) return code;
+    }
+    if (part & KG_GPU_TREE) {
+        if (!(shared && x.dcount > 1u))
+            return gpu_scope_fits(D, topo, x.dcount, g, level) ? 0u
+                                                                : (required ? KG_DEV_CODE_TOPO_SCOPED : KG_DEV_CODE_GPU_DEVICES);
+        if (required) return KG_DEV_CODE_MULTI_SHARED;
+    } else if (required) {
+        return KG_DEV_CODE_NO_TREE;
+    }
+    return (uint32_t)__popc(g.fit) >= x.dcount ? 0u : KG_DEV_CODE_INSUFFICIENT;
+}
+
 // GPUAllocator.Allocate for a pod with a GPU request on a node with D > 0 minors. topo / part: the node's
 // ZoneRec.dev_topo / dev_part; outside: minors used on the node outside the table (0 for the node's own).
 __device__ __forceinline__ GpuAlloc gpu_allocate(const KCfg& c, const ExtDev& e, const DevRec* __restrict__ d, int32_t D,
                                                  uint64_t topo, uint32_t part, const PodX& x, uint32_t outside,
                                                  bool want_mask) {
+    if (!want_mask) return {gpu_allocate_code(e, D, topo, part, x, gpu_minors(d, D, x, outside)), 0u};
     const bool shared = (x.dflags & KG_GPU_POD_SHARED) != 0;
     const uint32_t sfield = (x.dflags >> KG_GPU_POD_SCOPE_SHIFT) & 7u;
     const bool required = sfield != 0u;

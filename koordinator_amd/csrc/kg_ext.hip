@@ -8,7 +8,12 @@
 //                 a chunk of node records: feasibility + raw DeviceShare score, nominated reservation
 //                 score and the node order -> per-pod max / min by atomics;
 //   k_ext_select  lane = pod, wave walks a chunk of records: weighted total with the normalised terms,
-//                 running top-K per lane -> per-(chunk, pod) partials (merged by k_merge).
+//                 running top-K per lane -> per-(chunk, pod) partials (merged by k_merge), or at K = 1 on
+//                 fast-base batches an atomicMax into the pod's key.
+// Fast-base batches (every base plugin on the fast block, GPU pods classed) run pass 1 on the general records
+// only (F_BIG, storage class 1, the pod's views): on the fast-base records k_ext_select takes the DeviceShare
+// maximum to be the class's best fitting score (k_dev_sum's cls_max), records the real one, and k_ext_fix_rows
+// re-runs the rows whose guess was wrong, so no pair is evaluated twice unless its pod's guess failed.
 // Between the passes the multi-GPU path all-reduces the per-pod maxima over RCCL.
 // k_ext_replay   one pod per launch (lane = node record): applies the previous pod's Reserve in place
 //                (NodeInfo, LoadAware, NUMA zone, GPU minors, quota used), gates the next pod on its
@@ -44,51 +49,87 @@ constexpr uint32_t DSUM_CHUNK = 8;  // GPU request classes per thread of k_dev_s
 
 // DevSum of every record for the pod batch's GPU request classes: thread = (record, chunk of DSUM_CHUNK classes,
 // blockIdx.y); each thread sums the record's minors and, per class of its chunk, runs the GPU allocator and scores
-// one instance; chunk 0 also stores the sums.
+// one instance; chunk 0 also stores the sums. cls_max[class] = the best score over the fast-base records (below n0,
+// not F_BIG, with GPUs) the class fits on: the one-pass select's guess of the DeviceShare maximum.
 __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
-                                                 const DevRec* __restrict__ devs, uint32_t n_nodes,
+                                                 const DevRec* __restrict__ devs, uint32_t n_nodes, uint32_t n0,
                                                  const DevClass* __restrict__ cls, uint32_t n_cls, KCfg cfg, ExtDev e,
-                                                 DevSum* __restrict__ out) {
-    const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
-    if (rec >= n_nodes) return;
+                                                 DevSum* __restrict__ out, uint32_t* __restrict__ cls_max) {
+    const uint32_t rec0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = rec0 < n_nodes;
+    const uint32_t rec = live ? rec0 : n_nodes - 1;  // dead lanes compute a copy for the wave reductions
     const DevRec& d = devs[rec];
     const int32_t D = (int32_t)nodes[rec].v[N_DEV_MINORS];
-    const ZoneRec& zr = zones[rec];
+    const bool fbrec = live && rec < n0 && !((uint32_t)nodes[rec].v[N_FLAGS] & F_BIG) && D > 0;
+    const uint64_t topo = zones[rec].dev_topo;
+    const uint32_t part = zones[rec].dev_part;
+    // the record's minors once, in registers (16-B loads; lanes are 384 B apart, so every load instruction
+    // touches 64 lines: the per-class allocator reads them from here instead): free per (resource, minor), the
+    // class-independent minor sets, the sums of the Score
+    int64_t fr[DEV_R][DEV_MINORS];
+    uint32_t used = 0u, total = 0u, nonzero = 0u;
     DevSum o;
+#pragma unroll
     for (int r = 0; r < DEV_R; r++) {
         int64_t t = 0, f = 0;
-        for (int m = 0; m < DEV_MINORS; m++) {
-            t += d.total[r][m];
-            f += d.free_[r][m];
+#pragma unroll
+        for (int m = 0; m < DEV_MINORS; m += 2) {
+            const longlong2 tv = *reinterpret_cast<const longlong2*>(&d.total[r][m]);
+            const longlong2 fv = *reinterpret_cast<const longlong2*>(&d.free_[r][m]);
+            fr[r][m] = fv.x;
+            fr[r][m + 1] = fv.y;
+            t += tv.x + tv.y;
+            f += fv.x + fv.y;
+            const uint32_t b0 = m < D ? 1u << m : 0u, b1 = m + 1 < D ? 2u << m : 0u;
+            used |= (fv.x != tv.x ? b0 : 0u) | (fv.y != tv.y ? b1 : 0u);
+            total |= (tv.x != 0 ? b0 : 0u) | (tv.y != 0 ? b1 : 0u);
+            nonzero |= (fv.x != 0 ? b0 : 0u) | (fv.y != 0 ? b1 : 0u);
         }
         o.T[r] = t;
         o.F[r] = f;
         o.rcp[r] = t != 0 ? 1.0 / (double)t : 0.0;
     }
     DevSum& w = out[rec];
-    const uint32_t k0 = blockIdx.y * DSUM_CHUNK, k1 = min(k0 + DSUM_CHUNK, (uint32_t)DEV_CLASSES);
-    if (blockIdx.y == 0) {
+    const uint32_t k0 = blockIdx.y * DSUM_CHUNK;
+    if (blockIdx.y == 0 && live) {
         for (int r = 0; r < DEV_R; r++) {
             w.T[r] = o.T[r];
             w.F[r] = o.F[r];
             w.rcp[r] = o.rcp[r];
         }
     }
-    for (uint32_t k = k0; k < k1; k++) {
-        uint8_t code = 0, score = 0;
-        if (k < n_cls) {
-            PodX x{};
-            x.dkeys = cls[k].dkeys;
-            x.dcount = cls[k].dcount;
-            x.dflags = cls[k].dflags;
-            x.dbw = cls[k].dbw;
-            for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
-            // D <= 0 never reads the code (the pair is decided first)
-            code = (uint8_t)(D > 0 ? gpu_allocate(cfg, e, &d, D, zr.dev_topo, zr.dev_part, x, 0u, false).code : 0u);
-            score = (uint8_t)dev_sum_score(cfg, &o, x);
+    uint64_t codes = 0, scores = 0;  // DSUM_CHUNK = 8 bytes each: one store per chunk
+    static_assert(DSUM_CHUNK == 8 && offsetof(DevSum, code) % 8 == 0 && offsetof(DevSum, score) % 8 == 0, "packed stores");
+#pragma unroll 1
+    for (uint32_t i = 0; i < DSUM_CHUNK; i++) {
+        const uint32_t k = k0 + i;
+        if (k >= n_cls) break;
+        PodX x{};
+        x.dkeys = cls[k].dkeys;
+        x.dcount = cls[k].dcount;
+        x.dflags = cls[k].dflags;
+        x.dbw = cls[k].dbw;
+        for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
+        uint32_t le = 0u;
+#pragma unroll
+        for (int m = 0; m < DEV_MINORS; m++) {
+            bool ok = m < D;
+#pragma unroll
+            for (int r = 0; r < DEV_R; r++) ok &= !(((x.dkeys >> r) & 1u) && x.dreq[r] > fr[r][m]);
+            le |= ok ? 1u << m : 0u;
         }
-        w.code[k] = code;
-        w.score[k] = score;
+        const GpuMinors g{used, total, total & le, nonzero & le};
+        // D <= 0 never reads the code (the pair is decided first)
+        const uint32_t code = D > 0 ? gpu_allocate_code(e, D, topo, part, x, g) : 0u;
+        const uint32_t score = (uint32_t)dev_sum_score(cfg, &o, x);
+        codes |= (uint64_t)(code & 0xFFu) << (8 * i);
+        scores |= (uint64_t)(score & 0xFFu) << (8 * i);
+        const int32_t best = wmax_i32((fbrec && code == 0u) ? (int32_t)score : 0);
+        if (best > 0 && (threadIdx.x & 63u) == 0) atomicMax(cls_max + k, (uint32_t)best);
+    }
+    if (live) {
+        *reinterpret_cast<uint64_t*>(&w.code[k0]) = codes;
+        *reinterpret_cast<uint64_t*>(&w.score[k0]) = scores;
     }
 }
 
@@ -218,15 +259,13 @@ __global__ __launch_bounds__(256) void k_ext_verify_fin(uint32_t n_pods, uint32_
     }
 }
 
-// Pass 1: per-pod NormalizeScore inputs over the feasible nodes of records [lo, hi) of chunk blockIdx.y.
-// FB: base-plugin feasibility from the fast block where k_ext_select<FB> takes it (same conditions).
-// PART (FB launches split the records so that the fast kernel stays small): 1 = the fast-base records
-// only (the others are k_ext_stats_sp's), 0 = all records.
-template <bool EXACT, bool TOPO, bool FB, int PART = 0>
+// Pass 1: per-pod NormalizeScore inputs over the feasible nodes of records [lo, hi) of chunk blockIdx.y
+// (fast-base batches: k_ext_stats_sp over the general records only; the fast-base records' DeviceShare
+// maximum comes out of k_ext_select itself).
+template <bool EXACT, bool TOPO>
 __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                    ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
-                                                   uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
-                                                   uint32_t index_base,
+                                                   uint32_t n_list, uint32_t n_nodes, uint32_t chunk, uint32_t index_base,
                                                    KCfg cfg, const uint32_t* __restrict__ qst, uint32_t* __restrict__ dev_max,
                                                    uint32_t* __restrict__ rsv_max, uint64_t* __restrict__ pref) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -236,50 +275,17 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
     const PodX px = load_podx(pods, j);
     const uint32_t q = live ? qst[j] : 1u;
     const uint32_t lo = blockIdx.y * chunk, hi = min(n_nodes, lo + chunk);
+    const uint32_t dcls = pods.dev_cls ? pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
     uint32_t dmax = 0, rmax = 0;
     uint64_t pk = PREF_NONE;
-    PodF pff{};
-    KCfg cv = cfg;
-    if constexpr (FB) {
-        pff = to_podf(p, cfg);
-        cv = cfg_in_vgprs(cfg);
-    }
-    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
-    const uint32_t dcls = pods.dev_cls ? pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
     for (uint32_t rec = lo; rec < hi; rec++) {
-        const int64_t* __restrict__ n = nodes[rec].v;
-        if constexpr (FB) {
-            const uint32_t fl = (uint32_t)n[N_FLAGS];
-            const bool view = (cfg.plugins & KG_PLUGIN_RSV) && px.cls >= 0 && px.cls < RSV_MAX_CLASSES &&
-                              (((uint64_t)n[N_RSV_CLASSES] >> px.cls) & 1ull);
-            const bool fbrec = rec < n0 && !(fl & F_BIG) && !view;
-            if (fbrec) {
-                // no view: Reservation score and order are 0, only the DeviceShare maximum can move
-                uint32_t pv = 0;
-                if ((cfg.plugins & KG_PLUGIN_DEV) && px.dcount != 0) {
-                    const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
-                    const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, 0u);
-                    int64_t raw = 0;
-                    uint32_t st = (bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
-                    if (!st) st |= dev_eval_cls(n, e.dsum + rec, px, dcls, raw);
-                    if (!st) dmax = max(dmax, (uint32_t)raw);
-                    pv = 0x80000000u | (st ? 0u : (0x40000000u | ((uint32_t)(bk >> 32) << 7) | (uint32_t)raw));
-                }
-                if (e.pairs && live) e.pairs[(size_t)rec * e.pairs_ld + t] = pv;
-                continue;
-            }
-            if (e.pairs && live) e.pairs[(size_t)rec * e.pairs_ld + t] = 0u;
-        }
-        if constexpr (PART != 1) {
-            const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q,
-                                          pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES);
-            if (r.status) continue;
-            dmax = max(dmax, (uint32_t)r.s_dev);
-            rmax = max(rmax, (uint32_t)r.s_rsv);
-            if (r.order != 0) {
-                const uint64_t k = pref_key(r.order, index_base + node_index(nodes[rec]));
-                pk = k < pk ? k : pk;
-            }
+        const PairX r = eval_pair_ext<EXACT, TOPO, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q, dcls);
+        if (r.status) continue;
+        dmax = max(dmax, (uint32_t)r.s_dev);
+        rmax = max(rmax, (uint32_t)r.s_rsv);
+        if (r.order != 0) {
+            const uint64_t k = pref_key(r.order, index_base + node_index(nodes[rec]));
+            pk = k < pk ? k : pk;
         }
     }
     if (!live) return;
@@ -401,14 +407,31 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
                                                     const uint32_t* __restrict__ qst, const uint32_t* __restrict__ dev_max,
                                                     const uint32_t* __restrict__ rsv_max, const uint64_t* __restrict__ pref,
                                                     uint64_t* __restrict__ partial, uint32_t* __restrict__ pstat) {
-    // lane j = row j of the output; the pod is list[j] (list == nullptr: the batch in order)
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = j < n_pods;
+    // lane = row j of the output; the pod is list[j] (list == nullptr: the batch in order). Re-run launch
+    // (e.rows): lane t takes row e.rows[t] of the *e.n_rows rows k_ext_fix_rows listed.
+    constexpr bool FUSED = FB && PART == 1 && K == 1;  // top-1 straight into partial[row] by atomicMax
+    const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t j = t0;
+    bool live = j < n_pods;
+    if constexpr (FB) {
+        if (e.rows) {
+            const uint32_t nr = *e.n_rows;
+            if (blockIdx.x * blockDim.x >= nr) return;  // whole workgroup idle (no barrier in this kernel)
+            live = t0 < nr;
+            j = live ? e.rows[t0] : 0u;
+        }
+    }
     const uint32_t jj = live ? (list ? list[j] : j) : 0;
     const PodV p = load_pod(pods, jj);
     const PodX px = load_podx(pods, jj);
     const uint32_t q = live ? qst[jj] : 1u;
-    const uint32_t dm = dev_max[jj], rm = rsv_max[jj];
+    const uint32_t rm = rsv_max[jj];
+    uint32_t dm = dev_max[jj];
+    const uint32_t dcls = pods.dev_cls ? pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
+    // one-pass mode: the fast-base maximum is guessed as the class bound, the real one is collected
+    const bool guess = FB && e.cls_max && (cfg.plugins & KG_PLUGIN_DEV) && px.dcount != 0 && dcls < (uint32_t)DEV_CLASSES;
+    if (guess) dm = max(dm, e.cls_max[dcls]);
+    uint32_t fbmax = 0;
     const uint64_t pf = pref[jj];
     uint64_t top[K];
 #pragma unroll
@@ -421,9 +444,7 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
         cv = cfg_in_vgprs(cfg);
     }
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
-    const uint32_t dcls = pods.dev_cls ? pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
     const uint32_t mag = norm_magic(dm);
-    const int64_t prow = (FB && e.pairs && live && j >= e.pairs_row0) ? (int64_t)(j - e.pairs_row0) : -1;
     // pairs that need the host path come from eval_pair_ext only: FB records never do (a batch with a
     // cpuset-binding pod is not fast_ok, nodes with a CPU bind policy are F_BIG)
     uint32_t unsup = 0;
@@ -436,16 +457,6 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
             const bool fbrec = rec < n0 && !(fl & F_BIG) && !view;
             if (PART == 1 && !fbrec) continue;
             if (fbrec) {
-                if (prow >= 0) {  // pass 1 evaluated this pair: only the normalised terms are added
-                    const uint32_t pv = e.pairs[(size_t)rec * e.pairs_ld + prow];
-                    if (pv & 0x80000000u) {
-                        const uint32_t g = index_base + (uint32_t)((uint64_t)n[N_FLAGS] >> 32);
-                        const int64_t tot = total_fb(cfg, (uint64_t)((pv >> 7) & 0x7FFFFFu) << 32, (int64_t)(pv & 127u),
-                                                     dm, mag, g, pf);
-                        topk_ins<K>(top, (pv & 0x40000000u) ? (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)) : 0ull);
-                        continue;
-                    }
-                }
                 const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
                 const uint32_t g = index_base + (uint32_t)((uint64_t)fr.flags >> 32);
                 const uint64_t bk = eval_fast_key<7u, 0>(cv, fr, zones + rec, pff, g);
@@ -453,14 +464,14 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
                 int64_t s_dev = 0;
                 if ((cfg.plugins & KG_PLUGIN_DEV) && !st)  // only the key's zero-ness matters once st != 0
                     st |= dev_eval_cls(n, e.dsum + rec, px, dcls, s_dev);
+                if (!st) fbmax = max(fbmax, (uint32_t)s_dev);
                 const int64_t tot = total_fb(cfg, bk, s_dev, dm, mag, g, pf);
                 topk_ins<K>(top, st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - g)));
                 continue;
             }
         }
         if constexpr (PART != 1) {
-            const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q,
-                                          pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES);
+            const PairX r = eval_pair_ext<EXACT, TOPO>(cfg, e, n, zones + rec, dev_of(e, rec), rec, p, px, q, dcls);
             unsup |= r.status & KG_ST_UNSUPPORTED;
             const uint32_t g = index_base + node_index(nodes[rec]);
             const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
@@ -468,15 +479,42 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
         }
     }
     if (live) {
-        uint64_t* dst = partial + ((size_t)blockIdx.y * n_pods + j) * K;
+        if constexpr (FUSED) {
+            if (top[0]) atomicMax((unsigned long long*)(partial + j), (unsigned long long)top[0]);
+        } else {
+            uint64_t* dst = partial + ((size_t)blockIdx.y * n_pods + j) * K;
 #pragma unroll
-        for (int t = 0; t < K; t++) dst[t] = top[t];
+            for (int t = 0; t < K; t++) dst[t] = top[t];
+        }
         if (unsup) atomicOr(pstat + jj, unsup);
+        if (guess && fbmax) atomicMax(e.fb_max + jj, fbmax);
     }
 }
 
+// One-pass fast-base select: per GPU pod of the x list, the final DeviceShare maximum (general records' from
+// pass 1, fast-base records' from k_ext_select) goes to dev_max for the general-record kernel; rows whose
+// guessed maximum was not the final one are listed for a re-run (their fused key reset first). A pod the
+// quota gate rejected or with a required reservation affinity has no feasible fast-base pair: any guess holds.
+__global__ __launch_bounds__(256) void k_ext_fix_rows(PodsDev pods, const uint32_t* __restrict__ list, uint32_t n_pods,
+                                                      ExtDev e, uint32_t plugins, const uint32_t* __restrict__ qst,
+                                                      uint32_t* __restrict__ dev_max, uint32_t* __restrict__ rows,
+                                                      uint32_t* __restrict__ n_rows, uint64_t* __restrict__ fused) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_pods || !(plugins & KG_PLUGIN_DEV)) return;
+    const uint32_t jj = list ? list[j] : j;
+    const PodX px = load_podx(pods, jj);
+    const uint32_t dcls = pods.dev_cls ? pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
+    if (px.dcount == 0 || dcls >= (uint32_t)DEV_CLASSES) return;
+    const uint32_t gen = dev_max[jj], fin = max(gen, e.fb_max[jj]);
+    dev_max[jj] = fin;
+    const bool req_aff = (plugins & KG_PLUGIN_RSV) && (load_pod(pods, jj).flags & KG_POD_RSV_REQUIRED);
+    if (qst[jj] != 0u || req_aff || fin == max(gen, e.cls_max[dcls])) return;
+    if (fused) fused[j] = 0ull;
+    rows[atomicAdd(n_rows, 1u)] = j;
+}
+
 // Pass 2, general records of a fast-base launch (the complement of k_ext_select<.., 1>): partials of
-// chunk blockIdx.y go after the fast kernel's (part_off).
+// chunk blockIdx.y go after the fast kernel's (part_off); top-1 is fused (partial = the keys by row).
 template <int K>
 __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                        ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
@@ -508,9 +546,13 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
         topk_ins<K>(top, r.status ? 0ull : key);
     });
     if (live) {
-        uint64_t* dst = partial + (((size_t)blockIdx.y + part_off) * n_pods + j) * K;
+        if constexpr (K == 1) {  // fused top-1 like k_ext_select<1, .., FB>
+            if (top[0]) atomicMax((unsigned long long*)(partial + j), (unsigned long long)top[0]);
+        } else {
+            uint64_t* dst = partial + (((size_t)blockIdx.y + part_off) * n_pods + j) * K;
 #pragma unroll
-        for (int t = 0; t < K; t++) dst[t] = top[t];
+            for (int t = 0; t < K; t++) dst[t] = top[t];
+        }
         if (unsup) atomicOr(pstat + jj, unsup);
     }
 }
@@ -817,23 +859,35 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
                             uint32_t special_est, hipStream_t s) {
     if (n_list == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_list + 255) / 256, (n_nodes + chunk - 1) / chunk);
-    uint32_t chunk2, y2;
-    ext_part2_grid(special_est, grid.x, &chunk2, &y2);
-#define KG_EXT_ST(EX, TP, F, ...)                                                                                  \
-    k_ext_stats<EX, TP, F, ##__VA_ARGS__><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, n0, chunk, index_base, cfg, \
-                                                qst, dev_max, rsv_max, pref)
-    if (fb) {
-        KG_EXT_ST(false, false, true, 1);
+    if (fb) {  // the general records only (the fast-base records' maximum: k_ext_select)
+        uint32_t chunk2, y2;
+        ext_part2_grid(special_est, grid.x, &chunk2, &y2);
         k_ext_stats_sp<<<dim3(grid.x, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n0, chunk2, index_base, cfg,
                                                         qst, dev_max, rsv_max, pref, special);
-    } else if (exact) {
-        if (topo) KG_EXT_ST(true, true, false);
-        else KG_EXT_ST(true, false, false);
+        return hipGetLastError();
+    }
+#define KG_EXT_ST(EX, TP)                                                                                              \
+    k_ext_stats<EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n_nodes, chunk, index_base, cfg, qst, \
+                                             dev_max, rsv_max, pref)
+    if (exact) {
+        if (topo) KG_EXT_ST(true, true);
+        else KG_EXT_ST(true, false);
     } else {
-        if (topo) KG_EXT_ST(false, true, false);
-        else KG_EXT_ST(false, false, false);
+        if (topo) KG_EXT_ST(false, true);
+        else KG_EXT_ST(false, false);
     }
 #undef KG_EXT_ST
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_max_fold(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = max(dst[i], src[i]);
+}
+
+hipError_t launch_max_fold(uint32_t* dst, const uint32_t* src, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_max_fold<<<(n + 255) / 256, 256, 0, s>>>(dst, src, n);
     return hipGetLastError();
 }
 
@@ -854,13 +908,15 @@ hipError_t launch_rdev_codes(const NodeRec* nodes, const ZoneRec* zones, const D
     return hipGetLastError();
 }
 
-hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
-                          const KCfg& cfg, const ExtDev& e,
-                          DevSum* out, hipStream_t s) {
-    if (n_nodes == 0) return hipSuccess;
-    // every chunk of DEV_CLASSES is written (classes past n_cls get code / score 0)
-    const uint32_t chunks = ((uint32_t)DEV_CLASSES + DSUM_CHUNK - 1) / DSUM_CHUNK;
-    k_dev_sum<<<dim3((n_nodes + 255) / 256, chunks), 256, 0, s>>>(nodes, zones, devs, n_nodes, cls, n_cls, cfg, e, out);
+hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, uint32_t n0,
+                          const DevClass* cls, uint32_t n_cls, const KCfg& cfg, const ExtDev& e, DevSum* out,
+                          uint32_t* cls_max, hipStream_t s) {
+    hipError_t err = hipMemsetAsync(cls_max, 0, sizeof(uint32_t) * DEV_CLASSES, s);
+    if (err != hipSuccess || n_nodes == 0) return err;
+    // the chunks of the batch's classes (a class's code / score is read only by pods of that class)
+    const uint32_t chunks = std::max<uint32_t>(1u, (std::min<uint32_t>(n_cls, DEV_CLASSES) + DSUM_CHUNK - 1) / DSUM_CHUNK);
+    k_dev_sum<<<dim3((n_nodes + 255) / 256, chunks), 256, 0, s>>>(nodes, zones, devs, n_nodes, n0, cls, n_cls, cfg, e, out,
+                                                                  cls_max);
     return hipGetLastError();
 }
 
@@ -900,21 +956,15 @@ hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, co
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                              const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                              uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
-                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
-                             const uint32_t* special, uint32_t special_est, hipStream_t s) {
+                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat, hipStream_t s) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_pods + 255) / 256, (n_nodes + chunk - 1) / chunk);
-    const uint32_t y1 = grid.y;
-    uint32_t chunk2, y2;
-    ext_part2_grid(special_est, grid.x, &chunk2, &y2);
 #define KG_EXT_SEL(KK, EX, TP, F, ...)                                                                       \
     k_ext_select<KK, EX, TP, F, ##__VA_ARGS__><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n_nodes, n0, chunk, index_base, \
                                                      cfg, qst, dev_max, rsv_max, pref, partial, pstat)
 #define KG_EXT_SEL_K(KK)                              \
     if (fb) {                                         \
         KG_EXT_SEL(KK, false, false, true, 1);        \
-        k_ext_select_sp<KK><<<dim3(grid.x, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, \
-            index_base, cfg, qst, dev_max, rsv_max, pref, partial, pstat, special, y1); \
     } else if (exact) {                               \
         if (topo) KG_EXT_SEL(KK, true, true, false);  \
         else KG_EXT_SEL(KK, true, false, false);      \
@@ -929,6 +979,42 @@ hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const E
     }
 #undef KG_EXT_SEL_K
 #undef KG_EXT_SEL
+    return hipGetLastError();
+}
+
+hipError_t launch_ext_fix(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                          const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
+                          uint32_t index_base, const KCfg& cfg, const uint32_t* qst, uint32_t* dev_max,
+                          const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
+                          uint32_t* rows, uint32_t* n_rows, hipStream_t s) {
+    if (n_pods == 0 || n_nodes == 0) return hipSuccess;
+    hipError_t err = hipMemsetAsync(n_rows, 0, sizeof(uint32_t), s);
+    if (err != hipSuccess) return err;
+    k_ext_fix_rows<<<(n_pods + 255) / 256, 256, 0, s>>>(pods, list, n_pods, e, cfg.plugins, qst, dev_max, rows, n_rows,
+                                                        k == 1 ? partial : nullptr);
+    ExtDev f = e;
+    f.cls_max = nullptr;
+    f.rows = rows;
+    f.n_rows = n_rows;
+    return launch_ext_select(nodes, zones, f, pods, list, n_pods, n_nodes, n0, chunk, k, index_base, cfg, false, false, true,
+                             qst, dev_max, rsv_max, pref, partial, pstat, s);
+}
+
+hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                                const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
+                                uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
+                                const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
+                                const uint32_t* special, uint32_t special_est, hipStream_t s) {
+    if (n_pods == 0 || n_nodes == 0) return hipSuccess;
+    const uint32_t gx = (n_pods + 255) / 256, y1 = (n_nodes + chunk - 1) / chunk;
+    uint32_t chunk2, y2;
+    ext_part2_grid(special_est, gx, &chunk2, &y2);
+    if (k == 1)
+        k_ext_select_sp<1><<<dim3(gx, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, index_base, cfg, qst,
+                                                        dev_max, rsv_max, pref, partial, pstat, special, y1);
+    else
+        k_ext_select_sp<KG_TOPK_MAX><<<dim3(gx, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, index_base,
+                                                                  cfg, qst, dev_max, rsv_max, pref, partial, pstat, special, y1);
     return hipGetLastError();
 }
 

@@ -103,8 +103,23 @@ hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, co
 hipError_t launch_ext_select(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                              const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                              uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst, const uint32_t* dev_max,
-                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat, const uint32_t* special,
-                             uint32_t special_est, hipStream_t s);
+                             const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat, hipStream_t s);
+// dst[i] = max(dst[i], src[i])
+hipError_t launch_max_fold(uint32_t* dst, const uint32_t* src, uint32_t n, hipStream_t s);
+// One-pass fast-base select, second half: final DeviceShare maxima into dev_max, re-run of the rows whose guess
+// was wrong (fb launches; k = 1: partial = the fused keys by row).
+hipError_t launch_ext_fix(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                          const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
+                          uint32_t index_base, const KCfg& cfg, const uint32_t* qst, uint32_t* dev_max,
+                          const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
+                          uint32_t* rows, uint32_t* n_rows, hipStream_t s);
+// General records of a fast-base select (F_BIG, class 1, the lane's views); k > 1: partial chunks after the
+// fast-base kernel's (n_nodes / chunk of them).
+hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                                const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
+                                uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
+                                const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
+                                const uint32_t* special, uint32_t special_est, hipStream_t s);
 // out[map[t]] = rows t of src (k keys each; row map[t] with src_by_map, src may then be out); rows whose pod
 // has a nonzero qst[pod] get zero keys and pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the
 // host path)
@@ -149,9 +164,9 @@ hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t 
 hipError_t launch_rdev_codes(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, const DevRec* rdev,
                              const uint32_t* rdev_rec, uint32_t n_rdev, const DevClass* cls, uint32_t n_cls,
                              const KCfg& cfg, const ExtDev& e, uint8_t* out, hipStream_t s);
-hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, const DevClass* cls, uint32_t n_cls,
-                          const KCfg& cfg, const ExtDev& e,
-                          DevSum* out, hipStream_t s);
+hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, uint32_t n0,
+                          const DevClass* cls, uint32_t n_cls, const KCfg& cfg, const ExtDev& e, DevSum* out,
+                          uint32_t* cls_max, hipStream_t s);
 hipError_t launch_scatter_rows(const void* stage, const uint32_t* pos, uint32_t n, bool dev, NodeRec* nodes,
                                ZoneRec* zones, DevRec* devs, hipStream_t s);
 hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, uint32_t n_pods,

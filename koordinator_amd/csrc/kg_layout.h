@@ -409,11 +409,14 @@ struct ExtDev {
     const uint32_t* cls_begin;     // [RSV_MAX_CLASSES + 1] view range per class
     const DevRec* rdev;            // GPU restore tables of views / reservations (kg_rsv_dev)
     const DevSum* dsum;            // [record] of the current pod batch (fast-base select / stats only)
-    // Pair results of pass 1 kept for pass 2 (fast-base records of the GPU pods): [record][pairs_ld], lane
-    // row t of the stats list; bit 31 stored, bit 30 feasible, bits 7..29 base total, bits 0..6 DeviceShare
-    // raw score. pairs_row0: select-list row of stats row 0. nullptr = pass 2 evaluates every pair.
-    uint32_t* pairs;
-    uint32_t pairs_ld, pairs_row0;
+    // Fast-base select of the GPU pods in one pass (k_ext_select<FB>): the DeviceShare maximum over the fast-base
+    // records is taken as cls_max[class] (the class's best score over every fast-base record whose allocator
+    // succeeds: an upper bound, k_dev_sum), the real one goes to fb_max[pod]; k_ext_fix_rows lists the rows
+    // whose guess was wrong and the same kernel re-runs them (rows[0, *n_rows)) with the final maximum.
+    const uint32_t* cls_max;  // [DEV_CLASSES]; nullptr = dev_max is final
+    uint32_t* fb_max;         // [pod]
+    const uint32_t* rows;     // nullptr = every row
+    const uint32_t* n_rows;
     // GPU partition tables (kg_gpu_partition, grouped by table / GPU count / AllocationScore) and per (table,
     // GPU count) the entry range: part_rng[table * 9 + n] = begin | end << 16
     const kg_gpu_partition* parts;

@@ -175,10 +175,9 @@ struct kg_pods {
     size_t devsum_cap = 0;
     uint8_t* d_rcode = nullptr;    // [kg_rsv_dev table][DEV_CLASSES]: GPU allocator outcome on the restore tables
     size_t rcode_cap = 0;
-    // pass-1 pair results kept for pass 2 (ExtDev.pairs)
-    uint32_t* d_pairs = nullptr;
-    size_t pairs_cap = 0;  // entries
-    bool pairs_on = false;
+    // one-pass fast-base select of the GPU pods (ExtDev.cls_max / fb_max / rows): [cap] fast-base maxima, [cap] rows
+    // to re-run, [DEV_CLASSES] per-class bounds, row count
+    uint32_t* d_spec = nullptr;
     // replay / shard scratch
     uint64_t* d_winners = nullptr;
     uint32_t* d_step = nullptr;
@@ -1248,12 +1247,13 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_buckets, sizeof(uint64_t) * 3 * 128) == hipSuccess &&
               hipMalloc(&p->d_aout, sizeof(int32_t) * 2) == hipSuccess &&
               hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
+              hipMalloc(&p->d_spec, sizeof(uint32_t) * (2 * (size_t)capacity + DEV_CLASSES + 1)) == hipSuccess &&
               hipMalloc(&p->d_pstat, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_reason, sizeof(uint32_t) * (capacity + 1)) == hipSuccess;
     if (!ok) {
         for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_qst,
                         (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets,
-                        (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat, (void*)p->d_reason})
+                        (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_spec, (void*)p->d_pstat, (void*)p->d_reason})
             hipFree(b);
         hipHostFree(p->h_in);
         hipHostFree(p->h_keys);
@@ -1453,7 +1453,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
                     (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
                     (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
-                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_pairs, (void*)p->d_batch, (void*)p->d_rcode})
+                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_spec, (void*)p->d_batch, (void*)p->d_rcode})
         hipFree(b);
     hipHostFree(p->h_in);
     hipHostFree(p->h_keys);
@@ -1585,6 +1585,12 @@ static bool ext_fast_base(const kg_snap* s, const kg_pods* p) {
            (s->kcfg.plugins & 7u) == 7u && !p->dev_unclassed;
 }
 
+// Regions of kg_pods::d_spec (one-pass fast-base select of the GPU pods).
+static uint32_t* spec_fb_max(kg_pods* p) { return p->d_spec; }
+static uint32_t* spec_rows(kg_pods* p) { return p->d_spec + p->cap; }
+static uint32_t* spec_cls_max(kg_pods* p) { return p->d_spec + 2 * (size_t)p->cap; }
+static uint32_t* spec_n_rows(kg_pods* p) { return p->d_spec + 2 * (size_t)p->cap + DEV_CLASSES; }
+
 // config-5 matrix mode, pass 1: quota gate + per-pod NormalizeScore inputs of this shard
 // The batch's DevSum table over this snapshot's records (fast-base config-5 select with DeviceShare).
 static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
@@ -1599,8 +1605,8 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
         HIP_TRY(ctx, hipMalloc(&p->d_devsum, sizeof(DevSum) * std::max<uint32_t>(s->n, 1)));
         p->devsum_cap = s->n;
     }
-    HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(), p->d_devsum,
-                                ctx->stream));
+    HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(),
+                                p->d_devsum, spec_cls_max(p), ctx->stream));
     e.dsum = p->d_devsum;
     e.rcode = nullptr;
     if (s->n_rdev && s->d_rdev && p->n_dclass) {  // the GPU restore tables of the reservation views, per class
@@ -1620,45 +1626,10 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     return KG_OK;
 }
 
-// Pass 1 keeps each fast-base pair of the GPU pods (base total, feasibility, DeviceShare raw score) for
-// pass 2 when the weighted base total fits 23 bits and the table fits the budget (KG_PAIRS_GB, default 16).
-static kg_status ext_pairs(kg_snap* s, kg_pods* p, ExtDev& e) {
-    kg_ctx* ctx = s->ctx;
-    e.pairs = nullptr;
-    e.pairs_ld = e.pairs_row0 = 0;
-    p->pairs_on = false;
-    const uint32_t ng = p->n_stat - p->n_stat_cls;
-    const KCfg& c = s->kcfg;
-    if (!e.dsum || ng == 0 || 100ll * ((int64_t)c.w_nrf + c.w_la + c.w_numa) >= (1ll << 23)) return KG_OK;
-    const char* env = std::getenv("KG_PAIRS_GB");
-    const double budget = (env ? std::atof(env) : 16.0) * 1e9;
-    const uint32_t ld = (ng + 63u) & ~63u;
-    const size_t need = (size_t)ld * s->n;
-    if ((double)need * sizeof(uint32_t) > budget) return KG_OK;
-    if (need > p->pairs_cap) {
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        HIP_TRY(ctx, hipFree(p->d_pairs));
-        p->d_pairs = nullptr;
-        p->pairs_cap = 0;
-        if (hipMalloc(&p->d_pairs, sizeof(uint32_t) * need) != hipSuccess) {
-            (void)hipGetLastError();
-            return KG_OK;  // no room: pass 2 evaluates every pair
-        }
-        p->pairs_cap = need;
-    }
-    e.pairs = p->d_pairs;
-    e.pairs_ld = ld;
-    e.pairs_row0 = p->n_x - ng;  // GPU pods close both lists in the same order (kg_pods_upload)
-    p->pairs_on = true;
-    return KG_OK;
-}
-
 static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     kg_ctx* ctx = s->ctx;
     ExtDev e = s->ext_dev();
     kg_status dst = ext_dev_sum(s, p, e);
-    if (dst != KG_OK) return dst;
-    dst = ext_pairs(s, p, e);
     if (dst != KG_OK) return dst;
     if (ext_fast_base(s, p)) {  // records for the PART 2 kernels (pass 1 and pass 2 of this batch)
         if (!s->d_special) HIP_TRY(ctx, hipMalloc(&s->d_special, sizeof(uint32_t) * ((size_t)s->n + 1)));
@@ -1668,6 +1639,7 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
     HIP_TRY(ctx, hipMemsetAsync(p->d_dev_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_pref, 0xFF, sizeof(uint64_t) * p->n, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(spec_fb_max(p), 0, sizeof(uint32_t) * p->n, ctx->stream));
     if (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) {
         // pods without a GPU request only get statistics from the nodes holding a view of their
         // reservation class (elsewhere s_dev = s_rsv = order = 0): one lane per pod over those views
@@ -1749,20 +1721,26 @@ static LaunchSelect make_select(const kg_snap* s, const PodsDev& pods, const uin
 // (eval_pair_ext with dcount == 0, no view, no required affinity), so its keys are exactly the base
 // select's; those pods run the fast select through their lane list (d_pmap) straight into d_out, the
 // others k_ext_select by list. ElasticQuota rejections are applied by the scatters.
-static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out) {
+// Fast-base batches: k_ext_select<FB> over the fast-base records with the guessed DeviceShare maxima (plus their
+// real ones), [all-reduce of those over the shards,] k_ext_fix_rows + re-run of the wrong guesses, then the general
+// records with the final maxima; top-1 is fused (atomicMax into the row's key, no partials / merge).
+static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out, bool global = false) {
     kg_ctx* ctx = s->ctx;
     const bool split = !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok &&
                        !need_topo(s, p);
     const uint32_t n_x = split ? p->n_x : p->n;
     const uint32_t* xl = split ? p->d_xlist : nullptr;
     const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(n_x, 1), 8192);
+    const bool fb = n_x && ext_fast_base(s, p);
+    const bool fused = fb && kk == 1;
     // a fast-base launch writes the fast-record kernel's chunks, then the special-record kernel's
     uint32_t xparts = n_x ? (s->n + chunk - 1) / chunk : 0;
-    if (n_x && ext_fast_base(s, p)) {
+    if (fb) {
         uint32_t c2, y2;
         ext_part2_grid(s->special_est(), (n_x + 255) / 256, &c2, &y2);
         xparts += y2;
     }
+    if (fused) xparts = 0;
     const uint32_t n_plain = split ? p->n_plain : 0;
     uint32_t fparts = 0;
     LaunchSelect a = make_select(s, p->dev, p->d_pmap, n_plain, n_plain, p->n, kk, true, d_out, nullptr, p->d_pstat, &fparts);
@@ -1770,30 +1748,50 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     kg_status st = ensure_partial(p, std::max<size_t>(xneed + (size_t)fparts * p->n * kk, 1));
     if (st != KG_OK) return st;
     a.partial = p->d_partial + xneed;
-    hipEvent_t e0, e1;
-    st = record_begin(ctx, &e0, &e1);
-    if (st != KG_OK) return st;
+    uint64_t* xkeys = split ? p->d_tkeys : d_out;            // the x rows' merged keys
+    uint64_t* xpart = fused ? xkeys : p->d_partial;          // where the x kernels write
+    if (fused) HIP_TRY(ctx, hipMemsetAsync(xkeys, 0, sizeof(uint64_t) * n_x, ctx->stream));
     ExtDev xe = s->ext_dev();
     xe.dsum = (s->d_dev && ext_fast_base(s, p)) ? p->d_devsum : nullptr;  // ext_stats_local built it for this batch
     xe.rcode = (xe.dsum && s->n_rdev && p->n_dclass) ? p->d_rcode : nullptr;   // and the restore tables' codes
-    if (p->pairs_on && xe.dsum) {  // and the pass-1 pair table
-        xe.pairs = p->d_pairs;
-        xe.pairs_ld = (p->n_stat - p->n_stat_cls + 63u) & ~63u;
-        xe.pairs_row0 = p->n_x - (p->n_stat - p->n_stat_cls);
+    const bool guess = fb && xe.dsum && (s->cfg.plugins & KG_PLUGIN_DEV) && p->n_stat > p->n_stat_cls;
+    if (guess) {
+        xe.cls_max = spec_cls_max(p);
+        xe.fb_max = spec_fb_max(p);
+    }
+    if (global && !guess) {  // the shards that guessed hold fast-base maxima this one's kernels must see first
+        NCCL_TRY(ctx, ncclAllReduce(spec_fb_max(p), spec_fb_max(p), p->n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
+        HIP_TRY(ctx, launch_max_fold(p->d_dev_max, spec_fb_max(p), p->n, ctx->stream));
     }
     if (n_plain) HIP_TRY(ctx, launch_select(a, ctx->stream));  // zeroes d_out first at k = 1: before the x scatter
     if (n_x)
         HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
-                                       s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
-                                       p->d_pref, p->d_partial, p->d_pstat, s->d_special, s->special_est(), ctx->stream));
-    st = record_end(ctx, e0, e1);
-    if (st != KG_OK) return st;
+                                       s->kcfg, force_exact(), need_topo(s, p), fb, p->d_qst, p->d_dev_max, p->d_rsv_max,
+                                       p->d_pref, xpart, p->d_pstat, ctx->stream));
+    if (guess) {
+        if (global) NCCL_TRY(ctx, ncclAllReduce(xe.fb_max, xe.fb_max, p->n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
+        HIP_TRY(ctx, launch_ext_fix(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base, s->kcfg,
+                                    p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, xpart, p->d_pstat, spec_rows(p),
+                                    spec_n_rows(p), ctx->stream));
+        if (std::getenv("KG_TRACE_FIX")) {  // diagnostics: how many rows the guess missed
+            uint32_t nr = 0;
+            HIP_TRY(ctx, hipMemcpyAsync(&nr, spec_n_rows(p), sizeof(nr), hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            std::fprintf(stderr, "kg: one-pass select re-ran %u of %u rows\n", nr, n_x);
+        }
+    }
+    if (fb) {
+        xe.cls_max = nullptr;
+        HIP_TRY(ctx, launch_ext_select_sp(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base, s->kcfg,
+                                          p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, xpart, p->d_pstat, s->d_special,
+                                          s->special_est(), ctx->stream));
+    }
     if (!split) {
-        HIP_TRY(ctx, launch_merge(p->d_partial, xparts, p->n, kk, d_out, ctx->stream));
+        if (!fused) HIP_TRY(ctx, launch_merge(p->d_partial, xparts, p->n, kk, d_out, ctx->stream));
         return KG_OK;
     }
     if (n_x) {
-        HIP_TRY(ctx, launch_merge(p->d_partial, xparts, n_x, kk, p->d_tkeys, ctx->stream));
+        if (!fused) HIP_TRY(ctx, launch_merge(p->d_partial, xparts, n_x, kk, p->d_tkeys, ctx->stream));
         HIP_TRY(ctx, launch_scatter_keys(p->d_tkeys, p->d_xlist, n_x, kk, false, nullptr, d_out, nullptr, ctx->stream));
     }
     if (n_plain)  // the plain keys are in place: apply the ElasticQuota rejections
@@ -1817,9 +1815,15 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
             HIP_TRY(ctx, hipMemsetAsync(p->d_pstat, 0, sizeof(uint32_t) * p->n, ctx->stream));
             return KG_OK;
         }
+        // kernel-time bracket (kg_profile_read): the whole config-5 step, DevSum / pass 1 included
+        hipEvent_t e0, e1;
+        st0 = record_begin(ctx, &e0, &e1);
+        if (st0 != KG_OK) return st0;
         st0 = ext_stats_local(s, p);
         if (st0 != KG_OK) return st0;
-        return ext_select_local(s, p, kk, d_out);
+        st0 = ext_select_local(s, p, kk, d_out);
+        if (st0 != KG_OK) return st0;
+        return record_end(ctx, e0, e1);
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     p->k_last = k;
@@ -2767,15 +2771,26 @@ kg_status kg_shard_select(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* out_keys
         p->k_last = k;
         p->kk_last = kk;
         if (n == 0) return KG_OK;
+        hipEvent_t e0, e1;  // bracket: the whole shard step (its all-reduces included)
+        st = record_begin(ctx, &e0, &e1);
+        if (st != KG_OK) return st;
         st = ext_stats_local(s, p);
         if (st != KG_OK) return st;
         NCCL_TRY(ctx, ncclAllReduce(p->d_dev_max, p->d_dev_max, n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
         NCCL_TRY(ctx, ncclAllReduce(p->d_rsv_max, p->d_rsv_max, n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
         NCCL_TRY(ctx, ncclAllReduce(p->d_pref, p->d_pref, n, ncclUint64, ncclMin, ctx->comm, ctx->stream));
-        if (s->n == 0)
+        // the one-pass select's per-class bounds (k_dev_sum; zero on a shard that built none)
+        if (!(s->d_dev && ext_fast_base(s, p)))
+            HIP_TRY(ctx, hipMemsetAsync(spec_cls_max(p), 0, sizeof(uint32_t) * DEV_CLASSES, ctx->stream));
+        NCCL_TRY(ctx, ncclAllReduce(spec_cls_max(p), spec_cls_max(p), DEV_CLASSES, ncclUint32, ncclMax, ctx->comm,
+                                    ctx->stream));
+        if (s->n == 0) {
             HIP_TRY(ctx, hipMemsetAsync(local, 0, sizeof(uint64_t) * n * kk, ctx->stream));
-        else
-            st = ext_select_local(s, p, kk, local);
+            NCCL_TRY(ctx, ncclAllReduce(spec_fb_max(p), spec_fb_max(p), n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
+        } else
+            st = ext_select_local(s, p, kk, local, true);
+        if (st != KG_OK) return st;
+        st = record_end(ctx, e0, e1);
     } else {
         st = select_local(s, p, k, local);
     }

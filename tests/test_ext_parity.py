@@ -5,6 +5,8 @@ of NodeResourcesFit + LoadAware + NodeNUMAResource.
 Bar: bit-exact — filter status bits, int64 per-plugin raw scores, weighted totals after NormalizeScore,
 selected hosts (deterministic tie-break), replay placements, GPU minors and final device / quota state.
 """
+import re
+
 import numpy as np
 import pytest
 
@@ -107,6 +109,29 @@ def test_ext_select(ctx, k):
     want = oracle_lib.ext_select(kc, nodes, pods, k, 0, quotas, rsv)
     assert np.array_equal(got, want)
     assert (want[:, 0] == 0).any() and (want[:, 0] != 0).any()
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_ext_select_guess_rerun(ctx, capfd, monkeypatch, k):
+    """One-pass fast-base select (kg_ext.hip k_ext_select / k_ext_fix_rows): each GPU pod's DeviceShare maximum
+    over the fast-base records is first taken as its class's best fitting score. Here the nodes with the most
+    free GPU (the LeastAllocated maxima) have no CPU left, so the guesses miss and the rows are re-run with the
+    real maximum: keys still equal the oracle's."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(1500, 300, seed_config=23, rsv_frac=0.1)
+    free = nodes["dev_free"][:, abi.KG_DEV_CORE, :].sum(1)
+    top = np.argsort(-free, kind="stable")[:40]
+    nodes["req_cpu"][top] = nodes["alloc_cpu"][top]
+    nodes["nz_cpu"][top] = np.maximum(nodes["nz_cpu"][top], nodes["alloc_cpu"][top])
+    kc = cfg.kg_config()
+    monkeypatch.setenv("KG_TRACE_FIX", "1")
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_select(snap, batch, k)
+    want = oracle_lib.ext_select(kc, nodes, pods, k, 0, quotas, rsv)
+    assert np.array_equal(got, want)
+    m = re.search(r"re-ran (\d+) of (\d+) rows", capfd.readouterr().err)
+    assert m and int(m.group(1)) > 0, "no row re-run: the test no longer reaches k_ext_fix_rows"
+    gpu = pods["dev_count"] > 0
+    assert (want[gpu, 0] != 0).any()
 
 
 def plain_pods(pods):

@@ -11,6 +11,7 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_alloc_kat.py tests/test_ext
 tail -2 gpurun_out/gpu_tests_$TAG.log
 timeout -k 10 300 python bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench5_$TAG.json 2> gpurun_out/bench5_$TAG.err || exit 2
 python -c "import json;d=json.loads(open('gpurun_out/bench5_$TAG.json').read().strip().splitlines()[-1]);print('bench5', round(d['ms_per_step'],4), '%.4g'%d['value'])"
+KG_TRACE_FIX=1 timeout -k 10 300 python bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline --no-cycle --no-replay 2>&1 >/dev/null | grep "re-ran" | head -3 || true
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 cd /tmp || exit 1

@@ -1,7 +1,8 @@
 """Summarise a rocprofv3 collection of profiles/run_profile.sh into profiles/<out>.json.
 
-Per select launch (the kernels of one step's select bracket: the k_select kernels of both node storage
-classes for configs 1-4, k_ext_select + the plain pods' k_select for config 5), from the PMC passes:
+Per select step (the kernels of one step's bracket: the k_select kernels of both node storage classes for
+configs 1-4; for config 5 every kernel of the step: DevSum / restore codes, pass 1, the one-pass select and its
+re-run, the general records, the plain pods' k_select), summed over a step's dispatches, from the PMC passes:
   FETCH_SIZE (KB)  -> doubled per MI355X_MICROARCH.md § HBM (gfx950 reports 1/2 of wide streaming reads)
   WRITE_SIZE (KB)
   hbm_bytes_per_launch  = 1024 * (2 * FETCH_SIZE + WRITE_SIZE), summed over the bracket's kernels
@@ -23,10 +24,13 @@ sys.path.insert(0, ROOT)
 
 
 def per_kernel(path):
-    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    """{kernel: {counter: sum over its dispatches}}, {kernel: dispatches}."""
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    ids = collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
-        agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+        agg[r["Kernel_Name"]][r["Counter_Name"]] += float(r["Counter_Value"])
+        ids[r["Kernel_Name"]].add(r.get("Dispatch_Id") or r.get("Correlation_Id") or len(ids[r["Kernel_Name"]]))
+    return {k: dict(d) for k, d in agg.items()}, {k: len(v) for k, v in ids.items()}
 
 
 def main(prof, out, names):
@@ -35,13 +39,19 @@ def main(prof, out, names):
     stats = {}
     for r in csv.DictReader(open(os.path.join(prof, "trace", "run_kernel_stats.csv"))):
         stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+    # per step: a bracket kernel may run more than once a step (config 5's k_ext_select: the guess launch and the
+    # re-run), so counters are summed over dispatches and divided by the step count of the pass (the fewest
+    # dispatches of any bracket kernel: each runs at least once a step)
     counters = collections.defaultdict(dict)
     for d in sorted(os.listdir(prof)):
         p = os.path.join(prof, d, "run_counter_collection.csv")
         if d.startswith("pmc") and os.path.exists(p):
-            for k, v in per_kernel(p).items():
-                counters[k].update(v)
+            sums, calls = per_kernel(p)
+            steps = min([c for k, c in calls.items() if any(n in k for n in names)] or [1])
+            for k, v in sums.items():
+                counters[k].update({c: x / steps for c, x in v.items()})
     sel = {k: v for k, v in counters.items() if any(n in k for n in names)}
+    tsteps = min([v["calls"] for k, v in stats.items() if any(n in k for n in names)] or [1])
 
     def total(c):
         return sum(v.get(c, 0.0) for v in sel.values())
@@ -59,7 +69,8 @@ def main(prof, out, names):
         "valu_insts_per_launch": total("SQ_INSTS_VALU"),
         "salu_insts_per_launch": total("SQ_INSTS_SALU"),
         "kernels": {k: {"trace": stats.get(k), "counters": v} for k, v in sel.items()},
-        "select_avg_ns_sum": sum((stats.get(k) or {}).get("avg_ns", 0.0) for k in sel),
+        "select_avg_ns_sum": sum((stats.get(k) or {}).get("avg_ns", 0.0) * (stats.get(k) or {}).get("calls", 0) / tsteps
+                                 for k in sel),
         "all_kernels_trace": stats,
         "all_kernels_counters": counters,
     }

@@ -19,19 +19,27 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import isa_mix  # noqa: E402
 
 CYC_F32, CYC_OTHER = 2.0, 4.0
-KERNELS = ("k_select1", "k_select", "k_ext_select", "k_ext_stats", "k_big_init")
+KERNELS = ("k_select1", "k_select", "k_ext_select", "k_ext_select_sp", "k_ext_stats", "k_ext_stats_sp", "k_ext_stats_views",
+           "k_dev_sum", "k_rdev_codes", "k_big_init", "k_big_sel")
 
 
 def canon_mangled(nm):
-    """_ZN2kg9k_select1ILj7ELi0EEEv... -> k_select1<7,0>"""
-    m = re.match(r"_ZN2kg\d+(\w+?)I(.*?)EEv", nm)
+    """_ZN2kg9k_select1ILj7ELi0EEEv... -> k_select1<7,0>; _ZN2kg9k_dev_sumEPK... -> k_dev_sum"""
+    m = re.match(r"_ZN2kg(\d+)", nm)
     if not m:
         return None
-    args = re.findall(r"L([jib])(\d+)E", m.group(2))
+    name = nm[m.end():m.end() + int(m.group(1))]
+    rest = nm[m.end() + int(m.group(1)):]
+    if not rest.startswith("I"):
+        return name
+    m = re.match(r"I(.*?)EEv", rest)
+    if not m:
+        return None
+    args = re.findall(r"L([jib])(\d+)E", m.group(1))
     out = []
     for t, v in args:
         out.append(("true" if v == "1" else "false") if t == "b" else v)
-    return f"{m.group(1)}<{','.join(out)}>"
+    return f"{name}<{','.join(out)}>"
 
 
 def canon_demangled(nm):
