@@ -21,6 +21,22 @@
 
 namespace kg {
 
+// XCD-aware workgroup order of a (pod block x, record chunk y) select grid. Workgroups are dealt round-robin over
+// the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), each with its own L2, so in launch order every XCD's L2
+// would pull every record chunk. Renumbering the workgroups dealt to one XCD as a contiguous run of the chunk-major
+// order gives each XCD whole chunks (all their pod blocks): a chunk's records come from HBM once. Block order
+// changes no result (keys are merged by atomicMax or stored per (chunk, pod)).
+struct GridBlock {
+    uint32_t x, y;
+};
+__device__ __forceinline__ GridBlock xcd_block() {
+    const uint32_t gx = gridDim.x, total = gx * gridDim.y;
+    const uint32_t l = blockIdx.x + blockIdx.y * gx;
+    const uint32_t full = total & ~7u;  // the tail of < 8 workgroups keeps its place
+    const uint32_t n = l < full ? (l & 7u) * (full >> 3) + (l >> 3) : l;
+    return {n % gx, n / gx};
+}
+
 struct PodV {
     int64_t req_cpu, req_mem, req_eph, sc0, sc1, nz_cpu, nz_mem, est0, est1;
     uint32_t flags;

@@ -47,9 +47,10 @@ __device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) {
 
 constexpr uint32_t DSUM_CHUNK = 8;  // GPU request classes per thread of k_dev_sum / k_rdev_codes
 
-// DevSum of every record for the pod batch's GPU request classes: thread = (record, chunk of DSUM_CHUNK classes,
-// blockIdx.y); each thread sums the record's minors and, per class of its chunk, runs the GPU allocator and scores
-// one instance; chunk 0 also stores the sums. cls_max[class] = the best score over the fast-base records (below n0,
+// DevSum of every record for the pod batch's GPU request classes: thread = record; it loads the record's minors
+// once and, per class, runs the GPU allocator's Filter and scores one instance (codes / scores stored 8 classes at
+// a time). The kernel is bound by the latency of the record loads (lanes are a record apart), not by arithmetic, so
+// the classes are not split over more threads. cls_max[class] = the best score over the fast-base records (below n0,
 // not F_BIG, with GPUs) the class fits on: the one-pass select's guess of the DeviceShare maximum.
 __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                  const DevRec* __restrict__ devs, uint32_t n_nodes, uint32_t n0,
@@ -90,46 +91,48 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
         o.rcp[r] = t != 0 ? 1.0 / (double)t : 0.0;
     }
     DevSum& w = out[rec];
-    const uint32_t k0 = blockIdx.y * DSUM_CHUNK;
-    if (blockIdx.y == 0 && live) {
+    if (live) {
         for (int r = 0; r < DEV_R; r++) {
             w.T[r] = o.T[r];
             w.F[r] = o.F[r];
             w.rcp[r] = o.rcp[r];
         }
     }
-    uint64_t codes = 0, scores = 0;  // DSUM_CHUNK = 8 bytes each: one store per chunk
     static_assert(DSUM_CHUNK == 8 && offsetof(DevSum, code) % 8 == 0 && offsetof(DevSum, score) % 8 == 0, "packed stores");
+    const uint32_t nc = min(n_cls, (uint32_t)DEV_CLASSES);
+    for (uint32_t k0 = 0; k0 < nc; k0 += DSUM_CHUNK) {
+        uint64_t codes = 0, scores = 0;  // DSUM_CHUNK = 8 bytes each: one store per chunk
 #pragma unroll 1
-    for (uint32_t i = 0; i < DSUM_CHUNK; i++) {
-        const uint32_t k = k0 + i;
-        if (k >= n_cls) break;
-        PodX x{};
-        x.dkeys = cls[k].dkeys;
-        x.dcount = cls[k].dcount;
-        x.dflags = cls[k].dflags;
-        x.dbw = cls[k].dbw;
-        for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
-        uint32_t le = 0u;
+        for (uint32_t i = 0; i < DSUM_CHUNK; i++) {
+            const uint32_t k = k0 + i;
+            if (k >= nc) break;
+            PodX x{};
+            x.dkeys = cls[k].dkeys;
+            x.dcount = cls[k].dcount;
+            x.dflags = cls[k].dflags;
+            x.dbw = cls[k].dbw;
+            for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
+            uint32_t le = 0u;
 #pragma unroll
-        for (int m = 0; m < DEV_MINORS; m++) {
-            bool ok = m < D;
+            for (int m = 0; m < DEV_MINORS; m++) {
+                bool ok = m < D;
 #pragma unroll
-            for (int r = 0; r < DEV_R; r++) ok &= !(((x.dkeys >> r) & 1u) && x.dreq[r] > fr[r][m]);
-            le |= ok ? 1u << m : 0u;
+                for (int r = 0; r < DEV_R; r++) ok &= !(((x.dkeys >> r) & 1u) && x.dreq[r] > fr[r][m]);
+                le |= ok ? 1u << m : 0u;
+            }
+            const GpuMinors g{used, total, total & le, nonzero & le};
+            // D <= 0 never reads the code (the pair is decided first)
+            const uint32_t code = D > 0 ? gpu_allocate_code(e, D, topo, part, x, g) : 0u;
+            const uint32_t score = (uint32_t)dev_sum_score(cfg, &o, x);
+            codes |= (uint64_t)(code & 0xFFu) << (8 * i);
+            scores |= (uint64_t)(score & 0xFFu) << (8 * i);
+            const int32_t best = wmax_i32((fbrec && code == 0u) ? (int32_t)score : 0);
+            if (best > 0 && (threadIdx.x & 63u) == 0) atomicMax(cls_max + k, (uint32_t)best);
         }
-        const GpuMinors g{used, total, total & le, nonzero & le};
-        // D <= 0 never reads the code (the pair is decided first)
-        const uint32_t code = D > 0 ? gpu_allocate_code(e, D, topo, part, x, g) : 0u;
-        const uint32_t score = (uint32_t)dev_sum_score(cfg, &o, x);
-        codes |= (uint64_t)(code & 0xFFu) << (8 * i);
-        scores |= (uint64_t)(score & 0xFFu) << (8 * i);
-        const int32_t best = wmax_i32((fbrec && code == 0u) ? (int32_t)score : 0);
-        if (best > 0 && (threadIdx.x & 63u) == 0) atomicMax(cls_max + k, (uint32_t)best);
-    }
-    if (live) {
-        *reinterpret_cast<uint64_t*>(&w.code[k0]) = codes;
-        *reinterpret_cast<uint64_t*>(&w.score[k0]) = scores;
+        if (live) {
+            *reinterpret_cast<uint64_t*>(&w.code[k0]) = codes;
+            *reinterpret_cast<uint64_t*>(&w.score[k0]) = scores;
+        }
     }
 }
 
@@ -410,13 +413,14 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
     // lane = row j of the output; the pod is list[j] (list == nullptr: the batch in order). Re-run launch
     // (e.rows): lane t takes row e.rows[t] of the *e.n_rows rows k_ext_fix_rows listed.
     constexpr bool FUSED = FB && PART == 1 && K == 1;  // top-1 straight into partial[row] by atomicMax
-    const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const GridBlock b = xcd_block();
+    const uint32_t t0 = b.x * blockDim.x + threadIdx.x;
     uint32_t j = t0;
     bool live = j < n_pods;
     if constexpr (FB) {
         if (e.rows) {
             const uint32_t nr = *e.n_rows;
-            if (blockIdx.x * blockDim.x >= nr) return;  // whole workgroup idle (no barrier in this kernel)
+            if (b.x * blockDim.x >= nr) return;  // whole workgroup idle (no barrier in this kernel)
             live = t0 < nr;
             j = live ? e.rows[t0] : 0u;
         }
@@ -436,7 +440,7 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
     uint64_t top[K];
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
-    const uint32_t lo = blockIdx.y * chunk, hi = min(n_nodes, lo + chunk);
+    const uint32_t lo = b.y * chunk, hi = min(n_nodes, lo + chunk);
     PodF pff{};
     KCfg cv = cfg;
     if constexpr (FB) {
@@ -482,7 +486,7 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
         if constexpr (FUSED) {
             if (top[0]) atomicMax((unsigned long long*)(partial + j), (unsigned long long)top[0]);
         } else {
-            uint64_t* dst = partial + ((size_t)blockIdx.y * n_pods + j) * K;
+            uint64_t* dst = partial + ((size_t)b.y * n_pods + j) * K;
 #pragma unroll
             for (int t = 0; t < K; t++) dst[t] = top[t];
         }
@@ -913,9 +917,8 @@ hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevR
                           uint32_t* cls_max, hipStream_t s) {
     hipError_t err = hipMemsetAsync(cls_max, 0, sizeof(uint32_t) * DEV_CLASSES, s);
     if (err != hipSuccess || n_nodes == 0) return err;
-    // the chunks of the batch's classes (a class's code / score is read only by pods of that class)
-    const uint32_t chunks = std::max<uint32_t>(1u, (std::min<uint32_t>(n_cls, DEV_CLASSES) + DSUM_CHUNK - 1) / DSUM_CHUNK);
-    k_dev_sum<<<dim3((n_nodes + 255) / 256, chunks), 256, 0, s>>>(nodes, zones, devs, n_nodes, n0, cls, n_cls, cfg, e, out,
+    // the batch's classes only (a class's code / score is read only by pods of that class)
+    k_dev_sum<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, zones, devs, n_nodes, n0, cls, n_cls, cfg, e, out,
                                                                   cls_max);
     return hipGetLastError();
 }

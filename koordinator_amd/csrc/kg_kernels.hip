@@ -136,11 +136,12 @@ __global__ __launch_bounds__(256) void k_select1(const NodeRec* __restrict__ nod
                                                  PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
                                                  uint32_t chunk, uint32_t index_base, KCfg cfg,
                                                  uint64_t* __restrict__ out, const uint32_t* __restrict__ order) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const GridBlock b = xcd_block();
+    const uint32_t j = b.x * blockDim.x + threadIdx.x;
     const bool live = j < n_pods;
     const uint32_t o = live ? (order ? order[j] : j) : 0u;
     const PodV p = load_pod(pods, o);
-    const uint32_t lo = begin + blockIdx.y * chunk;
+    const uint32_t lo = begin + b.y * chunk;
     const uint32_t hi = min(end, lo + chunk);
     const PodF pf = to_podf(p, cfg);
     const KCfg cv = cfg_in_vgprs(cfg);

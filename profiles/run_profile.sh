@@ -29,7 +29,7 @@ timeout -s KILL 150 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM SQ_INSTS_LDS S
 cd "$R" || exit 1
 if [ "$CFG" = "5" ]; then
     python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_ext_select" "k_ext_stats" "k_ext_fix_rows" "k_dev_sum" \
-        "k_rdev_codes" "k_ext_gate" "k_special_scan" "k_select<" "k_select1<" "k_big_" || exit $?
+        "k_rdev_codes" "k_ext_gate" "k_special_scan" "k_scatter_keys" "k_select<" "k_select1<" "k_big_sel" || exit $?
 else
     python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_select<" "k_select1<" "k_big_init" || exit $?
 fi
