@@ -535,6 +535,15 @@ kg_status kg_replay(kg_snap* snap, kg_pods* pods, int32_t* out_node, int64_t* ou
  * Reserve fails on that node (BestEffort allocation), nothing applied. */
 kg_status kg_assume(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node);
 kg_status kg_forget(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t numa_zone);
+/* kg_assume that also returns the NodeNUMAResource allocation it made: *out_zone as kg_verify_out.numa_zone,
+ * out_zone_amounts[2 * KG_MAX_ZONES] = cpu (milli) per zone, then memory (bytes) per zone (zeros when no zone was
+ * allocated). The reference keeps that allocation for the Unreserve (nodenumaresource/plugin.go:585-635 Reserve,
+ * :700 Unreserve -> resource_manager.go:478-483 Release); kg_forget_numa takes it back, including a split over
+ * several zones (zone code 0x40 | mask), which kg_forget refuses. */
+kg_status kg_assume_numa(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t* out_zone,
+                         int64_t* out_zone_amounts);
+kg_status kg_forget_numa(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t numa_zone,
+                         const int64_t* zone_amounts);
 /* Reserve with every enabled plugin's state (NodeInfo, LoadAware, NUMA zone, DeviceShare minors via
  * defaultAllocateDevices order, ElasticQuota used); returns the NUMA zone and the GPU minor bitmask
  * the Unreserve needs (deviceshare/plugin.go:507-569, elasticquota/plugin.go:622-636). */

@@ -794,8 +794,10 @@ __device__ __forceinline__ uint64_t pair_key(const KCfg& c, const PairOut& o, ui
 
 // Reserve of a multi-zone NUMA allocation: the split recomputed on the zone state the pair was
 // evaluated on. Out of line, so that its private arrays stay out of the callers' frames.
+// split_out (nullable): the per-zone amounts taken, cpu [0, MAX_ZONES) then memory (the allocation the
+// Unreserve releases, resource_manager.go:478-483).
 __device__ __forceinline__ void numa_reserve_split(ZoneRec* zr, uint32_t Z, int64_t req_cpu, int64_t req_mem, uint32_t pflags,
-                                                uint32_t mask) {
+                                                uint32_t mask, int64_t* split_out = nullptr) {
     NumaZ x;
     numa_load(zr, Z, x);
     const int64_t req[2] = {req_cpu, req_mem};
@@ -805,12 +807,18 @@ __device__ __forceinline__ void numa_reserve_split(ZoneRec* zr, uint32_t Z, int6
         for (int z = 0; z < MAX_ZONES; z++) {
             zr->cpu_used[z] += al[0][z];
             zr->mem_used[z] += al[1][z];
+            if (split_out) {
+                split_out[z] = al[0][z];
+                split_out[MAX_ZONES + z] = al[1][z];
+            }
         }
 }
 
 // Reserve (sign = +1) / Unreserve (sign = -1) of pod p on node record n (a16).
+// split (nullable): a multi-zone allocation's per-zone amounts, written by the Reserve and taken back by the
+// Unreserve (cpu [0, MAX_ZONES) then memory).
 __device__ __forceinline__ void apply_assume(const KCfg& c, int64_t* n, ZoneRec* zr, const PodV& p, int32_t zone,
-                                             int64_t sign) {
+                                             int64_t sign, int64_t* split = nullptr) {
     n[N_REQ_CPU] += sign * p.req_cpu;
     n[N_REQ_MEM] += sign * p.req_mem;
     n[N_REQ_EPH] += sign * p.req_eph;
@@ -836,8 +844,18 @@ __device__ __forceinline__ void apply_assume(const KCfg& c, int64_t* n, ZoneRec*
     if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES) {
         zr->cpu_used[zone] += sign * p.req_cpu;
         zr->mem_used[zone] += sign * p.req_mem;
+        if (split && sign > 0) {
+            split[zone] = p.req_cpu;
+            split[MAX_ZONES + zone] = p.req_mem;
+        }
     } else if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0x40 && sign > 0) {
-        numa_reserve_split(zr, (flags >> F_NUMA_ZONES_SHIFT) & 15u, p.req_cpu, p.req_mem, p.flags, (uint32_t)zone & 0xFu);
+        numa_reserve_split(zr, (flags >> F_NUMA_ZONES_SHIFT) & 15u, p.req_cpu, p.req_mem, p.flags, (uint32_t)zone & 0xFu,
+                           split);
+    } else if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0x40 && zone < 0x80 && split) {
+        for (int z = 0; z < MAX_ZONES; z++) {
+            zr->cpu_used[z] += sign * split[z];
+            zr->mem_used[z] += sign * split[MAX_ZONES + z];
+        }
     }
     derive_node(*reinterpret_cast<NodeRec*>(n), *zr);
 }

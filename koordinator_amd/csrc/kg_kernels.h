@@ -177,6 +177,7 @@ hipError_t launch_replay_step(NodeRec* nodes, ZoneRec* zones, const PodsDev& pod
 hipError_t launch_bump(uint32_t* step_base, uint32_t by, hipStream_t s);
 hipError_t launch_rb_window(const LaunchRb& a, hipStream_t s);
 hipError_t launch_assume(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t pod, uint32_t node,
-                         int32_t zone, int64_t sign, const KCfg& cfg, bool exact, int32_t* zone_out, hipStream_t s);
+                         int32_t zone, int64_t sign, const KCfg& cfg, bool exact, int32_t* zone_out, hipStream_t s,
+                         int64_t* split = nullptr);
 
 }  // namespace kg

@@ -343,7 +343,8 @@ __global__ void k_bump(uint32_t* step_base, uint32_t by) {
 
 template <bool EXACT>
 __global__ void k_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, PodsDev pods, uint32_t pod,
-                         uint32_t node, int32_t zone_in, int64_t sign, KCfg cfg, int32_t* __restrict__ zone_out) {
+                         uint32_t node, int32_t zone_in, int64_t sign, KCfg cfg, int32_t* __restrict__ zone_out,
+                         int64_t* __restrict__ split) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const PodV q = load_pod(pods, pod);
     int64_t* n = nodes[node].v;
@@ -353,7 +354,7 @@ __global__ void k_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zone
         const PairOut o = eval_pair<EXACT>(cfg, n, zones + node, q);
         zone = o.zone;
     }
-    if (!zone_reserve_fails(zone)) apply_assume(cfg, n, zones + node, q, zone, sign);  // else nothing is applied
+    if (!zone_reserve_fails(zone)) apply_assume(cfg, n, zones + node, q, zone, sign, split);  // else nothing is applied
     if (zone_out) *zone_out = zone;
 }
 
@@ -1045,11 +1046,12 @@ hipError_t launch_bump(uint32_t* step_base, uint32_t by, hipStream_t s) {
 }
 
 hipError_t launch_assume(NodeRec* nodes, ZoneRec* zones, const PodsDev& pods, uint32_t pod, uint32_t node,
-                         int32_t zone, int64_t sign, const KCfg& cfg, bool exact, int32_t* zone_out, hipStream_t s) {
+                         int32_t zone, int64_t sign, const KCfg& cfg, bool exact, int32_t* zone_out, hipStream_t s,
+                         int64_t* split) {
     if (exact)
-        k_assume<true><<<1, 64, 0, s>>>(nodes, zones, pods, pod, node, zone, sign, cfg, zone_out);
+        k_assume<true><<<1, 64, 0, s>>>(nodes, zones, pods, pod, node, zone, sign, cfg, zone_out, split);
     else
-        k_assume<false><<<1, 64, 0, s>>>(nodes, zones, pods, pod, node, zone, sign, cfg, zone_out);
+        k_assume<false><<<1, 64, 0, s>>>(nodes, zones, pods, pod, node, zone, sign, cfg, zone_out, split);
     return KG_LAUNCH_CHECK();
 }
 

@@ -178,6 +178,7 @@ struct kg_pods {
     // one-pass fast-base select of the GPU pods (ExtDev.cls_max / fb_max / rows): [cap] fast-base maxima, [cap] rows
     // to re-run, [DEV_CLASSES] per-class bounds, row count
     uint32_t* d_spec = nullptr;
+    int64_t* d_split = nullptr;  // kg_assume_numa / kg_forget_numa: per-zone amounts of a NUMA allocation
     // replay / shard scratch
     uint64_t* d_winners = nullptr;
     uint32_t* d_step = nullptr;
@@ -1453,7 +1454,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
                     (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
                     (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
-                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_spec, (void*)p->d_batch, (void*)p->d_rcode})
+                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_spec, (void*)p->d_split, (void*)p->d_batch, (void*)p->d_rcode})
         hipFree(b);
     hipHostFree(p->h_in);
     hipHostFree(p->h_keys);
@@ -2139,46 +2140,76 @@ kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_tota
     return KG_OK;
 }
 
-kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) {
+// Reserve of (pod, node); split != nullptr: the NUMA allocation's per-zone amounts (2 x KG_MAX_ZONES) are returned.
+static kg_status assume_impl(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t* out_zone, int64_t* out_split) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (out_split && !p->d_split) HIP_TRY(ctx, hipMalloc(&p->d_split, sizeof(int64_t) * 2 * KG_MAX_ZONES));
     touch_views(s, node);
     HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 2, ctx->stream));
+    if (out_split) HIP_TRY(ctx, hipMemsetAsync(p->d_split, 0, sizeof(int64_t) * 2 * KG_MAX_ZONES, ctx->stream));
     if (s->has_cpu)
         HIP_TRY(ctx, launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, pod,
                                            s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, p->n, nullptr, p->d_aout,
                                            ctx->stream));
     HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], -1, 1, s->kcfg, force_exact(), p->d_aout,
-                               ctx->stream));
+                               ctx->stream, out_split ? p->d_split : nullptr));
     s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     int32_t zone = -1;
     HIP_TRY(ctx, hipMemcpyAsync(&zone, p->d_aout, sizeof(zone), hipMemcpyDeviceToHost, ctx->stream));
+    if (out_split)
+        HIP_TRY(ctx, hipMemcpyAsync(out_split, p->d_split, sizeof(int64_t) * 2 * KG_MAX_ZONES, hipMemcpyDeviceToHost,
+                                    ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (out_zone) *out_zone = zone;
     if (zone_reserve_fails(zone))
         return fail(ctx, KG_RESERVE_FAILED, "Reserve of pod %u on node %u failed: NUMA status 0x%x", pod, node, zone_fail_status(zone));
     return KG_OK;
 }
 
-kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone) {
+kg_status kg_assume(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node) { return assume_impl(s, p, pod, node, nullptr, nullptr); }
+
+kg_status kg_assume_numa(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t* out_zone, int64_t* out_zone_amounts) {
+    if (!out_zone || !out_zone_amounts) return s && s->ctx ? fail(s->ctx, KG_INVALID_ARG, "null output") : KG_INVALID_ARG;
+    return assume_impl(s, p, pod, node, out_zone, out_zone_amounts);
+}
+
+static kg_status forget_impl(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone, const int64_t* split) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
-    if (zone >= KG_MAX_ZONES) return fail(ctx, KG_UNSUPPORTED, "Unreserve of a multi-zone NUMA allocation (zone code 0x%x)", zone);
+    const bool multi = zone >= 0x40 && zone < 0x80;
+    if (zone >= KG_MAX_ZONES && !(multi && split))
+        return fail(ctx, KG_UNSUPPORTED, "Unreserve of a multi-zone NUMA allocation (zone code 0x%x) needs its per-zone "
+                                         "amounts (kg_forget_numa)", zone);
     if (cpuset_bound(s, p, pod, node)) return fail(ctx, KG_UNSUPPORTED, "Unreserve of a cpuset allocation");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (multi && !p->d_split) HIP_TRY(ctx, hipMalloc(&p->d_split, sizeof(int64_t) * 2 * KG_MAX_ZONES));
     touch_views(s, node);
-    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], zone, -1, s->kcfg, force_exact(), nullptr, ctx->stream));
+    if (multi)
+        HIP_TRY(ctx, hipMemcpyAsync(p->d_split, split, sizeof(int64_t) * 2 * KG_MAX_ZONES, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch_assume(s->d_nodes, s->d_zones, p->dev, pod, s->pos[node], zone, -1, s->kcfg, force_exact(), nullptr,
+                               ctx->stream, multi ? p->d_split : nullptr));
     s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return KG_OK;
+}
+
+kg_status kg_forget(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone) {
+    return forget_impl(s, p, pod, node, zone, nullptr);
+}
+
+kg_status kg_forget_numa(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int32_t zone, const int64_t* zone_amounts) {
+    if (!zone_amounts) return s && s->ctx ? fail(s->ctx, KG_INVALID_ARG, "null zone amounts") : KG_INVALID_ARG;
+    return forget_impl(s, p, pod, node, zone, zone_amounts);
 }
 
 static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total, uint32_t* out_reason) {

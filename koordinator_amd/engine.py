@@ -89,6 +89,10 @@ def lib():
     L.kg_assume.restype = st
     L.kg_forget.argtypes = [vp, vp, u32, u32, i32]
     L.kg_forget.restype = st
+    L.kg_assume_numa.argtypes = [vp, vp, u32, u32, P(i32), P(C.c_int64)]
+    L.kg_assume_numa.restype = st
+    L.kg_forget_numa.argtypes = [vp, vp, u32, u32, i32, P(C.c_int64)]
+    L.kg_forget_numa.restype = st
     L.kg_profile_enable.argtypes = [vp, C.c_int]
     L.kg_profile_enable.restype = st
     L.kg_profile_read.argtypes = [vp, P(C.c_double), P(u64), C.c_int]
@@ -361,6 +365,22 @@ def assume(snap: Snapshot, pods: PodBatch, pod: int, node: int):
 
 def forget(snap: Snapshot, pods: PodBatch, pod: int, node: int, zone: int):
     snap.ctx.check(snap.ctx.L.kg_forget(snap.h, pods.h, pod, node, zone), "kg_forget")
+
+
+def assume_numa(snap: Snapshot, pods: PodBatch, pod: int, node: int):
+    """kg_assume_numa: (zone code, [2, KG_MAX_ZONES] cpu / memory taken per zone)."""
+    zone = C.c_int32()
+    amounts = np.zeros(2 * abi.KG_MAX_ZONES, np.int64)
+    snap.ctx.check(snap.ctx.L.kg_assume_numa(snap.h, pods.h, pod, node, C.byref(zone),
+                                             amounts.ctypes.data_as(C.POINTER(C.c_int64))), "kg_assume_numa")
+    return zone.value, amounts.reshape(2, abi.KG_MAX_ZONES)
+
+
+def forget_numa(snap: Snapshot, pods: PodBatch, pod: int, node: int, zone: int, amounts: np.ndarray):
+    a = np.ascontiguousarray(amounts, np.int64).reshape(-1)
+    assert a.size == 2 * abi.KG_MAX_ZONES
+    snap.ctx.check(snap.ctx.L.kg_forget_numa(snap.h, pods.h, pod, node, zone, a.ctypes.data_as(C.POINTER(C.c_int64))),
+                   "kg_forget_numa")
 
 
 def replay_minors(pods: PodBatch) -> np.ndarray:

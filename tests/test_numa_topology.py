@@ -227,6 +227,52 @@ def test_topology_assume_forget(ctx):
 
 
 @pytest.mark.gpu
+def test_topology_multi_zone_unreserve(ctx):
+    """kg_assume_numa returns the allocation the Reserve made (per-zone cpu / memory; a split over several zones for
+    0x40 | mask codes) and kg_forget_numa releases exactly it (resource_manager.go:478-483 Release): Reserve of
+    several multi-zone and single-zone pods, their Unreserve in another order, every column back to the start. The
+    amounts of each split cover the pod's request and sit on the zones of its mask; the zone state after the
+    Reserves equals the oracle's."""
+    kc, nodes, pods = workload(6, 300, 96)
+    snap, batch = engine.Snapshot(ctx, kc, nodes), engine.PodBatch(ctx, pods)
+    ref = oracle_lib.eval_verify(kc, nodes, pods)
+    ost = oracle_lib.OracleState(kc, nodes)
+    before = snap.read_state()
+    ok = np.argwhere(ref.status == 0)
+    multi, used = [], set()
+    for j, i in ok:
+        if ref.numa_zone[j, i] >= 0x40 and i not in used:
+            multi.append((int(j), int(i)))
+            used.add(i)
+        if len(multi) == 4:
+            break
+    single = [(int(j), int(i)) for j, i in ok if 0 <= ref.numa_zone[j, i] < 4 and i not in used][:2]
+    assert len(multi) >= 2 and single
+    made = []
+    for j, i in multi + single:
+        zone, amounts = engine.assume_numa(snap, batch, j, i)
+        assert zone == int(ref.numa_zone[j, i])
+        ost.assume(i, pods, j)
+        mask = zone & 0xF if zone >= 0x40 else 1 << zone
+        off = [z for z in range(abi.KG_MAX_ZONES) if not (mask >> z) & 1]
+        assert not amounts[:, off].any()
+        if pods["flags"][j] & abi.KG_POD_HAS_CPU:
+            assert amounts[0].sum() == pods["req_cpu"][j]
+        if pods["flags"][j] & abi.KG_POD_HAS_MEM:
+            assert amounts[1].sum() == pods["req_mem"][j]
+        made.append((j, i, zone, amounts))
+    state, want = snap.read_state(), ost.table()
+    for z in range(abi.KG_MAX_ZONES):
+        assert np.array_equal(state[f"zone_cpu_used{z}"], want[f"zone_cpu_used{z}"])
+        assert np.array_equal(state[f"zone_mem_used{z}"], want[f"zone_mem_used{z}"])
+    for j, i, zone, amounts in made[1::2] + made[0::2]:
+        engine.forget_numa(snap, batch, j, i, zone, amounts)
+    after = snap.read_state()
+    for k in before:
+        assert np.array_equal(before[k], after[k]), k
+
+
+@pytest.mark.gpu
 def test_best_effort_reserve_failures(ctx):
     """The BestEffort semantics on the device: Filter / Score / select without the topology manager, the
     Reserve's zone (or failure) in verify, replays that leave a pod unscheduled when its selected node's
