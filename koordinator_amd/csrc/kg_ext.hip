@@ -56,6 +56,17 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
                                                  const DevRec* __restrict__ devs, uint32_t n_nodes, uint32_t n0,
                                                  const DevClass* __restrict__ cls, uint32_t n_cls, KCfg cfg, ExtDev e,
                                                  DevSum* __restrict__ out, uint32_t* __restrict__ cls_max) {
+    // the partition tables in LDS: allocateByPartition walks them per class in a dependent chain of loads
+    __shared__ kg_gpu_partition lparts[KG_GPU_MAX_PARTS];
+    __shared__ uint32_t lrng[KG_GPU_MAX_TABLES * 9];
+    if (e.parts) {
+        const uint32_t np = min(e.n_parts, (uint32_t)KG_GPU_MAX_PARTS);
+        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) lparts[i] = e.parts[i];
+        for (uint32_t i = threadIdx.x; i < (uint32_t)KG_GPU_MAX_TABLES * 9u; i += blockDim.x) lrng[i] = e.part_rng[i];
+        __syncthreads();
+        e.parts = lparts;
+        e.part_rng = lrng;
+    }
     const uint32_t rec0 = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = rec0 < n_nodes;
     const uint32_t rec = live ? rec0 : n_nodes - 1;  // dead lanes compute a copy for the wave reductions

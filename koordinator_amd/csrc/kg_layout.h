@@ -420,6 +420,7 @@ struct ExtDev {
     // GPU partition tables (kg_gpu_partition, grouped by table / GPU count / AllocationScore) and per (table,
     // GPU count) the entry range: part_rng[table * 9 + n] = begin | end << 16
     const kg_gpu_partition* parts;
+    uint32_t n_parts;
     const uint32_t* part_rng;
     const int64_t* binpack;  // [table][8, 4, 2 GPUs][allocated minors]: free partitions' AllocationScore sum
     // per batch (with dsum): the GPU allocator's code of every restore table (rdev) for every GPU request class,

@@ -122,11 +122,12 @@ struct kg_snap {
     kg_gpu_partition* d_parts = nullptr;
     uint32_t* d_part_rng = nullptr;  // [KG_GPU_MAX_TABLES * 9]
     int64_t* d_binpack = nullptr;    // [KG_GPU_MAX_TABLES][3][256]
-    uint32_t n_gpu_tables = 0;
+    uint32_t n_gpu_tables = 0, n_gpu_parts = 0;
     bool ext() const { return (cfg.plugins & KG_PLUGIN_EXT) != 0; }
     ExtDev ext_dev() const {
         ExtDev e{};
         e.parts = n_gpu_tables ? d_parts : nullptr;
+        e.n_parts = n_gpu_tables ? n_gpu_parts : 0u;
         e.part_rng = d_part_rng;
         e.binpack = d_binpack;
         e.dev = d_dev;
@@ -847,6 +848,7 @@ static kg_status upload_gpu_parts(kg_snap* s, const kg_node_columns* cols) {
         HIP_TRY(ctx, hipMemcpyAsync(s->d_parts, cols->gpu_parts, sizeof(kg_gpu_partition) * n, hipMemcpyHostToDevice, ctx->stream));
     }
     s->n_gpu_tables = tables;
+    if (n) s->n_gpu_parts = n;
     return KG_OK;
 }
 
