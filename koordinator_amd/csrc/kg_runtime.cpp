@@ -44,6 +44,9 @@ struct kg_ctx {
     uint64_t prof_launches = 0;
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
+    // config-5 select: the plain pods' k_select1 runs on `side` while `stream` builds DevSum and pass 1
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 struct kg_snap {
@@ -730,6 +733,9 @@ kg_status kg_close(kg_ctx* ctx) {
         hipEventDestroy(e.first);
         hipEventDestroy(e.second);
     }
+    if (ctx->side) hipStreamDestroy(ctx->side);
+    if (ctx->fork) hipEventDestroy(ctx->fork);
+    if (ctx->join) hipEventDestroy(ctx->join);
     hipStreamDestroy(ctx->stream);
     delete ctx;
     return KG_OK;
@@ -1629,20 +1635,28 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     return KG_OK;
 }
 
-static kg_status ext_stats_local(kg_snap* s, kg_pods* p) {
+// Quota gate (writes every pod's status first) and the pass-1 accumulators of the batch.
+static kg_status ext_gate_local(kg_snap* s, kg_pods* p) {
+    kg_ctx* ctx = s->ctx;
+    HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, s->ext_dev(), s->cfg.plugins, p->d_qst, p->d_pstat, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_dev_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_pref, 0xFF, sizeof(uint64_t) * p->n, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(spec_fb_max(p), 0, sizeof(uint32_t) * p->n, ctx->stream));
+    return KG_OK;
+}
+
+static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
     kg_ctx* ctx = s->ctx;
     ExtDev e = s->ext_dev();
-    kg_status dst = ext_dev_sum(s, p, e);
+    kg_status dst = gated ? KG_OK : ext_gate_local(s, p);
+    if (dst != KG_OK) return dst;
+    dst = ext_dev_sum(s, p, e);
     if (dst != KG_OK) return dst;
     if (ext_fast_base(s, p)) {  // records for the PART 2 kernels (pass 1 and pass 2 of this batch)
         if (!s->d_special) HIP_TRY(ctx, hipMalloc(&s->d_special, sizeof(uint32_t) * ((size_t)s->n + 1)));
         HIP_TRY(ctx, launch_special_scan(s->d_nodes, s->n, s->n0, s->d_special, ctx->stream));
     }
-    HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, e, s->cfg.plugins, p->d_qst, p->d_pstat, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(p->d_dev_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(p->d_pref, 0xFF, sizeof(uint64_t) * p->n, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(spec_fb_max(p), 0, sizeof(uint32_t) * p->n, ctx->stream));
     if (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) {
         // pods without a GPU request only get statistics from the nodes holding a view of their
         // reservation class (elsewhere s_dev = s_rsv = order = 0): one lane per pod over those views
@@ -1719,6 +1733,33 @@ static LaunchSelect make_select(const kg_snap* s, const PodsDev& pods, const uin
     return a;
 }
 
+// The plain pods' select can run beside the config-5 kernels when it is the fused top-1 (no partials shared
+// with the x lanes' merge).
+static bool plain_side_ok(const kg_snap* s, const kg_pods* p, uint32_t kk) {
+    const bool split = !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok &&
+                       !need_topo(s, p);
+    return split && kk == 1 && p->n_plain != 0 && !unfused();
+}
+
+static kg_status launch_plain_side(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out) {
+    kg_ctx* ctx = s->ctx;
+    if (!ctx->side) {
+        HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming));
+    }
+    uint32_t fparts = 0;
+    LaunchSelect a = make_select(s, p->dev, p->d_pmap, p->n_plain, p->n_plain, p->n, kk, true, d_out, nullptr, p->d_pstat,
+                                 &fparts);
+    if (fparts) return fail(ctx, KG_DEVICE_ERROR, "side-stream select needs %u partial rows", fparts);
+    a.partial = nullptr;
+    HIP_TRY(ctx, hipEventRecord(ctx->fork, ctx->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->side, ctx->fork, 0));
+    HIP_TRY(ctx, launch_select(a, ctx->side));
+    HIP_TRY(ctx, hipEventRecord(ctx->join, ctx->side));
+    return KG_OK;
+}
+
 // config-5 matrix mode, pass 2: totals with the normalised terms -> per-pod top-k in d_out.
 // Split: a plain pod's DeviceShare / Reservation terms are 0 and it passes their filters on every node
 // (eval_pair_ext with dcount == 0, no view, no required affinity), so its keys are exactly the base
@@ -1727,7 +1768,8 @@ static LaunchSelect make_select(const kg_snap* s, const PodsDev& pods, const uin
 // Fast-base batches: k_ext_select<FB> over the fast-base records with the guessed DeviceShare maxima (plus their
 // real ones), [all-reduce of those over the shards,] k_ext_fix_rows + re-run of the wrong guesses, then the general
 // records with the final maxima; top-1 is fused (atomicMax into the row's key, no partials / merge).
-static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out, bool global = false) {
+static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out, bool global = false,
+                                  bool plain_on_side = false) {
     kg_ctx* ctx = s->ctx;
     const bool split = !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok &&
                        !need_topo(s, p);
@@ -1766,7 +1808,8 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         NCCL_TRY(ctx, ncclAllReduce(spec_fb_max(p), spec_fb_max(p), p->n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
         HIP_TRY(ctx, launch_max_fold(p->d_dev_max, spec_fb_max(p), p->n, ctx->stream));
     }
-    if (n_plain) HIP_TRY(ctx, launch_select(a, ctx->stream));  // zeroes d_out first at k = 1: before the x scatter
+    if (n_plain && !plain_on_side)
+        HIP_TRY(ctx, launch_select(a, ctx->stream));  // zeroes d_out first at k = 1: before the x scatter
     if (n_x)
         HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
                                        s->kcfg, force_exact(), need_topo(s, p), fb, p->d_qst, p->d_dev_max, p->d_rsv_max,
@@ -1789,6 +1832,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
                                           p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, xpart, p->d_pstat, s->d_special,
                                           s->special_est(), ctx->stream));
     }
+    if (plain_on_side) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->join, 0));  // d_out zeroed + plain keys in
     if (!split) {
         if (!fused) HIP_TRY(ctx, launch_merge(p->d_partial, xparts, p->n, kk, d_out, ctx->stream));
         return KG_OK;
@@ -1822,9 +1866,18 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
         hipEvent_t e0, e1;
         st0 = record_begin(ctx, &e0, &e1);
         if (st0 != KG_OK) return st0;
-        st0 = ext_stats_local(s, p);
+        // the plain pods' fused select depends on nothing the config-5 kernels build: it runs on the side stream
+        // from the fork (after the quota gate has written every pod's status) and joins before the scatters
+        const bool side = plain_side_ok(s, p, kk) && !std::getenv("KG_NO_SIDE_STREAM");
+        if (side) {
+            st0 = ext_gate_local(s, p);
+            if (st0 != KG_OK) return st0;
+            st0 = launch_plain_side(s, p, kk, d_out);
+            if (st0 != KG_OK) return st0;
+        }
+        st0 = ext_stats_local(s, p, side);
         if (st0 != KG_OK) return st0;
-        st0 = ext_select_local(s, p, kk, d_out);
+        st0 = ext_select_local(s, p, kk, d_out, false, side);
         if (st0 != KG_OK) return st0;
         return record_end(ctx, e0, e1);
     }
