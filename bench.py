@@ -395,8 +395,9 @@ def main():
     evals = float(n_pods) * n_total * a.steps
     value = evals / elapsed
     avg_kernel_s = (kern_ms / 1e3) / max(launches, 1) if launches else None
-    # the committed PMC passes are per launch of one configuration (profiles/run_profile.sh: 2 and 5)
-    pmc = load_pmc({2: "select_pmc.json", 5: "ext_pmc.json"}[config]) if world == 1 and config in (2, 5) else None
+    # the committed PMC passes are per launch of one configuration (profiles/run_profile.sh: 2, 4 and 5)
+    pmc = load_pmc({2: "select_pmc.json", 4: "select4_pmc.json", 5: "ext_pmc.json"}[config]) \
+        if world == 1 and config in (2, 4, 5) else None
     fused = k == 1 and os.environ.get("KG_SELECT_UNFUSED", "0") in ("", "0")
     base = "k_big_sel + k_select1 (fused top-1)" if fused else "k_select + k_big_sel + k_merge"
     if config == 6:

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 collection for the select kernels (run on the GPU box from the repo root):
-#   bash profiles/run_profile.sh <tag> [config]      (config 2 default; 5 = the config-5 plugin set)
+#   bash profiles/run_profile.sh <tag> [config]      (config 2 default; 4 = 100k nodes top-3; 5 = the config-5 plugin set)
 # 1) kernel trace + stats of a bench run (per-kernel average durations);
 # 2) separate PMC passes (gfx950 slot limits): FETCH_SIZE, WRITE_SIZE, SQ instruction mix / cycles;
 # 3) tools/pmc_summary.py -> gpurun_out/prof_<tag>/summary.json (copy it to profiles/ to commit).
@@ -27,7 +27,9 @@ timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INST
 timeout -s KILL 150 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INST_CYCLES_VMEM -d "$OUT/pmc_clk" \
     -o run --output-format csv -- python3 "${PMC_BENCH[@]}" > /dev/null || exit $?
 cd "$R" || exit 1
-if [ "$CFG" = "5" ]; then
+if [ "$CFG" = "4" ]; then  # top-3: per-chunk partials merged by k_merge_list inside the bracket
+    python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_select<" "k_select1<" "k_big_sel" "k_merge" || exit $?
+elif [ "$CFG" = "5" ]; then
     python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_ext_select" "k_ext_stats" "k_ext_fix_rows" "k_dev_sum" \
         "k_rdev_codes" "k_ext_gate" "k_special_scan" "k_scatter_keys" "k_select<" "k_select1<" "k_big_sel" || exit $?
 else
