@@ -71,9 +71,8 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
                                                 uint64_t* __restrict__ partial, uint64_t* __restrict__ out,
                                                 const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat,
                                                 const uint32_t* __restrict__ order) {
-    const GridBlock b = xcd_block();  // whole record chunks per XCD (kg_eval.h)
-    const uint32_t j = b.x * blockDim.x + threadIdx.x;
-    const uint32_t c = b.y;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t c = blockIdx.y;
     const bool live = j < n_lanes;
     const uint32_t row = live ? (order ? order[j] : j) : 0u;
     const PodV p = load_pod(pods, row);
