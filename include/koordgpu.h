@@ -347,7 +347,8 @@ typedef struct kg_node_columns {
      * :150-275; all may be NULL = no tree, no partition table, Prefer policy):
      * dev_topo[i]: byte m = GPU minor m's place in the topology tree (GetGPUTopologyScope): high nibble the
      *   rank of its NUMA node id (numeric order), low nibble the rank of its (NUMA node, PCIe id) pair
-     *   (PCIe ids in string order within a NUMA node); KG_GPU_NO_SCOPE = the minor is in no NUMA / PCIe scope;
+     *   (PCIe ids in string order within a NUMA node); each rank < 8 (the device reads 3 bits of each nibble;
+     *   more than 8 NUMA nodes or pairs is unsupported); KG_GPU_NO_SCOPE = the minor is in no NUMA / PCIe scope;
      * dev_part[i]: bits 0-7 = 1 + the node's partition table in gpu_parts (0 = none: GetGPUPartitionIndexer of
      *   the Device annotation, else the designated table of the node's GPU model), KG_GPU_HONOR = the
      *   GPUPartitionPolicy label is Honor, KG_GPU_TREE = the node has a topology tree (every GPU DeviceInfo

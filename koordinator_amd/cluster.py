@@ -761,6 +761,31 @@ LABEL_RESERVATION_ORDER = "scheduling.koordinator.sh/reservation-order"
 RSV_VEC = (CPU, MEMORY, "ephemeral-storage")  # KG_RSV_R order: cpu, memory, ephemeral-storage, scalar0, scalar1
 
 
+ANN_RESERVATION_RESTRICTED_OPTIONS = "scheduling.koordinator.sh/reservation-restricted-options"
+
+
+def restricted_resources(names: List[str], annotations: Dict[str, str]) -> List[str]:
+    """NewReservationInfo's ResourceNames of a Restricted reservation (frameworkext/reservation_info.go:92-107):
+    the allocatable names intersected with the restricted-options annotation's resources
+    (GetReservationRestrictedResources, util/reservation/reservation.go:677-694), all names when the
+    intersection is empty; an annotation that does not parse (apis/extension/reservation.go:199-207) leaves the
+    names as they are."""
+    raw = annotations.get(ANN_RESERVATION_RESTRICTED_OPTIONS, "")
+    if not raw:
+        return names
+    try:
+        opts = json.loads(raw)
+    except ValueError:
+        return names
+    if not isinstance(opts, dict):
+        return names
+    want = opts.get("resources") or []
+    if not isinstance(want, list):
+        return names
+    out = [n for n in names if n in want]
+    return out or names
+
+
 class ReservationInfo:
     """frameworkext.ReservationInfo of a Reservation object: Allocatable (status), ResourceNames (its keys),
     Allocated = Σ Mask(requests, ResourceNames) of the assigned pods, the owners / policy / order the restore and
@@ -779,11 +804,13 @@ class ReservationInfo:
         self.node = status.get("nodeName", "")
         self.phase = status.get("phase", "")
         alloc = status.get("allocatable") or {}
-        self.names = [k for k in alloc]
         self.allocatable = self._vec(alloc)
         self.max_pods = value(alloc["pods"]) if "pods" in alloc else -1
         self.policy = {"Aligned": abi.KG_RSV_ALIGNED, "Restricted": abi.KG_RSV_RESTRICTED}.get(
             spec.get("allocatePolicy", ""), abi.KG_RSV_DEFAULT)
+        self.names = sorted(alloc)
+        if self.policy == abi.KG_RSV_RESTRICTED:
+            self.names = restricted_resources(self.names, md.get("annotations") or {})
         self.allocate_once = spec.get("allocateOnce", True) is not False
         self.terminating = md.get("deletionTimestamp") is not None
         try:
@@ -964,9 +991,15 @@ class QuotaCache:
         self.generation += 1
 
     def on_quota_delete(self, name: str):
+        """OnQuotaDelete (quota_handler.go:102-133): the quota info goes with its used; its pods migrate to the
+        default quota group, which this flat cache does not hold, so they leave the cache. A quota re-created
+        under the same name starts from zero used, as the reference's new QuotaInfo does; its pods count again
+        from their next OnPodAdd / OnPodUpdate (masked by the names current then, group_quota_manager.go:752)."""
         i = self.index.get(name)
         if i is not None:
             self.max[i] = None
+            for uid in [u for u, ent in self.pods.items() if ent[0] == i]:
+                del self.pods[uid]
             self.generation += 1
 
     def _quota_of(self, pod) -> Optional[int]:

@@ -846,12 +846,11 @@ static kg_status upload_gpu_parts(kg_snap* s, const kg_node_columns* cols) {
     HIP_TRY(ctx, hipMemcpyAsync(s->d_part_rng, rng.data(), sizeof(uint32_t) * rng.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_binpack, bp.data(), sizeof(int64_t) * bp.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // the staging vectors go out of scope
+    // fixed capacity, so the pointer a captured replay graph holds never changes (only the contents do)
+    if (!s->d_parts) HIP_TRY(ctx, hipMalloc(&s->d_parts, sizeof(kg_gpu_partition) * KG_GPU_MAX_PARTS));
     if (n) {
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        hipFree(s->d_parts);
-        s->d_parts = nullptr;
-        HIP_TRY(ctx, hipMalloc(&s->d_parts, sizeof(kg_gpu_partition) * n));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_parts, cols->gpu_parts, sizeof(kg_gpu_partition) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     s->n_gpu_tables = tables;
     if (n) s->n_gpu_parts = n;
@@ -1294,6 +1293,8 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             return fail(ctx, KG_INVALID_ARG, "pod %u: KG_GPU_POD_RING_BW without dev_ring_bw", j);
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
+    // the side stream's plain-pod select of the previous batch reads d_in: it has to finish before the copy
+    if (ctx->side) HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
     // the previous upload's copy has completed (every upload ends with a stream synchronisation), so the
     // pinned staging can be rewritten
     const PodLayout L = pod_layout(n);
@@ -1459,6 +1460,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     if (!p) return KG_INVALID_ARG;
     hipSetDevice(p->ctx->device);
     hipStreamSynchronize(p->ctx->stream);
+    if (p->ctx->side) hipStreamSynchronize(p->ctx->side);  // a plain-pod select may still read the batch there
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
                     (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
                     (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
@@ -1869,10 +1871,20 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
         // the plain pods' fused select depends on nothing the config-5 kernels build: it runs on the side stream
         // from the fork (after the quota gate has written every pod's status) and joins before the scatters
         const bool side = plain_side_ok(s, p, kk) && !std::getenv("KG_NO_SIDE_STREAM");
+        // every return after the fork joins the side stream back into ctx->stream, so nothing later on
+        // ctx->stream (an upload into d_in, a free) overtakes the side kernel
+        struct SideJoin {
+            kg_ctx* ctx;
+            bool on = false;
+            ~SideJoin() {
+                if (on) hipStreamWaitEvent(ctx->stream, ctx->join, 0);
+            }
+        } join{ctx};
         if (side) {
             st0 = ext_gate_local(s, p);
             if (st0 != KG_OK) return st0;
             st0 = launch_plain_side(s, p, kk, d_out);
+            join.on = ctx->join != nullptr;
             if (st0 != KG_OK) return st0;
         }
         st0 = ext_stats_local(s, p, side);
@@ -2105,9 +2117,20 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     kg_ctx* ctx = s->ctx;
     std::vector<uint8_t> key = replay_key(s, p, exact, reasons);
     auto put = [&key](const void* x, size_t n) { key.insert(key.end(), (const uint8_t*)x, (const uint8_t*)x + n); };
-    put(&s->d_dev, sizeof(s->d_dev));
-    put(&s->d_qstate, sizeof(s->d_qstate));
-    put(&s->n_quotas, sizeof(s->n_quotas));
+    // every ExtDev field the captured launches take by value (tables re-uploaded in place keep their pointers)
+    const ExtDev e = s->ext_dev();
+    put(&e.dev, sizeof(e.dev));
+    put(&e.qlim, sizeof(e.qlim));
+    put(&e.qstate, sizeof(e.qstate));
+    put(&e.n_quotas, sizeof(e.n_quotas));
+    put(&e.views, sizeof(e.views));
+    put(&e.infos, sizeof(e.infos));
+    put(&e.cls_begin, sizeof(e.cls_begin));
+    put(&e.rdev, sizeof(e.rdev));
+    put(&e.parts, sizeof(e.parts));
+    put(&e.n_parts, sizeof(e.n_parts));
+    put(&e.part_rng, sizeof(e.part_rng));
+    put(&e.binpack, sizeof(e.binpack));
     if (p->xexec && key == p->xkey) return KG_OK;
     if (p->xexec) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -2115,7 +2138,6 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
         p->xexec = nullptr;
     }
     hipGraph_t graph = nullptr;
-    const ExtDev e = s->ext_dev();
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
     hipError_t err = hipSuccess;
     for (uint32_t t = 0; t < REPLAY_G && err == hipSuccess; t++)

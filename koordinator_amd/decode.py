@@ -1311,8 +1311,9 @@ def gpu_topology(gpu_infos: Sequence[dict]) -> Tuple[int, bool]:
         return (1 << 64) - 1, False
     numa_ids = sorted({int(d["topology"].get("nodeID", 0)) for d in gpu_infos})
     pairs = sorted({(int(d["topology"].get("nodeID", 0)), str(d["topology"].get("pcieID", ""))) for d in gpu_infos})
-    if len(numa_ids) > 15 or len(pairs) > 16:
-        raise Unsupported("GPU topology with more than 15 NUMA nodes or 16 PCIe switches")
+    # the device decodes each rank with 3 bits into DEV_MINORS-entry tables (kg_ext.h gpu_scope)
+    if len(numa_ids) > abi.KG_DEV_MINORS or len(pairs) > abi.KG_DEV_MINORS:
+        raise Unsupported(f"GPU topology with more than {abi.KG_DEV_MINORS} NUMA nodes or PCIe switches")
     topo = (1 << 64) - 1
     for d in gpu_infos:
         m = int(d.get("minor", 0))

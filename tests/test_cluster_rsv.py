@@ -110,3 +110,38 @@ def test_quota_events():
     assert st.quotas.columns()["limit_keys"][0] == 0b01
     st.on_quota_delete("q1")
     assert st.quotas.columns()["limit_keys"][0] == 0
+
+
+def test_restricted_resources_kat():
+    """TestGetReservationRestrictedResources (util/reservation/reservation_test.go:997-1042), through the
+    annotation NewReservationInfo reads (frameworkext/reservation_info.go:99-106)."""
+    from koordinator_amd.cluster import ANN_RESERVATION_RESTRICTED_OPTIONS, restricted_resources
+    names = ["cpu", "memory"]
+    cases = [(None, ["cpu", "memory"]), (["cpu", "memory"], ["cpu", "memory"]), (["cpu"], ["cpu"]), ([], ["cpu", "memory"])]
+    for opt, want in cases:
+        ann = {} if opt is None else {ANN_RESERVATION_RESTRICTED_OPTIONS: json.dumps({"resources": opt})}
+        assert restricted_resources(names, ann) == want
+    # an annotation that does not parse keeps every name (the parse error is recorded, names unchanged)
+    assert restricted_resources(names, {ANN_RESERVATION_RESTRICTED_OPTIONS: "{bad"}) == names
+
+
+def test_restricted_reservation_masks_allocated():
+    """A Restricted reservation restricted to cpu: Allocated = Mask(requests, [cpu]) and the restore's names
+    bitmask carries cpu only (reservation_info.go:92-107)."""
+    from koordinator_amd.cluster import ANN_RESERVATION_RESTRICTED_OPTIONS
+    st = _state()
+    r = _rsv("r3", "n0", allocate_once=False)
+    r["spec"]["allocatePolicy"] = "Restricted"
+    r["metadata"]["annotations"] = {ANN_RESERVATION_RESTRICTED_OPTIONS: json.dumps({"resources": ["cpu"]})}
+    st.on_reservation(r)
+    ri = st.reservations.infos["r3"]
+    assert ri.names == ["cpu"]
+    st.on_pod_add(_pod("p-in", node="n0", cpu="1", mem="2Gi", labels={"app": "a"}, rsv="r3"))
+    assert ri.allocated[0] == 1000 and ri.allocated[1] == 0
+    _, _, rsv = st.reservation_restore([_pod("p-a", labels={"app": "a"})])
+    assert rsv.n_views == 1
+    # the plain variant (no annotation) keeps both names
+    r2 = _rsv("r4", "n1", allocate_once=False)
+    r2["spec"]["allocatePolicy"] = "Restricted"
+    st.on_reservation(r2)
+    assert st.reservations.infos["r4"].names == ["cpu", "memory"]
