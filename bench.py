@@ -320,7 +320,7 @@ def main():
     ctx = engine.Context(local)
     quotas = rsv = None
     if config == 5:
-        cfg, nodes, pods, quotas, rsv = synth.cluster5(100_000, 10_000)
+        cfg, nodes, pods, quotas, rsv = synth.config5()
     elif config == 6:
         cfg, nodes, pods = synth.mixed()
     else:

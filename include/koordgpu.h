@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 7
+#define KG_ABI_VERSION 9
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -118,7 +118,9 @@ typedef enum kg_status {
 #define KG_GPU_POD_RING_BW 0x8u     /* GPUPartitionSpec RingBusBandwidth set (kg_pod_columns.dev_ring_bw)          */
 #define KG_GPU_POD_SCOPE_SHIFT 4    /* 3 bits: DeviceTopologyScopeLevel of the required scope (0 none, 2 NUMANode,
                                      * 3 PCIe, 4 Device; apis/extension/device_share.go:185-190)               */
-#define KG_GPU_POD_TEMPLATE 0x100u  /* enforceGPUSharedResourceTemplate: not on the device path (KG_ST_UNSUPPORTED) */
+#define KG_GPU_POD_TEMPLATE 0x100u  /* enforceGPUSharedResourceTemplate (deviceshare/utils.go:540-547): the
+                                     * allocator starts at allocateByTemplate (allocator_gpu.go:135-159), per
+                                     * node key kg_pod_columns.dev_tmpl                                        */
 
 /* Reservation allocate policies (apis/scheduling/v1alpha1 ReservationAllocatePolicy). */
 #define KG_RSV_DEFAULT 0u
@@ -173,6 +175,9 @@ typedef enum kg_status {
 #define KG_DEV_CODE_PART_COUNT 7u        /* ErrUnsupportedGPURequests: no partition of that GPU count (honored)  */
 #define KG_DEV_CODE_NO_TREE 8u           /* ErrNodeMissingGPUDeviceTopologyTree (required topology scope)        */
 #define KG_DEV_CODE_MULTI_SHARED 9u      /* ErrUnsupportedMultiSharedGPU (required topology scope)               */
+#define KG_DEV_CODE_NUMA_SCOPED 10u      /* ErrInsufficientNUMAScopedDevices (topology_hint.go:34): the NUMA hint
+                                            provider found fewer GPUs in a NUMA mask than requested             */
+#define KG_DEV_CODE_NO_TEMPLATE 11u      /* ErrNoMatchedGPUSharedResourceTemplate (allocator_gpu.go:40,142-143)  */
 #define KG_ST_RSV_AFFINITY 0x04000000u     /* ErrReasonReservationAffinity (reservation/plugin.go:366-368)  */
 #define KG_ST_RSV_NODE 0x08000000u         /* "Insufficient <r> by node" (reservation/plugin.go:498-525)    */
 #define KG_ST_RSV_RESERVATION 0x10000000u  /* reservation-level reasons / no reservation meets the pod      */
@@ -280,6 +285,8 @@ typedef struct kg_cpuset_request {
 #define KG_GPU_NO_SCOPE 0xFFu
 #define KG_GPU_HONOR 0x100u
 #define KG_GPU_TREE 0x200u
+#define KG_GPU_TMPL_SHIFT 12 /* dev_part bits 12-15: the node's shared-resource template key (KG_GPU_TMPL_NONE = none) */
+#define KG_GPU_TMPL_NONE 15u
 #define KG_GPU_MAX_TABLES 16
 #define KG_GPU_MAX_PARTS 1024
 typedef struct kg_gpu_partition {
@@ -352,14 +359,25 @@ typedef struct kg_node_columns {
      * dev_part[i]: bits 0-7 = 1 + the node's partition table in gpu_parts (0 = none: GetGPUPartitionIndexer of
      *   the Device annotation, else the designated table of the node's GPU model), KG_GPU_HONOR = the
      *   GPUPartitionPolicy label is Honor, KG_GPU_TREE = the node has a topology tree (every GPU DeviceInfo
-     *   carries a Topology);
+     *   carries a Topology), bits 12-15 (KG_GPU_TMPL_SHIFT) = the index of the node's GPU shared-resource
+     *   template key buildGPUSharedResourceTemplatesKey(vendor, model) among the configured keys, or
+     *   KG_GPU_TMPL_NONE when the configuration holds no templates for that key;
      * gpu_parts: every partition of every table (kg_gpu_partition), grouped by table, then GPU count, then
      *   AllocationScore ascending; within a group in the table's order (GetGPUPartitionIndexer). */
     const uint64_t* dev_topo;
     const uint32_t* dev_part;
     const struct kg_gpu_partition* gpu_parts;
     uint32_t n_gpu_parts;
+    /* DeviceShare NUMA topology (deviceshare/numa_topology.go:43-100, NUMATopology.deviceToNodeID; NULL = every
+     * minor without a topology): nibble m of dev_numa[i] = GPU minor m's NUMA node id (0..7, the NRT zone of that
+     * id), KG_GPU_NUMA_ANY = its Topology.NodeID is -1 (in every NUMA mask, in no NUMA scope), KG_GPU_NUMA_NONE =
+     * no Topology (left out whenever a NUMA affinity restricts the allocation, device_allocator.go:155-159).
+     * GPU pods on nodes whose NUMA policy is not None join the topology manager's hint merge with these
+     * (deviceshare/topology_hint.go:40-290). */
+    const uint32_t* dev_numa;
 } kg_node_columns;
+#define KG_GPU_NUMA_ANY 0xEu
+#define KG_GPU_NUMA_NONE 0xFu
 
 /* Mutable node state that Assume/Forget change; used to read a snapshot back after kg_replay. */
 typedef struct kg_node_state {
@@ -399,6 +417,11 @@ typedef struct kg_pod_columns {
      * the GPUPartitionSpec RingBusBandwidth in bytes (read when KG_GPU_POD_RING_BW is set). */
     const uint32_t* dev_flags;
     const int64_t* dev_ring_bw;
+    /* candidateGPUSharedResourceTemplates of a KG_GPU_POD_TEMPLATE pod (deviceshare/utils.go:540-547,
+     * gpu_shared_resource_templates_cache.go:41-62): 2 bits per template key k < KG_GPU_TMPL_NONE (the node's
+     * key in dev_part bits 12-15) = how many templates of key k the pod's requestsPerGPU matched: 0 none, 1 one,
+     * 2 several. NULL = no template pods. */
+    const uint32_t* dev_tmpl;
 } kg_pod_columns;
 
 /* Verify-mode outputs, [n_pods][n_nodes] row-major, caller-allocated host buffers (NULL = skip). */
@@ -410,7 +433,11 @@ typedef struct kg_verify_out {
     int64_t* total;       /* Σ weight·score, -1 when infeasible                             */
     int8_t* numa_zone;    /* NUMA allocation the Reserve would make: -1 none, 0..3 one zone,
                              0x40 | zone mask for a split over several zones, 0x20 | bits when
-                             the Reserve fails (BestEffort: bits = KG_ST_NUMA_INSUF_* >> 12) */
+                             the Reserve fails (BestEffort: bits = KG_ST_NUMA_INSUF_* >> 12,
+                             0x08 the cpuset take), 0x30 | KG_DEV_CODE_* when the GPU allocation
+                             under the Reserve's NUMA affinity fails (a GPU pod on a BestEffort node).
+                             A GPU pod's Reserve allocates its minors inside the NUMA nodes of this
+                             affinity (deviceshare/plugin.go:585-600) */
     int64_t* score_dev;   /* DeviceShare Score before NormalizeScore (0 when infeasible)    */
     int64_t* score_rsv;   /* Reservation Score before NormalizeScore (1000 on the preferred
                              node, reservation/scoring.go:40,191-198; 0 when infeasible)     */

@@ -11,7 +11,7 @@ from typing import Dict
 
 import numpy as np
 
-KG_ABI_VERSION = 7
+KG_ABI_VERSION = 9
 KG_LA_R = 2
 KG_NSCALAR = 2
 KG_MAX_ZONES = 4
@@ -89,6 +89,8 @@ KG_ST_DEV_MASK = 0x030000C0  # 4-bit reason code: bits 24-25 low half, bits 6-7 
 KG_DEV_CODE_INSUFFICIENT, KG_DEV_CODE_NO_DEVICE, KG_DEV_CODE_GPU_DEVICES, KG_DEV_CODE_TOPO_SCOPED = 1, 2, 3, 4
 KG_DEV_CODE_PARTITIONED, KG_DEV_CODE_NO_PARTITION, KG_DEV_CODE_PART_COUNT, KG_DEV_CODE_NO_TREE = 5, 6, 7, 8
 KG_DEV_CODE_MULTI_SHARED = 9
+KG_DEV_CODE_NUMA_SCOPED = 10  # ErrInsufficientNUMAScopedDevices (deviceshare/topology_hint.go:34)
+KG_DEV_CODE_NO_TEMPLATE = 11  # ErrNoMatchedGPUSharedResourceTemplate (deviceshare/allocator_gpu.go:40)
 
 
 def dev_code(st: int) -> int:
@@ -103,8 +105,13 @@ def dev_status(code: int) -> int:
 
 # GPU topology / partitions (kg_node_columns.dev_topo / dev_part / gpu_parts, kg_pod_columns.dev_flags)
 KG_GPU_NO_SCOPE = 0xFF
+# kg_node_columns.dev_numa: a nibble per minor, the GPU's NUMA node id (deviceshare/numa_topology.go:43-100)
+KG_GPU_NUMA_ANY = 0xE   # Topology.NodeID == -1
+KG_GPU_NUMA_NONE = 0xF  # no Topology
 KG_GPU_HONOR = 0x100
 KG_GPU_TREE = 0x200
+KG_GPU_TMPL_SHIFT = 12  # dev_part bits 12-15: the node's shared-resource template key
+KG_GPU_TMPL_NONE = 15
 KG_GPU_MAX_TABLES = 16
 KG_GPU_POD_SHARED = 0x1
 KG_GPU_POD_HONOR = 0x2
@@ -194,6 +201,8 @@ class KgNodeColumns(C.Structure):
         ("cpu_strategy", C.POINTER(C.c_uint8)),
         # GPU topology tree / partition tables
         ("dev_topo", C.POINTER(C.c_uint64)), ("dev_part", _pu32), ("gpu_parts", C.c_void_p), ("n_gpu_parts", C.c_uint32),
+        # GPU NUMA node ids (DeviceShare as a NUMA hint provider)
+        ("dev_numa", _pu32),
     ]
 
 
@@ -222,7 +231,7 @@ class KgPodColumns(C.Structure):
         ("dev_req", _p64), ("dev_count", _pu32), ("dev_keys", _pu32),
         ("quota", _pi32), ("quota_keys", _pu32),
         ("rsv_class", _pi32),
-        ("dev_flags", _pu32), ("dev_ring_bw", _p64),
+        ("dev_flags", _pu32), ("dev_ring_bw", _p64), ("dev_tmpl", _pu32),
     ]
 
 
@@ -366,7 +375,8 @@ NODE_STATE = (
 POD_I64 = (["req_cpu", "req_mem", "req_eph"] + _indexed("sc_req", KG_NSCALAR) + ["nz_cpu", "nz_mem"]
            + _indexed("la_est", KG_LA_R))
 POD_U32 = ["flags", "numa_policy", "dev_count", "dev_keys", "quota_keys"]
-# optional GPURequirements columns (absent: no partition / topology requirement): dev_flags uint32, dev_ring_bw int64
+# optional GPURequirements columns (absent: no partition / topology requirement / template): dev_flags uint32,
+# dev_ring_bw int64, dev_tmpl uint32 (2 bits per template key: candidate templates 0 / 1 / several)
 POD_I32 = ["quota", "rsv_class"]
 
 Table = Dict[str, np.ndarray]
@@ -473,6 +483,9 @@ def node_columns(t: Table) -> KgNodeColumns:
     if "dev_part" in t:
         t["dev_part"] = np.ascontiguousarray(t["dev_part"], np.uint32)
         s.dev_part = _ptr(t["dev_part"], C.c_uint32)
+    if "dev_numa" in t:
+        t["dev_numa"] = np.ascontiguousarray(t["dev_numa"], np.uint32)
+        s.dev_numa = _ptr(t["dev_numa"], C.c_uint32)
     if "gpu_parts" in t and len(t["gpu_parts"]):
         t["gpu_parts"] = np.ascontiguousarray(t["gpu_parts"], GPU_PARTITION_DTYPE)
         s.gpu_parts = t["gpu_parts"].ctypes.data
@@ -529,13 +542,14 @@ def pod_columns(t: Table) -> KgPodColumns:
     s.flags = _ptr(t["flags"], C.c_uint32)
     s.numa_policy = _ptr(t["numa_policy"], C.c_uint32)
     # config-5 columns are optional, each on its own (absent: no GPU request / quota / reservation class)
-    _check(t, [k for k in POD_U32 + ["dev_flags"] if k in t], np.uint32)
+    _check(t, [k for k in POD_U32 + ["dev_flags", "dev_tmpl"] if k in t], np.uint32)
     _check(t, [k for k in POD_I32 if k in t], np.int32)
     if "dev_req" in t:
         t["dev_req"] = np.ascontiguousarray(t["dev_req"], np.int64)
         s.dev_req = _ptr(t["dev_req"], C.c_int64)
     for k, ct in (("dev_count", C.c_uint32), ("dev_keys", C.c_uint32), ("quota", C.c_int32),
-                  ("quota_keys", C.c_uint32), ("rsv_class", C.c_int32), ("dev_flags", C.c_uint32)):
+                  ("quota_keys", C.c_uint32), ("rsv_class", C.c_int32), ("dev_flags", C.c_uint32),
+                  ("dev_tmpl", C.c_uint32)):
         if k in t:
             setattr(s, k, _ptr(t[k], ct))
     if "dev_ring_bw" in t:

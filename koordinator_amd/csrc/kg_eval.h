@@ -265,16 +265,16 @@ __device__ __forceinline__ bool numa_excl_ok(uint32_t mask, uint32_t status) {
 }
 
 // mergePermutation + the bestHint update of mergeFilteredHints (policy.go:98-137,198-260) for a
-// permutation of np = 0, 1 or 2 hints (a, b)
+// permutation of np = 0..3 hints (a, b, c3)
 __device__ __forceinline__ void numa_merge_perm(uint32_t all, bool excl, uint32_t status, int np, const NumaHint& a,
-                                                const NumaHint& b, NumaHint& best) {
+                                                const NumaHint& b, NumaHint& best, const NumaHint& c3 = NumaHint{0u, true, false, 0}) {
     uint32_t merged = all, first = 0;
     bool pref = true, unsat = false;
     int naff = 0, maxc = 0;
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
+    for (int t = 0; t < 3; t++) {
         if (t >= np) break;
-        const NumaHint& v = t == 0 ? a : b;
+        const NumaHint& v = t == 0 ? a : t == 1 ? b : c3;
         if (v.mask) {
             if (naff == 0) first = v.mask;
             else if (v.mask != first) pref = false;
@@ -291,6 +291,7 @@ __device__ __forceinline__ void numa_merge_perm(uint32_t all, bool excl, uint32_
     int64_t score = 0;
     if (np >= 1 && a.mask && a.mask == merged) score += a.score;
     if (np >= 2 && b.mask && b.mask == merged) score += b.score;
+    if (np >= 3 && c3.mask && c3.mask == merged) score += c3.score;
     const NumaHint m{merged, pref, !satisfied, score};
     if (m.pref && !best.pref) {
         best = m;
@@ -308,6 +309,20 @@ __device__ __forceinline__ void numa_merge_perm(uint32_t all, bool excl, uint32_
 
 constexpr uint32_t NUMA_NIL_K = 15u;  // hint-list bit of the unsatisfied nil hint (filterProvidersHints)
 
+// DeviceShare's "gpu" hint list for the merge (deviceshare/topology_hint.go:159-280): entry t has the NUMA mask
+// nibble t of `masks`, Preferred bit t of `pref`, Score 500 when bit t of `s500`; `set` holds the entries
+// (after filterSingleNumaHints), NUMA_NIL_K = the provider's "no preference" hint (nil affinity, Preferred).
+struct GpuHints {
+    uint64_t masks;
+    uint32_t set, pref, s500;
+};
+
+__device__ __forceinline__ NumaHint gpu_hint_at(const GpuHints& g, uint32_t t) {
+    if (t == NUMA_NIL_K) return NumaHint{0u, true, false, 0};
+    return NumaHint{(uint32_t)(g.masks >> (4 * t)) & 15u, ((g.pref >> t) & 1u) != 0, false,
+                    ((g.s500 >> t) & 1u) ? 500 : 0};
+}
+
 __device__ __forceinline__ NumaHint numa_hint_at(uint64_t nib, uint32_t k, uint32_t pref_bits, uint64_t sc_lo, uint64_t sc_hi) {
     if (k == NUMA_NIL_K) return NumaHint{0u, false, true, 0};
     const uint32_t m = (uint32_t)(nib >> (4 * k)) & 15u;
@@ -315,10 +330,12 @@ __device__ __forceinline__ NumaHint numa_hint_at(uint64_t nib, uint32_t k, uint3
     return NumaHint{m, ((pref_bits >> k) & 1u) != 0, false, (int64_t)(sc & 0xFFu)};
 }
 
-// Policy merge: 0 = admitted with affinity `mask` (0 = none), else a KG_ST_NUMA_* reason.
-template <bool EXACT>
+// Policy merge: 0 = admitted with affinity `mask` (0 = none), else a KG_ST_NUMA_* reason. GPU: a third hint list,
+// DeviceShare's (gh, provider order: NodeNUMAResource's cpu, memory, then DeviceShare's gpu).
+template <bool EXACT, bool GPU = false>
 __device__ __forceinline__ uint32_t numa_admit(const KCfg& c, const NumaZ& x, const int64_t* req, const bool* has,
-                                              uint32_t policy, bool excl, uint32_t& mask_out) {
+                                              uint32_t policy, bool excl, uint32_t& mask_out,
+                                              const GpuHints* gh = nullptr) {
     const uint32_t Z = x.Z;
     const uint64_t nib = numa_mask_nib(Z);
     const uint32_t nm = (1u << Z) - 1u;
@@ -388,7 +405,39 @@ __device__ __forceinline__ uint32_t numa_admit(const KCfg& c, const NumaZ& x, co
     NumaHint best{all, false, false, 0};
     const NumaHint none{0u, false, false, 0};
     const int nl = (has[0] ? 1 : 0) + (has[1] ? 1 : 0);
-    if (nl == 0) {
+    if constexpr (GPU) {
+        // iterateAllProviderTopologyHints over [cpu,] [memory,] gpu (policy.go:262-299)
+        uint32_t G = gh->set;
+        if (policy == KG_NUMA_SINGLE_NODE) {  // filterSingleNumaHints on the gpu list
+            uint32_t keep = 0;
+            for (uint32_t l = G; l; l &= l - 1u) {
+                const uint32_t t = (uint32_t)(__ffs(l) - 1);
+                const NumaHint h = gpu_hint_at(*gh, t);
+                keep |= (h.pref && (h.mask == 0u || popc(h.mask) == 1)) ? 1u << t : 0u;
+            }
+            G = keep;
+        }
+        const uint32_t S0 = has[0] ? L0 : L1, P0 = has[0] ? pref0 : pref1;  // the first NUMA list present
+        if (nl == 0) {
+            for (uint32_t lc = G; lc; lc &= lc - 1u)
+                numa_merge_perm(all, excl, x.status, 1, gpu_hint_at(*gh, (uint32_t)(__ffs(lc) - 1)), none, best);
+        } else if (nl == 1) {
+            for (uint32_t la = S0; la; la &= la - 1u) {
+                const NumaHint ha = numa_hint_at(nib, (uint32_t)(__ffs(la) - 1), P0, sc_lo, sc_hi);
+                for (uint32_t lc = G; lc; lc &= lc - 1u)
+                    numa_merge_perm(all, excl, x.status, 2, ha, gpu_hint_at(*gh, (uint32_t)(__ffs(lc) - 1)), best);
+            }
+        } else {
+            for (uint32_t la = L0; la; la &= la - 1u) {
+                const NumaHint ha = numa_hint_at(nib, (uint32_t)(__ffs(la) - 1), pref0, sc_lo, sc_hi);
+                for (uint32_t lb = L1; lb; lb &= lb - 1u) {
+                    const NumaHint hb = numa_hint_at(nib, (uint32_t)(__ffs(lb) - 1), pref1, sc_lo, sc_hi);
+                    for (uint32_t lc = G; lc; lc &= lc - 1u)
+                        numa_merge_perm(all, excl, x.status, 3, ha, hb, best, gpu_hint_at(*gh, (uint32_t)(__ffs(lc) - 1)));
+                }
+            }
+        }
+    } else if (nl == 0) {
         numa_merge_perm(all, excl, x.status, 0, none, none, best);
     } else if (nl == 1) {
         const uint32_t L = has[0] ? L0 : L1, P = has[0] ? pref0 : pref1;

@@ -18,6 +18,7 @@ struct PodX {
     uint32_t qkeys;
     int32_t cls;
     uint32_t dflags;  // KG_GPU_POD_*
+    uint32_t dtmpl;   // candidate template counts per node key (KG_GPU_POD_TEMPLATE)
     int64_t dbw;      // ring bus bandwidth request (KG_GPU_POD_RING_BW)
 };
 
@@ -27,6 +28,7 @@ __device__ __forceinline__ PodX load_podx(const PodsDev& P, uint32_t j) {
     x.dkeys = P.dev_keys ? P.dev_keys[j] : 0u;
     x.dflags = (P.dev_flags && x.dcount) ? P.dev_flags[j] : 0u;
     x.dbw = (P.dev_bw && (x.dflags & KG_GPU_POD_RING_BW)) ? P.dev_bw[j] : 0;
+    x.dtmpl = (P.dev_tmpl && (x.dflags & KG_GPU_POD_TEMPLATE)) ? P.dev_tmpl[j] : 0u;
     for (int r = 0; r < DEV_R; r++) x.dreq[r] = (P.dev_req && ((x.dkeys >> r) & 1u)) ? P.dev_req[(size_t)j * DEV_R + r] : 0;
     x.quota = P.quota ? P.quota[j] : -1;
     x.qkeys = P.quota_keys ? P.quota_keys[j] : 0u;
@@ -67,8 +69,8 @@ __device__ __forceinline__ bool dev_minor_fits(const int64_t* fr, const PodX& x)
 
 // ---- GPU allocator (GPUAllocator.Allocate, deviceshare/allocator_gpu.go:72-133) ------------------------
 // Order of the reference: a partition table (allocateByPartition :177-237), then the topology tree
-// (allocateByDeviceTopology :312-451), then defaultAllocateDevices (device_allocator.go:355-437). Shared
-// resource templates (:135-159) are not on the device path (KG_GPU_POD_TEMPLATE -> KG_ST_UNSUPPORTED).
+// (allocateByDeviceTopology :312-451), then defaultAllocateDevices (device_allocator.go:355-437), behind
+// allocateByTemplate (:135-159) for a pod that enforces a shared-resource template (gpu_template).
 
 struct GpuAlloc {
     uint32_t code;  // KG_DEV_CODE_* (0 = allocated)
@@ -86,7 +88,10 @@ struct GpuMinors {
     uint32_t used, total, sat, fit;
 };
 
-__device__ __forceinline__ GpuMinors gpu_minors(const DevRec* __restrict__ d, int32_t D, const PodX& x, uint32_t outside) {
+// allowed: the minors a NUMA affinity keeps (nodeDevice.filter, device_cache.go:367-415): the others leave the
+// total, the satisfied and the fitting sets, and count as used outside the table (getRealUsed).
+__device__ __forceinline__ GpuMinors gpu_minors(const DevRec* __restrict__ d, int32_t D, const PodX& x, uint32_t outside,
+                                                uint32_t allowed = ~0u) {
     GpuMinors g{outside, 0u, 0u, 0u};
     for (int32_t m = 0; m < D; m++) {
         bool any_t = false, diff = false, le = true, any_f = false;
@@ -103,6 +108,10 @@ __device__ __forceinline__ GpuMinors gpu_minors(const DevRec* __restrict__ d, in
         g.sat |= (any_t && le) ? 1u << m : 0u;
         g.fit |= (any_f && le) ? 1u << m : 0u;
     }
+    g.used = (g.used & allowed) | outside;
+    g.total &= allowed;
+    g.sat &= allowed;
+    g.fit &= allowed;
     return g;
 }
 
@@ -306,11 +315,11 @@ __device__ __forceinline__ bool gpu_scope_fits(int32_t D, uint64_t topo, uint32_
 // numberOfGPUs whose free resources are not all zero and cover the request. want_mask = false: only whether
 // enough minors fit (the Filter).
 __device__ __forceinline__ GpuAlloc dev_default(const KCfg& c, const DevRec* __restrict__ d, int32_t D, const PodX& x,
-                                                bool want_mask) {
+                                                bool want_mask, uint32_t allowed = ~0u) {
     uint32_t fit = 0;
     for (int32_t m = 0; m < D; m++) {
         const int64_t fr[DEV_R] = {d->free_[0][m], d->free_[1][m], d->free_[2][m]};
-        fit += dev_minor_fits(fr, x) ? 1u : 0u;
+        fit += (((allowed >> m) & 1u) && dev_minor_fits(fr, x)) ? 1u : 0u;
     }
     if (fit < x.dcount) return {KG_DEV_CODE_INSUFFICIENT, 0u};
     if (!want_mask) return {0u, 0u};
@@ -339,23 +348,36 @@ __device__ __forceinline__ GpuAlloc dev_default(const KCfg& c, const DevRec* __r
     for (int32_t t = 0; t < D && got < x.dcount; t++) {
         const int m = ord[t];
         const int64_t fr[DEV_R] = {d->free_[0][m], d->free_[1][m], d->free_[2][m]};
-        if (!dev_minor_fits(fr, x)) continue;
+        if (!((allowed >> m) & 1u) || !dev_minor_fits(fr, x)) continue;
         mask |= 1u << m;
         got++;
     }
     return {0u, mask};
 }
 
+// allocateByTemplate (allocator_gpu.go:135-159): how many of the pod's candidate templates carry the node's
+// vendor-model key. 0 fails the allocation (KG_DEV_CODE_NO_TEMPLATE), 1 goes straight to generalAllocate (the
+// partition stage is skipped; the template name only annotates the allocation), more fall through. Pods that
+// enforce no template: 2.
+__device__ __forceinline__ uint32_t gpu_template(const PodX& x, uint32_t part) {
+    if (!(x.dflags & KG_GPU_POD_TEMPLATE)) return 2u;
+    const uint32_t key = (part >> KG_GPU_TMPL_SHIFT) & 15u;
+    return key == KG_GPU_TMPL_NONE ? 0u : (x.dtmpl >> (2 * key)) & 3u;
+}
+
 // GPUAllocator.Allocate's outcome (the Filter: no minors chosen) from the table's minor sets.
 __device__ __forceinline__ uint32_t gpu_allocate_code(const ExtDev& e, int32_t D, uint64_t topo, uint32_t part,
                                                       const PodX& x, const GpuMinors& g) {
+    // (g.fit already holds only the allowed minors)
+    const uint32_t tm = gpu_template(x, part);
+    if (tm == 0u) return KG_DEV_CODE_NO_TEMPLATE;
     const bool shared = (x.dflags & KG_GPU_POD_SHARED) != 0;
     const uint32_t sfield = (x.dflags >> KG_GPU_POD_SCOPE_SHIFT) & 7u;
     const bool required = sfield != 0u;
     const int32_t level = sfield > 4u ? 0 : (int32_t)sfield;
     const uint32_t tbl = part & 0xFFu;
     const bool honor = (x.dflags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR);
-    if (!shared && (tbl != 0u || honor)) {
+    if (!shared && tm != 1u && (tbl != 0u || honor)) {
         const uint32_t code = gpu_partition(e, tbl, x, g, false).code;
         if (code == 0u || honor) return code;
     }
@@ -374,8 +396,10 @@ __device__ __forceinline__ uint32_t gpu_allocate_code(const ExtDev& e, int32_t D
 // ZoneRec.dev_topo / dev_part; outside: minors used on the node outside the table (0 for the node's own).
 __device__ __forceinline__ GpuAlloc gpu_allocate(const KCfg& c, const ExtDev& e, const DevRec* __restrict__ d, int32_t D,
                                                  uint64_t topo, uint32_t part, const PodX& x, uint32_t outside,
-                                                 bool want_mask) {
-    if (!want_mask) return {gpu_allocate_code(e, D, topo, part, x, gpu_minors(d, D, x, outside)), 0u};
+                                                 bool want_mask, uint32_t allowed = ~0u) {
+    if (!want_mask) return {gpu_allocate_code(e, D, topo, part, x, gpu_minors(d, D, x, outside, allowed)), 0u};
+    const uint32_t tm = gpu_template(x, part);
+    if (tm == 0u) return {KG_DEV_CODE_NO_TEMPLATE, 0u};
     const bool shared = (x.dflags & KG_GPU_POD_SHARED) != 0;
     const uint32_t sfield = (x.dflags >> KG_GPU_POD_SCOPE_SHIFT) & 7u;
     const bool required = sfield != 0u;
@@ -383,15 +407,15 @@ __device__ __forceinline__ GpuAlloc gpu_allocate(const KCfg& c, const ExtDev& e,
     const bool tree = (part & KG_GPU_TREE) != 0;
     const uint32_t tbl = part & 0xFFu;
     // partitions apply to whole GPUs; a node without table or a non-honored miss falls through
-    if (!shared && (tbl != 0u || (x.dflags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR))) {
-        const GpuMinors g = gpu_minors(d, D, x, outside);
+    if (!shared && tm != 1u && (tbl != 0u || (x.dflags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR))) {
+        const GpuMinors g = gpu_minors(d, D, x, outside, allowed);
         const GpuAlloc pa = gpu_partition(e, tbl, x, g);
         if (pa.code == 0u) return pa;
         if ((x.dflags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR)) return pa;
     }
     if (tree) {
         if (!(shared && x.dcount > 1u)) {
-            const GpuMinors g = gpu_minors(d, D, x, outside);
+            const GpuMinors g = gpu_minors(d, D, x, outside, allowed);
             const uint32_t mask = gpu_scope(c, d, D, topo, x, g, level, shared);
             if (mask) return {0u, mask};
             return {required ? KG_DEV_CODE_TOPO_SCOPED : KG_DEV_CODE_GPU_DEVICES, 0u};
@@ -400,10 +424,82 @@ __device__ __forceinline__ GpuAlloc gpu_allocate(const KCfg& c, const ExtDev& e,
     } else if (required) {
         return {KG_DEV_CODE_NO_TREE, 0u};
     }
-    return dev_default(c, d, D, x, want_mask);
+    return dev_default(c, d, D, x, want_mask, allowed);
 }
 
 __device__ __forceinline__ uint32_t dev_code_status(uint32_t code) { return code ? KG_ST_DEV_MAKE(code) : 0u; }
+
+// ---- DeviceShare under a NUMA affinity (deviceshare/topology_hint.go:40-290, device_allocator.go:143-176) ---------
+
+// the minors filterNodeDevice keeps under NUMA affinity `numa` (bit per zone): a Topology whose NodeID is -1 or in
+// the affinity (device_allocator.go:155-159)
+__device__ __forceinline__ uint32_t gpu_numa_allowed(uint32_t dev_numa, int32_t D, uint32_t numa) {
+    uint32_t a = 0;
+    for (int32_t m = 0; m < D && m < DEV_MINORS; m++) {
+        const uint32_t q = (dev_numa >> (4 * m)) & 15u;
+        a |= (q == KG_GPU_NUMA_ANY || (q < (uint32_t)MAX_ZONES && ((numa >> q) & 1u))) ? 1u << m : 0u;
+    }
+    return a;
+}
+
+// The allocator on one table under NUMA affinity `numa` (0 = nil): the node's own devices (tab == nullptr, unfiltered
+// when numa is 0) or a reservation restore table (kg_rsv_dev, already a filtered nodeDevice). The filtered nodeDevice
+// keeps the table's minors the affinity allows (gpu_minors' `allowed`); getRealUsed (allocator_gpu.go:59-70) counts
+// the node's used minors it leaves out (`outside`). When no free is left the filter drops the GPU type, which every
+// allocator stage then fails on alike.
+__device__ __forceinline__ GpuAlloc gpu_alloc_tab_numa(const KCfg& c, const ExtDev& e, const DevRec* __restrict__ d,
+                                                       const DevRec* __restrict__ tab, int32_t D,
+                                                       const ZoneRec* __restrict__ zr, const PodX& x, uint32_t numa,
+                                                       bool want_mask) {
+    if (D == 0) return {KG_DEV_CODE_NO_DEVICE, 0u};  // Prepare (devicehandler_gpu.go:41-44)
+    uint32_t in = ~0u, outside = 0u;  // the node's own devices without an affinity: no filter
+    if (tab || numa) {
+        const uint32_t allowed = numa ? gpu_numa_allowed(zr->dev_numa, D, numa) : (D >= 32 ? ~0u : (1u << D) - 1u);
+        uint32_t in_tab = tab ? 0u : ~0u, node_used = 0;
+        for (int32_t m = 0; m < D && m < DEV_MINORS; m++) {
+            bool it = false, nu = false;
+#pragma unroll
+            for (int r = 0; r < DEV_R; r++) {
+                if (tab) it |= tab->total[r][m] != 0;
+                nu |= d->free_[r][m] != d->total[r][m];
+            }
+            in_tab |= it ? 1u << m : 0u;
+            node_used |= nu ? 1u << m : 0u;
+        }
+        in = allowed & in_tab;
+        outside = node_used & ~in;
+    }
+    return gpu_allocate(c, e, tab ? tab : d, D, zr->dev_topo, zr->dev_part, x, outside, want_mask, in);
+}
+
+__device__ __forceinline__ GpuAlloc gpu_alloc_numa(const KCfg& c, const ExtDev& e, const DevRec* __restrict__ d,
+                                                   int32_t D, const ZoneRec* __restrict__ zr, const PodX& x, uint32_t numa,
+                                                   bool want_mask) {
+    return gpu_alloc_tab_numa(c, e, d, nullptr, D, zr, x, numa, want_mask);
+}
+
+// AutopilotAllocator.score (device_allocator.go:486-508) on a table under NUMA affinity `numa`: scoreNode over the
+// filtered devices' sums; 0 when the filter drops the GPU type (no free left in the table; the node's unfiltered
+// devices without an affinity skip that check). tab == nullptr: the node's devices.
+__device__ __forceinline__ int64_t dev_score_tab_numa(const KCfg& c, const DevRec* __restrict__ d,
+                                                      const DevRec* __restrict__ tab, int32_t D, uint32_t dev_numa,
+                                                      const PodX& x, uint32_t numa) {
+    const DevRec* t = tab ? tab : d;
+    const int32_t Dt = tab ? DEV_MINORS : D;
+    const uint32_t allowed = numa ? gpu_numa_allowed(dev_numa, D, numa) : ~0u;
+    int64_t T[DEV_R] = {0, 0, 0}, F[DEV_R] = {0, 0, 0};
+    bool any = false;
+    for (int32_t m = 0; m < Dt; m++) {
+        const bool in = ((allowed >> m) & 1u) != 0;
+#pragma unroll
+        for (int r = 0; r < DEV_R; r++) {
+            T[r] += in ? t->total[r][m] : 0;
+            F[r] += in ? t->free_[r][m] : 0;
+            any |= t->free_[r][m] != 0;
+        }
+    }
+    return ((tab || numa) && !any) ? 0 : dev_least(c, T, F, x.dreq);
+}
 
 // Filter (GPUAllocator.Allocate succeeds) + node Score before NormalizeScore.
 __device__ __forceinline__ uint32_t dev_eval(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
@@ -414,7 +510,6 @@ __device__ __forceinline__ uint32_t dev_eval(const KCfg& c, const ExtDev& e, con
     const int32_t D = (int32_t)n[N_DEV_MINORS];
     if (D < 0) return 0;  // no Device object
     if (D == 0) return KG_ST_DEV_NO_DEVICE;
-    if (x.dflags & KG_GPU_POD_TEMPLATE) return KG_ST_UNSUPPORTED;
     const GpuAlloc a = gpu_allocate(c, e, d, D, zr->dev_topo, zr->dev_part, x, outside, false);
     if (a.code) return dev_code_status(a.code);
     int64_t T[DEV_R] = {0, 0, 0}, F[DEV_R] = {0, 0, 0};
@@ -496,13 +591,14 @@ __device__ __forceinline__ int64_t dev_score(const KCfg& c, const DevRec* __rest
     return any ? dev_least(c, T, F, x.dreq) : 0;
 }
 
-// Reserve: the minors GPUAllocator.Allocate takes on the node (0 when it fails).
+// Reserve: the minors GPUAllocator.Allocate takes on the node (0 when it fails), inside the NUMA affinity the
+// topology manager stored for the pair (DeviceShare Reserve, plugin.go:585-600): the pair's zone code.
 __device__ __forceinline__ uint32_t dev_choose(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
                                                const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
-                                               const PodX& x) {
+                                               const PodX& x, int32_t zone) {
     const int32_t D = (int32_t)n[N_DEV_MINORS];
     if (x.dcount == 0 || D <= 0) return 0;
-    const GpuAlloc a = gpu_allocate(c, e, d, D, zr->dev_topo, zr->dev_part, x, 0u, true);
+    const GpuAlloc a = gpu_alloc_numa(c, e, d, D, zr, x, zone_affinity(zone), true);
     return a.code ? 0u : a.mask;
 }
 
@@ -794,7 +890,6 @@ __device__ __forceinline__ uint32_t dev_filter_view(const KCfg& c, const ExtDev&
     const int32_t D = (int32_t)n[N_DEV_MINORS];
     if (D < 0) return 0;  // no Device object
     if (D == 0) return KG_ST_DEV_NO_DEVICE;
-    if (x.dflags & KG_GPU_POD_TEMPLATE) return KG_ST_UNSUPPORTED;
     const bool tab_codes = e.rcode && dcls < (uint32_t)DEV_CLASSES;
     bool any = false;
     for (uint32_t t = 0; t < v.count; t++) {
@@ -817,6 +912,222 @@ __device__ __forceinline__ uint32_t dev_filter_view(const KCfg& c, const ExtDev&
     }
     const DevRec* tab = v.dev_base >= 0 ? e.rdev + v.dev_base : d;
     return dev_eval(c, e, n, zr, tab, x, raw, tab == d ? 0u : dev_outside_used(d, tab, D));
+}
+
+// DeviceShare's allocation for a pair under NUMA affinity `numa`: off views the node's devices; on a view
+// tryAllocateFromReusable over the matched reservations reserving GPUs in view order (deviceshare/reservation.go
+// :344-410), then, unless the pod requires a reservation ("Reservation(s) Insufficient gpu devices"), the allocation
+// outside them (the view's base table). Returns 0 (minors in `minors`) or the status bits.
+__device__ __forceinline__ uint32_t gpu_alloc_site(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                                   const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
+                                                   const RsvView* v, const PodX& x, bool required, uint32_t numa,
+                                                   bool want_mask, uint32_t& minors) {
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    minors = 0;
+    if (v && D == 0) return KG_ST_DEV_NO_DEVICE;
+    // the candidate tables in order: the view's reservations reserving GPUs, then the base (t == count); off views
+    // only the node's own devices
+    const uint32_t count = v ? v->count : 0u;
+    bool any = false;
+    for (uint32_t t = 0; t <= count; t++) {
+        const DevRec* tab = nullptr;
+        if (t < count) {
+            const int32_t di = e.infos[v->first + t].dev;
+            if (di < 0) continue;
+            any = true;
+            tab = e.rdev + di;
+        } else {
+            if (any && required) return KG_ST_DEV_RSV;
+            if (v && v->dev_base >= 0) tab = e.rdev + v->dev_base;
+        }
+        const GpuAlloc a = gpu_alloc_tab_numa(c, e, d, tab, D, zr, x, numa, want_mask);
+        if (!a.code || t == count) {
+            minors = a.mask;
+            return dev_code_status(a.code);
+        }
+    }
+    return 0;  // not reached
+}
+
+// DeviceShare's Score of a feasible pair (scoring.go:45-104): on a view the nominated reservation's table (0 when it
+// reserves no GPU, scoreWithNominatedReservation) or the base table, off views the node's devices; under NUMA
+// affinity `numa` (0 = nil).
+__device__ __forceinline__ int64_t gpu_score_site(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                                  const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
+                                                  const RsvView* v, const PodX& x, uint32_t numa, int nom) {
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    const DevRec* tab = nullptr;
+    if (v) {
+        if (nom >= 0) {
+            const int32_t di = e.infos[v->first + (uint32_t)nom].dev;
+            if (di < 0) return 0;
+            tab = e.rdev + di;
+        } else if (v->dev_base >= 0) {
+            tab = e.rdev + v->dev_base;
+        }
+    }
+    return dev_score_tab_numa(c, d, tab, D, zr->dev_numa, x, numa);
+}
+
+__device__ __forceinline__ uint32_t gpu_numa_count(uint32_t dev_numa, int32_t D, uint32_t m) {
+    uint32_t cnt = 0;
+    for (int32_t mi = 0; mi < D && mi < DEV_MINORS; mi++) {
+        const uint32_t q = (dev_numa >> (4 * mi)) & 15u;
+        cnt += (q < (uint32_t)MAX_ZONES && ((m >> q) & 1u)) ? 1u : 0u;
+    }
+    return cnt;
+}
+
+// DeviceShare's NUMA hints (generateTopologyHints, topology_hint.go:159-280): per mask over the GPUs' NUMA node ids
+// (IterateBitMasks order) the GPUs inside must number the request and DeviceShare's allocation at the pair's site must
+// succeed under the mask; Preferred = narrowest feasible width, Score 500 when the allocation equals the full mask's.
+// Returns 0 with the list in h, or the status bits of the provider's failure: the full mask's status, which stands
+// even when narrower masks fit (:191-196,271-279); the full mask is the last one iterated, so it is evaluated first.
+__device__ __forceinline__ uint32_t gpu_numa_hints(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                                   const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
+                                                   const RsvView* v, const PodX& x, bool required, GpuHints& h) {
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    h.masks = 0;
+    h.set = h.pref = h.s500 = 0;
+    uint32_t ids = 0;
+    for (int32_t m = 0; m < D && m < DEV_MINORS; m++) {
+        const uint32_t q = (zr->dev_numa >> (4 * m)) & 15u;
+        ids |= q < (uint32_t)MAX_ZONES ? 1u << q : 0u;
+    }
+    if (!ids) {  // no GPU with a NUMA node: the provider has no preference
+        h.set = 1u << NUMA_NIL_K;
+        return 0;
+    }
+    const uint32_t gn = (uint32_t)popc(ids);
+    const uint64_t nib = numa_mask_nib(gn);
+    const uint32_t nm = (1u << gn) - 1u;
+    int minsize = (int)gn;
+    uint32_t full_alloc = 0, alloc_of[15];
+    uint32_t ok = 0;  // bit k: mask k feasible
+    // masks in the order nm-1 (the full mask), 0, 1, ..., nm-2: the full mask's allocation is the Score-500
+    // reference and its failure the provider's status
+    for (uint32_t step = 0; step < nm; step++) {
+        const uint32_t k = step == 0 ? nm - 1u : step - 1u;
+        const uint32_t km = (uint32_t)(nib >> (4 * k)) & 15u;
+        uint32_t m = 0, rest = ids;  // index bit b -> the b-th smallest NUMA id
+        for (uint32_t b = 0; b < gn; b++) {
+            const uint32_t id = (uint32_t)(__ffs(rest) - 1);
+            rest &= rest - 1u;
+            m |= ((km >> b) & 1u) ? 1u << id : 0u;
+        }
+        uint32_t st = gpu_numa_count(zr->dev_numa, D, m) < x.dcount ? (uint32_t)KG_ST_DEV_MAKE(KG_DEV_CODE_NUMA_SCOPED) : 0u;
+        uint32_t alloc = 0;
+        if (!st) st = gpu_alloc_site(c, e, n, zr, d, v, x, required, m, true, alloc);
+        if (step == 0) {
+            if (st) return st;
+            full_alloc = alloc;
+        }
+        if (st) continue;
+        ok |= 1u << k;
+        alloc_of[k] = alloc;
+        minsize = min(minsize, popc(m));
+        h.masks |= (uint64_t)m << (4 * k);
+    }
+    // the list in IterateBitMasks order: entry k = mask k (kept only if feasible)
+    for (uint32_t k = 0; k < nm; k++) {
+        if (!((ok >> k) & 1u)) continue;
+        h.set |= 1u << k;
+        h.pref |= popc((uint32_t)(h.masks >> (4 * k)) & 15u) == minsize ? 1u << k : 0u;
+        h.s500 |= alloc_of[k] == full_alloc ? 1u << k : 0u;
+    }
+    return 0;
+}
+
+// ---- DeviceShare in the NUMA topology manager ------------------------------------------------------------
+// A GPU pod on a node (off reservation views) whose merged NUMA policy is not None: NodeNUMAResource's topology
+// manager gathers DeviceShare's hints too (manager.go:65-154, topology_hint.go:40-290) and calls its Allocate
+// under the best hint; the stored affinity then replaces DeviceShare's own Filter (plugin.go:369-374) and
+// restricts its Score and Reserve. `b` is eval_pair's result: when NodeNUMAResource's Filter got as far as the
+// topology manager, its NUMA part is recomputed here. BestEffort: Filter and Score as they are, the Reserve's
+// zone with both providers (ZONE_GPU_FAIL | code when DeviceShare fails there).
+template <bool EXACT, bool SCORE>
+__device__ __forceinline__ void numa_gpu_eval(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                              const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d, const RsvView* v,
+                                              const PodV& p, const PodX& x, PairOut& b, bool& dev_done, uint32_t& dev_mask) {
+    if (p.flags & KG_POD_NUMA_SKIP) return;
+    const uint32_t flags = (uint32_t)n[N_FLAGS];
+    const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (p.flags >> 16) & 15u;
+    const uint32_t pol = pod_pol != KG_NUMA_NONE ? pod_pol : node_pol;
+    if (pol == KG_NUMA_NONE) return;
+    // the Filter stopped before the topology manager (policy conflict, amplified cpu, cpuset checks, the cpuset
+    // path under a NUMA policy): eval_pair's status stands
+    if (b.status & (KG_ST_NUMA_CONFLICT | KG_ST_NUMA_AMP_CPU | KG_ST_NUMA_CPU_BIND | KG_ST_NUMA_CPU_TOPO | KG_ST_NUMA_CPUS |
+                    KG_ST_UNSUPPORTED))
+        return;
+    const uint32_t Z = (flags >> F_NUMA_ZONES_SHIFT) & 15u;
+    const bool be = pol == KG_NUMA_BEST_EFFORT;  // admits at Reserve only: Filter / Score as eval_pair has them
+    if (!be) {
+        b.status &= ~(uint32_t)(KG_ST_NUMA_NO_RES | KG_ST_NUMA_ALIGN | KG_ST_NUMA_UNSATISFIED);
+        b.zone = -1;
+        b.s_numa = 0;
+    }
+    if (Z == 0) {  // FilterByNUMANode: "node(s) missing NUMA resources" (BestEffort: b.zone's Reserve failure)
+        if (!be) b.status |= KG_ST_NUMA_NO_RES;
+        return;
+    }
+    const bool excl = pod_pol != KG_NUMA_NONE;
+    const bool required = (p.flags & KG_POD_RSV_REQUIRED) != 0;
+    const int64_t req[2] = {p.req_cpu, p.req_mem};
+    const bool has[2] = {(p.flags & KG_POD_HAS_CPU) != 0, (p.flags & KG_POD_HAS_MEM) != 0};
+    GpuHints gh;
+    const uint32_t fst = gpu_numa_hints(c, e, n, zr, d, v, x, required, gh);
+    if (fst) {  // the provider's status (accumulateProvidersHints): the Filter fails / the Reserve fails
+        if (be) b.zone = zone_gpu_fail(fst);
+        else b.status |= fst;
+        return;
+    }
+    NumaZ xz;
+    numa_load(zr, Z, xz);
+    uint32_t mask = 0;
+    const uint32_t st = numa_admit<true, true>(c, xz, req, has, pol, excl, mask, &gh);
+    if (st) {  // not under BestEffort (its merge always admits)
+        b.status |= st;
+        return;
+    }
+    int64_t al[2][MAX_ZONES];
+    const uint32_t fail = mask ? numa_split(xz, mask, req, has, al) : 0u;
+    if (fail) {  // BestEffort: the Reserve's NUMA allocation fails; else not reached (a preferred hint places)
+        if (be) b.zone = ZONE_RESERVE_FAIL | (int32_t)fail;
+        else b.status |= KG_ST_UNSUPPORTED;
+        return;
+    }
+    // allocateResources: DeviceShare's Allocate at the pair's site under the best hint
+    uint32_t minors;
+    const uint32_t ast = gpu_alloc_site(c, e, n, zr, d, v, x, required, mask, false, minors);
+    if (be) {
+        b.zone = ast ? zone_gpu_fail(ast) : numa_code(mask);
+        return;
+    }
+    if (ast) {
+        b.status |= ast;
+        return;
+    }
+    dev_done = true;
+    dev_mask = mask;
+    b.zone = numa_code(mask);
+    if constexpr (!SCORE) return;
+    const bool most = (c.most & MOST_NUMA) != 0;
+    if (!mask) {  // no NUMA allocation: node allocatable / requested (the view's NodeInfo on a view)
+        const int64_t rc = v ? v->req[0] : n[N_REQ_CPU], rm = v ? v->req[1] : n[N_REQ_MEM];
+        b.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], rc + p.req_cpu,
+                                     as_f64(n[N_RCP_CPU]), n[N_ALLOC_MEM], rm + p.req_mem, as_f64(n[N_RCP_MEM]));
+        return;
+    }
+    int64_t T[2] = {0, 0}, U[2] = {0, 0};
+#pragma unroll
+    for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++) {
+        if (z >= Z || (al[0][z] == 0 && al[1][z] == 0)) continue;
+        for (int r = 0; r < 2; r++) {
+            T[r] += xz.tot[r][z];
+            U[r] += xz.used[r][z];
+        }
+    }
+    b.s_numa = numa_score_q(most, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + p.req_cpu, T[1], U[1] + p.req_mem);
 }
 
 // ---- one pair with every plugin ---------------------------------------------------------------------
@@ -844,7 +1155,6 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
         o.status = qst;
         return o;
     }
-    const uint32_t flags = (uint32_t)n[N_FLAGS];
     const RsvView* v = nullptr;
     if ((c.plugins & KG_PLUGIN_RSV) && x.cls >= 0 && x.cls < RSV_MAX_CLASSES &&
         (((uint64_t)n[N_RSV_CLASSES] >> x.cls) & 1ull))
@@ -857,28 +1167,34 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
         ov.nz_cpu = v->nz_cpu;
         ov.nz_mem = v->nz_mem;
         ov.num_pods = v->num_pods;
+        // NodeNUMAResource's restore keeps only reservations holding a NUMA / cpuset allocation
+        // (nodenumaresource/reservation.go:188-270); kg_rsv_info describes none, so the plugin runs on the node's
+        // zones with the view's NodeInfo
         b = eval_pair<EXACT, true, TOPO, SCORE>(c, n, zr, p, &ov);
-        const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u;
-        const bool binds = (p.flags & KG_POD_CPU_BIND) || ((zr->cpu_meta >> CPU_META_BIND_SHIFT) & 3u);
-        if ((c.plugins & KG_PLUGIN_NUMA) && (node_pol != KG_NUMA_NONE || binds) && !(p.flags & KG_POD_NUMA_SKIP))
-            b.status = (b.status & ~(uint32_t)KG_ST_NUMA_MASK) | KG_ST_UNSUPPORTED;  // NUMA / cpuset restore: host path
     } else {
         b = eval_pair<EXACT, false, TOPO, SCORE>(c, n, zr, p);
     }
+    // a GPU pod on a node with a Device object: DeviceShare is a NUMA hint provider there, at the pair's site
+    // (its reservation view, if any)
+    bool dev_done = false;
+    uint32_t dev_mask = 0;
+    if ((c.plugins & KG_PLUGIN_NUMA) && (c.plugins & KG_PLUGIN_DEV) && x.dcount > 0 && n[N_DEV_MINORS] >= 0)
+        numa_gpu_eval<EXACT, SCORE>(c, e, n, zr, d, v, p, x, b, dev_done, dev_mask);
     uint32_t st = b.status;
     int64_t dev_raw = 0;
     const bool dev_view = (c.plugins & KG_PLUGIN_DEV) && v && x.dcount > 0;
     if (c.plugins & KG_PLUGIN_DEV) {
-        if (dev_view)
-            st |= dev_filter_view(c, e, n, zr, d, *v, x, (p.flags & KG_POD_RSV_REQUIRED) != 0, rec, dcls);
-        else if (e.dsum && dcls < (uint32_t)DEV_CLASSES)
-            st |= dev_eval_sum(c, e, n, zr, d, e.dsum + rec, x, dcls, dev_raw);
-        else
-            st |= dev_eval(c, e, n, zr, d, x, dev_raw);
-        if (x.dcount > 0) {
-            const uint32_t node_pol = (flags >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (p.flags >> 16) & 15u;
-            if ((c.plugins & KG_PLUGIN_NUMA) && (node_pol != KG_NUMA_NONE || pod_pol != KG_NUMA_NONE))
-                st |= KG_ST_UNSUPPORTED;  // device NUMA hints (topology_hint.go): host path
+        if (dev_done) {  // the topology manager stored an affinity: DeviceShare's Filter passes
+        } else {
+            uint32_t ds;
+            if (dev_view)
+                ds = dev_filter_view(c, e, n, zr, d, *v, x, (p.flags & KG_POD_RSV_REQUIRED) != 0, rec, dcls);
+            else if (e.dsum && dcls < (uint32_t)DEV_CLASSES)
+                ds = dev_eval_sum(c, e, n, zr, d, e.dsum + rec, x, dcls, dev_raw);
+            else
+                ds = dev_eval(c, e, n, zr, d, x, dev_raw);
+            // NodeNUMAResource already failed with a DeviceShare reason: one reason code
+            st |= (b.status & KG_ST_DEV_MASK) ? (ds & ~(uint32_t)KG_ST_DEV_MASK) : ds;
         }
     }
     RsvPod q;
@@ -895,16 +1211,11 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     o.s_dev = dev_raw;
     int nom = -1;
     if (v) o.s_rsv = rsv_nominate_score(q, n, *v, e.infos, o.order, c.rsv_ign, nom);
-    if (dev_view) {
-        // Score (scoring.go:77-103): with a nominated reservation, its table, or 0 when it reserves no GPU
-        // (scoreWithNominatedReservation, reservation.go:492-520); without one, the view's base table
-        if (nom >= 0) {
-            const int32_t di = e.infos[v->first + nom].dev;
-            o.s_dev = di >= 0 ? dev_score(c, e.rdev + di, x) : 0;
-        } else {
-            o.s_dev = dev_score(c, v->dev_base >= 0 ? e.rdev + v->dev_base : d, x);
-        }
-    }
+    if (dev_view || dev_done)
+        // Score (scoring.go:45-104): with a nominated reservation, its table, or 0 when it reserves no GPU
+        // (scoreWithNominatedReservation, reservation.go:492-520); without one, the view's base table; off views
+        // the node's devices; under the stored NUMA affinity
+        o.s_dev = gpu_score_site(c, e, n, zr, d, v, x, dev_done ? dev_mask : 0u, nom);
     return o;
 }
 

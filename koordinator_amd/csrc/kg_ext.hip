@@ -121,6 +121,7 @@ __global__ __launch_bounds__(256) void k_dev_sum(const NodeRec* __restrict__ nod
             x.dkeys = cls[k].dkeys;
             x.dcount = cls[k].dcount;
             x.dflags = cls[k].dflags;
+            x.dtmpl = cls[k].dtmpl;
             x.dbw = cls[k].dbw;
             for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
             uint32_t le = 0u;
@@ -168,6 +169,7 @@ __global__ __launch_bounds__(256) void k_rdev_codes(const NodeRec* __restrict__ 
             x.dkeys = cls[k].dkeys;
             x.dcount = cls[k].dcount;
             x.dflags = cls[k].dflags;
+            x.dtmpl = cls[k].dtmpl;
             x.dbw = cls[k].dbw;
             for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
             code = (uint8_t)gpu_allocate(cfg, e, tab, D, zones[rec].dev_topo, zones[rec].dev_part, x, outside, false).code;
@@ -643,7 +645,7 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
             const PodX qx = load_podx(pods, step - 1);
             apply_assume(cfg, nodes[i].v, zones + i, q, prev_zone, 1);
             if ((cfg.plugins & KG_PLUGIN_DEV) && qx.dcount > 0) {
-                const uint32_t mask = dev_choose(cfg, e, nodes[i].v, zones + i, devs + i, qx);
+                const uint32_t mask = dev_choose(cfg, e, nodes[i].v, zones + i, devs + i, qx, prev_zone);
                 dev_apply(devs + i, mask, qx, 1);
                 minors[step - 1] = mask;
             }
@@ -737,7 +739,7 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
             }
             return;
         }
-        mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, e, n, zones + rec, devs + rec, qx) : 0u;
+        mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone) : 0u;
     }
     __syncthreads();  // every lane has read the state before lane 0 changes it
     if (threadIdx.x != 0) return;
@@ -796,7 +798,7 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
                 const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, qst);
                 st = r.status;
                 zone = r.zone;
-                if (!st && (cfg.plugins & KG_PLUGIN_DEV) && devs) mask = dev_choose(cfg, e, n, zones + rec, devs + rec, qx);
+                if (!st && !zone_reserve_fails(zone) && (cfg.plugins & KG_PLUGIN_DEV) && devs) mask = dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone);
             } else {
                 const PairOut r = eval_pair<EXACT>(cfg, n, zones + rec, q);
                 st = r.status;

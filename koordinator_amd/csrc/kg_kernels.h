@@ -37,6 +37,8 @@ struct LaunchSelect {
     const uint32_t* pmap;  // sub-batch row -> batch position for pstat (nullptr: identity)
     uint32_t* pstat;       // per batch position: KG_ST_UNSUPPORTED when some pair needs the host path
     bool fused;            // K == 1 fast path: atomicMax straight into out, no partials
+    bool fused_k;          // K > 1: every lane inserts its top-K into out[row] by the atomicMax cascade
+                           // (topk_atomic, kg_kernels.hip), no partials, no merge
     uint64_t* out;
     const uint32_t* big_list;
     const uint32_t* big_count;

@@ -36,6 +36,29 @@ __device__ __forceinline__ void topk_insert(uint64_t (&top)[K], uint64_t key) {
     }
 }
 
+// Insert a lane's top-K (descending, zeros = none) into the K shared slots of its pod, out[0..K), by an
+// atomicMax cascade: each key goes down the slots, an atomicMax at slot u keeps the larger of (slot, key) and
+// the smaller continues to slot u + 1. Whatever the interleaving of the lanes (chunks) that insert into one
+// pod, slot u ends as the u-th largest key inserted (the values passed below slot u are exactly its arrivals
+// minus their maximum), and slot u >= slot u + 1 at every instant; slots only grow. So a key that is not
+// above slot K-1 (read once, a lower bound of every slot from then on) can stop.
+template <int K>
+__device__ __forceinline__ void topk_atomic(uint64_t* out, const uint64_t (&top)[K]) {
+    if (top[0] == 0ull) return;
+    const uint64_t floor = __hip_atomic_load(out + (K - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int t = 0; t < K; t++) {
+        uint64_t carry = top[t];
+        if (carry <= floor) break;  // top is descending: every later key stops too
+#pragma unroll
+        for (int u = 0; u < K; u++) {
+            if (carry <= floor) break;
+            const uint64_t old = atomicMax((unsigned long long*)(out + u), (unsigned long long)carry);
+            carry = old < carry ? old : carry;
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t rec_gidx(const NodeRec& r, uint32_t index_base) {
     return index_base + node_index(r);
 }
@@ -71,8 +94,9 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
                                                 uint64_t* __restrict__ partial, uint64_t* __restrict__ out,
                                                 const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat,
                                                 const uint32_t* __restrict__ order) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t c = blockIdx.y;
+    const GridBlock b = xcd_block();  // whole record chunks per XCD (kg_eval.h)
+    const uint32_t j = b.x * blockDim.x + threadIdx.x;
+    const uint32_t c = b.y;
     const bool live = j < n_lanes;
     const uint32_t row = live ? (order ? order[j] : j) : 0u;
     const PodV p = load_pod(pods, row);
@@ -101,6 +125,8 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
     if (live) {
         if (K == 1 && out) {
             if (top[0]) atomicMax((unsigned long long*)(out + row), (unsigned long long)top[0]);
+        } else if (out) {
+            topk_atomic<K>(out + (size_t)row * K, top);
         } else {
             uint64_t* dst = partial + ((size_t)(part0 + c) * ld + row) * K;
 #pragma unroll
@@ -169,7 +195,7 @@ __global__ __launch_bounds__(256) void k_big_sel(const NodeRec* __restrict__ nod
                                                  const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat,
                                                  const uint32_t* __restrict__ order) {
     const uint32_t nb = *big_count;
-    const bool direct = K == 1 && out;
+    const bool direct = out != nullptr;
     if (nb == 0 && direct) return;  // uniform
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_lanes) return;
@@ -190,7 +216,11 @@ __global__ __launch_bounds__(256) void k_big_sel(const NodeRec* __restrict__ nod
         }
     }
     if (direct) {
-        if (top[0]) atomicMax((unsigned long long*)(out + row), (unsigned long long)top[0]);
+        if constexpr (K == 1) {
+            if (top[0]) atomicMax((unsigned long long*)(out + row), (unsigned long long)top[0]);
+        } else {
+            topk_atomic<K>(out + (size_t)row * K, top);
+        }
     } else {
         uint64_t* dst = partial + ((size_t)(part0 + blockIdx.y) * ld + row) * K;
 #pragma unroll
@@ -833,26 +863,29 @@ static void select_instance(const LaunchSelect& a, const SelectRange& r, uint32_
                                                              a.order ? a.order + lane0 : nullptr);
 }
 
+// K > 1 fused (a.fused_k): the lanes insert into out by the atomic cascade, no partial rows exist
 template <int K, int CLS>
 static void select_fast(const LaunchSelect& a, const SelectRange& r, hipStream_t s) {
+    const bool atom = K > 1 && a.fused_k;
     switch (a.cfg.plugins & 7u) {
-        case 0: select_instance<K, false, true, 0, CLS>(a, r, 0, a.n_fast, false, s); break;
-        case 1: select_instance<K, false, true, 1, CLS>(a, r, 0, a.n_fast, false, s); break;
-        case 2: select_instance<K, false, true, 2, CLS>(a, r, 0, a.n_fast, false, s); break;
-        case 3: select_instance<K, false, true, 3, CLS>(a, r, 0, a.n_fast, false, s); break;
-        case 4: select_instance<K, false, true, 4, CLS>(a, r, 0, a.n_fast, false, s); break;
-        case 5: select_instance<K, false, true, 5, CLS>(a, r, 0, a.n_fast, false, s); break;
-        case 6: select_instance<K, false, true, 6, CLS>(a, r, 0, a.n_fast, false, s); break;
-        default: select_instance<K, false, true, 7, CLS>(a, r, 0, a.n_fast, false, s); break;
+        case 0: select_instance<K, false, true, 0, CLS>(a, r, 0, a.n_fast, atom, s); break;
+        case 1: select_instance<K, false, true, 1, CLS>(a, r, 0, a.n_fast, atom, s); break;
+        case 2: select_instance<K, false, true, 2, CLS>(a, r, 0, a.n_fast, atom, s); break;
+        case 3: select_instance<K, false, true, 3, CLS>(a, r, 0, a.n_fast, atom, s); break;
+        case 4: select_instance<K, false, true, 4, CLS>(a, r, 0, a.n_fast, atom, s); break;
+        case 5: select_instance<K, false, true, 5, CLS>(a, r, 0, a.n_fast, atom, s); break;
+        case 6: select_instance<K, false, true, 6, CLS>(a, r, 0, a.n_fast, atom, s); break;
+        default: select_instance<K, false, true, 7, CLS>(a, r, 0, a.n_fast, atom, s); break;
     }
 }
 
 hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
     const uint32_t K = a.k == 1 ? 1u : (uint32_t)KG_TOPK_MAX;
     const uint32_t n_fast = a.fast ? a.n_fast : 0u, n_int = a.n_pods - n_fast;
-    // K == 1: the fused fast path and the integer lanes update out[row] by atomicMax
-    if (K == 1 && (a.fused || n_int)) {
-        hipError_t e = hipMemsetAsync(a.out, 0, sizeof(uint64_t) * a.n_rows, s);
+    // K == 1: the fused fast path and the integer lanes update out[row] by atomicMax; K > 1 fused: every lane
+    // by the atomicMax cascade
+    if ((K == 1 && (a.fused || n_int)) || (K > 1 && a.fused_k)) {
+        hipError_t e = hipMemsetAsync(a.out, 0, sizeof(uint64_t) * a.n_rows * K, s);
         if (e != hipSuccess) return e;
     }
     if (n_fast) {
@@ -867,7 +900,7 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
             else
                 k_big_sel<KG_TOPK_MAX><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, a.n_rows, a.big_list,
                                                               a.big_count, a.index_base, a.cfg, a.partial, a.big_part0,
-                                                              nullptr, a.pmap, a.pstat, a.order);
+                                                              a.fused_k ? a.out : nullptr, a.pmap, a.pstat, a.order);
         }
         for (int cls = 0; cls < 2; cls++) {
             const SelectRange& r = a.range[cls];
@@ -902,7 +935,7 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
                 else select_fast<KG_TOPK_MAX, 1>(a, r, s);
             }
         }
-        if (!a.fused) {
+        if (!a.fused && !a.fused_k) {
             hipError_t e = launch_merge_list(a.partial, 0, select_fparts(a), a.n_rows, a.order, n_fast, K, a.out, s);
             if (e != hipSuccess) return e;
         }
@@ -911,17 +944,17 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
         const SelectRange& r = a.irange;
         if (a.exact) {
             if (K == 1) select_instance<1, true, false, 0, 0>(a, r, n_fast, n_int, true, s);
-            else select_instance<KG_TOPK_MAX, true, false, 0, 0>(a, r, n_fast, n_int, false, s);
+            else select_instance<KG_TOPK_MAX, true, false, 0, 0>(a, r, n_fast, n_int, a.fused_k, s);
         } else {
             if (K == 1) select_instance<1, false, false, 0, 0>(a, r, n_fast, n_int, true, s);
-            else select_instance<KG_TOPK_MAX, false, false, 0, 0>(a, r, n_fast, n_int, false, s);
+            else select_instance<KG_TOPK_MAX, false, false, 0, 0>(a, r, n_fast, n_int, a.fused_k, s);
         }
-        if (K > 1) {
+        if (K > 1 && !a.fused_k) {
             hipError_t e = launch_merge_list(a.partial, r.part0, r.n_chunks, a.n_rows, a.order ? a.order + n_fast : nullptr,
                                              n_int, K, a.out, s);
             if (e != hipSuccess) return e;
         }
-    } else if (n_int && K > 1) {  // no records: no feasible node
+    } else if (n_int && K > 1 && !a.fused_k) {  // no records: no feasible node (fused: out is zeroed)
         hipError_t e = launch_merge_list(a.partial, 0, 0, a.n_rows, a.order ? a.order + n_fast : nullptr, n_int, K, a.out, s);
         if (e != hipSuccess) return e;
     }

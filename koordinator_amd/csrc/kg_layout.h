@@ -135,6 +135,9 @@ struct alignas(64) ZoneRec {
     // (NUMA rank << 4 | PCIe rank) or KG_GPU_NO_SCOPE, and the partition table / KG_GPU_HONOR / KG_GPU_TREE
     uint64_t dev_topo;
     uint32_t dev_part;
+    // per minor (nibble) the GPU's NUMA node id, KG_GPU_NUMA_ANY (NodeID -1) or KG_GPU_NUMA_NONE (no Topology):
+    // DeviceShare as a NUMA hint provider (kg_node_columns.dev_numa)
+    uint32_t dev_numa;
 };
 static_assert(sizeof(ZoneRec) == 640, "the cpuset and GPU topology fields live in ZoneRec's tail padding");
 // ZoneRec.cpu_meta: bits 0-7 maxRefCount, 8-9 node CPU bind policy (KG_NODE_CPU_BIND_*), 10 NUMA allocate
@@ -188,8 +191,20 @@ constexpr int32_t ZONE_RESERVE_FAIL = 0x20;
 KG_HD inline bool zone_reserve_fails(int32_t z) { return z >= 0x20 && z < 0x40; }
 // a cpuset-binding pod whose accumulator finds no CPUs at Reserve (resource_manager.go:385,427 ErrNotEnoughCPUs)
 constexpr int32_t ZONE_CPUSET_FAIL = ZONE_RESERVE_FAIL | 8;
+// a GPU pod whose DeviceShare hints or Allocate fail in the topology manager at Reserve (BestEffort node):
+// ZONE_GPU_FAIL | KG_DEV_CODE_*, or ZONE_GPU_FAIL | 0xF for "Reservation(s) Insufficient gpu devices"
+constexpr int32_t ZONE_GPU_FAIL = 0x30;
+KG_HD inline int32_t zone_gpu_fail(uint32_t st) {
+    return ZONE_GPU_FAIL | (int32_t)((st & KG_ST_DEV_RSV) ? 0xFu : KG_ST_DEV_CODE(st));
+}
 KG_HD inline uint32_t zone_fail_status(int32_t z) {
+    if ((uint32_t)z & 0x10u) return ((z & 0xF) == 0xF) ? (uint32_t)KG_ST_DEV_RSV : KG_ST_DEV_MAKE((uint32_t)z & 0xFu);
     return (((uint32_t)z & 7u) << 12) | (((uint32_t)z & 8u) ? KG_ST_NUMA_CPUS : 0u);
+}
+// the NUMA affinity (bit per zone) of a pair's zone code; 0 = none (nil affinity, or the Reserve fails)
+KG_HD inline uint32_t zone_affinity(int32_t z) {
+    if (z < 0 || zone_reserve_fails(z)) return 0u;
+    return z >= 0x40 ? ((uint32_t)z & 0xFu) : (1u << (uint32_t)z);
 }
 
 // Magnitude bound of the float64 fast path: operands below 2^44 keep 100 * headroom below 2^51
@@ -319,6 +334,7 @@ struct PodsDev {
     const uint8_t* dev_cls;     // GPU request class of the pod (DevSum.code / score index), DEV_CLASSES = none
     const uint32_t* dev_flags;  // KG_GPU_POD_*
     const int64_t* dev_bw;      // ring bus bandwidth request (KG_GPU_POD_RING_BW)
+    const uint32_t* dev_tmpl;   // candidate template counts per key (KG_GPU_POD_TEMPLATE)
 };
 
 // Scoring / filtering configuration passed by value to every kernel.
@@ -357,7 +373,7 @@ constexpr int DEV_CLASSES = 56;
 // A GPU request class: everything the allocator reads of a pod (GPURequirements).
 struct DevClass {
     int64_t dreq[DEV_R];
-    uint32_t dkeys, dcount, dflags, pad_;
+    uint32_t dkeys, dcount, dflags, dtmpl;
     int64_t dbw;
 };
 struct alignas(16) DevSum {

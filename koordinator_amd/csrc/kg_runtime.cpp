@@ -160,7 +160,7 @@ struct kg_pods {
     uint32_t* d_xlist = nullptr;  // config-5 pods through k_ext_select (batch positions)
     uint32_t* d_stat_list = nullptr;  // pods carrying a GPU request or a reservation class
     int64_t* d_dev_req = nullptr;     // [n][KG_DEV_R]
-    uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32), dev_flags: 6 x n
+    uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32), dev_flags, dev_tmpl: 7 x n
     uint8_t* d_dcls = nullptr;        // GPU request class per pod (DevSum nibble), DEV_CLASSES = none
     DevClass* d_dclass = nullptr;
     uint32_t n_dclass = 0;
@@ -191,7 +191,7 @@ struct kg_pods {
     bool fast_ok = false;  // every pod in the fast domain (no value >= 2^44, no pod NUMA policy, no cpuset binding)
     bool pod_policy = false;  // some pod carries its own NUMA policy
     bool any_cpu_bind = false;  // some pod binds cpusets (KG_POD_CPU_BIND)
-    bool dev_unclassed = false; // some GPU pod has no GPU request class (more than DEV_CLASSES, or a template pod)
+    bool dev_unclassed = false; // some GPU pod has no GPU request class (more than DEV_CLASSES)
     std::vector<uint32_t> h_flags;  // host copies for argument checks (kg_forget of a cpuset pod)
     std::vector<int64_t> h_req_cpu;
     // config-5 scratch
@@ -511,8 +511,15 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     // GPU topology tree / partition table (static)
     zr->dev_topo = s->dev_topo ? s->dev_topo[i] : ~0ull;
     zr->dev_part = s->dev_part ? s->dev_part[i] : 0u;
-    if ((zr->dev_part & ~(0xFFu | KG_GPU_HONOR | KG_GPU_TREE)) || (zr->dev_part & 0xFFu) > KG_GPU_MAX_TABLES)
+    if ((zr->dev_part & ~(0xFFu | KG_GPU_HONOR | KG_GPU_TREE | (15u << KG_GPU_TMPL_SHIFT))) || (zr->dev_part & 0xFFu) > KG_GPU_MAX_TABLES)
         return fail(ctx, KG_INVALID_ARG, "node %u: dev_part 0x%x", i, zr->dev_part);
+    // GPU NUMA node ids: each a zone id (< KG_MAX_ZONES), KG_GPU_NUMA_ANY or KG_GPU_NUMA_NONE
+    zr->dev_numa = s->dev_numa ? s->dev_numa[i] : 0xFFFFFFFFu;
+    for (int m = 0; m < KG_DEV_MINORS; m++) {
+        const uint32_t q = (zr->dev_numa >> (4 * m)) & 0xFu;
+        if (q >= (uint32_t)KG_MAX_ZONES && q != KG_GPU_NUMA_ANY && q != KG_GPU_NUMA_NONE)
+            return fail(ctx, KG_UNSUPPORTED, "node %u: GPU minor %d on NUMA node %u (>= %d zones)", i, m, q, KG_MAX_ZONES);
+    }
     derive_node(*rec, *zr);
     return KG_OK;
 }
@@ -1186,7 +1193,7 @@ PodLayout pod_layout(uint32_t n) {
     L.stat = take(sizeof(uint32_t) * (size_t)n);
     L.dev_req = take(sizeof(int64_t) * DEV_R * (size_t)n);
     L.dev_bw = take(sizeof(int64_t) * (size_t)n);
-    L.xcols = take(sizeof(uint32_t) * 6 * (size_t)n);
+    L.xcols = take(sizeof(uint32_t) * 7 * (size_t)n);
     L.dclass = take(sizeof(DevClass) * DEV_CLASSES);
     L.dcls = take((size_t)n);
     L.total = o;
@@ -1224,6 +1231,7 @@ void pod_views(kg_pods* p, uint32_t n) {
     v.quota_keys = p->d_xcols + 3 * (size_t)n;
     v.rsv_class = reinterpret_cast<const int32_t*>(p->d_xcols + 4 * (size_t)n);
     v.dev_flags = p->d_xcols + 5 * (size_t)n;
+    v.dev_tmpl = p->d_xcols + 6 * (size_t)n;
     v.dev_bw = reinterpret_cast<const int64_t*>(d + L.dev_bw);
     v.dev_cls = p->d_dcls;
 }
@@ -1291,6 +1299,8 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             return fail(ctx, KG_INVALID_ARG, "pod %u: GPU requirement flags 0x%x", j, df);
         if ((df & KG_GPU_POD_RING_BW) && !cols->dev_ring_bw)
             return fail(ctx, KG_INVALID_ARG, "pod %u: KG_GPU_POD_RING_BW without dev_ring_bw", j);
+        if ((df & KG_GPU_POD_TEMPLATE) && (!cols->dev_tmpl || (cols->dev_tmpl[j] >> (2 * KG_GPU_TMPL_NONE))))
+            return fail(ctx, KG_INVALID_ARG, "pod %u: KG_GPU_POD_TEMPLATE without a dev_tmpl entry", j);
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     // the side stream's plain-pod select of the previous batch reads d_in: it has to finish before the copy
@@ -1350,7 +1360,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     const uint32_t n_fast = cnt[0] + cnt[1] + cnt[2];
     // config-5 columns (absent columns: no GPU request, no quota, no reservation class)
     const bool ext_cols = cols->dev_req || cols->dev_count || cols->dev_keys || cols->quota || cols->quota_keys ||
-                          cols->rsv_class || cols->dev_flags;
+                          cols->rsv_class || cols->dev_flags || cols->dev_tmpl;
     uint32_t* xc = reinterpret_cast<uint32_t*>(h + L.xcols);
     uint32_t* pmap = reinterpret_cast<uint32_t*>(h + L.pmap);
     uint32_t* xlist = reinterpret_cast<uint32_t*>(h + L.xlist);
@@ -1370,21 +1380,23 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             const uint32_t cntj = cols->dev_count ? cols->dev_count[j] : 0u;
             const uint32_t keys = cols->dev_keys ? cols->dev_keys[j] : 0u;
             const uint32_t dfl = cols->dev_flags ? cols->dev_flags[j] : 0u;
+            const uint32_t tmpl = (dfl & KG_GPU_POD_TEMPLATE) ? cols->dev_tmpl[j] : 0u;
             for (int r = 0; r < DEV_R; r++) dreq[(size_t)j * DEV_R + r] = cols->dev_req ? cols->dev_req[(size_t)j * DEV_R + r] : 0;
             dbw[j] = (dfl & KG_GPU_POD_RING_BW) ? cols->dev_ring_bw[j] : 0;
             dcls[j] = (uint8_t)DEV_CLASSES;
-            if (cntj > 0 && !(dfl & KG_GPU_POD_TEMPLATE)) {  // GPU request class: everything the allocator and the Score read
+            if (cntj > 0) {  // GPU request class: everything the allocator and the Score read
                 DevClass c{};
                 c.dkeys = keys & 7u;
                 c.dcount = cntj;
                 c.dflags = dfl;
+                c.dtmpl = tmpl;
                 c.dbw = dbw[j];
                 for (int r = 0; r < DEV_R; r++) c.dreq[r] = dreq[(size_t)j * DEV_R + r];
                 size_t k = 0;
                 while (k < classes.size() && !(classes[k].dkeys == c.dkeys && classes[k].dreq[0] == c.dreq[0] &&
                                                classes[k].dreq[1] == c.dreq[1] && classes[k].dreq[2] == c.dreq[2] &&
                                                classes[k].dcount == c.dcount && classes[k].dflags == c.dflags &&
-                                               classes[k].dbw == c.dbw))
+                                               classes[k].dtmpl == c.dtmpl && classes[k].dbw == c.dbw))
                     k++;
                 if (k == classes.size() && classes.size() < (size_t)DEV_CLASSES) classes.push_back(c);
                 if (k < classes.size()) dcls[j] = (uint8_t)k;
@@ -1398,6 +1410,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             xc[3 * (size_t)n + j] = cols->quota_keys ? cols->quota_keys[j] : 0u;
             xc[4 * (size_t)n + j] = (uint32_t)cls;
             xc[5 * (size_t)n + j] = dfl;
+            xc[6 * (size_t)n + j] = tmpl;
             if (cntj > 0 || cls >= 0) stat[ns++] = j;
             if (cntj == 0 && cls < 0 && !(f[j] & KG_POD_RSV_REQUIRED)) pmap[np++] = j;
             else xlist[nx++] = j;
@@ -1433,8 +1446,8 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     if (n && !ext_copy) {
         HIP_TRY(ctx, hipMemsetAsync(p->d_dev_req, 0, sizeof(int64_t) * DEV_R * n, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(const_cast<int64_t*>(p->dev.dev_bw), 0, sizeof(int64_t) * n, ctx->stream));
-        const int xdef[6] = {0, 0, 0xFF, 0, 0xFF, 0};  // -1 quota / class
-        for (int c = 0; c < 6; c++)
+        const int xdef[7] = {0, 0, 0xFF, 0, 0xFF, 0, 0};  // -1 quota / class
+        for (int c = 0; c < 7; c++)
             HIP_TRY(ctx, hipMemsetAsync(p->d_xcols + (size_t)c * n, xdef[c], sizeof(uint32_t) * n, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(p->d_dcls, DEV_CLASSES, n, ctx->stream));
     }
@@ -1703,6 +1716,7 @@ static LaunchSelect make_select(const kg_snap* s, const PodsDev& pods, const uin
     a.big_list = s->d_big + 1;
     a.big_count = s->d_big;
     a.fused = a.fast && kk == 1 && !unfused();
+    a.fused_k = kk > 1 && !unfused();
     uint32_t np = 0;
     if (a.n_fast) {
         const uint32_t bounds[3] = {0, s->n0, s->n};
@@ -1713,13 +1727,13 @@ static LaunchSelect make_select(const kg_snap* s, const PodsDev& pods, const uin
             r.chunk = select_chunk(r.end - r.begin, a.n_fast);  // each class launch fills the chip on its own
             r.n_chunks = (r.end - r.begin + r.chunk - 1) / r.chunk;
             r.part0 = np;
-            if (!a.fused) np += r.n_chunks;
+            if (!a.fused && !a.fused_k) np += r.n_chunks;
         }
         const uint32_t pod_blocks = (a.n_fast + 255) / 256;
         const uint32_t want = std::max<uint32_t>(1, (2048 + pod_blocks - 1) / pod_blocks);
         a.big_y = std::max<uint32_t>(1, std::min<uint32_t>(want, (s->n_big_est + 7) / 8));
         a.big_part0 = np;
-        if (!a.fused) np += a.big_y;
+        if (!a.fused && !a.fused_k) np += a.big_y;
     }
     const uint32_t n_int = n_lanes - a.n_fast;
     if (n_int && s->n) {
@@ -1729,7 +1743,7 @@ static LaunchSelect make_select(const kg_snap* s, const PodsDev& pods, const uin
         r.chunk = select_chunk(s->n, n_int);
         r.n_chunks = (s->n + r.chunk - 1) / r.chunk;
         r.part0 = np;
-        if (kk > 1) np += r.n_chunks;  // top-1 of the integer lanes: atomicMax into out
+        if (kk > 1 && !a.fused_k) np += r.n_chunks;  // top-1 / fused top-K of the integer lanes: atomics into out
     }
     *parts = np;
     return a;

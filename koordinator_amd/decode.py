@@ -1327,6 +1327,34 @@ def gpu_topology(gpu_infos: Sequence[dict]) -> Tuple[int, bool]:
     return topo, True
 
 
+def gpu_numa(gpu_infos: Sequence[dict]) -> int:
+    """dev_numa of a node from its GPU DeviceInfos: nibble m = the NUMA node id of GPU minor m
+    (NUMATopology.deviceToNodeID, deviceshare/numa_topology.go:43-100), KG_GPU_NUMA_ANY for Topology.NodeID -1,
+    KG_GPU_NUMA_NONE without a Topology (or no such minor). Ids are NUMA zone ids below KG_MAX_ZONES."""
+    v = (1 << 32) - 1
+    ids = set()
+    for d in gpu_infos or ():
+        m = int(d.get("minor", 0))
+        if m >= abi.KG_DEV_MINORS:
+            raise Unsupported(f"GPU minor {m} >= {abi.KG_DEV_MINORS}")
+        t = d.get("topology")
+        if t is None:
+            q = abi.KG_GPU_NUMA_NONE
+        else:
+            q = int(t.get("nodeID", 0))
+            if q == -1:
+                q = abi.KG_GPU_NUMA_ANY
+            elif not 0 <= q < abi.KG_MAX_ZONES:
+                raise Unsupported(f"GPU NUMA node id {q} outside the device's {abi.KG_MAX_ZONES} zones")
+            else:
+                ids.add(q)
+        v &= ~(0xF << (4 * m))
+        v |= q << (4 * m)
+    if len(ids) > abi.KG_MAX_ZONES:
+        raise Unsupported(f"GPUs on more than {abi.KG_MAX_ZONES} NUMA nodes")
+    return v
+
+
 def gpu_pod_flags(pod: dict, shared: bool) -> Tuple[int, int]:
     """(dev_flags, dev_ring_bw) of a GPU pod: parseGPURequirements (deviceshare/utils.go:516-545) beyond the
     request: GPUPartitionSpec (apiext.GetGPUPartitionSpec: present -> honor, AllocatePolicy Restricted,
@@ -1351,3 +1379,93 @@ def gpu_pod_flags(pod: dict, shared: bool) -> Tuple[int, int]:
             level = abi.GPU_SCOPE_LEVEL.get(scope, 5)
             flags |= level << abi.KG_GPU_POD_SCOPE_SHIFT
     return flags, bw
+
+
+# ---- GPU shared-resource templates (deviceshare/gpu_shared_resource_templates_cache.go) ----------------------
+
+class NoMatchedTemplate(Exception):
+    """parseGPURequirements' PreFilter error ErrNoMatchedGPUSharedResourceTemplate (deviceshare/utils.go:544-546):
+    a pod enforcing a template matched none of any key; the pod fails PreFilter, no node is evaluated."""
+
+
+def gpu_template_key(node: dict) -> str:
+    """buildGPUSharedResourceTemplatesKey(vendor, model) of a node's labels (allocator_gpu.go:140,
+    gpu_shared_resource_templates_cache.go:80-82)."""
+    labels = node.get("metadata", {}).get("labels") or {}
+    return f"{labels.get(LABEL_GPU_VENDOR, '')}-{labels.get(LABEL_GPU_MODEL, '')}"
+
+
+class GpuSharedResourceTemplates:
+    """gpuSharedResourceTemplatesCache (gpu_shared_resource_templates_cache.go:30-78) with the plugin's
+    GPUSharedResourceTemplatesConfig.MatchedResources, and its device encoding: the configured keys in sorted
+    order are the template keys of dev_part bits 12-15 (at most KG_GPU_TMPL_NONE of them), a pod's
+    candidateGPUSharedResourceTemplates become 2 bits per key in kg_pod_columns.dev_tmpl."""
+
+    def __init__(self, infos: Optional[Dict[str, Dict[str, Dict[str, object]]]] = None,
+                 matched_resources: Sequence[str] = ()):
+        self.infos = {key: {name: {r: parse_quantity(q) for r, q in (tmpl or {}).items()}
+                            for name, tmpl in (templates or {}).items()}
+                      for key, templates in (infos or {}).items()}
+        self.matched_resources = set(matched_resources)
+        self.keys = sorted(self.infos)
+        if len(self.keys) > abi.KG_GPU_TMPL_NONE:
+            raise Unsupported(f"more than {abi.KG_GPU_TMPL_NONE} GPU shared-resource template keys")
+
+    @classmethod
+    def from_configmap(cls, cm: dict, matched_resources: Sequence[str] = ()) -> "GpuSharedResourceTemplates":
+        """setTemplatesInfosFromConfigMap (:71-78): the YAML map under data.yaml; a malformed one raises
+        ValueError (the cache keeps its previous infos in the reference's event handler)."""
+        import yaml
+        try:
+            infos = yaml.safe_load((cm.get("data") or {}).get("data.yaml", ""))
+        except yaml.YAMLError as e:
+            raise ValueError(f"invalid GPU shared-resource templates: {e}") from e
+        if infos is not None and not isinstance(infos, dict):
+            raise ValueError("invalid GPU shared-resource templates: not a map")
+        return cls(infos, matched_resources)
+
+    def find_matched(self, resources: Dict[str, object], strict: bool) -> Dict[str, Dict[str, Dict[str, Fraction]]]:
+        """findMatchedTemplates (:41-62): per key, the templates equal to `resources` (quotav1.Equals: the same
+        names with equal quantities); not strict, each template is first masked to the resource names."""
+        want = {r: parse_quantity(q) for r, q in resources.items()}
+        out = {}
+        for key, templates in self.infos.items():
+            matched = {}
+            for name, tmpl in templates.items():
+                t = tmpl if strict else {r: q for r, q in tmpl.items() if r in want}
+                if t == want:
+                    matched[name] = dict(tmpl)
+            if matched:
+                out[key] = matched
+        return out
+
+    def node_key(self, node: dict) -> int:
+        """The node's template key index for dev_part bits 12-15 (KG_GPU_TMPL_NONE: no templates for its key)."""
+        key = gpu_template_key(node)
+        return self.keys.index(key) if key in self.infos else abi.KG_GPU_TMPL_NONE
+
+    def requests_per_gpu(self, req: Sequence[int], keys: int) -> Dict[str, int]:
+        from .config import DEV_RESOURCES
+        return {DEV_RESOURCES[r]: int(req[r]) for r in range(abi.KG_DEV_R) if (keys >> r) & 1}
+
+    def pod_template(self, rpg: Dict[str, object], shared: bool) -> Tuple[int, int, Dict[str, Dict]]:
+        """(KG_GPU_POD_TEMPLATE or 0, dev_tmpl, candidate templates) of a GPU pod from its requestsPerGPU (resource
+        name -> quantity; requests_per_gpu() of gpu_requirements' vector): a shared request naming one of the
+        matched resources enforces a template (utils.go:540-547) and takes the strictly matched templates as
+        candidates; none at all raises NoMatchedTemplate."""
+        if not shared or not (set(rpg) & self.matched_resources):
+            return 0, 0, {}
+        cands = self.find_matched(rpg, True)
+        if not cands:
+            raise NoMatchedTemplate("no matched GPU shared resource template")
+        tmpl = 0
+        for key, matched in cands.items():
+            tmpl |= min(len(matched), 2) << (2 * self.keys.index(key))
+        return abi.KG_GPU_POD_TEMPLATE, tmpl, cands
+
+    @staticmethod
+    def allocation_template(cands: Dict[str, Dict], node: dict) -> Optional[str]:
+        """appendTemplateInfoToAllocations' name (allocator_gpu.go:144-153): the node key's only candidate, else
+        None (several candidates fall through to the plain allocator without a name)."""
+        matched = cands.get(gpu_template_key(node)) or {}
+        return next(iter(matched)) if len(matched) == 1 else None

@@ -95,6 +95,8 @@ DEV_CODE_REASONS = {
     abi.KG_DEV_CODE_PART_COUNT: "node(s) Unsupported number of GPU requests",
     abi.KG_DEV_CODE_NO_TREE: "node(s) missing GPU Device Topology Tree",
     abi.KG_DEV_CODE_MULTI_SHARED: "node(s) Unsupported Multi-Shared GPU",
+    abi.KG_DEV_CODE_NUMA_SCOPED: "Insufficient NUMA Scoped Devices",
+    abi.KG_DEV_CODE_NO_TEMPLATE: "no matched GPU shared resource template",
 }
 
 

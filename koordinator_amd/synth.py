@@ -132,7 +132,8 @@ GPU_MEM_PER_MINOR = 192 * GI
 N_RSV_CLASSES = 8
 
 
-def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 100, rsv_frac: float = 0.05):
+def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 100, rsv_frac: float = 0.05,
+             numa: str = "none", usage: str = "mixed"):
     """Config 5: configs 1-2's plugins plus DeviceShare (8 GPU minors per node: gpu-core
     100, gpu-memory-ratio 100, gpu-memory 192Gi; minors 40% idle, 30% fully used, 30% partially used),
     Reservation (5% of nodes hold 1-4 reservations of one of 8 owner classes, a third of them reserving
@@ -143,13 +144,21 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     gpu-memory 24Gi). NUMA policy None on every node (the NUMA zone restore of reservations and the
     DeviceShare NUMA hints stay on the host path).
 
+    usage: "mixed" (above) or "u01": each minor's used fraction U(0, 1) (gpu-core / ratio
+    int(100 u), gpu-memory the same percentage), so whole-GPU pods fit only the rare idle minors.
+    numa: "none" (above), "single" (the 20% SingleNUMANode nodes of configs 2-3 kept), or "mix" (own random
+    stream: None 40%, SingleNUMANode / Restricted / BestEffort 20% each, 10% of the pods with a NUMA policy of
+    their own, 5% of the GPU nodes with a GPU whose Topology.NodeID is -1): GPU pods on NUMA-policy nodes join
+    DeviceShare's NUMA hints (deviceshare/topology_hint.go) to the topology manager.
+
     Returns (cfg, nodes, pods, quotas, reservations): nodes already restored to the view of pods that
     match no reservation (decode.reservation_restore), reservations = abi.Reservations."""
     cfg = config5_profile()
     r = _rng(seed_config)
     t = nodes(n_nodes, seed_config, numa=True, rng=r)
     n = n_nodes
-    t["numa_policy"][:] = abi.KG_NUMA_NONE
+    if numa == "none":
+        t["numa_policy"][:] = abi.KG_NUMA_NONE
     # DeviceShare minors
     t["dev_minors"] = np.full(n, abi.KG_DEV_MINORS, np.int32)
     tot = np.zeros((n, abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
@@ -157,7 +166,10 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     tot[:, abi.KG_DEV_RATIO, :] = 100
     tot[:, abi.KG_DEV_MEM, :] = GPU_MEM_PER_MINOR
     state = r.random((n, abi.KG_DEV_MINORS))
-    used_pct = np.where(state < 0.4, 0, np.where(state < 0.7, 100, (r.random((n, abi.KG_DEV_MINORS)) * 20).astype(np.int64) * 5))
+    if usage == "u01":
+        used_pct = (state * 100).astype(np.int64)
+    else:
+        used_pct = np.where(state < 0.4, 0, np.where(state < 0.7, 100, (r.random((n, abi.KG_DEV_MINORS)) * 20).astype(np.int64) * 5))
     free = tot.copy()
     free[:, abi.KG_DEV_CORE, :] -= used_pct
     free[:, abi.KG_DEV_RATIO, :] -= used_pct
@@ -243,11 +255,24 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     p["quota"] = pr.integers(0, n_quotas, n_pods).astype(np.int32)
     p["flags"] |= np.where(pr.random(n_pods) < 0.10, abi.KG_POD_NON_PREEMPTIBLE, 0).astype(np.uint32)
     p["quota_keys"] = quota_keys(p, maxk)
-    gpu_topology5(t, p, seed_config)
+    gpu_topology5(t, p, seed_config, any_numa=numa == "mix")
+    if numa == "mix":
+        rm = _rng(seed_config, 3)
+        t["numa_policy"] = rm.choice([abi.KG_NUMA_NONE, abi.KG_NUMA_SINGLE_NODE, abi.KG_NUMA_RESTRICTED,
+                                      abi.KG_NUMA_BEST_EFFORT], n, p=[0.4, 0.2, 0.2, 0.2]).astype(np.uint32)
+        own = rm.random(n_pods) < 0.10
+        p["numa_policy"] = np.where(own, rm.choice([abi.KG_NUMA_SINGLE_NODE, abi.KG_NUMA_RESTRICTED], n_pods),
+                                    abi.KG_NUMA_NONE).astype(np.uint32)
     return cfg, t, p, q, abi.Reservations(views, infos, devs)
 
 
-def gpu_topology5(t: abi.Table, p: abi.Table, seed_config: int = 5):
+def config5(n_nodes: int = 100_000, n_pods: int = 10_000):
+    """BASELINE config 5 as SURVEY.md §8d states it: cluster5 with per-minor GPU usage U(0, 1) and the 20%
+    SingleNUMANode nodes of configs 2-3 (GPU pods there join DeviceShare's NUMA hints to the topology manager)."""
+    return cluster5(n_nodes, n_pods, numa="single", usage="u01")
+
+
+def gpu_topology5(t: abi.Table, p: abi.Table, seed_config: int = 5, any_numa: bool = False):
     """GPU topology and partitions of a config-5 cluster (own random stream, so the other draws do not
     move): 90% of the nodes report GPU topology (two NUMA nodes of four minors; half of them two GPUs per PCIe
     switch, half one, like the reference's fakeDeviceCR / fakeH800DeviceCR), 30% are labelled H100 (the
@@ -267,6 +292,16 @@ def gpu_topology5(t: abi.Table, p: abi.Table, seed_config: int = 5):
     hop = tabs.add(decode.gpu_partition_table(None, {"metadata": {"labels": {decode.LABEL_GPU_MODEL: "H100"}}})[0])
     t["dev_topo"] = np.where(has, np.where(pair, np.uint64(topos[0]), np.uint64(topos[1])),
                              np.uint64((1 << 64) - 1)).astype(np.uint64)
+    # the GPUs' NUMA node ids (NUMATopology.deviceToNodeID): minors 0-3 on NUMA node 0, 4-7 on node 1
+    numa_ids = decode.gpu_numa([{"minor": m, "topology": {"nodeID": q}} for m, (q, _) in enumerate(layouts[0])])
+    t["dev_numa"] = np.where(has, np.uint32(numa_ids), np.uint32(0xFFFFFFFF)).astype(np.uint32)
+    if any_numa:  # (own stream) minor 7 reports Topology.NodeID -1 on 5% of the GPU nodes
+        ra = _rng(seed_config, 4)
+        anyn = has & (ra.random(n) < 0.05)
+        l2 = [(q if m != 7 else -1, pc) for m, (q, pc) in enumerate(layouts[0])]
+        infos = [{"minor": m, "topology": {"nodeID": q, "pcieID": pc}} for m, (q, pc) in enumerate(l2)]
+        t["dev_topo"] = np.where(anyn, np.uint64(decode.gpu_topology(infos)[0]), t["dev_topo"]).astype(np.uint64)
+        t["dev_numa"] = np.where(anyn, np.uint32(decode.gpu_numa(infos)), t["dev_numa"]).astype(np.uint32)
     t["dev_part"] = (np.where(has, abi.KG_GPU_TREE, 0) | np.where(h100, hop, 0) |
                      np.where(honor, abi.KG_GPU_HONOR, 0)).astype(np.uint32)
     t["gpu_parts"] = tabs.array()

@@ -431,17 +431,55 @@ static void numa_merge_one(uint32_t all, int excl, uint32_t status, const numa_h
     *best = m;
 }
 
+/* The DeviceShare hint provider's answer for one (GPU pod, node) pair (deviceshare/topology_hint.go:40-290):
+ * fail = the provider's status is not a success (code: its KG_ST_* bits, a DeviceShare reason); nopref = no
+ * preference (no Device object, no GPU with a NUMA node: a single preferred nil hint); else the "gpu" hint list
+ * in IterateBitMasks order over the GPUs' NUMA node ids. */
+typedef struct gpu_hints {
+    int fail, nopref, n;
+    uint32_t code;
+    uint32_t mask[15];
+    int pref[15];
+    int64_t score[15];
+} gpu_hints;
+
 /* Policy Merge (policy_single_numa_node.go:69-90, policy_restricted.go:50-62, policy_best_effort.go:48-60).
  * Returns 0 admitted (affinity mask in *mask_out, 0 = none), else a KG_ST_NUMA_* reason. Permutations
- * run cpu-major; the reference iterates Go map order here, which matters only for BestEffort when no
- * merged hint is preferred (parity unpinned there). */
+ * run cpu-major, then memory, then the DeviceShare provider's "gpu" list (providers in plugin order,
+ * NodeNUMAResource before DeviceShare); the reference iterates Go map order over a provider's resources,
+ * which matters only when two merged hints tie on preference, width and score (parity unpinned there).
+ * gh (nullable): the DeviceShare provider's list of a GPU pod (not failed). */
 static uint32_t numa_admit(const kg_config* c, const numa_zones* x, const int64_t* req, const int* has, uint32_t policy,
-                           int excl, uint32_t* mask_out) {
+                           int excl, uint32_t* mask_out, const gpu_hints* gh) {
     numa_lists L;
     numa_hints(c, x, req, has, policy, &L);
     const uint32_t all = (1u << x->Z) - 1u;
     *mask_out = 0;
     if (L.reasons && policy != KG_NUMA_BEST_EFFORT) return KG_ST_NUMA_UNSATISFIED;
+    /* the third list: the provider's hints, or its "no preference" hint (filterProvidersHints, policy.go:145-152) */
+    numa_hint G[15];
+    int ng = 0;
+    if (gh) {
+        if (gh->nopref) {
+            G[ng].mask = 0;
+            G[ng].pref = 1;
+            G[ng].unsat = 0;
+            G[ng++].score = 0;
+        } else {
+            for (int t = 0; t < gh->n; t++) {
+                G[ng].mask = gh->mask[t];
+                G[ng].pref = gh->pref[t];
+                G[ng].unsat = 0;
+                G[ng++].score = gh->score[t];
+            }
+        }
+    }
+    if (policy == KG_NUMA_SINGLE_NODE && gh) { /* filterSingleNumaHints on the gpu list too */
+        int w = 0;
+        for (int t = 0; t < ng; t++)
+            if (G[t].pref && (G[t].mask == 0 || popcount32(G[t].mask) == 1)) G[w++] = G[t];
+        ng = w;
+    }
     if (policy == KG_NUMA_SINGLE_NODE) { /* filterSingleNumaHints */
         for (int li = 0; li < L.n_lists; li++) {
             int w = 0;
@@ -453,17 +491,32 @@ static uint32_t numa_admit(const kg_config* c, const numa_zones* x, const int64_
         }
     }
     numa_hint best = {all, 0, 0, 0};
-    if (L.n_lists == 0) {
+    /* iterateAllProviderTopologyHints (policy.go:262-299) over the lists [cpu,] [memory,] [gpu] */
+    const numa_hint* lists[3];
+    int lens[3], nl = 0;
+    for (int li = 0; li < L.n_lists; li++) {
+        lists[nl] = L.h[li];
+        lens[nl++] = L.len[li];
+    }
+    if (gh) {
+        lists[nl] = G;
+        lens[nl++] = ng;
+    }
+    if (nl == 0) {
         /* no NUMA resource requested: the providers' "no preference" hints */
         numa_merge_one(all, excl, x->status, NULL, 0, &best);
-    } else if (L.n_lists == 1) {
-        for (int a = 0; a < L.len[0]; a++) numa_merge_one(all, excl, x->status, &L.h[0][a], 1, &best);
     } else {
-        for (int a = 0; a < L.len[0]; a++)
-            for (int b = 0; b < L.len[1]; b++) {
-                numa_hint perm[2] = {L.h[0][a], L.h[1][b]};
-                numa_merge_one(all, excl, x->status, perm, 2, &best);
-            }
+        int idx[3] = {0, 0, 0};
+        int empty = 0;
+        for (int t = 0; t < nl; t++) empty |= lens[t] == 0;
+        while (!empty) {
+            numa_hint perm[3];
+            for (int t = 0; t < nl; t++) perm[t] = lists[t][idx[t]];
+            numa_merge_one(all, excl, x->status, perm, nl, &best);
+            int t = nl - 1;
+            while (t >= 0 && ++idx[t] == lens[t]) idx[t--] = 0;
+            if (t < 0) break;
+        }
     }
     if (policy == KG_NUMA_BEST_EFFORT) {
         *mask_out = best.unsat ? all : best.mask;
@@ -478,7 +531,11 @@ static uint32_t numa_admit(const kg_config* c, const numa_zones* x, const int64_
  * that fails: KGO_ZONE_RESERVE_FAIL | KG_ST_NUMA_INSUF_* >> 12 (the ABI's numa_zone codes) */
 #define KGO_ZONE_RESERVE_FAIL 0x20
 static int zone_fails(int32_t z) { return z >= 0x20 && z < 0x40; }
-static uint32_t zone_fail_bits(int32_t z) { return (((uint32_t)z & 7u) << 12) | ((z & 8) ? KG_ST_NUMA_CPUS : 0u); }
+static uint32_t zone_fail_bits(int32_t z) {
+    if (z & 0x10) /* DeviceShare in the Reserve's topology manager: its code, 0xF = Reservation(s) Insufficient gpu devices */
+        return ((z & 0xF) == 0xF) ? KG_ST_DEV_RSV : KG_ST_DEV_MAKE((uint32_t)z & 0xFu);
+    return (((uint32_t)z & 7u) << 12) | ((z & 8) ? KG_ST_NUMA_CPUS : 0u);
+}
 /* the cpuset accumulator finds no CPUs at Reserve (resource_manager.go:385,427 ErrNotEnoughCPUs) */
 #define KGO_ZONE_CPUSET_FAIL (KGO_ZONE_RESERVE_FAIL | 8)
 static int32_t numa_code(uint32_t mask) {
@@ -614,11 +671,35 @@ static uint32_t cpuset_filter(const kg_node_columns* n, uint32_t i, const kg_pod
     return 0;
 }
 
-/* Filter (plugin.go:363-459) + Score (scoring.go:67-151,153-199) of one pair. */
+/* DeviceShare as a NUMA hint provider for a GPU pod (defined with the GPU allocator below). The site: the pair's
+ * reservation view (v, its tables in e) or none. */
+typedef struct numa_gpu_out {
+    const struct kgo_ext* e;
+    const kg_rsv_view* v;
+    int done;      /* the topology manager admitted the pod with DeviceShare's Allocate: its Filter passes */
+    uint32_t mask; /* the stored affinity (0 = nil) DeviceShare's Score and Reserve then use */
+} numa_gpu_out;
+static void gpu_numa_hints(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j,
+                           const numa_gpu_out* gx, gpu_hints* h);
+static uint32_t gpu_alloc_site(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                               uint32_t j, const numa_gpu_out* gx, uint32_t numa, uint32_t* minors);
+#define KGO_ZONE_GPU_FAIL 0x30
+/* the zone code of a DeviceShare failure in the Reserve's topology manager: its code, 0xF for "Reservation(s)
+ * Insufficient gpu devices" */
+static int32_t zone_gpu_fail(uint32_t st) {
+    return KGO_ZONE_GPU_FAIL | (int32_t)((st & KG_ST_DEV_RSV) ? 0xFu : KG_ST_DEV_CODE(st));
+}
+
+/* Filter (plugin.go:363-459) + Score (scoring.go:67-151,153-199) of one pair. gx (nullable): a GPU pod on a
+ * node with a Device object (DeviceShare joins the topology manager: topology_hint.go:40-290, manager.go:65-154). */
 static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t i, const kgo_over* ov,
-                          const kg_pod_columns* p, uint32_t j, int64_t* score_out, int32_t* zone_out) {
+                          const kg_pod_columns* p, uint32_t j, int64_t* score_out, int32_t* zone_out, numa_gpu_out* gx) {
     *score_out = 0;
     *zone_out = -1;
+    if (gx) {
+        gx->done = 0;
+        gx->mask = 0;
+    }
     if (p->flags[j] & KG_POD_NUMA_SKIP) return 0; /* PreFilter Skip: no Filter, no Score */
     int conflict;
     uint32_t policy = numa_merge_policy(n->numa_policy[i], p->numa_policy[j], &conflict);
@@ -681,7 +762,18 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
             *zone_out = KGO_ZONE_RESERVE_FAIL | (int32_t)(KG_ST_NUMA_INSUF_NODE >> 12);
             return 0;
         }
-        numa_admit(c, &x, req, has, policy, excl, &mask);
+        /* a GPU pod: the DeviceShare provider's hints join the merge; a provider failure fails the Reserve
+         * (accumulateProvidersHints -> Admit, manager.go:80-87), so does DeviceShare's Allocate under the best hint
+         * (allocateResources, after the NUMA allocation) */
+        gpu_hints gh;
+        if (gx) {
+            gpu_numa_hints(c, n, i, p, j, gx, &gh);
+            if (gh.fail) {
+                *zone_out = zone_gpu_fail(gh.code);
+                return 0;
+            }
+        }
+        numa_admit(c, &x, req, has, policy, excl, &mask, gx ? &gh : NULL);
         int64_t al[2][KG_MAX_ZONES];
         int32_t fail = 0;
         for (int r = 0; r < 2 && mask; r++) {
@@ -689,13 +781,30 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
             if (one[r] && !numa_split(&x, mask, req, one, al)) fail |= 1 << r;
         }
         *zone_out = fail ? KGO_ZONE_RESERVE_FAIL | fail : numa_code(mask);
+        if (!fail && gx) {
+            uint32_t minors;
+            const uint32_t st = gpu_alloc_site(c, n, i, p, j, gx, mask, &minors);
+            if (st) *zone_out = zone_gpu_fail(st);
+        }
         return 0;
     }
     if (x.Z == 0) return KG_ST_NUMA_NO_RES;
-    uint32_t st = numa_admit(c, &x, req, has, policy, excl, &mask);
+    gpu_hints gh;
+    if (gx) {
+        gpu_numa_hints(c, n, i, p, j, gx, &gh);
+        if (gh.fail) return gh.code; /* the provider's status (manager.go:80-87) */
+    }
+    uint32_t st = numa_admit(c, &x, req, has, policy, excl, &mask, gx ? &gh : NULL);
     if (st) return st;
     int64_t al[2][KG_MAX_ZONES];
     if (mask && !numa_split(&x, mask, req, has, al)) return KG_ST_UNSUPPORTED; /* not reached: preferred hints place */
+    if (gx) { /* allocateResources: DeviceShare's Allocate under the best hint (topology_hint.go:100-157) */
+        uint32_t minors;
+        const uint32_t st2 = gpu_alloc_site(c, n, i, p, j, gx, mask, &minors);
+        if (st2) return st2;
+        gx->done = 1;
+        gx->mask = mask;
+    }
     *zone_out = numa_code(mask);
     if (!mask) {
         /* calculateAllocatableAndRequested without NUMA allocation: node allocatable / requested */
@@ -725,7 +834,7 @@ void kgo_eval_pair(const kg_config* c, const kg_node_columns* n, uint32_t i, con
     int32_t zone = -1;
     if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(c, n, i, NULL, p, j);
     if (c->plugins & KG_PLUGIN_LA) st |= la_filter(c, n, i, p, j);
-    if (c->plugins & KG_PLUGIN_NUMA) st |= numa_eval(c, n, i, NULL, p, j, &s_numa, &zone);
+    if (c->plugins & KG_PLUGIN_NUMA) st |= numa_eval(c, n, i, NULL, p, j, &s_numa, &zone, NULL);
     out->status = st;
     /* Score functions are defined for every node (the Go ScorePlugin.Score can be called on any
      * node); the NUMA score exists only where its Filter admitted the pod (it needs the hint). */
@@ -831,7 +940,7 @@ static void par_run(par_job* jb) {
                 int64_t s = 0;
                 int32_t z = -1;
                 if (jb->c->plugins & KG_PLUGIN_NUMA) {
-                    st |= numa_eval(jb->c, jb->n, i, NULL, jb->p, jb->pod, &s, &z);
+                    st |= numa_eval(jb->c, jb->n, i, NULL, jb->p, jb->pod, &s, &z, NULL);
                     jb->total[i] = s; /* NUMA score is produced by the same resource-manager walk */
                 }
                 jb->zone[i] = st ? -1 : z;
@@ -982,8 +1091,9 @@ struct kgo_state {
     double* amp;
     int32_t* dev_minors;          /* DeviceShare (NULL when the snapshot has no device tables) */
     int64_t *dev_total, *dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
-    uint64_t* dev_topo;            /* GPU topology / partition tables (static) */
+    uint64_t* dev_topo;            /* GPU topology / partition tables / GPU NUMA nodes (static) */
     uint32_t* dev_part;
+    uint32_t* dev_numa;
     kg_gpu_partition* gpu_parts;
     uint32_t n_gpu_parts;
     /* cpuset binding (NULL when no node has a CPU topology) */
@@ -1056,6 +1166,10 @@ kgo_state* kgo_state_new(const kg_node_columns* s, uint32_t n) {
             st->dev_topo = (uint64_t*)calloc(n ? n : 1, 8);
             memcpy(st->dev_topo, s->dev_topo, 8 * (size_t)n);
         }
+        if (s->dev_numa) {
+            st->dev_numa = (uint32_t*)calloc(n ? n : 1, 4);
+            memcpy(st->dev_numa, s->dev_numa, 4 * (size_t)n);
+        }
         if (s->dev_part) {
             st->dev_part = (uint32_t*)calloc(n ? n : 1, 4);
             memcpy(st->dev_part, s->dev_part, 4 * (size_t)n);
@@ -1097,6 +1211,7 @@ void kgo_state_free(kgo_state* st) {
     free(st->dev_minors);
     free(st->dev_topo);
     free(st->dev_part);
+    free(st->dev_numa);
     free(st->gpu_parts);
     free(st->dev_total);
     free(st->dev_free);
@@ -1152,6 +1267,7 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
     v->dev_free = st->dev_free;
     v->dev_topo = st->dev_topo;
     v->dev_part = st->dev_part;
+    v->dev_numa = st->dev_numa;
     v->gpu_parts = st->gpu_parts;
     v->n_gpu_parts = st->n_gpu_parts;
     v->cpu_topo = st->cpu_topo;
@@ -1384,6 +1500,7 @@ typedef struct gpu_req {
     int64_t preq[KG_DEV_R];
     uint32_t keys, n, flags;
     int64_t ring_bw;
+    uint32_t tmpl; /* candidate template counts per key (kg_pod_columns.dev_tmpl) */
 } gpu_req;
 
 static void gpu_req_of(const kg_pod_columns* p, uint32_t j, gpu_req* g) {
@@ -1391,6 +1508,7 @@ static void gpu_req_of(const kg_pod_columns* p, uint32_t j, gpu_req* g) {
     g->n = p->dev_count ? p->dev_count[j] : 0;
     g->flags = p->dev_flags ? p->dev_flags[j] : 0;
     g->ring_bw = (g->flags & KG_GPU_POD_RING_BW) && p->dev_ring_bw ? p->dev_ring_bw[j] : 0;
+    g->tmpl = (g->flags & KG_GPU_POD_TEMPLATE) && p->dev_tmpl ? p->dev_tmpl[j] : 0;
 }
 
 #define TAB(t, r, m) ((t)[(size_t)(r) * KG_DEV_MINORS + (size_t)(m)])
@@ -1659,9 +1777,8 @@ static uint32_t default_allocate(const kg_config* c, const int64_t* T, const int
     return 0;
 }
 
-/* GPUAllocator.Allocate: allocateByTemplate (not restated: template pods are flagged by the caller), then
- * allocateByPartition, then generalAllocate = allocateByDeviceTopology, then defaultAllocateDevices.
- * Returns 0 with the minors, or a KG_DEV_CODE_*. */
+/* GPUAllocator.Allocate: allocateByTemplate, then allocateByPartition, then generalAllocate =
+ * allocateByDeviceTopology, then defaultAllocateDevices. Returns 0 with the minors, or a KG_DEV_CODE_*. */
 static uint32_t gpu_allocate(const kg_config* c, const kg_node_columns* n, uint32_t i, const int64_t* T,
                              const int64_t* F, int32_t D, uint32_t outside, const gpu_req* g, uint32_t* mask) {
     *mask = 0;
@@ -1674,8 +1791,18 @@ static uint32_t gpu_allocate(const kg_config* c, const kg_node_columns* n, uint3
     const int honor = (g->flags & KG_GPU_POD_HONOR) || (part & KG_GPU_HONOR);
     const uint32_t used = used_minors_hash(T, F, D, outside);
     const uint32_t total = total_minors_hash(T, D);
+    /* allocateByTemplate (:135-159): the pod's candidate templates under the node's vendor-model key; none
+     * fails, exactly one goes straight to generalAllocate (the template name only annotates the allocation),
+     * several fall through (the volcano-style choice is a TODO in the reference) */
+    int by_template = 0;
+    if (g->flags & KG_GPU_POD_TEMPLATE) {
+        const uint32_t key = (part >> KG_GPU_TMPL_SHIFT) & 15u;
+        const uint32_t cand = key == KG_GPU_TMPL_NONE ? 0u : (g->tmpl >> (2 * key)) & 3u;
+        if (cand == 0) return KG_DEV_CODE_NO_TEMPLATE;
+        by_template = cand == 1;
+    }
     /* allocateByPartition: shared GPUs skip it; a failure stands only when partitions are honored */
-    if (!shared) {
+    if (!shared && !by_template) {
         uint32_t code = allocate_by_partition(n, part & 0xFFu, g, used, total, mask);
         if (code == 0) return 0;
         if (honor) return code;
@@ -1713,7 +1840,6 @@ static uint32_t dev_eval(const kg_config* c, const kg_node_columns* n, uint32_t 
     int32_t D = n->dev_minors ? n->dev_minors[i] : -1;
     if (D < 0) return 0;                                    /* no Device object: pass, Score 0 */
     if (D == 0) return KG_ST_DEV_NO_DEVICE;                 /* devicehandler_gpu.go:41-44 */
-    if (g.flags & KG_GPU_POD_TEMPLATE) return KG_ST_UNSUPPORTED; /* allocateByTemplate: host path */
     const int64_t* T = &DEVX(n->dev_total, i, 0, 0);
     const int64_t* F = &DEVX(n->dev_free, i, 0, 0);
     uint32_t mask;
@@ -1727,6 +1853,218 @@ static uint32_t dev_eval(const kg_config* c, const kg_node_columns* n, uint32_t 
         }
     *raw = dev_least(c, Ts, Fs, g.preq);
     return 0;
+}
+
+/* ---- DeviceShare under a NUMA affinity (topology_hint.go:40-290; AutopilotAllocator.filterNodeDevice,
+ *      device_allocator.go:143-176; nodeDevice.filter, device_cache.go:367-415) ----------------------------- */
+
+static uint32_t gpu_numa_nib(const kg_node_columns* n, uint32_t i, int m) {
+    return n->dev_numa ? (n->dev_numa[i] >> (4 * m)) & 0xFu : KG_GPU_NUMA_NONE;
+}
+
+/* the minors filterNodeDevice keeps under a NUMA affinity (bit per NUMA node id): a Topology whose NodeID is -1
+ * or in the affinity (device_allocator.go:155-159) */
+static uint32_t gpu_numa_allowed(const kg_node_columns* n, uint32_t i, int32_t D, uint32_t numa) {
+    uint32_t a = 0;
+    for (int32_t m = 0; m < D && m < KG_DEV_MINORS; m++) {
+        const uint32_t q = gpu_numa_nib(n, i, m);
+        if (q == KG_GPU_NUMA_ANY || (q < KG_GPU_NUMA_ANY && ((numa >> q) & 1u))) a |= 1u << m;
+    }
+    return a;
+}
+
+/* The allocator on one table under NUMA affinity `numa` (0 = nil): the node's own devices (t == NULL; unfiltered
+ * when numa is 0) or a reservation restore table (kg_rsv_dev, already a filtered nodeDevice). The filtered nodeDevice
+ * keeps the table's minors the affinity allows; getRealUsed (allocator_gpu.go:59-70) counts the node's used minors it
+ * leaves out. Returns 0 with the minors, or a KG_DEV_CODE_*. */
+static uint32_t gpu_alloc_tab_numa(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                                   uint32_t j, const kg_rsv_dev* t, uint32_t numa, uint32_t* minors) {
+    gpu_req g;
+    gpu_req_of(p, j, &g);
+    const int32_t D = n->dev_minors[i];
+    const int64_t* NT = &DEVX(n->dev_total, i, 0, 0);
+    const int64_t* NF = &DEVX(n->dev_free, i, 0, 0);
+    *minors = 0;
+    if (D == 0) return KG_DEV_CODE_NO_DEVICE; /* Prepare: no GPU on the Device (devicehandler_gpu.go:41-44) */
+    if (!t && !numa) return gpu_allocate(c, n, i, NT, NF, D, 0u, &g, minors);
+    const int64_t* T = t ? &t->total[0][0] : NT;
+    const int64_t* F = t ? &t->free[0][0] : NF;
+    const uint32_t allowed = numa ? gpu_numa_allowed(n, i, D, numa) : (D >= 32 ? ~0u : (1u << D) - 1u);
+    int64_t T2[KG_DEV_R * KG_DEV_MINORS], F2[KG_DEV_R * KG_DEV_MINORS];
+    uint32_t outside = 0;
+    for (int m = 0; m < KG_DEV_MINORS; m++) {
+        int in_tab = !t, node_used = 0;
+        for (int r = 0; r < KG_DEV_R; r++) {
+            if (t) in_tab |= TAB(T, r, m) != 0;
+            if (m < D) node_used |= TAB(NF, r, m) != TAB(NT, r, m);
+        }
+        const int in = m < D && ((allowed >> m) & 1u) && in_tab;
+        for (int r = 0; r < KG_DEV_R; r++) {
+            TAB(T2, r, m) = in ? TAB(T, r, m) : 0;
+            TAB(F2, r, m) = in ? TAB(F, r, m) : 0;
+        }
+        if (node_used && !in) outside |= 1u << m;
+    }
+    return gpu_allocate(c, n, i, T2, F2, D, outside, &g, minors);
+}
+
+/* DeviceShare's allocation for the pair under NUMA affinity `numa`: off views the node's devices; on a view
+ * tryAllocateFromReusable over the matched reservations reserving GPUs in view order (deviceshare/reservation.go
+ * :344-410), then, unless the pod requires a reservation ("Reservation(s) Insufficient gpu devices"), the allocation
+ * outside them (the view's base table). 0 with the minors, or the status bits. */
+static uint32_t gpu_alloc_site(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                               uint32_t j, const numa_gpu_out* gx, uint32_t numa, uint32_t* minors) {
+    const kg_rsv_view* v = gx ? gx->v : NULL;
+    uint32_t code;
+    if (!v) {
+        code = gpu_alloc_tab_numa(c, n, i, p, j, NULL, numa, minors);
+        return code ? KG_ST_DEV_MAKE(code) : 0u;
+    }
+    if (n->dev_minors[i] == 0) return KG_ST_DEV_NO_DEVICE;
+    int any = 0;
+    for (uint32_t t = 0; t < v->count; t++) {
+        const int32_t di = gx->e->infos[v->first + t].dev;
+        if (di < 0) continue;
+        any = 1;
+        if (!gpu_alloc_tab_numa(c, n, i, p, j, &gx->e->devs[di], numa, minors)) return 0;
+    }
+    if (any && (p->flags[j] & KG_POD_RSV_REQUIRED)) return KG_ST_DEV_RSV;
+    code = gpu_alloc_tab_numa(c, n, i, p, j, v->dev_base >= 0 ? &gx->e->devs[v->dev_base] : NULL, numa, minors);
+    return code ? KG_ST_DEV_MAKE(code) : 0u;
+}
+
+/* AutopilotAllocator.score (device_allocator.go:486-508) on a table under NUMA affinity `numa`: scoreNode over the
+ * filtered devices' sums; 0 when the filter drops the GPU type (no free left in the table; the node's unfiltered
+ * devices without an affinity skip that check). t == NULL: the node's devices. */
+static int64_t gpu_score_tab_numa(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                                  uint32_t j, const kg_rsv_dev* t, uint32_t numa) {
+    gpu_req g;
+    gpu_req_of(p, j, &g);
+    const int32_t D = n->dev_minors[i];
+    const int64_t* T = t ? &t->total[0][0] : &DEVX(n->dev_total, i, 0, 0);
+    const int64_t* F = t ? &t->free[0][0] : &DEVX(n->dev_free, i, 0, 0);
+    const int Dt = t ? KG_DEV_MINORS : D;
+    const uint32_t allowed = numa ? gpu_numa_allowed(n, i, D, numa) : ~0u;
+    int64_t Ts[KG_DEV_R] = {0, 0, 0}, Fs[KG_DEV_R] = {0, 0, 0};
+    int any = 0;
+    for (int m = 0; m < Dt; m++)
+        for (int r = 0; r < KG_DEV_R; r++) {
+            any |= TAB(F, r, m) != 0;
+            if (!((allowed >> m) & 1u)) continue;
+            Ts[r] += TAB(T, r, m);
+            Fs[r] += TAB(F, r, m);
+        }
+    if ((t || numa) && !any) return 0;
+    return dev_least(c, Ts, Fs, g.preq);
+}
+
+/* DeviceShare's Score of a feasible pair (scoring.go:45-104): on a view the nominated reservation's table (0 when it
+ * reserves no GPU, scoreWithNominatedReservation) or the base table, off views the node's devices; under the stored
+ * NUMA affinity. */
+static int64_t gpu_score_site(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                              uint32_t j, const kgo_ext* e, const kg_rsv_view* v, uint32_t numa, int nom) {
+    if (!v) return gpu_score_tab_numa(c, n, i, p, j, NULL, numa);
+    if (nom >= 0) {
+        const int32_t di = e->infos[v->first + (uint32_t)nom].dev;
+        return di >= 0 ? gpu_score_tab_numa(c, n, i, p, j, &e->devs[di], numa) : 0;
+    }
+    return gpu_score_tab_numa(c, n, i, p, j, v->dev_base >= 0 ? &e->devs[v->dev_base] : NULL, numa);
+}
+
+/* AutopilotAllocator.Allocate of the pod's GPUs on the node's own devices under NUMA affinity `numa` (Reserve). */
+static uint32_t gpu_alloc_numa(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                               uint32_t j, uint32_t numa, uint32_t* minors) {
+    return gpu_alloc_tab_numa(c, n, i, p, j, NULL, numa, minors);
+}
+
+/* GetPodTopologyHints -> generateTopologyHints (topology_hint.go:40-66,159-280): per NUMA mask over the GPUs' NUMA
+ * node ids (IterateBitMasks order), the GPUs inside must number the request ("Insufficient NUMA Scoped Devices") and
+ * DeviceShare's allocation at the pair's site must succeed under the mask; Preferred = the narrowest feasible width,
+ * Score 500 when the allocation equals the full mask's (hashAllocateResult). The full mask's failure is the provider's
+ * status even when narrower masks fit (:191-196,271-279). */
+static void gpu_numa_hints(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j,
+                           const numa_gpu_out* gx, gpu_hints* h) {
+    memset(h, 0, sizeof(*h));
+    gpu_req g;
+    gpu_req_of(p, j, &g);
+    const int32_t D = n->dev_minors ? n->dev_minors[i] : -1;
+    if (D < 0) { /* no nodeDevice: nil hints */
+        h->nopref = 1;
+        return;
+    }
+    uint32_t idset = 0;
+    for (int32_t m = 0; m < D && m < KG_DEV_MINORS; m++) {
+        const uint32_t q = gpu_numa_nib(n, i, m);
+        if (q < KG_GPU_NUMA_ANY) idset |= 1u << q;
+    }
+    if (!idset) { /* numaTopology.nodes is empty: no mask is iterated, the hints map stays empty */
+        h->nopref = 1;
+        return;
+    }
+    int ids[8], gn = 0;
+    for (int q = 0; q < 8; q++)
+        if ((idset >> q) & 1u) ids[gn++] = q;
+    const uint8_t* km = NUMA_MASKS[gn - 1];
+    uint32_t best_alloc = 0, full_st = 0, feas[15], allocs[15];
+    int minsize = gn, nf = 0;
+    for (uint32_t k = 0; k < NUMA_NMASKS[gn - 1]; k++) {
+        uint32_t m = 0;
+        for (int b = 0; b < gn; b++)
+            if ((km[k] >> b) & 1u) m |= 1u << ids[b];
+        const int full = popcount32(km[k]) == gn;
+        uint32_t cnt = 0;
+        for (int32_t mi = 0; mi < D && mi < KG_DEV_MINORS; mi++) {
+            const uint32_t q = gpu_numa_nib(n, i, mi);
+            if (q < KG_GPU_NUMA_ANY && ((m >> q) & 1u)) cnt++;
+        }
+        if (cnt < g.n) { /* calcTotalDevicesByNUMA */
+            if (full) full_st = KG_ST_DEV_MAKE(KG_DEV_CODE_NUMA_SCOPED);
+            continue;
+        }
+        uint32_t alloc;
+        const uint32_t st = gpu_alloc_site(c, n, i, p, j, gx, m, &alloc);
+        if (st) {
+            if (full) full_st = st;
+            continue;
+        }
+        if (full) best_alloc = alloc;
+        if (popcount32(m) < minsize) minsize = popcount32(m);
+        feas[nf] = m;
+        allocs[nf++] = alloc;
+    }
+    if (full_st || nf == 0) {
+        h->fail = 1;
+        h->code = full_st ? full_st : KG_ST_DEV_MAKE(KG_DEV_CODE_NUMA_SCOPED);
+        return;
+    }
+    h->n = nf;
+    for (int t = 0; t < nf; t++) {
+        h->mask[t] = feas[t];
+        h->pref[t] = popcount32(feas[t]) == minsize;
+        h->score[t] = allocs[t] == best_alloc ? 500 : 0; /* defaultNUMAScore */
+    }
+}
+
+/* kgo_gpu_numa_hints (tests): the provider's answer off reservation views as 0 = hints (n, masks, pref, scores),
+ * 1 = no preference, 2 = failure (*code = the KG_DEV_CODE_* of its status). */
+int kgo_gpu_numa_hints(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j,
+                       int* n_out, uint32_t* masks, int* pref, int64_t* scores, uint32_t* code) {
+    gpu_hints h;
+    gpu_numa_hints(c, n, i, p, j, NULL, &h);
+    *n_out = h.n;
+    *code = KG_ST_DEV_CODE(h.code);
+    for (int t = 0; t < h.n; t++) {
+        masks[t] = h.mask[t];
+        pref[t] = h.pref[t];
+        scores[t] = h.score[t];
+    }
+    return h.fail ? 2 : h.nopref ? 1 : 0;
+}
+
+/* kgo_gpu_alloc_numa (tests): DeviceShare's Allocate under a NUMA affinity (topology_hint.go:100-157). */
+uint32_t kgo_gpu_alloc_numa(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j,
+                            uint32_t numa, uint32_t* minors) {
+    return gpu_alloc_numa(c, n, i, p, j, numa, minors);
 }
 
 /* minors used on node i (free != total) that a restore table leaves out (total 0 everywhere) */
@@ -1760,7 +2098,6 @@ static uint32_t dev_eval_tab(const kg_config* c, const kg_node_columns* n, uint3
             any |= t->free[r][m] != 0;
         }
     *raw = any ? dev_least(c, T, F, g.preq) : 0;
-    if (g.flags & KG_GPU_POD_TEMPLATE) return KG_ST_UNSUPPORTED;
     uint32_t mask;
     return dev_code_status(gpu_allocate(c, n, i, &t->total[0][0], &t->free[0][0], D, outside_used(n, i, t, D), &g, &mask));
 }
@@ -1787,15 +2124,18 @@ static uint32_t dev_filter_view(const kg_config* c, const kg_node_columns* n, ui
     return dev_eval(c, n, i, p, j, &raw);
 }
 
-/* Reserve-time minors: the allocation GPUAllocator.Allocate makes on node i (0 when it fails). */
+/* Reserve-time minors: the allocation GPUAllocator.Allocate makes on node i (0 when it fails), inside the NUMA
+ * affinity the topology manager stored for the pair (DeviceShare Reserve, plugin.go:585-600): the zone code of
+ * the NodeNUMAResource allocation (-1 = nil affinity). */
 static uint32_t dev_choose(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
-                           uint32_t j) {
+                           uint32_t j, int32_t zone) {
     gpu_req g;
     gpu_req_of(p, j, &g);
     int32_t D = n->dev_minors ? n->dev_minors[i] : -1;
     if (g.n == 0 || D <= 0) return 0;
     uint32_t mask;
-    const uint32_t code = gpu_allocate(c, n, i, &DEVX(n->dev_total, i, 0, 0), &DEVX(n->dev_free, i, 0, 0), D, 0u, &g, &mask);
+    const uint32_t numa = (zone >= 0 && !zone_fails(zone)) ? numa_code_mask(zone) : 0u;
+    const uint32_t code = gpu_alloc_numa(c, n, i, p, j, numa, &mask);
     return code ? 0u : mask;
 }
 
@@ -2194,22 +2534,28 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
         int32_t zone = -1;
         if (c->plugins & KG_PLUGIN_NRF) st |= nrf_filter(c, n, i, ovp, p, j);
         if (c->plugins & KG_PLUGIN_LA) st |= la_filter(c, n, i, p, j);
+        /* a GPU pod on a node with a Device object: DeviceShare is a NUMA hint provider there, at the pair's site
+         * (its reservation view, if any). On a reservation view the
+         * NodeNUMAResource restore (nodenumaresource/reservation.go:188-270) keeps only reservations whose reserve pod
+         * holds a NUMA or cpuset allocation; kg_rsv_info describes none, so the plugin runs on the node's zones with
+         * the view's NodeInfo. */
+        const int gpu_numa = gpu_pod && n->dev_minors && n->dev_minors[i] >= 0;
+        numa_gpu_out gx = {e, v, 0, 0};
+        uint32_t numa_st = 0;
         if (c->plugins & KG_PLUGIN_NUMA) {
-            const int binds = (p->flags[j] & KG_POD_CPU_BIND) ||
-                              (n->cpu_bind_policy && n->cpu_bind_policy[i] != KG_NODE_CPU_BIND_NONE);
-            if (v && (n->numa_policy[i] != KG_NUMA_NONE || binds) && !(p->flags[j] & KG_POD_NUMA_SKIP))
-                st |= KG_ST_UNSUPPORTED; /* NUMA zone / cpuset restore of reservations: host path */
-            else
-                st |= numa_eval(c, n, i, ovp, p, j, &s_numa, &zone);
+            numa_st = numa_eval(c, n, i, ovp, p, j, &s_numa, &zone, gpu_numa ? &gx : NULL);
+            st |= numa_st;
         }
         int64_t dev_raw = 0;
         const int dev_view = gpu_pod && v;
-        if (c->plugins & KG_PLUGIN_DEV)
-            st |= dev_view ? dev_filter_view(c, n, i, p, j, e, v) : dev_eval(c, n, i, p, j, &dev_raw);
-        /* GPU pods under a NUMA policy (DeviceShare joins the NUMA hint merge, topology_hint.go): host path */
-        if (gpu_pod && (c->plugins & KG_PLUGIN_NUMA) &&
-            (n->numa_policy[i] != KG_NUMA_NONE || p->numa_policy[j] != KG_NUMA_NONE))
-            st |= KG_ST_UNSUPPORTED;
+        if (c->plugins & KG_PLUGIN_DEV) {
+            if (gx.done) { /* the topology manager stored an affinity: DeviceShare's Filter passes (plugin.go:369-374) */
+            } else {
+                const uint32_t ds = dev_view ? dev_filter_view(c, n, i, p, j, e, v) : dev_eval(c, n, i, p, j, &dev_raw);
+                /* NodeNUMAResource failed with DeviceShare's own reason (its hints or its Allocate): one code */
+                st |= (numa_st & KG_ST_DEV_MASK) ? (ds & ~(uint32_t)KG_ST_DEV_MASK) : ds;
+            }
+        }
         rsv_ctx x;
         if (c->plugins & KG_PLUGIN_RSV) {
             rsv_ctx_init(&x, c, n, i, v, e ? e->infos : NULL, p, j);
@@ -2224,21 +2570,11 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
         o->dev[i] = dev_raw;
         int nom = -1;
         if ((c->plugins & KG_PLUGIN_RSV) && v) o->rsv[i] = rsv_nominate_score(&x, &o->order[i], &nom);
-        if (dev_view) {
-            /* DeviceShare Score (scoring.go:77-103): the nominated reservation's table (0 when it reserves no
-             * GPU: scoreWithNominatedReservation, reservation.go:492-520), else the view's base table */
-            int32_t D = n->dev_minors[i];
-            int64_t raw = 0;
-            if (nom >= 0) {
-                int32_t di = e->infos[v->first + (uint32_t)nom].dev;
-                if (di >= 0) dev_eval_tab(c, n, i, &e->devs[di], D, p, j, &raw);
-            } else if (v->dev_base >= 0) {
-                dev_eval_tab(c, n, i, &e->devs[v->dev_base], D, p, j, &raw);
-            } else {
-                dev_eval(c, n, i, p, j, &raw);
-            }
-            o->dev[i] = raw;
-        }
+        if ((c->plugins & KG_PLUGIN_DEV) && (dev_view || gx.done))
+            /* DeviceShare Score (scoring.go:45-104): the nominated reservation's table (0 when it reserves no GPU:
+             * scoreWithNominatedReservation, reservation.go:492-520), else the view's base table; under the stored
+             * NUMA affinity */
+            o->dev[i] = gpu_score_site(c, n, i, p, j, e, v, gx.done ? gx.mask : 0u, nom);
     }
 }
 
@@ -2452,7 +2788,7 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
             int64_t preq[KG_DEV_R];
             uint32_t keys;
             dev_pod_req(p, j, preq, &keys);
-            uint32_t mask = dev_choose(c, &v, i, p, j);
+            uint32_t mask = dev_choose(c, &v, i, p, j, best_zone);
             dev_apply(st->dev_total, st->dev_free, i, mask, preq, keys, 1);
             if (out_minors) out_minors[j] = mask;
         }
@@ -2549,7 +2885,7 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                 dev_pod_req(p, j, preq, &keys);
                 kg_node_columns nv;
                 kgo_state_view(st, &nv);
-                uint32_t mask = dev_choose(c, &nv, (uint32_t)node, p, j);
+                uint32_t mask = dev_choose(c, &nv, (uint32_t)node, p, j, zone);
                 dev_apply(st->dev_total, st->dev_free, (uint32_t)node, mask, preq, keys, 1);
                 out_minors[j] = mask;
             }

@@ -113,6 +113,15 @@ int kgo_take_preferred_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t av
                             const kg_cpu_alloc* allocated, int needed, int bind_policy, int excl_policy, int strategy,
                             uint64_t out[4]);
 
+/* DeviceShare as a NUMA hint provider (deviceshare/topology_hint.go:40-290) for pod j on node i: 0 = a hint
+ * list (n_out entries of NUMA masks, Preferred, Score), 1 = no preference, 2 = the provider fails (*code =
+ * KG_DEV_CODE_*). masks / pref / scores hold up to 15 entries. */
+int kgo_gpu_numa_hints(const kg_config* cfg, const kg_node_columns* nodes, uint32_t node, const kg_pod_columns* pods,
+                       uint32_t pod, int* n_out, uint32_t* masks, int* pref, int64_t* scores, uint32_t* code);
+/* DeviceShare's Allocate under a NUMA affinity (bit per NUMA node id, 0 = nil): 0 + minors, or KG_DEV_CODE_*. */
+uint32_t kgo_gpu_alloc_numa(const kg_config* cfg, const kg_node_columns* nodes, uint32_t node, const kg_pod_columns* pods,
+                            uint32_t pod, uint32_t numa, uint32_t* minors);
+
 /* Helpers shared with tests. */
 int64_t kgo_amplify(int64_t origin, double ratio);
 int64_t kgo_la_usage_percent(int64_t estimated, int64_t total);

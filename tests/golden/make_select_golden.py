@@ -4,7 +4,7 @@ BASELINE configurations that are evaluated in matrix mode:
 
   config 2  synth.cluster(2):  10k nodes x 10k pods, NodeResourcesFit + LoadAware + NodeNUMAResource
   config 4  synth.cluster(4):  100k nodes x 10k pods, same plugins
-  config 5  synth.cluster5(100_000, 10_000): + DeviceShare, Reservation, ElasticQuota
+  config 5  synth.config5(): + DeviceShare, Reservation, ElasticQuota
   config 6  synth.mixed():     config 2 with Restricted / BestEffort nodes, node CPU bind policies and LSR
                                (cpuset-binding) pods (bench config 6)
 
@@ -40,7 +40,7 @@ def path(config: int) -> str:
 def workload(config: int):
     """(kg_config, nodes, pods, quotas, reservations) of a matrix-mode configuration."""
     if config == 5:
-        cfg, nodes, pods, quotas, rsv = synth.cluster5(100_000, 10_000)
+        cfg, nodes, pods, quotas, rsv = synth.config5()
         return cfg.kg_config(), nodes, pods, quotas, rsv
     if config == 6:
         cfg, nodes, pods = synth.mixed()

@@ -104,6 +104,12 @@ def lib():
                                            P(abi.KgPodColumns), C.c_uint32, P(KgoExt), P(C.c_uint32), P(C.c_uint32),
                                            P(C.c_uint64), C.c_uint32, P(C.c_uint64)]
         L.kgo_ext_shard_select.restype = C.c_int
+        L.kgo_gpu_numa_hints.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns),
+                                         C.c_uint32, P(C.c_int), P(C.c_uint32), P(C.c_int), P(C.c_int64), P(C.c_uint32)]
+        L.kgo_gpu_numa_hints.restype = C.c_int
+        L.kgo_gpu_alloc_numa.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns),
+                                         C.c_uint32, C.c_uint32, P(C.c_uint32)]
+        L.kgo_gpu_alloc_numa.restype = C.c_uint32
         L.kgo_mem_bytes_to_ratio.argtypes = [C.c_int64, C.c_int64]
         L.kgo_mem_bytes_to_ratio.restype = C.c_int64
         L.kgo_amplify.argtypes = [C.c_int64, C.c_double]
@@ -172,6 +178,32 @@ def ext_verify(cfg, nodes: abi.Table, pods: abi.Table, quotas=None, rsv=None) ->
     nc, pc, vo, e = abi.node_columns(nodes), abi.pod_columns(pods), res.struct(), make_ext(quotas, rsv)
     assert lib().kgo_ext_verify(C.byref(cfg), C.byref(nc), nn, C.byref(pc), np_, C.byref(e), C.byref(vo)) == 0
     return res
+
+
+def gpu_numa_hints(cfg, nodes: abi.Table, pods: abi.Table, node: int = 0, pod: int = 0):
+    """DeviceShare's NUMA hint provider (kgo_gpu_numa_hints): ("hints", [(mask, preferred, score)]),
+    ("nopref", None) or ("fail", KG_DEV_CODE_*)."""
+    nc, pc = abi.node_columns(nodes), abi.pod_columns(pods)
+    n = C.c_int(0)
+    code = C.c_uint32(0)
+    masks, pref, scores = np.zeros(15, np.uint32), np.zeros(15, np.int32), np.zeros(15, np.int64)
+    P = C.POINTER
+    r = lib().kgo_gpu_numa_hints(C.byref(cfg), C.byref(nc), node, C.byref(pc), pod, C.byref(n),
+                                 masks.ctypes.data_as(P(C.c_uint32)), pref.ctypes.data_as(P(C.c_int)),
+                                 scores.ctypes.data_as(P(C.c_int64)), C.byref(code))
+    if r == 2:
+        return "fail", int(code.value)
+    if r == 1:
+        return "nopref", None
+    return "hints", [(int(masks[t]), bool(pref[t]), int(scores[t])) for t in range(n.value)]
+
+
+def gpu_alloc_numa(cfg, nodes: abi.Table, pods: abi.Table, numa: int, node: int = 0, pod: int = 0):
+    """DeviceShare's Allocate under a NUMA affinity: (KG_DEV_CODE_* or 0, minors mask)."""
+    nc, pc = abi.node_columns(nodes), abi.pod_columns(pods)
+    minors = C.c_uint32(0)
+    code = lib().kgo_gpu_alloc_numa(C.byref(cfg), C.byref(nc), node, C.byref(pc), pod, numa, C.byref(minors))
+    return int(code), int(minors.value)
 
 
 def ext_select(cfg, nodes: abi.Table, pods: abi.Table, k: int = 1, index_base: int = 0, quotas=None,

@@ -281,15 +281,23 @@ def test_ext_shard_select_single_rank(ctx, k):
 
 @pytest.mark.parametrize("split", ["1", "0"])
 def test_ext_result_status(ctx, monkeypatch, split):
-    """kg_result_status on config 5: GPU pods on NUMA-policy nodes and pairs of cpuset-binding pods on
-    reservation views are flagged KG_ST_UNSUPPORTED, quota-rejected pods KG_ST_QUOTA — the OR of the
-    oracle verify rows' bits (a cpuset-binding pod on a node without CPU topology fails its Filter)."""
+    """kg_result_status on config 5: cpuset-binding pods on NUMA-policy nodes with a CPU topology (the cpuset
+    inside the NUMA hints, a host path) are flagged KG_ST_UNSUPPORTED, quota-rejected pods KG_ST_QUOTA — the OR
+    of the oracle verify rows' bits (a cpuset-binding pod on a node without CPU topology fails its Filter; GPU
+    pods on NUMA-policy nodes are on the device path)."""
     monkeypatch.setenv("KG_EXT_SPLIT", split)
     cfg, nodes, pods, quotas, rsv = synth.cluster5(1200, 400, seed_config=73, rsv_frac=0.2)
     nodes = {k: v.copy() for k, v in nodes.items()}
     pods = {k: v.copy() for k, v in pods.items()}
+    n = len(nodes["alloc_cpu"])
     nodes["numa_policy"][::50] = abi.KG_NUMA_SINGLE_NODE
     nodes["numa_zones"][::50] = np.maximum(nodes["numa_zones"][::50], 1)
+    ti = np.full(n, -1, np.int32)
+    ti[::25] = 0
+    nodes["cpu_topo"] = ti
+    nodes["cpu_topos"] = abi.cpu_topos_array([abi.cpu_topo_for_test(2, 1, 16, 2)])
+    nodes["cpu_alloc"] = np.zeros((n, 2 * abi.KG_MAX_CPUS), np.uint8)
+    nodes["cpu_max_ref"] = np.ones(n, np.uint8)
     pods["flags"][1::11] |= abi.KG_POD_CPU_BIND
     kc = cfg.kg_config()
     snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
