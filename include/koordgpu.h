@@ -287,6 +287,7 @@ typedef struct kg_cpuset_request {
 #define KG_GPU_TREE 0x200u
 #define KG_GPU_TMPL_SHIFT 12 /* dev_part bits 12-15: the node's shared-resource template key (KG_GPU_TMPL_NONE = none) */
 #define KG_GPU_TMPL_NONE 15u
+#define KG_ZONE_RECORD_SHIFT 8 /* numa_zone_status: zone z has an allocation record (node_allocation.go:145-154) */
 #define KG_GPU_MAX_TABLES 16
 #define KG_GPU_MAX_PARTS 1024
 typedef struct kg_gpu_partition {
@@ -336,7 +337,8 @@ typedef struct kg_node_columns {
     /* NUMA node shared status per zone, 2 bits each (0 idle, 1 single, 2 shared; NUMANodeSharedStatus,
      * nodenumaresource/node_allocation.go:52-68) for the Required exclusive policy of pods with a
      * pod-level NUMA policy (NULL = all idle). */
-    const uint32_t* numa_zone_status;
+    const uint32_t* numa_zone_status;  /* 2 bits per zone NUMANodeSharedStatus; bit KG_ZONE_RECORD_SHIFT + z: the
+                                        * NodeAllocation holds an allocatedResources record for zone z */
     /* cpuset binding (NodeNUMAResource, LSE/LSR pods; all may be NULL = no CPU topology anywhere):
      * cpu_topo[i] indexes cpu_topos (-1 = the node has no CPU topology: ErrInvalidCPUTopology for a
      * cpuset-binding pod); cpu_alloc[i] = the node's allocated CPUs (NULL = none). cpuset_alloc_milli must

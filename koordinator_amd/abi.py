@@ -112,6 +112,7 @@ KG_GPU_HONOR = 0x100
 KG_GPU_TREE = 0x200
 KG_GPU_TMPL_SHIFT = 12  # dev_part bits 12-15: the node's shared-resource template key
 KG_GPU_TMPL_NONE = 15
+KG_ZONE_RECORD_SHIFT = 8  # numa_zone_status bit 8 + z: zone z holds an allocatedResources record
 KG_GPU_MAX_TABLES = 16
 KG_GPU_POD_SHARED = 0x1
 KG_GPU_POD_HONOR = 0x2

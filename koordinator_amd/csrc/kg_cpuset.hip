@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kg_cpuset.h"
+#include "kg_eval.h"
 #include "kg_kernels.h"
 
 namespace kg {
@@ -57,11 +58,13 @@ hipError_t launch_cpuset_take(const kg_cpu_topo* topos, const kg_cpu_alloc* allo
 
 namespace kg {
 
-// NodeNUMAResource Reserve of a cpuset-binding pod on a NUMA-policy-None node (plugin.go:585-635 ->
-// resourceManager.Allocate/Update): the accumulator's CPUs enter the node's allocation (RefCount++, the
-// pod's exclusive policy, node_allocation.go:111-130), the Filter counts and cpuset_alloc_milli follow.
-// Runs before the Reserve of the NodeInfo columns (apply_assume, which re-derives the record). The pod
-// and record come from (pod, rec), or in replay from the previous step's winner.
+// NodeNUMAResource Reserve of a cpuset-binding pod (plugin.go:585-635 -> resourceManager.Allocate/Update): the
+// accumulator's CPUs enter the node's allocation (RefCount++, the pod's exclusive policy, node_allocation.go:111-130),
+// the Filter counts and cpuset_alloc_milli follow. Under a NUMA affinity (the pair's zone code: in replay the previous
+// step's, else evaluated here) allocateCPUSet takes per allocated NUMA node (resource_manager.go:391-429) and the
+// NUMA split with the CPUs is recorded here, before the take changes the counts it trims with (apply_assume leaves it,
+// cpuset_numa_reserve). Runs before the Reserve of the NodeInfo columns (apply_assume, which re-derives the record).
+// The pod and record come from (pod, rec), or in replay from the previous step's winner.
 __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
                                                        kg_cpu_alloc* __restrict__ allocs,
                                                        const kg_cpu_topo* __restrict__ topos, PodsDev pods, KCfg cfg,
@@ -90,7 +93,16 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
     const uint32_t node_bind = (z.cpu_meta >> CPU_META_BIND_SHIFT) & 3u;
     if (!((pf & KG_POD_CPU_BIND) || (node_bind != KG_NODE_CPU_BIND_NONE && req_cpu != 0))) return;
     const uint32_t node_pol = ((uint32_t)n[N_FLAGS] >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (pf >> 16) & 15u;
-    if ((pod_pol != KG_NUMA_NONE ? pod_pol : node_pol) != KG_NUMA_NONE) return;
+    const bool numa_pol = (pod_pol != KG_NUMA_NONE ? pod_pol : node_pol) != KG_NUMA_NONE;
+    uint32_t mask = 0;  // the NUMA affinity of the Reserve (0: the whole node)
+    if (numa_pol) {
+        __shared__ int32_t s_zone;
+        if (threadIdx.x == 0) s_zone = winners ? (int32_t)zsel[rec] : eval_pair<false>(cfg, n, &z, load_pod(pods, pod)).zone;
+        __syncthreads();
+        const int32_t zone = s_zone;
+        if (zone_reserve_fails(zone)) return;  // the Reserve fails on the pair's zone code (reported by the Reserve kernel)
+        mask = zone_affinity(zone);
+    }
     const uint32_t* src = reinterpret_cast<const uint32_t*>(topos + z.cpu_topo);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&st);
     for (uint32_t k = threadIdx.x; k < sizeof(kg_cpu_topo) / 4; k += 64) dst[k] = src[k];
@@ -136,14 +148,51 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
     q.excl = (int32_t)((pf >> KG_POD_CPU_EXCL_SHIFT) & 3u);
     q.strategy = (int32_t)((z.cpu_meta >> CPU_META_STRATEGY_SHIFT) & 1u);
     q.has_preferred = 0;
-    uint64_t res[4];
-    const int code = cpuset_take(&st, &sa, q, &acc, res);
+    uint64_t res[4] = {0, 0, 0, 0};
+    int code = 0;
+    int64_t al[2][MAX_ZONES];
+    if (!mask) {
+        code = cpuset_take(&st, &sa, q, &acc, res);
+    } else {
+        // the NUMA split with the CPUs (trimmed to the policy's CPUs, whole CPUs / cores per node) on the pre-take state,
+        // then one take per allocated NUMA node of min(its CPUs, allocated cpu / 1000)
+        const uint32_t Z = ((uint32_t)n[N_FLAGS] >> F_NUMA_ZONES_SHIFT) & 15u;
+        NumaZ x;
+        numa_load(&z, Z, x);
+        const NumaBind nb = numa_bind_of(&z, required, bind, req_cpu);
+        numa_bind_trim(x, nb);
+        const PodV pv = load_pod(pods, pod);
+        const int64_t req[2] = {pv.req_cpu, pv.req_mem};
+        const bool has[2] = {(pf & KG_POD_HAS_CPU) != 0, (pf & KG_POD_HAS_MEM) != 0};
+        code = (numa_split(x, mask, req, has, al, &nb) || numa_bind_check(nb, al[0], al[1], Z)) ? 1 : 0;
+        for (uint32_t zq = 0; zq < (uint32_t)MAX_ZONES && code == 0; zq++) {
+            if (zq >= Z || (al[0][zq] == 0 && al[1][zq] == 0)) continue;
+            const int64_t k = min(nb.cnt[zq], al[0][zq] / 1000);
+            if (k == 0) continue;
+            CpuTake qz = q;
+            for (int w = 0; w < 4; w++) qz.avail[w] = 0;
+            for (int c = 0; c < st.n_cpus; c++)
+                if (st.numa[c] == zq && ((q.avail[c >> 6] >> (c & 63)) & 1ull)) qz.avail[c >> 6] |= 1ull << (c & 63);
+            qz.needed = (int32_t)k;
+            uint64_t rz[4];
+            code = cpuset_take(&st, &sa, qz, &acc, rz);
+            __syncthreads();
+            for (int w = 0; w < 4; w++) res[w] |= rz[w];
+        }
+    }
     __syncthreads();
     if (threadIdx.x != 0) return;
     if (code != 0) {  // Allocate fails (ErrNotEnoughCPUs): the Reserve fails, nothing of the pod is applied
         if (winners) zsel[rec] = (int8_t)ZONE_CPUSET_FAIL;  // read by the replay step that applies the pod
         else if (fail_out) *fail_out = ZONE_CPUSET_FAIL;  // read by k_assume / k_ext_assume
         return;
+    }
+    if (mask) {  // resourceManager.Update: the NUMA split enters the zones, each gets its allocation record
+        for (int zq = 0; zq < MAX_ZONES; zq++) {
+            z.cpu_used[zq] += al[0][zq];
+            z.mem_used[zq] += al[1][zq];
+            z.status |= (al[0][zq] | al[1][zq]) ? 1u << (ZONE_RECORD_SHIFT + zq) : 0u;
+        }
     }
     kg_cpu_alloc& A = allocs[rec];
     uint32_t used = 0;  // NUMA nodes of the CPUs taken (addPodAllocation's usedNUMA)

@@ -164,7 +164,7 @@ __device__ __forceinline__ void numa_load(const ZoneRec* __restrict__ zr, uint32
         const bool on = z < Z;
         x.tot[0][z] = on ? zr->cpu[z] : 0;
         x.tot[1][z] = on ? zr->mem[z] : 0;
-        x.used[0][z] = on ? zr->cpu_used[z] : 0;
+        x.used[0][z] = on ? zone_cpu_alloc(*zr, z) : 0;
         x.used[1][z] = on ? zr->mem_used[z] : 0;
         for (int r = 0; r < 2; r++) x.avail[r][z] = x.tot[r][z] - x.used[r][z] < 0 ? 0 : x.tot[r][z] - x.used[r][z];
     }
@@ -184,9 +184,11 @@ __device__ __forceinline__ int64_t div_small(int64_t q, uint32_t d) {
 // than by the zone ids being sorted (insertion sort for n <= 12, so the swaps depend only on the
 // availability of zones 0..n-1); each zone in turn takes min(available, remaining / zones left).
 // Returns whether the whole request was placed; AL: the per-zone amounts into al (added).
+// bm (cpu of a cpuset-binding pod, splitQuantity :320-334): 1 = whole CPUs of quantity.Value() (rounded up), 2 = whole
+// cores of cpc CPUs (required FullPCPUs); 0 = the quantity itself (milli-cpu / bytes).
 template <bool AL>
 __device__ __forceinline__ bool numa_split_r(const NumaZ& x, uint32_t mask, const int64_t (&av)[MAX_ZONES], int64_t req,
-                                             int64_t (&al)[MAX_ZONES]) {
+                                             int64_t (&al)[MAX_ZONES], int bm = 0, int64_t cpc = 1) {
     uint32_t s = 0, n = 0;  // the mask's zones, ascending, 4 bits per position
 #pragma unroll
     for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++) {
@@ -210,7 +212,11 @@ __device__ __forceinline__ bool numa_split_r(const NumaZ& x, uint32_t mask, cons
 #pragma unroll
     for (uint32_t t = 0; t < (uint32_t)MAX_ZONES; t++) {
         if (t >= n) break;
-        const int64_t split = div_small(q, n - t);
+        int64_t split = div_small(q, n - t);
+        if (bm) {
+            const int64_t v = (q + 999) / 1000;
+            split = bm == 2 ? div_small(v / cpc, n - t) * cpc * 1000 : div_small(v, n - t) * 1000;
+        }
         const uint32_t zone = (s >> (4 * t)) & 15u;
         const int64_t a0 = sel4(av, zone);
         const int64_t got = a0 > split ? split : a0;
@@ -246,6 +252,53 @@ __device__ __forceinline__ int64_t numa_score_q(bool most, int64_t w_cpu, int64_
     }
     if (wsum == 0) return 0;
     return most ? qdiv(sum, wsum) : wdiv(sum, wsum);
+}
+
+// A cpuset-binding pod under a NUMA policy (oracle numa_bind, resource_manager.go:168-194,320-334,357-463): the CPU
+// side of every allocation under a hint. cnt: the available CPUs per NUMA node after the required policy's filter
+// (ZoneRec.cz_*).
+struct NumaBind {
+    bool required, full;
+    int64_t cpc, needed;
+    int64_t cnt[MAX_ZONES];
+};
+
+__device__ __forceinline__ NumaBind numa_bind_of(const ZoneRec* __restrict__ zr, bool required, uint32_t bind, int64_t pod_cpu) {
+    NumaBind b;
+    b.required = required;
+    b.full = bind == KG_CPU_BIND_FULL_PCPUS;
+    b.cpc = (zr->cpu_meta >> CPU_META_CPC_SHIFT) & 15u;
+    b.needed = pod_cpu / 1000;
+#pragma unroll
+    for (int z = 0; z < MAX_ZONES; z++)
+        b.cnt[z] = !required ? zr->cz_free[z] : b.full ? zr->cz_full[z] : zr->cz_cores[z];
+    return b;
+}
+
+__device__ __forceinline__ int numa_bind_mode(const NumaBind* b) { return !b ? 0 : (b->required && b->full) ? 2 : 1; }
+
+// trimNUMANodeResources (:168-194): a required policy's available cpu per NUMA node at most its filtered CPUs
+__device__ __forceinline__ void numa_bind_trim(NumaZ& x, const NumaBind& b) {
+    if (!b.required) return;
+#pragma unroll
+    for (int z = 0; z < MAX_ZONES; z++) x.avail[0][z] = min(x.avail[0][z], b.cnt[z] * 1000);
+}
+
+// allocateCPUSet over the allocated NUMA nodes (:391-429): min(available CPUs there, allocated cpu / 1000) per node,
+// numCPUsNeeded together, whole cores each under a required FullPCPUs policy. 0, KG_ST_NUMA_CPUS or KG_ST_NUMA_CPU_BIND.
+__device__ __forceinline__ uint32_t numa_bind_check(const NumaBind& b, const int64_t (&al0)[MAX_ZONES],
+                                                    const int64_t (&al1)[MAX_ZONES], uint32_t Z) {
+    int64_t sum = 0;
+    bool partial = false;
+#pragma unroll
+    for (uint32_t z = 0; z < (uint32_t)MAX_ZONES; z++) {
+        if (z >= Z || (al0[z] == 0 && al1[z] == 0)) continue;
+        const int64_t k = min(b.cnt[z], al0[z] / 1000);
+        sum += k;
+        partial = partial || (b.required && b.full && b.cpc != 0 && k % b.cpc != 0);
+    }
+    if (sum != b.needed) return KG_ST_NUMA_CPUS;
+    return partial ? (uint32_t)KG_ST_NUMA_CPU_BIND : 0u;
 }
 
 struct NumaHint {
@@ -332,10 +385,14 @@ __device__ __forceinline__ NumaHint numa_hint_at(uint64_t nib, uint32_t k, uint3
 
 // Policy merge: 0 = admitted with affinity `mask` (0 = none), else a KG_ST_NUMA_* reason. GPU: a third hint list,
 // DeviceShare's (gh, provider order: NodeNUMAResource's cpu, memory, then DeviceShare's gpu).
+// bind (nullable): a cpuset-binding pod (x already trimmed); score_cpu: the cpu request the hint scores count (amplified
+// for a cpuset-binding pod, getResourceOptions plugin.go:774-778)
 template <bool EXACT, bool GPU = false>
 __device__ __forceinline__ uint32_t numa_admit(const KCfg& c, const NumaZ& x, const int64_t* req, const bool* has,
                                               uint32_t policy, bool excl, uint32_t& mask_out,
-                                              const GpuHints* gh = nullptr) {
+                                              const GpuHints* gh = nullptr, const NumaBind* bind = nullptr,
+                                              int64_t score_cpu = -1) {
+    if (score_cpu < 0) score_cpu = req[0];
     const uint32_t Z = x.Z;
     const uint64_t nib = numa_mask_nib(Z);
     const uint32_t nm = (1u << Z) - 1u;
@@ -364,13 +421,20 @@ __device__ __forceinline__ uint32_t numa_admit(const KCfg& c, const NumaZ& x, co
         }
         // numaScorer over requested = SubtractWithNonNegativeResult(total, available) + the pod's request
         const int64_t sc = numa_score_q(most_hint, c.numa_hint_w_cpu, c.numa_hint_w_mem, T0,
-                                        (T0 - A0 < 0 ? 0 : T0 - A0) + req[0], T1, (T1 - A1 < 0 ? 0 : T1 - A1) + req[1]);
+                                        (T0 - A0 < 0 ? 0 : T0 - A0) + score_cpu, T1, (T1 - A1 < 0 ? 0 : T1 - A1) + req[1]);
         if (k < 8) sc_lo |= (uint64_t)(sc & 0xFF) << (8 * k);
         else sc_hi |= (uint64_t)(sc & 0xFF) << (8 * (k - 8));
         // tryAllocateFromNode under the mask: every requested resource must be placed
         bool ok = true;
-        if (has[0]) ok = numa_split_r<false>(x, m, x.avail[0], req[0], dummy);
-        if (ok && has[1]) ok = numa_split_r<false>(x, m, x.avail[1], req[1], dummy);
+        if (bind) {  // the whole allocation with the CPUs (tryAllocateFromNode)
+            int64_t al0[MAX_ZONES] = {0, 0, 0, 0}, al1[MAX_ZONES] = {0, 0, 0, 0};
+            if (has[0]) ok = numa_split_r<true>(x, m, x.avail[0], req[0], al0, numa_bind_mode(bind), bind->cpc);
+            if (ok && has[1]) ok = numa_split_r<true>(x, m, x.avail[1], req[1], al1);
+            ok = ok && numa_bind_check(*bind, al0, al1, Z) == 0u;
+        } else {
+            if (has[0]) ok = numa_split_r<false>(x, m, x.avail[0], req[0], dummy);
+            if (ok && has[1]) ok = numa_split_r<false>(x, m, x.avail[1], req[1], dummy);
+        }
         if (!ok) continue;
         const int pc = popc(m);
         if (has[0] && !(m & lack0)) {
@@ -471,34 +535,45 @@ __device__ __forceinline__ int32_t numa_code(uint32_t mask) {
 // tryBestToDistributeEvenly of the pod's cpu / memory over `mask`: the allocation and a failure bit per
 // resource (bit 0 cpu, bit 1 memory: "Insufficient NUMA <resource>", resource_manager.go:300-309)
 __device__ __forceinline__ uint32_t numa_split(const NumaZ& x, uint32_t mask, const int64_t* req, const bool* has,
-                                               int64_t (&al)[2][MAX_ZONES]) {
+                                               int64_t (&al)[2][MAX_ZONES], const NumaBind* bind = nullptr) {
     uint32_t fail = 0;
 #pragma unroll
     for (int r = 0; r < 2; r++) {
 #pragma unroll
         for (int z = 0; z < MAX_ZONES; z++) al[r][z] = 0;
-        if (has[r] && !numa_split_r<true>(x, mask, x.avail[r], req[r], al[r])) fail |= 1u << r;
+        const int bm = r == 0 ? numa_bind_mode(bind) : 0;
+        if (has[r] && !numa_split_r<true>(x, mask, x.avail[r], req[r], al[r], bm, bind ? bind->cpc : 1)) fail |= 1u << r;
     }
     return fail;
 }
 
 // The topology manager for one (pod, node) pair: hints, policy merge, the allocation's zone code and
 // the NUMA score (score_node when no allocation is made). Returns 0 or KG_ST_* bits.
+// bind (nullable): a cpuset-binding pod (its CPUs in every allocation, score_cpu its amplified cpu, bind_cpu the node's
+// cpuset CPUs amplified: the Score's requested cpu, scoring.go:190-197); node_take: without an affinity its CPUs come
+// from the whole node (allocateCPUSet without NUMA nodes) and fit there.
 __device__ __forceinline__ uint32_t numa_topology(const KCfg* cp, const ZoneRec* zr, uint32_t Z, int64_t req_cpu,
                                                int64_t req_mem, uint32_t pflags, uint32_t pol, bool excl,
-                                               int64_t score_node, int32_t* zone_out, int64_t* score_out) {
+                                               int64_t score_node, int32_t* zone_out, int64_t* score_out,
+                                               const NumaBind* bind = nullptr, int64_t score_cpu = -1,
+                                               int64_t bind_cpu = 0, bool node_take = true) {
     const KCfg& c = *cp;
     NumaZ x;
     numa_load(zr, Z, x);
+    if (bind) numa_bind_trim(x, *bind);
     const int64_t req[2] = {req_cpu, req_mem};
     const bool has[2] = {(pflags & KG_POD_HAS_CPU) != 0, (pflags & KG_POD_HAS_MEM) != 0};
     uint32_t mask = 0;
-    const uint32_t st = numa_admit<true>(c, x, req, has, pol, excl, mask);
+    const uint32_t st = numa_admit<true>(c, x, req, has, pol, excl, mask, nullptr, bind, score_cpu);
     if (st) return st;
     int64_t al[2][MAX_ZONES];
-    if (mask && numa_split(x, mask, req, has, al)) return KG_ST_UNSUPPORTED;  // a BestEffort Reserve that would fail: host path
+    // allocateResources under the best hint: a preferred best hint is one of the lists' feasible masks (not reached)
+    if (mask && numa_split(x, mask, req, has, al, bind)) return KG_ST_UNSUPPORTED;
+    if (mask && bind && numa_bind_check(*bind, al[0], al[1], Z)) return KG_ST_UNSUPPORTED;
+    if (!mask && bind && !node_take) return KG_ST_NUMA_CPUS;
     *zone_out = numa_code(mask);
-    if (pol == KG_NUMA_BEST_EFFORT || !mask) {
+    // no NUMANodeResources (no affinity, or no cpu / memory request): node allocatable / requested (scoring.go:168-189)
+    if (pol == KG_NUMA_BEST_EFFORT || !mask || !(req_cpu | req_mem)) {
         *score_out = score_node;
         return 0;
     }
@@ -511,8 +586,8 @@ __device__ __forceinline__ uint32_t numa_topology(const KCfg* cp, const ZoneRec*
             U[r] += x.used[r][z];
         }
     }
-    *score_out = numa_score_q((c.most & MOST_NUMA) != 0, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + req_cpu, T[1],
-                              U[1] + req_mem);
+    *score_out = numa_score_q((c.most & MOST_NUMA) != 0, c.numa_w_cpu, c.numa_w_mem, T[0],
+                              (bind ? bind_cpu : U[0]) + (score_cpu < 0 ? req_cpu : score_cpu), T[1], U[1] + req_mem);
     return 0;
 }
 
@@ -559,18 +634,23 @@ struct PairOut {
 // admits) and the allocation of its best hint; the zone code of the allocation, or ZONE_RESERVE_FAIL | bits
 // when the topology hints fail ("node(s) Insufficient NUMA Node resources", no zones) or the allocation does
 // ("Insufficient NUMA <resource>", resource_manager.go:300-309).
+// A cpuset-binding pod (bind): its CPUs join every allocation; allocateCPUSet failing fails the Reserve (ZONE_CPUSET_FAIL).
 __device__ __forceinline__ int32_t numa_reserve_best_effort(const KCfg& c, const ZoneRec* zr, uint32_t Z, const PodV& p,
-                                                            bool excl) {
+                                                            bool excl, const NumaBind* bind = nullptr,
+                                                            int64_t score_cpu = -1, bool node_take = true) {
     if (Z == 0) return ZONE_RESERVE_FAIL | (int32_t)(KG_ST_NUMA_INSUF_NODE >> 12);
     NumaZ x;
     numa_load(zr, Z, x);
+    if (bind) numa_bind_trim(x, *bind);
     const int64_t req[2] = {p.req_cpu, p.req_mem};
     const bool has[2] = {(p.flags & KG_POD_HAS_CPU) != 0, (p.flags & KG_POD_HAS_MEM) != 0};
     uint32_t mask = 0;
-    numa_admit<true>(c, x, req, has, KG_NUMA_BEST_EFFORT, excl, mask);
+    numa_admit<true>(c, x, req, has, KG_NUMA_BEST_EFFORT, excl, mask, nullptr, bind, score_cpu);
     int64_t al[2][MAX_ZONES];
-    const uint32_t fail = mask ? numa_split(x, mask, req, has, al) : 0u;
-    return fail ? ZONE_RESERVE_FAIL | (int32_t)fail : numa_code(mask);
+    const uint32_t fail = mask ? numa_split(x, mask, req, has, al, bind) : 0u;
+    if (fail) return ZONE_RESERVE_FAIL | (int32_t)fail;
+    if (bind && (mask ? numa_bind_check(*bind, al[0], al[1], Z) != 0u : !node_take)) return ZONE_CPUSET_FAIL;
+    return numa_code(mask);
 }
 
 // ZONE = false (select kernels): the pair's Reserve zone is not needed, so a BestEffort node skips its
@@ -609,6 +689,9 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             return;
         }
     }
+    NumaBind bind;
+    const NumaBind* bp = nullptr;
+    bool node_take = true;
     if (cpu_bind) {  // plugin.go:396-440
         if (zr->cpu_topo < 0) {
             o.status |= KG_ST_NUMA_CPU_TOPO;
@@ -625,38 +708,52 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             o.status |= KG_ST_NUMA_CPU_BIND;  // ErrCPUBindPolicyConflict / ErrSMTAlignmentError
             return;
         }
-        if (pol != KG_NUMA_NONE) {  // cpusets inside NUMA hints (resource_manager.go:357-499): host path
-            o.status |= KG_ST_UNSUPPORTED;
-            return;
-        }
-        if (required != KG_CPU_BIND_NONE) {
-            // tryAllocateFromNode: the required policy's CPUs (filterCPUsByRequiredCPUBindPolicy) must cover the
-            // pod; takeCPUs then always succeeds on them and the result satisfies the policy
-            const int64_t have = required == KG_CPU_BIND_FULL_PCPUS ? zr->cpu_free_full : zr->cpu_free_cores;
-            if (needed > have) {
+        // allocateCPUSet over the whole node: the required policy's CPUs (filterCPUsByRequiredCPUBindPolicy) or the
+        // available ones must cover the pod; takeCPUs then always succeeds on them and satisfies the policy
+        const int64_t have = required == KG_CPU_BIND_FULL_PCPUS    ? zr->cpu_free_full
+                             : required == KG_CPU_BIND_SPREAD_BY_PCPUS ? zr->cpu_free_cores
+                                                                       : zr->cpu_free;
+        node_take = needed <= have;
+        if (pol != KG_NUMA_NONE) {  // the CPUs join every allocation the topology manager tries
+            bind = numa_bind_of(zr, required != KG_CPU_BIND_NONE, required != KG_CPU_BIND_NONE ? required : cpu_pol, pod_cpu);
+            bp = &bind;
+        } else if (required != KG_CPU_BIND_NONE) {
+            if (!node_take) {  // tryAllocateFromNode in Filter
                 o.status |= KG_ST_NUMA_CPUS;
                 return;
             }
-        } else if (needed > zr->cpu_free) {
-            // no Filter check: the Reserve would fail (ErrNotEnoughCPUs) and the reference retries the pod
-            o.status |= KG_ST_UNSUPPORTED;
-            return;
+        } else if (!node_take) {
+            // no Filter check: the Reserve fails (ErrNotEnoughCPUs)
+            if constexpr (ZONE) o.zone = ZONE_CPUSET_FAIL;
         }
     }
+    // a cpuset-binding pod under a NUMA policy: its cpu request amplified where the options' requests count (hint and
+    // node scores, getResourceOptions plugin.go:774-778), the node's cpuset CPUs amplified as the Score's requested
+    // cpu (calculateAllocatableAndRequested, scoring.go:190-197)
+    const int64_t score_cpu = (bp && amp) ? (int64_t)ceil(__dmul_rn((double)pod_cpu, zr->amp_ratio)) : pod_cpu;
+    const int64_t bind_cpu = amp ? n[N_AMP_CPUSET] : n[N_CPUSET];
     const double rcp_cpu = as_f64(n[N_RCP_CPU]), rcp_mem = as_f64(n[N_RCP_MEM]);
     const bool most = (c.most & MOST_NUMA) != 0;
     // pods with their own NUMA policy default to the Required exclusive policy (plugin.go:449-454)
     const bool excl = pod_pol != KG_NUMA_NONE;
     if (pol == KG_NUMA_BEST_EFFORT) {
         // no FilterByNUMANode under BestEffort (plugin.go:446-455); Score without an allocation: node
-        // allocatable / requested as they are (scoring.go:184-189); the Reserve's zone from the topology manager
-        if constexpr (SCORE)
-            o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
-                                         rcp_cpu, n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
-        if constexpr (ZONE && TOPO) o.zone = numa_reserve_best_effort(c, zr, (flags >> F_NUMA_ZONES_SHIFT) & 15u, p, excl);
+        // allocatable / requested as they are (scoring.go:184-189; a cpuset-binding pod's CPUs from the whole node,
+        // score 0 when they do not fit); the Reserve's zone from the topology manager
+        if constexpr (SCORE) {
+            if (bp)
+                o.s_numa = node_take ? numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], bind_cpu + score_cpu,
+                                                         rcp_cpu, n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem)
+                                     : 0;
+            else
+                o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], nv<OV>(n, ov, N_REQ_CPU) + pod_cpu,
+                                             rcp_cpu, n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
+        }
+        if constexpr (ZONE && TOPO)
+            o.zone = numa_reserve_best_effort(c, zr, (flags >> F_NUMA_ZONES_SHIFT) & 15u, p, excl, bp, score_cpu, node_take);
         return;
     }
-    if (pol == KG_NUMA_RESTRICTED || (pol == KG_NUMA_SINGLE_NODE && excl)) {
+    if (pol == KG_NUMA_RESTRICTED || (pol == KG_NUMA_SINGLE_NODE && (excl || bp))) {
         if constexpr (!TOPO) {
             o.status |= KG_ST_UNSUPPORTED;  // unreachable under the host's TOPO selection
             return;
@@ -667,11 +764,12 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             return;
         }
         const int64_t score_node = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU],
-                                                     nv<OV>(n, ov, N_REQ_CPU) + pod_cpu, rcp_cpu, n[N_ALLOC_MEM],
-                                                     nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
+                                                     (bp ? bind_cpu : nv<OV>(n, ov, N_REQ_CPU)) + score_cpu, rcp_cpu,
+                                                     n[N_ALLOC_MEM], nv<OV>(n, ov, N_REQ_MEM) + p.req_mem, rcp_mem);
         int32_t zone = -1;
         int64_t s = 0;
-        const uint32_t st = numa_topology(&c, zr, Z, p.req_cpu, p.req_mem, p.flags, pol, excl, score_node, &zone, &s);
+        const uint32_t st = numa_topology(&c, zr, Z, p.req_cpu, p.req_mem, p.flags, pol, excl, score_node, &zone, &s, bp,
+                                          score_cpu, bind_cpu, node_take);
         if (st) {
             o.status |= st;
             return;
@@ -692,7 +790,7 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             int64_t best_score = 0;
             for (uint32_t z = 0; z < Z; z++) {
                 const int64_t tc = zr->cpu[z], tm = zr->mem[z];
-                const int64_t uc = zr->cpu_used[z], um = zr->mem_used[z];
+                const int64_t uc = zone_cpu_alloc(*zr, z), um = zr->mem_used[z];
                 const int64_t ac = tc - uc < 0 ? 0 : tc - uc;
                 const int64_t am = tm - um < 0 ? 0 : tm - um;
                 const bool ok = (!has_cpu || (ac != 0 && p.req_cpu <= ac)) && (!has_mem || (am != 0 && p.req_mem <= am));
@@ -727,7 +825,7 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             return;
         }
         o.zone = best;
-        o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, zr->cpu[best], zr->cpu_used[best] + pod_cpu,
+        o.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, zr->cpu[best], zone_cpu_alloc(*zr, best) + pod_cpu,
                                      zr->rcp_cpu[best], zr->mem[best], zr->mem_used[best] + p.req_mem,
                                      zr->rcp_mem[best]);
         return;
@@ -856,11 +954,24 @@ __device__ __forceinline__ void numa_reserve_split(ZoneRec* zr, uint32_t Z, int6
         for (int z = 0; z < MAX_ZONES; z++) {
             zr->cpu_used[z] += al[0][z];
             zr->mem_used[z] += al[1][z];
+            zr->status |= (al[0][z] | al[1][z]) ? 1u << (ZONE_RECORD_SHIFT + z) : 0u;
             if (split_out) {
                 split_out[z] = al[0][z];
                 split_out[MAX_ZONES + z] = al[1][z];
             }
         }
+}
+
+// A cpuset-binding pod under a NUMA policy on a node with a CPU topology: its Reserve's NUMA split (with the CPUs,
+// numa_split under NumaBind) is recorded by the cpuset Reserve kernel before the take changes the counts
+// (k_cpuset_reserve), not by apply_assume.
+__device__ __forceinline__ bool cpuset_numa_reserve(const KCfg& c, const int64_t* __restrict__ n, const ZoneRec* zr,
+                                                    const PodV& p) {
+    if (!(c.plugins & KG_PLUGIN_NUMA) || zr->cpu_topo < 0 || (p.flags & KG_POD_NUMA_SKIP)) return false;
+    const uint32_t node_bind = (zr->cpu_meta >> CPU_META_BIND_SHIFT) & 3u;
+    if (!((p.flags & KG_POD_CPU_BIND) || (node_bind != KG_NODE_CPU_BIND_NONE && p.req_cpu != 0))) return false;
+    const uint32_t node_pol = ((uint32_t)n[N_FLAGS] >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (p.flags >> 16) & 15u;
+    return (pod_pol != KG_NUMA_NONE ? pod_pol : node_pol) != KG_NUMA_NONE;
 }
 
 // Reserve (sign = +1) / Unreserve (sign = -1) of pod p on node record n (a16).
@@ -890,9 +1001,12 @@ __device__ __forceinline__ void apply_assume(const KCfg& c, int64_t* n, ZoneRec*
             n[N_LA_SBASE_PROD1] += d1;
         }
     }
-    if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES) {
+    if (sign > 0 && zone >= 0 && cpuset_numa_reserve(c, n, zr, p)) {
+        // the zone split is in place already (k_cpuset_reserve)
+    } else if ((c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES) {
         zr->cpu_used[zone] += sign * p.req_cpu;
         zr->mem_used[zone] += sign * p.req_mem;
+        if (sign > 0 && (p.req_cpu | p.req_mem)) zr->status |= 1u << (ZONE_RECORD_SHIFT + zone);
         if (split && sign > 0) {
             split[zone] = p.req_cpu;
             split[MAX_ZONES + zone] = p.req_mem;
@@ -1025,9 +1139,14 @@ __device__ __forceinline__ bool fast_kind_match(int kind, const PodV& p) {
 
 // fast_eval: the weighted total in `total`, feasibility as the return value (select loops fold it into
 // their top-key update); eval_fast_key: the selection key, 0 when infeasible.
-template <uint32_t PM, int CLS, int KIND = FK_ANY>
+// GZ (CLS 1, a GPU pod): DeviceShare's hints join the zone walk (gz = gpu_zone_sum's word of the record and the pod's
+// GPU request class): a zone needs its preferred single-zone GPU hint (unless the provider has no preference) and the
+// merged hint's score is the sum over the providers' lists, (cpu, memory listed) x the zone's hint score + 500 when
+// DeviceShare's hint scores 500 (policy.go mergePermutation); a failing provider fails the pair. Needs a cpu or memory
+// request (with neither, the merge runs on DeviceShare's list alone: general path).
+template <uint32_t PM, int CLS, int KIND = FK_ANY, bool GZ = false>
 __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr, const PodF& p,
-                                          uint32_t& total_out, int32_t* zone_out = nullptr) {
+                                          uint32_t& total_out, int32_t* zone_out = nullptr, uint64_t gz = 0) {
     constexpr bool KP = KIND == FK_PROD, KB = KIND == FK_BATCH;
     const uint32_t f = (uint32_t)r.flags;
     bool ok = true;
@@ -1112,15 +1231,28 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
             const bool has_any = KP ? true : has_cpu | has_mem;
             int32_t best = -1;
             uint32_t best_score = 0;
+            // with DeviceShare's hints (not "no preference") a zone is chosen even without a cpu / memory request
+            const bool gsel = GZ && !KB && (gz & 2ull) == 0;
             if constexpr (!KB) {
                 uint32_t best_hint = 0;
+                uint32_t gmask = 0xFu, g500 = 0u, mult = 1u;
+                if constexpr (GZ) {
+                    const bool nopref = (gz & 2ull) != 0;
+                    gmask = nopref ? 0xFu : (uint32_t)(gz >> 4) & 15u;
+                    g500 = nopref ? 0u : (uint32_t)(gz >> 8) & 15u;
+                    mult = (has_cpu ? 1u : 0u) + (has_mem ? 1u : 0u);
+                }
 #pragma unroll 1
                 for (uint32_t z = 0; z < Z; z++) {
                     const ZoneFast q = zr->zf[z];
-                    const bool elig = (!has_cpu | (p.cpu <= q.avail_cpu)) & (!has_mem | (p.mem <= q.avail_mem));
+                    bool elig = (!has_cpu | (p.cpu <= q.avail_cpu)) & (!has_mem | (p.mem <= q.avail_mem));
                     const uint32_t hc = lr100(q.hint_cpu, p.cpu, q.rcp_cpu), hm = lr100(q.hint_mem, p.mem, q.rcp_mem);
                     const uint32_t fc = lr100(q.free_cpu, p.cpu, q.rcp_cpu), fm = lr100(q.free_mem, p.mem, q.rcp_mem);
-                    const uint32_t hint = wq(mad24(hm, hi32(q.w_hint), mad24(hc, lo32(q.w_hint), 1u)), f32lo(q.hpack));
+                    uint32_t hint = wq(mad24(hm, hi32(q.w_hint), mad24(hc, lo32(q.w_hint), 1u)), f32lo(q.hpack));
+                    if constexpr (GZ) {
+                        elig = elig & (((gmask >> z) & 1u) != 0);
+                        hint = mult * hint + (((g500 >> z) & 1u) ? 500u : 0u);
+                    }
                     const uint32_t fin = wq(mad24(fm, hi32(q.w_score), mad24(fc, lo32(q.w_score), 1u)), f32hi(q.hpack));
                     const bool take = elig & ((best < 0) | (hint > best_hint));
                     best = take ? (int32_t)z : best;
@@ -1128,7 +1260,9 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
                     best_score = take ? fin : best_score;
                 }
             }
-            nok = nok & (Z != 0) & !(has_any & (best < 0));
+            const bool need = has_any | gsel;
+            nok = nok & (Z != 0) & !(need & (best < 0));
+            if constexpr (GZ) nok = nok & ((gz & 1ull) == 0);
             // a best hint equal to the default affinity (no request on NUMA resources, or one zone)
             // carries no affinity: node-level score without amplification
             uint32_t node_level = 0;
@@ -1136,8 +1270,10 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
                 const uint32_t sc = lr100(r.numa_free_cpu, p.cpu, r.rcp_cpu), sm = lr100(r.numa_free_mem, p.mem, r.rcp_mem);
                 node_level = wq(mad24(sm, hi32(r.w_numa), mad24(sc, lo32(r.w_numa), 1u)), f32lo(r.w_aux));
             }
+            // (a zone chosen by DeviceShare's hints alone allocates no cpu / memory: no NUMANodeResources, node-level
+            // score, calculateAllocatableAndRequested scoring.go:168-189)
             s_numa = (!has_any || Z == 1) ? node_level : best_score;
-            if (zone_out) *zone_out = (skip || !has_any || Z == 1) ? -1 : best;  // the Reserve's zone (eval_pair o.zone)
+            if (zone_out) *zone_out = (skip || !need || Z == 1) ? -1 : best;  // the Reserve's zone (eval_pair o.zone)
         } else {
             // amplified requested for pods with a cpu request: (free - r) + delta * {0, 1}
             const uint32_t sc = KB ? cvt_sat_u32(r.numa_free_cpu * r.rcp_cpu)
@@ -1152,11 +1288,11 @@ __device__ __forceinline__ bool fast_eval(const KCfg& c, const FastRec& r, const
     return ok;
 }
 
-template <uint32_t PM, int CLS>
+template <uint32_t PM, int CLS, bool GZ = false>
 __device__ __forceinline__ uint64_t eval_fast_key(const KCfg& c, const FastRec& r, const ZoneRec* __restrict__ zr,
-                                                  const PodF& p, uint32_t gidx, int32_t* zone_out = nullptr) {
+                                                  const PodF& p, uint32_t gidx, int32_t* zone_out = nullptr, uint64_t gz = 0) {
     uint32_t total;
-    const bool ok = fast_eval<PM, CLS>(c, r, zr, p, total, zone_out);
+    const bool ok = fast_eval<PM, CLS, FK_ANY, GZ>(c, r, zr, p, total, zone_out, gz);
     const uint64_t key = ((uint64_t)total << 32) | (uint64_t)(0xFFFFFFFFu - gidx);
     return ok ? key : 0ull;
 }

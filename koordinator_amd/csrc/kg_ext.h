@@ -1112,7 +1112,7 @@ __device__ __forceinline__ void numa_gpu_eval(const KCfg& c, const ExtDev& e, co
     b.zone = numa_code(mask);
     if constexpr (!SCORE) return;
     const bool most = (c.most & MOST_NUMA) != 0;
-    if (!mask) {  // no NUMA allocation: node allocatable / requested (the view's NodeInfo on a view)
+    if (!mask || !(p.req_cpu | p.req_mem)) {  // no NUMANodeResources: node allocatable / requested (the view's NodeInfo on a view)
         const int64_t rc = v ? v->req[0] : n[N_REQ_CPU], rm = v ? v->req[1] : n[N_REQ_MEM];
         b.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], rc + p.req_cpu,
                                      as_f64(n[N_RCP_CPU]), n[N_ALLOC_MEM], rm + p.req_mem, as_f64(n[N_RCP_MEM]));
@@ -1128,6 +1128,48 @@ __device__ __forceinline__ void numa_gpu_eval(const KCfg& c, const ExtDev& e, co
         }
     }
     b.s_numa = numa_score_q(most, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + p.req_cpu, T[1], U[1] + p.req_mem);
+}
+
+// ---- SingleNUMANode records on the fast-base path (storage class 1) --------------------------------------
+// What DeviceShare brings to the topology manager of a fast pod (no pod NUMA policy, no cpuset) on a SingleNUMANode
+// record off reservation views depends on the record and the pod's GPU request class only; k_gpu_zone_sum packs it
+// per (record, class) so the fast-base kernels merge it into the class-1 zone walk (fast_eval<.., GZ>):
+//   GZ_FAIL    the provider fails (its status stands: the pair is infeasible);
+//   GZ_NOPREF  no GPU with a NUMA node: its single hint is the preferred nil affinity;
+//   GZ_NODEV   no Device object: DeviceShare is no provider (its Filter / Score as without NUMA);
+//   bits 4-7   the zones z whose hint {z} is in the list and preferred (what filterSingleNumaHints keeps);
+//   bits 8-11  the zones whose hint {z} scores 500;
+//   bits 12-15 the zones z under whose affinity {z} the allocation succeeds (allocateResources);
+//   bits 16+8z DeviceShare's Score under the affinity {z} (0..100).
+constexpr uint64_t GZ_FAIL = 1, GZ_NOPREF = 2, GZ_NODEV = 4;
+
+__device__ __forceinline__ uint64_t gpu_zone_sum(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                                 const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d, const PodX& x) {
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    if (D < 0) return GZ_NOPREF | GZ_NODEV;
+    GpuHints gh;
+    if (gpu_numa_hints(c, e, n, zr, d, nullptr, x, false, gh)) return GZ_FAIL;
+    uint64_t w = 0;
+    if (gh.set == (1u << NUMA_NIL_K)) {
+        w |= GZ_NOPREF;
+    } else {
+        for (uint32_t l = gh.set; l; l &= l - 1u) {
+            const uint32_t t = (uint32_t)(__ffs(l) - 1);
+            const uint32_t m = (uint32_t)(gh.masks >> (4 * t)) & 15u;
+            if (popc(m) != 1) continue;
+            const uint32_t z = (uint32_t)(__ffs(m) - 1);
+            w |= ((gh.pref >> t) & 1u) ? (uint64_t)1 << (4 + z) : 0ull;
+            w |= ((gh.s500 >> t) & 1u) ? (uint64_t)1 << (8 + z) : 0ull;
+        }
+    }
+    const uint32_t Z = ((uint32_t)n[N_FLAGS] >> F_NUMA_ZONES_SHIFT) & 15u;
+    for (uint32_t z = 0; z < Z && z < (uint32_t)MAX_ZONES; z++) {
+        uint32_t minors;
+        if (gpu_alloc_site(c, e, n, zr, d, nullptr, x, false, 1u << z, false, minors)) continue;
+        w |= (uint64_t)1 << (12 + z);
+        w |= (uint64_t)((uint32_t)dev_score_tab_numa(c, d, nullptr, D, zr->dev_numa, x, 1u << z) & 0xFFu) << (16 + 8 * z);
+    }
+    return w;
 }
 
 // ---- one pair with every plugin ---------------------------------------------------------------------

@@ -178,6 +178,26 @@ __global__ __launch_bounds__(256) void k_rdev_codes(const NodeRec* __restrict__ 
     }
 }
 
+// gpu_zone_sum of every storage-class-1 record (SingleNUMANode, [n0, n_nodes)) for every GPU request class of the
+// batch: thread = (record, class). The special-record kernels of a fast-base launch merge it into the fast block's
+// zone walk (eval_c1) instead of running DeviceShare's hint provider per pair.
+__global__ __launch_bounds__(64) void k_gpu_zone_sum(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                     const DevRec* __restrict__ devs, uint32_t n_nodes, uint32_t n0,
+                                                     const DevClass* __restrict__ cls, KCfg cfg, ExtDev e,
+                                                     uint64_t* __restrict__ out) {
+    const uint32_t rec = n0 + blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = blockIdx.y;
+    if (rec >= n_nodes) return;
+    PodX x{};
+    x.dkeys = cls[k].dkeys;
+    x.dcount = cls[k].dcount;
+    x.dflags = cls[k].dflags;
+    x.dtmpl = cls[k].dtmpl;
+    x.dbw = cls[k].dbw;
+    for (int r = 0; r < DEV_R; r++) x.dreq[r] = cls[k].dreq[r];
+    out[(size_t)(rec - n0) * DEV_CLASSES + k] = gpu_zone_sum(cfg, e, nodes[rec].v, zones + rec, devs + rec, x);
+}
+
 // Records the fast-base kernels (PART 1) take for no pod: F_BIG or storage class 1. special[0] = count,
 // special[1..] = records (any order: keys are order-free).
 __global__ __launch_bounds__(256) void k_special_scan(const NodeRec* __restrict__ nodes, uint32_t n_nodes, uint32_t n0,
@@ -330,6 +350,48 @@ __device__ __forceinline__ void for_general_records(const NodeRec* __restrict__ 
         }
 }
 
+// A storage-class-1 (SingleNUMANode) record of a fast-base launch for a pod off its reservation views, with DeviceShare's hints from e.gz: the fast block's base key (0 = infeasible with the
+// NodeResourcesFit / LoadAware / NodeNUMAResource Filters, the quota gate or a required reservation affinity, as
+// k_ext_select<FB> has them) and, when feasible, DeviceShare's Filter under the admitted zone and its raw score.
+// Returns false when the pair takes the general path instead.
+struct C1Pair {
+    uint64_t bk;
+    int64_t s_dev;
+    uint32_t st, g;
+};
+
+__device__ __forceinline__ bool eval_c1(const KCfg& cfg, const KCfg& cv, const ExtDev& e, const int64_t* __restrict__ n,
+                                        const ZoneRec* __restrict__ zr, uint32_t rec, uint32_t n0, const PodF& pff,
+                                        const PodX& px, uint32_t dcls, uint32_t q, bool req_aff, uint32_t index_base,
+                                        C1Pair& o) {
+    const uint32_t fl = (uint32_t)n[N_FLAGS];
+    if (!e.gz || rec < n0 || (fl & F_BIG)) return false;
+    if ((cfg.plugins & KG_PLUGIN_RSV) && px.cls >= 0 && px.cls < RSV_MAX_CLASSES &&
+        (((uint64_t)n[N_RSV_CLASSES] >> px.cls) & 1ull))
+        return false;  // a view of the pod's class
+    const FastRec fr = *reinterpret_cast<const FastRec*>(&n[FAST_BEGIN]);
+    o.g = index_base + (uint32_t)((uint64_t)fr.flags >> 32);
+    o.s_dev = 0;
+    const bool dev = (cfg.plugins & KG_PLUGIN_DEV) && px.dcount != 0 && dcls < (uint32_t)DEV_CLASSES;
+    if (!dev) {
+        o.bk = eval_fast_key<7u, 1>(cv, fr, zr, pff, o.g);
+        o.st = (o.bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
+        return true;
+    }
+    const uint64_t gz = e.gz[(size_t)(rec - n0) * DEV_CLASSES + dcls];
+    int32_t zone = -1;
+    o.bk = eval_fast_key<7u, 1, true>(cv, fr, zr, pff, o.g, &zone, gz);
+    o.st = (o.bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
+    if (o.st) return true;
+    if (zone >= 0 && !(gz & GZ_NODEV)) {  // DeviceShare's Allocate under the admitted zone, its Score there
+        o.st = ((gz >> (12 + zone)) & 1ull) ? 0u : 1u;
+        o.s_dev = (int64_t)((gz >> (16 + 8 * zone)) & 0xFFull);
+    } else {  // no affinity (one zone) or no provider: the allocation on the node's devices
+        o.st = dev_eval_cls(n, e.dsum + rec, px, dcls, o.s_dev);
+    }
+    return true;
+}
+
 // Pass 1, general records of a fast-base launch (the complement of k_ext_stats<.., 1>).
 __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                       ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
@@ -343,11 +405,20 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
     const PodV p = load_pod(pods, j);
     const PodX px = load_podx(pods, j);
     const uint32_t q = live ? qst[j] : 1u;
+    const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
+    const PodF pff = to_podf(p, cfg);
+    const KCfg cv = cfg_in_vgprs(cfg);
+    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
     uint32_t dmax = 0, rmax = 0;
     uint64_t pk = PREF_NONE;
     for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, [&](uint32_t rec) {
+        C1Pair c1;
+        if (eval_c1(cfg, cv, e, nodes[rec].v, zones + rec, rec, n0, pff, px, dcls, q, req_aff, index_base, c1)) {
+            if (!c1.st) dmax = max(dmax, (uint32_t)c1.s_dev);
+            return;
+        }
         const PairX r = eval_pair_ext<false, false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
-                                          pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES);
+                                                           dcls);
         if (r.status) return;
         dmax = max(dmax, (uint32_t)r.s_dev);
         rmax = max(rmax, (uint32_t)r.s_rsv);
@@ -550,13 +621,23 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
     const uint32_t q = live ? qst[jj] : 1u;
     const uint32_t dm = dev_max[jj], rm = rsv_max[jj];
     const uint64_t pf = pref[jj];
+    const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
+    const PodF pff = to_podf(p, cfg);
+    const KCfg cv = cfg_in_vgprs(cfg);
+    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
+    const uint32_t mag = norm_magic(dm);
     uint64_t top[K];
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
     uint32_t unsup = 0;
     for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, [&](uint32_t rec) {
-        const PairX r = eval_pair_ext<false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
-                                          pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES);
+        C1Pair c1;
+        if (eval_c1(cfg, cv, e, nodes[rec].v, zones + rec, rec, n0, pff, px, dcls, q, req_aff, index_base, c1)) {
+            const int64_t tot = total_fb(cfg, c1.bk, c1.s_dev, dm, mag, c1.g, pf);
+            topk_ins<K>(top, c1.st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - c1.g)));
+            return;
+        }
+        const PairX r = eval_pair_ext<false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q, dcls);
         unsup |= r.status & KG_ST_UNSUPPORTED;
         const uint32_t g = index_base + node_index(nodes[rec]);
         const uint64_t key = ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
@@ -922,6 +1003,15 @@ hipError_t launch_rdev_codes(const NodeRec* nodes, const ZoneRec* zones, const D
     const uint32_t chunks = ((uint32_t)DEV_CLASSES + DSUM_CHUNK - 1) / DSUM_CHUNK;
     k_rdev_codes<<<dim3((n_rdev + 63) / 64, chunks), 64, 0, s>>>(nodes, zones, devs, rdev, rdev_rec, n_rdev, cls, n_cls, cfg, e,
                                                                  out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gpu_zone_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes,
+                               uint32_t n0, const DevClass* cls, uint32_t n_cls, const KCfg& cfg, const ExtDev& e,
+                               uint64_t* out, hipStream_t s) {
+    if (n_nodes <= n0 || n_cls == 0) return hipSuccess;
+    k_gpu_zone_sum<<<dim3((n_nodes - n0 + 63) / 64, std::min<uint32_t>(n_cls, (uint32_t)DEV_CLASSES)), 64, 0, s>>>(
+        nodes, zones, devs, n_nodes, n0, cls, cfg, e, out);
     return hipGetLastError();
 }
 

@@ -166,6 +166,9 @@ hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t 
 hipError_t launch_rdev_codes(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, const DevRec* rdev,
                              const uint32_t* rdev_rec, uint32_t n_rdev, const DevClass* cls, uint32_t n_cls,
                              const KCfg& cfg, const ExtDev& e, uint8_t* out, hipStream_t s);
+hipError_t launch_gpu_zone_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes,
+                               uint32_t n0, const DevClass* cls, uint32_t n_cls, const KCfg& cfg, const ExtDev& e,
+                               uint64_t* out, hipStream_t s);
 hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, uint32_t n0,
                           const DevClass* cls, uint32_t n_cls, const KCfg& cfg, const ExtDev& e, DevSum* out,
                           uint32_t* cls_max, hipStream_t s);

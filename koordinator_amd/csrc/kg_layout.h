@@ -138,8 +138,32 @@ struct alignas(64) ZoneRec {
     // per minor (nibble) the GPU's NUMA node id, KG_GPU_NUMA_ANY (NodeID -1) or KG_GPU_NUMA_NONE (no Topology):
     // DeviceShare as a NUMA hint provider (kg_node_columns.dev_numa)
     uint32_t dev_numa;
+    // per NUMA node (cpu_counts): available CPUs (RefCount < maxRefCount), of those the CPUs of whole free cores
+    // (required FullPCPUs), the cores with a free CPU (required SpreadByPCPUs), and the allocated CPUs (RefCount > 0,
+    // the amplified zone accounting of zone_cpu_alloc)
+    uint16_t cz_free[MAX_ZONES], cz_full[MAX_ZONES], cz_cores[MAX_ZONES], cz_alloc[MAX_ZONES];
 };
-static_assert(sizeof(ZoneRec) == 640, "the cpuset and GPU topology fields live in ZoneRec's tail padding");
+static_assert(sizeof(ZoneRec) == 704, "ZoneRec: zones, fast zone view, cpuset counts, GPU topology");
+// ZoneRec.status bit ZONE_RECORD_SHIFT + z: zone z holds an allocatedResources record (kg_node_columns.numa_zone_status)
+constexpr uint32_t ZONE_RECORD_SHIFT = KG_ZONE_RECORD_SHIFT;
+
+// extension.Amplify: ceil(v * ratio) for ratio > 1
+KG_HD inline int64_t amp_i64(int64_t v, double ratio) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return ratio > 1.0 ? (int64_t)ceil(__dmul_rn((double)v, ratio)) : v;
+#else
+    return ratio > 1.0 ? (int64_t)ceil((double)v * ratio) : v;
+#endif
+}
+
+// NodeAllocation.getAvailableNUMANodeResources (node_allocation.go:221-243): the cpu allocated in zone q as the topology
+// manager counts it; on an amplified node a zone with an allocation record counts its cpuset CPUs amplified
+KG_HD inline int64_t zone_cpu_alloc(const ZoneRec& z, uint32_t q) {
+    const int64_t u = z.cpu_used[q];
+    if (!((z.status >> (ZONE_RECORD_SHIFT + q)) & 1u) || !(z.amp_ratio > 1.0)) return u;
+    const int64_t cs = 1000 * (int64_t)z.cz_alloc[q];
+    return u - cs + amp_i64(cs, z.amp_ratio);
+}
 // ZoneRec.cpu_meta: bits 0-7 maxRefCount, 8-9 node CPU bind policy (KG_NODE_CPU_BIND_*), 10 NUMA allocate
 // strategy, 11-14 CPUs per core
 constexpr uint32_t CPU_META_BIND_SHIFT = 8, CPU_META_STRATEGY_SHIFT = 10, CPU_META_CPC_SHIFT = 11;
@@ -147,28 +171,45 @@ constexpr uint32_t CPU_META_BIND_SHIFT = 8, CPU_META_STRATEGY_SHIFT = 10, CPU_ME
 // The Filter's view of a node's allocated CPUs (ZoneRec.cpu_free / cpu_free_full / cpu_free_cores /
 // cpu_allocated), recomputed on the host at upload and on the device after a cpuset Reserve.
 KG_HD inline void cpu_counts(const kg_cpu_topo& t, const kg_cpu_alloc* a, int max_ref, ZoneRec& z) {
-    int free_core[KG_MAX_CPUS];
-    for (int k = 0; k < t.n_cores; k++) free_core[k] = 0;
+    int free_core[KG_MAX_CPUS], core_numa[KG_MAX_CPUS];
+    for (int k = 0; k < t.n_cores; k++) free_core[k] = 0, core_numa[k] = 0;
     int fr = 0, al = 0;
+    int zfree[MAX_ZONES] = {0, 0, 0, 0}, zalloc[MAX_ZONES] = {0, 0, 0, 0};
     for (int c = 0; c < t.n_cpus; c++) {
         const int ref = a ? a->ref[c] : 0;
+        const int q = t.numa[c];
+        core_numa[t.core[c]] = q;
         if (ref < max_ref) {
             fr++;
             free_core[t.core[c]]++;
+            if (q < MAX_ZONES) zfree[q]++;
         }
         al += ref > 0;
+        if (ref > 0 && q < MAX_ZONES) zalloc[q]++;
     }
     // filterCPUsByRequiredCPUBindPolicy counts a core for FullPCPUs when its free CPUs number CPUsPerCore()
     const int cpc = t.n_cores ? t.n_cpus / t.n_cores : 0;
     int full = 0, cores = 0;
+    int zfull[MAX_ZONES] = {0, 0, 0, 0}, zcores[MAX_ZONES] = {0, 0, 0, 0};
     for (int k = 0; k < t.n_cores; k++) {
         full += free_core[k] == cpc ? cpc : 0;
         cores += free_core[k] > 0;
+        const int q = core_numa[k];  // a core lies in one NUMA node
+        if (q < MAX_ZONES) {
+            zfull[q] += free_core[k] == cpc ? cpc : 0;
+            zcores[q] += free_core[k] > 0;
+        }
     }
     z.cpu_free = fr;
     z.cpu_free_full = full;
     z.cpu_free_cores = cores;
     z.cpu_allocated = al;
+    for (int q = 0; q < MAX_ZONES; q++) {
+        z.cz_free[q] = (uint16_t)zfree[q];
+        z.cz_full[q] = (uint16_t)zfull[q];
+        z.cz_cores[q] = (uint16_t)zcores[q];
+        z.cz_alloc[q] = (uint16_t)zalloc[q];
+    }
 }
 
 // NUMANodeSharedStatus after a cpuset allocation over the NUMA nodes `used` (bit per node): the pod's uid
@@ -240,8 +281,8 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
     }
     big = big || kg_big(v[N_CPUSET]) || kg_big(v[N_AMP_CPUSET]) || v[N_CPUSET] < 0 || v[N_AMP_CPUSET] < v[N_CPUSET];
     for (uint32_t q = 0; q < (uint32_t)MAX_ZONES; q++) {
-        const int64_t tc = z.cpu[q], tm = z.mem[q], uc = z.cpu_used[q], um = z.mem_used[q];
-        big = big || kg_big(tc) || kg_big(tm) || kg_big(uc) || kg_big(um) || uc < 0 || um < 0;
+        const int64_t tc = z.cpu[q], tm = z.mem[q], uc = zone_cpu_alloc(z, q), um = z.mem_used[q];
+        big = big || kg_big(tc) || kg_big(tm) || kg_big(uc) || kg_big(um) || z.cpu_used[q] < 0 || um < 0;
         const int64_t ac = tc - uc < 0 ? 0 : tc - uc, am = tm - um < 0 ? 0 : tm - um;
         const int64_t rc = tc - ac < 0 ? 0 : tc - ac, rm = tm - am < 0 ? 0 : tm - am;
         ZoneFast& zf = z.zf[q];
@@ -442,6 +483,9 @@ struct ExtDev {
     // per batch (with dsum): the GPU allocator's code of every restore table (rdev) for every GPU request class,
     // [table][DEV_CLASSES]; nullptr = run the allocator
     const uint8_t* rcode;
+    // per batch (with dsum): DeviceShare's contribution to the topology manager of the class-1 (SingleNUMANode)
+    // records, [record - n0][DEV_CLASSES] (gpu_zone_sum); nullptr = evaluate those records on the general path
+    const uint64_t* gz;
 };
 
 }  // namespace kg

@@ -177,6 +177,8 @@ struct kg_pods {
     uint32_t* d_reason = nullptr;  // replay: per pod OR of the filter status bits (kg_replay out_reason)
     DevSum* d_devsum = nullptr;    // per record DevSum of the last config-5 select
     size_t devsum_cap = 0;
+    uint64_t* d_gz = nullptr;      // gpu_zone_sum per (class-1 record, GPU request class) of the last config-5 select
+    size_t gz_cap = 0;
     uint8_t* d_rcode = nullptr;    // [kg_rsv_dev table][DEV_CLASSES]: GPU allocator outcome on the restore tables
     size_t rcode_cap = 0;
     // one-pass fast-base select of the GPU pods (ExtDev.cls_max / fb_max / rows): [cap] fast-base maxima, [cap] rows
@@ -507,7 +509,8 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
             return fail(ctx, KG_INVALID_ARG, "node %u: cpuset_alloc_milli %lld != 1000 x %d allocated CPUs", i,
                         (long long)v[N_CPUSET], zr->cpu_allocated);
     }
-    if (zr->status >> (2 * KG_MAX_ZONES)) return fail(ctx, KG_INVALID_ARG, "node %u: zone status 0x%x", i, zr->status);
+    if (zr->status >> (KG_ZONE_RECORD_SHIFT + KG_MAX_ZONES))  // 2 bits per zone, then the record bits
+        return fail(ctx, KG_INVALID_ARG, "node %u: zone status 0x%x", i, zr->status);
     // GPU topology tree / partition table (static)
     zr->dev_topo = s->dev_topo ? s->dev_topo[i] : ~0ull;
     zr->dev_part = s->dev_part ? s->dev_part[i] : 0u;
@@ -618,7 +621,9 @@ void count_topo(kg_snap* s) {
     uint32_t t = 0, b = 0;
     for (uint32_t p = 0; p < s->n; p++) {
         const uint32_t pol = rec_numa_policy(s->h_nodes[p]);
-        t += pol == KG_NUMA_BEST_EFFORT || pol == KG_NUMA_RESTRICTED;
+        // SingleNUMANode nodes with a node CPU bind policy bind every pod's cpus: the general topology manager too
+        const bool node_bind = p < s->h_zones.size() && ((s->h_zones[p].cpu_meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
+        t += pol == KG_NUMA_BEST_EFFORT || pol == KG_NUMA_RESTRICTED || (pol == KG_NUMA_SINGLE_NODE && node_bind);
         b += ((uint32_t)s->h_nodes[p].v[N_FLAGS] & F_BIG) != 0;
     }
     s->n_topo = t;
@@ -626,7 +631,10 @@ void count_topo(kg_snap* s) {
 }
 
 // Select-mode ext kernels may drop the general topology manager when nothing in the pair set needs it
-bool need_topo(const kg_snap* s, const kg_pods* p) { return s->n_topo != 0 || p->pod_policy; }
+// (a cpuset-binding pod on a SingleNUMANode node runs the general topology manager: its CPUs join every hint)
+bool need_topo(const kg_snap* s, const kg_pods* p) {
+    return s->n_topo != 0 || p->pod_policy || (p->any_cpu_bind && s->n > s->n0);
+}
 
 kg_status check_views(kg_snap* s) {
     if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->views_stale)
@@ -1477,7 +1485,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
                     (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
                     (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
-                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_spec, (void*)p->d_split, (void*)p->d_batch, (void*)p->d_rcode})
+                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_gz, (void*)p->d_spec, (void*)p->d_split, (void*)p->d_batch, (void*)p->d_rcode})
         hipFree(b);
     hipHostFree(p->h_in);
     hipHostFree(p->h_keys);
@@ -1616,6 +1624,13 @@ static uint32_t* spec_cls_max(kg_pods* p) { return p->d_spec + 2 * (size_t)p->ca
 static uint32_t* spec_n_rows(kg_pods* p) { return p->d_spec + 2 * (size_t)p->cap + DEV_CLASSES; }
 
 // config-5 matrix mode, pass 1: quota gate + per-pod NormalizeScore inputs of this shard
+// The fast-base kernels take the SingleNUMANode (class-1) records' DeviceShare hints from a per-class table.
+static bool gpu_zone_active(const kg_snap* s, const kg_pods* p) {
+    return s->n > s->n0 && (s->kcfg.plugins & KG_PLUGIN_DEV) && (s->kcfg.plugins & KG_PLUGIN_NUMA) && p->n_dclass != 0 &&
+           !std::getenv("KG_NO_GZ");
+}
+static bool gz_active(const kg_snap* s, const kg_pods* p) { return s->d_dev && ext_fast_base(s, p) && gpu_zone_active(s, p); }
+
 // The batch's DevSum table over this snapshot's records (fast-base config-5 select with DeviceShare).
 static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     kg_ctx* ctx = s->ctx;
@@ -1632,6 +1647,21 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(),
                                 p->d_devsum, spec_cls_max(p), ctx->stream));
     e.dsum = p->d_devsum;
+    e.gz = nullptr;
+    if (gz_active(s, p)) {  // DeviceShare's NUMA hints of the SingleNUMANode records, per class
+        const size_t need = (size_t)(s->n - s->n0) * DEV_CLASSES;
+        if (p->gz_cap < need) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(p->d_gz));
+            p->d_gz = nullptr;
+            p->gz_cap = 0;
+            HIP_TRY(ctx, hipMalloc(&p->d_gz, sizeof(uint64_t) * need));
+            p->gz_cap = need;
+        }
+        HIP_TRY(ctx, launch_gpu_zone_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg,
+                                         s->ext_dev(), p->d_gz, ctx->stream));
+        e.gz = p->d_gz;
+    }
     e.rcode = nullptr;
     if (s->n_rdev && s->d_rdev && p->n_dclass) {  // the GPU restore tables of the reservation views, per class
         const size_t need = (size_t)s->n_rdev * DEV_CLASSES;
@@ -1815,6 +1845,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     ExtDev xe = s->ext_dev();
     xe.dsum = (s->d_dev && ext_fast_base(s, p)) ? p->d_devsum : nullptr;  // ext_stats_local built it for this batch
     xe.rcode = (xe.dsum && s->n_rdev && p->n_dclass) ? p->d_rcode : nullptr;   // and the restore tables' codes
+    xe.gz = (xe.dsum && gz_active(s, p)) ? p->d_gz : nullptr;                 // and the class-1 records' GPU hints
     const bool guess = fb && xe.dsum && (s->cfg.plugins & KG_PLUGIN_DEV) && p->n_stat > p->n_stat_cls;
     if (guess) {
         xe.cls_max = spec_cls_max(p);

@@ -262,15 +262,33 @@ typedef struct numa_zones {
     int64_t tot[2][KG_MAX_ZONES], used[2][KG_MAX_ZONES], avail[2][KG_MAX_ZONES];
 } numa_zones;
 
+static const kg_cpu_topo* cpu_topology(const kg_node_columns* n, uint32_t i);
+
+/* CPUs of NUMA node z with an allocation (RefCount > 0): allocatedCPUs.CPUsInNUMANodes(z) */
+static void cpus_allocated_by_zone(const kg_node_columns* n, uint32_t i, const kg_cpu_topo* t, int64_t cs[KG_MAX_ZONES]) {
+    for (int z = 0; z < KG_MAX_ZONES; z++) cs[z] = 0;
+    for (int c = 0; t && n->cpu_alloc && c < t->n_cpus; c++)
+        if (n->cpu_alloc[i].ref[c] > 0 && t->numa[c] < KG_MAX_ZONES) cs[t->numa[c]]++;
+}
+
+/* NodeAllocation.getAvailableNUMANodeResources (node_allocation.go:221-243): a zone's allocated resources (its
+ * allocatedResources record, numa_zone_status bit KG_ZONE_RECORD_SHIFT + z) on an amplified node count the zone's
+ * cpuset CPUs amplified (allocated - cs * 1000 + Amplify(cs * 1000)); available = total - allocated, not below 0 */
 static void numa_zones_load(const kg_node_columns* n, uint32_t i, numa_zones* x) {
     memset(x, 0, sizeof(*x));
     x->Z = n->numa_zones[i];
     x->status = n->numa_zone_status ? n->numa_zone_status[i] : 0;
+    const double ratio = n->cpu_amp_ratio ? n->cpu_amp_ratio[i] : 1.0;
+    const kg_cpu_topo* t = ratio > 1 ? cpu_topology(n, i) : NULL;
+    int64_t cs[KG_MAX_ZONES];
+    cpus_allocated_by_zone(n, i, t, cs);
     for (uint32_t z = 0; z < x->Z && z < KG_MAX_ZONES; z++) {
         x->tot[0][z] = n->zone_cpu[z][i];
         x->tot[1][z] = n->zone_mem[z][i];
         x->used[0][z] = n->zone_cpu_used[z][i];
         x->used[1][z] = n->zone_mem_used[z][i];
+        if (t && ((x->status >> (KG_ZONE_RECORD_SHIFT + z)) & 1u))
+            x->used[0][z] += kgo_amplify(cs[z] * 1000, ratio) - cs[z] * 1000;
         for (int r = 0; r < 2; r++) x->avail[r][z] = sub_nonneg(x->tot[r][z], x->used[r][z]); /* node_allocation.go:240 */
     }
 }
@@ -279,8 +297,17 @@ static void numa_zones_load(const kg_node_columns* n, uint32_t i, numa_zones* x)
  * zones of `mask`. The per-resource zone order comes from sort.Slice whose less(i, j) reads
  * totalAvailable by the positions i, j rather than by the zone ids being sorted (:276-279); sort.Slice
  * runs insertion sort for n <= 12, so the swaps depend only on the availability of zones 0..n-1. */
+/* A cpuset-binding pod under a NUMA policy (ResourceOptions with requestCPUBind): what tryAllocateFromNode checks
+ * of its CPUs under a hint (resource_manager.go:168-194 trimNUMANodeResources, :320-334 splitQuantity, :357-463
+ * allocateCPUSet). cnt[z]: the available CPUs (RefCount < maxRefCount) of NUMA node z after
+ * filterCPUsByRequiredCPUBindPolicy when the policy is required. */
+typedef struct numa_bind {
+    int required, full, cpc, needed;
+    int64_t cnt[KG_MAX_ZONES];
+} numa_bind;
+
 static int numa_split(const numa_zones* x, uint32_t mask, const int64_t* req, const int* has,
-                      int64_t alloc[2][KG_MAX_ZONES]) {
+                      int64_t alloc[2][KG_MAX_ZONES], const numa_bind* b) {
     int nodes[KG_MAX_ZONES], n = 0;
     for (uint32_t z = 0; z < x->Z; z++)
         if ((mask >> z) & 1u) nodes[n++] = (int)z;
@@ -298,6 +325,10 @@ static int numa_split(const numa_zones* x, uint32_t mask, const int64_t* req, co
         int64_t q = req[r];
         for (int t = 0; t < n; t++) {
             int64_t split = q / (n - t); /* splitQuantity :320-334 (milli-cpu / bytes) */
+            if (r == 0 && b) {           /* requestCPUBind: whole CPUs of quantity.Value() (rounded up) */
+                const int64_t v = (q + 999) / 1000;
+                split = b->required && b->full ? (v / b->cpc) / (n - t) * b->cpc * 1000 : v / (n - t) * 1000;
+            }
             int64_t av = x->avail[r][s[t]];
             int64_t got = av > split ? split : av; /* allocateRes :336-355 */
             if (got != 0) {
@@ -308,6 +339,25 @@ static int numa_split(const numa_zones* x, uint32_t mask, const int64_t* req, co
         if (q != 0) return 0; /* "Insufficient NUMA <resource>" */
     }
     return 1;
+}
+
+/* allocateCPUSet over the allocated NUMA nodes (resource_manager.go:391-429): on each, min(its available CPUs,
+ * allocated cpu / 1000) CPUs (takePreferredCPUs takes exactly that many when they are available); together they must
+ * number numCPUsNeeded (ErrNotEnoughCPUs), and a required FullPCPUs policy needs whole cores on each
+ * (satisfiedRequiredCPUBindPolicy :452-460; the filtered CPUs hold whole free cores, so a take of a multiple of
+ * CPUsPerCore is whole cores). 0, KG_ST_NUMA_CPUS or KG_ST_NUMA_CPU_BIND. */
+static uint32_t numa_bind_check(const numa_bind* b, const int64_t al[2][KG_MAX_ZONES], uint32_t Z) {
+    int64_t sum = 0;
+    int partial = 0;
+    for (uint32_t z = 0; z < Z && z < KG_MAX_ZONES; z++) {
+        if (al[0][z] == 0 && al[1][z] == 0) continue; /* not an allocated NUMA node */
+        int64_t k = al[0][z] / 1000;
+        if (b->cnt[z] < k) k = b->cnt[z];
+        sum += k;
+        partial |= b->required && b->full && (k % b->cpc) != 0;
+    }
+    if (sum != b->needed) return KG_ST_NUMA_CPUS;
+    return partial ? KG_ST_NUMA_CPU_BIND : 0u;
 }
 
 typedef struct numa_hint {
@@ -328,7 +378,7 @@ typedef struct numa_lists {
  * size, or every hint under Restricted. A requested resource without hints contributes one unsatisfied
  * nil hint and a reason (policy.go:166-173). */
 static void numa_hints(const kg_config* c, const numa_zones* x, const int64_t* req, const int* has, uint32_t policy,
-                       numa_lists* L) {
+                       numa_lists* L, const numa_bind* b, int64_t score_cpu) {
     const uint32_t Z = x->Z;
     uint32_t lack[2] = {0, 0};
     for (uint32_t z = 0; z < Z; z++)
@@ -348,9 +398,11 @@ static void numa_hints(const kg_config* c, const numa_zones* x, const int64_t* r
                     A[r] += x->avail[r][z];
                 }
         /* numaScorer over requested = SubtractWithNonNegativeResult(total, available) */
-        score[k] = numa_hint_score(c, T[0], sub_nonneg(T[0], A[0]) + req[0], T[1], sub_nonneg(T[1], A[1]) + req[1]);
+        /* (the pod's requests as the options hold them: a cpuset-binding pod's cpu amplified, score_cpu) */
+        score[k] = numa_hint_score(c, T[0], sub_nonneg(T[0], A[0]) + score_cpu, T[1], sub_nonneg(T[1], A[1]) + req[1]);
         int64_t al[2][KG_MAX_ZONES];
-        if (!numa_split(x, m, req, has, al)) continue;
+        if (!numa_split(x, m, req, has, al, b)) continue;
+        if (b && numa_bind_check(b, al, Z)) continue;
         for (int r = 0; r < 2; r++) {
             if (!has[r] || (m & lack[r])) continue;
             if (popcount32(m) < minsize[r]) minsize[r] = popcount32(m);
@@ -450,9 +502,9 @@ typedef struct gpu_hints {
  * which matters only when two merged hints tie on preference, width and score (parity unpinned there).
  * gh (nullable): the DeviceShare provider's list of a GPU pod (not failed). */
 static uint32_t numa_admit(const kg_config* c, const numa_zones* x, const int64_t* req, const int* has, uint32_t policy,
-                           int excl, uint32_t* mask_out, const gpu_hints* gh) {
+                           int excl, uint32_t* mask_out, const gpu_hints* gh, const numa_bind* b, int64_t score_cpu) {
     numa_lists L;
-    numa_hints(c, x, req, has, policy, &L);
+    numa_hints(c, x, req, has, policy, &L, b, score_cpu);
     const uint32_t all = (1u << x->Z) - 1u;
     *mask_out = 0;
     if (L.reasons && policy != KG_NUMA_BEST_EFFORT) return KG_ST_NUMA_UNSATISFIED;
@@ -645,9 +697,11 @@ static int cpuset_allocate(const kg_node_columns* n, uint32_t i, const kg_pod_co
     return 0;
 }
 
-/* the cpuset part of Filter for a pod that binds CPUs on node i (plugin.go:396-440) */
+/* the cpuset part of Filter for a pod that binds CPUs on node i (plugin.go:396-440). Under a NUMA policy the CPUs
+ * are part of every allocation the topology manager tries (numa_bind); under None a required policy allocates in
+ * Filter (tryAllocateFromNode), a preferred one only at Reserve: *zone_out = KGO_ZONE_CPUSET_FAIL when that fails */
 static uint32_t cpuset_filter(const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j, uint32_t policy,
-                              uint32_t node_bind) {
+                              uint32_t node_bind, int32_t* zone_out) {
     const kg_cpu_topo* t = cpu_topology(n, i);
     if (!t) return KG_ST_NUMA_CPU_TOPO; /* ErrInvalidCPUTopology */
     const uint32_t pod_pol = (p->flags[j] >> KG_POD_CPU_POLICY_SHIFT) & 3u;
@@ -659,16 +713,32 @@ static uint32_t cpuset_filter(const kg_node_columns* n, uint32_t i, const kg_pod
     const int64_t needed = p->req_cpu[j] / 1000;
     if (required == KG_CPU_BIND_FULL_PCPUS && needed % (t->n_cpus / t->n_cores) != 0)
         return KG_ST_NUMA_CPU_BIND; /* ErrSMTAlignmentError */
-    if (policy != KG_NUMA_NONE) return KG_ST_UNSUPPORTED; /* cpusets inside NUMA hints: host path */
+    if (policy != KG_NUMA_NONE) return 0;
     uint64_t out[4];
     if (required != KG_CPU_BIND_NONE) {
         if (cpuset_allocate(n, i, p, j, node_bind, out)) return KG_ST_NUMA_CPUS; /* tryAllocateFromNode */
         return 0;
     }
-    /* no allocation in Filter; the Reserve's allocateCPUSet fails when the node has too few CPUs left, which
-     * the device path hands back to the host */
-    if (cpuset_allocate(n, i, p, j, node_bind, out)) return KG_ST_UNSUPPORTED;
+    /* no allocation in Filter; the Reserve's allocateCPUSet fails (ErrNotEnoughCPUs) when the node has too few CPUs */
+    if (cpuset_allocate(n, i, p, j, node_bind, out)) *zone_out = KGO_ZONE_CPUSET_FAIL;
     return 0;
+}
+
+/* numa_bind of a cpuset-binding pod on node i (getCPUBindPolicy, util.go:101-119; getAvailableCPUs and
+ * filterCPUsByRequiredCPUBindPolicy per NUMA node) */
+static void numa_bind_load(const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j, uint32_t node_bind,
+                           numa_bind* b) {
+    const kg_cpu_topo* t = cpu_topology(n, i);
+    const uint32_t bind = cpu_bind_policy(p, j, node_bind, &b->required);
+    b->full = bind == KG_CPU_BIND_FULL_PCPUS;
+    b->cpc = t->n_cores ? t->n_cpus / t->n_cores : 1;
+    b->needed = (int)(p->req_cpu[j] / 1000);
+    uint64_t avail[4];
+    cpu_available(n, i, t, avail);
+    if (b->required) cpu_filter_required(t, bind, avail);
+    for (int z = 0; z < KG_MAX_ZONES; z++) b->cnt[z] = 0;
+    for (int c = 0; c < t->n_cpus; c++)
+        if (((avail[c >> 6] >> (c & 63)) & 1ull) && t->numa[c] < KG_MAX_ZONES) b->cnt[t->numa[c]]++;
 }
 
 /* DeviceShare as a NUMA hint provider for a GPU pod (defined with the GPU allocator below). The site: the pair's
@@ -725,7 +795,7 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
         if (need > n->alloc_cpu[i] - requested) return KG_ST_NUMA_AMP_CPU;
     }
     if (cpu_bind) {
-        const uint32_t st = cpuset_filter(n, i, p, j, policy, node_bind);
+        const uint32_t st = cpuset_filter(n, i, p, j, policy, node_bind, zone_out);
         if (st) return st;
     }
     if (policy == KG_NUMA_NONE) {
@@ -750,6 +820,22 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
     /* podNUMAExclusive defaults to Required when the pod carries its own NUMA policy (plugin.go:449-454) */
     const int excl = p->numa_policy[j] != KG_NUMA_NONE;
     uint32_t mask = 0;
+    /* a cpuset-binding pod: the CPUs of every allocation under a hint (numa_bind), the cpu available to a required
+     * policy trimmed to its filtered CPUs (trimNUMANodeResources, resource_manager.go:159-194), its cpu request
+     * amplified where the options' requests count (hint scores, scores; getResourceOptions, plugin.go:774-778), and
+     * the Score's requested cpu = the node's cpuset CPUs amplified (calculateAllocatableAndRequested, scoring.go:190-197) */
+    numa_bind nb;
+    const numa_bind* bp = NULL;
+    int64_t score_cpu = pod_cpu;
+    if (cpu_bind) {
+        numa_bind_load(n, i, p, j, node_bind, &nb);
+        bp = &nb;
+        if (nb.required)
+            for (uint32_t z = 0; z < x.Z && z < KG_MAX_ZONES; z++)
+                if (x.avail[0][z] > nb.cnt[z] * 1000) x.avail[0][z] = nb.cnt[z] * 1000;
+        score_cpu = kgo_amplify(pod_cpu, ratio);
+    }
+    const int64_t bind_cpu = kgo_amplify(n->cpuset_alloc_milli[i], ratio);
     if (policy == KG_NUMA_BEST_EFFORT) {
         /* Filter: nothing more; Score: node allocatable / requested without an allocation (scoring.go:184-189).
          * The zone is what the Reserve would do: FilterByNUMANode under BestEffort (always admits) and the
@@ -758,6 +844,13 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
          * (resource_manager.go:133-136), tryBestToDistributeEvenly -> "Insufficient NUMA <r>" (:300-309) */
         *score_out = numa_node_score(c, n->alloc_cpu[i], N_REQ_CPU(n, i, ov) + pod_cpu, n->alloc_mem[i],
                                      N_REQ_MEM(n, i, ov) + p->req_mem[j]);
+        if (cpu_bind) { /* Score's tryAllocateFromNode without an affinity: the node's CPUs, else score 0 */
+            uint64_t out[4];
+            *score_out = cpuset_allocate(n, i, p, j, node_bind, out)
+                             ? 0
+                             : numa_node_score(c, n->alloc_cpu[i], bind_cpu + score_cpu, n->alloc_mem[i],
+                                               N_REQ_MEM(n, i, ov) + p->req_mem[j]);
+        }
         if (x.Z == 0) {
             *zone_out = KGO_ZONE_RESERVE_FAIL | (int32_t)(KG_ST_NUMA_INSUF_NODE >> 12);
             return 0;
@@ -773,14 +866,23 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
                 return 0;
             }
         }
-        numa_admit(c, &x, req, has, policy, excl, &mask, gx ? &gh : NULL);
+        numa_admit(c, &x, req, has, policy, excl, &mask, gx ? &gh : NULL, bp, score_cpu);
         int64_t al[2][KG_MAX_ZONES];
         int32_t fail = 0;
         for (int r = 0; r < 2 && mask; r++) {
             const int one[2] = {r == 0 && has[0], r == 1 && has[1]};
-            if (one[r] && !numa_split(&x, mask, req, one, al)) fail |= 1 << r;
+            if (one[r] && !numa_split(&x, mask, req, one, al, bp)) fail |= 1 << r;
         }
         *zone_out = fail ? KGO_ZONE_RESERVE_FAIL | fail : numa_code(mask);
+        if (!fail && bp) { /* allocateCPUSet over the allocated NUMA nodes (the whole node without an affinity) */
+            uint64_t out[4];
+            if (mask) {
+                numa_split(&x, mask, req, has, al, bp);
+                if (numa_bind_check(bp, al, x.Z)) fail = *zone_out = KGO_ZONE_CPUSET_FAIL;
+            } else if (cpuset_allocate(n, i, p, j, node_bind, out)) {
+                fail = *zone_out = KGO_ZONE_CPUSET_FAIL;
+            }
+        }
         if (!fail && gx) {
             uint32_t minors;
             const uint32_t st = gpu_alloc_site(c, n, i, p, j, gx, mask, &minors);
@@ -794,10 +896,17 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
         gpu_numa_hints(c, n, i, p, j, gx, &gh);
         if (gh.fail) return gh.code; /* the provider's status (manager.go:80-87) */
     }
-    uint32_t st = numa_admit(c, &x, req, has, policy, excl, &mask, gx ? &gh : NULL);
+    uint32_t st = numa_admit(c, &x, req, has, policy, excl, &mask, gx ? &gh : NULL, bp, score_cpu);
     if (st) return st;
     int64_t al[2][KG_MAX_ZONES];
-    if (mask && !numa_split(&x, mask, req, has, al)) return KG_ST_UNSUPPORTED; /* not reached: preferred hints place */
+    /* allocateResources under the best hint: not reached with a mask (a preferred best hint is one of the providers'
+     * feasible masks); without one a cpuset-binding pod takes CPUs from the whole node */
+    if (mask && !numa_split(&x, mask, req, has, al, bp)) return KG_ST_UNSUPPORTED;
+    if (mask && bp && numa_bind_check(bp, al, x.Z)) return KG_ST_UNSUPPORTED;
+    if (!mask && bp) {
+        uint64_t out[4];
+        if (cpuset_allocate(n, i, p, j, node_bind, out)) return KG_ST_NUMA_CPUS;
+    }
     if (gx) { /* allocateResources: DeviceShare's Allocate under the best hint (topology_hint.go:100-157) */
         uint32_t minors;
         const uint32_t st2 = gpu_alloc_site(c, n, i, p, j, gx, mask, &minors);
@@ -806,10 +915,11 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
         gx->mask = mask;
     }
     *zone_out = numa_code(mask);
-    if (!mask) {
-        /* calculateAllocatableAndRequested without NUMA allocation: node allocatable / requested */
-        *score_out = numa_node_score(c, n->alloc_cpu[i], N_REQ_CPU(n, i, ov) + pod_cpu, n->alloc_mem[i],
-                                     N_REQ_MEM(n, i, ov) + p->req_mem[j]);
+    if (!mask || !(p->req_cpu[j] | p->req_mem[j])) {
+        /* calculateAllocatableAndRequested without NUMANodeResources (no affinity, or no cpu / memory request):
+         * node allocatable / requested (scoring.go:168-189) */
+        *score_out = numa_node_score(c, n->alloc_cpu[i], (bp ? bind_cpu : N_REQ_CPU(n, i, ov)) + score_cpu,
+                                     n->alloc_mem[i], N_REQ_MEM(n, i, ov) + p->req_mem[j]);
         return 0;
     }
     /* the zones that received an allocation: their totals and their allocated */
@@ -821,7 +931,7 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
             U[r] += x.used[r][z];
         }
     }
-    *score_out = numa_node_score(c, T[0], U[0] + pod_cpu, T[1], U[1] + p->req_mem[j]);
+    *score_out = numa_node_score(c, T[0], (bp ? bind_cpu : U[0]) + score_cpu, T[1], U[1] + p->req_mem[j]);
     return 0;
 }
 
@@ -1282,20 +1392,117 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
 /* NodeNUMAResource Reserve of a cpuset-binding pod on a NUMA-policy-None node: the accumulator's CPUs
  * enter NodeAllocation.allocatedCPUs (addPodAllocation, node_allocation.go:111-130: RefCount++, the pod's
  * exclusive policy), and cpuset_alloc_milli follows the allocated CPU count */
-static int cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j) {
+/* resourceManager.Allocate of a cpuset-binding pod on node i (resource_manager.go:197-262,357-463): under the NUMA
+ * affinity `mask` the split of its requests over those NUMA nodes (*al, *have_al = 1) and one take per allocated node,
+ * without one a take over the node; the CPUs in out. Returns 1 when it fails. */
+static int numa_bind_take(const kg_node_columns* v, uint32_t i, const kg_pod_columns* p, uint32_t j, uint32_t node_bind,
+                          uint32_t mask, uint64_t out[4], int64_t al[2][KG_MAX_ZONES], int* have_al) {
+    *have_al = 0;
+    for (int w = 0; w < 4; w++) out[w] = 0;
+    if (!mask) return cpuset_allocate(v, i, p, j, node_bind, out) ? 1 : 0;
+    const kg_cpu_topo* t = cpu_topology(v, i);
+    if (!t) return 1;
+    numa_zones x;
+    numa_zones_load(v, i, &x);
+    numa_bind nb;
+    numa_bind_load(v, i, p, j, node_bind, &nb);
+    if (nb.required)
+        for (uint32_t z = 0; z < x.Z && z < KG_MAX_ZONES; z++)
+            if (x.avail[0][z] > nb.cnt[z] * 1000) x.avail[0][z] = nb.cnt[z] * 1000;
+    const int64_t req[2] = {p->req_cpu[j], p->req_mem[j]};
+    const int has[2] = {(p->flags[j] & KG_POD_HAS_CPU) != 0, (p->flags[j] & KG_POD_HAS_MEM) != 0};
+    if (!numa_split(&x, mask, req, has, al, &nb) || numa_bind_check(&nb, al, x.Z)) return 1;
+    *have_al = 1;
+    int required;
+    const uint32_t pol = cpu_bind_policy(p, j, node_bind, &required);
+    const uint32_t excl = (p->flags[j] >> KG_POD_CPU_EXCL_SHIFT) & 3u;
+    uint64_t avail[4];
+    cpu_available(v, i, t, avail);
+    if (required) cpu_filter_required(t, pol, avail);
+    const uint32_t strategy = v->cpu_strategy ? v->cpu_strategy[i] : KG_NUMA_MOST_ALLOCATED;
+    const kg_cpu_alloc* alloc = v->cpu_alloc ? &v->cpu_alloc[i] : NULL;
+    for (uint32_t z = 0; z < x.Z && z < KG_MAX_ZONES; z++) {
+        if (al[0][z] == 0 && al[1][z] == 0) continue;
+        int64_t k = al[0][z] / 1000;
+        if (nb.cnt[z] < k) k = nb.cnt[z];
+        if (k == 0) continue;
+        uint64_t in_z[4] = {0, 0, 0, 0}, got[4];
+        for (int cc = 0; cc < t->n_cpus; cc++)
+            if (t->numa[cc] == z && ((avail[cc >> 6] >> (cc & 63)) & 1ull)) in_z[cc >> 6] |= 1ull << (cc & 63);
+        if (kgo_take_cpus(t, cpu_max_ref(v, i), in_z, alloc, (int)k, (int)pol, (int)excl, (int)strategy, got)) return 1;
+        for (int w = 0; w < 4; w++) out[w] |= got[w];
+    }
+    return 0;
+}
+
+int kgo_numa_hints(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j,
+                   uint32_t policy, uint32_t out[2 * 16], int32_t len[2]) {
+    numa_zones x;
+    numa_zones_load(n, i, &x);
+    if (x.Z == 0) return -1;
+    const uint32_t node_bind = n->cpu_bind_policy ? n->cpu_bind_policy[i] : KG_NODE_CPU_BIND_NONE;
+    const int bind = (p->flags[j] & KG_POD_CPU_BIND) || (node_bind != KG_NODE_CPU_BIND_NONE && p->req_cpu[j] != 0);
+    numa_bind nb;
+    int64_t score_cpu = p->req_cpu[j];
+    if (bind) {
+        numa_bind_load(n, i, p, j, node_bind, &nb);
+        if (nb.required)
+            for (uint32_t z = 0; z < x.Z && z < KG_MAX_ZONES; z++)
+                if (x.avail[0][z] > nb.cnt[z] * 1000) x.avail[0][z] = nb.cnt[z] * 1000;
+        score_cpu = kgo_amplify(p->req_cpu[j], n->cpu_amp_ratio[i]);
+    }
+    const int64_t req[2] = {p->req_cpu[j], p->req_mem[j]};
+    const int has[2] = {(p->flags[j] & KG_POD_HAS_CPU) != 0, (p->flags[j] & KG_POD_HAS_MEM) != 0};
+    numa_lists L;
+    numa_hints(c, &x, req, has, policy, &L, bind ? &nb : NULL, score_cpu);
+    for (int li = 0; li < L.n_lists; li++) {
+        len[li] = L.len[li];
+        for (int t = 0; t < L.len[li]; t++)
+            out[16 * li + t] = L.h[li][t].mask | (L.h[li][t].pref ? 0x100u : 0u) | (L.h[li][t].unsat ? 0x200u : 0u);
+    }
+    return L.n_lists;
+}
+
+int kgo_numa_allocate(const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j, uint32_t mask,
+                      uint64_t cpus[4], int64_t al_out[2 * KG_MAX_ZONES]) {
+    const uint32_t node_bind = n->cpu_bind_policy ? n->cpu_bind_policy[i] : KG_NODE_CPU_BIND_NONE;
+    const int bind = (p->flags[j] & KG_POD_CPU_BIND) || (node_bind != KG_NODE_CPU_BIND_NONE && p->req_cpu[j] != 0);
+    int64_t al[2][KG_MAX_ZONES];
+    memset(al, 0, sizeof(al));
+    for (int w = 0; w < 4; w++) cpus[w] = 0;
+    if (bind) {
+        int have;
+        if (numa_bind_take(n, i, p, j, node_bind, mask, cpus, al, &have)) return 1;
+    } else if (mask) {
+        numa_zones x;
+        numa_zones_load(n, i, &x);
+        const int64_t req[2] = {p->req_cpu[j], p->req_mem[j]};
+        const int has[2] = {(p->flags[j] & KG_POD_HAS_CPU) != 0, (p->flags[j] & KG_POD_HAS_MEM) != 0};
+        if (!numa_split(&x, mask, req, has, al, NULL)) return 1;
+    }
+    memcpy(al_out, al, sizeof(al));
+    return 0;
+}
+
+/* NodeNUMAResource Reserve of a cpuset-binding pod (plugin.go:585-635 -> resourceManager.Allocate / Update): the CPUs
+ * of numa_bind_take under the affinity of the pair's zone code enter the node's allocation (*al: the NUMA split the
+ * Reserve records). Returns 1 when Allocate fails (nothing of the pod is applied). */
+static int cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,
+                          int64_t al[2][KG_MAX_ZONES], int* have_al) {
+    *have_al = 0;
     if (!(c->plugins & KG_PLUGIN_NUMA) || !st->cpu_topo || (p->flags[j] & KG_POD_NUMA_SKIP)) return 0;
     const uint32_t node_bind = st->cpu_bind[i];
     const int bind = (p->flags[j] & KG_POD_CPU_BIND) || (node_bind != KG_NODE_CPU_BIND_NONE && p->req_cpu[j] != 0);
     if (!bind) return 0;
     int conflict;
-    if (numa_merge_policy(st->numa_policy[i], p->numa_policy[j], &conflict) != KG_NUMA_NONE) return 0;
+    const uint32_t policy = numa_merge_policy(st->numa_policy[i], p->numa_policy[j], &conflict);
     kg_node_columns v;
     kgo_state_view(st, &v);
     uint64_t out[4];
-    /* Allocate fails (Reserve returns the error, plugin.go:585-635): nothing of the pod is applied */
-    if (cpuset_allocate(&v, i, p, j, node_bind, out)) return 1;
     const uint32_t excl = (p->flags[j] >> KG_POD_CPU_EXCL_SHIFT) & 3u;
     const kg_cpu_topo* t = cpu_topology(&v, i);
+    const uint32_t mask = (policy != KG_NUMA_NONE && zone >= 0 && !zone_fails(zone)) ? numa_code_mask(zone) : 0u;
+    if (numa_bind_take(&v, i, p, j, node_bind, mask, out, al, have_al)) return 1;
     int allocated = 0;
     uint32_t used = 0; /* usedNUMA: NUMA nodes of the CPUs taken */
     for (int cc = 0; cc < t->n_cpus; cc++) {
@@ -1323,7 +1530,9 @@ static int cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const k
  * cpuset accumulator fails (nothing applied), else 0 */
 static int apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,
                  int64_t sign) {
-    if (sign > 0 && cpuset_reserve(c, st, i, p, j)) return KGO_ZONE_CPUSET_FAIL;
+    int64_t bal[2][KG_MAX_ZONES];
+    int have_bal = 0;
+    if (sign > 0 && cpuset_reserve(c, st, i, p, j, zone, bal, &have_bal)) return KGO_ZONE_CPUSET_FAIL;
     /* upstream NodeInfo.AddPod / RemovePod: Requested, NonZeroRequested, len(Pods) */
     st->col[C_REQ_CPU][i] += sign * p->req_cpu[j];
     st->col[C_REQ_MEM][i] += sign * p->req_mem[j];
@@ -1353,7 +1562,9 @@ static int apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_col
         uint32_t mask = numa_code_mask(zone);
         int64_t al[2][KG_MAX_ZONES];
         memset(al, 0, sizeof(al));
-        if (popcount32(mask) == 1) {
+        if (have_bal) {
+            memcpy(al, bal, sizeof(al));
+        } else if (popcount32(mask) == 1) {
             int z = __builtin_ctz(mask);
             al[0][z] = p->req_cpu[j];
             al[1][z] = p->req_mem[j];
@@ -1365,11 +1576,13 @@ static int apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_col
             const int64_t req[2] = {p->req_cpu[j], p->req_mem[j]};
             const int has[2] = {(p->flags[j] & KG_POD_HAS_CPU) != 0, (p->flags[j] & KG_POD_HAS_MEM) != 0};
             /* a multi-zone split is only reproducible before the Reserve: Unreserve of one is not restated */
-            if (sign > 0) numa_split(&x, mask, req, has, al);
+            if (sign > 0) numa_split(&x, mask, req, has, al, NULL);
         }
         for (uint32_t z = 0; z < KG_MAX_ZONES; z++) {
             st->col[C_ZONE_CPU_USED + z][i] += sign * al[0][z];
             st->col[C_ZONE_MEM_USED + z][i] += sign * al[1][z];
+            /* addPodAllocation creates the zone's allocatedResources record; release never removes it */
+            if (sign > 0 && (al[0][z] != 0 || al[1][z] != 0)) st->zone_status[i] |= 1u << (KG_ZONE_RECORD_SHIFT + z);
         }
     }
     return 0;

@@ -107,6 +107,15 @@ int kgo_ext_shard_select(const kg_config* cfg, const kg_node_columns* nodes, uin
 
 /* cpuset accumulator (nodenumaresource/cpu_accumulator.go takeCPUs / takePreferredCPUs, kg_cpuset.c):
  * 0 = ok (out = the chosen CPUs), -1 = ErrNotEnoughCPUs, -2 = "failed to allocate cpus". */
+/* Test hook: resourceManager.Allocate of pod j on node i under the NUMA affinity `mask` (0 = none): 0 with the CPUs of a
+ * cpuset-binding pod and the NUMA split [resource][zone] (cpu milli, memory bytes), or 1 (resource_manager.go:197-262). */
+/* Test hook: the NodeNUMAResource hint lists of pod j on node i (resourceManager.GetTopologyHints + filterProvidersHints)
+ * for the requested resources, cpu then memory: per hint mask | 0x100 Preferred | 0x200 the unsatisfied nil hint of an
+ * empty list. Returns the number of lists, -1 without NUMA nodes. */
+int kgo_numa_hints(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j,
+                   uint32_t policy, uint32_t out[2 * 16], int32_t len[2]);
+int kgo_numa_allocate(const kg_node_columns* n, uint32_t i, const kg_pod_columns* p, uint32_t j, uint32_t mask,
+                      uint64_t cpus[4], int64_t al[2 * KG_MAX_ZONES]);
 int kgo_take_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t avail[4], const kg_cpu_alloc* allocated,
                   int needed, int bind_policy, int excl_policy, int strategy, uint64_t out[4]);
 int kgo_take_preferred_cpus(const kg_cpu_topo* t, int max_ref, const uint64_t avail[4], const uint64_t preferred[4],

@@ -110,6 +110,12 @@ def lib():
         L.kgo_gpu_alloc_numa.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns),
                                          C.c_uint32, C.c_uint32, P(C.c_uint32)]
         L.kgo_gpu_alloc_numa.restype = C.c_uint32
+        L.kgo_numa_allocate.argtypes = [P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns), C.c_uint32, C.c_uint32,
+                                        P(C.c_uint64), P(C.c_int64)]
+        L.kgo_numa_allocate.restype = C.c_int
+        L.kgo_numa_hints.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
+                                     C.c_uint32, P(C.c_uint32), P(C.c_int32)]
+        L.kgo_numa_hints.restype = C.c_int
         L.kgo_mem_bytes_to_ratio.argtypes = [C.c_int64, C.c_int64]
         L.kgo_mem_bytes_to_ratio.restype = C.c_int64
         L.kgo_amplify.argtypes = [C.c_int64, C.c_double]
@@ -204,6 +210,31 @@ def gpu_alloc_numa(cfg, nodes: abi.Table, pods: abi.Table, numa: int, node: int 
     minors = C.c_uint32(0)
     code = lib().kgo_gpu_alloc_numa(C.byref(cfg), C.byref(nc), node, C.byref(pc), pod, numa, C.byref(minors))
     return int(code), int(minors.value)
+
+
+def numa_hints(cfg, nodes: abi.Table, pods: abi.Table, policy: int, node: int = 0, pod: int = 0):
+    """NodeNUMAResource's hint lists of the requested resources (cpu, then memory): [[(mask, preferred)]]; an empty
+    list for a resource without hints."""
+    nc, pc = abi.node_columns(nodes), abi.pod_columns(pods)
+    out = np.zeros(32, np.uint32)
+    ln = np.zeros(2, np.int32)
+    n = lib().kgo_numa_hints(C.byref(cfg), C.byref(nc), node, C.byref(pc), pod, policy,
+                             out.ctypes.data_as(C.POINTER(C.c_uint32)), ln.ctypes.data_as(C.POINTER(C.c_int32)))
+    lists = []
+    for li in range(max(n, 0)):
+        hs = [int(v) for v in out[16 * li:16 * li + ln[li]]]
+        lists.append([] if len(hs) == 1 and hs[0] & 0x200 else [(h & 0xFF, bool(h & 0x100)) for h in hs])
+    return lists
+
+
+def numa_allocate(nodes: abi.Table, pods: abi.Table, mask: int, node: int = 0, pod: int = 0):
+    """resourceManager.Allocate under a NUMA affinity: (ok, CPUs of a cpuset-binding pod, split [resource][zone])."""
+    nc, pc = abi.node_columns(nodes), abi.pod_columns(pods)
+    cpus = np.zeros(4, np.uint64)
+    al = np.zeros(2 * abi.KG_MAX_ZONES, np.int64)
+    rc = lib().kgo_numa_allocate(C.byref(nc), node, C.byref(pc), pod, mask, cpus.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                 al.ctypes.data_as(C.POINTER(C.c_int64)))
+    return rc == 0, abi.mask_cpus(cpus), al.reshape(2, abi.KG_MAX_ZONES)
 
 
 def ext_select(cfg, nodes: abi.Table, pods: abi.Table, k: int = 1, index_base: int = 0, quotas=None,

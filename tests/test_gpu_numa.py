@@ -244,6 +244,23 @@ def test_gpu_numa_select_device(ctx, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,gz", [(1, True), (3, True), (1, False)])
+def test_gpu_numa_single_fast_base(ctx, monkeypatch, k, gz):
+    """Config 5's shape (synth.config5: SingleNUMANode nodes, U(0, 1) GPU usage) on the fast-base select: the
+    SingleNUMANode records take DeviceShare's hints from the per-class table (k_gpu_zone_sum + eval_c1), or with
+    KG_NO_GZ the general path; both equal the oracle."""
+    from koordinator_amd import engine
+    if not gz:
+        monkeypatch.setenv("KG_NO_GZ", "1")
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(3000, 512, seed_config=35, rsv_frac=0.1, numa="single", usage="u01")
+    kc = cfg.kg_config()
+    assert (nodes["numa_policy"] == abi.KG_NUMA_SINGLE_NODE).sum() > 300
+    snap, batch = _make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_select(snap, batch, k)
+    assert np.array_equal(got, oracle_lib.ext_select(kc, nodes, pods, k, 0, quotas, rsv))
+
+
+@pytest.mark.gpu
 def test_gpu_numa_replay_device(ctx):
     """One pod per cycle: the winner's Reserve allocates its GPUs inside the stored NUMA affinity (BestEffort nodes
     included, whose Reserve can fail on DeviceShare's hints); nodes, minors, reasons and quota state as the oracle."""

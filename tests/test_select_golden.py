@@ -2,8 +2,8 @@
 
 The committed vectors tests/golden/select_config{2,4,5}.npz hold the oracle's top-3 keys of EVERY pod of
 config 2 (10k x 10k), config 4 (100k nodes x 10k pods, one GPU), config 5 (100k x 10k with DeviceShare,
-Reservation and ElasticQuota) and the mixed bench config 6 (10k x 10k, Restricted / BestEffort / CPU-bind-policy
-nodes, LSR pods), made by tests/golden/make_select_golden.py. The CPU tests pin the vectors to
+Reservation and ElasticQuota, 20% SingleNUMANode nodes) and the mixed bench config 6 (10k x 10k, Restricted /
+BestEffort / CPU-bind-policy nodes, LSR pods: cpusets under NUMA policies too), made by tests/golden/make_select_golden.py. The CPU tests pin the vectors to
 today's generator (cluster digest) and re-check a pod sample on the oracle; the GPU tests run the whole
 batch through the C ABI (kg_eval_select, k = 1 and k = 3) and compare every key bit for bit."""
 import os
@@ -62,8 +62,7 @@ def test_select_whole_batch_bit_exact(ctx, config):
     for k in (1, 3):
         got = engine.eval_select(snap, batch, k)
         st = engine.result_status(batch)
-        if config != 6:  # config 6's cpuset pods on NUMA-policy nodes are flagged for the host path
-            assert not np.any(st & abi.KG_ST_UNSUPPORTED), "a pair left the device path"
+        assert not np.any(st & abi.KG_ST_UNSUPPORTED), "a pair left the device path"
         bad = np.flatnonzero(np.any(got != want[:, :k], axis=1))
         assert len(bad) == 0, (f"config {config} k={k}: {len(bad)} pods differ, first {bad[0]}: "
                                f"gpu {got[bad[0]]} oracle {want[bad[0], :k]}")
