@@ -31,7 +31,7 @@ from . import abi
 from .config import CPU, DEV_RESOURCES, MEMORY, SchedulerConfig
 from .decode import (ANN_AMPLIFICATION, LoadAwareNodeCache, NODEINFO_KEYS, Unsupported, _is_terminated, _rl, amplify,
                      assign_info, is_reserve_pod, la_cols, milli_value, node_static_cols, nodeinfo_cols,
-                     pod_request_vec, pod_requests, value, zone_used_cols)
+                     pod_request_vec, pod_requests, value, zone_used_cols, ResourceList)
 
 ANN_RESOURCE_STATUS = "scheduling.koordinator.sh/resource-status"
 ANN_DEVICE_ALLOCATED = "scheduling.koordinator.sh/device-allocated"
@@ -612,8 +612,7 @@ class ClusterState:
         matchable reservations (rsvmatch.match_classes), then decode.reservation_restore over the current rows.
         Returns (rsv_class per pod, restored node table, abi.Reservations)."""
         from . import decode, rsvmatch
-        infos = [ri for ri in self.reservations.infos.values() if ri.matchable() and ri.node in self.index]
-        infos.sort(key=lambda ri: (self.index[ri.node], ri.uid))
+        infos = self.reservations.matchable_infos(self.index)
         nodes_by_name = {n: self.nodes[i] for n, i in self.index.items()}
         cls, rsv_cls, _ = rsvmatch.match_classes(list(pods), [pod_requests(p) for p in pods], [ri.obj for ri in infos],
                                                  nodes_by_name)
@@ -623,8 +622,8 @@ class ClusterState:
         t, views, vinfos, devs = decode.reservation_restore(table, resv)
         return np.array(cls, np.int32), t, abi.Reservations(views, vinfos, devs)
 
-    def on_quota(self, q: dict):
-        self.quotas.on_quota(q)
+    def on_quota(self, q: dict, add: bool = False):
+        self.quotas.on_quota(q, add)
 
     def on_quota_delete(self, name: str):
         self.quotas.on_quota_delete(name)
@@ -769,7 +768,7 @@ def restricted_resources(names: List[str], annotations: Dict[str, str]) -> List[
     the allocatable names intersected with the restricted-options annotation's resources
     (GetReservationRestrictedResources, util/reservation/reservation.go:677-694), all names when the
     intersection is empty; an annotation that does not parse (apis/extension/reservation.go:199-207) leaves the
-    names as they are."""
+    names as they are (and is the info's ParseError, restricted_options_ok)."""
     raw = annotations.get(ANN_RESERVATION_RESTRICTED_OPTIONS, "")
     if not raw:
         return names
@@ -786,31 +785,88 @@ def restricted_resources(names: List[str], annotations: Dict[str, str]) -> List[
     return out or names
 
 
+def restricted_options_ok(annotations: Dict[str, str]) -> bool:
+    """GetReservationRestrictedOptions (apis/extension/reservation.go:199-207) parses the annotation without error."""
+    raw = annotations.get(ANN_RESERVATION_RESTRICTED_OPTIONS, "")
+    if not raw:
+        return True
+    try:
+        opts = json.loads(raw)
+    except ValueError:
+        return False
+    return isinstance(opts, dict) and isinstance(opts.get("resources") or [], list)
+
+
+# quotav1 (k8s.io/apiserver/pkg/quota/v1) over ResourceList (name -> exact Fraction)
+def quota_add(a: Optional[ResourceList], b: ResourceList) -> ResourceList:
+    """quotav1.Add: every key of a and b, summed."""
+    out = dict(a or {})
+    for k, v in b.items():
+        out[k] = out.get(k, Fraction(0)) + v
+    return out
+
+
+def quota_sub_nonneg(a: Optional[ResourceList], b: ResourceList) -> ResourceList:
+    """quotav1.SubtractWithNonNegativeResult: a - b per key of a (floored at 0), keys only in b at 0."""
+    out = {}
+    for k, v in (a or {}).items():
+        d = v - b.get(k, Fraction(0))
+        out[k] = d if d > 0 else Fraction(0)
+    for k in b:
+        out.setdefault(k, Fraction(0))
+    return out
+
+
+def quota_mask(a: Optional[ResourceList], names: Iterable[str]) -> ResourceList:
+    """quotav1.Mask: the keys of a among names."""
+    names = set(names)
+    return {k: v for k, v in (a or {}).items() if k in names}
+
+
+def reservation_requests(r: dict) -> ResourceList:
+    """reservationutil.ReservationRequests (util/reservation/reservation.go:393-404): status.allocatable of an
+    Available reservation on a node, else the PodRequests of its template."""
+    status, spec = r.get("status") or {}, r.get("spec") or {}
+    if status.get("phase") == "Available" and status.get("nodeName"):
+        return _rl(status.get("allocatable"))
+    tmpl = spec.get("template")
+    if tmpl is not None:
+        return pod_requests({"spec": (tmpl or {}).get("spec") or {}})
+    return {}
+
+
 class ReservationInfo:
-    """frameworkext.ReservationInfo of a Reservation object: Allocatable (status), ResourceNames (its keys),
-    Allocated = Σ Mask(requests, ResourceNames) of the assigned pods, the owners / policy / order the restore and
-    the matching read."""
+    """frameworkext.ReservationInfo of a Reservation object (reservation_info.go:92-132,400-442,490-569):
+    Allocatable (ReservationRequests), ResourceNames (its keys, sorted; restricted for a Restricted policy),
+    Allocated (quotav1.Add of each assigned pod's Mask(requests, ResourceNames) at its add, nil until the first
+    pod; masked again when ResourceNames change; SubtractWithNonNegativeResult at a pod's removal), AssignedPods,
+    and the owners / policy / order the restore and the matching read."""
 
     def __init__(self, r: dict, cfg: SchedulerConfig):
         self.cfg = cfg
-        self.assigned: Dict[str, List[int]] = {}  # pod uid -> masked request vector
-        self.update(r)
+        self.assigned: Dict[str, ResourceList] = {}  # AssignedPods: pod uid -> PodRequirement.Requests
+        self.allocated_rl: Optional[ResourceList] = None
+        self._set(r)
 
-    def update(self, r: dict):
+    def _set(self, r: dict):
         self.obj = r
         md, spec, status = _md(r), r.get("spec") or {}, r.get("status") or {}
         self.uid = md.get("uid", "")
         self.name = md.get("name", "")
         self.node = status.get("nodeName", "")
         self.phase = status.get("phase", "")
+        self.allocatable_rl = reservation_requests(r)
         alloc = status.get("allocatable") or {}
-        self.allocatable = self._vec(alloc)
         self.max_pods = value(alloc["pods"]) if "pods" in alloc else -1
         self.policy = {"Aligned": abi.KG_RSV_ALIGNED, "Restricted": abi.KG_RSV_RESTRICTED}.get(
             spec.get("allocatePolicy", ""), abi.KG_RSV_DEFAULT)
-        self.names = sorted(alloc)
+        names = sorted(self.allocatable_rl)
+        ann = md.get("annotations") or {}
+        self.parse_error = False
         if self.policy == abi.KG_RSV_RESTRICTED:
-            self.names = restricted_resources(self.names, md.get("annotations") or {})
+            names = restricted_resources(names, ann)
+            self.parse_error = not restricted_options_ok(ann)
+        self.names = names
         self.allocate_once = spec.get("allocateOnce", True) is not False
         self.terminating = md.get("deletionTimestamp") is not None
         try:
@@ -818,41 +874,99 @@ class ReservationInfo:
         except ValueError:
             self.order = 0
 
-    def _vec(self, rl: dict) -> List[int]:
+    def update(self, r: dict):
+        """UpdateReservation (reservation_info.go:400-442): Allocated masked by the new ResourceNames."""
+        self._set(r)
+        if self.allocated_rl is not None:
+            self.allocated_rl = quota_mask(self.allocated_rl, self.names)
+
+    def add_assigned_pod(self, uid: str, requests: ResourceList) -> bool:
+        """AddAssignedPod (:490-500): a repeated pod is skipped."""
+        if uid in self.assigned:
+            return False
+        self.allocated_rl = quota_add(self.allocated_rl, quota_mask(requests, self.names))
+        self.assigned[uid] = dict(requests)
+        return True
+
+    def remove_assigned_pod(self, uid: str) -> bool:
+        """RemoveAssignedPod (:502-514)."""
+        req = self.assigned.pop(uid, None)
+        if req is None:
+            return False
+        if req:
+            self.allocated_rl = quota_sub_nonneg(self.allocated_rl, quota_mask(req, self.names))
+        return True
+
+    @property
+    def allocated_pods(self) -> int:
+        return len(self.assigned)
+
+    def _vec(self, rl: Optional[ResourceList]) -> List[int]:
         names = [self.cfg.scalar_resources[k] if k < len(self.cfg.scalar_resources) else "" for k in range(abi.KG_NSCALAR)]
         out = []
-        for k, key in enumerate(list(RSV_VEC) + names):
-            q = rl.get(key)
+        for key in list(RSV_VEC) + names:
+            q = (rl or {}).get(key)
             out.append(0 if q is None else (milli_value(q) if key == CPU else value(q)))
         return out
 
-    def mask(self, req: Dict[str, object]) -> List[int]:
-        """quotav1.Mask(requests, ResourceNames) as a KG_RSV_R vector."""
-        return self._vec({k: v for k, v in req.items() if k in self.names})
+    @property
+    def allocatable(self) -> List[int]:
+        return self._vec(self.allocatable_rl)
 
     @property
     def allocated(self) -> List[int]:
-        tot = [0] * abi.KG_RSV_R
-        for v in self.assigned.values():
-            tot = [a + b for a, b in zip(tot, v)]
-        return tot
+        """Allocated as a KG_RSV_R vector (zeros while nil)."""
+        return self._vec(self.allocated_rl)
 
-    def matchable(self) -> bool:
-        """IsMatchable (reservation_info.go:546-569): Available, and not an allocate-once reservation with pods."""
-        if self.phase != "Available":
+    def allocated_keys(self) -> int:
+        """The cpu / memory keys present in Allocated (bit 0 / 1): GetNonZeroRequestForResource reads the value of a
+        present key and the default of a missing one (reservation_info.go:516-529,581-605)."""
+        a = self.allocated_rl or {}
+        return (1 if CPU in a else 0) | (2 if MEMORY in a else 0)
+
+    def is_matchable(self) -> bool:
+        """IsMatchable (reservation_info.go:546-569): Available on a node, no parse error, not an allocate-once
+        reservation with pods."""
+        if self.phase != "Available" or not self.node or self.parse_error:
             return False
-        return not (self.allocate_once and len(self.assigned) > 0)
+        return not (self.allocate_once and self.allocated_pods > 0)
+
+    matchable = is_matchable
 
 
 class ReservationCache:
-    """reservationCache: reservation infos by uid, the reservations of each node, and the assigned-pod
-    bookkeeping of addPod / updatePod / deletePod (keyed by the pod's reservation-allocated annotation)."""
+    """reservationCache (reservation/cache.go:761-1205): reservation infos by uid, reservationsOnNode,
+    matchableOnNode and allocatedOnNode (refreshed the way the reference refreshes them: matchable on reservation
+    updates only, allocated on pod adds / removals too), and the assigned-pod bookkeeping of addPod / updatePod /
+    deletePod (keyed by the pod's reservation-allocated annotation)."""
 
     def __init__(self, cfg: SchedulerConfig, on_change: Callable[[str], None] = lambda node: None):
         self.cfg = cfg
         self.infos: Dict[str, ReservationInfo] = {}
         self.on_node: Dict[str, Set[str]] = {}
+        self.matchable_on_node: Dict[str, Set[str]] = {}
+        self.allocated_on_node: Dict[str, Set[str]] = {}
         self.on_change = on_change
+
+    @staticmethod
+    def _drop(m: Dict[str, Set[str]], node: str, uid: str):
+        s = m.get(node)
+        if s is not None:
+            s.discard(uid)
+            if not s:
+                del m[node]
+
+    def _refresh(self, ri: ReservationInfo, node: str):
+        """The matchable / allocated refresh of updateReservation / updateReservationIfExists (:813-843)."""
+        if ri.is_matchable():
+            self.matchable_on_node.setdefault(node, set()).add(ri.uid)
+            if ri.allocated_pods > 0:
+                self.allocated_on_node.setdefault(node, set()).add(ri.uid)
+            elif node in self.allocated_on_node:
+                self.allocated_on_node[node].discard(ri.uid)
+        else:
+            self._drop(self.matchable_on_node, node, ri.uid)
+            self._drop(self.allocated_on_node, node, ri.uid)
 
     def update_reservation(self, r: dict):
         """updateReservation / assumeReservation (cache.go:785-844)."""
@@ -864,20 +978,58 @@ class ReservationCache:
         else:
             ri.update(r)
         if old_node and old_node != ri.node:
-            self.on_node.get(old_node, set()).discard(uid)
             self.on_change(old_node)
         if ri.node:
             self.on_node.setdefault(ri.node, set()).add(uid)
+            self._refresh(ri, ri.node)
+            self.on_change(ri.node)
+
+    def update_reservation_if_exists(self, r: dict):
+        """updateReservationIfExists (cache.go:846-891): an unknown reservation is not created."""
+        uid = _md(r).get("uid", "")
+        ri = self.infos.get(uid)
+        if ri is None:
+            return
+        ri.update(r)
+        if ri.node:
+            self._refresh(ri, ri.node)
             self.on_change(ri.node)
 
     def delete_reservation(self, r: dict):
-        """DeleteReservation / forgetReservation (cache.go:789-791,893-918)."""
+        """DeleteReservation / forgetReservation (cache.go:789-791,893-918): the sets of the object's node."""
         uid = _md(r).get("uid", "")
         ri = self.infos.pop(uid, None)
-        node = (r.get("status") or {}).get("nodeName", "") or (ri.node if ri else "")
-        if node:
-            self.on_node.get(node, set()).discard(uid)
-            self.on_change(node)
+        node = (r.get("status") or {}).get("nodeName", "")
+        for m in (self.on_node, self.matchable_on_node, self.allocated_on_node):
+            self._drop(m, node, uid)
+        for n in {node, ri.node if ri else ""} - {""}:
+            self.on_change(n)
+        return ri
+
+    def get(self, uid: str) -> Optional[ReservationInfo]:
+        """getReservationInfoByUID (cache.go:1115-1123)."""
+        return self.infos.get(uid)
+
+    def list_all_nodes(self, matchable: bool) -> List[str]:
+        """ListAllNodes (cache.go:1138-1160): nodes with matchable reservations, or (matchable False) with allocated
+        ones; nothing when no node has a matchable reservation."""
+        if not self.matchable_on_node:
+            return []
+        return sorted(self.matchable_on_node if matchable else self.allocated_on_node)
+
+    def for_each_matchable(self, node: str, fn) -> None:
+        """ForEachMatchableReservationOnNode (cache.go:1162-1180): fn(info) -> continue?"""
+        for uid in sorted(self.matchable_on_node.get(node, ())):
+            if not fn(self.infos[uid]):
+                return
+
+    def list_available(self, node: str, list_all: bool) -> List[ReservationInfo]:
+        """ListAvailableReservationInfosOnNode (cache.go:1182-1205)."""
+        if not list_all:
+            out: List[ReservationInfo] = []
+            self.for_each_matchable(node, lambda ri: out.append(ri) or True)
+            return out
+        return [self.infos[u] for u in sorted(self.on_node.get(node, ())) if u in self.infos]
 
     @staticmethod
     def reservation_of(pod) -> str:
@@ -885,30 +1037,48 @@ class ReservationCache:
         return (json.loads(raw) or {}).get("uid", "") if raw else ""
 
     def _add(self, ruid: str, pod) -> bool:
+        """addPods (cache.go:1020-1045): unknown / terminating reservations refuse."""
         ri = self.infos.get(ruid)
-        if ri is None or ri.terminating or _uid(pod) in ri.assigned:
-            return False  # addPods: unknown / terminating reservation; AddAssignedPod skips repeats
-        ri.assigned[_uid(pod)] = ri.mask(pod_requests(pod))
+        if ri is None or ri.terminating:
+            return False
+        added = ri.add_assigned_pod(_uid(pod), pod_requests(pod))
+        if ri.is_matchable() and ri.allocated_pods > 0 and ri.node:
+            self.allocated_on_node.setdefault(ri.node, set()).add(ruid)
         self.on_change(ri.node)
-        return True
+        return added
 
     def _remove(self, ruid: str, pod):
+        """deletePods (cache.go:1085-1105)."""
         ri = self.infos.get(ruid)
-        if ri is not None and ri.assigned.pop(_uid(pod), None) is not None:
-            self.on_change(ri.node)
+        if ri is None:
+            return
+        ri.remove_assigned_pod(_uid(pod))
+        if ri.allocated_pods == 0 and ri.node:
+            self._drop(self.allocated_on_node, ri.node, ruid)
+        self.on_change(ri.node)
 
     def add_pod(self, pod):
         ruid = self.reservation_of(pod)
         if ruid:
             self._add(ruid, pod)
 
-    def update_pod(self, old, pod):
+    def update_pod_in(self, old_ruid: str, new_ruid: str, old, pod):
         """updatePod (cache.go:1047-1079): the old reservation forgets the pod, the new one adds it."""
+        ri = self.infos.get(old_ruid)
+        if ri is not None and old is not None:
+            self._remove(old_ruid, old)
+        ri = self.infos.get(new_ruid)
+        if ri is not None and pod is not None:
+            ri.add_assigned_pod(_uid(pod), pod_requests(pod))
+            if ri.is_matchable() and ri.allocated_pods > 0 and ri.node:
+                self.allocated_on_node.setdefault(ri.node, set()).add(new_ruid)
+            self.on_change(ri.node)
+
+    def update_pod(self, old, pod):
+        """The pod event handler's update: reservations named by the old and new reservation-allocated
+        annotations (a terminated pod leaves its reservation)."""
         o, n = self.reservation_of(old) if old else "", self.reservation_of(pod)
-        if o:
-            self._remove(o, old)
-        if n and not _is_terminated(pod):
-            self._add(n, pod)
+        self.update_pod_in(o, n if not _is_terminated(pod) else "", old, pod)
 
     def delete_pod(self, pod):
         ruid = self.reservation_of(pod)
@@ -922,26 +1092,29 @@ class ReservationCache:
     def forget_pod(self, ruid: str, pod):
         self._remove(ruid, pod)
 
+    def matchable_infos(self, node_index: Dict[str, int]) -> List[ReservationInfo]:
+        """The reservations ForEachMatchableReservationOnNode visits on the indexed nodes, in node order."""
+        out = []
+        for name in sorted(self.matchable_on_node, key=lambda nm: node_index.get(nm, -1)):
+            if name in node_index:
+                self.for_each_matchable(name, lambda ri: out.append(ri) or True)
+        return out
+
     def restore_inputs(self, node_index: Dict[str, int], classes_of=None) -> List[dict]:
         """The matchable reservations of every node as decode.reservation_restore reads them
         (ForEachMatchableReservationOnNode, cache.go:1162-1180); classes_of(info) -> owner-match classes."""
         out = []
-        for name in sorted(self.on_node, key=lambda nm: node_index.get(nm, -1)):
-            i = node_index.get(name)
-            if i is None:
-                continue
-            for uid in sorted(self.on_node[name]):
-                ri = self.infos[uid]
-                if not ri.matchable():
-                    continue
-                names = 0
-                for k, key in enumerate(list(RSV_VEC) + list(self.cfg.scalar_resources[:abi.KG_NSCALAR])):
-                    if key in ri.names:
-                        names |= 1 << k
-                out.append(dict(node=i, cls=classes_of(ri) if classes_of else [], uid=uid,
-                                allocatable=ri.allocatable, allocated=ri.allocated if ri.assigned else None,
-                                reserved=None, allocated_pods=len(ri.assigned), policy=ri.policy, order=ri.order,
-                                allocate_once=ri.allocate_once, max_pods=ri.max_pods, names=names))
+        for ri in self.matchable_infos(node_index):
+            names = 0
+            for k, key in enumerate(list(RSV_VEC) + list(self.cfg.scalar_resources[:abi.KG_NSCALAR])):
+                if key in ri.names:
+                    names |= 1 << k
+            out.append(dict(node=node_index[ri.node], cls=classes_of(ri) if classes_of else [], uid=ri.uid,
+                            allocatable=ri.allocatable,
+                            allocated=ri.allocated if ri.allocated_rl is not None else None,
+                            allocated_keys=ri.allocated_keys(), reserved=None, allocated_pods=ri.allocated_pods,
+                            policy=ri.policy, order=ri.order, allocate_once=ri.allocate_once, max_pods=ri.max_pods,
+                            names=names))
         return out
 
 
@@ -978,9 +1151,16 @@ class QuotaCache:
             v.append(0 if q is None else (milli_value(q) if key == CPU else value(q)))
         return v, keys
 
-    def on_quota(self, q: dict):
-        name = _md(q).get("name", "")
+    def on_quota(self, q: dict, add: bool = False):
+        """OnQuotaAdd (add=True) / OnQuotaUpdate (quota_handler.go:35-100): a quota being deleted is ignored; an Add
+        of a quota already held does not overwrite it."""
+        md = _md(q)
+        name = md.get("name", "")
         spec = q.get("spec") or {}
+        if md.get("deletionTimestamp") is not None:
+            return
+        if add and name in self.index and self.max[self.index[name]] is not None:
+            return
         if name not in self.index:
             self.index[name] = len(self.max)
             self.max.append(None)

@@ -95,14 +95,21 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
     const uint32_t node_pol = ((uint32_t)n[N_FLAGS] >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (pf >> 16) & 15u;
     const bool numa_pol = (pod_pol != KG_NUMA_NONE ? pod_pol : node_pol) != KG_NUMA_NONE;
     uint32_t mask = 0;  // the NUMA affinity of the Reserve (0: the whole node)
-    if (numa_pol) {
-        __shared__ int32_t s_zone;
-        if (threadIdx.x == 0) s_zone = winners ? (int32_t)zsel[rec] : eval_pair<false>(cfg, n, &z, load_pod(pods, pod)).zone;
-        __syncthreads();
-        const int32_t zone = s_zone;
-        if (zone_reserve_fails(zone)) return;  // the Reserve fails on the pair's zone code (reported by the Reserve kernel)
-        mask = zone_affinity(zone);
+    // the pair's zone code on the pre-Reserve state: in replay the select step's; else the one k_ext_assume's evaluation
+    // pass preset, or evaluated here. Outside replay it is handed on to the kernel that applies the pod (ZONE_PRESET).
+    __shared__ int32_t s_zone;
+    if (threadIdx.x == 0) {
+        const int32_t w = (!winners && fail_out) ? *fail_out : 0;
+        s_zone = winners ? (numa_pol ? (int32_t)zsel[rec] : -1)
+               : zone_is_preset(w) ? zone_of_preset(w) : eval_pair<false>(cfg, n, &z, load_pod(pods, pod)).zone;
     }
+    __syncthreads();
+    const int32_t zone = s_zone;
+    if (zone_reserve_fails(zone)) {  // the Reserve fails on the pair's zone code (reported by the Reserve kernel)
+        if (!winners && fail_out && threadIdx.x == 0) *fail_out = zone_preset(zone);
+        return;
+    }
+    if (numa_pol) mask = zone_affinity(zone);
     const uint32_t* src = reinterpret_cast<const uint32_t*>(topos + z.cpu_topo);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&st);
     for (uint32_t k = threadIdx.x; k < sizeof(kg_cpu_topo) / 4; k += 64) dst[k] = src[k];
@@ -184,9 +191,10 @@ __global__ __launch_bounds__(64) void k_cpuset_reserve(NodeRec* __restrict__ nod
     if (threadIdx.x != 0) return;
     if (code != 0) {  // Allocate fails (ErrNotEnoughCPUs): the Reserve fails, nothing of the pod is applied
         if (winners) zsel[rec] = (int8_t)ZONE_CPUSET_FAIL;  // read by the replay step that applies the pod
-        else if (fail_out) *fail_out = ZONE_CPUSET_FAIL;  // read by k_assume / k_ext_assume
+        else if (fail_out) *fail_out = zone_preset(ZONE_CPUSET_FAIL);  // read by k_assume / k_ext_assume
         return;
     }
+    if (!winners && fail_out) *fail_out = zone_preset(zone);
     if (mask) {  // resourceManager.Update: the NUMA split enters the zones, each gets its allocation record
         for (int zq = 0; zq < MAX_ZONES; zq++) {
             z.cpu_used[zq] += al[0][zq];

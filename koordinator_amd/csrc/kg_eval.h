@@ -301,6 +301,24 @@ __device__ __forceinline__ uint32_t numa_bind_check(const NumaBind& b, const int
     return partial ? (uint32_t)KG_ST_NUMA_CPU_BIND : 0u;
 }
 
+// requestCPUBind + getCPUBindPolicy (util.go:101-138) of a pair whose numa_eval checks passed: the pod's NumaBind
+// and whether its CPUs fit the whole node (node_take); false when the pod binds no CPUs there
+__device__ __forceinline__ bool numa_bind_pair(const ZoneRec* __restrict__ zr, const PodV& p, NumaBind& b, bool& node_take) {
+    const uint32_t node_bind = (zr->cpu_meta >> CPU_META_BIND_SHIFT) & 3u;
+    const bool cpu_bind = (p.flags & KG_POD_CPU_BIND) || (p.req_cpu != 0 && node_bind != KG_NODE_CPU_BIND_NONE);
+    if (!cpu_bind || zr->cpu_topo < 0) return false;
+    const uint32_t cpu_pol = (p.flags >> KG_POD_CPU_POLICY_SHIFT) & 3u;
+    uint32_t required = (p.flags & KG_POD_CPU_REQUIRED) ? cpu_pol : KG_CPU_BIND_NONE;
+    if (node_bind == KG_NODE_CPU_BIND_FULL_PCPUS_ONLY) required = KG_CPU_BIND_FULL_PCPUS;
+    else if (node_bind == KG_NODE_CPU_BIND_SPREAD_BY_PCPUS) required = KG_CPU_BIND_SPREAD_BY_PCPUS;
+    const int64_t have = required == KG_CPU_BIND_FULL_PCPUS    ? zr->cpu_free_full
+                         : required == KG_CPU_BIND_SPREAD_BY_PCPUS ? zr->cpu_free_cores
+                                                                   : zr->cpu_free;
+    node_take = p.req_cpu / 1000 <= have;
+    b = numa_bind_of(zr, required != KG_CPU_BIND_NONE, required != KG_CPU_BIND_NONE ? required : cpu_pol, p.req_cpu);
+    return true;
+}
+
 struct NumaHint {
     uint32_t mask;  // 0 = nil affinity
     bool pref, unsat;

@@ -1083,18 +1083,33 @@ __device__ __forceinline__ void numa_gpu_eval(const KCfg& c, const ExtDev& e, co
     }
     NumaZ xz;
     numa_load(zr, Z, xz);
+    // a cpuset-binding pod: its CPUs join every allocation (numa_eval's bind block)
+    NumaBind bind;
+    bool node_take = true;
+    const NumaBind* bp = numa_bind_pair(zr, p, bind, node_take) ? &bind : nullptr;
+    const bool amp = (flags & F_AMP) != 0;
+    const int64_t score_cpu = (bp && amp) ? (int64_t)ceil(__dmul_rn((double)p.req_cpu, zr->amp_ratio)) : p.req_cpu;
+    if (bp) numa_bind_trim(xz, bind);
     uint32_t mask = 0;
-    const uint32_t st = numa_admit<true, true>(c, xz, req, has, pol, excl, mask, &gh);
+    const uint32_t st = numa_admit<true, true>(c, xz, req, has, pol, excl, mask, &gh, bp, score_cpu);
     if (st) {  // not under BestEffort (its merge always admits)
         b.status |= st;
         return;
     }
     int64_t al[2][MAX_ZONES];
-    const uint32_t fail = mask ? numa_split(xz, mask, req, has, al) : 0u;
+    const uint32_t fail = mask ? numa_split(xz, mask, req, has, al, bp) : 0u;
     if (fail) {  // BestEffort: the Reserve's NUMA allocation fails; else not reached (a preferred hint places)
         if (be) b.zone = ZONE_RESERVE_FAIL | (int32_t)fail;
         else b.status |= KG_ST_UNSUPPORTED;
         return;
+    }
+    if (bp) {  // allocateCPUSet over the allocated NUMA nodes, or the whole node without an affinity
+        const bool cfail = mask ? numa_bind_check(bind, al[0], al[1], Z) != 0u : !node_take;
+        if (cfail) {
+            if (be) b.zone = ZONE_CPUSET_FAIL;
+            else b.status |= mask ? (uint32_t)KG_ST_UNSUPPORTED : (uint32_t)KG_ST_NUMA_CPUS;
+            return;
+        }
     }
     // allocateResources: DeviceShare's Allocate at the pair's site under the best hint
     uint32_t minors;
@@ -1112,9 +1127,11 @@ __device__ __forceinline__ void numa_gpu_eval(const KCfg& c, const ExtDev& e, co
     b.zone = numa_code(mask);
     if constexpr (!SCORE) return;
     const bool most = (c.most & MOST_NUMA) != 0;
+    // a cpuset-binding pod's requested cpu: the node's cpuset CPUs (amplified), its own request amplified
+    const int64_t bind_cpu = amp ? n[N_AMP_CPUSET] : n[N_CPUSET];
     if (!mask || !(p.req_cpu | p.req_mem)) {  // no NUMANodeResources: node allocatable / requested (the view's NodeInfo on a view)
-        const int64_t rc = v ? v->req[0] : n[N_REQ_CPU], rm = v ? v->req[1] : n[N_REQ_MEM];
-        b.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], rc + p.req_cpu,
+        const int64_t rc = bp ? bind_cpu : v ? v->req[0] : n[N_REQ_CPU], rm = v ? v->req[1] : n[N_REQ_MEM];
+        b.s_numa = numa_score<EXACT>(most, c.numa_w_cpu, c.numa_w_mem, n[N_ALLOC_CPU], rc + score_cpu,
                                      as_f64(n[N_RCP_CPU]), n[N_ALLOC_MEM], rm + p.req_mem, as_f64(n[N_RCP_MEM]));
         return;
     }
@@ -1127,7 +1144,8 @@ __device__ __forceinline__ void numa_gpu_eval(const KCfg& c, const ExtDev& e, co
             U[r] += xz.used[r][z];
         }
     }
-    b.s_numa = numa_score_q(most, c.numa_w_cpu, c.numa_w_mem, T[0], U[0] + p.req_cpu, T[1], U[1] + p.req_mem);
+    b.s_numa = numa_score_q(most, c.numa_w_cpu, c.numa_w_mem, T[0], (bp ? bind_cpu : U[0]) + score_cpu, T[1],
+                            U[1] + p.req_mem);
 }
 
 // ---- SingleNUMANode records on the fast-base path (storage class 1) --------------------------------------

@@ -797,7 +797,8 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
     }
 }
 
-// Reserve (sign +1: zone and minors chosen here) / Unreserve (sign -1: the given zone and minors).
+// Reserve (sign +1: zone and minors chosen here, or preset in out by an evaluation pass) / Unreserve (sign -1: the
+// given zone and minors). sign 0: the evaluation pass alone, which presets out for a cpuset Reserve and the Reserve.
 template <bool EXACT>
 __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, DevRec* __restrict__ devs, ExtDev e,
                              PodsDev pods, uint32_t pod, uint32_t rec, int32_t zone_in, uint32_t minors_in, int64_t sign,
@@ -809,18 +810,30 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     int64_t* n = nodes[rec].v;
     int32_t zone = zone_in;
     uint32_t mask = minors_in;
-    if (sign > 0) {
-        if (out && zone_reserve_fails(out[0])) return;  // the cpuset Reserve that ran first failed (out[0] preset)
+    if (sign >= 0 && out && zone_is_preset(out[0])) {
+        // the evaluation pass ran before the cpuset Reserve (which may have failed it): zone and minors of the
+        // pre-take state
+        zone = zone_of_preset(out[0]);
+        mask = (uint32_t)out[1];
+        if (zone_reserve_fails(zone)) {
+            if (threadIdx.x == 0) out[0] = zone, out[1] = 0;
+            return;
+        }
+    } else if (sign >= 0) {
         const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, 0u);
         zone = r.status ? -1 : r.zone;
         if (zone_reserve_fails(zone)) {  // the NodeNUMAResource Reserve fails: nothing is applied
             if (out && threadIdx.x == 0) {
-                out[0] = zone;
+                out[0] = sign == 0 ? zone_preset(zone) : zone;
                 out[1] = 0;
             }
             return;
         }
         mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone) : 0u;
+        if (sign == 0) {  // evaluation pass only (a cpuset Reserve runs next)
+            if (out && threadIdx.x == 0) out[0] = zone_preset(zone), out[1] = (int32_t)mask;
+            return;
+        }
     }
     __syncthreads();  // every lane has read the state before lane 0 changes it
     if (threadIdx.x != 0) return;

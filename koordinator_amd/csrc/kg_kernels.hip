@@ -380,9 +380,9 @@ __global__ void k_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zone
     int64_t* n = nodes[node].v;
     int32_t zone = zone_in;
     if (sign > 0) {
-        if (zone_out && zone_reserve_fails(*zone_out)) return;  // the cpuset Reserve that ran first failed
-        const PairOut o = eval_pair<EXACT>(cfg, n, zones + node, q);
-        zone = o.zone;
+        // a cpuset Reserve that ran first hands over the zone of the pre-take state (or its failure)
+        const int32_t w = zone_out ? *zone_out : 0;
+        zone = zone_is_preset(w) ? zone_of_preset(w) : eval_pair<EXACT>(cfg, n, zones + node, q).zone;
     }
     if (!zone_reserve_fails(zone)) apply_assume(cfg, n, zones + node, q, zone, sign, split);  // else nothing is applied
     if (zone_out) *zone_out = zone;
@@ -596,6 +596,15 @@ __device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& 
     const int64_t nv = old + add;
     const bool zone_hit = zl && (c.plugins & KG_PLUGIN_NUMA) && zone >= 0 && zone < MAX_ZONES && (uint32_t)zone == q;
     if (zone_hit) uc += pt.req_cpu, um += pt.req_mem;
+    // the zone's allocation record (apply_assume) and the amplified accounting of zone_cpu_alloc on the new state
+    const uint32_t st0 = z.status;
+    const uint32_t st = st0 | ((uint32_t)((__ballot(zone_hit && (pt.req_cpu | pt.req_mem)) >> 32) & 0xFull)
+                               << ZONE_RECORD_SHIFT);
+    int64_t ua = uc;
+    if (zl && ((st >> (ZONE_RECORD_SHIFT + q)) & 1u) && z.amp_ratio > 1.0) {
+        const int64_t cz = 1000 * (int64_t)z.cz_alloc[q];
+        ua = uc - cz + amp_i64(cz, z.amp_ratio);
+    }
     // derive_node on the new values
     const int64_t always_fail = kg_bits(-1.0), never_fail = kg_bits(4611686018427387904.0);
     const uint32_t f0 = flags & ~(uint32_t)F_DERIVED_MASK;
@@ -608,14 +617,14 @@ __device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& 
     if (lane == 63) big = kg_big(cs) || kg_big(acs) || cs < 0 || acs < cs;
     double zv[6] = {0, 0, 0, 0, 0, 0};
     if (zl) {
-        big = kg_big(tc) || kg_big(tm) || kg_big(uc) || kg_big(um) || uc < 0 || um < 0;
-        const int64_t ac = tc - uc < 0 ? 0 : tc - uc, am = tm - um < 0 ? 0 : tm - um;
+        big = kg_big(tc) || kg_big(tm) || kg_big(ua) || kg_big(um) || uc < 0 || um < 0;
+        const int64_t ac = tc - ua < 0 ? 0 : tc - ua, am = tm - um < 0 ? 0 : tm - um;
         const int64_t rc = tc - ac < 0 ? 0 : tc - ac, rm = tm - am < 0 ? 0 : tm - am;
         zv[0] = ac != 0 ? x100(ac) : -1.0;
         zv[1] = am != 0 ? x100(am) : -1.0;
         zv[2] = x100(tc - rc);
         zv[3] = x100(tm - rm);
-        zv[4] = x100(tc - uc);
+        zv[4] = x100(tc - ua);
         zv[5] = x100(tm - um);
     }
     const uint32_t pol0 = (f0 >> F_NUMA_POLICY_SHIFT) & 15u;
@@ -659,6 +668,7 @@ __device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& 
         zf.free_cpu = zv[4];
         zf.free_mem = zv[5];
     }
+    if (lane == 32u && st != st0) z.status = st;
     if (lane == 63) v[N_FLAGS] = (int64_t)((fl & 0xFFFFFFFF00000000ull) | f);
     wave_lds_sync();
 }

@@ -242,6 +242,13 @@ KG_HD inline uint32_t zone_fail_status(int32_t z) {
     if ((uint32_t)z & 0x10u) return ((z & 0xF) == 0xF) ? (uint32_t)KG_ST_DEV_RSV : KG_ST_DEV_MAKE((uint32_t)z & 0xFu);
     return (((uint32_t)z & 7u) << 12) | (((uint32_t)z & 8u) ? KG_ST_NUMA_CPUS : 0u);
 }
+// Reserve of one (pod, node): the zone code the pre-Reserve state gives, handed from the kernel that evaluates it
+// (k_ext_assume's evaluation pass, k_cpuset_reserve) to the one that applies (k_assume / k_ext_assume) in the
+// pair's out word, so that the cpuset take in between does not change the pair's Reserve (zone codes fit a byte)
+constexpr int32_t ZONE_PRESET = 0x40000000;
+KG_HD inline int32_t zone_preset(int32_t z) { return ZONE_PRESET | (z & 0xFF); }
+KG_HD inline bool zone_is_preset(int32_t w) { return (w & ZONE_PRESET) != 0; }
+KG_HD inline int32_t zone_of_preset(int32_t w) { return (int32_t)(int8_t)(uint8_t)(w & 0xFF); }
 // the NUMA affinity (bit per zone) of a pair's zone code; 0 = none (nil affinity, or the Reserve fails)
 KG_HD inline uint32_t zone_affinity(int32_t z) {
     if (z < 0 || zone_reserve_fails(z)) return 0u;

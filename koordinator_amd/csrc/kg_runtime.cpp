@@ -2400,10 +2400,14 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     touch_views(s, node);
     HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 2, ctx->stream));
-    if (sign > 0 && s->has_cpu)
+    if (sign > 0 && s->has_cpu) {
+        // the pair evaluated before the cpuset take changes the counts it reads (zone and minors preset in d_aout)
+        HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone,
+                                       minors, 0, s->kcfg, force_exact(), p->d_aout, ctx->stream));
         HIP_TRY(ctx, launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, pod,
                                            s->pos[node], nullptr, nullptr, 0, s->d_pos, s->base, p->n, nullptr, p->d_aout,
                                            ctx->stream));
+    }
     HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone, minors,
                                    sign, s->kcfg, force_exact(), p->d_aout, ctx->stream));
     s->gen++;

@@ -1083,7 +1083,8 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
     `nodes` is the true NodeInfo view (reserve pods and the pods allocated to reservations both
     counted, as NodeInfo accounts them). Each reservation is a dict: node, cls (owner-match class, or the
     list of classes that match it as rsvmatch.match_classes returns them),
-    allocatable / allocated / reserved (KG_RSV_R vectors, allocated None when no pod is assigned),
+    allocatable / allocated / reserved (KG_RSV_R vectors, allocated None while Allocated is nil; allocated_keys:
+    bit 0 / 1 when Allocated holds a cpu / memory key, default both),
     allocated_pods, policy, order, allocate_once, max_pods.
 
     Returns (nodes_default, views, infos, devs): the snapshot columns as seen by pods matching nothing on
@@ -1108,9 +1109,11 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
         v = r.get(key)
         return [0] * abi.KG_RSV_R if v is None else [int(a) for a in v]
 
-    def nz(v, present):
-        cpu = v[0] if present else 100           # DefaultMilliCPURequest
-        mem = v[1] if present else 200 * 1024 * 1024  # DefaultMemoryRequest
+    def nz(v, r):
+        # GetNonZeroRequestForResource per key of Allocated: the value of a present key, else the default
+        keys = r.get("allocated_keys", 3) if r.get("allocated") is not None else 0
+        cpu = v[0] if keys & 1 else 100                  # DefaultMilliCPURequest
+        mem = v[1] if keys & 2 else 200 * 1024 * 1024    # DefaultMemoryRequest
         return cpu, mem
 
     for i, xs in by_node.items():
@@ -1120,7 +1123,7 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
                 a = vec(r, "allocated")
                 for k, c in enumerate(req_cols):
                     out[c][i] -= a[k]
-                ncpu, nmem = nz(a, r.get("allocated") is not None)
+                ncpu, nmem = nz(a, r)
                 out["nz_cpu"][i] -= ncpu
                 out["nz_mem"][i] -= nmem
     views, infos, devs = [], [], []
@@ -1167,14 +1170,14 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
                     for k in range(abi.KG_RSV_R):
                         req[k] += a[k]
                         pod_requested[k] += a[k]
-                    ncpu, nmem = nz(a, r.get("allocated") is not None)
+                    ncpu, nmem = nz(a, r)
                     nzc += ncpu
                     nzm += nmem
                 rp = vec(r, "allocatable")  # restoreMatchedReservation: RemovePod(reserve pod)
                 for k in range(abi.KG_RSV_R):
                     req[k] -= rp[k]
                     r_alloc[k] += a[k]
-                ncpu, nmem = nz(rp, True)
+                ncpu, nmem = nz(rp, {"allocated": rp})
                 nzc -= ncpu
                 nzm -= nmem
             dev_base, dev_idx = -1, {}

@@ -399,3 +399,17 @@ class OracleState:
             raw = C.string_at(v.cpu_alloc, n * 2 * abi.KG_MAX_CPUS)
             t["cpu_alloc"] = np.frombuffer(raw, np.uint8).reshape(n, 2 * abi.KG_MAX_CPUS).copy()
         return t
+
+
+def assert_state_restored(before, after):
+    """Every column of `after` equals `before`, except the allocation records of numa_zone_status (bits
+    KG_ZONE_RECORD_SHIFT + z), which Unreserve leaves in place (resource_manager.go:478-483 Release keeps the zone's
+    allocatedResources entry): those may only have been added."""
+    from koordinator_amd import abi
+    low = np.uint32((1 << abi.KG_ZONE_RECORD_SHIFT) - 1)
+    for k in before:
+        if k == "numa_zone_status":
+            assert np.array_equal(before[k] & low, after[k] & low), k
+            assert not (before[k] & ~after[k]).any(), k
+        else:
+            assert np.array_equal(before[k], after[k]), k

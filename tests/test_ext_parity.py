@@ -281,10 +281,10 @@ def test_ext_shard_select_single_rank(ctx, k):
 
 @pytest.mark.parametrize("split", ["1", "0"])
 def test_ext_result_status(ctx, monkeypatch, split):
-    """kg_result_status on config 5: cpuset-binding pods on NUMA-policy nodes with a CPU topology (the cpuset
-    inside the NUMA hints, a host path) are flagged KG_ST_UNSUPPORTED, quota-rejected pods KG_ST_QUOTA — the OR
-    of the oracle verify rows' bits (a cpuset-binding pod on a node without CPU topology fails its Filter; GPU
-    pods on NUMA-policy nodes are on the device path)."""
+    """kg_result_status on config 5 with cpuset-binding pods, some on SingleNUMANode nodes with a CPU topology (the
+    cpuset inside the NUMA hints, on the device since ABI 9): quota-rejected pods are flagged KG_ST_QUOTA, no pod
+    KG_ST_UNSUPPORTED — the OR of the oracle verify rows' bits (a cpuset-binding pod on a node without CPU topology
+    fails its Filter; GPU pods on NUMA-policy nodes are on the device path too)."""
     monkeypatch.setenv("KG_EXT_SPLIT", split)
     cfg, nodes, pods, quotas, rsv = synth.cluster5(1200, 400, seed_config=73, rsv_frac=0.2)
     nodes = {k: v.copy() for k, v in nodes.items()}
@@ -315,7 +315,10 @@ def test_ext_result_status(ctx, monkeypatch, split):
     assert not len(bad), [(int(j), hex(gstat[j]), hex(wstat[j]), hex(pods["flags"][j]),
                            [(int(i), hex(ref.status[j, i])) for i in np.flatnonzero(ref.status[j] & abi.KG_ST_UNSUPPORTED)[:4]])
                           for j in bad[:6]]
-    assert (wstat & abi.KG_ST_UNSUPPORTED).any() and (wstat & abi.KG_ST_QUOTA).any() and (wstat == 0).any()
+    assert not (wstat & abi.KG_ST_UNSUPPORTED).any() and (wstat & abi.KG_ST_QUOTA).any() and (wstat == 0).any()
+    # the cpuset-under-NUMA pairs were evaluated (some admitted with a zone)
+    sel = ((pods["flags"] & abi.KG_POD_CPU_BIND) != 0)[:, None] & ((nodes["numa_policy"] != 0) & (ti >= 0))[None, :]
+    assert (sel & (ref.status == 0)).any()
 
 
 def test_views_stale_after_assume_on_view_node(ctx):

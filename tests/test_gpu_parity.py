@@ -194,9 +194,7 @@ def test_assume_forget_round_trip(ctx):
         st2.assume(i, pods, j)
     for (j, i, _), z in zip(reversed(placed), reversed(zones)):
         engine.forget(snap, batch, j, i, z)
-    after = snap.read_state()
-    for k, v in after.items():
-        assert np.array_equal(v, before[k]), k
+    oracle_lib.assert_state_restored(before, snap.read_state())
 
 
 def test_update_rows(ctx):
@@ -433,20 +431,19 @@ def test_replay_reasons_match_oracle(ctx, ext):
                (x for w in why[unsched] for x in reasons.reasons(int(w))))
 
 
-def test_result_status_flags_host_path_pods(ctx):
-    """kg_result_status: pods with a pair the device cannot decide (a cpuset-binding pod on a node with a
-    NUMA topology policy, or one whose preferred-policy accumulator fails in Filter) are flagged
-    KG_ST_UNSUPPORTED, exactly the pods whose oracle verify row carries the bit; every other pod's keys
-    are complete."""
+def test_result_status_cpuset_cluster(ctx):
+    """kg_result_status on a cpuset cluster with NUMA topology policies: the device decides every pair (cpusets under
+    a NUMA policy, preferred-policy accumulators), so no pod is flagged KG_ST_UNSUPPORTED, as no oracle verify row
+    carries the bit, and every pod's select keys equal the oracle's."""
     cfg, nodes, pods = synth.cpuset_cluster(300, 120, seed=23)
     kc = cfg.kg_config()
     snap = engine.Snapshot(ctx, kc, nodes)
     batch = engine.PodBatch(ctx, pods)
     ref = oracle_lib.eval_verify(kc, nodes, pods)
     want = np.bitwise_or.reduce(ref.status & abi.KG_ST_UNSUPPORTED, axis=1)
+    assert not want.any()
     for k in (1, 4):
         keys = engine.eval_select(snap, batch, k)
         assert np.array_equal(keys, oracle_lib.select(kc, nodes, pods, k))
         got = engine.result_status(batch)
         assert np.array_equal(got, want)
-    assert (want != 0).any() and (want == 0).any()

@@ -208,9 +208,7 @@ def test_topology_assume_forget(ctx):
         ost.assume(int(i), pods, int(j))
     for j, i in single[::-1]:
         engine.forget(snap, batch, int(j), int(i), int(ref.numa_zone[j, i]))
-    after = snap.read_state()
-    for k in before:
-        assert np.array_equal(before[k], after[k]), k
+    oracle_lib.assert_state_restored(before, snap.read_state())
     for j, i in multi:
         engine.assume(snap, batch, int(j), int(i))
     for j, i in single[::-1]:
@@ -267,9 +265,7 @@ def test_topology_multi_zone_unreserve(ctx):
         assert np.array_equal(state[f"zone_mem_used{z}"], want[f"zone_mem_used{z}"])
     for j, i, zone, amounts in made[1::2] + made[0::2]:
         engine.forget_numa(snap, batch, j, i, zone, amounts)
-    after = snap.read_state()
-    for k in before:
-        assert np.array_equal(before[k], after[k]), k
+    oracle_lib.assert_state_restored(before, snap.read_state())
 
 
 @pytest.mark.gpu
@@ -296,6 +292,4 @@ def test_best_effort_reserve_failures(ctx):
     before = snap.read_state()
     with pytest.raises(engine.ReserveFailed):
         engine.assume(snap, batch, int(j), int(i))
-    after = snap.read_state()
-    for k in before:
-        assert np.array_equal(before[k], after[k]), k
+    oracle_lib.assert_state_restored(before, snap.read_state())

@@ -9,7 +9,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 if [ "$K" != "NONE" ]; then
   if [ "$K" = "ALL" ]; then KA=(); else KA=(-k "$K"); fi
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread "${KA[@]}" \
+  timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=${MAXFAIL:-1} -q --timeout 120 --timeout-method thread "${KA[@]}" \
     > gpurun_out/gpu_tests_$TAG.log 2>&1 || { tail -40 gpurun_out/gpu_tests_$TAG.log; exit 1; }
   tail -2 gpurun_out/gpu_tests_$TAG.log
 fi
