@@ -62,3 +62,54 @@ def test_guard_detects_a_call(tmp_path):
     asm = _compile(tmp_path, "__device__ __attribute__((noinline)) uint64_t twist(uint64_t x) { return x * 3 + 1; }",
                    "^ twist(i)")
     assert _calls(asm) >= 1
+
+
+# ---- the round-3 gpu_partition discrepancy: misaligned scalar-load bases ------------------------------------------
+# Root cause (tools/dbg_part.hip, DESIGN.md "Toolchain findings"): for a loop over an array of 16-byte partition
+# records reading a byte field (offset 2) and an int field (offset 4) at a wave-uniform index, the gfx950 backend
+# strength-reduced both to one pointer (record + 2) and read the int with `s_load_dword sX, s[base], 0x2`. The sum is
+# dword aligned, but the hardware drops SBASE[1:0] before adding the offset (tools/sload_probe.hip measures it), so
+# the load returned the record's first dword and every score comparison failed. Fingerprint: a scalar load whose
+# immediate offset is not a multiple of 4 (its base must then be misaligned for the access to be aligned).
+_SLOAD = None
+
+
+def _misaligned_sloads(asm_lines):
+    import re
+    global _SLOAD
+    if _SLOAD is None:
+        _SLOAD = re.compile(r"^\s*(s_(?:load|buffer_load)_\S+)\s+[^,]+,\s*[^,]+,\s*(\S+)(?:\s+offset:(0x[0-9a-fA-F]+))?")
+    bad = []
+    for line in asm_lines:
+        m = _SLOAD.match(line)
+        if m and any(g and g.startswith("0x") and int(g, 16) % 4 for g in (m.group(2), m.group(3))):
+            bad.append(line.strip())
+    return bad
+
+
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc not in this image")
+def test_reproducer_shows_misaligned_sload(tmp_path):
+    """Self-check of the detector: the reproducer's first gpu_partition form compiles to scalar loads at offset 2."""
+    root = os.path.dirname(CSRC.rstrip("/").rsplit("/", 1)[0])
+    asm = tmp_path / "part.s"
+    subprocess.check_call([HIPCC, *FLAGS, os.path.join(root, "tools", "dbg_part.hip"), "-o", str(asm)],
+                          stderr=subprocess.DEVNULL)
+    assert len(_misaligned_sloads(asm.read_text().splitlines())) >= 1
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"), reason="llvm-objdump not in this image")
+def test_library_has_no_misaligned_sloads(tmp_path):
+    """The built engine (every gfx950 code object in libkoordgpu.so) carries no scalar load of the miscompiled form."""
+    root = os.path.dirname(CSRC.rstrip("/").rsplit("/", 1)[0])
+    lib = os.path.join(root, "koordinator_amd", "libkoordgpu.so")
+    if not os.path.exists(lib):
+        pytest.skip("libkoordgpu.so not built")
+    import sys
+    sys.path.insert(0, os.path.join(root, "tools"))
+    from code_objects import extract
+    files = extract(lib, str(tmp_path))
+    assert files
+    for f in files:
+        with open(f) as fh:
+            bad = _misaligned_sloads(fh)
+        assert not bad, (f, bad[:4])
