@@ -199,13 +199,16 @@ __global__ __launch_bounds__(64) void k_gpu_zone_sum(const NodeRec* __restrict__
 }
 
 // Records the fast-base kernels (PART 1) take for no pod: F_BIG or storage class 1. special[0] = count,
-// special[1..] = records (any order: keys are order-free).
+// special[1..] = records (any order: keys are order-free). c1 (nullable): the storage-class-1 records that are not
+// F_BIG go to their own list (c1[0] = count), for the light class-1 kernels (eval_c1); special then holds F_BIG only.
 __global__ __launch_bounds__(256) void k_special_scan(const NodeRec* __restrict__ nodes, uint32_t n_nodes, uint32_t n0,
-                                                      uint32_t* __restrict__ special) {
+                                                      uint32_t* __restrict__ special, uint32_t* __restrict__ c1) {
     const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
     if (rec >= n_nodes) return;
     const int64_t* n = nodes[rec].v;
-    if (rec >= n0 || ((uint32_t)n[N_FLAGS] & F_BIG)) special[1 + atomicAdd(special, 1u)] = rec;
+    const bool big = ((uint32_t)n[N_FLAGS] & F_BIG) != 0;
+    if (c1 && rec >= n0 && !big) c1[1 + atomicAdd(c1, 1u)] = rec;
+    else if (rec >= n0 || big) special[1 + atomicAdd(special, 1u)] = rec;
 }
 
 // Weighted total of a fast-base pair (FB paths): base total from the fast block + the normalised
@@ -330,13 +333,13 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
     if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
 }
 
-// The records a fast-base pass leaves to the general path for lane t: the special records (F_BIG, class
-// 1; grid-stride over chunks of `chunk`) for every lane, then the views of the lane's reservation class
-// that are not special. fn(rec) evaluates one pair.
+// The records a fast-base pass leaves to the general path for lane t: the special records (F_BIG, and class
+// 1 unless c1_split; grid-stride over chunks of `chunk`) for every lane, then the views of the lane's reservation
+// class that are not in the special list. fn(rec) evaluates one pair.
 template <typename Fn>
 __device__ __forceinline__ void for_general_records(const NodeRec* __restrict__ nodes, const ExtDev& e,
                                                     const uint32_t* __restrict__ special, uint32_t n0, uint32_t chunk,
-                                                    int32_t cls, Fn&& fn) {
+                                                    int32_t cls, bool c1_split, Fn&& fn) {
     const uint32_t nsp = special[0], step = gridDim.y * chunk;
     for (uint32_t x = blockIdx.y * chunk; x < nsp; x += step)
         for (uint32_t y = x, ye = min(x + chunk, nsp); y < ye; y++) fn(special[1 + y]);
@@ -345,9 +348,17 @@ __device__ __forceinline__ void for_general_records(const NodeRec* __restrict__ 
     for (uint32_t x = cb + blockIdx.y * chunk; x < ce; x += step)
         for (uint32_t v = x, ve = min(x + chunk, ce); v < ve; v++) {
             const uint32_t rec = e.views[v].rec;
-            if (rec >= n0 || ((uint32_t)nodes[rec].v[N_FLAGS] & F_BIG)) continue;  // special: done above
+            if (((uint32_t)nodes[rec].v[N_FLAGS] & F_BIG) || (rec >= n0 && !c1_split)) continue;  // special: done above
             fn(rec);
         }
+}
+
+// The class-1 records of a split fast-base pass (k_special_scan's c1 list) for lane t, grid-stride over chunks.
+template <typename Fn>
+__device__ __forceinline__ void for_c1_records(const uint32_t* __restrict__ c1, uint32_t chunk, Fn&& fn) {
+    const uint32_t nc = c1[0], step = gridDim.y * chunk;
+    for (uint32_t x = blockIdx.y * chunk; x < nc; x += step)
+        for (uint32_t y = x, ye = min(x + chunk, nc); y < ye; y++) fn(c1[1 + y]);
 }
 
 // A storage-class-1 (SingleNUMANode) record of a fast-base launch for a pod off its reservation views, with DeviceShare's hints from e.gz: the fast block's base key (0 = infeasible with the
@@ -365,7 +376,7 @@ __device__ __forceinline__ bool eval_c1(const KCfg& cfg, const KCfg& cv, const E
                                         const PodX& px, uint32_t dcls, uint32_t q, bool req_aff, uint32_t index_base,
                                         C1Pair& o) {
     const uint32_t fl = (uint32_t)n[N_FLAGS];
-    if (!e.gz || rec < n0 || (fl & F_BIG)) return false;
+    if (rec < n0 || (fl & F_BIG)) return false;
     if ((cfg.plugins & KG_PLUGIN_RSV) && px.cls >= 0 && px.cls < RSV_MAX_CLASSES &&
         (((uint64_t)n[N_RSV_CLASSES] >> px.cls) & 1ull))
         return false;  // a view of the pod's class
@@ -378,6 +389,7 @@ __device__ __forceinline__ bool eval_c1(const KCfg& cfg, const KCfg& cv, const E
         o.st = (o.bk == 0ull || q != 0u || req_aff) ? 1u : 0u;
         return true;
     }
+    if (!e.gz) return false;  // (not in a split pass: k_special_scan splits only with the table or without GPU pods)
     const uint64_t gz = e.gz[(size_t)(rec - n0) * DEV_CLASSES + dcls];
     int32_t zone = -1;
     o.bk = eval_fast_key<7u, 1, true>(cv, fr, zr, pff, o.g, &zone, gz);
@@ -398,7 +410,8 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
                                                       uint32_t n_list, uint32_t n0, uint32_t chunk, uint32_t index_base,
                                                       KCfg cfg, const uint32_t* __restrict__ qst,
                                                       uint32_t* __restrict__ dev_max, uint32_t* __restrict__ rsv_max,
-                                                      uint64_t* __restrict__ pref, const uint32_t* __restrict__ special) {
+                                                      uint64_t* __restrict__ pref, const uint32_t* __restrict__ special,
+                                                      bool c1_split) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = t < n_list;
     const uint32_t j = live ? list[t] : 0;
@@ -406,17 +419,9 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
     const PodX px = load_podx(pods, j);
     const uint32_t q = live ? qst[j] : 1u;
     const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
-    const PodF pff = to_podf(p, cfg);
-    const KCfg cv = cfg_in_vgprs(cfg);
-    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
     uint32_t dmax = 0, rmax = 0;
     uint64_t pk = PREF_NONE;
-    for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, [&](uint32_t rec) {
-        C1Pair c1;
-        if (eval_c1(cfg, cv, e, nodes[rec].v, zones + rec, rec, n0, pff, px, dcls, q, req_aff, index_base, c1)) {
-            if (!c1.st) dmax = max(dmax, (uint32_t)c1.s_dev);
-            return;
-        }
+    for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split, [&](uint32_t rec) {
         const PairX r = eval_pair_ext<false, false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
                                                            dcls);
         if (r.status) return;
@@ -431,6 +436,34 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
     if (dmax) atomicMax(dev_max + j, dmax);
     if (rmax) atomicMax(rsv_max + j, rmax);
     if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
+}
+
+// Pass 1, class-1 records of a split fast-base launch (k_special_scan's c1 list): eval_c1 with DeviceShare's hints
+// from e.gz; a record holding a view of the pod's class is left to k_ext_stats_sp's view walk. Off a view the
+// Reservation score and order are 0: only DeviceShare's maximum comes out.
+__global__ __launch_bounds__(256) void k_ext_stats_c1(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                      ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
+                                                      uint32_t n_list, uint32_t n0, uint32_t chunk, uint32_t index_base,
+                                                      KCfg cfg, const uint32_t* __restrict__ qst,
+                                                      uint32_t* __restrict__ dev_max, const uint32_t* __restrict__ c1) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = t < n_list;
+    const uint32_t j = live ? list[t] : 0;
+    const PodV p = load_pod(pods, j);
+    const PodX px = load_podx(pods, j);
+    if (!((cfg.plugins & KG_PLUGIN_DEV) && px.dcount != 0)) return;  // s_dev = 0 everywhere
+    const uint32_t q = live ? qst[j] : 1u;
+    const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
+    const PodF pff = to_podf(p, cfg);
+    const KCfg cv = cfg_in_vgprs(cfg);
+    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
+    uint32_t dmax = 0;
+    for_c1_records(c1, chunk, [&](uint32_t rec) {
+        C1Pair o;
+        if (eval_c1(cfg, cv, e, nodes[rec].v, zones + rec, rec, n0, pff, px, dcls, q, req_aff, index_base, o) && !o.st)
+            dmax = max(dmax, (uint32_t)o.s_dev);
+    });
+    if (live && dmax) atomicMax(dev_max + j, dmax);
 }
 
 // Pass 1 for pods without a GPU request: only the nodes holding a view of the pod's reservation class
@@ -612,7 +645,7 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
                                                        const uint32_t* __restrict__ rsv_max,
                                                        const uint64_t* __restrict__ pref, uint64_t* __restrict__ partial,
                                                        uint32_t* __restrict__ pstat, const uint32_t* __restrict__ special,
-                                                       uint32_t part_off) {
+                                                       uint32_t part_off, bool c1_split) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = j < n_pods;
     const uint32_t jj = live ? (list ? list[j] : j) : 0;
@@ -622,21 +655,11 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
     const uint32_t dm = dev_max[jj], rm = rsv_max[jj];
     const uint64_t pf = pref[jj];
     const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
-    const PodF pff = to_podf(p, cfg);
-    const KCfg cv = cfg_in_vgprs(cfg);
-    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
-    const uint32_t mag = norm_magic(dm);
     uint64_t top[K];
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
     uint32_t unsup = 0;
-    for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, [&](uint32_t rec) {
-        C1Pair c1;
-        if (eval_c1(cfg, cv, e, nodes[rec].v, zones + rec, rec, n0, pff, px, dcls, q, req_aff, index_base, c1)) {
-            const int64_t tot = total_fb(cfg, c1.bk, c1.s_dev, dm, mag, c1.g, pf);
-            topk_ins<K>(top, c1.st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - c1.g)));
-            return;
-        }
+    for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split, [&](uint32_t rec) {
         const PairX r = eval_pair_ext<false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q, dcls);
         unsup |= r.status & KG_ST_UNSUPPORTED;
         const uint32_t g = index_base + node_index(nodes[rec]);
@@ -652,6 +675,49 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
             for (int t = 0; t < K; t++) dst[t] = top[t];
         }
         if (unsup) atomicOr(pstat + jj, unsup);
+    }
+}
+
+// Pass 2, class-1 records of a split fast-base launch (the light complement of k_ext_select_sp): eval_c1 per pair,
+// a record holding a view of the pod's class left to k_ext_select_sp's view walk. Partials of chunk blockIdx.y go
+// after part_off; top-1 is fused.
+template <int K>
+__global__ __launch_bounds__(256) void k_ext_select_c1(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                       ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
+                                                       uint32_t n_pods, uint32_t n0, uint32_t chunk, uint32_t index_base,
+                                                       KCfg cfg, const uint32_t* __restrict__ qst,
+                                                       const uint32_t* __restrict__ dev_max, const uint64_t* __restrict__ pref,
+                                                       uint64_t* __restrict__ partial, const uint32_t* __restrict__ c1,
+                                                       uint32_t part_off) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = j < n_pods;
+    const uint32_t jj = live ? (list ? list[j] : j) : 0;
+    const PodV p = load_pod(pods, jj);
+    const PodX px = load_podx(pods, jj);
+    const uint32_t q = live ? qst[jj] : 1u;
+    const uint32_t dm = dev_max[jj];
+    const uint64_t pf = pref[jj];
+    const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
+    const PodF pff = to_podf(p, cfg);
+    const KCfg cv = cfg_in_vgprs(cfg);
+    const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
+    const uint32_t mag = norm_magic(dm);
+    uint64_t top[K];
+#pragma unroll
+    for (int t = 0; t < K; t++) top[t] = 0;
+    for_c1_records(c1, chunk, [&](uint32_t rec) {
+        C1Pair o;
+        if (!eval_c1(cfg, cv, e, nodes[rec].v, zones + rec, rec, n0, pff, px, dcls, q, req_aff, index_base, o)) return;
+        const int64_t tot = total_fb(cfg, o.bk, o.s_dev, dm, mag, o.g, pf);
+        topk_ins<K>(top, o.st ? 0ull : (((uint64_t)tot << 32) | (uint64_t)(0xFFFFFFFFu - o.g)));
+    });
+    if (!live) return;
+    if constexpr (K == 1) {
+        if (top[0]) atomicMax((unsigned long long*)(partial + j), (unsigned long long)top[0]);
+    } else {
+        uint64_t* dst = partial + (((size_t)blockIdx.y + part_off) * n_pods + j) * K;
+#pragma unroll
+        for (int t = 0; t < K; t++) dst[t] = top[t];
     }
 }
 
@@ -967,14 +1033,20 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
                             const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
                             uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, const uint32_t* special,
-                            uint32_t special_est, hipStream_t s) {
+                            uint32_t special_est, const uint32_t* c1, uint32_t c1_est, hipStream_t s) {
     if (n_list == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_list + 255) / 256, (n_nodes + chunk - 1) / chunk);
     if (fb) {  // the general records only (the fast-base records' maximum: k_ext_select)
         uint32_t chunk2, y2;
         ext_part2_grid(special_est, grid.x, &chunk2, &y2);
         k_ext_stats_sp<<<dim3(grid.x, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n0, chunk2, index_base, cfg,
-                                                        qst, dev_max, rsv_max, pref, special);
+                                                        qst, dev_max, rsv_max, pref, special, c1 != nullptr);
+        if (c1) {
+            uint32_t chunk3, y3;
+            ext_part2_grid(c1_est, grid.x, &chunk3, &y3);
+            k_ext_stats_c1<<<dim3(grid.x, y3), 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n0, chunk3, index_base, cfg,
+                                                            qst, dev_max, c1);
+        }
         return hipGetLastError();
     }
 #define KG_EXT_ST(EX, TP)                                                                                              \
@@ -1002,10 +1074,12 @@ hipError_t launch_max_fold(uint32_t* dst, const uint32_t* src, uint32_t n, hipSt
     return hipGetLastError();
 }
 
-hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, hipStream_t s) {
+hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, uint32_t* c1,
+                               hipStream_t s) {
     hipError_t e = hipMemsetAsync(special, 0, sizeof(uint32_t), s);
+    if (e == hipSuccess && c1) e = hipMemsetAsync(c1, 0, sizeof(uint32_t), s);
     if (e != hipSuccess || n_nodes == 0) return e;
-    k_special_scan<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, n_nodes, n0, special);
+    k_special_scan<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, n_nodes, n0, special, c1);
     return hipGetLastError();
 }
 
@@ -1123,17 +1197,29 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
                                 const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                                 uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
                                 const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
-                                const uint32_t* special, uint32_t special_est, hipStream_t s) {
+                                const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est,
+                                hipStream_t s) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     const uint32_t gx = (n_pods + 255) / 256, y1 = (n_nodes + chunk - 1) / chunk;
-    uint32_t chunk2, y2;
+    uint32_t chunk2, y2, chunk3 = 0, y3 = 0;
     ext_part2_grid(special_est, gx, &chunk2, &y2);
-    if (k == 1)
+    if (c1) ext_part2_grid(c1_est, gx, &chunk3, &y3);
+    const bool sp = c1 != nullptr;
+    if (k == 1) {
         k_ext_select_sp<1><<<dim3(gx, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, index_base, cfg, qst,
-                                                        dev_max, rsv_max, pref, partial, pstat, special, y1);
-    else
+                                                        dev_max, rsv_max, pref, partial, pstat, special, y1, sp);
+        if (c1)
+            k_ext_select_c1<1><<<dim3(gx, y3), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk3, index_base, cfg,
+                                                            qst, dev_max, pref, partial, c1, y1 + y2);
+    } else {
         k_ext_select_sp<KG_TOPK_MAX><<<dim3(gx, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, index_base,
-                                                                  cfg, qst, dev_max, rsv_max, pref, partial, pstat, special, y1);
+                                                                  cfg, qst, dev_max, rsv_max, pref, partial, pstat, special, y1,
+                                                                  sp);
+        if (c1)
+            k_ext_select_c1<KG_TOPK_MAX><<<dim3(gx, y3), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk3,
+                                                                      index_base, cfg, qst, dev_max, pref, partial, c1,
+                                                                      y1 + y2);
+    }
     return hipGetLastError();
 }
 

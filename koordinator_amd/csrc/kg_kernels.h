@@ -96,7 +96,7 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
                             const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
                             uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, const uint32_t* special,
-                            uint32_t special_est, hipStream_t s);
+                            uint32_t special_est, const uint32_t* c1, uint32_t c1_est, hipStream_t s);
 hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                                   const uint32_t* list, uint32_t n_list, uint32_t max_views, uint32_t index_base,
                                   const KCfg& cfg, bool exact,
@@ -115,13 +115,15 @@ hipError_t launch_ext_fix(const NodeRec* nodes, const ZoneRec* zones, const ExtD
                           uint32_t index_base, const KCfg& cfg, const uint32_t* qst, uint32_t* dev_max,
                           const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
                           uint32_t* rows, uint32_t* n_rows, hipStream_t s);
-// General records of a fast-base select (F_BIG, class 1, the lane's views); k > 1: partial chunks after the
-// fast-base kernel's (n_nodes / chunk of them).
+// General records of a fast-base select (F_BIG, class 1 unless split off into c1, the lane's views); k > 1: partial
+// chunks after the fast-base kernel's (n_nodes / chunk of them), then the class-1 kernel's (c1 != nullptr:
+// k_special_scan's c1 list, evaluated by the light k_ext_select_c1).
 hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                                 const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                                 uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
                                 const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
-                                const uint32_t* special, uint32_t special_est, hipStream_t s);
+                                const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est,
+                                hipStream_t s);
 // out[map[t]] = rows t of src (k keys each; row map[t] with src_by_map, src may then be out); rows whose pod
 // has a nonzero qst[pod] get zero keys and pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the
 // host path)
@@ -162,7 +164,8 @@ inline void ext_part2_grid(uint32_t special_est, uint32_t pod_blocks, uint32_t* 
     *chunk = est / want < 4u ? 4u : (est + want - 1) / want;
     *n_chunks = (est + *chunk - 1) / *chunk;
 }
-hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, hipStream_t s);
+hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, uint32_t* c1,
+                               hipStream_t s);
 hipError_t launch_rdev_codes(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, const DevRec* rdev,
                              const uint32_t* rdev_rec, uint32_t n_rdev, const DevClass* cls, uint32_t n_cls,
                              const KCfg& cfg, const ExtDev& e, uint8_t* out, hipStream_t s);

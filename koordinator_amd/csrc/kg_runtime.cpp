@@ -1631,6 +1631,20 @@ static bool gpu_zone_active(const kg_snap* s, const kg_pods* p) {
 }
 static bool gz_active(const kg_snap* s, const kg_pods* p) { return s->d_dev && ext_fast_base(s, p) && gpu_zone_active(s, p); }
 
+// Fast-base batch whose storage-class-1 records (not F_BIG) run the light eval_c1 kernels off k_special_scan's second
+// list: DeviceShare's hints are tabulated (e.gz), or no pod of the batch requests GPUs.
+static bool c1_split(const kg_snap* s, const kg_pods* p) {
+    return ext_fast_base(s, p) && s->n > s->n0 &&
+           (gz_active(s, p) || p->n_dclass == 0 || !(s->kcfg.plugins & KG_PLUGIN_DEV));
+}
+static const uint32_t* c1_list(const kg_snap* s, const kg_pods* p) {
+    return c1_split(s, p) ? s->d_special + s->n + 1 : nullptr;
+}
+// grid sizing of the general-record kernels: F_BIG records (plus class 1 unless split) or the largest class's views
+static uint32_t special_est(const kg_snap* s, const kg_pods* p) {
+    return c1_split(s, p) ? std::max(s->n_big_est, s->max_cls_views) : s->special_est();
+}
+
 // The batch's DevSum table over this snapshot's records (fast-base config-5 select with DeviceShare).
 static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     kg_ctx* ctx = s->ctx;
@@ -1699,8 +1713,9 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
     dst = ext_dev_sum(s, p, e);
     if (dst != KG_OK) return dst;
     if (ext_fast_base(s, p)) {  // records for the PART 2 kernels (pass 1 and pass 2 of this batch)
-        if (!s->d_special) HIP_TRY(ctx, hipMalloc(&s->d_special, sizeof(uint32_t) * ((size_t)s->n + 1)));
-        HIP_TRY(ctx, launch_special_scan(s->d_nodes, s->n, s->n0, s->d_special, ctx->stream));
+        if (!s->d_special) HIP_TRY(ctx, hipMalloc(&s->d_special, sizeof(uint32_t) * 2 * ((size_t)s->n + 1)));
+        HIP_TRY(ctx, launch_special_scan(s->d_nodes, s->n, s->n0, s->d_special, const_cast<uint32_t*>(c1_list(s, p)),
+                                         ctx->stream));
     }
     if (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) {
         // pods without a GPU request only get statistics from the nodes holding a view of their
@@ -1714,7 +1729,7 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
         const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(ng, 1), 8192);
         HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, s->n0, chunk, s->base,
                                       s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
-                                      s->d_special, s->special_est(), ctx->stream));
+                                      s->d_special, special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream));
     }
     return KG_OK;
 }
@@ -1828,8 +1843,12 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     uint32_t xparts = n_x ? (s->n + chunk - 1) / chunk : 0;
     if (fb) {
         uint32_t c2, y2;
-        ext_part2_grid(s->special_est(), (n_x + 255) / 256, &c2, &y2);
+        ext_part2_grid(special_est(s, p), (n_x + 255) / 256, &c2, &y2);
         xparts += y2;
+        if (c1_split(s, p)) {
+            ext_part2_grid(s->n - s->n0, (n_x + 255) / 256, &c2, &y2);
+            xparts += y2;
+        }
     }
     if (fused) xparts = 0;
     const uint32_t n_plain = split ? p->n_plain : 0;
@@ -1877,7 +1896,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         xe.cls_max = nullptr;
         HIP_TRY(ctx, launch_ext_select_sp(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base, s->kcfg,
                                           p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, xpart, p->d_pstat, s->d_special,
-                                          s->special_est(), ctx->stream));
+                                          special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream));
     }
     if (plain_on_side) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->join, 0));  // d_out zeroed + plain keys in
     if (!split) {
