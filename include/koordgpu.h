@@ -532,6 +532,13 @@ kg_status kg_snapshot_read_quotas(kg_snap* snap, int64_t* used, uint32_t* used_k
 kg_status kg_snapshot_upload_reservations(kg_snap* snap, const kg_rsv_view* views, uint32_t n_views,
                                           const kg_rsv_info* infos, uint32_t n_infos, const kg_rsv_dev* devs,
                                           uint32_t n_devs);
+/* Replace the views (with their reservations and GPU restore tables) of the nodes in nodes[0, n_nodes) by views[0, n_views)
+ * (each naming one of those nodes; a listed node without views loses its views); every other node keeps its views.
+ * The incremental form of kg_snapshot_upload_reservations for the nodes a Reserve / Unreserve or an event changed
+ * (the Reservation transformer's per-node restore, reservation/transformer.go:740-935): it clears their staleness. */
+kg_status kg_snapshot_update_views(kg_snap* snap, const uint32_t* nodes, uint32_t n_nodes, const kg_rsv_view* views,
+                                   uint32_t n_views, const kg_rsv_info* infos, uint32_t n_infos, const kg_rsv_dev* devs,
+                                   uint32_t n_devs);
 kg_status kg_snapshot_destroy(kg_snap* snap);
 
 kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out);

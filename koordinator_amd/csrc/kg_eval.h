@@ -521,6 +521,15 @@ __device__ __forceinline__ uint32_t numa_admit(const KCfg& c, const NumaZ& x, co
         }
     } else if (nl == 0) {
         numa_merge_perm(all, excl, x.status, 0, none, none, best);
+    } else if (nl == 2 && policy != KG_NUMA_BEST_EFFORT) {
+        // mergeFilteredHints over (cpu, memory) without a nil hint (nil lists fail above): a merged hint is preferred
+        // only when both lists' masks are equal and preferred (and the exclusive check passes); once one exists no
+        // non-preferred hint replaces it, and without one the policy fails (KG_ST_NUMA_ALIGN) whatever the mask. The
+        // preferred candidates come out of the nested loops in ascending k (la = lb = k): visit only those.
+        for (uint32_t l = L0 & L1 & pref0 & pref1; l; l &= l - 1u) {
+            const NumaHint h = numa_hint_at(nib, (uint32_t)(__ffs(l) - 1), pref0, sc_lo, sc_hi);
+            numa_merge_perm(all, excl, x.status, 2, h, h, best);
+        }
     } else if (nl == 1) {
         const uint32_t L = has[0] ? L0 : L1, P = has[0] ? pref0 : pref1;
         for (uint32_t l = L; l; l &= l - 1u) {

@@ -203,12 +203,25 @@ __global__ __launch_bounds__(64) void k_gpu_zone_sum(const NodeRec* __restrict__
 // F_BIG go to their own list (c1[0] = count), for the light class-1 kernels (eval_c1); special then holds F_BIG only.
 __global__ __launch_bounds__(256) void k_special_scan(const NodeRec* __restrict__ nodes, uint32_t n_nodes, uint32_t n0,
                                                       uint32_t* __restrict__ special, uint32_t* __restrict__ c1) {
-    const uint32_t rec = blockIdx.x * blockDim.x + threadIdx.x;
-    if (rec >= n_nodes) return;
+    const uint32_t rec0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = rec0 < n_nodes;
+    const uint32_t rec = live ? rec0 : 0u;  // every lane takes part in the ballots
     const int64_t* n = nodes[rec].v;
     const bool big = ((uint32_t)n[N_FLAGS] & F_BIG) != 0;
-    if (c1 && rec >= n0 && !big) c1[1 + atomicAdd(c1, 1u)] = rec;
-    else if (rec >= n0 || big) special[1 + atomicAdd(special, 1u)] = rec;
+    const bool to_c1 = live && c1 && rec >= n0 && !big, to_sp = live && !to_c1 && (rec >= n0 || big);
+    // one atomic per wave and list: the lanes' slots from the ballot's prefix counts
+    const uint64_t bc = __ballot(to_c1), bs = __ballot(to_sp);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    const uint32_t leader_c = bc ? (uint32_t)__ffsll((unsigned long long)bc) - 1u : 64u;
+    const uint32_t leader_s = bs ? (uint32_t)__ffsll((unsigned long long)bs) - 1u : 64u;
+    uint32_t base_c = 0, base_s = 0;
+    if (lane == leader_c) base_c = atomicAdd(c1, (uint32_t)__popcll(bc));
+    if (lane == leader_s) base_s = atomicAdd(special, (uint32_t)__popcll(bs));
+    base_c = __shfl(base_c, (int)(leader_c & 63u), 64);
+    base_s = __shfl(base_s, (int)(leader_s & 63u), 64);
+    if (to_c1) c1[1 + base_c + (uint32_t)__popcll(bc & below)] = rec;
+    if (to_sp) special[1 + base_s + (uint32_t)__popcll(bs & below)] = rec;
 }
 
 // Weighted total of a fast-base pair (FB paths): base total from the fast block + the normalised

@@ -208,9 +208,32 @@ __global__ __launch_bounds__(256) void k_big_sel(const NodeRec* __restrict__ nod
     uint32_t unsup = 0;
     if (lo < hi) {
         const PodV p = load_pod(pods, row);
+        // direct (fused) launches run after the fast records' kernels: a record whose NodeResourcesFit / LoadAware
+        // part fails, or whose best possible total (that part + the NUMA weight x 100) stays below the pod's current
+        // K-th best key, cannot change the result and skips the integer path. The fast block's NRF / LA part is exact
+        // on records that are F_BIG only for their NUMA / CPU bind policies (not F_VBIG); prune is off for a pod
+        // outside the fast domain (the lanes here are fast lanes).
+        uint64_t floor_key = 0;
+        if (direct) {
+            floor_key = ~0ull;
+#pragma unroll
+            for (int t = 0; t < K; t++) floor_key = min(floor_key, (uint64_t)out[(size_t)row * K + t]);
+        }
+        const PodF pf = to_podf(p, cfg);
+        const KCfg cv = cfg_in_vgprs(cfg);  // the fast path's form of the weights
         for (uint32_t b = lo; b < hi; b++) {
             const uint32_t i = big_list[b];
-            const PairOut o = eval_pair<false, false, true, true, false>(cfg, nodes[i].v, zones + i, p);
+            const int64_t* nv = nodes[i].v;
+            const uint32_t fl = (uint32_t)nv[N_FLAGS];
+            if (direct && !(fl & F_VBIG)) {
+                const FastRec& fr = *reinterpret_cast<const FastRec*>(&nv[FAST_BEGIN]);
+                uint32_t part = 0;
+                const bool ok = fast_eval<KG_PLUGIN_NRF | KG_PLUGIN_LA, 0>(cv, fr, zones + i, pf, part);
+                if (!ok) continue;  // the pair fails NodeResourcesFit / LoadAware: key 0
+                const uint64_t bound = ((uint64_t)(part + (uint32_t)cfg.w_numa * 100u) << 32) | 0xFFFFFFFFull;
+                if (bound < floor_key) continue;
+            }
+            const PairOut o = eval_pair<false, false, true, true, false>(cfg, nv, zones + i, p);
             unsup |= o.status & KG_ST_UNSUPPORTED;
             topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
         }
@@ -629,8 +652,10 @@ __device__ __forceinline__ void assume_wave(const KCfg& c, NodeRec& r, ZoneRec& 
     }
     const uint32_t pol0 = (f0 >> F_NUMA_POLICY_SHIFT) & 15u;
     const bool pol_host = pol0 == 2u /* KG_NUMA_RESTRICTED */;
-    const bool big_all = (__ballot(big) != 0ull) || pol_host || ((meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
-    const uint32_t f = f0 | (full ? (uint32_t)F_PODS_FULL : 0u) | (big_all ? (uint32_t)F_BIG : 0u);
+    const bool vbig = __ballot(big) != 0ull;
+    const bool big_all = vbig || pol_host || ((meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
+    const uint32_t f = f0 | (full ? (uint32_t)F_PODS_FULL : 0u) | (big_all ? (uint32_t)F_BIG : 0u) |
+                       (vbig ? (uint32_t)F_VBIG : 0u);
     // derived slot dl.dst of this lane (lanes < N_DER)
     uint32_t a = dl.a, b = dl.b, mode = (f >> F_LA_FMODE_NP_SHIFT) & 3u;
     if (dl.op == DER_HEAD && a >= (uint32_t)N_LA_FCUT_PROD0) {  // prod heads: the non-prod ones without prod thresholds
@@ -900,18 +925,6 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
     }
     if (n_fast) {
         const uint32_t pod_blocks = (n_fast + 255) / 256;
-        // F_BIG records of the fast lanes: integer path, chunked over the device's list
-        {
-            dim3 grid(pod_blocks, a.big_y), block(256);
-            if (K == 1)
-                k_big_sel<1><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, a.n_rows, a.big_list, a.big_count,
-                                                    a.index_base, a.cfg, a.partial, a.big_part0, a.fused ? a.out : nullptr,
-                                                    a.pmap, a.pstat, a.order);
-            else
-                k_big_sel<KG_TOPK_MAX><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, a.n_rows, a.big_list,
-                                                              a.big_count, a.index_base, a.cfg, a.partial, a.big_part0,
-                                                              a.fused_k ? a.out : nullptr, a.pmap, a.pstat, a.order);
-        }
         for (int cls = 0; cls < 2; cls++) {
             const SelectRange& r = a.range[cls];
             if (r.n_chunks == 0) continue;
@@ -944,6 +957,19 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
                 if (cls == 0) select_fast<KG_TOPK_MAX, 0>(a, r, s);
                 else select_fast<KG_TOPK_MAX, 1>(a, r, s);
             }
+        }
+        // F_BIG records of the fast lanes: integer path, chunked over the device's list; after the fast records'
+        // kernels, whose keys in out let a direct launch skip records that cannot enter the pod's top-K
+        {
+            dim3 grid(pod_blocks, a.big_y), block(256);
+            if (K == 1)
+                k_big_sel<1><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, a.n_rows, a.big_list, a.big_count,
+                                                    a.index_base, a.cfg, a.partial, a.big_part0, a.fused ? a.out : nullptr,
+                                                    a.pmap, a.pstat, a.order);
+            else
+                k_big_sel<KG_TOPK_MAX><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, a.n_rows, a.big_list,
+                                                              a.big_count, a.index_base, a.cfg, a.partial, a.big_part0,
+                                                              a.fused_k ? a.out : nullptr, a.pmap, a.pstat, a.order);
         }
         if (!a.fused && !a.fused_k) {
             hipError_t e = launch_merge_list(a.partial, 0, select_fparts(a), a.n_rows, a.order, n_fast, K, a.out, s);

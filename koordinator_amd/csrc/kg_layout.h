@@ -100,7 +100,9 @@ enum : uint32_t {
     F_BIG = 1u << 18,          // some value is outside the exact float64 fast path (derived)
     F_TOPO = 1u << 19,         // BestEffort node: Filter / Score like policy None, the Reserve runs the topology
                                // manager (window replay takes the integer path for the Reserve's zone)
-    F_DERIVED_MASK = F_PODS_FULL | F_BIG,
+    F_VBIG = 1u << 20,         // F_BIG for a value outside the fast path (not only for the node's policies): the fast
+                               // block's NodeResourcesFit / LoadAware part is exact unless this is set (derived)
+    F_DERIVED_MASK = F_PODS_FULL | F_BIG | F_VBIG,
 };
 enum : uint32_t { FMODE_CHECK = 0, FMODE_PASS = 1, FMODE_FAIL_EXPIRED = 2 };
 
@@ -300,6 +302,7 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
         zf.free_cpu = x100(tc - uc);
         zf.free_mem = x100(tm - um);
     }
+    if (big) f |= F_VBIG;
     // Restricted nodes run the general NUMA topology manager in Filter, on the integer path (BestEffort
     // nodes do not admit in Filter, plugin.go:446-455: their Filter / Score fit the fast path)
     const uint32_t pol0 = (f >> F_NUMA_POLICY_SHIFT) & 15u;

@@ -87,13 +87,18 @@ struct kg_snap {
     uint32_t special_est() const { return std::max(n - n0, max_cls_views); }
     uint32_t n_views = 0;
     uint32_t max_cls_views = 0;  // views of the largest reservation class
-    std::vector<kg_rsv_view> h_views;  // as uploaded (local snapshot indices)
+    std::vector<kg_rsv_view> h_views;  // as uploaded (local snapshot indices; kg_snapshot_update_views / record moves)
     std::vector<kg_rsv_info> h_infos;
     std::vector<uint64_t> cls_mask;  // per snapshot index: classes with a view on the node
     // A Reserve / Unreserve / row update on a node that holds views changes what its views restore
     // (absolute restored Requested etc.): the caller recomputes the restore (the reference reruns the
     // Reservation transformer every cycle) and re-uploads; until then selects on the snapshot refuse.
     bool views_stale = false;
+    // the uploaded reservation views in ABI form (by node index: they survive record moves), for per-node updates;
+    // stale[i]: node i holds views and changed since they were computed
+    std::vector<kg_rsv_dev> h_rdevs;
+    std::vector<uint8_t> stale;
+    uint32_t n_stale = 0;
     // Generation: bumped by every call that changes what the snapshot holds (upload, row update, Assume /
     // Forget, replay, quota / reservation upload); kg_snapshot_generation reads it.
     uint64_t gen = 0;
@@ -112,6 +117,8 @@ struct kg_snap {
         QuotaState* q = nullptr;
         uint32_t nq = 0;
         bool valid = false, views_stale = false;
+        std::vector<uint8_t> stale;
+        uint32_t n_stale = 0;
     } ck, bk;
     void invalidate_saved() { ck.valid = bk.valid = false; }
     // cpuset binding: CPU topology table, per-record allocations (device order, like h_dev)
@@ -639,13 +646,19 @@ bool need_topo(const kg_snap* s, const kg_pods* p) {
 kg_status check_views(kg_snap* s) {
     if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->views_stale)
         return fail(s->ctx, KG_UNSUPPORTED,
-                    "reservation views are stale after a state change on a node holding one: re-upload them "
-                    "(kg_snapshot_upload_reservations)");
+                    "reservation views are stale after a state change on %u node(s) holding them: update them "
+                    "(kg_snapshot_update_views) or re-upload them (kg_snapshot_upload_reservations)", s->n_stale);
     return KG_OK;
 }
 
 void touch_views(kg_snap* s, uint32_t node) {
-    if (node < s->cls_mask.size() && s->cls_mask[node]) s->views_stale = true;
+    if (node < s->cls_mask.size() && s->cls_mask[node]) {
+        if (node < s->stale.size() && !s->stale[node]) {
+            s->stale[node] = 1;
+            s->n_stale++;
+        }
+        s->views_stale = true;
+    }
 }
 
 
@@ -696,6 +709,11 @@ kg_status record_end(kg_ctx* ctx, hipEvent_t a, hipEvent_t b) {
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
+extern "C" {  // defined with the reservation entry points
+static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv, const kg_rsv_info* infos, uint32_t ni,
+                              const kg_rsv_dev* devs, uint32_t nd);
+}
+
 extern "C" {
 
 int kg_abi_version(void) { return KG_ABI_VERSION; }
@@ -977,7 +995,6 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
         if (dev) build_dev(cols, k, &devs[k]);
         moved |= node_class(recs[k]) != (s->pos[rows[k]] < s->n0 ? 0u : 1u);
     }
-    if (moved && s->n_views) return fail(ctx, KG_UNSUPPORTED, "row update moves a record while reservation views are uploaded");
     {
         kg_status st = check_gpu_tables(ctx, cols, n, s->n_gpu_tables);  // rows name the uploaded tables
         if (st != KG_OK) return st;
@@ -1030,6 +1047,19 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
         HIP_TRY(ctx, hipMemcpyAsync(s->d_nodes, s->h_nodes.data(), sizeof(NodeRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, s->h_dev.data(), sizeof(DevRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
+        if (s->n_views) {  // the views name records by position: re-place them (their staleness stays as it is)
+            const std::vector<uint8_t> keep = s->stale;
+            const uint32_t keep_n = s->n_stale;
+            const std::vector<kg_rsv_view> v = s->h_views;
+            const std::vector<kg_rsv_info> in = s->h_infos;
+            const std::vector<kg_rsv_dev> d = s->h_rdevs;
+            kg_status st = upload_views(s, v.data(), (uint32_t)v.size(), in.data(), (uint32_t)in.size(), d.data(),
+                                        (uint32_t)d.size());
+            if (st != KG_OK) return st;
+            s->stale = keep;
+            s->n_stale = keep_n;
+            s->views_stale = keep_n != 0;
+        }
     } else if (n) {
         // one staged copy of every changed record, then one scatter launch to their positions
         const size_t rb = sizeof(NodeRec) + sizeof(ZoneRec) + (dev ? sizeof(DevRec) : 0);
@@ -2536,6 +2566,8 @@ static kg_status save_state(kg_snap* s, kg_snap::Saved& k) {
         HIP_TRY(ctx, hipMemcpyAsync(k.q, s->d_qstate, sizeof(QuotaState) * 2 * (size_t)s->n_quotas, hipMemcpyDeviceToDevice,
                                     ctx->stream));
     k.views_stale = s->views_stale;
+    k.stale = s->stale;
+    k.n_stale = s->n_stale;
     k.valid = true;
     return KG_OK;
 }
@@ -2552,6 +2584,8 @@ static kg_status restore_state(kg_snap* s, kg_snap::Saved& k) {
                                     ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     s->views_stale = k.views_stale;
+    s->stale = k.stale;
+    s->n_stale = k.n_stale;
     s->gen++;
     return KG_OK;
 }
@@ -2741,12 +2775,10 @@ kg_status kg_snapshot_read_quotas(kg_snap* s, int64_t* used, uint32_t* used_keys
     return KG_OK;
 }
 
-kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, uint32_t nv, const kg_rsv_info* infos,
-                                          uint32_t ni, const kg_rsv_dev* devs, uint32_t nd) {
-    if (!s || (!views && nv) || (!infos && ni) || (!devs && nd)) return KG_INVALID_ARG;
+// the views / reservations / GPU restore tables of the whole snapshot onto the device (caller holds the lock)
+static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv, const kg_rsv_info* infos, uint32_t ni,
+                              const kg_rsv_dev* devs, uint32_t nd) {
     kg_ctx* ctx = s->ctx;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
     // views sorted by (class, record position); node class masks
     std::vector<uint32_t> order(nv);
     std::vector<uint64_t> mask(s->n, 0);
@@ -2855,10 +2887,91 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->n_views = nv;
     s->views_stale = false;
+    s->h_views.assign(views, views + nv);
+    s->h_infos.assign(infos, infos + ni);
+    s->h_rdevs.assign(devs, devs + nd);
+    s->stale.assign(s->n, 0);
+    s->n_stale = 0;
     s->gen++;
     s->invalidate_saved();
     s->max_cls_views = 0;
     for (int c = 0; c < RSV_MAX_CLASSES; c++) s->max_cls_views = std::max(s->max_cls_views, cb[c + 1] - cb[c]);
+    return KG_OK;
+}
+
+kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, uint32_t nv, const kg_rsv_info* infos,
+                                          uint32_t ni, const kg_rsv_dev* devs, uint32_t nd) {
+    if (!s || (!views && nv) || (!infos && ni) || (!devs && nd)) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
+    return upload_views(s, views, nv, infos, ni, devs, nd);
+}
+
+kg_status kg_snapshot_update_views(kg_snap* s, const uint32_t* nodes, uint32_t n_nodes, const kg_rsv_view* views, uint32_t nv,
+                                   const kg_rsv_info* infos, uint32_t ni, const kg_rsv_dev* devs, uint32_t nd) {
+    if (!s || (!nodes && n_nodes) || (!views && nv) || (!infos && ni) || (!devs && nd)) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
+    std::vector<uint8_t> listed(s->n, 0);
+    for (uint32_t k = 0; k < n_nodes; k++) {
+        if (nodes[k] >= s->n) return fail(ctx, KG_INVALID_ARG, "node %u >= %u", nodes[k], s->n);
+        listed[nodes[k]] = 1;
+    }
+    for (uint32_t v = 0; v < nv; v++)
+        if (views[v].node >= s->n || !listed[views[v].node])
+            return fail(ctx, KG_INVALID_ARG, "view %u: node %u is not among the updated nodes", v, views[v].node);
+    // the kept views of the other nodes (their reservations and GPU tables re-indexed), then the new ones
+    std::vector<kg_rsv_view> av;
+    std::vector<kg_rsv_info> ai;
+    std::vector<kg_rsv_dev> ad;
+    std::vector<int32_t> dmap(s->h_rdevs.size(), -1);
+    auto dev_of = [&](int32_t d) {
+        if (d < 0) return d;
+        if (dmap[d] < 0) {
+            dmap[d] = (int32_t)ad.size();
+            ad.push_back(s->h_rdevs[d]);
+        }
+        return dmap[d];
+    };
+    for (const kg_rsv_view& x : s->h_views) {
+        if (listed[x.node]) continue;
+        kg_rsv_view y = x;
+        y.first = (uint32_t)ai.size();
+        y.dev_base = dev_of(x.dev_base);
+        for (uint32_t t = x.first; t < x.first + x.count; t++) {
+            kg_rsv_info r = s->h_infos[t];
+            r.dev = dev_of(r.dev);
+            ai.push_back(r);
+        }
+        av.push_back(y);
+    }
+    const uint32_t i0 = (uint32_t)ai.size(), d0 = (uint32_t)ad.size();
+    for (uint32_t v = 0; v < nv; v++) {
+        kg_rsv_view y = views[v];
+        if ((uint64_t)y.first + y.count > ni) return fail(ctx, KG_INVALID_ARG, "view %u: reservations out of range", v);
+        y.first += i0;
+        if (y.dev_base >= 0) y.dev_base += (int32_t)d0;
+        av.push_back(y);
+    }
+    for (uint32_t t = 0; t < ni; t++) {
+        kg_rsv_info r = infos[t];
+        if (r.dev >= 0) r.dev += (int32_t)d0;
+        ai.push_back(r);
+    }
+    ad.insert(ad.end(), devs, devs + nd);
+    const std::vector<uint8_t> keep = s->stale;
+    kg_status st = upload_views(s, av.data(), (uint32_t)av.size(), ai.data(), (uint32_t)ai.size(), ad.data(),
+                                (uint32_t)ad.size());
+    if (st != KG_OK) return st;
+    // the listed nodes are fresh; any other stale node stays stale
+    for (uint32_t i = 0; i < s->n && i < keep.size(); i++)
+        if (keep[i] && !listed[i] && s->cls_mask[i]) {
+            s->stale[i] = 1;
+            s->n_stale++;
+        }
+    s->views_stale = s->n_stale != 0;
     return KG_OK;
 }
 

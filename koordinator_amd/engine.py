@@ -117,6 +117,9 @@ def lib():
     L.kg_snapshot_read_quotas.restype = st
     L.kg_snapshot_upload_reservations.argtypes = [vp, P(abi.KgRsvView), u32, P(abi.KgRsvInfo), u32, P(abi.KgRsvDev), u32]
     L.kg_snapshot_upload_reservations.restype = st
+    L.kg_snapshot_update_views.argtypes = [vp, P(u32), u32, P(abi.KgRsvView), u32, P(abi.KgRsvInfo), u32,
+                                           P(abi.KgRsvDev), u32]
+    L.kg_snapshot_update_views.restype = st
     L.kg_assume_ext.argtypes = [vp, vp, u32, u32, P(i32), P(u32)]
     L.kg_assume_ext.restype = st
     L.kg_forget_ext.argtypes = [vp, vp, u32, u32, i32, u32]
@@ -272,6 +275,15 @@ class Snapshot:
             self.h, C.cast(rsv.views, C.POINTER(abi.KgRsvView)), rsv.n_views,
             C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos,
             C.cast(rsv.devs, C.POINTER(abi.KgRsvDev)), rsv.n_devs), "kg_snapshot_upload_reservations")
+
+    def update_views(self, nodes, rsv: abi.Reservations):
+        """kg_snapshot_update_views: the views of `nodes` replaced by rsv's (which name only those nodes)."""
+        nd = np.ascontiguousarray(np.asarray(nodes, np.uint32))
+        self.ctx.check(self.ctx.L.kg_snapshot_update_views(
+            self.h, nd.ctypes.data_as(C.POINTER(C.c_uint32)), len(nd),
+            C.cast(rsv.views, C.POINTER(abi.KgRsvView)), rsv.n_views,
+            C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos,
+            C.cast(rsv.devs, C.POINTER(abi.KgRsvDev)), rsv.n_devs), "kg_snapshot_update_views")
 
     def close(self):
         if getattr(self, "h", None) and getattr(self.ctx, "h", None):

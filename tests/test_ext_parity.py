@@ -321,18 +321,71 @@ def test_ext_result_status(ctx, monkeypatch, split):
     assert (sel & (ref.status == 0)).any()
 
 
-def test_views_stale_after_assume_on_view_node(ctx):
-    """A Reserve on a node holding reservation views changes what the views restore: selects refuse
-    (KG_UNSUPPORTED) until the caller re-uploads the recomputed views."""
+def _views_after_plain_pod(rsv, node, pods, j):
+    """The restore of `node` after a pod that matches none of its reservations (and binds no GPU) lands there: the
+    true NodeInfo and the default columns grow by the pod's requests, so every view of the node does too
+    (transformer.go:740-811: view = default + the matched reservations' corrections). Returns (full, delta): the
+    whole reservation set with those views shifted, and the node's views alone for kg_snapshot_update_views."""
+    import ctypes as C
+    def shifted(v):
+        w = abi.KgRsvView()
+        C.pointer(w)[0] = v
+        for k, col in enumerate(("req_cpu", "req_mem", "req_eph", "sc_req0", "sc_req1")):
+            w.req[k] += int(pods[col][j])
+            w.pod_requested[k] += int(pods[col][j])
+        w.nz_cpu += int(pods["nz_cpu"][j])
+        w.nz_mem += int(pods["nz_mem"][j])
+        w.num_pods += 1
+        return w
+    full = abi.Reservations([], [])
+    full.views = (abi.KgRsvView * max(1, rsv.n_views))()
+    mine = []
+    for x in range(rsv.n_views):
+        v = rsv.views[x]
+        full.views[x] = shifted(v) if v.node == node else v
+        if v.node == node:
+            mine.append(full.views[x])
+    full.n_views = rsv.n_views
+    full.infos, full.n_infos, full.devs, full.n_devs = rsv.infos, rsv.n_infos, rsv.devs, rsv.n_devs
+    delta = abi.Reservations([], [])
+    delta.views = (abi.KgRsvView * max(1, len(mine)))(*mine)
+    delta.n_views = len(mine)
+    delta.infos, delta.n_infos, delta.devs, delta.n_devs = rsv.infos, rsv.n_infos, rsv.devs, rsv.n_devs
+    return full, delta
+
+
+def test_view_update_after_assume_on_view_node(ctx):
+    """A Reserve on a node holding reservation views makes its views stale: selects refuse (KG_UNSUPPORTED) until
+    kg_snapshot_update_views replaces that node's views with the recomputed restore; the next select then equals
+    the oracle's on the updated state (the other nodes' views untouched)."""
     cfg, nodes, pods, quotas, rsv = synth.cluster5(600, 64, seed_config=74, rsv_frac=0.5)
+    pods = {k: v.copy() for k, v in pods.items()}
     kc = cfg.kg_config()
-    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
     view_nodes = sorted({int(v.node) for v in rsv.view_list()})
+    plain = [j for j in range(64) if pods["rsv_class"][j] < 0 and pods["dev_count"][j] == 0]
+    pick = [(j, i) for j in plain for i in view_nodes if ref.status[j, i] == 0]
+    assert pick
+    j, i = pick[0]
+    pods["quota"][j] = -1  # no ElasticQuota Reserve to follow in the oracle table
+    ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
+    assert ref.status[j, i] == 0
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
     engine.eval_select(snap, batch, 1)
-    zone, minors = engine.assume_ext(snap, batch, 0, view_nodes[0])
+    engine.assume_ext(snap, batch, j, i)
     with pytest.raises(engine.Unsupported):
         engine.eval_select(snap, batch, 1)
-    snap.upload_reservations(rsv)
+    full, delta = _views_after_plain_pod(rsv, i, pods, j)
+    snap.update_views([i], delta)
+    st = oracle_lib.OracleState(kc, nodes)
+    st.assume(i, pods, j)
+    after = dict(nodes)
+    after.update(st.table())
+    for k in (1, 3):
+        got = engine.eval_select(snap, batch, k)
+        assert np.array_equal(got, oracle_lib.ext_select(kc, after, pods, k, 0, quotas, full)), k
+    # a listed node without views loses them; the rest of the snapshot keeps its own
+    snap.update_views([i], abi.Reservations([], []))
     engine.eval_select(snap, batch, 1)
 
 
