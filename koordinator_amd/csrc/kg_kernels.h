@@ -45,6 +45,13 @@ struct LaunchSelect {
     uint32_t big_y, big_part0;  // F_BIG chunks (blockIdx.y) and their first partial row (unfused)
     const uint32_t* order;  // lane -> row: fast lanes (grouped by wave kind) then integer lanes; nullptr: identity
     uint32_t n_fast;        // fast lanes (0 unless `fast`)
+    // integer lanes with atomics into out (K == 1, or fused_k): pruned evaluation when ipairs is set -- records
+    // [0, iseed) seed each lane's top-K on the integer path, then only the pairs whose fast-path NodeResourcesFit /
+    // LoadAware bound can still enter it (survivors, (lane << 32) | record, at most ipairs_cap) are evaluated
+    uint64_t* ipairs;       // per filter workgroup a segment of 256 x chunk slots
+    uint32_t* ipair_count;  // per segment: survivors
+    uint64_t ipairs_cap;    // slots of ipairs
+    uint32_t iseg_cap, iseed;  // entries of ipair_count; seed records
 };
 inline uint32_t select_fparts(const LaunchSelect& a) { return a.big_part0 + a.big_y; }
 

@@ -136,6 +136,120 @@ __global__ __launch_bounds__(256) void k_select(const NodeRec* __restrict__ node
     }
 }
 
+// ---- integer lanes, pruned (LaunchSelect.ipairs) ------------------------------------------------------------
+// The lanes whose pods cannot take the fast path (a NUMA policy of their own, cpuset binding) evaluate every record on
+// the integer path. Pruned form, exact for top-K into out: (1) k_int_seed: records [0, iseed) on the integer path,
+// their keys into out (real pairs: out's K-th key is then a lower bound of the pod's final K-th key); (2)
+// k_int_filter: records [iseed, end) with the fast path's NodeResourcesFit / LoadAware part (exact for a pod in the
+// fast value domain on a record that is not F_VBIG): a pair failing those filters has key 0, and one whose total
+// cannot exceed that part + the NUMA weight x 100 is dropped when that bound is below out's K-th key; the rest are
+// appended to ipairs (a full list: the lane evaluates them itself); (3) k_int_pairs: the survivors on the integer
+// path, one pair per lane. (NodeNUMAResource's KG_ST_UNSUPPORTED is never produced for a pair these filters drop:
+// it is not reached on the device.)
+template <int K>
+__device__ __forceinline__ void int_insert(uint64_t* out, uint32_t row, const uint64_t (&top)[K]) {
+    if constexpr (K == 1) {
+        if (top[0]) atomicMax((unsigned long long*)(out + row), (unsigned long long)top[0]);
+    } else {
+        topk_atomic<K>(out + (size_t)row * K, top);
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_int_seed(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                  PodsDev pods, uint32_t n_lanes, const uint32_t* __restrict__ order,
+                                                  uint32_t seed, uint32_t index_base, KCfg cfg, uint64_t* __restrict__ out,
+                                                  const uint32_t* __restrict__ pmap, uint32_t* __restrict__ pstat) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_lanes) return;
+    const uint32_t row = order ? order[j] : j;
+    const PodV p = load_pod(pods, row);
+    uint64_t top[K];
+#pragma unroll
+    for (int t = 0; t < K; t++) top[t] = 0;
+    uint32_t unsup = 0;
+    const uint32_t lo = blockIdx.y * ((seed + gridDim.y - 1) / gridDim.y), hi = min(seed, lo + (seed + gridDim.y - 1) / gridDim.y);
+    for (uint32_t i = lo; i < hi; i++) {
+        const PairOut o = eval_pair<false, false, true, true, false>(cfg, nodes[i].v, zones + i, p);
+        unsup |= o.status & KG_ST_UNSUPPORTED;
+        topk_insert<K>(top, pair_key(cfg, o, rec_gidx(nodes[i], index_base)));
+    }
+    int_insert<K>(out, row, top);
+    if (unsup) atomicOr(pstat + (pmap ? pmap[row] : row), unsup);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_int_filter(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                    PodsDev pods, uint32_t n_lanes, const uint32_t* __restrict__ order,
+                                                    uint32_t begin, uint32_t end, uint32_t chunk, uint32_t index_base,
+                                                    KCfg cfg, uint64_t* __restrict__ out, uint64_t* __restrict__ pairs,
+                                                    uint32_t* __restrict__ seg_count) {
+    // survivors go to this workgroup's own segment of `pairs` (256 x chunk slots: room for every pair it walks),
+    // counted in LDS; no global atomics
+    __shared__ uint32_t cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    const uint32_t seg = blockIdx.y * gridDim.x + blockIdx.x;
+    uint64_t* dst = pairs + (size_t)seg * 256u * chunk;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = j < n_lanes;
+    const uint32_t row = live ? (order ? order[j] : j) : 0u;
+    const PodV p = load_pod(pods, row);
+    const bool fastv = live && (p.flags & POD_FASTV) != 0;
+    const PodF pf = to_podf(p, cfg);
+    const KCfg cv = cfg_in_vgprs(cfg);
+    const uint64_t floor_key = live ? out[(size_t)row * K + (K - 1)] : ~0ull;
+    const uint32_t bonus = (uint32_t)cfg.w_numa * 100u;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+    const uint32_t lo = begin + blockIdx.y * chunk, hi = min(end, lo + chunk);
+    for (uint32_t i = lo; i < hi; i++) {
+        const int64_t* nv = nodes[i].v;
+        bool keep = live;
+        if (fastv && !((uint32_t)nv[N_FLAGS] & F_VBIG)) {
+            const FastRec& fr = *reinterpret_cast<const FastRec*>(&nv[FAST_BEGIN]);
+            uint32_t part = 0;
+            const bool ok = fast_eval<KG_PLUGIN_NRF | KG_PLUGIN_LA, 0>(cv, fr, zones + i, pf, part);
+            keep = ok && ((((uint64_t)(part + bonus)) << 32) | 0xFFFFFFFFull) >= floor_key;
+        }
+        const uint64_t bk = __ballot(keep);
+        if (bk == 0ull) continue;
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)bk) - 1u;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&cnt, (uint32_t)__popcll(bk));
+        base = __shfl(base, (int)leader, 64);
+        if (keep) dst[base + (uint32_t)__popcll(bk & below)] = ((uint64_t)j << 32) | i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) seg_count[seg] = cnt;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_int_pairs(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+                                                   PodsDev pods, const uint32_t* __restrict__ order,
+                                                   const uint64_t* __restrict__ pairs, const uint32_t* __restrict__ seg_count,
+                                                   uint32_t n_segs, uint32_t seg_cap, uint32_t index_base, KCfg cfg,
+                                                   uint64_t* __restrict__ out, const uint32_t* __restrict__ pmap,
+                                                   uint32_t* __restrict__ pstat) {
+    // one workgroup per segment at a time, its lanes over the segment's survivors
+    for (uint32_t seg = blockIdx.x; seg < n_segs; seg += gridDim.x) {
+        const uint32_t n = seg_count[seg];
+        for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+            const uint64_t e = pairs[(size_t)seg * seg_cap + t];
+            const uint32_t j = (uint32_t)(e >> 32), i = (uint32_t)e;
+            const uint32_t row = order ? order[j] : j;
+            const PodV p = load_pod(pods, row);
+            const PairOut o = eval_pair<false, false, true, true, false>(cfg, nodes[i].v, zones + i, p);
+            uint64_t top[K];
+#pragma unroll
+            for (int u = 0; u < K; u++) top[u] = 0;
+            top[0] = pair_key(cfg, o, rec_gidx(nodes[i], index_base));
+            int_insert<K>(out, row, top);
+            if (o.status & KG_ST_UNSUPPORTED) atomicOr(pstat + (pmap ? pmap[row] : row), o.status & KG_ST_UNSUPPORTED);
+        }
+    }
+}
+
 // Fused top-1 select of one storage class: lane = pod, blockIdx.y = chunk of records [begin, end); the
 // lane's best key goes to out[pod] by atomicMax (out zeroed by the launcher; the F_BIG records come from
 // k_big_sel); no per-chunk partials, no merge pass. `order` (nullable) lists the fast lanes grouped by
@@ -976,7 +1090,40 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
     }
-    if (n_int && a.irange.n_chunks) {
+    const uint32_t seed_n = a.irange.n_chunks ? min(a.iseed, a.irange.end) : 0u;
+    const uint32_t i_lb = (n_int + 255) / 256;
+    const uint32_t i_chunk = max(64u, (a.irange.end - seed_n + max(1u, 2048u / max(1u, i_lb)) - 1) / max(1u, 2048u / max(1u, i_lb)));
+    const uint32_t i_fy = a.irange.n_chunks ? (a.irange.end - seed_n + i_chunk - 1) / i_chunk : 0u;
+    const bool pruned = n_int && a.irange.n_chunks && a.ipairs && !a.exact && (K == 1 || a.fused_k) &&
+                        (uint64_t)i_lb * i_fy * 256u * i_chunk <= a.ipairs_cap && (uint64_t)i_lb * i_fy <= a.iseg_cap;
+    if (pruned) {
+        // pruned integer lanes (see k_int_seed): seed, filter into per-workgroup segments, survivors
+        const uint32_t* io = a.order ? a.order + n_fast : nullptr;
+        const uint32_t sy = max(1u, min(64u, (2048u + i_lb - 1) / i_lb));
+        const uint32_t n_segs = i_lb * i_fy;
+        if (K == 1) {
+            if (seed_n) k_int_seed<1><<<dim3(i_lb, sy), 256, 0, s>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n, a.index_base,
+                                                                     a.cfg, a.out, a.pmap, a.pstat);
+            if (i_fy) k_int_filter<1><<<dim3(i_lb, i_fy), 256, 0, s>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n,
+                                                                       a.irange.end, i_chunk, a.index_base, a.cfg, a.out,
+                                                                       a.ipairs, a.ipair_count);
+            if (n_segs) k_int_pairs<1><<<min(n_segs, 4096u), 256, 0, s>>>(a.nodes, a.zones, a.pods, io, a.ipairs, a.ipair_count,
+                                                                          n_segs, 256u * i_chunk, a.index_base, a.cfg, a.out,
+                                                                          a.pmap, a.pstat);
+        } else {
+            if (seed_n)
+                k_int_seed<KG_TOPK_MAX><<<dim3(i_lb, sy), 256, 0, s>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n, a.index_base,
+                                                                       a.cfg, a.out, a.pmap, a.pstat);
+            if (i_fy)
+                k_int_filter<KG_TOPK_MAX><<<dim3(i_lb, i_fy), 256, 0, s>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n,
+                                                                           a.irange.end, i_chunk, a.index_base, a.cfg, a.out,
+                                                                           a.ipairs, a.ipair_count);
+            if (n_segs)
+                k_int_pairs<KG_TOPK_MAX><<<min(n_segs, 4096u), 256, 0, s>>>(a.nodes, a.zones, a.pods, io, a.ipairs,
+                                                                            a.ipair_count, n_segs, 256u * i_chunk,
+                                                                            a.index_base, a.cfg, a.out, a.pmap, a.pstat);
+        }
+    } else if (n_int && a.irange.n_chunks) {
         const SelectRange& r = a.irange;
         if (a.exact) {
             if (K == 1) select_instance<1, true, false, 0, 0>(a, r, n_fast, n_int, true, s);

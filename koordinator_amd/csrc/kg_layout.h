@@ -363,7 +363,11 @@ KG_HD inline int node_class(const NodeRec& r) {
     return (((uint32_t)r.v[N_FLAGS] >> F_NUMA_POLICY_SHIFT) & 15u) == 3u /* KG_NUMA_SINGLE_NODE */ ? 1 : 0;
 }
 
-// Pod batch (device pointers, SoA). flags: low 16 bits KG_POD_*, bits 16..19 pod NUMA policy.
+// Pod flag bit 20 (set by the host): every request value is inside the float64 fast domain (the pod may still take
+// the integer lanes for its NUMA policy or cpuset binding): its NodeResourcesFit / LoadAware fast part is exact.
+constexpr uint32_t POD_FASTV = 1u << 20;
+
+// Pod batch (device pointers, SoA). flags: low 16 bits KG_POD_*, bits 16..19 pod NUMA policy, bit 20 POD_FASTV.
 struct PodsDev {
     // config-5 columns (nullptr unless the snapshot enables DeviceShare / Reservation / ElasticQuota)
     const int64_t* dev_req;     // [pod][KG_DEV_R]

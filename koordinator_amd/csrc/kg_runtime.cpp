@@ -176,6 +176,9 @@ struct kg_pods {
     uint32_t n_plain = 0, n_x = 0;
     // select results
     uint64_t* d_partial = nullptr;
+    uint64_t* d_ipairs = nullptr;       // pruned integer lanes: surviving (lane, record) pairs (LaunchSelect.ipairs)
+    uint32_t* d_ipair_count = nullptr;
+    size_t ipairs_cap = 0;
     size_t partial_cap = 0;  // entries
     uint64_t* d_keys = nullptr;
     uint32_t k_last = 0, kk_last = 0;
@@ -1369,6 +1372,8 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         any_pol |= pol != KG_NUMA_NONE;
         any_bind |= (f[j] & KG_POD_CPU_BIND) != 0;
         any_rsv_req |= (f[j] & KG_POD_RSV_REQUIRED) != 0;
+        // values inside the fast domain: the pruned integer lanes may bound the pod with the fast path (POD_FASTV)
+        if (!slow[j]) f[j] |= POD_FASTV;
         // the fast block has no CPU counts and no pod-level NUMA policy: such pods take the integer path
         slow[j] |= pol != KG_NUMA_NONE || (f[j] & KG_POD_CPU_BIND) != 0;
     }
@@ -1512,6 +1517,8 @@ kg_status kg_pods_destroy(kg_pods* p) {
     hipSetDevice(p->ctx->device);
     hipStreamSynchronize(p->ctx->stream);
     if (p->ctx->side) hipStreamSynchronize(p->ctx->side);  // a plain-pod select may still read the batch there
+    for (void* b : {(void*)p->d_ipairs, (void*)p->d_ipair_count})
+        hipFree(b);
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
                     (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
                     (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
@@ -2002,6 +2009,28 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     kg_status st = ensure_partial(p, std::max<size_t>((size_t)parts * p->n * kk, 1));
     if (st != KG_OK) return st;
     a.partial = p->d_partial;
+    const uint32_t n_int = a.n_pods - a.n_fast;
+    if (n_int && !a.exact && s->weights_small && (kk == 1 || a.fused_k) && !std::getenv("KG_NO_IPRUNE")) {
+        // room for every (lane, record) pair the filter walks (lanes padded to workgroups, records to chunks);
+        // a launch that needs more than 2^26 slots keeps the unpruned kernel
+        const size_t cap = std::min<size_t>((size_t)(n_int + 255) / 256 * 256 * ((size_t)s->n + 4096), (size_t)1 << 26);
+        if (p->ipairs_cap < cap) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            hipFree(p->d_ipairs);
+            hipFree(p->d_ipair_count);
+            p->d_ipairs = nullptr;
+            p->d_ipair_count = nullptr;
+            p->ipairs_cap = 0;
+            HIP_TRY(ctx, hipMalloc(&p->d_ipairs, sizeof(uint64_t) * cap));
+            HIP_TRY(ctx, hipMalloc(&p->d_ipair_count, sizeof(uint32_t) * (cap / (256 * 64) + 1)));
+            p->ipairs_cap = cap;
+        }
+        a.ipairs = p->d_ipairs;
+        a.ipair_count = p->d_ipair_count;
+        a.ipairs_cap = p->ipairs_cap;
+        a.iseg_cap = (uint32_t)(p->ipairs_cap / (256 * 64) + 1);
+        a.iseed = 256;
+    }
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
