@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 9
+#define KG_ABI_VERSION 10
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -486,6 +486,11 @@ typedef struct kg_rsv_info {
     int64_t allocatable[KG_RSV_R], allocated[KG_RSV_R], reserved[KG_RSV_R];
     int64_t max_pods;                    /* "pods" in Allocatable, -1 = absent                       */
     int64_t allocated_pods;              /* len(AssignedPods)                                        */
+    uint32_t rid;                        /* the reservation's id on its node: the copies of one reservation
+                                          * in the views of several classes share it (a Reserve into it
+                                          * updates all of them)                                       */
+    uint32_t allocated_keys;             /* bit 0 / 1: Allocated holds a cpu / memory key (0 while nil):
+                                          * GetNonZeroRequestForResource of the unmatched correction   */
 } kg_rsv_info;
 
 /* GPU minors as one restore sees them (nodeDevice.calcFreeWithPreemptible / filter, deviceshare/
@@ -566,7 +571,13 @@ kg_status kg_result_status(kg_pods* pods, uint32_t* out_status);
  * out_reason (may be NULL): per pod, the OR of the KG_ST_* filter status bits over every node of the
  * snapshot as it stood in that pod's cycle (0 when every node passed) — the per-plugin reasons the
  * caller turns into the FitError diagnosis of an unschedulable pod (load_aware.go:48-51,
- * nodenumaresource/plugin.go:54-63). */
+ * nodenumaresource/plugin.go:54-63).
+ * With reservation views (KG_PLUGIN_RSV) each placement runs Reservation.Reserve on the device
+ * (reservation/plugin.go:1295-1408): the pod joins its nominated reservation (Allocated += Mask(requests,
+ * ResourceNames), one more assigned pod, every copy of it sharing kg_rsv_info.rid) and the node's views change as the
+ * next cycle's restore would give them (transformer.go:740-935); the Reservation score (nominated reservation's
+ * score, reservation order) is normalised per pod like in kg_eval_select. KG_UNSUPPORTED while a reservation holds
+ * GPUs (its DeviceShare restore tables follow the reserve pods' allocations). */
 kg_status kg_replay(kg_snap* snap, kg_pods* pods, int32_t* out_node, int64_t* out_total, uint32_t* out_reason);
 /* Reserve/Unreserve of pod `pod` (batch index) on local node `node`. KG_RESERVE_FAILED: the NodeNUMAResource
  * Reserve fails on that node (BestEffort allocation), nothing applied. */
@@ -583,7 +594,10 @@ kg_status kg_forget_numa(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t no
                          const int64_t* zone_amounts);
 /* Reserve with every enabled plugin's state (NodeInfo, LoadAware, NUMA zone, DeviceShare minors via
  * defaultAllocateDevices order, ElasticQuota used); returns the NUMA zone and the GPU minor bitmask
- * the Unreserve needs (deviceshare/plugin.go:507-569, elasticquota/plugin.go:622-636). */
+ * the Unreserve needs (deviceshare/plugin.go:507-569, elasticquota/plugin.go:622-636). With reservation views
+ * and no GPU-holding reservation it also runs Reservation.Reserve on the node's views (as kg_replay does); the
+ * host copies are read back before the next kg_snapshot_update_views. kg_forget_ext cannot name the reservation:
+ * the node's views turn stale until the caller re-uploads them (kg_snapshot_update_views). */
 kg_status kg_assume_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t* out_zone,
                         uint32_t* out_minors);
 kg_status kg_forget_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, int32_t numa_zone,

@@ -11,7 +11,7 @@ from typing import Dict
 
 import numpy as np
 
-KG_ABI_VERSION = 9
+KG_ABI_VERSION = 10
 KG_LA_R = 2
 KG_NSCALAR = 2
 KG_MAX_ZONES = 4
@@ -264,7 +264,8 @@ class KgRsvView(C.Structure):
 class KgRsvInfo(C.Structure):
     _fields_ = [("policy", C.c_uint32), ("names", C.c_uint32), ("allocate_once", C.c_uint32), ("dev", C.c_int32),
                 ("order", C.c_int64), ("allocatable", C.c_int64 * KG_RSV_R), ("allocated", C.c_int64 * KG_RSV_R),
-                ("reserved", C.c_int64 * KG_RSV_R), ("max_pods", C.c_int64), ("allocated_pods", C.c_int64)]
+                ("reserved", C.c_int64 * KG_RSV_R), ("max_pods", C.c_int64), ("allocated_pods", C.c_int64),
+                ("rid", C.c_uint32), ("allocated_keys", C.c_uint32)]
 
 
 class KgRsvDev(C.Structure):

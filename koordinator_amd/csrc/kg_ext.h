@@ -1196,6 +1196,7 @@ struct PairX {
     uint32_t status;
     int32_t zone;
     int64_t s_nrf, s_la, s_numa, s_dev, s_rsv, order;
+    int32_t nom;  // the nominated reservation (index into e.infos), -1 = none
 };
 
 // SCORE = false (statistics pass): status, raw DeviceShare score and the nominated reservation only;
@@ -1210,6 +1211,7 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     PairX o;
     o.status = 0;
     o.zone = -1;
+    o.nom = -1;
     o.s_nrf = o.s_la = o.s_numa = o.s_dev = o.s_rsv = o.order = 0;
     if (qst) {  // ElasticQuota PreFilter rejected the pod: no node is evaluated
         o.status = qst;
@@ -1271,12 +1273,88 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     o.s_dev = dev_raw;
     int nom = -1;
     if (v) o.s_rsv = rsv_nominate_score(q, n, *v, e.infos, o.order, c.rsv_ign, nom);
+    if (v && nom >= 0) o.nom = (int32_t)(v->first + (uint32_t)nom);
     if (dev_view || dev_done)
         // Score (scoring.go:45-104): with a nominated reservation, its table, or 0 when it reserves no GPU
         // (scoreWithNominatedReservation, reservation.go:492-520); without one, the view's base table; off views
         // the node's devices; under the stored NUMA affinity
         o.s_dev = gpu_score_site(c, e, n, zr, d, v, x, dev_done ? dev_mask : 0u, nom);
     return o;
+}
+
+// ---- Reservation.Reserve (reservation/plugin.go:1295-1408) -------------------------------------------------------
+// The pod (already in the node's NodeInfo: apply_assume) joins its nominated reservation (index nom into e.infos, -1 =
+// none): AddAssignedPod adds m = Mask(requests, ResourceNames) to the reservation's Allocated
+// (reservation_info.go:490-500), and the next cycle's restore (transformer.go:740-935) sees it: the record (the view
+// of pods matching nothing) and the views where the reservation is not matched give back m (its unmatched correction
+// grows) and the change of its NonZeroRequested correction (present keys count their value, a missing key the
+// 100m / 200Mi default); the views where it is matched keep the pod and count m in rAllocated; every view of the node
+// counts one more pod. Oracle: kg_oracle.c rsv_reserve. Called by one lane; the node's views are its own.
+__device__ __forceinline__ void rsv_nonzero_dev(const int64_t* a, uint32_t keys, int64_t& c0, int64_t& c1) {
+    c0 = (keys & 1u) ? a[0] : 100;
+    c1 = (keys & 2u) ? a[1] : 200ll * 1024 * 1024;
+}
+
+__device__ __forceinline__ void rsv_reserve_dev(const ExtDev& e, int64_t* n, ZoneRec* zr, uint32_t rec, const PodV& p,
+                                                int32_t nom) {
+    const int64_t preq[RSV_R] = {p.req_cpu, p.req_mem, p.req_eph, p.sc0, p.sc1};
+    int64_t m[RSV_R] = {0, 0, 0, 0, 0};
+    int64_t d0 = 0, d1 = 0;
+    uint32_t rid = 0xFFFFFFFFu, keys1 = 0;
+    RsvInfo* infos = const_cast<RsvInfo*>(e.infos);
+    RsvView* views = const_cast<RsvView*>(e.views);
+    if (nom >= 0) {
+        const RsvInfo& r = infos[nom];
+        rid = r.rid;
+#pragma unroll
+        for (int k = 0; k < RSV_R; k++) m[k] = ((r.names >> k) & 1u) ? preq[k] : 0;
+        const uint32_t keys_m = (((p.flags & KG_POD_HAS_CPU) && (r.names & 1u)) ? 1u : 0u) |
+                                (((p.flags & KG_POD_HAS_MEM) && (r.names & 2u)) ? 2u : 0u);
+        int64_t a1[RSV_R], c00 = 0, c01 = 0, c10, c11;
+        if (r.allocated_pods > 0) rsv_nonzero_dev(r.allocated, r.allocated_keys, c00, c01);
+#pragma unroll
+        for (int k = 0; k < RSV_R; k++) a1[k] = r.allocated[k] + m[k];
+        keys1 = r.allocated_keys | keys_m;
+        rsv_nonzero_dev(a1, keys1, c10, c11);
+        d0 = c10 - c00;
+        d1 = c11 - c01;
+        n[N_REQ_CPU] -= m[0];
+        n[N_REQ_MEM] -= m[1];
+        n[N_REQ_EPH] -= m[2];
+        n[N_SC_REQ0] -= m[3];
+        n[N_SC_REQ1] -= m[4];
+        n[N_NZ_CPU] -= d0;
+        n[N_NZ_MEM] -= d1;
+        derive_node(*reinterpret_cast<NodeRec*>(n), *zr);
+    }
+    const uint64_t mask = (uint64_t)n[N_RSV_CLASSES];
+    for (uint64_t l = mask; l; l &= l - 1ull) {
+        const int32_t cls = (int32_t)(__ffsll((unsigned long long)l) - 1);
+        const RsvView* cv = find_view(e, cls, rec);
+        if (!cv) continue;
+        RsvView& v = views[cv - e.views];
+        bool matched = false;
+        for (uint32_t t = v.first; t < v.first + v.count && rid != 0xFFFFFFFFu; t++) matched = matched || infos[t].rid == rid;
+#pragma unroll
+        for (int k = 0; k < RSV_R; k++) {
+            const int64_t d = preq[k] - (matched ? 0 : m[k]);
+            v.req[k] += d;
+            v.pod_requested[k] += d;
+            if (matched) v.r_allocated[k] += m[k];
+        }
+        v.nz_cpu += p.nz_cpu - (matched ? 0 : d0);
+        v.nz_mem += p.nz_mem - (matched ? 0 : d1);
+        v.num_pods += 1;
+        if (!matched) continue;
+        for (uint32_t t = v.first; t < v.first + v.count; t++) {
+            RsvInfo& r = infos[t];
+            if (r.rid != rid) continue;
+#pragma unroll
+            for (int k = 0; k < RSV_R; k++) r.allocated[k] += m[k];
+            r.allocated_pods += 1;
+            r.allocated_keys = keys1;
+        }
+    }
 }
 
 // per-pod NormalizeScore inputs: max DeviceShare raw score, max nominated Reservation score, and the

@@ -756,7 +756,9 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
                                                    const uint32_t* __restrict__ step_base, uint32_t step_off,
                                                    uint64_t* __restrict__ winners, uint32_t* __restrict__ minors,
                                                    uint64_t* __restrict__ buckets, int8_t* __restrict__ zsel,
-                                                   uint32_t* __restrict__ reason, const uint32_t* __restrict__ pos) {
+                                                   uint32_t* __restrict__ reason, const uint32_t* __restrict__ pos,
+                                                   int32_t* __restrict__ nsel, RsvStep* __restrict__ rs,
+                                                   uint64_t* __restrict__ rlist) {
     const uint32_t step = (step_base ? *step_base : 0u) + step_off;
     if (step > n_pods) return;  // uniform
     const uint32_t lane = threadIdx.x;
@@ -764,9 +766,12 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
     const bool live = i < n_nodes;
     const bool has_next = step < n_pods;
     // winner of the previous step from its score buckets: M = highest DeviceShare raw score among the
-    // feasible nodes; key = (base + w_dev * 100 s / M) << 32 | index
+    // feasible nodes; key = (base + w_dev * 100 s / M) << 32 | index. With reservation views the Reservation
+    // score term joins: k_ext_replay_pick combined both into rs[(step - 1) % 3].win
     uint64_t prev = 0;
-    if (step > 0) {
+    if (rs) {
+        if (step > 0) prev = rs[(step - 1) % 3].win;
+    } else if (step > 0) {
         const uint64_t* B = buckets + (size_t)((step - 1) % 3) * 128;
         const uint64_t b0 = B[lane], b1 = B[lane + 64];
         const int32_t M = wmax_i32(max(b0 ? (int32_t)lane : -1, b1 ? (int32_t)lane + 64 : -1));
@@ -796,6 +801,13 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
         Z[lane] = 0;
         Z[lane + 64] = 0;
         if (lane == 0 && step > 0) winners[step - 1] = prev;
+        if (rs && lane == 0) {  // slot of step + 1 (last read at step - 1)
+            RsvStep& z = rs[(step + 1) % 3];
+            z.win = 0;
+            z.pref = PREF_NONE;
+            z.cnt = 0;
+            z.rmax = 0;
+        }
     }
     // Reserve of pod step-1 on its winner
     if (live && prev != 0ull) {
@@ -809,6 +821,9 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
                 dev_apply(devs + i, mask, qx, 1);
                 minors[step - 1] = mask;
             }
+            // Reservation.Reserve into the nominated reservation of the winning pair (nsel, double-buffered like zsel)
+            if ((cfg.plugins & KG_PLUGIN_RSV) && nsel && nodes[i].v[N_RSV_CLASSES] != 0)
+                rsv_reserve_dev(e, nodes[i].v, zones + i, i, q, nsel[(size_t)((step - 1) & 1u) * n_nodes + i]);
         }
     }
     // ElasticQuota: buffer (step-1)&1 holds the state after pods < step-1; buffer step&1 becomes the
@@ -849,11 +864,23 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
     if (live) {
         const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, qst);
         zsel[(size_t)(step & 1u) * n_nodes + i] = (int8_t)r.zone;
+        if (nsel) nsel[(size_t)(step & 1u) * n_nodes + i] = r.nom;
         stat = r.status;
         if (!r.status) {
             const int64_t base = (int64_t)cfg.w_nrf * r.s_nrf + (int64_t)cfg.w_la * r.s_la + (int64_t)cfg.w_numa * r.s_numa;
-            kb = ((uint64_t)base << 32) | (uint64_t)(0xFFFFFFFFu - (index_base + node_index(nodes[i])));
+            const uint32_t g = index_base + node_index(nodes[i]);
+            kb = ((uint64_t)base << 32) | (uint64_t)(0xFFFFFFFFu - g);
             s = (int32_t)r.s_dev;
+            if (rs && (r.s_rsv != 0 || r.order != 0)) {
+                // a pair whose Reservation score term can be nonzero: listed for k_ext_replay_pick (its bucket
+                // entry stays, a lower bound of its total)
+                RsvStep& z = rs[step % 3];
+                const uint32_t at = atomicAdd(&z.cnt, 1u);
+                rlist[((size_t)(step % 3) * n_nodes + at) * 2] = kb;
+                rlist[((size_t)(step % 3) * n_nodes + at) * 2 + 1] = ((uint64_t)(uint32_t)r.s_dev << 32) | (uint32_t)r.s_rsv;
+                if (r.s_rsv) atomicMax(&z.rmax, (uint32_t)r.s_rsv);
+                if (r.order != 0) atomicMin((unsigned long long*)&z.pref, (unsigned long long)pref_key(r.order, g));
+            }
         }
     }
     if (reason) {  // FitError diagnosis: OR of the filter status bits over the nodes
@@ -876,6 +903,54 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
     }
 }
 
+// Winner of a replay step with reservation views (one workgroup, after k_ext_replay evaluated pod `step`):
+// NormalizeScore of DeviceShare (M from the score buckets) and of Reservation (the listed pairs' maximum, or 1000 and
+// the preferred node at 1000 when a reservation order exists, total_ext). A pair off the list has a zero Reservation
+// term, so its bucket key is its total; a listed pair's bucket key is a lower bound of its total: the maximum over
+// the buckets and the list is the step's winner.
+__global__ __launch_bounds__(256) void k_ext_replay_pick(uint32_t n_pods, uint32_t n_nodes, KCfg cfg,
+                                                        const uint32_t* __restrict__ step_base, uint32_t step_off,
+                                                        const uint64_t* __restrict__ buckets, RsvStep* __restrict__ rs,
+                                                        const uint64_t* __restrict__ rlist) {
+    const uint32_t step = (step_base ? *step_base : 0u) + step_off;
+    if (step >= n_pods) return;  // uniform
+    __shared__ int32_t s_m[4];
+    __shared__ uint64_t s_k[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t* B = buckets + (size_t)(step % 3) * 128;
+    const uint64_t b = t < 128 ? B[t] : 0ull;
+    const int32_t mw = wmax_i32(b ? (int32_t)t : -1);
+    if (lane == 0) s_m[w] = mw;
+    __syncthreads();
+    const int32_t M = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+    RsvStep& z = rs[step % 3];
+    const uint64_t pf = z.pref;
+    const int64_t rm = pf != PREF_NONE ? 1000 : (int64_t)z.rmax;
+    uint64_t best = 0;
+    if (M >= 0) {
+        if (b) best = ((uint64_t)((int64_t)(b >> 32) + (int64_t)cfg.w_dev * norm100((int64_t)t, M)) << 32) | (b & 0xFFFFFFFFull);
+        const uint32_t cnt = z.cnt;
+        const uint64_t* L = rlist + (size_t)(step % 3) * n_nodes * 2;
+        for (uint32_t k = t; k < cnt; k += 256) {
+            const uint64_t kb = L[2 * (size_t)k], sc = L[2 * (size_t)k + 1];
+            const uint32_t g = 0xFFFFFFFFu - (uint32_t)(kb & 0xFFFFFFFFull);
+            const int64_t sd = (int64_t)(uint32_t)(sc >> 32);
+            const int64_t rsv = (pf != PREF_NONE && (uint32_t)pf == g) ? 1000 : (int64_t)(uint32_t)sc;
+            const int64_t tot = (int64_t)(kb >> 32) + (int64_t)cfg.w_dev * norm100(sd, M) + (int64_t)cfg.w_rsv * norm100(rsv, rm);
+            const uint64_t key = ((uint64_t)tot << 32) | (kb & 0xFFFFFFFFull);
+            best = key > best ? key : best;
+        }
+    }
+    const uint64_t bw = wmax_u64(best);
+    if (lane == 0) s_k[w] = bw;
+    __syncthreads();
+    if (t == 0) {
+        uint64_t m = s_k[0];
+        for (int k = 1; k < 4; k++) m = s_k[k] > m ? s_k[k] : m;
+        z.win = m;
+    }
+}
+
 // Reserve (sign +1: zone and minors chosen here, or preset in out by an evaluation pass) / Unreserve (sign -1: the
 // given zone and minors). sign 0: the evaluation pass alone, which presets out for a cpuset Reserve and the Reserve.
 template <bool EXACT>
@@ -889,11 +964,13 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     int64_t* n = nodes[rec].v;
     int32_t zone = zone_in;
     uint32_t mask = minors_in;
+    int32_t nom = -1;
     if (sign >= 0 && out && zone_is_preset(out[0])) {
-        // the evaluation pass ran before the cpuset Reserve (which may have failed it): zone and minors of the
-        // pre-take state
+        // the evaluation pass ran before the cpuset Reserve (which may have failed it): zone, minors and nominated
+        // reservation of the pre-take state
         zone = zone_of_preset(out[0]);
         mask = (uint32_t)out[1];
+        nom = out[2];
         if (zone_reserve_fails(zone)) {
             if (threadIdx.x == 0) out[0] = zone, out[1] = 0;
             return;
@@ -901,6 +978,7 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     } else if (sign >= 0) {
         const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, 0u);
         zone = r.status ? -1 : r.zone;
+        nom = r.status ? -1 : r.nom;
         if (zone_reserve_fails(zone)) {  // the NodeNUMAResource Reserve fails: nothing is applied
             if (out && threadIdx.x == 0) {
                 out[0] = sign == 0 ? zone_preset(zone) : zone;
@@ -910,7 +988,7 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
         }
         mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone) : 0u;
         if (sign == 0) {  // evaluation pass only (a cpuset Reserve runs next)
-            if (out && threadIdx.x == 0) out[0] = zone_preset(zone), out[1] = (int32_t)mask;
+            if (out && threadIdx.x == 0) out[0] = zone_preset(zone), out[1] = (int32_t)mask, out[2] = nom;
             return;
         }
     }
@@ -918,6 +996,8 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     if (threadIdx.x != 0) return;
     apply_assume(cfg, n, zones + rec, q, zone, sign);
     if ((cfg.plugins & KG_PLUGIN_DEV) && devs && qx.dcount > 0) dev_apply(devs + rec, mask, qx, sign);
+    // Reservation.Reserve (sign +1 only: an Unreserve does not know the reservation; the runtime marks the views stale)
+    if (sign > 0 && (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
     if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
         quota_add(e.qstate[qx.quota], q, qx, sign);
         quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, sign);
@@ -1239,14 +1319,16 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
-                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, hipStream_t s) {
+                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, int32_t* nsel,
+                                  RsvStep* rs, uint64_t* rlist, hipStream_t s) {
     dim3 grid((n_nodes + 63) / 64), block(64);
     if (exact)
         k_ext_replay<true><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                  step_off, winners, minors, buckets, zsel, reason, pos);
+                                                  step_off, winners, minors, buckets, zsel, reason, pos, nsel, rs, rlist);
     else
         k_ext_replay<false><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                   step_off, winners, minors, buckets, zsel, reason, pos);
+                                                   step_off, winners, minors, buckets, zsel, reason, pos, nsel, rs, rlist);
+    if (rs) k_ext_replay_pick<<<1, 256, 0, s>>>(n_pods, n_nodes, cfg, step_base, step_off, buckets, rs, rlist);
     return hipGetLastError();
 }
 

@@ -52,6 +52,10 @@ struct LaunchSelect {
     uint32_t* ipair_count;  // per segment: survivors
     uint64_t ipairs_cap;    // slots of ipairs
     uint32_t iseg_cap, iseed;  // entries of ipair_count; seed records
+    // optional second stream for the pruned integer lanes (they write only their own rows of out): forked from
+    // the launch stream before the fast kernels, joined back after them
+    hipStream_t side;
+    hipEvent_t fork, join;
 };
 inline uint32_t select_fparts(const LaunchSelect& a) { return a.big_part0 + a.big_y; }
 
@@ -139,7 +143,8 @@ hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
-                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, hipStream_t s);
+                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, int32_t* nsel,
+                                  RsvStep* rs, uint64_t* rlist, hipStream_t s);
 hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                              uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
                              bool exact, int32_t* out, hipStream_t s);

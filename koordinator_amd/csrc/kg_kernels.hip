@@ -1037,6 +1037,51 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
         hipError_t e = hipMemsetAsync(a.out, 0, sizeof(uint64_t) * a.n_rows * K, s);
         if (e != hipSuccess) return e;
     }
+    const uint32_t seed_n = a.irange.n_chunks ? min(a.iseed, a.irange.end) : 0u;
+    const uint32_t i_lb = (n_int + 255) / 256;
+    const uint32_t i_chunk = max(64u, (a.irange.end - seed_n + max(1u, 2048u / max(1u, i_lb)) - 1) / max(1u, 2048u / max(1u, i_lb)));
+    const uint32_t i_fy = a.irange.n_chunks ? (a.irange.end - seed_n + i_chunk - 1) / i_chunk : 0u;
+    const bool pruned = n_int && a.irange.n_chunks && a.ipairs && !a.exact && (K == 1 || a.fused_k) &&
+                        (uint64_t)i_lb * i_fy * 256u * i_chunk <= a.ipairs_cap && (uint64_t)i_lb * i_fy <= a.iseg_cap;
+    const bool side = pruned && a.side && a.fork && a.join;
+    hipStream_t si = side ? a.side : s;
+    if (side) {
+        hipError_t e = hipEventRecord(a.fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(a.side, a.fork, 0);
+        if (e != hipSuccess) return e;
+    }
+    if (pruned) {
+        // pruned integer lanes (see k_int_seed): seed, filter into per-workgroup segments, survivors
+        const uint32_t* io = a.order ? a.order + n_fast : nullptr;
+        const uint32_t sy = max(1u, min(64u, (2048u + i_lb - 1) / i_lb));
+        const uint32_t n_segs = i_lb * i_fy;
+        if (K == 1) {
+            if (seed_n) k_int_seed<1><<<dim3(i_lb, sy), 256, 0, si>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n, a.index_base,
+                                                                     a.cfg, a.out, a.pmap, a.pstat);
+            if (i_fy) k_int_filter<1><<<dim3(i_lb, i_fy), 256, 0, si>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n,
+                                                                       a.irange.end, i_chunk, a.index_base, a.cfg, a.out,
+                                                                       a.ipairs, a.ipair_count);
+            if (n_segs) k_int_pairs<1><<<min(n_segs, 4096u), 256, 0, si>>>(a.nodes, a.zones, a.pods, io, a.ipairs, a.ipair_count,
+                                                                          n_segs, 256u * i_chunk, a.index_base, a.cfg, a.out,
+                                                                          a.pmap, a.pstat);
+        } else {
+            if (seed_n)
+                k_int_seed<KG_TOPK_MAX><<<dim3(i_lb, sy), 256, 0, si>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n, a.index_base,
+                                                                       a.cfg, a.out, a.pmap, a.pstat);
+            if (i_fy)
+                k_int_filter<KG_TOPK_MAX><<<dim3(i_lb, i_fy), 256, 0, si>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n,
+                                                                           a.irange.end, i_chunk, a.index_base, a.cfg, a.out,
+                                                                           a.ipairs, a.ipair_count);
+            if (n_segs)
+                k_int_pairs<KG_TOPK_MAX><<<min(n_segs, 4096u), 256, 0, si>>>(a.nodes, a.zones, a.pods, io, a.ipairs,
+                                                                            a.ipair_count, n_segs, 256u * i_chunk,
+                                                                            a.index_base, a.cfg, a.out, a.pmap, a.pstat);
+        }
+        if (side) {
+            hipError_t e = hipEventRecord(a.join, a.side);
+            if (e != hipSuccess) return e;
+        }
+    }
     if (n_fast) {
         const uint32_t pod_blocks = (n_fast + 255) / 256;
         for (int cls = 0; cls < 2; cls++) {
@@ -1090,39 +1135,8 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
     }
-    const uint32_t seed_n = a.irange.n_chunks ? min(a.iseed, a.irange.end) : 0u;
-    const uint32_t i_lb = (n_int + 255) / 256;
-    const uint32_t i_chunk = max(64u, (a.irange.end - seed_n + max(1u, 2048u / max(1u, i_lb)) - 1) / max(1u, 2048u / max(1u, i_lb)));
-    const uint32_t i_fy = a.irange.n_chunks ? (a.irange.end - seed_n + i_chunk - 1) / i_chunk : 0u;
-    const bool pruned = n_int && a.irange.n_chunks && a.ipairs && !a.exact && (K == 1 || a.fused_k) &&
-                        (uint64_t)i_lb * i_fy * 256u * i_chunk <= a.ipairs_cap && (uint64_t)i_lb * i_fy <= a.iseg_cap;
     if (pruned) {
-        // pruned integer lanes (see k_int_seed): seed, filter into per-workgroup segments, survivors
-        const uint32_t* io = a.order ? a.order + n_fast : nullptr;
-        const uint32_t sy = max(1u, min(64u, (2048u + i_lb - 1) / i_lb));
-        const uint32_t n_segs = i_lb * i_fy;
-        if (K == 1) {
-            if (seed_n) k_int_seed<1><<<dim3(i_lb, sy), 256, 0, s>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n, a.index_base,
-                                                                     a.cfg, a.out, a.pmap, a.pstat);
-            if (i_fy) k_int_filter<1><<<dim3(i_lb, i_fy), 256, 0, s>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n,
-                                                                       a.irange.end, i_chunk, a.index_base, a.cfg, a.out,
-                                                                       a.ipairs, a.ipair_count);
-            if (n_segs) k_int_pairs<1><<<min(n_segs, 4096u), 256, 0, s>>>(a.nodes, a.zones, a.pods, io, a.ipairs, a.ipair_count,
-                                                                          n_segs, 256u * i_chunk, a.index_base, a.cfg, a.out,
-                                                                          a.pmap, a.pstat);
-        } else {
-            if (seed_n)
-                k_int_seed<KG_TOPK_MAX><<<dim3(i_lb, sy), 256, 0, s>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n, a.index_base,
-                                                                       a.cfg, a.out, a.pmap, a.pstat);
-            if (i_fy)
-                k_int_filter<KG_TOPK_MAX><<<dim3(i_lb, i_fy), 256, 0, s>>>(a.nodes, a.zones, a.pods, n_int, io, seed_n,
-                                                                           a.irange.end, i_chunk, a.index_base, a.cfg, a.out,
-                                                                           a.ipairs, a.ipair_count);
-            if (n_segs)
-                k_int_pairs<KG_TOPK_MAX><<<min(n_segs, 4096u), 256, 0, s>>>(a.nodes, a.zones, a.pods, io, a.ipairs,
-                                                                            a.ipair_count, n_segs, 256u * i_chunk,
-                                                                            a.index_base, a.cfg, a.out, a.pmap, a.pstat);
-        }
+        // launched above (before the fast lanes)
     } else if (n_int && a.irange.n_chunks) {
         const SelectRange& r = a.irange;
         if (a.exact) {
@@ -1139,6 +1153,10 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
         }
     } else if (n_int && K > 1 && !a.fused_k) {  // no records: no feasible node (fused: out is zeroed)
         hipError_t e = launch_merge_list(a.partial, 0, 0, a.n_rows, a.order ? a.order + n_fast : nullptr, n_int, K, a.out, s);
+        if (e != hipSuccess) return e;
+    }
+    if (side) {
+        hipError_t e = hipStreamWaitEvent(s, a.join, 0);
         if (e != hipSuccess) return e;
     }
     return KG_LAUNCH_CHECK();

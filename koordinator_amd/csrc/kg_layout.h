@@ -467,6 +467,18 @@ struct alignas(16) RsvInfo {
     int64_t order;
     int64_t allocatable[RSV_R], allocated[RSV_R], reserved[RSV_R];
     int64_t max_pods, allocated_pods;
+    uint32_t rid, allocated_keys;  // kg_rsv_info.rid / .allocated_keys
+    uint64_t pad_;
+};
+
+// Replay with reservation views: per step (ring of 3) the pairs whose Reservation score term can be nonzero (a
+// nominated reservation's score or a reservation order), its maximum and the preferred-node key, and the step's
+// winner (k_ext_replay_pick).
+struct alignas(16) RsvStep {
+    uint64_t win;   // winning key of the step (0 = none)
+    uint64_t pref;  // min pref_key over the feasible pairs with an order (~0 = none)
+    uint32_t cnt;   // entries in the step's list
+    uint32_t rmax;  // max nominated-reservation score over the feasible pairs
 };
 
 // Device pointers of the config-5 tables of a snapshot (nullptr when the plugin is off).

@@ -99,6 +99,13 @@ struct kg_snap {
     std::vector<kg_rsv_dev> h_rdevs;
     std::vector<uint8_t> stale;
     uint32_t n_stale = 0;
+    // Reservation.Reserve on the device (kg_replay / kg_assume_ext) updates the views in place while no reservation
+    // holds GPUs (rsv_gpu false); views_on_device: the host copies trail the device ones (read back before use)
+    bool rsv_gpu = false, views_on_device = false;
+    std::vector<uint32_t> view_order;  // device view t -> h_views index
+    int32_t* d_nsel = nullptr;         // replay: nominated reservation of each record's pair (2 x n, like d_zsel)
+    RsvStep* d_rstep = nullptr;        // replay with views: [3] per-step Reservation normalisation and winner
+    uint64_t* d_rlist = nullptr;       // replay with views: [3][n] pairs with a Reservation score term (2 x u64)
     // Generation: bumped by every call that changes what the snapshot holds (upload, row update, Assume /
     // Forget, replay, quota / reservation upload); kg_snapshot_generation reads it.
     uint64_t gen = 0;
@@ -116,6 +123,10 @@ struct kg_snap {
         kg_cpu_alloc* cpu = nullptr;
         QuotaState* q = nullptr;
         uint32_t nq = 0;
+        RsvView* views = nullptr;  // the views and reservations Reservation.Reserve changes on the device
+        RsvInfo* infos = nullptr;
+        uint32_t nv = 0, ni = 0;
+        bool views_on_device = false;
         bool valid = false, views_stale = false;
         std::vector<uint8_t> stale;
         uint32_t n_stale = 0;
@@ -715,6 +726,7 @@ kg_status record_end(kg_ctx* ctx, hipEvent_t a, hipEvent_t b) {
 extern "C" {  // defined with the reservation entry points
 static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv, const kg_rsv_info* infos, uint32_t ni,
                               const kg_rsv_dev* devs, uint32_t nd);
+static kg_status sync_views_from_device(kg_snap* s);
 }
 
 extern "C" {
@@ -820,6 +832,7 @@ kg_status kg_snapshot_create(kg_ctx* ctx, const kg_config* cfg, uint32_t n_nodes
     if (hipMalloc(&s->d_nodes, nb) != hipSuccess || hipMalloc(&s->d_zones, zb) != hipSuccess ||
         hipMalloc(&s->d_big, sizeof(uint32_t) * ((size_t)n_nodes + 1)) != hipSuccess ||
         hipMalloc(&s->d_zsel, 2 * (size_t)std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
+        hipMalloc(&s->d_nsel, sizeof(int32_t) * 2 * (size_t)std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
         hipMalloc(&s->d_pos, sizeof(uint32_t) * std::max<uint32_t>(n_nodes, 1)) != hipSuccess ||
         hipMemset(s->d_big, 0, sizeof(uint32_t)) != hipSuccess) {
         hipFree(s->d_nodes);
@@ -1051,6 +1064,8 @@ kg_status kg_snapshot_update_rows(kg_snap* s, const uint32_t* rows, uint32_t n, 
         HIP_TRY(ctx, hipMemcpyAsync(s->d_zones, s->h_zones.data(), sizeof(ZoneRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         if (dev) HIP_TRY(ctx, hipMemcpyAsync(s->d_dev, s->h_dev.data(), sizeof(DevRec) * s->n, hipMemcpyHostToDevice, ctx->stream));
         if (s->n_views) {  // the views name records by position: re-place them (their staleness stays as it is)
+            kg_status sst = sync_views_from_device(s);
+            if (sst != KG_OK) return sst;
             const std::vector<uint8_t> keep = s->stale;
             const uint32_t keep_n = s->n_stale;
             const std::vector<kg_rsv_view> v = s->h_views;
@@ -1178,6 +1193,9 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_zones);
     hipFree(s->d_big);
     hipFree(s->d_zsel);
+    hipFree(s->d_nsel);
+    hipFree(s->d_rstep);
+    hipFree(s->d_rlist);
     hipFree(s->d_pos);
     hipFree(s->d_dev);
     hipFree(s->d_parts);
@@ -1199,6 +1217,8 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
         hipFree(k->dev);
         hipFree(k->cpu);
         hipFree(k->q);
+        hipFree(k->views);
+        hipFree(k->infos);
     }
     hipFree(s->d_cpu_topos);
     hipFree(s->d_cpu_alloc);
@@ -1302,7 +1322,7 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_pref, sizeof(uint64_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_minors, sizeof(uint32_t) * (capacity + 1)) == hipSuccess &&
               hipMalloc(&p->d_buckets, sizeof(uint64_t) * 3 * 128) == hipSuccess &&
-              hipMalloc(&p->d_aout, sizeof(int32_t) * 2) == hipSuccess &&
+              hipMalloc(&p->d_aout, sizeof(int32_t) * 4) == hipSuccess &&
               hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
               hipMalloc(&p->d_spec, sizeof(uint32_t) * (2 * (size_t)capacity + DEV_CLASSES + 1)) == hipSuccess &&
               hipMalloc(&p->d_pstat, sizeof(uint32_t) * capacity) == hipSuccess &&
@@ -1839,13 +1859,19 @@ static bool plain_side_ok(const kg_snap* s, const kg_pods* p, uint32_t kk) {
     return split && kk == 1 && p->n_plain != 0 && !unfused();
 }
 
-static kg_status launch_plain_side(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out) {
-    kg_ctx* ctx = s->ctx;
+static kg_status ensure_side(kg_ctx* ctx) {
     if (!ctx->side) {
         HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
         HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
         HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming));
     }
+    return KG_OK;
+}
+
+static kg_status launch_plain_side(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out) {
+    kg_ctx* ctx = s->ctx;
+    kg_status sst = ensure_side(ctx);
+    if (sst != KG_OK) return sst;
     uint32_t fparts = 0;
     LaunchSelect a = make_select(s, p->dev, p->d_pmap, p->n_plain, p->n_plain, p->n, kk, true, d_out, nullptr, p->d_pstat,
                                  &fparts);
@@ -2030,6 +2056,13 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
         a.ipairs_cap = p->ipairs_cap;
         a.iseg_cap = (uint32_t)(p->ipairs_cap / (256 * 64) + 1);
         a.iseed = 256;
+        if (!std::getenv("KG_NO_SIDE_STREAM")) {  // beside the fast lanes' kernels (disjoint rows of out)
+            st = ensure_side(ctx);
+            if (st != KG_OK) return st;
+            a.side = ctx->side;
+            a.fork = ctx->fork;
+            a.join = ctx->join;
+        }
     }
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
@@ -2235,6 +2268,9 @@ kg_status rb_graph(kg_snap* s, kg_pods* p, bool exact) {
     return KG_OK;
 }
 
+// the replay follows reservation views (their Reservation score term and Reservation.Reserve)
+bool rsv_replay(const kg_snap* s) { return (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views; }
+
 // config-5 replay steps (DeviceShare minors, ElasticQuota used, NormalizeScore via score buckets)
 kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     kg_ctx* ctx = s->ctx;
@@ -2254,6 +2290,9 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     put(&e.n_parts, sizeof(e.n_parts));
     put(&e.part_rng, sizeof(e.part_rng));
     put(&e.binpack, sizeof(e.binpack));
+    RsvStep* rs = rsv_replay(s) ? s->d_rstep : nullptr;
+    put(&rs, sizeof(rs));
+    put(&s->d_rlist, sizeof(s->d_rlist));
     if (p->xexec && key == p->xkey) return KG_OK;
     if (p->xexec) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -2266,7 +2305,9 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     for (uint32_t t = 0; t < REPLAY_G && err == hipSuccess; t++)
         err = launch_ext_replay_step(s->d_nodes, s->d_zones, s->d_dev, e, p->dev, p->n, s->n, s->base, s->kcfg, exact,
                                      p->d_step, t, p->d_winners, p->d_minors, p->d_buckets, s->d_zsel,
-                                     reasons ? p->d_reason : nullptr, s->d_pos, ctx->stream);
+                                     reasons ? p->d_reason : nullptr, s->d_pos,
+                                     (s->cfg.plugins & KG_PLUGIN_RSV) ? s->d_nsel : nullptr, rs, s->d_rlist,
+                                     ctx->stream);
     if (err == hipSuccess) err = launch_bump(p->d_step, REPLAY_G, ctx->stream);
     hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
     if (err == hipSuccess) err = ec;
@@ -2414,16 +2455,27 @@ kg_status kg_forget_numa(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, in
 
 static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total, uint32_t* out_reason) {
     kg_ctx* ctx = s->ctx;
-    if (s->cfg.plugins & KG_PLUGIN_RSV)
-        return fail(ctx, KG_UNSUPPORTED, "replay with Reservation views (their restore changes with every placement)");
+    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->rsv_gpu)
+        return fail(ctx, KG_UNSUPPORTED, "replay with reservations holding GPUs (their DeviceShare restore tables change "
+                                         "with every placement)");
     if (cpuset_active(s, p)) return fail(ctx, KG_UNSUPPORTED, "config-5 replay with cpuset-binding pods");
     kg_status st = check_ext(s);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint32_t n = p->n;
     const bool exact = force_exact();
+    if (rsv_replay(s) && !s->d_rstep) {
+        HIP_TRY(ctx, hipMalloc(&s->d_rstep, sizeof(RsvStep) * 3));
+        HIP_TRY(ctx, hipMalloc(&s->d_rlist, sizeof(uint64_t) * 2 * 3 * (size_t)std::max<uint32_t>(s->n, 1)));
+    }
     st = ext_replay_graph(s, p, exact, out_reason != nullptr);
     if (st != KG_OK) return st;
+    if (rsv_replay(s)) {
+        RsvStep z[3];
+        for (RsvStep& x : z) x.win = 0, x.pref = ~0ull, x.cnt = 0, x.rmax = 0;
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_rstep, z, sizeof(z), hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // z is on this stack
+    }
     if (out_reason) HIP_TRY(ctx, hipMemsetAsync(p->d_reason, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_minors, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
@@ -2437,6 +2489,7 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
+    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views) s->views_on_device = true;  // Reservation.Reserve ran there
     if ((s->cfg.plugins & KG_PLUGIN_QUOTA) && s->n_quotas) {
         // the final state sits in buffer n & 1; make both buffers agree again
         const size_t qb = sizeof(QuotaState) * s->n_quotas;
@@ -2476,8 +2529,11 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     st = check_ext(s);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    touch_views(s, node);
-    HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 2, ctx->stream));
+    // a Reserve follows Reservation.Reserve on the device's views (k_ext_assume, rsv_reserve_dev) unless a reservation
+    // holds GPUs; an Unreserve does not know the reservation: the node's views are stale then
+    if (sign < 0 || s->rsv_gpu || !(s->cfg.plugins & KG_PLUGIN_RSV)) touch_views(s, node);
+    else if (s->n_views && node < s->cls_mask.size() && s->cls_mask[node]) s->views_on_device = true;
+    HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 4, ctx->stream));
     if (sign > 0 && s->has_cpu) {
         // the pair evaluated before the cpuset take changes the counts it reads (zone and minors preset in d_aout)
         HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone,
@@ -2594,6 +2650,22 @@ static kg_status save_state(kg_snap* s, kg_snap::Saved& k) {
     if (s->n_quotas && s->d_qstate)
         HIP_TRY(ctx, hipMemcpyAsync(k.q, s->d_qstate, sizeof(QuotaState) * 2 * (size_t)s->n_quotas, hipMemcpyDeviceToDevice,
                                     ctx->stream));
+    const uint32_t ni = (uint32_t)s->h_infos.size();
+    if (s->n_views && (k.nv < s->n_views || k.ni < ni || !k.views)) {
+        hipFree(k.views);
+        hipFree(k.infos);
+        k.views = nullptr;
+        k.infos = nullptr;
+        HIP_TRY(ctx, hipMalloc(&k.views, sizeof(RsvView) * s->n_views));
+        HIP_TRY(ctx, hipMalloc(&k.infos, sizeof(RsvInfo) * std::max<uint32_t>(ni, 1)));
+    }
+    k.nv = s->n_views;
+    k.ni = ni;
+    if (s->n_views) {
+        HIP_TRY(ctx, hipMemcpyAsync(k.views, s->d_views, sizeof(RsvView) * s->n_views, hipMemcpyDeviceToDevice, ctx->stream));
+        if (ni) HIP_TRY(ctx, hipMemcpyAsync(k.infos, s->d_infos, sizeof(RsvInfo) * ni, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    k.views_on_device = s->views_on_device;
     k.views_stale = s->views_stale;
     k.stale = s->stale;
     k.n_stale = s->n_stale;
@@ -2612,6 +2684,11 @@ static kg_status restore_state(kg_snap* s, kg_snap::Saved& k) {
         HIP_TRY(ctx, hipMemcpyAsync(s->d_qstate, k.q, sizeof(QuotaState) * 2 * (size_t)k.nq, hipMemcpyDeviceToDevice,
                                     ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
+    if (k.nv && k.nv == s->n_views && k.views) {
+        HIP_TRY(ctx, hipMemcpyAsync(s->d_views, k.views, sizeof(RsvView) * k.nv, hipMemcpyDeviceToDevice, ctx->stream));
+        if (k.ni) HIP_TRY(ctx, hipMemcpyAsync(s->d_infos, k.infos, sizeof(RsvInfo) * k.ni, hipMemcpyDeviceToDevice, ctx->stream));
+        s->views_on_device = k.views_on_device;
+    }
     s->views_stale = k.views_stale;
     s->stale = k.stale;
     s->n_stale = k.n_stale;
@@ -2804,6 +2881,38 @@ kg_status kg_snapshot_read_quotas(kg_snap* s, int64_t* used, uint32_t* used_keys
     return KG_OK;
 }
 
+// After Reservation.Reserve ran on the device (kg_replay / kg_assume_ext), bring the host copies of the views and
+// reservations up to date (caller holds the lock)
+static kg_status sync_views_from_device(kg_snap* s) {
+    if (!s->views_on_device || !s->n_views) return KG_OK;
+    kg_ctx* ctx = s->ctx;
+    std::vector<RsvView> dv(s->n_views);
+    std::vector<RsvInfo> di(s->h_infos.size());
+    HIP_TRY(ctx, hipMemcpyAsync(dv.data(), s->d_views, sizeof(RsvView) * dv.size(), hipMemcpyDeviceToHost, ctx->stream));
+    if (!di.empty())
+        HIP_TRY(ctx, hipMemcpyAsync(di.data(), s->d_infos, sizeof(RsvInfo) * di.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t t = 0; t < s->n_views && t < s->view_order.size(); t++) {
+        kg_rsv_view& h = s->h_views[s->view_order[t]];
+        for (int k = 0; k < RSV_R; k++) {
+            h.req[k] = dv[t].req[k];
+            h.pod_requested[k] = dv[t].pod_requested[k];
+            h.r_allocated[k] = dv[t].r_allocated[k];
+        }
+        h.nz_cpu = dv[t].nz_cpu;
+        h.nz_mem = dv[t].nz_mem;
+        h.num_pods = dv[t].num_pods;
+    }
+    for (size_t t = 0; t < di.size(); t++) {
+        kg_rsv_info& h = s->h_infos[t];
+        for (int k = 0; k < RSV_R; k++) h.allocated[k] = di[t].allocated[k];
+        h.allocated_pods = di[t].allocated_pods;
+        h.allocated_keys = di[t].allocated_keys;
+    }
+    s->views_on_device = false;
+    return KG_OK;
+}
+
 // the views / reservations / GPU restore tables of the whole snapshot onto the device (caller holds the lock)
 static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv, const kg_rsv_info* infos, uint32_t ni,
                               const kg_rsv_dev* devs, uint32_t nd) {
@@ -2871,6 +2980,8 @@ static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv,
         }
         d.max_pods = x.max_pods;
         d.allocated_pods = x.allocated_pods;
+        d.rid = x.rid;
+        d.allocated_keys = x.allocated_keys;
     }
     // the node record of every GPU restore table (a table belongs to one view: its base or one of its reservations)
     std::vector<uint32_t> rrec(std::max<uint32_t>(nd, 1), 0u);
@@ -2916,6 +3027,11 @@ static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv,
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->n_views = nv;
     s->views_stale = false;
+    s->rsv_gpu = false;
+    for (uint32_t v = 0; v < nv; v++) s->rsv_gpu = s->rsv_gpu || views[v].dev_base >= 0;
+    for (uint32_t t = 0; t < ni; t++) s->rsv_gpu = s->rsv_gpu || infos[t].dev >= 0;
+    s->view_order = order;
+    s->views_on_device = false;
     s->h_views.assign(views, views + nv);
     s->h_infos.assign(infos, infos + ni);
     s->h_rdevs.assign(devs, devs + nd);
@@ -2943,6 +3059,8 @@ kg_status kg_snapshot_update_views(kg_snap* s, const uint32_t* nodes, uint32_t n
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
     if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
+    kg_status sst = sync_views_from_device(s);
+    if (sst != KG_OK) return sst;
     std::vector<uint8_t> listed(s->n, 0);
     for (uint32_t k = 0; k < n_nodes; k++) {
         if (nodes[k] >= s->n) return fail(ctx, KG_INVALID_ARG, "node %u >= %u", nodes[k], s->n);

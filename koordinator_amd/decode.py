@@ -1208,7 +1208,9 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
                                   allocate_once=int(bool(r.get("allocate_once", True))), order=int(r.get("order", 0)),
                                   allocatable=alloc, allocated=vec(r, "allocated"), reserved=vec(r, "reserved"),
                                   max_pods=int(r.get("max_pods", -1)), allocated_pods=int(r.get("allocated_pods", 0)),
-                                  dev=dev_idx.get(x, -1)))
+                                  dev=dev_idx.get(x, -1), rid=x,
+                                  allocated_keys=(int(r.get("allocated_keys", 3)) if r.get("allocated") is not None
+                                                  else 0)))
             views.append(dict(node=i, cls=c, first=first, count=len(matched), req=req, nz_cpu=nzc, nz_mem=nzm,
                               num_pods=int(out["num_pods"][i]) - len(matched), pod_requested=pod_requested,
                               r_allocated=r_alloc, dev_base=dev_base))

@@ -133,7 +133,7 @@ N_RSV_CLASSES = 8
 
 
 def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 100, rsv_frac: float = 0.05,
-             numa: str = "none", usage: str = "mixed"):
+             numa: str = "none", usage: str = "mixed", rsv_gpu: bool = True, raw: bool = False):
     """Config 5: configs 1-2's plugins plus DeviceShare (8 GPU minors per node: gpu-core
     100, gpu-memory-ratio 100, gpu-memory 192Gi; minors 40% idle, 30% fully used, 30% partially used),
     Reservation (5% of nodes hold 1-4 reservations of one of 8 owner classes, a third of them reserving
@@ -151,8 +151,11 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     their own, 5% of the GPU nodes with a GPU whose Topology.NodeID is -1): GPU pods on NUMA-policy nodes join
     DeviceShare's NUMA hints (deviceshare/topology_hint.go) to the topology manager.
 
+    rsv_gpu=False: no reservation holds GPUs (the replay follows reservation Reserves on the device only then).
+
     Returns (cfg, nodes, pods, quotas, reservations): nodes already restored to the view of pods that
-    match no reservation (decode.reservation_restore), reservations = abi.Reservations."""
+    match no reservation (decode.reservation_restore), reservations = abi.Reservations; raw=True appends the
+    true NodeInfo table and the reservation dicts the restore was computed from."""
     cfg = config5_profile()
     r = _rng(seed_config)
     t = nodes(n_nodes, seed_config, numa=True, rng=r)
@@ -195,7 +198,7 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
             # GPUs: the reserve pod holds whole idle minors; assigned pods use part of them (both counted
             # in the node's used, as nodeDevice.deviceUsed counts every allocation)
             dev_alloc = dev_allocated = None
-            if idle and r.random() < 1 / 3:
+            if idle and r.random() < 1 / 3 and rsv_gpu:
                 k = min(len(idle), int(r.integers(1, 3)))
                 ms = [idle.pop(int(r.integers(0, len(idle)))) for _ in range(k)]
                 dev_alloc = np.zeros((abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
@@ -218,6 +221,7 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
             t["nz_mem"][i] += mem + (allocated[1] if allocated else 0)
             t["num_pods"][i] += 1 + ap
     t["dev_total"], t["dev_free"], t["dev_used"] = tot, np.maximum(tot - used, 0), used
+    true_t = {k: np.array(v, copy=True) for k, v in t.items()}
     t, views, infos, devs = reservation_restore(t, resv)
     # Pods
     pr = _rng(seed_config, 1)
@@ -263,6 +267,10 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
         own = rm.random(n_pods) < 0.10
         p["numa_policy"] = np.where(own, rm.choice([abi.KG_NUMA_SINGLE_NODE, abi.KG_NUMA_RESTRICTED], n_pods),
                                     abi.KG_NUMA_NONE).astype(np.uint32)
+    if raw:
+        for k in set(t) - set(true_t):  # columns set after the restore (GPU topology) hold for the true table too
+            true_t[k] = np.array(t[k], copy=True)
+        return cfg, t, p, q, abi.Reservations(views, infos, devs), true_t, resv
     return cfg, t, p, q, abi.Reservations(views, infos, devs)
 
 

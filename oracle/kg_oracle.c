@@ -2717,6 +2717,7 @@ static int64_t normalize(int64_t s, int64_t max) { return max == 0 ? s : s * MAX
 typedef struct ext_row {
     uint32_t* st;
     int64_t *nrf, *la, *numa, *dev, *rsv, *total, *order;
+    int64_t* nom; /* the nominated reservation (index into the views' infos), -1 = none */
     int32_t* zone;
 } ext_row;
 
@@ -2727,6 +2728,7 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
     const int gpu_pod = (c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0;
     for (uint32_t i = 0; i < nn; i++) {
         o->nrf[i] = o->la[i] = o->numa[i] = o->dev[i] = o->rsv[i] = o->order[i] = 0;
+        o->nom[i] = -1;
         o->zone[i] = -1;
         o->total[i] = -1;
         if (qst) { /* PreFilter rejected the pod: no node is evaluated */
@@ -2783,6 +2785,7 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
         o->dev[i] = dev_raw;
         int nom = -1;
         if ((c->plugins & KG_PLUGIN_RSV) && v) o->rsv[i] = rsv_nominate_score(&x, &o->order[i], &nom);
+        if (nom >= 0) o->nom[i] = (int64_t)v->first + nom;
         if ((c->plugins & KG_PLUGIN_DEV) && (dev_view || gx.done))
             /* DeviceShare Score (scoring.go:45-104): the nominated reservation's table (0 when it reserves no GPU:
              * scoreWithNominatedReservation, reservation.go:492-520), else the view's base table; under the stored
@@ -2851,6 +2854,7 @@ static int ext_buf_new(ext_buf* b, uint32_t nn) {
     b->r.rsv = q + 4 * m;
     b->r.total = q + 5 * m;
     b->r.order = q + 6 * m;
+    b->r.nom = q + 7 * m;
     b->r.st = (uint32_t*)(q + 8 * m);
     b->r.zone = (int32_t*)(b->r.st + m);
     return 0;
@@ -2953,17 +2957,129 @@ int kgo_ext_shard_select(const kg_config* c, const kg_node_columns* n, uint32_t 
 /* Sequential scheduling with every Reserve applied before the next pod (DeviceShare minors,
  * ElasticQuota used, NodeInfo / LoadAware / NUMA). Reservation views are not replayed (their restore
  * changes with every placement): returns -1 when KG_PLUGIN_RSV is enabled. out_minors may be NULL. */
+/* The reservation NominateReservation picks for pod j on node i (index into e->infos, -1 = none / infeasible pair). */
+int64_t kgo_ext_pair_nominated(const kg_config* c, const kg_node_columns* n, uint32_t nn, uint32_t i,
+                               const kg_pod_columns* p, uint32_t j, const kgo_ext* e) {
+    ext_buf b;
+    if (i >= nn || ext_buf_new(&b, nn)) return -1;
+    kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    view_index vx;
+    view_index_build(&vx, e, nn);
+    ext_eval_pod(c, n, nn, p, j, e, &vx, q, &b.r);
+    const int64_t r = b.r.st[i] ? -1 : b.r.nom[i];
+    free(vx.v);
+    quota_state_free(q);
+    free(b.mem);
+    return r;
+}
+
+/* GetNonZeroRequestForResource of a reservation's Allocated for the unmatched correction
+ * (updateNodeInfoRequestedForUnmatched, transformer.go:918-935; reservation_info.go:516-529,581-605): the value of a
+ * present cpu / memory key, the default of a missing one */
+static void rsv_nonzero(const int64_t* a, uint32_t keys, int64_t* nz) {
+    nz[0] = (keys & 1u) ? a[0] : 100;
+    nz[1] = (keys & 2u) ? a[1] : 200ll * 1024 * 1024;
+}
+
+/* Reservation.Reserve of pod j on node i (reservation/plugin.go:1295-1408: assumePod into the nominated reservation,
+ * AddAssignedPod: Allocated += Mask(requests, ResourceNames), reservation_info.go:490-500) as the next cycle's
+ * restore sees it (transformer.go:740-935). The node's NodeInfo already holds the pod (apply). Every view of the node
+ * grows by the pod's requests; with a nominated reservation r the default columns and the views where r is not matched
+ * give back its new Allocated share m (r's unmatched correction grows by m, its NonZeroRequested correction changes
+ * with its keys), the views where r is matched keep the pod and account m in rAllocated; r's copies take m and the
+ * pod. nom: index into infos of r in the pod's view, -1 = none. */
+static void rsv_reserve(kgo_state* st, kg_rsv_view* views, uint32_t nv, kg_rsv_info* infos, uint32_t i,
+                        const kg_pod_columns* p, uint32_t j, int64_t nom) {
+    const int64_t preq[KG_RSV_R] = {p->req_cpu[j], p->req_mem[j], p->req_eph ? p->req_eph[j] : 0,
+                                    p->sc_req[0] ? p->sc_req[0][j] : 0, p->sc_req[1] ? p->sc_req[1][j] : 0};
+    const int64_t pnz[2] = {p->nz_cpu[j], p->nz_mem[j]};
+    int64_t m[KG_RSV_R] = {0, 0, 0, 0, 0}, dnz[2] = {0, 0};
+    uint32_t rid = UINT32_MAX, keys1 = 0;
+    if (nom >= 0) {
+        const kg_rsv_info* r = &infos[nom];
+        rid = r->rid;
+        for (int k = 0; k < KG_RSV_R; k++) m[k] = ((r->names >> k) & 1u) ? preq[k] : 0;
+        const uint32_t f = p->flags[j];
+        const uint32_t keys_m = (((f & KG_POD_HAS_CPU) && (r->names & 1u)) ? 1u : 0u) |
+                                (((f & KG_POD_HAS_MEM) && (r->names & 2u)) ? 2u : 0u);
+        int64_t c0[2] = {0, 0}, c1[2], a1[KG_RSV_R];
+        if (r->allocated_pods > 0) rsv_nonzero(r->allocated, r->allocated_keys, c0);
+        for (int k = 0; k < KG_RSV_R; k++) a1[k] = r->allocated[k] + m[k];
+        keys1 = r->allocated_keys | keys_m;
+        rsv_nonzero(a1, keys1, c1);
+        dnz[0] = c1[0] - c0[0];
+        dnz[1] = c1[1] - c0[1];
+        st->col[C_REQ_CPU][i] -= m[0];
+        st->col[C_REQ_MEM][i] -= m[1];
+        st->col[C_REQ_EPH][i] -= m[2];
+        for (int k = 0; k < KG_NSCALAR; k++) st->col[C_SC_REQ + k][i] -= m[3 + k];
+        st->col[C_NZ_CPU][i] -= dnz[0];
+        st->col[C_NZ_MEM][i] -= dnz[1];
+    }
+    for (uint32_t x = 0; x < nv; x++) {
+        kg_rsv_view* v = &views[x];
+        if (v->node != i) continue;
+        int matched = 0;
+        for (uint32_t t = v->first; t < v->first + v->count && rid != UINT32_MAX; t++) matched |= infos[t].rid == rid;
+        for (int k = 0; k < KG_RSV_R; k++) {
+            const int64_t d = preq[k] - (matched ? 0 : m[k]);
+            v->req[k] += d;
+            v->pod_requested[k] += d;
+            if (matched) v->r_allocated[k] += m[k];
+        }
+        v->nz_cpu += pnz[0] - (matched ? 0 : dnz[0]);
+        v->nz_mem += pnz[1] - (matched ? 0 : dnz[1]);
+        v->num_pods += 1;
+        for (uint32_t t = v->first; t < v->first + v->count && matched; t++) {
+            kg_rsv_info* r = &infos[t];
+            if (r->rid != rid) continue;
+            for (int k = 0; k < KG_RSV_R; k++) r->allocated[k] += m[k];
+            r->allocated_pods += 1;
+            r->allocated_keys = keys1;
+        }
+    }
+}
+
+/* The replay can follow the reservations' restore on the device only while none of them holds GPUs (their
+ * DeviceShare restore tables are derived from the reserve pods' and assigned pods' GPU allocations). */
+static int rsv_has_gpu_tables(const kgo_ext* e) {
+    if (!e) return 0;
+    for (uint32_t v = 0; v < e->n_views; v++)
+        if (e->views[v].dev_base >= 0) return 1;
+    for (uint32_t t = 0; t < e->n_infos; t++)
+        if (e->infos[t].dev >= 0) return 1;
+    return 0;
+}
+
 int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
                    const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
                    int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason) {
-    if (c->plugins & KG_PLUGIN_RSV) return -1;
+    const int rsv = (c->plugins & KG_PLUGIN_RSV) != 0;
+    if (rsv && rsv_has_gpu_tables(e)) return -1;
     kg_node_columns v;
     kgo_state_view(st, &v);
     ext_buf b;
     if (ext_buf_new(&b, st->n)) return -1;
     kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    /* mutable copies of the views and their reservations (the Reserve updates them) */
+    kgo_ext e2;
+    kg_rsv_view* mv = NULL;
+    kg_rsv_info* mi = NULL;
+    view_index vx = {NULL, 0, 0};
+    const kgo_ext* ee = e;
+    if (rsv && e) {
+        e2 = *e;
+        mv = (kg_rsv_view*)malloc(sizeof(kg_rsv_view) * (e->n_views ? e->n_views : 1));
+        mi = (kg_rsv_info*)malloc(sizeof(kg_rsv_info) * (e->n_infos ? e->n_infos : 1));
+        if (e->n_views) memcpy(mv, e->views, sizeof(kg_rsv_view) * e->n_views);
+        if (e->n_infos) memcpy(mi, e->infos, sizeof(kg_rsv_info) * e->n_infos);
+        e2.views = mv;
+        e2.infos = mi;
+        ee = &e2;
+        view_index_build(&vx, ee, st->n);
+    }
     for (uint32_t j = 0; j < np; j++) {
-        ext_eval_pod(c, &v, st->n, p, j, e, NULL, q, &b.r);
+        ext_eval_pod(c, &v, st->n, p, j, ee, rsv ? &vx : NULL, q, &b.r);
         ext_pod_finish(c, &b.r, st->n, base);
         uint64_t best = 0;
         int32_t best_zone = -1;
@@ -3006,7 +3122,11 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
             if (out_minors) out_minors[j] = mask;
         }
         quota_apply(q, p, j, 1);
+        if (rsv && mv) rsv_reserve(st, mv, ee->n_views, mi, i, p, j, b.r.nom[i]);
     }
+    free(vx.v);
+    free(mv);
+    free(mi);
     if (q) {
         if (quota_used_out) memcpy(quota_used_out, q->used, (size_t)q->n * KG_QUOTA_R * 8);
         if (quota_np_used_out) memcpy(quota_np_used_out, q->np_used, (size_t)q->n * KG_QUOTA_R * 8);

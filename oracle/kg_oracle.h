@@ -91,6 +91,8 @@ int kgo_ext_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, con
                    uint32_t n_pods, const kgo_ext* ext, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
                    int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason);
 int64_t kgo_mem_bytes_to_ratio(int64_t bytes, int64_t total);
+int64_t kgo_ext_pair_nominated(const kg_config* c, const kg_node_columns* n, uint32_t nn, uint32_t i,
+                               const kg_pod_columns* p, uint32_t j, const kgo_ext* e);
 /* Inline batch cycle of a planned job (batch/engine.go:92-294): per-pod KG_BATCH_* codes, status bits, NUMA
  * zone and GPU minors; a failed job leaves the state as it was. -1 with KG_PLUGIN_RSV. */
 int kgo_batch_schedule(const kg_config* cfg, kgo_state* st, const kg_pod_columns* pods, uint32_t n_pods,

@@ -86,6 +86,9 @@ def lib():
                                      P(KgoExt), P(C.c_int32), P(C.c_int64), P(C.c_uint32), P(C.c_int64),
                                      P(C.c_int64), P(C.c_uint32)]
         L.kgo_ext_replay.restype = C.c_int
+        L.kgo_ext_pair_nominated.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
+                                             P(abi.KgPodColumns), C.c_uint32, P(KgoExt)]
+        L.kgo_ext_pair_nominated.restype = C.c_int64
         L.kgo_batch_schedule.argtypes = [P(abi.KgConfig), C.c_void_p, P(abi.KgPodColumns), C.c_uint32, P(KgoExt),
                                          P(C.c_int32), P(C.c_uint32), P(C.c_uint32), P(C.c_int32), P(C.c_uint32),
                                          P(C.c_int64), P(C.c_int64)]
@@ -317,7 +320,7 @@ class OracleState:
         assert rc == 0
         return out_node, out_total
 
-    def ext_replay(self, pods: abi.Table, quotas=None, index_base: int = 0, reasons: bool = False):
+    def ext_replay(self, pods: abi.Table, quotas=None, index_base: int = 0, reasons: bool = False, rsv=None):
         np_ = abi.table_len(pods)
         out_node = np.zeros(np_, np.int32)
         out_total = np.zeros(np_, np.int64)
@@ -326,7 +329,7 @@ class OracleState:
         nq = len(quotas["used"]) if quotas is not None else 0
         qu = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
         qn = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
-        pc, e = abi.pod_columns(pods), make_ext(quotas, None)
+        pc, e = abi.pod_columns(pods), make_ext(quotas, rsv)
         P = C.POINTER
         rc = lib().kgo_ext_replay(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_, C.byref(e),
                                   out_node.ctypes.data_as(P(C.c_int32)), out_total.ctypes.data_as(P(C.c_int64)),
@@ -413,3 +416,10 @@ def assert_state_restored(before, after):
             assert not (before[k] & ~after[k]).any(), k
         else:
             assert np.array_equal(before[k], after[k]), k
+
+
+def ext_pair_nominated(kc, nodes, i, pods, j, quotas=None, rsv=None) -> int:
+    """kgo_ext_pair_nominated: the reservation (index into rsv's infos) pod j is nominated to on node i, -1 = none."""
+    nc, pc, e = abi.node_columns(nodes), abi.pod_columns(pods), make_ext(quotas, rsv)
+    return int(lib().kgo_ext_pair_nominated(C.byref(kc), C.byref(nc), abi.table_len(nodes), i, C.byref(pc), j,
+                                            C.byref(e)))

@@ -1,0 +1,108 @@
+"""Reservation.Reserve in the config-5 replay (reservation/plugin.go:1295-1408, frameworkext/reservation_info.go:490-500):
+a pod placed into its nominated reservation adds Mask(requests, ResourceNames) to that reservation's Allocated and
+joins its AssignedPods, and the next cycle's restore (reservation/transformer.go:740-935) sees the node through it.
+
+- Oracle self-consistency (CPU): the oracle replay, which updates the node's views and reservations in place after
+  each placement (kg_oracle.c rsv_reserve), places every pod where a step-by-step replay places it that recomputes the
+  whole restore from the true NodeInfo and the reservation bookkeeping before each pod (decode.reservation_restore,
+  the host restatement of the transformer).
+- Device parity (GPU): kg_replay with reservation views equals the oracle replay (placements, totals, reasons).
+
+The replay follows reservation Reserves while no reservation holds GPUs (their DeviceShare restore tables derive
+from the reserve pods' GPU allocations); synth.cluster5(rsv_gpu=False) builds such clusters."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from koordinator_amd import abi, decode, synth
+
+RSV_COLS = ("req_cpu", "req_mem", "req_eph", "sc_req0", "sc_req1")
+
+
+def _cluster(n_nodes=300, n_pods=80, seed=81):
+    cfg, nodes, pods, quotas, rsv, true_t, resv = synth.cluster5(n_nodes, n_pods, seed_config=seed, rsv_frac=0.5,
+                                                                 rsv_gpu=False, raw=True)
+    pods = {k: v.copy() for k, v in pods.items()}
+    # most pods match one owner class (so that many land in reservations)
+    rng = np.random.default_rng(seed)
+    pods["rsv_class"] = np.where(rng.random(n_pods) < 0.7, rng.integers(0, synth.N_RSV_CLASSES, n_pods),
+                                 -1).astype(np.int32)
+    pods["flags"] &= ~np.uint32(abi.KG_POD_RSV_REQUIRED)
+    return cfg, nodes, pods, quotas, rsv, true_t, resv
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from koordinator_amd import engine
+    c = engine.Context(0)
+    yield c
+    c.close()
+
+
+def _reserve_into(r: dict, info: dict, pods, j):
+    """AddAssignedPod on the reservation dict: Allocated += Mask(requests, names), one more pod, the Allocated keys."""
+    names = int(info["names"])
+    a = list(r["allocated"]) if r.get("allocated") is not None else [0] * abi.KG_RSV_R
+    for k, col in enumerate(RSV_COLS):
+        if (names >> k) & 1:
+            a[k] += int(pods[col][j])
+    f = int(pods["flags"][j])
+    keys_m = (1 if (f & abi.KG_POD_HAS_CPU) and (names & 1) else 0) | (2 if (f & abi.KG_POD_HAS_MEM) and (names & 2) else 0)
+    keys0 = int(r.get("allocated_keys", 3)) if r.get("allocated") is not None else 0
+    r["allocated"] = a
+    r["allocated_keys"] = keys0 | keys_m
+    r["allocated_pods"] = int(r.get("allocated_pods", 0)) + 1
+
+
+def test_oracle_replay_follows_the_restore():
+    cfg, nodes, pods, quotas, rsv, true_t, resv = _cluster()
+    kc = cfg.kg_config()
+    # the step-by-step side below follows NodeInfo and the reservations (no quota state, no GPU minors)
+    kc.plugins &= ~(abi.KG_PLUGIN_QUOTA | abi.KG_PLUGIN_DEV)
+    rnode, rtotal, _, _, _ = oracle_lib.OracleState(kc, nodes).ext_replay(pods, None, rsv=rsv)
+    T = {k: np.array(v, copy=True) for k, v in true_t.items()}
+    R = [dict(r) for r in resv]
+    n_pods = abi.table_len(pods)
+    into = 0
+    for j in range(n_pods):
+        D, views, infos, devs = decode.reservation_restore(T, R)
+        rs = abi.Reservations(views, infos, devs)
+        one = abi.take(pods, np.array([j]))
+        v = oracle_lib.ext_verify(kc, D, one, None, rs)
+        tot = np.where(v.status[0] == 0, v.total[0], -1)
+        want = int(np.argmax(tot)) if tot.max() >= 0 else -1
+        assert rnode[j] == want, (j, rnode[j], want)
+        if want < 0:
+            continue
+        assert rtotal[j] == tot[want]
+        nom = oracle_lib.ext_pair_nominated(kc, D, want, one, 0, None, rs)
+        if nom >= 0:
+            x = int(infos[nom]["rid"])
+            _reserve_into(R[x], infos[nom], pods, j)
+            into += 1
+        st = oracle_lib.OracleState(kc, T)
+        st.assume(want, one, 0)
+        T.update(st.table())
+    assert into >= 5  # pods did land in reservations
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [81, 82])
+def test_replay_with_reservation_views(ctx, seed):
+    """kg_replay of a config-5 batch with reservation views (no GPU-holding reservation): placements, totals, reasons
+    and the quota state equal the oracle replay's, which follows every Reservation.Reserve."""
+    from koordinator_amd import engine
+    cfg, nodes, pods, quotas, rsv, _, _ = _cluster(1200, 300, seed)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    snap.upload_quotas(quotas)
+    snap.upload_reservations(rsv)
+    batch = engine.PodBatch(ctx, pods)
+    node, total, why = engine.replay(snap, batch, reasons=True)
+    onode, ototal, _, qu, qn, owhy = oracle_lib.OracleState(kc, nodes).ext_replay(pods, quotas, rsv=rsv, reasons=True)
+    assert np.array_equal(node, onode)
+    assert np.array_equal(total, ototal)
+    assert np.array_equal(why, owhy)
+    used, _, npu, _ = snap.read_quotas()
+    assert np.array_equal(used, qu) and np.array_equal(npu, qn)
+    assert (node >= 0).sum() > 100
