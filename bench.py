@@ -130,7 +130,7 @@ def roofline(pmc, kernel_s, evals_per_launch, b_eval, kernel_name):
                          "note": "SURVEY §8d scan model (node row read once per eval); pod tiling reads a row "
                                  "once per 64 pods, so this is not an HBM utilisation and may exceed 8 TB/s"}
     if not pmc or not kernel_s:
-        out["note"] = ("no PMC summary for these kernel sources and this configuration (N = 1, configs 2 and 5): "
+        out["note"] = ("no PMC summary for these kernel sources and this configuration (N = 1, configs 2, 4, 5, 6): "
                        "issue / HBM fractions not available")
         return out
     valu = pmc.get("valu_insts_per_launch")
@@ -279,6 +279,55 @@ def replay_rate(ctx, cfg, with_cpu, cpu_s, config=3):
     return out
 
 
+def replay5_rate(ctx, with_cpu, cpu_s):
+    """Config 5 one pod per cycle: the config-5 cluster (100k nodes x 10k pods, every plugin) with reservations
+    that hold no GPU, so that kg_replay runs Reservation.Reserve and the ElasticQuota / DeviceShare Reserve on the
+    device between pods."""
+    import numpy as np
+
+    from koordinator_amd import abi, engine, synth
+
+    cfg, nodes, pods, quotas, rsv = synth.config5(rsv_gpu=False)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    snap.upload_quotas(quotas)
+    snap.upload_reservations(rsv)
+    small = engine.PodBatch(ctx, abi.take(pods, np.arange(256)))
+    engine.replay(snap, small)  # warm-up (graph instantiate, code load)
+    snap.upload(nodes)
+    snap.upload_quotas(quotas)
+    snap.upload_reservations(rsv)
+    batch = engine.PodBatch(ctx, pods)
+    t0 = time.perf_counter()
+    node, _ = engine.replay(snap, batch)
+    dt = time.perf_counter() - t0
+    placed = int((node >= 0).sum())
+    out = {"pods_placed_per_s": batch.n / dt, "pods": batch.n, "placed": placed, "seconds": round(dt, 4),
+           "workload": (f"config5: {snap.n // 1000}k nodes x {batch.n // 1000}k pods, one pod per cycle, Reserve of "
+                        "every plugin (NodeInfo, LoadAware, NUMA, GPU minors, ElasticQuota, Reservation) on device; "
+                        "reservations hold no GPU")}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib  # test infrastructure: the CPU baseline leg only
+
+        probe = 4
+        t0 = time.perf_counter()
+        oracle_lib.OracleState(kc, nodes).ext_replay(abi.take(pods, np.arange(probe)), quotas, rsv=rsv)
+        per = max(time.perf_counter() - t0, 1e-6) / probe
+        n = int(min(batch.n, max(probe * 2, cpu_s / 2 / per)))
+        t0 = time.perf_counter()
+        want = oracle_lib.OracleState(kc, nodes).ext_replay(abi.take(pods, np.arange(n)), quotas, rsv=rsv)[0]
+        cdt = time.perf_counter() - t0
+        assert np.array_equal(want, node[:n])  # same placements as the device replay
+        out["cpu_baseline"] = {"value": n / cdt, "unit": "pods/s", "cores": 1, "kind": "port",
+                               "sample": f"first {n} pods of the sequence in {cdt:.2f} s; oracle/kg_oracle.c "
+                                         "kgo_ext_replay, one thread"}
+    snap.close()
+    batch.close()
+    small.close()
+    return out
+
+
 def cycle_rate(ctx, snap, pods_table, steps):
     """One end-to-end PreFilter cycle as the plugin pays it: pod batch upload (host columns -> HBM), the
     select over every node, and the download of the per-pod keys."""
@@ -396,12 +445,12 @@ def main():
     value = evals / elapsed
     avg_kernel_s = (kern_ms / 1e3) / max(launches, 1) if launches else None
     # the committed PMC passes are per launch of one configuration (profiles/run_profile.sh: 2, 4 and 5)
-    pmc = load_pmc({2: "select_pmc.json", 4: "select4_pmc.json", 5: "ext_pmc.json"}[config]) \
-        if world == 1 and config in (2, 4, 5) else None
+    pmc = load_pmc({2: "select_pmc.json", 4: "select4_pmc.json", 5: "ext_pmc.json", 6: "select6_pmc.json"}[config]) \
+        if world == 1 and config in (2, 4, 5, 6) else None
     fused = k == 1 and os.environ.get("KG_SELECT_UNFUSED", "0") in ("", "0")
     base = "k_big_sel + k_select1 (fused top-1)" if fused else "k_select + k_big_sel + k_merge"
     if config == 6:
-        base += " + k_select<integer path> (LSR lanes)"
+        base += " + k_int_seed / k_int_filter / k_int_pairs (pruned LSR lanes)"
     kname = base if config != 5 else (f"config-5 step: k_dev_sum + k_rdev_codes + k_ext_stats_sp/views + k_ext_select "
                                       f"(one pass + re-run) + k_ext_select_sp + plain pods' {base} (one bracket)")
     out = {
@@ -430,6 +479,10 @@ def main():
         if config == 5:
             if not a.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline_ext(kc, nodes, pods, quotas, rsv, a.cpu_seconds)
+            if not a.no_replay:
+                snap.close()
+                batch.close()
+                out["replay"] = replay5_rate(ctx, not a.no_cpu_baseline, a.cpu_seconds)
         else:
             if not a.no_replay and config in (1, 2):
                 out["replay"] = replay_rate(ctx, cfg, not a.no_cpu_baseline, a.cpu_seconds)

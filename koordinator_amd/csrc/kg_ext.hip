@@ -1042,6 +1042,7 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
             uint32_t st;
             int32_t zone;
             uint32_t mask = 0;
+            int32_t nom = -1;
             PodX qx{};
             if constexpr (EXT) {
                 qx = load_podx(pods, j);
@@ -1051,6 +1052,7 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
                 const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, qst);
                 st = r.status;
                 zone = r.zone;
+                nom = r.nom;
                 if (!st && !zone_reserve_fails(zone) && (cfg.plugins & KG_PLUGIN_DEV) && devs) mask = dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone);
             } else {
                 const PairOut r = eval_pair<EXACT>(cfg, n, zones + rec, q);
@@ -1071,6 +1073,8 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
                     quota_add(e.qstate[qx.quota], q, qx, 1);
                     quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, 1);
                 }
+                // Reservation.Reserve on the node's views (a group's node is its lane's alone)
+                if ((cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
             }
             result[j] = KG_BATCH_ASSUMED;
             status[j] = 0;

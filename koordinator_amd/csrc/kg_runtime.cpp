@@ -2067,7 +2067,11 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
-    HIP_TRY(ctx, launch_select(a, ctx->stream));
+    const hipError_t le = launch_select(a, ctx->stream);
+    // a launch error after the fork leaves the pruned lanes' kernels unjoined: drain the side stream before anything
+    // later on ctx->stream (an upload into the pod columns, a free) can overtake them
+    if (le != hipSuccess && a.side) hipStreamSynchronize(a.side);
+    HIP_TRY(ctx, le);
     return record_end(ctx, e0, e1);
 }
 
@@ -2729,8 +2733,9 @@ kg_status kg_batch_schedule(kg_snap* s, kg_pods* p, const int32_t* plan_node, ui
     kg_ctx* ctx = s->ctx;
     if ((!plan_node || !out_result || !out_status) && p->n) return fail(ctx, KG_INVALID_ARG, "null plan / result buffer");
     std::lock_guard<std::mutex> g(ctx->mu);
-    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views)
-        return fail(ctx, KG_UNSUPPORTED, "batch schedule with Reservation views (a Reserve into a view changes its restore)");
+    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->rsv_gpu)
+        return fail(ctx, KG_UNSUPPORTED, "batch schedule with reservations holding GPUs (their DeviceShare restore tables "
+                                         "change with every placement)");
     if (cpuset_active(s, p)) return fail(ctx, KG_UNSUPPORTED, "batch schedule with cpuset-binding pods");
     if (s->ext()) {
         st = check_ext(s);
@@ -2808,6 +2813,7 @@ kg_status kg_batch_schedule(kg_snap* s, kg_pods* p, const int32_t* plan_node, ui
     } else {
         HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views) s->views_on_device = true;  // Reservation.Reserve ran there
     }
     s->bk.valid = false;
     for (uint32_t j = 0; j < n; j++) {

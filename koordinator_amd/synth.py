@@ -274,10 +274,11 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     return cfg, t, p, q, abi.Reservations(views, infos, devs)
 
 
-def config5(n_nodes: int = 100_000, n_pods: int = 10_000):
+def config5(n_nodes: int = 100_000, n_pods: int = 10_000, rsv_gpu: bool = True):
     """BASELINE config 5 as SURVEY.md §8d states it: cluster5 with per-minor GPU usage U(0, 1) and the 20%
-    SingleNUMANode nodes of configs 2-3 (GPU pods there join DeviceShare's NUMA hints to the topology manager)."""
-    return cluster5(n_nodes, n_pods, numa="single", usage="u01")
+    SingleNUMANode nodes of configs 2-3 (GPU pods there join DeviceShare's NUMA hints to the topology manager).
+    rsv_gpu=False: no reservation holds GPUs (the form kg_replay follows through Reservation.Reserve)."""
+    return cluster5(n_nodes, n_pods, numa="single", usage="u01", rsv_gpu=rsv_gpu)
 
 
 def gpu_topology5(t: abi.Table, p: abi.Table, seed_config: int = 5, any_numa: bool = False):

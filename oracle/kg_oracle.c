@@ -3145,11 +3145,13 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
  * of a group gives its later pods the same status (engine.go:188-192). If any pod failed, every Reserve is
  * undone (CleanupAssumedPods): here by restoring the state copied before the cycle. Codes are the ABI's
  * KG_BATCH_*. Groups run one after another, as lane 0 of k_batch does when ElasticQuota is on; without
- * quota the groups touch disjoint nodes, so their order changes nothing. -1 with KG_PLUGIN_RSV. */
+ * quota the groups touch disjoint nodes, so their order changes nothing. With reservation views each Reserve also
+ * runs Reservation.Reserve on the node's views (rsv_reserve); -1 while a reservation holds GPUs. */
 int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* p, uint32_t np, const kgo_ext* e,
                        const int32_t* plan_node, uint32_t* out_result, uint32_t* out_status, int32_t* out_zone,
                        uint32_t* out_minors, int64_t* quota_used_out, int64_t* quota_np_used_out) {
-    if (c->plugins & KG_PLUGIN_RSV) return -1;
+    const int rsv = (c->plugins & KG_PLUGIN_RSV) != 0 && e && e->n_views;
+    if (rsv && rsv_has_gpu_tables(e)) return -1;
     for (uint32_t j = 0; j < np; j++) {
         out_zone[j] = -1;
         out_minors[j] = 0;
@@ -3168,6 +3170,23 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
     kgo_state* saved = kgo_state_new(&v, st->n);
     ext_buf b;
     if (ext_buf_new(&b, st->n)) return -1;
+    /* mutable copies of the views and their reservations (Reservation.Reserve updates them; a cleanup drops them) */
+    kgo_ext e2;
+    kg_rsv_view* mv = NULL;
+    kg_rsv_info* mi = NULL;
+    view_index vx = {NULL, 0, 0};
+    const kgo_ext* ee = e;
+    if (rsv) {
+        e2 = *e;
+        mv = (kg_rsv_view*)malloc(sizeof(kg_rsv_view) * e->n_views);
+        mi = (kg_rsv_info*)malloc(sizeof(kg_rsv_info) * (e->n_infos ? e->n_infos : 1));
+        memcpy(mv, e->views, sizeof(kg_rsv_view) * e->n_views);
+        if (e->n_infos) memcpy(mi, e->infos, sizeof(kg_rsv_info) * e->n_infos);
+        e2.views = mv;
+        e2.infos = mi;
+        ee = &e2;
+        view_index_build(&vx, ee, st->n);
+    }
     uint8_t* done = (uint8_t*)calloc(np ? np : 1, 1);
     int failed_any = 0;
     for (uint32_t j0 = 0; j0 < np; j0++) {
@@ -3186,7 +3205,7 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
             uint32_t s;
             int32_t zone;
             if (ext) {
-                ext_eval_pod(c, &v, st->n, p, j, e, NULL, q, &b.r);
+                ext_eval_pod(c, &v, st->n, p, j, ee, rsv ? &vx : NULL, q, &b.r);
                 s = b.r.st[node];
                 zone = b.r.zone[node];
             } else {
@@ -3223,6 +3242,7 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                 out_minors[j] = mask;
             }
             quota_apply(q, p, j, 1);
+            if (rsv) rsv_reserve(st, mv, ee->n_views, mi, (uint32_t)node, p, j, b.r.nom[node]);
             out_result[j] = KG_BATCH_ASSUMED;
             out_zone[j] = zone;
         }
@@ -3247,6 +3267,9 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
     }
     quota_state_free(q);
     kgo_state_free(saved);
+    free(vx.v);
+    free(mv);
+    free(mi);
     free(done);
     free(b.mem);
     return 0;

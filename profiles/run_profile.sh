@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 collection for the select kernels (run on the GPU box from the repo root):
-#   bash profiles/run_profile.sh <tag> [config]      (config 2 default; 4 = 100k nodes top-3; 5 = the config-5 plugin set)
+#   bash profiles/run_profile.sh <tag> [config]      (config 2 default; 4 = 100k nodes top-3; 5 = the config-5 plugin set; 6 = mixed)
 # 1) kernel trace + stats of a bench run (per-kernel average durations);
 # 2) separate PMC passes (gfx950 slot limits): FETCH_SIZE, WRITE_SIZE, SQ instruction mix / cycles;
 # 3) tools/pmc_summary.py -> gpurun_out/prof_<tag>/summary.json (copy it to profiles/ to commit).
@@ -32,6 +32,9 @@ if [ "$CFG" = "4" ]; then  # top-3: per-chunk partials merged by k_merge_list in
 elif [ "$CFG" = "5" ]; then
     python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_ext_select" "k_ext_stats" "k_ext_fix_rows" "k_dev_sum" \
         "k_rdev_codes" "k_ext_gate" "k_special_scan" "k_scatter_keys" "k_select<" "k_select1<" "k_big_sel" || exit $?
+elif [ "$CFG" = "6" ]; then  # mixed cluster: fast lanes, pruned F_BIG pairs, pruned integer (LSR) lanes
+    python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_select<" "k_select1<" "k_big_init" "k_big_sel" \
+        "k_int_seed" "k_int_filter" "k_int_pairs" "k_merge" || exit $?
 else
     python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_select<" "k_select1<" "k_big_init" || exit $?
 fi

@@ -340,7 +340,7 @@ class OracleState:
             return out_node, out_total, out_minors, qu[:nq], qn[:nq], out_reason
         return out_node, out_total, out_minors, qu[:nq], qn[:nq]
 
-    def batch_schedule(self, pods: abi.Table, plan_node, quotas=None):
+    def batch_schedule(self, pods: abi.Table, plan_node, quotas=None, rsv=None):
         """kgo_batch_schedule: (result codes, status bits, zone, minors, quota used, quota np_used)."""
         np_ = abi.table_len(pods)
         plan = np.ascontiguousarray(plan_node, np.int32)
@@ -351,7 +351,7 @@ class OracleState:
         nq = len(quotas["used"]) if quotas is not None else 0
         qu = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
         qn = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
-        pc, e = abi.pod_columns(pods), make_ext(quotas, None)
+        pc, e = abi.pod_columns(pods), make_ext(quotas, rsv)
         P = C.POINTER
         rc = lib().kgo_batch_schedule(C.byref(self.cfg), self.h, C.byref(pc), np_, C.byref(e),
                                       plan.ctypes.data_as(P(C.c_int32)), res.ctypes.data_as(P(C.c_uint32)),
