@@ -234,6 +234,30 @@ __device__ __forceinline__ void scope_merge(ScopeRes& best, const ScopeRes& r, b
     if (shared && best.depth == r.depth && best.cne == r.cne && best.score < r.score) best = r;
 }
 
+// The node's GPU tree from dev_topo: per NUMA rank and per PCIe rank the minor mask, 8 bits per rank (ranks and
+// minors < 8), and per PCIe rank its NUMA rank (3 bits each). Packed in registers: indexed local arrays would live in
+// scratch memory.
+struct GpuTree {
+    uint64_t numa, pcie;
+    uint32_t pcie_numa;
+};
+
+__device__ __forceinline__ GpuTree gpu_tree(int32_t D, uint64_t topo) {
+    GpuTree t{0ull, 0ull, 0u};
+    for (int32_t m = 0; m < D; m++) {
+        const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
+        if (b == KG_GPU_NO_SCOPE) continue;
+        const uint32_t q = (b >> 4) & 7u, r = b & 7u;
+        t.numa |= (uint64_t)(1u << m) << (8u * q);
+        t.pcie |= (uint64_t)(1u << m) << (8u * r);
+        t.pcie_numa = (t.pcie_numa & ~(7u << (3u * r))) | (q << (3u * r));
+    }
+    return t;
+}
+__device__ __forceinline__ uint32_t tree_numa(const GpuTree& t, uint32_t q) { return (uint32_t)(t.numa >> (8u * q)) & 0xFFu; }
+__device__ __forceinline__ uint32_t tree_pcie(const GpuTree& t, uint32_t r) { return (uint32_t)(t.pcie >> (8u * r)) & 0xFFu; }
+__device__ __forceinline__ uint32_t tree_pcie_numa(const GpuTree& t, uint32_t r) { return (t.pcie_numa >> (3u * r)) & 7u; }
+
 // allocateFromScope over the node -> NUMA node -> PCIe tree of dev_topo (GetGPUTopologyScope,
 // allocator_gpu_helper.go:201-262: NUMA scopes in NUMA id order, PCIe scopes in PCIe id order). `level`:
 // DeviceTopologyScopeLevel of the required scope (0 = none). Depth: node 1, NUMA 2, PCIe 3.
@@ -243,30 +267,20 @@ __device__ __forceinline__ uint32_t gpu_scope(const KCfg& c, const DevRec* __res
     const uint32_t root = D >= 32 ? ~0u : (1u << D) - 1u;
     if ((uint32_t)__popc(root) < N) return 0u;
     // scope minor sets from the per-minor ranks (dense: NUMA ranks 0..nq-1, PCIe ranks 0..np-1, both <= D)
-    uint32_t numa[DEV_MINORS], pcie[DEV_MINORS], pcie_numa[DEV_MINORS];
-#pragma unroll
-    for (int k = 0; k < DEV_MINORS; k++) numa[k] = pcie[k] = pcie_numa[k] = 0u;
-    for (int32_t m = 0; m < D; m++) {
-        const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
-        if (b == KG_GPU_NO_SCOPE) continue;
-        const uint32_t q = (b >> 4) & 7u, r = b & 7u;
-        numa[q] |= 1u << m;
-        pcie[r] |= 1u << m;
-        pcie_numa[r] = q;
-    }
+    const GpuTree tr = gpu_tree(D, topo);
     const int32_t cne1 = (root & g.used) ? 1 : 0;
     ScopeRes best{0u, 0, 0, -1};
     for (uint32_t q = 0; q < (uint32_t)DEV_MINORS; q++) {  // NUMA scopes in rank order
-        const uint32_t qm = numa[q];
+        const uint32_t qm = tree_numa(tr, q);
         if (!qm) break;
         if ((uint32_t)__popc(qm) < N) continue;
         const int32_t cne2 = cne1 + ((qm & g.used) ? 1 : 0);
         ScopeRes bq{0u, 0, 0, -1};
         if (level <= 3) {  // a PCIe scope has no children; below the required level it yields nothing
             for (uint32_t r = 0; r < (uint32_t)DEV_MINORS; r++) {  // PCIe scopes of this NUMA node in rank order
-                const uint32_t rm = pcie[r];
+                const uint32_t rm = tree_pcie(tr, r);
                 if (!rm) break;
-                if (pcie_numa[r] != q || (uint32_t)__popc(rm) < N) continue;
+                if (tree_pcie_numa(tr, r) != q || (uint32_t)__popc(rm) < N) continue;
                 scope_merge(bq, scope_take(c, d, x, rm, g, shared, 3, cne2 + ((rm & g.used) ? 1 : 0)), shared);
             }
         }
@@ -285,26 +299,16 @@ __device__ __forceinline__ bool gpu_scope_fits(int32_t D, uint64_t topo, uint32_
     const uint32_t root = D >= 32 ? ~0u : (1u << D) - 1u;
     if ((uint32_t)__popc(root) < N) return false;
     if (level <= 1) return (uint32_t)__popc(root & g.sat) >= N;
-    uint32_t numa[DEV_MINORS], pcie[DEV_MINORS], pcie_numa[DEV_MINORS];
-#pragma unroll
-    for (int k = 0; k < DEV_MINORS; k++) numa[k] = pcie[k] = pcie_numa[k] = 0u;
-    for (int32_t m = 0; m < D; m++) {
-        const uint32_t b = (uint32_t)(topo >> (8 * m)) & 0xFFu;
-        if (b == KG_GPU_NO_SCOPE) continue;
-        const uint32_t q = (b >> 4) & 7u, r = b & 7u;
-        numa[q] |= 1u << m;
-        pcie[r] |= 1u << m;
-        pcie_numa[r] = q;
-    }
+    const GpuTree tr = gpu_tree(D, topo);
     for (uint32_t q = 0; q < (uint32_t)DEV_MINORS; q++) {
-        const uint32_t qm = numa[q];
+        const uint32_t qm = tree_numa(tr, q);
         if (!qm) break;
         if ((uint32_t)__popc(qm) < N) continue;
         if (level <= 3)
             for (uint32_t r = 0; r < (uint32_t)DEV_MINORS; r++) {
-                const uint32_t rm = pcie[r];
+                const uint32_t rm = tree_pcie(tr, r);
                 if (!rm) break;
-                if (pcie_numa[r] == q && (uint32_t)__popc(rm) >= N && (uint32_t)__popc(rm & g.sat) >= N) return true;
+                if (tree_pcie_numa(tr, r) == q && (uint32_t)__popc(rm) >= N && (uint32_t)__popc(rm & g.sat) >= N) return true;
             }
         if (level <= 2 && (uint32_t)__popc(qm & g.sat) >= N) return true;
     }
@@ -323,9 +327,14 @@ __device__ __forceinline__ GpuAlloc dev_default(const KCfg& c, const DevRec* __r
     }
     if (fit < x.dcount) return {KG_DEV_CODE_INSUFFICIENT, 0u};
     if (!want_mask) return {0u, 0u};
+    // the minors in (score desc, minor asc) order (the reference's stable sort) by repeated selection of the best
+    // remaining one; the loops over DEV_MINORS unroll, so sc[] and the fitting set stay in registers
     int64_t sc[DEV_MINORS];
-    int ord[DEV_MINORS];
-    for (int32_t m = 0; m < D; m++) {
+    uint32_t fits = 0;
+#pragma unroll
+    for (int m = 0; m < DEV_MINORS; m++) {
+        sc[m] = 0;
+        if (m >= D) continue;
         int64_t t[DEV_R], f[DEV_R];
 #pragma unroll
         for (int r = 0; r < DEV_R; r++) {
@@ -333,24 +342,23 @@ __device__ __forceinline__ GpuAlloc dev_default(const KCfg& c, const DevRec* __r
             f[r] = d->free_[r][m];
         }
         sc[m] = dev_least(c, t, f, x.dreq);
-        ord[m] = m;
+        fits |= (((allowed >> m) & 1u) && dev_minor_fits(f, x)) ? 1u << m : 0u;
     }
-    for (int32_t a = 1; a < D; a++) {
-        const int v = ord[a];
-        int32_t b = a;
-        while (b > 0 && sc[ord[b - 1]] < sc[v]) {
-            ord[b] = ord[b - 1];
-            b--;
+    uint32_t left = D >= 32 ? ~0u : (1u << D) - 1u, mask = 0, got = 0;
+    while (left && got < x.dcount) {
+        int32_t bm = -1;
+        int64_t bs = 0;
+#pragma unroll
+        for (int m = 0; m < DEV_MINORS; m++) {
+            const bool take = ((left >> m) & 1u) && (bm < 0 || sc[m] > bs);
+            bs = take ? sc[m] : bs;
+            bm = take ? m : bm;
         }
-        ord[b] = v;
-    }
-    uint32_t mask = 0, got = 0;
-    for (int32_t t = 0; t < D && got < x.dcount; t++) {
-        const int m = ord[t];
-        const int64_t fr[DEV_R] = {d->free_[0][m], d->free_[1][m], d->free_[2][m]};
-        if (!((allowed >> m) & 1u) || !dev_minor_fits(fr, x)) continue;
-        mask |= 1u << m;
-        got++;
+        left &= ~(1u << bm);
+        if ((fits >> bm) & 1u) {
+            mask |= 1u << bm;
+            got++;
+        }
     }
     return {0u, mask};
 }

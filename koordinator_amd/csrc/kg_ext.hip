@@ -353,15 +353,24 @@ template <typename Fn>
 __device__ __forceinline__ void for_general_records(const NodeRec* __restrict__ nodes, const ExtDev& e,
                                                     const uint32_t* __restrict__ special, uint32_t n0, uint32_t chunk,
                                                     int32_t cls, bool c1_split, Fn&& fn) {
+    // one iteration space (the special list, then the class's views) and one call site of fn: with two, the
+    // compiler outlined the evaluation lambda (an out-of-line call, its state through scratch memory)
     const uint32_t nsp = special[0], step = gridDim.y * chunk;
-    for (uint32_t x = blockIdx.y * chunk; x < nsp; x += step)
-        for (uint32_t y = x, ye = min(x + chunk, nsp); y < ye; y++) fn(special[1 + y]);
-    if (cls < 0 || cls >= RSV_MAX_CLASSES || !e.cls_begin) return;
-    const uint32_t cb = e.cls_begin[cls], ce = e.cls_begin[cls + 1];
-    for (uint32_t x = cb + blockIdx.y * chunk; x < ce; x += step)
-        for (uint32_t v = x, ve = min(x + chunk, ce); v < ve; v++) {
-            const uint32_t rec = e.views[v].rec;
-            if (((uint32_t)nodes[rec].v[N_FLAGS] & F_BIG) || (rec >= n0 && !c1_split)) continue;  // special: done above
+    uint32_t cb = 0, ce = 0;
+    if (cls >= 0 && cls < RSV_MAX_CLASSES && e.cls_begin) {
+        cb = e.cls_begin[cls];
+        ce = e.cls_begin[cls + 1];
+    }
+    const uint32_t total = nsp + (ce - cb);
+    for (uint32_t x = blockIdx.y * chunk; x < total; x += step)
+        for (uint32_t u = x, ue = min(x + chunk, total); u < ue; u++) {
+            uint32_t rec;
+            if (u < nsp) {
+                rec = special[1 + u];
+            } else {
+                rec = e.views[cb + (u - nsp)].rec;
+                if (((uint32_t)nodes[rec].v[N_FLAGS] & F_BIG) || (rec >= n0 && !c1_split)) continue;  // special list
+            }
             fn(rec);
         }
 }

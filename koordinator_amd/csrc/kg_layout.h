@@ -172,7 +172,7 @@ constexpr uint32_t CPU_META_BIND_SHIFT = 8, CPU_META_STRATEGY_SHIFT = 10, CPU_ME
 
 // The Filter's view of a node's allocated CPUs (ZoneRec.cpu_free / cpu_free_full / cpu_free_cores /
 // cpu_allocated), recomputed on the host at upload and on the device after a cpuset Reserve.
-KG_HD inline void cpu_counts(const kg_cpu_topo& t, const kg_cpu_alloc* a, int max_ref, ZoneRec& z) {
+KG_HD inline __attribute__((always_inline)) void cpu_counts(const kg_cpu_topo& t, const kg_cpu_alloc* a, int max_ref, ZoneRec& z) {
     int free_core[KG_MAX_CPUS], core_numa[KG_MAX_CPUS];
     for (int k = 0; k < t.n_cores; k++) free_core[k] = 0, core_numa[k] = 0;
     int fr = 0, al = 0;

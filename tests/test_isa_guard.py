@@ -99,7 +99,9 @@ def test_reproducer_shows_misaligned_sload(tmp_path):
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"), reason="llvm-objdump not in this image")
 def test_library_has_no_misaligned_sloads(tmp_path):
-    """The built engine (every gfx950 code object in libkoordgpu.so) carries no scalar load of the miscompiled form."""
+    """The built engine (every gfx950 code object in libkoordgpu.so) carries no scalar load of the miscompiled form,
+    and no out-of-line device call (s_swappc_b64): round 4 found the config-5 view kernels calling their evaluation
+    lambda out of line (its state through scratch memory) when it had two call sites."""
     root = os.path.dirname(CSRC.rstrip("/").rsplit("/", 1)[0])
     lib = os.path.join(root, "koordinator_amd", "libkoordgpu.so")
     if not os.path.exists(lib):
@@ -109,7 +111,17 @@ def test_library_has_no_misaligned_sloads(tmp_path):
     from code_objects import extract
     files = extract(lib, str(tmp_path))
     assert files
+    import re
     for f in files:
         with open(f) as fh:
-            bad = _misaligned_sloads(fh)
+            lines = fh.read().splitlines()
+        bad = _misaligned_sloads(lines)
         assert not bad, (f, bad[:4])
+        calls, cur = [], None
+        for line in lines:
+            m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+            if m:
+                cur = m.group(1)
+            elif "s_swappc_b64" in line:
+                calls.append(cur)
+        assert not calls, (f, sorted(set(calls))[:4])
