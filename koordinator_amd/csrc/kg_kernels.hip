@@ -26,6 +26,9 @@ __device__ __forceinline__ void topk_insert(uint64_t (&top)[K], uint64_t key) {
     if constexpr (K == 1) {
         top[0] = key > top[0] ? key : top[0];
     } else {
+        // a wave-uniform skip when no lane's key enters its top-K (most records once the lists have filled): the
+        // cascade below leaves top unchanged for a key not above top[K-1], so the lanes that do not insert may run it
+        if (!__any(key > top[K - 1])) return;
 #pragma unroll
         for (int t = 0; t < K; t++) {
             const uint64_t cur = top[t];
