@@ -1046,7 +1046,10 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
     const uint32_t i_fy = a.irange.n_chunks ? (a.irange.end - seed_n + i_chunk - 1) / i_chunk : 0u;
     const bool pruned = n_int && a.irange.n_chunks && a.ipairs && !a.exact && (K == 1 || a.fused_k) &&
                         (uint64_t)i_lb * i_fy * 256u * i_chunk <= a.ipairs_cap && (uint64_t)i_lb * i_fy <= a.iseg_cap;
-    const bool side = pruned && a.side && a.fork && a.join;
+    // the side stream (when the caller gives one) takes the pruned integer lanes or, without them, the fused top-1
+    // select of storage class 1 (both write out by atomics only; k_big_sel reads out's keys as a lower bound)
+    const bool c1_side = !pruned && K == 1 && a.fused && n_fast && a.range[1].n_chunks && a.range[0].n_chunks;
+    const bool side = (pruned || c1_side) && a.side && a.fork && a.join;
     hipStream_t si = side ? a.side : s;
     if (side) {
         hipError_t e = hipEventRecord(a.fork, s);
@@ -1092,14 +1095,15 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
             if (r.n_chunks == 0) continue;
             if (a.fused) {
                 dim3 grid(pod_blocks, r.n_chunks), block(256);
+                hipStream_t sc = (cls == 1 && c1_side && side) ? si : s;
 #define KG_SEL1(PMV)                                                                                               \
     do {                                                                                                           \
         if (cls == 0)                                                                                              \
-            k_select1<PMV, 0><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, r.begin, r.end, r.chunk,    \
-                                                     a.index_base, a.cfg, a.out, a.order);                         \
+            k_select1<PMV, 0><<<grid, block, 0, sc>>>(a.nodes, a.zones, a.pods, n_fast, r.begin, r.end, r.chunk,   \
+                                                      a.index_base, a.cfg, a.out, a.order);                        \
         else                                                                                                       \
-            k_select1<PMV, 1><<<grid, block, 0, s>>>(a.nodes, a.zones, a.pods, n_fast, r.begin, r.end, r.chunk,    \
-                                                     a.index_base, a.cfg, a.out, a.order);                         \
+            k_select1<PMV, 1><<<grid, block, 0, sc>>>(a.nodes, a.zones, a.pods, n_fast, r.begin, r.end, r.chunk,   \
+                                                      a.index_base, a.cfg, a.out, a.order);                        \
     } while (0)
                 switch (a.cfg.plugins & 7u) {
                     case 0: KG_SEL1(0); break;
@@ -1112,6 +1116,10 @@ hipError_t launch_select(const LaunchSelect& a, hipStream_t s) {
                     default: KG_SEL1(7); break;
                 }
 #undef KG_SEL1
+                if (cls == 1 && c1_side && side) {
+                    hipError_t e = hipEventRecord(a.join, a.side);
+                    if (e != hipSuccess) return e;
+                }
             } else if (K == 1) {
                 if (cls == 0) select_fast<1, 0>(a, r, s);
                 else select_fast<1, 1>(a, r, s);

@@ -2056,13 +2056,15 @@ static kg_status select_local(kg_snap* s, kg_pods* p, uint32_t k, uint64_t* d_ou
         a.ipairs_cap = p->ipairs_cap;
         a.iseg_cap = (uint32_t)(p->ipairs_cap / (256 * 64) + 1);
         a.iseed = 256;
-        if (!std::getenv("KG_NO_SIDE_STREAM")) {  // beside the fast lanes' kernels (disjoint rows of out)
-            st = ensure_side(ctx);
-            if (st != KG_OK) return st;
-            a.side = ctx->side;
-            a.fork = ctx->fork;
-            a.join = ctx->join;
-        }
+    }
+    if (!std::getenv("KG_NO_SIDE_STREAM")) {
+        // beside the fast lanes' kernels: the pruned integer lanes (disjoint rows of out) or, without them, the
+        // fused top-1 select of storage class 1 (atomicMax into the same rows)
+        st = ensure_side(ctx);
+        if (st != KG_OK) return st;
+        a.side = ctx->side;
+        a.fork = ctx->fork;
+        a.join = ctx->join;
     }
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
