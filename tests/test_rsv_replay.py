@@ -106,3 +106,38 @@ def test_replay_with_reservation_views(ctx, seed):
     used, _, npu, _ = snap.read_quotas()
     assert np.array_equal(used, qu) and np.array_equal(npu, qn)
     assert (node >= 0).sum() > 100
+
+
+@pytest.mark.gpu
+def test_assume_ext_follows_reservation_reserve(ctx):
+    """kg_assume_ext runs Reservation.Reserve on the node's views: after the oracle replay's first m placements are
+    assumed one by one, the select of the next pod equals the oracle replay's choice for it, and the whole select of
+    the rest equals the one after kg_replay of the same m pods."""
+    from koordinator_amd import engine
+    m = 120
+    cfg, nodes, pods, quotas, rsv, _, _ = _cluster(1200, 300, 83)
+    kc = cfg.kg_config()
+    onode, ototal, *_ = oracle_lib.OracleState(kc, nodes).ext_replay(pods, quotas, rsv=rsv)
+    head, rest = abi.take(pods, np.arange(m)), abi.take(pods, np.arange(m, abi.table_len(pods)))
+    snap_a = engine.Snapshot(ctx, kc, nodes)
+    snap_a.upload_quotas(quotas)
+    snap_a.upload_reservations(rsv)
+    ba = engine.PodBatch(ctx, head)
+    for j in range(m):
+        if onode[j] >= 0:
+            engine.assume_ext(snap_a, ba, j, int(onode[j]))
+    snap_b = engine.Snapshot(ctx, kc, nodes)
+    snap_b.upload_quotas(quotas)
+    snap_b.upload_reservations(rsv)
+    node_b, _ = engine.replay(snap_b, engine.PodBatch(ctx, head))
+    assert np.array_equal(node_b, onode[:m])
+    br = engine.PodBatch(ctx, rest)
+    keys_a = engine.eval_select(snap_a, br, 1)
+    keys_b = engine.eval_select(snap_b, br, 1)
+    assert np.array_equal(keys_a, keys_b)
+    first = keys_a[0, 0]
+    if onode[m] >= 0:
+        assert int(abi.key_node(first)) == int(onode[m]) and int(first >> np.uint64(32)) == int(ototal[m])
+    else:
+        assert first == 0
+    assert sum(1 for j in range(m) if onode[j] >= 0) > 60
