@@ -1139,19 +1139,35 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
                             const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
                             uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, const uint32_t* special,
-                            uint32_t special_est, const uint32_t* c1, uint32_t c1_est, hipStream_t s) {
+                            uint32_t special_est, const uint32_t* c1, uint32_t c1_est, hipStream_t s, const SideLane* lane) {
     if (n_list == 0 || n_nodes == 0) return hipSuccess;
     dim3 grid((n_list + 255) / 256, (n_nodes + chunk - 1) / chunk);
     if (fb) {  // the general records only (the fast-base records' maximum: k_ext_select)
+        // the class-1 kernel on the side lane beside the general one (both only atomicMax / atomicMin per pod)
+        const bool two = c1 && lane && lane->s && lane->fork && lane->join;
+        hipStream_t s3 = two ? lane->s : s;
+        if (two) {
+            hipError_t err = hipEventRecord(lane->fork, s);
+            if (err == hipSuccess) err = hipStreamWaitEvent(lane->s, lane->fork, 0);
+            if (err != hipSuccess) return err;
+        }
+        if (c1) {
+            uint32_t chunk3, y3;
+            ext_part2_grid(c1_est, grid.x, &chunk3, &y3);
+            k_ext_stats_c1<<<dim3(grid.x, y3), 256, 0, s3>>>(nodes, zones, e, pods, list, n_list, n0, chunk3, index_base, cfg,
+                                                             qst, dev_max, c1);
+            if (two) {
+                hipError_t err = hipEventRecord(lane->join, lane->s);
+                if (err != hipSuccess) return err;
+            }
+        }
         uint32_t chunk2, y2;
         ext_part2_grid(special_est, grid.x, &chunk2, &y2);
         k_ext_stats_sp<<<dim3(grid.x, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n0, chunk2, index_base, cfg,
                                                         qst, dev_max, rsv_max, pref, special, c1 != nullptr);
-        if (c1) {
-            uint32_t chunk3, y3;
-            ext_part2_grid(c1_est, grid.x, &chunk3, &y3);
-            k_ext_stats_c1<<<dim3(grid.x, y3), 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n0, chunk3, index_base, cfg,
-                                                            qst, dev_max, c1);
+        if (two) {
+            hipError_t err = hipStreamWaitEvent(s, lane->join, 0);
+            if (err != hipSuccess) return err;
         }
         return hipGetLastError();
     }
@@ -1304,27 +1320,44 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
                                 uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
                                 const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
                                 const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est,
-                                hipStream_t s) {
+                                hipStream_t s, const SideLane* lane) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     const uint32_t gx = (n_pods + 255) / 256, y1 = (n_nodes + chunk - 1) / chunk;
     uint32_t chunk2, y2, chunk3 = 0, y3 = 0;
     ext_part2_grid(special_est, gx, &chunk2, &y2);
     if (c1) ext_part2_grid(c1_est, gx, &chunk3, &y3);
     const bool sp = c1 != nullptr;
-    if (k == 1) {
+    // the class-1 kernel on the side lane beside the general one (disjoint partial rows: y1 + y2 on)
+    const bool two = c1 && lane && lane->s && lane->fork && lane->join;
+    hipStream_t s3 = two ? lane->s : s;
+    if (two) {
+        hipError_t err = hipEventRecord(lane->fork, s);
+        if (err == hipSuccess) err = hipStreamWaitEvent(lane->s, lane->fork, 0);
+        if (err != hipSuccess) return err;
+    }
+    if (c1) {
+        if (k == 1)
+            k_ext_select_c1<1><<<dim3(gx, y3), 256, 0, s3>>>(nodes, zones, e, pods, list, n_pods, n0, chunk3, index_base, cfg,
+                                                             qst, dev_max, pref, partial, c1, y1 + y2);
+        else
+            k_ext_select_c1<KG_TOPK_MAX><<<dim3(gx, y3), 256, 0, s3>>>(nodes, zones, e, pods, list, n_pods, n0, chunk3,
+                                                                       index_base, cfg, qst, dev_max, pref, partial, c1,
+                                                                       y1 + y2);
+        if (two) {
+            hipError_t err = hipEventRecord(lane->join, lane->s);
+            if (err != hipSuccess) return err;
+        }
+    }
+    if (k == 1)
         k_ext_select_sp<1><<<dim3(gx, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, index_base, cfg, qst,
                                                         dev_max, rsv_max, pref, partial, pstat, special, y1, sp);
-        if (c1)
-            k_ext_select_c1<1><<<dim3(gx, y3), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk3, index_base, cfg,
-                                                            qst, dev_max, pref, partial, c1, y1 + y2);
-    } else {
+    else
         k_ext_select_sp<KG_TOPK_MAX><<<dim3(gx, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, index_base,
                                                                   cfg, qst, dev_max, rsv_max, pref, partial, pstat, special, y1,
                                                                   sp);
-        if (c1)
-            k_ext_select_c1<KG_TOPK_MAX><<<dim3(gx, y3), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk3,
-                                                                      index_base, cfg, qst, dev_max, pref, partial, c1,
-                                                                      y1 + y2);
+    if (two) {
+        hipError_t err = hipStreamWaitEvent(s, lane->join, 0);
+        if (err != hipSuccess) return err;
     }
     return hipGetLastError();
 }

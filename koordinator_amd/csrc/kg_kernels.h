@@ -103,11 +103,17 @@ hipError_t launch_ext_gate(const PodsDev& pods, uint32_t n_pods, const ExtDev& e
 hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                              uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                              const uint32_t* qst, const ExtVerifyDev& o, hipStream_t s);
+// A second stream for one independent kernel of a launcher (forked from and joined back into the launch stream
+// inside the launcher; nullptr / null members: everything on the launch stream).
+struct SideLane {
+    hipStream_t s;
+    hipEvent_t fork, join;
+};
 hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                             const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
                             uint32_t* dev_max, uint32_t* rsv_max, uint64_t* pref, const uint32_t* special,
-                            uint32_t special_est, const uint32_t* c1, uint32_t c1_est, hipStream_t s);
+                            uint32_t special_est, const uint32_t* c1, uint32_t c1_est, hipStream_t s, const SideLane* lane = nullptr);
 hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                                   const uint32_t* list, uint32_t n_list, uint32_t max_views, uint32_t index_base,
                                   const KCfg& cfg, bool exact,
@@ -134,7 +140,7 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
                                 uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
                                 const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
                                 const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est,
-                                hipStream_t s);
+                                hipStream_t s, const SideLane* lane = nullptr);
 // out[map[t]] = rows t of src (k keys each; row map[t] with src_by_map, src may then be out); rows whose pod
 // has a nonzero qst[pod] get zero keys and pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the
 // host path)

@@ -47,6 +47,9 @@ struct kg_ctx {
     // config-5 select: the plain pods' k_select1 runs on `side` while `stream` builds DevSum and pass 1
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    // a second side lane: config 5's class-1 kernels beside the general ones (forked and joined inside a launcher)
+    hipStream_t side2 = nullptr;
+    hipEvent_t fork2 = nullptr, join2 = nullptr;
 };
 
 struct kg_snap {
@@ -784,6 +787,9 @@ kg_status kg_close(kg_ctx* ctx) {
     if (ctx->side) hipStreamDestroy(ctx->side);
     if (ctx->fork) hipEventDestroy(ctx->fork);
     if (ctx->join) hipEventDestroy(ctx->join);
+    if (ctx->side2) hipStreamDestroy(ctx->side2);
+    if (ctx->fork2) hipEventDestroy(ctx->fork2);
+    if (ctx->join2) hipEventDestroy(ctx->join2);
     hipStreamDestroy(ctx->stream);
     delete ctx;
     return KG_OK;
@@ -1366,6 +1372,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     // the side stream's plain-pod select of the previous batch reads d_in: it has to finish before the copy
     if (ctx->side) HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
+    if (ctx->side2) HIP_TRY(ctx, hipStreamSynchronize(ctx->side2));
     // the previous upload's copy has completed (every upload ends with a stream synchronisation), so the
     // pinned staging can be rewritten
     const PodLayout L = pod_layout(n);
@@ -1762,9 +1769,25 @@ static kg_status ext_gate_local(kg_snap* s, kg_pods* p) {
     return KG_OK;
 }
 
+// the second side lane (nullptr when KG_NO_SIDE_STREAM is set or it cannot be created: one stream then)
+static const SideLane* side_lane2(kg_ctx* ctx, SideLane& l) {
+    if (std::getenv("KG_NO_SIDE_STREAM")) return nullptr;
+    if (!ctx->side2) {
+        if (hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&ctx->fork2, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ctx->join2, hipEventDisableTiming) != hipSuccess)
+            return nullptr;
+    }
+    l.s = ctx->side2;
+    l.fork = ctx->fork2;
+    l.join = ctx->join2;
+    return (l.s && l.fork && l.join) ? &l : nullptr;
+}
+
 static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
     kg_ctx* ctx = s->ctx;
     ExtDev e = s->ext_dev();
+    SideLane lane{};
     kg_status dst = gated ? KG_OK : ext_gate_local(s, p);
     if (dst != KG_OK) return dst;
     dst = ext_dev_sum(s, p, e);
@@ -1786,7 +1809,8 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
         const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(ng, 1), 8192);
         HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, s->n0, chunk, s->base,
                                       s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
-                                      s->d_special, special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream));
+                                      s->d_special, special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream,
+                                      side_lane2(ctx, lane)));
     }
     return KG_OK;
 }
@@ -1895,6 +1919,7 @@ static kg_status launch_plain_side(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t
 static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t* d_out, bool global = false,
                                   bool plain_on_side = false) {
     kg_ctx* ctx = s->ctx;
+    SideLane lane2{};
     const bool split = !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok &&
                        !need_topo(s, p);
     const uint32_t n_x = split ? p->n_x : p->n;
@@ -1959,7 +1984,8 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         xe.cls_max = nullptr;
         HIP_TRY(ctx, launch_ext_select_sp(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base, s->kcfg,
                                           p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, xpart, p->d_pstat, s->d_special,
-                                          special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream));
+                                          special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream,
+                                          side_lane2(ctx, lane2)));
     }
     if (plain_on_side) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->join, 0));  // d_out zeroed + plain keys in
     if (!split) {
