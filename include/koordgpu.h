@@ -371,8 +371,8 @@ typedef struct kg_node_columns {
     const struct kg_gpu_partition* gpu_parts;
     uint32_t n_gpu_parts;
     /* DeviceShare NUMA topology (deviceshare/numa_topology.go:43-100, NUMATopology.deviceToNodeID; NULL = every
-     * minor without a topology): nibble m of dev_numa[i] = GPU minor m's NUMA node id (0..7, the NRT zone of that
-     * id), KG_GPU_NUMA_ANY = its Topology.NodeID is -1 (in every NUMA mask, in no NUMA scope), KG_GPU_NUMA_NONE =
+     * minor without a topology): nibble m of dev_numa[i] = GPU minor m's NUMA node id (0..KG_MAX_ZONES-1, the NRT zone of
+     * that id; the upload rejects larger ids), KG_GPU_NUMA_ANY = its Topology.NodeID is -1 (in every NUMA mask, in no NUMA scope), KG_GPU_NUMA_NONE =
      * no Topology (left out whenever a NUMA affinity restricts the allocation, device_allocator.go:155-159).
      * GPU pods on nodes whose NUMA policy is not None join the topology manager's hint merge with these
      * (deviceshare/topology_hint.go:40-290). */

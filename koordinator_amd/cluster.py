@@ -612,7 +612,7 @@ class ClusterState:
         matchable reservations (rsvmatch.match_classes), then decode.reservation_restore over the current rows.
         Returns (rsv_class per pod, restored node table, abi.Reservations)."""
         from . import decode, rsvmatch
-        infos = self.reservations.matchable_infos(self.index)
+        infos = list({ri.uid: ri for _, ri in self.reservations.matchable_infos(self.index)}.values())
         nodes_by_name = {n: self.nodes[i] for n, i in self.index.items()}
         cls, rsv_cls, _ = rsvmatch.match_classes(list(pods), [pod_requests(p) for p in pods], [ri.obj for ri in infos],
                                                  nodes_by_name)
@@ -1000,6 +1000,8 @@ class ReservationCache:
         uid = _md(r).get("uid", "")
         ri = self.infos.pop(uid, None)
         node = (r.get("status") or {}).get("nodeName", "")
+        # the reference clears the object's node only; a tombstone without nodeName would leave the uid in the sets of
+        # the node the cache knew, where for_each_matchable skips it (infos no longer hold it)
         for m in (self.on_node, self.matchable_on_node, self.allocated_on_node):
             self._drop(m, node, uid)
         for n in {node, ri.node if ri else ""} - {""}:
@@ -1020,7 +1022,10 @@ class ReservationCache:
     def for_each_matchable(self, node: str, fn) -> None:
         """ForEachMatchableReservationOnNode (cache.go:1162-1180): fn(info) -> continue?"""
         for uid in sorted(self.matchable_on_node.get(node, ())):
-            if not fn(self.infos[uid]):
+            ri = self.infos.get(uid)
+            if ri is None:  # a delete whose object named another node left the uid here
+                continue
+            if not fn(ri):
                 return
 
     def list_available(self, node: str, list_all: bool) -> List[ReservationInfo]:
@@ -1092,24 +1097,27 @@ class ReservationCache:
     def forget_pod(self, ruid: str, pod):
         self._remove(ruid, pod)
 
-    def matchable_infos(self, node_index: Dict[str, int]) -> List[ReservationInfo]:
-        """The reservations ForEachMatchableReservationOnNode visits on the indexed nodes, in node order."""
-        out = []
+    def matchable_infos(self, node_index: Dict[str, int]) -> List[Tuple[str, ReservationInfo]]:
+        """The (node, reservation) pairs ForEachMatchableReservationOnNode visits on the indexed nodes, in node order,
+        keyed by the node walked: a reservation whose nodeName changed stays in its old node's sets (updateReservation
+        adds it to the new node's and removes nothing, cache.go:793-844), so the old node's walk visits it as well."""
+        out: List[Tuple[str, ReservationInfo]] = []
         for name in sorted(self.matchable_on_node, key=lambda nm: node_index.get(nm, -1)):
             if name in node_index:
-                self.for_each_matchable(name, lambda ri: out.append(ri) or True)
+                self.for_each_matchable(name, lambda ri, nm=name: out.append((nm, ri)) or True)
         return out
 
     def restore_inputs(self, node_index: Dict[str, int], classes_of=None) -> List[dict]:
         """The matchable reservations of every node as decode.reservation_restore reads them
-        (ForEachMatchableReservationOnNode, cache.go:1162-1180); classes_of(info) -> owner-match classes."""
+        (ForEachMatchableReservationOnNode, cache.go:1162-1180), one entry per (node walked, reservation);
+        classes_of(info) -> owner-match classes."""
         out = []
-        for ri in self.matchable_infos(node_index):
+        for name, ri in self.matchable_infos(node_index):
             names = 0
             for k, key in enumerate(list(RSV_VEC) + list(self.cfg.scalar_resources[:abi.KG_NSCALAR])):
                 if key in ri.names:
                     names |= 1 << k
-            out.append(dict(node=node_index[ri.node], cls=classes_of(ri) if classes_of else [], uid=ri.uid,
+            out.append(dict(node=node_index[name], cls=classes_of(ri) if classes_of else [], uid=ri.uid,
                             allocatable=ri.allocatable,
                             allocated=ri.allocated if ri.allocated_rl is not None else None,
                             allocated_keys=ri.allocated_keys(), reserved=None, allocated_pods=ri.allocated_pods,
@@ -1121,6 +1129,8 @@ class ReservationCache:
 # ---- ElasticQuota cache (elasticquota/quota_handler.go, core/group_quota_manager.go) ------------------------
 
 LABEL_QUOTA_NAME = "quota.scheduling.koordinator.sh/name"
+DEFAULT_QUOTA_NAME = "koordinator-default-quota"  # apis/extension/elastic_quota.go DefaultQuotaName
+SYSTEM_QUOTA_NAME = "koordinator-system-quota"  # SystemQuotaName
 QUOTA_VEC = (CPU, MEMORY)  # KG_QUOTA_R order: cpu, memory, scalar0, scalar1
 
 
@@ -1159,7 +1169,9 @@ class QuotaCache:
         spec = q.get("spec") or {}
         if md.get("deletionTimestamp") is not None:
             return
-        if add and name in self.index and self.max[self.index[name]] is not None:
+        # OnQuotaAdd (quota_handler.go:55-58) keeps a quota it already holds, except the default and system quotas
+        if add and name in self.index and self.max[self.index[name]] is not None and \
+                name not in (DEFAULT_QUOTA_NAME, SYSTEM_QUOTA_NAME):
             return
         if name not in self.index:
             self.index[name] = len(self.max)

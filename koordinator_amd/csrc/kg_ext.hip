@@ -1135,6 +1135,13 @@ hipError_t launch_ext_verify(const NodeRec* nodes, const ZoneRec* zones, const E
     return hipGetLastError();
 }
 
+// An error after the fork of a side lane: its kernels may still run with no join back into the main stream, so the
+// lane is drained before the error goes up (the caller may free the buffers they write).
+static hipError_t drain_lane(const SideLane* lane, hipError_t err) {
+    hipStreamSynchronize(lane->s);
+    return err;
+}
+
 hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                             const uint32_t* list, uint32_t n_list, uint32_t n_nodes, uint32_t n0, uint32_t chunk,
                             uint32_t index_base, const KCfg& cfg, bool exact, bool topo, bool fb, const uint32_t* qst,
@@ -1158,7 +1165,7 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
                                                              qst, dev_max, c1);
             if (two) {
                 hipError_t err = hipEventRecord(lane->join, lane->s);
-                if (err != hipSuccess) return err;
+                if (err != hipSuccess) return drain_lane(lane, err);
             }
         }
         uint32_t chunk2, y2;
@@ -1167,7 +1174,7 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
                                                         qst, dev_max, rsv_max, pref, special, c1 != nullptr);
         if (two) {
             hipError_t err = hipStreamWaitEvent(s, lane->join, 0);
-            if (err != hipSuccess) return err;
+            if (err != hipSuccess) return drain_lane(lane, err);
         }
         return hipGetLastError();
     }
@@ -1345,7 +1352,7 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
                                                                        y1 + y2);
         if (two) {
             hipError_t err = hipEventRecord(lane->join, lane->s);
-            if (err != hipSuccess) return err;
+            if (err != hipSuccess) return drain_lane(lane, err);
         }
     }
     if (k == 1)
@@ -1357,7 +1364,7 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
                                                                   sp);
     if (two) {
         hipError_t err = hipStreamWaitEvent(s, lane->join, 0);
-        if (err != hipSuccess) return err;
+        if (err != hipSuccess) return drain_lane(lane, err);
     }
     return hipGetLastError();
 }

@@ -1544,6 +1544,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     hipSetDevice(p->ctx->device);
     hipStreamSynchronize(p->ctx->stream);
     if (p->ctx->side) hipStreamSynchronize(p->ctx->side);  // a plain-pod select may still read the batch there
+    if (p->ctx->side2) hipStreamSynchronize(p->ctx->side2);  // and a class-1 lane of the config-5 kernels
     for (void* b : {(void*)p->d_ipairs, (void*)p->d_ipair_count})
         hipFree(b);
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,

@@ -221,6 +221,11 @@ def test_quota_add_ignores_deleting_quota():
     assert c.max[c.index["1"]] == {"cpu": "0", "memory": "0"}
     c.on_quota(_quota("1", "4", "4Gi"))
     assert c.max[c.index["1"]] == {"cpu": "4", "memory": "4Gi"}
+    # the default and system quotas are updated by an Add too (quota_handler.go:55)
+    for name in ("koordinator-default-quota", "koordinator-system-quota"):
+        c.on_quota(_quota(name, "1", "1Gi"), add=True)
+        c.on_quota(_quota(name, "2", "2Gi"), add=True)
+        assert c.max[c.index[name]] == {"cpu": "2", "memory": "2Gi"}
 
 
 def test_quota_pod_used_flat():
@@ -237,3 +242,33 @@ def test_quota_pod_used_flat():
     t = c.columns()
     assert list(t["used"][c.index["test1"]][:2]) == [40000, 100]
     assert list(t["used"][c.index["test2"]][:2]) == [0, 0]
+
+
+def test_cache_reservation_node_move_walks_both_nodes():
+    """updateReservation (cache.go:793-844) adds a moved reservation to its new node's sets and removes nothing from
+    the old node's: ForEachMatchableReservationOnNode visits it on both nodes, and the restore inputs key each entry
+    by the node walked, so the reservation is restored once per node (never twice on the new one)."""
+    c = _cache()
+    c.update_reservation(_rsv("u1", "r1", "node-a", "4", "4Gi"))
+    c.update_reservation(_rsv("u1", "r1", "node-b", "4", "4Gi"))
+    assert "u1" in c.matchable_on_node["node-a"] and "u1" in c.matchable_on_node["node-b"]
+    index = {"node-a": 0, "node-b": 1}
+    pairs = c.matchable_infos(index)
+    assert [(n, ri.uid) for n, ri in pairs] == [("node-a", "u1"), ("node-b", "u1")]
+    entries = c.restore_inputs(index)
+    assert sorted(e["node"] for e in entries) == [0, 1]
+
+
+def test_cache_delete_tombstone_without_node():
+    """DeleteReservation clears the sets of the object's nodeName only (cache.go:893-918): a tombstone without one
+    leaves the uid on the node, and the walk skips it instead of failing on the missing info."""
+    c = _cache()
+    c.update_reservation(_rsv("u1", "r1", "node-a", "4", "4Gi"))
+    c.update_reservation(_rsv("u2", "r2", "node-a", "2", "2Gi"))
+    tomb = _rsv("u1", "r1", "", "4", "4Gi")
+    c.delete_reservation(tomb)
+    assert c.get("u1") is None
+    seen = []
+    c.for_each_matchable("node-a", lambda ri: seen.append(ri.uid) or True)
+    assert seen == ["u2"]
+    assert [e["uid"] for e in c.restore_inputs({"node-a": 0})] == ["u2"]
