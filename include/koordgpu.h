@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 10
+#define KG_ABI_VERSION 11
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -377,6 +377,12 @@ typedef struct kg_node_columns {
      * GPU pods on nodes whose NUMA policy is not None join the topology manager's hint merge with these
      * (deviceshare/topology_hint.go:40-290). */
     const uint32_t* dev_numa;
+    /* The cpuset pods behind numa_zone_status (NodeAllocation.singleNUMANode / sharedNode, node_allocation.go:111-143):
+     * byte z (z < KG_MAX_ZONES) = pods whose CPUs lie in NUMA node z only, byte KG_MAX_ZONES + z = pods whose CPUs span z
+     * and another node (saturating at 255). A cpuset Release (kg_unreserve) takes its pod out again, so the statuses it
+     * leaves follow from these counts. NULL: one pod per non-idle status (single -> 1 / 0, shared -> 0 / 1); when given,
+     * the 2-bit statuses of numa_zone_status are derived from them. */
+    const uint64_t* numa_zone_pods;
 } kg_node_columns;
 #define KG_GPU_NUMA_ANY 0xEu
 #define KG_GPU_NUMA_NONE 0xFu
@@ -392,6 +398,7 @@ typedef struct kg_node_state {
     int64_t* cpuset_alloc_milli;
     kg_cpu_alloc* cpu_alloc; /* [node] (nodes without a CPU topology: zeros) */
     uint32_t* numa_zone_status; /* NUMANodeSharedStatus, 2 bits per zone (a cpuset Reserve changes it) */
+    uint64_t* numa_zone_pods;   /* kg_node_columns.numa_zone_pods */
 } kg_node_state;
 
 /* Pending pods, struct-of-arrays host columns (caller-owned, copied). */
@@ -604,6 +611,35 @@ kg_status kg_forget_ext(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t nod
                         uint32_t minors);
 /* GPU minors chosen for each pod by the last kg_replay (bitmask; 0 = none), n_pods entries. */
 kg_status kg_replay_minors(kg_pods* pods, uint32_t* out);
+
+/* What one Reserve took, as the reference keeps it for the Unreserve (CycleState and the plugins' caches): the NUMA
+ * zone code and per-zone amounts (nodenumaresource/plugin.go:585-635 -> resource_manager.go Update), the cpuset CPUs
+ * (NodeAllocation.addPodAllocation), the GPU minors (deviceshare/plugin.go:507-569) and the reservation the pod joined
+ * (reservation/plugin.go:1295-1408 assumePods; rsv_rid = kg_rsv_info.rid on the node, -1 = none). */
+typedef struct kg_reserve_record {
+    int32_t numa_zone;                        /* the pair's kg_verify_out.numa_zone (-1 = none)              */
+    uint32_t gpu_minors;                      /* DeviceShare minors taken (bit m = minor m)                  */
+    int32_t rsv_rid;                          /* nominated reservation's rid, -1 = none                      */
+    uint32_t flags;                           /* KG_RECORD_*                                                 */
+    int64_t zone_amounts[2 * KG_MAX_ZONES];   /* cpu milli per zone, then memory bytes per zone              */
+    uint64_t cpus[KG_MAX_CPUS / 64];          /* cpuset CPUs taken                                           */
+} kg_reserve_record;
+#define KG_RECORD_CPUSET 0x1u  /* the Reserve took cpuset CPUs (cpus) */
+#define KG_RECORD_QUOTA 0x2u   /* the Reserve added the pod to its ElasticQuota's used */
+
+/* Reserve of pod `pod` on local node `node` with every enabled plugin (kg_assume / kg_assume_ext: NodeInfo,
+ * LoadAware, NodeNUMAResource incl. cpusets, DeviceShare, ElasticQuota, Reservation.Reserve on the node's views),
+ * filling *out with what the Unreserve needs. KG_RESERVE_FAILED: nothing applied. */
+kg_status kg_reserve(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, kg_reserve_record* out);
+/* Unreserve of a kg_reserve: every plugin gives back what the record says it took (load_aware.go:231-233,
+ * nodenumaresource/plugin.go:700-720 -> resource_manager.go:478-483 Release incl. the cpuset CPUs and the NUMA
+ * single / shared sets, deviceshare/plugin.go Unreserve, elasticquota/plugin.go:638-652, reservation/plugin.go:1409-1460
+ * forgetPods: the reservation's Allocated and assigned pods, and the node's views as the next restore builds them). */
+kg_status kg_unreserve(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, const kg_reserve_record* rec);
+/* Copy of the snapshot's reservation views and infos as the device holds them (after Reservation.Reserve /
+ * Unreserve on the device): n_views / n_infos entries as uploaded, in upload order. */
+kg_status kg_snapshot_read_reservations(kg_snap* snap, kg_rsv_view* views, uint32_t n_views, kg_rsv_info* infos,
+                                        uint32_t n_infos);
 
 /* Device cpuset accumulator, one request per workgroup: out[4 * i] = the CPUs chosen for request i,
  * rc[i] = 0, -1 (ErrNotEnoughCPUs: fewer allocatable CPUs than needed) or -2 ("failed to allocate cpus").

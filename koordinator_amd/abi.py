@@ -11,7 +11,7 @@ from typing import Dict
 
 import numpy as np
 
-KG_ABI_VERSION = 10
+KG_ABI_VERSION = 11
 KG_LA_R = 2
 KG_NSCALAR = 2
 KG_MAX_ZONES = 4
@@ -204,6 +204,8 @@ class KgNodeColumns(C.Structure):
         ("dev_topo", C.POINTER(C.c_uint64)), ("dev_part", _pu32), ("gpu_parts", C.c_void_p), ("n_gpu_parts", C.c_uint32),
         # GPU NUMA node ids (DeviceShare as a NUMA hint provider)
         ("dev_numa", _pu32),
+        # cpuset pods per NUMA node in singleNUMANode (byte z) / sharedNode (byte KG_MAX_ZONES + z)
+        ("numa_zone_pods", C.POINTER(C.c_uint64)),
     ]
 
 
@@ -218,7 +220,18 @@ class KgNodeState(C.Structure):
         ("dev_free", _p64),
         ("cpuset_alloc_milli", _p64), ("cpu_alloc", C.c_void_p),
         ("numa_zone_status", C.POINTER(C.c_uint32)),
+        ("numa_zone_pods", C.POINTER(C.c_uint64)),
     ]
+
+
+KG_RECORD_CPUSET = 0x1
+KG_RECORD_QUOTA = 0x2
+
+
+class KgReserveRecord(C.Structure):
+    """kg_reserve_record: what one kg_reserve took, for its kg_unreserve."""
+    _fields_ = [("numa_zone", C.c_int32), ("gpu_minors", C.c_uint32), ("rsv_rid", C.c_int32), ("flags", C.c_uint32),
+                ("zone_amounts", C.c_int64 * (2 * KG_MAX_ZONES)), ("cpus", C.c_uint64 * 4)]  # KG_MAX_CPUS / 64
 
 
 class KgPodColumns(C.Structure):
@@ -488,6 +501,9 @@ def node_columns(t: Table) -> KgNodeColumns:
     if "dev_numa" in t:
         t["dev_numa"] = np.ascontiguousarray(t["dev_numa"], np.uint32)
         s.dev_numa = _ptr(t["dev_numa"], C.c_uint32)
+    if "numa_zone_pods" in t:
+        t["numa_zone_pods"] = np.ascontiguousarray(t["numa_zone_pods"], np.uint64)
+        s.numa_zone_pods = t["numa_zone_pods"].ctypes.data_as(C.POINTER(C.c_uint64))
     if "gpu_parts" in t and len(t["gpu_parts"]):
         t["gpu_parts"] = np.ascontiguousarray(t["gpu_parts"], GPU_PARTITION_DTYPE)
         s.gpu_parts = t["gpu_parts"].ctypes.data
@@ -518,6 +534,8 @@ def node_state_struct(t: Table) -> KgNodeState:
         s.cpu_alloc = t["cpu_alloc"].ctypes.data
     if "numa_zone_status" in t:
         s.numa_zone_status = _ptr(t["numa_zone_status"], C.c_uint32)
+    if "numa_zone_pods" in t:
+        s.numa_zone_pods = t["numa_zone_pods"].ctypes.data_as(C.POINTER(C.c_uint64))
     s._keep = t
     return s
 
@@ -528,6 +546,7 @@ def empty_node_state(n: int) -> Table:
     t["cpuset_alloc_milli"] = np.zeros(n, np.int64)
     t["cpu_alloc"] = np.zeros((n, 2 * KG_MAX_CPUS), np.uint8)
     t["numa_zone_status"] = np.zeros(n, np.uint32)
+    t["numa_zone_pods"] = np.zeros(n, np.uint64)
     return t
 
 

@@ -229,6 +229,15 @@ class NodeAllocation:
                 for k, q in _rl(res).items():
                     cur[k] = max(cur.get(k, 0) - q, 0)
 
+    def zone_pods(self, n_zones: int) -> int:
+        """The pods behind the statuses (kg_node_columns.numa_zone_pods): byte z = singleNUMANode[z], byte 4 + z =
+        sharedNode[z] (saturating at 255), so that a device Release leaves the statuses the reference leaves."""
+        w = 0
+        for z in range(min(n_zones, abi.KG_MAX_ZONES)):
+            w |= min(len(self.single.get(z, ())), 255) << (8 * z)
+            w |= min(len(self.shared.get(z, ())), 255) << (8 * (abi.KG_MAX_ZONES + z))
+        return w
+
     def zone_status(self, n_zones: int) -> int:
         """NUMANodeSharedStatus per zone (:52-68), 2 bits each."""
         st = 0
@@ -713,12 +722,14 @@ class ClusterState:
         used, cpuset_milli = self._zone_used(i)
         row.update(zone_used_cols(used, cpuset_milli))
         row["numa_zone_status"] = self.numa[i].zone_status(len(t.zones)) if t.cpu_zone else 0
+        row["numa_zone_pods"] = self.numa[i].zone_pods(len(t.zones)) if t.cpu_zone else 0
         row["dev_minors"], row["dev_total"], row["dev_free"] = self.devices.columns(name)
         return row
 
     def table(self, rows: Optional[Iterable[int]] = None) -> abi.Table:
         rows = range(len(self.nodes)) if rows is None else list(rows)
         t = abi.empty_nodes(len(rows))
+        t["numa_zone_pods"] = np.zeros(len(rows), np.uint64)
         for k, i in enumerate(rows):
             for key, v in self.row(int(i)).items():
                 t[key][k] = v

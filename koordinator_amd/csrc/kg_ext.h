@@ -1365,6 +1365,90 @@ __device__ __forceinline__ void rsv_reserve_dev(const ExtDev& e, int64_t* n, Zon
     }
 }
 
+// ---- Reservation.Unreserve (reservation/plugin.go:1409-1460) ------------------------------------------------------
+// The pod leaves the reservation it joined (forgetPods -> RemoveAssignedPod, reservation_info.go:502-514: Allocated -=
+// Mask(requests, ResourceNames) with a non-negative result, one assigned pod less; keys stay) and the node's views as
+// the next restore (transformer.go:740-935) builds them: the unmatched correction of the reservation is its Allocated
+// while it has pods and nothing after the last one (restoreUnmatchedReservations :891-903), so the record and the views
+// that do not match it change by the pod and the change of that correction; the views that match it lose the pod and
+// count the new Allocated in rAllocated; every view counts one pod less. rid: the reservation's kg_rsv_info.rid (found
+// among the node's views; none: the pod joined no reservation). The NodeInfo part is apply_assume(-1)'s. One lane.
+__device__ __forceinline__ void rsv_unreserve_dev(const ExtDev& e, int64_t* n, ZoneRec* zr, uint32_t rec, const PodV& p,
+                                                  int32_t rid_in) {
+    const int64_t preq[RSV_R] = {p.req_cpu, p.req_mem, p.req_eph, p.sc0, p.sc1};
+    RsvInfo* infos = const_cast<RsvInfo*>(e.infos);
+    RsvView* views = const_cast<RsvView*>(e.views);
+    const uint64_t cmask = (uint64_t)n[N_RSV_CLASSES];
+    const uint32_t rid = rid_in < 0 ? 0xFFFFFFFFu : (uint32_t)rid_in;
+    // the reservation as the node's views hold it (every copy agrees)
+    const RsvInfo* r = nullptr;
+    for (uint64_t l = cmask; l && rid != 0xFFFFFFFFu && !r; l &= l - 1ull) {
+        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec);
+        if (!cv) continue;
+        for (uint32_t t = cv->first; t < cv->first + cv->count; t++)
+            if (infos[t].rid == rid) {
+                r = &infos[t];
+                break;
+            }
+    }
+    int64_t a1[RSV_R] = {0, 0, 0, 0, 0}, dc[RSV_R] = {0, 0, 0, 0, 0}, dra[RSV_R] = {0, 0, 0, 0, 0};
+    int64_t dn0 = 0, dn1 = 0, p1 = 0;
+    if (r) {
+        const int64_t p0 = r->allocated_pods;
+        p1 = p0 > 0 ? p0 - 1 : 0;
+        int64_t n00 = 0, n01 = 0, n10 = 0, n11 = 0;
+#pragma unroll
+        for (int k = 0; k < RSV_R; k++) {
+            const int64_t m = ((r->names >> k) & 1u) ? preq[k] : 0;
+            a1[k] = r->allocated[k] - m < 0 ? 0 : r->allocated[k] - m;
+            dc[k] = (p1 > 0 ? a1[k] : 0) - (p0 > 0 ? r->allocated[k] : 0);
+            dra[k] = a1[k] - r->allocated[k];
+        }
+        if (p0 > 0) rsv_nonzero_dev(r->allocated, r->allocated_keys, n00, n01);
+        if (p1 > 0) rsv_nonzero_dev(a1, r->allocated_keys, n10, n11);
+        dn0 = n10 - n00;
+        dn1 = n11 - n01;
+        n[N_REQ_CPU] -= dc[0];
+        n[N_REQ_MEM] -= dc[1];
+        n[N_REQ_EPH] -= dc[2];
+        n[N_SC_REQ0] -= dc[3];
+        n[N_SC_REQ1] -= dc[4];
+        n[N_NZ_CPU] -= dn0;
+        n[N_NZ_MEM] -= dn1;
+        derive_node(*reinterpret_cast<NodeRec*>(n), *zr);
+    }
+    for (uint64_t l = cmask; l; l &= l - 1ull) {
+        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec);
+        if (!cv) continue;
+        RsvView& v = views[cv - e.views];
+        bool matched = false;
+        for (uint32_t t = v.first; t < v.first + v.count && r; t++) matched = matched || infos[t].rid == rid;
+#pragma unroll
+        for (int k = 0; k < RSV_R; k++) {
+            const int64_t d = -preq[k] - (matched ? 0 : dc[k]);
+            v.req[k] += d;
+            v.pod_requested[k] += d;
+            if (matched) v.r_allocated[k] += dra[k];
+        }
+        v.nz_cpu += -p.nz_cpu - (matched ? 0 : dn0);
+        v.nz_mem += -p.nz_mem - (matched ? 0 : dn1);
+        v.num_pods -= 1;
+    }
+    if (!r) return;
+    // every copy of the reservation (after the views: r points into infos)
+    for (uint64_t l = cmask; l; l &= l - 1ull) {
+        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec);
+        if (!cv) continue;
+        for (uint32_t t = cv->first; t < cv->first + cv->count; t++) {
+            RsvInfo& x = infos[t];
+            if (x.rid != rid || x.allocated_pods != p1 + 1) continue;
+#pragma unroll
+            for (int k = 0; k < RSV_R; k++) x.allocated[k] = a1[k];
+            x.allocated_pods = p1;
+        }
+    }
+}
+
 // per-pod NormalizeScore inputs: max DeviceShare raw score, max nominated Reservation score, and the
 // preferred node key ((order + 2^31) << 32 | snapshot index, minimum; ~0 = none)
 constexpr uint64_t PREF_NONE = ~0ull;

@@ -16,13 +16,14 @@
 // re-runs the rows whose guess was wrong, so no pair is evaluated twice unless its pod's guess failed.
 // Between the passes the multi-GPU path all-reduces the per-pod maxima over RCCL.
 // k_ext_replay   one pod per launch (lane = node record): applies the previous pod's Reserve in place
-//                (NodeInfo, LoadAware, NUMA zone, GPU minors, quota used), gates the next pod on its
-//                quota, evaluates it, and reduces per DeviceShare raw score bucket so that the next
-//                launch can normalise without another grid-wide pass.
+//                (NodeInfo, LoadAware, NUMA zone, GPU minors, quota used, Reservation), gates the next pod on its
+//                quota, evaluates it, and reduces per DeviceShare raw score bucket; the launch's last workgroup
+//                normalises over the buckets and picks the pod's winner (no second launch per step).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 
+#include "kg_cpuset_reserve.h"
 #include "kg_ext.h"
 #include "kg_kernels.h"
 
@@ -757,7 +758,51 @@ __global__ __launch_bounds__(256) void k_scatter_keys(const uint64_t* src, const
     if (rejected && pstat) pstat[j] = qst[j];
 }
 
-// One replay step (see file header). buckets: [3][128] ring of per-DeviceShare-score best keys.
+// Winner of pod `step` (one wave: the last workgroup of the step's launch, after every other workgroup evaluated the
+// pod): NormalizeScore of DeviceShare from the score buckets (M = the highest raw score among the feasible nodes; a
+// bucket's key is base total << 32 | index, so key(b) = base + w_dev * 100 s / M) and, with reservation views, of
+// Reservation (the listed pairs' maximum, or 1000 and the preferred node at 1000 when a reservation order exists,
+// total_ext). A pair off the list has a zero Reservation term, so its bucket key is its total; a listed pair's bucket
+// key is a lower bound of its total: the maximum over the buckets and the list is the winner.
+__device__ __forceinline__ uint64_t ext_replay_pick(uint32_t step, uint32_t n_nodes, const KCfg& cfg,
+                                                    const uint64_t* __restrict__ buckets, const RsvStep* __restrict__ rs,
+                                                    const uint64_t* __restrict__ rlist) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t* B = buckets + (size_t)(step % 3) * 128;
+    const uint64_t b0 = B[lane], b1 = B[lane + 64];
+    const int32_t M = wmax_i32(max(b0 ? (int32_t)lane : -1, b1 ? (int32_t)lane + 64 : -1));
+    if (M < 0) return 0ull;  // no feasible node (a listed pair is also in its bucket)
+    auto cand = [&](uint64_t b, int64_t sd) -> uint64_t {
+        if (!b) return 0ull;
+        const int64_t tot = (int64_t)(b >> 32) + (int64_t)cfg.w_dev * norm100(sd, M);
+        return ((uint64_t)tot << 32) | (b & 0xFFFFFFFFull);
+    };
+    const uint64_t c0 = cand(b0, lane), c1 = cand(b1, lane + 64);
+    uint64_t best = c0 > c1 ? c0 : c1;
+    if (rs) {
+        const RsvStep& z = rs[step % 3];
+        const uint64_t pf = z.pref;
+        const int64_t rm = pf != PREF_NONE ? 1000 : (int64_t)z.rmax;
+        const uint32_t cnt = z.cnt;
+        const uint64_t* L = rlist + (size_t)(step % 3) * n_nodes * 2;
+        for (uint32_t k = lane; k < cnt; k += 64) {
+            const uint64_t kb = L[2 * (size_t)k], sc = L[2 * (size_t)k + 1];
+            const uint32_t g = 0xFFFFFFFFu - (uint32_t)(kb & 0xFFFFFFFFull);
+            const int64_t sd = (int64_t)(uint32_t)(sc >> 32);
+            const int64_t rsv = (pf != PREF_NONE && (uint32_t)pf == g) ? 1000 : (int64_t)(uint32_t)sc;
+            const int64_t tot = (int64_t)(kb >> 32) + (int64_t)cfg.w_dev * norm100(sd, M) + (int64_t)cfg.w_rsv * norm100(rsv, rm);
+            const uint64_t key = ((uint64_t)tot << 32) | (kb & 0xFFFFFFFFull);
+            best = key > best ? key : best;
+        }
+    }
+    return wmax_u64(best);
+}
+
+// One replay step (see file header). buckets: [3][128] ring of per-DeviceShare-score best keys. winners[step - 1] holds
+// the key the previous launch picked for pod step - 1; every workgroup drops it when the pair's Reserve fails (zone code
+// of its pair, or a cpuset Reserve that failed in between, k_cpuset_reserve), applies the Reserve, gates and evaluates
+// pod `step`. The last workgroup to finish (done counter) then picks pod step's winner into winners[step] and settles
+// winners[step - 1] (0 when its Reserve failed): no other launch per step.
 template <bool EXACT>
 __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
                                                    DevRec* __restrict__ devs, ExtDev e, PodsDev pods, uint32_t n_pods,
@@ -767,36 +812,17 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
                                                    uint64_t* __restrict__ buckets, int8_t* __restrict__ zsel,
                                                    uint32_t* __restrict__ reason, const uint32_t* __restrict__ pos,
                                                    int32_t* __restrict__ nsel, RsvStep* __restrict__ rs,
-                                                   uint64_t* __restrict__ rlist) {
+                                                   uint64_t* __restrict__ rlist, uint32_t* __restrict__ done) {
     const uint32_t step = (step_base ? *step_base : 0u) + step_off;
     if (step > n_pods) return;  // uniform
     const uint32_t lane = threadIdx.x;
     const uint32_t i = blockIdx.x * 64u + lane;
     const bool live = i < n_nodes;
     const bool has_next = step < n_pods;
-    // winner of the previous step from its score buckets: M = highest DeviceShare raw score among the
-    // feasible nodes; key = (base + w_dev * 100 s / M) << 32 | index. With reservation views the Reservation
-    // score term joins: k_ext_replay_pick combined both into rs[(step - 1) % 3].win
-    uint64_t prev = 0;
-    if (rs) {
-        if (step > 0) prev = rs[(step - 1) % 3].win;
-    } else if (step > 0) {
-        const uint64_t* B = buckets + (size_t)((step - 1) % 3) * 128;
-        const uint64_t b0 = B[lane], b1 = B[lane + 64];
-        const int32_t M = wmax_i32(max(b0 ? (int32_t)lane : -1, b1 ? (int32_t)lane + 64 : -1));
-        if (M >= 0) {
-            auto cand = [&](uint64_t b, int64_t s) -> uint64_t {
-                if (!b) return 0ull;
-                const int64_t tot = (int64_t)(b >> 32) + (int64_t)cfg.w_dev * norm100(s, M);
-                return ((uint64_t)tot << 32) | (b & 0xFFFFFFFFull);
-            };
-            const uint64_t c0 = cand(b0, lane), c1 = cand(b1, lane + 64);
-            prev = wmax_u64(c0 > c1 ? c0 : c1);
-        }
-    }
-    // the winner's Reserve fails (BestEffort NUMA allocation: zone code of its pair): the pod stays unscheduled.
-    // zsel is double-buffered by step parity: every block reads the previous step's codes while this step's
-    // are written
+    uint64_t prev = step > 0 ? __hip_atomic_load(&winners[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    // the winner's Reserve fails (BestEffort NUMA allocation, or a cpuset Reserve that failed between the launches: zone
+    // code of its pair): the pod stays unscheduled. zsel is double-buffered by step parity: every block reads the
+    // previous step's codes while this step's are written
     int32_t prev_zone = -1;
     if (prev != 0ull) {
         prev_zone = zsel[(size_t)((step - 1) & 1u) * n_nodes + pos[(0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull)) - index_base]];
@@ -806,11 +832,10 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
         }
     }
     if (blockIdx.x == 0) {
-        uint64_t* Z = buckets + (size_t)((step + 1) % 3) * 128;  // last read at step - 1
+        uint64_t* Z = buckets + (size_t)((step + 1) % 3) * 128;  // last read by the pick of step - 2
         Z[lane] = 0;
         Z[lane + 64] = 0;
-        if (lane == 0 && step > 0) winners[step - 1] = prev;
-        if (rs && lane == 0) {  // slot of step + 1 (last read at step - 1)
+        if (rs && lane == 0) {  // slot of step + 1 (last read by the pick of step - 2)
             RsvStep& z = rs[(step + 1) % 3];
             z.win = 0;
             z.pref = PREF_NONE;
@@ -836,7 +861,8 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
         }
     }
     // ElasticQuota: buffer (step-1)&1 holds the state after pods < step-1; buffer step&1 becomes the
-    // state after pods < step (block 0, nobody reads it during this launch)
+    // state after pods < step (block 0, nobody reads it during this launch). winners[step - 2] was settled by the last
+    // workgroup of the previous launch.
     uint32_t qst = 0;
     PodV p = load_pod(pods, has_next ? step : 0);
     PodX px = load_podx(pods, has_next ? step : 0);
@@ -866,106 +892,81 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
             if (placed1 && x1.quota >= 0 && (uint32_t)x1.quota < nq) quota_add(wr[x1.quota], p1, x1, 1);
         }
     }
-    if (!has_next) return;  // the final step only applies the last Reserve
-    uint64_t kb = 0;
-    int32_t s = 0;
-    uint32_t stat = 0;
-    if (live) {
-        const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, qst);
-        zsel[(size_t)(step & 1u) * n_nodes + i] = (int8_t)r.zone;
-        if (nsel) nsel[(size_t)(step & 1u) * n_nodes + i] = r.nom;
-        stat = r.status;
-        if (!r.status) {
-            const int64_t base = (int64_t)cfg.w_nrf * r.s_nrf + (int64_t)cfg.w_la * r.s_la + (int64_t)cfg.w_numa * r.s_numa;
-            const uint32_t g = index_base + node_index(nodes[i]);
-            kb = ((uint64_t)base << 32) | (uint64_t)(0xFFFFFFFFu - g);
-            s = (int32_t)r.s_dev;
-            if (rs && (r.s_rsv != 0 || r.order != 0)) {
-                // a pair whose Reservation score term can be nonzero: listed for k_ext_replay_pick (its bucket
-                // entry stays, a lower bound of its total)
-                RsvStep& z = rs[step % 3];
-                const uint32_t at = atomicAdd(&z.cnt, 1u);
-                rlist[((size_t)(step % 3) * n_nodes + at) * 2] = kb;
-                rlist[((size_t)(step % 3) * n_nodes + at) * 2 + 1] = ((uint64_t)(uint32_t)r.s_dev << 32) | (uint32_t)r.s_rsv;
-                if (r.s_rsv) atomicMax(&z.rmax, (uint32_t)r.s_rsv);
-                if (r.order != 0) atomicMin((unsigned long long*)&z.pref, (unsigned long long)pref_key(r.order, g));
+    if (has_next) {  // the final step only applies the last Reserve
+        uint64_t kb = 0;
+        int32_t s = 0;
+        uint32_t stat = 0;
+        if (live) {
+            const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, qst);
+            zsel[(size_t)(step & 1u) * n_nodes + i] = (int8_t)r.zone;
+            if (nsel) nsel[(size_t)(step & 1u) * n_nodes + i] = r.nom;
+            stat = r.status;
+            if (!r.status) {
+                const int64_t base = (int64_t)cfg.w_nrf * r.s_nrf + (int64_t)cfg.w_la * r.s_la + (int64_t)cfg.w_numa * r.s_numa;
+                const uint32_t g = index_base + node_index(nodes[i]);
+                kb = ((uint64_t)base << 32) | (uint64_t)(0xFFFFFFFFu - g);
+                s = (int32_t)r.s_dev;
+                if (rs && (r.s_rsv != 0 || r.order != 0)) {
+                    // a pair whose Reservation score term can be nonzero: listed for the pick (its bucket entry stays, a
+                    // lower bound of its total)
+                    RsvStep& z = rs[step % 3];
+                    const uint32_t at = atomicAdd(&z.cnt, 1u);
+                    rlist[((size_t)(step % 3) * n_nodes + at) * 2] = kb;
+                    rlist[((size_t)(step % 3) * n_nodes + at) * 2 + 1] = ((uint64_t)(uint32_t)r.s_dev << 32) | (uint32_t)r.s_rsv;
+                    if (r.s_rsv) atomicMax(&z.rmax, (uint32_t)r.s_rsv);
+                    if (r.order != 0) atomicMin((unsigned long long*)&z.pref, (unsigned long long)pref_key(r.order, g));
+                }
             }
         }
-    }
-    if (reason) {  // FitError diagnosis: OR of the filter status bits over the nodes
+        if (reason) {  // FitError diagnosis: OR of the filter status bits over the nodes
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) stat |= (uint32_t)__shfl_xor((int)stat, off, 64);
-        if (lane == 0 && stat) atomicOr(reason + step, stat);
-    }
-    // per-score-bucket wave max, one atomic per distinct score in the wave
-    uint64_t* B = buckets + (size_t)(step % 3) * 128;
-    bool pending = kb != 0ull;
-    uint64_t m = __ballot(pending);
-    while (m) {
-        const int leader = __ffsll((long long)m) - 1;
-        const int32_t sl = __shfl(s, leader, 64);
-        const bool mine = pending && s == sl;
-        const uint64_t v = wmax_u64(mine ? kb : 0ull);
-        if ((int)lane == leader) atomicMax((unsigned long long*)(B + sl), (unsigned long long)v);
-        pending = pending && !mine;
-        m = __ballot(pending);
-    }
-}
-
-// Winner of a replay step with reservation views (one workgroup, after k_ext_replay evaluated pod `step`):
-// NormalizeScore of DeviceShare (M from the score buckets) and of Reservation (the listed pairs' maximum, or 1000 and
-// the preferred node at 1000 when a reservation order exists, total_ext). A pair off the list has a zero Reservation
-// term, so its bucket key is its total; a listed pair's bucket key is a lower bound of its total: the maximum over
-// the buckets and the list is the step's winner.
-__global__ __launch_bounds__(256) void k_ext_replay_pick(uint32_t n_pods, uint32_t n_nodes, KCfg cfg,
-                                                        const uint32_t* __restrict__ step_base, uint32_t step_off,
-                                                        const uint64_t* __restrict__ buckets, RsvStep* __restrict__ rs,
-                                                        const uint64_t* __restrict__ rlist) {
-    const uint32_t step = (step_base ? *step_base : 0u) + step_off;
-    if (step >= n_pods) return;  // uniform
-    __shared__ int32_t s_m[4];
-    __shared__ uint64_t s_k[4];
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    const uint64_t* B = buckets + (size_t)(step % 3) * 128;
-    const uint64_t b = t < 128 ? B[t] : 0ull;
-    const int32_t mw = wmax_i32(b ? (int32_t)t : -1);
-    if (lane == 0) s_m[w] = mw;
-    __syncthreads();
-    const int32_t M = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
-    RsvStep& z = rs[step % 3];
-    const uint64_t pf = z.pref;
-    const int64_t rm = pf != PREF_NONE ? 1000 : (int64_t)z.rmax;
-    uint64_t best = 0;
-    if (M >= 0) {
-        if (b) best = ((uint64_t)((int64_t)(b >> 32) + (int64_t)cfg.w_dev * norm100((int64_t)t, M)) << 32) | (b & 0xFFFFFFFFull);
-        const uint32_t cnt = z.cnt;
-        const uint64_t* L = rlist + (size_t)(step % 3) * n_nodes * 2;
-        for (uint32_t k = t; k < cnt; k += 256) {
-            const uint64_t kb = L[2 * (size_t)k], sc = L[2 * (size_t)k + 1];
-            const uint32_t g = 0xFFFFFFFFu - (uint32_t)(kb & 0xFFFFFFFFull);
-            const int64_t sd = (int64_t)(uint32_t)(sc >> 32);
-            const int64_t rsv = (pf != PREF_NONE && (uint32_t)pf == g) ? 1000 : (int64_t)(uint32_t)sc;
-            const int64_t tot = (int64_t)(kb >> 32) + (int64_t)cfg.w_dev * norm100(sd, M) + (int64_t)cfg.w_rsv * norm100(rsv, rm);
-            const uint64_t key = ((uint64_t)tot << 32) | (kb & 0xFFFFFFFFull);
-            best = key > best ? key : best;
+            for (int off = 32; off > 0; off >>= 1) stat |= (uint32_t)__shfl_xor((int)stat, off, 64);
+            if (lane == 0 && stat) atomicOr(reason + step, stat);
+        }
+        // per-score-bucket wave max, one atomic per distinct score in the wave
+        uint64_t* B = buckets + (size_t)(step % 3) * 128;
+        bool pending = kb != 0ull;
+        uint64_t m = __ballot(pending);
+        while (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            const int32_t sl = __shfl(s, leader, 64);
+            const bool mine = pending && s == sl;
+            const uint64_t v = wmax_u64(mine ? kb : 0ull);
+            if ((int)lane == leader) atomicMax((unsigned long long*)(B + sl), (unsigned long long)v);
+            pending = pending && !mine;
+            m = __ballot(pending);
         }
     }
-    const uint64_t bw = wmax_u64(best);
-    if (lane == 0) s_k[w] = bw;
-    __syncthreads();
-    if (t == 0) {
-        uint64_t m = s_k[0];
-        for (int k = 1; k < 4; k++) m = s_k[k] > m ? s_k[k] : m;
-        z.win = m;
+    // the last workgroup of the launch: pick pod step's winner, settle pod step-1's
+    __threadfence();  // this workgroup's list entries / bucket atomics before its arrival
+    uint32_t ticket = 0;
+    if (lane == 0) ticket = atomicAdd(done, 1u);
+    ticket = (uint32_t)__shfl((int)ticket, 0, 64);
+    if (ticket != gridDim.x - 1u) return;  // uniform per workgroup
+    __threadfence();  // every other workgroup's writes are visible from here
+    if (has_next) {
+        const uint64_t w = ext_replay_pick(step, n_nodes, cfg, buckets, rs, rlist);
+        if (lane == 0) winners[step] = w;
+    }
+    if (lane == 0) {
+        if (step > 0 && prev == 0ull) winners[step - 1] = 0ull;  // the Reserve failed: unscheduled
+        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 // Reserve (sign +1: zone and minors chosen here, or preset in out by an evaluation pass) / Unreserve (sign -1: the
 // given zone and minors). sign 0: the evaluation pass alone, which presets out for a cpuset Reserve and the Reserve.
+// out: [0] zone, [1] minors, [2] nominated reservation (index into e.infos), [3] its rid (-1 = none).
+// split (nullable): the NUMA allocation's per-zone amounts (cpu, then memory), written by a Reserve (zeroed by the
+// caller; a cpuset Reserve under a NUMA affinity wrote them already) and given back by an Unreserve with the zone code
+// 0x40 | mask. rsv: Reservation.Reserve / Unreserve on the node's views (an Unreserve into the reservation rid_in).
+// cpus (Unreserve, nullable): the cpuset CPUs to release (NodeAllocation.release).
 template <bool EXACT>
 __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, DevRec* __restrict__ devs, ExtDev e,
                              PodsDev pods, uint32_t pod, uint32_t rec, int32_t zone_in, uint32_t minors_in, int64_t sign,
-                             KCfg cfg, int32_t* __restrict__ out) {
+                             KCfg cfg, int32_t* __restrict__ out, int64_t* __restrict__ split, bool rsv, int32_t rid_in,
+                             kg_cpu_alloc* __restrict__ allocs, const kg_cpu_topo* __restrict__ topos,
+                             const uint64_t* __restrict__ cpus) {
     if (blockIdx.x != 0) return;
     // the whole wave evaluates (uniform work on a full exec mask), lane 0 applies
     const PodV q = load_pod(pods, pod);
@@ -1003,10 +1004,13 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     }
     __syncthreads();  // every lane has read the state before lane 0 changes it
     if (threadIdx.x != 0) return;
-    apply_assume(cfg, n, zones + rec, q, zone, sign);
+    if (sign < 0 && cpus && allocs && topos) cpuset_release_lane(nodes, zones, allocs, topos, rec, cpus);
+    apply_assume(cfg, n, zones + rec, q, zone, sign, split);
     if ((cfg.plugins & KG_PLUGIN_DEV) && devs && qx.dcount > 0) dev_apply(devs + rec, mask, qx, sign);
-    // Reservation.Reserve (sign +1 only: an Unreserve does not know the reservation; the runtime marks the views stale)
-    if (sign > 0 && (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
+    if (rsv && (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views) {
+        if (sign > 0) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
+        else rsv_unreserve_dev(e, n, zones + rec, rec, q, rid_in);
+    }
     if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
         quota_add(e.qstate[qx.quota], q, qx, sign);
         quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, sign);
@@ -1014,6 +1018,8 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     if (out) {
         out[0] = zone;
         out[1] = (int32_t)mask;
+        out[2] = nom;
+        out[3] = nom >= 0 ? (int32_t)e.infos[nom].rid : -1;
     }
 }
 
@@ -1373,25 +1379,29 @@ hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, 
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
                                   uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, int32_t* nsel,
-                                  RsvStep* rs, uint64_t* rlist, hipStream_t s) {
+                                  RsvStep* rs, uint64_t* rlist, uint32_t* done, hipStream_t s) {
+    if (n_nodes == 0 || !done) return hipErrorInvalidValue;  // a zero grid would be a malformed dispatch
     dim3 grid((n_nodes + 63) / 64), block(64);
     if (exact)
         k_ext_replay<true><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                  step_off, winners, minors, buckets, zsel, reason, pos, nsel, rs, rlist);
+                                                  step_off, winners, minors, buckets, zsel, reason, pos, nsel, rs, rlist, done);
     else
         k_ext_replay<false><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                   step_off, winners, minors, buckets, zsel, reason, pos, nsel, rs, rlist);
-    if (rs) k_ext_replay_pick<<<1, 256, 0, s>>>(n_pods, n_nodes, cfg, step_base, step_off, buckets, rs, rlist);
+                                                   step_off, winners, minors, buckets, zsel, reason, pos, nsel, rs, rlist,
+                                                   done);
     return hipGetLastError();
 }
 
 hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                              uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
-                             bool exact, int32_t* out, hipStream_t s) {
+                             bool exact, int32_t* out, hipStream_t s, int64_t* split, bool rsv, int32_t rid,
+                             kg_cpu_alloc* allocs, const kg_cpu_topo* topos, const uint64_t* cpus) {
     if (exact)
-        k_ext_assume<true><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, pod, rec, zone, minors, sign, cfg, out);
+        k_ext_assume<true><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, pod, rec, zone, minors, sign, cfg, out, split, rsv,
+                                            rid, allocs, topos, cpus);
     else
-        k_ext_assume<false><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, pod, rec, zone, minors, sign, cfg, out);
+        k_ext_assume<false><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, pod, rec, zone, minors, sign, cfg, out, split, rsv,
+                                             rid, allocs, topos, cpus);
     return hipGetLastError();
 }
 

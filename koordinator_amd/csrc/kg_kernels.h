@@ -150,10 +150,15 @@ hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, 
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
                                   uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, int32_t* nsel,
-                                  RsvStep* rs, uint64_t* rlist, hipStream_t s);
+                                  RsvStep* rs, uint64_t* rlist, uint32_t* done, hipStream_t s);
+// k_ext_assume: Reserve (sign 1, sign 0 = its evaluation pass) / Unreserve (sign -1) with every enabled plugin; rsv:
+// Reservation.Reserve / Unreserve on the node's views (rid: the reservation an Unreserve leaves); split: the NUMA
+// allocation's per-zone amounts; cpus: the cpuset CPUs an Unreserve releases
 hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                              uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
-                             bool exact, int32_t* out, hipStream_t s);
+                             bool exact, int32_t* out, hipStream_t s, int64_t* split = nullptr, bool rsv = true,
+                             int32_t rid = -1, kg_cpu_alloc* allocs = nullptr, const kg_cpu_topo* topos = nullptr,
+                             const uint64_t* cpus = nullptr);
 // batch of cpuset accumulator requests (kg_cpuset.hip)
 hipError_t launch_cpuset_take(const kg_cpu_topo* topos, const kg_cpu_alloc* allocs, const kg_cpuset_request* reqs,
                               uint32_t n, uint64_t* out, int32_t* rc, hipStream_t s);
@@ -161,7 +166,8 @@ hipError_t launch_cpuset_take(const kg_cpu_topo* topos, const kg_cpu_alloc* allo
 hipError_t launch_cpuset_reserve(NodeRec* nodes, ZoneRec* zones, kg_cpu_alloc* allocs, const kg_cpu_topo* topos,
                                  const PodsDev& pods, const KCfg& cfg, uint32_t pod, uint32_t rec, const uint64_t* winners,
                                  const uint32_t* step_base, uint32_t step_off, const uint32_t* pos, uint32_t index_base,
-                                 uint32_t n_pods, int8_t* zsel, int32_t* fail_out, hipStream_t s);
+                                 uint32_t n_pods, int8_t* zsel, int32_t* fail_out, hipStream_t s, uint32_t zsel_stride = 0,
+                                 uint64_t* taken_out = nullptr);
 // inline batch cycle of a whole-job plan (k_batch); ext = the snapshot carries the config-5 tables
 hipError_t launch_batch(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                         const uint32_t* grp_begin, const uint32_t* grp_pods, const uint32_t* grp_rec, uint32_t n_groups,

@@ -144,6 +144,10 @@ struct alignas(64) ZoneRec {
     // (required FullPCPUs), the cores with a free CPU (required SpreadByPCPUs), and the allocated CPUs (RefCount > 0,
     // the amplified zone accounting of zone_cpu_alloc)
     uint16_t cz_free[MAX_ZONES], cz_full[MAX_ZONES], cz_cores[MAX_ZONES], cz_alloc[MAX_ZONES];
+    // per NUMA node the cpuset pods in NodeAllocation.singleNUMANode / sharedNode (node_allocation.go:111-143): the
+    // statuses (bits 0-7 of status) follow from them, and a cpuset Release takes its pod out again
+    // (kg_node_columns.numa_zone_pods; saturating at 255)
+    uint8_t cz_single[MAX_ZONES], cz_shared[MAX_ZONES];
 };
 static_assert(sizeof(ZoneRec) == 704, "ZoneRec: zones, fast zone view, cpuset counts, GPU topology");
 // ZoneRec.status bit ZONE_RECORD_SHIFT + z: zone z holds an allocatedResources record (kg_node_columns.numa_zone_status)
@@ -214,19 +218,14 @@ KG_HD inline __attribute__((always_inline)) void cpu_counts(const kg_cpu_topo& t
     }
 }
 
-// NUMANodeSharedStatus after a cpuset allocation over the NUMA nodes `used` (bit per node): the pod's uid
-// joins singleNUMANode of its one node, or sharedNode of each of several (node_allocation.go:111-143);
-// a zone's status is then shared if any shared pod is there, single if only single pods, idle if none
-// (NUMANodeSharedStatus :60-68). Status bits cover zones < MAX_ZONES.
-KG_HD inline uint32_t cpuset_zone_status(uint32_t status, uint32_t used) {
-    const bool multi = (used & (used - 1)) != 0;
-    for (uint32_t q = 0; q < 4u; q++) {
-        if (!((used >> q) & 1u)) continue;
-        const uint32_t s = (status >> (2 * q)) & 3u;
-        const uint32_t ns = multi ? 2u : (s == 0u ? 1u : s);
-        status = (status & ~(3u << (2 * q))) | (ns << (2 * q));
-    }
-    return status;
+// NUMANodeSharedStatus (node_allocation.go:60-68) from the zone's single / shared pod counts: shared if any shared pod
+// is there, single if only single pods, idle if none; the other status bits (allocation records) are kept. Status bits
+// cover zones < MAX_ZONES.
+KG_HD inline uint32_t zone_status_of_counts(const ZoneRec& z) {
+    uint32_t st = z.status & ~0xFFu;
+    for (uint32_t q = 0; q < (uint32_t)MAX_ZONES; q++)
+        st |= (z.cz_shared[q] ? 2u : z.cz_single[q] ? 1u : 0u) << (2 * q);
+    return st;
 }
 
 // Zone code of a pair whose Reserve fails (BestEffort allocation): 0x20 | KG_ST_NUMA_INSUF_* >> 12.
@@ -473,7 +472,7 @@ struct alignas(16) RsvInfo {
 
 // Replay with reservation views: per step (ring of 3) the pairs whose Reservation score term can be nonzero (a
 // nominated reservation's score or a reservation order), its maximum and the preferred-node key, and the step's
-// winner (k_ext_replay_pick).
+// winner (picked by the step launch's last workgroup).
 struct alignas(16) RsvStep {
     uint64_t win;   // winning key of the step (0 = none)
     uint64_t pref;  // min pref_key over the feasible pairs with an order (~0 = none)

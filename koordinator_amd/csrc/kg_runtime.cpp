@@ -227,7 +227,9 @@ struct kg_pods {
     uint64_t* d_pref = nullptr;
     uint32_t* d_minors = nullptr;     // replay: GPU minors chosen per pod
     uint64_t* d_buckets = nullptr;    // replay: [3][128] per-score best keys
+    uint32_t* d_done = nullptr;       // config-5 replay: workgroups done in the current step launch (last one picks)
     int32_t* d_aout = nullptr;        // kg_assume_ext outputs
+    uint64_t* d_rec = nullptr;        // kg_reserve / kg_unreserve: cpuset CPUs [4] + NUMA zone amounts [8]
     uint32_t* d_batch = nullptr;      // kg_batch_schedule: groups + per-pod outputs (7 x cap + 1 words)
     hipGraphExec_t xexec = nullptr;   // ext replay graph
     std::vector<uint8_t> xkey;
@@ -509,6 +511,18 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
         zf.hpack = pack_f32(half_rcp((hc + hm) / 2), half_rcp((fc + fm) / 2));
     }
     zr->status = COL(s->numa_zone_status, i);
+    // the cpuset pods behind the statuses (a Release takes its pod out of them): given, or one per non-idle status
+    for (int z = 0; z < MAX_ZONES; z++) {
+        if (s->numa_zone_pods) {
+            zr->cz_single[z] = (uint8_t)(s->numa_zone_pods[i] >> (8 * z));
+            zr->cz_shared[z] = (uint8_t)(s->numa_zone_pods[i] >> (8 * (MAX_ZONES + z)));
+        } else {
+            const uint32_t st = (zr->status >> (2 * z)) & 3u;
+            zr->cz_single[z] = st == 1u ? 1 : 0;
+            zr->cz_shared[z] = st >= 2u ? 1 : 0;
+        }
+    }
+    if (s->numa_zone_pods) zr->status = zone_status_of_counts(*zr);
     zr->amp_ratio = ratio > 1 ? ratio : 1.0;
     zr->cpu_topo = -1;
     zr->cpu_meta = 1u;
@@ -1180,6 +1194,12 @@ kg_status kg_snapshot_read_state(kg_snap* s, kg_node_state* o) {
         }
         if (o->cpuset_alloc_milli) o->cpuset_alloc_milli[i] = v[N_CPUSET];
         if (o->numa_zone_status) o->numa_zone_status[i] = zr.status;
+        if (o->numa_zone_pods) {
+            uint64_t w = 0;
+            for (int zz = 0; zz < MAX_ZONES; zz++)
+                w |= (uint64_t)zr.cz_single[zz] << (8 * zz) | (uint64_t)zr.cz_shared[zz] << (8 * (MAX_ZONES + zz));
+            o->numa_zone_pods[i] = w;
+        }
         if (o->cpu_alloc) {
             if (!ca.empty()) o->cpu_alloc[i] = ca[pp];
             else std::memset(&o->cpu_alloc[i], 0, sizeof(kg_cpu_alloc));
@@ -1550,7 +1570,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
                     (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
                     (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
-                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_gz, (void*)p->d_spec, (void*)p->d_split, (void*)p->d_batch, (void*)p->d_rcode})
+                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_gz, (void*)p->d_spec, (void*)p->d_split, (void*)p->d_batch, (void*)p->d_rcode, (void*)p->d_done, (void*)p->d_rec})
         hipFree(b);
     hipHostFree(p->h_in);
     hipHostFree(p->h_keys);
@@ -2326,6 +2346,12 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     RsvStep* rs = rsv_replay(s) ? s->d_rstep : nullptr;
     put(&rs, sizeof(rs));
     put(&s->d_rlist, sizeof(s->d_rlist));
+    const bool cs = cpuset_active(s, p);
+    put(&cs, sizeof(cs));
+    put(&s->d_cpu_alloc, sizeof(s->d_cpu_alloc));
+    put(&s->d_cpu_topos, sizeof(s->d_cpu_topos));
+    put(&s->d_pos, sizeof(s->d_pos));
+    put(&p->d_done, sizeof(p->d_done));
     if (p->xexec && key == p->xkey) return KG_OK;
     if (p->xexec) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -2335,12 +2361,20 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     hipGraph_t graph = nullptr;
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
     hipError_t err = hipSuccess;
-    for (uint32_t t = 0; t < REPLAY_G && err == hipSuccess; t++)
-        err = launch_ext_replay_step(s->d_nodes, s->d_zones, s->d_dev, e, p->dev, p->n, s->n, s->base, s->kcfg, exact,
-                                     p->d_step, t, p->d_winners, p->d_minors, p->d_buckets, s->d_zsel,
-                                     reasons ? p->d_reason : nullptr, s->d_pos,
-                                     (s->cfg.plugins & KG_PLUGIN_RSV) ? s->d_nsel : nullptr, rs, s->d_rlist,
-                                     ctx->stream);
+    for (uint32_t t = 0; t < REPLAY_G && err == hipSuccess; t++) {
+        // the previous pod's cpuset Reserve runs before the step that applies its other Reserves (zone codes of its
+        // step in the step-parity half of zsel)
+        if (cs)
+            err = launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, 0, 0,
+                                        p->d_winners, p->d_step, t, s->d_pos, s->base, p->n, s->d_zsel, nullptr, ctx->stream,
+                                        s->n);
+        if (err == hipSuccess)
+            err = launch_ext_replay_step(s->d_nodes, s->d_zones, s->d_dev, e, p->dev, p->n, s->n, s->base, s->kcfg, exact,
+                                         p->d_step, t, p->d_winners, p->d_minors, p->d_buckets, s->d_zsel,
+                                         reasons ? p->d_reason : nullptr, s->d_pos,
+                                         (s->cfg.plugins & KG_PLUGIN_RSV) ? s->d_nsel : nullptr, rs, s->d_rlist,
+                                         p->d_done, ctx->stream);
+    }
     if (err == hipSuccess) err = launch_bump(p->d_step, REPLAY_G, ctx->stream);
     hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
     if (err == hipSuccess) err = ec;
@@ -2491,7 +2525,6 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
     if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->rsv_gpu)
         return fail(ctx, KG_UNSUPPORTED, "replay with reservations holding GPUs (their DeviceShare restore tables change "
                                          "with every placement)");
-    if (cpuset_active(s, p)) return fail(ctx, KG_UNSUPPORTED, "config-5 replay with cpuset-binding pods");
     kg_status st = check_ext(s);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -2501,6 +2534,8 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
         HIP_TRY(ctx, hipMalloc(&s->d_rstep, sizeof(RsvStep) * 3));
         HIP_TRY(ctx, hipMalloc(&s->d_rlist, sizeof(uint64_t) * 2 * 3 * (size_t)std::max<uint32_t>(s->n, 1)));
     }
+    if (!p->d_done) HIP_TRY(ctx, hipMalloc(&p->d_done, sizeof(uint32_t)));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_done, 0, sizeof(uint32_t), ctx->stream));
     st = ext_replay_graph(s, p, exact, out_reason != nullptr);
     if (st != KG_OK) return st;
     if (rsv_replay(s)) {
@@ -2576,7 +2611,7 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
                                            ctx->stream));
     }
     HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone, minors,
-                                   sign, s->kcfg, force_exact(), p->d_aout, ctx->stream));
+                                   sign, s->kcfg, force_exact(), p->d_aout, ctx->stream, nullptr, sign > 0));
     s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     int32_t o[2] = {-1, 0};
@@ -2599,6 +2634,98 @@ kg_status kg_forget_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, int
     if (s && p && node < s->n && cpuset_bound(s, p, pod, node))
         return fail(s->ctx, KG_UNSUPPORTED, "Unreserve of a cpuset allocation");
     return assume_ext(s, p, pod, node, zone, minors, -1, nullptr, nullptr);
+}
+
+// ---- Reserve / Unreserve with the allocation record -------------------------------------------------------------
+
+kg_status kg_reserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, kg_reserve_record* out) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    if (!out) return fail(ctx, KG_INVALID_ARG, "null record");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
+    if (s->ext()) {
+        st = check_ext(s);
+        if (st != KG_OK) return st;
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!p->d_rec) HIP_TRY(ctx, hipMalloc(&p->d_rec, sizeof(uint64_t) * 16));
+    // Reservation.Reserve follows the node's views on the device unless a reservation there holds GPUs (their DeviceShare
+    // restore tables follow the reserve pods' allocations: the caller re-uploads the node's views)
+    const bool rsv = (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && !s->rsv_gpu;
+    if (!rsv) touch_views(s, node);
+    else if (node < s->cls_mask.size() && s->cls_mask[node]) s->views_on_device = true;
+    HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 4, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_rec, 0, sizeof(uint64_t) * 16, ctx->stream));
+    const ExtDev e = s->ext_dev();
+    const uint32_t rec = s->pos[node];
+    if (s->has_cpu) {
+        // the pair evaluated before the cpuset take changes the counts it reads (zone, minors, reservation preset)
+        HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, e, p->dev, pod, rec, -1, 0, 0, s->kcfg,
+                                       force_exact(), p->d_aout, ctx->stream, nullptr, rsv));
+        HIP_TRY(ctx, launch_cpuset_reserve(s->d_nodes, s->d_zones, s->d_cpu_alloc, s->d_cpu_topos, p->dev, s->kcfg, pod, rec,
+                                           nullptr, nullptr, 0, s->d_pos, s->base, p->n, nullptr, p->d_aout, ctx->stream, 0,
+                                           p->d_rec));
+    }
+    HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, e, p->dev, pod, rec, -1, 0, 1, s->kcfg, force_exact(),
+                                   p->d_aout, ctx->stream, reinterpret_cast<int64_t*>(p->d_rec + 4), rsv));
+    s->gen++;
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
+    int32_t o[4] = {-1, 0, -1, -1};
+    uint64_t r[16];
+    HIP_TRY(ctx, hipMemcpyAsync(o, p->d_aout, sizeof(o), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(r, p->d_rec, sizeof(r), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    std::memset(out, 0, sizeof(*out));
+    out->numa_zone = o[0];
+    out->rsv_rid = -1;
+    if (zone_reserve_fails(o[0]))
+        return fail(ctx, KG_RESERVE_FAILED, "Reserve of pod %u on node %u failed: NUMA status 0x%x", pod, node, zone_fail_status(o[0]));
+    out->gpu_minors = (uint32_t)o[1];
+    out->rsv_rid = rsv ? o[3] : -1;
+    for (int w = 0; w < 4; w++) out->cpus[w] = r[w];
+    for (int z = 0; z < 2 * KG_MAX_ZONES; z++) out->zone_amounts[z] = (int64_t)r[4 + z];
+    if (r[0] | r[1] | r[2] | r[3]) out->flags |= KG_RECORD_CPUSET;
+    if (s->ext() && (s->cfg.plugins & KG_PLUGIN_QUOTA) && s->n_quotas) out->flags |= KG_RECORD_QUOTA;
+    return KG_OK;
+}
+
+kg_status kg_unreserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, const kg_reserve_record* rec) {
+    kg_status st = check_pair(s, p);
+    if (st != KG_OK) return st;
+    kg_ctx* ctx = s->ctx;
+    if (!rec) return fail(ctx, KG_INVALID_ARG, "null record");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
+    if (zone_reserve_fails(rec->numa_zone)) return fail(ctx, KG_INVALID_ARG, "the record's Reserve failed: nothing to give back");
+    if (s->ext()) {
+        st = check_ext(s);
+        if (st != KG_OK) return st;
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!p->d_rec) HIP_TRY(ctx, hipMalloc(&p->d_rec, sizeof(uint64_t) * 16));
+    const bool rsv = (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && !s->rsv_gpu;
+    if (!rsv) touch_views(s, node);
+    else if (node < s->cls_mask.size() && s->cls_mask[node]) s->views_on_device = true;
+    uint64_t r[16] = {0};
+    for (int w = 0; w < 4; w++) r[w] = s->has_cpu ? rec->cpus[w] : 0;
+    bool any = false;
+    for (int z = 0; z < 2 * KG_MAX_ZONES; z++) {
+        r[4 + z] = (uint64_t)rec->zone_amounts[z];
+        any = any || rec->zone_amounts[z] != 0;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(p->d_rec, r, sizeof(r), hipMemcpyHostToDevice, ctx->stream));
+    // the NUMA allocation is given back by its recorded per-zone amounts (zone code 0x40 | every zone)
+    const int32_t zone = rec->numa_zone < 0 ? -1 : any ? 0x4F : rec->numa_zone;
+    HIP_TRY(ctx, launch_ext_assume(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, pod, s->pos[node], zone,
+                                   rec->gpu_minors, -1, s->kcfg, force_exact(), nullptr, ctx->stream,
+                                   reinterpret_cast<int64_t*>(p->d_rec + 4), rsv, rec->rsv_rid, s->d_cpu_alloc,
+                                   s->d_cpu_topos, (rec->flags & KG_RECORD_CPUSET) ? p->d_rec : nullptr));
+    s->gen++;
+    HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // r is on this stack
+    return KG_OK;
 }
 
 // ---- cpuset accumulator (batch entry) -----------------------------------------------------------------
@@ -2945,6 +3072,21 @@ static kg_status sync_views_from_device(kg_snap* s) {
         h.allocated_keys = di[t].allocated_keys;
     }
     s->views_on_device = false;
+    return KG_OK;
+}
+
+kg_status kg_snapshot_read_reservations(kg_snap* s, kg_rsv_view* views, uint32_t n_views, kg_rsv_info* infos,
+                                        uint32_t n_infos) {
+    if (!s) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n_views != s->h_views.size() || n_infos != s->h_infos.size() || (n_views && !views) || (n_infos && !infos))
+        return fail(ctx, KG_INVALID_ARG, "%u views / %u infos uploaded", (uint32_t)s->h_views.size(), (uint32_t)s->h_infos.size());
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    kg_status st = sync_views_from_device(s);
+    if (st != KG_OK) return st;
+    std::copy(s->h_views.begin(), s->h_views.end(), views);
+    std::copy(s->h_infos.begin(), s->h_infos.end(), infos);
     return KG_OK;
 }
 

@@ -135,6 +135,12 @@ def lib():
     L.kg_cpuset_take.argtypes = [vp, P(abi.KgCpuTopo), u32, P(abi.KgCpuAlloc), u32, P(abi.KgCpusetRequest), u32,
                                  P(u64), P(i32)]
     L.kg_cpuset_take.restype = st
+    L.kg_reserve.argtypes = [vp, vp, u32, u32, P(abi.KgReserveRecord)]
+    L.kg_reserve.restype = st
+    L.kg_unreserve.argtypes = [vp, vp, u32, u32, P(abi.KgReserveRecord)]
+    L.kg_unreserve.restype = st
+    L.kg_snapshot_read_reservations.argtypes = [vp, P(abi.KgRsvView), u32, P(abi.KgRsvInfo), u32]
+    L.kg_snapshot_read_reservations.restype = st
     if L.kg_abi_version() != abi.KG_ABI_VERSION:
         raise ImportError(f"libkoordgpu ABI {L.kg_abi_version()} != {abi.KG_ABI_VERSION}")
     _lib = L
@@ -276,6 +282,19 @@ class Snapshot:
             C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos,
             C.cast(rsv.devs, C.POINTER(abi.KgRsvDev)), rsv.n_devs), "kg_snapshot_upload_reservations")
 
+    def read_reservations(self, rsv: abi.Reservations) -> abi.Reservations:
+        """The views and infos as the device holds them now (Reservation.Reserve / Unreserve ran there), in the
+        layout of the uploaded `rsv` (same counts; its GPU restore tables are shared)."""
+        out = abi.Reservations([], [])
+        out.views = (abi.KgRsvView * max(1, rsv.n_views))()
+        out.infos = (abi.KgRsvInfo * max(1, rsv.n_infos))()
+        out.n_views, out.n_infos = rsv.n_views, rsv.n_infos
+        out.devs, out.n_devs = rsv.devs, rsv.n_devs
+        self.ctx.check(self.ctx.L.kg_snapshot_read_reservations(
+            self.h, C.cast(out.views, C.POINTER(abi.KgRsvView)), rsv.n_views,
+            C.cast(out.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos), "kg_snapshot_read_reservations")
+        return out
+
     def update_views(self, nodes, rsv: abi.Reservations):
         """kg_snapshot_update_views: the views of `nodes` replaced by rsv's (which name only those nodes)."""
         nd = np.ascontiguousarray(np.asarray(nodes, np.uint32))
@@ -409,6 +428,17 @@ def assume_ext(snap: Snapshot, pods: PodBatch, pod: int, node: int):
 
 def forget_ext(snap: Snapshot, pods: PodBatch, pod: int, node: int, zone: int, minors: int):
     snap.ctx.check(snap.ctx.L.kg_forget_ext(snap.h, pods.h, pod, node, zone, minors), "kg_forget_ext")
+
+
+def reserve(snap: Snapshot, pods: PodBatch, pod: int, node: int) -> abi.KgReserveRecord:
+    """kg_reserve: every enabled plugin's Reserve; the record its kg_unreserve gives back."""
+    rec = abi.KgReserveRecord()
+    snap.ctx.check(snap.ctx.L.kg_reserve(snap.h, pods.h, pod, node, C.byref(rec)), "kg_reserve")
+    return rec
+
+
+def unreserve(snap: Snapshot, pods: PodBatch, pod: int, node: int, rec: abi.KgReserveRecord):
+    snap.ctx.check(snap.ctx.L.kg_unreserve(snap.h, pods.h, pod, node, C.byref(rec)), "kg_unreserve")
 
 
 def batch_schedule(snap: Snapshot, pods: PodBatch, plan_node):

@@ -442,6 +442,54 @@ def cpuset_cluster(n_nodes: int, n_pods: int, seed: int = 0, bind_frac: float = 
     return cfg, t, pt
 
 
+def add_cpusets(t: abi.Table, p: abi.Table, seed: int = 0, bind_frac: float = 0.08, node_bind_frac: float = 0.05):
+    """Cpuset binding on any cluster (own random stream): a CPU topology on every node (2 sockets x 1 NUMA node x
+    cores/2 cores x 2 threads, matching its cpu allocatable before amplification), an existing allocation of up to
+    half the CPUs where cpuset_alloc_milli holds one, node CPU bind policies on a few policy-None nodes, and LSR pods
+    (prod pods with whole-core cpu requests binding cpusets, Full / Spread, a third required, random exclusive
+    policy). Used to put cpuset pods into the config-5 replay and batch cycle."""
+    r = _rng(300 + seed, 9)
+    n, m = abi.table_len(t), abi.table_len(p)
+    ratio = np.where(t["cpu_amp_ratio"] > 1, t["cpu_amp_ratio"], 1.0) if "cpu_amp_ratio" in t else np.ones(n)
+    cores = np.rint(t["alloc_cpu"] / ratio / 1000).astype(np.int64)
+    shapes = {32: 0, 64: 1, 96: 2}
+    topos = [abi.cpu_topo_for_test(2, 1, c // 4, 2) for c in (32, 64, 96)]
+    ti = np.array([shapes.get(int(c), 0) for c in cores], np.int32)
+    ncpu = np.array([32, 64, 96])[ti]
+    alloc = np.zeros((n, 2 * abi.KG_MAX_CPUS), np.uint8)
+    cs = np.zeros(n, np.int64)
+    have = t["cpuset_alloc_milli"] if "cpuset_alloc_milli" in t else np.zeros(n, np.int64)
+    for i in np.nonzero(have > 0)[0]:
+        k = int(min(have[i] // 1000, ncpu[i] // 2))
+        cpus = r.choice(int(ncpu[i]), size=k, replace=False)
+        alloc[i, cpus] = 1
+        alloc[i, abi.KG_MAX_CPUS + cpus] = r.integers(0, 3, k)
+        cs[i] = 1000 * k
+    t["cpu_topo"] = ti
+    t["cpu_topos"] = abi.cpu_topos_array(topos)
+    t["cpu_alloc"] = alloc
+    t["cpu_max_ref"] = np.ones(n, np.uint8)
+    t["cpuset_alloc_milli"] = cs
+    nb = np.zeros(n, np.uint8)
+    pick = (t["numa_policy"] == abi.KG_NUMA_NONE) & (r.random(n) < node_bind_frac)
+    nb[pick & (r.random(n) < 0.5)] = abi.KG_NODE_CPU_BIND_FULL_PCPUS_ONLY
+    nb[pick & (nb == 0)] = abi.KG_NODE_CPU_BIND_SPREAD_BY_PCPUS
+    t["cpu_bind_policy"] = nb
+    t["cpu_strategy"] = r.integers(0, 2, n).astype(np.uint8)
+    bind = (r.random(m) < bind_frac) & ((p["flags"] & abi.KG_POD_PROD) != 0)
+    whole = r.choice([1, 2, 4, 8], m)
+    p["req_cpu"] = np.where(bind, whole * 1000, p["req_cpu"]).astype(np.int64)
+    p["nz_cpu"] = np.where(bind, whole * 1000, p["nz_cpu"]).astype(np.int64)
+    cpol = r.integers(1, 3, m).astype(np.uint32)
+    req = r.random(m) < 1 / 3
+    excl = r.integers(0, 3, m).astype(np.uint32)
+    f = p["flags"].astype(np.uint32)
+    p["flags"] = np.where(bind, f | abi.KG_POD_CPU_BIND | (cpol << abi.KG_POD_CPU_POLICY_SHIFT) |
+                          np.where(req, abi.KG_POD_CPU_REQUIRED, 0).astype(np.uint32) | (excl << abi.KG_POD_CPU_EXCL_SHIFT),
+                          f).astype(np.uint32)
+    return t, p
+
+
 def mixed(n_nodes: int = 10_000, n_pods: int = 10_000, seed: int = 6):
     """A realistic mixed cluster (bench config 6): config 2's nodes and pods, plus
     - kubelet topology-manager policies: 20% SingleNUMANode (as config 2), 10% Restricted, 10% BestEffort;

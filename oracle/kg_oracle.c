@@ -1198,6 +1198,7 @@ struct kgo_state {
     uint32_t n;
     int64_t* col[C_NCOLS];
     uint32_t *la_flags, *numa_policy, *numa_zones, *zone_status;
+    uint64_t* zone_pods; /* cpuset pods per NUMA node: byte z singleNUMANode, byte KG_MAX_ZONES + z sharedNode */
     double* amp;
     int32_t* dev_minors;          /* DeviceShare (NULL when the snapshot has no device tables) */
     int64_t *dev_total, *dev_free; /* [node][KG_DEV_R][KG_DEV_MINORS] */
@@ -1218,6 +1219,32 @@ static int64_t* dup64(const int64_t* s, uint32_t n) {
     int64_t* d = (int64_t*)calloc(n ? n : 1, sizeof(int64_t));
     if (s) memcpy(d, s, sizeof(int64_t) * n);
     return d;
+}
+
+/* NUMANodeSharedStatus (node_allocation.go:60-68) of node i from its single / shared cpuset pod counts; the allocation
+ * record bits stay */
+static void zone_pods_status(kgo_state* st, uint32_t i) {
+    uint32_t x = st->zone_status[i] & ~0xFFu;
+    for (int z = 0; z < KG_MAX_ZONES; z++) {
+        const uint32_t single = (uint32_t)(st->zone_pods[i] >> (8 * z)) & 0xFFu;
+        const uint32_t shared = (uint32_t)(st->zone_pods[i] >> (8 * (KG_MAX_ZONES + z))) & 0xFFu;
+        x |= (shared ? 2u : single ? 1u : 0u) << (2 * z);
+    }
+    st->zone_status[i] = x;
+}
+
+/* addPodAllocation / release (node_allocation.go:111-143,164-200): the pod's uid joins (sign 1) or leaves (-1)
+ * singleNUMANode of its one NUMA node, or sharedNode of each of several (used: NUMA nodes of its CPUs) */
+static void zone_pods_add(kgo_state* st, uint32_t i, uint32_t used, int sign) {
+    const int multi = (used & (used - 1)) != 0;
+    for (int z = 0; z < KG_MAX_ZONES; z++) {
+        if (!((used >> z) & 1u)) continue;
+        const int sh = 8 * (multi ? KG_MAX_ZONES + z : z);
+        int c = (int)((st->zone_pods[i] >> sh) & 0xFFu) + sign;
+        c = c < 0 ? 0 : c > 255 ? 255 : c;
+        st->zone_pods[i] = (st->zone_pods[i] & ~(0xFFull << sh)) | ((uint64_t)c << sh);
+    }
+    zone_pods_status(st, i);
 }
 
 kgo_state* kgo_state_new(const kg_node_columns* s, uint32_t n) {
@@ -1260,6 +1287,19 @@ kgo_state* kgo_state_new(const kg_node_columns* s, uint32_t n) {
     st->amp = (double*)calloc(n ? n : 1, 8);
     st->zone_status = (uint32_t*)calloc(n ? n : 1, 4);
     if (s->numa_zone_status) memcpy(st->zone_status, s->numa_zone_status, 4 * (size_t)n);
+    st->zone_pods = (uint64_t*)calloc(n ? n : 1, 8);
+    for (uint32_t i = 0; i < n; i++) {
+        if (s->numa_zone_pods) {
+            st->zone_pods[i] = s->numa_zone_pods[i];
+            zone_pods_status(st, i);
+        } else { /* one pod per non-idle status */
+            for (int z = 0; z < KG_MAX_ZONES; z++) {
+                const uint32_t x = (st->zone_status[i] >> (2 * z)) & 3u;
+                if (x == 1u) st->zone_pods[i] |= 1ull << (8 * z);
+                if (x >= 2u) st->zone_pods[i] |= 1ull << (8 * (KG_MAX_ZONES + z));
+            }
+        }
+    }
     if (s->la_flags) memcpy(st->la_flags, s->la_flags, 4 * (size_t)n);
     if (s->numa_policy) memcpy(st->numa_policy, s->numa_policy, 4 * (size_t)n);
     if (s->numa_zones) memcpy(st->numa_zones, s->numa_zones, 4 * (size_t)n);
@@ -1318,6 +1358,7 @@ void kgo_state_free(kgo_state* st) {
     free(st->numa_zones);
     free(st->amp);
     free(st->zone_status);
+    free(st->zone_pods);
     free(st->dev_minors);
     free(st->dev_topo);
     free(st->dev_part);
@@ -1372,6 +1413,7 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
         v->zone_mem_used[z] = st->col[C_ZONE_MEM_USED + z];
     }
     v->numa_zone_status = st->zone_status;
+    v->numa_zone_pods = st->zone_pods;
     v->dev_minors = st->dev_minors;
     v->dev_total = st->dev_total;
     v->dev_free = st->dev_free;
@@ -1488,7 +1530,7 @@ int kgo_numa_allocate(const kg_node_columns* n, uint32_t i, const kg_pod_columns
  * of numa_bind_take under the affinity of the pair's zone code enter the node's allocation (*al: the NUMA split the
  * Reserve records). Returns 1 when Allocate fails (nothing of the pod is applied). */
 static int cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,
-                          int64_t al[2][KG_MAX_ZONES], int* have_al) {
+                          int64_t al[2][KG_MAX_ZONES], int* have_al, uint64_t* taken) {
     *have_al = 0;
     if (!(c->plugins & KG_PLUGIN_NUMA) || !st->cpu_topo || (p->flags[j] & KG_POD_NUMA_SKIP)) return 0;
     const uint32_t node_bind = st->cpu_bind[i];
@@ -1516,23 +1558,43 @@ static int cpuset_reserve(const kg_config* c, kgo_state* st, uint32_t i, const k
     st->col[C_CPUSET][i] = 1000 * (int64_t)allocated;
     /* addPodAllocation (node_allocation.go:111-143): the uid joins singleNUMANode of its one NUMA node or
      * sharedNode of each of several; NUMANodeSharedStatus (:60-68) follows (2 bits per zone < 4) */
-    const int multi = (used & (used - 1)) != 0;
-    for (uint32_t q = 0; q < KG_MAX_ZONES; q++) {
-        if (!((used >> q) & 1u)) continue;
-        const uint32_t s = (st->zone_status[i] >> (2 * q)) & 3u;
-        const uint32_t ns = multi ? 2u : (s == 0u ? 1u : s);
-        st->zone_status[i] = (st->zone_status[i] & ~(3u << (2 * q))) | (ns << (2 * q));
-    }
+    zone_pods_add(st, i, used, 1);
+    if (taken)
+        for (int w = 0; w < 4; w++) taken[w] = out[w];
     return 0;
+}
+
+/* NodeAllocation.release of a cpuset pod's CPUs (node_allocation.go:164-200): RefCount-- (a CPU at 0 leaves
+ * allocatedCPUs), the uid leaves the NUMA nodes' single / shared sets, cpuset_alloc_milli follows */
+static void cpuset_release(kgo_state* st, uint32_t i, const uint64_t* cpus) {
+    if (!st->cpu_topo || st->cpu_topo[i] < 0) return;
+    kg_node_columns v;
+    kgo_state_view(st, &v);
+    const kg_cpu_topo* t = cpu_topology(&v, i);
+    if (!t) return;
+    uint32_t used = 0;
+    int allocated = 0;
+    for (int cc = 0; cc < t->n_cpus; cc++) {
+        if (((cpus[cc >> 6] >> (cc & 63)) & 1ull) && st->cpu_alloc[i].ref[cc] > 0) {
+            if (--st->cpu_alloc[i].ref[cc] == 0) st->cpu_alloc[i].excl[cc] = 0;
+            used |= 1u << t->numa[cc];
+        }
+        allocated += st->cpu_alloc[i].ref[cc] > 0;
+    }
+    st->col[C_CPUSET][i] = 1000 * (int64_t)allocated;
+    zone_pods_add(st, i, used, -1);
 }
 
 /* Reserve (sign 1) / Unreserve (-1) of pod j on node i; a Reserve returns KGO_ZONE_CPUSET_FAIL when the
  * cpuset accumulator fails (nothing applied), else 0 */
+/* amounts (nullable): the NUMA allocation per zone (cpu, then memory), written by a Reserve and given back by an
+ * Unreserve; cpus (nullable): the cpuset CPUs a Reserve took / an Unreserve releases */
 static int apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone,
-                 int64_t sign) {
+                 int64_t sign, int64_t* amounts, uint64_t* cpus) {
     int64_t bal[2][KG_MAX_ZONES];
     int have_bal = 0;
-    if (sign > 0 && cpuset_reserve(c, st, i, p, j, zone, bal, &have_bal)) return KGO_ZONE_CPUSET_FAIL;
+    if (sign > 0 && cpuset_reserve(c, st, i, p, j, zone, bal, &have_bal, cpus)) return KGO_ZONE_CPUSET_FAIL;
+    if (sign < 0 && cpus) cpuset_release(st, i, cpus);
     /* upstream NodeInfo.AddPod / RemovePod: Requested, NonZeroRequested, len(Pods) */
     st->col[C_REQ_CPU][i] += sign * p->req_cpu[j];
     st->col[C_REQ_MEM][i] += sign * p->req_mem[j];
@@ -1562,7 +1624,12 @@ static int apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_col
         uint32_t mask = numa_code_mask(zone);
         int64_t al[2][KG_MAX_ZONES];
         memset(al, 0, sizeof(al));
-        if (have_bal) {
+        if (sign < 0 && amounts) {
+            for (int z = 0; z < KG_MAX_ZONES; z++) {
+                al[0][z] = amounts[z];
+                al[1][z] = amounts[KG_MAX_ZONES + z];
+            }
+        } else if (have_bal) {
             memcpy(al, bal, sizeof(al));
         } else if (popcount32(mask) == 1) {
             int z = __builtin_ctz(mask);
@@ -1583,6 +1650,10 @@ static int apply(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_col
             st->col[C_ZONE_MEM_USED + z][i] += sign * al[1][z];
             /* addPodAllocation creates the zone's allocatedResources record; release never removes it */
             if (sign > 0 && (al[0][z] != 0 || al[1][z] != 0)) st->zone_status[i] |= 1u << (KG_ZONE_RECORD_SHIFT + z);
+            if (sign > 0 && amounts) {
+                amounts[z] = al[0][z];
+                amounts[KG_MAX_ZONES + z] = al[1][z];
+            }
         }
     }
     return 0;
@@ -1596,11 +1667,11 @@ int kgo_assume(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_colum
     kgo_eval_pair(c, &v, i, p, j, &r);
     int32_t zone = r.status ? -1 : r.zone;
     if (zone_fails(zone)) return 1;
-    return apply(c, st, i, p, j, zone, 1) != 0;
+    return apply(c, st, i, p, j, zone, 1, NULL, NULL) != 0;
 }
 
 void kgo_forget(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, int32_t zone) {
-    (void)apply(c, st, i, p, j, zone, -1);
+    (void)apply(c, st, i, p, j, zone, -1, NULL, NULL);
 }
 
 void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
@@ -1630,7 +1701,7 @@ void kgo_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_c
             continue;
         }
         uint32_t g = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
-        const int32_t f = apply(c, st, g - base, p, j, best_zone, 1);
+        const int32_t f = apply(c, st, g - base, p, j, best_zone, 1, NULL, NULL);
         if (f) { /* the cpuset Reserve fails: the pod stays unscheduled */
             if (out_reason) out_reason[j] |= zone_fail_bits(f);
             out_node[j] = -1;
@@ -1659,7 +1730,7 @@ int kgo_replay_parallel(const kg_config* c, kgo_state* st, uint32_t base, const 
             continue;
         }
         const uint32_t g = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
-        if (apply(c, st, g - base, p, j, zone, 1)) {
+        if (apply(c, st, g - base, p, j, zone, 1, NULL, NULL)) {
             out_node[j] = -1;
             if (out_total) out_total[j] = -1;
             continue;
@@ -3103,7 +3174,7 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
         }
         uint32_t g = 0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFu);
         uint32_t i = g - base;
-        const int32_t f = apply(c, st, i, p, j, best_zone, 1);
+        const int32_t f = apply(c, st, i, p, j, best_zone, 1, NULL, NULL);
         if (f) { /* the cpuset Reserve fails: the pod stays unscheduled */
             if (out_reason) out_reason[j] |= zone_fail_bits(f);
             out_node[j] = -1;
@@ -3222,7 +3293,7 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                 out_status[j] = s;
                 continue;
             }
-            const int32_t f = apply(c, st, (uint32_t)node, p, j, zone, 1);
+            const int32_t f = apply(c, st, (uint32_t)node, p, j, zone, 1, NULL, NULL);
             if (f) { /* the cpuset Reserve fails */
                 failed = zone_fail_bits(f);
                 failed_any = 1;
@@ -3273,4 +3344,73 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
     free(done);
     free(b.mem);
     return 0;
+}
+
+/* Reserve of pod j on node i with the plugins kgo_state holds (NodeInfo, LoadAware, NodeNUMAResource incl. cpusets,
+ * DeviceShare minors; no quota or reservation state) and the record its Unreserve gives back (kg_reserve_record): 0,
+ * or 1 when the NodeNUMAResource Reserve fails (nothing applied; rec->numa_zone holds the failing zone code). */
+int kgo_reserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j, kg_reserve_record* rec) {
+    memset(rec, 0, sizeof(*rec));
+    rec->numa_zone = -1;
+    rec->rsv_rid = -1;
+    kg_node_columns v;
+    kgo_state_view(st, &v);
+    int32_t zone;
+    if (c->plugins & KG_PLUGIN_DEV) { /* DeviceShare joins the NUMA hints: the config-5 evaluation of the pair */
+        ext_buf b;
+        if (ext_buf_new(&b, st->n)) return -1;
+        kg_config c2 = *c;
+        c2.plugins &= ~(KG_PLUGIN_QUOTA | KG_PLUGIN_RSV);
+        ext_eval_pod(&c2, &v, st->n, p, j, NULL, NULL, NULL, &b.r);
+        zone = b.r.st[i] ? -1 : b.r.zone[i];
+        free(b.mem);
+    } else {
+        kgo_pair r;
+        kgo_eval_pair(c, &v, i, p, j, &r);
+        zone = r.status ? -1 : r.zone;
+    }
+    rec->numa_zone = zone;
+    if (zone_fails(zone)) return 1;
+    uint32_t mask = 0;
+    if ((c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0 && st->dev_minors && st->dev_minors[i] > 0)
+        mask = dev_choose(c, &v, i, p, j, zone);
+    uint64_t cpus[4] = {0, 0, 0, 0};
+    int64_t amounts[2 * KG_MAX_ZONES] = {0};
+    const int32_t f = apply(c, st, i, p, j, zone, 1, amounts, cpus);
+    if (f) {
+        rec->numa_zone = f;
+        return 1;
+    }
+    if (mask) {
+        int64_t preq[KG_DEV_R];
+        uint32_t keys;
+        dev_pod_req(p, j, preq, &keys);
+        dev_apply(st->dev_total, st->dev_free, i, mask, preq, keys, 1);
+    }
+    rec->gpu_minors = mask;
+    memcpy(rec->zone_amounts, amounts, sizeof(amounts));
+    memcpy(rec->cpus, cpus, sizeof(cpus));
+    if (cpus[0] | cpus[1] | cpus[2] | cpus[3]) rec->flags |= KG_RECORD_CPUSET;
+    return 0;
+}
+
+/* Unreserve of a kgo_reserve: NodeInfo / LoadAware (RemovePod, podAssignCache.unAssign), NodeNUMAResource Release of
+ * the recorded NUMA amounts and cpuset CPUs (resource_manager.go:478-483, node_allocation.go:164-200), the DeviceShare
+ * minors. */
+void kgo_unreserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_columns* p, uint32_t j,
+                   const kg_reserve_record* rec) {
+    int64_t amounts[2 * KG_MAX_ZONES];
+    uint64_t cpus[4];
+    memcpy(amounts, rec->zone_amounts, sizeof(amounts));
+    memcpy(cpus, rec->cpus, sizeof(cpus));
+    int any = 0;
+    for (int z = 0; z < 2 * KG_MAX_ZONES; z++) any |= amounts[z] != 0;
+    const int32_t zone = rec->numa_zone < 0 ? -1 : any ? 0x4F : rec->numa_zone;
+    (void)apply(c, st, i, p, j, zone, -1, any ? amounts : NULL, (rec->flags & KG_RECORD_CPUSET) ? cpus : NULL);
+    if (rec->gpu_minors && st->dev_total) {
+        int64_t preq[KG_DEV_R];
+        uint32_t keys;
+        dev_pod_req(p, j, preq, &keys);
+        dev_apply(st->dev_total, st->dev_free, i, rec->gpu_minors, preq, keys, -1);
+    }
 }

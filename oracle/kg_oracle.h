@@ -57,6 +57,13 @@ int kgo_assume(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_
 /* Unreserve (reverse of kgo_assume with the zone chosen at Reserve). */
 void kgo_forget(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod,
                 int32_t zone);
+/* Reserve with the record its Unreserve gives back (kg_reserve_record; plugins of the state: NodeInfo, LoadAware,
+ * NodeNUMAResource incl. cpusets, DeviceShare minors): 0, or 1 when the NodeNUMAResource Reserve fails. */
+int kgo_reserve(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod,
+                kg_reserve_record* rec);
+/* Unreserve of a kgo_reserve (NUMA amounts and cpuset CPUs of the record released, GPU minors given back). */
+void kgo_unreserve(const kg_config* cfg, kgo_state* st, uint32_t node, const kg_pod_columns* pods, uint32_t pod,
+                   const kg_reserve_record* rec);
 /* One-pod-per-cycle scheduling with Assume between pods. out_reason (may be NULL): per pod, the OR of
  * the filter status bits over every node in that pod's cycle (the FitError diagnosis). */
 void kgo_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, const kg_pod_columns* pods,

@@ -119,6 +119,11 @@ def lib():
         L.kgo_numa_hints.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
                                      C.c_uint32, P(C.c_uint32), P(C.c_int32)]
         L.kgo_numa_hints.restype = C.c_int
+        L.kgo_reserve.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
+                                  P(abi.KgReserveRecord)]
+        L.kgo_reserve.restype = C.c_int
+        L.kgo_unreserve.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
+                                    P(abi.KgReserveRecord)]
         L.kgo_mem_bytes_to_ratio.argtypes = [C.c_int64, C.c_int64]
         L.kgo_mem_bytes_to_ratio.restype = C.c_int64
         L.kgo_amplify.argtypes = [C.c_int64, C.c_double]
@@ -297,6 +302,18 @@ class OracleState:
         pc = abi.pod_columns(pods)
         lib().kgo_forget(C.byref(self.cfg), self.h, node, C.byref(pc), pod, zone)
 
+    def reserve(self, node: int, pods: abi.Table, pod: int):
+        """kgo_reserve: (ok, record)."""
+        pc = abi.pod_columns(pods)
+        rec = abi.KgReserveRecord()
+        rc = lib().kgo_reserve(C.byref(self.cfg), self.h, node, C.byref(pc), pod, C.byref(rec))
+        assert rc >= 0
+        return rc == 0, rec
+
+    def unreserve(self, node: int, pods: abi.Table, pod: int, rec):
+        pc = abi.pod_columns(pods)
+        lib().kgo_unreserve(C.byref(self.cfg), self.h, node, C.byref(pc), pod, C.byref(rec))
+
     def replay(self, pods: abi.Table, index_base: int = 0, reasons: bool = False):
         np_ = abi.table_len(pods)
         out_node = np.zeros(np_, np.int32)
@@ -395,6 +412,7 @@ class OracleState:
         t["numa_policy"] = grab(v.numa_policy, np.uint32)
         t["numa_zones"] = grab(v.numa_zones, np.uint32)
         t["numa_zone_status"] = grab(v.numa_zone_status, np.uint32)
+        t["numa_zone_pods"] = grab(v.numa_zone_pods, np.uint64)
         t["cpu_amp_ratio"] = grab(v.cpu_amp_ratio, np.float64)
         df = self.dev_free()
         t["dev_free"] = df if df is not None else np.zeros((n, abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)

@@ -35,7 +35,7 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
     names = ["kg_config", "kg_node_columns", "kg_node_state", "kg_pod_columns", "kg_verify_out",
              "kg_quota_columns", "kg_rsv_view", "kg_rsv_info", "kg_rsv_dev", "kg_cpu_topo", "kg_cpu_alloc",
-             "kg_cpuset_request"]
+             "kg_cpuset_request", "kg_reserve_record"]
     src = tmp_path / "sz.c"
     hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "koordgpu.h")
     src.write_text(f'#include "{hdr}"\n#include <stdio.h>\nint main(void){{' +
@@ -45,7 +45,7 @@ def test_struct_layouts_match_header(tmp_path):
     sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     mirrors = [abi.KgConfig, abi.KgNodeColumns, abi.KgNodeState, abi.KgPodColumns, abi.KgVerifyOut,
                abi.KgQuotaColumns, abi.KgRsvView, abi.KgRsvInfo, abi.KgRsvDev, abi.KgCpuTopo, abi.KgCpuAlloc,
-               abi.KgCpusetRequest]
+               abi.KgCpusetRequest, abi.KgReserveRecord]
     for n, c_size, m in zip(names, sizes, mirrors):
         assert C.sizeof(m) == c_size, n
 

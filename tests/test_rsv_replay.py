@@ -141,3 +141,41 @@ def test_assume_ext_follows_reservation_reserve(ctx):
     else:
         assert first == 0
     assert sum(1 for j in range(m) if onode[j] >= 0) > 60
+
+
+def _cpuset_cluster5(n_nodes, n_pods, seed, numa):
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(n_nodes, n_pods, seed_config=seed, numa=numa, usage="u01",
+                                                   rsv_gpu=False, rsv_frac=0.2)
+    pods = {k: v.copy() for k, v in pods.items()}
+    nodes, pods = synth.add_cpusets(nodes, pods, seed, bind_frac=0.15)
+    return cfg, nodes, pods, quotas, rsv
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("numa,seed", [("single", 91), ("mix", 92)])
+def test_replay_with_cpuset_pods(ctx, numa, seed):
+    """kg_replay of a config-5 batch with cpuset-binding (LSR) pods and CPU-bind-policy nodes, every plugin and
+    reservation views: the cpuset Reserve (k_cpuset_reserve, NodeNUMAResource Reserve -> resourceManager.Allocate /
+    Update) runs between the steps of the config-5 replay; placements, totals, reasons, quota used and the final node
+    state (CPU RefCounts, zone statuses, NodeInfo) equal the oracle replay's."""
+    from koordinator_amd import engine
+    cfg, nodes, pods, quotas, rsv = _cpuset_cluster5(1200, 300, seed, numa)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    snap.upload_quotas(quotas)
+    snap.upload_reservations(rsv)
+    batch = engine.PodBatch(ctx, pods)
+    node, total, why = engine.replay(snap, batch, reasons=True)
+    st = oracle_lib.OracleState(kc, nodes)
+    onode, ototal, _, qu, qn, owhy = st.ext_replay(pods, quotas, rsv=rsv, reasons=True)
+    assert np.array_equal(node, onode)
+    assert np.array_equal(total, ototal)
+    assert np.array_equal(why, owhy)
+    used, _, npu, _ = snap.read_quotas()
+    assert np.array_equal(used, qu) and np.array_equal(npu, qn)
+    bind = (pods["flags"] & abi.KG_POD_CPU_BIND) != 0
+    assert (onode[bind] >= 0).sum() >= 5  # cpuset pods were placed
+    dev = snap.read_state()
+    want = st.table()
+    for k in ("req_cpu", "req_mem", "num_pods", "cpuset_alloc_milli", "numa_zone_status", "cpu_alloc"):
+        assert np.array_equal(dev[k], want[k]), k
