@@ -1099,14 +1099,98 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
     }
 }
 
+// The batch cycle with cpuset-binding pods (NodeNUMAResource Reserve -> resourceManager.Allocate: a take by the device
+// accumulator, a whole wave in LDS): one workgroup of one wave runs the groups in order, every lane evaluates each pod
+// (uniform work), the wave takes the CPUs, lane 0 applies the other Reserves. Same results as k_batch plus the cpusets
+// (a failed take fails the pod and its group's later pods: ErrNotEnoughCPUs, zone code ZONE_CPUSET_FAIL).
+template <bool EXACT>
+__global__ __launch_bounds__(64) void k_batch_coop(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
+                                                   DevRec* __restrict__ devs, ExtDev e, PodsDev pods,
+                                                   const uint32_t* __restrict__ grp_begin,
+                                                   const uint32_t* __restrict__ grp_pods,
+                                                   const uint32_t* __restrict__ grp_rec, uint32_t n_groups, KCfg cfg,
+                                                   kg_cpu_alloc* __restrict__ allocs, const kg_cpu_topo* __restrict__ topos,
+                                                   uint32_t* __restrict__ result, uint32_t* __restrict__ status,
+                                                   int32_t* __restrict__ zone_out, uint32_t* __restrict__ minors_out) {
+    __shared__ CpusetLds L;
+    const bool lead = threadIdx.x == 0;
+    for (uint32_t g = 0; g < n_groups; g++) {
+        const uint32_t rec = grp_rec[g];
+        int64_t* n = nodes[rec].v;
+        uint32_t failed = 0;
+        for (uint32_t t = grp_begin[g]; t < grp_begin[g + 1]; t++) {
+            const uint32_t j = grp_pods[t];
+            if (failed) {
+                if (lead) {
+                    result[j] = KG_BATCH_SIBLING;
+                    status[j] = failed;
+                    zone_out[j] = -1;
+                    minors_out[j] = 0;
+                }
+                continue;
+            }
+            const PodV q = load_pod(pods, j);
+            const PodX qx = load_podx(pods, j);
+            uint32_t qst = 0;
+            if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas)
+                qst = quota_gate(e.qlim[qx.quota], e.qstate[qx.quota], q, qx);
+            const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, qst);
+            uint32_t st = r.status;
+            const int32_t zone = r.zone;
+            uint32_t mask = 0;
+            if (!st && !zone_reserve_fails(zone) && (cfg.plugins & KG_PLUGIN_DEV) && devs)
+                mask = dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone);
+            if (!st && zone_reserve_fails(zone)) st = zone_fail_status(zone);  // Reserve fails (engine.go:270-280)
+            __syncthreads();  // every lane has read the state the pod was evaluated on
+            if (!st && (cfg.plugins & KG_PLUGIN_NUMA) && cpuset_bound_dev(zones[rec], q.flags, q.req_cpu) &&
+                cpuset_reserve_wave(nodes, zones, allocs, topos, pods, j, rec, zone, L, nullptr) != 0)
+                st = zone_fail_status(ZONE_CPUSET_FAIL);
+            if (st) {
+                failed = st;
+                if (lead) {
+                    result[j] = KG_BATCH_FAILED;
+                    status[j] = st;
+                    zone_out[j] = -1;
+                    minors_out[j] = 0;
+                }
+                __syncthreads();
+                continue;
+            }
+            if (lead) {
+                apply_assume(cfg, n, zones + rec, q, zone, 1);
+                if ((cfg.plugins & KG_PLUGIN_DEV) && devs && qx.dcount > 0) dev_apply(devs + rec, mask, qx, 1);
+                if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
+                    quota_add(e.qstate[qx.quota], q, qx, 1);
+                    quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, 1);
+                }
+                if ((cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views) rsv_reserve_dev(e, n, zones + rec, rec, q, r.nom);
+                result[j] = KG_BATCH_ASSUMED;
+                status[j] = 0;
+                zone_out[j] = zone;
+                minors_out[j] = mask;
+            }
+            __syncthreads();  // lane 0's Reserve before the next pod's evaluation
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // launchers
 
 hipError_t launch_batch(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                         const uint32_t* grp_begin, const uint32_t* grp_pods, const uint32_t* grp_rec, uint32_t n_groups,
                         bool ext, const KCfg& cfg, bool exact, uint32_t* result, uint32_t* status, int32_t* zone,
-                        uint32_t* minors, hipStream_t s) {
+                        uint32_t* minors, hipStream_t s, kg_cpu_alloc* allocs, const kg_cpu_topo* topos) {
     if (n_groups == 0) return hipSuccess;
+    if (allocs && topos) {  // cpuset-binding pods: the cooperative cycle
+        if (exact)
+            k_batch_coop<true><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, grp_begin, grp_pods, grp_rec, n_groups, cfg,
+                                                allocs, topos, result, status, zone, minors);
+        else
+            k_batch_coop<false><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, grp_begin, grp_pods, grp_rec, n_groups, cfg,
+                                                 allocs, topos, result, status, zone, minors);
+        return hipGetLastError();
+    }
     const bool serial = ext && (cfg.plugins & KG_PLUGIN_QUOTA);
     const dim3 grid(serial ? 1u : (n_groups + 63) / 64), block(64);
 #define KG_BATCH(EX, XT)                                                                                              \

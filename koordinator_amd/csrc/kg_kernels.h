@@ -172,7 +172,8 @@ hipError_t launch_cpuset_reserve(NodeRec* nodes, ZoneRec* zones, kg_cpu_alloc* a
 hipError_t launch_batch(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                         const uint32_t* grp_begin, const uint32_t* grp_pods, const uint32_t* grp_rec, uint32_t n_groups,
                         bool ext, const KCfg& cfg, bool exact, uint32_t* result, uint32_t* status, int32_t* zone,
-                        uint32_t* minors, hipStream_t s);
+                        uint32_t* minors, hipStream_t s, kg_cpu_alloc* allocs = nullptr,
+                        const kg_cpu_topo* topos = nullptr);
 hipError_t launch_merge(const uint64_t* partial, uint32_t n_parts, uint32_t n_pods, uint32_t k, uint64_t* out,
                         hipStream_t s);
 // merge of partial rows [part0, part0 + n_parts) (row stride ld pods) for the rows list[0..n) (nullptr: 0..n)

@@ -2892,7 +2892,6 @@ kg_status kg_batch_schedule(kg_snap* s, kg_pods* p, const int32_t* plan_node, ui
     if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->rsv_gpu)
         return fail(ctx, KG_UNSUPPORTED, "batch schedule with reservations holding GPUs (their DeviceShare restore tables "
                                          "change with every placement)");
-    if (cpuset_active(s, p)) return fail(ctx, KG_UNSUPPORTED, "batch schedule with cpuset-binding pods");
     if (s->ext()) {
         st = check_ext(s);
         if (st != KG_OK) return st;
@@ -2947,8 +2946,10 @@ kg_status kg_batch_schedule(kg_snap* s, kg_pods* p, const int32_t* plan_node, ui
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
+    const bool cs = cpuset_active(s, p);  // cpuset-binding pods: the cooperative cycle takes their CPUs on the device
     HIP_TRY(ctx, launch_batch(s->d_nodes, s->d_zones, s->d_dev, s->ext_dev(), p->dev, d, d + G + 1, d + G + 1 + n, G, s->ext(),
-                              s->kcfg, force_exact(), d_res, d_res + n, (int32_t*)(d_res + 2 * n), d_res + 3 * n, ctx->stream));
+                              s->kcfg, force_exact(), d_res, d_res + n, (int32_t*)(d_res + 2 * n), d_res + 3 * n, ctx->stream,
+                              cs ? s->d_cpu_alloc : nullptr, cs ? s->d_cpu_topos : nullptr));
     st = record_end(ctx, e0, e1);
     if (st != KG_OK) return st;
     std::vector<uint32_t> out(4 * (size_t)n);

@@ -343,3 +343,70 @@ def test_planner_and_batch_scheduler_end_to_end(ctx):
         assert np.array_equal(got2[k], got[k]), k
     missing = batch.BatchScheduleResult(m3[:2], {m3[0].key: names[1]})
     assert sched.batch_schedule(missing, {}).status.code == batch.ERROR
+
+
+def _cpuset_batch_case(overfill, ext):
+    """A planned job with cpuset-binding pods: the mixed cluster (cpusets under every NUMA policy), or config 5 with
+    reservation views, quotas and cpusets; the plan is the oracle replay's placement (overfill: the second half of the
+    job crowded onto one node so that its takes fail)."""
+    if ext:
+        cfg, nodes, pods, quotas, rsv = synth.cluster5(600, 160, seed_config=97, numa="mix", usage="u01", rsv_gpu=False,
+                                                       rsv_frac=0.3)
+        pods = {k: v.copy() for k, v in pods.items()}
+        nodes, pods = synth.add_cpusets(nodes, pods, 97, bind_frac=0.25)
+        kc = cfg.kg_config()
+        ref_node, *_ = oracle_lib.OracleState(kc, nodes).ext_replay(pods, quotas, rsv=rsv)
+    else:
+        cfg, nodes, pods = synth.mixed(500, 200, seed=98)
+        quotas = rsv = None
+        kc = cfg.kg_config()
+        ref_node, _ = oracle_lib.OracleState(kc, nodes).replay(pods)
+    ok = np.flatnonzero(ref_node >= 0)
+    sub, plan = abi.take(pods, ok), ref_node[ok].astype(np.int32)
+    if overfill:
+        bind = np.flatnonzero((sub["flags"] & abi.KG_POD_CPU_BIND) != 0)
+        plan[bind] = plan[bind[0]]
+        plan[len(plan) // 2:] = plan[bind[0]]
+    order = grouped(plan)
+    return kc, nodes, quotas, rsv, abi.take(sub, np.asarray(order)), plan[order]
+
+
+@pytest.mark.parametrize("ext", [False, True])
+def test_oracle_batch_with_cpuset_pods(ext):
+    """The oracle's batch cycle of a replayed plan with cpuset pods commits whole (each take on its planned node)."""
+    kc, nodes, quotas, rsv, sub, plan = _cpuset_batch_case(False, ext)
+    assert ((sub["flags"] & abi.KG_POD_CPU_BIND) != 0).sum() >= 5
+    res, stat, *_ = oracle_lib.OracleState(kc, nodes).batch_schedule(sub, plan, quotas, rsv)
+    assert (res == abi.KG_BATCH_ASSUMED).all(), stat[res != abi.KG_BATCH_ASSUMED]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ext,overfill", [(False, False), (False, True), (True, False), (True, True)])
+def test_batch_schedule_with_cpuset_pods(ctx, ext, overfill):
+    """kg_batch_schedule with cpuset-binding pods (the cooperative cycle: each pod's CPUs taken by the device
+    accumulator on its planned node): results, zones, minors, quota used and the node state (CPU RefCounts, zone
+    statuses and pod counts) equal the oracle's; a failed job restores everything."""
+    from koordinator_amd import engine
+    kc, nodes, quotas, rsv, sub, plan = _cpuset_batch_case(overfill, ext)
+    snap = engine.Snapshot(ctx, kc, nodes)
+    if ext:
+        snap.upload_quotas(quotas)
+        snap.upload_reservations(rsv)
+    before = snap.read_state()
+    pb = engine.PodBatch(ctx, sub)
+    res, stat, zone, minors = engine.batch_schedule(snap, pb, plan)
+    ost = oracle_lib.OracleState(kc, nodes)
+    rres, rstat, rzone, rminors, qu, _qn = ost.batch_schedule(sub, plan, quotas, rsv)
+    assert np.array_equal(res, rres) and np.array_equal(stat, rstat)
+    assert np.array_equal(zone, rzone) and np.array_equal(minors, rminors)
+    got, want = snap.read_state(), ost.table()
+    for k in ("req_cpu", "cpuset_alloc_milli", "numa_zone_status", "numa_zone_pods", "cpu_alloc", "zone_cpu_used0",
+              "zone_cpu_used1"):
+        assert np.array_equal(got[k], want[k]), k
+    if ext:
+        assert np.array_equal(snap.read_quotas()[0], qu)
+    if overfill:
+        assert (res == abi.KG_BATCH_FAILED).sum() >= 1
+        oracle_lib.assert_state_restored(before, got)
+    else:
+        assert (res == abi.KG_BATCH_ASSUMED).all()
