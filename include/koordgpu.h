@@ -544,6 +544,24 @@ kg_status kg_snapshot_read_quotas(kg_snap* snap, int64_t* used, uint32_t* used_k
 kg_status kg_snapshot_upload_reservations(kg_snap* snap, const kg_rsv_view* views, uint32_t n_views,
                                           const kg_rsv_info* infos, uint32_t n_infos, const kg_rsv_dev* devs,
                                           uint32_t n_devs);
+/* DeviceShare restore inputs of the reservations that hold GPUs (deviceshare/reservation.go:139-198 RestoreReservation
+ * reads them from nodeDevice every cycle): per such node one entry with rid -1 whose `a` is the node's deviceUsed, and
+ * one entry per GPU-holding reservation on it (kg_rsv_info.rid): `a` = its reserve pod's allocation (allocatable),
+ * `b` = its assigned pods' allocations on those minors (allocated), its policy and assigned pod count. With them
+ * kg_replay, kg_batch_schedule and kg_reserve / kg_unreserve follow a Reserve into such a node on the device (the
+ * node's used, the reservation the pod joins, and the restore tables of the record, the views and the reservations,
+ * rebuilt as transformer.go:740-935 + reservation.go:139-198,278-380 would); without them those calls refuse
+ * (KG_UNSUPPORTED) or mark the node's views stale. kg_snapshot_upload_reservations / kg_snapshot_update_views drop
+ * the inputs (upload them again after). */
+typedef struct kg_rsv_gpu {
+    uint32_t node;           /* local node index                                                        */
+    int32_t rid;             /* kg_rsv_info.rid, -1 = the node's entry                                  */
+    uint32_t policy;         /* KG_RSV_* (reservation entries)                                          */
+    uint32_t allocated_pods; /* len(AssignedPods) (reservation entries)                                 */
+    int64_t a[KG_DEV_R][KG_DEV_MINORS];
+    int64_t b[KG_DEV_R][KG_DEV_MINORS];
+} kg_rsv_gpu;
+kg_status kg_snapshot_upload_rsv_gpu(kg_snap* snap, const kg_rsv_gpu* entries, uint32_t n);
 /* Replace the views (with their reservations and GPU restore tables) of the nodes in nodes[0, n_nodes) by views[0, n_views)
  * (each naming one of those nodes; a listed node without views loses its views); every other node keeps its views.
  * The incremental form of kg_snapshot_upload_reservations for the nodes a Reserve / Unreserve or an event changed

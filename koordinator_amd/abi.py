@@ -604,14 +604,34 @@ def quota_columns(t: Table) -> KgQuotaColumns:
     return s
 
 
-class Reservations:
-    """Reservation restore views and matched reservations (kg_rsv_view / kg_rsv_info arrays)."""
+class KgRsvGpu(C.Structure):
+    """kg_rsv_gpu: DeviceShare restore inputs of a GPU-holding reservation (or, rid -1, of its node)."""
+    _fields_ = [("node", C.c_uint32), ("rid", C.c_int32), ("policy", C.c_uint32), ("allocated_pods", C.c_uint32),
+                ("a", (C.c_int64 * KG_DEV_MINORS) * KG_DEV_R), ("b", (C.c_int64 * KG_DEV_MINORS) * KG_DEV_R)]
 
-    def __init__(self, views, infos, devs=()):
+
+class Reservations:
+    """Reservation restore views and matched reservations (kg_rsv_view / kg_rsv_info arrays), their GPU restore tables
+    and (gpu) the DeviceShare restore inputs of the GPU-holding reservations (kg_rsv_gpu dicts: node, rid, policy,
+    allocated_pods, a, b)."""
+
+    def __init__(self, views, infos, devs=(), gpu=()):
         self.views = (KgRsvView * max(1, len(views)))()
         self.infos = (KgRsvInfo * max(1, len(infos)))()
         self.devs = (KgRsvDev * max(1, len(devs)))()
         self.n_views, self.n_infos, self.n_devs = len(views), len(infos), len(devs)
+        self.gpu = (KgRsvGpu * max(1, len(gpu)))()
+        self.n_gpu = len(gpu)
+        for x, g in enumerate(gpu):
+            e = self.gpu[x]
+            e.node, e.rid = int(g["node"]), int(g["rid"])
+            e.policy, e.allocated_pods = int(g.get("policy", 0)), int(g.get("allocated_pods", 0))
+            for key in ("a", "b"):
+                t = np.asarray(g.get(key, np.zeros((KG_DEV_R, KG_DEV_MINORS))), np.int64).reshape(KG_DEV_R, KG_DEV_MINORS)
+                arr = getattr(e, key)
+                for r in range(KG_DEV_R):
+                    for m in range(KG_DEV_MINORS):
+                        arr[r][m] = int(t[r, m])
         for x in range(len(views)):
             self.views[x].dev_base = -1
         for x in range(len(infos)):
@@ -647,6 +667,12 @@ class Reservations:
         r.n_views = len(keep)
         r.infos, r.n_infos = self.infos, self.n_infos
         r.devs, r.n_devs = self.devs, self.n_devs
+        keep_g = [self.gpu[x] for x in range(self.n_gpu) if lo <= self.gpu[x].node < hi]
+        r.gpu = (KgRsvGpu * max(1, len(keep_g)))()
+        for x, g in enumerate(keep_g):
+            C.pointer(r.gpu[x])[0] = g
+            r.gpu[x].node = g.node - lo
+        r.n_gpu = len(keep_g)
         return r
 
 

@@ -1449,6 +1449,211 @@ __device__ __forceinline__ void rsv_unreserve_dev(const ExtDev& e, int64_t* n, Z
     }
 }
 
+// ---- DeviceShare restore of reservations that hold GPUs (deviceshare/reservation.go:139-198,278-380) ---------------
+// A device table is [DEV_R][DEV_MINORS] with a minor mask (a deviceResources map holds a minor or not); host restatement:
+// decode.dev_effective / dev_reusable / reservation_restore.
+
+__device__ __forceinline__ uint32_t dtab_mask(const int64_t (&t)[DEV_R][DEV_MINORS]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < DEV_MINORS; k++) m |= (t[0][k] != 0 || t[1][k] != 0 || t[2][k] != 0) ? 1u << k : 0u;
+    return m;
+}
+
+// nodeDevice.calcFreeWithPreemptible + filter (device_cache.go:322-410): a minor holding preemptible resources frees
+// them from its used (never below zero); if any such minor then has something left, those minors take that remainder
+// and the others keep their free; allocating from a reservation's required resources (req != nullptr) keeps only the
+// required minors, each capped by them. Minors outside have total and free 0. free = max(0, total - used).
+__device__ inline void dev_effective(const DevRec& node, const int64_t (&used)[DEV_R][DEV_MINORS],
+                                     const int64_t (&pre)[DEV_R][DEV_MINORS], uint32_t pre_mask,
+                                     const int64_t (*req)[DEV_MINORS], uint32_t req_mask, DevRec& out) {
+    bool merged[DEV_MINORS];
+    int64_t rem[DEV_R][DEV_MINORS];
+    bool any = false;
+    for (int m = 0; m < DEV_MINORS; m++) {
+        bool nz = false;
+        for (int r = 0; r < DEV_R; r++) {
+            const int64_t u = max(used[r][m] - pre[r][m], (int64_t)0);
+            rem[r][m] = max(node.total[r][m] - u, (int64_t)0);
+            nz |= rem[r][m] != 0;
+        }
+        merged[m] = ((pre_mask >> m) & 1u) && nz;
+        any |= merged[m];
+    }
+    for (int m = 0; m < DEV_MINORS; m++)
+        for (int r = 0; r < DEV_R; r++) {
+            int64_t f = max(node.total[r][m] - used[r][m], (int64_t)0);
+            if (any && merged[m]) f = rem[r][m];
+            int64_t t = node.total[r][m];
+            if (req) {
+                if ((req_mask >> m) & 1u) f = min(f, req[r][m]);
+                else f = 0, t = 0;
+            }
+            out.total[r][m] = t;
+            out.free_[r][m] = f;
+        }
+}
+
+__device__ __forceinline__ const GpuRawRsv* raw_rsv(const ExtDev& e, const GpuRawNode& N, uint32_t rid) {
+    for (uint32_t r = N.first; r < N.first + N.count; r++)
+        if (e.grsv[r].rid == rid) return &e.grsv[r];
+    return nullptr;
+}
+
+// the parts of one reservation (dev_reservation_parts): allocatable (alloc, its mask), allocated masked by it, remained =
+// alloc - allocated (negative kept) and the used part max(allocated, 0)
+__device__ __forceinline__ void raw_parts(const GpuRawRsv& R, int64_t (&al)[DEV_R][DEV_MINORS], int64_t (&rm)[DEV_R][DEV_MINORS],
+                                          int64_t (&up)[DEV_R][DEV_MINORS], uint32_t& amask) {
+    amask = dtab_mask(R.alloc);
+    for (int r = 0; r < DEV_R; r++)
+        for (int m = 0; m < DEV_MINORS; m++) {
+            al[r][m] = ((amask >> m) & 1u) ? R.allocated[r][m] : 0;
+            rm[r][m] = R.alloc[r][m] - al[r][m];
+            up[r][m] = max(al[r][m], (int64_t)0);
+        }
+}
+
+// RestoreReservation + dev_reusable of every view of record `rec` and the record's own free (pods matching nothing see
+// every GPU reservation with assigned pods as unmatched), from the raw inputs: rewrites d->free_ and the views' base and
+// reservation tables (e.rdev). One lane.
+__device__ inline void gpu_restore_rebuild(const ExtDev& e, const int64_t* __restrict__ n, uint32_t rec, DevRec* d) {
+    const GpuRawNode& N = e.gnodes[e.graw[rec]];
+    DevRec* rdev = const_cast<DevRec*>(e.rdev);
+    int64_t pre[DEV_R][DEV_MINORS], al[DEV_R][DEV_MINORS], rm[DEV_R][DEV_MINORS], up[DEV_R][DEV_MINORS];
+    uint32_t am = 0;
+    {  // the record
+        uint32_t pm = 0;
+        for (int r = 0; r < DEV_R; r++)
+            for (int m = 0; m < DEV_MINORS; m++) pre[r][m] = 0;
+        for (uint32_t x = N.first; x < N.first + N.count; x++) {
+            if (e.grsv[x].pods <= 0) continue;
+            raw_parts(e.grsv[x], al, rm, up, am);
+            for (int r = 0; r < DEV_R; r++)
+                for (int m = 0; m < DEV_MINORS; m++) pre[r][m] += up[r][m];
+            pm |= dtab_mask(up);
+        }
+        DevRec out;
+        dev_effective(*d, N.used, pre, pm, nullptr, 0u, out);
+        for (int r = 0; r < DEV_R; r++)
+            for (int m = 0; m < DEV_MINORS; m++) d->free_[r][m] = out.free_[r][m];
+    }
+    const uint64_t cmask = (uint64_t)n[N_RSV_CLASSES];
+    for (uint64_t l = cmask; l; l &= l - 1ull) {
+        const RsvView* v = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec);
+        if (!v || v->dev_base < 0) continue;
+        // matched GPU reservations of the view (by rid), the others with pods are unmatched
+        int64_t uu[DEV_R][DEV_MINORS], ma[DEV_R][DEV_MINORS], mal[DEV_R][DEV_MINORS];
+        uint32_t uum = 0, mam = 0, malm = 0;
+        for (int r = 0; r < DEV_R; r++)
+            for (int m = 0; m < DEV_MINORS; m++) uu[r][m] = ma[r][m] = mal[r][m] = 0;
+        for (uint32_t x = N.first; x < N.first + N.count; x++) {
+            const GpuRawRsv& R = e.grsv[x];
+            bool matched = false;
+            for (uint32_t t = v->first; t < v->first + v->count; t++) matched = matched || (e.infos[t].dev >= 0 && e.infos[t].rid == R.rid);
+            raw_parts(R, al, rm, up, am);
+            if (matched) {
+                for (int r = 0; r < DEV_R; r++)
+                    for (int m = 0; m < DEV_MINORS; m++) ma[r][m] += al[r][m], mal[r][m] += R.alloc[r][m];
+                mam |= dtab_mask(al);
+                malm |= am;
+            } else if (R.pods > 0) {
+                for (int r = 0; r < DEV_R; r++)
+                    for (int m = 0; m < DEV_MINORS; m++) uu[r][m] += up[r][m];
+                uum |= dtab_mask(up);
+            }
+        }
+        // outside the reservations (plugin.go:417-419): unmatched used + matched allocatable
+        for (int r = 0; r < DEV_R; r++)
+            for (int m = 0; m < DEV_MINORS; m++) pre[r][m] = uu[r][m] + mal[r][m];
+        dev_effective(*d, N.used, pre, uum | malm, nullptr, 0u, rdev[v->dev_base]);
+        // each matched reservation (tryAllocateFromReusable :344-410): unmatched used + matched allocated + its remained;
+        // the Restricted policy only its minors, capped by calcRequiredDeviceResources (:436-455)
+        for (uint32_t t = v->first; t < v->first + v->count; t++) {
+            const RsvInfo& I = e.infos[t];
+            if (I.dev < 0) continue;
+            const GpuRawRsv* R = raw_rsv(e, N, I.rid);
+            if (!R) continue;
+            raw_parts(*R, al, rm, up, am);
+            const uint32_t rmask = dtab_mask(rm);
+            for (int r = 0; r < DEV_R; r++)
+                for (int m = 0; m < DEV_MINORS; m++) pre[r][m] = uu[r][m] + ma[r][m] + rm[r][m];
+            const uint32_t pm = uum | mam | rmask;
+            if (R->policy == KG_RSV_RESTRICTED) {
+                int64_t req[DEV_R][DEV_MINORS];
+                for (int r = 0; r < DEV_R; r++)
+                    for (int m = 0; m < DEV_MINORS; m++) req[r][m] = ((rmask >> m) & 1u) ? rm[r][m] : 0;
+                const uint32_t qm = (rmask ? rmask : am) & am;
+                dev_effective(*d, N.used, pre, pm, req, qm, rdev[I.dev]);
+            } else {
+                dev_effective(*d, N.used, pre, pm, nullptr, 0u, rdev[I.dev]);
+            }
+        }
+    }
+}
+
+// the pod's reservation view on record rec (nullptr: none)
+__device__ __forceinline__ const RsvView* pod_view(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                                   uint32_t rec, const PodX& x) {
+    if (!(c.plugins & KG_PLUGIN_RSV) || !e.views || x.cls < 0 || x.cls >= RSV_MAX_CLASSES ||
+        !(((uint64_t)n[N_RSV_CLASSES] >> x.cls) & 1ull))
+        return nullptr;
+    return find_view(e, x.cls, rec);
+}
+
+// DeviceShare's allocate at Reserve (plugin.go:573-637): from the nominated reservation's table when it holds GPUs
+// (allocateWithNominated -> tryAllocateFromReusable, not required), else or on its failure outside the reservations
+// (the view's base table; off views the node's devices), under the pair's NUMA affinity. The minors taken (0 = none).
+__device__ __forceinline__ uint32_t dev_choose_site(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n,
+                                                    const ZoneRec* __restrict__ zr, const DevRec* __restrict__ d,
+                                                    const RsvView* v, int32_t nom, const PodX& x, int32_t zone) {
+    const int32_t D = (int32_t)n[N_DEV_MINORS];
+    if (x.dcount == 0 || D <= 0) return 0;
+    const uint32_t numa = zone_affinity(zone);
+    if (v && nom >= 0 && e.infos[nom].dev >= 0) {
+        const GpuAlloc a = gpu_alloc_tab_numa(c, e, d, e.rdev + e.infos[nom].dev, D, zr, x, numa, true);
+        if (!a.code) return a.mask;
+    }
+    const DevRec* tab = (v && v->dev_base >= 0) ? e.rdev + v->dev_base : nullptr;
+    const GpuAlloc a = gpu_alloc_tab_numa(c, e, d, tab, D, zr, x, numa, true);
+    return a.code ? 0u : a.mask;
+}
+
+// A GPU pod's Reserve (sign 1) / Unreserve (-1) of `mask` on a record with GPU-holding reservations: the node's used
+// (updateCacheUsed), the reservation the pod joins / leaves (rid, -1 = none: its assigned pods' allocations on its own
+// minors, appendAllocatedByHints, and its pod count), then the restore tables. Instead of dev_apply. One lane.
+__device__ inline void gpu_restore_apply(const ExtDev& e, const int64_t* __restrict__ n, uint32_t rec, DevRec* d,
+                                         uint32_t mask, const PodX& x, int32_t rid, int64_t sign) {
+    GpuRawNode& N = e.gnodes[e.graw[rec]];
+    GpuRawRsv* R = rid >= 0 ? const_cast<GpuRawRsv*>(raw_rsv(e, N, (uint32_t)rid)) : nullptr;
+    const uint32_t hints = R ? dtab_mask(R->alloc) : 0u;
+    for (int m = 0; m < DEV_MINORS; m++) {
+        if (!((mask >> m) & 1u)) continue;
+        int64_t a[DEV_R];
+        dev_alloc_of(x, d->total[2][m], a);
+        for (int r = 0; r < DEV_R; r++) {
+            N.used[r][m] = sign > 0 ? N.used[r][m] + a[r] : max(N.used[r][m] - a[r], (int64_t)0);
+            if (R && ((hints >> m) & 1u))
+                R->allocated[r][m] = sign > 0 ? R->allocated[r][m] + a[r] : max(R->allocated[r][m] - a[r], (int64_t)0);
+        }
+    }
+    if (R) R->pods = max(R->pods + sign, (int64_t)0);
+    gpu_restore_rebuild(e, n, rec, d);
+}
+
+// DeviceShare + Reservation Reserve bookkeeping of a placed pod with the minors `mask` it took (mask from
+// dev_choose_site) and its nominated reservation nom (index into e.infos, -1 = none): on a record with GPU-holding
+// reservations the raw inputs and restore tables (gpu_restore_apply, every pod: the reservation's assigned pods count
+// too), else the node's minors. sign -1: the Unreserve (rid of the reservation left). One lane.
+__device__ __forceinline__ void dev_reserve_apply(const KCfg& c, const ExtDev& e, const int64_t* __restrict__ n, uint32_t rec,
+                                                  DevRec* d, uint32_t mask, const PodX& x, int32_t rid, int64_t sign) {
+    if (!(c.plugins & KG_PLUGIN_DEV) || !d) return;
+    if (e.graw && e.graw[rec] >= 0) {
+        gpu_restore_apply(e, n, rec, d, x.dcount > 0 ? mask : 0u, x, rid, sign);
+        return;
+    }
+    if (x.dcount > 0) dev_apply(d, mask, x, sign);
+}
+
 // per-pod NormalizeScore inputs: max DeviceShare raw score, max nominated Reservation score, and the
 // preferred node key ((order + 2^31) << 32 | snapshot index, minimum; ~0 = none)
 constexpr uint64_t PREF_NONE = ~0ull;

@@ -850,14 +850,20 @@ __global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, 
             const PodV q = load_pod(pods, step - 1);
             const PodX qx = load_podx(pods, step - 1);
             apply_assume(cfg, nodes[i].v, zones + i, q, prev_zone, 1);
+            // the nominated reservation of the winning pair (nsel, double-buffered like zsel)
+            const int32_t nom = ((cfg.plugins & KG_PLUGIN_RSV) && nsel && nodes[i].v[N_RSV_CLASSES] != 0)
+                                    ? nsel[(size_t)((step - 1) & 1u) * n_nodes + i] : -1;
+            uint32_t mask = 0;
             if ((cfg.plugins & KG_PLUGIN_DEV) && qx.dcount > 0) {
-                const uint32_t mask = dev_choose(cfg, e, nodes[i].v, zones + i, devs + i, qx, prev_zone);
-                dev_apply(devs + i, mask, qx, 1);
+                mask = dev_choose_site(cfg, e, nodes[i].v, zones + i, devs + i, pod_view(cfg, e, nodes[i].v, i, qx), nom, qx,
+                                       prev_zone);
                 minors[step - 1] = mask;
             }
-            // Reservation.Reserve into the nominated reservation of the winning pair (nsel, double-buffered like zsel)
+            // Reservation.Reserve into the nominated reservation, then DeviceShare's (the node's minors, or the
+            // restore inputs and tables of GPU-holding reservations)
             if ((cfg.plugins & KG_PLUGIN_RSV) && nsel && nodes[i].v[N_RSV_CLASSES] != 0)
-                rsv_reserve_dev(e, nodes[i].v, zones + i, i, q, nsel[(size_t)((step - 1) & 1u) * n_nodes + i]);
+                rsv_reserve_dev(e, nodes[i].v, zones + i, i, q, nom);
+            dev_reserve_apply(cfg, e, nodes[i].v, i, devs + i, mask, qx, nom >= 0 ? (int32_t)e.infos[nom].rid : -1, 1);
         }
     }
     // ElasticQuota: buffer (step-1)&1 holds the state after pods < step-1; buffer step&1 becomes the
@@ -996,7 +1002,8 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
             }
             return;
         }
-        mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs) ? dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone) : 0u;
+        mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs)
+                   ? dev_choose_site(cfg, e, n, zones + rec, devs + rec, pod_view(cfg, e, n, rec, qx), nom, qx, zone) : 0u;
         if (sign == 0) {  // evaluation pass only (a cpuset Reserve runs next)
             if (out && threadIdx.x == 0) out[0] = zone_preset(zone), out[1] = (int32_t)mask, out[2] = nom;
             return;
@@ -1006,11 +1013,13 @@ __global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ 
     if (threadIdx.x != 0) return;
     if (sign < 0 && cpus && allocs && topos) cpuset_release_lane(nodes, zones, allocs, topos, rec, cpus);
     apply_assume(cfg, n, zones + rec, q, zone, sign, split);
-    if ((cfg.plugins & KG_PLUGIN_DEV) && devs && qx.dcount > 0) dev_apply(devs + rec, mask, qx, sign);
-    if (rsv && (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views) {
+    const bool rsv_on = rsv && (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views;
+    if (rsv_on) {
         if (sign > 0) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
         else rsv_unreserve_dev(e, n, zones + rec, rec, q, rid_in);
     }
+    const int32_t rid = sign > 0 ? (nom >= 0 ? (int32_t)e.infos[nom].rid : -1) : rid_in;
+    dev_reserve_apply(cfg, e, n, rec, devs ? devs + rec : nullptr, mask, qx, rsv_on ? rid : -1, sign);
     if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
         quota_add(e.qstate[qx.quota], q, qx, sign);
         quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, sign);
@@ -1068,7 +1077,8 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
                 st = r.status;
                 zone = r.zone;
                 nom = r.nom;
-                if (!st && !zone_reserve_fails(zone) && (cfg.plugins & KG_PLUGIN_DEV) && devs) mask = dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone);
+                if (!st && !zone_reserve_fails(zone) && (cfg.plugins & KG_PLUGIN_DEV) && devs)
+                    mask = dev_choose_site(cfg, e, n, zones + rec, devs + rec, pod_view(cfg, e, n, rec, qx), nom, qx, zone);
             } else {
                 const PairOut r = eval_pair<EXACT>(cfg, n, zones + rec, q);
                 st = r.status;
@@ -1083,13 +1093,15 @@ __global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneR
             }
             apply_assume(cfg, n, zones + rec, q, zone, 1);
             if constexpr (EXT) {
-                if ((cfg.plugins & KG_PLUGIN_DEV) && devs && qx.dcount > 0) dev_apply(devs + rec, mask, qx, 1);
                 if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
                     quota_add(e.qstate[qx.quota], q, qx, 1);
                     quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, 1);
                 }
-                // Reservation.Reserve on the node's views (a group's node is its lane's alone)
-                if ((cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
+                // Reservation.Reserve on the node's views (a group's node is its lane's alone), then DeviceShare's
+                const bool rsv_on = (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views;
+                if (rsv_on) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
+                dev_reserve_apply(cfg, e, n, rec, devs ? devs + rec : nullptr, mask, qx,
+                                  (rsv_on && nom >= 0) ? (int32_t)e.infos[nom].rid : -1, 1);
             }
             result[j] = KG_BATCH_ASSUMED;
             status[j] = 0;
@@ -1139,7 +1151,7 @@ __global__ __launch_bounds__(64) void k_batch_coop(NodeRec* __restrict__ nodes, 
             const int32_t zone = r.zone;
             uint32_t mask = 0;
             if (!st && !zone_reserve_fails(zone) && (cfg.plugins & KG_PLUGIN_DEV) && devs)
-                mask = dev_choose(cfg, e, n, zones + rec, devs + rec, qx, zone);
+                mask = dev_choose_site(cfg, e, n, zones + rec, devs + rec, pod_view(cfg, e, n, rec, qx), r.nom, qx, zone);
             if (!st && zone_reserve_fails(zone)) st = zone_fail_status(zone);  // Reserve fails (engine.go:270-280)
             __syncthreads();  // every lane has read the state the pod was evaluated on
             if (!st && (cfg.plugins & KG_PLUGIN_NUMA) && cpuset_bound_dev(zones[rec], q.flags, q.req_cpu) &&
@@ -1158,12 +1170,14 @@ __global__ __launch_bounds__(64) void k_batch_coop(NodeRec* __restrict__ nodes, 
             }
             if (lead) {
                 apply_assume(cfg, n, zones + rec, q, zone, 1);
-                if ((cfg.plugins & KG_PLUGIN_DEV) && devs && qx.dcount > 0) dev_apply(devs + rec, mask, qx, 1);
                 if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
                     quota_add(e.qstate[qx.quota], q, qx, 1);
                     quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, 1);
                 }
-                if ((cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views) rsv_reserve_dev(e, n, zones + rec, rec, q, r.nom);
+                const bool rsv_on = (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views;
+                if (rsv_on) rsv_reserve_dev(e, n, zones + rec, rec, q, r.nom);
+                dev_reserve_apply(cfg, e, n, rec, devs ? devs + rec : nullptr, mask, qx,
+                                  (rsv_on && r.nom >= 0) ? (int32_t)e.infos[r.nom].rid : -1, 1);
                 result[j] = KG_BATCH_ASSUMED;
                 status[j] = 0;
                 zone_out[j] = zone;

@@ -480,6 +480,22 @@ struct alignas(16) RsvStep {
     uint32_t rmax;  // max nominated-reservation score over the feasible pairs
 };
 
+// DeviceShare restore inputs of the nodes whose reservations hold GPUs (kg_rsv_gpu): the node's raw used
+// (nodeDevice.deviceUsed) and its GPU-holding reservations [first, first + count) of GpuRawRsv; per reservation the
+// reserve pod's allocation, its assigned pods' allocations on those minors, policy and assigned pod count. A GPU pod's
+// Reserve on such a node updates them and rebuilds the node's restore tables (gpu_restore_rebuild, kg_ext.h).
+struct alignas(16) GpuRawNode {
+    int64_t used[DEV_R][DEV_MINORS];
+    uint32_t first, count;
+    uint64_t pad_;
+};
+struct alignas(16) GpuRawRsv {
+    int64_t alloc[DEV_R][DEV_MINORS];
+    int64_t allocated[DEV_R][DEV_MINORS];
+    uint32_t rid, policy;
+    int64_t pods;
+};
+
 // Device pointers of the config-5 tables of a snapshot (nullptr when the plugin is off).
 struct ExtDev {
     const DevRec* dev;             // [record]
@@ -511,6 +527,11 @@ struct ExtDev {
     // per batch (with dsum): DeviceShare's contribution to the topology manager of the class-1 (SingleNUMANode)
     // records, [record - n0][DEV_CLASSES] (gpu_zone_sum); nullptr = evaluate those records on the general path
     const uint64_t* gz;
+    // GPU-holding reservations (kg_snapshot_upload_rsv_gpu): per record its GpuRawNode (-1 = none; nullptr = no node
+    // has one), the nodes' and reservations' raw restore inputs
+    const int32_t* graw;
+    GpuRawNode* gnodes;
+    GpuRawRsv* grsv;
 };
 
 }  // namespace kg

@@ -105,6 +105,15 @@ struct kg_snap {
     // Reservation.Reserve on the device (kg_replay / kg_assume_ext) updates the views in place while no reservation
     // holds GPUs (rsv_gpu false); views_on_device: the host copies trail the device ones (read back before use)
     bool rsv_gpu = false, views_on_device = false;
+    // DeviceShare restore inputs of the GPU-holding reservations (kg_snapshot_upload_rsv_gpu): with them the Reserves
+    // follow those reservations on the device (gpu_restore_apply); an upload / update of the views drops them
+    int32_t* d_graw = nullptr;       // [record] GpuRawNode index, -1 = none
+    GpuRawNode* d_gnodes = nullptr;
+    GpuRawRsv* d_grsv = nullptr;
+    uint32_t n_gnodes = 0, n_grsv = 0;
+    bool gpu_raw = false;
+    // a Reserve can follow every reservation of the snapshot on the device (none holds GPUs, or their inputs are here)
+    bool rsv_follow() const { return !rsv_gpu || gpu_raw; }
     std::vector<uint32_t> view_order;  // device view t -> h_views index
     int32_t* d_nsel = nullptr;         // replay: nominated reservation of each record's pair (2 x n, like d_zsel)
     RsvStep* d_rstep = nullptr;        // replay with views: [3] per-step Reservation normalisation and winner
@@ -129,6 +138,10 @@ struct kg_snap {
         RsvView* views = nullptr;  // the views and reservations Reservation.Reserve changes on the device
         RsvInfo* infos = nullptr;
         uint32_t nv = 0, ni = 0;
+        DevRec* rdev = nullptr;  // GPU restore tables and their raw inputs (GPU-holding reservations)
+        GpuRawNode* gnodes = nullptr;
+        GpuRawRsv* grsv = nullptr;
+        uint32_t nrd = 0, ngn = 0, ngr = 0;
         bool views_on_device = false;
         bool valid = false, views_stale = false;
         std::vector<uint8_t> stale;
@@ -162,6 +175,9 @@ struct kg_snap {
         e.infos = d_infos;
         e.cls_begin = d_cls_begin;
         e.rdev = d_rdev;
+        e.graw = gpu_raw ? d_graw : nullptr;
+        e.gnodes = d_gnodes;
+        e.grsv = d_grsv;
         return e;
     }
 };
@@ -1245,7 +1261,13 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
         hipFree(k->q);
         hipFree(k->views);
         hipFree(k->infos);
+        hipFree(k->rdev);
+        hipFree(k->gnodes);
+        hipFree(k->grsv);
     }
+    hipFree(s->d_graw);
+    hipFree(s->d_gnodes);
+    hipFree(s->d_grsv);
     hipFree(s->d_cpu_topos);
     hipFree(s->d_cpu_alloc);
     delete s;
@@ -2522,9 +2544,9 @@ kg_status kg_forget_numa(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, in
 
 static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_total, uint32_t* out_reason) {
     kg_ctx* ctx = s->ctx;
-    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->rsv_gpu)
-        return fail(ctx, KG_UNSUPPORTED, "replay with reservations holding GPUs (their DeviceShare restore tables change "
-                                         "with every placement)");
+    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && !s->rsv_follow())
+        return fail(ctx, KG_UNSUPPORTED, "replay with reservations holding GPUs and no restore inputs "
+                                         "(kg_snapshot_upload_rsv_gpu)");
     kg_status st = check_ext(s);
     if (st != KG_OK) return st;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
@@ -2599,7 +2621,7 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     // a Reserve follows Reservation.Reserve on the device's views (k_ext_assume, rsv_reserve_dev) unless a reservation
     // holds GPUs; an Unreserve does not know the reservation: the node's views are stale then
-    if (sign < 0 || s->rsv_gpu || !(s->cfg.plugins & KG_PLUGIN_RSV)) touch_views(s, node);
+    if (sign < 0 || !s->rsv_follow() || !(s->cfg.plugins & KG_PLUGIN_RSV)) touch_views(s, node);
     else if (s->n_views && node < s->cls_mask.size() && s->cls_mask[node]) s->views_on_device = true;
     HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 4, ctx->stream));
     if (sign > 0 && s->has_cpu) {
@@ -2653,7 +2675,7 @@ kg_status kg_reserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, kg_res
     if (!p->d_rec) HIP_TRY(ctx, hipMalloc(&p->d_rec, sizeof(uint64_t) * 16));
     // Reservation.Reserve follows the node's views on the device unless a reservation there holds GPUs (their DeviceShare
     // restore tables follow the reserve pods' allocations: the caller re-uploads the node's views)
-    const bool rsv = (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && !s->rsv_gpu;
+    const bool rsv = (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->rsv_follow();
     if (!rsv) touch_views(s, node);
     else if (node < s->cls_mask.size() && s->cls_mask[node]) s->views_on_device = true;
     HIP_TRY(ctx, hipMemsetAsync(p->d_aout, 0, sizeof(int32_t) * 4, ctx->stream));
@@ -2705,7 +2727,7 @@ kg_status kg_unreserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, cons
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     if (!p->d_rec) HIP_TRY(ctx, hipMalloc(&p->d_rec, sizeof(uint64_t) * 16));
-    const bool rsv = (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && !s->rsv_gpu;
+    const bool rsv = (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->rsv_follow();
     if (!rsv) touch_views(s, node);
     else if (node < s->cls_mask.size() && s->cls_mask[node]) s->views_on_device = true;
     uint64_t r[16] = {0};
@@ -2825,6 +2847,23 @@ static kg_status save_state(kg_snap* s, kg_snap::Saved& k) {
         HIP_TRY(ctx, hipMemcpyAsync(k.views, s->d_views, sizeof(RsvView) * s->n_views, hipMemcpyDeviceToDevice, ctx->stream));
         if (ni) HIP_TRY(ctx, hipMemcpyAsync(k.infos, s->d_infos, sizeof(RsvInfo) * ni, hipMemcpyDeviceToDevice, ctx->stream));
     }
+    if (s->gpu_raw) {  // the GPU restore tables and inputs a Reserve rebuilds
+        if (k.nrd < s->n_rdev || k.ngn < s->n_gnodes || k.ngr < s->n_grsv || !k.rdev) {
+            for (void* b : {(void*)k.rdev, (void*)k.gnodes, (void*)k.grsv}) hipFree(b);
+            k.rdev = nullptr, k.gnodes = nullptr, k.grsv = nullptr;
+            HIP_TRY(ctx, hipMalloc(&k.rdev, sizeof(DevRec) * std::max<uint32_t>(s->n_rdev, 1)));
+            HIP_TRY(ctx, hipMalloc(&k.gnodes, sizeof(GpuRawNode) * std::max<uint32_t>(s->n_gnodes, 1)));
+            HIP_TRY(ctx, hipMalloc(&k.grsv, sizeof(GpuRawRsv) * std::max<uint32_t>(s->n_grsv, 1)));
+        }
+        k.nrd = s->n_rdev, k.ngn = s->n_gnodes, k.ngr = s->n_grsv;
+        if (s->n_rdev) HIP_TRY(ctx, hipMemcpyAsync(k.rdev, s->d_rdev, sizeof(DevRec) * s->n_rdev, hipMemcpyDeviceToDevice, ctx->stream));
+        if (s->n_gnodes)
+            HIP_TRY(ctx, hipMemcpyAsync(k.gnodes, s->d_gnodes, sizeof(GpuRawNode) * s->n_gnodes, hipMemcpyDeviceToDevice, ctx->stream));
+        if (s->n_grsv)
+            HIP_TRY(ctx, hipMemcpyAsync(k.grsv, s->d_grsv, sizeof(GpuRawRsv) * s->n_grsv, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+        k.nrd = k.ngn = k.ngr = 0;
+    }
     k.views_on_device = s->views_on_device;
     k.views_stale = s->views_stale;
     k.stale = s->stale;
@@ -2848,6 +2887,12 @@ static kg_status restore_state(kg_snap* s, kg_snap::Saved& k) {
         HIP_TRY(ctx, hipMemcpyAsync(s->d_views, k.views, sizeof(RsvView) * k.nv, hipMemcpyDeviceToDevice, ctx->stream));
         if (k.ni) HIP_TRY(ctx, hipMemcpyAsync(s->d_infos, k.infos, sizeof(RsvInfo) * k.ni, hipMemcpyDeviceToDevice, ctx->stream));
         s->views_on_device = k.views_on_device;
+    }
+    if (s->gpu_raw && k.rdev && k.nrd == s->n_rdev && k.ngn == s->n_gnodes && k.ngr == s->n_grsv) {
+        if (k.nrd) HIP_TRY(ctx, hipMemcpyAsync(s->d_rdev, k.rdev, sizeof(DevRec) * k.nrd, hipMemcpyDeviceToDevice, ctx->stream));
+        if (k.ngn)
+            HIP_TRY(ctx, hipMemcpyAsync(s->d_gnodes, k.gnodes, sizeof(GpuRawNode) * k.ngn, hipMemcpyDeviceToDevice, ctx->stream));
+        if (k.ngr) HIP_TRY(ctx, hipMemcpyAsync(s->d_grsv, k.grsv, sizeof(GpuRawRsv) * k.ngr, hipMemcpyDeviceToDevice, ctx->stream));
     }
     s->views_stale = k.views_stale;
     s->stale = k.stale;
@@ -2889,9 +2934,9 @@ kg_status kg_batch_schedule(kg_snap* s, kg_pods* p, const int32_t* plan_node, ui
     kg_ctx* ctx = s->ctx;
     if ((!plan_node || !out_result || !out_status) && p->n) return fail(ctx, KG_INVALID_ARG, "null plan / result buffer");
     std::lock_guard<std::mutex> g(ctx->mu);
-    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && s->rsv_gpu)
-        return fail(ctx, KG_UNSUPPORTED, "batch schedule with reservations holding GPUs (their DeviceShare restore tables "
-                                         "change with every placement)");
+    if ((s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views && !s->rsv_follow())
+        return fail(ctx, KG_UNSUPPORTED, "batch schedule with reservations holding GPUs and no restore inputs "
+                                         "(kg_snapshot_upload_rsv_gpu)");
     if (s->ext()) {
         st = check_ext(s);
         if (st != KG_OK) return st;
@@ -3205,6 +3250,7 @@ static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv,
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     s->n_views = nv;
     s->views_stale = false;
+    s->gpu_raw = false;  // the restore inputs of GPU-holding reservations go with the views they were given for
     s->rsv_gpu = false;
     for (uint32_t v = 0; v < nv; v++) s->rsv_gpu = s->rsv_gpu || views[v].dev_base >= 0;
     for (uint32_t t = 0; t < ni; t++) s->rsv_gpu = s->rsv_gpu || infos[t].dev >= 0;
@@ -3229,6 +3275,66 @@ kg_status kg_snapshot_upload_reservations(kg_snap* s, const kg_rsv_view* views, 
     std::lock_guard<std::mutex> g(ctx->mu);
     if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
     return upload_views(s, views, nv, infos, ni, devs, nd);
+}
+
+kg_status kg_snapshot_upload_rsv_gpu(kg_snap* s, const kg_rsv_gpu* g, uint32_t n) {
+    if (!s || (!g && n)) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
+    if (!s->d_dev) return fail(ctx, KG_INVALID_ARG, "no DeviceShare tables in this snapshot");
+    // node entries (rid -1) and each node's reservation entries, grouped by node
+    std::vector<int32_t> node_entry(s->n, -1);
+    std::vector<std::vector<uint32_t>> rsv_of(s->n);
+    for (uint32_t k = 0; k < n; k++) {
+        if (g[k].node >= s->n) return fail(ctx, KG_INVALID_ARG, "entry %u: node %u >= %u", k, g[k].node, s->n);
+        if (g[k].rid < 0) {
+            if (node_entry[g[k].node] >= 0) return fail(ctx, KG_INVALID_ARG, "node %u: two used entries", g[k].node);
+            node_entry[g[k].node] = (int32_t)k;
+        } else {
+            rsv_of[g[k].node].push_back(k);
+        }
+    }
+    std::vector<GpuRawNode> gn;
+    std::vector<GpuRawRsv> gr;
+    std::vector<int32_t> graw(std::max<uint32_t>(s->n, 1), -1);
+    for (uint32_t i = 0; i < s->n; i++) {
+        if (rsv_of[i].empty() && node_entry[i] < 0) continue;
+        if (node_entry[i] < 0) return fail(ctx, KG_INVALID_ARG, "node %u: reservation entries without its used entry", i);
+        GpuRawNode x;
+        std::memset(&x, 0, sizeof(x));
+        std::memcpy(x.used, g[node_entry[i]].a, sizeof(x.used));
+        x.first = (uint32_t)gr.size();
+        x.count = (uint32_t)rsv_of[i].size();
+        for (uint32_t k : rsv_of[i]) {
+            GpuRawRsv r;
+            std::memset(&r, 0, sizeof(r));
+            std::memcpy(r.alloc, g[k].a, sizeof(r.alloc));
+            std::memcpy(r.allocated, g[k].b, sizeof(r.allocated));
+            r.rid = (uint32_t)g[k].rid;
+            r.policy = g[k].policy;
+            r.pods = g[k].allocated_pods;
+            gr.push_back(r);
+        }
+        graw[s->pos[i]] = (int32_t)gn.size();
+        gn.push_back(x);
+    }
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (void* b : {(void*)s->d_graw, (void*)s->d_gnodes, (void*)s->d_grsv}) hipFree(b);
+    s->d_graw = nullptr, s->d_gnodes = nullptr, s->d_grsv = nullptr;
+    HIP_TRY(ctx, hipMalloc(&s->d_graw, sizeof(int32_t) * graw.size()));
+    HIP_TRY(ctx, hipMalloc(&s->d_gnodes, sizeof(GpuRawNode) * std::max<size_t>(gn.size(), 1)));
+    HIP_TRY(ctx, hipMalloc(&s->d_grsv, sizeof(GpuRawRsv) * std::max<size_t>(gr.size(), 1)));
+    HIP_TRY(ctx, hipMemcpy(s->d_graw, graw.data(), sizeof(int32_t) * graw.size(), hipMemcpyHostToDevice));
+    if (!gn.empty()) HIP_TRY(ctx, hipMemcpy(s->d_gnodes, gn.data(), sizeof(GpuRawNode) * gn.size(), hipMemcpyHostToDevice));
+    if (!gr.empty()) HIP_TRY(ctx, hipMemcpy(s->d_grsv, gr.data(), sizeof(GpuRawRsv) * gr.size(), hipMemcpyHostToDevice));
+    s->n_gnodes = (uint32_t)gn.size();
+    s->n_grsv = (uint32_t)gr.size();
+    s->gpu_raw = true;
+    s->gen++;
+    s->invalidate_saved();
+    return KG_OK;
 }
 
 kg_status kg_snapshot_update_views(kg_snap* s, const uint32_t* nodes, uint32_t n_nodes, const kg_rsv_view* views, uint32_t nv,

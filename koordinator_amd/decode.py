@@ -1217,6 +1217,30 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
     return out, views, infos, devs
 
 
+def reservation_gpu_raw(nodes: abi.Table, reservations: Sequence[dict]) -> List[dict]:
+    """The DeviceShare restore inputs of the GPU-holding reservations (kg_rsv_gpu entries for abi.Reservations(gpu=)):
+    per node holding one, its raw used (nodeDevice.deviceUsed: `dev_used`, else total - free) as the rid -1 entry, and
+    per such reservation (rid = its index, as reservation_restore numbers them) its reserve pod's allocation, its
+    assigned pods' allocations on those minors, policy and assigned pod count (RestoreReservation's inputs,
+    deviceshare/reservation.go:149-186). A device Reserve into such a node follows them (kg_snapshot_upload_rsv_gpu)."""
+    if "dev_minors" not in nodes or "dev_total" not in nodes:
+        return []
+    out, seen = [], set()
+    for x, r in enumerate(reservations):
+        parts = dev_reservation_parts(r)
+        i = int(r["node"])
+        if parts is None or int(nodes["dev_minors"][i]) < 0:
+            continue
+        if i not in seen:
+            seen.add(i)
+            tot = np.asarray(nodes["dev_total"][i], np.int64)
+            used = np.asarray(nodes["dev_used"][i], np.int64) if "dev_used" in nodes else tot - np.asarray(nodes["dev_free"][i], np.int64)
+            out.append(dict(node=i, rid=-1, a=used))
+        out.append(dict(node=i, rid=x, policy=int(r.get("policy", abi.KG_RSV_DEFAULT)),
+                        allocated_pods=int(r.get("allocated_pods", 0)), a=parts[0][0], b=parts[1][0]))
+    return out
+
+
 def quota_keys(pods: abi.Table, max_keys: np.ndarray) -> np.ndarray:
     """Keys of quotav1.Mask(PodRequests, Max names) over KG_QUOTA_R = {cpu, memory, scalar0, scalar1}
     (elasticquota/plugin.go:279-280): a key is present when the pod requests it."""

@@ -141,6 +141,8 @@ def lib():
     L.kg_unreserve.restype = st
     L.kg_snapshot_read_reservations.argtypes = [vp, P(abi.KgRsvView), u32, P(abi.KgRsvInfo), u32]
     L.kg_snapshot_read_reservations.restype = st
+    L.kg_snapshot_upload_rsv_gpu.argtypes = [vp, P(abi.KgRsvGpu), u32]
+    L.kg_snapshot_upload_rsv_gpu.restype = st
     if L.kg_abi_version() != abi.KG_ABI_VERSION:
         raise ImportError(f"libkoordgpu ABI {L.kg_abi_version()} != {abi.KG_ABI_VERSION}")
     _lib = L
@@ -281,6 +283,9 @@ class Snapshot:
             self.h, C.cast(rsv.views, C.POINTER(abi.KgRsvView)), rsv.n_views,
             C.cast(rsv.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos,
             C.cast(rsv.devs, C.POINTER(abi.KgRsvDev)), rsv.n_devs), "kg_snapshot_upload_reservations")
+        if getattr(rsv, "n_gpu", 0):  # the DeviceShare restore inputs of GPU-holding reservations
+            self.ctx.check(self.ctx.L.kg_snapshot_upload_rsv_gpu(self.h, C.cast(rsv.gpu, C.POINTER(abi.KgRsvGpu)),
+                                                                 rsv.n_gpu), "kg_snapshot_upload_rsv_gpu")
 
     def read_reservations(self, rsv: abi.Reservations) -> abi.Reservations:
         """The views and infos as the device holds them now (Reservation.Reserve / Unreserve ran there), in the

@@ -10,7 +10,7 @@ import numpy as np
 from . import abi
 from .config import GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, SchedulerConfig, bench_profile, config5_profile
 from . import decode
-from .decode import amplify, gpu_requirements, quota_keys, reservation_restore
+from .decode import amplify, gpu_requirements, quota_keys, reservation_gpu_raw, reservation_restore
 
 SEED = 0x6B6F6F7264
 GI = 1 << 30
@@ -222,6 +222,7 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
             t["num_pods"][i] += 1 + ap
     t["dev_total"], t["dev_free"], t["dev_used"] = tot, np.maximum(tot - used, 0), used
     true_t = {k: np.array(v, copy=True) for k, v in t.items()}
+    gpu_raw = reservation_gpu_raw(t, resv)
     t, views, infos, devs = reservation_restore(t, resv)
     # Pods
     pr = _rng(seed_config, 1)
@@ -270,8 +271,8 @@ def cluster5(n_nodes: int, n_pods: int, seed_config: int = 5, n_quotas: int = 10
     if raw:
         for k in set(t) - set(true_t):  # columns set after the restore (GPU topology) hold for the true table too
             true_t[k] = np.array(t[k], copy=True)
-        return cfg, t, p, q, abi.Reservations(views, infos, devs), true_t, resv
-    return cfg, t, p, q, abi.Reservations(views, infos, devs)
+        return cfg, t, p, q, abi.Reservations(views, infos, devs, gpu_raw), true_t, resv
+    return cfg, t, p, q, abi.Reservations(views, infos, devs, gpu_raw)
 
 
 def config5(n_nodes: int = 100_000, n_pods: int = 10_000, rsv_gpu: bool = True):

@@ -3111,6 +3111,182 @@ static void rsv_reserve(kgo_state* st, kg_rsv_view* views, uint32_t nv, kg_rsv_i
     }
 }
 
+/* ---- DeviceShare restore of reservations that hold GPUs (deviceshare/reservation.go:139-198,278-380) ----------------
+ * A table is [KG_DEV_R][KG_DEV_MINORS] with a minor mask (host restatement: decode.dev_effective / dev_reusable /
+ * reservation_restore). The inputs (kg_rsv_gpu, mutable copies): per node its raw used (rid -1), per GPU-holding
+ * reservation its allocatable, its pods' allocated, policy and assigned pods. */
+#define TX(t, r, m) ((t)[(size_t)(r) * KG_DEV_MINORS + (size_t)(m)])
+
+static uint32_t tab_minors(const int64_t* t) {
+    uint32_t m = 0;
+    for (int k = 0; k < KG_DEV_MINORS; k++)
+        for (int r = 0; r < KG_DEV_R; r++) m |= TX(t, r, k) != 0 ? 1u << k : 0u;
+    return m;
+}
+
+/* nodeDevice.calcFreeWithPreemptible + filter (device_cache.go:322-410), free = max(0, total - used) */
+static void dev_effective_o(const int64_t* tot, const int64_t* used, const int64_t* pre, uint32_t pm, const int64_t* req,
+                            uint32_t qm, int64_t* T, int64_t* F) {
+    int merged[KG_DEV_MINORS], any = 0;
+    int64_t rem[KG_DEV_R * KG_DEV_MINORS];
+    for (int m = 0; m < KG_DEV_MINORS; m++) {
+        int nz = 0;
+        for (int r = 0; r < KG_DEV_R; r++) {
+            int64_t u = TX(used, r, m) - TX(pre, r, m);
+            u = u < 0 ? 0 : u;
+            const int64_t x = TX(tot, r, m) - u;
+            TX(rem, r, m) = x < 0 ? 0 : x;
+            nz |= TX(rem, r, m) != 0;
+        }
+        merged[m] = ((pm >> m) & 1u) && nz;
+        any |= merged[m];
+    }
+    for (int m = 0; m < KG_DEV_MINORS; m++)
+        for (int r = 0; r < KG_DEV_R; r++) {
+            int64_t f = TX(tot, r, m) - TX(used, r, m);
+            f = f < 0 ? 0 : f;
+            if (any && merged[m]) f = TX(rem, r, m);
+            int64_t t = TX(tot, r, m);
+            if (req) {
+                if ((qm >> m) & 1u) f = f < TX(req, r, m) ? f : TX(req, r, m);
+                else f = 0, t = 0;
+            }
+            TX(T, r, m) = t;
+            TX(F, r, m) = f;
+        }
+}
+
+typedef struct gpu_raw {
+    kg_rsv_gpu* g;
+    uint32_t n;
+} gpu_raw;
+
+static kg_rsv_gpu* raw_entry(gpu_raw* x, uint32_t i, int32_t rid) {
+    for (uint32_t k = 0; k < x->n; k++)
+        if (x->g[k].node == i && x->g[k].rid == rid) return &x->g[k];
+    return NULL;
+}
+
+/* allocated masked by the allocatable minors, remained = allocatable - allocated, used part max(allocated, 0) */
+static void raw_parts_o(const kg_rsv_gpu* R, int64_t* al, int64_t* rm, int64_t* up, uint32_t* am) {
+    *am = tab_minors(&R->a[0][0]);
+    for (int r = 0; r < KG_DEV_R; r++)
+        for (int m = 0; m < KG_DEV_MINORS; m++) {
+            TX(al, r, m) = ((*am >> m) & 1u) ? R->b[r][m] : 0;
+            TX(rm, r, m) = R->a[r][m] - TX(al, r, m);
+            TX(up, r, m) = TX(al, r, m) > 0 ? TX(al, r, m) : 0;
+        }
+}
+
+/* RestoreReservation + dev_reusable of node i's views and its record (pods matching nothing) from the raw inputs */
+static void gpu_rebuild_o(kgo_state* st, const kgo_ext* e, kg_rsv_dev* devs, gpu_raw* x, uint32_t i) {
+    const kg_rsv_gpu* N = raw_entry(x, i, -1);
+    if (!N) return;
+    const int64_t* tot = &DEVX(st->dev_total, i, 0, 0);
+    const int64_t* used = &N->a[0][0];
+    const size_t TB = KG_DEV_R * KG_DEV_MINORS;
+    int64_t pre[KG_DEV_R * KG_DEV_MINORS], al[KG_DEV_R * KG_DEV_MINORS], rm[KG_DEV_R * KG_DEV_MINORS];
+    int64_t up[KG_DEV_R * KG_DEV_MINORS], T[KG_DEV_R * KG_DEV_MINORS];
+    uint32_t am, pm = 0;
+    memset(pre, 0, sizeof(pre));
+    for (uint32_t k = 0; k < x->n; k++) {
+        const kg_rsv_gpu* R = &x->g[k];
+        if (R->node != i || R->rid < 0 || R->allocated_pods == 0) continue;
+        raw_parts_o(R, al, rm, up, &am);
+        for (size_t q = 0; q < TB; q++) pre[q] += up[q];
+        pm |= tab_minors(up);
+    }
+    dev_effective_o(tot, used, pre, pm, NULL, 0, T, &DEVX(st->dev_free, i, 0, 0));
+    for (uint32_t v = 0; v < e->n_views; v++) {
+        const kg_rsv_view* vw = &e->views[v];
+        if (vw->node != i || vw->dev_base < 0) continue;
+        int64_t uu[KG_DEV_R * KG_DEV_MINORS], ma[KG_DEV_R * KG_DEV_MINORS], mal[KG_DEV_R * KG_DEV_MINORS];
+        uint32_t uum = 0, mam = 0, malm = 0;
+        memset(uu, 0, sizeof(uu));
+        memset(ma, 0, sizeof(ma));
+        memset(mal, 0, sizeof(mal));
+        for (uint32_t k = 0; k < x->n; k++) {
+            const kg_rsv_gpu* R = &x->g[k];
+            if (R->node != i || R->rid < 0) continue;
+            int matched = 0;
+            for (uint32_t t = vw->first; t < vw->first + vw->count; t++)
+                matched |= e->infos[t].dev >= 0 && (int32_t)e->infos[t].rid == R->rid;
+            raw_parts_o(R, al, rm, up, &am);
+            if (matched) {
+                for (size_t q = 0; q < TB; q++) ma[q] += al[q], mal[q] += (&R->a[0][0])[q];
+                mam |= tab_minors(al);
+                malm |= am;
+            } else if (R->allocated_pods > 0) {
+                for (size_t q = 0; q < TB; q++) uu[q] += up[q];
+                uum |= tab_minors(up);
+            }
+        }
+        for (size_t q = 0; q < TB; q++) pre[q] = uu[q] + mal[q];
+        kg_rsv_dev* b = &devs[vw->dev_base];
+        dev_effective_o(tot, used, pre, uum | malm, NULL, 0, &b->total[0][0], &b->free[0][0]);
+        for (uint32_t t = vw->first; t < vw->first + vw->count; t++) {
+            const kg_rsv_info* I = &e->infos[t];
+            if (I->dev < 0) continue;
+            const kg_rsv_gpu* R = raw_entry(x, i, (int32_t)I->rid);
+            if (!R) continue;
+            raw_parts_o(R, al, rm, up, &am);
+            const uint32_t rmask = tab_minors(rm);
+            for (size_t q = 0; q < TB; q++) pre[q] = uu[q] + ma[q] + rm[q];
+            kg_rsv_dev* d = &devs[I->dev];
+            if (R->policy == KG_RSV_RESTRICTED) {
+                int64_t req[KG_DEV_R * KG_DEV_MINORS];
+                for (int r = 0; r < KG_DEV_R; r++)
+                    for (int m = 0; m < KG_DEV_MINORS; m++) TX(req, r, m) = ((rmask >> m) & 1u) ? TX(rm, r, m) : 0;
+                dev_effective_o(tot, used, pre, uum | mam | rmask, req, (rmask ? rmask : am) & am, &d->total[0][0],
+                                &d->free[0][0]);
+            } else {
+                dev_effective_o(tot, used, pre, uum | mam | rmask, NULL, 0, &d->total[0][0], &d->free[0][0]);
+            }
+        }
+    }
+}
+
+/* DeviceShare's allocate at Reserve (plugin.go:573-637): the nominated reservation's table when it holds GPUs
+ * (allocateWithNominated, not required), else or on failure outside (the view's base table, off views the node's) */
+static uint32_t dev_choose_site_o(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                                  uint32_t j, const kgo_ext* e, const kg_rsv_view* v, int64_t nom, int32_t zone) {
+    gpu_req g;
+    gpu_req_of(p, j, &g);
+    const int32_t D = n->dev_minors ? n->dev_minors[i] : -1;
+    if (g.n == 0 || D <= 0) return 0;
+    const uint32_t numa = (zone >= 0 && !zone_fails(zone)) ? numa_code_mask(zone) : 0u;
+    uint32_t mask;
+    if (v && nom >= 0 && e->infos[nom].dev >= 0 && !gpu_alloc_tab_numa(c, n, i, p, j, &e->devs[e->infos[nom].dev], numa, &mask))
+        return mask;
+    const uint32_t code = gpu_alloc_tab_numa(c, n, i, p, j, (v && v->dev_base >= 0) ? &e->devs[v->dev_base] : NULL, numa, &mask);
+    return code ? 0u : mask;
+}
+
+/* A pod's Reserve on a node with GPU-holding reservations: used += its minors' allocation (updateCacheUsed), the
+ * reservation it joined (rid) counts the allocation on its own minors (appendAllocatedByHints) and one more pod, then
+ * the tables are rebuilt (every pod: the assigned pod count decides which reservations are unmatched with pods) */
+static void gpu_apply_o(kgo_state* st, const kgo_ext* e, kg_rsv_dev* devs, gpu_raw* x, uint32_t i, uint32_t mask,
+                        const kg_pod_columns* p, uint32_t j, int32_t rid) {
+    kg_rsv_gpu* N = raw_entry(x, i, -1);
+    if (!N) return;
+    kg_rsv_gpu* R = rid >= 0 ? raw_entry(x, i, rid) : NULL;
+    const uint32_t hints = R ? tab_minors(&R->a[0][0]) : 0u;
+    int64_t preq[KG_DEV_R];
+    uint32_t keys;
+    dev_pod_req(p, j, preq, &keys);
+    for (int m = 0; m < KG_DEV_MINORS; m++) {
+        if (!((mask >> m) & 1u)) continue;
+        int64_t a[KG_DEV_R];
+        dev_alloc_of(preq, keys, DEVX(st->dev_total, i, KG_DEV_MEM, m), a);
+        for (int r = 0; r < KG_DEV_R; r++) {
+            N->a[r][m] += a[r];
+            if (R && ((hints >> m) & 1u)) R->b[r][m] += a[r];
+        }
+    }
+    if (R) R->allocated_pods += 1;
+    gpu_rebuild_o(st, e, devs, x, i);
+}
+
 /* The replay can follow the reservations' restore on the device only while none of them holds GPUs (their
  * DeviceShare restore tables are derived from the reserve pods' and assigned pods' GPU allocations). */
 static int rsv_has_gpu_tables(const kgo_ext* e) {
@@ -3126,26 +3302,34 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
                    const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
                    int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason) {
     const int rsv = (c->plugins & KG_PLUGIN_RSV) != 0;
-    if (rsv && rsv_has_gpu_tables(e)) return -1;
+    if (rsv && rsv_has_gpu_tables(e) && !e->n_gpu) return -1;
     kg_node_columns v;
     kgo_state_view(st, &v);
     ext_buf b;
     if (ext_buf_new(&b, st->n)) return -1;
     kgo_quota_state* q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
-    /* mutable copies of the views and their reservations (the Reserve updates them) */
+    /* mutable copies of the views, their reservations, the GPU restore tables and inputs (the Reserve updates them) */
     kgo_ext e2;
     kg_rsv_view* mv = NULL;
     kg_rsv_info* mi = NULL;
+    kg_rsv_dev* md = NULL;
+    gpu_raw gx = {NULL, 0};
     view_index vx = {NULL, 0, 0};
     const kgo_ext* ee = e;
     if (rsv && e) {
         e2 = *e;
         mv = (kg_rsv_view*)malloc(sizeof(kg_rsv_view) * (e->n_views ? e->n_views : 1));
         mi = (kg_rsv_info*)malloc(sizeof(kg_rsv_info) * (e->n_infos ? e->n_infos : 1));
+        md = (kg_rsv_dev*)malloc(sizeof(kg_rsv_dev) * (e->n_devs ? e->n_devs : 1));
         if (e->n_views) memcpy(mv, e->views, sizeof(kg_rsv_view) * e->n_views);
         if (e->n_infos) memcpy(mi, e->infos, sizeof(kg_rsv_info) * e->n_infos);
+        if (e->n_devs) memcpy(md, e->devs, sizeof(kg_rsv_dev) * e->n_devs);
+        gx.n = e->n_gpu;
+        gx.g = (kg_rsv_gpu*)malloc(sizeof(kg_rsv_gpu) * (e->n_gpu ? e->n_gpu : 1));
+        if (e->n_gpu) memcpy(gx.g, e->gpu, sizeof(kg_rsv_gpu) * e->n_gpu);
         e2.views = mv;
         e2.infos = mi;
+        e2.devs = md;
         ee = &e2;
         view_index_build(&vx, ee, st->n);
     }
@@ -3183,21 +3367,31 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
         }
         out_node[j] = (int32_t)g;
         if (out_total) out_total[j] = (int64_t)(best >> 32);
+        const int64_t nom = b.r.nom[i];
+        const int raw = rsv && mv && raw_entry(&gx, i, -1) != NULL;
+        uint32_t mask = 0;
         if ((c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0 && st->dev_minors &&
             st->dev_minors[i] > 0) {
-            int64_t preq[KG_DEV_R];
-            uint32_t keys;
-            dev_pod_req(p, j, preq, &keys);
-            uint32_t mask = dev_choose(c, &v, i, p, j, best_zone);
-            dev_apply(st->dev_total, st->dev_free, i, mask, preq, keys, 1);
+            const int32_t cls = p->rsv_class ? p->rsv_class[j] : -1;
+            const kg_rsv_view* vw = (rsv && mv) ? find_view(&vx, ee, cls, i) : NULL;
+            mask = dev_choose_site_o(c, &v, i, p, j, ee, vw, nom, best_zone);
+            if (!raw) {
+                int64_t preq[KG_DEV_R];
+                uint32_t keys;
+                dev_pod_req(p, j, preq, &keys);
+                dev_apply(st->dev_total, st->dev_free, i, mask, preq, keys, 1);
+            }
             if (out_minors) out_minors[j] = mask;
         }
         quota_apply(q, p, j, 1);
-        if (rsv && mv) rsv_reserve(st, mv, ee->n_views, mi, i, p, j, b.r.nom[i]);
+        if (rsv && mv) rsv_reserve(st, mv, ee->n_views, mi, i, p, j, nom);
+        if (raw) gpu_apply_o(st, ee, md, &gx, i, mask, p, j, nom >= 0 ? (int32_t)mi[nom].rid : -1);
     }
     free(vx.v);
     free(mv);
     free(mi);
+    free(md);
+    free(gx.g);
     if (q) {
         if (quota_used_out) memcpy(quota_used_out, q->used, (size_t)q->n * KG_QUOTA_R * 8);
         if (quota_np_used_out) memcpy(quota_np_used_out, q->np_used, (size_t)q->n * KG_QUOTA_R * 8);
@@ -3222,7 +3416,7 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                        const int32_t* plan_node, uint32_t* out_result, uint32_t* out_status, int32_t* out_zone,
                        uint32_t* out_minors, int64_t* quota_used_out, int64_t* quota_np_used_out) {
     const int rsv = (c->plugins & KG_PLUGIN_RSV) != 0 && e && e->n_views;
-    if (rsv && rsv_has_gpu_tables(e)) return -1;
+    if (rsv && rsv_has_gpu_tables(e) && !e->n_gpu) return -1;
     for (uint32_t j = 0; j < np; j++) {
         out_zone[j] = -1;
         out_minors[j] = 0;
@@ -3245,16 +3439,24 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
     kgo_ext e2;
     kg_rsv_view* mv = NULL;
     kg_rsv_info* mi = NULL;
+    kg_rsv_dev* md = NULL;
+    gpu_raw gx = {NULL, 0};
     view_index vx = {NULL, 0, 0};
     const kgo_ext* ee = e;
     if (rsv) {
         e2 = *e;
         mv = (kg_rsv_view*)malloc(sizeof(kg_rsv_view) * e->n_views);
         mi = (kg_rsv_info*)malloc(sizeof(kg_rsv_info) * (e->n_infos ? e->n_infos : 1));
+        md = (kg_rsv_dev*)malloc(sizeof(kg_rsv_dev) * (e->n_devs ? e->n_devs : 1));
         memcpy(mv, e->views, sizeof(kg_rsv_view) * e->n_views);
         if (e->n_infos) memcpy(mi, e->infos, sizeof(kg_rsv_info) * e->n_infos);
+        if (e->n_devs) memcpy(md, e->devs, sizeof(kg_rsv_dev) * e->n_devs);
+        gx.n = e->n_gpu;
+        gx.g = (kg_rsv_gpu*)malloc(sizeof(kg_rsv_gpu) * (e->n_gpu ? e->n_gpu : 1));
+        if (e->n_gpu) memcpy(gx.g, e->gpu, sizeof(kg_rsv_gpu) * e->n_gpu);
         e2.views = mv;
         e2.infos = mi;
+        e2.devs = md;
         ee = &e2;
         view_index_build(&vx, ee, st->n);
     }
@@ -3301,6 +3503,9 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                 out_status[j] = failed;
                 continue;
             }
+            const int64_t nom = ext ? b.r.nom[node] : -1;
+            const int raw = rsv && raw_entry(&gx, (uint32_t)node, -1) != NULL;
+            uint32_t mask = 0;
             if ((c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0 && st->dev_minors &&
                 st->dev_minors[node] > 0) {
                 int64_t preq[KG_DEV_R];
@@ -3308,12 +3513,15 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
                 dev_pod_req(p, j, preq, &keys);
                 kg_node_columns nv;
                 kgo_state_view(st, &nv);
-                uint32_t mask = dev_choose(c, &nv, (uint32_t)node, p, j, zone);
-                dev_apply(st->dev_total, st->dev_free, (uint32_t)node, mask, preq, keys, 1);
+                const int32_t cls = p->rsv_class ? p->rsv_class[j] : -1;
+                const kg_rsv_view* vw = rsv ? find_view(&vx, ee, cls, (uint32_t)node) : NULL;
+                mask = dev_choose_site_o(c, &nv, (uint32_t)node, p, j, ee, vw, nom, zone);
+                if (!raw) dev_apply(st->dev_total, st->dev_free, (uint32_t)node, mask, preq, keys, 1);
                 out_minors[j] = mask;
             }
             quota_apply(q, p, j, 1);
-            if (rsv) rsv_reserve(st, mv, ee->n_views, mi, (uint32_t)node, p, j, b.r.nom[node]);
+            if (rsv) rsv_reserve(st, mv, ee->n_views, mi, (uint32_t)node, p, j, nom);
+            if (raw) gpu_apply_o(st, ee, md, &gx, (uint32_t)node, mask, p, j, nom >= 0 ? (int32_t)mi[nom].rid : -1);
             out_result[j] = KG_BATCH_ASSUMED;
             out_zone[j] = zone;
         }
@@ -3341,6 +3549,8 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
     free(vx.v);
     free(mv);
     free(mi);
+    free(md);
+    free(gx.g);
     free(done);
     free(b.mem);
     return 0;

@@ -84,6 +84,8 @@ typedef struct kgo_ext {
     uint32_t n_infos;
     const kg_rsv_dev* devs; /* GPU restore tables named by kg_rsv_view.dev_base / kg_rsv_info.dev */
     uint32_t n_devs;
+    const kg_rsv_gpu* gpu;  /* DeviceShare restore inputs of GPU-holding reservations (replay / batch follow them) */
+    uint32_t n_gpu;
 } kgo_ext;
 
 /* Verify matrix with every enabled plugin incl. KG_PLUGIN_DEV / RSV / QUOTA: raw Score values, totals

@@ -25,7 +25,8 @@ class KgoExt(C.Structure):
     _fields_ = [("quotas", C.POINTER(abi.KgQuotaColumns)), ("n_quotas", C.c_uint32),
                 ("views", C.POINTER(abi.KgRsvView)), ("n_views", C.c_uint32),
                 ("infos", C.POINTER(abi.KgRsvInfo)), ("n_infos", C.c_uint32),
-                ("devs", C.POINTER(abi.KgRsvDev)), ("n_devs", C.c_uint32)]
+                ("devs", C.POINTER(abi.KgRsvDev)), ("n_devs", C.c_uint32),
+                ("gpu", C.POINTER(abi.KgRsvGpu)), ("n_gpu", C.c_uint32)]
 
 
 def make_ext(quotas=None, rsv=None) -> KgoExt:
@@ -43,6 +44,9 @@ def make_ext(quotas=None, rsv=None) -> KgoExt:
         e.n_infos = rsv.n_infos
         e.devs = C.cast(rsv.devs, C.POINTER(abi.KgRsvDev))
         e.n_devs = rsv.n_devs
+        if getattr(rsv, "n_gpu", 0):
+            e.gpu = C.cast(rsv.gpu, C.POINTER(abi.KgRsvGpu))
+            e.n_gpu = rsv.n_gpu
         keep.append(rsv)
     e._keep = keep
     return e

@@ -227,18 +227,45 @@ def test_batch_schedule_ext(ctx, overfill):
 
 
 @pytest.mark.gpu
-def test_batch_schedule_refuses_gpu_reservations(ctx):
-    """Reservations that hold GPUs: their DeviceShare restore tables follow the reserve pods' minors (host path)."""
+@pytest.mark.parametrize("overfill", [False, True])
+def test_batch_schedule_with_gpu_reservations(ctx, overfill):
+    """Reservations that hold GPUs: the batch cycle follows each GPU pod's Reserve into the node's DeviceShare restore
+    inputs and tables (kg_snapshot_upload_rsv_gpu); results, minors, quota used and the GPU tables equal the oracle's,
+    and a failed job restores them (the select after it equals the oracle's on the untouched cluster)."""
     from koordinator_amd import engine
-    cfg, nodes, pods, quotas, rsv = synth.cluster5(300, 32, seed_config=48, rsv_frac=0.3)
-    assert any(int(i.dev) >= 0 for i in rsv.infos[:rsv.n_infos])
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(600, 160, seed_config=48, rsv_frac=0.5)
+    assert any(int(i.dev) >= 0 for i in rsv.infos[:rsv.n_infos]) and rsv.n_gpu > 0
+    pods = {k: v.copy() for k, v in pods.items()}
+    rng = np.random.default_rng(48)
+    pods["rsv_class"] = np.where(rng.random(len(pods["rsv_class"])) < 0.7,
+                                 rng.integers(0, synth.N_RSV_CLASSES, len(pods["rsv_class"])), -1).astype(np.int32)
+    pods["flags"] &= ~np.uint32(abi.KG_POD_RSV_REQUIRED)
     kc = cfg.kg_config()
+    ref_node, *_ = oracle_lib.OracleState(kc, nodes).ext_replay(pods, quotas, rsv=rsv)
+    ok = np.flatnonzero(ref_node >= 0)
+    sub, plan = abi.take(pods, ok), ref_node[ok].astype(np.int32)
+    if overfill:
+        plan[len(plan) // 2:] = plan[0]
+    order = grouped(plan)
+    sub, plan = abi.take(sub, np.asarray(order)), plan[order]
     snap = engine.Snapshot(ctx, kc, nodes)
     snap.upload_quotas(quotas)
     snap.upload_reservations(rsv)
-    pb = engine.PodBatch(ctx, pods)
-    with pytest.raises(engine.Unsupported):
-        engine.batch_schedule(snap, pb, np.zeros(32, np.int32))
+    pb = engine.PodBatch(ctx, sub)
+    res, stat, zone, minors = engine.batch_schedule(snap, pb, plan)
+    ost = oracle_lib.OracleState(kc, nodes)
+    rres, rstat, rzone, rminors, qu, _qn = ost.batch_schedule(sub, plan, quotas, rsv)
+    assert np.array_equal(res, rres) and np.array_equal(stat, rstat)
+    assert np.array_equal(zone, rzone) and np.array_equal(minors, rminors)
+    assert np.array_equal(snap.read_quotas()[0], qu)
+    assert np.array_equal(snap.read_state()["dev_free"], ost.dev_free())
+    if overfill:
+        assert (res == abi.KG_BATCH_FAILED).sum() >= 1
+        keys = engine.eval_select(snap, pb, 1)
+        want = oracle_lib.ext_select(kc, nodes, sub, 1, quotas=quotas, rsv=rsv)
+        assert np.array_equal(keys, want)
+    else:
+        assert (res == abi.KG_BATCH_ASSUMED).all() and (minors != 0).any()
 
 
 def _rsv_batch_case(overfill):

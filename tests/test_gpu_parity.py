@@ -207,7 +207,8 @@ def test_update_rows(ctx):
     snap.update_rows(rows, other)
     merged = {k: v.copy() for k, v in nodes.items()}
     for k in merged:
-        merged[k][rows] = other[k]
+        if k in other:  # (the oracle state also reports numa_zone_pods, which these tables leave to the default)
+            merged[k][rows] = other[k]
     assert_verify_equal(engine.eval_verify(snap, batch), oracle_lib.eval_verify(kc, merged, pods), "update_rows")
 
 
@@ -232,7 +233,8 @@ def test_update_rows_changing_numa_policy_keeps_assumed_state(ctx):
     snap.update_rows(rows, upd)
     merged = {k: v.copy() for k, v in state.items()}
     for k in merged:
-        merged[k][rows] = upd[k]
+        if k in upd:
+            merged[k][rows] = upd[k]
     rest = abi.take(pods, np.arange(200, 400))
     batch = engine.PodBatch(ctx, rest)
     assert_verify_equal(engine.eval_verify(snap, batch), oracle_lib.eval_verify(kc, merged, rest), "regroup")

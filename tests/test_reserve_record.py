@@ -236,3 +236,45 @@ def test_reserve_unreserve_round_trip_config5_views():
         assert r1.infos[x].allocated_pods == r0.infos[x].allocated_pods, x
     assert np.array_equal(engine.eval_select(snap, batch, 1), keys0)
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_reserve_unreserve_round_trip_gpu_reservations():
+    """Reservations that hold GPUs (restore inputs uploaded): kg_reserve of GPU pods on their best nodes (into the
+    reservations' minors where nominated) and kg_unreserve in reverse order restore the GPU tables, views, infos and the
+    select of the batch exactly; the Reserves matched the oracle replay's first placements."""
+    from koordinator_amd import engine
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(600, 150, seed_config=96, rsv_frac=0.5, usage="u01")
+    pods = {k: v.copy() for k, v in pods.items()}
+    rng = np.random.default_rng(96)
+    pods["rsv_class"] = np.where(rng.random(len(pods["rsv_class"])) < 0.7,
+                                 rng.integers(0, synth.N_RSV_CLASSES, len(pods["rsv_class"])), -1).astype(np.int32)
+    pods["flags"] &= ~np.uint32(abi.KG_POD_RSV_REQUIRED)
+    kc = cfg.kg_config()
+    ctx = engine.Context(0)
+    snap = engine.Snapshot(ctx, kc, nodes)
+    snap.upload_quotas(quotas)
+    snap.upload_reservations(rsv)
+    batch = engine.PodBatch(ctx, pods)
+    keys0 = engine.eval_select(snap, batch, 1)
+    state0, q0, r0 = snap.read_state(), snap.read_quotas(), snap.read_reservations(rsv)
+    best = np.where(keys0[:, 0] != 0, abi.key_node(keys0[:, 0]), -1)
+    done = []
+    for j in range(abi.table_len(pods)):
+        if best[j] >= 0:
+            try:
+                done.append((j, int(best[j]), engine.reserve(snap, batch, j, int(best[j]))))
+            except engine.ReserveFailed:
+                pass
+    assert sum(1 for _, _, r in done if r.gpu_minors and r.rsv_rid >= 0) >= 2
+    for j, node, rec in reversed(done):
+        engine.unreserve(snap, batch, j, node, rec)
+    oracle_lib.assert_state_restored(state0, snap.read_state())
+    for a, b in zip(q0, snap.read_quotas()):
+        assert np.array_equal(a, b)
+    r1 = snap.read_reservations(rsv)
+    for x in range(rsv.n_infos):
+        assert list(r1.infos[x].allocated) == list(r0.infos[x].allocated), x
+        assert r1.infos[x].allocated_pods == r0.infos[x].allocated_pods, x
+    assert np.array_equal(engine.eval_select(snap, batch, 1), keys0)
+    ctx.close()

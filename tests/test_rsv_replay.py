@@ -179,3 +179,116 @@ def test_replay_with_cpuset_pods(ctx, numa, seed):
     want = st.table()
     for k in ("req_cpu", "req_mem", "num_pods", "cpuset_alloc_milli", "numa_zone_status", "cpu_alloc"):
         assert np.array_equal(dev[k], want[k]), k
+
+
+def _gpu_cluster(n_nodes=300, n_pods=120, seed=85, numa="none"):
+    cfg, nodes, pods, quotas, rsv, true_t, resv = synth.cluster5(n_nodes, n_pods, seed_config=seed, rsv_frac=0.5,
+                                                                 rsv_gpu=True, raw=True, numa=numa)
+    pods = {k: v.copy() for k, v in pods.items()}
+    rng = np.random.default_rng(seed)
+    pods["rsv_class"] = np.where(rng.random(n_pods) < 0.7, rng.integers(0, synth.N_RSV_CLASSES, n_pods),
+                                 -1).astype(np.int32)
+    pods["flags"] &= ~np.uint32(abi.KG_POD_RSV_REQUIRED)
+    return cfg, nodes, pods, quotas, rsv, true_t, resv
+
+
+def _dev_alloc_of(pods, j, total_mem):
+    """fillGPUTotalMem's per-minor allocation of pod j (gpu-core, ratio, memory)."""
+    keys = int(pods["dev_keys"][j])
+    req = pods["dev_req"][j]
+    core = int(req[abi.KG_DEV_CORE]) if keys & (1 << abi.KG_DEV_CORE) else 0
+    hr, hm = keys & (1 << abi.KG_DEV_RATIO), keys & (1 << abi.KG_DEV_MEM)
+    if hr and hm:
+        return core, int(req[abi.KG_DEV_RATIO]), int(req[abi.KG_DEV_MEM])
+    if hm:
+        mem = int(req[abi.KG_DEV_MEM])
+        return core, int(oracle_lib.lib().kgo_mem_bytes_to_ratio(mem, int(total_mem))), mem
+    ratio = int(req[abi.KG_DEV_RATIO]) if hr else 0
+    return core, ratio, ratio * int(total_mem) // 100
+
+
+@pytest.mark.parametrize("seed,numa", [(85, "none"), (86, "single")])
+def test_oracle_replay_follows_the_gpu_restore(seed, numa):
+    """Reservations that hold GPUs (deviceshare/reservation.go:139-198): the oracle replay, which follows each
+    placement into the node's raw used, the joined reservation's allocated minors and every restore table of the node
+    (gpu_rebuild_o), places every pod where a step-by-step replay places it that recomputes the whole restore, GPU
+    tables included, from the true NodeInfo, device used and reservation bookkeeping before each pod
+    (decode.reservation_restore); and its final record GPU tables equal that restore's."""
+    cfg, nodes, pods, quotas, rsv, true_t, resv = _gpu_cluster(300, 200, seed, numa)
+    assert rsv.n_gpu > 0
+    kc = cfg.kg_config()
+    kc.plugins &= ~abi.KG_PLUGIN_QUOTA
+    st0 = oracle_lib.OracleState(kc, nodes)
+    rnode, rtotal, rminors, _, _ = st0.ext_replay(pods, None, rsv=rsv)
+    T = {k: np.array(v, copy=True) for k, v in true_t.items()}
+    R = [dict(r) for r in resv]
+    for r in R:
+        for key in ("dev_alloc", "dev_allocated"):
+            if r.get(key) is not None:
+                r[key] = np.array(r[key], copy=True)
+    n_pods = abi.table_len(pods)
+    gpu_into = 0
+    for j in range(n_pods):
+        D, views, infos, devs = decode.reservation_restore(T, R)
+        rs = abi.Reservations(views, infos, devs)
+        one = abi.take(pods, np.array([j]))
+        v = oracle_lib.ext_verify(kc, D, one, None, rs)
+        tot = np.where(v.status[0] == 0, v.total[0], -1)
+        want = int(np.argmax(tot)) if tot.max() >= 0 else -1
+        assert rnode[j] == want, (j, rnode[j], want)
+        if want < 0:
+            continue
+        assert rtotal[j] == tot[want]
+        nom = oracle_lib.ext_pair_nominated(kc, D, want, one, 0, None, rs)
+        x = int(infos[nom]["rid"]) if nom >= 0 else -1
+        if x >= 0:
+            _reserve_into(R[x], infos[nom], pods, j)
+        mask = int(rminors[j])
+        for m in range(abi.KG_DEV_MINORS):
+            if not (mask >> m) & 1:
+                continue
+            a = _dev_alloc_of(pods, j, T["dev_total"][want, abi.KG_DEV_MEM, m])
+            for r_ in range(abi.KG_DEV_R):
+                T["dev_used"][want, r_, m] += a[r_]
+                if x >= 0 and R[x].get("dev_alloc") is not None and np.any(R[x]["dev_alloc"][:, m] != 0):
+                    if R[x].get("dev_allocated") is None:
+                        R[x]["dev_allocated"] = np.zeros((abi.KG_DEV_R, abi.KG_DEV_MINORS), np.int64)
+                    R[x]["dev_allocated"][r_, m] += a[r_]
+                    gpu_into += r_ == 0
+        T["dev_free"][want] = np.maximum(T["dev_total"][want] - T["dev_used"][want], 0)
+        st = oracle_lib.OracleState(kc, T)
+        st.assume(want, one, 0)
+        for k, val in st.table().items():
+            if k in T and k not in ("dev_free",):
+                T[k] = val
+    assert gpu_into >= 2  # GPU pods did land inside GPU-holding reservations
+    D, _, _, _ = decode.reservation_restore(T, R)
+    assert np.array_equal(st0.dev_free(), D["dev_free"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,numa", [(87, "none"), (88, "single")])
+def test_replay_with_gpu_reservations(ctx, seed, numa):
+    """kg_replay of a config-5 batch whose reservations hold GPUs (their DeviceShare restore inputs uploaded with the
+    views): every GPU pod's Reserve follows the node's used, the joined reservation's allocated minors and the node's
+    restore tables on the device; placements, totals, reasons, minors, quota used and the final GPU tables equal the
+    oracle replay's (which the CPU test above pins against the restore recomputed every step)."""
+    from koordinator_amd import engine
+    cfg, nodes, pods, quotas, rsv, _, _ = _gpu_cluster(1200, 300, seed, numa)
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    snap.upload_quotas(quotas)
+    snap.upload_reservations(rsv)
+    batch = engine.PodBatch(ctx, pods)
+    node, total, why = engine.replay(snap, batch, reasons=True)
+    minors = engine.replay_minors(batch)
+    st = oracle_lib.OracleState(kc, nodes)
+    onode, ototal, ominors, qu, qn, owhy = st.ext_replay(pods, quotas, rsv=rsv, reasons=True)
+    assert np.array_equal(node, onode)
+    assert np.array_equal(total, ototal)
+    assert np.array_equal(why, owhy)
+    assert np.array_equal(minors, ominors)
+    used, _, npu, _ = snap.read_quotas()
+    assert np.array_equal(used, qu) and np.array_equal(npu, qn)
+    assert np.array_equal(snap.read_state()["dev_free"], st.dev_free())
+    assert (node >= 0).sum() > 100

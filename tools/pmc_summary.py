@@ -33,6 +33,28 @@ def per_kernel(path):
     return {k: dict(d) for k, d in agg.items()}, {k: len(v) for k, v in ids.items()}
 
 
+def per_kernel_issue(name, trace, counters, tsteps):
+    """One bracket kernel: its trace entry, counters per step, its time per step (average duration x dispatches per
+    step: config 5's k_ext_select runs twice a step, the guess launch and a short re-run) and its VALU issue fraction
+    with the instruction costs of profiles/valu_mix.json (the kernel's loop priced per opcode; 4.1 cycles without one)."""
+    import bench
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from valu_mix import canon_demangled
+    out = {"trace": trace, "counters": counters}
+    if not trace:
+        return out
+    ns = trace["avg_ns"] * trace["calls"] / max(tsteps, 1)
+    out["ns_per_step"] = ns
+    mix = bench.load_pmc("valu_mix.json")
+    m = (mix or {}).get("kernels", {}).get(canon_demangled(name) or "")
+    cyc = m["cyc_per_valu"] if m else 4.1
+    v = counters.get("SQ_INSTS_VALU", 0.0)
+    if ns > 0:
+        out["issue"] = {"cycles_per_valu": cyc, "frac": v * cyc / (ns * 1e-9 * bench.SIMD_CYCLES),
+                        "priced_by": "profiles/valu_mix.json" if m else "4.1 cycles (no ISA mix)"}
+    return out
+
+
 def main(prof, out, names):
     import bench
 
@@ -68,7 +90,7 @@ def main(prof, out, names):
         "hbm_bytes_per_launch": 1024.0 * (2.0 * total("FETCH_SIZE") + total("WRITE_SIZE")),
         "valu_insts_per_launch": total("SQ_INSTS_VALU"),
         "salu_insts_per_launch": total("SQ_INSTS_SALU"),
-        "kernels": {k: {"trace": stats.get(k), "counters": v} for k, v in sel.items()},
+        "kernels": {k: per_kernel_issue(k, stats.get(k), v, tsteps) for k, v in sel.items()},
         "select_avg_ns_sum": sum((stats.get(k) or {}).get("avg_ns", 0.0) * (stats.get(k) or {}).get("calls", 0) / tsteps
                                  for k in sel),
         "all_kernels_trace": stats,
