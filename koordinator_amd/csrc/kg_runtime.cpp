@@ -3282,7 +3282,10 @@ kg_status kg_snapshot_upload_rsv_gpu(kg_snap* s, const kg_rsv_gpu* g, uint32_t n
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!s->uploaded) return fail(ctx, KG_INVALID_ARG, "snapshot not uploaded");
-    if (!s->d_dev) return fail(ctx, KG_INVALID_ARG, "no DeviceShare tables in this snapshot");
+    if (!s->d_dev) {  // DeviceShare is off here: the GPU restore tables matter to no plugin
+        s->gpu_raw = true;
+        return KG_OK;
+    }
     // node entries (rid -1) and each node's reservation entries, grouped by node
     std::vector<int32_t> node_entry(s->n, -1);
     std::vector<std::vector<uint32_t>> rsv_of(s->n);

@@ -209,11 +209,24 @@ def test_ext_replay(ctx):
     assert (node < 0).any() and (minors != 0).any()
 
 
-def test_ext_replay_rejects_reservations(ctx):
+def _without_gpu_inputs(rsv):
+    """The same views and tables without the DeviceShare restore inputs of GPU-holding reservations."""
+    r = abi.Reservations([], [])
+    r.views, r.n_views, r.infos, r.n_infos, r.devs, r.n_devs = rsv.views, rsv.n_views, rsv.infos, rsv.n_infos, rsv.devs, \
+        rsv.n_devs
+    return r
+
+
+def test_ext_replay_rejects_gpu_reservations_without_inputs(ctx):
+    """Reservations that hold GPUs and no restore inputs: the replay cannot follow their DeviceShare tables
+    (KG_UNSUPPORTED); with the inputs it runs (tests/test_rsv_replay.py checks it against the oracle)."""
     cfg, nodes, pods, quotas, rsv = synth.cluster5(300, 20, seed_config=42)
-    snap, batch = make(ctx, cfg.kg_config(), nodes, pods, quotas, rsv)
+    assert rsv.n_gpu > 0
+    snap, batch = make(ctx, cfg.kg_config(), nodes, pods, quotas, _without_gpu_inputs(rsv))
     with pytest.raises(engine.Unsupported):
         engine.replay(snap, batch)
+    snap.upload_reservations(rsv)
+    engine.replay(snap, batch)
 
 
 def test_ext_assume_forget_roundtrip(ctx):
@@ -370,7 +383,8 @@ def test_view_update_after_assume_on_view_node(ctx):
     pods["quota"][j] = -1  # no ElasticQuota Reserve to follow in the oracle table
     ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
     assert ref.status[j, i] == 0
-    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    # without the GPU restore inputs the Reserve cannot follow the node's GPU-holding reservations: its views go stale
+    snap, batch = make(ctx, kc, nodes, pods, quotas, _without_gpu_inputs(rsv))
     engine.eval_select(snap, batch, 1)
     engine.assume_ext(snap, batch, j, i)
     with pytest.raises(engine.Unsupported):
