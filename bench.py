@@ -280,14 +280,15 @@ def replay_rate(ctx, cfg, with_cpu, cpu_s, config=3):
 
 
 def replay5_rate(ctx, with_cpu, cpu_s):
-    """Config 5 one pod per cycle: the config-5 cluster (100k nodes x 10k pods, every plugin) with reservations
-    that hold no GPU, so that kg_replay runs Reservation.Reserve and the ElasticQuota / DeviceShare Reserve on the
-    device between pods."""
+    """Config 5 one pod per cycle: the config-5 cluster of the select (100k nodes x 10k pods, every plugin, reservations
+    holding GPUs with their DeviceShare restore inputs), kg_replay running every plugin's Reserve on the device between
+    pods: NodeInfo, LoadAware, NUMA, GPU minors (and the GPU-holding reservations' restore tables), ElasticQuota and
+    Reservation.Reserve."""
     import numpy as np
 
     from koordinator_amd import abi, engine, synth
 
-    cfg, nodes, pods, quotas, rsv = synth.config5(rsv_gpu=False)
+    cfg, nodes, pods, quotas, rsv = synth.config5()
     kc = cfg.kg_config()
     snap = engine.Snapshot(ctx, kc, nodes)
     snap.upload_quotas(quotas)
@@ -305,7 +306,7 @@ def replay5_rate(ctx, with_cpu, cpu_s):
     out = {"pods_placed_per_s": batch.n / dt, "pods": batch.n, "placed": placed, "seconds": round(dt, 4),
            "workload": (f"config5: {snap.n // 1000}k nodes x {batch.n // 1000}k pods, one pod per cycle, Reserve of "
                         "every plugin (NodeInfo, LoadAware, NUMA, GPU minors, ElasticQuota, Reservation) on device; "
-                        "reservations hold no GPU")}
+                        "reservations holding GPUs followed through their restore tables")}
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib  # test infrastructure: the CPU baseline leg only
