@@ -15,38 +15,18 @@
 // maximum to be the class's best fitting score (k_dev_sum's cls_max), records the real one, and k_ext_fix_rows
 // re-runs the rows whose guess was wrong, so no pair is evaluated twice unless its pod's guess failed.
 // Between the passes the multi-GPU path all-reduces the per-pod maxima over RCCL.
-// k_ext_replay   one pod per launch (lane = node record): applies the previous pod's Reserve in place
-//                (NodeInfo, LoadAware, NUMA zone, GPU minors, quota used, Reservation), gates the next pod on its
-//                quota, evaluates it, and reduces per DeviceShare raw score bucket; the launch's last workgroup
-//                normalises over the buckets and picks the pod's winner (no second launch per step).
+// The sequential replay's step kernel (k_ext_replay, k_ext_assume) lives in kg_ext_replay.hip, the batch cycle
+// (k_batch, k_batch_coop) in kg_ext_batch.hip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 
 #include "kg_cpuset_reserve.h"
 #include "kg_ext.h"
+#include "kg_ext_wave.h"
 #include "kg_kernels.h"
 
 namespace kg {
-
-__device__ __forceinline__ uint64_t wmax_u64(uint64_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(v, off, 64);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-__device__ __forceinline__ int32_t wmax_i32(int32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-    return v;
-}
-
-__device__ __forceinline__ const DevRec* dev_of(const ExtDev& e, uint32_t rec) { return e.dev ? e.dev + rec : nullptr; }
-
-constexpr uint32_t DSUM_CHUNK = 8;  // GPU request classes per thread of k_dev_sum / k_rdev_codes
 
 // DevSum of every record for the pod batch's GPU request classes: thread = record; it loads the record's minors
 // once and, per class, runs the GPU allocator's Filter and scores one instance (codes / scores stored 8 classes at
@@ -758,465 +738,8 @@ __global__ __launch_bounds__(256) void k_scatter_keys(const uint64_t* src, const
     if (rejected && pstat) pstat[j] = qst[j];
 }
 
-// Winner of pod `step` (one wave: the last workgroup of the step's launch, after every other workgroup evaluated the
-// pod): NormalizeScore of DeviceShare from the score buckets (M = the highest raw score among the feasible nodes; a
-// bucket's key is base total << 32 | index, so key(b) = base + w_dev * 100 s / M) and, with reservation views, of
-// Reservation (the listed pairs' maximum, or 1000 and the preferred node at 1000 when a reservation order exists,
-// total_ext). A pair off the list has a zero Reservation term, so its bucket key is its total; a listed pair's bucket
-// key is a lower bound of its total: the maximum over the buckets and the list is the winner.
-__device__ __forceinline__ uint64_t ext_replay_pick(uint32_t step, uint32_t n_nodes, const KCfg& cfg,
-                                                    const uint64_t* __restrict__ buckets, const RsvStep* __restrict__ rs,
-                                                    const uint64_t* __restrict__ rlist) {
-    const uint32_t lane = threadIdx.x;
-    const uint64_t* B = buckets + (size_t)(step % 3) * 128;
-    const uint64_t b0 = B[lane], b1 = B[lane + 64];
-    const int32_t M = wmax_i32(max(b0 ? (int32_t)lane : -1, b1 ? (int32_t)lane + 64 : -1));
-    if (M < 0) return 0ull;  // no feasible node (a listed pair is also in its bucket)
-    auto cand = [&](uint64_t b, int64_t sd) -> uint64_t {
-        if (!b) return 0ull;
-        const int64_t tot = (int64_t)(b >> 32) + (int64_t)cfg.w_dev * norm100(sd, M);
-        return ((uint64_t)tot << 32) | (b & 0xFFFFFFFFull);
-    };
-    const uint64_t c0 = cand(b0, lane), c1 = cand(b1, lane + 64);
-    uint64_t best = c0 > c1 ? c0 : c1;
-    if (rs) {
-        const RsvStep& z = rs[step % 3];
-        const uint64_t pf = z.pref;
-        const int64_t rm = pf != PREF_NONE ? 1000 : (int64_t)z.rmax;
-        const uint32_t cnt = z.cnt;
-        const uint64_t* L = rlist + (size_t)(step % 3) * n_nodes * 2;
-        for (uint32_t k = lane; k < cnt; k += 64) {
-            const uint64_t kb = L[2 * (size_t)k], sc = L[2 * (size_t)k + 1];
-            const uint32_t g = 0xFFFFFFFFu - (uint32_t)(kb & 0xFFFFFFFFull);
-            const int64_t sd = (int64_t)(uint32_t)(sc >> 32);
-            const int64_t rsv = (pf != PREF_NONE && (uint32_t)pf == g) ? 1000 : (int64_t)(uint32_t)sc;
-            const int64_t tot = (int64_t)(kb >> 32) + (int64_t)cfg.w_dev * norm100(sd, M) + (int64_t)cfg.w_rsv * norm100(rsv, rm);
-            const uint64_t key = ((uint64_t)tot << 32) | (kb & 0xFFFFFFFFull);
-            best = key > best ? key : best;
-        }
-    }
-    return wmax_u64(best);
-}
-
-// One replay step (see file header). buckets: [3][128] ring of per-DeviceShare-score best keys. winners[step - 1] holds
-// the key the previous launch picked for pod step - 1; every workgroup drops it when the pair's Reserve fails (zone code
-// of its pair, or a cpuset Reserve that failed in between, k_cpuset_reserve), applies the Reserve, gates and evaluates
-// pod `step`. The last workgroup to finish (done counter) then picks pod step's winner into winners[step] and settles
-// winners[step - 1] (0 when its Reserve failed): no other launch per step.
-template <bool EXACT>
-__global__ __launch_bounds__(64) void k_ext_replay(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
-                                                   DevRec* __restrict__ devs, ExtDev e, PodsDev pods, uint32_t n_pods,
-                                                   uint32_t n_nodes, uint32_t index_base, KCfg cfg,
-                                                   const uint32_t* __restrict__ step_base, uint32_t step_off,
-                                                   uint64_t* __restrict__ winners, uint32_t* __restrict__ minors,
-                                                   uint64_t* __restrict__ buckets, int8_t* __restrict__ zsel,
-                                                   uint32_t* __restrict__ reason, const uint32_t* __restrict__ pos,
-                                                   int32_t* __restrict__ nsel, RsvStep* __restrict__ rs,
-                                                   uint64_t* __restrict__ rlist, uint32_t* __restrict__ done) {
-    const uint32_t step = (step_base ? *step_base : 0u) + step_off;
-    if (step > n_pods) return;  // uniform
-    const uint32_t lane = threadIdx.x;
-    const uint32_t i = blockIdx.x * 64u + lane;
-    const bool live = i < n_nodes;
-    const bool has_next = step < n_pods;
-    uint64_t prev = step > 0 ? __hip_atomic_load(&winners[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-    // the winner's Reserve fails (BestEffort NUMA allocation, or a cpuset Reserve that failed between the launches: zone
-    // code of its pair): the pod stays unscheduled. zsel is double-buffered by step parity: every block reads the
-    // previous step's codes while this step's are written
-    int32_t prev_zone = -1;
-    if (prev != 0ull) {
-        prev_zone = zsel[(size_t)((step - 1) & 1u) * n_nodes + pos[(0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull)) - index_base]];
-        if (zone_reserve_fails(prev_zone)) {
-            if (blockIdx.x == 0 && lane == 0 && reason) atomicOr(reason + step - 1, zone_fail_status(prev_zone));
-            prev = 0ull;
-        }
-    }
-    if (blockIdx.x == 0) {
-        uint64_t* Z = buckets + (size_t)((step + 1) % 3) * 128;  // last read by the pick of step - 2
-        Z[lane] = 0;
-        Z[lane + 64] = 0;
-        if (rs && lane == 0) {  // slot of step + 1 (last read by the pick of step - 2)
-            RsvStep& z = rs[(step + 1) % 3];
-            z.win = 0;
-            z.pref = PREF_NONE;
-            z.cnt = 0;
-            z.rmax = 0;
-        }
-    }
-    // Reserve of pod step-1 on its winner
-    if (live && prev != 0ull) {
-        const uint32_t g = 0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull);
-        if (g == index_base + node_index(nodes[i])) {
-            const PodV q = load_pod(pods, step - 1);
-            const PodX qx = load_podx(pods, step - 1);
-            apply_assume(cfg, nodes[i].v, zones + i, q, prev_zone, 1);
-            // the nominated reservation of the winning pair (nsel, double-buffered like zsel)
-            const int32_t nom = ((cfg.plugins & KG_PLUGIN_RSV) && nsel && nodes[i].v[N_RSV_CLASSES] != 0)
-                                    ? nsel[(size_t)((step - 1) & 1u) * n_nodes + i] : -1;
-            uint32_t mask = 0;
-            if ((cfg.plugins & KG_PLUGIN_DEV) && qx.dcount > 0) {
-                mask = dev_choose_site(cfg, e, nodes[i].v, zones + i, devs + i, pod_view(cfg, e, nodes[i].v, i, qx), nom, qx,
-                                       prev_zone);
-                minors[step - 1] = mask;
-            }
-            // Reservation.Reserve into the nominated reservation, then DeviceShare's (the node's minors, or the
-            // restore inputs and tables of GPU-holding reservations)
-            if ((cfg.plugins & KG_PLUGIN_RSV) && nsel && nodes[i].v[N_RSV_CLASSES] != 0)
-                rsv_reserve_dev(e, nodes[i].v, zones + i, i, q, nom);
-            dev_reserve_apply(cfg, e, nodes[i].v, i, devs + i, mask, qx, nom >= 0 ? (int32_t)e.infos[nom].rid : -1, 1);
-        }
-    }
-    // ElasticQuota: buffer (step-1)&1 holds the state after pods < step-1; buffer step&1 becomes the
-    // state after pods < step (block 0, nobody reads it during this launch). winners[step - 2] was settled by the last
-    // workgroup of the previous launch.
-    uint32_t qst = 0;
-    PodV p = load_pod(pods, has_next ? step : 0);
-    PodX px = load_podx(pods, has_next ? step : 0);
-    if (cfg.plugins & KG_PLUGIN_QUOTA) {
-        const uint32_t nq = e.n_quotas;
-        const QuotaState* rd = e.qstate + (size_t)((step - 1) & 1u) * nq;
-        PodX x1;
-        PodV p1;
-        bool placed1 = false;
-        if (step > 0) {
-            p1 = load_pod(pods, step - 1);
-            x1 = load_podx(pods, step - 1);
-            placed1 = prev != 0ull;
-        }
-        if (has_next && px.quota >= 0 && (uint32_t)px.quota < nq) {
-            QuotaState S = rd[px.quota];
-            if (placed1 && x1.quota == px.quota) quota_add(S, p1, x1, 1);
-            qst = quota_gate(e.qlim[px.quota], S, p, px);
-        }
-        if (blockIdx.x == 0 && lane == 0) {
-            QuotaState* wr = e.qstate + (size_t)(step & 1u) * nq;
-            if (step > 1 && winners[step - 2] != 0ull) {
-                const PodV p2 = load_pod(pods, step - 2);
-                const PodX x2 = load_podx(pods, step - 2);
-                if (x2.quota >= 0 && (uint32_t)x2.quota < nq) quota_add(wr[x2.quota], p2, x2, 1);
-            }
-            if (placed1 && x1.quota >= 0 && (uint32_t)x1.quota < nq) quota_add(wr[x1.quota], p1, x1, 1);
-        }
-    }
-    if (has_next) {  // the final step only applies the last Reserve
-        uint64_t kb = 0;
-        int32_t s = 0;
-        uint32_t stat = 0;
-        if (live) {
-            const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, qst);
-            zsel[(size_t)(step & 1u) * n_nodes + i] = (int8_t)r.zone;
-            if (nsel) nsel[(size_t)(step & 1u) * n_nodes + i] = r.nom;
-            stat = r.status;
-            if (!r.status) {
-                const int64_t base = (int64_t)cfg.w_nrf * r.s_nrf + (int64_t)cfg.w_la * r.s_la + (int64_t)cfg.w_numa * r.s_numa;
-                const uint32_t g = index_base + node_index(nodes[i]);
-                kb = ((uint64_t)base << 32) | (uint64_t)(0xFFFFFFFFu - g);
-                s = (int32_t)r.s_dev;
-                if (rs && (r.s_rsv != 0 || r.order != 0)) {
-                    // a pair whose Reservation score term can be nonzero: listed for the pick (its bucket entry stays, a
-                    // lower bound of its total)
-                    RsvStep& z = rs[step % 3];
-                    const uint32_t at = atomicAdd(&z.cnt, 1u);
-                    rlist[((size_t)(step % 3) * n_nodes + at) * 2] = kb;
-                    rlist[((size_t)(step % 3) * n_nodes + at) * 2 + 1] = ((uint64_t)(uint32_t)r.s_dev << 32) | (uint32_t)r.s_rsv;
-                    if (r.s_rsv) atomicMax(&z.rmax, (uint32_t)r.s_rsv);
-                    if (r.order != 0) atomicMin((unsigned long long*)&z.pref, (unsigned long long)pref_key(r.order, g));
-                }
-            }
-        }
-        if (reason) {  // FitError diagnosis: OR of the filter status bits over the nodes
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) stat |= (uint32_t)__shfl_xor((int)stat, off, 64);
-            if (lane == 0 && stat) atomicOr(reason + step, stat);
-        }
-        // per-score-bucket wave max, one atomic per distinct score in the wave
-        uint64_t* B = buckets + (size_t)(step % 3) * 128;
-        bool pending = kb != 0ull;
-        uint64_t m = __ballot(pending);
-        while (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            const int32_t sl = __shfl(s, leader, 64);
-            const bool mine = pending && s == sl;
-            const uint64_t v = wmax_u64(mine ? kb : 0ull);
-            if ((int)lane == leader) atomicMax((unsigned long long*)(B + sl), (unsigned long long)v);
-            pending = pending && !mine;
-            m = __ballot(pending);
-        }
-    }
-    // the last workgroup of the launch: pick pod step's winner, settle pod step-1's
-    __threadfence();  // this workgroup's list entries / bucket atomics before its arrival
-    uint32_t ticket = 0;
-    if (lane == 0) ticket = atomicAdd(done, 1u);
-    ticket = (uint32_t)__shfl((int)ticket, 0, 64);
-    if (ticket != gridDim.x - 1u) return;  // uniform per workgroup
-    __threadfence();  // every other workgroup's writes are visible from here
-    if (has_next) {
-        const uint64_t w = ext_replay_pick(step, n_nodes, cfg, buckets, rs, rlist);
-        if (lane == 0) winners[step] = w;
-    }
-    if (lane == 0) {
-        if (step > 0 && prev == 0ull) winners[step - 1] = 0ull;  // the Reserve failed: unscheduled
-        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Reserve (sign +1: zone and minors chosen here, or preset in out by an evaluation pass) / Unreserve (sign -1: the
-// given zone and minors). sign 0: the evaluation pass alone, which presets out for a cpuset Reserve and the Reserve.
-// out: [0] zone, [1] minors, [2] nominated reservation (index into e.infos), [3] its rid (-1 = none).
-// split (nullable): the NUMA allocation's per-zone amounts (cpu, then memory), written by a Reserve (zeroed by the
-// caller; a cpuset Reserve under a NUMA affinity wrote them already) and given back by an Unreserve with the zone code
-// 0x40 | mask. rsv: Reservation.Reserve / Unreserve on the node's views (an Unreserve into the reservation rid_in).
-// cpus (Unreserve, nullable): the cpuset CPUs to release (NodeAllocation.release).
-template <bool EXACT>
-__global__ void k_ext_assume(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones, DevRec* __restrict__ devs, ExtDev e,
-                             PodsDev pods, uint32_t pod, uint32_t rec, int32_t zone_in, uint32_t minors_in, int64_t sign,
-                             KCfg cfg, int32_t* __restrict__ out, int64_t* __restrict__ split, bool rsv, int32_t rid_in,
-                             kg_cpu_alloc* __restrict__ allocs, const kg_cpu_topo* __restrict__ topos,
-                             const uint64_t* __restrict__ cpus) {
-    if (blockIdx.x != 0) return;
-    // the whole wave evaluates (uniform work on a full exec mask), lane 0 applies
-    const PodV q = load_pod(pods, pod);
-    const PodX qx = load_podx(pods, pod);
-    int64_t* n = nodes[rec].v;
-    int32_t zone = zone_in;
-    uint32_t mask = minors_in;
-    int32_t nom = -1;
-    if (sign >= 0 && out && zone_is_preset(out[0])) {
-        // the evaluation pass ran before the cpuset Reserve (which may have failed it): zone, minors and nominated
-        // reservation of the pre-take state
-        zone = zone_of_preset(out[0]);
-        mask = (uint32_t)out[1];
-        nom = out[2];
-        if (zone_reserve_fails(zone)) {
-            if (threadIdx.x == 0) out[0] = zone, out[1] = 0;
-            return;
-        }
-    } else if (sign >= 0) {
-        const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, 0u);
-        zone = r.status ? -1 : r.zone;
-        nom = r.status ? -1 : r.nom;
-        if (zone_reserve_fails(zone)) {  // the NodeNUMAResource Reserve fails: nothing is applied
-            if (out && threadIdx.x == 0) {
-                out[0] = sign == 0 ? zone_preset(zone) : zone;
-                out[1] = 0;
-            }
-            return;
-        }
-        mask = ((cfg.plugins & KG_PLUGIN_DEV) && devs)
-                   ? dev_choose_site(cfg, e, n, zones + rec, devs + rec, pod_view(cfg, e, n, rec, qx), nom, qx, zone) : 0u;
-        if (sign == 0) {  // evaluation pass only (a cpuset Reserve runs next)
-            if (out && threadIdx.x == 0) out[0] = zone_preset(zone), out[1] = (int32_t)mask, out[2] = nom;
-            return;
-        }
-    }
-    __syncthreads();  // every lane has read the state before lane 0 changes it
-    if (threadIdx.x != 0) return;
-    if (sign < 0 && cpus && allocs && topos) cpuset_release_lane(nodes, zones, allocs, topos, rec, cpus);
-    apply_assume(cfg, n, zones + rec, q, zone, sign, split);
-    const bool rsv_on = rsv && (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views;
-    if (rsv_on) {
-        if (sign > 0) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
-        else rsv_unreserve_dev(e, n, zones + rec, rec, q, rid_in);
-    }
-    const int32_t rid = sign > 0 ? (nom >= 0 ? (int32_t)e.infos[nom].rid : -1) : rid_in;
-    dev_reserve_apply(cfg, e, n, rec, devs ? devs + rec : nullptr, mask, qx, rsv_on ? rid : -1, sign);
-    if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
-        quota_add(e.qstate[qx.quota], q, qx, sign);
-        quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, sign);
-    }
-    if (out) {
-        out[0] = zone;
-        out[1] = (int32_t)mask;
-        out[2] = nom;
-        out[3] = nom >= 0 ? (int32_t)e.infos[nom].rid : -1;
-    }
-}
-
-// Inline batch scheduling cycle of a whole-job plan (batch/engine.go:92-294 RunSchedulingCycle): the
-// plan's pods are grouped by planned node; per group, in the caller's order, PreFilter (the ElasticQuota
-// gate against the current used) + Filter on that node, then Reserve (NodeInfo, LoadAware, NUMA zone,
-// GPU minors, quota used). The first failure in a group stops it: the later pods of the group get the
-// same status (engine.go:188-192 "for k := j"), the earlier ones stay assumed until the host decides on
-// cleanup. Groups hold disjoint nodes, so one lane per group runs them in parallel like the engine's
-// parallelizer.Until over podRequestsByNode; with ElasticQuota on (a state every group shares) lane 0
-// runs the groups in order instead, which keeps the quota verdicts deterministic.
-template <bool EXACT, bool EXT>
-__global__ __launch_bounds__(64) void k_batch(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
-                                              DevRec* __restrict__ devs, ExtDev e, PodsDev pods,
-                                              const uint32_t* __restrict__ grp_begin, const uint32_t* __restrict__ grp_pods,
-                                              const uint32_t* __restrict__ grp_rec, uint32_t n_groups, bool serial,
-                                              KCfg cfg, uint32_t* __restrict__ result, uint32_t* __restrict__ status,
-                                              int32_t* __restrict__ zone_out, uint32_t* __restrict__ minors_out) {
-    const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t g0 = serial ? 0u : lane, g1 = serial ? (lane == 0 ? n_groups : 0u) : min(lane + 1u, n_groups);
-    for (uint32_t g = g0; g < g1; g++) {
-        const uint32_t rec = grp_rec[g];
-        int64_t* n = nodes[rec].v;
-        uint32_t failed = 0;
-        for (uint32_t t = grp_begin[g]; t < grp_begin[g + 1]; t++) {
-            const uint32_t j = grp_pods[t];
-            zone_out[j] = -1;
-            minors_out[j] = 0;
-            if (failed) {
-                result[j] = KG_BATCH_SIBLING;
-                status[j] = failed;
-                continue;
-            }
-            const PodV q = load_pod(pods, j);
-            uint32_t st;
-            int32_t zone;
-            uint32_t mask = 0;
-            int32_t nom = -1;
-            PodX qx{};
-            if constexpr (EXT) {
-                qx = load_podx(pods, j);
-                uint32_t qst = 0;
-                if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas)
-                    qst = quota_gate(e.qlim[qx.quota], e.qstate[qx.quota], q, qx);
-                const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, qst);
-                st = r.status;
-                zone = r.zone;
-                nom = r.nom;
-                if (!st && !zone_reserve_fails(zone) && (cfg.plugins & KG_PLUGIN_DEV) && devs)
-                    mask = dev_choose_site(cfg, e, n, zones + rec, devs + rec, pod_view(cfg, e, n, rec, qx), nom, qx, zone);
-            } else {
-                const PairOut r = eval_pair<EXACT>(cfg, n, zones + rec, q);
-                st = r.status;
-                zone = r.zone;
-            }
-            if (!st && zone_reserve_fails(zone)) st = zone_fail_status(zone);  // Reserve fails (engine.go:270-280)
-            if (st) {
-                failed = st;
-                result[j] = KG_BATCH_FAILED;
-                status[j] = st;
-                continue;
-            }
-            apply_assume(cfg, n, zones + rec, q, zone, 1);
-            if constexpr (EXT) {
-                if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
-                    quota_add(e.qstate[qx.quota], q, qx, 1);
-                    quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, 1);
-                }
-                // Reservation.Reserve on the node's views (a group's node is its lane's alone), then DeviceShare's
-                const bool rsv_on = (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views;
-                if (rsv_on) rsv_reserve_dev(e, n, zones + rec, rec, q, nom);
-                dev_reserve_apply(cfg, e, n, rec, devs ? devs + rec : nullptr, mask, qx,
-                                  (rsv_on && nom >= 0) ? (int32_t)e.infos[nom].rid : -1, 1);
-            }
-            result[j] = KG_BATCH_ASSUMED;
-            status[j] = 0;
-            zone_out[j] = zone;
-            minors_out[j] = mask;
-        }
-    }
-}
-
-// The batch cycle with cpuset-binding pods (NodeNUMAResource Reserve -> resourceManager.Allocate: a take by the device
-// accumulator, a whole wave in LDS): one workgroup of one wave runs the groups in order, every lane evaluates each pod
-// (uniform work), the wave takes the CPUs, lane 0 applies the other Reserves. Same results as k_batch plus the cpusets
-// (a failed take fails the pod and its group's later pods: ErrNotEnoughCPUs, zone code ZONE_CPUSET_FAIL).
-template <bool EXACT>
-__global__ __launch_bounds__(64) void k_batch_coop(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
-                                                   DevRec* __restrict__ devs, ExtDev e, PodsDev pods,
-                                                   const uint32_t* __restrict__ grp_begin,
-                                                   const uint32_t* __restrict__ grp_pods,
-                                                   const uint32_t* __restrict__ grp_rec, uint32_t n_groups, KCfg cfg,
-                                                   kg_cpu_alloc* __restrict__ allocs, const kg_cpu_topo* __restrict__ topos,
-                                                   uint32_t* __restrict__ result, uint32_t* __restrict__ status,
-                                                   int32_t* __restrict__ zone_out, uint32_t* __restrict__ minors_out) {
-    __shared__ CpusetLds L;
-    const bool lead = threadIdx.x == 0;
-    for (uint32_t g = 0; g < n_groups; g++) {
-        const uint32_t rec = grp_rec[g];
-        int64_t* n = nodes[rec].v;
-        uint32_t failed = 0;
-        for (uint32_t t = grp_begin[g]; t < grp_begin[g + 1]; t++) {
-            const uint32_t j = grp_pods[t];
-            if (failed) {
-                if (lead) {
-                    result[j] = KG_BATCH_SIBLING;
-                    status[j] = failed;
-                    zone_out[j] = -1;
-                    minors_out[j] = 0;
-                }
-                continue;
-            }
-            const PodV q = load_pod(pods, j);
-            const PodX qx = load_podx(pods, j);
-            uint32_t qst = 0;
-            if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas)
-                qst = quota_gate(e.qlim[qx.quota], e.qstate[qx.quota], q, qx);
-            const PairX r = eval_pair_ext<EXACT>(cfg, e, n, zones + rec, devs ? devs + rec : nullptr, rec, q, qx, qst);
-            uint32_t st = r.status;
-            const int32_t zone = r.zone;
-            uint32_t mask = 0;
-            if (!st && !zone_reserve_fails(zone) && (cfg.plugins & KG_PLUGIN_DEV) && devs)
-                mask = dev_choose_site(cfg, e, n, zones + rec, devs + rec, pod_view(cfg, e, n, rec, qx), r.nom, qx, zone);
-            if (!st && zone_reserve_fails(zone)) st = zone_fail_status(zone);  // Reserve fails (engine.go:270-280)
-            __syncthreads();  // every lane has read the state the pod was evaluated on
-            if (!st && (cfg.plugins & KG_PLUGIN_NUMA) && cpuset_bound_dev(zones[rec], q.flags, q.req_cpu) &&
-                cpuset_reserve_wave(nodes, zones, allocs, topos, pods, j, rec, zone, L, nullptr) != 0)
-                st = zone_fail_status(ZONE_CPUSET_FAIL);
-            if (st) {
-                failed = st;
-                if (lead) {
-                    result[j] = KG_BATCH_FAILED;
-                    status[j] = st;
-                    zone_out[j] = -1;
-                    minors_out[j] = 0;
-                }
-                __syncthreads();
-                continue;
-            }
-            if (lead) {
-                apply_assume(cfg, n, zones + rec, q, zone, 1);
-                if ((cfg.plugins & KG_PLUGIN_QUOTA) && qx.quota >= 0 && (uint32_t)qx.quota < e.n_quotas) {
-                    quota_add(e.qstate[qx.quota], q, qx, 1);
-                    quota_add(e.qstate[e.n_quotas + qx.quota], q, qx, 1);
-                }
-                const bool rsv_on = (cfg.plugins & KG_PLUGIN_RSV) && n[N_RSV_CLASSES] != 0 && e.views;
-                if (rsv_on) rsv_reserve_dev(e, n, zones + rec, rec, q, r.nom);
-                dev_reserve_apply(cfg, e, n, rec, devs ? devs + rec : nullptr, mask, qx,
-                                  (rsv_on && r.nom >= 0) ? (int32_t)e.infos[r.nom].rid : -1, 1);
-                result[j] = KG_BATCH_ASSUMED;
-                status[j] = 0;
-                zone_out[j] = zone;
-                minors_out[j] = mask;
-            }
-            __syncthreads();  // lane 0's Reserve before the next pod's evaluation
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // launchers
-
-hipError_t launch_batch(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
-                        const uint32_t* grp_begin, const uint32_t* grp_pods, const uint32_t* grp_rec, uint32_t n_groups,
-                        bool ext, const KCfg& cfg, bool exact, uint32_t* result, uint32_t* status, int32_t* zone,
-                        uint32_t* minors, hipStream_t s, kg_cpu_alloc* allocs, const kg_cpu_topo* topos) {
-    if (n_groups == 0) return hipSuccess;
-    if (allocs && topos) {  // cpuset-binding pods: the cooperative cycle
-        if (exact)
-            k_batch_coop<true><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, grp_begin, grp_pods, grp_rec, n_groups, cfg,
-                                                allocs, topos, result, status, zone, minors);
-        else
-            k_batch_coop<false><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, grp_begin, grp_pods, grp_rec, n_groups, cfg,
-                                                 allocs, topos, result, status, zone, minors);
-        return hipGetLastError();
-    }
-    const bool serial = ext && (cfg.plugins & KG_PLUGIN_QUOTA);
-    const dim3 grid(serial ? 1u : (n_groups + 63) / 64), block(64);
-#define KG_BATCH(EX, XT)                                                                                              \
-    k_batch<EX, XT><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, grp_begin, grp_pods, grp_rec, n_groups, serial, \
-                                           cfg, result, status, zone, minors)
-    if (exact && ext) KG_BATCH(true, true);
-    else if (exact) KG_BATCH(true, false);
-    else if (ext) KG_BATCH(false, true);
-    else KG_BATCH(false, false);
-#undef KG_BATCH
-    return hipGetLastError();
-}
 
 hipError_t launch_ext_gate(const PodsDev& pods, uint32_t n_pods, const ExtDev& e, uint32_t plugins, uint32_t* qst,
                            uint32_t* pstat, hipStream_t s) {
@@ -1470,36 +993,6 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
         hipError_t err = hipStreamWaitEvent(s, lane->join, 0);
         if (err != hipSuccess) return drain_lane(lane, err);
     }
-    return hipGetLastError();
-}
-
-hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
-                                  uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
-                                  const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
-                                  uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, int32_t* nsel,
-                                  RsvStep* rs, uint64_t* rlist, uint32_t* done, hipStream_t s) {
-    if (n_nodes == 0 || !done) return hipErrorInvalidValue;  // a zero grid would be a malformed dispatch
-    dim3 grid((n_nodes + 63) / 64), block(64);
-    if (exact)
-        k_ext_replay<true><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                  step_off, winners, minors, buckets, zsel, reason, pos, nsel, rs, rlist, done);
-    else
-        k_ext_replay<false><<<grid, block, 0, s>>>(nodes, zones, devs, e, pods, n_pods, n_nodes, index_base, cfg, step_base,
-                                                   step_off, winners, minors, buckets, zsel, reason, pos, nsel, rs, rlist,
-                                                   done);
-    return hipGetLastError();
-}
-
-hipError_t launch_ext_assume(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
-                             uint32_t pod, uint32_t rec, int32_t zone, uint32_t minors, int64_t sign, const KCfg& cfg,
-                             bool exact, int32_t* out, hipStream_t s, int64_t* split, bool rsv, int32_t rid,
-                             kg_cpu_alloc* allocs, const kg_cpu_topo* topos, const uint64_t* cpus) {
-    if (exact)
-        k_ext_assume<true><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, pod, rec, zone, minors, sign, cfg, out, split, rsv,
-                                            rid, allocs, topos, cpus);
-    else
-        k_ext_assume<false><<<1, 64, 0, s>>>(nodes, zones, devs, e, pods, pod, rec, zone, minors, sign, cfg, out, split, rsv,
-                                             rid, allocs, topos, cpus);
     return hipGetLastError();
 }
 

@@ -146,11 +146,17 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
 // host path)
 hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_t n, uint32_t k, bool src_by_map,
                                const uint32_t* qst, uint64_t* out, uint32_t* pstat, hipStream_t s);
+// arrival counters of a replay step launch (the last workgroup picks): REPLAY_DONE_SHARDS shard counters and one top
+// counter, each on a 128-B line of its own; uint32 words, zeroed once, left zeroed by every launch
+constexpr uint32_t REPLAY_DONE_SHARDS = 32, REPLAY_DONE_STRIDE = 32;
+constexpr uint32_t REPLAY_WG = 256;  // threads (node records) per workgroup of a replay step launch
+constexpr uint32_t REPLAY_DONE_WORDS = (REPLAY_DONE_SHARDS + 1) * REPLAY_DONE_STRIDE;
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,
                                   const uint32_t* step_base, uint32_t step_off, uint64_t* winners, uint32_t* minors,
                                   uint64_t* buckets, int8_t* zsel, uint32_t* reason, const uint32_t* pos, int32_t* nsel,
-                                  RsvStep* rs, uint64_t* rlist, uint32_t* done, hipStream_t s);
+                                  RsvStep* rs, uint64_t* rlist, uint32_t* done, const DevClass* dclass, uint32_t n_dclass,
+                                  bool fb, uint32_t n0, hipStream_t s);
 // k_ext_assume: Reserve (sign 1, sign 0 = its evaluation pass) / Unreserve (sign -1) with every enabled plugin; rsv:
 // Reservation.Reserve / Unreserve on the node's views (rid: the reservation an Unreserve leaves); split: the NUMA
 // allocation's per-zone amounts; cpus: the cpuset CPUs an Unreserve releases

@@ -1752,33 +1752,63 @@ static uint32_t special_est(const kg_snap* s, const kg_pods* p) {
     return c1_split(s, p) ? std::max(s->n_big_est, s->max_cls_views) : s->special_est();
 }
 
+// room for the batch's DevSum table over this snapshot's records
+static kg_status devsum_reserve(kg_snap* s, kg_pods* p) {
+    kg_ctx* ctx = s->ctx;
+    if (p->devsum_cap >= s->n) return KG_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(p->d_devsum));
+    p->d_devsum = nullptr;
+    p->devsum_cap = 0;
+    HIP_TRY(ctx, hipMalloc(&p->d_devsum, sizeof(DevSum) * std::max<uint32_t>(s->n, 1)));
+    p->devsum_cap = s->n;
+    return KG_OK;
+}
+
+// room for the batch's e.gz table (gpu_zone_sum per SingleNUMANode record and GPU request class)
+static kg_status gz_reserve(kg_snap* s, kg_pods* p) {
+    kg_ctx* ctx = s->ctx;
+    const size_t need = (size_t)(s->n - s->n0) * DEV_CLASSES;
+    if (p->gz_cap >= need) return KG_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipFree(p->d_gz));
+    p->d_gz = nullptr;
+    p->gz_cap = 0;
+    HIP_TRY(ctx, hipMalloc(&p->d_gz, sizeof(uint64_t) * std::max<size_t>(need, 1)));
+    p->gz_cap = need;
+    return KG_OK;
+}
+
+// The replay reads DeviceShare off reservation views from the batch's DevSum table (built at its start, the winner's
+// entry refreshed by each step after a Reserve that changed its minors): every GPU request class fits the table.
+static bool replay_dsum(const kg_snap* s, const kg_pods* p) {
+    return s->d_dev && (s->kcfg.plugins & KG_PLUGIN_DEV) && p->n_dclass != 0 && s->n != 0;
+}
+
+// Fast-base replay (k_ext_replay<false, true>): the pairs on fast-base records run the fast-base select's arithmetic
+// (fast block, DevSum, e.gz on SingleNUMANode records); not with FitError reasons (the fast pairs carry no filter bits).
+static bool replay_fb(const kg_snap* s, const kg_pods* p, bool exact, bool reasons) {
+    if (exact || reasons || !ext_fast_base(s, p)) return false;
+    return !((s->kcfg.plugins & KG_PLUGIN_DEV) && p->n_dclass != 0) || replay_dsum(s, p);
+}
+static bool replay_gz(const kg_snap* s, const kg_pods* p, bool exact, bool reasons) {
+    return replay_fb(s, p, exact, reasons) && s->d_dev && gpu_zone_active(s, p);
+}
+
 // The batch's DevSum table over this snapshot's records (fast-base config-5 select with DeviceShare).
 static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     kg_ctx* ctx = s->ctx;
     e.dsum = nullptr;
     if (!s->d_dev || !ext_fast_base(s, p)) return KG_OK;
-    if (p->devsum_cap < s->n) {
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        HIP_TRY(ctx, hipFree(p->d_devsum));
-        p->d_devsum = nullptr;
-        p->devsum_cap = 0;
-        HIP_TRY(ctx, hipMalloc(&p->d_devsum, sizeof(DevSum) * std::max<uint32_t>(s->n, 1)));
-        p->devsum_cap = s->n;
-    }
+    const kg_status st = devsum_reserve(s, p);
+    if (st != KG_OK) return st;
     HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(),
                                 p->d_devsum, spec_cls_max(p), ctx->stream));
     e.dsum = p->d_devsum;
     e.gz = nullptr;
     if (gz_active(s, p)) {  // DeviceShare's NUMA hints of the SingleNUMANode records, per class
-        const size_t need = (size_t)(s->n - s->n0) * DEV_CLASSES;
-        if (p->gz_cap < need) {
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-            HIP_TRY(ctx, hipFree(p->d_gz));
-            p->d_gz = nullptr;
-            p->gz_cap = 0;
-            HIP_TRY(ctx, hipMalloc(&p->d_gz, sizeof(uint64_t) * need));
-            p->gz_cap = need;
-        }
+        const kg_status gst = gz_reserve(s, p);
+        if (gst != KG_OK) return gst;
         HIP_TRY(ctx, launch_gpu_zone_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg,
                                          s->ext_dev(), p->d_gz, ctx->stream));
         e.gz = p->d_gz;
@@ -2352,8 +2382,20 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
     std::vector<uint8_t> key = replay_key(s, p, exact, reasons);
     auto put = [&key](const void* x, size_t n) { key.insert(key.end(), (const uint8_t*)x, (const uint8_t*)x + n); };
     // every ExtDev field the captured launches take by value (tables re-uploaded in place keep their pointers)
-    const ExtDev e = s->ext_dev();
+    ExtDev e = s->ext_dev();
+    e.dsum = replay_dsum(s, p) ? p->d_devsum : nullptr;
+    const bool fb = replay_fb(s, p, exact, reasons);
+    e.gz = replay_gz(s, p, exact, reasons) ? p->d_gz : nullptr;
     put(&e.dev, sizeof(e.dev));
+    put(&e.dsum, sizeof(e.dsum));
+    put(&e.gz, sizeof(e.gz));
+    put(&fb, sizeof(fb));
+    put(&s->n0, sizeof(s->n0));
+    put(&p->d_dclass, sizeof(p->d_dclass));
+    put(&p->n_dclass, sizeof(p->n_dclass));
+    put(&e.graw, sizeof(e.graw));
+    put(&e.gnodes, sizeof(e.gnodes));
+    put(&e.grsv, sizeof(e.grsv));
     put(&e.qlim, sizeof(e.qlim));
     put(&e.qstate, sizeof(e.qstate));
     put(&e.n_quotas, sizeof(e.n_quotas));
@@ -2395,7 +2437,7 @@ kg_status ext_replay_graph(kg_snap* s, kg_pods* p, bool exact, bool reasons) {
                                          p->d_step, t, p->d_winners, p->d_minors, p->d_buckets, s->d_zsel,
                                          reasons ? p->d_reason : nullptr, s->d_pos,
                                          (s->cfg.plugins & KG_PLUGIN_RSV) ? s->d_nsel : nullptr, rs, s->d_rlist,
-                                         p->d_done, ctx->stream);
+                                         p->d_done, p->d_dclass, p->n_dclass, fb, s->n0, ctx->stream);
     }
     if (err == hipSuccess) err = launch_bump(p->d_step, REPLAY_G, ctx->stream);
     hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
@@ -2556,9 +2598,18 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
         HIP_TRY(ctx, hipMalloc(&s->d_rstep, sizeof(RsvStep) * 3));
         HIP_TRY(ctx, hipMalloc(&s->d_rlist, sizeof(uint64_t) * 2 * 3 * (size_t)std::max<uint32_t>(s->n, 1)));
     }
-    if (!p->d_done) HIP_TRY(ctx, hipMalloc(&p->d_done, sizeof(uint32_t)));
-    HIP_TRY(ctx, hipMemsetAsync(p->d_done, 0, sizeof(uint32_t), ctx->stream));
-    st = ext_replay_graph(s, p, exact, out_reason != nullptr);
+    if (!p->d_done) HIP_TRY(ctx, hipMalloc(&p->d_done, REPLAY_DONE_WORDS * sizeof(uint32_t)));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_done, 0, REPLAY_DONE_WORDS * sizeof(uint32_t), ctx->stream));
+    const bool reasons = out_reason != nullptr;
+    if (replay_dsum(s, p)) {
+        st = devsum_reserve(s, p);
+        if (st != KG_OK) return st;
+    }
+    if (replay_gz(s, p, exact, reasons)) {
+        st = gz_reserve(s, p);
+        if (st != KG_OK) return st;
+    }
+    st = ext_replay_graph(s, p, exact, reasons);
     if (st != KG_OK) return st;
     if (rsv_replay(s)) {
         RsvStep z[3];
@@ -2575,6 +2626,13 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
     if (st != KG_OK) return st;
+    // the tables of the replay's starting state (inside the timed region)
+    if (replay_dsum(s, p))
+        HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg,
+                                    s->ext_dev(), p->d_devsum, spec_cls_max(p), ctx->stream));
+    if (replay_gz(s, p, exact, reasons))
+        HIP_TRY(ctx, launch_gpu_zone_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg,
+                                         s->ext_dev(), p->d_gz, ctx->stream));
     for (uint32_t done = 0; done <= n; done += REPLAY_G) HIP_TRY(ctx, hipGraphLaunch(p->xexec, ctx->stream));
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     st = record_end(ctx, e0, e1);
