@@ -689,18 +689,12 @@ __device__ __forceinline__ void quota_add(QuotaState& S, const PodV& p, const Po
 
 // ---- Reservation ------------------------------------------------------------------------------------
 
-__device__ __forceinline__ const RsvView* find_view(const ExtDev& e, int32_t cls, uint32_t rec) {
-    uint32_t lo = e.cls_begin[cls], hi = e.cls_begin[cls + 1];
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const uint32_t r = e.views[mid].rec;
-        if (r == rec) return &e.views[mid];
-        if (r < rec)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return nullptr;
+__device__ __forceinline__ const RsvView* find_view(const ExtDev& e, int32_t cls, uint32_t rec,
+                                                   const int64_t* __restrict__ n) {
+    // one dependent load instead of a binary search over the class's views
+    const uint64_t mask = (uint64_t)n[N_RSV_CLASSES];
+    if (!((mask >> cls) & 1ull)) return nullptr;
+    return &e.views[e.vmap[e.vfirst[rec] + (uint32_t)__popcll(mask & ((1ull << cls) - 1ull))]];
 }
 
 struct RsvPod {
@@ -1228,7 +1222,7 @@ __device__ __forceinline__ PairX eval_pair_ext(const KCfg& c, const ExtDev& e, c
     const RsvView* v = nullptr;
     if ((c.plugins & KG_PLUGIN_RSV) && x.cls >= 0 && x.cls < RSV_MAX_CLASSES &&
         (((uint64_t)n[N_RSV_CLASSES] >> x.cls) & 1ull))
-        v = find_view(e, x.cls, rec);
+        v = find_view(e, x.cls, rec, n);
     PairOut b;
     if (v) {
         Over ov;
@@ -1338,7 +1332,7 @@ __device__ __forceinline__ void rsv_reserve_dev(const ExtDev& e, int64_t* n, Zon
     const uint64_t mask = (uint64_t)n[N_RSV_CLASSES];
     for (uint64_t l = mask; l; l &= l - 1ull) {
         const int32_t cls = (int32_t)(__ffsll((unsigned long long)l) - 1);
-        const RsvView* cv = find_view(e, cls, rec);
+        const RsvView* cv = find_view(e, cls, rec, n);
         if (!cv) continue;
         RsvView& v = views[cv - e.views];
         bool matched = false;
@@ -1383,7 +1377,7 @@ __device__ __forceinline__ void rsv_unreserve_dev(const ExtDev& e, int64_t* n, Z
     // the reservation as the node's views hold it (every copy agrees)
     const RsvInfo* r = nullptr;
     for (uint64_t l = cmask; l && rid != 0xFFFFFFFFu && !r; l &= l - 1ull) {
-        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec);
+        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec, n);
         if (!cv) continue;
         for (uint32_t t = cv->first; t < cv->first + cv->count; t++)
             if (infos[t].rid == rid) {
@@ -1418,7 +1412,7 @@ __device__ __forceinline__ void rsv_unreserve_dev(const ExtDev& e, int64_t* n, Z
         derive_node(*reinterpret_cast<NodeRec*>(n), *zr);
     }
     for (uint64_t l = cmask; l; l &= l - 1ull) {
-        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec);
+        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec, n);
         if (!cv) continue;
         RsvView& v = views[cv - e.views];
         bool matched = false;
@@ -1437,7 +1431,7 @@ __device__ __forceinline__ void rsv_unreserve_dev(const ExtDev& e, int64_t* n, Z
     if (!r) return;
     // every copy of the reservation (after the views: r points into infos)
     for (uint64_t l = cmask; l; l &= l - 1ull) {
-        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec);
+        const RsvView* cv = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec, n);
         if (!cv) continue;
         for (uint32_t t = cv->first; t < cv->first + cv->count; t++) {
             RsvInfo& x = infos[t];
@@ -1539,7 +1533,7 @@ __device__ inline void gpu_restore_rebuild(const ExtDev& e, const int64_t* __res
     }
     const uint64_t cmask = (uint64_t)n[N_RSV_CLASSES];
     for (uint64_t l = cmask; l; l &= l - 1ull) {
-        const RsvView* v = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec);
+        const RsvView* v = find_view(e, (int32_t)(__ffsll((unsigned long long)l) - 1), rec, n);
         if (!v || v->dev_base < 0) continue;
         // matched GPU reservations of the view (by rid), the others with pods are unmatched
         int64_t uu[DEV_R][DEV_MINORS], ma[DEV_R][DEV_MINORS], mal[DEV_R][DEV_MINORS];
@@ -1597,7 +1591,7 @@ __device__ __forceinline__ const RsvView* pod_view(const KCfg& c, const ExtDev& 
     if (!(c.plugins & KG_PLUGIN_RSV) || !e.views || x.cls < 0 || x.cls >= RSV_MAX_CLASSES ||
         !(((uint64_t)n[N_RSV_CLASSES] >> x.cls) & 1ull))
         return nullptr;
-    return find_view(e, x.cls, rec);
+    return find_view(e, x.cls, rec, n);
 }
 
 // DeviceShare's allocate at Reserve (plugin.go:573-637): from the nominated reservation's table when it holds GPUs

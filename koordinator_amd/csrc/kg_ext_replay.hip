@@ -22,8 +22,8 @@ __device__ __forceinline__ uint64_t ext_replay_pick(uint32_t step, uint32_t n_no
                                                     const uint64_t* __restrict__ buckets, const RsvStep* __restrict__ rs,
                                                     const uint64_t* __restrict__ rlist) {
     const uint32_t lane = threadIdx.x;
-    const uint64_t* B = buckets + (size_t)(step % 3) * 128;
-    const uint64_t b0 = ld_agent(B + lane), b1 = ld_agent(B + lane + 64);
+    const uint64_t* B = buckets + (size_t)(step % 3) * 128 * REPLAY_BUCKET_STRIDE;
+    const uint64_t b0 = ld_agent(B + lane * REPLAY_BUCKET_STRIDE), b1 = ld_agent(B + (lane + 64) * REPLAY_BUCKET_STRIDE);
     const int32_t M = wmax_i32(max(b0 ? (int32_t)lane : -1, b1 ? (int32_t)lane + 64 : -1));
     if (M < 0) return 0ull;  // no feasible node (a listed pair is also in its bucket)
     auto cand = [&](uint64_t b, int64_t sd) -> uint64_t {
@@ -141,13 +141,46 @@ __device__ __forceinline__ void replay_refresh(const KCfg& cfg, const ExtDev& e,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the entries, before the winner lane's evaluation reads them
 }
 
-// One replay step (see file header). buckets: [3][128] ring of per-DeviceShare-score best keys. winners[step - 1] holds
-// the key the previous launch picked for pod step - 1; every workgroup drops it when the pair's Reserve fails (zone code
-// of its pair, or a cpuset Reserve that failed in between, k_cpuset_reserve), applies the Reserve, gates and evaluates
-// pod `step`. The last workgroup to finish (done counter) then picks pod step's winner into winners[step] and settles
+// Reserve of pod q (step - 1) on its winner record i by the record's lane (the zone code of its pair: prev_zone, its
+// nominated reservation in nsel): NodeInfo, LoadAware, NUMA zone, GPU minors, Reservation and DeviceShare bookkeeping.
+// Returns whether the record's minors changed (its DevSum / e.gz entries are refreshed next).
+__device__ __forceinline__ bool replay_reserve(const KCfg& cfg, const ExtDev& e, NodeRec* __restrict__ nodes,
+                                            ZoneRec* __restrict__ zones, DevRec* __restrict__ devs, const PodsDev& pods,
+                                            uint32_t q_idx, uint32_t i, int32_t prev_zone, int32_t nom_in,
+                                            uint32_t* __restrict__ minors_out) {
+    const PodV q = load_pod(pods, q_idx);
+    const PodX qx = load_podx(pods, q_idx);
+    const bool refresh = e.dsum && (cfg.plugins & KG_PLUGIN_DEV) && (qx.dcount > 0 || (e.graw && e.graw[i] >= 0));
+    apply_assume(cfg, nodes[i].v, zones + i, q, prev_zone, 1);
+    const int32_t nom = (nom_in >= 0 && nodes[i].v[N_RSV_CLASSES] != 0) ? nom_in : -1;
+    uint32_t mask = 0;
+    if ((cfg.plugins & KG_PLUGIN_DEV) && qx.dcount > 0) {
+        mask = dev_choose_site(cfg, e, nodes[i].v, zones + i, devs + i, pod_view(cfg, e, nodes[i].v, i, qx), nom, qx,
+                               prev_zone);
+        *minors_out = mask;
+    }
+    // Reservation.Reserve into the nominated reservation, then DeviceShare's (the node's minors, or the restore inputs
+    // and tables of GPU-holding reservations)
+    if ((cfg.plugins & KG_PLUGIN_RSV) && nom_in != -2 && nodes[i].v[N_RSV_CLASSES] != 0)
+        rsv_reserve_dev(e, nodes[i].v, zones + i, i, q, nom);
+    dev_reserve_apply(cfg, e, nodes[i].v, i, devs + i, mask, qx, nom >= 0 ? (int32_t)e.infos[nom].rid : -1, 1);
+    return refresh;
+}
+
+template <bool EXACT>
+__device__ __forceinline__ PairX replay_general_pair(const KCfg& cfg, const ExtDev& e, const int64_t* __restrict__ n,
+                                                  const ZoneRec* __restrict__ zr, const DevRec* d, uint32_t rec,
+                                                  const PodV& p, const PodX& px, uint32_t dcls) {
+    return eval_pair_ext<EXACT>(cfg, e, n, zr, d, rec, p, px, 0u, dcls);
+}
+
+// One replay step (see file header). buckets: [3][128] ring of per-DeviceShare-score best keys (REPLAY_BUCKET_STRIDE). winners[step - 1] holds
+// the key the previous launch picked for pod step - 1; the winner record's lane applies its Reserve unless it fails
+// (zone code of its pair, or a cpuset Reserve that failed in between, k_cpuset_reserve), every lane evaluates pod `step`
+// on its record, then gates it on its quota. The last workgroup to finish (done counter) then picks pod step's winner into winners[step] and settles
 // winners[step - 1] (0 when its Reserve failed): no other launch per step.
 template <bool EXACT, bool FB>
-__global__ __launch_bounds__(REPLAY_WG) void k_ext_replay(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
+__global__ __launch_bounds__(REPLAY_WG, 2) void k_ext_replay(NodeRec* __restrict__ nodes, ZoneRec* __restrict__ zones,
                                                    DevRec* __restrict__ devs, ExtDev e, PodsDev pods, uint32_t n_pods,
                                                    uint32_t n_nodes, uint32_t index_base, KCfg cfg,
                                                    const uint32_t* __restrict__ step_base, uint32_t step_off,
@@ -163,25 +196,15 @@ __global__ __launch_bounds__(REPLAY_WG) void k_ext_replay(NodeRec* __restrict__ 
     const uint32_t i = blockIdx.x * REPLAY_WG + threadIdx.x;
     // the workgroup's per-score-bucket maxima (one global atomic per bucket and workgroup)
     __shared__ uint64_t lb[128];
-    if (threadIdx.x < 128u) lb[threadIdx.x] = 0ull;
+    for (uint32_t t = threadIdx.x; t < 128u; t += REPLAY_WG) lb[t] = 0ull;
     const bool live = i < n_nodes;
     const bool has_next = step < n_pods;
-    uint64_t prev = step > 0 ? __hip_atomic_load(&winners[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-    // the winner's Reserve fails (BestEffort NUMA allocation, or a cpuset Reserve that failed between the launches: zone
-    // code of its pair): the pod stays unscheduled. zsel is double-buffered by step parity: every block reads the
-    // previous step's codes while this step's are written
-    int32_t prev_zone = -1;
-    if (prev != 0ull) {
-        prev_zone = zsel[(size_t)((step - 1) & 1u) * n_nodes + pos[(0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull)) - index_base]];
-        if (zone_reserve_fails(prev_zone)) {
-            if (blockIdx.x == 0 && threadIdx.x == 0 && reason) atomicOr(reason + step - 1, zone_fail_status(prev_zone));
-            prev = 0ull;
-        }
-    }
+    const uint64_t prev = step > 0 ? __hip_atomic_load(&winners[step - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const uint32_t gprev = 0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull);
     if (blockIdx.x == 0 && threadIdx.x < 64u) {
-        uint64_t* Z = buckets + (size_t)((step + 1) % 3) * 128;  // last read by the pick of step - 2
-        Z[lane] = 0;
-        Z[lane + 64] = 0;
+        uint64_t* Z = buckets + (size_t)((step + 1) % 3) * 128 * REPLAY_BUCKET_STRIDE;  // last read by the pick of step - 2
+        Z[lane * REPLAY_BUCKET_STRIDE] = 0;
+        Z[(lane + 64) * REPLAY_BUCKET_STRIDE] = 0;
         if (rs && lane == 0) {  // slot of step + 1 (last read by the pick of step - 2)
             RsvStep& z = rs[(step + 1) % 3];
             z.win = 0;
@@ -190,75 +213,34 @@ __global__ __launch_bounds__(REPLAY_WG) void k_ext_replay(NodeRec* __restrict__ 
             z.rmax = 0;
         }
     }
-    // Reserve of pod step-1 on its winner
+    // Reserve of pod step-1 on its winner, by the winner record's lane. It fails (BestEffort NUMA allocation, or a
+    // cpuset Reserve that failed between the launches) on the zone code of its pair: the pod stays unscheduled. zsel is
+    // double-buffered by step parity: the previous step's codes are read while this step's are written.
     bool refresh = false;  // the winner's minors changed: its DevSum entry is refreshed below
-    if (live && prev != 0ull) {
-        const uint32_t g = 0xFFFFFFFFu - (uint32_t)(prev & 0xFFFFFFFFull);
-        if (g == index_base + node_index(nodes[i])) {
-            const PodV q = load_pod(pods, step - 1);
-            const PodX qx = load_podx(pods, step - 1);
-            refresh = e.dsum && (cfg.plugins & KG_PLUGIN_DEV) && (qx.dcount > 0 || (e.graw && e.graw[i] >= 0));
-            apply_assume(cfg, nodes[i].v, zones + i, q, prev_zone, 1);
-            // the nominated reservation of the winning pair (nsel, double-buffered like zsel)
-            const int32_t nom = ((cfg.plugins & KG_PLUGIN_RSV) && nsel && nodes[i].v[N_RSV_CLASSES] != 0)
-                                    ? nsel[(size_t)((step - 1) & 1u) * n_nodes + i] : -1;
-            uint32_t mask = 0;
-            if ((cfg.plugins & KG_PLUGIN_DEV) && qx.dcount > 0) {
-                mask = dev_choose_site(cfg, e, nodes[i].v, zones + i, devs + i, pod_view(cfg, e, nodes[i].v, i, qx), nom, qx,
-                                       prev_zone);
-                minors[step - 1] = mask;
-            }
-            // Reservation.Reserve into the nominated reservation, then DeviceShare's (the node's minors, or the
-            // restore inputs and tables of GPU-holding reservations)
-            if ((cfg.plugins & KG_PLUGIN_RSV) && nsel && nodes[i].v[N_RSV_CLASSES] != 0)
-                rsv_reserve_dev(e, nodes[i].v, zones + i, i, q, nom);
-            dev_reserve_apply(cfg, e, nodes[i].v, i, devs + i, mask, qx, nom >= 0 ? (int32_t)e.infos[nom].rid : -1, 1);
+    if (live && prev != 0ull && gprev == index_base + node_index(nodes[i])) {
+        const int32_t prev_zone = zsel[(size_t)((step - 1) & 1u) * n_nodes + i];
+        if (!zone_reserve_fails(prev_zone)) {
+            // the nominated reservation of the winning pair (nsel, double-buffered like zsel); -2: no Reservation.Reserve
+            const int32_t nom = ((cfg.plugins & KG_PLUGIN_RSV) && nsel) ? nsel[(size_t)((step - 1) & 1u) * n_nodes + i] : -2;
+            refresh = replay_reserve(cfg, e, nodes, zones, devs, pods, step - 1, i, prev_zone, nom, minors + step - 1);
         }
     }
     if (const uint64_t own = __ballot(refresh))  // uniform per wave: the winner's workgroup
         replay_refresh(cfg, e, nodes, zones, devs, (i - lane) + (uint32_t)(__ffsll((unsigned long long)own) - 1), n0,
                        dclass, n_dclass);
-    // ElasticQuota: buffer (step-1)&1 holds the state after pods < step-1; buffer step&1 becomes the
-    // state after pods < step (block 0, nobody reads it during this launch). winners[step - 2] was settled by the last
-    // workgroup of the previous launch.
-    uint32_t qst = 0;
-    PodV p = load_pod(pods, has_next ? step : 0);
-    PodX px = load_podx(pods, has_next ? step : 0);
-    if (cfg.plugins & KG_PLUGIN_QUOTA) {
-        const uint32_t nq = e.n_quotas;
-        const QuotaState* rd = e.qstate + (size_t)((step - 1) & 1u) * nq;
-        PodX x1;
-        PodV p1;
-        bool placed1 = false;
-        if (step > 0) {
-            p1 = load_pod(pods, step - 1);
-            x1 = load_podx(pods, step - 1);
-            placed1 = prev != 0ull;
-        }
-        if (has_next && px.quota >= 0 && (uint32_t)px.quota < nq) {
-            QuotaState S = rd[px.quota];
-            if (placed1 && x1.quota == px.quota) quota_add(S, p1, x1, 1);
-            qst = quota_gate(e.qlim[px.quota], S, p, px);
-        }
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            QuotaState* wr = e.qstate + (size_t)(step & 1u) * nq;
-            if (step > 1 && winners[step - 2] != 0ull) {
-                const PodV p2 = load_pod(pods, step - 2);
-                const PodX x2 = load_podx(pods, step - 2);
-                if (x2.quota >= 0 && (uint32_t)x2.quota < nq) quota_add(wr[x2.quota], p2, x2, 1);
-            }
-            if (placed1 && x1.quota >= 0 && (uint32_t)x1.quota < nq) quota_add(wr[x1.quota], p1, x1, 1);
-        }
-    }
+    // pod `step` on every record, before its ElasticQuota gate (a uniform verdict applied below: the pair loads do not
+    // wait for the previous Reserve's outcome)
+    const PodV p = load_pod(pods, has_next ? step : 0);
+    const PodX px = load_podx(pods, has_next ? step : 0);
+    uint64_t kb = 0;
+    int32_t s = 0;
+    uint32_t stat = 0;
     if (has_next) {  // the final step only applies the last Reserve
-        uint64_t kb = 0;
-        int32_t s = 0;
-        uint32_t stat = 0;
         bool fast = false;
         if constexpr (FB) {  // the fast-base pairs (uniform per step: the pod's fast-path operands)
             const PodF pff = to_podf(p, cfg);
             const KCfg cv = cfg_in_vgprs(cfg);
-            const bool off = qst != 0u || ((cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED));
+            const bool off = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
             const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[step] : (uint32_t)DEV_CLASSES;
             int32_t zone = -1;
             if (live) fast = replay_fast_pair(cfg, cv, e, nodes[i].v, zones + i, i, n0, pff, px, dcls, off,
@@ -270,7 +252,7 @@ __global__ __launch_bounds__(REPLAY_WG) void k_ext_replay(NodeRec* __restrict__ 
         }
         if (live && !fast) {
             const uint32_t dcls = (e.dsum && pods.dev_cls) ? (uint32_t)pods.dev_cls[step] : (uint32_t)DEV_CLASSES;
-            const PairX r = eval_pair_ext<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, qst, dcls);
+            const PairX r = replay_general_pair<EXACT>(cfg, e, nodes[i].v, zones + i, devs ? devs + i : nullptr, i, p, px, dcls);
             zsel[(size_t)(step & 1u) * n_nodes + i] = (int8_t)r.zone;
             if (nsel) nsel[(size_t)(step & 1u) * n_nodes + i] = r.nom;
             stat = r.status;
@@ -292,6 +274,47 @@ __global__ __launch_bounds__(REPLAY_WG) void k_ext_replay(NodeRec* __restrict__ 
                 }
             }
         }
+    }
+    // the previous Reserve's outcome, from the zone code of the winner's pair (the same word in every lane)
+    bool placed1 = false;
+    if (prev != 0ull) {
+        const int32_t pz = zsel[(size_t)((step - 1) & 1u) * n_nodes + pos[gprev - index_base]];
+        placed1 = !zone_reserve_fails(pz);
+        if (!placed1 && blockIdx.x == 0 && threadIdx.x == 0 && reason) atomicOr(reason + step - 1, zone_fail_status(pz));
+    }
+    // ElasticQuota: buffer (step-1)&1 holds the state after pods < step-1; buffer step&1 becomes the
+    // state after pods < step (block 0, nobody reads it during this launch). winners[step - 2] was settled by the last
+    // workgroup of the previous launch.
+    uint32_t qst = 0;
+    if (cfg.plugins & KG_PLUGIN_QUOTA) {
+        const uint32_t nq = e.n_quotas;
+        const QuotaState* rd = e.qstate + (size_t)((step - 1) & 1u) * nq;
+        PodX x1;
+        PodV p1;
+        if (step > 0) {
+            p1 = load_pod(pods, step - 1);
+            x1 = load_podx(pods, step - 1);
+        }
+        if (has_next && px.quota >= 0 && (uint32_t)px.quota < nq) {
+            QuotaState S = rd[px.quota];
+            if (placed1 && x1.quota == px.quota) quota_add(S, p1, x1, 1);
+            qst = quota_gate(e.qlim[px.quota], S, p, px);
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            QuotaState* wr = e.qstate + (size_t)(step & 1u) * nq;
+            if (step > 1 && winners[step - 2] != 0ull) {
+                const PodV p2 = load_pod(pods, step - 2);
+                const PodX x2 = load_podx(pods, step - 2);
+                if (x2.quota >= 0 && (uint32_t)x2.quota < nq) quota_add(wr[x2.quota], p2, x2, 1);
+            }
+            if (placed1 && x1.quota >= 0 && (uint32_t)x1.quota < nq) quota_add(wr[x1.quota], p1, x1, 1);
+        }
+    }
+    if (has_next) {
+        if (qst) {  // PreFilter rejected the pod: no node is evaluated (eval_pair_ext's status)
+            kb = 0ull;
+            stat = live ? qst : 0u;
+        }
         if (reason) {  // FitError diagnosis: OR of the filter status bits over the nodes
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) stat |= (uint32_t)__shfl_xor((int)stat, off, 64);
@@ -302,8 +325,10 @@ __global__ __launch_bounds__(REPLAY_WG) void k_ext_replay(NodeRec* __restrict__ 
         __syncthreads();  // lb zeroed
         if (kb != 0ull) atomicMax((unsigned long long*)(lb + s), (unsigned long long)kb);
         __syncthreads();
-        if (threadIdx.x < 128u && lb[threadIdx.x] != 0ull)
-            atomicMax((unsigned long long*)(buckets + (size_t)(step % 3) * 128 + threadIdx.x), (unsigned long long)lb[threadIdx.x]);
+        for (uint32_t t = threadIdx.x; t < 128u; t += REPLAY_WG)
+            if (lb[t] != 0ull)
+                atomicMax((unsigned long long*)(buckets + ((size_t)(step % 3) * 128 + t) * REPLAY_BUCKET_STRIDE),
+                          (unsigned long long)lb[t]);
     }
     // the last workgroup of the launch: pick pod step's winner, settle pod step-1's. The hand-off to it without an
     // agent-scope fence (which writes back the XCD's L2 and invalidates the CU's L1 in every one of the ~400
@@ -317,10 +342,10 @@ __global__ __launch_bounds__(REPLAY_WG) void k_ext_replay(NodeRec* __restrict__ 
     __syncthreads();
     if (!last || threadIdx.x >= 64u) return;  // uniform per workgroup / per wave: the first wave picks
     if (has_next) {
-        const uint64_t w = ext_replay_pick(step, n_nodes, cfg, buckets, rs, rlist);
+        const uint64_t w = qst ? 0ull : ext_replay_pick(step, n_nodes, cfg, buckets, rs, rlist);
         if (lane == 0) winners[step] = w;
     }
-    if (lane == 0 && step > 0 && prev == 0ull) winners[step - 1] = 0ull;  // the Reserve failed: unscheduled
+    if (lane == 0 && step > 0 && prev != 0ull && !placed1) winners[step - 1] = 0ull;  // the Reserve failed: unscheduled
 }
 
 // Reserve (sign +1: zone and minors chosen here, or preset in out by an evaluation pass) / Unreserve (sign -1: the

@@ -150,6 +150,10 @@ hipError_t launch_scatter_keys(const uint64_t* src, const uint32_t* map, uint32_
 // counter, each on a 128-B line of its own; uint32 words, zeroed once, left zeroed by every launch
 constexpr uint32_t REPLAY_DONE_SHARDS = 32, REPLAY_DONE_STRIDE = 32;
 constexpr uint32_t REPLAY_WG = 256;  // threads (node records) per workgroup of a replay step launch
+// score buckets of a replay step: [3 steps][128 scores], one bucket per 128-B line (every workgroup's atomicMax on a
+// bucket would otherwise queue behind the other buckets of its line)
+constexpr uint32_t REPLAY_BUCKET_STRIDE = 16;
+constexpr size_t REPLAY_BUCKET_WORDS = (size_t)3 * 128 * REPLAY_BUCKET_STRIDE;
 constexpr uint32_t REPLAY_DONE_WORDS = (REPLAY_DONE_SHARDS + 1) * REPLAY_DONE_STRIDE;
 hipError_t launch_ext_replay_step(NodeRec* nodes, ZoneRec* zones, DevRec* devs, const ExtDev& e, const PodsDev& pods,
                                   uint32_t n_pods, uint32_t n_nodes, uint32_t index_base, const KCfg& cfg, bool exact,

@@ -505,6 +505,10 @@ struct ExtDev {
     const RsvView* views;          // sorted by class, then record position
     const RsvInfo* infos;
     const uint32_t* cls_begin;     // [RSV_MAX_CLASSES + 1] view range per class
+    // direct view lookup: the record's views in class order are vmap[vfirst[rec] + k] (k = the rank of the class among
+    // the record's N_RSV_CLASSES bits), each an index into views
+    const uint32_t* vfirst;        // [record]
+    const uint32_t* vmap;          // [view]
     const DevRec* rdev;            // GPU restore tables of views / reservations (kg_rsv_dev)
     const DevSum* dsum;            // [record] of the current pod batch (fast-base select / stats only)
     // Fast-base select of the GPU pods in one pass (k_ext_select<FB>): the DeviceShare maximum over the fast-base

@@ -79,6 +79,8 @@ struct kg_snap {
     QuotaState* d_qstate = nullptr;  // [2][n_quotas]
     uint32_t n_quotas = 0;
     RsvView* d_views = nullptr;
+    uint32_t* d_vfirst = nullptr;  // ExtDev::vfirst / vmap
+    uint32_t* d_vmap = nullptr;
     RsvInfo* d_infos = nullptr;
     uint32_t* d_cls_begin = nullptr;  // [RSV_MAX_CLASSES + 1]
     DevRec* d_rdev = nullptr;         // kg_rsv_dev tables
@@ -174,6 +176,8 @@ struct kg_snap {
         e.views = d_views;
         e.infos = d_infos;
         e.cls_begin = d_cls_begin;
+        e.vfirst = d_vfirst;
+        e.vmap = d_vmap;
         e.rdev = d_rdev;
         e.graw = gpu_raw ? d_graw : nullptr;
         e.gnodes = d_gnodes;
@@ -242,7 +246,7 @@ struct kg_pods {
     uint32_t* d_rsv_max = nullptr;
     uint64_t* d_pref = nullptr;
     uint32_t* d_minors = nullptr;     // replay: GPU minors chosen per pod
-    uint64_t* d_buckets = nullptr;    // replay: [3][128] per-score best keys
+    uint64_t* d_buckets = nullptr;    // replay: [3][128] per-score best keys (REPLAY_BUCKET_STRIDE apart)
     uint32_t* d_done = nullptr;       // config-5 replay: workgroups done in the current step launch (last one picks)
     int32_t* d_aout = nullptr;        // kg_assume_ext outputs
     uint64_t* d_rec = nullptr;        // kg_reserve / kg_unreserve: cpuset CPUs [4] + NUMA zone amounts [8]
@@ -1247,6 +1251,8 @@ kg_status kg_snapshot_destroy(kg_snap* s) {
     hipFree(s->d_qlim);
     hipFree(s->d_qstate);
     hipFree(s->d_views);
+    hipFree(s->d_vfirst);
+    hipFree(s->d_vmap);
     hipFree(s->d_infos);
     hipFree(s->d_cls_begin);
     hipFree(s->d_rdev);
@@ -1369,7 +1375,7 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_rsv_max, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_pref, sizeof(uint64_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_minors, sizeof(uint32_t) * (capacity + 1)) == hipSuccess &&
-              hipMalloc(&p->d_buckets, sizeof(uint64_t) * 3 * 128) == hipSuccess &&
+              hipMalloc(&p->d_buckets, sizeof(uint64_t) * REPLAY_BUCKET_WORDS) == hipSuccess &&
               hipMalloc(&p->d_aout, sizeof(int32_t) * 4) == hipSuccess &&
               hipMalloc(&p->d_tkeys, sizeof(uint64_t) * KG_TOPK_MAX * capacity) == hipSuccess &&
               hipMalloc(&p->d_spec, sizeof(uint32_t) * (2 * (size_t)capacity + DEV_CLASSES + 1)) == hipSuccess &&
@@ -1794,7 +1800,6 @@ static bool replay_fb(const kg_snap* s, const kg_pods* p, bool exact, bool reaso
 static bool replay_gz(const kg_snap* s, const kg_pods* p, bool exact, bool reasons) {
     return replay_fb(s, p, exact, reasons) && s->d_dev && gpu_zone_active(s, p);
 }
-
 // The batch's DevSum table over this snapshot's records (fast-base config-5 select with DeviceShare).
 static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     kg_ctx* ctx = s->ctx;
@@ -2621,7 +2626,7 @@ static kg_status ext_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* 
     HIP_TRY(ctx, hipMemsetAsync(p->d_winners, 0, sizeof(uint64_t) * (n + 1), ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_minors, 0, sizeof(uint32_t) * (n + 1), ctx->stream));
     s->gen++;
-    HIP_TRY(ctx, hipMemsetAsync(p->d_buckets, 0, sizeof(uint64_t) * 3 * 128, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(p->d_buckets, 0, sizeof(uint64_t) * REPLAY_BUCKET_WORDS, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_step, 0, sizeof(uint32_t), ctx->stream));
     hipEvent_t e0, e1;
     st = record_begin(ctx, &e0, &e1);
@@ -3274,8 +3279,11 @@ static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv,
     }
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    for (void* b : {(void*)s->d_views, (void*)s->d_infos, (void*)s->d_cls_begin, (void*)s->d_rdev, (void*)s->d_rdev_rec})
+    for (void* b : {(void*)s->d_views, (void*)s->d_infos, (void*)s->d_cls_begin, (void*)s->d_rdev, (void*)s->d_rdev_rec,
+                    (void*)s->d_vfirst, (void*)s->d_vmap})
         hipFree(b);
+    s->d_vfirst = nullptr;
+    s->d_vmap = nullptr;
     s->d_views = nullptr;
     s->d_infos = nullptr;
     s->d_cls_begin = nullptr;
@@ -3293,6 +3301,25 @@ static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv,
     HIP_TRY(ctx, hipMemcpyAsync(s->d_views, dv.data(), sizeof(RsvView) * dv.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_infos, di.data(), sizeof(RsvInfo) * di.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s->d_cls_begin, cb.data(), sizeof(uint32_t) * cb.size(), hipMemcpyHostToDevice, ctx->stream));
+    // direct view lookup (find_view): per record the start of its views in vmap, in class order
+    std::vector<uint32_t> vfirst(std::max<uint32_t>(s->n, 1), 0u), vmap(std::max<uint32_t>(nv, 1), 0u);
+    {
+        std::vector<uint64_t> rmask(s->n, 0);
+        for (uint32_t i = 0; i < s->n; i++) rmask[s->pos[i]] = mask[i];
+        uint32_t at = 0;
+        for (uint32_t r = 0; r < s->n; r++) {
+            vfirst[r] = at;
+            at += (uint32_t)__builtin_popcountll(rmask[r]);
+        }
+        for (uint32_t t = 0; t < nv; t++) {
+            const uint32_t r = dv[t].rec;
+            vmap[vfirst[r] + (uint32_t)__builtin_popcountll(rmask[r] & ((1ull << dv[t].cls) - 1ull))] = t;
+        }
+    }
+    HIP_TRY(ctx, hipMalloc(&s->d_vfirst, sizeof(uint32_t) * vfirst.size()));
+    HIP_TRY(ctx, hipMalloc(&s->d_vmap, sizeof(uint32_t) * vmap.size()));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_vfirst, vfirst.data(), sizeof(uint32_t) * vfirst.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s->d_vmap, vmap.data(), sizeof(uint32_t) * vmap.size(), hipMemcpyHostToDevice, ctx->stream));
     // class masks into slot N_RSV_CLASSES of every record (a strided 8-byte column copy)
     s->cls_mask = mask;
     s->n_view_nodes = 0;
