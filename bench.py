@@ -48,7 +48,7 @@ PLUGINS = {1: "+LoadAware", 2: "+LoadAware+NodeNUMAResource", 4: "+LoadAware+Nod
            6: "+LoadAware+NodeNUMAResource; mixed: 20% SingleNUMANode, 10% Restricted, 10% BestEffort, 5% CPU-bind-"
               "policy nodes, 5% LSR cpuset pods",
            5: "+LoadAware+NodeNUMAResource+DeviceShare+Reservation+ElasticQuota"}
-KERNEL_SOURCES = ("kg_eval.h", "kg_ext.h", "kg_kernels.h", "kg_layout.h", "kg_kernels.hip", "kg_ext.hip")
+KERNEL_SOURCES = ("kg_eval.h", "kg_ext.h", "kg_ext_wave.h", "kg_kernels.h", "kg_layout.h", "kg_kernels.hip", "kg_ext.hip")
 
 
 def parse():
