@@ -8,7 +8,7 @@ minors 4-7 on NUMA node 1 (PCIe 2: {4, 5}, PCIe 3: {6, 7}); every GPU 100 gpu-co
 Only the GPU device type is modelled: the RDMA / FPGA halves of the reference cases are dropped. In
 "generate gpu&rdma hints" (:69-86) the GPU list does not depend on the RDMA request (no joint allocation, every mask
 also fits the RDMA VFs), so its GPU list is the GPU-only answer. Cases of other device types only (fpga, rdma VF
-hints, joint allocation) and Test_generateDesignatedHints (:421, designated allocations are not on the device path)
+hints) and Test_generateDesignatedHints (:421, designated allocations are not on the device path)
 are not transcribed.
 
 Hints: (NUMA node ids of the affinity, Preferred, Score); defaultNUMAScore = 500 (topology_hint.go:36)."""
@@ -26,12 +26,20 @@ CASES = [
     # gpuRequests (core 100, ratio 100) assigned on minor 0 (:103-112, the pod requests 4 GPUs)
     dict(name="generate gpu hints with assigned devices", line=97, gpu_core=400, gpu_ratio=400,
          assigned=[[0, 100, 100]], result="hints", want=[[[1], True, 500], [[0, 1], False, 500]]),
+    # the joint GPU & RDMA allocation (:186-211): on fakeDeviceCR every GPU mask also holds RDMA VFs under the same
+    # PCIe switches, so the GPU list the test asserts is the GPU-only answer of :69 (the RDMA half is not modelled)
+    dict(name="generate joint-allocate gpu&rdma hints (GPU list)", line=186, gpu_core=100, gpu_ratio=100, assigned=[],
+         result="hints", want=[[[0], True, 500], [[1], True, 0], [[0, 1], False, 500]]),
 ]
 
 # TestPlugin_Allocate (topology_hint_test.go:272-419): gpuRequests there = gpu-core 100 + gpu-memory 8Gi
 ALLOCATE = [
     dict(name="allocate gpu&rdma by affinity (GPU part)", line=295, gpu_core=100, gpu_mem=8 << 30, affinity=[0],
          error=False),
+    # :362 "generate joint-allocate gpu&rdma hints" (Allocate under NUMA node 0): its GPU part; the other cases of
+    # TestPlugin_Allocate (:305-361) request FPGA / RDMA only
+    dict(name="allocate joint gpu&rdma under NUMA node 0 (GPU part)", line=362, gpu_core=100, gpu_mem=8 << 30,
+         affinity=[0], error=False),
 ]
 
 DEVICE = {"numa": [0, 0, 0, 0, 1, 1, 1, 1], "pcie": ["0", "0", "1", "1", "2", "2", "3", "3"],
