@@ -270,6 +270,24 @@ def test_config5_full_size_sampled(ctx):
     assert (keys != 0).mean() > 0.5
 
 
+def test_config5_full_size_verify_sampled(ctx):
+    """Per-plugin parity at full size on the round-4 config-5 workload (synth.config5(): 100k nodes with 20 %
+    SingleNUMANode, U(0, 1) GPU minor usage, reservations that hold GPUs): status bits, raw scores, totals and NUMA
+    zones of a pod sample (GPU pods with and without a reservation class, class pods, plain pods) on every node."""
+    cfg, nodes, pods, quotas, rsv = synth.config5()
+    kc = cfg.kg_config()
+    rng = np.random.default_rng(9)
+    gpu, cls = pods["dev_count"] > 0, pods["rsv_class"] >= 0
+    groups = [np.flatnonzero(gpu & cls), np.flatnonzero(gpu & ~cls), np.flatnonzero(~gpu & cls), np.flatnonzero(~gpu & ~cls)]
+    idx = np.concatenate([rng.choice(g, 4, replace=False) for g in groups])
+    sample = abi.take(pods, idx)
+    snap, batch = make(ctx, kc, nodes, sample, quotas, rsv)
+    got = engine.eval_verify(snap, batch)
+    ref = oracle_lib.ext_verify(kc, nodes, sample, quotas, rsv)
+    assert_equal(got, ref, "config5 full size")
+    assert (ref.status == 0).any() and (ref.score_dev > 0).any() and (ref.score_rsv > 0).any()
+
+
 @pytest.mark.parametrize("k", [1, 3])
 def test_ext_shard_select_single_rank(ctx, k):
     """kg_shard_select's config-5 path (stats pass, RCCL all-reduce of the NormalizeScore inputs,
