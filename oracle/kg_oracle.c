@@ -2792,12 +2792,12 @@ typedef struct ext_row {
     int32_t* zone;
 } ext_row;
 
-static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t nn, const kg_pod_columns* p,
-                         uint32_t j, const kgo_ext* e, const view_index* vx, const kgo_quota_state* q, ext_row* o) {
-    uint32_t qst = (c->plugins & KG_PLUGIN_QUOTA) ? quota_gate(q, p, j) : 0;
+/* Filter + raw Score of pod j on nodes [lo, hi) (qst: the pod's ElasticQuota PreFilter verdict). */
+static void ext_eval_nodes(const kg_config* c, const kg_node_columns* n, uint32_t lo, uint32_t hi, const kg_pod_columns* p,
+                           uint32_t j, const kgo_ext* e, const view_index* vx, uint32_t qst, ext_row* o) {
     const int32_t cls = (c->plugins & KG_PLUGIN_RSV) && p->rsv_class ? p->rsv_class[j] : -1;
     const int gpu_pod = (c->plugins & KG_PLUGIN_DEV) && p->dev_count && p->dev_count[j] > 0;
-    for (uint32_t i = 0; i < nn; i++) {
+    for (uint32_t i = lo; i < hi; i++) {
         o->nrf[i] = o->la[i] = o->numa[i] = o->dev[i] = o->rsv[i] = o->order[i] = 0;
         o->nom[i] = -1;
         o->zone[i] = -1;
@@ -2863,6 +2863,49 @@ static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t 
              * NUMA affinity */
             o->dev[i] = gpu_score_site(c, n, i, p, j, e, v, gx.done ? gx.mask : 0u, nom);
     }
+}
+
+static void ext_eval_pod(const kg_config* c, const kg_node_columns* n, uint32_t nn, const kg_pod_columns* p,
+                         uint32_t j, const kgo_ext* e, const view_index* vx, const kgo_quota_state* q, ext_row* o) {
+    ext_eval_nodes(c, n, 0, nn, p, j, e, vx, (c->plugins & KG_PLUGIN_QUOTA) ? quota_gate(q, p, j) : 0, o);
+}
+
+/* Worker pool of the parallel config-5 replay: one job per cycle, chunks of nodes taken by an atomic counter (the
+ * reference's parallelizer.Until over the nodes, parallelism.go:29-49); the calling thread is worker 0. */
+typedef struct ext_par {
+    pthread_t* th;
+    int n, workers, quit;
+    pthread_barrier_t start, done;
+    const kg_config* c;
+    const kg_node_columns* nodes;
+    uint32_t nn, pod, qst;
+    const kg_pod_columns* p;
+    const kgo_ext* e;
+    const view_index* vx;
+    ext_row* o;
+    int chunk;
+    volatile int next;
+} ext_par;
+
+static void ext_par_run(ext_par* x) {
+    for (;;) {
+        const int c0 = __atomic_fetch_add(&x->next, 1, __ATOMIC_RELAXED);
+        const uint32_t lo = (uint32_t)c0 * (uint32_t)x->chunk;
+        if (lo >= x->nn) break;
+        const uint32_t hi = lo + (uint32_t)x->chunk < x->nn ? lo + (uint32_t)x->chunk : x->nn;
+        ext_eval_nodes(x->c, x->nodes, lo, hi, x->p, x->pod, x->e, x->vx, x->qst, x->o);
+    }
+}
+
+static void* ext_par_worker(void* arg) {
+    ext_par* x = (ext_par*)arg;
+    for (;;) {
+        pthread_barrier_wait(&x->start);
+        if (x->quit) break;
+        ext_par_run(x);
+        pthread_barrier_wait(&x->done);
+    }
+    return NULL;
 }
 
 /* PreScore preferredNode (reservation/scoring.go:113-121: smallest non-zero order among the feasible
@@ -3298,9 +3341,29 @@ static int rsv_has_gpu_tables(const kgo_ext* e) {
     return 0;
 }
 
+static int ext_replay_impl(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
+                           const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
+                           int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason, int workers);
+
 int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
                    const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
                    int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason) {
+    return ext_replay_impl(c, st, base, p, np, e, out_node, out_total, out_minors, quota_used_out, quota_np_used_out,
+                           out_reason, 1);
+}
+
+/* kgo_ext_replay with each cycle's Filter / Score over the nodes on `workers` threads (the Reserve between cycles
+ * stays serial): the CPU baseline of the config-5 replay, same results. */
+int kgo_ext_replay_parallel(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
+                            const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
+                            int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason, int workers) {
+    return ext_replay_impl(c, st, base, p, np, e, out_node, out_total, out_minors, quota_used_out, quota_np_used_out,
+                           out_reason, workers);
+}
+
+static int ext_replay_impl(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
+                           const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
+                           int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason, int workers) {
     const int rsv = (c->plugins & KG_PLUGIN_RSV) != 0;
     if (rsv && rsv_has_gpu_tables(e) && !e->n_gpu) return -1;
     kg_node_columns v;
@@ -3333,8 +3396,35 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
         ee = &e2;
         view_index_build(&vx, ee, st->n);
     }
+    ext_par par;
+    memset(&par, 0, sizeof(par));
+    if (workers > 1) {
+        par.workers = workers;
+        par.n = workers - 1;
+        par.th = (pthread_t*)calloc((size_t)par.n, sizeof(pthread_t));
+        pthread_barrier_init(&par.start, NULL, (unsigned)workers);
+        pthread_barrier_init(&par.done, NULL, (unsigned)workers);
+        for (int t = 0; t < par.n; t++) pthread_create(&par.th[t], NULL, ext_par_worker, &par);
+    }
     for (uint32_t j = 0; j < np; j++) {
-        ext_eval_pod(c, &v, st->n, p, j, ee, rsv ? &vx : NULL, q, &b.r);
+        if (workers > 1) {
+            par.c = c;
+            par.nodes = &v;
+            par.nn = st->n;
+            par.pod = j;
+            par.qst = (c->plugins & KG_PLUGIN_QUOTA) ? quota_gate(q, p, j) : 0;
+            par.p = p;
+            par.e = ee;
+            par.vx = rsv ? &vx : NULL;
+            par.o = &b.r;
+            par.chunk = chunk_size((int)st->n, workers);
+            par.next = 0;
+            pthread_barrier_wait(&par.start);
+            ext_par_run(&par);
+            pthread_barrier_wait(&par.done);
+        } else {
+            ext_eval_pod(c, &v, st->n, p, j, ee, rsv ? &vx : NULL, q, &b.r);
+        }
         ext_pod_finish(c, &b.r, st->n, base);
         uint64_t best = 0;
         int32_t best_zone = -1;
@@ -3386,6 +3476,14 @@ int kgo_ext_replay(const kg_config* c, kgo_state* st, uint32_t base, const kg_po
         quota_apply(q, p, j, 1);
         if (rsv && mv) rsv_reserve(st, mv, ee->n_views, mi, i, p, j, nom);
         if (raw) gpu_apply_o(st, ee, md, &gx, i, mask, p, j, nom >= 0 ? (int32_t)mi[nom].rid : -1);
+    }
+    if (workers > 1) {
+        par.quit = 1;
+        pthread_barrier_wait(&par.start);
+        for (int t = 0; t < par.n; t++) pthread_join(par.th[t], NULL);
+        pthread_barrier_destroy(&par.start);
+        pthread_barrier_destroy(&par.done);
+        free(par.th);
     }
     free(vx.v);
     free(mv);

@@ -99,6 +99,10 @@ int kgo_ext_select(const kg_config* cfg, const kg_node_columns* nodes, uint32_t 
 int kgo_ext_replay(const kg_config* cfg, kgo_state* st, uint32_t index_base, const kg_pod_columns* pods,
                    uint32_t n_pods, const kgo_ext* ext, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
                    int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason);
+/* kgo_ext_replay with each cycle's nodes evaluated on `workers` threads (the CPU baseline of the config-5 replay). */
+int kgo_ext_replay_parallel(const kg_config* c, kgo_state* st, uint32_t base, const kg_pod_columns* p, uint32_t np,
+                            const kgo_ext* e, int32_t* out_node, int64_t* out_total, uint32_t* out_minors,
+                            int64_t* quota_used_out, int64_t* quota_np_used_out, uint32_t* out_reason, int workers);
 int64_t kgo_mem_bytes_to_ratio(int64_t bytes, int64_t total);
 int64_t kgo_ext_pair_nominated(const kg_config* c, const kg_node_columns* n, uint32_t nn, uint32_t i,
                                const kg_pod_columns* p, uint32_t j, const kgo_ext* e);

@@ -90,6 +90,8 @@ def lib():
                                      P(KgoExt), P(C.c_int32), P(C.c_int64), P(C.c_uint32), P(C.c_int64),
                                      P(C.c_int64), P(C.c_uint32)]
         L.kgo_ext_replay.restype = C.c_int
+        L.kgo_ext_replay_parallel.argtypes = L.kgo_ext_replay.argtypes + [C.c_int]
+        L.kgo_ext_replay_parallel.restype = C.c_int
         L.kgo_ext_pair_nominated.argtypes = [P(abi.KgConfig), P(abi.KgNodeColumns), C.c_uint32, C.c_uint32,
                                              P(abi.KgPodColumns), C.c_uint32, P(KgoExt)]
         L.kgo_ext_pair_nominated.restype = C.c_int64
@@ -341,7 +343,9 @@ class OracleState:
         assert rc == 0
         return out_node, out_total
 
-    def ext_replay(self, pods: abi.Table, quotas=None, index_base: int = 0, reasons: bool = False, rsv=None):
+    def ext_replay(self, pods: abi.Table, quotas=None, index_base: int = 0, reasons: bool = False, rsv=None,
+                   workers: int = 1):
+        """kgo_ext_replay (workers > 1: kgo_ext_replay_parallel, each cycle's nodes on worker threads)."""
         np_ = abi.table_len(pods)
         out_node = np.zeros(np_, np.int32)
         out_total = np.zeros(np_, np.int64)
@@ -352,10 +356,11 @@ class OracleState:
         qn = np.zeros((max(nq, 1), abi.KG_QUOTA_R), np.int64)
         pc, e = abi.pod_columns(pods), make_ext(quotas, rsv)
         P = C.POINTER
-        rc = lib().kgo_ext_replay(C.byref(self.cfg), self.h, index_base, C.byref(pc), np_, C.byref(e),
-                                  out_node.ctypes.data_as(P(C.c_int32)), out_total.ctypes.data_as(P(C.c_int64)),
-                                  out_minors.ctypes.data_as(P(C.c_uint32)), qu.ctypes.data_as(P(C.c_int64)),
-                                  qn.ctypes.data_as(P(C.c_int64)), out_reason.ctypes.data_as(P(C.c_uint32)))
+        args = (C.byref(self.cfg), self.h, index_base, C.byref(pc), np_, C.byref(e),
+                out_node.ctypes.data_as(P(C.c_int32)), out_total.ctypes.data_as(P(C.c_int64)),
+                out_minors.ctypes.data_as(P(C.c_uint32)), qu.ctypes.data_as(P(C.c_int64)),
+                qn.ctypes.data_as(P(C.c_int64)), out_reason.ctypes.data_as(P(C.c_uint32)))
+        rc = lib().kgo_ext_replay_parallel(*args, int(workers)) if workers > 1 else lib().kgo_ext_replay(*args)
         assert rc == 0
         if reasons:
             return out_node, out_total, out_minors, qu[:nq], qn[:nq], out_reason

@@ -292,3 +292,17 @@ def test_replay_with_gpu_reservations(ctx, seed, numa):
     assert np.array_equal(used, qu) and np.array_equal(npu, qn)
     assert np.array_equal(snap.read_state()["dev_free"], st.dev_free())
     assert (node >= 0).sum() > 100
+
+
+@pytest.mark.parametrize("seed,numa", [(89, "single")])
+def test_oracle_parallel_ext_replay_equals_serial(seed, numa):
+    """kgo_ext_replay_parallel (each cycle's nodes on worker threads: the config-5 replay's CPU baseline) places,
+    scores and reserves exactly as the serial oracle replay."""
+    cfg, nodes, pods, quotas, rsv, _, _ = _gpu_cluster(600, 120, seed, numa)
+    kc = cfg.kg_config()
+    a = oracle_lib.OracleState(kc, nodes).ext_replay(pods, quotas, rsv=rsv, reasons=True)
+    st = oracle_lib.OracleState(kc, nodes)
+    b = st.ext_replay(pods, quotas, rsv=rsv, reasons=True, workers=4)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert (a[0] >= 0).sum() > 30
