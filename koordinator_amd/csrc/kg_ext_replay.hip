@@ -36,17 +36,29 @@ __device__ __forceinline__ uint64_t ext_replay_pick(uint32_t step, uint32_t n_no
     if (rs) {
         const RsvStep& z = rs[step % 3];
         const uint64_t pf = ld_agent(&z.pref);
-        const int64_t rm = pf != PREF_NONE ? 1000 : (int64_t)ld_agent(&z.rmax);
-        const uint32_t cnt = ld_agent(&z.cnt);
+        const uint32_t rmax = ld_agent(&z.rmax), cnt = ld_agent(&z.cnt);
+        const int64_t rm = pf != PREF_NONE ? 1000 : (int64_t)rmax;
         const uint64_t* L = rlist + (size_t)(step % 3) * n_nodes * 2;
-        for (uint32_t k = lane; k < cnt; k += 64) {
-            const uint64_t kb = ld_agent(L + 2 * (size_t)k), sc = ld_agent(L + 2 * (size_t)k + 1);
-            const uint32_t g = 0xFFFFFFFFu - (uint32_t)(kb & 0xFFFFFFFFull);
-            const int64_t sd = (int64_t)(uint32_t)(sc >> 32);
-            const int64_t rsv = (pf != PREF_NONE && (uint32_t)pf == g) ? 1000 : (int64_t)(uint32_t)sc;
-            const int64_t tot = (int64_t)(kb >> 32) + (int64_t)cfg.w_dev * norm100(sd, M) + (int64_t)cfg.w_rsv * norm100(rsv, rm);
-            const uint64_t key = ((uint64_t)tot << 32) | (kb & 0xFFFFFFFFull);
-            best = key > best ? key : best;
+        // the listed pairs, U entries per lane in flight per round trip (a class pod lists up to its class's views)
+        constexpr uint32_t U = 8;
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64u * U) {
+            uint64_t kb[U], sc[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t k = k0 + u * 64u + lane;
+                kb[u] = k < cnt ? ld_agent(L + 2 * (size_t)k) : 0ull;
+                sc[u] = k < cnt ? ld_agent(L + 2 * (size_t)k + 1) : 0ull;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t g = 0xFFFFFFFFu - (uint32_t)(kb[u] & 0xFFFFFFFFull);
+                const int64_t sd = (int64_t)(uint32_t)(sc[u] >> 32);
+                const int64_t rsv = (pf != PREF_NONE && (uint32_t)pf == g) ? 1000 : (int64_t)(uint32_t)sc[u];
+                const int64_t tot =
+                    (int64_t)(kb[u] >> 32) + (int64_t)cfg.w_dev * norm100(sd, M) + (int64_t)cfg.w_rsv * norm100(rsv, rm);
+                const uint64_t key = kb[u] ? (((uint64_t)tot << 32) | (kb[u] & 0xFFFFFFFFull)) : 0ull;
+                best = key > best ? key : best;
+            }
         }
     }
     return wmax_u64(best);
