@@ -715,7 +715,7 @@ class ClusterState:
         """Snapshot row of node i from the incrementally maintained caches."""
         name = self.names[i]
         t = self.topo[i]
-        row = node_static_cols(self.nodes[i], self.cfg, t.zones, t.kubelet_policy)
+        row = node_static_cols(self.nodes[i], self.cfg, t.zones, t.kubelet_policy, self.la)
         row.update(nodeinfo_cols(self.req[i], int(self.num_pods[i])))
         cache = self.assign_cache.get(name) or LoadAwareNodeCache(la=self.la)
         row.update(la_cols(self.nodes[i], cache.metric, cache, self.la, self.clock()))

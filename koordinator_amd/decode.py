@@ -10,6 +10,7 @@ Times are float seconds relative to the frozen snapshot time ``now`` (None = uns
 """
 from __future__ import annotations
 
+import functools
 import json
 import math
 import re
@@ -49,7 +50,16 @@ def parse_quantity(q) -> Fraction:
         return Fraction(q)
     if isinstance(q, float):
         return Fraction(q)
-    m = _QRE.match(str(q).strip())
+    if isinstance(q, str):
+        return _parse_quantity_str(q)
+    return _parse_quantity_str(str(q))
+
+
+@functools.lru_cache(maxsize=65536)
+def _parse_quantity_str(q: str) -> Fraction:
+    """parse_quantity of a string, memoised: an event stream repeats a few hundred distinct quantities, and a
+    Fraction is immutable (the host event layer spent a third of its time here)."""
+    m = _QRE.match(q.strip())
     if not m:
         raise ValueError(f"invalid quantity {q!r}")
     num, suf = m.groups()
@@ -825,10 +835,11 @@ def nodeinfo_cols(requested: Sequence[int], num_pods: int) -> Dict[str, object]:
 
 
 def node_static_cols(node: dict, cfg: SchedulerConfig, zones: Optional[List[Dict[str, str]]] = None,
-                     kubelet_numa_policy: str = "") -> Dict[str, object]:
+                     kubelet_numa_policy: str = "", la=None) -> Dict[str, object]:
     """Columns that follow the Node object (allocatable, LoadAware thresholds, NUMA policy and amplification)
-    and the NodeResourceTopology zones."""
-    la = cfg.la()
+    and the NodeResourceTopology zones. la: cfg.la() when the caller holds it (defaulting deep-copies the args)."""
+    if la is None:
+        la = cfg.la()
     alloc = _rl((node.get("status") or {}).get("allocatable"))
     row: Dict[str, object] = {
         "alloc_cpu": milli_value(alloc.get(CPU, 0)),
@@ -928,7 +939,7 @@ def zone_used_cols(used: Optional[List[Dict[str, str]]], cpuset_allocated_milli:
 def node_row(ni: NodeInput, cfg: SchedulerConfig, now: float = 0.0) -> Dict[str, object]:
     """Snapshot row of one node built from scratch (the incremental path is cluster.ClusterState)."""
     la = cfg.la()
-    row = node_static_cols(ni.node, cfg, ni.numa_zones, ni.kubelet_numa_policy)
+    row = node_static_cols(ni.node, cfg, ni.numa_zones, ni.kubelet_numa_policy, la)
     req = [0] * (len(NODEINFO_KEYS) + abi.KG_NSCALAR)
     for p in ni.pods:  # NodeInfo.AddPod for every pod on the node
         for i, x in enumerate(pod_request_vec(p, cfg)):
