@@ -103,7 +103,7 @@ def _rl(d) -> ResourceList:
 
 def _add(dst: ResourceList, src: ResourceList):
     for k, v in src.items():
-        dst[k] = dst.get(k, Fraction(0)) + v
+        dst[k] = dst[k] + v if k in dst else v
 
 
 def _max(dst: ResourceList, src: ResourceList):
@@ -137,12 +137,15 @@ def pod_requests(pod, non_missing: Optional[ResourceList] = None) -> ResourceLis
                     r[k] = v
         return r
 
+    containers, inits = _containers(pod), _init_containers(pod)
+    if len(containers) == 1 and not inits and not (pod.get("spec") or {}).get("overhead"):
+        return creqs(containers[0])  # the common pod: one container, its requests as they are
     reqs: ResourceList = {}
-    for c in _containers(pod):
+    for c in containers:
         _add(reqs, creqs(c))
     restartable: ResourceList = {}
     init_reqs: ResourceList = {}
-    for c in _init_containers(pod):
+    for c in inits:
         cr = creqs(c)
         if _restartable(c):
             _add(reqs, cr)
