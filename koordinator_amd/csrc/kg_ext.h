@@ -1658,6 +1658,19 @@ __device__ __forceinline__ uint64_t pref_key(int64_t order, uint32_t gidx) {
 
 __device__ __forceinline__ int64_t norm100(int64_t s, int64_t mx) { return mx == 0 ? s : qdiv(s * 100, mx); }
 
+// A general pair's selection inputs as the statistics pass stores them (ExtDev::xpairs): infeasible, infeasible with
+// KG_ST_UNSUPPORTED, "evaluate again" (a value outside the packing), or bit 63 | base total << 24 | raw DeviceShare score
+// << 12 | nominated-reservation score (the weighted NodeResourcesFit / LoadAware / NodeNUMAResource part is below 2^31:
+// weights <= 2^20, scores <= 100).
+constexpr uint64_t XPAIR_INFEASIBLE = 0, XPAIR_LIVE = 1, XPAIR_UNSUP = 2;
+
+__device__ __forceinline__ uint64_t xpair_pack(const KCfg& c, const PairX& r) {
+    if (r.status) return (r.status & KG_ST_UNSUPPORTED) ? XPAIR_UNSUP : XPAIR_INFEASIBLE;
+    const int64_t base = (int64_t)c.w_nrf * r.s_nrf + (int64_t)c.w_la * r.s_la + (int64_t)c.w_numa * r.s_numa;
+    if (base < 0 || base >= (1ll << 31) || r.s_dev < 0 || r.s_dev > 4095 || r.s_rsv < 0 || r.s_rsv > 4095) return XPAIR_LIVE;
+    return (1ull << 63) | ((uint64_t)base << 24) | ((uint64_t)r.s_dev << 12) | (uint64_t)r.s_rsv;
+}
+
 __device__ __forceinline__ int64_t total_ext(const KCfg& c, const PairX& o, uint32_t gidx, uint32_t dev_max,
                                              uint32_t rsv_max, uint64_t pref) {
     const bool has_pref = pref != PREF_NONE;
@@ -1665,6 +1678,17 @@ __device__ __forceinline__ int64_t total_ext(const KCfg& c, const PairX& o, uint
     const int64_t rmax = has_pref ? 1000 : (int64_t)rsv_max;
     return (int64_t)c.w_nrf * o.s_nrf + (int64_t)c.w_la * o.s_la + (int64_t)c.w_numa * o.s_numa +
            (int64_t)c.w_dev * norm100(o.s_dev, dev_max) + (int64_t)c.w_rsv * norm100(rsv, rmax);
+}
+
+// total_ext of a packed pair (xpair_pack, bit 63 set)
+__device__ __forceinline__ int64_t total_xpair(const KCfg& c, uint64_t x, uint32_t gidx, uint32_t dev_max, uint32_t rsv_max,
+                                               uint64_t pref) {
+    const bool has_pref = pref != PREF_NONE;
+    const int64_t s_rsv = (int64_t)(x & 0xFFFull), s_dev = (int64_t)((x >> 12) & 0xFFFull);
+    const int64_t rsv = (has_pref && (uint32_t)pref == gidx) ? 1000 : s_rsv;
+    const int64_t rmax = has_pref ? 1000 : (int64_t)rsv_max;
+    return (int64_t)((x >> 24) & 0x7FFFFFFFull) + (int64_t)c.w_dev * norm100(s_dev, dev_max) +
+           (int64_t)c.w_rsv * norm100(rsv, rmax);
 }
 
 }  // namespace kg

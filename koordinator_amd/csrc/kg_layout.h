@@ -536,6 +536,12 @@ struct ExtDev {
     const int32_t* graw;
     GpuRawNode* gnodes;
     GpuRawRsv* grsv;
+    // fast-base config-5 batch: the general pairs' selection inputs, stored by the statistics pass
+    // (k_ext_stats_sp: a GPU pod's every general pair; k_ext_stats_views: a class pod's views) for the select pass
+    // (k_ext_select_sp), [pod][xT] by the pair's position in for_general_records (XPAIR_*); nullptr = none
+    uint64_t* xpairs;
+    uint32_t xT;
+    const uint32_t* xsp;  // the special list the positions count from (k_special_scan)
 };
 
 }  // namespace kg

@@ -248,6 +248,9 @@ struct kg_pods {
     uint32_t* d_minors = nullptr;     // replay: GPU minors chosen per pod
     uint64_t* d_buckets = nullptr;    // replay: [3][128] per-score best keys (REPLAY_BUCKET_STRIDE apart)
     uint32_t* d_done = nullptr;       // config-5 replay: workgroups done in the current step launch (last one picks)
+    uint64_t* d_xpairs = nullptr;     // fast-base config-5 select: stored general pairs (ExtDev::xpairs)
+    size_t xpairs_cap = 0;            // entries
+    uint32_t xT = 0;                  // row length of the pairs the last ext_stats_local stored (0 = none)
     int32_t* d_aout = nullptr;        // kg_assume_ext outputs
     uint64_t* d_rec = nullptr;        // kg_reserve / kg_unreserve: cpuset CPUs [4] + NUMA zone amounts [8]
     uint32_t* d_batch = nullptr;      // kg_batch_schedule: groups + per-pod outputs (7 x cap + 1 words)
@@ -1598,7 +1601,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
     for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_partial,
                     (void*)p->d_gather, (void*)p->d_qst, (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref,
                     (void*)p->d_minors, (void*)p->d_buckets, (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_pstat,
-                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_gz, (void*)p->d_spec, (void*)p->d_split, (void*)p->d_batch, (void*)p->d_rcode, (void*)p->d_done, (void*)p->d_rec})
+                    (void*)p->d_reason, (void*)p->d_devsum, (void*)p->d_gz, (void*)p->d_spec, (void*)p->d_split, (void*)p->d_batch, (void*)p->d_rcode, (void*)p->d_done, (void*)p->d_rec, (void*)p->d_xpairs})
         hipFree(b);
     hipHostFree(p->h_in);
     hipHostFree(p->h_keys);
@@ -1875,6 +1878,26 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
         HIP_TRY(ctx, launch_special_scan(s->d_nodes, s->n, s->n0, s->d_special, const_cast<uint32_t*>(c1_list(s, p)),
                                          ctx->stream));
     }
+    p->xT = 0;
+    if (ext_fast_base(s, p) && (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) && !std::getenv("KG_NO_XPAIRS")) {
+        // the general pairs' selection inputs, stored for the select pass: [pod][special list + largest class's views]
+        const uint32_t T = special_est(s, p) + s->max_cls_views + 64;
+        const size_t need = (size_t)p->n * T;
+        if (need * sizeof(uint64_t) <= ((size_t)4 << 30)) {
+            if (p->xpairs_cap < need) {
+                HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+                HIP_TRY(ctx, hipFree(p->d_xpairs));
+                p->d_xpairs = nullptr;
+                p->xpairs_cap = 0;
+                HIP_TRY(ctx, hipMalloc(&p->d_xpairs, sizeof(uint64_t) * std::max<size_t>(need, 1)));
+                p->xpairs_cap = need;
+            }
+            p->xT = T;
+            e.xpairs = p->d_xpairs;
+            e.xT = T;
+            e.xsp = s->d_special;
+        }
+    }
     if (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) {
         // pods without a GPU request only get statistics from the nodes holding a view of their
         // reservation class (elsewhere s_dev = s_rsv = order = 0): one lane per pod over those views
@@ -2029,6 +2052,12 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     if (fused) HIP_TRY(ctx, hipMemsetAsync(xkeys, 0, sizeof(uint64_t) * n_x, ctx->stream));
     ExtDev xe = s->ext_dev();
     xe.dsum = (s->d_dev && ext_fast_base(s, p)) ? p->d_devsum : nullptr;  // ext_stats_local built it for this batch
+    if (fb && p->xT) {  // the general pairs ext_stats_local stored for this batch
+        xe.xpairs = p->d_xpairs;
+        xe.xT = p->xT;
+        xe.xsp = s->d_special;
+    }
+    p->xT = 0;
     xe.rcode = (xe.dsum && s->n_rdev && p->n_dclass) ? p->d_rcode : nullptr;   // and the restore tables' codes
     xe.gz = (xe.dsum && gz_active(s, p)) ? p->d_gz : nullptr;                 // and the class-1 records' GPU hints
     const bool guess = fb && xe.dsum && (s->cfg.plugins & KG_PLUGIN_DEV) && p->n_stat > p->n_stat_cls;
