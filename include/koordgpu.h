@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KG_ABI_VERSION 11
+#define KG_ABI_VERSION 12
 
 /* LoadAware resource vector width: the default vectorizer is {cpu, memory}
  * (pkg/scheduler/plugins/loadaware/helper.go:162-173, sorted by name). */
@@ -644,6 +644,7 @@ typedef struct kg_reserve_record {
 } kg_reserve_record;
 #define KG_RECORD_CPUSET 0x1u  /* the Reserve took cpuset CPUs (cpus) */
 #define KG_RECORD_QUOTA 0x2u   /* the Reserve added the pod to its ElasticQuota's used */
+#define KG_RECORD_RELEASED 0x4u /* kg_unreserve gave the record back: a second Unreserve of it is refused */
 
 /* Reserve of pod `pod` on local node `node` with every enabled plugin (kg_assume / kg_assume_ext: NodeInfo,
  * LoadAware, NodeNUMAResource incl. cpusets, DeviceShare, ElasticQuota, Reservation.Reserve on the node's views),
@@ -652,8 +653,10 @@ kg_status kg_reserve(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, 
 /* Unreserve of a kg_reserve: every plugin gives back what the record says it took (load_aware.go:231-233,
  * nodenumaresource/plugin.go:700-720 -> resource_manager.go:478-483 Release incl. the cpuset CPUs and the NUMA
  * single / shared sets, deviceshare/plugin.go Unreserve, elasticquota/plugin.go:638-652, reservation/plugin.go:1409-1460
- * forgetPods: the reservation's Allocated and assigned pods, and the node's views as the next restore builds them). */
-kg_status kg_unreserve(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, const kg_reserve_record* rec);
+ * forgetPods: the reservation's Allocated and assigned pods, and the node's views as the next restore builds them).
+ * The record is marked KG_RECORD_RELEASED on success; a record so marked is refused (KG_INVALID_ARG, nothing applied):
+ * the reference's NodeAllocation.release and forgetPods do nothing for a pod they no longer hold (ABI 12). */
+kg_status kg_unreserve(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node, kg_reserve_record* rec);
 /* Copy of the snapshot's reservation views and infos as the device holds them (after Reservation.Reserve /
  * Unreserve on the device): n_views / n_infos entries as uploaded, in upload order. */
 kg_status kg_snapshot_read_reservations(kg_snap* snap, kg_rsv_view* views, uint32_t n_views, kg_rsv_info* infos,

@@ -11,7 +11,7 @@ from typing import Dict
 
 import numpy as np
 
-KG_ABI_VERSION = 11
+KG_ABI_VERSION = 12
 KG_LA_R = 2
 KG_NSCALAR = 2
 KG_MAX_ZONES = 4

@@ -33,7 +33,8 @@ __device__ __forceinline__ void cpuset_zone_count(ZoneRec& z, uint32_t used, int
     for (uint32_t q = 0; q < (uint32_t)MAX_ZONES; q++) {
         if (!((used >> q) & 1u)) continue;
         uint8_t& c = multi ? z.cz_shared[q] : z.cz_single[q];
-        c = (uint8_t)((int)c + sign < 0 ? 0 : (int)c + sign);
+        const int v = (int)c + sign;  // saturating at 0 and 255, as the host's zone_pods and the oracle count
+        c = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
     }
     z.status = zone_status_of_counts(z);
 }

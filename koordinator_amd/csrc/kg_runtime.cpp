@@ -1889,13 +1889,20 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
                 HIP_TRY(ctx, hipFree(p->d_xpairs));
                 p->d_xpairs = nullptr;
                 p->xpairs_cap = 0;
-                HIP_TRY(ctx, hipMalloc(&p->d_xpairs, sizeof(uint64_t) * std::max<size_t>(need, 1)));
-                p->xpairs_cap = need;
+                // the stored pairs are a speed-up only: without the memory the select evaluates those pairs again
+                if (hipMalloc(&p->d_xpairs, sizeof(uint64_t) * std::max<size_t>(need, 1)) != hipSuccess) {
+                    (void)hipGetLastError();
+                    p->d_xpairs = nullptr;
+                } else {
+                    p->xpairs_cap = need;
+                }
             }
-            p->xT = T;
-            e.xpairs = p->d_xpairs;
-            e.xT = T;
-            e.xsp = s->d_special;
+            if (p->d_xpairs) {
+                p->xT = T;
+                e.xpairs = p->d_xpairs;
+                e.xT = T;
+                e.xsp = s->d_special;
+            }
         }
     }
     if (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) {
@@ -2805,7 +2812,7 @@ kg_status kg_reserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, kg_res
     return KG_OK;
 }
 
-kg_status kg_unreserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, const kg_reserve_record* rec) {
+kg_status kg_unreserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, kg_reserve_record* rec) {
     kg_status st = check_pair(s, p);
     if (st != KG_OK) return st;
     kg_ctx* ctx = s->ctx;
@@ -2813,6 +2820,7 @@ kg_status kg_unreserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, cons
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     if (zone_reserve_fails(rec->numa_zone)) return fail(ctx, KG_INVALID_ARG, "the record's Reserve failed: nothing to give back");
+    if (rec->flags & KG_RECORD_RELEASED) return fail(ctx, KG_INVALID_ARG, "the record was already given back");
     if (s->ext()) {
         st = check_ext(s);
         if (st != KG_OK) return st;
@@ -2839,6 +2847,7 @@ kg_status kg_unreserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, cons
     s->gen++;
     HIP_TRY(ctx, launch_big_scan(s->d_nodes, s->n, s->d_big + 1, s->d_big, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // r is on this stack
+    rec->flags |= KG_RECORD_RELEASED;
     return KG_OK;
 }
 
@@ -3410,6 +3419,24 @@ kg_status kg_snapshot_upload_rsv_gpu(kg_snap* s, const kg_rsv_gpu* g, uint32_t n
             node_entry[g[k].node] = (int32_t)k;
         } else {
             rsv_of[g[k].node].push_back(k);
+        }
+    }
+    // the inputs must cover every GPU-holding view and reservation: a node left out would keep stale restore tables
+    // after a Reserve there (its record has no raw entry), so a partial upload is refused and the calls keep refusing
+    for (const kg_rsv_view& v : s->h_views) {
+        if (v.node >= s->n) continue;
+        if (v.dev_base >= 0 && node_entry[v.node] < 0)
+            return fail(ctx, KG_INVALID_ARG, "node %u: a view holds GPU restore tables but no used entry was given", v.node);
+        for (uint32_t t = v.first; t < v.first + v.count && t < s->h_infos.size(); t++) {
+            if (s->h_infos[t].dev < 0) continue;
+            if (node_entry[v.node] < 0)
+                return fail(ctx, KG_INVALID_ARG, "node %u: reservation %u holds GPUs but no used entry was given", v.node,
+                            s->h_infos[t].rid);
+            bool found = false;
+            for (uint32_t k : rsv_of[v.node]) found = found || (uint32_t)g[k].rid == s->h_infos[t].rid;
+            if (!found)
+                return fail(ctx, KG_INVALID_ARG, "node %u: reservation %u holds GPUs but has no entry", v.node,
+                            s->h_infos[t].rid);
         }
     }
     std::vector<GpuRawNode> gn;

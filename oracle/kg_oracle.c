@@ -3309,7 +3309,7 @@ static uint32_t dev_choose_site_o(const kg_config* c, const kg_node_columns* n, 
  * reservation it joined (rid) counts the allocation on its own minors (appendAllocatedByHints) and one more pod, then
  * the tables are rebuilt (every pod: the assigned pod count decides which reservations are unmatched with pods) */
 static void gpu_apply_o(kgo_state* st, const kgo_ext* e, kg_rsv_dev* devs, gpu_raw* x, uint32_t i, uint32_t mask,
-                        const kg_pod_columns* p, uint32_t j, int32_t rid) {
+                        const kg_pod_columns* p, uint32_t j, int32_t rid, int64_t sign) {
     kg_rsv_gpu* N = raw_entry(x, i, -1);
     if (!N) return;
     kg_rsv_gpu* R = rid >= 0 ? raw_entry(x, i, rid) : NULL;
@@ -3322,16 +3322,22 @@ static void gpu_apply_o(kgo_state* st, const kgo_ext* e, kg_rsv_dev* devs, gpu_r
         int64_t a[KG_DEV_R];
         dev_alloc_of(preq, keys, DEVX(st->dev_total, i, KG_DEV_MEM, m), a);
         for (int r = 0; r < KG_DEV_R; r++) {
-            N->a[r][m] += a[r];
-            if (R && ((hints >> m) & 1u)) R->b[r][m] += a[r];
+            /* the Unreserve (sign -1): updateCacheUsed(add=false) subtracts with a non-negative result, and the pod
+             * leaves the reservation's AssignedPods (its allocation no longer counts in allocated) */
+            const int64_t u = N->a[r][m] + sign * a[r];
+            N->a[r][m] = u < 0 ? 0 : u;
+            if (R && ((hints >> m) & 1u)) {
+                const int64_t b = R->b[r][m] + sign * a[r];
+                R->b[r][m] = b < 0 ? 0 : b;
+            }
         }
     }
-    if (R) R->allocated_pods += 1;
+    if (R) R->allocated_pods = sign > 0 ? R->allocated_pods + 1 : (R->allocated_pods > 0 ? R->allocated_pods - 1 : 0);
     gpu_rebuild_o(st, e, devs, x, i);
 }
 
-/* The replay can follow the reservations' restore on the device only while none of them holds GPUs (their
- * DeviceShare restore tables are derived from the reserve pods' and assigned pods' GPU allocations). */
+/* Reservations holding GPUs: their DeviceShare restore tables derive from the reserve pods' and assigned pods' GPU
+ * allocations, so the replay and the batch cycle follow them only with the raw inputs (kgo_ext.gpu). */
 static int rsv_has_gpu_tables(const kgo_ext* e) {
     if (!e) return 0;
     for (uint32_t v = 0; v < e->n_views; v++)
@@ -3475,7 +3481,7 @@ static int ext_replay_impl(const kg_config* c, kgo_state* st, uint32_t base, con
         }
         quota_apply(q, p, j, 1);
         if (rsv && mv) rsv_reserve(st, mv, ee->n_views, mi, i, p, j, nom);
-        if (raw) gpu_apply_o(st, ee, md, &gx, i, mask, p, j, nom >= 0 ? (int32_t)mi[nom].rid : -1);
+        if (raw) gpu_apply_o(st, ee, md, &gx, i, mask, p, j, nom >= 0 ? (int32_t)mi[nom].rid : -1, 1);
     }
     if (workers > 1) {
         par.quit = 1;
@@ -3619,7 +3625,7 @@ int kgo_batch_schedule(const kg_config* c, kgo_state* st, const kg_pod_columns* 
             }
             quota_apply(q, p, j, 1);
             if (rsv) rsv_reserve(st, mv, ee->n_views, mi, (uint32_t)node, p, j, nom);
-            if (raw) gpu_apply_o(st, ee, md, &gx, (uint32_t)node, mask, p, j, nom >= 0 ? (int32_t)mi[nom].rid : -1);
+            if (raw) gpu_apply_o(st, ee, md, &gx, (uint32_t)node, mask, p, j, nom >= 0 ? (int32_t)mi[nom].rid : -1, 1);
             out_result[j] = KG_BATCH_ASSUMED;
             out_zone[j] = zone;
         }
@@ -3720,5 +3726,245 @@ void kgo_unreserve(const kg_config* c, kgo_state* st, uint32_t i, const kg_pod_c
         uint32_t keys;
         dev_pod_req(p, j, preq, &keys);
         dev_apply(st->dev_total, st->dev_free, i, rec->gpu_minors, preq, keys, -1);
+    }
+}
+
+/* ---- Reserve / Unreserve with every config-5 plugin (a session over one kgo_state) ------------------------------------ */
+
+/* Reservation.Unreserve of pod j on node i (reservation/plugin.go:1409-1460 -> reservationCache.forgetPods ->
+ * ReservationInfo.RemoveAssignedPod, frameworkext/reservation_info.go:502-514): the reservation rid the pod joined loses
+ * Mask(requests, ResourceNames) from Allocated (quotav1.SubtractWithNonNegativeResult; its keys stay) and one assigned
+ * pod. The next cycle's restore (transformer.go:740-935) then sees the node through it: NodeInfo no longer holds the pod
+ * (apply has removed it from the state's columns); the reservation's unmatched correction (restoreUnmatchedReservations
+ * :891-903: Allocated and its NonZeroRequested while it has assigned pods, nothing after the last) changes from its old
+ * to its new value in the record's columns and in the views that do not match it; the views that match it lose the pod
+ * and count the new Allocated in rAllocated (:786-790); every view of the node has one pod less. rid -1: the pod joined
+ * no reservation (only the pod leaves the views). */
+static void rsv_unreserve(kgo_state* st, kg_rsv_view* views, uint32_t nv, kg_rsv_info* infos, uint32_t i,
+                          const kg_pod_columns* p, uint32_t j, int32_t rid) {
+    const int64_t preq[KG_RSV_R] = {p->req_cpu[j], p->req_mem[j], p->req_eph ? p->req_eph[j] : 0,
+                                    p->sc_req[0] ? p->sc_req[0][j] : 0, p->sc_req[1] ? p->sc_req[1][j] : 0};
+    const int64_t pnz[2] = {p->nz_cpu[j], p->nz_mem[j]};
+    /* the reservation as the node's views hold it (its copies agree) */
+    const kg_rsv_info* r = NULL;
+    for (uint32_t x = 0; x < nv && rid >= 0 && !r; x++) {
+        if (views[x].node != i) continue;
+        for (uint32_t t = views[x].first; t < views[x].first + views[x].count; t++)
+            if ((int32_t)infos[t].rid == rid) {
+                r = &infos[t];
+                break;
+            }
+    }
+    int64_t old_a[KG_RSV_R] = {0}, new_a[KG_RSV_R] = {0}, corr0[KG_RSV_R] = {0}, corr1[KG_RSV_R] = {0};
+    int64_t nz0[2] = {0, 0}, nz1[2] = {0, 0}, pods1 = 0;
+    uint32_t keys = 0;
+    if (r) {
+        keys = r->allocated_keys;
+        const int64_t pods0 = r->allocated_pods;
+        pods1 = pods0 > 0 ? pods0 - 1 : 0;
+        for (int k = 0; k < KG_RSV_R; k++) {
+            const int64_t m = ((r->names >> k) & 1u) ? preq[k] : 0;
+            old_a[k] = r->allocated[k];
+            new_a[k] = old_a[k] - m < 0 ? 0 : old_a[k] - m;
+            corr0[k] = pods0 > 0 ? old_a[k] : 0;
+            corr1[k] = pods1 > 0 ? new_a[k] : 0;
+        }
+        if (pods0 > 0) rsv_nonzero(old_a, keys, nz0);
+        if (pods1 > 0) rsv_nonzero(new_a, keys, nz1);
+        /* the record (pods matching nothing): the correction is subtracted from NodeInfo's Requested */
+        st->col[C_REQ_CPU][i] -= corr1[0] - corr0[0];
+        st->col[C_REQ_MEM][i] -= corr1[1] - corr0[1];
+        st->col[C_REQ_EPH][i] -= corr1[2] - corr0[2];
+        for (int k = 0; k < KG_NSCALAR; k++) st->col[C_SC_REQ + k][i] -= corr1[3 + k] - corr0[3 + k];
+        st->col[C_NZ_CPU][i] -= nz1[0] - nz0[0];
+        st->col[C_NZ_MEM][i] -= nz1[1] - nz0[1];
+    }
+    for (uint32_t x = 0; x < nv; x++) {
+        kg_rsv_view* v = &views[x];
+        if (v->node != i) continue;
+        int matched = 0;
+        for (uint32_t t = v->first; t < v->first + v->count && r; t++) matched |= (int32_t)infos[t].rid == rid;
+        for (int k = 0; k < KG_RSV_R; k++) {
+            const int64_t d = -preq[k] - (matched ? 0 : corr1[k] - corr0[k]);
+            v->req[k] += d;
+            v->pod_requested[k] += d;
+            if (matched) v->r_allocated[k] += new_a[k] - old_a[k];
+        }
+        v->nz_cpu += -pnz[0] - (matched ? 0 : nz1[0] - nz0[0]);
+        v->nz_mem += -pnz[1] - (matched ? 0 : nz1[1] - nz0[1]);
+        v->num_pods -= 1;
+    }
+    if (!r) return;
+    for (uint32_t x = 0; x < nv; x++) {
+        if (views[x].node != i) continue;
+        for (uint32_t t = views[x].first; t < views[x].first + views[x].count; t++) {
+            kg_rsv_info* c = &infos[t];
+            if ((int32_t)c->rid != rid) continue;
+            for (int k = 0; k < KG_RSV_R; k++) c->allocated[k] = new_a[k];
+            c->allocated_pods = pods1;
+        }
+    }
+}
+
+struct kgo_ext_session {
+    kg_config c;
+    kgo_state* st; /* borrowed */
+    kgo_ext e2;
+    kg_rsv_view* mv;
+    kg_rsv_info* mi;
+    kg_rsv_dev* md;
+    gpu_raw gx;
+    view_index vx;
+    kgo_quota_state* q;
+    int rsv;
+    ext_buf b;
+};
+
+kgo_ext_session* kgo_ext_session_new(const kg_config* c, kgo_state* st, const kgo_ext* e) {
+    kgo_ext_session* x = (kgo_ext_session*)calloc(1, sizeof(*x));
+    if (!x) return NULL;
+    x->c = *c;
+    x->st = st;
+    x->rsv = (c->plugins & KG_PLUGIN_RSV) && e && e->n_views;
+    if (x->rsv && rsv_has_gpu_tables(e) && !e->n_gpu) { /* the GPU restore cannot be followed without its inputs */
+        free(x);
+        return NULL;
+    }
+    if (e) x->e2 = *e;
+    if (x->rsv) {
+        x->mv = (kg_rsv_view*)malloc(sizeof(kg_rsv_view) * e->n_views);
+        x->mi = (kg_rsv_info*)malloc(sizeof(kg_rsv_info) * (e->n_infos ? e->n_infos : 1));
+        x->md = (kg_rsv_dev*)malloc(sizeof(kg_rsv_dev) * (e->n_devs ? e->n_devs : 1));
+        memcpy(x->mv, e->views, sizeof(kg_rsv_view) * e->n_views);
+        if (e->n_infos) memcpy(x->mi, e->infos, sizeof(kg_rsv_info) * e->n_infos);
+        if (e->n_devs) memcpy(x->md, e->devs, sizeof(kg_rsv_dev) * e->n_devs);
+        x->gx.n = e->n_gpu;
+        x->gx.g = (kg_rsv_gpu*)malloc(sizeof(kg_rsv_gpu) * (e->n_gpu ? e->n_gpu : 1));
+        if (e->n_gpu) memcpy(x->gx.g, e->gpu, sizeof(kg_rsv_gpu) * e->n_gpu);
+        x->e2.views = x->mv;
+        x->e2.infos = x->mi;
+        x->e2.devs = x->md;
+        view_index_build(&x->vx, &x->e2, st->n);
+    }
+    x->q = (c->plugins & KG_PLUGIN_QUOTA) && e ? quota_state_new(e->quotas, e->n_quotas) : NULL;
+    if (ext_buf_new(&x->b, st->n)) {
+        kgo_ext_session_free(x);
+        return NULL;
+    }
+    return x;
+}
+
+void kgo_ext_session_free(kgo_ext_session* x) {
+    if (!x) return;
+    free(x->mv);
+    free(x->mi);
+    free(x->md);
+    free(x->gx.g);
+    free(x->vx.v);
+    quota_state_free(x->q);
+    free(x->b.mem);
+    free(x);
+}
+
+/* Reserve of pod j on node i with every enabled plugin, as one scheduling cycle's Reserve runs them on the pair
+ * (NodeInfo + LoadAware, NodeNUMAResource incl. cpusets, DeviceShare at the site its Reserve allocates from,
+ * ElasticQuota used, Reservation.Reserve into the nominated reservation with the views and the GPU restore following):
+ * 0 + the record its Unreserve gives back, or 1 when the NodeNUMAResource Reserve fails (nothing applied). */
+int kgo_ext_reserve(kgo_ext_session* x, uint32_t i, const kg_pod_columns* p, uint32_t j, kg_reserve_record* rec) {
+    const kg_config* c = &x->c;
+    kgo_state* st = x->st;
+    memset(rec, 0, sizeof(*rec));
+    rec->numa_zone = -1;
+    rec->rsv_rid = -1;
+    kg_node_columns v;
+    kgo_state_view(st, &v);
+    const kgo_ext* ee = x->rsv ? &x->e2 : NULL;
+    kg_config c2 = *c;
+    if (!x->rsv) c2.plugins &= ~KG_PLUGIN_RSV;
+    /* the pair's evaluation (the PreFilter's quota gate is not part of it) */
+    ext_eval_nodes(&c2, &v, i, i + 1, p, j, ee ? ee : &x->e2, x->rsv ? &x->vx : NULL, 0, &x->b.r);
+    const uint32_t s = x->b.r.st[i];
+    const int32_t zone = s ? -1 : x->b.r.zone[i];
+    const int64_t nom = s ? -1 : x->b.r.nom[i];
+    rec->numa_zone = zone;
+    if (zone_fails(zone)) return 1;
+    const int32_t cls = p->rsv_class ? p->rsv_class[j] : -1;
+    const kg_rsv_view* vw = x->rsv ? find_view(&x->vx, &x->e2, cls, i) : NULL;
+    uint32_t mask = 0;
+    if ((c->plugins & KG_PLUGIN_DEV) && st->dev_minors)
+        mask = dev_choose_site_o(c, &v, i, p, j, &x->e2, vw, nom, zone);
+    uint64_t cpus[4] = {0, 0, 0, 0};
+    int64_t amounts[2 * KG_MAX_ZONES] = {0};
+    const int32_t f = apply(c, st, i, p, j, zone, 1, amounts, cpus);
+    if (f) {
+        rec->numa_zone = f;
+        return 1;
+    }
+    const int raw = x->rsv && raw_entry(&x->gx, i, -1) != NULL;
+    if (mask && !raw) {
+        int64_t preq[KG_DEV_R];
+        uint32_t keys;
+        dev_pod_req(p, j, preq, &keys);
+        dev_apply(st->dev_total, st->dev_free, i, mask, preq, keys, 1);
+    }
+    if (x->q) {
+        quota_apply(x->q, p, j, 1);
+        rec->flags |= KG_RECORD_QUOTA;
+    }
+    const int32_t rid = nom >= 0 ? (int32_t)x->mi[nom].rid : -1;
+    if (x->rsv) rsv_reserve(st, x->mv, x->e2.n_views, x->mi, i, p, j, nom);
+    if (raw) gpu_apply_o(st, &x->e2, x->md, &x->gx, i, mask, p, j, rid, 1);
+    rec->gpu_minors = mask;
+    rec->rsv_rid = x->rsv ? rid : -1;
+    memcpy(rec->zone_amounts, amounts, sizeof(amounts));
+    memcpy(rec->cpus, cpus, sizeof(cpus));
+    if (cpus[0] | cpus[1] | cpus[2] | cpus[3]) rec->flags |= KG_RECORD_CPUSET;
+    return 0;
+}
+
+/* Unreserve of a kgo_ext_reserve: every plugin gives back what the record says it took (load_aware.go:231-233,
+ * nodenumaresource/plugin.go:700-720 -> resource_manager.go:478-483 Release, deviceshare Unreserve -> updateCacheUsed,
+ * elasticquota/plugin.go:638-652, reservation/plugin.go:1409-1460). -1 (nothing applied) for a record already given
+ * back; the record is then marked KG_RECORD_RELEASED. */
+int kgo_ext_unreserve(kgo_ext_session* x, uint32_t i, const kg_pod_columns* p, uint32_t j, kg_reserve_record* rec) {
+    if (rec->flags & KG_RECORD_RELEASED) return -1;
+    const kg_config* c = &x->c;
+    kgo_state* st = x->st;
+    int64_t amounts[2 * KG_MAX_ZONES];
+    uint64_t cpus[4];
+    memcpy(amounts, rec->zone_amounts, sizeof(amounts));
+    memcpy(cpus, rec->cpus, sizeof(cpus));
+    int any = 0;
+    for (int z = 0; z < 2 * KG_MAX_ZONES; z++) any |= amounts[z] != 0;
+    const int32_t zone = rec->numa_zone < 0 ? -1 : any ? 0x4F : rec->numa_zone;
+    (void)apply(c, st, i, p, j, zone, -1, any ? amounts : NULL, (rec->flags & KG_RECORD_CPUSET) ? cpus : NULL);
+    if (x->rsv) rsv_unreserve(st, x->mv, x->e2.n_views, x->mi, i, p, j, rec->rsv_rid);
+    const int raw = x->rsv && raw_entry(&x->gx, i, -1) != NULL;
+    if (raw) {
+        gpu_apply_o(st, &x->e2, x->md, &x->gx, i, (p->dev_count && p->dev_count[j] > 0) ? rec->gpu_minors : 0u, p, j,
+                    rec->rsv_rid, -1);
+    } else if (rec->gpu_minors && st->dev_total) {
+        int64_t preq[KG_DEV_R];
+        uint32_t keys;
+        dev_pod_req(p, j, preq, &keys);
+        dev_apply(st->dev_total, st->dev_free, i, rec->gpu_minors, preq, keys, -1);
+    }
+    if (x->q && (rec->flags & KG_RECORD_QUOTA)) quota_apply(x->q, p, j, -1);
+    rec->flags |= KG_RECORD_RELEASED;
+    return 0;
+}
+
+/* The session's reservation views, infos and GPU restore tables (as uploaded: n_views / n_infos / n_devs entries) and the
+ * quota used / non-preemptible used [quota][KG_QUOTA_R]; any pointer may be NULL. */
+void kgo_ext_session_read(const kgo_ext_session* x, kg_rsv_view* views, kg_rsv_info* infos, kg_rsv_dev* devs,
+                          int64_t* quota_used, int64_t* quota_np_used) {
+    if (x->rsv) {
+        if (views) memcpy(views, x->mv, sizeof(kg_rsv_view) * x->e2.n_views);
+        if (infos && x->e2.n_infos) memcpy(infos, x->mi, sizeof(kg_rsv_info) * x->e2.n_infos);
+        if (devs && x->e2.n_devs) memcpy(devs, x->md, sizeof(kg_rsv_dev) * x->e2.n_devs);
+    }
+    if (x->q) {
+        if (quota_used) memcpy(quota_used, x->q->used, (size_t)x->q->n * KG_QUOTA_R * 8);
+        if (quota_np_used) memcpy(quota_np_used, x->q->np_used, (size_t)x->q->n * KG_QUOTA_R * 8);
     }
 }

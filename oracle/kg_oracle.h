@@ -111,6 +111,17 @@ int64_t kgo_ext_pair_nominated(const kg_config* c, const kg_node_columns* n, uin
 int kgo_batch_schedule(const kg_config* cfg, kgo_state* st, const kg_pod_columns* pods, uint32_t n_pods,
                        const kgo_ext* ext, const int32_t* plan_node, uint32_t* out_result, uint32_t* out_status,
                        int32_t* out_zone, uint32_t* out_minors, int64_t* quota_used_out, int64_t* quota_np_used_out);
+/* Reserve / Unreserve with every config-5 plugin over one kgo_state (borrowed; it must outlive the session): the
+ * session holds mutable copies of the reservation views / infos / GPU restore tables and inputs and the quota used,
+ * which kgo_ext_reserve / kgo_ext_unreserve follow as kg_reserve / kg_unreserve do on the device. NULL when the
+ * reservations hold GPUs without their restore inputs. */
+typedef struct kgo_ext_session kgo_ext_session;
+kgo_ext_session* kgo_ext_session_new(const kg_config* cfg, kgo_state* st, const kgo_ext* ext);
+void kgo_ext_session_free(kgo_ext_session* x);
+int kgo_ext_reserve(kgo_ext_session* x, uint32_t node, const kg_pod_columns* pods, uint32_t pod, kg_reserve_record* rec);
+int kgo_ext_unreserve(kgo_ext_session* x, uint32_t node, const kg_pod_columns* pods, uint32_t pod, kg_reserve_record* rec);
+void kgo_ext_session_read(const kgo_ext_session* x, kg_rsv_view* views, kg_rsv_info* infos, kg_rsv_dev* devs,
+                          int64_t* quota_used, int64_t* quota_np_used);
 /* Node-sharded two-pass selection: per-shard NormalizeScore inputs (to be max / min all-reduced over
  * the shards), then the shard's top-k with the global inputs. */
 int kgo_ext_shard_stats(const kg_config* cfg, const kg_node_columns* nodes, uint32_t n_nodes, uint32_t index_base,

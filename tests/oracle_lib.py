@@ -130,6 +130,15 @@ def lib():
         L.kgo_reserve.restype = C.c_int
         L.kgo_unreserve.argtypes = [P(abi.KgConfig), C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32,
                                     P(abi.KgReserveRecord)]
+        L.kgo_ext_session_new.argtypes = [P(abi.KgConfig), C.c_void_p, P(KgoExt)]
+        L.kgo_ext_session_new.restype = C.c_void_p
+        L.kgo_ext_session_free.argtypes = [C.c_void_p]
+        L.kgo_ext_reserve.argtypes = [C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32, P(abi.KgReserveRecord)]
+        L.kgo_ext_reserve.restype = C.c_int
+        L.kgo_ext_unreserve.argtypes = [C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32, P(abi.KgReserveRecord)]
+        L.kgo_ext_unreserve.restype = C.c_int
+        L.kgo_ext_session_read.argtypes = [C.c_void_p, P(abi.KgRsvView), P(abi.KgRsvInfo), P(abi.KgRsvDev), P(C.c_int64),
+                                           P(C.c_int64)]
         L.kgo_mem_bytes_to_ratio.argtypes = [C.c_int64, C.c_int64]
         L.kgo_mem_bytes_to_ratio.restype = C.c_int64
         L.kgo_amplify.argtypes = [C.c_int64, C.c_double]
@@ -429,6 +438,56 @@ class OracleState:
             raw = C.string_at(v.cpu_alloc, n * 2 * abi.KG_MAX_CPUS)
             t["cpu_alloc"] = np.frombuffer(raw, np.uint8).reshape(n, 2 * abi.KG_MAX_CPUS).copy()
         return t
+
+
+class ExtSession:
+    """kgo_ext_session: Reserve / Unreserve with every config-5 plugin (NodeInfo, LoadAware, NUMA incl. cpusets,
+    DeviceShare with the GPU restore, ElasticQuota, Reservation) over an OracleState, the oracle side of
+    kg_reserve / kg_unreserve."""
+
+    def __init__(self, state: OracleState, quotas=None, rsv=None):
+        self.state = state
+        self.rsv = rsv
+        self.nq = len(quotas["used"]) if quotas is not None else 0
+        self.e = make_ext(quotas, rsv)
+        self.h = lib().kgo_ext_session_new(C.byref(state.cfg), state.h, C.byref(self.e))
+        assert self.h, "GPU-holding reservations without their restore inputs"
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().kgo_ext_session_free(self.h)
+            self.h = None
+
+    def reserve(self, node: int, pods: abi.Table, pod: int):
+        """(ok, record); ok False when the NodeNUMAResource Reserve fails (nothing applied)."""
+        pc = abi.pod_columns(pods)
+        rec = abi.KgReserveRecord()
+        rc = lib().kgo_ext_reserve(self.h, node, C.byref(pc), pod, C.byref(rec))
+        return rc == 0, rec
+
+    def unreserve(self, node: int, pods: abi.Table, pod: int, rec) -> bool:
+        """False (nothing applied) for a record already given back."""
+        pc = abi.pod_columns(pods)
+        return lib().kgo_ext_unreserve(self.h, node, C.byref(pc), pod, C.byref(rec)) == 0
+
+    def read_reservations(self) -> abi.Reservations:
+        """The views / infos / GPU restore tables as the session holds them, in the layout of the uploaded rsv."""
+        r = self.rsv
+        out = abi.Reservations([], [])
+        out.views = (abi.KgRsvView * max(1, r.n_views))()
+        out.infos = (abi.KgRsvInfo * max(1, r.n_infos))()
+        out.devs = (abi.KgRsvDev * max(1, r.n_devs))()
+        out.n_views, out.n_infos, out.n_devs = r.n_views, r.n_infos, r.n_devs
+        lib().kgo_ext_session_read(self.h, out.views, out.infos, out.devs, None, None)
+        return out
+
+    def read_quotas(self):
+        used = np.zeros((max(self.nq, 1), abi.KG_QUOTA_R), np.int64)
+        npu = np.zeros((max(self.nq, 1), abi.KG_QUOTA_R), np.int64)
+        P = C.POINTER
+        lib().kgo_ext_session_read(self.h, None, None, None, used.ctypes.data_as(P(C.c_int64)),
+                                   npu.ctypes.data_as(P(C.c_int64)))
+        return used[:self.nq], npu[:self.nq]
 
 
 def assert_state_restored(before, after):

@@ -278,3 +278,36 @@ def test_reserve_unreserve_round_trip_gpu_reservations():
         assert r1.infos[x].allocated_pods == r0.infos[x].allocated_pods, x
     assert np.array_equal(engine.eval_select(snap, batch, 1), keys0)
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_zone_pod_counts_saturate_at_255():
+    """NUMANodeSharedStatus pod counts are kept in one byte and saturate at 255, on the device as in the oracle (and the
+    host's zone_pods): a cpuset Reserve on NUMA nodes that already count 255 single-NUMA pods keeps 255 (the node stays
+    busy), and its Unreserve then counts one less."""
+    from koordinator_amd import engine
+    cfg, t, p = _one_node([range(0, 2)], max_ref=1)
+    t["numa_zone_pods"] = np.array([255 | (255 << 8)], np.uint64)
+    t["numa_zone_status"] = np.array([1 | (1 << 2)], np.uint32)
+    kc = cfg.kg_config()
+    st = oracle_lib.OracleState(kc, t)
+    ok, orec = st.reserve(0, p, 0)
+    assert ok and orec.flags & abi.KG_RECORD_CPUSET
+    ctx = engine.Context(0)
+    try:
+        snap = engine.Snapshot(ctx, kc, t)
+        batch = engine.PodBatch(ctx, p)
+        drec = engine.reserve(snap, batch, 0, 0)
+        assert list(drec.cpus) == list(orec.cpus)
+        dev, want = snap.read_state(), st.table()
+        assert int(want["numa_zone_pods"][0]) & 0xFFFF == 255 | (255 << 8)
+        for c in ("numa_zone_pods", "numa_zone_status", "cpu_alloc"):
+            assert np.array_equal(dev[c], want[c]), c
+        engine.unreserve(snap, batch, 0, 0, drec)
+        st.unreserve(0, p, 0, orec)
+        dev, want = snap.read_state(), st.table()
+        assert int(want["numa_zone_pods"][0]) & 0xFFFF != 255 | (255 << 8)  # one NUMA node counts 254 now
+        for c in ("numa_zone_pods", "numa_zone_status", "cpu_alloc"):
+            assert np.array_equal(dev[c], want[c]), c
+    finally:
+        ctx.close()

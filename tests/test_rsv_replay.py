@@ -294,6 +294,52 @@ def test_replay_with_gpu_reservations(ctx, seed, numa):
     assert (node >= 0).sum() > 100
 
 
+@pytest.mark.gpu
+def test_partial_rsv_gpu_upload_is_refused(ctx):
+    """kg_snapshot_upload_rsv_gpu must cover every GPU-holding view and reservation: an empty upload, one without a
+    node's used entry, or one without a reservation's entry is KG_INVALID_ARG, and the replay keeps refusing the
+    snapshot (KG_UNSUPPORTED) instead of scoring later pods against restore tables nothing rebuilds."""
+    import ctypes as C
+    from koordinator_amd import engine
+    cfg, nodes, pods, quotas, rsv, _, _ = _gpu_cluster(300, 40, 87)
+    assert rsv.n_gpu > 2
+    kc = cfg.kg_config()
+    snap = engine.Snapshot(ctx, kc, nodes)
+    snap.upload_quotas(quotas)
+    gpu, n_gpu = rsv.gpu, rsv.n_gpu
+    rsv.n_gpu = 0
+    try:
+        snap.upload_reservations(rsv)  # the views only
+    finally:
+        rsv.n_gpu = n_gpu
+    batch = engine.PodBatch(ctx, pods)
+    with pytest.raises(engine.Unsupported):
+        engine.replay(snap, batch)
+    entries = [gpu[k] for k in range(n_gpu)]
+    gpu_views = set()  # (node, rid) of every GPU-holding reservation in a view; rid -1 = a view's own GPU table
+    for v in range(rsv.n_views):
+        w = rsv.views[v]
+        if w.dev_base >= 0:
+            gpu_views.add((w.node, -1))
+        for t in range(w.first, w.first + w.count):
+            if rsv.infos[t].dev >= 0:
+                gpu_views.add((w.node, -1))
+                gpu_views.add((w.node, int(rsv.infos[t].rid)))
+    node_k = next(k for k, e in enumerate(entries) if e.rid < 0 and (e.node, -1) in gpu_views)
+    rsv_k = next(k for k, e in enumerate(entries) if e.rid >= 0 and (e.node, int(e.rid)) in gpu_views)
+    for drop in (list(range(n_gpu)), [node_k], [rsv_k]):
+        keep = [e for k, e in enumerate(entries) if k not in drop]
+        arr = (abi.KgRsvGpu * max(1, len(keep)))(*keep)
+        s = ctx.L.kg_snapshot_upload_rsv_gpu(snap.h, C.cast(arr, C.POINTER(abi.KgRsvGpu)), len(keep))
+        assert s == abi.KG_INVALID_ARG, drop
+        with pytest.raises(engine.Unsupported):
+            engine.replay(snap, batch)
+    # the whole set is accepted and the replay runs
+    ctx.check(ctx.L.kg_snapshot_upload_rsv_gpu(snap.h, C.cast(gpu, C.POINTER(abi.KgRsvGpu)), n_gpu), "upload_rsv_gpu")
+    node, _ = engine.replay(snap, batch)
+    assert (node >= 0).sum() > 10
+
+
 @pytest.mark.parametrize("seed,numa", [(89, "single")])
 def test_oracle_parallel_ext_replay_equals_serial(seed, numa):
     """kgo_ext_replay_parallel (each cycle's nodes on worker threads: the config-5 replay's CPU baseline) places,
