@@ -661,6 +661,9 @@ kg_status kg_unreserve(kg_snap* snap, kg_pods* pods, uint32_t pod, uint32_t node
  * Unreserve on the device): n_views / n_infos entries as uploaded, in upload order. */
 kg_status kg_snapshot_read_reservations(kg_snap* snap, kg_rsv_view* views, uint32_t n_views, kg_rsv_info* infos,
                                         uint32_t n_infos);
+/* Copy of the GPU restore tables (kg_rsv_dev, n_devs as uploaded) as the device holds them: a Reserve / Unreserve into a
+ * node with GPU-holding reservations rebuilds that node's tables (ABI 12). */
+kg_status kg_snapshot_read_rsv_devs(kg_snap* snap, kg_rsv_dev* devs, uint32_t n_devs);
 
 /* Device cpuset accumulator, one request per workgroup: out[4 * i] = the CPUs chosen for request i,
  * rc[i] = 0, -1 (ErrNotEnoughCPUs: fewer allocatable CPUs than needed) or -2 ("failed to allocate cpus").

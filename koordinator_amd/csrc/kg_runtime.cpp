@@ -3218,6 +3218,13 @@ static kg_status sync_views_from_device(kg_snap* s) {
         h.allocated_pods = di[t].allocated_pods;
         h.allocated_keys = di[t].allocated_keys;
     }
+    // the GPU restore tables a Reserve into a node with GPU-holding reservations rebuilt (gpu_restore_rebuild): a later
+    // kg_snapshot_update_views keeps the other nodes' tables from these copies
+    if (s->gpu_raw && s->d_rdev && s->n_rdev && s->h_rdevs.size() == s->n_rdev) {
+        HIP_TRY(ctx, hipMemcpyAsync(s->h_rdevs.data(), s->d_rdev, sizeof(DevRec) * s->n_rdev, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
     s->views_on_device = false;
     return KG_OK;
 }
@@ -3234,6 +3241,19 @@ kg_status kg_snapshot_read_reservations(kg_snap* s, kg_rsv_view* views, uint32_t
     if (st != KG_OK) return st;
     std::copy(s->h_views.begin(), s->h_views.end(), views);
     std::copy(s->h_infos.begin(), s->h_infos.end(), infos);
+    return KG_OK;
+}
+
+kg_status kg_snapshot_read_rsv_devs(kg_snap* s, kg_rsv_dev* devs, uint32_t n_devs) {
+    if (!s) return KG_INVALID_ARG;
+    kg_ctx* ctx = s->ctx;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n_devs != s->h_rdevs.size() || (n_devs && !devs))
+        return fail(ctx, KG_INVALID_ARG, "%u GPU restore tables uploaded", (uint32_t)s->h_rdevs.size());
+    if (!n_devs) return KG_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemcpyAsync(devs, s->d_rdev, sizeof(DevRec) * n_devs, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return KG_OK;
 }
 

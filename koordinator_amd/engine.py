@@ -141,6 +141,8 @@ def lib():
     L.kg_unreserve.restype = st
     L.kg_snapshot_read_reservations.argtypes = [vp, P(abi.KgRsvView), u32, P(abi.KgRsvInfo), u32]
     L.kg_snapshot_read_reservations.restype = st
+    L.kg_snapshot_read_rsv_devs.argtypes = [vp, P(abi.KgRsvDev), u32]
+    L.kg_snapshot_read_rsv_devs.restype = st
     L.kg_snapshot_upload_rsv_gpu.argtypes = [vp, P(abi.KgRsvGpu), u32]
     L.kg_snapshot_upload_rsv_gpu.restype = st
     if L.kg_abi_version() != abi.KG_ABI_VERSION:
@@ -288,8 +290,8 @@ class Snapshot:
                                                                  rsv.n_gpu), "kg_snapshot_upload_rsv_gpu")
 
     def read_reservations(self, rsv: abi.Reservations) -> abi.Reservations:
-        """The views and infos as the device holds them now (Reservation.Reserve / Unreserve ran there), in the
-        layout of the uploaded `rsv` (same counts; its GPU restore tables are shared)."""
+        """The views, infos and GPU restore tables as the device holds them now (Reservation.Reserve / Unreserve ran
+        there), in the layout of the uploaded `rsv` (same counts)."""
         out = abi.Reservations([], [])
         out.views = (abi.KgRsvView * max(1, rsv.n_views))()
         out.infos = (abi.KgRsvInfo * max(1, rsv.n_infos))()
@@ -298,6 +300,10 @@ class Snapshot:
         self.ctx.check(self.ctx.L.kg_snapshot_read_reservations(
             self.h, C.cast(out.views, C.POINTER(abi.KgRsvView)), rsv.n_views,
             C.cast(out.infos, C.POINTER(abi.KgRsvInfo)), rsv.n_infos), "kg_snapshot_read_reservations")
+        if rsv.n_devs:  # the GPU restore tables as the device rebuilt them
+            out.devs = (abi.KgRsvDev * rsv.n_devs)()
+            self.ctx.check(self.ctx.L.kg_snapshot_read_rsv_devs(self.h, C.cast(out.devs, C.POINTER(abi.KgRsvDev)),
+                                                                rsv.n_devs), "kg_snapshot_read_rsv_devs")
         return out
 
     def update_views(self, nodes, rsv: abi.Reservations):

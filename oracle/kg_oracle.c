@@ -3922,6 +3922,19 @@ int kgo_ext_reserve(kgo_ext_session* x, uint32_t i, const kg_pod_columns* p, uin
     return 0;
 }
 
+/* The pair's Filter status (every enabled plugin but the PreFilter's quota gate) on the session's current state: the
+ * Reserve runs only on a node that passed it. */
+uint32_t kgo_ext_session_filter(kgo_ext_session* x, uint32_t i, const kg_pod_columns* p, uint32_t j) {
+    kg_node_columns v;
+    kgo_state_view(x->st, &v);
+    kg_config c2 = x->c;
+    if (!x->rsv) c2.plugins &= ~KG_PLUGIN_RSV;
+    ext_eval_nodes(&c2, &v, i, i + 1, p, j, &x->e2, x->rsv ? &x->vx : NULL, 0, &x->b.r);
+    uint32_t s = x->b.r.st[i];
+    if (!s && zone_fails(x->b.r.zone[i])) s = zone_fail_bits(x->b.r.zone[i]);
+    return s;
+}
+
 /* Unreserve of a kgo_ext_reserve: every plugin gives back what the record says it took (load_aware.go:231-233,
  * nodenumaresource/plugin.go:700-720 -> resource_manager.go:478-483 Release, deviceshare Unreserve -> updateCacheUsed,
  * elasticquota/plugin.go:638-652, reservation/plugin.go:1409-1460). -1 (nothing applied) for a record already given

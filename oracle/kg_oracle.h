@@ -118,6 +118,7 @@ int kgo_batch_schedule(const kg_config* cfg, kgo_state* st, const kg_pod_columns
 typedef struct kgo_ext_session kgo_ext_session;
 kgo_ext_session* kgo_ext_session_new(const kg_config* cfg, kgo_state* st, const kgo_ext* ext);
 void kgo_ext_session_free(kgo_ext_session* x);
+uint32_t kgo_ext_session_filter(kgo_ext_session* x, uint32_t node, const kg_pod_columns* pods, uint32_t pod);
 int kgo_ext_reserve(kgo_ext_session* x, uint32_t node, const kg_pod_columns* pods, uint32_t pod, kg_reserve_record* rec);
 int kgo_ext_unreserve(kgo_ext_session* x, uint32_t node, const kg_pod_columns* pods, uint32_t pod, kg_reserve_record* rec);
 void kgo_ext_session_read(const kgo_ext_session* x, kg_rsv_view* views, kg_rsv_info* infos, kg_rsv_dev* devs,

@@ -133,6 +133,8 @@ def lib():
         L.kgo_ext_session_new.argtypes = [P(abi.KgConfig), C.c_void_p, P(KgoExt)]
         L.kgo_ext_session_new.restype = C.c_void_p
         L.kgo_ext_session_free.argtypes = [C.c_void_p]
+        L.kgo_ext_session_filter.argtypes = [C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32]
+        L.kgo_ext_session_filter.restype = C.c_uint32
         L.kgo_ext_reserve.argtypes = [C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32, P(abi.KgReserveRecord)]
         L.kgo_ext_reserve.restype = C.c_int
         L.kgo_ext_unreserve.argtypes = [C.c_void_p, C.c_uint32, P(abi.KgPodColumns), C.c_uint32, P(abi.KgReserveRecord)]
@@ -457,6 +459,11 @@ class ExtSession:
         if getattr(self, "h", None):
             lib().kgo_ext_session_free(self.h)
             self.h = None
+
+    def filter(self, node: int, pods: abi.Table, pod: int) -> int:
+        """The pair's Filter status bits on the current state (0 = feasible; a failing Reserve's NUMA bits too)."""
+        pc = abi.pod_columns(pods)
+        return int(lib().kgo_ext_session_filter(self.h, node, C.byref(pc), pod))
 
     def reserve(self, node: int, pods: abi.Table, pod: int):
         """(ok, record); ok False when the NodeNUMAResource Reserve fails (nothing applied)."""

@@ -146,6 +146,8 @@ def test_oracle_session_follows_the_restore(seed):
 
     for j in range(abi.table_len(pods)):
         node = target[j]
+        if sess.filter(node, pods, j):  # the Reserve follows a passing Filter only
+            continue
         ok, rec = sess.reserve(node, pods, j)
         if ok:
             book(node, j, rec, 1)
@@ -179,12 +181,15 @@ def _dev_vs_oracle(ctx, cfg, nodes, pods, quotas, rsv, target, check_every=1):
     st = oracle_lib.OracleState(kc, nodes)
     sess = oracle_lib.ExtSession(st, quotas, rsv)
     held = []
-    stats = dict(reserved=0, into=0, gpu_into=0, cpuset=0, back=0, failed=0)
+    stats = dict(reserved=0, into=0, gpu_into=0, cpuset=0, back=0, failed=0, infeasible=0)
     keys = ("req_cpu", "req_mem", "num_pods", "nz_cpu", "nz_mem", "cpuset_alloc_milli", "numa_zone_status",
             "numa_zone_pods", "zone_cpu_used0", "zone_cpu_used1", "zone_mem_used0", "zone_mem_used1", "la_fbase_np0",
             "dev_free")
     for j in range(abi.table_len(pods)):
         node = target[j]
+        if sess.filter(node, pods, j):  # the Reserve follows a passing Filter only
+            stats["infeasible"] += 1
+            continue
         ok, orec = sess.reserve(node, pods, j)
         try:
             drec = engine.reserve(snap, batch, j, node)
@@ -251,7 +256,7 @@ def test_interleaved_reserve_unreserve_cluster5_device_vs_oracle(seed, numa):
         s = _dev_vs_oracle(ctx, cfg, nodes, pods, quotas, rsv, target)
     finally:
         ctx.close()
-    assert s["into"] >= 20 and s["gpu_into"] >= 2 and s["back"] >= 40, s
+    assert s["into"] >= 20 and s["gpu_into"] >= 2 and s["back"] >= 30, s
 
 
 @pytest.mark.gpu
@@ -267,4 +272,4 @@ def test_interleaved_reserve_unreserve_cluster5_cpusets_device_vs_oracle():
         s = _dev_vs_oracle(ctx, cfg, nodes, pods, quotas, rsv, target)
     finally:
         ctx.close()
-    assert s["into"] >= 20 and s["cpuset"] >= 3 and s["back"] >= 40, s
+    assert s["into"] >= 20 and s["cpuset"] >= 3 and s["back"] >= 25, s

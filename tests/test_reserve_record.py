@@ -289,6 +289,7 @@ def test_zone_pod_counts_saturate_at_255():
     cfg, t, p = _one_node([range(0, 2)], max_ref=1)
     t["numa_zone_pods"] = np.array([255 | (255 << 8)], np.uint64)
     t["numa_zone_status"] = np.array([1 | (1 << 2)], np.uint32)
+    p["flags"] = ((p["flags"] & ~np.uint32(abi.KG_POD_NUMA_SKIP)) | abi.KG_POD_HAS_CPU).astype(np.uint32)
     kc = cfg.kg_config()
     st = oracle_lib.OracleState(kc, t)
     ok, orec = st.reserve(0, p, 0)
