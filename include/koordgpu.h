@@ -498,6 +498,11 @@ typedef struct kg_rsv_info {
                                           * updates all of them)                                       */
     uint32_t allocated_keys;             /* bit 0 / 1: Allocated holds a cpu / memory key (0 while nil):
                                           * GetNonZeroRequestForResource of the unmatched correction   */
+    uint32_t dev_minors;                 /* the GPU minors the reservation reserves (bit m; ABI 12): a pod allocating
+                                          * from it takes them first (tryAllocateFromReusable's preferred set,
+                                          * deviceshare/reservation.go:308; defaultAllocateDevices ->
+                                          * sortDeviceResourcesByMinor, device_resources.go:187-209)      */
+    uint32_t pad_;
 } kg_rsv_info;
 
 /* GPU minors as one restore sees them (nodeDevice.calcFreeWithPreemptible / filter, deviceshare/

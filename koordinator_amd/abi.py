@@ -278,7 +278,7 @@ class KgRsvInfo(C.Structure):
     _fields_ = [("policy", C.c_uint32), ("names", C.c_uint32), ("allocate_once", C.c_uint32), ("dev", C.c_int32),
                 ("order", C.c_int64), ("allocatable", C.c_int64 * KG_RSV_R), ("allocated", C.c_int64 * KG_RSV_R),
                 ("reserved", C.c_int64 * KG_RSV_R), ("max_pods", C.c_int64), ("allocated_pods", C.c_int64),
-                ("rid", C.c_uint32), ("allocated_keys", C.c_uint32)]
+                ("rid", C.c_uint32), ("allocated_keys", C.c_uint32), ("dev_minors", C.c_uint32), ("pad_", C.c_uint32)]
 
 
 class KgRsvDev(C.Structure):

@@ -315,11 +315,13 @@ __device__ __forceinline__ bool gpu_scope_fits(int32_t D, uint64_t topo, uint32_
     return false;
 }
 
-// defaultAllocateDevices (device_allocator.go:355-437): minors by (scoreDevice desc, minor asc), the first
-// numberOfGPUs whose free resources are not all zero and cover the request. want_mask = false: only whether
-// enough minors fit (the Filter).
+// defaultAllocateDevices (device_allocator.go:355-437): minors by (preferred first, scoreDevice desc, minor asc;
+// sortDeviceResourcesByMinor, device_resources.go:187-209), the first numberOfGPUs whose free resources are not all
+// zero and cover the request. pref: the preferred minors (a reservation's reserved ones when the pod allocates from it,
+// deviceshare/reservation.go:308). want_mask = false: only whether enough minors fit (the Filter; the order cannot
+// change that).
 __device__ __forceinline__ GpuAlloc dev_default(const KCfg& c, const DevRec* __restrict__ d, int32_t D, const PodX& x,
-                                                bool want_mask, uint32_t allowed = ~0u) {
+                                                bool want_mask, uint32_t allowed = ~0u, uint32_t pref = 0u) {
     uint32_t fit = 0;
     for (int32_t m = 0; m < D; m++) {
         const int64_t fr[DEV_R] = {d->free_[0][m], d->free_[1][m], d->free_[2][m]};
@@ -350,7 +352,8 @@ __device__ __forceinline__ GpuAlloc dev_default(const KCfg& c, const DevRec* __r
         int64_t bs = 0;
 #pragma unroll
         for (int m = 0; m < DEV_MINORS; m++) {
-            const bool take = ((left >> m) & 1u) && (bm < 0 || sc[m] > bs);
+            const bool pm = (pref >> m) & 1u, pb = bm >= 0 && ((pref >> bm) & 1u);
+            const bool take = ((left >> m) & 1u) && (bm < 0 || (pm && !pb) || (pm == pb && sc[m] > bs));
             bs = take ? sc[m] : bs;
             bm = take ? m : bm;
         }
@@ -404,7 +407,7 @@ __device__ __forceinline__ uint32_t gpu_allocate_code(const ExtDev& e, int32_t D
 // ZoneRec.dev_topo / dev_part; outside: minors used on the node outside the table (0 for the node's own).
 __device__ __forceinline__ GpuAlloc gpu_allocate(const KCfg& c, const ExtDev& e, const DevRec* __restrict__ d, int32_t D,
                                                  uint64_t topo, uint32_t part, const PodX& x, uint32_t outside,
-                                                 bool want_mask, uint32_t allowed = ~0u) {
+                                                 bool want_mask, uint32_t allowed = ~0u, uint32_t pref = 0u) {
     if (!want_mask) return {gpu_allocate_code(e, D, topo, part, x, gpu_minors(d, D, x, outside, allowed)), 0u};
     const uint32_t tm = gpu_template(x, part);
     if (tm == 0u) return {KG_DEV_CODE_NO_TEMPLATE, 0u};
@@ -432,7 +435,7 @@ __device__ __forceinline__ GpuAlloc gpu_allocate(const KCfg& c, const ExtDev& e,
     } else if (required) {
         return {KG_DEV_CODE_NO_TREE, 0u};
     }
-    return dev_default(c, d, D, x, want_mask, allowed);
+    return dev_default(c, d, D, x, want_mask, allowed, pref);
 }
 
 __device__ __forceinline__ uint32_t dev_code_status(uint32_t code) { return code ? KG_ST_DEV_MAKE(code) : 0u; }
@@ -458,7 +461,7 @@ __device__ __forceinline__ uint32_t gpu_numa_allowed(uint32_t dev_numa, int32_t 
 __device__ __forceinline__ GpuAlloc gpu_alloc_tab_numa(const KCfg& c, const ExtDev& e, const DevRec* __restrict__ d,
                                                        const DevRec* __restrict__ tab, int32_t D,
                                                        const ZoneRec* __restrict__ zr, const PodX& x, uint32_t numa,
-                                                       bool want_mask) {
+                                                       bool want_mask, uint32_t pref = 0u) {
     if (D == 0) return {KG_DEV_CODE_NO_DEVICE, 0u};  // Prepare (devicehandler_gpu.go:41-44)
     uint32_t in = ~0u, outside = 0u;  // the node's own devices without an affinity: no filter
     if (tab || numa) {
@@ -477,7 +480,7 @@ __device__ __forceinline__ GpuAlloc gpu_alloc_tab_numa(const KCfg& c, const ExtD
         in = allowed & in_tab;
         outside = node_used & ~in;
     }
-    return gpu_allocate(c, e, tab ? tab : d, D, zr->dev_topo, zr->dev_part, x, outside, want_mask, in);
+    return gpu_allocate(c, e, tab ? tab : d, D, zr->dev_topo, zr->dev_part, x, outside, want_mask, in, pref);
 }
 
 __device__ __forceinline__ GpuAlloc gpu_alloc_numa(const KCfg& c, const ExtDev& e, const DevRec* __restrict__ d,
@@ -1604,7 +1607,8 @@ __device__ __forceinline__ uint32_t dev_choose_site(const KCfg& c, const ExtDev&
     if (x.dcount == 0 || D <= 0) return 0;
     const uint32_t numa = zone_affinity(zone);
     if (v && nom >= 0 && e.infos[nom].dev >= 0) {
-        const GpuAlloc a = gpu_alloc_tab_numa(c, e, d, e.rdev + e.infos[nom].dev, D, zr, x, numa, true);
+        // the reservation's reserved minors first (tryAllocateFromReusable's preferred set)
+        const GpuAlloc a = gpu_alloc_tab_numa(c, e, d, e.rdev + e.infos[nom].dev, D, zr, x, numa, true, e.infos[nom].dev_pref);
         if (!a.code) return a.mask;
     }
     const DevRec* tab = (v && v->dev_base >= 0) ? e.rdev + v->dev_base : nullptr;

@@ -467,7 +467,9 @@ struct alignas(16) RsvInfo {
     int64_t allocatable[RSV_R], allocated[RSV_R], reserved[RSV_R];
     int64_t max_pods, allocated_pods;
     uint32_t rid, allocated_keys;  // kg_rsv_info.rid / .allocated_keys
-    uint64_t pad_;
+    uint32_t dev_pref;             // kg_rsv_info.dev_minors: the reserved GPU minors, taken first
+    uint32_t pad_;
+    uint64_t pad2_;
 };
 
 // Replay with reservation views: per step (ring of 3) the pairs whose Reservation score term can be nonzero (a

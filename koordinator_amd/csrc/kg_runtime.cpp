@@ -3326,6 +3326,7 @@ static kg_status upload_views(kg_snap* s, const kg_rsv_view* views, uint32_t nv,
         d.allocated_pods = x.allocated_pods;
         d.rid = x.rid;
         d.allocated_keys = x.allocated_keys;
+        d.dev_pref = x.dev_minors;
     }
     // the node record of every GPU restore table (a table belongs to one view: its base or one of its reservations)
     std::vector<uint32_t> rrec(std::max<uint32_t>(nd, 1), 0u);

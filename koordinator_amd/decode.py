@@ -1224,7 +1224,11 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
                                   max_pods=int(r.get("max_pods", -1)), allocated_pods=int(r.get("allocated_pods", 0)),
                                   dev=dev_idx.get(x, -1), rid=x,
                                   allocated_keys=(int(r.get("allocated_keys", 3)) if r.get("allocated") is not None
-                                                  else 0)))
+                                                  else 0),
+                                  # the reserved minors a pod allocating from the reservation takes first
+                                  # (tryAllocateFromReusable's preferred set, deviceshare/reservation.go:308)
+                                  dev_minors=(int(sum(1 << int(m) for m in np.nonzero(parts[x][0][1])[0]))
+                                              if dev_on and parts[x] is not None and x in dev_idx else 0)))
             views.append(dict(node=i, cls=c, first=first, count=len(matched), req=req, nz_cpu=nzc, nz_mem=nzm,
                               num_pods=int(out["num_pods"][i]) - len(matched), pod_requested=pod_requested,
                               r_allocated=r_alloc, dev_base=dev_base))

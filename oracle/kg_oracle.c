@@ -2020,10 +2020,11 @@ static void build_scope(uint64_t topo, int32_t D, gpu_scope* root, gpu_scope* nu
     }
 }
 
-/* defaultAllocateDevices (device_allocator.go:355-437): scoreDevices + sortDeviceResourcesByMinor (score
- * desc, minor asc, device_resources.go:171-209), the first numberOfGPUs minors that fit. */
+/* defaultAllocateDevices (device_allocator.go:355-437): scoreDevices + sortDeviceResourcesByMinor (the preferred
+ * minors first, then score desc, minor asc, device_resources.go:171-209), the first numberOfGPUs minors that fit.
+ * pref: requestCtx.preferred, the reserved minors of the reservation the pod allocates from (reservation.go:308). */
 static uint32_t default_allocate(const kg_config* c, const int64_t* T, const int64_t* F, int32_t D, const gpu_req* g,
-                                 uint32_t* mask) {
+                                 uint32_t pref, uint32_t* mask) {
     int64_t sc[KG_DEV_MINORS];
     int order[KG_DEV_MINORS];
     for (int32_t m = 0; m < D; m++) {
@@ -2035,10 +2036,12 @@ static uint32_t default_allocate(const kg_config* c, const int64_t* T, const int
         sc[m] = dev_least(c, t, f, g->preq);
         order[m] = m;
     }
-    for (int32_t a = 1; a < D; a++) { /* stable insertion sort by score desc (minor asc on ties) */
+    for (int32_t a = 1; a < D; a++) { /* stable insertion sort: preferred first, score desc (minor asc on ties) */
         int v = order[a];
         int32_t b = a;
-        while (b > 0 && sc[order[b - 1]] < sc[v]) {
+        const int pv = (pref >> v) & 1u;
+        while (b > 0 && (((pref >> order[b - 1]) & 1u) < (uint32_t)pv ||
+                         (((pref >> order[b - 1]) & 1u) == (uint32_t)pv && sc[order[b - 1]] < sc[v]))) {
             order[b] = order[b - 1];
             b--;
         }
@@ -2064,7 +2067,8 @@ static uint32_t default_allocate(const kg_config* c, const int64_t* T, const int
 /* GPUAllocator.Allocate: allocateByTemplate, then allocateByPartition, then generalAllocate =
  * allocateByDeviceTopology, then defaultAllocateDevices. Returns 0 with the minors, or a KG_DEV_CODE_*. */
 static uint32_t gpu_allocate(const kg_config* c, const kg_node_columns* n, uint32_t i, const int64_t* T,
-                             const int64_t* F, int32_t D, uint32_t outside, const gpu_req* g, uint32_t* mask) {
+                             const int64_t* F, int32_t D, uint32_t outside, const gpu_req* g, uint32_t pref,
+                             uint32_t* mask) {
     *mask = 0;
     const uint32_t part = n->dev_part ? n->dev_part[i] : 0u;
     const uint64_t topo = n->dev_topo ? n->dev_topo[i] : ~0ull;
@@ -2108,7 +2112,7 @@ static uint32_t gpu_allocate(const kg_config* c, const kg_node_columns* n, uint3
         }
         return required ? KG_DEV_CODE_TOPO_SCOPED : KG_DEV_CODE_GPU_DEVICES;
     }
-    return default_allocate(c, T, F, D, g, mask);
+    return default_allocate(c, T, F, D, g, pref, mask);
 }
 
 static uint32_t dev_code_status(uint32_t code) { return code ? KG_ST_DEV_MAKE(code) : 0u; }
@@ -2127,7 +2131,7 @@ static uint32_t dev_eval(const kg_config* c, const kg_node_columns* n, uint32_t 
     const int64_t* T = &DEVX(n->dev_total, i, 0, 0);
     const int64_t* F = &DEVX(n->dev_free, i, 0, 0);
     uint32_t mask;
-    const uint32_t code = gpu_allocate(c, n, i, T, F, D, 0u, &g, &mask);
+    const uint32_t code = gpu_allocate(c, n, i, T, F, D, 0u, &g, 0u, &mask);
     if (code) return dev_code_status(code);
     int64_t Ts[KG_DEV_R] = {0, 0, 0}, Fs[KG_DEV_R] = {0, 0, 0};
     for (int32_t m = 0; m < D; m++)
@@ -2161,8 +2165,9 @@ static uint32_t gpu_numa_allowed(const kg_node_columns* n, uint32_t i, int32_t D
  * when numa is 0) or a reservation restore table (kg_rsv_dev, already a filtered nodeDevice). The filtered nodeDevice
  * keeps the table's minors the affinity allows; getRealUsed (allocator_gpu.go:59-70) counts the node's used minors it
  * leaves out. Returns 0 with the minors, or a KG_DEV_CODE_*. */
-static uint32_t gpu_alloc_tab_numa(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
-                                   uint32_t j, const kg_rsv_dev* t, uint32_t numa, uint32_t* minors) {
+static uint32_t gpu_alloc_tab_numa_pref(const kg_config* c, const kg_node_columns* n, uint32_t i,
+                                        const kg_pod_columns* p, uint32_t j, const kg_rsv_dev* t, uint32_t numa,
+                                        uint32_t pref, uint32_t* minors) {
     gpu_req g;
     gpu_req_of(p, j, &g);
     const int32_t D = n->dev_minors[i];
@@ -2170,7 +2175,7 @@ static uint32_t gpu_alloc_tab_numa(const kg_config* c, const kg_node_columns* n,
     const int64_t* NF = &DEVX(n->dev_free, i, 0, 0);
     *minors = 0;
     if (D == 0) return KG_DEV_CODE_NO_DEVICE; /* Prepare: no GPU on the Device (devicehandler_gpu.go:41-44) */
-    if (!t && !numa) return gpu_allocate(c, n, i, NT, NF, D, 0u, &g, minors);
+    if (!t && !numa) return gpu_allocate(c, n, i, NT, NF, D, 0u, &g, pref, minors);
     const int64_t* T = t ? &t->total[0][0] : NT;
     const int64_t* F = t ? &t->free[0][0] : NF;
     const uint32_t allowed = numa ? gpu_numa_allowed(n, i, D, numa) : (D >= 32 ? ~0u : (1u << D) - 1u);
@@ -2189,7 +2194,12 @@ static uint32_t gpu_alloc_tab_numa(const kg_config* c, const kg_node_columns* n,
         }
         if (node_used && !in) outside |= 1u << m;
     }
-    return gpu_allocate(c, n, i, T2, F2, D, outside, &g, minors);
+    return gpu_allocate(c, n, i, T2, F2, D, outside, &g, pref, minors);
+}
+
+static uint32_t gpu_alloc_tab_numa(const kg_config* c, const kg_node_columns* n, uint32_t i, const kg_pod_columns* p,
+                                   uint32_t j, const kg_rsv_dev* t, uint32_t numa, uint32_t* minors) {
+    return gpu_alloc_tab_numa_pref(c, n, i, p, j, t, numa, 0u, minors);
 }
 
 /* DeviceShare's allocation for the pair under NUMA affinity `numa`: off views the node's devices; on a view
@@ -2383,7 +2393,7 @@ static uint32_t dev_eval_tab(const kg_config* c, const kg_node_columns* n, uint3
         }
     *raw = any ? dev_least(c, T, F, g.preq) : 0;
     uint32_t mask;
-    return dev_code_status(gpu_allocate(c, n, i, &t->total[0][0], &t->free[0][0], D, outside_used(n, i, t, D), &g, &mask));
+    return dev_code_status(gpu_allocate(c, n, i, &t->total[0][0], &t->free[0][0], D, outside_used(n, i, t, D), &g, 0u, &mask));
 }
 
 /* DeviceShare Filter of a GPU pod on a reservation view (deviceshare/plugin.go:397-419):
@@ -3299,7 +3309,9 @@ static uint32_t dev_choose_site_o(const kg_config* c, const kg_node_columns* n, 
     if (g.n == 0 || D <= 0) return 0;
     const uint32_t numa = (zone >= 0 && !zone_fails(zone)) ? numa_code_mask(zone) : 0u;
     uint32_t mask;
-    if (v && nom >= 0 && e->infos[nom].dev >= 0 && !gpu_alloc_tab_numa(c, n, i, p, j, &e->devs[e->infos[nom].dev], numa, &mask))
+    /* the reservation's reserved minors first (tryAllocateFromReusable's preferred set) */
+    if (v && nom >= 0 && e->infos[nom].dev >= 0 &&
+        !gpu_alloc_tab_numa_pref(c, n, i, p, j, &e->devs[e->infos[nom].dev], numa, e->infos[nom].dev_minors, &mask))
         return mask;
     const uint32_t code = gpu_alloc_tab_numa(c, n, i, p, j, (v && v->dev_base >= 0) ? &e->devs[v->dev_base] : NULL, numa, &mask);
     return code ? 0u : mask;
