@@ -155,6 +155,7 @@ def _run(case, device):
         specs = [{"cls": -1, "gpu": u["gpu"]}]
         cfg, T, resv, p = _build(case, specs)
         kc = cfg.kg_config()
+        kc.plugins &= ~abi.KG_PLUGIN_QUOTA
         t, rsv = _restore(T, resv)
         rec = abi.KgReserveRecord()
         rec.numa_zone, rec.rsv_rid, rec.gpu_minors = -1, -1, _mask(u["minors"])
