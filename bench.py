@@ -349,7 +349,7 @@ def cycle_rate(ctx, snap, pods_table, steps):
     n = batch.n
     batch.close()
     return {"ms_per_cycle": dt * 1e3, "evals_per_s": n * snap.n / dt, "pods": n, "nodes": snap.n,
-            "note": "kg_pods_upload + kg_eval_select + kg_result_keys per cycle, host buffers in pageable memory"}
+            "note": "kg_pods_upload (host columns copied into pinned staging, one async copy) + kg_eval_select + kg_result_keys per cycle"}
 
 
 def main():

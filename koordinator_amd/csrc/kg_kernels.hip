@@ -274,8 +274,13 @@ __device__ __forceinline__ uint64_t select1_loop(const NodeRec* __restrict__ nod
     return top;
 }
 
+// (round 6: amdgpu_waves_per_eu(8) -> 78 SGPRs, 8 instead of 6 workgroups per CU, measured no faster: 0.2238 / 0.2251
+// vs 0.2231 / 0.2217 ms per config-2 step; the loop is VALU-issue bound, not latency bound)
+#ifndef KG_SEL1_ATTR
+#define KG_SEL1_ATTR
+#endif
 template <uint32_t PM, int CLS>
-__global__ __launch_bounds__(256) void k_select1(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+__global__ __launch_bounds__(256) KG_SEL1_ATTR void k_select1(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                  PodsDev pods, uint32_t n_pods, uint32_t begin, uint32_t end,
                                                  uint32_t chunk, uint32_t index_base, KCfg cfg,
                                                  uint64_t* __restrict__ out, const uint32_t* __restrict__ order) {

@@ -193,6 +193,8 @@ struct kg_pods {
     // pod_layout(n) order; the PodsDev and list pointers below point into it for the current batch.
     uint8_t* d_in = nullptr;
     uint8_t* h_in = nullptr;  // pinned host staging of the same size
+    hipEvent_t in_copied = nullptr;  // the last upload's copy out of h_in (the next upload rewrites h_in after it)
+    bool in_pending = false;
     size_t in_bytes = 0;
     PodsDev dev{};
     uint32_t* d_order = nullptr;  // lanes of the base select: fast pods grouped by wave kind, then integer-path pods
@@ -1384,7 +1386,9 @@ kg_status kg_pods_create(kg_ctx* ctx, uint32_t capacity, kg_pods** out) {
               hipMalloc(&p->d_spec, sizeof(uint32_t) * (2 * (size_t)capacity + DEV_CLASSES + 1)) == hipSuccess &&
               hipMalloc(&p->d_pstat, sizeof(uint32_t) * capacity) == hipSuccess &&
               hipMalloc(&p->d_reason, sizeof(uint32_t) * (capacity + 1)) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&p->in_copied, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
+        if (p->in_copied) hipEventDestroy(p->in_copied);
         for (void* b : {(void*)p->d_in, (void*)p->d_keys, (void*)p->d_winners, (void*)p->d_step, (void*)p->d_qst,
                         (void*)p->d_dev_max, (void*)p->d_rsv_max, (void*)p->d_pref, (void*)p->d_minors, (void*)p->d_buckets,
                         (void*)p->d_aout, (void*)p->d_tkeys, (void*)p->d_spec, (void*)p->d_pstat, (void*)p->d_reason})
@@ -1424,8 +1428,12 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     // the side stream's plain-pod select of the previous batch reads d_in: it has to finish before the copy
     if (ctx->side) HIP_TRY(ctx, hipStreamSynchronize(ctx->side));
     if (ctx->side2) HIP_TRY(ctx, hipStreamSynchronize(ctx->side2));
-    // the previous upload's copy has completed (every upload ends with a stream synchronisation), so the
-    // pinned staging can be rewritten
+    // the previous upload's copy out of the pinned staging has completed before it is rewritten (the upload itself
+    // returns without waiting for its copy: the launches that read the batch follow it on the same stream)
+    if (p->in_pending) {
+        HIP_TRY(ctx, hipEventSynchronize(p->in_copied));
+        p->in_pending = false;
+    }
     const PodLayout L = pod_layout(n);
     uint8_t* h = p->h_in;
     int64_t* hc = reinterpret_cast<int64_t*>(h + L.cols);
@@ -1572,7 +1580,10 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             HIP_TRY(ctx, hipMemsetAsync(p->d_xcols + (size_t)c * n, xdef[c], sizeof(uint32_t) * n, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(p->d_dcls, DEV_CLASSES, n, ctx->stream));
     }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (bytes) {
+        HIP_TRY(ctx, hipEventRecord(p->in_copied, ctx->stream));
+        p->in_pending = true;
+    }
     // ---- commit
     p->n = n;
     p->n_fast = n_fast;
@@ -1605,6 +1616,7 @@ kg_status kg_pods_destroy(kg_pods* p) {
         hipFree(b);
     hipHostFree(p->h_in);
     hipHostFree(p->h_keys);
+    if (p->in_copied) hipEventDestroy(p->in_copied);
     hipFree(p->d_rbpart);
     hipFree(p->d_rbtops);
     if (p->rexec) hipGraphExecDestroy(p->rexec);
