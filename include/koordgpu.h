@@ -383,6 +383,15 @@ typedef struct kg_node_columns {
      * leaves follow from these counts. NULL: one pod per non-idle status (single -> 1 / 0, shared -> 0 / 1); when given,
      * the 2-bit statuses of numa_zone_status are derived from them. */
     const uint64_t* numa_zone_pods;
+    /* 1: a reservation on the node (matched by the pod or not) holds a NUMA or cpuset allocation (its reserve pod's
+     * resource status). NodeNUMAResource's RestoreReservation (nodenumaresource/reservation.go:188-262) gives such
+     * allocations back to the owners of a matched reservation and the double-counted owner usage of unmatched ones,
+     * in the hints (resource_manager.go:131-160), tryAllocateFromReusable / tryAllocateFromNode (plugin.go:428-439,
+     * 807-851) and the Reserve; the device does not follow that restore, so every pair on such a node where the
+     * plugin reads it (the pod binds CPUs there, or the merged NUMA policy is not None) is KG_ST_UNSUPPORTED and the
+     * sequential calls (kg_replay, kg_batch_schedule, kg_reserve, kg_assume*) refuse those pods (KG_UNSUPPORTED).
+     * NULL = none (ABI 12). */
+    const uint8_t* rsv_numa;
 } kg_node_columns;
 #define KG_GPU_NUMA_ANY 0xEu
 #define KG_GPU_NUMA_NONE 0xFu

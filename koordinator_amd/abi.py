@@ -206,6 +206,8 @@ class KgNodeColumns(C.Structure):
         ("dev_numa", _pu32),
         # cpuset pods per NUMA node in singleNUMANode (byte z) / sharedNode (byte KG_MAX_ZONES + z)
         ("numa_zone_pods", C.POINTER(C.c_uint64)),
+        # a reservation on the node holds a NUMA / cpuset allocation (the device does not follow its restore)
+        ("rsv_numa", C.POINTER(C.c_uint8)),
     ]
 
 
@@ -504,6 +506,9 @@ def node_columns(t: Table) -> KgNodeColumns:
     if "numa_zone_pods" in t:
         t["numa_zone_pods"] = np.ascontiguousarray(t["numa_zone_pods"], np.uint64)
         s.numa_zone_pods = t["numa_zone_pods"].ctypes.data_as(C.POINTER(C.c_uint64))
+    if "rsv_numa" in t:  # a reservation on the node holds a NUMA / cpuset allocation
+        t["rsv_numa"] = np.ascontiguousarray(t["rsv_numa"], np.uint8)
+        s.rsv_numa = t["rsv_numa"].ctypes.data_as(C.POINTER(C.c_uint8))
     if "gpu_parts" in t and len(t["gpu_parts"]):
         t["gpu_parts"] = np.ascontiguousarray(t["gpu_parts"], GPU_PARTITION_DTYPE)
         s.gpu_parts = t["gpu_parts"].ctypes.data

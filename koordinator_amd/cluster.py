@@ -599,22 +599,31 @@ class ClusterState:
         allocatable."""
         md, status = _md(r), r.get("status") or {}
         alloc = {k: v for k, v in (status.get("allocatable") or {}).items() if k != "pods"}
-        return {"metadata": {"uid": "reserve-pod/" + md.get("uid", ""), "name": md.get("name", "")},
+        # the reservation's annotations travel with it (its resource status: the cpuset / NUMA resources it holds)
+        return {"metadata": {"uid": "reserve-pod/" + md.get("uid", ""), "name": md.get("name", ""),
+                             "annotations": dict(md.get("annotations") or {})},
                 "spec": {"nodeName": status.get("nodeName", ""), "containers": [{"resources": {"requests": alloc}}]}}
 
     def on_reservation(self, r: dict):
         """Reservation add / update: the reservation cache (updateReservation) and its reserve pod in NodeInfo
-        while it is Available on a node."""
+        while it is Available on a node; the NUMA resource manager takes the reserve pod's resource status like a
+        pod's (NewReservationToPodEventHandler, nodenumaresource/pod_eventhandler.go:47-49)."""
         self.reservations.update_reservation(r)
         rp = self._reserve_pod(r)
         if (r.get("status") or {}).get("phase") == "Available" and _node_name(rp):
             self._nodeinfo_update(rp)
+            self._numa_update(None, rp)
         else:
             self._nodeinfo_remove(_uid(rp))
+            if _node_name(rp):
+                self._numa_release(_node_name(rp), _uid(rp))
 
     def on_reservation_delete(self, r: dict):
         self.reservations.delete_reservation(r)
-        self._nodeinfo_remove(_uid(self._reserve_pod(r)))
+        rp = self._reserve_pod(r)
+        self._nodeinfo_remove(_uid(rp))
+        if _node_name(rp):
+            self._numa_release(_node_name(rp), _uid(rp))
 
     def reservation_restore(self, pods: Sequence[dict], rows: Optional[abi.Table] = None):
         """The Reservation transformer's restore for a pending batch: owner-match classes of the pods over the
@@ -723,6 +732,8 @@ class ClusterState:
         row.update(zone_used_cols(used, cpuset_milli))
         row["numa_zone_status"] = self.numa[i].zone_status(len(t.zones)) if t.cpu_zone else 0
         row["numa_zone_pods"] = self.numa[i].zone_pods(len(t.zones)) if t.cpu_zone else 0
+        # a reservation's reserve pod holds a NUMA / cpuset allocation here (kg_node_columns.rsv_numa)
+        row["rsv_numa"] = int(any(uid.startswith("reserve-pod/") for uid in self.numa[i].pods))
         row["dev_minors"], row["dev_total"], row["dev_free"] = self.devices.columns(name)
         return row
 
@@ -730,6 +741,7 @@ class ClusterState:
         rows = range(len(self.nodes)) if rows is None else list(rows)
         t = abi.empty_nodes(len(rows))
         t["numa_zone_pods"] = np.zeros(len(rows), np.uint64)
+        t["rsv_numa"] = np.zeros(len(rows), np.uint8)
         for k, i in enumerate(rows):
             for key, v in self.row(int(i)).items():
                 t[key][k] = v

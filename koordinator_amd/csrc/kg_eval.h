@@ -735,6 +735,10 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             o.status |= KG_ST_NUMA_CPU_BIND;  // ErrCPUBindPolicyConflict / ErrSMTAlignmentError
             return;
         }
+        if (flags & F_RSV_NUMA) {  // below: the restore of NUMA / cpuset-holding reservations (rsv_numa_unsupported)
+            o.status |= KG_ST_UNSUPPORTED;
+            return;
+        }
         // allocateCPUSet over the whole node: the required policy's CPUs (filterCPUsByRequiredCPUBindPolicy) or the
         // available ones must cover the pod; takeCPUs then always succeeds on them and satisfies the policy
         const int64_t have = required == KG_CPU_BIND_FULL_PCPUS    ? zr->cpu_free_full
@@ -753,6 +757,14 @@ __device__ __forceinline__ void numa_eval(const KCfg& c, const int64_t* __restri
             // no Filter check: the Reserve fails (ErrNotEnoughCPUs)
             if constexpr (ZONE) o.zone = ZONE_CPUSET_FAIL;
         }
+    }
+    // reservations on the node hold NUMA / cpuset allocations: RestoreReservation (nodenumaresource/reservation.go
+    // :188-262) gives them back to the pod (matched) or returns the owners' double-counted usage (unmatched) on every
+    // path that reads them from here on (hints, tryAllocateFromReusable / FromNode, the Reserve); the device does not
+    // follow it (kg_node_columns.rsv_numa)
+    if ((flags & F_RSV_NUMA) && pol != KG_NUMA_NONE) {
+        o.status |= KG_ST_UNSUPPORTED;
+        return;
     }
     // a cpuset-binding pod under a NUMA policy: its cpu request amplified where the options' requests count (hint and
     // node scores, getResourceOptions plugin.go:774-778), the node's cpuset CPUs amplified as the Score's requested

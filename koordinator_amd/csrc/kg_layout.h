@@ -102,6 +102,8 @@ enum : uint32_t {
                                // manager (window replay takes the integer path for the Reserve's zone)
     F_VBIG = 1u << 20,         // F_BIG for a value outside the fast path (not only for the node's policies): the fast
                                // block's NodeResourcesFit / LoadAware part is exact unless this is set (derived)
+    F_RSV_NUMA = 1u << 21,     // a reservation on the node holds a NUMA / cpuset allocation (kg_node_columns.rsv_numa):
+                               // pairs whose NodeNUMAResource reads its restore are KG_ST_UNSUPPORTED
     F_DERIVED_MASK = F_PODS_FULL | F_BIG | F_VBIG,
 };
 enum : uint32_t { FMODE_CHECK = 0, FMODE_PASS = 1, FMODE_FAIL_EXPIRED = 2 };
@@ -308,6 +310,8 @@ KG_HD inline void derive_node(NodeRec& r, ZoneRec& z) {
     big = big || pol0 == 2u /* KG_NUMA_RESTRICTED */;
     // a node CPU bind policy makes every pod with a cpu request bind cpusets there (util.go:121-138)
     big = big || ((z.cpu_meta >> CPU_META_BIND_SHIFT) & 3u) != 0u;
+    // a NUMA policy on a node whose reservations hold NUMA / cpuset allocations: the integer path reports the pairs
+    big = big || ((f & F_RSV_NUMA) && pol0 != 0u /* KG_NUMA_NONE */);
     if (big) f |= F_BIG;
     v[N_FLAGS] = (int64_t)(((uint64_t)v[N_FLAGS] & 0xFFFFFFFF00000000ull) | f);
     auto fit = [](int64_t x) { return kg_bits(x100(x < 0 ? 0 : x)); };

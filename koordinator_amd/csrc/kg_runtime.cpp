@@ -195,6 +195,7 @@ struct kg_pods {
     uint8_t* h_in = nullptr;  // pinned host staging of the same size
     hipEvent_t in_copied = nullptr;  // the last upload's copy out of h_in (the next upload rewrites h_in after it)
     bool in_pending = false;
+    uint32_t defaults_n = 0;  // the config-5 regions hold the absent-column defaults for a batch of this size (0: no)
     size_t in_bytes = 0;
     PodsDev dev{};
     uint32_t* d_order = nullptr;  // lanes of the base select: fast pods grouped by wave kind, then integer-path pods
@@ -482,6 +483,7 @@ kg_status build_row(kg_ctx* ctx, const kg_config& c, const kg_node_columns* s, u
     f |= pol << F_NUMA_POLICY_SHIFT;
     f |= Z << F_NUMA_ZONES_SHIFT;
     if (pol == KG_NUMA_BEST_EFFORT) f |= F_TOPO;  // the Reserve runs the topology manager (window replay: integer path)
+    if (s->rsv_numa && s->rsv_numa[i]) f |= F_RSV_NUMA;
     const double ratio = s->cpu_amp_ratio ? s->cpu_amp_ratio[i] : 0.0;
     if (ratio > 1) f |= F_AMP;
     v[N_FLAGS] = f;
@@ -1572,7 +1574,9 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
     const bool ext_copy = ext_cols || any_rsv_req;
     const size_t bytes = n ? (ext_copy ? L.total : L.ext) : 0;
     if (bytes) HIP_TRY(ctx, hipMemcpyAsync(p->d_in, h, bytes, hipMemcpyHostToDevice, ctx->stream));
-    if (n && !ext_copy) {
+    // absent config-5 columns: their defaults, unless the previous batch of the same size left them there (nothing else
+    // writes those regions)
+    if (n && !ext_copy && p->defaults_n != n) {
         HIP_TRY(ctx, hipMemsetAsync(p->d_dev_req, 0, sizeof(int64_t) * DEV_R * n, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(const_cast<int64_t*>(p->dev.dev_bw), 0, sizeof(int64_t) * n, ctx->stream));
         const int xdef[7] = {0, 0, 0xFF, 0, 0xFF, 0, 0};  // -1 quota / class
@@ -1580,6 +1584,7 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
             HIP_TRY(ctx, hipMemsetAsync(p->d_xcols + (size_t)c * n, xdef[c], sizeof(uint32_t) * n, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(p->d_dcls, DEV_CLASSES, n, ctx->stream));
     }
+    p->defaults_n = ext_copy ? 0u : n;
     if (bytes) {
         HIP_TRY(ctx, hipEventRecord(p->in_copied, ctx->stream));
         p->in_pending = true;
@@ -2280,6 +2285,31 @@ bool cpuset_bound(const kg_snap* s, const kg_pods* p, uint32_t pod, uint32_t nod
     return z.cpu_topo >= 0 && ((p->h_flags[pod] & KG_POD_CPU_BIND) || (node_bind && p->h_req_cpu[pod] != 0));
 }
 
+// NodeNUMAResource of pod `pod` on `node` reads the restore of reservations holding NUMA / cpuset allocations there
+// (kg_node_columns.rsv_numa, nodenumaresource/reservation.go:188-262), which the device does not follow: the pod binds
+// CPUs there or its merged NUMA policy is not None (the pairs the select reports KG_ST_UNSUPPORTED)
+bool rsv_numa_pair(const kg_snap* s, const kg_pods* p, uint32_t pod, uint32_t node) {
+    if (!(s->kcfg.plugins & KG_PLUGIN_NUMA) || node >= s->n || pod >= p->h_flags.size()) return false;
+    const uint32_t f = (uint32_t)s->h_nodes[s->pos[node]].v[N_FLAGS];
+    if (!(f & F_RSV_NUMA) || (p->h_flags[pod] & KG_POD_NUMA_SKIP)) return false;
+    const uint32_t node_pol = (f >> F_NUMA_POLICY_SHIFT) & 15u, pod_pol = (p->h_flags[pod] >> 16) & 15u;
+    return node_pol != KG_NUMA_NONE || pod_pol != KG_NUMA_NONE || cpuset_bound(s, p, pod, node);
+}
+
+// some pod of the batch may meet such a pair in a sequential call (kg_replay): it refuses the batch
+bool rsv_numa_batch(const kg_snap* s, const kg_pods* p) {
+    if (!(s->kcfg.plugins & KG_PLUGIN_NUMA)) return false;
+    bool any = false;
+    for (uint32_t r = 0; r < s->n; r++) {
+        const uint32_t f = (uint32_t)s->h_nodes[r].v[N_FLAGS];
+        if (!(f & F_RSV_NUMA)) continue;
+        any = true;
+        if (((f >> F_NUMA_POLICY_SHIFT) & 15u) != KG_NUMA_NONE) return true;
+        if (r < s->h_zones.size() && ((s->h_zones[r].cpu_meta >> CPU_META_BIND_SHIFT) & 3u) != 0u) return true;
+    }
+    return any && (p->pod_policy || p->any_cpu_bind);
+}
+
 // cpuset Reserves happen in this (snapshot, batch): the replay runs the device accumulator between steps
 bool cpuset_active(const kg_snap* s, const kg_pods* p) {
     return s->has_cpu && (s->kcfg.plugins & KG_PLUGIN_NUMA) && (p->any_cpu_bind || s->node_bind);
@@ -2514,6 +2544,9 @@ kg_status kg_replay(kg_snap* s, kg_pods* p, int32_t* out_node, int64_t* out_tota
     std::lock_guard<std::mutex> g(ctx->mu);
     st = check_views(s);
     if (st != KG_OK) return st;
+    if (rsv_numa_batch(s, p))
+        return fail(ctx, KG_UNSUPPORTED, "replay over nodes whose reservations hold NUMA / cpuset allocations "
+                                         "(kg_node_columns.rsv_numa) with pods that bind CPUs or a NUMA policy");
     if (s->ext()) return ext_replay(s, p, out_node, out_total, out_reason);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint32_t n = p->n;
@@ -2572,6 +2605,8 @@ static kg_status assume_impl(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node
     kg_ctx* ctx = s->ctx;
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
+    if (rsv_numa_pair(s, p, pod, node))
+        return fail(ctx, KG_UNSUPPORTED, "pod %u on node %u: NUMA / cpuset restore of its reservations", pod, node);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     if (out_split && !p->d_split) HIP_TRY(ctx, hipMalloc(&p->d_split, sizeof(int64_t) * 2 * KG_MAX_ZONES));
     touch_views(s, node);
@@ -2729,6 +2764,8 @@ static kg_status assume_ext(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node,
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
     st = check_ext(s);
     if (st != KG_OK) return st;
+    if (sign > 0 && rsv_numa_pair(s, p, pod, node))
+        return fail(ctx, KG_UNSUPPORTED, "pod %u on node %u: NUMA / cpuset restore of its reservations", pod, node);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     // a Reserve follows Reservation.Reserve on the device's views (k_ext_assume, rsv_reserve_dev) unless a reservation
     // holds GPUs; an Unreserve does not know the reservation: the node's views are stale then
@@ -2778,6 +2815,8 @@ kg_status kg_reserve(kg_snap* s, kg_pods* p, uint32_t pod, uint32_t node, kg_res
     if (!out) return fail(ctx, KG_INVALID_ARG, "null record");
     std::lock_guard<std::mutex> g(ctx->mu);
     if (pod >= p->n || node >= s->n) return fail(ctx, KG_INVALID_ARG, "pod %u / node %u out of range", pod, node);
+    if (rsv_numa_pair(s, p, pod, node))
+        return fail(ctx, KG_UNSUPPORTED, "pod %u on node %u: NUMA / cpuset restore of its reservations", pod, node);
     if (s->ext()) {
         st = check_ext(s);
         if (st != KG_OK) return st;

@@ -1114,6 +1114,14 @@ def reservation_restore(nodes: abi.Table, reservations: Sequence[dict]):
     columns' dev_free then give back what pods use inside unmatched reservations, and `devs` holds the
     (total, free) tables views (dev_base) and matched reservations (dev) allocate from (dev_reusable)."""
     out = {k: np.array(v, copy=True) for k, v in nodes.items()}
+    # a reservation whose reserve pod holds a NUMA / cpuset allocation (`numa_held`): NodeNUMAResource's own restore
+    # (nodenumaresource/reservation.go:188-262) is not restated; the node is marked for the engine (rsv_numa)
+    held = sorted({int(r["node"]) for r in reservations if r.get("numa_held")})
+    if held or "rsv_numa" in out:
+        n_rows = len(next(iter(nodes.values())))
+        rn = np.array(out["rsv_numa"], np.uint8, copy=True) if "rsv_numa" in out else np.zeros(n_rows, np.uint8)
+        rn[held] = 1
+        out["rsv_numa"] = rn
     req_cols = ["req_cpu", "req_mem", "req_eph", "sc_req0", "sc_req1"]
     by_node: Dict[int, List[int]] = {}
     for x, r in enumerate(reservations):

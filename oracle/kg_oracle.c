@@ -713,6 +713,9 @@ static uint32_t cpuset_filter(const kg_node_columns* n, uint32_t i, const kg_pod
     const int64_t needed = p->req_cpu[j] / 1000;
     if (required == KG_CPU_BIND_FULL_PCPUS && needed % (t->n_cpus / t->n_cores) != 0)
         return KG_ST_NUMA_CPU_BIND; /* ErrSMTAlignmentError */
+    /* the allocation from here on reads the restore of NUMA / cpuset-holding reservations (plugin.go:428-439,
+     * reservation.go:188-262): not restated (kg_node_columns.rsv_numa) */
+    if (n->rsv_numa && n->rsv_numa[i]) return KG_ST_UNSUPPORTED;
     if (policy != KG_NUMA_NONE) return 0;
     uint64_t out[4];
     if (required != KG_CPU_BIND_NONE) {
@@ -798,6 +801,9 @@ static uint32_t numa_eval(const kg_config* c, const kg_node_columns* n, uint32_t
         const uint32_t st = cpuset_filter(n, i, p, j, policy, node_bind, zone_out);
         if (st) return st;
     }
+    /* a NUMA policy on a node whose reservations hold NUMA / cpuset allocations: the hints and allocations read their
+     * restore (resource_manager.go:131-160), not restated */
+    if (policy != KG_NUMA_NONE && n->rsv_numa && n->rsv_numa[i]) return KG_ST_UNSUPPORTED;
     if (policy == KG_NUMA_NONE) {
         /* scoreWithAmplifiedCPUs, scoring.go:132-151 */
         int64_t req_cpu = N_REQ_CPU(n, i, ov);
@@ -1213,6 +1219,7 @@ struct kgo_state {
     uint32_t n_cpu_topos;
     kg_cpu_alloc* cpu_alloc;
     uint8_t *cpu_max_ref, *cpu_bind, *cpu_strategy;
+    uint8_t* rsv_numa; /* a reservation on the node holds a NUMA / cpuset allocation (static; NULL = none) */
 };
 
 static int64_t* dup64(const int64_t* s, uint32_t n) {
@@ -1288,6 +1295,10 @@ kgo_state* kgo_state_new(const kg_node_columns* s, uint32_t n) {
     st->zone_status = (uint32_t*)calloc(n ? n : 1, 4);
     if (s->numa_zone_status) memcpy(st->zone_status, s->numa_zone_status, 4 * (size_t)n);
     st->zone_pods = (uint64_t*)calloc(n ? n : 1, 8);
+    if (s->rsv_numa) {
+        st->rsv_numa = (uint8_t*)calloc(n ? n : 1, 1);
+        memcpy(st->rsv_numa, s->rsv_numa, n);
+    }
     for (uint32_t i = 0; i < n; i++) {
         if (s->numa_zone_pods) {
             st->zone_pods[i] = s->numa_zone_pods[i];
@@ -1363,6 +1374,7 @@ void kgo_state_free(kgo_state* st) {
     free(st->dev_topo);
     free(st->dev_part);
     free(st->dev_numa);
+    free(st->rsv_numa);
     free(st->gpu_parts);
     free(st->dev_total);
     free(st->dev_free);
@@ -1420,6 +1432,7 @@ void kgo_state_view(kgo_state* st, kg_node_columns* v) {
     v->dev_topo = st->dev_topo;
     v->dev_part = st->dev_part;
     v->dev_numa = st->dev_numa;
+    v->rsv_numa = st->rsv_numa;
     v->gpu_parts = st->gpu_parts;
     v->n_gpu_parts = st->n_gpu_parts;
     v->cpu_topo = st->cpu_topo;

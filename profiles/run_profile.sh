@@ -30,7 +30,7 @@ cd "$R" || exit 1
 if [ "$CFG" = "4" ]; then  # top-3: per-chunk partials merged by k_merge_list inside the bracket
     python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_select<" "k_select1<" "k_big_sel" "k_merge" || exit $?
 elif [ "$CFG" = "5" ]; then
-    python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_ext_select" "k_ext_stats" "k_ext_fix_rows" "k_dev_sum" \
+    python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_ext_select" "k_ext_stats" "k_ext_fix_rows" "k_dev_sum" "k_gpu_zone_sum" \
         "k_rdev_codes" "k_ext_gate" "k_special_scan" "k_scatter_keys" "k_select<" "k_select1<" "k_big_sel" || exit $?
 elif [ "$CFG" = "6" ]; then  # mixed cluster: fast lanes, pruned F_BIG pairs, pruned integer (LSR) lanes
     python3 tools/pmc_summary.py "$OUT" "$OUT/summary.json" "k_select<" "k_select1<" "k_big_init" "k_big_sel" \

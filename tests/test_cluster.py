@@ -408,6 +408,7 @@ class World:
     def reference_table(self):
         t = abi.empty_nodes(len(self.nodes))
         t["numa_zone_pods"] = np.zeros(len(self.nodes), np.uint64)  # no cpuset pods in this world
+        t["rsv_numa"] = np.zeros(len(self.nodes), np.uint8)  # no reservation holds NUMA resources in this world
         for i, node in enumerate(self.nodes):
             name = self.names[i]
             pods = [p for p in self.pods.values() if p["spec"].get("nodeName") == name]
