@@ -102,9 +102,17 @@ def test_device_marks_the_same_pairs_and_sequential_calls_refuse():
             assert np.array_equal(getattr(got, name), getattr(want, name)), name
         keys = engine.eval_select(snap, batch, 1)
         assert np.array_equal(keys, oracle_lib.select(kc, marked, pods, 1))
+        # a pod is flagged when an unsupported pair could change its selection: the select may skip a pair whose best
+        # possible total (NodeResourcesFit and LoadAware scores + the NUMA weight x 100: the restore changes only the
+        # NUMA part) cannot beat the pod's key (k_big_sel), so the unflagged pods' keys are exact
         flagged = (engine.result_status(batch) & abi.KG_ST_UNSUPPORTED) != 0
-        unsup_pod = ((want.status & abi.KG_ST_UNSUPPORTED) != 0).any(axis=1)
-        assert np.array_equal(flagged, unsup_pod)
+        unsup = (want.status & abi.KG_ST_UNSUPPORTED) != 0
+        assert not (flagged & ~unsup.any(axis=1)).any()
+        assert flagged.sum() >= 5
+        bound = kc.weight_nrf * want.score_nrf + kc.weight_la * want.score_la + kc.weight_numa * 100
+        for j in np.nonzero(unsup.any(axis=1) & ~flagged)[0]:
+            for i in np.nonzero(unsup[j])[0]:
+                assert int(abi.make_key(int(bound[j, i]), int(i))) < int(keys[j, 0]), (j, i)
         with pytest.raises(engine.Unsupported):
             engine.replay(snap, batch)
         aff = _affected(marked, pods)
