@@ -424,13 +424,14 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
     const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
     uint32_t dmax = 0, rmax = 0;
     uint64_t pk = PREF_NONE;
-    uint64_t* const xrow = (e.xpairs && live) ? e.xpairs + (size_t)j * e.xT : nullptr;
+    const uint32_t xp = (e.xpairs && live) ? (e.xpos ? e.xpos[j] : j) : 0xFFFFFFFFu;
+    uint64_t* const xcol = xp < e.xn ? e.xpairs + xp : nullptr;  // position u at xcol[u * xn]
     for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split,
                         [&](uint32_t rec, uint32_t u) {
         // the whole pair (the select pass reads it back instead of evaluating it again)
         const PairX r = eval_pair_ext<false, false, true>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
                                                           dcls);
-        if (xrow && u < e.xT) xrow[u] = xpair_pack(cfg, r);
+        if (xcol && u < e.xT) xcol[(size_t)u * e.xn] = xpair_pack(cfg, r);
         if (r.status) return;
         dmax = max(dmax, (uint32_t)r.s_dev);
         rmax = max(rmax, (uint32_t)r.s_rsv);
@@ -495,13 +496,14 @@ __global__ __launch_bounds__(256) void k_ext_stats_views(const NodeRec* __restri
     const uint32_t cb = e.cls_begin[px.cls], ce = e.cls_begin[px.cls + 1];
     const uint32_t vb = cb + blockIdx.y * chunk, ve = min(ce, vb + chunk);
     // stored pairs: position = the special list's length + the view's rank in its class (for_general_records)
-    uint64_t* const xrow = (e.xpairs && e.xsp) ? e.xpairs + (size_t)j * e.xT : nullptr;
-    const uint32_t nsp = xrow ? e.xsp[0] : 0u;
+    const uint32_t xp = (e.xpairs && e.xsp) ? (e.xpos ? e.xpos[j] : j) : 0xFFFFFFFFu;
+    uint64_t* const xcol = xp < e.xn ? e.xpairs + xp : nullptr;  // position u at xcol[u * xn]
+    const uint32_t nsp = xcol ? e.xsp[0] : 0u;
     for (uint32_t v = vb; v < ve; v++) {
         const uint32_t rec = e.views[v].rec;
         const PairX r = eval_pair_ext<EXACT, TOPO, true>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
                                          pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES);
-        if (xrow && nsp + (v - cb) < e.xT) xrow[nsp + (v - cb)] = xpair_pack(cfg, r);
+        if (xcol && nsp + (v - cb) < e.xT) xcol[(size_t)(nsp + (v - cb)) * e.xn] = xpair_pack(cfg, r);
         if (r.status) continue;
         rmax = max(rmax, (uint32_t)r.s_rsv);
         if (r.order != 0) {
@@ -672,12 +674,13 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
     uint32_t unsup = 0;
     // the statistics pass stored this pod's pairs: a GPU pod's every general pair, a class pod's views (positions from
     // the special list's length on); a pod its quota gate rejected was not evaluated there
-    const bool xs = e.xpairs && live && q == 0u, xs_all = xs && px.dcount > 0;
-    const uint64_t* const xrow = xs ? e.xpairs + (size_t)jj * e.xT : nullptr;
+    const uint32_t xp = (e.xpairs && live && q == 0u) ? (e.xpos ? e.xpos[jj] : jj) : 0xFFFFFFFFu;
+    const bool xs = xp < e.xn, xs_all = xs && px.dcount > 0;
+    const uint64_t* const xcol = xs ? e.xpairs + xp : nullptr;  // position u at xcol[u * xn]
     const uint32_t nsp = special[0];
     for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split,
                         [&](uint32_t rec, uint32_t u) {
-        const uint64_t x = (xrow && u < e.xT && (xs_all || u >= nsp)) ? xrow[u] : XPAIR_LIVE;
+        const uint64_t x = (xcol && u < e.xT && (xs_all || u >= nsp)) ? xcol[(size_t)u * e.xn] : XPAIR_LIVE;
         const uint32_t g = index_base + node_index(nodes[rec]);
         uint64_t key = 0;
         if (x >> 63) {

@@ -544,9 +544,13 @@ struct ExtDev {
     GpuRawRsv* grsv;
     // fast-base config-5 batch: the general pairs' selection inputs, stored by the statistics pass
     // (k_ext_stats_sp: a GPU pod's every general pair; k_ext_stats_views: a class pod's views) for the select pass
-    // (k_ext_select_sp), [pod][xT] by the pair's position in for_general_records (XPAIR_*); nullptr = none
+    // (k_ext_select_sp), [position][xpos[pod]] (position: the pair's rank in for_general_records, < xT; xpos: the pod's
+    // lane in the select pass's list, xn lanes; nullptr = the pod's batch index): neighbouring lanes of both passes
+    // store and load neighbouring words
+    // (XPAIR_*); nullptr = none
     uint64_t* xpairs;
-    uint32_t xT;
+    uint32_t xT, xn;
+    const uint32_t* xpos;
     const uint32_t* xsp;  // the special list the positions count from (k_special_scan)
 };
 

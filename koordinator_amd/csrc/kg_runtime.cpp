@@ -202,6 +202,7 @@ struct kg_pods {
     uint32_t n_fast = 0;          // pods in the float64 fast domain (the leading d_order entries)
     uint32_t* d_pmap = nullptr;   // config-5 "plain" pods (batch positions) grouped by wave kind
     uint32_t* d_xlist = nullptr;  // config-5 pods through k_ext_select (batch positions)
+    uint32_t* d_xpos = nullptr;   // per pod its lane in d_xlist (~0 = a plain pod): the stored pairs' column
     uint32_t* d_stat_list = nullptr;  // pods carrying a GPU request or a reservation class
     int64_t* d_dev_req = nullptr;     // [n][KG_DEV_R]
     uint32_t* d_xcols = nullptr;      // dev_count, dev_keys, quota (int32), quota_keys, rsv_class (int32), dev_flags, dev_tmpl: 7 x n
@@ -1295,7 +1296,7 @@ namespace {
 // first; the config-5 regions after `ext` are copied only when the batch carries config-5 data (else they
 // are set on the device). The layout depends on n only, so cached replay graphs keyed on n stay valid.
 struct PodLayout {
-    size_t cols, flags, order, pmap, ext, xlist, stat, dev_req, dev_bw, xcols, dclass, dcls, total;
+    size_t cols, flags, order, pmap, ext, xlist, xpos, stat, dev_req, dev_bw, xcols, dclass, dcls, total;
 };
 
 PodLayout pod_layout(uint32_t n) {
@@ -1312,6 +1313,7 @@ PodLayout pod_layout(uint32_t n) {
     L.pmap = take(sizeof(uint32_t) * (size_t)n);
     L.ext = o;
     L.xlist = take(sizeof(uint32_t) * (size_t)n);
+    L.xpos = take(sizeof(uint32_t) * (size_t)n);
     L.stat = take(sizeof(uint32_t) * (size_t)n);
     L.dev_req = take(sizeof(int64_t) * DEV_R * (size_t)n);
     L.dev_bw = take(sizeof(int64_t) * (size_t)n);
@@ -1341,6 +1343,7 @@ void pod_views(kg_pods* p, uint32_t n) {
     p->d_order = reinterpret_cast<uint32_t*>(d + L.order);
     p->d_pmap = reinterpret_cast<uint32_t*>(d + L.pmap);
     p->d_xlist = reinterpret_cast<uint32_t*>(d + L.xlist);
+    p->d_xpos = reinterpret_cast<uint32_t*>(d + L.xpos);
     p->d_stat_list = reinterpret_cast<uint32_t*>(d + L.stat);
     p->d_dev_req = reinterpret_cast<int64_t*>(d + L.dev_req);
     p->d_xcols = reinterpret_cast<uint32_t*>(d + L.xcols);
@@ -1558,6 +1561,9 @@ kg_status kg_pods_upload(kg_pods* p, const kg_pod_columns* cols, uint32_t n) {
         auto by_kind = [&](uint32_t a, uint32_t b) { return kind(a) < kind(b); };
         std::stable_sort(stat, stat + ns, by_kind);
         std::stable_sort(xlist, xlist + nx, by_kind);
+        uint32_t* xpos = reinterpret_cast<uint32_t*>(h + L.xpos);
+        std::memset(xpos, 0xFF, sizeof(uint32_t) * n);
+        for (uint32_t k = 0; k < nx; k++) xpos[xlist[k]] = k;
         // plain lanes grouped by wave kind (stable buckets)
         std::vector<uint32_t> by;
         by.reserve(np);
@@ -1882,6 +1888,12 @@ static const SideLane* side_lane2(kg_ctx* ctx, SideLane& l) {
     return (l.s && l.fork && l.join) ? &l : nullptr;
 }
 
+// config-5 select: plain pods (no GPU request, no reservation class or affinity) take the base select by lane list
+// and the others k_ext_select by d_xlist (ext_select_local)
+static bool ext_split(const kg_snap* s, const kg_pods* p) {
+    return !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok && !need_topo(s, p);
+}
+
 static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
     kg_ctx* ctx = s->ctx;
     ExtDev e = s->ext_dev();
@@ -1897,9 +1909,12 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
     }
     p->xT = 0;
     if (ext_fast_base(s, p) && (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) && !std::getenv("KG_NO_XPAIRS")) {
-        // the general pairs' selection inputs, stored for the select pass: [pod][special list + largest class's views]
+        // the general pairs' selection inputs, stored for the select pass: [special list + largest class's views][the
+        // select pass's lane]
         const uint32_t T = special_est(s, p) + s->max_cls_views + 64;
-        const size_t need = (size_t)p->n * T;
+        const bool split = ext_split(s, p);
+        const uint32_t xn = split ? p->n_x : p->n;
+        const size_t need = (size_t)xn * T;
         if (need * sizeof(uint64_t) <= ((size_t)4 << 30)) {
             if (p->xpairs_cap < need) {
                 HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1918,6 +1933,8 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
                 p->xT = T;
                 e.xpairs = p->d_xpairs;
                 e.xT = T;
+                e.xn = xn;
+                e.xpos = split ? p->d_xpos : nullptr;
                 e.xsp = s->d_special;
             }
         }
@@ -2045,8 +2062,7 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
                                   bool plain_on_side = false) {
     kg_ctx* ctx = s->ctx;
     SideLane lane2{};
-    const bool split = !ext_split_off() && !force_exact() && !force_int() && s->weights_small && p->fast_ok &&
-                       !need_topo(s, p);
+    const bool split = ext_split(s, p);
     const uint32_t n_x = split ? p->n_x : p->n;
     const uint32_t* xl = split ? p->d_xlist : nullptr;
     const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(n_x, 1), 8192);
@@ -2079,6 +2095,8 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     if (fb && p->xT) {  // the general pairs ext_stats_local stored for this batch
         xe.xpairs = p->d_xpairs;
         xe.xT = p->xT;
+        xe.xn = n_x;
+        xe.xpos = xl ? p->d_xpos : nullptr;
         xe.xsp = s->d_special;
     }
     p->xT = 0;
