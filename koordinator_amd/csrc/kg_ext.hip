@@ -327,13 +327,18 @@ __global__ __launch_bounds__(256) void k_ext_stats(const NodeRec* __restrict__ n
     if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
 }
 
+// The kernels around the whole evaluator (eval_pair_ext) need the full 256 VGPRs; its one accumulation register took
+// them to one wave per SIMD, with every dependent load chain of the evaluator (views -> infos -> restore tables)
+// exposed. Two waves per SIMD keep every register and hide half of that latency.
+#define KG_EVAL_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+
 // The records a fast-base pass leaves to the general path for lane t: the special records (F_BIG, and class
 // 1 unless c1_split; grid-stride over chunks of `chunk`) for every lane, then the views of the lane's reservation
-// class that are not in the special list. fn(rec) evaluates one pair.
+// class that are not in the special list, positions below lim. fn(rec, position) evaluates one pair.
 template <typename Fn>
 __device__ __forceinline__ void for_general_records(const NodeRec* __restrict__ nodes, const ExtDev& e,
                                                     const uint32_t* __restrict__ special, uint32_t n0, uint32_t chunk,
-                                                    int32_t cls, bool c1_split, Fn&& fn) {
+                                                    uint32_t by, int32_t cls, bool c1_split, uint32_t lim, Fn&& fn) {
     // one iteration space (the special list, then the class's views) and one call site of fn: with two, the
     // compiler outlined the evaluation lambda (an out-of-line call, its state through scratch memory)
     const uint32_t nsp = special[0], step = gridDim.y * chunk;
@@ -342,8 +347,8 @@ __device__ __forceinline__ void for_general_records(const NodeRec* __restrict__ 
         cb = e.cls_begin[cls];
         ce = e.cls_begin[cls + 1];
     }
-    const uint32_t total = nsp + (ce - cb);
-    for (uint32_t x = blockIdx.y * chunk; x < total; x += step)
+    const uint32_t total = min(nsp + (ce - cb), lim);  // lim: the lane's positions end there
+    for (uint32_t x = by * chunk; x < total; x += step)
         for (uint32_t u = x, ue = min(x + chunk, total); u < ue; u++) {
             uint32_t rec;
             if (u < nsp) {
@@ -358,9 +363,9 @@ __device__ __forceinline__ void for_general_records(const NodeRec* __restrict__ 
 
 // The class-1 records of a split fast-base pass (k_special_scan's c1 list) for lane t, grid-stride over chunks.
 template <typename Fn>
-__device__ __forceinline__ void for_c1_records(const uint32_t* __restrict__ c1, uint32_t chunk, Fn&& fn) {
+__device__ __forceinline__ void for_c1_records(const uint32_t* __restrict__ c1, uint32_t chunk, uint32_t by, Fn&& fn) {
     const uint32_t nc = c1[0], step = gridDim.y * chunk;
-    for (uint32_t x = blockIdx.y * chunk; x < nc; x += step)
+    for (uint32_t x = by * chunk; x < nc; x += step)
         for (uint32_t y = x, ye = min(x + chunk, nc); y < ye; y++) fn(c1[1 + y]);
 }
 
@@ -415,7 +420,10 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
                                                       uint32_t* __restrict__ dev_max, uint32_t* __restrict__ rsv_max,
                                                       uint64_t* __restrict__ pref, const uint32_t* __restrict__ special,
                                                       bool c1_split) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    // launch order (not xcd_block): its work sits in the few pod blocks of the class pods, and whole chunks per XCD
+    // measured slower (1.58 vs 1.13 ms on config 5)
+    const GridBlock b{blockIdx.x, blockIdx.y};
+    const uint32_t t = b.x * blockDim.x + threadIdx.x;
     const bool live = t < n_list;
     const uint32_t j = live ? list[t] : 0;
     const PodV p = load_pod(pods, j);
@@ -426,12 +434,17 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
     uint64_t pk = PREF_NONE;
     const uint32_t xp = (e.xpairs && live) ? (e.xpos ? e.xpos[j] : j) : 0xFFFFFFFFu;
     uint64_t* const xcol = xp < e.xn ? e.xpairs + xp : nullptr;  // position u at xcol[u * xn]
-    for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split,
+    bool xlive = false;  // a pair the select pass must evaluate again (not stored, or outside the packing)
+    for_general_records(nodes, e, special, n0, chunk, b.y, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split, 0xFFFFFFFFu,
                         [&](uint32_t rec, uint32_t u) {
         // the whole pair (the select pass reads it back instead of evaluating it again)
         const PairX r = eval_pair_ext<false, false, true>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
                                                           dcls);
-        if (xcol && u < e.xT) xcol[(size_t)u * e.xn] = xpair_pack(cfg, r);
+        if (xcol) {
+            const uint64_t x = xpair_pack(cfg, r);
+            if (u < e.xT) xcol[(size_t)u * e.xn] = x;
+            xlive |= u >= e.xT || x == XPAIR_LIVE;
+        }
         if (r.status) return;
         dmax = max(dmax, (uint32_t)r.s_dev);
         rmax = max(rmax, (uint32_t)r.s_rsv);
@@ -441,6 +454,7 @@ __global__ __launch_bounds__(256) void k_ext_stats_sp(const NodeRec* __restrict_
         }
     });
     if (!live) return;
+    if (xlive) xcol[(size_t)e.xT * e.xn] = 1ull;  // the lane's flag row (zeroed before the pass)
     if (dmax) atomicMax(dev_max + j, dmax);
     if (rmax) atomicMax(rsv_max + j, rmax);
     if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
@@ -454,7 +468,8 @@ __global__ __launch_bounds__(256) void k_ext_stats_c1(const NodeRec* __restrict_
                                                       uint32_t n_list, uint32_t n0, uint32_t chunk, uint32_t index_base,
                                                       KCfg cfg, const uint32_t* __restrict__ qst,
                                                       uint32_t* __restrict__ dev_max, const uint32_t* __restrict__ c1) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const GridBlock b = xcd_block();  // whole record chunks per XCD (kg_eval.h)
+    const uint32_t t = b.x * blockDim.x + threadIdx.x;
     const bool live = t < n_list;
     const uint32_t j = live ? list[t] : 0;
     const PodV p = load_pod(pods, j);
@@ -466,7 +481,7 @@ __global__ __launch_bounds__(256) void k_ext_stats_c1(const NodeRec* __restrict_
     const KCfg cv = cfg_in_vgprs(cfg);
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
     uint32_t dmax = 0;
-    for_c1_records(c1, chunk, [&](uint32_t rec) {
+    for_c1_records(c1, chunk, b.y, [&](uint32_t rec) {
         C1Pair o;
         if (eval_c1(cfg, cv, e, nodes[rec].v, zones + rec, rec, n0, pff, px, dcls, q, req_aff, index_base, o) && !o.st)
             dmax = max(dmax, (uint32_t)o.s_dev);
@@ -475,16 +490,17 @@ __global__ __launch_bounds__(256) void k_ext_stats_c1(const NodeRec* __restrict_
 }
 
 // Pass 1 for pods without a GPU request: only the nodes holding a view of the pod's reservation class
-// can carry a Reservation score or order, so lane t walks chunk blockIdx.y of that class's views
+// can carry a Reservation score or order, so lane t walks chunk b.y of that class's views
 // (record order) instead of every record.
 template <bool EXACT, bool TOPO>
-__global__ __launch_bounds__(256) void k_ext_stats_views(const NodeRec* __restrict__ nodes,
+__global__ __launch_bounds__(256) KG_EVAL_ATTR void k_ext_stats_views(const NodeRec* __restrict__ nodes,
                                                          const ZoneRec* __restrict__ zones, ExtDev e, PodsDev pods,
                                                          const uint32_t* __restrict__ list, uint32_t n_list,
                                                          uint32_t chunk, uint32_t index_base, KCfg cfg,
                                                          const uint32_t* __restrict__ qst,
                                                          uint32_t* __restrict__ rsv_max, uint64_t* __restrict__ pref) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const GridBlock b = xcd_block();  // whole view chunks per XCD (kg_eval.h)
+    const uint32_t t = b.x * blockDim.x + threadIdx.x;
     if (t >= n_list) return;
     const uint32_t j = list[t];
     const PodV p = load_pod(pods, j);
@@ -493,17 +509,24 @@ __global__ __launch_bounds__(256) void k_ext_stats_views(const NodeRec* __restri
     if (q || px.cls < 0 || px.cls >= RSV_MAX_CLASSES) return;
     uint32_t rmax = 0;
     uint64_t pk = PREF_NONE;
-    const uint32_t cb = e.cls_begin[px.cls], ce = e.cls_begin[px.cls + 1];
-    const uint32_t vb = cb + blockIdx.y * chunk, ve = min(ce, vb + chunk);
     // stored pairs: position = the special list's length + the view's rank in its class (for_general_records)
     const uint32_t xp = (e.xpairs && e.xsp) ? (e.xpos ? e.xpos[j] : j) : 0xFFFFFFFFu;
     uint64_t* const xcol = xp < e.xn ? e.xpairs + xp : nullptr;  // position u at xcol[u * xn]
     const uint32_t nsp = xcol ? e.xsp[0] : 0u;
+    const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES;
+    bool xlive = false;  // as in k_ext_stats_sp
+    const uint32_t cb = e.cls_begin[px.cls], ce = e.cls_begin[px.cls + 1];
+    const uint32_t vb = cb + b.y * chunk, ve = min(ce, vb + chunk);
     for (uint32_t v = vb; v < ve; v++) {
         const uint32_t rec = e.views[v].rec;
         const PairX r = eval_pair_ext<EXACT, TOPO, true>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q,
-                                         pods.dev_cls ? (uint32_t)pods.dev_cls[j] : (uint32_t)DEV_CLASSES);
-        if (xcol && nsp + (v - cb) < e.xT) xcol[(size_t)(nsp + (v - cb)) * e.xn] = xpair_pack(cfg, r);
+                                                         dcls);
+        if (xcol) {
+            const uint64_t x = xpair_pack(cfg, r);
+            const uint32_t u = nsp + (v - cb);
+            if (u < e.xT) xcol[(size_t)u * e.xn] = x;
+            xlive |= u >= e.xT || x == XPAIR_LIVE;
+        }
         if (r.status) continue;
         rmax = max(rmax, (uint32_t)r.s_rsv);
         if (r.order != 0) {
@@ -511,6 +534,7 @@ __global__ __launch_bounds__(256) void k_ext_stats_views(const NodeRec* __restri
             pk = k < pk ? k : pk;
         }
     }
+    if (xlive) xcol[(size_t)e.xT * e.xn] = 1ull;
     if (rmax) atomicMax(rsv_max + j, rmax);
     if (pk != PREF_NONE) atomicMin((unsigned long long*)(pref + j), (unsigned long long)pk);
 }
@@ -647,10 +671,86 @@ __global__ __launch_bounds__(256) void k_ext_fix_rows(PodsDev pods, const uint32
     rows[atomicAdd(n_rows, 1u)] = j;
 }
 
-// Pass 2, general records of a fast-base launch (the complement of k_ext_select<.., 1>): partials of
-// chunk blockIdx.y go after the fast kernel's (part_off); top-1 is fused (partial = the keys by row).
+// Pass 2, general records of a fast-base launch (the complement of k_ext_select<.., 1>), in two kernels: the pairs
+// the statistics pass stored (k_ext_select_xs: a load and the weighted total, no evaluator in the kernel, so its
+// occupancy is not the evaluator's one wave per SIMD) and the pairs evaluated here (k_ext_select_sp). A lane's stored
+// column: a GPU pod's every general pair, a class pod's views (positions from the special list's length on); a pod its
+// quota gate rejected was not evaluated there (its keys are 0, k_ext_gate wrote its status). The flag row (position xT)
+// marks the lanes with a pair outside the stored form: k_ext_select_sp then takes the lane's every pair.
+// Partials of chunk b.y go after the fast kernel's (part_off); top-1 is fused (partial = the keys by row).
+struct XLane {
+    const uint64_t* col;  // the lane's stored column (position u at col[u * xn]), nullptr = none
+    bool all, flagged;    // every general pair stored (a GPU pod); a pair to evaluate again
+};
+
+__device__ __forceinline__ XLane xlane(const ExtDev& e, const PodX& px, uint32_t jj, bool live, uint32_t q) {
+    XLane l{nullptr, false, false};
+    const uint32_t xp = (e.xpairs && live && q == 0u) ? (e.xpos ? e.xpos[jj] : jj) : 0xFFFFFFFFu;
+    if (xp < e.xn) {
+        l.col = e.xpairs + xp;
+        l.all = px.dcount > 0;
+        l.flagged = l.col[(size_t)e.xT * e.xn] != 0ull;
+    }
+    return l;
+}
+
 template <int K>
-__global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
+__device__ __forceinline__ void put_partial(uint64_t* partial, const uint64_t (&top)[K], uint32_t j, uint32_t n_pods,
+                                            uint32_t by, uint32_t part_off) {
+    if constexpr (K == 1) {  // fused top-1 like k_ext_select<1, .., FB>
+        if (top[0]) atomicMax((unsigned long long*)(partial + j), (unsigned long long)top[0]);
+    } else {
+        uint64_t* dst = partial + (((size_t)by + part_off) * n_pods + j) * K;
+#pragma unroll
+        for (int t = 0; t < K; t++) dst[t] = top[t];
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_ext_select_xs(const NodeRec* __restrict__ nodes, ExtDev e, PodsDev pods,
+                                                       const uint32_t* __restrict__ list, uint32_t n_pods, uint32_t n0,
+                                                       uint32_t chunk, uint32_t index_base, KCfg cfg,
+                                                       const uint32_t* __restrict__ qst,
+                                                       const uint32_t* __restrict__ dev_max,
+                                                       const uint32_t* __restrict__ rsv_max,
+                                                       const uint64_t* __restrict__ pref, uint64_t* __restrict__ partial,
+                                                       uint32_t* __restrict__ pstat, const uint32_t* __restrict__ special,
+                                                       uint32_t part_off, bool c1_split) {
+    const GridBlock b = xcd_block();
+    const uint32_t j = b.x * blockDim.x + threadIdx.x;
+    const bool live = j < n_pods;
+    const uint32_t jj = live ? (list ? list[j] : j) : 0;
+    const PodX px = load_podx(pods, jj);
+    const uint32_t q = live ? qst[jj] : 1u;
+    const XLane l = xlane(e, px, jj, live, q);
+    uint64_t top[K];
+#pragma unroll
+    for (int t = 0; t < K; t++) top[t] = 0;
+    uint32_t unsup = 0;
+    if (l.col && !l.flagged) {
+        const uint32_t dm = dev_max[jj], rm = rsv_max[jj];
+        const uint64_t pf = pref[jj];
+        const uint32_t nsp = special[0];
+        for_general_records(nodes, e, special, n0, chunk, b.y, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split,
+                            0xFFFFFFFFu, [&](uint32_t rec, uint32_t u) {
+            if (!l.all && u < nsp) return;  // k_ext_select_sp's
+            const uint64_t x = l.col[(size_t)u * e.xn];
+            if (!(x >> 63)) {  // infeasible (XPAIR_LIVE only in flagged lanes)
+                unsup |= x == XPAIR_UNSUP ? (uint32_t)KG_ST_UNSUPPORTED : 0u;
+                return;
+            }
+            const uint32_t g = index_base + node_index(nodes[rec]);
+            topk_ins<K>(top, ((uint64_t)total_xpair(cfg, x, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g));
+        });
+    }
+    if (live) {
+        put_partial<K>(partial, top, j, n_pods, b.y, part_off);
+        if (unsup) atomicOr(pstat + jj, unsup);
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) KG_EVAL_ATTR void k_ext_select_sp(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
                                                        ExtDev e, PodsDev pods, const uint32_t* __restrict__ list,
                                                        uint32_t n_pods, uint32_t n0, uint32_t chunk, uint32_t index_base,
                                                        KCfg cfg, const uint32_t* __restrict__ qst,
@@ -659,55 +759,51 @@ __global__ __launch_bounds__(256) void k_ext_select_sp(const NodeRec* __restrict
                                                        const uint64_t* __restrict__ pref, uint64_t* __restrict__ partial,
                                                        uint32_t* __restrict__ pstat, const uint32_t* __restrict__ special,
                                                        uint32_t part_off, bool c1_split) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const GridBlock b = xcd_block();
+    const uint32_t j = b.x * blockDim.x + threadIdx.x;
     const bool live = j < n_pods;
     const uint32_t jj = live ? (list ? list[j] : j) : 0;
     const PodV p = load_pod(pods, jj);
     const PodX px = load_podx(pods, jj);
     const uint32_t q = live ? qst[jj] : 1u;
-    const uint32_t dm = dev_max[jj], rm = rsv_max[jj];
-    const uint64_t pf = pref[jj];
-    const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
+    const XLane l = xlane(e, px, jj, live, q);
     uint64_t top[K];
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
     uint32_t unsup = 0;
-    // the statistics pass stored this pod's pairs: a GPU pod's every general pair, a class pod's views (positions from
-    // the special list's length on); a pod its quota gate rejected was not evaluated there
-    const uint32_t xp = (e.xpairs && live && q == 0u) ? (e.xpos ? e.xpos[jj] : jj) : 0xFFFFFFFFu;
-    const bool xs = xp < e.xn, xs_all = xs && px.dcount > 0;
-    const uint64_t* const xcol = xs ? e.xpairs + xp : nullptr;  // position u at xcol[u * xn]
     const uint32_t nsp = special[0];
-    for_general_records(nodes, e, special, n0, chunk, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split,
-                        [&](uint32_t rec, uint32_t u) {
-        const uint64_t x = (xcol && u < e.xT && (xs_all || u >= nsp)) ? xcol[(size_t)u * e.xn] : XPAIR_LIVE;
-        const uint32_t g = index_base + node_index(nodes[rec]);
-        uint64_t key = 0;
-        if (x >> 63) {
-            key = ((uint64_t)total_xpair(cfg, x, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
-        } else if (x == XPAIR_LIVE) {
-            const PairX r = eval_pair_ext<false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px, q, dcls);
-            unsup |= r.status & KG_ST_UNSUPPORTED;
-            key = r.status ? 0ull : ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
-        } else if (x == XPAIR_UNSUP) {
-            unsup |= KG_ST_UNSUPPORTED;
-        }
-        topk_ins<K>(top, key);
-    });
+    // a flagged or unstored lane: every pair (the stored ones read back); a stored class pod: its special-list pairs
+    const uint32_t lim = (q != 0u || !live) ? 0u : (l.col && !l.flagged) ? (l.all ? 0u : nsp) : 0xFFFFFFFFu;
+    if (lim) {
+        const uint32_t dm = dev_max[jj], rm = rsv_max[jj];
+        const uint64_t pf = pref[jj];
+        const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
+        for_general_records(nodes, e, special, n0, chunk, b.y, (cfg.plugins & KG_PLUGIN_RSV) ? px.cls : -1, c1_split, lim,
+                            [&](uint32_t rec, uint32_t u) {
+            const uint64_t x = (l.col && u < e.xT && (l.all || u >= nsp)) ? l.col[(size_t)u * e.xn] : XPAIR_LIVE;
+            const uint32_t g = index_base + node_index(nodes[rec]);
+            uint64_t key = 0;
+            if (x >> 63) {
+                key = ((uint64_t)total_xpair(cfg, x, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
+            } else if (x == XPAIR_LIVE) {
+                const PairX r = eval_pair_ext<false, false>(cfg, e, nodes[rec].v, zones + rec, dev_of(e, rec), rec, p, px,
+                                                            q, dcls);
+                unsup |= r.status & KG_ST_UNSUPPORTED;
+                key = r.status ? 0ull : ((uint64_t)total_ext(cfg, r, g, dm, rm, pf) << 32) | (uint64_t)(0xFFFFFFFFu - g);
+            } else if (x == XPAIR_UNSUP) {
+                unsup |= KG_ST_UNSUPPORTED;
+            }
+            topk_ins<K>(top, key);
+        });
+    }
     if (live) {
-        if constexpr (K == 1) {  // fused top-1 like k_ext_select<1, .., FB>
-            if (top[0]) atomicMax((unsigned long long*)(partial + j), (unsigned long long)top[0]);
-        } else {
-            uint64_t* dst = partial + (((size_t)blockIdx.y + part_off) * n_pods + j) * K;
-#pragma unroll
-            for (int t = 0; t < K; t++) dst[t] = top[t];
-        }
+        put_partial<K>(partial, top, j, n_pods, b.y, part_off);
         if (unsup) atomicOr(pstat + jj, unsup);
     }
 }
 
 // Pass 2, class-1 records of a split fast-base launch (the light complement of k_ext_select_sp): eval_c1 per pair,
-// a record holding a view of the pod's class left to k_ext_select_sp's view walk. Partials of chunk blockIdx.y go
+// a record holding a view of the pod's class left to k_ext_select_sp's view walk. Partials of chunk b.y go
 // after part_off; top-1 is fused.
 template <int K>
 __global__ __launch_bounds__(256) void k_ext_select_c1(const NodeRec* __restrict__ nodes, const ZoneRec* __restrict__ zones,
@@ -717,7 +813,8 @@ __global__ __launch_bounds__(256) void k_ext_select_c1(const NodeRec* __restrict
                                                        const uint32_t* __restrict__ dev_max, const uint64_t* __restrict__ pref,
                                                        uint64_t* __restrict__ partial, const uint32_t* __restrict__ c1,
                                                        uint32_t part_off) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const GridBlock b = xcd_block();  // whole record chunks per XCD (kg_eval.h)
+    const uint32_t j = b.x * blockDim.x + threadIdx.x;
     const bool live = j < n_pods;
     const uint32_t jj = live ? (list ? list[j] : j) : 0;
     const PodV p = load_pod(pods, jj);
@@ -733,7 +830,7 @@ __global__ __launch_bounds__(256) void k_ext_select_c1(const NodeRec* __restrict
     uint64_t top[K];
 #pragma unroll
     for (int t = 0; t < K; t++) top[t] = 0;
-    for_c1_records(c1, chunk, [&](uint32_t rec) {
+    for_c1_records(c1, chunk, b.y, [&](uint32_t rec) {
         C1Pair o;
         if (!eval_c1(cfg, cv, e, nodes[rec].v, zones + rec, rec, n0, pff, px, dcls, q, req_aff, index_base, o)) return;
         const int64_t tot = total_fb(cfg, o.bk, o.s_dev, dm, mag, o.g, pf);
@@ -743,7 +840,7 @@ __global__ __launch_bounds__(256) void k_ext_select_c1(const NodeRec* __restrict
     if constexpr (K == 1) {
         if (top[0]) atomicMax((unsigned long long*)(partial + j), (unsigned long long)top[0]);
     } else {
-        uint64_t* dst = partial + (((size_t)blockIdx.y + part_off) * n_pods + j) * K;
+        uint64_t* dst = partial + (((size_t)b.y + part_off) * n_pods + j) * K;
 #pragma unroll
         for (int t = 0; t < K; t++) dst[t] = top[t];
     }
@@ -978,7 +1075,7 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
                                 const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                                 uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
                                 const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
-                                const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est,
+                                const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est, uint32_t live_est,
                                 hipStream_t s, const SideLane* lane) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     const uint32_t gx = (n_pods + 255) / 256, y1 = (n_nodes + chunk - 1) / chunk;
@@ -1007,13 +1104,27 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
             if (err != hipSuccess) return drain_lane(lane, err);
         }
     }
-    if (k == 1)
-        k_ext_select_sp<1><<<dim3(gx, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, index_base, cfg, qst,
-                                                        dev_max, rsv_max, pref, partial, pstat, special, y1, sp);
-    else
-        k_ext_select_sp<KG_TOPK_MAX><<<dim3(gx, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk2, index_base,
-                                                                  cfg, qst, dev_max, rsv_max, pref, partial, pstat, special, y1,
+    // the stored pairs (rows y1..), then the ones evaluated here (rows after the class-1 kernel's) over a grid sized
+    // for live_est positions (with stored pairs: the special list; the kernel's 256-VGPR workgroups would otherwise
+    // queue behind the class-1 kernel on the side lane only to find nothing to do)
+    const uint32_t y4 = y1 + y2 + y3;
+    uint32_t chunk5, y5;
+    ext_part2_grid(live_est, gx, &chunk5, &y5);
+    if (k == 1) {
+        if (e.xpairs)
+            k_ext_select_xs<1><<<dim3(gx, y2), 256, 0, s>>>(nodes, e, pods, list, n_pods, n0, chunk2, index_base, cfg, qst,
+                                                            dev_max, rsv_max, pref, partial, pstat, special, y1, sp);
+        k_ext_select_sp<1><<<dim3(gx, y5), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk5, index_base, cfg, qst,
+                                                        dev_max, rsv_max, pref, partial, pstat, special, y4, sp);
+    } else {
+        // (without stored pairs it writes its rows' zero keys)
+        k_ext_select_xs<KG_TOPK_MAX><<<dim3(gx, y2), 256, 0, s>>>(nodes, e, pods, list, n_pods, n0, chunk2, index_base, cfg,
+                                                                  qst, dev_max, rsv_max, pref, partial, pstat, special, y1,
                                                                   sp);
+        k_ext_select_sp<KG_TOPK_MAX><<<dim3(gx, y5), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk5, index_base,
+                                                                  cfg, qst, dev_max, rsv_max, pref, partial, pstat, special, y4,
+                                                                  sp);
+    }
     if (two) {
         hipError_t err = hipStreamWaitEvent(s, lane->join, 0);
         if (err != hipSuccess) return drain_lane(lane, err);

@@ -139,7 +139,7 @@ hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, cons
                                 const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                                 uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
                                 const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
-                                const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est,
+                                const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est, uint32_t live_est,
                                 hipStream_t s, const SideLane* lane = nullptr);
 // out[map[t]] = rows t of src (k keys each; row map[t] with src_by_map, src may then be out); rows whose pod
 // has a nonzero qst[pod] get zero keys and pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the

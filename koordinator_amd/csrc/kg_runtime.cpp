@@ -1784,6 +1784,12 @@ static uint32_t special_est(const kg_snap* s, const kg_pods* p) {
     return c1_split(s, p) ? std::max(s->n_big_est, s->max_cls_views) : s->special_est();
 }
 
+// grid sizing of k_ext_select_sp: with the general pairs stored it evaluates the special list's pairs of the class pods
+// (and the pairs of the rare lanes the statistics pass flagged), else every general pair
+static uint32_t live_est(const kg_snap* s, const kg_pods* p) {
+    return p->xT ? std::max<uint32_t>(c1_split(s, p) ? s->n_big_est : s->n - s->n0 + s->n_big_est, 1u) : special_est(s, p);
+}
+
 // room for the batch's DevSum table over this snapshot's records
 static kg_status devsum_reserve(kg_snap* s, kg_pods* p) {
     kg_ctx* ctx = s->ctx;
@@ -1910,11 +1916,13 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
     p->xT = 0;
     if (ext_fast_base(s, p) && (s->cfg.plugins & (KG_PLUGIN_DEV | KG_PLUGIN_RSV)) && !std::getenv("KG_NO_XPAIRS")) {
         // the general pairs' selection inputs, stored for the select pass: [special list + largest class's views][the
-        // select pass's lane]
-        const uint32_t T = special_est(s, p) + s->max_cls_views + 64;
+        // select pass's lane], then a flag row (a lane with a pair the select pass evaluates again)
+        uint32_t T = special_est(s, p) + s->max_cls_views + 64;
+        if (const char* cap = std::getenv("KG_XPAIRS_T"))  // tests: fewer positions, so that lanes get flagged
+            T = std::max(1u, std::min<uint32_t>(T, (uint32_t)std::strtoul(cap, nullptr, 10)));
         const bool split = ext_split(s, p);
         const uint32_t xn = split ? p->n_x : p->n;
-        const size_t need = (size_t)xn * T;
+        const size_t need = (size_t)xn * (T + 1);
         if (need * sizeof(uint64_t) <= ((size_t)4 << 30)) {
             if (p->xpairs_cap < need) {
                 HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1930,6 +1938,7 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
                 }
             }
             if (p->d_xpairs) {
+                HIP_TRY(ctx, hipMemsetAsync(p->d_xpairs + (size_t)T * xn, 0, sizeof(uint64_t) * xn, ctx->stream));
                 p->xT = T;
                 e.xpairs = p->d_xpairs;
                 e.xT = T;
@@ -2068,12 +2077,14 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(n_x, 1), 8192);
     const bool fb = n_x && ext_fast_base(s, p);
     const bool fused = fb && kk == 1;
+    const uint32_t lest = live_est(s, p);  // (before p->xT is consumed below)
     // a fast-base launch writes the fast-record kernel's chunks, then the special-record kernel's
     uint32_t xparts = n_x ? (s->n + chunk - 1) / chunk : 0;
-    if (fb) {
-        uint32_t c2, y2;
+    if (fb) {  // k_ext_select_xs's and k_ext_select_sp's rows
+        uint32_t c2, y2, c5, y5;
         ext_part2_grid(special_est(s, p), (n_x + 255) / 256, &c2, &y2);
-        xparts += y2;
+        ext_part2_grid(lest, (n_x + 255) / 256, &c5, &y5);
+        xparts += y2 + y5;
         if (c1_split(s, p)) {
             ext_part2_grid(s->n - s->n0, (n_x + 255) / 256, &c2, &y2);
             xparts += y2;
@@ -2129,11 +2140,26 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
             std::fprintf(stderr, "kg: one-pass select re-ran %u of %u rows\n", nr, n_x);
         }
     }
+    if (fb && std::getenv("KG_TRACE_SP")) {  // diagnostics: the general records' work of this batch
+        uint32_t nsp = 0, nc1 = 0;
+        std::vector<uint64_t> flag(xe.xpairs ? n_x : 0);
+        HIP_TRY(ctx, hipMemcpyAsync(&nsp, s->d_special, sizeof(nsp), hipMemcpyDeviceToHost, ctx->stream));
+        if (c1_list(s, p))
+            HIP_TRY(ctx, hipMemcpyAsync(&nc1, c1_list(s, p), sizeof(nc1), hipMemcpyDeviceToHost, ctx->stream));
+        if (!flag.empty())
+            HIP_TRY(ctx, hipMemcpyAsync(flag.data(), xe.xpairs + (size_t)xe.xT * xe.xn, sizeof(uint64_t) * n_x,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        size_t nf = 0;
+        for (uint64_t f : flag) nf += f != 0;
+        std::fprintf(stderr, "kg: general records: special %u, class-1 %u, largest class %u views, n_x %u (stat %u, class-only %u), "
+                     "xT %u, flagged lanes %zu\n", nsp, nc1, s->max_cls_views, n_x, p->n_stat, p->n_stat_cls, xe.xT, nf);
+    }
     if (fb) {
         xe.cls_max = nullptr;
         HIP_TRY(ctx, launch_ext_select_sp(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base, s->kcfg,
                                           p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, xpart, p->d_pstat, s->d_special,
-                                          special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream,
+                                          special_est(s, p), c1_list(s, p), s->n - s->n0, lest, ctx->stream,
                                           side_lane2(ctx, lane2)));
     }
     if (plain_on_side) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->join, 0));  // d_out zeroed + plain keys in

@@ -436,3 +436,27 @@ def test_pod_batch_without_config5_columns(ctx):
         got = engine.eval_select(snap, batch, k)
         assert np.array_equal(got, oracle_lib.ext_select(kc, nodes, plain, k, 0, quotas, rsv)), k
     assert not (engine.result_status(batch) & abi.KG_ST_QUOTA).any()
+
+
+@pytest.mark.parametrize("numa", ["single", "mix"])
+@pytest.mark.parametrize("mode", ["stored", "capped", "off"])
+@pytest.mark.parametrize("k", [1, 3])
+def test_ext_select_stored_pairs(ctx, monkeypatch, numa, mode, k):
+    """The fast-base select's general records through its two kernels (k_ext_select_xs: the pairs the statistics pass
+    stored; k_ext_select_sp: the special list's pairs of class pods, the lanes flagged because a pair was not stored,
+    every pair without the store) equal the oracle's selection. "capped" stores 40 positions per lane (KG_XPAIRS_T), so
+    class pods with more views are flagged; "off" stores nothing (KG_NO_XPAIRS); numa "mix" puts Restricted (F_BIG)
+    records in the special list."""
+    if mode == "capped":
+        monkeypatch.setenv("KG_XPAIRS_T", "40")
+    elif mode == "off":
+        monkeypatch.setenv("KG_NO_XPAIRS", "1")
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(2000, 300, seed_config=67, rsv_frac=0.3, numa=numa, usage="u01")
+    kc = cfg.kg_config()
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_select(snap, batch, k)
+    want = oracle_lib.ext_select(kc, nodes, pods, k, 0, quotas, rsv)
+    assert np.array_equal(got, want), np.argwhere(got != want)[:8].tolist()
+    ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
+    wstat = np.bitwise_or.reduce(ref.status & (abi.KG_ST_UNSUPPORTED | abi.KG_ST_QUOTA), axis=1)
+    assert np.array_equal(engine.result_status(batch), wstat)
