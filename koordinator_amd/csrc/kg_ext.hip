@@ -25,6 +25,7 @@
 #include "kg_ext.h"
 #include "kg_ext_wave.h"
 #include "kg_kernels.h"
+#include <cstdlib>
 
 namespace kg {
 
@@ -863,6 +864,11 @@ __global__ __launch_bounds__(256) void k_scatter_keys(const uint64_t* src, const
 // ------------------------------------------------------------------------------------------------
 // launchers
 
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* v = std::getenv(name);
+    return v ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
+}
+
 hipError_t launch_ext_gate(const PodsDev& pods, uint32_t n_pods, const ExtDev& e, uint32_t plugins, uint32_t* qst,
                            uint32_t* pstat, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
@@ -918,7 +924,9 @@ hipError_t launch_ext_stats(const NodeRec* nodes, const ZoneRec* zones, const Ex
             }
         }
         uint32_t chunk2, y2;
-        ext_part2_grid(special_est, grid.x, &chunk2, &y2);
+        // short chunks: a wave's pairs run one after another, each a chain of dependent loads through the views, the
+        // reservations and their GPU tables (config 5: ~8k workgroups of 3 positions 0.60 ms, ~2k of 9 1.12 ms)
+        ext_part2_grid(special_est, grid.x, &chunk2, &y2, env_u32("KG_SP_TARGET", 8192u), env_u32("KG_SP_MIN", 1u));
         k_ext_stats_sp<<<dim3(grid.x, y2), 256, 0, s>>>(nodes, zones, e, pods, list, n_list, n0, chunk2, index_base, cfg,
                                                         qst, dev_max, rsv_max, pref, special, c1 != nullptr);
         if (two) {
@@ -1007,8 +1015,8 @@ hipError_t launch_ext_stats_views(const NodeRec* nodes, const ZoneRec* zones, co
     if (n_list == 0 || max_views == 0) return hipSuccess;
     // split every class's views over enough chunks to fill the chip (~2048 workgroups)
     const uint32_t pod_blocks = (n_list + 255) / 256;
-    const uint32_t want = std::max<uint32_t>(1, 2048 / pod_blocks);
-    const uint32_t chunk = std::max<uint32_t>(4, (max_views + want - 1) / want);
+    const uint32_t want = std::max<uint32_t>(1, env_u32("KG_SV_TARGET", 2048u) / pod_blocks);
+    const uint32_t chunk = std::max<uint32_t>(env_u32("KG_SV_MIN", 4u), (max_views + want - 1) / want);
     dim3 grid(pod_blocks, (max_views + chunk - 1) / chunk);
 #define KG_EXT_SV(EX, TP)                                                                                        \
     k_ext_stats_views<EX, TP><<<grid, 256, 0, s>>>(nodes, zones, e, pods, list, n_list, chunk, index_base, cfg, qst, \

@@ -193,10 +193,11 @@ hipError_t launch_big_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t* big
                            hipStream_t s);
 // Grid of the PART 2 ext kernels (special records, grid-stride): chunk and chunk count for an estimate
 // of the special-record count and the pod blocks of the launch (~2048 workgroups in all).
-inline void ext_part2_grid(uint32_t special_est, uint32_t pod_blocks, uint32_t* chunk, uint32_t* n_chunks) {
-    const uint32_t want = pod_blocks ? (2048u + pod_blocks - 1) / pod_blocks : 1u;
+inline void ext_part2_grid(uint32_t special_est, uint32_t pod_blocks, uint32_t* chunk, uint32_t* n_chunks,
+                           uint32_t target = 2048u, uint32_t min_chunk = 4u) {
+    const uint32_t want = pod_blocks ? (target + pod_blocks - 1) / pod_blocks : 1u;
     const uint32_t est = special_est ? special_est : 1u;
-    *chunk = est / want < 4u ? 4u : (est + want - 1) / want;
+    *chunk = est / want < min_chunk ? min_chunk : (est + want - 1) / want;
     *n_chunks = (est + *chunk - 1) / *chunk;
 }
 hipError_t launch_special_scan(const NodeRec* nodes, uint32_t n_nodes, uint32_t n0, uint32_t* special, uint32_t* c1,

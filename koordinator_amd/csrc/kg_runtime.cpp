@@ -1833,38 +1833,66 @@ static bool replay_gz(const kg_snap* s, const kg_pods* p, bool exact, bool reaso
     return replay_fb(s, p, exact, reasons) && s->d_dev && gpu_zone_active(s, p);
 }
 // The batch's DevSum table over this snapshot's records (fast-base config-5 select with DeviceShare).
+static const SideLane* side_lane2(kg_ctx* ctx, SideLane& l);
+
 static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
     kg_ctx* ctx = s->ctx;
     e.dsum = nullptr;
     if (!s->d_dev || !ext_fast_base(s, p)) return KG_OK;
     const kg_status st = devsum_reserve(s, p);
     if (st != KG_OK) return st;
-    HIP_TRY(ctx, launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(),
-                                p->d_devsum, spec_cls_max(p), ctx->stream));
-    e.dsum = p->d_devsum;
-    e.gz = nullptr;
-    if (gz_active(s, p)) {  // DeviceShare's NUMA hints of the SingleNUMANode records, per class
+    const bool gz = gz_active(s, p);
+    if (gz) {  // (may synchronise: before the fork)
         const kg_status gst = gz_reserve(s, p);
         if (gst != KG_OK) return gst;
-        HIP_TRY(ctx, launch_gpu_zone_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg,
-                                         s->ext_dev(), p->d_gz, ctx->stream));
+    }
+    const bool codes = s->n_rdev && s->d_rdev && p->n_dclass;
+    if (codes && p->rcode_cap < (size_t)s->n_rdev * DEV_CLASSES) {
+        const size_t need = (size_t)s->n_rdev * DEV_CLASSES;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipFree(p->d_rcode));
+        p->d_rcode = nullptr;
+        p->rcode_cap = 0;
+        HIP_TRY(ctx, hipMalloc(&p->d_rcode, need));
+        p->rcode_cap = need;
+    }
+    // DeviceShare's NUMA hints of the SingleNUMANode records (per class) on the second side lane beside DevSum and
+    // the restore tables' codes: the three tables are independent, the statistics kernels read all of them
+    SideLane lane{};
+    const SideLane* l2 = gz ? side_lane2(ctx, lane) : nullptr;
+    if (l2) {
+        HIP_TRY(ctx, hipEventRecord(l2->fork, ctx->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(l2->s, l2->fork, 0));
+    }
+    auto drain = [&]() {
+        if (l2) hipStreamSynchronize(l2->s);
+    };
+    e.gz = nullptr;
+    if (gz) {
+        if (launch_gpu_zone_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg,
+                                s->ext_dev(), p->d_gz, l2 ? l2->s : ctx->stream) != hipSuccess ||
+            (l2 && hipEventRecord(l2->join, l2->s) != hipSuccess)) {
+            drain();
+            return fail(ctx, KG_DEVICE_ERROR, "gpu zone sum launch failed");
+        }
         e.gz = p->d_gz;
     }
+    if (launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(),
+                       p->d_devsum, spec_cls_max(p), ctx->stream) != hipSuccess) {
+        drain();
+        return fail(ctx, KG_DEVICE_ERROR, "dev sum launch failed");
+    }
+    e.dsum = p->d_devsum;
     e.rcode = nullptr;
-    if (s->n_rdev && s->d_rdev && p->n_dclass) {  // the GPU restore tables of the reservation views, per class
-        const size_t need = (size_t)s->n_rdev * DEV_CLASSES;
-        if (p->rcode_cap < need) {
-            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-            HIP_TRY(ctx, hipFree(p->d_rcode));
-            p->d_rcode = nullptr;
-            p->rcode_cap = 0;
-            HIP_TRY(ctx, hipMalloc(&p->d_rcode, need));
-            p->rcode_cap = need;
+    if (codes) {  // the GPU restore tables of the reservation views, per class
+        if (launch_rdev_codes(s->d_nodes, s->d_zones, s->d_dev, s->d_rdev, s->d_rdev_rec, s->n_rdev, p->d_dclass,
+                              p->n_dclass, s->kcfg, s->ext_dev(), p->d_rcode, ctx->stream) != hipSuccess) {
+            drain();
+            return fail(ctx, KG_DEVICE_ERROR, "restore codes launch failed");
         }
-        HIP_TRY(ctx, launch_rdev_codes(s->d_nodes, s->d_zones, s->d_dev, s->d_rdev, s->d_rdev_rec, s->n_rdev, p->d_dclass,
-                                       p->n_dclass, s->kcfg, s->ext_dev(), p->d_rcode, ctx->stream));
         e.rcode = p->d_rcode;
     }
+    if (l2) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, l2->join, 0));
     return KG_OK;
 }
 
