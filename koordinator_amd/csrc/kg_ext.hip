@@ -574,10 +574,10 @@ __global__ __launch_bounds__(256, 3) void k_ext_select(const NodeRec* __restrict
     bool live = j < n_pods;
     if constexpr (FB) {
         if (e.rows) {
-            const uint32_t nr = *e.n_rows;
-            if (b.x * blockDim.x >= nr) return;  // whole workgroup idle (no barrier in this kernel)
-            live = t0 < nr;
-            j = live ? e.rows[t0] : 0u;
+            const uint32_t nr = *e.n_rows, t = t0 + e.rows_from;
+            if (b.x * blockDim.x + e.rows_from >= nr) return;  // whole workgroup idle (no barrier in this kernel)
+            live = t < nr;
+            j = live ? e.rows[t] : 0u;
         }
     }
     const uint32_t jj = live ? (list ? list[j] : j) : 0;
@@ -1075,6 +1075,21 @@ hipError_t launch_ext_fix(const NodeRec* nodes, const ZoneRec* zones, const ExtD
     f.cls_max = nullptr;
     f.rows = rows;
     f.n_rows = n_rows;
+    f.rows_from = 0;
+    if (k == 1) {
+        // a handful of rows (the guesses the class bound missed): the launch takes as long as one workgroup's walk of
+        // its record chunk, so the first 256 rows go over short chunks in one pod block, the rest (if any) as before
+        const uint32_t c1 = std::max<uint32_t>(16u, chunk / 8u), gx = (n_pods + 255) / 256;
+        k_ext_select<1, false, false, true, 1><<<dim3(1, (n_nodes + c1 - 1) / c1), 256, 0, s>>>(
+            nodes, zones, f, pods, list, n_pods, n_nodes, n0, c1, index_base, cfg, qst, dev_max, rsv_max, pref, partial, pstat);
+        if (gx > 1) {
+            f.rows_from = 256;
+            k_ext_select<1, false, false, true, 1><<<dim3(gx - 1, (n_nodes + chunk - 1) / chunk), 256, 0, s>>>(
+                nodes, zones, f, pods, list, n_pods, n_nodes, n0, chunk, index_base, cfg, qst, dev_max, rsv_max, pref, partial,
+                pstat);
+        }
+        return hipGetLastError();
+    }
     return launch_ext_select(nodes, zones, f, pods, list, n_pods, n_nodes, n0, chunk, k, index_base, cfg, false, false, true,
                              qst, dev_max, rsv_max, pref, partial, pstat, s);
 }

@@ -525,6 +525,7 @@ struct ExtDev {
     uint32_t* fb_max;         // [pod]
     const uint32_t* rows;     // nullptr = every row
     const uint32_t* n_rows;
+    uint32_t rows_from;       // the launch's first pod block takes rows[rows_from ...]
     // GPU partition tables (kg_gpu_partition, grouped by table / GPU count / AllocationScore) and per (table,
     // GPU count) the entry range: part_rng[table * 9 + n] = begin | end << 16
     const kg_gpu_partition* parts;
