@@ -22,7 +22,7 @@ import isa_mix  # noqa: E402
 
 OPS_TABLE = os.path.join(ROOT, "profiles", "r5", "ubench_ops.jsonl")
 CYC_DEFAULT = 4.1
-KERNELS = ("k_select1", "k_select", "k_ext_select", "k_ext_select_sp", "k_ext_select_c1", "k_ext_stats", "k_ext_stats_sp",
+KERNELS = ("k_select1", "k_select", "k_ext_select", "k_ext_select_sp", "k_ext_select_xs", "k_ext_select_c1", "k_ext_stats", "k_ext_stats_sp",
            "k_ext_stats_c1", "k_ext_stats_views", "k_dev_sum", "k_rdev_codes", "k_gpu_zone_sum", "k_big_init", "k_big_sel",
            "k_int_seed", "k_int_filter", "k_int_pairs", "k_ext_replay", "k_replay")
 
