@@ -815,15 +815,24 @@ __global__ __launch_bounds__(256) void k_ext_select_c1(const NodeRec* __restrict
                                                        uint64_t* __restrict__ partial, const uint32_t* __restrict__ c1,
                                                        uint32_t part_off) {
     const GridBlock b = xcd_block();  // whole record chunks per XCD (kg_eval.h)
-    const uint32_t j = b.x * blockDim.x + threadIdx.x;
-    const bool live = j < n_pods;
+    uint32_t j = b.x * blockDim.x + threadIdx.x;
+    bool live = j < n_pods;
+    if (e.rows) {  // re-run of the rows k_ext_fix_rows listed (top-1), as k_ext_select<FB>'s
+        const uint32_t nr = *e.n_rows, t = j + e.rows_from;
+        if (b.x * blockDim.x + e.rows_from >= nr) return;  // whole workgroup idle (no barrier in this kernel)
+        live = t < nr;
+        j = live ? e.rows[t] : 0u;
+    }
     const uint32_t jj = live ? (list ? list[j] : j) : 0;
     const PodV p = load_pod(pods, jj);
     const PodX px = load_podx(pods, jj);
     const uint32_t q = live ? qst[jj] : 1u;
-    const uint32_t dm = dev_max[jj];
+    uint32_t dm = dev_max[jj];
     const uint64_t pf = pref[jj];
     const uint32_t dcls = pods.dev_cls ? (uint32_t)pods.dev_cls[jj] : (uint32_t)DEV_CLASSES;
+    // beside the one-pass select: the same guessed maximum (its wrong rows are re-run after k_ext_fix_rows)
+    if (e.cls_max && (cfg.plugins & KG_PLUGIN_DEV) && px.dcount != 0 && dcls < (uint32_t)DEV_CLASSES)
+        dm = max(dm, e.cls_max[dcls]);
     const PodF pff = to_podf(p, cfg);
     const KCfg cv = cfg_in_vgprs(cfg);
     const bool req_aff = (cfg.plugins & KG_PLUGIN_RSV) && (p.flags & KG_POD_RSV_REQUIRED);
@@ -1094,18 +1103,46 @@ hipError_t launch_ext_fix(const NodeRec* nodes, const ZoneRec* zones, const ExtD
                              qst, dev_max, rsv_max, pref, partial, pstat, s);
 }
 
+hipError_t launch_ext_select_c1_top1(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                                     const uint32_t* list, uint32_t n_pods, uint32_t n0, uint32_t index_base, const KCfg& cfg,
+                                     const uint32_t* qst, const uint32_t* dev_max, const uint64_t* pref, uint64_t* keys,
+                                     const uint32_t* c1, uint32_t c1_est, hipStream_t s) {
+    if (n_pods == 0 || !c1) return hipSuccess;
+    const uint32_t gx = (n_pods + 255) / 256;
+    uint32_t chunk3, y3;
+    ext_part2_grid(c1_est, gx, &chunk3, &y3);
+    if (!e.rows) {
+        k_ext_select_c1<1><<<dim3(gx, y3), 256, 0, s>>>(nodes, zones, e, pods, list, n_pods, n0, chunk3, index_base, cfg, qst,
+                                                        dev_max, pref, keys, c1, 0);
+        return hipGetLastError();
+    }
+    // re-run rows: the first 256 over short chunks in one pod block (as launch_ext_fix), the rest as before
+    ExtDev f = e;
+    f.rows_from = 0;
+    uint32_t cs, ys;
+    ext_part2_grid(c1_est, 1, &cs, &ys, 4096u, 8u);
+    k_ext_select_c1<1><<<dim3(1, ys), 256, 0, s>>>(nodes, zones, f, pods, list, n_pods, n0, cs, index_base, cfg, qst, dev_max,
+                                                   pref, keys, c1, 0);
+    if (gx > 1) {
+        f.rows_from = 256;
+        k_ext_select_c1<1><<<dim3(gx - 1, y3), 256, 0, s>>>(nodes, zones, f, pods, list, n_pods, n0, chunk3, index_base, cfg,
+                                                            qst, dev_max, pref, keys, c1, 0);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                                 const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                                 uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
                                 const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
                                 const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est, uint32_t live_est,
-                                hipStream_t s, const SideLane* lane) {
+                                bool c1_split, hipStream_t s, const SideLane* lane) {
     if (n_pods == 0 || n_nodes == 0) return hipSuccess;
     const uint32_t gx = (n_pods + 255) / 256, y1 = (n_nodes + chunk - 1) / chunk;
     uint32_t chunk2, y2, chunk3 = 0, y3 = 0;
     ext_part2_grid(special_est, gx, &chunk2, &y2);
     if (c1) ext_part2_grid(c1_est, gx, &chunk3, &y3);
-    const bool sp = c1 != nullptr;
+    const bool sp = c1_split;  // (c1 == nullptr with c1_split: k_ext_select_c1 ran beside the one-pass select)
     // the class-1 kernel on the side lane beside the general one (disjoint partial rows: y1 + y2 on)
     const bool two = c1 && lane && lane->s && lane->fork && lane->join;
     hipStream_t s3 = two ? lane->s : s;

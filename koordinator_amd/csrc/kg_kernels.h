@@ -135,11 +135,17 @@ hipError_t launch_ext_fix(const NodeRec* nodes, const ZoneRec* zones, const ExtD
 // General records of a fast-base select (F_BIG, class 1 unless split off into c1, the lane's views); k > 1: partial
 // chunks after the fast-base kernel's (n_nodes / chunk of them), then the class-1 kernel's (c1 != nullptr:
 // k_special_scan's c1 list, evaluated by the light k_ext_select_c1).
+// k_ext_select_c1 at top-1 straight into keys: beside the one-pass select (e.cls_max: its guessed maxima) or, with
+// e.rows, on the rows k_ext_fix_rows listed
+hipError_t launch_ext_select_c1_top1(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
+                                     const uint32_t* list, uint32_t n_pods, uint32_t n0, uint32_t index_base, const KCfg& cfg,
+                                     const uint32_t* qst, const uint32_t* dev_max, const uint64_t* pref, uint64_t* keys,
+                                     const uint32_t* c1, uint32_t c1_est, hipStream_t s);
 hipError_t launch_ext_select_sp(const NodeRec* nodes, const ZoneRec* zones, const ExtDev& e, const PodsDev& pods,
                                 const uint32_t* list, uint32_t n_pods, uint32_t n_nodes, uint32_t n0, uint32_t chunk, uint32_t k,
                                 uint32_t index_base, const KCfg& cfg, const uint32_t* qst, const uint32_t* dev_max,
                                 const uint32_t* rsv_max, const uint64_t* pref, uint64_t* partial, uint32_t* pstat,
-                                const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est, uint32_t live_est,
+                                const uint32_t* special, uint32_t special_est, const uint32_t* c1, uint32_t c1_est, uint32_t live_est, bool c1_split,
                                 hipStream_t s, const SideLane* lane = nullptr);
 // out[map[t]] = rows t of src (k keys each; row map[t] with src_by_map, src may then be out); rows whose pod
 // has a nonzero qst[pod] get zero keys and pstat[pod] = qst[pod] (the gate decided the pod: no pair needs the

@@ -2152,15 +2152,44 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
     }
     if (n_plain && !plain_on_side)
         HIP_TRY(ctx, launch_select(a, ctx->stream));  // zeroes d_out first at k = 1: before the x scatter
-    if (n_x)
-        HIP_TRY(ctx, launch_ext_select(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
-                                       s->kcfg, force_exact(), need_topo(s, p), fb, p->d_qst, p->d_dev_max, p->d_rsv_max,
-                                       p->d_pref, xpart, p->d_pstat, ctx->stream));
+    // top-1 one-pass select with a class-1 list: the class-1 kernel runs on the second side lane beside the one-pass
+    // select with the same guessed maxima (instead of after the re-run, at the end of the step), joins before
+    // k_ext_fix_rows (which zeroes the wrong rows' keys) and re-runs on the wrong rows after it
+    const uint32_t* c1l = fb ? c1_list(s, p) : nullptr;
+    const SideLane* l2 = (fused && guess && c1l && n_x) ? side_lane2(ctx, lane2) : nullptr;
+    if (l2) {
+        HIP_TRY(ctx, hipEventRecord(l2->fork, ctx->stream));
+        HIP_TRY(ctx, hipStreamWaitEvent(l2->s, l2->fork, 0));
+        if (launch_ext_select_c1_top1(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n0, s->base, s->kcfg, p->d_qst,
+                                      p->d_dev_max, p->d_pref, xpart, c1l, s->n - s->n0, l2->s) != hipSuccess ||
+            hipEventRecord(l2->join, l2->s) != hipSuccess) {
+            hipStreamSynchronize(l2->s);
+            return fail(ctx, KG_DEVICE_ERROR, "class-1 select launch failed");
+        }
+    }
+    if (n_x) {
+        const hipError_t err = launch_ext_select(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base,
+                                                 s->kcfg, force_exact(), need_topo(s, p), fb, p->d_qst, p->d_dev_max,
+                                                 p->d_rsv_max, p->d_pref, xpart, p->d_pstat, ctx->stream);
+        if (err != hipSuccess) {
+            if (l2) hipStreamSynchronize(l2->s);
+            return fail(ctx, KG_DEVICE_ERROR, "one-pass select launch failed: %s", hipGetErrorString(err));
+        }
+    }
+    if (l2) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, l2->join, 0));
     if (guess) {
         if (global) NCCL_TRY(ctx, ncclAllReduce(xe.fb_max, xe.fb_max, p->n, ncclUint32, ncclMax, ctx->comm, ctx->stream));
         HIP_TRY(ctx, launch_ext_fix(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base, s->kcfg,
                                     p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, xpart, p->d_pstat, spec_rows(p),
                                     spec_n_rows(p), ctx->stream));
+        if (l2) {  // the class-1 pairs of the re-run rows with their final maxima
+            ExtDev f = xe;
+            f.cls_max = nullptr;
+            f.rows = spec_rows(p);
+            f.n_rows = spec_n_rows(p);
+            HIP_TRY(ctx, launch_ext_select_c1_top1(s->d_nodes, s->d_zones, f, p->dev, xl, n_x, s->n0, s->base, s->kcfg,
+                                                   p->d_qst, p->d_dev_max, p->d_pref, xpart, c1l, s->n - s->n0, ctx->stream));
+        }
         if (std::getenv("KG_TRACE_FIX")) {  // diagnostics: how many rows the guess missed
             uint32_t nr = 0;
             HIP_TRY(ctx, hipMemcpyAsync(&nr, spec_n_rows(p), sizeof(nr), hipMemcpyDeviceToHost, ctx->stream));
@@ -2187,8 +2216,8 @@ static kg_status ext_select_local(kg_snap* s, kg_pods* p, uint32_t kk, uint64_t*
         xe.cls_max = nullptr;
         HIP_TRY(ctx, launch_ext_select_sp(s->d_nodes, s->d_zones, xe, p->dev, xl, n_x, s->n, s->n0, chunk, kk, s->base, s->kcfg,
                                           p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, xpart, p->d_pstat, s->d_special,
-                                          special_est(s, p), c1_list(s, p), s->n - s->n0, lest, ctx->stream,
-                                          side_lane2(ctx, lane2)));
+                                          special_est(s, p), l2 ? nullptr : c1l, s->n - s->n0, lest, c1_split(s, p),
+                                          ctx->stream, side_lane2(ctx, lane2)));
     }
     if (plain_on_side) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->join, 0));  // d_out zeroed + plain keys in
     if (!split) {
