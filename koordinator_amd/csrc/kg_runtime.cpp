@@ -1980,16 +1980,39 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
         // pods without a GPU request only get statistics from the nodes holding a view of their
         // reservation class (elsewhere s_dev = s_rsv = order = 0): one lane per pod over those views
         const uint32_t nc = p->n_stat_cls, ng = p->n_stat - nc;
-        if (nc && (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views)
-            HIP_TRY(ctx, launch_ext_stats_views(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list, nc, s->max_cls_views,
-                                                s->base, s->kcfg, force_exact(), need_topo(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max,
-                                                p->d_pref, ctx->stream));
+        const bool views = nc && (s->cfg.plugins & KG_PLUGIN_RSV) && s->n_views;
+        // the class pods' views on the second side lane, ahead of the class-1 statistics launch_ext_stats puts there:
+        // both beside the GPU pods' general records on the main stream (disjoint pods)
+        const SideLane* l2 = (views && ng) ? side_lane2(ctx, lane) : nullptr;
+        if (l2) {
+            HIP_TRY(ctx, hipEventRecord(l2->fork, ctx->stream));
+            HIP_TRY(ctx, hipStreamWaitEvent(l2->s, l2->fork, 0));
+        }
+        if (views) {
+            const hipError_t err = launch_ext_stats_views(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list, nc,
+                                                          s->max_cls_views, s->base, s->kcfg, force_exact(), need_topo(s, p),
+                                                          p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
+                                                          l2 ? l2->s : ctx->stream);
+            if (err != hipSuccess) {
+                if (l2) hipStreamSynchronize(l2->s);
+                return fail(ctx, KG_DEVICE_ERROR, "view statistics launch failed: %s", hipGetErrorString(err));
+            }
+        }
         // config-5 waves cost unequal amounts (GPU count, views): more, smaller chunks shorten the tail
         const uint32_t chunk = select_chunk(s->n, std::max<uint32_t>(ng, 1), 8192);
-        HIP_TRY(ctx, launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, s->n0, chunk, s->base,
-                                      s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p), p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref,
-                                      s->d_special, special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream,
-                                      side_lane2(ctx, lane)));
+        const hipError_t err = launch_ext_stats(s->d_nodes, s->d_zones, e, p->dev, p->d_stat_list + nc, ng, s->n, s->n0, chunk,
+                                                s->base, s->kcfg, force_exact(), need_topo(s, p), ext_fast_base(s, p),
+                                                p->d_qst, p->d_dev_max, p->d_rsv_max, p->d_pref, s->d_special,
+                                                special_est(s, p), c1_list(s, p), s->n - s->n0, ctx->stream,
+                                                side_lane2(ctx, lane));
+        if (err != hipSuccess) {
+            if (l2) hipStreamSynchronize(l2->s);
+            return fail(ctx, KG_DEVICE_ERROR, "statistics launch failed: %s", hipGetErrorString(err));
+        }
+        if (l2) {  // (launch_ext_stats joins the lane only when it used it)
+            HIP_TRY(ctx, hipEventRecord(l2->join, l2->s));
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, l2->join, 0));
+        }
     }
     return KG_OK;
 }
