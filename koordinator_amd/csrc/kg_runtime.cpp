@@ -1835,7 +1835,9 @@ static bool replay_gz(const kg_snap* s, const kg_pods* p, bool exact, bool reaso
 // The batch's DevSum table over this snapshot's records (fast-base config-5 select with DeviceShare).
 static const SideLane* side_lane2(kg_ctx* ctx, SideLane& l);
 
-static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
+// *lane_open: k_gpu_zone_sum went to the second side lane and is not joined yet (only the class-1 kernels read its
+// table: they run on that lane after it; the caller joins the lane into the main stream before the select)
+static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e, bool* lane_open) {
     kg_ctx* ctx = s->ctx;
     e.dsum = nullptr;
     if (!s->d_dev || !ext_fast_base(s, p)) return KG_OK;
@@ -1892,7 +1894,7 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e) {
         }
         e.rcode = p->d_rcode;
     }
-    if (l2) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, l2->join, 0));
+    *lane_open = l2 != nullptr;
     return KG_OK;
 }
 
@@ -1934,7 +1936,8 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
     SideLane lane{};
     kg_status dst = gated ? KG_OK : ext_gate_local(s, p);
     if (dst != KG_OK) return dst;
-    dst = ext_dev_sum(s, p, e);
+    bool zone_lane = false;
+    dst = ext_dev_sum(s, p, e, &zone_lane);
     if (dst != KG_OK) return dst;
     if (ext_fast_base(s, p)) {  // records for the PART 2 kernels (pass 1 and pass 2 of this batch)
         if (!s->d_special) HIP_TRY(ctx, hipMalloc(&s->d_special, sizeof(uint32_t) * 2 * ((size_t)s->n + 1)));
@@ -2010,6 +2013,15 @@ static kg_status ext_stats_local(kg_snap* s, kg_pods* p, bool gated = false) {
             return fail(ctx, KG_DEVICE_ERROR, "statistics launch failed: %s", hipGetErrorString(err));
         }
         if (l2) {  // (launch_ext_stats joins the lane only when it used it)
+            HIP_TRY(ctx, hipEventRecord(l2->join, l2->s));
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, l2->join, 0));
+            zone_lane = false;
+        }
+    }
+    if (zone_lane) {  // the GPU zone hints' lane, not joined by the statistics
+        SideLane z{};
+        const SideLane* l2 = side_lane2(ctx, z);
+        if (l2) {
             HIP_TRY(ctx, hipEventRecord(l2->join, l2->s));
             HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, l2->join, 0));
         }
