@@ -999,8 +999,8 @@ hipError_t launch_gpu_zone_sum(const NodeRec* nodes, const ZoneRec* zones, const
 
 hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, uint32_t n0,
                           const DevClass* cls, uint32_t n_cls, const KCfg& cfg, const ExtDev& e, DevSum* out,
-                          uint32_t* cls_max, hipStream_t s) {
-    hipError_t err = hipMemsetAsync(cls_max, 0, sizeof(uint32_t) * DEV_CLASSES, s);
+                          uint32_t* cls_max, hipStream_t s, bool zero_cls_max) {
+    hipError_t err = zero_cls_max ? hipMemsetAsync(cls_max, 0, sizeof(uint32_t) * DEV_CLASSES, s) : hipSuccess;
     if (err != hipSuccess || n_nodes == 0) return err;
     // the batch's classes only (a class's code / score is read only by pods of that class)
     k_dev_sum<<<(n_nodes + 255) / 256, 256, 0, s>>>(nodes, zones, devs, n_nodes, n0, cls, n_cls, cfg, e, out,

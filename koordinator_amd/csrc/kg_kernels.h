@@ -216,7 +216,7 @@ hipError_t launch_gpu_zone_sum(const NodeRec* nodes, const ZoneRec* zones, const
                                uint64_t* out, hipStream_t s);
 hipError_t launch_dev_sum(const NodeRec* nodes, const ZoneRec* zones, const DevRec* devs, uint32_t n_nodes, uint32_t n0,
                           const DevClass* cls, uint32_t n_cls, const KCfg& cfg, const ExtDev& e, DevSum* out,
-                          uint32_t* cls_max, hipStream_t s);
+                          uint32_t* cls_max, hipStream_t s, bool zero_cls_max = true);
 hipError_t launch_scatter_rows(const void* stage, const uint32_t* pos, uint32_t n, bool dev, NodeRec* nodes,
                                ZoneRec* zones, DevRec* devs, hipStream_t s);
 hipError_t launch_verify(const NodeRec* nodes, const ZoneRec* zones, const PodsDev& pods, uint32_t n_pods,

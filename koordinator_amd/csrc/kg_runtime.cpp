@@ -1859,30 +1859,27 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e, bool* lane_open)
         p->rcode_cap = need;
     }
     // DeviceShare's NUMA hints of the SingleNUMANode records (per class) on the second side lane beside DevSum and
-    // the restore tables' codes: the three tables are independent, the statistics kernels read all of them
+    // the restore tables' codes: the three tables are independent. DevSum is submitted first (the accumulators and its
+    // cls_max were zeroed before the quota gate, ext_gate_local): the statistics wait for it.
     SideLane lane{};
     const SideLane* l2 = gz ? side_lane2(ctx, lane) : nullptr;
-    if (l2) {
-        HIP_TRY(ctx, hipEventRecord(l2->fork, ctx->stream));
-        HIP_TRY(ctx, hipStreamWaitEvent(l2->s, l2->fork, 0));
-    }
+    if (l2) HIP_TRY(ctx, hipEventRecord(l2->fork, ctx->stream));
     auto drain = [&]() {
         if (l2) hipStreamSynchronize(l2->s);
     };
+    if (launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(),
+                       p->d_devsum, spec_cls_max(p), ctx->stream, false) != hipSuccess)
+        return fail(ctx, KG_DEVICE_ERROR, "dev sum launch failed");
     e.gz = nullptr;
     if (gz) {
-        if (launch_gpu_zone_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg,
+        if ((l2 && hipStreamWaitEvent(l2->s, l2->fork, 0) != hipSuccess) ||
+            launch_gpu_zone_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg,
                                 s->ext_dev(), p->d_gz, l2 ? l2->s : ctx->stream) != hipSuccess ||
             (l2 && hipEventRecord(l2->join, l2->s) != hipSuccess)) {
             drain();
             return fail(ctx, KG_DEVICE_ERROR, "gpu zone sum launch failed");
         }
         e.gz = p->d_gz;
-    }
-    if (launch_dev_sum(s->d_nodes, s->d_zones, s->d_dev, s->n, s->n0, p->d_dclass, p->n_dclass, s->kcfg, s->ext_dev(),
-                       p->d_devsum, spec_cls_max(p), ctx->stream) != hipSuccess) {
-        drain();
-        return fail(ctx, KG_DEVICE_ERROR, "dev sum launch failed");
     }
     e.dsum = p->d_devsum;
     e.rcode = nullptr;
@@ -1899,13 +1896,17 @@ static kg_status ext_dev_sum(kg_snap* s, kg_pods* p, ExtDev& e, bool* lane_open)
 }
 
 // Quota gate (writes every pod's status first) and the pass-1 accumulators of the batch.
+// (the accumulators are zeroed before the gate kernel: the plain pods' select forks right behind it, and k_dev_sum is
+// then the main stream's next dispatch — behind a fill it lost the race for the CUs to the select's ~8k workgroups,
+// 0.21 -> 0.96 ms)
 static kg_status ext_gate_local(kg_snap* s, kg_pods* p) {
     kg_ctx* ctx = s->ctx;
-    HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, s->ext_dev(), s->cfg.plugins, p->d_qst, p->d_pstat, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_dev_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_rsv_max, 0, sizeof(uint32_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(p->d_pref, 0xFF, sizeof(uint64_t) * p->n, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(spec_fb_max(p), 0, sizeof(uint32_t) * p->n, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(spec_cls_max(p), 0, sizeof(uint32_t) * DEV_CLASSES, ctx->stream));  // k_dev_sum's
+    HIP_TRY(ctx, launch_ext_gate(p->dev, p->n, s->ext_dev(), s->cfg.plugins, p->d_qst, p->d_pstat, ctx->stream));
     return KG_OK;
 }
 
