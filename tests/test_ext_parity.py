@@ -460,3 +460,27 @@ def test_ext_select_stored_pairs(ctx, monkeypatch, numa, mode, k):
     ref = oracle_lib.ext_verify(kc, nodes, pods, quotas, rsv)
     wstat = np.bitwise_or.reduce(ref.status & (abi.KG_ST_UNSUPPORTED | abi.KG_ST_QUOTA), axis=1)
     assert np.array_equal(engine.result_status(batch), wstat)
+
+
+def test_ext_select_c1_beside_rerun(ctx, capfd, monkeypatch):
+    """Top-1 with SingleNUMANode records: k_ext_select_c1 runs beside the one-pass select with the guessed maxima and
+    re-runs on the rows k_ext_fix_rows lists (the first 256 over short chunks in one pod block, the rest in a second
+    launch). The nodes with the most free GPU have no CPU left, so more than 256 rows are re-run; keys still equal the
+    oracle's."""
+    cfg, nodes, pods, quotas, rsv = synth.cluster5(1500, 2600, seed_config=29, rsv_frac=0.1, numa="single")
+    free = nodes["dev_free"][:, abi.KG_DEV_CORE, :].sum(1)
+    top = np.argsort(-free, kind="stable")[:60]
+    nodes["req_cpu"][top] = nodes["alloc_cpu"][top]
+    nodes["nz_cpu"][top] = np.maximum(nodes["nz_cpu"][top], nodes["alloc_cpu"][top])
+    kc = cfg.kg_config()
+    monkeypatch.setenv("KG_TRACE_FIX", "1")
+    monkeypatch.setenv("KG_TRACE_SP", "1")
+    snap, batch = make(ctx, kc, nodes, pods, quotas, rsv)
+    got = engine.eval_select(snap, batch, 1)
+    want = oracle_lib.ext_select(kc, nodes, pods, 1, 0, quotas, rsv)
+    assert np.array_equal(got, want), np.argwhere(got != want)[:8].tolist()
+    err = capfd.readouterr().err
+    m = re.search(r"re-ran (\d+) of (\d+) rows", err)
+    c = re.search(r"class-1 (\d+)", err)
+    assert m and int(m.group(1)) > 256, err[-400:]
+    assert c and int(c.group(1)) > 0, "no class-1 list: the test no longer reaches the class-1 kernels"
